@@ -1,0 +1,25 @@
+# liborbx.so (HIP, gfx950) + the CPU oracle used by the tests.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := multiagent_orb_slam2_amd
+SRC := $(PKG)/csrc
+HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result
+HDRS := include/orbx.h $(SRC)/orbx_common.h $(SRC)/orbx_pattern.h
+OBJS := $(SRC)/orbx_extract.o $(SRC)/orbx_match.o
+
+all: $(PKG)/liborbx.so oracle
+
+$(SRC)/%.o: $(SRC)/%.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/liborbx.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -f $(OBJS) $(PKG)/liborbx.so
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean

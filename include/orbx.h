@@ -1,0 +1,191 @@
+/*
+ * orbx.h — C-ABI of the MI355X-native ORB front-end and Hamming matchers (liborbx.so).
+ *
+ * Drop-in boundary for the hot path of andresenwc/MultiAgent_ORB_SLAM2 (reference paths below are
+ * relative to the reference root).  The reference's C++ classes ORB_SLAM2::ORBextractor
+ * (include/ORBextractor.h:45-111) and ORB_SLAM2::ORBmatcher (include/ORBmatcher.h:37-102) keep their
+ * signatures; their bodies call the functions below (adapter in INTEGRATION.md).  Plain pointers and
+ * sizes only; every function returns an int status (ORBX_OK = 0, < 0 on error; text via
+ * orbx_last_error()) and never throws.  Host buffers are owned by the caller, device buffers made by
+ * a context are owned by the context.  A context is used by one host thread at a time (the reference
+ * constructs one ORBextractor per camera per agent, Tracking.cc:119-125, and stack ORBmatchers per
+ * thread); distinct contexts may be used concurrently from different threads.
+ *
+ * "_device" entry points take device pointers and a hipStream_t (passed as void*; NULL = the HIP
+ * null stream, as in the HIP API) and do not synchronise; all other entry points take host pointers,
+ * run on the context's own stream and return after the results are in host memory.
+ */
+#ifndef ORBX_H
+#define ORBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    ORBX_OK = 0,
+    ORBX_ERR_ARG = -1,        /* invalid argument */
+    ORBX_ERR_HIP = -2,        /* HIP runtime error (no device, launch failure, OOM) */
+    ORBX_ERR_CAPACITY = -3,   /* output capacity too small; *n_out holds the required count */
+    ORBX_ERR_UNSUPPORTED = -4 /* configuration outside the compiled limits */
+};
+
+/* Layout-identical to cv::KeyPoint (28 B): pt.x, pt.y, size, angle, response, octave, class_id. */
+typedef struct orbx_keypoint {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbx_keypoint;
+
+/* Last error message of the calling thread ("" if none). */
+const char* orbx_last_error(void);
+/* Library version string. */
+const char* orbx_version(void);
+/* Number of visible HIP devices (0 when none; never fails). */
+int orbx_device_count(void);
+
+/* ------------------------------------------------------------------------------------------------
+ * Extractor — replaces ORBextractor (src/ORBextractor.cc:410-1132)
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct orbx_extractor orbx_extractor;
+
+/* ORBextractor::ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+ * (src/ORBextractor.cc:410-470).  Binds the context to 'device' (HIP ordinal) and creates its stream. */
+int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST,
+                          int device, orbx_extractor** out);
+int orbx_extractor_destroy(orbx_extractor* ex);
+
+/* Getters — ORBextractor::GetLevels/GetScaleFactor/GetScaleFactors/GetInverseScaleFactors/
+ * GetScaleSigmaSquares/GetInverseScaleSigmaSquares (include/ORBextractor.h:63-83).  Arrays hold nlevels. */
+int orbx_extractor_get_levels(const orbx_extractor* ex);
+float orbx_extractor_get_scale_factor(const orbx_extractor* ex);
+int orbx_extractor_get_scale_factors(const orbx_extractor* ex, float* out);
+int orbx_extractor_get_inverse_scale_factors(const orbx_extractor* ex, float* out);
+int orbx_extractor_get_scale_sigma_squares(const orbx_extractor* ex, float* out);
+int orbx_extractor_get_inverse_scale_sigma_squares(const orbx_extractor* ex, float* out);
+/* mnFeaturesPerLevel (src/ORBextractor.cc:435-446). */
+int orbx_extractor_get_features_per_level(const orbx_extractor* ex, int* out);
+
+/* Configure the context for images of rows x cols, up to max_batch images per device call
+ * (allocates HBM once).  Called implicitly by orbx_extract with max_batch 1. */
+int orbx_extractor_reserve(orbx_extractor* ex, int rows, int cols, int max_batch);
+/* Maximum keypoints one image can yield for rows x cols (output capacity to allocate). */
+int orbx_extractor_max_keypoints(orbx_extractor* ex, int rows, int cols);
+/* Pyramid geometry for rows x cols: level sizes (nlevels each). */
+int orbx_extractor_level_sizes(orbx_extractor* ex, int rows, int cols, int* level_rows, int* level_cols);
+
+/* ORBextractor::operator()(image, mask, keypoints, descriptors) (src/ORBextractor.cc:1043-1105).
+ * image: host 8UC1, rows x cols, row stride 'step' bytes.  Writes *n_out keypoints (level-major,
+ * quadtree order within a level, coordinates scaled to level 0) and n_out x 32 descriptor bytes.
+ * An empty image (rows or cols 0) returns ORBX_OK with *n_out = 0 (reference: :1046-1047).
+ * If capacity < needed, returns ORBX_ERR_CAPACITY with *n_out = needed and writes nothing. */
+int orbx_extract(orbx_extractor* ex, const uint8_t* image, int rows, int cols, size_t step,
+                 orbx_keypoint* keypoints, uint8_t* descriptors, int capacity, int* n_out);
+
+/* mvImagePyramid (include/ORBextractor.h:85): copy level 'level' of image 'index' of the last call
+ * into a host buffer with row stride dst_step (unpadded level view, as Frame::ComputeStereoMatches
+ * reads it, src/Frame.cc:563-580). */
+int orbx_extractor_copy_level(orbx_extractor* ex, int index, int level, uint8_t* dst, size_t dst_step);
+
+/* Batched device entry: 'batch' images of rows x cols at d_images + i*image_stride (row stride 'step').
+ * Outputs per image i: d_keypoints[i*capacity ...], d_descriptors[(i*capacity ...)*32], d_counts[i].
+ * capacity must be >= orbx_extractor_max_keypoints(). */
+int orbx_extract_batch_device(orbx_extractor* ex, const uint8_t* d_images, int batch, int rows, int cols,
+                              size_t step, size_t image_stride, orbx_keypoint* d_keypoints,
+                              uint8_t* d_descriptors, int32_t* d_counts, int capacity, void* stream);
+
+/* Device pointer of pyramid level 'level' of batch image 'index' (contiguous rows, stride = cols). */
+int orbx_extractor_level_device(orbx_extractor* ex, int index, int level, const uint8_t** d_level,
+                                int* rows, int* cols);
+
+/* Optional per-stage timing of device calls (HIP events on the launch stream).  When enabled, each
+ * orbx_extract_batch_device records events around every stage; orbx_extractor_stage_times returns
+ * the accumulated milliseconds per stage and the number of recorded calls.  Stage names via
+ * orbx_extractor_stage_name. */
+int orbx_extractor_enable_timing(orbx_extractor* ex, int enable);
+int orbx_extractor_stage_count(void);
+const char* orbx_extractor_stage_name(int stage);
+int orbx_extractor_stage_times(orbx_extractor* ex, double* ms_per_stage, int* calls);
+
+/* ------------------------------------------------------------------------------------------------
+ * Matchers — replace ORBmatcher (src/ORBmatcher.cc) and the descriptor search of
+ * Frame::ComputeStereoMatches (src/Frame.cc:466-552)
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct orbx_matcher orbx_matcher;
+
+/* ORBmatcher::ORBmatcher(nnratio, checkOri) (src/ORBmatcher.cc:41-43), bound to 'device'. */
+int orbx_matcher_create(float nnratio, int checkOri, int device, orbx_matcher** out);
+int orbx_matcher_destroy(orbx_matcher* m);
+
+/* ORBmatcher::TH_HIGH / TH_LOW / HISTO_LENGTH (src/ORBmatcher.cc:37-39). */
+int orbx_th_high(void);
+int orbx_th_low(void);
+int orbx_histo_length(void);
+
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1649-1665) for n row pairs (a_i, b_i), device. */
+int orbx_descriptor_distance_device(orbx_matcher* m, const uint8_t* d_a, const uint8_t* d_b, int n,
+                                    int32_t* d_dist, void* stream);
+
+/* Brute-force all-pairs 256-bit Hamming: for each query row the smallest distance, the lowest train
+ * index attaining it and the second smallest distance (multiset), with the reference's
+ * best/second update rule (init 256, strict <; src/ORBmatcher.cc:568-598).  Host and device forms. */
+int orbx_bf_match(orbx_matcher* m, const uint8_t* query, int nq, const uint8_t* train, int nt,
+                  int32_t* best_idx, int32_t* best_dist, int32_t* second_dist);
+int orbx_bf_match_device(orbx_matcher* m, const uint8_t* d_query, int nq, const uint8_t* d_train, int nt,
+                         int32_t* d_best_idx, int32_t* d_best_dist, int32_t* d_second_dist, void* stream);
+
+/* Stereo L<->R descriptor search of Frame::ComputeStereoMatches (src/Frame.cc:466-552): for each left
+ * keypoint, the right keypoint in the row band of (int)vL (+-2*scale[octave] rows), octave within +-1
+ * and uR in [uL - bf/b, uL] with the smallest distance (init TH_HIGH, strict <, ties -> lowest right
+ * index).  best_idx = -1 unless best_dist < (TH_HIGH+TH_LOW)/2.  scale_factors: nlevels entries;
+ * rows = level-0 image rows.  Returns the number of accepted matches in *n_matched. */
+int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* desc_l, int nl,
+                      const orbx_keypoint* kpr, const uint8_t* desc_r, int nr, const float* scale_factors,
+                      int nlevels, int rows, float bf, float b, int32_t* best_idx, int32_t* best_dist,
+                      int* n_matched);
+/* Batched device form over 'batch' stereo pairs laid out like orbx_extract_batch_device output
+ * (keypoints/descriptors at i*capacity, counts per image).  Outputs at i*capacity. */
+int orbx_stereo_match_batch_device(orbx_matcher* m, const orbx_keypoint* d_kpl, const uint8_t* d_desc_l,
+                                   const int32_t* d_nl, const orbx_keypoint* d_kpr, const uint8_t* d_desc_r,
+                                   const int32_t* d_nr, int batch, int capacity, const float* scale_factors,
+                                   int nlevels, int rows, float bf, float b, int32_t* d_best_idx,
+                                   int32_t* d_best_dist, void* stream);
+
+/* DBoW2::FeatureVector (Thirdparty/DBoW2/DBoW2/FeatureVector.h:21-22) as CSR: node ids ascending,
+ * offsets[n_nodes+1], feature indices (ascending within a node). */
+typedef struct orbx_featvec {
+    const uint32_t* node_ids;
+    const int32_t* offsets;
+    int n_nodes;
+    const int32_t* indices;
+} orbx_featvec;
+
+/* ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&) (src/ORBmatcher.cc:524-657).
+ * valid1/valid2[i] != 0 when keypoint i has a non-bad MapPoint.  match12[i] = KF2 index or -1. */
+int orbx_search_by_bow_kfkf(orbx_matcher* m, const uint8_t* desc1, const float* angle1, const uint8_t* valid1,
+                            int n1, orbx_featvec fv1, const uint8_t* desc2, const float* angle2,
+                            const uint8_t* valid2, int n2, orbx_featvec fv2, int32_t* match12, int* n_matches);
+
+/* ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (src/ORBmatcher.cc:161-290).
+ * validk[i] != 0 when KF keypoint i has a non-bad MapPoint.  matchf[j] = KF index or -1. */
+int orbx_search_by_bow_kff(orbx_matcher* m, const uint8_t* desck, const float* anglek, const uint8_t* validk,
+                           int nk, orbx_featvec fvk, const uint8_t* descf, const float* anglef, int nf,
+                           orbx_featvec fvf, int32_t* matchf, int* n_matches);
+
+/* ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:659-825).  has_mp1/2: keypoint already has a
+ * MapPoint; uright1/2 >= 0 marks stereo keypoints; F12 row-major 3x3; sigma2_2/scale_2: KF2 level
+ * tables; (ex, ey): epipole of KF1 in KF2.  match12[i] = KF2 index or -1 (pairs in idx1 order). */
+int orbx_search_for_triangulation(orbx_matcher* m, const uint8_t* desc1, const orbx_keypoint* kp1,
+                                  const uint8_t* has_mp1, const float* uright1, int n1, orbx_featvec fv1,
+                                  const uint8_t* desc2, const orbx_keypoint* kp2, const uint8_t* has_mp2,
+                                  const float* uright2, int n2, orbx_featvec fv2, const float* F12,
+                                  const float* sigma2_2, const float* scale_2, int nlevels, float ex, float ey,
+                                  int only_stereo, int32_t* match12, int* n_matches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORBX_H */

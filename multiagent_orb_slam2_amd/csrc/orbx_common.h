@@ -1,0 +1,110 @@
+// Shared helpers for the orbx HIP sources (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/orbx.h"
+
+namespace orbx {
+
+// ---------------------------------------------------------------------------------------------
+// Error reporting: every C-ABI entry returns a status and leaves a message for orbx_last_error().
+// ---------------------------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+
+#define ORBX_HIP(call)                                                                          \
+    do {                                                                                        \
+        hipError_t e_ = (call);                                                                 \
+        if (e_ != hipSuccess) {                                                                 \
+            ::orbx::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+            return ORBX_ERR_HIP;                                                                \
+        }                                                                                       \
+    } while (0)
+
+#define ORBX_REQUIRE(cond, code, ...)      \
+    do {                                   \
+        if (!(cond)) {                     \
+            ::orbx::set_error(__VA_ARGS__); \
+            return (code);                 \
+        }                                  \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------------------------
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
+
+// number of set bits of 'mask' in lanes below this lane
+__device__ __forceinline__ int lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        int t = __shfl_up(v, o, kWave);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+
+// Block-wide exclusive scan of one int per thread.  'tmp' = LDS scratch of >= (blockDim/64 + 1) ints.
+// Returns the exclusive prefix; *total receives the block sum.  Contains two barriers.
+__device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int inc = wave_incl_scan(v);
+    if (lane_id() == kWave - 1) tmp[w] = inc;
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int i = 0; i < nw; ++i) {
+        const int t = tmp[i];
+        off += (i < w) ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+// Exclusive scan over n items held in 'a' (LDS), in place, using the whole block: each thread owns a
+// contiguous chunk.  Returns the total.  'tmp' as above.
+__device__ __forceinline__ int block_scan_array(int* a, int n, int* tmp) {
+    const int T = blockDim.x;
+    const int per = (n + T - 1) / T;
+    const int b = threadIdx.x * per, e = min(b + per, n);
+    int s = 0;
+    for (int i = b; i < e; ++i) s += a[i];
+    int total;
+    int off = block_excl_scan(s, tmp, &total);
+    for (int i = b; i < e; ++i) {
+        const int t = a[i];
+        a[i] = off;
+        off += t;
+    }
+    __syncthreads();
+    return total;
+}
+
+__device__ __forceinline__ int popc32(uint32_t v) { return __builtin_popcount(v); }
+
+// 256-bit Hamming distance (ORBmatcher::DescriptorDistance, src/ORBmatcher.cc:1649-1665): the
+// reference's SWAR popcount of 8 XORed 32-bit words equals the bit count, here v_bcnt_u32_b32.
+__device__ __forceinline__ int hamming256(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
+    return popc32(a0.x ^ b0.x) + popc32(a0.y ^ b0.y) + popc32(a0.z ^ b0.z) + popc32(a0.w ^ b0.w) +
+           popc32(a1.x ^ b1.x) + popc32(a1.y ^ b1.y) + popc32(a1.z ^ b1.z) + popc32(a1.w ^ b1.w);
+}
+
+}  // namespace orbx

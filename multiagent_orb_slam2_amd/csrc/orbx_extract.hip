@@ -1,0 +1,1322 @@
+// =====================================================================================================
+// orbx_extract.hip — MI355X (gfx950) ORB extractor: the hot path of ORBextractor::operator()
+// (reference src/ORBextractor.cc:1043-1105) as batched HIP kernels behind the C-ABI of include/orbx.h.
+//
+// Per device call over a batch of B images (all rows x cols), one stream, 5 + (nlevels-1) launches:
+//   k_copy_level0   image -> pyramid level 0                        (ComputePyramid :1127)
+//   k_resize        level l-1 -> level l, l = 1..L-1 (chained)       (ComputePyramid :1120)
+//   k_fast_cells    one workgroup per (30-px grid cell, image): FAST-9 score map in LDS, 3x3 strict
+//                   NMS at iniThFAST, fallback to minThFAST when the cell is empty, row-major
+//                   compaction into per-cell candidate slots          (ComputeKeyPointsOctTree :789-829)
+//   k_blur7         7x7 sigma-2 Gaussian on every level (REFLECT_101) (operator() :1085-1086)
+//   k_quadtree      one workgroup per (level, image): DistributeOctTree's list/quadtree as data-parallel
+//                   passes over LDS node arrays                     (:539-763, :834-847)
+//   k_describe      one wave per keypoint: IC angle on the level, steered BRIEF on the blurred level,
+//                   level-major output with coordinates scaled to level 0   (:77-147, :851-852, :1075-1104)
+// Pinned arithmetic (identical to oracle/orb_oracle.cpp): fixed-point resize and blur,
+// round-half-even, no FMA contraction (-ffp-contract=off + explicit __f*_rn), correctly rounded
+// float cos/sin of the BRIEF angle, quadtree phase-2 ties in creation order.
+// =====================================================================================================
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "orbx_common.h"
+#include "orbx_pattern.h"
+
+namespace orbx {
+
+// ---------------------------------------------------------------------------------------------
+// error plumbing (shared by every translation unit of liborbx)
+// ---------------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+constexpr int kEdge = 19;          // EDGE_THRESHOLD (src/ORBextractor.cc:74)
+constexpr int kHalfPatch = 15;     // HALF_PATCH_SIZE (:73)
+constexpr int kMaxRoi = 72;        // cell ROI side bound: wCell < 60 (+6)
+constexpr int kQtThreads = 256;
+constexpr int kMaxLevels = 32;
+
+// ---------------------------------------------------------------------------------------------
+// device-side geometry records
+// ---------------------------------------------------------------------------------------------
+struct LevelDev {
+    int w, h;            // level size
+    int pyr_off;         // offset of the level inside one image's pyramid
+    int cell_begin, cell_end;
+    int cand_off;        // candidate slot region (per image) of the level
+    int cand_cap;
+    int out_off;         // quadtree output slot region (per image)
+    int out_cap;
+    int N;               // mnFeaturesPerLevel
+    int nIni;
+    float hX;
+    int win_w, win_h;    // maxBorder - minBorder
+    float scale;         // mvScaleFactor
+    int patch;           // (int)(PATCH_SIZE * scale)
+};
+
+struct CellDev {
+    int level;
+    int x0, y0;          // ROI origin in level coords (iniX, iniY)
+    int W, H;            // ROI size (maxX - iniX, maxY - iniY)
+    int slot_off;        // candidate slot offset (per image)
+    int slot_cap;
+    int pad;
+};
+
+struct ResizeTab {       // per level >= 1, device arrays
+    int* x0; int* x1; int* a0; int* a1;   // [w]
+    int* y0; int* y1; int* b0; int* b1;   // [h]
+};
+
+__constant__ signed char c_pattern[ORBX_PATTERN_TESTS * 4];
+__constant__ int c_umax[16];
+
+// =============================================================================================
+// kernels
+// =============================================================================================
+
+__global__ __launch_bounds__(256) void k_copy_level0(const uint8_t* __restrict__ src, size_t step, size_t istride,
+                                                     uint8_t* __restrict__ pyr, size_t pyr_stride, int w, int h) {
+    const int img = blockIdx.z, y = blockIdx.y;
+    const uint8_t* s = src + img * istride + (size_t)y * step;
+    uint8_t* d = pyr + img * pyr_stride + (size_t)y * w;
+    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < w; x += gridDim.x * blockDim.x) d[x] = s[x];
+}
+
+// resize INTER_LINEAR 8U, fixed point (pinned OpenCV 3.2 generic path): horizontal taps a0/a1 (x2048)
+// with clamped source columns, vertical (r0*b0 + r1*b1 + 2^21) >> 22 saturated.
+__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride, int src_off, int sw,
+                                                int dst_off, int dw, int dh, ResizeTab t) {
+    const int img = blockIdx.z, y = blockIdx.y;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= dw || y >= dh) return;
+    const uint8_t* S = pyr + img * pyr_stride + src_off;
+    const uint8_t* r0 = S + (size_t)t.y0[y] * sw;
+    const uint8_t* r1 = S + (size_t)t.y1[y] * sw;
+    const int xa = t.x0[x], xb = t.x1[x], a0 = t.a0[x], a1 = t.a1[x];
+    const int h0 = (int)r0[xa] * a0 + (int)r0[xb] * a1;
+    const int h1 = (int)r1[xa] * a0 + (int)r1[xb] * a1;
+    int v = (h0 * t.b0[y] + h1 * t.b1[y] + (1 << 21)) >> 22;
+    v = min(max(v, 0), 255);
+    pyr[img * pyr_stride + dst_off + (size_t)y * dw + x] = (uint8_t)v;
+}
+
+// FAST-9/16 corner score in closed form.  For pixel value v and circle values p_k (Bresenham r=3,
+// OpenCV order), with d_k = v - p_k:  m_dark = max over the 16 arcs of 9 of min d, m_bright = max
+// over arcs of min(-d).  OpenCV's cornerScore<16> returns max(t, m_dark, m_bright) - 1 and the pixel
+// is a corner at threshold t iff max(m_dark, m_bright) > t; hence s = max(m_dark, m_bright) - 1 is
+// threshold independent and "corner at t" <=> s >= t.
+__device__ __forceinline__ int fast_score(const uint8_t* p, int W) {
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * W];      d[1] = v - p[3 * W + 1];  d[2] = v - p[2 * W + 2];  d[3] = v - p[W + 3];
+    d[4] = v - p[3];          d[5] = v - p[-W + 3];     d[6] = v - p[-2 * W + 2]; d[7] = v - p[-3 * W + 1];
+    d[8] = v - p[-3 * W];     d[9] = v - p[-3 * W - 1]; d[10] = v - p[-2 * W - 2]; d[11] = v - p[-W - 3];
+    d[12] = v - p[-3];        d[13] = v - p[W - 3];     d[14] = v - p[2 * W - 2]; d[15] = v - p[3 * W - 1];
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { mn2[k] = min(d[k], d[(k + 1) & 15]); mx2[k] = max(d[k], d[(k + 1) & 15]); }
+    int mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { mn4[k] = min(mn2[k], mn2[(k + 2) & 15]); mx4[k] = max(mx2[k], mx2[(k + 2) & 15]); }
+    int dark = -1000, brightneg = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+        dark = max(dark, mn9);
+        brightneg = min(brightneg, mx9);
+    }
+    return max(dark, -brightneg) - 1;
+}
+
+// One workgroup per (cell, image).  Cell geometry from ComputeKeyPointsOctTree (:784-807); FAST on the
+// ROI detects rows/cols [3, dim-3) of the ROI, NMS compares against the 8 neighbours' scores inside
+// the ROI's detection window (0 outside), strict '>' (OpenCV FAST_t).  Empty at iniTh -> minTh (:812-816).
+__global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                    const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
+                                                    int iniTh, int minTh, uint32_t* __restrict__ cand_xy,
+                                                    uint8_t* __restrict__ cand_s, int cand_stride,
+                                                    int* __restrict__ cell_cnt, int ncells) {
+    __shared__ uint8_t roi[kMaxRoi * kMaxRoi];
+    __shared__ int16_t sc[kMaxRoi * kMaxRoi];
+    __shared__ int red[8];
+    const int img = blockIdx.y, c = blockIdx.x, tid = threadIdx.x;
+    const CellDev cd = cells[c];
+    const LevelDev L = levels[cd.level];
+    const uint8_t* base = pyr + img * pyr_stride + L.pyr_off;
+    const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
+    for (int i = tid; i < W * H; i += blockDim.x) {
+        const int r = i / W, q = i - r * W;
+        roi[i] = base[(size_t)(cd.y0 + r) * L.w + cd.x0 + q];
+    }
+    __syncthreads();
+    const int npx = (Wd > 0 && Hd > 0) ? Wd * Hd : 0;
+    for (int i = tid; i < npx; i += blockDim.x) {
+        const int r = i / Wd, q = i - r * Wd;
+        sc[i] = (int16_t)fast_score(roi + (r + 3) * W + (q + 3), W);
+    }
+    __syncthreads();
+
+    auto is_kp = [&](int i, int t) -> bool {
+        const int r = i / Wd, q = i - r * Wd;
+        const int s = sc[i];
+        if (s < t) return false;
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                if (!dy && !dx) continue;
+                const int rr = r + dy, qq = q + dx;
+                int n = 0;
+                if (rr >= 0 && rr < Hd && qq >= 0 && qq < Wd) {
+                    n = sc[rr * Wd + qq];
+                    if (n < t) n = 0;
+                }
+                if (!(s > n)) return false;
+            }
+        return true;
+    };
+
+    const int t_ini = min(max(iniTh, 0), 255), t_min = min(max(minTh, 0), 255);
+    int mine = 0;
+    for (int i = tid; i < npx; i += blockDim.x) mine += is_kp(i, t_ini) ? 1 : 0;
+    const int found = __syncthreads_or(mine);
+    const int t = found ? t_ini : t_min;
+
+    // row-major compaction (order of OpenCV's keypoint output) into the cell's slots
+    uint32_t* oxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
+    uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
+    const int w = tid >> 6, nw = blockDim.x >> 6;
+    int running = 0;
+    for (int b = 0; b < npx; b += blockDim.x) {
+        const int i = b + tid;
+        const bool k = (i < npx) && is_kp(i, t);
+        const uint64_t m = __ballot(k);
+        if (lane_id() == 0) red[w] = __popcll(m);
+        __syncthreads();
+        int before = running, tot = 0;
+        for (int j = 0; j < nw; ++j) { before += (j < w) ? red[j] : 0; tot += red[j]; }
+        if (k) {
+            const int pos = before + lanes_below(m);
+            if (pos < cd.slot_cap) {
+                const int r = i / Wd, q = i - r * Wd;
+                oxy[pos] = (uint32_t)(cd.x0 + q + 3) | ((uint32_t)(cd.y0 + r + 3) << 16);
+                os[pos] = (uint8_t)sc[i];
+            }
+        }
+        running += tot;
+        __syncthreads();
+    }
+    if (tid == 0) cell_cnt[(size_t)img * ncells + c] = min(running, cd.slot_cap);
+}
+
+// GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, integer separable path: taps {18,34,49,55,49,34,18},
+// column pass (acc + 2^15) >> 16 saturated.  Tile 64 x 16 per workgroup; tiles of all levels in one grid.
+struct BlurTile { int level, tx, ty, pad; };
+
+__device__ __forceinline__ int refl101(int i, int n) {
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) i = (i < 0) ? -i : 2 * n - 2 - i;
+    return i;
+}
+
+__global__ __launch_bounds__(256) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                               size_t pyr_stride, const LevelDev* __restrict__ levels,
+                                               const BlurTile* __restrict__ tiles) {
+    constexpr int TW = 64, TH = 16;
+    __shared__ uint8_t in[(TH + 6) * (TW + 6)];
+    __shared__ int hs[(TH + 6) * TW];
+    const int img = blockIdx.y, tid = threadIdx.x;
+    const BlurTile bt = tiles[blockIdx.x];
+    const LevelDev L = levels[bt.level];
+    const uint8_t* S = pyr + img * pyr_stride + L.pyr_off;
+    uint8_t* D = blur + img * pyr_stride + L.pyr_off;
+    const int X0 = bt.tx * TW, Y0 = bt.ty * TH;
+    for (int i = tid; i < (TH + 6) * (TW + 6); i += blockDim.x) {
+        const int r = i / (TW + 6), q = i - r * (TW + 6);
+        const int y = refl101(Y0 + r - 3, L.h), x = refl101(X0 + q - 3, L.w);
+        in[i] = S[(size_t)y * L.w + x];
+    }
+    __syncthreads();
+    const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;
+    for (int i = tid; i < (TH + 6) * TW; i += blockDim.x) {
+        const int r = i / TW, q = i - r * TW;
+        const uint8_t* p = in + r * (TW + 6) + q;
+        hs[i] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
+    }
+    __syncthreads();
+    for (int i = tid; i < TH * TW; i += blockDim.x) {
+        const int r = i / TW, q = i - r * TW;
+        const int y = Y0 + r, x = X0 + q;
+        if (y >= L.h || x >= L.w) continue;
+        const int* p = hs + r * TW + q;
+        const int acc = k0 * (p[0] + p[6 * TW]) + k1 * (p[TW] + p[5 * TW]) + k2 * (p[2 * TW] + p[4 * TW]) + k3 * p[3 * TW];
+        D[(size_t)y * L.w + x] = (uint8_t)min(max((acc + (1 << 15)) >> 16, 0), 255);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Quadtree: DistributeOctTree (:539-763) as data-parallel passes.
+//
+// The reference keeps a std::list of nodes.  One phase-1 pass splits every node holding >1 key and
+// pushes the non-empty children (n1,n2,n3,n4) to the list FRONT, so after a pass the list reads:
+// [children of the last split node (n4..n1), ..., children of the first split node, unsplit nodes in
+// their previous order].  A phase-2 pass sorts the expandable nodes by (size, creation order),
+// splits from the largest down and stops as soon as the list holds >= N nodes.  Both are positional
+// permutations computable with prefix sums: node arrays live in LDS (double-buffered, list order),
+// each key carries the list position of its node (key_node), child counts come from LDS atomics.
+// ---------------------------------------------------------------------------------------------
+struct QtScratch {
+    uint32_t* key_xy;    // window-relative (x | y << 16), reference order
+    uint8_t* key_r;      // FAST response
+    int16_t* key_node;   // list position of the key's node
+};
+
+__device__ __forceinline__ void child_rect(int x0, int x1, int y0, int y1, int q, int& cx0, int& cx1, int& cy0,
+                                           int& cy1) {
+    // ExtractorNode::DivideNode (:483-509): halfX = ceil((float)(UR.x-UL.x)/2)
+    const int hx = (int)ceilf(__fdiv_rn((float)(x1 - x0), 2.0f));
+    const int hy = (int)ceilf(__fdiv_rn((float)(y1 - y0), 2.0f));
+    const int mx = x0 + hx, my = y0 + hy;
+    cx0 = (q & 1) ? mx : x0;
+    cx1 = (q & 1) ? x1 : mx;
+    cy0 = (q & 2) ? my : y0;
+    cy1 = (q & 2) ? y1 : my;
+}
+
+__device__ __forceinline__ int quadrant(uint32_t xy, int x0, int x1, int y0, int y1) {
+    const int hx = (int)ceilf(__fdiv_rn((float)(x1 - x0), 2.0f));
+    const int hy = (int)ceilf(__fdiv_rn((float)(y1 - y0), 2.0f));
+    const int x = (int)(xy & 0xffff), y = (int)(xy >> 16);
+    return (x < x0 + hx ? 0 : 1) + (y < y0 + hy ? 0 : 2);   // (:515-525)
+}
+
+// number of non-empty children with quadrant index > q (children are pushed n1..n4 to the front, so
+// the group reads n4, n3, n2, n1)
+__device__ __forceinline__ int rank_desc(const int* cc, int q) {
+    int r = 0;
+#pragma unroll
+    for (int k = 3; k >= 0; --k) r += (k > q && cc[k] > 0) ? 1 : 0;
+    return r;
+}
+__device__ __forceinline__ int rank_asc(const int* cc, int q) {
+    int r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r += (k < q && cc[k] > 0) ? 1 : 0;
+    return r;
+}
+
+__global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
+                                                         const uint32_t* __restrict__ cand_xy, const uint8_t* __restrict__ cand_s,
+                                                         int cand_stride, const int* __restrict__ cell_cnt, int ncells,
+                                                         QtScratch qs, uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r,
+                                                         int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
+                                                         int scan_cap, int* __restrict__ err) {
+    extern __shared__ int smem[];
+    const int lvl = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
+    const LevelDev L = levels[lvl];
+    // LDS layout
+    int* A_xr = smem;              // x0 | x1 << 16
+    int* A_yr = A_xr + cap;        // y0 | y1 << 16
+    int* A_cnt = A_yr + cap;
+    int* A_seq = A_cnt + cap;
+    int* B_xr = A_seq + cap;
+    int* B_yr = B_xr + cap;
+    int* B_cnt = B_yr + cap;
+    int* B_seq = B_cnt + cap;
+    int* cc = B_seq + cap;         // [cap][4] child counts
+    int* base = cc + 4 * cap;      // new list position (unsplit) / group base (split)
+    int* sa = base + cap;          // scan array [scan_cap]
+    int* sb = sa + scan_cap;       // scan array [scan_cap]
+    int* tmp = sb + scan_cap;      // 32 ints
+    int* misc = tmp + 32;          // 16 ints
+    unsigned long long* sk = (unsigned long long*)(misc + 16 + ((misc + 16 - smem) & 1));  // [pow2 >= cap]
+    const int ncl = L.cell_end - L.cell_begin;
+
+    // ---- 1. compact the level's cell candidates into reference order (cell row-major, then FAST order)
+    for (int i = tid; i < ncl; i += T) sa[i] = cell_cnt[(size_t)img * ncells + L.cell_begin + i];
+    __syncthreads();
+    const int K = block_scan_array(sa, ncl, tmp);
+    uint32_t* kxy = qs.key_xy + (size_t)img * cand_stride + L.cand_off;
+    uint8_t* kr = qs.key_r + (size_t)img * cand_stride + L.cand_off;
+    int16_t* kn = qs.key_node + (size_t)img * cand_stride + L.cand_off;
+    const int minB = kEdge - 3;
+    {
+        const int w = tid >> 6, nw = T >> 6, ln = lane_id();
+        for (int c = w; c < ncl; c += nw) {
+            const CellDev cd = cells[L.cell_begin + c];
+            const int n = cell_cnt[(size_t)img * ncells + L.cell_begin + c];
+            const uint32_t* sxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
+            const uint8_t* ss = cand_s + (size_t)img * cand_stride + cd.slot_off;
+            for (int e = ln; e < n; e += kWave) {
+                const uint32_t xy = sxy[e];
+                kxy[sa[c] + e] = ((xy & 0xffff) - minB) | (((xy >> 16) - minB) << 16);
+                kr[sa[c] + e] = ss[e];
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- 2. root nodes (:543-585)
+    const int nIni = L.nIni;
+    const float hX = L.hX;
+    for (int i = tid; i < nIni; i += T) {
+        const int x0 = (int)__fmul_rn(hX, (float)i), x1 = (int)__fmul_rn(hX, (float)(i + 1));
+        A_xr[i] = (x0 & 0xffff) | (x1 << 16);
+        A_yr[i] = 0 | (L.win_h << 16);
+        A_cnt[i] = 0;
+        A_seq[i] = i;
+    }
+    __syncthreads();
+    for (int k = tid; k < K; k += T) {
+        const int x = (int)(kxy[k] & 0xffff);
+        int r = (int)__fdiv_rn((float)x, hX);
+        r = min(r, nIni - 1);
+        kn[k] = (int16_t)r;
+        atomicAdd(&A_cnt[r], 1);
+    }
+    __syncthreads();
+    // drop empty roots (order preserved)
+    for (int i = tid; i < nIni; i += T) sa[i] = A_cnt[i] > 0 ? 1 : 0;
+    __syncthreads();
+    int n = block_scan_array(sa, nIni, tmp);
+    for (int i = tid; i < nIni; i += T) {
+        if (A_cnt[i] > 0) {
+            const int p = sa[i];
+            B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < K; k += T) kn[k] = (int16_t)sa[kn[k]];
+    for (int i = tid; i < n; i += T) { A_xr[i] = B_xr[i]; A_yr[i] = B_yr[i]; A_cnt[i] = B_cnt[i]; A_seq[i] = B_seq[i]; }
+    __syncthreads();
+
+    const int N = L.N;
+    bool phase2 = false, finished = false;
+    while (!finished) {
+        const int prev = n;
+        // -- child counts of every expandable node (phase 1 splits all of them, phase 2 needs their sizes)
+        for (int i = tid; i < 4 * n; i += T) cc[i] = 0;
+        __syncthreads();
+        for (int k = tid; k < K; k += T) {
+            const int i = kn[k];
+            if (A_cnt[i] > 1) {
+                const int q = quadrant(kxy[k], A_xr[i] & 0xffff, A_xr[i] >> 16, A_yr[i] & 0xffff, A_yr[i] >> 16);
+                atomicAdd(&cc[4 * i + q], 1);
+            }
+        }
+        __syncthreads();
+
+        if (!phase2) {
+            // ---------------- phase 1 pass (:606-665)
+            for (int i = tid; i < n; i += T) {
+                const int* c4 = cc + 4 * i;
+                const bool split = A_cnt[i] > 1;
+                sa[i] = split ? (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0) : 0;   // children
+                sb[i] = split ? 0 : 1;                                                       // survivors
+            }
+            if (tid == 0) misc[0] = 0;
+            __syncthreads();
+            int nexp = 0;
+            for (int i = tid; i < n; i += T) {
+                if (A_cnt[i] > 1) {
+                    const int* c4 = cc + 4 * i;
+                    nexp += (c4[0] > 1) + (c4[1] > 1) + (c4[2] > 1) + (c4[3] > 1);
+                }
+            }
+            nexp = wave_sum(nexp);
+            if (lane_id() == 0) atomicAdd(&misc[0], nexp);
+            // keep children counts before the scan overwrites sa
+            for (int i = tid; i < n; i += T) base[i] = sa[i];
+            __syncthreads();
+            const int C = block_scan_array(sa, n, tmp);     // sa = children before node i (creation order)
+            const int U = block_scan_array(sb, n, tmp);     // sb = survivors before node i
+            const int nToExpand = misc[0];
+            const int nn = C + U;
+            if (nn > cap) { if (tid == 0) atomicOr(err, 1); finished = true; break; }
+            for (int i = tid; i < n; i += T) {
+                const int nch = base[i];
+                if (A_cnt[i] > 1) {
+                    const int gb = C - sa[i] - nch;
+                    base[i] = gb;
+                    const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
+                    const int* c4 = cc + 4 * i;
+                    for (int q = 0; q < 4; ++q) {
+                        if (c4[q] == 0) continue;
+                        int cx0, cx1, cy0, cy1;
+                        child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
+                        const int p = gb + rank_desc(c4, q);
+                        B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
+                        B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
+                        B_cnt[p] = c4[q];
+                        B_seq[p] = sa[i] + rank_asc(c4, q);
+                    }
+                } else {
+                    const int p = C + sb[i];
+                    base[i] = p;
+                    B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
+                }
+            }
+            __syncthreads();
+            for (int k = tid; k < K; k += T) {
+                const int i = kn[k];
+                if (A_cnt[i] > 1) {
+                    const int q = quadrant(kxy[k], A_xr[i] & 0xffff, A_xr[i] >> 16, A_yr[i] & 0xffff, A_yr[i] >> 16);
+                    kn[k] = (int16_t)(base[i] + rank_desc(cc + 4 * i, q));
+                } else {
+                    kn[k] = (int16_t)base[i];
+                }
+            }
+            __syncthreads();
+            for (int i = tid; i < nn; i += T) { A_xr[i] = B_xr[i]; A_yr[i] = B_yr[i]; A_cnt[i] = B_cnt[i]; A_seq[i] = B_seq[i]; }
+            n = nn;
+            __syncthreads();
+            if (n >= N || n == prev) finished = true;              // :669-672
+            else if (n + nToExpand * 3 > N) phase2 = true;         // :673
+        } else {
+            // ---------------- phase 2 pass (:676-737)
+            // expandable nodes -> sort keys (size, creation order, node)
+            for (int i = tid; i < n; i += T) sa[i] = A_cnt[i] > 1 ? 1 : 0;
+            __syncthreads();
+            const int nV = block_scan_array(sa, n, tmp);
+            int P2 = 1;
+            while (P2 < nV) P2 <<= 1;
+            for (int i = tid; i < P2; i += T) sk[i] = ~0ull;
+            __syncthreads();
+            for (int i = tid; i < n; i += T)
+                if (A_cnt[i] > 1)
+                    sk[sa[i]] = ((unsigned long long)A_cnt[i] << 40) | ((unsigned long long)A_seq[i] << 20) | (unsigned long long)i;
+            __syncthreads();
+            // bitonic sort ascending
+            for (int kk = 2; kk <= P2; kk <<= 1) {
+                for (int j = kk >> 1; j > 0; j >>= 1) {
+                    for (int i = tid; i < P2; i += T) {
+                        const int ixj = i ^ j;
+                        if (ixj > i) {
+                            const unsigned long long a = sk[i], b = sk[ixj];
+                            const bool up = (i & kk) == 0;
+                            if ((a > b) == up) { sk[i] = b; sk[ixj] = a; }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            // processing order p = 0.. is descending key order; delta_p = children_p - 1
+            for (int p = tid; p < nV; p += T) {
+                const int i = (int)(sk[nV - 1 - p] & 0xfffff);
+                const int* c4 = cc + 4 * i;
+                sb[p] = (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0);
+            }
+            if (tid == 0) misc[1] = nV;          // break index (first p reaching N), nV = none
+            __syncthreads();
+            for (int p = tid; p < nV; p += T) sa[p] = sb[p] - 1;
+            __syncthreads();
+            block_scan_array(sa, nV, tmp);        // exclusive prefix of deltas
+            for (int p = tid; p < nV; p += T)
+                if (n + sa[p] + sb[p] - 1 >= N) atomicMin(&misc[1], p);
+            __syncthreads();
+            const int nproc = min(misc[1] + 1, nV);
+            // children counts prefix over processed nodes (creation order)
+            for (int p = tid; p < nV; p += T) sa[p] = (p < nproc) ? sb[p] : 0;
+            __syncthreads();
+            const int Cn = block_scan_array(sa, nV, tmp);
+            // mark processed nodes: base = group base; survivors ranked after the groups
+            for (int i = tid; i < n; i += T) base[i] = -1;
+            __syncthreads();
+            for (int p = tid; p < nproc; p += T) {
+                const int i = (int)(sk[nV - 1 - p] & 0xfffff);
+                base[i] = Cn - sa[p] - sb[p];
+                A_seq[i] = -1 - sa[p];           // stash creation prefix (node is erased anyway)
+            }
+            __syncthreads();
+            for (int i = tid; i < n; i += T) sb[i] = (base[i] < 0) ? 1 : 0;
+            __syncthreads();
+            const int U = block_scan_array(sb, n, tmp);
+            const int nn = Cn + U;
+            if (nn > cap) { if (tid == 0) atomicOr(err, 1); finished = true; break; }
+            for (int i = tid; i < n; i += T) {
+                if (base[i] >= 0) {
+                    const int gb = base[i];
+                    const int cre = -1 - A_seq[i];
+                    const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
+                    const int* c4 = cc + 4 * i;
+                    for (int q = 0; q < 4; ++q) {
+                        if (c4[q] == 0) continue;
+                        int cx0, cx1, cy0, cy1;
+                        child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
+                        const int p = gb + rank_desc(c4, q);
+                        B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
+                        B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
+                        B_cnt[p] = c4[q];
+                        B_seq[p] = cre + rank_asc(c4, q);
+                    }
+                } else {
+                    const int p = Cn + sb[i];
+                    B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
+                }
+            }
+            __syncthreads();
+            for (int k = tid; k < K; k += T) {
+                const int i = kn[k];
+                if (base[i] >= 0) {
+                    const int q = quadrant(kxy[k], A_xr[i] & 0xffff, A_xr[i] >> 16, A_yr[i] & 0xffff, A_yr[i] >> 16);
+                    kn[k] = (int16_t)(base[i] + rank_desc(cc + 4 * i, q));
+                } else {
+                    kn[k] = (int16_t)(Cn + sb[i]);
+                }
+            }
+            __syncthreads();
+            for (int i = tid; i < nn; i += T) { A_xr[i] = B_xr[i]; A_yr[i] = B_yr[i]; A_cnt[i] = B_cnt[i]; A_seq[i] = B_seq[i]; }
+            n = nn;
+            __syncthreads();
+            if (n >= N || n == prev) finished = true;              // :734-735
+        }
+    }
+
+    // ---- retain the first maximum-response key of every node (:742-760)
+    for (int i = tid; i < n; i += T) sk[i] = 0ull;
+    __syncthreads();
+    for (int k = tid; k < K; k += T) {
+        const unsigned long long v = ((unsigned long long)kr[k] << 32) | (unsigned long long)(0xffffffffu - (uint32_t)k);
+        atomicMax(&sk[kn[k]], v);
+    }
+    __syncthreads();
+    uint32_t* oxy = out_xy + (size_t)img * out_stride + L.out_off;
+    uint8_t* orr = out_r + (size_t)img * out_stride + L.out_off;
+    const int nout = min(n, L.out_cap);
+    for (int i = tid; i < nout; i += T) {
+        const uint32_t k = 0xffffffffu - (uint32_t)(sk[i] & 0xffffffffu);
+        const uint32_t xy = kxy[k];
+        oxy[i] = ((xy & 0xffff) + minB) | (((xy >> 16) + minB) << 16);
+        orr[i] = kr[k];
+    }
+    if (tid == 0) level_cnt[img * nlevels + lvl] = nout;
+}
+
+// ---------------------------------------------------------------------------------------------
+// IC angle + steered BRIEF + output assembly: one wave per keypoint slot.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float fast_atan2_deg(float y, float x) {   // OpenCV fastAtan2 (pinned, :103)
+    const float k = (float)(180.0 / M_PI);
+    const float p1 = __fmul_rn(0.9997878412794807f, k), p3 = __fmul_rn(-0.3258083974640975f, k);
+    const float p5 = __fmul_rn(0.1555786518463281f, k), p7 = __fmul_rn(-0.04432655554792128f, k);
+    const float eps = (float)2.2204460492503131e-016;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = __fdiv_rn(ay, __fadd_rn(ax, eps));
+        c2 = __fmul_rn(c, c);
+        a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
+    } else {
+        c = __fdiv_rn(ax, __fadd_rn(ay, eps));
+        c2 = __fmul_rn(c, c);
+        a = __fsub_rn(90.f, __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c));
+    }
+    if (x < 0) a = __fsub_rn(180.f, a);
+    if (y < 0) a = __fsub_rn(360.f, a);
+    return a;
+}
+
+__global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                                                  size_t pyr_stride, const LevelDev* __restrict__ levels, int nlevels,
+                                                  const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
+                                                  int out_stride, const int* __restrict__ level_cnt,
+                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
+                                                  int capacity, int total_slots) {
+    const int img = blockIdx.y;
+    const int slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int ln = lane_id();
+    if (slot >= total_slots) return;
+    // slot -> (level, index)
+    int lvl = 0;
+    while (lvl + 1 < nlevels && slot >= levels[lvl + 1].out_off) ++lvl;
+    const LevelDev L = levels[lvl];
+    const int i = slot - L.out_off;
+    const int* lc = level_cnt + img * nlevels;
+    int off = 0, total = 0;
+    for (int l = 0; l < nlevels; ++l) {
+        off += (l < lvl) ? lc[l] : 0;
+        total += lc[l];
+    }
+    if (slot == 0 && ln == 0) counts[img] = min(total, capacity);
+    if (i >= lc[lvl]) return;
+    const int o = off + i;
+    if (o >= capacity) return;
+
+    const uint32_t xy = lvl_xy[(size_t)img * out_stride + L.out_off + i];
+    const int cx = (int)(xy & 0xffff), cy = (int)(xy >> 16);
+    // --- IC_Angle (:77-104): m10 = sum u*I, m01 = sum v*I over the radius-15 disc
+    const uint8_t* P = pyr + img * pyr_stride + L.pyr_off;
+    int m10 = 0, m01 = 0;
+    {
+        const int h = ln >> 5, u = (ln & 31) - kHalfPatch;
+        for (int it = 0; it < 16; ++it) {
+            const int v = -kHalfPatch + 2 * it + h;
+            if (v > kHalfPatch || (ln & 31) > 30) continue;
+            const int av = v < 0 ? -v : v;
+            if (u < -c_umax[av] || u > c_umax[av]) continue;
+            const int val = P[(size_t)(cy + v) * L.w + cx + u];
+            m10 += u * val;
+            m01 += v * val;
+        }
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+
+    // --- computeOrbDescriptor (:108-147) on the blurred level
+    const float toRad = (float)(M_PI / 180.f);
+    const float ang = __fmul_rn(angle, toRad);
+    const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+    const uint8_t* B = blur + img * pyr_stride + L.pyr_off;
+    const uint8_t* center = B + (size_t)cy * L.w + cx;
+    const int step = L.w;
+    uint64_t bits[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int t = g * 64 + ln;
+        const signed char* pp = c_pattern + 4 * t;
+        int vals[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float fx = (float)pp[2 * e], fy = (float)pp[2 * e + 1];
+            const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
+            const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
+            vals[e] = center[__float2int_rn(ry) * step + __float2int_rn(rx)];
+        }
+        bits[g] = __ballot(vals[0] < vals[1]);
+    }
+    uint64_t* drow = reinterpret_cast<uint64_t*>(desc + ((size_t)img * capacity + o) * 32);
+    if (ln < 4) drow[ln] = bits[0] * (ln == 0) + bits[1] * (ln == 1) + bits[2] * (ln == 2) + bits[3] * (ln == 3);
+    if (ln == 0) {
+        orbx_keypoint k;
+        float x = (float)cx, y = (float)cy;
+        if (lvl != 0) { x = __fmul_rn(x, L.scale); y = __fmul_rn(y, L.scale); }
+        k.x = x; k.y = y;
+        k.size = (float)L.patch;
+        k.angle = angle;
+        k.response = (float)lvl_r[(size_t)img * out_stride + L.out_off + i];
+        k.octave = lvl;
+        k.class_id = -1;
+        kps[(size_t)img * capacity + o] = k;
+    }
+}
+
+// =============================================================================================
+// host side
+// =============================================================================================
+static int round_even_f(float v) { return (int)std::nearbyintf(v); }
+static int round_even_d(double v) { return (int)std::nearbyint(v); }
+
+enum Stage { ST_COPY = 0, ST_RESIZE, ST_FAST, ST_BLUR, ST_QUADTREE, ST_DESCRIBE, ST_COUNT };
+static const char* kStageNames[ST_COUNT] = {"copy_level0", "resize", "fast_cells", "blur7", "quadtree", "describe"};
+
+struct Extractor {
+    // ORBextractor parameters and tables (:410-470)
+    int nfeatures, nlevels, iniTh, minTh;
+    double scaleFactor;
+    std::vector<float> scale, invScale, sigma2, invSigma2;
+    std::vector<int> nPerLevel;
+    int umax[16];
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+
+    // geometry for the reserved size
+    int rows = 0, cols = 0, max_batch = 0;
+    std::vector<LevelDev> lv;
+    std::vector<CellDev> cellv;
+    std::vector<BlurTile> tilev;
+    size_t pyr_size = 0;      // bytes per image pyramid
+    int cand_stride = 0;      // candidate slots per image
+    int out_stride = 0;       // quadtree output slots per image
+    int node_cap = 0;
+    int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
+    int out_capacity = 0;     // max keypoints per image
+
+    // device buffers
+    LevelDev* d_levels = nullptr;
+    CellDev* d_cells = nullptr;
+    BlurTile* d_tiles = nullptr;
+    std::vector<ResizeTab> rtab;
+    std::vector<void*> rtab_mem;
+    uint8_t* d_pyr = nullptr;
+    uint8_t* d_blur = nullptr;
+    uint32_t* d_cand_xy = nullptr;
+    uint8_t* d_cand_s = nullptr;
+    int* d_cell_cnt = nullptr;
+    uint32_t* d_key_xy = nullptr;
+    uint8_t* d_key_r = nullptr;
+    int16_t* d_key_node = nullptr;
+    uint32_t* d_lvl_xy = nullptr;
+    uint8_t* d_lvl_r = nullptr;
+    int* d_lvl_cnt = nullptr;
+    int* d_err = nullptr;
+    // host-API staging
+    uint8_t* d_in = nullptr;
+    size_t in_bytes = 0;
+    orbx_keypoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int32_t* d_cnt = nullptr;
+    int last_batch = 0;
+
+    // timing: a pool of event sets recorded on the launch stream, resolved lazily (no host sync per call)
+    struct EventSet { hipEvent_t ev[ST_COUNT + 1]; bool pending; };
+    bool timing = false;
+    std::vector<EventSet> tpool;
+    size_t tnext = 0;
+    double stage_ms[ST_COUNT] = {};
+    int timed_calls = 0;
+    int resolve(EventSet& es) {
+        if (!es.pending) return ORBX_OK;
+        ORBX_HIP(hipEventSynchronize(es.ev[ST_COUNT]));
+        for (int k = 0; k < ST_COUNT; ++k) {
+            float ms = 0;
+            ORBX_HIP(hipEventElapsedTime(&ms, es.ev[k], es.ev[k + 1]));
+            stage_ms[k] += ms;
+        }
+        es.pending = false;
+        timed_calls++;
+        return ORBX_OK;
+    }
+
+    void free_buffers();
+    int configure(int r, int c, int batch);
+};
+
+static void compute_tables(Extractor* e) {
+    const int nl = e->nlevels;
+    e->scale.assign(nl, 1.0f);
+    e->sigma2.assign(nl, 1.0f);
+    for (int i = 1; i < nl; ++i) {
+        e->scale[i] = (float)((double)e->scale[i - 1] * e->scaleFactor);
+        e->sigma2[i] = e->scale[i] * e->scale[i];
+    }
+    e->invScale.resize(nl);
+    e->invSigma2.resize(nl);
+    for (int i = 0; i < nl; ++i) {
+        e->invScale[i] = 1.0f / e->scale[i];
+        e->invSigma2[i] = 1.0f / e->sigma2[i];
+    }
+    const float factor = (float)(1.0f / e->scaleFactor);
+    float want = (float)e->nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nl));
+    e->nPerLevel.assign(nl, 0);
+    int acc = 0;
+    for (int l = 0; l < nl - 1; ++l) {
+        e->nPerLevel[l] = round_even_f(want);
+        acc += e->nPerLevel[l];
+        want *= factor;
+    }
+    e->nPerLevel[nl - 1] = std::max(e->nfeatures - acc, 0);
+    const int R = kHalfPatch;
+    const int vmax = (int)std::floor(R * std::sqrt(2.f) / 2 + 1);
+    const int vmin = (int)std::ceil(R * std::sqrt(2.f) / 2);
+    for (int v = 0; v <= vmax; ++v) e->umax[v] = round_even_d(std::sqrt((double)R * R - v * v));
+    for (int v = R, v0 = 0; v >= vmin; --v) {
+        while (e->umax[v0] == e->umax[v0 + 1]) ++v0;
+        e->umax[v] = v0;
+        ++v0;
+    }
+}
+
+static void level_dims(const Extractor* e, int rows, int cols, int l, int* w, int* h) {
+    *w = round_even_f((float)cols * e->invScale[l]);
+    *h = round_even_f((float)rows * e->invScale[l]);
+}
+
+void Extractor::free_buffers() {
+    auto F = [](auto*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } };
+    F(d_levels); F(d_cells); F(d_tiles); F(d_pyr); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
+    F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
+    F(d_kps); F(d_desc); F(d_cnt);
+    for (void* p : rtab_mem) (void)hipFree(p);
+    rtab_mem.clear();
+    rtab.clear();
+    rows = cols = max_batch = 0;
+    in_bytes = 0;
+}
+
+static size_t qt_lds_bytes(int cap, int scan_cap);
+
+template <typename T>
+static int dev_alloc(T** p, size_t count) {
+    ORBX_HIP(hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T)));
+    return ORBX_OK;
+}
+
+int Extractor::configure(int r, int c, int batch) {
+    if (r == rows && c == cols && batch <= max_batch) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(device));
+    if (stream) ORBX_HIP(hipStreamSynchronize(stream));
+    const int keep_batch = std::max(batch, (r == rows && c == cols) ? max_batch : 0);
+    free_buffers();
+    ORBX_REQUIRE(r > 0 && c > 0 && batch > 0, ORBX_ERR_ARG, "configure: bad size %dx%d batch %d", r, c, batch);
+    ORBX_REQUIRE(c < 32768 && r < 32768, ORBX_ERR_UNSUPPORTED, "image too large (%dx%d)", r, c);
+    batch = keep_batch;
+
+    // ---- level geometry, cells (ComputeKeyPointsOctTree :771-807), DistributeOctTree roots (:543-545)
+    lv.assign(nlevels, LevelDev{});
+    cellv.clear();
+    tilev.clear();
+    size_t poff = 0;
+    int cand = 0, outs = 0, cap = 4;
+    for (int l = 0; l < nlevels; ++l) {
+        LevelDev& L = lv[l];
+        level_dims(this, r, c, l, &L.w, &L.h);
+        ORBX_REQUIRE(L.w > 0 && L.h > 0, ORBX_ERR_UNSUPPORTED, "level %d is empty for %dx%d", l, r, c);
+        L.pyr_off = (int)poff;
+        poff += (size_t)L.w * L.h;
+        L.scale = scale[l];
+        L.patch = (int)(31 * scale[l]);
+        L.N = nPerLevel[l];
+        const int minB = kEdge - 3, maxBX = L.w - kEdge + 3, maxBY = L.h - kEdge + 3;
+        L.win_w = maxBX - minB;
+        L.win_h = maxBY - minB;
+        L.cell_begin = (int)cellv.size();
+        L.cand_off = cand;
+        const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
+        const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
+        if (nCols > 0 && nRows > 0 && L.win_w > 0 && L.win_h > 0) {
+            const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+            for (int i = 0; i < nRows; ++i) {
+                const float iniY = (float)(minB + i * hCell);
+                float maxY = iniY + hCell + 6;
+                if (iniY >= maxBY - 3) continue;
+                if (maxY > maxBY) maxY = (float)maxBY;
+                for (int j = 0; j < nCols; ++j) {
+                    const float iniX = (float)(minB + j * wCell);
+                    float maxX = iniX + wCell + 6;
+                    if (iniX >= maxBX - 6) continue;
+                    if (maxX > maxBX) maxX = (float)maxBX;
+                    CellDev cd{};
+                    cd.level = l;
+                    cd.x0 = (int)iniX; cd.y0 = (int)iniY;
+                    cd.W = (int)maxX - cd.x0; cd.H = (int)maxY - cd.y0;
+                    ORBX_REQUIRE(cd.W <= kMaxRoi && cd.H <= kMaxRoi, ORBX_ERR_UNSUPPORTED, "cell ROI too large");
+                    const int wd = std::max(cd.W - 6, 0), hd = std::max(cd.H - 6, 0);
+                    cd.slot_cap = ((wd + 1) / 2) * ((hd + 1) / 2);   // strict 3x3 NMS: <= 1 per 2x2 block
+                    cd.slot_off = cand;
+                    cand += cd.slot_cap;
+                    cellv.push_back(cd);
+                }
+            }
+        }
+        L.cell_end = (int)cellv.size();
+        L.cand_cap = cand - L.cand_off;
+        ORBX_REQUIRE(L.cand_cap < (1 << 20), ORBX_ERR_UNSUPPORTED, "too many FAST candidates per level");
+        if (L.win_w > 0 && L.win_h > 0) {
+            // nIni = 0 (window more than twice as tall as wide) is undefined in the reference; pinned to 1
+            L.nIni = std::max(1, (int)std::round((float)(maxBX - minB) / (maxBY - minB)));
+            L.hX = (float)(maxBX - minB) / L.nIni;
+        } else {
+            L.nIni = 1; L.hX = 1.f;
+        }
+        L.out_cap = std::max(L.N + 3, 4 * L.nIni + 1);
+        L.out_off = outs;
+        outs += L.out_cap;
+        cap = std::max(cap, L.out_cap);
+        // blur tiles
+        for (int ty = 0; ty < (L.h + 15) / 16; ++ty)
+            for (int tx = 0; tx < (L.w + 63) / 64; ++tx) tilev.push_back(BlurTile{l, tx, ty, 0});
+    }
+    ORBX_REQUIRE(cap < 32768 && cap < (1 << 20), ORBX_ERR_UNSUPPORTED, "node capacity %d too large", cap);
+    int scap = cap;
+    for (const LevelDev& L : lv) scap = std::max(scap, std::max(L.cell_end - L.cell_begin, L.nIni));
+    scan_cap = scap + 1;
+    {
+        const size_t lds = qt_lds_bytes(cap, scan_cap);
+        ORBX_REQUIRE(lds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "quadtree LDS %zu B exceeds 160 KiB", lds);
+        if (lds > 64 * 1024)
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
+    pyr_size = (poff + 255) & ~(size_t)255;
+    cand_stride = std::max(cand, 1);
+    out_stride = outs;
+    node_cap = cap;
+    out_capacity = outs;
+    rows = r; cols = c; max_batch = batch;
+
+    int st;
+    if ((st = dev_alloc(&d_levels, nlevels))) return st;
+    if ((st = dev_alloc(&d_cells, cellv.size()))) return st;
+    if ((st = dev_alloc(&d_tiles, tilev.size()))) return st;
+    ORBX_HIP(hipMemcpy(d_levels, lv.data(), sizeof(LevelDev) * nlevels, hipMemcpyHostToDevice));
+    if (!cellv.empty()) ORBX_HIP(hipMemcpy(d_cells, cellv.data(), sizeof(CellDev) * cellv.size(), hipMemcpyHostToDevice));
+    ORBX_HIP(hipMemcpy(d_tiles, tilev.data(), sizeof(BlurTile) * tilev.size(), hipMemcpyHostToDevice));
+
+    // ---- resize tables (pinned OpenCV 3.2 INTER_LINEAR fixed point), level l from level l-1
+    rtab.assign(nlevels, ResizeTab{});
+    for (int l = 1; l < nlevels; ++l) {
+        const int sw = lv[l - 1].w, sh = lv[l - 1].h, dw = lv[l].w, dh = lv[l].h;
+        const double sxs = 1.0 / ((double)dw / sw), sys = 1.0 / ((double)dh / sh);
+        std::vector<int> hx0(dw), hx1(dw), ha0(dw), ha1(dw), hy0(dh), hy1(dh), hb0(dh), hb1(dh);
+        int xlim = dw;
+        for (int x = 0; x < dw; ++x) {
+            float fx = (float)((x + 0.5) * sxs - 0.5);
+            int ix = (int)std::floor(fx);
+            fx -= ix;
+            if (ix < 0) { fx = 0; ix = 0; }
+            if (ix + 1 >= sw) {
+                xlim = std::min(xlim, x);
+                if (ix >= sw - 1) { fx = 0; ix = sw - 1; }
+            }
+            hx0[x] = ix;
+            hx1[x] = std::min(ix + 1, sw - 1);
+            ha0[x] = std::min(std::max(round_even_f((1.f - fx) * 2048), -32768), 32767);
+            ha1[x] = std::min(std::max(round_even_f(fx * 2048), -32768), 32767);
+        }
+        for (int x = xlim; x < dw; ++x) { ha0[x] = 2048; ha1[x] = 0; hx1[x] = hx0[x]; }
+        for (int y = 0; y < dh; ++y) {
+            float fy = (float)((y + 0.5) * sys - 0.5);
+            int iy = (int)std::floor(fy);
+            fy -= iy;
+            hb0[y] = std::min(std::max(round_even_f((1.f - fy) * 2048), -32768), 32767);
+            hb1[y] = std::min(std::max(round_even_f(fy * 2048), -32768), 32767);
+            hy0[y] = std::min(std::max(iy, 0), sh - 1);
+            hy1[y] = std::min(std::max(iy + 1, 0), sh - 1);
+        }
+        int* mem;
+        if ((st = dev_alloc(&mem, 4 * (size_t)dw + 4 * (size_t)dh))) return st;
+        rtab_mem.push_back(mem);
+        ResizeTab t;
+        t.x0 = mem; t.x1 = mem + dw; t.a0 = mem + 2 * dw; t.a1 = mem + 3 * dw;
+        t.y0 = mem + 4 * dw; t.y1 = t.y0 + dh; t.b0 = t.y1 + dh; t.b1 = t.b0 + dh;
+        std::vector<int> host;
+        host.reserve(4 * dw + 4 * dh);
+        for (auto* v : {&hx0, &hx1, &ha0, &ha1, &hy0, &hy1, &hb0, &hb1}) host.insert(host.end(), v->begin(), v->end());
+        ORBX_HIP(hipMemcpy(mem, host.data(), host.size() * sizeof(int), hipMemcpyHostToDevice));
+        rtab[l] = t;
+    }
+
+    // ---- batch buffers (HBM): pyramid + blurred pyramid + candidates + quadtree scratch
+    const size_t B = (size_t)batch;
+    if ((st = dev_alloc(&d_pyr, B * pyr_size))) return st;
+    if ((st = dev_alloc(&d_blur, B * pyr_size))) return st;
+    if ((st = dev_alloc(&d_cand_xy, B * cand_stride))) return st;
+    if ((st = dev_alloc(&d_cand_s, B * cand_stride))) return st;
+    if ((st = dev_alloc(&d_cell_cnt, B * std::max<size_t>(cellv.size(), 1)))) return st;
+    if ((st = dev_alloc(&d_key_xy, B * cand_stride))) return st;
+    if ((st = dev_alloc(&d_key_r, B * cand_stride))) return st;
+    if ((st = dev_alloc(&d_key_node, B * cand_stride))) return st;
+    if ((st = dev_alloc(&d_lvl_xy, B * out_stride))) return st;
+    if ((st = dev_alloc(&d_lvl_r, B * out_stride))) return st;
+    if ((st = dev_alloc(&d_lvl_cnt, B * nlevels))) return st;
+    if ((st = dev_alloc(&d_err, 1))) return st;
+    ORBX_HIP(hipMemset(d_err, 0, sizeof(int)));
+    ORBX_HIP(hipMemset(d_cell_cnt, 0, sizeof(int) * B * std::max<size_t>(cellv.size(), 1)));
+    return ORBX_OK;
+}
+
+static size_t qt_lds_bytes(int cap, int scan_cap) {
+    int p2 = 1;
+    while (p2 < cap) p2 <<= 1;
+    const size_t ints = 8 * (size_t)cap + 4 * (size_t)cap + (size_t)cap + 2 * (size_t)scan_cap + 32 + 16 + 2;
+    return ints * 4 + (size_t)p2 * 8;
+}
+
+static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t step, size_t istride,
+                     orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int capacity, hipStream_t s) {
+    const int nl = e->nlevels;
+    const size_t ps = e->pyr_size;
+    Extractor::EventSet* es = nullptr;
+    if (e->timing && !e->tpool.empty()) {
+        es = &e->tpool[e->tnext++ % e->tpool.size()];
+        int st = e->resolve(*es);
+        if (st) return st;
+        es->pending = true;
+    }
+    auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], s); };
+    mark(0);
+    {
+        dim3 g((e->lv[0].w + 255) / 256, e->lv[0].h, batch);
+        hipLaunchKernelGGL(k_copy_level0, g, dim3(256), 0, s, d_images, step, istride, e->d_pyr, ps, e->lv[0].w, e->lv[0].h);
+    }
+    mark(1);
+    for (int l = 1; l < nl; ++l) {
+        dim3 g((e->lv[l].w + 255) / 256, e->lv[l].h, batch);
+        hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, e->d_pyr, ps, e->lv[l - 1].pyr_off, e->lv[l - 1].w,
+                           e->lv[l].pyr_off, e->lv[l].w, e->lv[l].h, e->rtab[l]);
+    }
+    mark(2);
+    const int ncells = (int)e->cellv.size();
+    if (ncells > 0) {
+        dim3 g(ncells, batch);
+        hipLaunchKernelGGL(k_fast_cells, g, dim3(256), 0, s, e->d_pyr, ps, e->d_levels, e->d_cells, e->iniTh, e->minTh,
+                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells);
+    }
+    mark(3);
+    {
+        dim3 g((unsigned)e->tilev.size(), batch);
+        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles);
+    }
+    mark(4);
+    {
+        QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
+        dim3 g(nl, batch);
+        hipLaunchKernelGGL(k_quadtree, g, dim3(kQtThreads), qt_lds_bytes(e->node_cap, e->scan_cap), s, e->d_levels, e->d_cells,
+                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
+                           e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err);
+    }
+    mark(5);
+    {
+        const int total_slots = e->out_stride;
+        dim3 g((total_slots * 64 + 255) / 256, batch);
+        hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
+                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, total_slots);
+    }
+    mark(6);
+    ORBX_HIP(hipGetLastError());
+    e->last_batch = batch;
+    return ORBX_OK;
+}
+
+static std::once_flag g_const_once;
+static int g_const_status = ORBX_OK;
+
+static int upload_constants(const Extractor* e) {
+    // pattern is a fixed table; umax is the same for every extractor (depends only on HALF_PATCH_SIZE)
+    ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)));
+    ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), e->umax, sizeof(int) * 16));
+    return ORBX_OK;
+}
+
+}  // namespace orbx
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+using namespace orbx;
+
+struct orbx_extractor : public orbx::Extractor {};
+
+extern "C" {
+
+const char* orbx_last_error(void) { return orbx::g_err.c_str(); }
+const char* orbx_version(void) { return "orbx 0.1 (gfx950)"; }
+int orbx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST, int device,
+                          orbx_extractor** out) {
+    ORBX_REQUIRE(out, ORBX_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    ORBX_REQUIRE(nfeatures >= 0 && nlevels >= 1 && nlevels <= kMaxLevels && scaleFactor > 1.0f, ORBX_ERR_ARG,
+                 "bad extractor parameters");
+    int ndev = 0;
+    ORBX_HIP(hipGetDeviceCount(&ndev));
+    ORBX_REQUIRE(device >= 0 && device < ndev, ORBX_ERR_ARG, "device %d out of range (%d devices)", device, ndev);
+    orbx_extractor* e = new orbx_extractor();
+    e->nfeatures = nfeatures;
+    e->nlevels = nlevels;
+    e->iniTh = iniThFAST;
+    e->minTh = minThFAST;
+    e->scaleFactor = (double)scaleFactor;
+    e->device = device;
+    compute_tables(e);
+    hipError_t he = hipSetDevice(device);
+    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he != hipSuccess) {
+        set_error("stream create: %s", hipGetErrorString(he));
+        delete e;
+        return ORBX_ERR_HIP;
+    }
+    e->own_stream = true;
+    std::call_once(g_const_once, [&] { g_const_status = upload_constants(e); });
+    if (g_const_status != ORBX_OK) {
+        (void)hipStreamDestroy(e->stream);
+        delete e;
+        return g_const_status;
+    }
+    *out = e;
+    return ORBX_OK;
+}
+
+int orbx_extractor_destroy(orbx_extractor* e) {
+    if (!e) return ORBX_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    e->free_buffers();
+    for (auto& es : e->tpool)
+        for (auto& ev : es.ev) (void)hipEventDestroy(ev);
+    if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return ORBX_OK;
+}
+
+int orbx_extractor_get_levels(const orbx_extractor* e) { return e ? e->nlevels : ORBX_ERR_ARG; }
+float orbx_extractor_get_scale_factor(const orbx_extractor* e) { return e ? (float)e->scaleFactor : 0.f; }
+
+static int copy_vec(const std::vector<float>& v, float* out) {
+    ORBX_REQUIRE(out, ORBX_ERR_ARG, "out is NULL");
+    std::memcpy(out, v.data(), v.size() * sizeof(float));
+    return ORBX_OK;
+}
+int orbx_extractor_get_scale_factors(const orbx_extractor* e, float* out) {
+    ORBX_REQUIRE(e, ORBX_ERR_ARG, "null extractor");
+    return copy_vec(e->scale, out);
+}
+int orbx_extractor_get_inverse_scale_factors(const orbx_extractor* e, float* out) {
+    ORBX_REQUIRE(e, ORBX_ERR_ARG, "null extractor");
+    return copy_vec(e->invScale, out);
+}
+int orbx_extractor_get_scale_sigma_squares(const orbx_extractor* e, float* out) {
+    ORBX_REQUIRE(e, ORBX_ERR_ARG, "null extractor");
+    return copy_vec(e->sigma2, out);
+}
+int orbx_extractor_get_inverse_scale_sigma_squares(const orbx_extractor* e, float* out) {
+    ORBX_REQUIRE(e, ORBX_ERR_ARG, "null extractor");
+    return copy_vec(e->invSigma2, out);
+}
+int orbx_extractor_get_features_per_level(const orbx_extractor* e, int* out) {
+    ORBX_REQUIRE(e && out, ORBX_ERR_ARG, "null argument");
+    std::memcpy(out, e->nPerLevel.data(), e->nPerLevel.size() * sizeof(int));
+    return ORBX_OK;
+}
+
+int orbx_extractor_reserve(orbx_extractor* e, int rows, int cols, int max_batch) {
+    ORBX_REQUIRE(e, ORBX_ERR_ARG, "null extractor");
+    return e->configure(rows, cols, max_batch);
+}
+
+int orbx_extractor_max_keypoints(orbx_extractor* e, int rows, int cols) {
+    ORBX_REQUIRE(e, ORBX_ERR_ARG, "null extractor");
+    int st = e->configure(rows, cols, std::max(e->max_batch, 1));
+    if (st) return st;
+    return e->out_capacity;
+}
+
+int orbx_extractor_level_sizes(orbx_extractor* e, int rows, int cols, int* lr, int* lc) {
+    ORBX_REQUIRE(e && lr && lc, ORBX_ERR_ARG, "null argument");
+    for (int l = 0; l < e->nlevels; ++l) level_dims(e, rows, cols, l, &lc[l], &lr[l]);
+    return ORBX_OK;
+}
+
+int orbx_extract_batch_device(orbx_extractor* e, const uint8_t* d_images, int batch, int rows, int cols, size_t step,
+                              size_t image_stride, orbx_keypoint* d_keypoints, uint8_t* d_descriptors, int32_t* d_counts,
+                              int capacity, void* stream) {
+    ORBX_REQUIRE(e && d_images && d_keypoints && d_descriptors && d_counts, ORBX_ERR_ARG, "null argument");
+    ORBX_REQUIRE(batch > 0 && rows > 0 && cols > 0 && step >= (size_t)cols, ORBX_ERR_ARG, "bad batch geometry");
+    ORBX_HIP(hipSetDevice(e->device));
+    int st = e->configure(rows, cols, batch);
+    if (st) return st;
+    ORBX_REQUIRE(capacity >= e->out_capacity, ORBX_ERR_CAPACITY, "capacity %d < required %d", capacity, e->out_capacity);
+    hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
+    return run_batch(e, d_images, batch, step, image_stride, d_keypoints, d_descriptors, d_counts, capacity, s);
+}
+
+int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, size_t step, orbx_keypoint* kps,
+                 uint8_t* desc, int capacity, int* n_out) {
+    ORBX_REQUIRE(e && n_out, ORBX_ERR_ARG, "null argument");
+    *n_out = 0;
+    if (!image || rows <= 0 || cols <= 0) return ORBX_OK;   // _image.empty() -> return (:1046-1047)
+    ORBX_REQUIRE(step >= (size_t)cols, ORBX_ERR_ARG, "step < cols");
+    ORBX_HIP(hipSetDevice(e->device));
+    int st = e->configure(rows, cols, std::max(e->max_batch, 1));
+    if (st) return st;
+    const size_t nb = (size_t)rows * cols;
+    if (e->in_bytes < nb) {
+        if (e->d_in) (void)hipFree(e->d_in);
+        e->d_in = nullptr;
+        if ((st = dev_alloc(&e->d_in, nb))) return st;
+        e->in_bytes = nb;
+    }
+    if (!e->d_kps) {
+        if ((st = dev_alloc(&e->d_kps, e->out_capacity))) return st;
+        if ((st = dev_alloc(&e->d_desc, (size_t)e->out_capacity * 32))) return st;
+        if ((st = dev_alloc(&e->d_cnt, 1))) return st;
+    }
+    ORBX_HIP(hipMemcpy2DAsync(e->d_in, cols, image, step, cols, rows, hipMemcpyHostToDevice, e->stream));
+    st = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, e->stream);
+    if (st) return st;
+    int n = 0, err = 0;
+    ORBX_HIP(hipMemcpyAsync(&n, e->d_cnt, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    ORBX_HIP(hipMemcpyAsync(&err, e->d_err, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    ORBX_HIP(hipStreamSynchronize(e->stream));
+    ORBX_REQUIRE(err == 0, ORBX_ERR_UNSUPPORTED, "quadtree node capacity exceeded (err=%d)", err);
+    *n_out = n;
+    if (n > capacity) {
+        set_error("capacity %d < %d keypoints", capacity, n);
+        return ORBX_ERR_CAPACITY;
+    }
+    if (n > 0) {
+        ORBX_REQUIRE(kps && desc, ORBX_ERR_ARG, "null output buffers");
+        ORBX_HIP(hipMemcpyAsync(kps, e->d_kps, sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, e->stream));
+        ORBX_HIP(hipMemcpyAsync(desc, e->d_desc, (size_t)n * 32, hipMemcpyDeviceToHost, e->stream));
+        ORBX_HIP(hipStreamSynchronize(e->stream));
+    }
+    return ORBX_OK;
+}
+
+int orbx_extractor_level_device(orbx_extractor* e, int index, int level, const uint8_t** d_level, int* rows, int* cols) {
+    ORBX_REQUIRE(e && d_level && rows && cols, ORBX_ERR_ARG, "null argument");
+    ORBX_REQUIRE(e->d_pyr && level >= 0 && level < e->nlevels && index >= 0 && index < e->max_batch, ORBX_ERR_ARG,
+                 "no pyramid for index %d level %d", index, level);
+    *d_level = e->d_pyr + (size_t)index * e->pyr_size + e->lv[level].pyr_off;
+    *rows = e->lv[level].h;
+    *cols = e->lv[level].w;
+    return ORBX_OK;
+}
+
+int orbx_extractor_copy_level(orbx_extractor* e, int index, int level, uint8_t* dst, size_t dst_step) {
+    const uint8_t* p;
+    int r, c;
+    int st = orbx_extractor_level_device(e, index, level, &p, &r, &c);
+    if (st) return st;
+    ORBX_REQUIRE(dst && dst_step >= (size_t)c, ORBX_ERR_ARG, "bad destination");
+    ORBX_HIP(hipSetDevice(e->device));
+    ORBX_HIP(hipMemcpy2DAsync(dst, dst_step, p, c, c, r, hipMemcpyDeviceToHost, e->stream));
+    ORBX_HIP(hipStreamSynchronize(e->stream));
+    return ORBX_OK;
+}
+
+int orbx_extractor_enable_timing(orbx_extractor* e, int enable) {
+    ORBX_REQUIRE(e, ORBX_ERR_ARG, "null extractor");
+    ORBX_HIP(hipSetDevice(e->device));
+    for (auto& es : e->tpool) es.pending = false;
+    if (enable && e->tpool.empty()) {
+        e->tpool.resize(64);
+        for (auto& es : e->tpool) {
+            es.pending = false;
+            for (auto& ev : es.ev) ORBX_HIP(hipEventCreate(&ev));
+        }
+    }
+    e->timing = enable != 0;
+    for (double& v : e->stage_ms) v = 0;
+    e->timed_calls = 0;
+    return ORBX_OK;
+}
+int orbx_extractor_stage_count(void) { return ST_COUNT; }
+const char* orbx_extractor_stage_name(int s) { return (s >= 0 && s < ST_COUNT) ? kStageNames[s] : ""; }
+int orbx_extractor_stage_times(orbx_extractor* e, double* ms, int* calls) {
+    ORBX_REQUIRE(e && ms, ORBX_ERR_ARG, "null argument");
+    ORBX_HIP(hipSetDevice(e->device));
+    for (auto& es : e->tpool) {
+        int st = e->resolve(es);
+        if (st) return st;
+    }
+    for (int k = 0; k < ST_COUNT; ++k) ms[k] = e->stage_ms[k];
+    if (calls) *calls = e->timed_calls;
+    return ORBX_OK;
+}
+
+}  // extern "C"

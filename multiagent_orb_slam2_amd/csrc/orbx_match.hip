@@ -1,0 +1,788 @@
+// =====================================================================================================
+// orbx_match.hip — MI355X (gfx950) 256-bit Hamming matchers behind include/orbx.h.
+//
+//   k_hamming_pairs     ORBmatcher::DescriptorDistance over n row pairs        (src/ORBmatcher.cc:1649-1665)
+//   k_bf_tile/k_bf_merge tiled all-pairs match: 64 queries per workgroup (one per lane, descriptor in
+//                        8 VGPRs), train descriptors staged through LDS in 256-row blocks and read as
+//                        wave-uniform broadcasts; v_xor + v_bcnt_u32_b32; per-(query, train-chunk)
+//                        partial best/second merged by a second launch.  No MFMA: popcount-bound.
+//   k_stereo            Frame::ComputeStereoMatches descriptor search (src/Frame.cc:466-552), one wave
+//                        per left keypoint, band/octave/disparity mask, packed (dist, index) wave min.
+//   k_bow_kfkf / k_bow_kff / k_triangulate   BoW-bucketed matchers (src/ORBmatcher.cc:161-290, 524-657,
+//                        659-825): one wave per FeatureVector node of the first view; the greedy
+//                        "already matched" state is node-local (a feature belongs to one node), so the
+//                        wave walks the node's queries in order with lanes over the candidates.
+//   k_rot_filter        rotation-consistency histogram + ComputeThreeMaxima (src/ORBmatcher.cc:1603-1644).
+// =====================================================================================================
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "orbx_common.h"
+
+namespace orbx {
+
+constexpr int kThHigh = 100, kThLow = 50, kHisto = 30;   // src/ORBmatcher.cc:37-39
+
+__device__ __forceinline__ void load_desc(const uint8_t* p, uint4& a, uint4& b) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    a = q[0];
+    b = q[1];
+}
+
+__global__ __launch_bounds__(256) void k_hamming_pairs(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int n,
+                                                       int32_t* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint4 a0, a1, b0, b1;
+    load_desc(a + 32 * (size_t)i, a0, a1);
+    load_desc(b + 32 * (size_t)i, b0, b1);
+    out[i] = hamming256(a0, a1, b0, b1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// all-pairs brute force
+// ---------------------------------------------------------------------------------------------
+constexpr int kBfQ = 256;      // queries per workgroup (4 waves, one query per lane)
+constexpr int kBfStage = 256;  // train rows staged in LDS per step (8 KB)
+
+// partial record: best (dist << 20 | train idx), second dist
+__global__ __launch_bounds__(256) void k_bf_tile(const uint8_t* __restrict__ q, int nq, const uint8_t* __restrict__ t, int nt,
+                                                 int chunk, uint32_t* __restrict__ pbest, int32_t* __restrict__ psecond) {
+    __shared__ uint4 tile[kBfStage * 2];
+    const int qi = blockIdx.x * kBfQ + threadIdx.x;
+    const int c = blockIdx.y;
+    const int t0 = c * chunk, t1 = min(nt, t0 + chunk);
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    if (qi < nq) load_desc(q + 32 * (size_t)qi, a0, a1);
+    uint32_t best = 256u << 20;   // a distance of 256 never updates (init 256, strict <)
+    int second = 256;
+    for (int s = t0; s < t1; s += kBfStage) {
+        const int cnt = min(kBfStage, t1 - s);
+        __syncthreads();
+        for (int r = threadIdx.x; r < cnt * 2; r += blockDim.x)
+            tile[r] = reinterpret_cast<const uint4*>(t + 32 * (size_t)s)[r];
+        __syncthreads();
+#pragma unroll 4
+        for (int j = 0; j < cnt; ++j) {
+            const int d = hamming256(a0, a1, tile[2 * j], tile[2 * j + 1]);
+            const uint32_t key = ((uint32_t)d << 20) | (uint32_t)(s + j);
+            // reference update: d < best -> (second = best, best = d); else d < second -> second = d
+            const uint32_t bd = best >> 20;
+            if (key < best) {          // same as d < bd, since indices grow
+                second = (int)bd;
+                best = key;
+            } else if (d < second) {
+                second = d;
+            }
+        }
+    }
+    if (qi < nq) {
+        pbest[(size_t)c * nq + qi] = best;
+        psecond[(size_t)c * nq + qi] = second;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_bf_merge(const uint32_t* __restrict__ pbest, const int32_t* __restrict__ psecond,
+                                                  int nq, int nchunks, int32_t* __restrict__ best_idx,
+                                                  int32_t* __restrict__ best_dist, int32_t* __restrict__ second_dist) {
+    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (qi >= nq) return;
+    uint32_t best = 256u << 20;
+    int second = 256;
+    for (int c = 0; c < nchunks; ++c) {   // chunks in ascending train order: same rule as a sequential scan
+        const uint32_t b = pbest[(size_t)c * nq + qi];
+        const int s = psecond[(size_t)c * nq + qi];
+        const int bd = (int)(best >> 20), cd = (int)(b >> 20);
+        if (cd < bd) {
+            second = min(bd, s);
+            best = b;
+        } else {
+            second = min(second, cd);   // the chunk's best is a non-improving value: d >= best
+            second = min(second, s);
+        }
+    }
+    const int bd = (int)(best >> 20);
+    best_dist[qi] = bd;
+    best_idx[qi] = bd < 256 ? (int)(best & 0xfffff) : -1;
+    second_dist[qi] = second;
+}
+
+// ---------------------------------------------------------------------------------------------
+// stereo band match
+// ---------------------------------------------------------------------------------------------
+struct StereoArgs {
+    const orbx_keypoint* kl; const uint8_t* dl; const int32_t* nl;
+    const orbx_keypoint* kr; const uint8_t* dr; const int32_t* nr;
+    int capacity;           // per-image stride of the batched layout
+    int nl_fixed, nr_fixed; // used when nl/nr are null
+    float scale[32];
+    int nlevels, rows;
+    float maxD;             // bf / b (Frame.cc:496-498)
+    int32_t* best_idx; int32_t* best_dist;
+};
+
+__global__ __launch_bounds__(256) void k_stereo(StereoArgs A) {
+    const int img = blockIdx.y;
+    const int iL = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int ln = lane_id();
+    const int nl = A.nl ? A.nl[img] : A.nl_fixed;
+    const int nr = A.nr ? A.nr[img] : A.nr_fixed;
+    if (iL >= nl) return;
+    const size_t ob = (size_t)img * A.capacity;
+    const orbx_keypoint kL = A.kl[ob + iL];
+    const int vrow = (int)kL.y;                      // vRowIndices[vL] (:511)
+    const float uL = kL.x;
+    const float minU = uL - A.maxD, maxU = uL - 0.0f;
+    uint32_t best = 0xffffffffu;
+    if (vrow >= 0 && vrow < A.rows && !(maxU < 0)) {
+        uint4 a0, a1;
+        load_desc(A.dl + 32 * (ob + iL), a0, a1);
+        for (int iR = ln; iR < nr; iR += kWave) {
+            const orbx_keypoint kR = A.kr[ob + iR];
+            const float r = 2.0f * A.scale[kR.octave];                       // :487
+            const int maxr = (int)ceilf(kR.y + r), minr = (int)floorf(kR.y - r);
+            if (vrow < minr || vrow > maxr) continue;                        // row band (:491-492)
+            if (kR.octave < kL.octave - 1 || kR.octave > kL.octave + 1) continue;   // :533
+            if (!(kR.x >= minU && kR.x <= maxU)) continue;                   // :538
+            uint4 b0, b1;
+            load_desc(A.dr + 32 * (ob + iR), b0, b1);
+            const uint32_t key = ((uint32_t)hamming256(a0, a1, b0, b1) << 20) | (uint32_t)iR;
+            best = min(best, key);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+    if (ln == 0) {
+        int d = (best == 0xffffffffu) ? kThHigh : (int)(best >> 20);
+        d = min(d, kThHigh);                                                // init TH_HIGH, strict < (:522-547)
+        const int thOrb = (kThHigh + kThLow) / 2;                           // :471
+        A.best_dist[ob + iL] = d;
+        A.best_idx[ob + iL] = (d < thOrb) ? (int)(best & 0xfffff) : -1;    // :552
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// BoW-bucketed matchers
+// ---------------------------------------------------------------------------------------------
+struct FvDev { const uint32_t* node; const int32_t* off; int n; const int32_t* idx; };
+
+__device__ __forceinline__ int fv_lower_bound(const FvDev& f, uint32_t id) {
+    int lo = 0, hi = f.n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (f.node[mid] < id) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ int rot_bin(float a1, float a2) {   // src/ORBmatcher.cc:609-614
+    float rot = __fsub_rn(a1, a2);
+    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+    int bin = (int)roundf(__fmul_rn(rot, 1.0f / kHisto));
+    if (bin == kHisto) bin = 0;
+    return bin;
+}
+
+// best (lowest position on ties) and multiset-second over one wave's candidates; values 256 = none
+__device__ __forceinline__ void wave_best2(int d, int pos, int& b1, int& bpos, int& b2) {
+    uint32_t key = ((uint32_t)d << 20) | (uint32_t)pos;
+    uint32_t m = key;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, kWave));
+    b1 = (int)(m >> 20);
+    bpos = (int)(m & 0xfffff);
+    int s = (key == m) ? 256 : d;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s = min(s, __shfl_xor(s, o, kWave));
+    b2 = s;
+}
+
+struct BowArgs {
+    // view 1 (queries) and view 2 (candidates)
+    const uint8_t* d1; const float* a1; const uint8_t* v1; FvDev f1;
+    const uint8_t* d2; const float* a2; const uint8_t* v2; FvDev f2;
+    float nnratio;
+    int checkOri;
+    int kff;               // 0: KF-KF (TH_LOW strict, greedy on view-2 index, result indexed by view 1)
+                           // 1: KF-F  (TH_LOW inclusive, greedy on frame index, result indexed by frame)
+    int32_t* match;        // KF-KF: [n1] -> idx2; KF-F: [n2] -> idx1
+    int32_t* bin;          // rotation bin per result index
+    int32_t* hist;         // [30]
+    int32_t* nmatch;
+};
+
+// one wave per node of view 1
+__global__ __launch_bounds__(64) void k_bow(BowArgs A) {
+    __shared__ uint8_t taken[4096];
+    const int a = blockIdx.x, ln = lane_id();
+    if (a >= A.f1.n) return;
+    const uint32_t id = A.f1.node[a];
+    const int b = fv_lower_bound(A.f2, id);
+    if (b >= A.f2.n || A.f2.node[b] != id) return;
+    const int q0 = A.f1.off[a], q1 = A.f1.off[a + 1];
+    const int c0 = A.f2.off[b], c1 = A.f2.off[b + 1];
+    const int nc = c1 - c0;
+    for (int j = ln; j < min(nc, 4096); j += kWave) taken[j] = 0;
+    __syncthreads();
+    int local = 0;
+    for (int p = q0; p < q1; ++p) {
+        const int i1 = A.f1.idx[p];
+        if (!A.v1[i1]) continue;
+        uint4 x0, x1;
+        load_desc(A.d1 + 32 * (size_t)i1, x0, x1);
+        int b1 = 256, bp = 0xfffff, b2 = 256;
+        for (int base = 0; base < nc; base += kWave) {
+            const int j = base + ln;
+            int d = 256;
+            if (j < nc) {
+                const int i2 = A.f2.idx[c0 + j];
+                const bool ok = A.kff ? !taken[j] : (!taken[j] && A.v2[i2]);
+                if (ok) {
+                    uint4 y0, y1;
+                    load_desc(A.d2 + 32 * (size_t)i2, y0, y1);
+                    d = hamming256(x0, x1, y0, y1);
+                }
+            }
+            int cb1, cbp, cb2;
+            wave_best2(d, j < nc ? j : 0xfffff, cb1, cbp, cb2);
+            // merge chunk result with the running one (chunks in candidate order)
+            if (cb1 < b1) { b2 = min(b1, cb2); b1 = cb1; bp = cbp; }
+            else { b2 = min(b2, min(cb1, cb2)); }
+        }
+        const bool pass = A.kff ? (b1 <= kThLow) : (b1 < kThLow);          // :230 vs :600
+        if (pass && (float)b1 < A.nnratio * (float)b2) {
+            const int i2 = A.f2.idx[c0 + bp];
+            if (ln == 0) {
+                taken[bp] = 1;
+                const int ridx = A.kff ? i2 : i1;
+                A.match[ridx] = A.kff ? i1 : i2;
+                if (A.checkOri) {
+                    const int bn = rot_bin(A.a1[i1], A.a2[i2]);
+                    A.bin[ridx] = bn;
+                    atomicAdd(&A.hist[bn], 1);
+                }
+            }
+            ++local;
+        }
+        __syncthreads();
+    }
+    if (ln == 0 && local) atomicAdd(A.nmatch, local);
+}
+
+struct TriArgs {
+    const uint8_t* d1; const orbx_keypoint* k1; const uint8_t* mp1; const float* ur1; FvDev f1;
+    const uint8_t* d2; const orbx_keypoint* k2; const uint8_t* mp2; const float* ur2; FvDev f2;
+    float F[9];
+    float sigma2[32], scale2[32];
+    float ex, ey;
+    int onlyStereo, checkOri;
+    int32_t* match; int32_t* bin; int32_t* hist; int32_t* nmatch;
+};
+
+// SearchForTriangulation: no greedy coupling between queries (vbMatched2 is never set, :679,727), so
+// the result of a query is the LAST candidate (in node order) among those with the minimum distance
+// that pass the epipole and epipolar tests (dist <= TH_LOW, ties replace: :740).
+__global__ __launch_bounds__(64) void k_triangulate(TriArgs A) {
+    const int a = blockIdx.x, ln = lane_id();
+    if (a >= A.f1.n) return;
+    const uint32_t id = A.f1.node[a];
+    const int b = fv_lower_bound(A.f2, id);
+    if (b >= A.f2.n || A.f2.node[b] != id) return;
+    const int q0 = A.f1.off[a], q1 = A.f1.off[a + 1];
+    const int c0 = A.f2.off[b], c1 = A.f2.off[b + 1];
+    int local = 0;
+    for (int p = q0; p < q1; ++p) {
+        const int i1 = A.f1.idx[p];
+        if (A.mp1[i1]) continue;
+        const bool st1 = A.ur1[i1] >= 0;
+        if (A.onlyStereo && !st1) continue;
+        const orbx_keypoint kp1 = A.k1[i1];
+        uint4 x0, x1;
+        load_desc(A.d1 + 32 * (size_t)i1, x0, x1);
+        // CheckDistEpipolarLine (:142-159) line coefficients
+        const float la = __fadd_rn(__fadd_rn(__fmul_rn(kp1.x, A.F[0]), __fmul_rn(kp1.y, A.F[3])), A.F[6]);
+        const float lb = __fadd_rn(__fadd_rn(__fmul_rn(kp1.x, A.F[1]), __fmul_rn(kp1.y, A.F[4])), A.F[7]);
+        const float lc = __fadd_rn(__fadd_rn(__fmul_rn(kp1.x, A.F[2]), __fmul_rn(kp1.y, A.F[5])), A.F[8]);
+        const float den = __fadd_rn(__fmul_rn(la, la), __fmul_rn(lb, lb));
+        uint32_t bestkey = 0;   // ((256 - d) << 20 | pos): max -> min distance, last position
+        for (int j = c0 + ln; j < c1; j += kWave) {
+            const int i2 = A.f2.idx[j];
+            if (A.mp2[i2]) continue;
+            const bool st2 = A.ur2[i2] >= 0;
+            if (A.onlyStereo && !st2) continue;
+            uint4 y0, y1;
+            load_desc(A.d2 + 32 * (size_t)i2, y0, y1);
+            const int d = hamming256(x0, x1, y0, y1);
+            if (d > kThLow) continue;
+            const orbx_keypoint kp2 = A.k2[i2];
+            if (!st1 && !st2) {
+                const float dx = __fsub_rn(A.ex, kp2.x), dy = __fsub_rn(A.ey, kp2.y);
+                if (__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < __fmul_rn(100.0f, A.scale2[kp2.octave])) continue;
+            }
+            if (den == 0.0f) continue;
+            const float num = __fadd_rn(__fadd_rn(__fmul_rn(la, kp2.x), __fmul_rn(lb, kp2.y)), lc);
+            const float dsqr = __fdiv_rn(__fmul_rn(num, num), den);
+            if (!((double)dsqr < 3.84 * (double)A.sigma2[kp2.octave])) continue;
+            const uint32_t key = ((uint32_t)(256 - d) << 20) | (uint32_t)(j - c0);
+            bestkey = max(bestkey, key);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) bestkey = max(bestkey, (uint32_t)__shfl_xor((int)bestkey, o, kWave));
+        if (bestkey != 0) {
+            const int i2 = A.f2.idx[c0 + (int)(bestkey & 0xfffff)];
+            if (ln == 0) {
+                A.match[i1] = i2;
+                if (A.checkOri) {
+                    const int bn = rot_bin(kp1.angle, A.k2[i2].angle);
+                    A.bin[i1] = bn;
+                    atomicAdd(&A.hist[bn], 1);
+                }
+            }
+            ++local;
+        }
+    }
+    if (ln == 0 && local) atomicAdd(A.nmatch, local);
+}
+
+// rotation-consistency filter: keep matches whose bin is one of the three largest bins
+// (ComputeThreeMaxima, :1603-1644, with the 10 % rule); single workgroup.
+__global__ __launch_bounds__(256) void k_rot_filter(int32_t* match, const int32_t* bin, int n, const int32_t* hist,
+                                                    int32_t* nmatch) {
+    __shared__ int keep[3];
+    __shared__ int removed;
+    if (threadIdx.x == 0) {
+        int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
+        for (int i = 0; i < kHisto; ++i) {
+            const int s = hist[i];
+            if (s > m1) { m3 = m2; m2 = m1; m1 = s; i3 = i2; i2 = i1; i1 = i; }
+            else if (s > m2) { m3 = m2; m2 = s; i3 = i2; i2 = i; }
+            else if (s > m3) { m3 = s; i3 = i; }
+        }
+        if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+        else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+        keep[0] = i1; keep[1] = i2; keep[2] = i3;
+        removed = 0;
+    }
+    __syncthreads();
+    int r = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        if (match[i] < 0) continue;
+        const int b = bin[i];
+        if (b == keep[0] || b == keep[1] || b == keep[2]) continue;
+        match[i] = -1;
+        ++r;
+    }
+    r = wave_sum(r);
+    if (lane_id() == 0 && r) atomicAdd(&removed, r);
+    __syncthreads();
+    if (threadIdx.x == 0) nmatch[0] -= removed;
+}
+
+// =============================================================================================
+// host side
+// =============================================================================================
+struct Matcher {
+    float nnratio;
+    int checkOri;
+    int device;
+    hipStream_t stream = nullptr;
+    // growable device scratch
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    int reserve(size_t bytes) {
+        if (bytes <= scratch_bytes) return ORBX_OK;
+        if (scratch) { (void)hipStreamSynchronize(stream); (void)hipFree(scratch); scratch = nullptr; }
+        size_t nb = std::max(bytes, scratch_bytes * 2);
+        ORBX_HIP(hipMalloc(&scratch, nb));
+        scratch_bytes = nb;
+        return ORBX_OK;
+    }
+};
+
+// bump allocator over the scratch buffer (256-B aligned pieces)
+struct Bump {
+    uint8_t* base; size_t off = 0;
+    template <typename T> T* take(size_t n) {
+        T* p = (T*)(base + off);
+        off += (n * sizeof(T) + 255) & ~(size_t)255;
+        return p;
+    }
+};
+static size_t a256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static int bf_launch(Matcher* m, const uint8_t* dq, int nq, const uint8_t* dt, int nt, int32_t* bi, int32_t* bd, int32_t* sd,
+                     hipStream_t s, void* scratch) {
+    // chunk the train set so that the grid fills the chip (>= ~1024 workgroups when possible)
+    const int qb = (nq + kBfQ - 1) / kBfQ;
+    int nch = std::max(1, std::min((nt + kBfStage - 1) / kBfStage, (2048 + qb - 1) / qb));
+    const int chunk = (nt + nch - 1) / nch;
+    nch = (nt + chunk - 1) / chunk;
+    uint32_t* pb = (uint32_t*)scratch;
+    int32_t* ps = (int32_t*)((uint8_t*)scratch + a256((size_t)nch * nq * 4));
+    hipLaunchKernelGGL(k_bf_tile, dim3(qb, nch), dim3(256), 0, s, dq, nq, dt, nt, chunk, pb, ps);
+    hipLaunchKernelGGL(k_bf_merge, dim3((nq + 255) / 256), dim3(256), 0, s, pb, ps, nq, nch, bi, bd, sd);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+static size_t bf_scratch(int nq, int nt) {
+    const int qb = (nq + kBfQ - 1) / kBfQ;
+    int nch = std::max(1, std::min((nt + kBfStage - 1) / kBfStage, (2048 + qb - 1) / qb));
+    return 2 * a256((size_t)nch * nq * 4) + 256;
+}
+
+}  // namespace orbx
+
+using namespace orbx;
+struct orbx_matcher : public orbx::Matcher {};
+
+extern "C" {
+
+int orbx_th_high(void) { return kThHigh; }
+int orbx_th_low(void) { return kThLow; }
+int orbx_histo_length(void) { return kHisto; }
+
+int orbx_matcher_create(float nnratio, int checkOri, int device, orbx_matcher** out) {
+    ORBX_REQUIRE(out, ORBX_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    int ndev = 0;
+    ORBX_HIP(hipGetDeviceCount(&ndev));
+    ORBX_REQUIRE(device >= 0 && device < ndev, ORBX_ERR_ARG, "device %d out of range (%d devices)", device, ndev);
+    orbx_matcher* m = new orbx_matcher();
+    m->nnratio = nnratio;
+    m->checkOri = checkOri;
+    m->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        set_error("stream create: %s", hipGetErrorString(e));
+        delete m;
+        return ORBX_ERR_HIP;
+    }
+    *out = m;
+    return ORBX_OK;
+}
+
+int orbx_matcher_destroy(orbx_matcher* m) {
+    if (!m) return ORBX_OK;
+    (void)hipSetDevice(m->device);
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    if (m->scratch) (void)hipFree(m->scratch);
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+    return ORBX_OK;
+}
+
+int orbx_descriptor_distance_device(orbx_matcher* m, const uint8_t* a, const uint8_t* b, int n, int32_t* d, void* stream) {
+    ORBX_REQUIRE(m && a && b && d && n >= 0, ORBX_ERR_ARG, "bad argument");
+    if (n == 0) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(m->device));
+    hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
+    hipLaunchKernelGGL(k_hamming_pairs, dim3((n + 255) / 256), dim3(256), 0, s, a, b, n, d);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_bf_match_device(orbx_matcher* m, const uint8_t* dq, int nq, const uint8_t* dt, int nt, int32_t* bi, int32_t* bd,
+                         int32_t* sd, void* stream) {
+    ORBX_REQUIRE(m && nq >= 0 && nt >= 0, ORBX_ERR_ARG, "bad argument");
+    ORBX_REQUIRE(nt < (1 << 20), ORBX_ERR_UNSUPPORTED, "train set too large (%d)", nt);
+    if (nq == 0) return ORBX_OK;
+    ORBX_REQUIRE(dq && bi && bd && sd && (nt == 0 || dt), ORBX_ERR_ARG, "null pointer");
+    ORBX_HIP(hipSetDevice(m->device));
+    hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
+    int st = m->reserve(bf_scratch(nq, std::max(nt, 1)));
+    if (st) return st;
+    if (nt == 0) {
+        std::vector<int32_t> neg(nq, -1), d256(nq, 256);
+        ORBX_HIP(hipMemcpyAsync(bi, neg.data(), 4 * (size_t)nq, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(bd, d256.data(), 4 * (size_t)nq, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(sd, d256.data(), 4 * (size_t)nq, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipStreamSynchronize(s));
+        return ORBX_OK;
+    }
+    return bf_launch(m, dq, nq, dt, nt, bi, bd, sd, s, m->scratch);
+}
+
+int orbx_bf_match(orbx_matcher* m, const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* bi, int32_t* bd, int32_t* sd) {
+    ORBX_REQUIRE(m && nq >= 0 && nt >= 0, ORBX_ERR_ARG, "bad argument");
+    if (nq == 0) return ORBX_OK;
+    ORBX_REQUIRE(q && bi && bd && sd && (nt == 0 || t), ORBX_ERR_ARG, "null pointer");
+    ORBX_REQUIRE(nt < (1 << 20), ORBX_ERR_UNSUPPORTED, "train set too large (%d)", nt);
+    ORBX_HIP(hipSetDevice(m->device));
+    const size_t io = a256((size_t)nq * 32) + a256((size_t)std::max(nt, 1) * 32) + 3 * a256((size_t)nq * 4);
+    int st = m->reserve(io + bf_scratch(nq, std::max(nt, 1)));
+    if (st) return st;
+    Bump bp{(uint8_t*)m->scratch};
+    uint8_t* dq = bp.take<uint8_t>((size_t)nq * 32);
+    uint8_t* dt = bp.take<uint8_t>((size_t)std::max(nt, 1) * 32);
+    int32_t* dbi = bp.take<int32_t>(nq);
+    int32_t* dbd = bp.take<int32_t>(nq);
+    int32_t* dsd = bp.take<int32_t>(nq);
+    hipStream_t s = m->stream;
+    ORBX_HIP(hipMemcpyAsync(dq, q, (size_t)nq * 32, hipMemcpyHostToDevice, s));
+    if (nt > 0) {
+        ORBX_HIP(hipMemcpyAsync(dt, t, (size_t)nt * 32, hipMemcpyHostToDevice, s));
+        st = bf_launch(m, dq, nq, dt, nt, dbi, dbd, dsd, s, (uint8_t*)m->scratch + bp.off);
+        if (st) return st;
+        ORBX_HIP(hipMemcpyAsync(bi, dbi, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
+        ORBX_HIP(hipMemcpyAsync(bd, dbd, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
+        ORBX_HIP(hipMemcpyAsync(sd, dsd, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
+        ORBX_HIP(hipStreamSynchronize(s));
+    } else {
+        for (int i = 0; i < nq; ++i) { bi[i] = -1; bd[i] = 256; sd[i] = 256; }
+    }
+    return ORBX_OK;
+}
+
+static int stereo_common(orbx_matcher* m, StereoArgs& A, const float* scale, int nlevels, int rows, float bf, float b) {
+    ORBX_REQUIRE(nlevels >= 1 && nlevels <= 32 && scale, ORBX_ERR_ARG, "bad level table");
+    ORBX_REQUIRE(b != 0.0f, ORBX_ERR_ARG, "baseline is zero");
+    for (int l = 0; l < nlevels; ++l) A.scale[l] = scale[l];
+    A.nlevels = nlevels;
+    A.rows = rows;
+    A.maxD = bf / b;   // minZ = mb, maxD = mbf/minZ (Frame.cc:496-498)
+    (void)m;
+    return ORBX_OK;
+}
+
+int orbx_stereo_match_batch_device(orbx_matcher* m, const orbx_keypoint* kl, const uint8_t* dl, const int32_t* nl,
+                                   const orbx_keypoint* kr, const uint8_t* dr, const int32_t* nr, int batch, int capacity,
+                                   const float* scale, int nlevels, int rows, float bf, float b, int32_t* bi, int32_t* bd,
+                                   void* stream) {
+    ORBX_REQUIRE(m && kl && dl && nl && kr && dr && nr && bi && bd && batch > 0 && capacity > 0, ORBX_ERR_ARG, "bad argument");
+    ORBX_REQUIRE(capacity < (1 << 20), ORBX_ERR_UNSUPPORTED, "capacity too large");
+    StereoArgs A{};
+    int st = stereo_common(m, A, scale, nlevels, rows, bf, b);
+    if (st) return st;
+    A.kl = kl; A.dl = dl; A.nl = nl; A.kr = kr; A.dr = dr; A.nr = nr; A.capacity = capacity;
+    A.best_idx = bi; A.best_dist = bd;
+    ORBX_HIP(hipSetDevice(m->device));
+    hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
+    hipLaunchKernelGGL(k_stereo, dim3((capacity * 64 + 255) / 256, batch), dim3(256), 0, s, A);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* desc_l, int nl, const orbx_keypoint* kpr,
+                      const uint8_t* desc_r, int nr, const float* scale, int nlevels, int rows, float bf, float b,
+                      int32_t* best_idx, int32_t* best_dist, int* n_matched) {
+    ORBX_REQUIRE(m && n_matched && nl >= 0 && nr >= 0, ORBX_ERR_ARG, "bad argument");
+    *n_matched = 0;
+    if (nl == 0) return ORBX_OK;
+    ORBX_REQUIRE(kpl && desc_l && best_idx && best_dist && (nr == 0 || (kpr && desc_r)), ORBX_ERR_ARG, "null pointer");
+    ORBX_REQUIRE(nr < (1 << 20), ORBX_ERR_UNSUPPORTED, "too many right keypoints");
+    StereoArgs A{};
+    int st = stereo_common(m, A, scale, nlevels, rows, bf, b);
+    if (st) return st;
+    ORBX_HIP(hipSetDevice(m->device));
+    const size_t bytes = a256(28 * (size_t)nl) + a256(32 * (size_t)nl) + a256(28 * (size_t)std::max(nr, 1)) +
+                         a256(32 * (size_t)std::max(nr, 1)) + 2 * a256(4 * (size_t)nl);
+    if ((st = m->reserve(bytes))) return st;
+    Bump bp{(uint8_t*)m->scratch};
+    orbx_keypoint* dkl = bp.take<orbx_keypoint>(nl);
+    uint8_t* ddl = bp.take<uint8_t>(32 * (size_t)nl);
+    orbx_keypoint* dkr = bp.take<orbx_keypoint>(std::max(nr, 1));
+    uint8_t* ddr = bp.take<uint8_t>(32 * (size_t)std::max(nr, 1));
+    int32_t* dbi = bp.take<int32_t>(nl);
+    int32_t* dbd = bp.take<int32_t>(nl);
+    hipStream_t s = m->stream;
+    ORBX_HIP(hipMemcpyAsync(dkl, kpl, 28 * (size_t)nl, hipMemcpyHostToDevice, s));
+    ORBX_HIP(hipMemcpyAsync(ddl, desc_l, 32 * (size_t)nl, hipMemcpyHostToDevice, s));
+    if (nr > 0) {
+        ORBX_HIP(hipMemcpyAsync(dkr, kpr, 28 * (size_t)nr, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(ddr, desc_r, 32 * (size_t)nr, hipMemcpyHostToDevice, s));
+    }
+    A.kl = dkl; A.dl = ddl; A.kr = dkr; A.dr = ddr; A.nl = nullptr; A.nr = nullptr;
+    A.nl_fixed = nl; A.nr_fixed = nr; A.capacity = std::max(nl, nr);
+    A.best_idx = dbi; A.best_dist = dbd;
+    hipLaunchKernelGGL(k_stereo, dim3((nl * 64 + 255) / 256, 1), dim3(256), 0, s, A);
+    ORBX_HIP(hipGetLastError());
+    ORBX_HIP(hipMemcpyAsync(best_idx, dbi, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(best_dist, dbd, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+    int n = 0;
+    for (int i = 0; i < nl; ++i) n += best_idx[i] >= 0;
+    *n_matched = n;
+    return ORBX_OK;
+}
+
+// -------- host staging of a FeatureVector into the bump region
+static FvDev stage_fv(Bump& bp, const orbx_featvec& f, int nfeat, hipStream_t s, int* st) {
+    FvDev d{};
+    d.n = f.n_nodes;
+    uint32_t* node = bp.take<uint32_t>(std::max(f.n_nodes, 1));
+    int32_t* off = bp.take<int32_t>((size_t)f.n_nodes + 1);
+    const int nidx = f.n_nodes > 0 ? f.offsets[f.n_nodes] : 0;
+    int32_t* idx = bp.take<int32_t>(std::max(nidx, 1));
+    (void)nfeat;
+    *st = ORBX_OK;
+    if (f.n_nodes > 0) {
+        if (hipMemcpyAsync(node, f.node_ids, 4 * (size_t)f.n_nodes, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(off, f.offsets, 4 * ((size_t)f.n_nodes + 1), hipMemcpyHostToDevice, s) != hipSuccess ||
+            (nidx > 0 && hipMemcpyAsync(idx, f.indices, 4 * (size_t)nidx, hipMemcpyHostToDevice, s) != hipSuccess)) {
+            set_error("featvec upload failed");
+            *st = ORBX_ERR_HIP;
+        }
+    }
+    d.node = node; d.off = off; d.idx = idx;
+    return d;
+}
+static size_t fv_bytes(const orbx_featvec& f) {
+    const int nidx = f.n_nodes > 0 ? f.offsets[f.n_nodes] : 0;
+    return a256(4 * (size_t)std::max(f.n_nodes, 1)) + a256(4 * ((size_t)f.n_nodes + 1)) + a256(4 * (size_t)std::max(nidx, 1));
+}
+static int check_fv(const orbx_featvec& f, int nfeat) {
+    ORBX_REQUIRE(f.n_nodes >= 0 && (f.n_nodes == 0 || (f.node_ids && f.offsets && f.indices)), ORBX_ERR_ARG, "bad featvec");
+    for (int i = 0; i < f.n_nodes; ++i) {
+        ORBX_REQUIRE(f.offsets[i + 1] >= f.offsets[i], ORBX_ERR_ARG, "featvec offsets not monotone");
+        ORBX_REQUIRE(i == 0 || f.node_ids[i] > f.node_ids[i - 1], ORBX_ERR_ARG, "featvec node ids not ascending");
+        ORBX_REQUIRE(f.offsets[i + 1] - f.offsets[i] <= 4096, ORBX_ERR_UNSUPPORTED, "node with > 4096 features");
+    }
+    const int nidx = f.n_nodes > 0 ? f.offsets[f.n_nodes] : 0;
+    for (int i = 0; i < nidx; ++i) ORBX_REQUIRE(f.indices[i] >= 0 && f.indices[i] < nfeat, ORBX_ERR_ARG, "featvec index out of range");
+    return ORBX_OK;
+}
+
+static int run_bow(orbx_matcher* m, int kff, const uint8_t* d1, const float* a1, const uint8_t* v1, int n1, orbx_featvec fv1,
+                   const uint8_t* d2, const float* a2, const uint8_t* v2, int n2, orbx_featvec fv2, int32_t* match,
+                   int nres, int* n_matches) {
+    int st;
+    if ((st = check_fv(fv1, n1)) || (st = check_fv(fv2, n2))) return st;
+    ORBX_HIP(hipSetDevice(m->device));
+    const size_t N1 = std::max(n1, 1), N2 = std::max(n2, 1), NR = std::max(nres, 1);
+    const size_t bytes = a256(32 * N1) + a256(4 * N1) + a256(N1) + a256(32 * N2) + a256(4 * N2) + a256(N2) + fv_bytes(fv1) +
+                         fv_bytes(fv2) + 2 * a256(4 * NR) + a256(4 * 32) + 256;
+    if ((st = m->reserve(bytes))) return st;
+    hipStream_t s = m->stream;
+    Bump bp{(uint8_t*)m->scratch};
+    uint8_t* dd1 = bp.take<uint8_t>(32 * N1);
+    float* da1 = bp.take<float>(N1);
+    uint8_t* dv1 = bp.take<uint8_t>(N1);
+    uint8_t* dd2 = bp.take<uint8_t>(32 * N2);
+    float* da2 = bp.take<float>(N2);
+    uint8_t* dv2 = bp.take<uint8_t>(N2);
+    FvDev f1 = stage_fv(bp, fv1, n1, s, &st);
+    if (st) return st;
+    FvDev f2 = stage_fv(bp, fv2, n2, s, &st);
+    if (st) return st;
+    int32_t* dm = bp.take<int32_t>(NR);
+    int32_t* db = bp.take<int32_t>(NR);
+    int32_t* dh = bp.take<int32_t>(32);   // hist[30], nmatch at [31]
+    if (n1) {
+        ORBX_HIP(hipMemcpyAsync(dd1, d1, 32 * (size_t)n1, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(da1, a1, 4 * (size_t)n1, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(dv1, v1, (size_t)n1, hipMemcpyHostToDevice, s));
+    }
+    if (n2) {
+        ORBX_HIP(hipMemcpyAsync(dd2, d2, 32 * (size_t)n2, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(da2, a2, 4 * (size_t)n2, hipMemcpyHostToDevice, s));
+        if (v2) ORBX_HIP(hipMemcpyAsync(dv2, v2, (size_t)n2, hipMemcpyHostToDevice, s));
+    }
+    ORBX_HIP(hipMemsetAsync(dm, 0xff, 4 * NR, s));
+    ORBX_HIP(hipMemsetAsync(dh, 0, 4 * 32, s));
+    BowArgs A{};
+    A.d1 = dd1; A.a1 = da1; A.v1 = dv1; A.f1 = f1;
+    A.d2 = dd2; A.a2 = da2; A.v2 = dv2; A.f2 = f2;
+    A.nnratio = m->nnratio; A.checkOri = m->checkOri; A.kff = kff;
+    A.match = dm; A.bin = db; A.hist = dh; A.nmatch = dh + 31;
+    if (fv1.n_nodes > 0) hipLaunchKernelGGL(k_bow, dim3(fv1.n_nodes), dim3(64), 0, s, A);
+    if (m->checkOri) hipLaunchKernelGGL(k_rot_filter, dim3(1), dim3(256), 0, s, dm, db, nres, dh, dh + 31);
+    ORBX_HIP(hipGetLastError());
+    int nm = 0;
+    if (nres) ORBX_HIP(hipMemcpyAsync(match, dm, 4 * (size_t)nres, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(&nm, dh + 31, 4, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+    *n_matches = nm;
+    return ORBX_OK;
+}
+
+int orbx_search_by_bow_kfkf(orbx_matcher* m, const uint8_t* desc1, const float* angle1, const uint8_t* valid1, int n1,
+                            orbx_featvec fv1, const uint8_t* desc2, const float* angle2, const uint8_t* valid2, int n2,
+                            orbx_featvec fv2, int32_t* match12, int* n_matches) {
+    ORBX_REQUIRE(m && n_matches && n1 >= 0 && n2 >= 0 && (n1 == 0 || (desc1 && angle1 && valid1 && match12)) &&
+                     (n2 == 0 || (desc2 && angle2 && valid2)),
+                 ORBX_ERR_ARG, "bad argument");
+    *n_matches = 0;
+    return run_bow(m, 0, desc1, angle1, valid1, n1, fv1, desc2, angle2, valid2, n2, fv2, match12, n1, n_matches);
+}
+
+int orbx_search_by_bow_kff(orbx_matcher* m, const uint8_t* desck, const float* anglek, const uint8_t* validk, int nk,
+                           orbx_featvec fvk, const uint8_t* descf, const float* anglef, int nf, orbx_featvec fvf,
+                           int32_t* matchf, int* n_matches) {
+    ORBX_REQUIRE(m && n_matches && nk >= 0 && nf >= 0 && (nk == 0 || (desck && anglek && validk)) &&
+                     (nf == 0 || (descf && anglef && matchf)),
+                 ORBX_ERR_ARG, "bad argument");
+    *n_matches = 0;
+    return run_bow(m, 1, desck, anglek, validk, nk, fvk, descf, anglef, nullptr, nf, fvf, matchf, nf, n_matches);
+}
+
+int orbx_search_for_triangulation(orbx_matcher* m, const uint8_t* desc1, const orbx_keypoint* kp1, const uint8_t* has_mp1,
+                                  const float* uright1, int n1, orbx_featvec fv1, const uint8_t* desc2, const orbx_keypoint* kp2,
+                                  const uint8_t* has_mp2, const float* uright2, int n2, orbx_featvec fv2, const float* F12,
+                                  const float* sigma2_2, const float* scale_2, int nlevels, float ex, float ey, int only_stereo,
+                                  int32_t* match12, int* n_matches) {
+    ORBX_REQUIRE(m && n_matches && F12 && sigma2_2 && scale_2 && nlevels >= 1 && nlevels <= 32 && n1 >= 0 && n2 >= 0,
+                 ORBX_ERR_ARG, "bad argument");
+    ORBX_REQUIRE((n1 == 0 || (desc1 && kp1 && has_mp1 && uright1 && match12)) && (n2 == 0 || (desc2 && kp2 && has_mp2 && uright2)),
+                 ORBX_ERR_ARG, "null pointer");
+    *n_matches = 0;
+    int st;
+    if ((st = check_fv(fv1, n1)) || (st = check_fv(fv2, n2))) return st;
+    ORBX_HIP(hipSetDevice(m->device));
+    const size_t N1 = std::max(n1, 1), N2 = std::max(n2, 1);
+    const size_t bytes = a256(32 * N1) + a256(28 * N1) + a256(N1) + a256(4 * N1) + a256(32 * N2) + a256(28 * N2) + a256(N2) +
+                         a256(4 * N2) + fv_bytes(fv1) + fv_bytes(fv2) + 2 * a256(4 * N1) + a256(4 * 32) + 256;
+    if ((st = m->reserve(bytes))) return st;
+    hipStream_t s = m->stream;
+    Bump bp{(uint8_t*)m->scratch};
+    uint8_t* dd1 = bp.take<uint8_t>(32 * N1);
+    orbx_keypoint* dk1 = bp.take<orbx_keypoint>(N1);
+    uint8_t* dm1 = bp.take<uint8_t>(N1);
+    float* du1 = bp.take<float>(N1);
+    uint8_t* dd2 = bp.take<uint8_t>(32 * N2);
+    orbx_keypoint* dk2 = bp.take<orbx_keypoint>(N2);
+    uint8_t* dm2 = bp.take<uint8_t>(N2);
+    float* du2 = bp.take<float>(N2);
+    FvDev f1 = stage_fv(bp, fv1, n1, s, &st);
+    if (st) return st;
+    FvDev f2 = stage_fv(bp, fv2, n2, s, &st);
+    if (st) return st;
+    int32_t* dm = bp.take<int32_t>(N1);
+    int32_t* db = bp.take<int32_t>(N1);
+    int32_t* dh = bp.take<int32_t>(32);
+    if (n1) {
+        ORBX_HIP(hipMemcpyAsync(dd1, desc1, 32 * (size_t)n1, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(dk1, kp1, 28 * (size_t)n1, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(dm1, has_mp1, (size_t)n1, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(du1, uright1, 4 * (size_t)n1, hipMemcpyHostToDevice, s));
+    }
+    if (n2) {
+        ORBX_HIP(hipMemcpyAsync(dd2, desc2, 32 * (size_t)n2, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(dk2, kp2, 28 * (size_t)n2, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(dm2, has_mp2, (size_t)n2, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(du2, uright2, 4 * (size_t)n2, hipMemcpyHostToDevice, s));
+    }
+    ORBX_HIP(hipMemsetAsync(dm, 0xff, 4 * N1, s));
+    ORBX_HIP(hipMemsetAsync(dh, 0, 4 * 32, s));
+    TriArgs A{};
+    A.d1 = dd1; A.k1 = dk1; A.mp1 = dm1; A.ur1 = du1; A.f1 = f1;
+    A.d2 = dd2; A.k2 = dk2; A.mp2 = dm2; A.ur2 = du2; A.f2 = f2;
+    for (int i = 0; i < 9; ++i) A.F[i] = F12[i];
+    for (int l = 0; l < nlevels; ++l) { A.sigma2[l] = sigma2_2[l]; A.scale2[l] = scale_2[l]; }
+    A.ex = ex; A.ey = ey; A.onlyStereo = only_stereo; A.checkOri = m->checkOri;
+    A.match = dm; A.bin = db; A.hist = dh; A.nmatch = dh + 31;
+    if (fv1.n_nodes > 0) hipLaunchKernelGGL(k_triangulate, dim3(fv1.n_nodes), dim3(64), 0, s, A);
+    if (m->checkOri) hipLaunchKernelGGL(k_rot_filter, dim3(1), dim3(256), 0, s, dm, db, n1, dh, dh + 31);
+    ORBX_HIP(hipGetLastError());
+    int nm = 0;
+    if (n1) ORBX_HIP(hipMemcpyAsync(match12, dm, 4 * (size_t)n1, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(&nm, dh + 31, 4, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+    *n_matches = nm;
+    return ORBX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,384 @@
+"""Host-side mirror of the reference's ORBextractor / ORBmatcher class API over liborbx.so (C-ABI in
+include/orbx.h).
+
+The reference classes are ORB_SLAM2::ORBextractor (include/ORBextractor.h:45-111) and
+ORB_SLAM2::ORBmatcher (include/ORBmatcher.h:37-102); method names and argument meaning follow them.
+Every compute call runs the HIP kernels in liborbx.so; there is no CPU fallback — if the library or a
+GPU is missing the constructors raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborbx.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "orbx.h")
+
+ORBX_OK, ORBX_ERR_ARG, ORBX_ERR_HIP, ORBX_ERR_CAPACITY, ORBX_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
+
+# cv::KeyPoint layout (28 B) — orbx_keypoint
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+class OrbxError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"orbx error {code}: {what}")
+        self.code = code
+
+
+class FeatVec(C.Structure):
+    _fields_ = [("node_ids", C.c_void_p), ("offsets", C.c_void_p), ("n_nodes", C.c_int), ("indices", C.c_void_p)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load liborbx.so (raises if it was not built: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"liborbx.so not found at {path}; run `make` (or __graft_entry__.build())")
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so (SONAME libamdhip64.so.7).
+    # Loading torch first lets liborbx's DT_NEEDED libamdhip64.so.7 bind to that same copy, so device
+    # pointers, streams and events are shared with torch (and torch.distributed/RCCL).  Loading liborbx
+    # first would pull /opt/rocm's copy and torch would then load a second, conflicting runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = C.CDLL(path)
+    vp, i32, f32 = C.c_void_p, C.c_int, C.c_float
+    lib.orbx_last_error.restype = C.c_char_p
+    lib.orbx_version.restype = C.c_char_p
+    lib.orbx_extractor_stage_name.restype = C.c_char_p
+    lib.orbx_extractor_get_scale_factor.restype = f32
+    lib.orbx_extractor_get_scale_factor.argtypes = [vp]
+    lib.orbx_extractor_create.argtypes = [i32, f32, i32, i32, i32, i32, C.POINTER(vp)]
+    lib.orbx_matcher_create.argtypes = [f32, i32, i32, C.POINTER(vp)]
+    for name in ("orbx_extractor_destroy", "orbx_matcher_destroy", "orbx_extractor_get_levels"):
+        getattr(lib, name).argtypes = [vp]
+    lib.orbx_extract.argtypes = [vp, vp, i32, i32, C.c_size_t, vp, vp, i32, C.POINTER(i32)]
+    lib.orbx_extract_batch_device.argtypes = [vp, vp, i32, i32, i32, C.c_size_t, C.c_size_t, vp, vp, vp, i32, vp]
+    lib.orbx_extractor_reserve.argtypes = [vp, i32, i32, i32]
+    lib.orbx_extractor_max_keypoints.argtypes = [vp, i32, i32]
+    lib.orbx_extractor_level_sizes.argtypes = [vp, i32, i32, vp, vp]
+    lib.orbx_extractor_copy_level.argtypes = [vp, i32, i32, vp, C.c_size_t]
+    lib.orbx_extractor_level_device.argtypes = [vp, i32, i32, C.POINTER(vp), C.POINTER(i32), C.POINTER(i32)]
+    lib.orbx_extractor_enable_timing.argtypes = [vp, i32]
+    lib.orbx_extractor_stage_times.argtypes = [vp, vp, C.POINTER(i32)]
+    for name in ("orbx_extractor_get_scale_factors", "orbx_extractor_get_inverse_scale_factors",
+                 "orbx_extractor_get_scale_sigma_squares", "orbx_extractor_get_inverse_scale_sigma_squares",
+                 "orbx_extractor_get_features_per_level"):
+        getattr(lib, name).argtypes = [vp, vp]
+    lib.orbx_descriptor_distance_device.argtypes = [vp, vp, vp, i32, vp, vp]
+    lib.orbx_bf_match.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp]
+    lib.orbx_bf_match_device.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, vp]
+    lib.orbx_stereo_match.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, i32, i32, f32, f32, vp, vp, C.POINTER(i32)]
+    lib.orbx_stereo_match_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, f32, f32, vp,
+                                                   vp, vp]
+    lib.orbx_search_by_bow_kfkf.argtypes = [vp, vp, vp, vp, i32, FeatVec, vp, vp, vp, i32, FeatVec, vp,
+                                            C.POINTER(i32)]
+    lib.orbx_search_by_bow_kff.argtypes = [vp, vp, vp, vp, i32, FeatVec, vp, vp, i32, FeatVec, vp, C.POINTER(i32)]
+    lib.orbx_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, i32, FeatVec, vp, vp, vp, vp, i32, FeatVec,
+                                                  vp, vp, vp, i32, f32, f32, i32, vp, C.POINTER(i32)]
+    _lib = lib
+    return lib
+
+
+def declared_symbols(header: str = HEADER_PATH) -> list[str]:
+    """Function names declared in include/orbx.h."""
+    text = open(header).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w]+\**\s+\**(orbx_\w+)\s*\(", text, flags=re.M)))
+
+
+def _check(code: int):
+    if code != ORBX_OK:
+        raise OrbxError(code, load_library().orbx_last_error().decode())
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _tp(t):
+    """device pointer of a torch tensor"""
+    return C.c_void_p(t.data_ptr())
+
+
+def device_count() -> int:
+    return load_library().orbx_device_count()
+
+
+def _featvec(fv):
+    """(node_ids, offsets, indices) -> FeatVec struct (keeps arrays alive)."""
+    node = np.ascontiguousarray(fv[0], np.uint32)
+    off = np.ascontiguousarray(fv[1], np.int32)
+    idx = np.ascontiguousarray(fv[2], np.int32)
+    s = FeatVec(_p(node), _p(off), len(node), _p(idx))
+    s._keep = (node, off, idx)
+    return s
+
+
+class ORBextractor:
+    """ORB_SLAM2::ORBextractor (src/ORBextractor.cc:410-1132) on a MI355X."""
+
+    def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int, minThFAST: int,
+                 device: int = 0):
+        self._lib = load_library()
+        h = C.c_void_p()
+        _check(self._lib.orbx_extractor_create(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device,
+                                               C.byref(h)))
+        self._h = h
+        self.nfeatures, self.nlevels, self.device = nfeatures, nlevels, device
+        self._last_shape = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.orbx_extractor_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- getters (include/ORBextractor.h:63-83)
+    def GetLevels(self) -> int:
+        return self._lib.orbx_extractor_get_levels(self._h)
+
+    def GetScaleFactor(self) -> float:
+        return self._lib.orbx_extractor_get_scale_factor(self._h)
+
+    def _vec(self, fn, dtype=np.float32):
+        out = np.zeros(self.nlevels, dtype)
+        _check(fn(self._h, _p(out)))
+        return out
+
+    def GetScaleFactors(self):
+        return self._vec(self._lib.orbx_extractor_get_scale_factors)
+
+    def GetInverseScaleFactors(self):
+        return self._vec(self._lib.orbx_extractor_get_inverse_scale_factors)
+
+    def GetScaleSigmaSquares(self):
+        return self._vec(self._lib.orbx_extractor_get_scale_sigma_squares)
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._vec(self._lib.orbx_extractor_get_inverse_scale_sigma_squares)
+
+    def features_per_level(self):
+        return self._vec(self._lib.orbx_extractor_get_features_per_level, np.int32)
+
+    def max_keypoints(self, rows: int, cols: int) -> int:
+        n = self._lib.orbx_extractor_max_keypoints(self._h, rows, cols)
+        if n < 0:
+            _check(n)
+        return n
+
+    def level_sizes(self, rows: int, cols: int):
+        r = np.zeros(self.nlevels, np.int32)
+        c = np.zeros(self.nlevels, np.int32)
+        _check(self._lib.orbx_extractor_level_sizes(self._h, rows, cols, _p(r), _p(c)))
+        return list(zip(r.tolist(), c.tolist()))
+
+    def reserve(self, rows: int, cols: int, max_batch: int):
+        _check(self._lib.orbx_extractor_reserve(self._h, rows, cols, max_batch))
+
+    # --- operator() (src/ORBextractor.cc:1043-1105)
+    def __call__(self, image: np.ndarray, mask=None):
+        """Returns (keypoints: structured array KP_DTYPE, descriptors: (n, 32) uint8).  Mask is ignored, as in
+        the reference (include/ORBextractor.h:58)."""
+        img = np.ascontiguousarray(image, np.uint8)
+        if img.size == 0:
+            return np.zeros(0, KP_DTYPE), np.zeros((0, 32), np.uint8)
+        assert img.ndim == 2, "8UC1 image expected"
+        rows, cols = img.shape
+        cap = self.max_keypoints(rows, cols)
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int()
+        _check(self._lib.orbx_extract(self._h, _p(img), rows, cols, img.strides[0], _p(kps), _p(desc), cap,
+                                      C.byref(n)))
+        self._last_shape = (rows, cols)
+        return kps[: n.value].copy(), desc[: n.value].copy()
+
+    @property
+    def mvImagePyramid(self):
+        """Host copies of the pyramid levels of the last image (include/ORBextractor.h:85)."""
+        if self._last_shape is None:
+            return []
+        out = []
+        for l, (h, w) in enumerate(self.level_sizes(*self._last_shape)):
+            a = np.zeros((h, w), np.uint8)
+            _check(self._lib.orbx_extractor_copy_level(self._h, 0, l, _p(a), w))
+            out.append(a)
+        return out
+
+    # --- batched device path (torch tensors on cuda:device)
+    def extract_batch_device(self, images, kps=None, desc=None, counts=None, stream=None):
+        """images: uint8 tensor (B, rows, cols) on the GPU.  Returns (kps (B, cap, 28) uint8 view-able as
+        KP_DTYPE, desc (B, cap, 32) uint8, counts (B,) int32), all device tensors."""
+        import torch
+        B, rows, cols = images.shape
+        cap = self.max_keypoints(rows, cols)
+        dev = images.device
+        if kps is None:
+            kps = torch.empty((B, cap, 28), dtype=torch.uint8, device=dev)
+        if desc is None:
+            desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+        if counts is None:
+            counts = torch.empty((B,), dtype=torch.int32, device=dev)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream)
+        _check(self._lib.orbx_extract_batch_device(self._h, _tp(images), B, rows, cols, images.stride(1),
+                                                   images.stride(0), _tp(kps), _tp(desc), _tp(counts), cap, s))
+        return kps, desc, counts
+
+    def enable_timing(self, on: bool = True):
+        _check(self._lib.orbx_extractor_enable_timing(self._h, int(on)))
+
+    def stage_times(self):
+        n = self._lib.orbx_extractor_stage_count()
+        ms = np.zeros(n, np.float64)
+        calls = C.c_int()
+        _check(self._lib.orbx_extractor_stage_times(self._h, _p(ms), C.byref(calls)))
+        names = [self._lib.orbx_extractor_stage_name(i).decode() for i in range(n)]
+        return dict(zip(names, ms.tolist())), calls.value
+
+
+@dataclass
+class StereoResult:
+    best_idx: np.ndarray   # right index or -1 (accepted if best_dist < 75)
+    best_dist: np.ndarray
+    n_matched: int
+
+
+class ORBmatcher:
+    """ORB_SLAM2::ORBmatcher (src/ORBmatcher.cc) on a MI355X."""
+
+    TH_HIGH = 100
+    TH_LOW = 50
+    HISTO_LENGTH = 30
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0):
+        self._lib = load_library()
+        h = C.c_void_p()
+        _check(self._lib.orbx_matcher_create(nnratio, int(checkOri), device, C.byref(h)))
+        self._h = h
+        self.mfNNratio, self.mbCheckOrientation, self.device = nnratio, checkOri, device
+        assert self._lib.orbx_th_high() == self.TH_HIGH and self._lib.orbx_th_low() == self.TH_LOW
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.orbx_matcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def DescriptorDistance(self, a, b):
+        """ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1649-1665) for row-aligned descriptor arrays
+        (one pair or many), computed on the GPU."""
+        import torch
+        a = np.atleast_2d(np.ascontiguousarray(a, np.uint8))
+        b = np.atleast_2d(np.ascontiguousarray(b, np.uint8))
+        dev = torch.device("cuda", self.device)
+        ta, tb = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+        out = torch.empty(a.shape[0], dtype=torch.int32, device=dev)
+        s = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _check(self._lib.orbx_descriptor_distance_device(self._h, _tp(ta), _tp(tb), a.shape[0], _tp(out), s))
+        r = out.cpu().numpy()
+        return int(r[0]) if r.shape[0] == 1 else r
+
+    def bf_match(self, query, train):
+        q = np.ascontiguousarray(query, np.uint8)
+        t = np.ascontiguousarray(train, np.uint8)
+        n = q.shape[0]
+        bi, bd, sd = (np.zeros(n, np.int32) for _ in range(3))
+        _check(self._lib.orbx_bf_match(self._h, _p(q), n, _p(t), t.shape[0], _p(bi), _p(bd), _p(sd)))
+        return bi, bd, sd
+
+    def bf_match_device(self, query, train, stream=None):
+        import torch
+        n = query.shape[0]
+        bi, bd, sd = (torch.empty(n, dtype=torch.int32, device=query.device) for _ in range(3))
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(query.device).cuda_stream)
+        _check(self._lib.orbx_bf_match_device(self._h, _tp(query), n, _tp(train), train.shape[0], _tp(bi), _tp(bd),
+                                              _tp(sd), s))
+        return bi, bd, sd
+
+    def ComputeStereoMatches(self, kps_left, desc_left, kps_right, desc_right, scale_factors, rows, bf, b):
+        """Descriptor search of Frame::ComputeStereoMatches (src/Frame.cc:466-552)."""
+        kl = np.ascontiguousarray(kps_left, KP_DTYPE)
+        kr = np.ascontiguousarray(kps_right, KP_DTYPE)
+        dl = np.ascontiguousarray(desc_left, np.uint8)
+        dr = np.ascontiguousarray(desc_right, np.uint8)
+        sc = np.ascontiguousarray(scale_factors, np.float32)
+        bi = np.zeros(len(kl), np.int32)
+        bd = np.zeros(len(kl), np.int32)
+        n = C.c_int()
+        _check(self._lib.orbx_stereo_match(self._h, _p(kl), _p(dl), len(kl), _p(kr), _p(dr), len(kr), _p(sc), len(sc),
+                                           rows, bf, b, _p(bi), _p(bd), C.byref(n)))
+        return StereoResult(bi, bd, n.value)
+
+    def stereo_match_batch_device(self, kl, dl, nl, kr, dr, nr, capacity, scale_factors, rows, bf, b, stream=None):
+        import torch
+        B = nl.shape[0]
+        bi = torch.empty((B, capacity), dtype=torch.int32, device=kl.device)
+        bd = torch.empty((B, capacity), dtype=torch.int32, device=kl.device)
+        sc = np.ascontiguousarray(scale_factors, np.float32)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(kl.device).cuda_stream)
+        _check(self._lib.orbx_stereo_match_batch_device(self._h, _tp(kl), _tp(dl), _tp(nl), _tp(kr), _tp(dr), _tp(nr), B,
+                                                        capacity, _p(sc), len(sc), rows, bf, b, _tp(bi), _tp(bd), s))
+        return bi, bd
+
+    def SearchByBoW_KF_KF(self, desc1, angle1, valid1, fv1, desc2, angle2, valid2, fv2):
+        """ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, ...) (src/ORBmatcher.cc:524-657).  Returns
+        (nmatches, match12) with match12[i1] = KF2 index or -1."""
+        d1, d2 = np.ascontiguousarray(desc1, np.uint8), np.ascontiguousarray(desc2, np.uint8)
+        a1, a2 = np.ascontiguousarray(angle1, np.float32), np.ascontiguousarray(angle2, np.float32)
+        v1, v2 = np.ascontiguousarray(valid1, np.uint8), np.ascontiguousarray(valid2, np.uint8)
+        m = np.zeros(len(d1), np.int32)
+        n = C.c_int()
+        _check(self._lib.orbx_search_by_bow_kfkf(self._h, _p(d1), _p(a1), _p(v1), len(d1), _featvec(fv1), _p(d2),
+                                                 _p(a2), _p(v2), len(d2), _featvec(fv2), _p(m), C.byref(n)))
+        return n.value, m
+
+    def SearchByBoW_KF_F(self, desck, anglek, validk, fvk, descf, anglef, fvf):
+        """ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) (src/ORBmatcher.cc:161-290).  Returns
+        (nmatches, matchF) with matchF[iF] = KF index or -1."""
+        dk, df = np.ascontiguousarray(desck, np.uint8), np.ascontiguousarray(descf, np.uint8)
+        ak, af = np.ascontiguousarray(anglek, np.float32), np.ascontiguousarray(anglef, np.float32)
+        vk = np.ascontiguousarray(validk, np.uint8)
+        m = np.zeros(len(df), np.int32)
+        n = C.c_int()
+        _check(self._lib.orbx_search_by_bow_kff(self._h, _p(dk), _p(ak), _p(vk), len(dk), _featvec(fvk), _p(df),
+                                                _p(af), len(df), _featvec(fvf), _p(m), C.byref(n)))
+        return n.value, m
+
+    def SearchForTriangulation(self, desc1, kps1, has_mp1, uright1, fv1, desc2, kps2, has_mp2, uright2, fv2, F12,
+                               sigma2_2, scale_2, ex, ey, bOnlyStereo=False):
+        """ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:659-825).  Returns (nmatches, match12)."""
+        arrs = [np.ascontiguousarray(x, t) for x, t in
+                ((desc1, np.uint8), (kps1, KP_DTYPE), (has_mp1, np.uint8), (uright1, np.float32), (desc2, np.uint8),
+                 (kps2, KP_DTYPE), (has_mp2, np.uint8), (uright2, np.float32), (F12, np.float32),
+                 (sigma2_2, np.float32), (scale_2, np.float32))]
+        d1, k1, m1, u1, d2, k2, m2, u2, F, s2, sc2 = arrs
+        m = np.zeros(len(d1), np.int32)
+        n = C.c_int()
+        _check(self._lib.orbx_search_for_triangulation(self._h, _p(d1), _p(k1), _p(m1), _p(u1), len(d1), _featvec(fv1),
+                                                       _p(d2), _p(k2), _p(m2), _p(u2), len(d2), _featvec(fv2), _p(F),
+                                                       _p(s2), _p(sc2), len(s2), ex, ey, int(bOnlyStereo), _p(m),
+                                                       C.byref(n)))
+        return n.value, m

@@ -1,0 +1,204 @@
+"""ctypes wrapper of the CPU oracle (oracle/orb_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, never by the product package.  Parity status: "parity unpinned" (see orb_oracle.cpp header and
+DESIGN.md §Oracle).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborb_oracle.so")
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.orc_fast_atan2.restype = C.c_float
+        _lib.orc_fast_atan2.argtypes = [C.c_float, C.c_float]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class FV(C.Structure):
+    _fields_ = [("node", C.c_void_p), ("off", C.c_void_p), ("n_nodes", C.c_int), ("idx", C.c_void_p)]
+
+
+def make_fv(fv):
+    node, off, idx = (np.ascontiguousarray(fv[0], np.uint32), np.ascontiguousarray(fv[1], np.int32),
+                      np.ascontiguousarray(fv[2], np.int32))
+    s = FV(_p(node), _p(off), len(node), _p(idx))
+    s._keep = (node, off, idx)
+    return s
+
+
+def tables(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7):
+    f = lambda: np.zeros(nlevels, np.float32)
+    scale, inv, s2, is2 = f(), f(), f(), f()
+    npl = np.zeros(nlevels, np.int32)
+    umax = np.zeros(16, np.int32)
+    lib().orc_tables(nfeatures, C.c_float(scale_factor), nlevels, ini_th, min_th, _p(scale), _p(inv), _p(s2),
+                     _p(is2), _p(npl), _p(umax))
+    return dict(scale=scale, inv_scale=inv, sigma2=s2, inv_sigma2=is2, n_per_level=npl, umax=umax)
+
+
+def level_sizes(rows, cols, nlevels=8, scale_factor=1.2):
+    inv = tables(nlevels=nlevels, scale_factor=scale_factor)["inv_scale"]
+    out = []
+    for l in range(nlevels):
+        w = int(np.rint(np.float32(cols) * inv[l]))
+        h = int(np.rint(np.float32(rows) * inv[l]))
+        out.append((h, w))
+    return out
+
+
+def extract(img, nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, want_pyramid=False):
+    img = np.ascontiguousarray(img, np.uint8)
+    rows, cols = img.shape
+    cap = 4 * nfeatures + 64 * nlevels
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    sizes = level_sizes(rows, cols, nlevels, scale_factor)
+    pyr = np.zeros(sum(h * w for h, w in sizes), np.uint8) if want_pyramid else None
+    ncand = np.zeros(nlevels, np.int32)
+    n = lib().orc_extract(nfeatures, C.c_float(scale_factor), nlevels, ini_th, min_th, _p(img), rows, cols, cols,
+                          _p(kps), _p(desc), cap, _p(pyr) if pyr is not None else None, _p(ncand))
+    if n < 0:
+        raise RuntimeError("oracle capacity too small: %d" % -n)
+    out = dict(kps=kps[:n].copy(), desc=desc[:n].copy(), ncand=ncand)
+    if want_pyramid:
+        levels, o = [], 0
+        for h, w in sizes:
+            levels.append(pyr[o:o + h * w].reshape(h, w).copy())
+            o += h * w
+        out["pyramid"] = levels
+    return out
+
+
+def resize(src, dh, dw):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().orc_resize(_p(src), src.shape[1], src.shape[0], _p(dst), dw, dh)
+    return dst
+
+
+def blur7(src):
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros_like(src)
+    lib().orc_blur7(_p(src), src.shape[1], src.shape[0], _p(dst))
+    return dst
+
+
+def fast_atan2(y, x):
+    return lib().orc_fast_atan2(float(y), float(x))
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().orc_descriptor_distance(_p(a), _p(b))
+
+
+def bf_match(q, t):
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    nq = q.shape[0]
+    bi, b1, b2 = (np.zeros(nq, np.int32) for _ in range(3))
+    lib().orc_bf_match(_p(q), nq, _p(t), t.shape[0], _p(bi), _p(b1), _p(b2))
+    return bi, b1, b2
+
+
+def stereo_match(kl, dl, kr, dr, scale, rows, bf, b):
+    kl, kr = np.ascontiguousarray(kl, KP_DTYPE), np.ascontiguousarray(kr, KP_DTYPE)
+    dl, dr = np.ascontiguousarray(dl, np.uint8), np.ascontiguousarray(dr, np.uint8)
+    scale = np.ascontiguousarray(scale, np.float32)
+    idx = np.zeros(len(kl), np.int32)
+    dist = np.zeros(len(kl), np.int32)
+    n = lib().orc_stereo_match(_p(kl), _p(dl), len(kl), _p(kr), _p(dr), len(kr), _p(scale), rows,
+                               C.c_float(bf), C.c_float(b), _p(idx), _p(dist))
+    return n, idx, dist
+
+
+def search_by_bow_kfkf(d1, ang1, valid1, fv1, d2, ang2, valid2, fv2, nnratio=0.75, check_ori=True):
+    d1, d2 = np.ascontiguousarray(d1, np.uint8), np.ascontiguousarray(d2, np.uint8)
+    ang1, ang2 = np.ascontiguousarray(ang1, np.float32), np.ascontiguousarray(ang2, np.float32)
+    v1, v2 = np.ascontiguousarray(valid1, np.uint8), np.ascontiguousarray(valid2, np.uint8)
+    m = np.zeros(len(d1), np.int32)
+    f1, f2 = make_fv(fv1), make_fv(fv2)
+    n = lib().orc_search_by_bow_kfkf(_p(d1), _p(ang1), _p(v1), len(d1), f1, _p(d2), _p(ang2), _p(v2), len(d2), f2,
+                                     C.c_float(nnratio), int(check_ori), _p(m))
+    return n, m
+
+
+def search_by_bow_kff(dk, angk, validk, fvk, df, angf, fvf, nnratio=0.7, check_ori=True):
+    dk, df = np.ascontiguousarray(dk, np.uint8), np.ascontiguousarray(df, np.uint8)
+    angk, angf = np.ascontiguousarray(angk, np.float32), np.ascontiguousarray(angf, np.float32)
+    vk = np.ascontiguousarray(validk, np.uint8)
+    m = np.zeros(len(df), np.int32)
+    fk, ff = make_fv(fvk), make_fv(fvf)
+    n = lib().orc_search_by_bow_kff(_p(dk), _p(angk), _p(vk), len(dk), fk, _p(df), _p(angf), len(df), ff,
+                                    C.c_float(nnratio), int(check_ori), _p(m))
+    return n, m
+
+
+def search_for_triangulation(d1, k1, mp1, ur1, fv1, d2, k2, mp2, ur2, fv2, F12, sigma2, scale2, ex, ey,
+                             only_stereo=False, check_ori=True):
+    a = [np.ascontiguousarray(x, t) for x, t in
+         ((d1, np.uint8), (k1, KP_DTYPE), (mp1, np.uint8), (ur1, np.float32), (d2, np.uint8), (k2, KP_DTYPE),
+          (mp2, np.uint8), (ur2, np.float32), (F12, np.float32), (sigma2, np.float32), (scale2, np.float32))]
+    d1, k1, mp1, ur1, d2, k2, mp2, ur2, F12, sigma2, scale2 = a
+    m = np.zeros(len(d1), np.int32)
+    f1, f2 = make_fv(fv1), make_fv(fv2)
+    n = lib().orc_search_for_triangulation(_p(d1), _p(k1), _p(mp1), _p(ur1), len(d1), f1, _p(d2), _p(k2), _p(mp2),
+                                           _p(ur2), len(d2), f2, _p(F12), _p(sigma2), _p(scale2), C.c_float(ex),
+                                           C.c_float(ey), int(only_stereo), int(check_ori), _p(m))
+    return n, m
+
+
+def level_candidates(img, nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7):
+    """FAST candidates per level in reference order, window-relative (x, y, response)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    cap = img.size
+    xyr = np.zeros((cap, 3), np.float32)
+    per = np.zeros(nlevels, np.int32)
+    n = lib().orc_level_candidates(nfeatures, C.c_float(scale_factor), nlevels, ini_th, min_th, _p(img),
+                                   img.shape[0], img.shape[1], _p(xyr), cap, _p(per))
+    if n < 0:
+        raise RuntimeError("capacity")
+    out, o = [], 0
+    for c in per:
+        out.append(xyr[o:o + c].copy())
+        o += c
+    return out
+
+
+def distribute(xyr, minX, maxX, minY, maxY, N):
+    xyr = np.ascontiguousarray(xyr, np.float32).reshape(-1, 3)
+    cap = max(4 * len(xyr) + 64, 64)
+    out = np.zeros((cap, 3), np.float32)
+    m = lib().orc_distribute(_p(xyr), len(xyr), minX, maxX, minY, maxY, N, _p(out), cap)
+    if m < 0:
+        raise RuntimeError("capacity")
+    return out[:m].copy()
