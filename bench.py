@@ -54,7 +54,6 @@ def algorithmic_bytes(ex, mean_cand, mean_kps):
     px = [h * w for h, w in sizes]
     P = sum(px)
     return {
-        "copy_level0": 2 * px[0],
         "resize": sum(px[l - 1] + px[l] for l in range(1, len(px))),
         "fast_cells": P + 5 * mean_cand,                 # read every level once, write candidates (xy + score)
         "blur7": 2 * P,                                  # read + write every level

@@ -96,9 +96,10 @@ int orbx_extract_batch_device(orbx_extractor* ex, const uint8_t* d_images, int b
                               size_t step, size_t image_stride, orbx_keypoint* d_keypoints,
                               uint8_t* d_descriptors, int32_t* d_counts, int capacity, void* stream);
 
-/* Device pointer of pyramid level 'level' of batch image 'index' (contiguous rows, stride = cols). */
+/* Device pointer and row step of pyramid level 'level' of image 'index' of the last call.  Level 0 is
+ * the caller's input image itself (read in place, never copied): valid while the caller keeps it. */
 int orbx_extractor_level_device(orbx_extractor* ex, int index, int level, const uint8_t** d_level,
-                                int* rows, int* cols);
+                                int* rows, int* cols, size_t* step);
 
 /* Optional per-stage timing of device calls (HIP events on the launch stream).  When enabled, each
  * orbx_extract_batch_device records events around every stage; orbx_extractor_stage_times returns

@@ -2,13 +2,13 @@
 // orbx_extract.hip — MI355X (gfx950) ORB extractor: the hot path of ORBextractor::operator()
 // (reference src/ORBextractor.cc:1043-1105) as batched HIP kernels behind the C-ABI of include/orbx.h.
 //
-// Per device call over a batch of B images (all rows x cols), one stream, 5 + (nlevels-1) launches:
-//   k_copy_level0   image -> pyramid level 0                        (ComputePyramid :1127)
+// Per device call over a batch of B images (all rows x cols), one stream, 4 + (nlevels-1) launches:
+//   (level 0 is read in place from the caller's images: no copy)   (ComputePyramid :1127)
 //   k_resize        level l-1 -> level l, l = 1..L-1 (chained)       (ComputePyramid :1120)
 //   k_fast_cells    one workgroup per (30-px grid cell, image): FAST-9 score map in LDS, 3x3 strict
 //                   NMS at iniThFAST, fallback to minThFAST when the cell is empty, row-major
 //                   compaction into per-cell candidate slots          (ComputeKeyPointsOctTree :789-829)
-//   k_blur7         7x7 sigma-2 Gaussian on every level (REFLECT_101) (operator() :1085-1086)
+//   k_blur7         7x7 sigma-2 Gaussian on every level (REFLECT_101), register-streaming (:1085-1086)
 //   k_quadtree      one workgroup per (level, image): DistributeOctTree's list/quadtree as data-parallel
 //                   passes over LDS node arrays                     (:539-763, :834-847)
 //   k_describe      one wave per keypoint: IC angle on the level, steered BRIEF on the blurred level,
@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -79,36 +80,45 @@ struct CellDev {
     int pad;
 };
 
+// Level 0 is the caller's image itself (no copy): base pointer, row step and image stride.
+struct Src0 {
+    const uint8_t* p;
+    size_t step, istride;
+};
+
+__device__ __forceinline__ const uint8_t* level_pixels(const uint8_t* pyr, size_t pyr_stride, const LevelDev& L,
+                                                       int lvl, int img, const Src0& s0, int& stride) {
+    if (lvl == 0) {
+        stride = (int)s0.step;
+        return s0.p + img * s0.istride;
+    }
+    stride = L.w;
+    return pyr + img * pyr_stride + L.pyr_off;
+}
+
 struct ResizeTab {       // per level >= 1, device arrays
     int* x0; int* x1; int* a0; int* a1;   // [w]
     int* y0; int* y1; int* b0; int* b1;   // [h]
 };
 
 __constant__ signed char c_pattern[ORBX_PATTERN_TESTS * 4];
-__constant__ int c_umax[16];
+// umax for HALF_PATCH_SIZE = 15 (ORBextractor ctor :454-469); the host recomputes it and checks equality
+constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
 // =============================================================================================
 // kernels
 // =============================================================================================
 
-__global__ __launch_bounds__(256) void k_copy_level0(const uint8_t* __restrict__ src, size_t step, size_t istride,
-                                                     uint8_t* __restrict__ pyr, size_t pyr_stride, int w, int h) {
-    const int img = blockIdx.z, y = blockIdx.y;
-    const uint8_t* s = src + img * istride + (size_t)y * step;
-    uint8_t* d = pyr + img * pyr_stride + (size_t)y * w;
-    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < w; x += gridDim.x * blockDim.x) d[x] = s[x];
-}
-
 // resize INTER_LINEAR 8U, fixed point (pinned OpenCV 3.2 generic path): horizontal taps a0/a1 (x2048)
 // with clamped source columns, vertical (r0*b0 + r1*b1 + 2^21) >> 22 saturated.
-__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride, int src_off, int sw,
-                                                int dst_off, int dw, int dh, ResizeTab t) {
+__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
+                                                size_t src_step, size_t src_istride, int dst_off, int dw, int dh, ResizeTab t) {
     const int img = blockIdx.z, y = blockIdx.y;
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= dw || y >= dh) return;
-    const uint8_t* S = pyr + img * pyr_stride + src_off;
-    const uint8_t* r0 = S + (size_t)t.y0[y] * sw;
-    const uint8_t* r1 = S + (size_t)t.y1[y] * sw;
+    const uint8_t* S = src + img * src_istride;
+    const uint8_t* r0 = S + (size_t)t.y0[y] * src_step;
+    const uint8_t* r1 = S + (size_t)t.y1[y] * src_step;
     const int xa = t.x0[x], xb = t.x1[x], a0 = t.a0[x], a1 = t.a1[x];
     const int h0 = (int)r0[xa] * a0 + (int)r0[xb] * a1;
     const int h1 = (int)r1[xa] * a0 + (int)r1[xb] * a1;
@@ -121,105 +131,190 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
 // OpenCV order), with d_k = v - p_k:  m_dark = max over the 16 arcs of 9 of min d, m_bright = max
 // over arcs of min(-d).  OpenCV's cornerScore<16> returns max(t, m_dark, m_bright) - 1 and the pixel
 // is a corner at threshold t iff max(m_dark, m_bright) > t; hence s = max(m_dark, m_bright) - 1 is
-// threshold independent and "corner at t" <=> s >= t.
-__device__ __forceinline__ int fast_score(const uint8_t* p, int W) {
-    const int v = p[0];
-    int d[16];
-    d[0] = v - p[3 * W];      d[1] = v - p[3 * W + 1];  d[2] = v - p[2 * W + 2];  d[3] = v - p[W + 3];
-    d[4] = v - p[3];          d[5] = v - p[-W + 3];     d[6] = v - p[-2 * W + 2]; d[7] = v - p[-3 * W + 1];
-    d[8] = v - p[-3 * W];     d[9] = v - p[-3 * W - 1]; d[10] = v - p[-2 * W - 2]; d[11] = v - p[-W - 3];
-    d[12] = v - p[-3];        d[13] = v - p[W - 3];     d[14] = v - p[2 * W - 2]; d[15] = v - p[3 * W - 1];
-    int mn2[16], mx2[16];
+// threshold independent and "corner at t" <=> s >= t.  Computed for two horizontally
+// adjacent pixels at once in packed 16-bit lanes (v_pk_sub/min/max_i16).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ s16x2 pmin(s16x2 a, s16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ s16x2 pmax(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
+
+constexpr int kPairStride = 48;   // dwords per LDS pair-image row (== 16 mod 32: rows 16 pairs apart hit other banks)
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// The ROI lives in LDS as two pair images of 2 x u16 per dword:  E[r][i] = (roi[r][2i], roi[r][2i+1])
+// and O[r][i] = (roi[r][2i+1], roi[r][2i+2]).  The pixel pair (x, x+1) at odd x is O[r][(x-1)/2]; a tap
+// at horizontal offset dx reads O (dx even) or E (dx odd) -- every one of the 17 reads for two pixels is
+// a 4-byte-aligned ds_read_b32 with a compile-time offset (2-byte-misaligned 32-bit LDS reads measured
+// ~2x slower on gfx950).  The reads are explicit (inline asm) so the compiler does not merge neighbours
+// into misaligned b64/b128 reads.
+__device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, const uint32_t* __restrict__ O, int y, int j) {
+    const uint32_t* eb = E + (y - 3) * kPairStride + j;   // row y-3, pair index j; offsets >= 0
+    const uint32_t* ob = O + (y - 3) * kPairStride + j;
+    uint32_t r[17];
+#define ORBX_TAP(k, dx, dy) \
+    r[k] = ((dx) & 1) ? eb[((dy) + 3) * kPairStride + (3 + (dx)) / 2] : ob[((dy) + 3) * kPairStride + 1 + (dx) / 2]
+    ORBX_TAP(16, 0, 0);
+    ORBX_TAP(0, 0, 3);    ORBX_TAP(1, 1, 3);    ORBX_TAP(2, 2, 2);    ORBX_TAP(3, 3, 1);
+    ORBX_TAP(4, 3, 0);    ORBX_TAP(5, 3, -1);   ORBX_TAP(6, 2, -2);   ORBX_TAP(7, 1, -3);
+    ORBX_TAP(8, 0, -3);   ORBX_TAP(9, -1, -3);  ORBX_TAP(10, -2, -2); ORBX_TAP(11, -3, -1);
+    ORBX_TAP(12, -3, 0);  ORBX_TAP(13, -3, 1);  ORBX_TAP(14, -2, 2);  ORBX_TAP(15, -1, 3);
+#undef ORBX_TAP
+    const s16x2 v = as_s2(r[16]);
+    s16x2 d[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { mn2[k] = min(d[k], d[(k + 1) & 15]); mx2[k] = max(d[k], d[(k + 1) & 15]); }
-    int mn4[16], mx4[16];
+    for (int k = 0; k < 16; ++k) d[k] = v - as_s2(r[k]);
+    s16x2 mn2[16], mx2[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { mn4[k] = min(mn2[k], mn2[(k + 2) & 15]); mx4[k] = max(mx2[k], mx2[(k + 2) & 15]); }
-    int dark = -1000, brightneg = 1000;
+    for (int k = 0; k < 16; ++k) { mn2[k] = pmin(d[k], d[(k + 1) & 15]); mx2[k] = pmax(d[k], d[(k + 1) & 15]); }
+    s16x2 mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { mn4[k] = pmin(mn2[k], mn2[(k + 2) & 15]); mx4[k] = pmax(mx2[k], mx2[(k + 2) & 15]); }
+    s16x2 mn9[16], mx9[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        dark = max(dark, mn9);
-        brightneg = min(brightneg, mx9);
+        mn9[k] = pmin(pmin(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+        mx9[k] = pmax(pmax(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
     }
-    return max(dark, -brightneg) - 1;
+#pragma unroll
+    for (int w = 8; w > 0; w >>= 1)      // balanced reductions (short dependency chains)
+#pragma unroll
+        for (int k = 0; k < w; ++k) { mn9[k] = pmax(mn9[k], mn9[k + w]); mx9[k] = pmin(mx9[k], mx9[k + w]); }
+    return pmax(mn9[0], (s16x2)(0) - mx9[0]) - (s16x2)(1);
+}
+
+// NMS for a pixel pair from a 3x4 int16 window of the padded score map (pad ring -1): flags of the two
+// pixels at both thresholds (bit0/1: pixel 0/1 at iniTh, bit2/3: at minTh).  A pixel is kept iff it is
+// a strict local maximum of the masked scores (neighbour s if s >= t else 0) and s >= t (FAST_t NMS).
+__device__ __forceinline__ int nms_pair(const int16_t (&a)[3][4], int ti, int tm, bool second) {
+    int out = 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int s = a[1][1 + e];
+        int mi = 0, mm = 0;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                if (dy == 1 && dx == 1) continue;
+                const int n = a[dy][e + dx];
+                mi = max(mi, n >= ti ? n : 0);
+                mm = max(mm, n >= tm ? n : 0);
+            }
+        const bool valid = (e == 0) || second;
+        out |= ((valid && s >= ti && s > mi) ? 1 : 0) << e;
+        out |= ((valid && s >= tm && s > mm) ? 1 : 0) << (2 + e);
+    }
+    return out;
 }
 
 // One workgroup per (cell, image).  Cell geometry from ComputeKeyPointsOctTree (:784-807); FAST on the
 // ROI detects rows/cols [3, dim-3) of the ROI, NMS compares against the 8 neighbours' scores inside
 // the ROI's detection window (0 outside), strict '>' (OpenCV FAST_t).  Empty at iniTh -> minTh (:812-816).
+// Dynamic LDS: E and O pair images (max_rows x kPairStride dwords each) + padded int16 score map whose
+// pixel pairs are dword aligned (det column x at map column x + 2, pad ring at columns 1 and Wd + 2).
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                     const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
                                                     int iniTh, int minTh, uint32_t* __restrict__ cand_xy,
                                                     uint8_t* __restrict__ cand_s, int cand_stride,
-                                                    int* __restrict__ cell_cnt, int ncells) {
-    __shared__ uint8_t roi[kMaxRoi * kMaxRoi];
-    __shared__ int16_t sc[kMaxRoi * kMaxRoi];
+                                                    int* __restrict__ cell_cnt, int ncells, int stop_after, Src0 s0,
+                                                    int max_rows) {
+    extern __shared__ uint32_t fsm[];
     __shared__ int red[8];
+    uint32_t* E = fsm;
+    uint32_t* O = fsm + max_rows * kPairStride;
+    int16_t* sc = (int16_t*)(fsm + 2 * max_rows * kPairStride);
     const int img = blockIdx.y, c = blockIdx.x, tid = threadIdx.x;
+    const int w = tid >> 6, nw = blockDim.x >> 6, ln = lane_id();
     const CellDev cd = cells[c];
     const LevelDev L = levels[cd.level];
-    const uint8_t* base = pyr + img * pyr_stride + L.pyr_off;
+    int lstride;
+    const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
     const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
-    for (int i = tid; i < W * H; i += blockDim.x) {
-        const int r = i / W, q = i - r * W;
-        roi[i] = base[(size_t)(cd.y0 + r) * L.w + cd.x0 + q];
+    if (Wd <= 0 || Hd <= 0) {
+        if (tid == 0) cell_cnt[(size_t)img * ncells + c] = 0;
+        return;
     }
-    __syncthreads();
-    const int npx = (Wd > 0 && Hd > 0) ? Wd * Hd : 0;
-    for (int i = tid; i < npx; i += blockDim.x) {
-        const int r = i / Wd, q = i - r * Wd;
-        sc[i] = (int16_t)fast_score(roi + (r + 3) * W + (q + 3), W);
-    }
-    __syncthreads();
-
-    auto is_kp = [&](int i, int t) -> bool {
-        const int r = i / Wd, q = i - r * Wd;
-        const int s = sc[i];
-        if (s < t) return false;
+    // 1. every ROI byte loaded once (lane = column, one wave per row, all loads issued before the first
+    //    wait) and stored twice as u16: E at column q, O at column q - 1
+    const int SW = (Wd + 5) & ~1;        // int16 per score-map row (even: rows stay dword aligned)
+    {
+        constexpr int kRowsPerWave = kMaxRoi / 4;
+        uint16_t* E16 = (uint16_t*)E;
+        uint16_t* O16 = (uint16_t*)O;
+        const uint8_t* src0 = base + (size_t)cd.y0 * lstride + cd.x0;
+        for (int q0 = 0; q0 < W + 2; q0 += kWave) {
+            const int q = q0 + ln, qc = min(q, W - 1);
+            uint32_t v[kRowsPerWave];
 #pragma unroll
-        for (int dy = -1; dy <= 1; ++dy)
+            for (int k = 0; k < kRowsPerWave; ++k) v[k] = src0[(size_t)min(w + 4 * k, H - 1) * lstride + qc];
 #pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-                if (!dy && !dx) continue;
-                const int rr = r + dy, qq = q + dx;
-                int n = 0;
-                if (rr >= 0 && rr < Hd && qq >= 0 && qq < Wd) {
-                    n = sc[rr * Wd + qq];
-                    if (n < t) n = 0;
+            for (int k = 0; k < kRowsPerWave; ++k) {
+                const int r = w + 4 * k;
+                if (r < H && q < W + 2) {
+                    const uint16_t b = q < W ? (uint16_t)v[k] : 0;
+                    E16[r * 2 * kPairStride + q] = b;
+                    if (q >= 1) O16[r * 2 * kPairStride + q - 1] = b;
                 }
-                if (!(s > n)) return false;
             }
-        return true;
-    };
-
-    const int t_ini = min(max(iniTh, 0), 255), t_min = min(max(minTh, 0), 255);
-    int mine = 0;
-    for (int i = tid; i < npx; i += blockDim.x) mine += is_kp(i, t_ini) ? 1 : 0;
-    const int found = __syncthreads_or(mine);
-    const int t = found ? t_ini : t_min;
-
-    // row-major compaction (order of OpenCV's keypoint output) into the cell's slots
+        }
+    }
+    for (int i = tid; i < SW; i += blockDim.x) { sc[i] = -1; sc[(Hd + 1) * SW + i] = -1; }
+    for (int r = tid; r < Hd + 2; r += blockDim.x) { sc[r * SW + 1] = -1; sc[r * SW + Wd + 2] = -1; }
+    __syncthreads();
+    if (stop_after == 1) { if (tid == 0) cell_cnt[(size_t)img * ncells + c] = (int)(E[tid] & 0); return; }
+    // 2. scores, two pixels per lane: pair q -> det row rr, pixels x = 3 + 2j, x + 1 (ROI coords)
+    const int PR = (Wd + 1) >> 1, NP = Hd * PR;
+    for (int q = tid; q < NP; q += blockDim.x) {
+        const int rr = q / PR, j = q - rr * PR;
+        const s16x2 s2 = fast_score2(E, O, rr + 3, j);
+        *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
+    }
+    __syncthreads();
+    if (stop_after == 2) { if (tid == 0) cell_cnt[(size_t)img * ncells + c] = sc[tid * 5] & 0; return; }
+    // 3. NMS at iniTh and minTh in one pass from 3 x 3 aligned dwords per pair; 4 flag bits per pair
+    //    iteration kept in a register
+    const int ti = min(max(iniTh, 0), 255), tm = min(max(minTh, 0), 255);
+    uint32_t flags = 0;
+    int it = 0;
+    for (int q = tid; q < NP; q += blockDim.x, ++it) {
+        const int rr = q / PR, j = q - rr * PR;
+        int16_t a[3][4];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+            const uint32_t* rowp = (const uint32_t*)(sc + (rr + dy) * SW + 2 * j);
+            const s16x2 d0 = as_s2(rowp[0]), d1 = as_s2(rowp[1]), d2 = as_s2(rowp[2]);
+            a[dy][0] = d0.y; a[dy][1] = d1.x; a[dy][2] = d1.y; a[dy][3] = d2.x;
+        }
+        flags |= (uint32_t)nms_pair(a, ti, tm, 2 * j + 1 < Wd) << (4 * it);
+    }
+    const int any_ini = __syncthreads_or((flags & 0x33333333u) != 0);
+    const int sel = any_ini ? 0 : 2;          // cell empty at iniTh -> minTh (:812-816)
+    if (stop_after == 3) { if (tid == 0) cell_cnt[(size_t)img * ncells + c] = (int)(flags & 0); return; }
+    // 4. row-major compaction (OpenCV's output order) into the cell's slots
     uint32_t* oxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
     uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
-    const int w = tid >> 6, nw = blockDim.x >> 6;
     int running = 0;
-    for (int b = 0; b < npx; b += blockDim.x) {
-        const int i = b + tid;
-        const bool k = (i < npx) && is_kp(i, t);
-        const uint64_t m = __ballot(k);
-        if (lane_id() == 0) red[w] = __popcll(m);
+    it = 0;
+    for (int b = 0; b < NP; b += blockDim.x, ++it) {
+        const int q = b + tid;
+        const bool f0 = q < NP && ((flags >> (4 * it + sel)) & 1u);
+        const bool f1 = q < NP && ((flags >> (4 * it + sel + 1)) & 1u);
+        const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
+        if (ln == 0) red[w] = __popcll(m0) + __popcll(m1);
         __syncthreads();
         int before = running, tot = 0;
-        for (int j = 0; j < nw; ++j) { before += (j < w) ? red[j] : 0; tot += red[j]; }
-        if (k) {
-            const int pos = before + lanes_below(m);
-            if (pos < cd.slot_cap) {
-                const int r = i / Wd, q = i - r * Wd;
-                oxy[pos] = (uint32_t)(cd.x0 + q + 3) | ((uint32_t)(cd.y0 + r + 3) << 16);
-                os[pos] = (uint8_t)sc[i];
-            }
+        for (int k = 0; k < nw; ++k) { before += (k < w) ? red[k] : 0; tot += red[k]; }
+        if (f0 || f1) {
+            const int rr = q / PR, j = q - rr * PR;
+            const int16_t* cp = sc + (rr + 1) * SW + 2 + 2 * j;
+            int pos = before + lanes_below(m0) + lanes_below(m1);
+            const uint32_t yv = (uint32_t)(cd.y0 + rr + 3) << 16;
+            if (f0 && pos < cd.slot_cap) { oxy[pos] = (uint32_t)(cd.x0 + 3 + 2 * j) | yv; os[pos] = (uint8_t)cp[0]; }
+            pos += f0 ? 1 : 0;
+            if (f1 && pos < cd.slot_cap) { oxy[pos] = (uint32_t)(cd.x0 + 4 + 2 * j) | yv; os[pos] = (uint8_t)cp[1]; }
         }
         running += tot;
         __syncthreads();
@@ -237,39 +332,68 @@ __device__ __forceinline__ int refl101(int i, int n) {
     return i;
 }
 
+// Register-streaming form: one wave per (level, 256-column strip, 32-row band).  Lane l owns the 4
+// output columns x0 = strip*256 + 4l .. x0+3, walks down the band's 38 input rows once, and keeps the
+// last 7 rows of horizontal sums in registers (a ring unrolled by 7, so no moves); no LDS, no
+// divisions.  Reflection only at the level borders (scalar for rows, per byte for edge lanes).
+constexpr int kBlurBand = 32, kBlurStrip = 256;
+
+__device__ __forceinline__ void blur_hrow(const uint8_t* __restrict__ row, int x0, int w, bool interior, int h[4]) {
+    int b[10];
+    if (interior) {
+#pragma unroll
+        for (int i = 0; i < 10; ++i) b[i] = row[x0 - 3 + i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 10; ++i) b[i] = row[refl101(x0 - 3 + i, w)];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        h[j] = 18 * (b[j] + b[j + 6]) + 34 * (b[j + 1] + b[j + 5]) + 49 * (b[j + 2] + b[j + 4]) + 55 * b[j + 3];
+}
+
 __global__ __launch_bounds__(256) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                size_t pyr_stride, const LevelDev* __restrict__ levels,
-                                               const BlurTile* __restrict__ tiles) {
-    constexpr int TW = 64, TH = 16;
-    __shared__ uint8_t in[(TH + 6) * (TW + 6)];
-    __shared__ int hs[(TH + 6) * TW];
-    const int img = blockIdx.y, tid = threadIdx.x;
-    const BlurTile bt = tiles[blockIdx.x];
+                                               const BlurTile* __restrict__ tiles, int ntiles, Src0 s0) {
+    const int img = blockIdx.y;
+    const int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (t >= ntiles) return;
+    const BlurTile bt = tiles[t];
     const LevelDev L = levels[bt.level];
-    const uint8_t* S = pyr + img * pyr_stride + L.pyr_off;
+    const int x0 = bt.tx * kBlurStrip + 4 * lane_id();
+    if (x0 >= L.w) return;
+    int sstride;
+    const uint8_t* S = level_pixels(pyr, pyr_stride, L, bt.level, img, s0, sstride);
     uint8_t* D = blur + img * pyr_stride + L.pyr_off;
-    const int X0 = bt.tx * TW, Y0 = bt.ty * TH;
-    for (int i = tid; i < (TH + 6) * (TW + 6); i += blockDim.x) {
-        const int r = i / (TW + 6), q = i - r * (TW + 6);
-        const int y = refl101(Y0 + r - 3, L.h), x = refl101(X0 + q - 3, L.w);
-        in[i] = S[(size_t)y * L.w + x];
+    const int y0 = bt.ty * kBlurBand, y1 = min(y0 + kBlurBand, L.h);
+    const bool interior = (x0 - 3 >= 0) && (x0 + 7 <= L.w);
+    int r0[4], r1[4], r2[4], r3[4], r4[4], r5[4], r6[4];
+#define ORBX_HROW(dst, yy) blur_hrow(S + (size_t)refl101((yy), L.h) * sstride, x0, L.w, interior, dst)
+    ORBX_HROW(r0, y0 - 3);
+    ORBX_HROW(r1, y0 - 2);
+    ORBX_HROW(r2, y0 - 1);
+    ORBX_HROW(r3, y0);
+    ORBX_HROW(r4, y0 + 1);
+    ORBX_HROW(r5, y0 + 2);
+    auto emit = [&](int y, const int* a, const int* b, const int* c, const int* d, const int* e, const int* f, const int* g) {
+        uint8_t* o = D + (size_t)y * L.w + x0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int acc = 18 * (a[j] + g[j]) + 34 * (b[j] + f[j]) + 49 * (c[j] + e[j]) + 55 * d[j];
+            if (x0 + j < L.w) o[j] = (uint8_t)min(max((acc + (1 << 15)) >> 16, 0), 255);
+        }
+    };
+    // ring of 7 row sums; each unrolled step loads row y+3 into the slot freed by row y-4
+    for (int y = y0; y < y1; y += 7) {
+        ORBX_HROW(r6, y + 3); emit(y, r0, r1, r2, r3, r4, r5, r6); if (y + 1 >= y1) break;
+        ORBX_HROW(r0, y + 4); emit(y + 1, r1, r2, r3, r4, r5, r6, r0); if (y + 2 >= y1) break;
+        ORBX_HROW(r1, y + 5); emit(y + 2, r2, r3, r4, r5, r6, r0, r1); if (y + 3 >= y1) break;
+        ORBX_HROW(r2, y + 6); emit(y + 3, r3, r4, r5, r6, r0, r1, r2); if (y + 4 >= y1) break;
+        ORBX_HROW(r3, y + 7); emit(y + 4, r4, r5, r6, r0, r1, r2, r3); if (y + 5 >= y1) break;
+        ORBX_HROW(r4, y + 8); emit(y + 5, r5, r6, r0, r1, r2, r3, r4); if (y + 6 >= y1) break;
+        ORBX_HROW(r5, y + 9); emit(y + 6, r6, r0, r1, r2, r3, r4, r5);
     }
-    __syncthreads();
-    const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;
-    for (int i = tid; i < (TH + 6) * TW; i += blockDim.x) {
-        const int r = i / TW, q = i - r * TW;
-        const uint8_t* p = in + r * (TW + 6) + q;
-        hs[i] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
-    }
-    __syncthreads();
-    for (int i = tid; i < TH * TW; i += blockDim.x) {
-        const int r = i / TW, q = i - r * TW;
-        const int y = Y0 + r, x = X0 + q;
-        if (y >= L.h || x >= L.w) continue;
-        const int* p = hs + r * TW + q;
-        const int acc = k0 * (p[0] + p[6 * TW]) + k1 * (p[TW] + p[5 * TW]) + k2 * (p[2 * TW] + p[4 * TW]) + k3 * p[3 * TW];
-        D[(size_t)y * L.w + x] = (uint8_t)min(max((acc + (1 << 15)) >> 16, 0), 255);
-    }
+#undef ORBX_HROW
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -639,7 +763,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                   const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
                                                   int out_stride, const int* __restrict__ level_cnt,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
-                                                  int capacity, int total_slots) {
+                                                  int capacity, int total_slots, Src0 s0) {
     const int img = blockIdx.y;
     const int slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int ln = lane_id();
@@ -663,18 +787,29 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     const uint32_t xy = lvl_xy[(size_t)img * out_stride + L.out_off + i];
     const int cx = (int)(xy & 0xffff), cy = (int)(xy >> 16);
     // --- IC_Angle (:77-104): m10 = sum u*I, m01 = sum v*I over the radius-15 disc
-    const uint8_t* P = pyr + img * pyr_stride + L.pyr_off;
+    int pstride;
+    const uint8_t* P = level_pixels(pyr, pyr_stride, L, lvl, img, s0, pstride);
     int m10 = 0, m01 = 0;
     {
+        // lane: column u = (ln & 31) - 15, row parity h = ln >> 5; rows v = -15 + 2*it + h.  All 16 loads
+        // are issued unconditionally (row clamped to the disc) and masked afterwards.
         const int h = ln >> 5, u = (ln & 31) - kHalfPatch;
+        const int au = u < 0 ? -u : u;
+        const uint8_t* col = P + (size_t)cy * pstride + cx + min(u, kHalfPatch);
+        int val[16];
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int v = min(-kHalfPatch + 2 * it + h, kHalfPatch);
+            val[it] = col[v * pstride];
+        }
+#pragma unroll
         for (int it = 0; it < 16; ++it) {
             const int v = -kHalfPatch + 2 * it + h;
-            if (v > kHalfPatch || (ln & 31) > 30) continue;
             const int av = v < 0 ? -v : v;
-            if (u < -c_umax[av] || u > c_umax[av]) continue;
-            const int val = P[(size_t)(cy + v) * L.w + cx + u];
-            m10 += u * val;
-            m01 += v * val;
+            const bool in = (v <= kHalfPatch) && ((ln & 31) <= 30) && (au <= kUmax[av > 15 ? 15 : av]);
+            const int x = in ? val[it] : 0;
+            m10 += u * x;
+            m01 += v * x;
         }
     }
     m10 = wave_sum(m10);
@@ -725,8 +860,8 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
 static int round_even_f(float v) { return (int)std::nearbyintf(v); }
 static int round_even_d(double v) { return (int)std::nearbyint(v); }
 
-enum Stage { ST_COPY = 0, ST_RESIZE, ST_FAST, ST_BLUR, ST_QUADTREE, ST_DESCRIBE, ST_COUNT };
-static const char* kStageNames[ST_COUNT] = {"copy_level0", "resize", "fast_cells", "blur7", "quadtree", "describe"};
+enum Stage { ST_RESIZE = 0, ST_FAST, ST_BLUR, ST_QUADTREE, ST_DESCRIBE, ST_COUNT };
+static const char* kStageNames[ST_COUNT] = {"resize", "fast_cells", "blur7", "quadtree", "describe"};
 
 struct Extractor {
     // ORBextractor parameters and tables (:410-470)
@@ -748,6 +883,8 @@ struct Extractor {
     int cand_stride = 0;      // candidate slots per image
     int out_stride = 0;       // quadtree output slots per image
     int node_cap = 0;
+    int cell_max_rows = 0, cell_max_cols = 0;
+    int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
     int out_capacity = 0;     // max keypoints per image
 
@@ -776,6 +913,7 @@ struct Extractor {
     uint8_t* d_desc = nullptr;
     int32_t* d_cnt = nullptr;
     int last_batch = 0;
+    Src0 last_src0{nullptr, 0, 0};   // level 0 of the last device call = the caller's images
 
     // timing: a pool of event sets recorded on the launch stream, resolved lazily (no host sync per call)
     struct EventSet { hipEvent_t ev[ST_COUNT + 1]; bool pending; };
@@ -854,6 +992,9 @@ void Extractor::free_buffers() {
 }
 
 static size_t qt_lds_bytes(int cap, int scan_cap);
+static size_t fast_lds_bytes(const Extractor* e) {
+    return (size_t)2 * e->cell_max_rows * kPairStride * 4 + (size_t)(e->cell_max_rows - 4) * (e->cell_max_cols) * 2 + 16;
+}
 
 template <typename T>
 static int dev_alloc(T** p, size_t count) {
@@ -910,6 +1051,7 @@ int Extractor::configure(int r, int c, int batch) {
                     cd.x0 = (int)iniX; cd.y0 = (int)iniY;
                     cd.W = (int)maxX - cd.x0; cd.H = (int)maxY - cd.y0;
                     ORBX_REQUIRE(cd.W <= kMaxRoi && cd.H <= kMaxRoi, ORBX_ERR_UNSUPPORTED, "cell ROI too large");
+                    ORBX_REQUIRE((cd.H - 6) * ((cd.W - 5) / 2) <= 8 * 256, ORBX_ERR_UNSUPPORTED, "cell too large");
                     const int wd = std::max(cd.W - 6, 0), hd = std::max(cd.H - 6, 0);
                     cd.slot_cap = ((wd + 1) / 2) * ((hd + 1) / 2);   // strict 3x3 NMS: <= 1 per 2x2 block
                     cd.slot_off = cand;
@@ -933,10 +1075,13 @@ int Extractor::configure(int r, int c, int batch) {
         outs += L.out_cap;
         cap = std::max(cap, L.out_cap);
         // blur tiles
-        for (int ty = 0; ty < (L.h + 15) / 16; ++ty)
-            for (int tx = 0; tx < (L.w + 63) / 64; ++tx) tilev.push_back(BlurTile{l, tx, ty, 0});
+        for (int ty = 0; ty < (L.h + kBlurBand - 1) / kBlurBand; ++ty)
+            for (int tx = 0; tx < (L.w + kBlurStrip - 1) / kBlurStrip; ++tx) tilev.push_back(BlurTile{l, tx, ty, 0});
     }
     ORBX_REQUIRE(cap < 32768 && cap < (1 << 20), ORBX_ERR_UNSUPPORTED, "node capacity %d too large", cap);
+    cell_max_rows = 8; cell_max_cols = 8;
+    for (const CellDev& cd : cellv) { cell_max_rows = std::max(cell_max_rows, cd.H); cell_max_cols = std::max(cell_max_cols, cd.W); }
+    ORBX_REQUIRE((cell_max_cols + 2) / 2 <= kPairStride, ORBX_ERR_UNSUPPORTED, "cell too wide");
     int scap = cap;
     for (const LevelDev& L : lv) scap = std::max(scap, std::max(L.cell_end - L.cell_begin, L.nIni));
     scan_cap = scap + 1;
@@ -1043,30 +1188,31 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         es->pending = true;
     }
     auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], s); };
+    const Src0 s0{d_images, step, istride};
+    e->last_src0 = s0;
     mark(0);
-    {
-        dim3 g((e->lv[0].w + 255) / 256, e->lv[0].h, batch);
-        hipLaunchKernelGGL(k_copy_level0, g, dim3(256), 0, s, d_images, step, istride, e->d_pyr, ps, e->lv[0].w, e->lv[0].h);
-    }
-    mark(1);
     for (int l = 1; l < nl; ++l) {
         dim3 g((e->lv[l].w + 255) / 256, e->lv[l].h, batch);
-        hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, e->d_pyr, ps, e->lv[l - 1].pyr_off, e->lv[l - 1].w,
-                           e->lv[l].pyr_off, e->lv[l].w, e->lv[l].h, e->rtab[l]);
+        const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
+        const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
+        hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis, e->lv[l].pyr_off, e->lv[l].w,
+                           e->lv[l].h, e->rtab[l]);
     }
-    mark(2);
+    mark(1);
     const int ncells = (int)e->cellv.size();
     if (ncells > 0) {
         dim3 g(ncells, batch);
-        hipLaunchKernelGGL(k_fast_cells, g, dim3(256), 0, s, e->d_pyr, ps, e->d_levels, e->d_cells, e->iniTh, e->minTh,
-                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells);
+        hipLaunchKernelGGL(k_fast_cells, g, dim3(256), fast_lds_bytes(e), s, e->d_pyr, ps, e->d_levels, e->d_cells, e->iniTh, e->minTh,
+                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, e->fast_stop_after, s0,
+                           e->cell_max_rows);
+    }
+    mark(2);
+    {
+        const int nt = (int)e->tilev.size();
+        dim3 g((nt + 3) / 4, batch);
+        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles, nt, s0);
     }
     mark(3);
-    {
-        dim3 g((unsigned)e->tilev.size(), batch);
-        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles);
-    }
-    mark(4);
     {
         QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
         dim3 g(nl, batch);
@@ -1074,14 +1220,14 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
                            e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
                            e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err);
     }
-    mark(5);
+    mark(4);
     {
         const int total_slots = e->out_stride;
         dim3 g((total_slots * 64 + 255) / 256, batch);
         hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
-                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, total_slots);
+                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, total_slots, s0);
     }
-    mark(6);
+    mark(5);
     ORBX_HIP(hipGetLastError());
     e->last_batch = batch;
     return ORBX_OK;
@@ -1093,7 +1239,8 @@ static int g_const_status = ORBX_OK;
 static int upload_constants(const Extractor* e) {
     // pattern is a fixed table; umax is the same for every extractor (depends only on HALF_PATCH_SIZE)
     ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)));
-    ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), e->umax, sizeof(int) * 16));
+    for (int v = 0; v < 16; ++v)
+        ORBX_REQUIRE(e->umax[v] == kUmax[v], ORBX_ERR_UNSUPPORTED, "umax table mismatch at %d", v);
     return ORBX_OK;
 }
 
@@ -1141,6 +1288,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
         return ORBX_ERR_HIP;
     }
     e->own_stream = true;
+    if (const char* ab = std::getenv("ORBX_FAST_ABLATE")) e->fast_stop_after = std::atoi(ab);
     std::call_once(g_const_once, [&] { g_const_status = upload_constants(e); });
     if (g_const_status != ORBX_OK) {
         (void)hipStreamDestroy(e->stream);
@@ -1267,11 +1415,18 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     return ORBX_OK;
 }
 
-int orbx_extractor_level_device(orbx_extractor* e, int index, int level, const uint8_t** d_level, int* rows, int* cols) {
-    ORBX_REQUIRE(e && d_level && rows && cols, ORBX_ERR_ARG, "null argument");
-    ORBX_REQUIRE(e->d_pyr && level >= 0 && level < e->nlevels && index >= 0 && index < e->max_batch, ORBX_ERR_ARG,
-                 "no pyramid for index %d level %d", index, level);
-    *d_level = e->d_pyr + (size_t)index * e->pyr_size + e->lv[level].pyr_off;
+int orbx_extractor_level_device(orbx_extractor* e, int index, int level, const uint8_t** d_level, int* rows, int* cols,
+                                size_t* step) {
+    ORBX_REQUIRE(e && d_level && rows && cols && step, ORBX_ERR_ARG, "null argument");
+    ORBX_REQUIRE(e->d_pyr && e->last_src0.p && level >= 0 && level < e->nlevels && index >= 0 && index < e->last_batch,
+                 ORBX_ERR_ARG, "no pyramid for index %d level %d", index, level);
+    if (level == 0) {
+        *d_level = e->last_src0.p + (size_t)index * e->last_src0.istride;
+        *step = e->last_src0.step;
+    } else {
+        *d_level = e->d_pyr + (size_t)index * e->pyr_size + e->lv[level].pyr_off;
+        *step = (size_t)e->lv[level].w;
+    }
     *rows = e->lv[level].h;
     *cols = e->lv[level].w;
     return ORBX_OK;
@@ -1280,11 +1435,12 @@ int orbx_extractor_level_device(orbx_extractor* e, int index, int level, const u
 int orbx_extractor_copy_level(orbx_extractor* e, int index, int level, uint8_t* dst, size_t dst_step) {
     const uint8_t* p;
     int r, c;
-    int st = orbx_extractor_level_device(e, index, level, &p, &r, &c);
+    size_t sp;
+    int st = orbx_extractor_level_device(e, index, level, &p, &r, &c, &sp);
     if (st) return st;
     ORBX_REQUIRE(dst && dst_step >= (size_t)c, ORBX_ERR_ARG, "bad destination");
     ORBX_HIP(hipSetDevice(e->device));
-    ORBX_HIP(hipMemcpy2DAsync(dst, dst_step, p, c, c, r, hipMemcpyDeviceToHost, e->stream));
+    ORBX_HIP(hipMemcpy2DAsync(dst, dst_step, p, sp, c, r, hipMemcpyDeviceToHost, e->stream));
     ORBX_HIP(hipStreamSynchronize(e->stream));
     return ORBX_OK;
 }

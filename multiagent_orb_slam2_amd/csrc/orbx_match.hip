@@ -6,8 +6,9 @@
 //                        8 VGPRs), train descriptors staged through LDS in 256-row blocks and read as
 //                        wave-uniform broadcasts; v_xor + v_bcnt_u32_b32; per-(query, train-chunk)
 //                        partial best/second merged by a second launch.  No MFMA: popcount-bound.
-//   k_stereo            Frame::ComputeStereoMatches descriptor search (src/Frame.cc:466-552), one wave
-//                        per left keypoint, band/octave/disparity mask, packed (dist, index) wave min.
+//   k_stereo_rows/k_stereo  Frame::ComputeStereoMatches descriptor search (src/Frame.cc:466-552): right
+//                        keypoints bucketed by row, then one wave per left keypoint over the rows its
+//                        band can reach, band/octave/disparity mask, packed (dist, index) wave min.
 //   k_bow_kfkf / k_bow_kff / k_triangulate   BoW-bucketed matchers (src/ORBmatcher.cc:161-290, 524-657,
 //                        659-825): one wave per FeatureVector node of the first view; the greedy
 //                        "already matched" state is node-local (a feature belongs to one node), so the
@@ -120,16 +121,44 @@ struct StereoArgs {
     int nl_fixed, nr_fixed; // used when nl/nr are null
     float scale[32];
     int nlevels, rows;
+    int band;               // rows a right keypoint's band can reach: ceil(2 * max scale) + 2
     float maxD;             // bf / b (Frame.cc:496-498)
+    int32_t* row_start;     // [batch][rows + 1]  right keypoints bucketed by floor(y)
+    int32_t* row_idx;       // [batch][capacity]
     int32_t* best_idx; int32_t* best_dist;
 };
+
+// Counting sort of one image pair's right keypoints by row (the row table of Frame.cc:476-493, kept as
+// a bucket per floor(y) instead of one list per covered row); order inside a bucket is irrelevant
+// because the search below reduces with a (distance, index) minimum.
+__global__ __launch_bounds__(1024) void k_stereo_rows(StereoArgs A) {
+    extern __shared__ int cnt[];   // rows + 1
+    __shared__ int tmp[40];
+    const int img = blockIdx.x, tid = threadIdx.x;
+    const int nr = A.nr ? A.nr[img] : A.nr_fixed;
+    const size_t ob = (size_t)img * A.capacity;
+    for (int r = tid; r <= A.rows; r += blockDim.x) cnt[r] = 0;
+    __syncthreads();
+    for (int i = tid; i < nr; i += blockDim.x) {
+        const int r = min(max((int)floorf(A.kr[ob + i].y), 0), A.rows - 1);
+        atomicAdd(&cnt[r], 1);
+    }
+    __syncthreads();
+    block_scan_array(cnt, A.rows + 1, tmp);
+    int32_t* rs = A.row_start + (size_t)img * (A.rows + 1);
+    for (int r = tid; r <= A.rows; r += blockDim.x) rs[r] = cnt[r];
+    __syncthreads();
+    for (int i = tid; i < nr; i += blockDim.x) {
+        const int r = min(max((int)floorf(A.kr[ob + i].y), 0), A.rows - 1);
+        A.row_idx[ob + atomicAdd(&cnt[r], 1)] = i;
+    }
+}
 
 __global__ __launch_bounds__(256) void k_stereo(StereoArgs A) {
     const int img = blockIdx.y;
     const int iL = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int ln = lane_id();
     const int nl = A.nl ? A.nl[img] : A.nl_fixed;
-    const int nr = A.nr ? A.nr[img] : A.nr_fixed;
     if (iL >= nl) return;
     const size_t ob = (size_t)img * A.capacity;
     const orbx_keypoint kL = A.kl[ob + iL];
@@ -140,7 +169,10 @@ __global__ __launch_bounds__(256) void k_stereo(StereoArgs A) {
     if (vrow >= 0 && vrow < A.rows && !(maxU < 0)) {
         uint4 a0, a1;
         load_desc(A.dl + 32 * (ob + iL), a0, a1);
-        for (int iR = ln; iR < nr; iR += kWave) {
+        const int32_t* rs = A.row_start + (size_t)img * (A.rows + 1);
+        const int c0 = rs[max(vrow - A.band, 0)], c1 = rs[min(vrow + A.band, A.rows - 1) + 1];
+        for (int c = c0 + ln; c < c1; c += kWave) {
+            const int iR = A.row_idx[ob + c];
             const orbx_keypoint kR = A.kr[ob + iR];
             const float r = 2.0f * A.scale[kR.octave];                       // :487
             const int maxr = (int)ceilf(kR.y + r), minr = (int)floorf(kR.y - r);
@@ -392,9 +424,16 @@ struct Matcher {
     // growable device scratch
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
-    int reserve(size_t bytes) {
+    int reserve(size_t bytes) { return reserve_on(bytes, stream); }
+    // grow the scratch buffer; work already queued on 'on' (and on the own stream) may still use the old one
+    int reserve_on(size_t bytes, hipStream_t on) {
         if (bytes <= scratch_bytes) return ORBX_OK;
-        if (scratch) { (void)hipStreamSynchronize(stream); (void)hipFree(scratch); scratch = nullptr; }
+        if (scratch) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamSynchronize(on);
+            (void)hipFree(scratch);
+            scratch = nullptr;
+        }
         size_t nb = std::max(bytes, scratch_bytes * 2);
         ORBX_HIP(hipMalloc(&scratch, nb));
         scratch_bytes = nb;
@@ -493,7 +532,7 @@ int orbx_bf_match_device(orbx_matcher* m, const uint8_t* dq, int nq, const uint8
     ORBX_REQUIRE(dq && bi && bd && sd && (nt == 0 || dt), ORBX_ERR_ARG, "null pointer");
     ORBX_HIP(hipSetDevice(m->device));
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
-    int st = m->reserve(bf_scratch(nq, std::max(nt, 1)));
+    int st = m->reserve_on(bf_scratch(nq, std::max(nt, 1)), s);
     if (st) return st;
     if (nt == 0) {
         std::vector<int32_t> neg(nq, -1), d256(nq, 256);
@@ -540,12 +579,26 @@ int orbx_bf_match(orbx_matcher* m, const uint8_t* q, int nq, const uint8_t* t, i
 static int stereo_common(orbx_matcher* m, StereoArgs& A, const float* scale, int nlevels, int rows, float bf, float b) {
     ORBX_REQUIRE(nlevels >= 1 && nlevels <= 32 && scale, ORBX_ERR_ARG, "bad level table");
     ORBX_REQUIRE(b != 0.0f, ORBX_ERR_ARG, "baseline is zero");
-    for (int l = 0; l < nlevels; ++l) A.scale[l] = scale[l];
+    ORBX_REQUIRE(rows > 0 && rows <= 16384, ORBX_ERR_ARG, "bad row count %d", rows);
+    float smax = 0.f;
+    for (int l = 0; l < nlevels; ++l) { A.scale[l] = scale[l]; smax = std::max(smax, scale[l]); }
     A.nlevels = nlevels;
     A.rows = rows;
+    A.band = (int)std::ceil(2.0f * smax) + 2;
     A.maxD = bf / b;   // minZ = mb, maxD = mbf/minZ (Frame.cc:496-498)
     (void)m;
     return ORBX_OK;
+}
+
+static int stereo_launch(StereoArgs& A, int batch, int nl_max, hipStream_t s) {
+    hipLaunchKernelGGL(k_stereo_rows, dim3(batch), dim3(1024), (size_t)(A.rows + 1) * sizeof(int), s, A);
+    hipLaunchKernelGGL(k_stereo, dim3((nl_max * 64 + 255) / 256, batch), dim3(256), 0, s, A);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+static size_t stereo_scratch(int batch, int rows, int capacity) {
+    return a256((size_t)batch * (rows + 1) * 4) + a256((size_t)batch * capacity * 4);
 }
 
 int orbx_stereo_match_batch_device(orbx_matcher* m, const orbx_keypoint* kl, const uint8_t* dl, const int32_t* nl,
@@ -557,13 +610,15 @@ int orbx_stereo_match_batch_device(orbx_matcher* m, const orbx_keypoint* kl, con
     StereoArgs A{};
     int st = stereo_common(m, A, scale, nlevels, rows, bf, b);
     if (st) return st;
-    A.kl = kl; A.dl = dl; A.nl = nl; A.kr = kr; A.dr = dr; A.nr = nr; A.capacity = capacity;
-    A.best_idx = bi; A.best_dist = bd;
     ORBX_HIP(hipSetDevice(m->device));
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
-    hipLaunchKernelGGL(k_stereo, dim3((capacity * 64 + 255) / 256, batch), dim3(256), 0, s, A);
-    ORBX_HIP(hipGetLastError());
-    return ORBX_OK;
+    if ((st = m->reserve_on(stereo_scratch(batch, rows, capacity), s))) return st;
+    Bump bp{(uint8_t*)m->scratch};
+    A.row_start = bp.take<int32_t>((size_t)batch * (rows + 1));
+    A.row_idx = bp.take<int32_t>((size_t)batch * capacity);
+    A.kl = kl; A.dl = dl; A.nl = nl; A.kr = kr; A.dr = dr; A.nr = nr; A.capacity = capacity;
+    A.best_idx = bi; A.best_dist = bd;
+    return stereo_launch(A, batch, capacity, s);
 }
 
 int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* desc_l, int nl, const orbx_keypoint* kpr,
@@ -573,21 +628,24 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
     *n_matched = 0;
     if (nl == 0) return ORBX_OK;
     ORBX_REQUIRE(kpl && desc_l && best_idx && best_dist && (nr == 0 || (kpr && desc_r)), ORBX_ERR_ARG, "null pointer");
-    ORBX_REQUIRE(nr < (1 << 20), ORBX_ERR_UNSUPPORTED, "too many right keypoints");
+    ORBX_REQUIRE(nr < (1 << 20) && nl < (1 << 20), ORBX_ERR_UNSUPPORTED, "too many keypoints");
     StereoArgs A{};
     int st = stereo_common(m, A, scale, nlevels, rows, bf, b);
     if (st) return st;
     ORBX_HIP(hipSetDevice(m->device));
-    const size_t bytes = a256(28 * (size_t)nl) + a256(32 * (size_t)nl) + a256(28 * (size_t)std::max(nr, 1)) +
-                         a256(32 * (size_t)std::max(nr, 1)) + 2 * a256(4 * (size_t)nl);
+    const int cap = std::max(nl, std::max(nr, 1));
+    const size_t bytes = a256(28 * (size_t)cap) * 2 + a256(32 * (size_t)cap) * 2 + 2 * a256(4 * (size_t)cap) +
+                         stereo_scratch(1, rows, cap);
     if ((st = m->reserve(bytes))) return st;
     Bump bp{(uint8_t*)m->scratch};
-    orbx_keypoint* dkl = bp.take<orbx_keypoint>(nl);
-    uint8_t* ddl = bp.take<uint8_t>(32 * (size_t)nl);
-    orbx_keypoint* dkr = bp.take<orbx_keypoint>(std::max(nr, 1));
-    uint8_t* ddr = bp.take<uint8_t>(32 * (size_t)std::max(nr, 1));
-    int32_t* dbi = bp.take<int32_t>(nl);
-    int32_t* dbd = bp.take<int32_t>(nl);
+    orbx_keypoint* dkl = bp.take<orbx_keypoint>(cap);
+    uint8_t* ddl = bp.take<uint8_t>(32 * (size_t)cap);
+    orbx_keypoint* dkr = bp.take<orbx_keypoint>(cap);
+    uint8_t* ddr = bp.take<uint8_t>(32 * (size_t)cap);
+    int32_t* dbi = bp.take<int32_t>(cap);
+    int32_t* dbd = bp.take<int32_t>(cap);
+    A.row_start = bp.take<int32_t>((size_t)rows + 1);
+    A.row_idx = bp.take<int32_t>(cap);
     hipStream_t s = m->stream;
     ORBX_HIP(hipMemcpyAsync(dkl, kpl, 28 * (size_t)nl, hipMemcpyHostToDevice, s));
     ORBX_HIP(hipMemcpyAsync(ddl, desc_l, 32 * (size_t)nl, hipMemcpyHostToDevice, s));
@@ -596,10 +654,9 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
         ORBX_HIP(hipMemcpyAsync(ddr, desc_r, 32 * (size_t)nr, hipMemcpyHostToDevice, s));
     }
     A.kl = dkl; A.dl = ddl; A.kr = dkr; A.dr = ddr; A.nl = nullptr; A.nr = nullptr;
-    A.nl_fixed = nl; A.nr_fixed = nr; A.capacity = std::max(nl, nr);
+    A.nl_fixed = nl; A.nr_fixed = nr; A.capacity = cap;
     A.best_idx = dbi; A.best_dist = dbd;
-    hipLaunchKernelGGL(k_stereo, dim3((nl * 64 + 255) / 256, 1), dim3(256), 0, s, A);
-    ORBX_HIP(hipGetLastError());
+    if ((st = stereo_launch(A, 1, nl, s))) return st;
     ORBX_HIP(hipMemcpyAsync(best_idx, dbi, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
     ORBX_HIP(hipMemcpyAsync(best_dist, dbd, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
     ORBX_HIP(hipStreamSynchronize(s));

@@ -71,7 +71,8 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_extractor_max_keypoints.argtypes = [vp, i32, i32]
     lib.orbx_extractor_level_sizes.argtypes = [vp, i32, i32, vp, vp]
     lib.orbx_extractor_copy_level.argtypes = [vp, i32, i32, vp, C.c_size_t]
-    lib.orbx_extractor_level_device.argtypes = [vp, i32, i32, C.POINTER(vp), C.POINTER(i32), C.POINTER(i32)]
+    lib.orbx_extractor_level_device.argtypes = [vp, i32, i32, C.POINTER(vp), C.POINTER(i32), C.POINTER(i32),
+                                                C.POINTER(C.c_size_t)]
     lib.orbx_extractor_enable_timing.argtypes = [vp, i32]
     lib.orbx_extractor_stage_times.argtypes = [vp, vp, C.POINTER(i32)]
     for name in ("orbx_extractor_get_scale_factors", "orbx_extractor_get_inverse_scale_factors",
