@@ -185,29 +185,31 @@ __device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, con
     return pmax(mn9[0], (s16x2)(0) - mx9[0]) - (s16x2)(1);
 }
 
-// NMS for a pixel pair from a 3x4 int16 window of the padded score map (pad ring -1): flags of the two
-// pixels at both thresholds (bit0/1: pixel 0/1 at iniTh, bit2/3: at minTh).  A pixel is kept iff it is
-// a strict local maximum of the masked scores (neighbour s if s >= t else 0) and s >= t (FAST_t NMS).
-__device__ __forceinline__ int nms_pair(const int16_t (&a)[3][4], int ti, int tm, bool second) {
-    int out = 0;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        const int s = a[1][1 + e];
-        int mi = 0, mm = 0;
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx) {
-                if (dy == 1 && dx == 1) continue;
-                const int n = a[dy][e + dx];
-                mi = max(mi, n >= ti ? n : 0);
-                mm = max(mm, n >= tm ? n : 0);
-            }
-        const bool valid = (e == 0) || second;
-        out |= ((valid && s >= ti && s > mi) ? 1 : 0) << e;
-        out |= ((valid && s >= tm && s > mm) ? 1 : 0) << (2 + e);
-    }
-    return out;
+// OpenCV's NMS keeps a corner (s >= t) iff s > every neighbour's buffer value (s_n if s_n >= t, else
+// 0).  For s >= max(t, 1) a neighbour with s_n < t never blocks (s_n < t <= s, and 0 < s), so the rule
+// is: s >= max(t, 1) and s > max of the 8 raw neighbour scores -- one maximum serves both thresholds.
+// For a pixel pair the 8 neighbour pairs come from 3 aligned dwords per row (v_alignbit for the odd
+// shifts) and 7 v_pk_max_i16.
+__device__ __forceinline__ uint32_t align16(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbit(hi, lo, 16); }
+
+__device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, int rr, int j, int T1, int T2,
+                                        bool second) {
+    const uint32_t* r0 = (const uint32_t*)(sc + rr * SW + 2 * j);
+    const uint32_t* r1 = r0 + (SW >> 1);
+    const uint32_t* r2 = r1 + (SW >> 1);
+    const uint32_t a0 = r0[0], a1 = r0[1], a2 = r0[2];
+    const uint32_t b0 = r1[0], b1 = r1[1], b2 = r1[2];
+    const uint32_t c0 = r2[0], c1 = r2[1], c2 = r2[2];
+    s16x2 m = pmax(as_s2(align16(a1, a0)), as_s2(a1));
+    m = pmax(m, as_s2(align16(a2, a1)));
+    m = pmax(m, as_s2(align16(b1, b0)));
+    m = pmax(m, as_s2(align16(b2, b1)));
+    m = pmax(m, as_s2(align16(c1, c0)));
+    m = pmax(m, as_s2(c1));
+    m = pmax(m, as_s2(align16(c2, c1)));
+    const s16x2 sv = as_s2(b1);
+    const int g0 = sv.x > m.x, g1 = second && (sv.y > m.y);
+    return (g0 & (sv.x >= T1)) | ((g1 & (sv.y >= T1)) << 1) | ((g0 & (sv.x >= T2)) << 2) | ((g1 & (sv.y >= T2)) << 3);
 }
 
 // One workgroup per (cell, image).  Cell geometry from ComputeKeyPointsOctTree (:784-807); FAST on the
@@ -267,8 +269,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     if (stop_after == 1) { if (tid == 0) cell_cnt[(size_t)img * ncells + c] = (int)(E[tid] & 0); return; }
     // 2. scores, two pixels per lane: pair q -> det row rr, pixels x = 3 + 2j, x + 1 (ROI coords)
     const int PR = (Wd + 1) >> 1, NP = Hd * PR;
-    for (int q = tid; q < NP; q += blockDim.x) {
-        const int rr = q / PR, j = q - rr * PR;
+    // pair q = tid + 256*it -> (row rr, pair column j), walked incrementally (no per-iteration division)
+    const int rr0 = tid / PR, j0 = tid - rr0 * PR;
+    const int dq = (int)blockDim.x / PR, dj = (int)blockDim.x - dq * PR;
+    auto next = [&](int& rr, int& j) { rr += dq; j += dj; if (j >= PR) { j -= PR; ++rr; } };
+    for (int q = tid, rr = rr0, j = j0; q < NP; q += blockDim.x, next(rr, j)) {
         const s16x2 s2 = fast_score2(E, O, rr + 3, j);
         *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
     }
@@ -276,20 +281,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     if (stop_after == 2) { if (tid == 0) cell_cnt[(size_t)img * ncells + c] = sc[tid * 5] & 0; return; }
     // 3. NMS at iniTh and minTh in one pass from 3 x 3 aligned dwords per pair; 4 flag bits per pair
     //    iteration kept in a register
-    const int ti = min(max(iniTh, 0), 255), tm = min(max(minTh, 0), 255);
+    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
     uint32_t flags = 0;
     int it = 0;
-    for (int q = tid; q < NP; q += blockDim.x, ++it) {
-        const int rr = q / PR, j = q - rr * PR;
-        int16_t a[3][4];
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-            const uint32_t* rowp = (const uint32_t*)(sc + (rr + dy) * SW + 2 * j);
-            const s16x2 d0 = as_s2(rowp[0]), d1 = as_s2(rowp[1]), d2 = as_s2(rowp[2]);
-            a[dy][0] = d0.y; a[dy][1] = d1.x; a[dy][2] = d1.y; a[dy][3] = d2.x;
-        }
-        flags |= (uint32_t)nms_pair(a, ti, tm, 2 * j + 1 < Wd) << (4 * it);
-    }
+    for (int q = tid, rr = rr0, j = j0; q < NP; q += blockDim.x, ++it, next(rr, j))
+        flags |= (uint32_t)nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd) << (4 * it);
     const int any_ini = __syncthreads_or((flags & 0x33333333u) != 0);
     const int sel = any_ini ? 0 : 2;          // cell empty at iniTh -> minTh (:812-816)
     if (stop_after == 3) { if (tid == 0) cell_cnt[(size_t)img * ncells + c] = (int)(flags & 0); return; }
@@ -298,7 +294,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
     int running = 0;
     it = 0;
-    for (int b = 0; b < NP; b += blockDim.x, ++it) {
+    int rr = rr0, j = j0;
+    for (int b = 0; b < NP; b += blockDim.x, ++it, next(rr, j)) {
         const int q = b + tid;
         const bool f0 = q < NP && ((flags >> (4 * it + sel)) & 1u);
         const bool f1 = q < NP && ((flags >> (4 * it + sel + 1)) & 1u);
@@ -308,7 +305,6 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
         int before = running, tot = 0;
         for (int k = 0; k < nw; ++k) { before += (k < w) ? red[k] : 0; tot += red[k]; }
         if (f0 || f1) {
-            const int rr = q / PR, j = q - rr * PR;
             const int16_t* cp = sc + (rr + 1) * SW + 2 + 2 * j;
             int pos = before + lanes_below(m0) + lanes_below(m1);
             const uint32_t yv = (uint32_t)(cd.y0 + rr + 3) << 16;
