@@ -169,6 +169,19 @@ int orbx_search_by_bow_kfkf(orbx_matcher* m, const uint8_t* desc1, const float* 
                             int n1, orbx_featvec fv1, const uint8_t* desc2, const float* angle2,
                             const uint8_t* valid2, int n2, orbx_featvec fv2, int32_t* match12, int* n_matches);
 
+/* Many SearchByBoW(KeyFrame*, KeyFrame*) pairs in one launch over a device keyframe store — MapFusion's
+ * cross-agent matches (src/MapFusion.cc:275 ComputeSim3, :849 CovisibilityDiscovery).  Store slot k:
+ * descriptors d_desc[k*capacity*32], keypoints d_kps[k*capacity] (angle = KeyPoint::angle), MapPoint-valid
+ * flags d_valid[k*capacity], FeatureVector CSR d_fv_nodes[k*capacity], d_fv_offsets[k*(capacity+1)],
+ * d_fv_indices[k*capacity], d_n_fv[k] (the layouts orbx_extract_batch_device and
+ * orbx_vocab_transform_batch_device write).  d_pairs: n_pairs (kf1, kf2) slot pairs; max_fv_nodes >= every
+ * kf1's node count.  Outputs: d_match12[p*capacity + i1] = KF2 index or -1, d_nmatches[p]. */
+int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const uint8_t* d_desc, const orbx_keypoint* d_kps,
+                                         const uint8_t* d_valid, const uint32_t* d_fv_nodes,
+                                         const int32_t* d_fv_offsets, const int32_t* d_fv_indices,
+                                         const int32_t* d_n_fv, int capacity, const int32_t* d_pairs, int n_pairs,
+                                         int max_fv_nodes, int32_t* d_match12, int32_t* d_nmatches, void* stream);
+
 /* ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (src/ORBmatcher.cc:161-290).
  * validk[i] != 0 when KF keypoint i has a non-bad MapPoint.  matchf[j] = KF index or -1. */
 int orbx_search_by_bow_kff(orbx_matcher* m, const uint8_t* desck, const float* anglek, const uint8_t* validk,
@@ -184,6 +197,41 @@ int orbx_search_for_triangulation(orbx_matcher* m, const uint8_t* desc1, const o
                                   const float* uright2, int n2, orbx_featvec fv2, const float* F12,
                                   const float* sigma2_2, const float* scale_2, int nlevels, float ex, float ey,
                                   int only_stereo, int32_t* match12, int* n_matches);
+
+/* ------------------------------------------------------------------------------------------------
+ * DBoW2 vocabulary — replaces TemplatedVocabulary<FORB>::transform (Thirdparty/DBoW2/DBoW2/
+ * TemplatedVocabulary.h:1125-1259), i.e. Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:395-402),
+ * which produce the FeatureVector that SearchByBoW buckets on.  Supported: L1/L2 scoring with any
+ * weighting (ORBvoc.txt is "10 6 0 0": k 10, L 6, L1_NORM, TF_IDF).
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct orbx_vocab orbx_vocab;
+
+/* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424). */
+int orbx_vocab_load_text(const char* path, int device, orbx_vocab** out);
+/* The same tree from arrays: n_lines node lines in file order (node id = line + 1, root = 0): parent id,
+ * is_leaf, 32-byte descriptor, weight. */
+int orbx_vocab_create(int k, int L, int scoring, int weighting, int n_lines, const int32_t* parent,
+                      const uint8_t* is_leaf, const uint8_t* desc, const double* weight, int device, orbx_vocab** out);
+int orbx_vocab_destroy(orbx_vocab* v);
+int orbx_vocab_info(const orbx_vocab* v, int* k, int* L, int* n_nodes, int* n_words);
+
+/* transform(features, BowVector&, FeatureVector&, levelsup) for n descriptors (host buffers, n <= 4096).
+ * BowVector: *n_words (word id ascending, value); FeatureVector: CSR with *n_fv_nodes node ids ascending,
+ * fv_offsets[n_fv_nodes + 1], fv_indices (feature indices ascending within a node).  Capacities: n. */
+int orbx_vocab_transform(orbx_vocab* v, const uint8_t* desc, int n, int levelsup, uint32_t* bow_words,
+                         double* bow_values, int* n_words, uint32_t* fv_nodes, int32_t* fv_offsets,
+                         int32_t* fv_indices, int* n_fv_nodes);
+/* Per-descriptor transform(feature, word_id, weight, &nid, levelsup) (:1218-1259), device buffers. */
+int orbx_vocab_words_device(orbx_vocab* v, const uint8_t* d_desc, int n, int levelsup, int32_t* d_word,
+                            double* d_weight, int32_t* d_node, void* stream);
+/* Batched device transform of 'batch' descriptor sets laid out like orbx_extract_batch_device output
+ * (descriptors at i*capacity, d_counts[i]).  Per set i: words/weights/nodes and BoW arrays at i*capacity,
+ * fv offsets at i*(capacity+1); d_n_words[i], d_n_fv_nodes[i].  capacity <= 4096. */
+int orbx_vocab_transform_batch_device(orbx_vocab* v, const uint8_t* d_desc, const int32_t* d_counts, int batch,
+                                      int capacity, int levelsup, int32_t* d_word, double* d_weight,
+                                      int32_t* d_node, uint32_t* d_bow_words, double* d_bow_values,
+                                      int32_t* d_n_words, uint32_t* d_fv_nodes, int32_t* d_fv_offsets,
+                                      int32_t* d_fv_indices, int32_t* d_n_fv_nodes, void* stream);
 
 #ifdef __cplusplus
 }

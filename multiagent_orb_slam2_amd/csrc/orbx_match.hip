@@ -233,9 +233,10 @@ __device__ __forceinline__ void wave_best2(int d, int pos, int& b1, int& bpos, i
 }
 
 struct BowArgs {
-    // view 1 (queries) and view 2 (candidates)
-    const uint8_t* d1; const float* a1; const uint8_t* v1; FvDev f1;
-    const uint8_t* d2; const float* a2; const uint8_t* v2; FvDev f2;
+    // view 1 (queries) and view 2 (candidates); angles read with a float stride (1 for a plain array,
+    // 7 for orbx_keypoint records, where angle is field 3)
+    const uint8_t* d1; const float* a1; int as1; const uint8_t* v1; FvDev f1;
+    const uint8_t* d2; const float* a2; int as2; const uint8_t* v2; FvDev f2;
     float nnratio;
     int checkOri;
     int kff;               // 0: KF-KF (TH_LOW strict, greedy on view-2 index, result indexed by view 1)
@@ -246,18 +247,18 @@ struct BowArgs {
     int32_t* nmatch;
 };
 
-// one wave per node of view 1
-__global__ __launch_bounds__(64) void k_bow(BowArgs A) {
-    __shared__ uint8_t taken[4096];
-    const int a = blockIdx.x, ln = lane_id();
-    if (a >= A.f1.n) return;
+// One FeatureVector node of view 1 against the same node of view 2 (merge-join of :547-634 by binary
+// search), queries in node order with lanes over the candidates; the greedy "already matched" flags are
+// node-local (a feature belongs to exactly one node) and live in LDS.
+__device__ void bow_node(const BowArgs& A, int a, uint8_t* taken) {
+    const int ln = lane_id();
     const uint32_t id = A.f1.node[a];
     const int b = fv_lower_bound(A.f2, id);
     if (b >= A.f2.n || A.f2.node[b] != id) return;
     const int q0 = A.f1.off[a], q1 = A.f1.off[a + 1];
     const int c0 = A.f2.off[b], c1 = A.f2.off[b + 1];
-    const int nc = c1 - c0;
-    for (int j = ln; j < min(nc, 4096); j += kWave) taken[j] = 0;
+    const int nc = min(c1 - c0, 4096);
+    for (int j = ln; j < nc; j += kWave) taken[j] = 0;
     __syncthreads();
     int local = 0;
     for (int p = q0; p < q1; ++p) {
@@ -292,7 +293,7 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs A) {
                 const int ridx = A.kff ? i2 : i1;
                 A.match[ridx] = A.kff ? i1 : i2;
                 if (A.checkOri) {
-                    const int bn = rot_bin(A.a1[i1], A.a2[i2]);
+                    const int bn = rot_bin(A.a1[(size_t)i1 * A.as1], A.a2[(size_t)i2 * A.as2]);
                     A.bin[ridx] = bn;
                     atomicAdd(&A.hist[bn], 1);
                 }
@@ -302,6 +303,48 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs A) {
         __syncthreads();
     }
     if (ln == 0 && local) atomicAdd(A.nmatch, local);
+}
+
+// one wave per node of view 1
+__global__ __launch_bounds__(64) void k_bow(BowArgs A) {
+    __shared__ uint8_t taken[4096];
+    if ((int)blockIdx.x >= A.f1.n) return;
+    bow_node(A, blockIdx.x, taken);
+}
+
+// Keyframe store on the device (extractor + vocabulary batch outputs, slot stride 'cap'): many
+// SearchByBoW(KF, KF) pairs in one launch -- MapFusion's cross-agent matches (src/MapFusion.cc:275, :849).
+struct KfStore {
+    const uint8_t* desc; const orbx_keypoint* kps; const uint8_t* valid;
+    const uint32_t* fv_nodes; const int32_t* fv_off; const int32_t* fv_idx; const int32_t* n_fv;
+    int cap;
+};
+
+__device__ __forceinline__ FvDev store_fv(const KfStore& S, int k) {
+    FvDev f;
+    f.node = S.fv_nodes + (size_t)k * S.cap;
+    f.off = S.fv_off + (size_t)k * (S.cap + 1);
+    f.idx = S.fv_idx + (size_t)k * S.cap;
+    f.n = S.n_fv[k];
+    return f;
+}
+
+__global__ __launch_bounds__(64) void k_bow_pairs(KfStore S, const int32_t* __restrict__ pairs, float nnratio, int checkOri,
+                                                  int32_t* match, int32_t* bin, int32_t* hist, int32_t* nmatch) {
+    __shared__ uint8_t taken[4096];
+    const int pr = blockIdx.y;
+    const int k1 = pairs[2 * pr], k2 = pairs[2 * pr + 1];
+    BowArgs A;
+    A.f1 = store_fv(S, k1);
+    if ((int)blockIdx.x >= A.f1.n) return;
+    A.f2 = store_fv(S, k2);
+    A.d1 = S.desc + (size_t)k1 * S.cap * 32; A.d2 = S.desc + (size_t)k2 * S.cap * 32;
+    A.a1 = &S.kps[(size_t)k1 * S.cap].angle; A.a2 = &S.kps[(size_t)k2 * S.cap].angle; A.as1 = A.as2 = 7;
+    A.v1 = S.valid + (size_t)k1 * S.cap; A.v2 = S.valid + (size_t)k2 * S.cap;
+    A.nnratio = nnratio; A.checkOri = checkOri; A.kff = 0;
+    A.match = match + (size_t)pr * S.cap; A.bin = bin + (size_t)pr * S.cap;
+    A.hist = hist + (size_t)pr * 32; A.nmatch = nmatch + pr;
+    bow_node(A, blockIdx.x, taken);
 }
 
 struct TriArgs {
@@ -382,9 +425,13 @@ __global__ __launch_bounds__(64) void k_triangulate(TriArgs A) {
 // rotation-consistency filter: keep matches whose bin is one of the three largest bins
 // (ComputeThreeMaxima, :1603-1644, with the 10 % rule); single workgroup.
 __global__ __launch_bounds__(256) void k_rot_filter(int32_t* match, const int32_t* bin, int n, const int32_t* hist,
-                                                    int32_t* nmatch) {
+                                                    int32_t* nmatch, int stride) {
     __shared__ int keep[3];
     __shared__ int removed;
+    match += (size_t)blockIdx.x * stride;
+    bin += (size_t)blockIdx.x * stride;
+    hist += (size_t)blockIdx.x * 32;
+    nmatch += blockIdx.x;
     if (threadIdx.x == 0) {
         int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
         for (int i = 0; i < kHisto; ++i) {
@@ -741,12 +788,12 @@ static int run_bow(orbx_matcher* m, int kff, const uint8_t* d1, const float* a1,
     ORBX_HIP(hipMemsetAsync(dm, 0xff, 4 * NR, s));
     ORBX_HIP(hipMemsetAsync(dh, 0, 4 * 32, s));
     BowArgs A{};
-    A.d1 = dd1; A.a1 = da1; A.v1 = dv1; A.f1 = f1;
-    A.d2 = dd2; A.a2 = da2; A.v2 = dv2; A.f2 = f2;
+    A.d1 = dd1; A.a1 = da1; A.as1 = 1; A.v1 = dv1; A.f1 = f1;
+    A.d2 = dd2; A.a2 = da2; A.as2 = 1; A.v2 = dv2; A.f2 = f2;
     A.nnratio = m->nnratio; A.checkOri = m->checkOri; A.kff = kff;
     A.match = dm; A.bin = db; A.hist = dh; A.nmatch = dh + 31;
     if (fv1.n_nodes > 0) hipLaunchKernelGGL(k_bow, dim3(fv1.n_nodes), dim3(64), 0, s, A);
-    if (m->checkOri) hipLaunchKernelGGL(k_rot_filter, dim3(1), dim3(256), 0, s, dm, db, nres, dh, dh + 31);
+    if (m->checkOri) hipLaunchKernelGGL(k_rot_filter, dim3(1), dim3(256), 0, s, dm, db, nres, dh, dh + 31, 0);
     ORBX_HIP(hipGetLastError());
     int nm = 0;
     if (nres) ORBX_HIP(hipMemcpyAsync(match, dm, 4 * (size_t)nres, hipMemcpyDeviceToHost, s));
@@ -774,6 +821,33 @@ int orbx_search_by_bow_kff(orbx_matcher* m, const uint8_t* desck, const float* a
                  ORBX_ERR_ARG, "bad argument");
     *n_matches = 0;
     return run_bow(m, 1, desck, anglek, validk, nk, fvk, descf, anglef, nullptr, nf, fvf, matchf, nf, n_matches);
+}
+
+int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const uint8_t* d_desc, const orbx_keypoint* d_kps,
+                                         const uint8_t* d_valid, const uint32_t* d_fv_nodes, const int32_t* d_fv_offsets,
+                                         const int32_t* d_fv_indices, const int32_t* d_n_fv, int capacity,
+                                         const int32_t* d_pairs, int n_pairs, int max_fv_nodes, int32_t* d_match12,
+                                         int32_t* d_nmatches, void* stream) {
+    ORBX_REQUIRE(m && d_desc && d_kps && d_valid && d_fv_nodes && d_fv_offsets && d_fv_indices && d_n_fv && d_pairs &&
+                     d_match12 && d_nmatches && capacity > 0 && n_pairs >= 0 && max_fv_nodes >= 0,
+                 ORBX_ERR_ARG, "bad argument");
+    if (n_pairs == 0 || max_fv_nodes == 0) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(m->device));
+    hipStream_t s = (hipStream_t)stream;
+    int st = m->reserve_on(a256((size_t)n_pairs * capacity * 4) + a256((size_t)n_pairs * 32 * 4), s);
+    if (st) return st;
+    int32_t* bin = (int32_t*)m->scratch;
+    int32_t* hist = (int32_t*)((uint8_t*)m->scratch + a256((size_t)n_pairs * capacity * 4));
+    ORBX_HIP(hipMemsetAsync(d_match12, 0xff, (size_t)n_pairs * capacity * 4, s));
+    ORBX_HIP(hipMemsetAsync(d_nmatches, 0, (size_t)n_pairs * 4, s));
+    ORBX_HIP(hipMemsetAsync(hist, 0, (size_t)n_pairs * 32 * 4, s));
+    KfStore S{d_desc, d_kps, d_valid, d_fv_nodes, d_fv_offsets, d_fv_indices, d_n_fv, capacity};
+    hipLaunchKernelGGL(k_bow_pairs, dim3(max_fv_nodes, n_pairs), dim3(64), 0, s, S, d_pairs, m->nnratio, m->checkOri, d_match12,
+                       bin, hist, d_nmatches);
+    if (m->checkOri)
+        hipLaunchKernelGGL(k_rot_filter, dim3(n_pairs), dim3(256), 0, s, d_match12, bin, capacity, hist, d_nmatches, capacity);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
 }
 
 int orbx_search_for_triangulation(orbx_matcher* m, const uint8_t* desc1, const orbx_keypoint* kp1, const uint8_t* has_mp1,
@@ -832,7 +906,7 @@ int orbx_search_for_triangulation(orbx_matcher* m, const uint8_t* desc1, const o
     A.ex = ex; A.ey = ey; A.onlyStereo = only_stereo; A.checkOri = m->checkOri;
     A.match = dm; A.bin = db; A.hist = dh; A.nmatch = dh + 31;
     if (fv1.n_nodes > 0) hipLaunchKernelGGL(k_triangulate, dim3(fv1.n_nodes), dim3(64), 0, s, A);
-    if (m->checkOri) hipLaunchKernelGGL(k_rot_filter, dim3(1), dim3(256), 0, s, dm, db, n1, dh, dh + 31);
+    if (m->checkOri) hipLaunchKernelGGL(k_rot_filter, dim3(1), dim3(256), 0, s, dm, db, n1, dh, dh + 31, 0);
     ORBX_HIP(hipGetLastError());
     int nm = 0;
     if (n1) ORBX_HIP(hipMemcpyAsync(match12, dm, 4 * (size_t)n1, hipMemcpyDeviceToHost, s));

@@ -90,6 +90,14 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_search_by_bow_kff.argtypes = [vp, vp, vp, vp, i32, FeatVec, vp, vp, i32, FeatVec, vp, C.POINTER(i32)]
     lib.orbx_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, i32, FeatVec, vp, vp, vp, vp, i32, FeatVec,
                                                   vp, vp, vp, i32, f32, f32, i32, vp, C.POINTER(i32)]
+    lib.orbx_search_by_bow_kfkf_pairs_device.argtypes = [vp] * 8 + [i32, vp, i32, i32, vp, vp, vp]
+    lib.orbx_vocab_load_text.argtypes = [C.c_char_p, i32, C.POINTER(vp)]
+    lib.orbx_vocab_create.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, C.POINTER(vp)]
+    lib.orbx_vocab_destroy.argtypes = [vp]
+    lib.orbx_vocab_info.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
+    lib.orbx_vocab_transform.argtypes = [vp, vp, i32, i32, vp, vp, C.POINTER(i32), vp, vp, vp, C.POINTER(i32)]
+    lib.orbx_vocab_words_device.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
+    lib.orbx_vocab_transform_batch_device.argtypes = [vp, vp, vp, i32, i32, i32] + [vp] * 11
     _lib = lib
     return lib
 
@@ -356,6 +364,21 @@ class ORBmatcher:
                                                  _p(a2), _p(v2), len(d2), _featvec(fv2), _p(m), C.byref(n)))
         return n.value, m
 
+    def SearchByBoW_pairs_device(self, desc, kps, valid, fv_nodes, fv_offsets, fv_indices, n_fv, pairs, max_fv_nodes,
+                                 stream=None):
+        """MapFusion's cross-agent SearchByBoW(KF, KF) for many (kf1, kf2) store-slot pairs in one launch.
+        All arguments are device tensors in the extractor/vocabulary batch layouts; pairs: (P, 2) int32.
+        Returns (match12 (P, capacity) int32, nmatches (P,) int32) device tensors."""
+        import torch
+        P, cap = pairs.shape[0], desc.shape[1]
+        m12 = torch.empty((P, cap), dtype=torch.int32, device=desc.device)
+        nm = torch.empty((P,), dtype=torch.int32, device=desc.device)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(desc.device).cuda_stream)
+        _check(self._lib.orbx_search_by_bow_kfkf_pairs_device(
+            self._h, _tp(desc), _tp(kps), _tp(valid), _tp(fv_nodes), _tp(fv_offsets), _tp(fv_indices), _tp(n_fv), cap,
+            _tp(pairs), P, int(max_fv_nodes), _tp(m12), _tp(nm), s))
+        return m12, nm
+
     def SearchByBoW_KF_F(self, desck, anglek, validk, fvk, descf, anglef, fvf):
         """ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) (src/ORBmatcher.cc:161-290).  Returns
         (nmatches, matchF) with matchF[iF] = KF index or -1."""
@@ -383,3 +406,85 @@ class ORBmatcher:
                                                        _p(s2), _p(sc2), len(s2), ex, ey, int(bOnlyStereo), _p(m),
                                                        C.byref(n)))
         return n.value, m
+
+
+@dataclass
+class BowResult:
+    bow_words: np.ndarray    # uint32, ascending word ids (DBoW2::BowVector keys)
+    bow_values: np.ndarray   # float64, normalised weights
+    featvec: tuple           # (node_ids, offsets, indices) CSR of DBoW2::FeatureVector
+
+
+class ORBVocabulary:
+    """DBoW2 TemplatedVocabulary<FORB> (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h) on a MI355X:
+    loadFromTextFile + transform(features, BowVector&, FeatureVector&, levelsup)."""
+
+    def __init__(self, handle, device):
+        self._lib = load_library()
+        self._h = handle
+        self.device = device
+
+    @classmethod
+    def load_text(cls, path: str, device: int = 0):
+        lib = load_library()
+        h = C.c_void_p()
+        _check(lib.orbx_vocab_load_text(path.encode(), device, C.byref(h)))
+        return cls(h, device)
+
+    @classmethod
+    def from_arrays(cls, voc: dict, device: int = 0):
+        lib = load_library()
+        P = np.ascontiguousarray(voc["parent"], np.int32)
+        lf = np.ascontiguousarray(voc["is_leaf"], np.uint8)
+        D = np.ascontiguousarray(voc["desc"], np.uint8)
+        W = np.ascontiguousarray(voc["weight"], np.float64)
+        h = C.c_void_p()
+        _check(lib.orbx_vocab_create(voc["k"], voc["L"], voc["scoring"], voc["weighting"], len(P), _p(P), _p(lf), _p(D),
+                                     _p(W), device, C.byref(h)))
+        return cls(h, device)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.orbx_vocab_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        k, L, nn, nw = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        _check(self._lib.orbx_vocab_info(self._h, C.byref(k), C.byref(L), C.byref(nn), C.byref(nw)))
+        return dict(k=k.value, L=L.value, n_nodes=nn.value, n_words=nw.value)
+
+    def transform(self, descriptors, levelsup: int = 4) -> BowResult:
+        """Frame::ComputeBoW (src/Frame.cc:395-402): BowVector and FeatureVector of a descriptor set."""
+        d = np.ascontiguousarray(descriptors, np.uint8).reshape(-1, 32)
+        n = len(d)
+        bw, bv = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.float64)
+        fn, fo, fi = np.zeros(max(n, 1), np.uint32), np.zeros(n + 1, np.int32), np.zeros(max(n, 1), np.int32)
+        nw, nf = C.c_int(), C.c_int()
+        _check(self._lib.orbx_vocab_transform(self._h, _p(d), n, levelsup, _p(bw), _p(bv), C.byref(nw), _p(fn), _p(fo),
+                                              _p(fi), C.byref(nf)))
+        no = int(fo[nf.value]) if nf.value else 0
+        return BowResult(bw[:nw.value].copy(), bv[:nw.value].copy(),
+                         (fn[:nf.value].copy(), fo[:nf.value + 1].copy(), fi[:no].copy()))
+
+    def transform_batch_device(self, desc, counts, levelsup: int = 4, stream=None):
+        """Batched transform of (B, capacity, 32) device descriptors; returns a dict of device tensors."""
+        import torch
+        B, cap = desc.shape[0], desc.shape[1]
+        dev = desc.device
+        t = lambda shape, dt: torch.empty(shape, dtype=dt, device=dev)
+        out = dict(word=t((B, cap), torch.int32), weight=t((B, cap), torch.float64), node=t((B, cap), torch.int32),
+                   bow_words=t((B, cap), torch.int32), bow_values=t((B, cap), torch.float64), n_words=t((B,), torch.int32),
+                   fv_nodes=t((B, cap), torch.int32), fv_offsets=t((B, cap + 1), torch.int32),
+                   fv_indices=t((B, cap), torch.int32), n_fv=t((B,), torch.int32))
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream)
+        _check(self._lib.orbx_vocab_transform_batch_device(
+            self._h, _tp(desc), _tp(counts), B, cap, levelsup, _tp(out["word"]), _tp(out["weight"]), _tp(out["node"]),
+            _tp(out["bow_words"]), _tp(out["bow_values"]), _tp(out["n_words"]), _tp(out["fv_nodes"]),
+            _tp(out["fv_offsets"]), _tp(out["fv_indices"]), _tp(out["n_fv"]), s))
+        return out

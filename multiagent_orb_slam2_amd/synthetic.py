@@ -94,3 +94,50 @@ def random_featvec(seed: int, n: int, n_nodes: int = 60, node_space: int = 100):
     keep = counts > 0
     offs = np.concatenate([[0], np.cumsum(counts[keep])]).astype(np.int32)
     return ids[keep], offs, order.astype(np.int32)
+
+
+def synthetic_vocabulary(seed: int, k: int = 10, L: int = 4, flip_p: float = 0.12, stop_frac: float = 0.02,
+                         scoring: int = 0, weighting: int = 0):
+    """A DBoW2-style k-ary vocabulary tree of depth L (ORBvoc.txt itself is absent).
+
+    Children descriptors are their parent's with Bernoulli(flip_p) bit flips, so descending the tree
+    is meaningful for ORB descriptors; leaves get idf-like weights log(N/n_i) with a few stopped (0)
+    words.  Returns the node lines in loadFromTextFile order (node id = line + 1, root = 0):
+    dict(k, L, scoring, weighting, parent, is_leaf, desc, weight)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    parent, leaf, desc, weight = [], [], [], []
+    frontier = [(0, rng.integers(0, 256, 32, dtype=np.uint8), 0)]   # (node id, descriptor, depth)
+    next_id = 1
+    while frontier:
+        nxt = []
+        for nid, d, depth in frontier:
+            bits = np.unpackbits(d)
+            for _ in range(k):
+                flips = rng.random(256) < flip_p
+                cd = np.packbits(bits ^ flips)
+                is_leaf = depth + 1 == L
+                parent.append(nid)
+                leaf.append(1 if is_leaf else 0)
+                desc.append(cd)
+                if is_leaf:
+                    w = 0.0 if rng.random() < stop_frac else float(np.log(1e6 / rng.integers(1, 5000)))
+                else:
+                    w = 0.0
+                weight.append(w)
+                if not is_leaf:
+                    nxt.append((next_id, cd, depth + 1))
+                next_id += 1
+        frontier = nxt
+    return dict(k=k, L=L, scoring=scoring, weighting=weighting, parent=np.array(parent, np.int32),
+                is_leaf=np.array(leaf, np.uint8), desc=np.stack(desc).astype(np.uint8),
+                weight=np.array(weight, np.float64))
+
+
+def write_vocabulary_text(voc, path: str):
+    """DBoW2 text format (TemplatedVocabulary::saveToTextFile): header 'k L scoring weighting', then
+    'parent isLeaf d0 .. d31 weight' per node (no trailing newline)."""
+    lines = [f"{voc['k']} {voc['L']} {voc['scoring']} {voc['weighting']}"]
+    for p, lf, d, w in zip(voc["parent"], voc["is_leaf"], voc["desc"], voc["weight"]):
+        lines.append(f"{int(p)} {int(lf)} " + " ".join(str(int(x)) for x in d) + " " + repr(float(w)))
+    with open(path, "w") as f:
+        f.write("\n".join(lines))

@@ -202,3 +202,21 @@ def distribute(xyr, minX, maxX, minY, maxY, N):
     if m < 0:
         raise RuntimeError("capacity")
     return out[:m].copy()
+
+
+def vocab_transform(voc, feats, levelsup):
+    """Oracle TemplatedVocabulary::transform; voc = dict(k, L, scoring, weighting, parent, is_leaf, desc, weight)."""
+    feats = np.ascontiguousarray(feats, np.uint8)
+    n = len(feats)
+    P = np.ascontiguousarray(voc["parent"], np.int32)
+    leaf = np.ascontiguousarray(voc["is_leaf"], np.uint8)
+    D = np.ascontiguousarray(voc["desc"], np.uint8)
+    W = np.ascontiguousarray(voc["weight"], np.float64)
+    bw, bv = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.float64)
+    fn, fo, fi = np.zeros(max(n, 1), np.uint32), np.zeros(n + 1, np.int32), np.zeros(max(n, 1), np.int32)
+    nw, nf = C.c_int(), C.c_int()
+    lib().orc_vocab_transform(voc["k"], voc["L"], voc["scoring"], voc["weighting"], len(P), _p(P), _p(leaf), _p(D),
+                              _p(W), _p(feats), n, levelsup, _p(bw), _p(bv), C.byref(nw), _p(fn), _p(fo), _p(fi),
+                              C.byref(nf))
+    return dict(bow_words=bw[:nw.value].copy(), bow_values=bv[:nw.value].copy(), fv_nodes=fn[:nf.value].copy(),
+                fv_offsets=fo[:nf.value + 1].copy(), fv_indices=fi[:fo[nf.value]].copy())

@@ -27,6 +27,7 @@
 #include <cstdint>
 #include <cstring>
 #include <list>
+#include <map>
 #include <vector>
 
 #include "../multiagent_orb_slam2_amd/csrc/orbx_pattern.h"
@@ -929,6 +930,74 @@ int orc_search_for_triangulation(const uint8_t* d1, const orc_kp* k1, const uint
     if (checkOri) nm = rot_filter(m, bins, nm);
     std::memcpy(match12, m.data(), sizeof(int) * n1);
     return nm;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// DBoW2 TemplatedVocabulary<FORB>::transform (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1125-1187,
+// :1218-1259): std::map BowVector / FeatureVector exactly as DBoW2 builds them.  Node numbering as in
+// loadFromTextFile (:1338-1424): line i = node i + 1, root 0.
+// ---------------------------------------------------------------------------------------------------
+int orc_vocab_transform(int /*k*/, int L, int scoring, int weighting, int n_lines, const int32_t* parent,
+                        const uint8_t* is_leaf, const uint8_t* vdesc, const double* vweight, const uint8_t* feats, int n,
+                        int levelsup, uint32_t* bow_words, double* bow_values, int* n_words, uint32_t* fv_nodes,
+                        int32_t* fv_off, int32_t* fv_idx, int* n_fv) {
+    const int N = n_lines + 1;
+    std::vector<std::vector<int>> children(N);
+    std::vector<int> word(N, -1);
+    std::vector<double> w(N, 0.0);
+    int nw = 0;
+    for (int i = 0; i < n_lines; ++i) {
+        children[parent[i]].push_back(i + 1);
+        w[i + 1] = vweight[i];
+        if (is_leaf[i]) word[i + 1] = nw++;
+    }
+    std::map<uint32_t, double> bow;
+    std::map<uint32_t, std::vector<unsigned>> fv;
+    const int nid_level = L - levelsup;
+    for (int f = 0; f < n; ++f) {
+        const uint8_t* x = feats + 32 * (size_t)f;
+        unsigned nid = 0, final_id = 0;
+        int level = 0;
+        do {
+            ++level;
+            const std::vector<int>& nodes = children[final_id];
+            final_id = nodes[0];
+            double best_d = hamming(x, vdesc + 32 * (size_t)(final_id - 1));
+            for (size_t c = 1; c < nodes.size(); ++c) {
+                const double d = hamming(x, vdesc + 32 * (size_t)(nodes[c] - 1));
+                if (d < best_d) { best_d = d; final_id = nodes[c]; }
+            }
+            if (level == nid_level) nid = final_id;
+        } while (!children[final_id].empty());
+        const double wt = w[final_id];
+        if (wt > 0) {
+            const uint32_t id = (uint32_t)word[final_id];
+            if (weighting == 0 || weighting == 1) {   // TF_IDF, TF: addWeight
+                auto it = bow.find(id);
+                if (it != bow.end()) it->second += wt; else bow.emplace(id, wt);
+            } else {                                  // IDF, BINARY: addIfNotExist
+                bow.emplace(id, wt);
+            }
+            fv[nid].push_back((unsigned)f);
+        }
+    }
+    double norm = 0.0;                                // BowVector::normalize (L1 or L2)
+    if (scoring == 0) { for (auto& kv : bow) norm += std::fabs(kv.second); }
+    else { for (auto& kv : bow) norm += kv.second * kv.second; norm = std::sqrt(norm); }
+    if (norm > 0.0) for (auto& kv : bow) kv.second /= norm;
+    int i = 0;
+    for (auto& kv : bow) { bow_words[i] = kv.first; bow_values[i] = kv.second; ++i; }
+    *n_words = i;
+    int j = 0, o = 0;
+    for (auto& kv : fv) {
+        fv_nodes[j] = kv.first;
+        fv_off[j] = o;
+        for (unsigned idx : kv.second) fv_idx[o++] = (int32_t)idx;
+        ++j;
+    }
+    fv_off[j] = o;
+    *n_fv = j;
+    return 0;
 }
 
 }  // extern "C"
