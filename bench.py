@@ -5,9 +5,14 @@ at KITTI size 1242x375, 8 levels, 2000 keypoints, on 1..N MI355X (one agent per 
 A "step" = one batch of --batch synthetic stereo frames per GPU through the hot path:
   ORBextractor on 2*batch images (src/ORBextractor.cc:1043-1105)  +  the descriptor search of
   Frame::ComputeStereoMatches on batch pairs (src/Frame.cc:466-552)
-and, when N > 1, the keyframe exchange: every rank's new keyframes (1 in 5 frames: keypoints +
-descriptors) are all-gathered over RCCL into every rank's MapFusion store (src/MapFusion.cc:83-88
-replaced by ncclAllGather).  Inputs are resident in HBM before the timed region; weak scaling.
+and the keyframe path: every 5th left frame becomes a keyframe (MapPoint-valid = stereo-matched, as
+Tracking::CreateNewKeyFrame makes stereo MapPoints), its DBoW2 FeatureVector is computed on the GPU
+(KeyFrame::ComputeBoW, synthetic k=10 L=6 vocabulary of ORBvoc's shape), the keyframe packets are
+all-gathered over RCCL into every rank's MapFusion store (src/MapFusion.cc:83-88 replaced by
+ncclAllGather; a local insert at N=1) and each new keyframe is matched with SearchByBoW against 16
+candidate keyframes (other agents' at N>1 -- MapFusion.cc:275; the agent's own earlier ones at N=1 --
+LoopClosing.cc:288), so every rank does the same work at every N.  Inputs are resident in HBM before
+the timed region; weak scaling.
 
 Prints ONE JSON line on rank 0 (driver contract).  Run: python bench.py [--gpus N --steps K --warmup W]
 """
@@ -29,6 +34,8 @@ ROWS, COLS, NFEAT, NLEV, SCALE, INI, MINTH = 375, 1242, 2000, 8, 1.2, 20, 7
 BF, BASELINE_B = 386.1448, 0.537165          # KITTI stereo (Examples/Stereo/KITTI00-02.yaml)
 HBM_PEAK_GBS = 8000.0                         # MI355X HBM3E peak (MI355X_MICROARCH.md)
 KF_EVERY = 5
+KF_CANDIDATES = 16
+STORE_STEPS = 3                               # keyframe store ring = 3 steps of every agent's keyframes
 
 
 def parse():
@@ -113,13 +120,22 @@ def main():
     kps = torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev)
     desc = torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev)
     cnt = torch.empty((2 * B,), dtype=torch.int32, device=dev)
-    stream = torch.cuda.Stream(dev)                    # one queue for extractor, matcher and RCCL
+    stream = torch.cuda.Stream(dev)                    # one queue for extractor, matchers and RCCL
     torch.cuda.set_stream(stream)
     n_kf = max(1, B // KF_EVERY)
-    kf_local = torch.empty((n_kf, cap, 60), dtype=torch.uint8, device=dev)
-    kf_all = torch.empty((world * n_kf, cap, 60), dtype=torch.uint8, device=dev) if world > 1 else None
+    kf_rows = torch.arange(0, KF_EVERY * n_kf, KF_EVERY, device=dev)
+    voc = S.synthetic_vocabulary(2024, k=10, L=6)      # ORBvoc.txt's shape ("10 6 0 0"); the file is absent
+    vocab = pkg.ORBVocabulary.from_arrays(voc, device=dev.index)
+    del voc
+    from multiagent_orb_slam2_amd import multiagent as MA
+    fusion = MA.KeyframeFusion(pkg.ORBmatcher(0.75, True, device=dev.index), vocab, cap,
+                               slots=STORE_STEPS * world * n_kf, device=dev, agent=rank,
+                               exchange=MA.KeyframeExchange() if world > 1 else None, candidates=KF_CANDIDATES)
+    frame_no = [0]
+    gate = torch.zeros((), dtype=torch.int64, device=dev)
 
     stereo_ms = []
+    kf_ms = []
 
     def step(time_stereo=False):
         ex.extract_batch_device(imgs, kps, desc, cnt, stream=stream)
@@ -131,12 +147,24 @@ def main():
         if time_stereo:
             e1.record(stream)
             stereo_ms.append((e0, e1))
-        if world > 1:
-            # keyframe packets (keypoints 28 B + descriptors 32 B per slot) -> all ranks (MapFusion ingress)
-            kf_local[:, :, :28].copy_(kps[0:B:KF_EVERY][:n_kf])
-            kf_local[:, :, 28:].copy_(desc[0:B:KF_EVERY][:n_kf])
-            dist.all_gather_into_tensor(kf_all, kf_local)
+        # keyframe path: BoW -> packets -> all-gather (N>1) into the store -> batched SearchByBoW
+        if time_stereo:
+            e2 = torch.cuda.Event(enable_timing=True)
+            e2.record(stream)
+        valid = (bi.index_select(0, kf_rows) >= 0).to(torch.uint8)
+        frames = [frame_no[0] + KF_EVERY * i for i in range(n_kf)]
+        frame_no[0] += B
+        _, _, nm, passed = fusion.step(kps.index_select(0, kf_rows), desc.index_select(0, kf_rows),
+                                       cnt.index_select(0, kf_rows), valid, frames, stream=stream)
+        gate.add_(passed.sum())
+        if time_stereo:
+            e3 = torch.cuda.Event(enable_timing=True)
+            e3.record(stream)
+            kf_ms.append((e2, e3))
         return bi, bd
+
+    for _ in range(STORE_STEPS):                       # fill the keyframe store ring (setup, untimed)
+        step()
 
     for _ in range(args.warmup):
         step()
@@ -165,7 +193,10 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": "C2+C3 stereo frame: ORBextractor x2 (1242x375, 8 levels, 2000 kpts) + stereo "
-                               "L<->R 256-bit Hamming band match" + (" + RCCL all-gather of KF packets" if world > 1 else ""),
+                               "L<->R 256-bit Hamming band match; every 5th frame a keyframe: DBoW2 transform (k=10, "
+                               "L=6) + " + ("RCCL all-gather of KF packets + " if world > 1 else "") +
+                               f"SearchByBoW vs {KF_CANDIDATES} candidate KFs",
+                   "keyframes_per_gpu_per_step": n_kf, "bow_pairs_per_gpu_per_step": n_kf * KF_CANDIDATES,
                    "global_batch": B * world, "frames_per_gpu_per_step": B, "image": [ROWS, COLS],
                    "nfeatures": NFEAT, "nlevels": NLEV, "parallelism": f"agent-per-gpu x{world}"},
     }
@@ -175,6 +206,8 @@ def main():
         per_call = {k: v / max(calls, 1) for k, v in st.items()}
         sms = [a.elapsed_time(b) for a, b in stereo_ms]
         per_call["stereo_match"] = float(np.mean(sms)) if sms else 0.0
+        kms = [a.elapsed_time(b) for a, b in kf_ms]
+        per_call["keyframe_bow_fusion"] = float(np.mean(kms)) if kms else 0.0
         counts = cnt.cpu().numpy()
         mean_kps = float(counts.mean())
         mean_cand = float(mean_kps * 4)   # replaced below by the measured candidate count if available
@@ -185,7 +218,7 @@ def main():
             pass
         alg = algorithmic_bytes(ex, mean_cand, mean_kps)
         alg["stereo_match"] = 2 * cap * 0 + 2 * mean_kps * 60 + mean_kps * 8
-        dom = max(per_call, key=per_call.get)
+        dom = max((k for k in per_call if k in alg), key=per_call.get)
         n_units = 2 * B if dom != "stereo_match" else B
         bytes_launch = alg[dom] * n_units
         achieved = bytes_launch / (per_call[dom] * 1e-3) / 1e9
@@ -208,6 +241,7 @@ def main():
         out["cpu_baseline"] = {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
                                "sample": f"{n} stereo frames (2 extractions + stereo match each) of the same synthetic "
                                          f"inputs, oracle/orb_oracle.cpp -O2, 1 thread, {secs:.1f} s"}
+    out["fusion_gate_passed_per_step"] = round(int(gate.item()) / (args.steps + args.warmup + STORE_STEPS), 2)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

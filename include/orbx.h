@@ -96,6 +96,24 @@ int orbx_extract_batch_device(orbx_extractor* ex, const uint8_t* d_images, int b
                               size_t step, size_t image_stride, orbx_keypoint* d_keypoints,
                               uint8_t* d_descriptors, int32_t* d_counts, int capacity, void* stream);
 
+/* The image pyramids of the last extraction call, as one device-side description (what
+ * ORBextractor::mvImagePyramid exposes, include/ORBextractor.h:85): level 0 of image i is the caller's
+ * image at level0 + i*level0_image_stride (row step level0_step); level l >= 1 of image i is at
+ * levels + i*image_stride + offset[l] with row step cols[l].  scale / inv_scale: mvScaleFactor /
+ * mvInvScaleFactor.  Valid until the next call on the extractor (and while the caller keeps level 0). */
+#define ORBX_MAX_LEVELS 32
+typedef struct orbx_pyramid {
+    int nlevels, batch;
+    const uint8_t* level0;
+    size_t level0_step, level0_image_stride;
+    const uint8_t* levels;
+    size_t image_stride;
+    size_t offset[ORBX_MAX_LEVELS];
+    int rows[ORBX_MAX_LEVELS], cols[ORBX_MAX_LEVELS];
+    float scale[ORBX_MAX_LEVELS], inv_scale[ORBX_MAX_LEVELS];
+} orbx_pyramid;
+int orbx_extractor_pyramid_device(const orbx_extractor* ex, orbx_pyramid* out);
+
 /* Device pointer and row step of pyramid level 'level' of image 'index' of the last call.  Level 0 is
  * the caller's input image itself (read in place, never copied): valid while the caller keeps it. */
 int orbx_extractor_level_device(orbx_extractor* ex, int index, int level, const uint8_t** d_level,
@@ -154,6 +172,27 @@ int orbx_stereo_match_batch_device(orbx_matcher* m, const orbx_keypoint* d_kpl, 
                                    int nlevels, int rows, float bf, float b, int32_t* d_best_idx,
                                    int32_t* d_best_dist, void* stream);
 
+/* The sub-pixel half of Frame::ComputeStereoMatches (src/Frame.cc:554-639) over 'batch' stereo pairs, after
+ * orbx_stereo_match_batch_device: for each left keypoint with an accepted right match, the 11x11 SAD
+ * window slid over +-5 px on the left keypoint's pyramid level (left image left_first+i of 'left', right
+ * image right_first+i of 'right' -- the same pyramid when one extractor made both), parabola fit,
+ * disparity check in [0, bf/b), then the median-SAD outlier rejection per pair (thDist = 1.5*1.4*median).
+ * Outputs mvuRight / mvDepth (-1 = no stereo) at i*capacity + iL for iL < capacity. */
+int orbx_stereo_refine_batch_device(orbx_matcher* m, const orbx_keypoint* d_kpl, const int32_t* d_nl,
+                                    const orbx_keypoint* d_kpr, const int32_t* d_best_idx, int batch, int capacity,
+                                    const orbx_pyramid* left, int left_first, const orbx_pyramid* right,
+                                    int right_first, float bf, float b, float* d_uright, float* d_depth,
+                                    void* stream);
+
+/* Frame::ComputeStereoMatches (src/Frame.cc:466-639) as one host call: the keypoints/descriptors the two
+ * extractors returned from their last host orbx_extract, whose pyramids (image 0) it reads, like the
+ * reference reads mpORBextractorLeft/Right->mvImagePyramid.  uright/depth: nl floats (-1 = none);
+ * *n_stereo = keypoints with depth. */
+int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, const orbx_extractor* right,
+                                const orbx_keypoint* kpl, const uint8_t* desc_l, int nl, const orbx_keypoint* kpr,
+                                const uint8_t* desc_r, int nr, float bf, float b, float* uright, float* depth,
+                                int* n_stereo);
+
 /* DBoW2::FeatureVector (Thirdparty/DBoW2/DBoW2/FeatureVector.h:21-22) as CSR: node ids ascending,
  * offsets[n_nodes+1], feature indices (ascending within a node). */
 typedef struct orbx_featvec {
@@ -169,18 +208,31 @@ int orbx_search_by_bow_kfkf(orbx_matcher* m, const uint8_t* desc1, const float* 
                             int n1, orbx_featvec fv1, const uint8_t* desc2, const float* angle2,
                             const uint8_t* valid2, int n2, orbx_featvec fv2, int32_t* match12, int* n_matches);
 
+/* A keyframe store on the device: slot k's field F lives at (const uint8_t*)F + k * F_stride (bytes), so the
+ * same struct describes the batch outputs of orbx_extract_batch_device / orbx_vocab_transform_batch_device
+ * (field-major: desc_stride = capacity*32, ...) and an array of exchanged keyframe packets (slot-major: every
+ * stride = packet bytes).  desc and kps must be 16- and 4-byte aligned per slot.
+ *   desc[capacity][32], kps[capacity] (KeyPoint::angle used), valid[capacity] (keypoint has a non-bad
+ *   MapPoint), FeatureVector CSR fv_nodes[n_fv] / fv_offsets[n_fv+1] / fv_indices, n_fv (int32). */
+typedef struct orbx_kf_store {
+    const uint8_t* desc;        size_t desc_stride;
+    const orbx_keypoint* kps;   size_t kps_stride;
+    const uint8_t* valid;       size_t valid_stride;
+    const uint32_t* fv_nodes;   size_t fv_nodes_stride;
+    const int32_t* fv_offsets;  size_t fv_offsets_stride;
+    const int32_t* fv_indices;  size_t fv_indices_stride;
+    const int32_t* n_fv;        size_t n_fv_stride;
+    int capacity;
+} orbx_kf_store;
+
 /* Many SearchByBoW(KeyFrame*, KeyFrame*) pairs in one launch over a device keyframe store — MapFusion's
- * cross-agent matches (src/MapFusion.cc:275 ComputeSim3, :849 CovisibilityDiscovery).  Store slot k:
- * descriptors d_desc[k*capacity*32], keypoints d_kps[k*capacity] (angle = KeyPoint::angle), MapPoint-valid
- * flags d_valid[k*capacity], FeatureVector CSR d_fv_nodes[k*capacity], d_fv_offsets[k*(capacity+1)],
- * d_fv_indices[k*capacity], d_n_fv[k] (the layouts orbx_extract_batch_device and
- * orbx_vocab_transform_batch_device write).  d_pairs: n_pairs (kf1, kf2) slot pairs; max_fv_nodes >= every
- * kf1's node count.  Outputs: d_match12[p*capacity + i1] = KF2 index or -1, d_nmatches[p]. */
-int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const uint8_t* d_desc, const orbx_keypoint* d_kps,
-                                         const uint8_t* d_valid, const uint32_t* d_fv_nodes,
-                                         const int32_t* d_fv_offsets, const int32_t* d_fv_indices,
-                                         const int32_t* d_n_fv, int capacity, const int32_t* d_pairs, int n_pairs,
-                                         int max_fv_nodes, int32_t* d_match12, int32_t* d_nmatches, void* stream);
+ * cross-agent matches (src/MapFusion.cc:275 ComputeSim3, :849 CovisibilityDiscovery) and LoopClosing's
+ * (src/LoopClosing.cc ComputeSim3).  d_pairs: n_pairs (kf1, kf2) slot pairs (int32); max_fv_nodes is the
+ * launch width per pair (workgroups stride over kf1's FeatureVector nodes, so any value >= 1 is correct; the
+ * largest node count is the fastest).  Outputs: d_match12[p*capacity + i1] = KF2 index or -1, d_nmatches[p]. */
+int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const orbx_kf_store* store, const int32_t* d_pairs,
+                                         int n_pairs, int max_fv_nodes, int32_t* d_match12, int32_t* d_nmatches,
+                                         void* stream);
 
 /* ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (src/ORBmatcher.cc:161-290).
  * validk[i] != 0 when KF keypoint i has a non-bad MapPoint.  matchf[j] = KF index or -1. */

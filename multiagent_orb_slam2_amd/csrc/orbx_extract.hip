@@ -1411,6 +1411,27 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     return ORBX_OK;
 }
 
+int orbx_extractor_pyramid_device(const orbx_extractor* e, orbx_pyramid* out) {
+    ORBX_REQUIRE(e && out, ORBX_ERR_ARG, "null argument");
+    ORBX_REQUIRE(e->d_pyr && e->last_src0.p && e->last_batch > 0, ORBX_ERR_ARG, "no pyramid: extract first");
+    std::memset(out, 0, sizeof(*out));
+    out->nlevels = e->nlevels;
+    out->batch = e->last_batch;
+    out->level0 = e->last_src0.p;
+    out->level0_step = e->last_src0.step;
+    out->level0_image_stride = e->last_src0.istride;
+    out->levels = e->d_pyr;
+    out->image_stride = e->pyr_size;
+    for (int l = 0; l < e->nlevels; ++l) {
+        out->offset[l] = (size_t)e->lv[l].pyr_off;
+        out->rows[l] = e->lv[l].h;
+        out->cols[l] = e->lv[l].w;
+        out->scale[l] = e->scale[l];
+        out->inv_scale[l] = e->invScale[l];
+    }
+    return ORBX_OK;
+}
+
 int orbx_extractor_level_device(orbx_extractor* e, int index, int level, const uint8_t** d_level, int* rows, int* cols,
                                 size_t* step) {
     ORBX_REQUIRE(e && d_level && rows && cols && step, ORBX_ERR_ARG, "null argument");

@@ -314,22 +314,21 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs A) {
 
 // Keyframe store on the device (extractor + vocabulary batch outputs, slot stride 'cap'): many
 // SearchByBoW(KF, KF) pairs in one launch -- MapFusion's cross-agent matches (src/MapFusion.cc:275, :849).
-struct KfStore {
-    const uint8_t* desc; const orbx_keypoint* kps; const uint8_t* valid;
-    const uint32_t* fv_nodes; const int32_t* fv_off; const int32_t* fv_idx; const int32_t* n_fv;
-    int cap;
-};
+template <typename T>
+__device__ __forceinline__ const T* slot_ptr(const T* base, size_t stride, int k) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const uint8_t*>(base) + (size_t)k * stride);
+}
 
-__device__ __forceinline__ FvDev store_fv(const KfStore& S, int k) {
+__device__ __forceinline__ FvDev store_fv(const orbx_kf_store& S, int k) {
     FvDev f;
-    f.node = S.fv_nodes + (size_t)k * S.cap;
-    f.off = S.fv_off + (size_t)k * (S.cap + 1);
-    f.idx = S.fv_idx + (size_t)k * S.cap;
-    f.n = S.n_fv[k];
+    f.node = slot_ptr(S.fv_nodes, S.fv_nodes_stride, k);
+    f.off = slot_ptr(S.fv_offsets, S.fv_offsets_stride, k);
+    f.idx = slot_ptr(S.fv_indices, S.fv_indices_stride, k);
+    f.n = *slot_ptr(S.n_fv, S.n_fv_stride, k);
     return f;
 }
 
-__global__ __launch_bounds__(64) void k_bow_pairs(KfStore S, const int32_t* __restrict__ pairs, float nnratio, int checkOri,
+__global__ __launch_bounds__(64) void k_bow_pairs(orbx_kf_store S, const int32_t* __restrict__ pairs, float nnratio, int checkOri,
                                                   int32_t* match, int32_t* bin, int32_t* hist, int32_t* nmatch) {
     __shared__ uint8_t taken[4096];
     const int pr = blockIdx.y;
@@ -338,13 +337,13 @@ __global__ __launch_bounds__(64) void k_bow_pairs(KfStore S, const int32_t* __re
     A.f1 = store_fv(S, k1);
     if ((int)blockIdx.x >= A.f1.n) return;
     A.f2 = store_fv(S, k2);
-    A.d1 = S.desc + (size_t)k1 * S.cap * 32; A.d2 = S.desc + (size_t)k2 * S.cap * 32;
-    A.a1 = &S.kps[(size_t)k1 * S.cap].angle; A.a2 = &S.kps[(size_t)k2 * S.cap].angle; A.as1 = A.as2 = 7;
-    A.v1 = S.valid + (size_t)k1 * S.cap; A.v2 = S.valid + (size_t)k2 * S.cap;
+    A.d1 = slot_ptr(S.desc, S.desc_stride, k1); A.d2 = slot_ptr(S.desc, S.desc_stride, k2);
+    A.a1 = &slot_ptr(S.kps, S.kps_stride, k1)->angle; A.a2 = &slot_ptr(S.kps, S.kps_stride, k2)->angle; A.as1 = A.as2 = 7;
+    A.v1 = slot_ptr(S.valid, S.valid_stride, k1); A.v2 = slot_ptr(S.valid, S.valid_stride, k2);
     A.nnratio = nnratio; A.checkOri = checkOri; A.kff = 0;
-    A.match = match + (size_t)pr * S.cap; A.bin = bin + (size_t)pr * S.cap;
+    A.match = match + (size_t)pr * S.capacity; A.bin = bin + (size_t)pr * S.capacity;
     A.hist = hist + (size_t)pr * 32; A.nmatch = nmatch + pr;
-    bow_node(A, blockIdx.x, taken);
+    for (int a = blockIdx.x; a < A.f1.n; a += gridDim.x) bow_node(A, a, taken);   // grid.x is only a width hint
 }
 
 struct TriArgs {
@@ -458,6 +457,154 @@ __global__ __launch_bounds__(256) void k_rot_filter(int32_t* match, const int32_
     if (lane_id() == 0 && r) atomicAdd(&removed, r);
     __syncthreads();
     if (threadIdx.x == 0) nmatch[0] -= removed;
+}
+
+// ---------------------------------------------------------------------------------------------
+// stereo sub-pixel refinement (src/Frame.cc:554-639)
+// ---------------------------------------------------------------------------------------------
+struct RefineArgs {
+    const orbx_keypoint* kl; const int32_t* nl; int nl_fixed;
+    const orbx_keypoint* kr; const int32_t* best_idx;
+    int capacity;
+    orbx_pyramid L, R;
+    int left_first, right_first;
+    float bf, maxD;
+    float* uright; float* depth; int32_t* sad;
+};
+
+constexpr int kRefKp = 23;   // keypoints per 256-thread workgroup: 23 x 11 window shifts = 253 lanes
+
+__device__ __forceinline__ const uint8_t* pyr_level(const orbx_pyramid& P, int img, int l, int& step) {
+    if (l == 0) {
+        step = (int)P.level0_step;
+        return P.level0 + (size_t)img * P.level0_image_stride;
+    }
+    step = P.cols[l];
+    return P.levels + (size_t)img * P.image_stride + P.offset[l];
+}
+
+// Lane (keypoint q, shift inc) computes one 11x11 SAD of the centre-subtracted windows: every value is a
+// small integer, so the reference's float Mats and cv::norm(NORM_L1) give exactly this integer.  The
+// shift-(-5) lane of each keypoint then runs the reference's sequential tail (first minimum, parabola,
+// disparity test) in float with the same operation order.
+__global__ __launch_bounds__(256) void k_stereo_sad(RefineArgs A) {
+    __shared__ int dist[kRefKp][11];
+    const int img = blockIdx.y, t = threadIdx.x;
+    const int q = t / 11, inc = t % 11 - 5;
+    const int l = blockIdx.x * kRefKp + q;
+    if (q >= kRefKp || l >= A.capacity) return;          // whole keypoints only: no barrier below is split
+    const int nl = A.nl ? A.nl[img] : A.nl_fixed;
+    const size_t o = (size_t)img * A.capacity + l;
+    const int bi = l < nl ? A.best_idx[o] : -1;
+    constexpr int w = 5, W = 2 * w + 1, Ls = 5;
+    int oct = 0, ivL = 0, iuL = 0, iuR0 = 0;
+    float suR0 = 0.f, uL = 0.f;
+    bool ok = bi >= 0;
+    if (ok) {
+        const orbx_keypoint kp = A.kl[o];
+        oct = kp.octave;
+        uL = kp.x;
+        const float sf = A.L.inv_scale[oct];
+        const float uR0 = A.kr[(size_t)img * A.capacity + bi].x;
+        const float suL = __builtin_roundf(__fmul_rn(kp.x, sf)), svL = __builtin_roundf(__fmul_rn(kp.y, sf));
+        suR0 = __builtin_roundf(__fmul_rn(uR0, sf));
+        iuL = (int)suL; ivL = (int)svL; iuR0 = (int)suR0;
+        ok = !(ivL - w < 0 || ivL + w >= A.L.rows[oct] || iuL - w < 0 || iuL + w >= A.L.cols[oct] ||
+               ivL + w >= A.R.rows[oct] || iuR0 - Ls - w < 0);
+        const float endu = suR0 + (float)(Ls + w + 1);
+        ok = ok && !(suR0 < 0.f || endu >= (float)A.R.cols[oct]);   // iniu = scaleduR0 + L - w
+    }
+    if (ok) {
+        int sl, sr;
+        const uint8_t* IL = pyr_level(A.L, A.left_first + img, oct, sl) + (size_t)(ivL - w) * sl + (iuL - w);
+        const uint8_t* IR = pyr_level(A.R, A.right_first + img, oct, sr) + (size_t)(ivL - w) * sr + (iuR0 + inc - w);
+        const int cL = IL[(size_t)w * sl + w], cR = IR[(size_t)w * sr + w];
+        int d = 0;
+#pragma unroll
+        for (int y = 0; y < W; ++y) {
+#pragma unroll
+            for (int x = 0; x < W; ++x) d += abs((IL[(size_t)y * sl + x] - cL) - (IR[(size_t)y * sr + x] - cR));
+        }
+        dist[q][inc + Ls] = d;
+    }
+    __syncthreads();
+    if (inc != -Ls) return;
+    float ur = -1.0f, dp = -1.0f;
+    int sd = -1;
+    if (ok) {
+        int best = 0x7fffffff, binc = 0;
+        for (int k = -Ls; k <= Ls; ++k) {
+            const int d = dist[q][k + Ls];
+            if ((float)d < (float)best) { best = d; binc = k; }
+        }
+        if (binc != -Ls && binc != Ls) {
+            const float d1 = (float)dist[q][Ls + binc - 1], d2 = (float)dist[q][Ls + binc], d3 = (float)dist[q][Ls + binc + 1];
+            const float den = __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2)));
+            const float deltaR = __fdiv_rn(__fsub_rn(d1, d3), den);
+            if (!(deltaR < -1.f || deltaR > 1.f)) {
+                float bestuR = __fmul_rn(A.L.scale[oct], __fadd_rn(__fadd_rn(suR0, (float)binc), deltaR));
+                float disparity = __fsub_rn(uL, bestuR);
+                if (disparity >= 0.f && disparity < A.maxD) {
+                    if (disparity <= 0.f) {
+                        disparity = 0.01f;
+                        bestuR = (float)((double)uL - 0.01);
+                    }
+                    dp = __fdiv_rn(A.bf, disparity);
+                    ur = bestuR;
+                    sd = best;
+                }
+            }
+        }
+    }
+    A.uright[o] = ur;
+    A.depth[o] = dp;
+    A.sad[o] = sd;
+}
+
+// Median-SAD outlier rejection of one stereo pair (src/Frame.cc:627-639): sort the accepted SAD values,
+// median = element n/2, reject every match with SAD >= 1.5*1.4*median (the reference's backward loop
+// stops at the first value below the threshold of an ascending list).
+__global__ __launch_bounds__(1024) void k_stereo_median(RefineArgs A) {
+    __shared__ uint32_t key[4096];
+    __shared__ int cnt;
+    const int img = blockIdx.x, tid = threadIdx.x;
+    const int nl = min(A.nl ? A.nl[img] : A.nl_fixed, A.capacity);
+    const size_t o = (size_t)img * A.capacity;
+    int P2 = 1;
+    while (P2 < nl) P2 <<= 1;
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    int c = 0;
+    for (int i = tid; i < P2; i += blockDim.x) {
+        const int v = i < nl ? A.sad[o + i] : -1;
+        key[i] = v >= 0 ? (uint32_t)v : 0xffffffffu;
+        c += v >= 0;
+    }
+    c = wave_sum(c);
+    if (lane_id() == 0 && c) atomicAdd(&cnt, c);
+    for (int k = 2; k <= P2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            __syncthreads();
+            for (int i = tid; i < P2; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t x = key[i], y = key[ixj];
+                    if ((x > y) == ((i & k) == 0)) { key[i] = y; key[ixj] = x; }
+                }
+            }
+        }
+    __syncthreads();
+    const int n = cnt;
+    if (n == 0) return;
+    const float median = (float)key[n / 2];
+    const float thDist = __fmul_rn(__fmul_rn(1.5f, 1.4f), median);
+    for (int i = tid; i < nl; i += blockDim.x) {
+        const int v = A.sad[o + i];
+        if (v >= 0 && !((float)v < thDist)) {
+            A.uright[o + i] = -1.0f;
+            A.depth[o + i] = -1.0f;
+        }
+    }
 }
 
 // =============================================================================================
@@ -713,6 +860,101 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
     return ORBX_OK;
 }
 
+static int refine_launch(RefineArgs& A, int batch, hipStream_t s) {
+    hipLaunchKernelGGL(k_stereo_sad, dim3((A.capacity + kRefKp - 1) / kRefKp, batch), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_stereo_median, dim3(batch), dim3(1024), 0, s, A);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+static int check_pyramid(const orbx_pyramid* P, int first, int batch, const char* which) {
+    ORBX_REQUIRE(P && P->level0 && P->nlevels >= 1 && P->nlevels <= ORBX_MAX_LEVELS, ORBX_ERR_ARG, "bad %s pyramid", which);
+    ORBX_REQUIRE(first >= 0 && first + batch <= P->batch, ORBX_ERR_ARG, "%s images [%d, %d) outside the pyramid batch %d",
+                 which, first, first + batch, P->batch);
+    ORBX_REQUIRE(P->nlevels == 1 || P->levels, ORBX_ERR_ARG, "bad %s pyramid", which);
+    return ORBX_OK;
+}
+
+int orbx_stereo_refine_batch_device(orbx_matcher* m, const orbx_keypoint* kl, const int32_t* nl, const orbx_keypoint* kr,
+                                    const int32_t* best_idx, int batch, int capacity, const orbx_pyramid* left, int left_first,
+                                    const orbx_pyramid* right, int right_first, float bf, float b, float* uright, float* depth,
+                                    void* stream) {
+    ORBX_REQUIRE(m && kl && nl && kr && best_idx && uright && depth && batch > 0 && capacity > 0, ORBX_ERR_ARG, "bad argument");
+    ORBX_REQUIRE(capacity <= 4096, ORBX_ERR_UNSUPPORTED, "capacity %d > 4096", capacity);
+    ORBX_REQUIRE(b != 0.0f, ORBX_ERR_ARG, "baseline is zero");
+    int st;
+    if ((st = check_pyramid(left, left_first, batch, "left"))) return st;
+    if ((st = check_pyramid(right, right_first, batch, "right"))) return st;
+    ORBX_REQUIRE(left->nlevels == right->nlevels, ORBX_ERR_ARG, "left/right pyramids differ in levels");
+    ORBX_HIP(hipSetDevice(m->device));
+    hipStream_t s = (hipStream_t)stream;
+    if ((st = m->reserve_on(a256((size_t)batch * capacity * 4), s))) return st;
+    RefineArgs A{};
+    A.kl = kl; A.nl = nl; A.kr = kr; A.best_idx = best_idx; A.capacity = capacity;
+    A.L = *left; A.R = *right; A.left_first = left_first; A.right_first = right_first;
+    A.bf = bf; A.maxD = bf / b;
+    A.uright = uright; A.depth = depth; A.sad = (int32_t*)m->scratch;
+    return refine_launch(A, batch, s);
+}
+
+int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, const orbx_extractor* right, const orbx_keypoint* kpl,
+                                const uint8_t* desc_l, int nl, const orbx_keypoint* kpr, const uint8_t* desc_r, int nr, float bf,
+                                float b, float* uright, float* depth, int* n_stereo) {
+    ORBX_REQUIRE(m && left && right && n_stereo && nl >= 0 && nr >= 0, ORBX_ERR_ARG, "bad argument");
+    *n_stereo = 0;
+    if (nl == 0) return ORBX_OK;
+    ORBX_REQUIRE(kpl && desc_l && uright && depth && (nr == 0 || (kpr && desc_r)), ORBX_ERR_ARG, "null pointer");
+    ORBX_REQUIRE(nl <= 4096 && nr < (1 << 20), ORBX_ERR_UNSUPPORTED, "too many keypoints");
+    orbx_pyramid PL, PR;
+    int st;
+    if ((st = orbx_extractor_pyramid_device(left, &PL))) return st;
+    if ((st = orbx_extractor_pyramid_device(right, &PR))) return st;
+    ORBX_REQUIRE(PL.nlevels == PR.nlevels, ORBX_ERR_ARG, "left/right extractors differ in levels");
+    StereoArgs A{};
+    if ((st = stereo_common(m, A, PL.scale, PL.nlevels, PL.rows[0], bf, b))) return st;
+    ORBX_HIP(hipSetDevice(m->device));
+    const int cap = std::max(nl, std::max(nr, 1));
+    const size_t bytes = a256(28 * (size_t)cap) * 2 + a256(32 * (size_t)cap) * 2 + 2 * a256(4 * (size_t)cap) +
+                         stereo_scratch(1, PL.rows[0], cap) + 3 * a256(4 * (size_t)cap);
+    if ((st = m->reserve(bytes))) return st;
+    Bump bp{(uint8_t*)m->scratch};
+    orbx_keypoint* dkl = bp.take<orbx_keypoint>(cap);
+    uint8_t* ddl = bp.take<uint8_t>(32 * (size_t)cap);
+    orbx_keypoint* dkr = bp.take<orbx_keypoint>(cap);
+    uint8_t* ddr = bp.take<uint8_t>(32 * (size_t)cap);
+    int32_t* dbi = bp.take<int32_t>(cap);
+    int32_t* dbd = bp.take<int32_t>(cap);
+    A.row_start = bp.take<int32_t>((size_t)PL.rows[0] + 1);
+    A.row_idx = bp.take<int32_t>(cap);
+    float* dur = bp.take<float>(cap);
+    float* ddp = bp.take<float>(cap);
+    int32_t* dsad = bp.take<int32_t>(cap);
+    hipStream_t s = m->stream;
+    ORBX_HIP(hipMemcpyAsync(dkl, kpl, 28 * (size_t)nl, hipMemcpyHostToDevice, s));
+    ORBX_HIP(hipMemcpyAsync(ddl, desc_l, 32 * (size_t)nl, hipMemcpyHostToDevice, s));
+    if (nr > 0) {
+        ORBX_HIP(hipMemcpyAsync(dkr, kpr, 28 * (size_t)nr, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(ddr, desc_r, 32 * (size_t)nr, hipMemcpyHostToDevice, s));
+    }
+    A.kl = dkl; A.dl = ddl; A.kr = dkr; A.dr = ddr; A.nl = nullptr; A.nr = nullptr;
+    A.nl_fixed = nl; A.nr_fixed = nr; A.capacity = cap;
+    A.best_idx = dbi; A.best_dist = dbd;
+    if ((st = stereo_launch(A, 1, nl, s))) return st;
+    RefineArgs R{};
+    R.kl = dkl; R.nl = nullptr; R.nl_fixed = nl; R.kr = dkr; R.best_idx = dbi; R.capacity = cap;
+    R.L = PL; R.R = PR; R.left_first = 0; R.right_first = 0;
+    R.bf = bf; R.maxD = bf / b;
+    R.uright = dur; R.depth = ddp; R.sad = dsad;
+    if ((st = refine_launch(R, 1, s))) return st;
+    ORBX_HIP(hipMemcpyAsync(uright, dur, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(depth, ddp, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+    int n = 0;
+    for (int i = 0; i < nl; ++i) n += depth[i] > 0;
+    *n_stereo = n;
+    return ORBX_OK;
+}
+
 // -------- host staging of a FeatureVector into the bump region
 static FvDev stage_fv(Bump& bp, const orbx_featvec& f, int nfeat, hipStream_t s, int* st) {
     FvDev d{};
@@ -823,29 +1065,34 @@ int orbx_search_by_bow_kff(orbx_matcher* m, const uint8_t* desck, const float* a
     return run_bow(m, 1, desck, anglek, validk, nk, fvk, descf, anglef, nullptr, nf, fvf, matchf, nf, n_matches);
 }
 
-int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const uint8_t* d_desc, const orbx_keypoint* d_kps,
-                                         const uint8_t* d_valid, const uint32_t* d_fv_nodes, const int32_t* d_fv_offsets,
-                                         const int32_t* d_fv_indices, const int32_t* d_n_fv, int capacity,
-                                         const int32_t* d_pairs, int n_pairs, int max_fv_nodes, int32_t* d_match12,
-                                         int32_t* d_nmatches, void* stream) {
-    ORBX_REQUIRE(m && d_desc && d_kps && d_valid && d_fv_nodes && d_fv_offsets && d_fv_indices && d_n_fv && d_pairs &&
-                     d_match12 && d_nmatches && capacity > 0 && n_pairs >= 0 && max_fv_nodes >= 0,
-                 ORBX_ERR_ARG, "bad argument");
-    if (n_pairs == 0 || max_fv_nodes == 0) return ORBX_OK;
+int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const orbx_kf_store* store, const int32_t* d_pairs, int n_pairs,
+                                         int max_fv_nodes, int32_t* d_match12, int32_t* d_nmatches, void* stream) {
+    ORBX_REQUIRE(m && store && d_pairs && d_match12 && d_nmatches && n_pairs >= 0 && max_fv_nodes >= 0, ORBX_ERR_ARG,
+                 "bad argument");
+    const orbx_kf_store& S = *store;
+    ORBX_REQUIRE(S.desc && S.kps && S.valid && S.fv_nodes && S.fv_offsets && S.fv_indices && S.n_fv && S.capacity > 0,
+                 ORBX_ERR_ARG, "incomplete keyframe store");
+    ORBX_REQUIRE(((uintptr_t)S.desc % 16) == 0 && S.desc_stride % 16 == 0 && ((uintptr_t)S.kps % 4) == 0 &&
+                     S.kps_stride % 4 == 0 && S.fv_nodes_stride % 4 == 0 && S.fv_offsets_stride % 4 == 0 &&
+                     S.fv_indices_stride % 4 == 0 && S.n_fv_stride % 4 == 0,
+                 ORBX_ERR_ARG, "misaligned keyframe store");
+    ORBX_REQUIRE(S.desc_stride >= 32 * (size_t)S.capacity && S.kps_stride >= sizeof(orbx_keypoint) * (size_t)S.capacity,
+                 ORBX_ERR_ARG, "keyframe store strides smaller than capacity");
+    if (n_pairs == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(m->device));
     hipStream_t s = (hipStream_t)stream;
-    int st = m->reserve_on(a256((size_t)n_pairs * capacity * 4) + a256((size_t)n_pairs * 32 * 4), s);
+    const size_t cap = (size_t)S.capacity;
+    ORBX_HIP(hipMemsetAsync(d_match12, 0xff, (size_t)n_pairs * cap * 4, s));
+    ORBX_HIP(hipMemsetAsync(d_nmatches, 0, (size_t)n_pairs * 4, s));
+    int st = m->reserve_on(a256((size_t)n_pairs * cap * 4) + a256((size_t)n_pairs * 32 * 4), s);
     if (st) return st;
     int32_t* bin = (int32_t*)m->scratch;
-    int32_t* hist = (int32_t*)((uint8_t*)m->scratch + a256((size_t)n_pairs * capacity * 4));
-    ORBX_HIP(hipMemsetAsync(d_match12, 0xff, (size_t)n_pairs * capacity * 4, s));
-    ORBX_HIP(hipMemsetAsync(d_nmatches, 0, (size_t)n_pairs * 4, s));
+    int32_t* hist = (int32_t*)((uint8_t*)m->scratch + a256((size_t)n_pairs * cap * 4));
     ORBX_HIP(hipMemsetAsync(hist, 0, (size_t)n_pairs * 32 * 4, s));
-    KfStore S{d_desc, d_kps, d_valid, d_fv_nodes, d_fv_offsets, d_fv_indices, d_n_fv, capacity};
-    hipLaunchKernelGGL(k_bow_pairs, dim3(max_fv_nodes, n_pairs), dim3(64), 0, s, S, d_pairs, m->nnratio, m->checkOri, d_match12,
+    hipLaunchKernelGGL(k_bow_pairs, dim3(std::max(1, std::min(max_fv_nodes, 4096)), n_pairs), dim3(64), 0, s, S, d_pairs, m->nnratio, m->checkOri, d_match12,
                        bin, hist, d_nmatches);
     if (m->checkOri)
-        hipLaunchKernelGGL(k_rot_filter, dim3(n_pairs), dim3(256), 0, s, d_match12, bin, capacity, hist, d_nmatches, capacity);
+        hipLaunchKernelGGL(k_rot_filter, dim3(n_pairs), dim3(256), 0, s, d_match12, bin, S.capacity, hist, d_nmatches, S.capacity);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }

@@ -20,7 +20,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-HEADER = 16        # int32 count, int32 agent, int32 frame, int32 reserved
+HEADER = 16        # int32 count, int32 agent, int32 frame, int32 n_fv (FeatureVector node count)
 KP_BYTES = 28
 DESC_BYTES = 32
 
@@ -39,28 +39,62 @@ def split_sequence(n_frames: int, n_agents: int) -> list[range]:
     return out
 
 
+def _a16(x: int) -> int:
+    return (x + 15) & ~15
+
+
+class PacketLayout:
+    """Byte layout of one keyframe packet (every field 16-byte aligned, so a packet array is directly an
+    orbx_kf_store with all strides = packet bytes):
+
+        header 16 | kps cap*28 | desc cap*32 | fv_nodes cap*4 | fv_offsets (cap+1)*4 | fv_indices cap*4 | valid cap
+
+    i.e. what KeyFrame carries into MapFusion for SearchByBoW: keypoints (angle), descriptors, the BoW
+    FeatureVector (KeyFrame::mFeatVec) and the MapPoint-valid flags (KeyFrame.h:171-185)."""
+
+    def __init__(self, capacity: int):
+        self.capacity = capacity
+        o = HEADER
+        self.offsets = {}
+        for name, size in (("kps", capacity * KP_BYTES), ("desc", capacity * DESC_BYTES), ("fv_nodes", capacity * 4),
+                           ("fv_offsets", (capacity + 1) * 4), ("fv_indices", capacity * 4), ("valid", capacity)):
+            self.offsets[name] = o
+            o = _a16(o + size)
+        self.bytes = o
+
+
 def packet_bytes(capacity: int) -> int:
-    return HEADER + capacity * (KP_BYTES + DESC_BYTES + 1)
+    return PacketLayout(capacity).bytes
 
 
-def pack_keyframes(kps, desc, counts, valid, agent: int, frames, capacity: int):
+def pack_keyframes(kps, desc, counts, valid, agent: int, frames, capacity: int, fv=None):
     """Pack n keyframes into a (n, packet_bytes) uint8 tensor on the same device.
 
     kps: (n, capacity, 28) uint8, desc: (n, capacity, 32) uint8, counts: (n,) int32,
-    valid: (n, capacity) uint8 (keypoint has a MapPoint), frames: (n,) frame ids."""
+    valid: (n, capacity) uint8 (keypoint has a MapPoint), frames: (n,) frame ids,
+    fv: optional dict of the vocabulary batch outputs (fv_nodes (n, cap), fv_offsets (n, cap+1),
+    fv_indices (n, cap), n_fv (n,)), as ORBVocabulary.transform_batch_device returns them."""
     import torch
     n = kps.shape[0]
     dev = kps.device
-    out = torch.zeros((n, packet_bytes(capacity)), dtype=torch.uint8, device=dev)
+    lay = PacketLayout(capacity)
+    out = torch.zeros((n, lay.bytes), dtype=torch.uint8, device=dev)
+    n_fv = fv["n_fv"].to(torch.int32) if fv is not None else torch.zeros_like(counts, dtype=torch.int32)
     hdr = torch.stack([counts.to(torch.int32), torch.full_like(counts, agent, dtype=torch.int32),
-                       torch.as_tensor(frames, dtype=torch.int32, device=dev), torch.zeros_like(counts, dtype=torch.int32)], 1)
+                       torch.as_tensor(frames, dtype=torch.int32, device=dev), n_fv], 1)
     out[:, :HEADER] = hdr.contiguous().view(torch.uint8).view(n, HEADER)
-    o = HEADER
-    out[:, o:o + capacity * KP_BYTES] = kps.reshape(n, -1)
-    o += capacity * KP_BYTES
-    out[:, o:o + capacity * DESC_BYTES] = desc.reshape(n, -1)
-    o += capacity * DESC_BYTES
-    out[:, o:o + capacity] = valid.reshape(n, -1)
+
+    def put(name, t, nbytes):
+        o = lay.offsets[name]
+        out[:, o:o + nbytes] = t.contiguous().view(torch.uint8).reshape(n, -1)
+
+    put("kps", kps, capacity * KP_BYTES)
+    put("desc", desc, capacity * DESC_BYTES)
+    put("valid", valid, capacity)
+    if fv is not None:
+        put("fv_nodes", fv["fv_nodes"], capacity * 4)
+        put("fv_offsets", fv["fv_offsets"], (capacity + 1) * 4)
+        put("fv_indices", fv["fv_indices"], capacity * 4)
     return out
 
 
@@ -72,21 +106,27 @@ class KeyframeView:
     kps: np.ndarray      # structured KP_DTYPE (count,)
     desc: np.ndarray     # (count, 32) uint8
     valid: np.ndarray    # (count,) uint8
+    featvec: tuple = None  # (node ids uint32, offsets int32, indices int32) or None
 
 
 def unpack_keyframes(packets, capacity: int) -> list[KeyframeView]:
     from .orbx import KP_DTYPE
     p = packets.cpu().numpy() if hasattr(packets, "cpu") else np.asarray(packets)
+    lay = PacketLayout(capacity)
+    o = lay.offsets
     out = []
     for row in p:
-        cnt, agent, frame, _ = row[:HEADER].view(np.int32)
-        o = HEADER
-        kp = row[o:o + capacity * KP_BYTES].view(KP_DTYPE)[:cnt].copy()
-        o += capacity * KP_BYTES
-        d = row[o:o + capacity * DESC_BYTES].reshape(capacity, DESC_BYTES)[:cnt].copy()
-        o += capacity * DESC_BYTES
-        v = row[o:o + capacity][:cnt].copy()
-        out.append(KeyframeView(int(cnt), int(agent), int(frame), kp, d, v))
+        cnt, agent, frame, n_fv = row[:HEADER].view(np.int32)
+        kp = row[o["kps"]:o["kps"] + capacity * KP_BYTES].view(KP_DTYPE)[:cnt].copy()
+        d = row[o["desc"]:o["desc"] + capacity * DESC_BYTES].reshape(capacity, DESC_BYTES)[:cnt].copy()
+        v = row[o["valid"]:o["valid"] + capacity][:cnt].copy()
+        fv = None
+        if n_fv > 0:
+            nodes = row[o["fv_nodes"]:o["fv_nodes"] + 4 * capacity].view(np.uint32)[:n_fv].copy()
+            offs = row[o["fv_offsets"]:o["fv_offsets"] + 4 * (capacity + 1)].view(np.int32)[:n_fv + 1].copy()
+            idx = row[o["fv_indices"]:o["fv_indices"] + 4 * capacity].view(np.int32)[:offs[-1]].copy()
+            fv = (nodes, offs, idx)
+        out.append(KeyframeView(int(cnt), int(agent), int(frame), kp, d, v, fv))
     return out
 
 
@@ -104,11 +144,13 @@ class KeyframeExchange:
         self.bytes_moved = 0
         self.calls = 0
 
-    def exchange(self, packets):
-        """packets: (n, P) uint8 on this rank (same n and P on every rank) -> (world*n, P), rank-major."""
+    def exchange(self, packets, out=None):
+        """packets: (n, P) uint8 on this rank (same n and P on every rank) -> (world*n, P), rank-major
+        (written into `out` when given, e.g. a slice of a DeviceKeyframeStore ring)."""
         import torch
         n, P = packets.shape
-        out = torch.empty((self.world * n, P), dtype=torch.uint8, device=packets.device)
+        if out is None:
+            out = torch.empty((self.world * n, P), dtype=torch.uint8, device=packets.device)
         if hasattr(self.dist, "all_gather_into_tensor") and packets.is_cuda:
             self.dist.all_gather_into_tensor(out, packets.contiguous(), group=self.group)
         else:
@@ -144,3 +186,129 @@ def cross_agent_match(matcher, query: KeyframeView, query_fv, candidates: list[K
                                            c.desc, c.kps["angle"], c.valid, featvec_of(c))
         out.append((ci, n, m12, n >= min_matches))
     return out
+
+
+class DeviceKeyframeStore:
+    """MapFusion's keyframe store on the GPU: a ring of `slots` keyframe packets (PacketLayout) that the
+    exchange all-gathers into directly, seen by the matcher as one orbx_kf_store (all strides = packet
+    bytes).  Host-side bookkeeping records which agent owns each slot and the insertion order."""
+
+    def __init__(self, capacity: int, slots: int, device):
+        import torch
+        self.layout = PacketLayout(capacity)
+        self.capacity = capacity
+        self.slots = slots
+        self.buf = torch.zeros((slots, self.layout.bytes), dtype=torch.uint8, device=device)
+        self.agent_of = [-1] * slots
+        self.stamp = [-1] * slots        # insertion sequence number per slot
+        self.pos = 0
+        self.seq = 0
+        self._store = None
+
+    def _reserve(self, n: int) -> int:
+        if n > self.slots:
+            raise ValueError(f"{n} keyframes do not fit a store of {self.slots} slots")
+        if self.pos + n > self.slots:
+            self.pos = 0
+        base = self.pos
+        self.pos += n
+        return base
+
+    def _record(self, base: int, agents):
+        for i, a in enumerate(agents):
+            self.agent_of[base + i] = int(a)
+            self.stamp[base + i] = self.seq
+            self.seq += 1
+
+    def insert(self, packets, agent: int) -> range:
+        """Local insert (single agent): copy packets into the ring; returns their slots."""
+        n = packets.shape[0]
+        base = self._reserve(n)
+        self.buf[base:base + n].copy_(packets)
+        self._record(base, [agent] * n)
+        return range(base, base + n)
+
+    def exchange_into(self, exchange: "KeyframeExchange", packets) -> range:
+        """All-gather every rank's packets straight into the ring (rank-major); returns the new slots."""
+        n = packets.shape[0]
+        w = exchange.world
+        base = self._reserve(w * n)
+        exchange.exchange(packets, out=self.buf[base:base + w * n])
+        self._record(base, [r for r in range(w) for _ in range(n)])
+        return range(base, base + w * n)
+
+    def kf_store(self):
+        """orbx_kf_store over the ring (pointers are fixed for the store's lifetime)."""
+        if self._store is None:
+            from .orbx import KfStore
+            P, o, b = self.layout.bytes, self.layout.offsets, self.buf
+            f = lambda name: (b[0, o[name]:], P)
+            self._store = KfStore.from_fields(self.capacity, desc=f("desc"), kps=f("kps"), valid=f("valid"),
+                                              fv_nodes=f("fv_nodes"), fv_offsets=f("fv_offsets"),
+                                              fv_indices=f("fv_indices"), n_fv=(b[0, 12:], P))
+        return self._store
+
+    def candidate_pairs(self, query_slots, agent: int, k: int, other_agents_only: bool = True) -> np.ndarray:
+        """(query, candidate) slot pairs: for every query, the k most recently inserted keyframes of the
+        other agents (MapFusion drops same-map candidates, src/MapFusion.cc:136-144) -- or, with
+        other_agents_only=False (single agent: LoopClosing's own-map candidates), the k keyframes inserted
+        most recently before it.  Stands in for KeyFrameDatabase::DetectMapFusionCandidates's BoW scoring
+        (src/KeyFrameDatabase.cc:199-308)."""
+        filled = [s for s in range(self.slots) if self.stamp[s] >= 0]
+        by_recency = sorted(filled, key=lambda s: -self.stamp[s])
+        pairs = []
+        for q in query_slots:
+            if other_agents_only:
+                c = [s for s in by_recency if self.agent_of[s] != agent]
+            else:
+                c = [s for s in by_recency if self.stamp[s] < self.stamp[q]]
+            pairs.extend((q, s) for s in c[:k])
+        return np.array(pairs, np.int32).reshape(-1, 2)
+
+
+class KeyframeFusion:
+    """The per-agent keyframe path after the front-end, all on the device:
+
+        new keyframes (extractor batch rows) -> ORBVocabulary::transform (BoW FeatureVector, level L-4,
+        src/KeyFrame.cc ComputeBoW) -> packets -> all-gather into every rank's DeviceKeyframeStore
+        (MapFusion ingress, src/MapFusion.cc:83-88) -> SearchByBoW(new KF, candidate KF) for this rank's
+        new keyframes only (sharded by query keyframe) -> MapFusion's 20-match gate (src/MapFusion.cc:275-281).
+
+    With one agent (no exchange) the candidates are the agent's own earlier keyframes, as LoopClosing's
+    ComputeSim3 matches them (src/LoopClosing.cc), so every rank does the same work at every N."""
+
+    def __init__(self, matcher, vocab, capacity: int, slots: int, device, agent: int = 0, exchange=None,
+                 candidates: int = 16, levelsup: int = 4, min_matches: int = 20):
+        self.matcher, self.vocab, self.capacity = matcher, vocab, capacity
+        self.store = DeviceKeyframeStore(capacity, slots, device)
+        self.agent, self.exchange = agent, exchange
+        self.k, self.levelsup, self.min_matches = candidates, levelsup, min_matches
+        info = vocab.info()
+        self.max_fv_nodes = min(capacity, info["k"] ** max(info["L"] - levelsup, 0) + 1)   # launch width hint
+        self._pairs = {}
+
+    def _device_pairs(self, pairs: np.ndarray, device):
+        import torch
+        key = pairs.tobytes()
+        t = self._pairs.get(key)
+        if t is None:
+            t = torch.from_numpy(pairs).to(device)
+            self._pairs[key] = t
+        return t
+
+    def step(self, kps, desc, counts, valid, frames, stream=None):
+        """kps (n, cap, 28) u8, desc (n, cap, 32) u8, counts (n,), valid (n, cap) u8: this agent's new
+        keyframes.  Returns (pairs (P, 2) device, match12 (P, cap), nmatches (P,), passed (P,) bool)."""
+        n = kps.shape[0]
+        fv = self.vocab.transform_batch_device(desc.contiguous(), counts.contiguous(), self.levelsup, stream=stream)
+        pk = pack_keyframes(kps, desc, counts, valid, self.agent, frames, self.capacity, fv)
+        multi = self.exchange is not None and self.exchange.world > 1
+        if multi:
+            slots = self.store.exchange_into(self.exchange, pk)
+            mine = slots[self.agent * n:(self.agent + 1) * n]
+        else:
+            mine = self.store.insert(pk, self.agent)
+        pairs = self.store.candidate_pairs(mine, self.agent, self.k, other_agents_only=multi)
+        pr = self._device_pairs(pairs, kps.device)
+        m12, nm = self.matcher.SearchByBoW_pairs_device(self.store.kf_store(), pr, self.max_fv_nodes, stream=stream)
+        return pr, m12, nm, nm >= self.min_matches

@@ -36,6 +36,39 @@ class FeatVec(C.Structure):
     _fields_ = [("node_ids", C.c_void_p), ("offsets", C.c_void_p), ("n_nodes", C.c_int), ("indices", C.c_void_p)]
 
 
+class KfStore(C.Structure):
+    """orbx_kf_store: per-field device pointer + slot stride in bytes (include/orbx.h)."""
+    _fields_ = [("desc", C.c_void_p), ("desc_stride", C.c_size_t), ("kps", C.c_void_p), ("kps_stride", C.c_size_t),
+                ("valid", C.c_void_p), ("valid_stride", C.c_size_t), ("fv_nodes", C.c_void_p),
+                ("fv_nodes_stride", C.c_size_t), ("fv_offsets", C.c_void_p), ("fv_offsets_stride", C.c_size_t),
+                ("fv_indices", C.c_void_p), ("fv_indices_stride", C.c_size_t), ("n_fv", C.c_void_p),
+                ("n_fv_stride", C.c_size_t), ("capacity", C.c_int)]
+
+    FIELDS = ("desc", "kps", "valid", "fv_nodes", "fv_offsets", "fv_indices", "n_fv")
+
+    @classmethod
+    def from_fields(cls, capacity: int, **fields):
+        """fields: name -> (device tensor whose data_ptr is slot 0 of that field, slot stride in bytes).
+        The tensors are kept alive by the returned struct."""
+        s = cls()
+        s._keep = []
+        for name in cls.FIELDS:
+            t, stride = fields[name]
+            setattr(s, name, t.data_ptr())
+            setattr(s, name + "_stride", int(stride))
+            s._keep.append(t)
+        s.capacity = int(capacity)
+        return s
+
+
+class Pyramid(C.Structure):
+    """orbx_pyramid (include/orbx.h): device description of an extractor's last image pyramids."""
+    _fields_ = [("nlevels", C.c_int), ("batch", C.c_int), ("level0", C.c_void_p), ("level0_step", C.c_size_t),
+                ("level0_image_stride", C.c_size_t), ("levels", C.c_void_p), ("image_stride", C.c_size_t),
+                ("offset", C.c_size_t * 32), ("rows", C.c_int * 32), ("cols", C.c_int * 32),
+                ("scale", C.c_float * 32), ("inv_scale", C.c_float * 32)]
+
+
 _lib = None
 
 
@@ -85,12 +118,16 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_stereo_match.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, i32, i32, f32, f32, vp, vp, C.POINTER(i32)]
     lib.orbx_stereo_match_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, f32, f32, vp,
                                                    vp, vp]
+    lib.orbx_extractor_pyramid_device.argtypes = [vp, C.POINTER(Pyramid)]
+    lib.orbx_stereo_refine_batch_device.argtypes = [vp, vp, vp, vp, vp, i32, i32, C.POINTER(Pyramid), i32,
+                                                    C.POINTER(Pyramid), i32, f32, f32, vp, vp, vp]
+    lib.orbx_compute_stereo_matches.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, i32, f32, f32, vp, vp, C.POINTER(i32)]
     lib.orbx_search_by_bow_kfkf.argtypes = [vp, vp, vp, vp, i32, FeatVec, vp, vp, vp, i32, FeatVec, vp,
                                             C.POINTER(i32)]
     lib.orbx_search_by_bow_kff.argtypes = [vp, vp, vp, vp, i32, FeatVec, vp, vp, i32, FeatVec, vp, C.POINTER(i32)]
     lib.orbx_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, i32, FeatVec, vp, vp, vp, vp, i32, FeatVec,
                                                   vp, vp, vp, i32, f32, f32, i32, vp, C.POINTER(i32)]
-    lib.orbx_search_by_bow_kfkf_pairs_device.argtypes = [vp] * 8 + [i32, vp, i32, i32, vp, vp, vp]
+    lib.orbx_search_by_bow_kfkf_pairs_device.argtypes = [vp, C.POINTER(KfStore), vp, i32, i32, vp, vp, vp]
     lib.orbx_vocab_load_text.argtypes = [C.c_char_p, i32, C.POINTER(vp)]
     lib.orbx_vocab_create.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, C.POINTER(vp)]
     lib.orbx_vocab_destroy.argtypes = [vp]
@@ -221,6 +258,12 @@ class ORBextractor:
         return kps[: n.value].copy(), desc[: n.value].copy()
 
     @property
+    def pyramid_device(self) -> "Pyramid":
+        """orbx_pyramid of the last call (device pointers; valid until the next call on this extractor)."""
+        p = Pyramid()
+        _check(self._lib.orbx_extractor_pyramid_device(self._h, C.byref(p)))
+        return p
+
     def mvImagePyramid(self):
         """Host copies of the pyramid levels of the last image (include/ORBextractor.h:85)."""
         if self._last_shape is None:
@@ -327,8 +370,8 @@ class ORBmatcher:
                                               _tp(sd), s))
         return bi, bd, sd
 
-    def ComputeStereoMatches(self, kps_left, desc_left, kps_right, desc_right, scale_factors, rows, bf, b):
-        """Descriptor search of Frame::ComputeStereoMatches (src/Frame.cc:466-552)."""
+    def stereo_descriptor_search(self, kps_left, desc_left, kps_right, desc_right, scale_factors, rows, bf, b):
+        """Descriptor search half of Frame::ComputeStereoMatches (src/Frame.cc:466-552)."""
         kl = np.ascontiguousarray(kps_left, KP_DTYPE)
         kr = np.ascontiguousarray(kps_right, KP_DTYPE)
         dl = np.ascontiguousarray(desc_left, np.uint8)
@@ -340,6 +383,34 @@ class ORBmatcher:
         _check(self._lib.orbx_stereo_match(self._h, _p(kl), _p(dl), len(kl), _p(kr), _p(dr), len(kr), _p(sc), len(sc),
                                            rows, bf, b, _p(bi), _p(bd), C.byref(n)))
         return StereoResult(bi, bd, n.value)
+
+    def ComputeStereoMatches(self, left, right, kps_left, desc_left, kps_right, desc_right, bf, b):
+        """Frame::ComputeStereoMatches (src/Frame.cc:466-639): left/right are the ORBextractors whose last
+        host call produced the keypoints (their pyramids are read).  Returns (mvuRight, mvDepth)."""
+        kl = np.ascontiguousarray(kps_left, KP_DTYPE)
+        kr = np.ascontiguousarray(kps_right, KP_DTYPE)
+        dl = np.ascontiguousarray(desc_left, np.uint8)
+        dr = np.ascontiguousarray(desc_right, np.uint8)
+        ur = np.zeros(len(kl), np.float32)
+        dp = np.zeros(len(kl), np.float32)
+        n = C.c_int()
+        _check(self._lib.orbx_compute_stereo_matches(self._h, left._h, right._h, _p(kl), _p(dl), len(kl), _p(kr), _p(dr),
+                                                     len(kr), bf, b, _p(ur), _p(dp), C.byref(n)))
+        return ur, dp
+
+    def stereo_refine_batch_device(self, kl, nl, kr, best_idx, left_pyramid, left_first, right_pyramid, right_first,
+                                   bf, b, stream=None):
+        """Sub-pixel half of Frame::ComputeStereoMatches (src/Frame.cc:554-639) on device batches; pyramids
+        from ORBextractor.pyramid_device().  Returns (uright, depth) (B, capacity) float32 device tensors."""
+        import torch
+        B, cap = best_idx.shape
+        ur = torch.empty((B, cap), dtype=torch.float32, device=kl.device)
+        dp = torch.empty((B, cap), dtype=torch.float32, device=kl.device)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(kl.device).cuda_stream)
+        _check(self._lib.orbx_stereo_refine_batch_device(self._h, _tp(kl), _tp(nl), _tp(kr), _tp(best_idx), B, cap,
+                                                         C.byref(left_pyramid), left_first, C.byref(right_pyramid),
+                                                         right_first, bf, b, _tp(ur), _tp(dp), s))
+        return ur, dp
 
     def stereo_match_batch_device(self, kl, dl, nl, kr, dr, nr, capacity, scale_factors, rows, bf, b, stream=None):
         import torch
@@ -364,19 +435,18 @@ class ORBmatcher:
                                                  _p(a2), _p(v2), len(d2), _featvec(fv2), _p(m), C.byref(n)))
         return n.value, m
 
-    def SearchByBoW_pairs_device(self, desc, kps, valid, fv_nodes, fv_offsets, fv_indices, n_fv, pairs, max_fv_nodes,
-                                 stream=None):
-        """MapFusion's cross-agent SearchByBoW(KF, KF) for many (kf1, kf2) store-slot pairs in one launch.
-        All arguments are device tensors in the extractor/vocabulary batch layouts; pairs: (P, 2) int32.
+    def SearchByBoW_pairs_device(self, store: "KfStore", pairs, max_fv_nodes, stream=None):
+        """SearchByBoW(KF, KF) for many (kf1, kf2) slot pairs of a device keyframe store in one launch
+        (MapFusion.cc:275 / :849 call shape).  pairs: (P, 2) int32 device tensor.
         Returns (match12 (P, capacity) int32, nmatches (P,) int32) device tensors."""
         import torch
-        P, cap = pairs.shape[0], desc.shape[1]
-        m12 = torch.empty((P, cap), dtype=torch.int32, device=desc.device)
-        nm = torch.empty((P,), dtype=torch.int32, device=desc.device)
-        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(desc.device).cuda_stream)
-        _check(self._lib.orbx_search_by_bow_kfkf_pairs_device(
-            self._h, _tp(desc), _tp(kps), _tp(valid), _tp(fv_nodes), _tp(fv_offsets), _tp(fv_indices), _tp(n_fv), cap,
-            _tp(pairs), P, int(max_fv_nodes), _tp(m12), _tp(nm), s))
+        P, cap = pairs.shape[0], store.capacity
+        dev = pairs.device
+        m12 = torch.empty((P, cap), dtype=torch.int32, device=dev)
+        nm = torch.empty((P,), dtype=torch.int32, device=dev)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream)
+        _check(self._lib.orbx_search_by_bow_kfkf_pairs_device(self._h, C.byref(store), _tp(pairs), P, int(max_fv_nodes),
+                                                              _tp(m12), _tp(nm), s))
         return m12, nm
 
     def SearchByBoW_KF_F(self, desck, anglek, validk, fvk, descf, anglef, fvf):

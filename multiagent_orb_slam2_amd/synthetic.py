@@ -105,32 +105,34 @@ def synthetic_vocabulary(seed: int, k: int = 10, L: int = 4, flip_p: float = 0.1
     words.  Returns the node lines in loadFromTextFile order (node id = line + 1, root = 0):
     dict(k, L, scoring, weighting, parent, is_leaf, desc, weight)."""
     rng = np.random.Generator(np.random.PCG64(seed))
+    flip_t = int(round(flip_p * 256))                      # bit flips with probability flip_t/256
+    f_ids = np.zeros(1, np.int64)
+    f_bits = np.unpackbits(rng.integers(0, 256, (1, 32), dtype=np.uint8), axis=1)
     parent, leaf, desc, weight = [], [], [], []
-    frontier = [(0, rng.integers(0, 256, 32, dtype=np.uint8), 0)]   # (node id, descriptor, depth)
     next_id = 1
-    while frontier:
-        nxt = []
-        for nid, d, depth in frontier:
-            bits = np.unpackbits(d)
-            for _ in range(k):
-                flips = rng.random(256) < flip_p
-                cd = np.packbits(bits ^ flips)
-                is_leaf = depth + 1 == L
-                parent.append(nid)
-                leaf.append(1 if is_leaf else 0)
-                desc.append(cd)
-                if is_leaf:
-                    w = 0.0 if rng.random() < stop_frac else float(np.log(1e6 / rng.integers(1, 5000)))
-                else:
-                    w = 0.0
-                weight.append(w)
-                if not is_leaf:
-                    nxt.append((next_id, cd, depth + 1))
-                next_id += 1
-        frontier = nxt
-    return dict(k=k, L=L, scoring=scoring, weighting=weighting, parent=np.array(parent, np.int32),
-                is_leaf=np.array(leaf, np.uint8), desc=np.stack(desc).astype(np.uint8),
-                weight=np.array(weight, np.float64))
+    for depth in range(L):                                 # breadth first: the order saveToTextFile writes
+        n = len(f_ids) * k
+        par = np.repeat(f_ids, k)
+        bits = np.repeat(f_bits, k, axis=0)
+        for c0 in range(0, n, 1 << 16):                     # chunked: L=6 has 10^6 leaves
+            c1 = min(n, c0 + (1 << 16))
+            bits[c0:c1] ^= (rng.integers(0, 256, (c1 - c0, 256), dtype=np.uint8) < flip_t).astype(np.uint8)
+        is_leaf = depth + 1 == L
+        parent.append(par.astype(np.int32))
+        leaf.append(np.full(n, 1 if is_leaf else 0, np.uint8))
+        desc.append(np.packbits(bits, axis=1))
+        if is_leaf:
+            stop = rng.random(n) < stop_frac
+            w = np.log(1e6 / rng.integers(1, 5000, n).astype(np.float64))
+            weight.append(np.where(stop, 0.0, w))
+        else:
+            weight.append(np.zeros(n))
+        f_ids = next_id + np.arange(n, dtype=np.int64)
+        f_bits = bits
+        next_id += n
+    return dict(k=k, L=L, scoring=scoring, weighting=weighting, parent=np.concatenate(parent),
+                is_leaf=np.concatenate(leaf), desc=np.concatenate(desc).astype(np.uint8),
+                weight=np.concatenate(weight).astype(np.float64))
 
 
 def write_vocabulary_text(voc, path: str):

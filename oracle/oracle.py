@@ -141,6 +141,36 @@ def stereo_match(kl, dl, kr, dr, scale, rows, bf, b):
     return n, idx, dist
 
 
+def stereo_refine(kl, kr, best_idx, scale, inv_scale, pyr_l, pyr_r, bf, b):
+    """Frame.cc:554-639 (SAD window, parabola, median rejection) -> (n, uright, depth, sad)."""
+    kl, kr = np.ascontiguousarray(kl, KP_DTYPE), np.ascontiguousarray(kr, KP_DTYPE)
+    bi = np.ascontiguousarray(best_idx, np.int32)
+    scale, inv_scale = np.ascontiguousarray(scale, np.float32), np.ascontiguousarray(inv_scale, np.float32)
+    n = len(kl)
+    ur, dp, sad = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.int32)
+
+    def lv(pyr):
+        pyr = [np.ascontiguousarray(x, np.uint8) for x in pyr]
+        ptrs = (C.c_void_p * len(pyr))(*[x.ctypes.data for x in pyr])
+        step = np.array([x.strides[0] for x in pyr], np.int32)
+        rows = np.array([x.shape[0] for x in pyr], np.int32)
+        cols = np.array([x.shape[1] for x in pyr], np.int32)
+        return pyr, ptrs, step, rows, cols
+
+    L, R = lv(pyr_l), lv(pyr_r)
+    k = lib().orc_stereo_refine(_p(kl), n, _p(kr), _p(bi), _p(scale), _p(inv_scale), L[1], _p(L[2]), _p(L[3]), _p(L[4]),
+                                R[1], _p(R[2]), _p(R[3]), _p(R[4]), C.c_float(bf), C.c_float(b), _p(ur), _p(dp), _p(sad))
+    return k, ur, dp, sad
+
+
+def compute_stereo_matches(left, right, scale, inv_scale, rows, bf, b):
+    """Frame::ComputeStereoMatches (src/Frame.cc:466-639) on two oracle extractions made with
+    want_pyramid=True -> (uright, depth)."""
+    _, bi, _ = stereo_match(left["kps"], left["desc"], right["kps"], right["desc"], scale, rows, bf, b)
+    _, ur, dp, _ = stereo_refine(left["kps"], right["kps"], bi, scale, inv_scale, left["pyramid"], right["pyramid"], bf, b)
+    return ur, dp
+
+
 def search_by_bow_kfkf(d1, ang1, valid1, fv1, d2, ang2, valid2, fv2, nnratio=0.75, check_ori=True):
     d1, d2 = np.ascontiguousarray(d1, np.uint8), np.ascontiguousarray(d2, np.uint8)
     ang1, ang2 = np.ascontiguousarray(ang1, np.float32), np.ascontiguousarray(ang2, np.float32)

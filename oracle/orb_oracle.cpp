@@ -790,6 +790,80 @@ int orc_stereo_match(const orc_kp* kl, const uint8_t* dl, int nl, const orc_kp* 
     return n;
 }
 
+// Frame::ComputeStereoMatches sub-pixel part (src/Frame.cc:554-639), after the descriptor search above:
+// for each left keypoint with an accepted right match, an 11x11 SAD window (centre-subtracted, exact
+// integer arithmetic as the float Mats hold small integers) slid over +-5 px on the left keypoint's
+// pyramid level, parabola fit, disparity check, then the median-distance outlier rejection.  Level l of
+// the left/right pyramids: lvl*[l] with row step step*[l] and size rows*[l] x cols*[l].  Bounds of the left
+// window and of the right window's low side are not checked by the reference (cv::Mat::colRange would
+// assert); extractor keypoints never reach them, here such keypoints get no depth.  An empty accepted set
+// skips the median step (the reference indexes vDistIdx[0] of an empty vector).
+int orc_stereo_refine(const orc_kp* kl, int nl, const orc_kp* kr, const int32_t* best_idx, const float* scale,
+                      const float* inv_scale, const uint8_t* const* lvlL, const int* stepL, const int* rowsL,
+                      const int* colsL, const uint8_t* const* lvlR, const int* stepR, const int* rowsR, const int* colsR,
+                      float bf, float b, float* uright, float* depth, int32_t* sad) {
+    const float minZ = b, minD = 0, maxD = bf / minZ;
+    std::vector<std::pair<int, int>> distIdx;
+    for (int l = 0; l < nl; ++l) {
+        uright[l] = -1.0f; depth[l] = -1.0f; sad[l] = -1;
+        if (best_idx[l] < 0) continue;
+        const int oct = kl[l].octave;
+        const float uL = kl[l].x;
+        const float uR0 = kr[best_idx[l]].x;
+        const float sf = inv_scale[oct];
+        const float suL = std::round(kl[l].x * sf), svL = std::round(kl[l].y * sf), suR0 = std::round(uR0 * sf);
+        const int w = 5, L = 5;
+        const int iuL = (int)suL, ivL = (int)svL, iuR0 = (int)suR0;
+        if (ivL - w < 0 || ivL + w >= rowsL[oct] || iuL - w < 0 || iuL + w >= colsL[oct] || ivL + w >= rowsR[oct] ||
+            iuR0 - L - w < 0)
+            continue;
+        const float iniu = suR0 + L - w, endu = suR0 + L + w + 1;
+        if (iniu < 0 || endu >= colsR[oct]) continue;
+        const uint8_t* IL = lvlL[oct] + (size_t)(ivL - w) * stepL[oct] + (iuL - w);
+        const int cL = IL[(size_t)w * stepL[oct] + w];
+        int bestDist = 0x7fffffff, bestInc = 0;
+        int dists[11];
+        for (int inc = -L; inc <= L; ++inc) {
+            const uint8_t* IR = lvlR[oct] + (size_t)(ivL - w) * stepR[oct] + (iuR0 + inc - w);
+            const int cR = IR[(size_t)w * stepR[oct] + w];
+            int d = 0;
+            for (int y = 0; y < 2 * w + 1; ++y)
+                for (int x = 0; x < 2 * w + 1; ++x)
+                    d += std::abs((IL[(size_t)y * stepL[oct] + x] - cL) - (IR[(size_t)y * stepR[oct] + x] - cR));
+            if ((float)d < (float)bestDist) { bestDist = d; bestInc = inc; }
+            dists[L + inc] = d;
+        }
+        if (bestInc == -L || bestInc == L) continue;
+        const float d1 = (float)dists[L + bestInc - 1], d2 = (float)dists[L + bestInc], d3 = (float)dists[L + bestInc + 1];
+        const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));
+        if (deltaR < -1 || deltaR > 1) continue;
+        float bestuR = scale[oct] * ((float)suR0 + (float)bestInc + deltaR);
+        float disparity = uL - bestuR;
+        if (disparity >= minD && disparity < maxD) {
+            if (disparity <= 0) {
+                disparity = 0.01;
+                bestuR = uL - 0.01;
+            }
+            depth[l] = bf / disparity;
+            uright[l] = bestuR;
+            sad[l] = bestDist;
+            distIdx.push_back({bestDist, l});
+        }
+    }
+    if (distIdx.empty()) return 0;
+    std::sort(distIdx.begin(), distIdx.end());
+    const float median = distIdx[distIdx.size() / 2].first;
+    const float thDist = 1.5f * 1.4f * median;
+    int n = (int)distIdx.size();
+    for (int i = (int)distIdx.size() - 1; i >= 0; --i) {
+        if (distIdx[i].first < thDist) break;
+        uright[distIdx[i].second] = -1;
+        depth[distIdx[i].second] = -1;
+        --n;
+    }
+    return n;
+}
+
 // FeatureVector as CSR: node ids ascending, offsets[n_nodes+1], feature indices.
 struct orc_fv { const uint32_t* node; const int32_t* off; int n_nodes; const int32_t* idx; };
 

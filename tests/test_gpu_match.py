@@ -65,7 +65,7 @@ def test_stereo_band_match(gpu, stereo_pair):
     from oracle import oracle as O
     p = stereo_pair
     m = pkg.ORBmatcher()
-    res = m.ComputeStereoMatches(p["kl"], p["dl"], p["kr"], p["dr"], p["scale"], p["rows"], BF, B)
+    res = m.stereo_descriptor_search(p["kl"], p["dl"], p["kr"], p["dr"], p["scale"], p["rows"], BF, B)
     n, idx, dist = O.stereo_match(p["kl"], p["dl"], p["kr"], p["dr"], p["scale"], p["rows"], BF, B)
     assert np.array_equal(res.best_idx, idx)
     assert np.array_equal(res.best_dist, dist)

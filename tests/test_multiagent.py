@@ -151,3 +151,126 @@ def test_two_agent_exchange_and_sharded_matching_gloo():
                 exp.append((a, qi, ci, int(n)))
     assert flat == sorted(exp)
     assert max(r[3] for r in flat) >= 20   # the revisited place passes MapFusion's 20-match gate
+
+
+def _fv_dict(views_fv, cap):
+    n = len(views_fv)
+    d = dict(fv_nodes=np.zeros((n, cap), np.int32), fv_offsets=np.zeros((n, cap + 1), np.int32),
+             fv_indices=np.zeros((n, cap), np.int32), n_fv=np.zeros(n, np.int32))
+    for i, (ids, offs, idx) in enumerate(views_fv):
+        d["fv_nodes"][i, :len(ids)] = ids
+        d["fv_offsets"][i, :len(offs)] = offs
+        d["fv_indices"][i, :len(idx)] = idx
+        d["n_fv"][i] = len(ids)
+    return {k: torch.from_numpy(v) for k, v in d.items()}
+
+
+def test_packet_layout_aligned_and_featvec_roundtrip():
+    cap = 320
+    lay = MA.PacketLayout(cap)
+    assert lay.bytes % 16 == 0 and all(o % 16 == 0 for o in lay.offsets.values())
+    kps, desc, valid, counts = _keyframes(0, 2, cap)
+    fvs = [S.random_featvec(40 + i, int(counts[i]), n_nodes=30) for i in range(2)]
+    pk = MA.pack_keyframes(torch.from_numpy(kps.view(np.uint8).reshape(2, cap, 28)), torch.from_numpy(desc),
+                           torch.from_numpy(counts), torch.from_numpy(valid), agent=1, frames=[0, 5], capacity=cap,
+                           fv=_fv_dict(fvs, cap))
+    for i, v in enumerate(MA.unpack_keyframes(pk, cap)):
+        assert v.count == counts[i] and np.array_equal(v.desc, desc[i, :counts[i]])
+        for a, b in zip(v.featvec, fvs[i]):
+            assert np.array_equal(a, b)
+
+
+def test_store_ring_and_candidate_pairs():
+    cap = 64
+    st = MA.DeviceKeyframeStore(cap, slots=12, device="cpu")
+    P = MA.packet_bytes(cap)
+    for step in range(5):                                # ring wraps: 5 steps x 4 slots > 12
+        pk = torch.full((4, P), step, dtype=torch.uint8)
+        slots = st.insert(pk, agent=step % 2)
+        assert len(slots) == 4 and (st.buf[slots.start:slots.stop] == step).all()
+    assert list(slots) == [4, 5, 6, 7]                  # step 4 landed after step 3 (slots 0-3)
+    # other-agent candidates: most recent first, never the querying agent
+    pr = st.candidate_pairs([4, 5], agent=0, k=3)
+    # step 3 (agent 1) wrapped into slots 0-3, so those are agent 1's most recent keyframes
+    assert pr.tolist() == [[4, 3], [4, 2], [4, 1], [5, 3], [5, 2], [5, 1]]
+    own = st.candidate_pairs([6], agent=0, k=2, other_agents_only=False)
+    assert own.tolist() == [[6, 5], [6, 4]]
+
+
+def _store_worker(rank, world, port, cap, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ex = MA.KeyframeExchange()
+    st = MA.DeviceKeyframeStore(cap, slots=8, device="cpu")
+    for step in range(3):
+        kps, desc, valid, counts = _keyframes(rank, 2, cap)
+        fvs = [S.random_featvec(100 * rank + 10 * step + i, int(counts[i]), n_nodes=20) for i in range(2)]
+        pk = MA.pack_keyframes(torch.from_numpy(kps.view(np.uint8).reshape(2, cap, 28)), torch.from_numpy(desc),
+                               torch.from_numpy(counts), torch.from_numpy(valid), agent=rank,
+                               frames=[10 * step, 10 * step + 5], capacity=cap, fv=_fv_dict(fvs, cap))
+        slots = st.exchange_into(ex, pk)
+    pairs = st.candidate_pairs(slots[2 * rank:2 * rank + 2], rank, k=3)
+    if rank == 0:
+        q.put((st.buf.numpy().copy(), list(st.agent_of), list(st.stamp), list(slots), pairs.tolist()))
+    dist.destroy_process_group()
+
+
+def test_two_agent_store_exchange_gloo():
+    cap, world = 320, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_store_worker, args=(r, world, port, cap, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    buf, agent_of, stamp, slots, pairs = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert slots == [0, 1, 2, 3]                         # third step wrapped (3 x 4 > 8 slots)
+    assert agent_of[:4] == [0, 0, 1, 1] and stamp[:4] == [8, 9, 10, 11]
+    views = MA.unpack_keyframes(torch.from_numpy(buf[:4]), cap)
+    assert [v.agent for v in views] == [0, 0, 1, 1] and [v.frame for v in views] == [20, 25, 20, 25]
+    for v in views:
+        fv_exp = S.random_featvec(100 * v.agent + 20 + (v.frame - 20) // 5, v.count, n_nodes=20)
+        assert all(np.array_equal(a, b) for a, b in zip(v.featvec, fv_exp))
+    # rank 0's queries (slots 0, 1) get agent 1's most recent keyframes: slots 3, 2 (this step), then 7 (step 1)
+    assert pairs == [[0, 3], [0, 2], [0, 7], [1, 3], [1, 2], [1, 7]]
+
+
+@pytest.mark.gpu
+def test_gpu_keyframe_fusion_store_vs_oracle(gpu):
+    """Extractor -> stereo valid flags -> vocabulary -> packets -> device store -> batched SearchByBoW,
+    every (query, candidate) pair checked against the oracle on the unpacked host keyframes."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    dev = torch.device("cuda", 0)
+    voc = S.synthetic_vocabulary(31, k=10, L=4)
+    v = pkg.ORBVocabulary.from_arrays(voc)
+    ex = pkg.ORBextractor(1200, 1.2, 8, 20, 7)
+    m = pkg.ORBmatcher(0.75, True)
+    base = S.kitti_like_image(77)
+    imgs = np.stack([base] + [S.shifted_right_view(base, 3 + i, max_disp=12) for i in range(5)])
+    kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).to(dev))
+    cap = kps.shape[1]
+    valid = (torch.arange(cap, device=dev)[None, :] < cnt[:, None]).to(torch.uint8)
+    valid[:, ::4] = 0                                   # a quarter without MapPoints
+    fus = MA.KeyframeFusion(m, v, cap, slots=6, device=dev, candidates=4, levelsup=2)
+    out = []
+    for step in range(2):
+        r = slice(3 * step, 3 * step + 3)
+        out.append(fus.step(kps[r], desc[r], cnt[r], valid[r], frames=[3 * step, 3 * step + 1, 3 * step + 2]))
+    torch.cuda.synchronize()
+    views = MA.unpack_keyframes(fus.store.buf, cap)
+    total = 0
+    for pr, m12, nm, passed in out:
+        prh, m12h, nmh = pr.cpu().numpy(), m12.cpu().numpy(), nm.cpu().numpy()
+        assert len(prh) > 0
+        for p, (a, b) in enumerate(prh):
+            A, B = views[a], views[b]
+            rn, rm = O.search_by_bow_kfkf(A.desc, A.kps["angle"], A.valid, A.featvec, B.desc, B.kps["angle"], B.valid,
+                                          B.featvec, 0.75, True)
+            assert nmh[p] == rn and np.array_equal(m12h[p, :A.count], rm), (p, a, b)
+            total += rn
+        assert np.array_equal(passed.cpu().numpy(), nmh >= 20)
+    assert total > 100

@@ -145,8 +145,10 @@ def test_gpu_bow_pairs_over_keyframe_store(gpu, check_ori):
     pairs = torch.from_numpy(pairs_h).cuda()
     m = pkg.ORBmatcher(0.75, check_ori)
     n_fv = out["n_fv"]
-    m12, nm = m.SearchByBoW_pairs_device(desc, kps, valid, out["fv_nodes"], out["fv_offsets"], out["fv_indices"],
-                                         n_fv, pairs, int(n_fv.max().item()))
+    store = pkg.orbx.KfStore.from_fields(
+        cap, desc=(desc, cap * 32), kps=(kps, cap * 28), valid=(valid, cap), fv_nodes=(out["fv_nodes"], cap * 4),
+        fv_offsets=(out["fv_offsets"], (cap + 1) * 4), fv_indices=(out["fv_indices"], cap * 4), n_fv=(n_fv, 4))
+    m12, nm = m.SearchByBoW_pairs_device(store, pairs, int(n_fv.max().item()))
     torch.cuda.synchronize()
     kh, dh, ch = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
     o = {k: out[k].cpu().numpy() for k in ("fv_nodes", "fv_offsets", "fv_indices", "n_fv")}
