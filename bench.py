@@ -3,8 +3,8 @@
 at KITTI size 1242x375, 8 levels, 2000 keypoints, on 1..N MI355X (one agent per GPU).
 
 A "step" = one batch of --batch synthetic stereo frames per GPU through the hot path:
-  ORBextractor on 2*batch images (src/ORBextractor.cc:1043-1105)  +  the descriptor search of
-  Frame::ComputeStereoMatches on batch pairs (src/Frame.cc:466-552)
+  ORBextractor on 2*batch images (src/ORBextractor.cc:1043-1105)  +  Frame::ComputeStereoMatches on
+  batch pairs (descriptor band search, SAD sub-pixel refinement, median rejection; src/Frame.cc:466-639)
 and the keyframe path: every 5th left frame becomes a keyframe (MapPoint-valid = stereo-matched, as
 Tracking::CreateNewKeyFrame makes stereo MapPoints), its DBoW2 FeatureVector is computed on the GPU
 (KeyFrame::ComputeBoW, synthetic k=10 L=6 vocabulary of ORBvoc's shape), the keyframe packets are
@@ -69,20 +69,30 @@ def algorithmic_bytes(ex, mean_cand, mean_kps):
     }
 
 
-def cpu_baseline(lefts, rights, scale, seconds):
+def cpu_baseline(lefts, rights, tables, voc, seconds):
+    """The same per-frame work on one host core with the oracle: extract L and R, ComputeStereoMatches
+    (band search + SAD refinement), and every KF_EVERY-th frame a keyframe: BoW transform + SearchByBoW
+    against the KF_CANDIDATES previous keyframes."""
     from oracle import oracle as O
+    vocab = O.Vocabulary(voc)
+    kfs = []
     t0 = time.perf_counter()
     n = 0
-    i = 0
     while True:
-        l, r = lefts[i % len(lefts)], rights[i % len(rights)]
-        a = O.extract(l, nfeatures=NFEAT)
-        b = O.extract(r, nfeatures=NFEAT)
-        O.stereo_match(a["kps"], a["desc"], b["kps"], b["desc"], scale, ROWS, BF, BASELINE_B)
+        l, r = lefts[n % len(lefts)], rights[n % len(rights)]
+        a = O.extract(l, nfeatures=NFEAT, want_pyramid=True)
+        b = O.extract(r, nfeatures=NFEAT, want_pyramid=True)
+        _, depth = O.compute_stereo_matches(a, b, tables["scale"], tables["inv_scale"], ROWS, BF, BASELINE_B)
+        if n % KF_EVERY == 0:
+            bow = vocab.transform(a["desc"], 4)
+            kf = (a["desc"], a["kps"]["angle"], (depth > 0).astype(np.uint8),
+                  (bow["fv_nodes"], bow["fv_offsets"], bow["fv_indices"]))
+            for c in kfs[-KF_CANDIDATES:]:
+                O.search_by_bow_kfkf(*kf, *c, 0.75, True)
+            kfs.append(kf)
         n += 1
-        i += 1
         el = time.perf_counter() - t0
-        if el >= seconds and n >= 3:
+        if el >= seconds and n >= KF_EVERY:
             break
     return n / el, n, el
 
@@ -136,6 +146,7 @@ def main():
 
     stereo_ms = []
     kf_ms = []
+    pyr = []
 
     def step(time_stereo=False):
         ex.extract_batch_device(imgs, kps, desc, cnt, stream=stream)
@@ -144,6 +155,10 @@ def main():
             e0.record(stream)
         bi, bd = m.stereo_match_batch_device(kps[:B], desc[:B], cnt[:B], kps[B:], desc[B:], cnt[B:], cap, scale,
                                              ROWS, BF, BASELINE_B, stream=stream)
+        if not pyr:
+            pyr.append(ex.pyramid_device())            # device pointers are fixed for this input / config
+        ur, depth = m.stereo_refine_batch_device(kps[:B], cnt[:B], kps[B:], bi, pyr[0], 0, pyr[0], B, BF, BASELINE_B,
+                                                 stream=stream)
         if time_stereo:
             e1.record(stream)
             stereo_ms.append((e0, e1))
@@ -151,7 +166,7 @@ def main():
         if time_stereo:
             e2 = torch.cuda.Event(enable_timing=True)
             e2.record(stream)
-        valid = (bi.index_select(0, kf_rows) >= 0).to(torch.uint8)
+        valid = (depth.index_select(0, kf_rows) > 0).to(torch.uint8)   # stereo keypoints get MapPoints
         frames = [frame_no[0] + KF_EVERY * i for i in range(n_kf)]
         frame_no[0] += B
         _, _, nm, passed = fusion.step(kps.index_select(0, kf_rows), desc.index_select(0, kf_rows),
@@ -193,7 +208,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": "C2+C3 stereo frame: ORBextractor x2 (1242x375, 8 levels, 2000 kpts) + stereo "
-                               "L<->R 256-bit Hamming band match; every 5th frame a keyframe: DBoW2 transform (k=10, "
+                               "L<->R 256-bit Hamming band match + SAD sub-pixel refinement; every 5th frame a keyframe: DBoW2 transform (k=10, "
                                "L=6) + " + ("RCCL all-gather of KF packets + " if world > 1 else "") +
                                f"SearchByBoW vs {KF_CANDIDATES} candidate KFs",
                    "keyframes_per_gpu_per_step": n_kf, "bow_pairs_per_gpu_per_step": n_kf * KF_CANDIDATES,
@@ -237,10 +252,14 @@ def main():
         out["stage_ms_per_step"] = {k: round(v, 4) for k, v in per_call.items()}
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        fps, n, secs = cpu_baseline(lefts, rights, scale, args.cpu_seconds)
+        from oracle import oracle as O
+        fps, n, secs = cpu_baseline(lefts, rights, O.tables(NFEAT), S.synthetic_vocabulary(2024, k=10, L=6),
+                                    args.cpu_seconds)
         out["cpu_baseline"] = {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": f"{n} stereo frames (2 extractions + stereo match each) of the same synthetic "
-                                         f"inputs, oracle/orb_oracle.cpp -O2, 1 thread, {secs:.1f} s"}
+                               "sample": f"{n} stereo frames of the same synthetic inputs and the same per-frame work "
+                                         f"(2 extractions + ComputeStereoMatches; every {KF_EVERY}th frame BoW + "
+                                         f"SearchByBoW vs {KF_CANDIDATES} earlier keyframes), oracle/orb_oracle.cpp -O2, "
+                                         f"1 thread, {secs:.1f} s"}
     out["fusion_gate_passed_per_step"] = round(int(gate.item()) / (args.steps + args.warmup + STORE_STEPS), 2)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -257,13 +257,13 @@ class ORBextractor:
         self._last_shape = (rows, cols)
         return kps[: n.value].copy(), desc[: n.value].copy()
 
-    @property
     def pyramid_device(self) -> "Pyramid":
         """orbx_pyramid of the last call (device pointers; valid until the next call on this extractor)."""
         p = Pyramid()
         _check(self._lib.orbx_extractor_pyramid_device(self._h, C.byref(p)))
         return p
 
+    @property
     def mvImagePyramid(self):
         """Host copies of the pyramid levels of the last image (include/ORBextractor.h:85)."""
         if self._last_shape is None:

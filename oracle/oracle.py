@@ -234,6 +234,34 @@ def distribute(xyr, minX, maxX, minY, maxY, N):
     return out[:m].copy()
 
 
+class Vocabulary:
+    """Oracle vocabulary built once (for timing many transforms: bench.py's cpu_baseline)."""
+
+    def __init__(self, voc):
+        self._arrs = [np.ascontiguousarray(voc["parent"], np.int32), np.ascontiguousarray(voc["is_leaf"], np.uint8),
+                      np.ascontiguousarray(voc["desc"], np.uint8), np.ascontiguousarray(voc["weight"], np.float64)]
+        P, lf, D, W = self._arrs
+        lib().orc_vocab_new.restype = C.c_void_p
+        self._h = C.c_void_p(lib().orc_vocab_new(voc["L"], voc["scoring"], voc["weighting"], len(P), _p(P), _p(lf),
+                                                 _p(D), _p(W)))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_vocab_free(self._h)
+            self._h = None
+
+    def transform(self, feats, levelsup):
+        feats = np.ascontiguousarray(feats, np.uint8)
+        n = len(feats)
+        bw, bv = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.float64)
+        fn, fo, fi = np.zeros(max(n, 1), np.uint32), np.zeros(n + 1, np.int32), np.zeros(max(n, 1), np.int32)
+        nw, nf = C.c_int(), C.c_int()
+        lib().orc_vocab_apply(self._h, _p(feats), n, levelsup, _p(bw), _p(bv), C.byref(nw), _p(fn), _p(fo), _p(fi),
+                              C.byref(nf))
+        return dict(bow_words=bw[:nw.value].copy(), bow_values=bv[:nw.value].copy(), fv_nodes=fn[:nf.value].copy(),
+                    fv_offsets=fo[:nf.value + 1].copy(), fv_indices=fi[:fo[nf.value]].copy())
+
+
 def vocab_transform(voc, feats, levelsup):
     """Oracle TemplatedVocabulary::transform; voc = dict(k, L, scoring, weighting, parent, is_leaf, desc, weight)."""
     feats = np.ascontiguousarray(feats, np.uint8)

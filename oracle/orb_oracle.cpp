@@ -1011,52 +1011,71 @@ int orc_search_for_triangulation(const uint8_t* d1, const orc_kp* k1, const uint
 // :1218-1259): std::map BowVector / FeatureVector exactly as DBoW2 builds them.  Node numbering as in
 // loadFromTextFile (:1338-1424): line i = node i + 1, root 0.
 // ---------------------------------------------------------------------------------------------------
-int orc_vocab_transform(int /*k*/, int L, int scoring, int weighting, int n_lines, const int32_t* parent,
-                        const uint8_t* is_leaf, const uint8_t* vdesc, const double* vweight, const uint8_t* feats, int n,
-                        int levelsup, uint32_t* bow_words, double* bow_values, int* n_words, uint32_t* fv_nodes,
-                        int32_t* fv_off, int32_t* fv_idx, int* n_fv) {
+struct OrcVocab {
+    int L, scoring, weighting;
+    std::vector<std::vector<int>> children;
+    std::vector<int> word;
+    std::vector<double> w;
+    std::vector<uint8_t> desc;   // node id - 1
+};
+
+// TemplatedVocabulary::loadFromTextFile's tree (TemplatedVocabulary.h:1338-1424), built once.
+void* orc_vocab_new(int L, int scoring, int weighting, int n_lines, const int32_t* parent, const uint8_t* is_leaf,
+                    const uint8_t* vdesc, const double* vweight) {
+    OrcVocab* v = new OrcVocab();
+    v->L = L; v->scoring = scoring; v->weighting = weighting;
     const int N = n_lines + 1;
-    std::vector<std::vector<int>> children(N);
-    std::vector<int> word(N, -1);
-    std::vector<double> w(N, 0.0);
+    v->children.assign(N, {});
+    v->word.assign(N, -1);
+    v->w.assign(N, 0.0);
+    v->desc.assign(vdesc, vdesc + 32 * (size_t)n_lines);
     int nw = 0;
     for (int i = 0; i < n_lines; ++i) {
-        children[parent[i]].push_back(i + 1);
-        w[i + 1] = vweight[i];
-        if (is_leaf[i]) word[i + 1] = nw++;
+        v->children[parent[i]].push_back(i + 1);
+        v->w[i + 1] = vweight[i];
+        if (is_leaf[i]) v->word[i + 1] = nw++;
     }
+    return v;
+}
+
+void orc_vocab_free(void* h) { delete static_cast<OrcVocab*>(h); }
+
+// TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup) (:1125-1187, :1218-1259).
+int orc_vocab_apply(void* h, const uint8_t* feats, int n, int levelsup, uint32_t* bow_words, double* bow_values, int* n_words,
+                    uint32_t* fv_nodes, int32_t* fv_off, int32_t* fv_idx, int* n_fv) {
+    const OrcVocab& V = *static_cast<OrcVocab*>(h);
     std::map<uint32_t, double> bow;
     std::map<uint32_t, std::vector<unsigned>> fv;
-    const int nid_level = L - levelsup;
+    const int nid_level = V.L - levelsup;
     for (int f = 0; f < n; ++f) {
         const uint8_t* x = feats + 32 * (size_t)f;
         unsigned nid = 0, final_id = 0;
         int level = 0;
         do {
             ++level;
-            const std::vector<int>& nodes = children[final_id];
+            const std::vector<int>& nodes = V.children[final_id];
             final_id = nodes[0];
-            double best_d = hamming(x, vdesc + 32 * (size_t)(final_id - 1));
+            double best_d = hamming(x, V.desc.data() + 32 * (size_t)(final_id - 1));
             for (size_t c = 1; c < nodes.size(); ++c) {
-                const double d = hamming(x, vdesc + 32 * (size_t)(nodes[c] - 1));
+                const double d = hamming(x, V.desc.data() + 32 * (size_t)(nodes[c] - 1));
                 if (d < best_d) { best_d = d; final_id = nodes[c]; }
             }
             if (level == nid_level) nid = final_id;
-        } while (!children[final_id].empty());
-        const double wt = w[final_id];
+        } while (!V.children[final_id].empty());
+        const double wt = V.w[final_id];
         if (wt > 0) {
-            const uint32_t id = (uint32_t)word[final_id];
-            if (weighting == 0 || weighting == 1) {   // TF_IDF, TF: addWeight
+            const uint32_t id = (uint32_t)V.word[final_id];
+            if (V.weighting == 0 || V.weighting == 1) {   // TF_IDF, TF: addWeight
                 auto it = bow.find(id);
                 if (it != bow.end()) it->second += wt; else bow.emplace(id, wt);
-            } else {                                  // IDF, BINARY: addIfNotExist
+            } else {                                      // IDF, BINARY: addIfNotExist
                 bow.emplace(id, wt);
             }
             fv[nid].push_back((unsigned)f);
         }
     }
-    double norm = 0.0;                                // BowVector::normalize (L1 or L2)
-    if (scoring == 0) { for (auto& kv : bow) norm += std::fabs(kv.second); }
+    double norm = 0.0;                                    // BowVector::normalize (L1 or L2)
+    if (V.scoring == 0) { for (auto& kv : bow) norm += std::fabs(kv.second); }
     else { for (auto& kv : bow) norm += kv.second * kv.second; norm = std::sqrt(norm); }
     if (norm > 0.0) for (auto& kv : bow) kv.second /= norm;
     int i = 0;
@@ -1072,6 +1091,16 @@ int orc_vocab_transform(int /*k*/, int L, int scoring, int weighting, int n_line
     fv_off[j] = o;
     *n_fv = j;
     return 0;
+}
+
+int orc_vocab_transform(int /*k*/, int L, int scoring, int weighting, int n_lines, const int32_t* parent,
+                        const uint8_t* is_leaf, const uint8_t* vdesc, const double* vweight, const uint8_t* feats, int n,
+                        int levelsup, uint32_t* bow_words, double* bow_values, int* n_words, uint32_t* fv_nodes,
+                        int32_t* fv_off, int32_t* fv_idx, int* n_fv) {
+    void* h = orc_vocab_new(L, scoring, weighting, n_lines, parent, is_leaf, vdesc, vweight);
+    const int r = orc_vocab_apply(h, feats, n, levelsup, bow_words, bow_values, n_words, fv_nodes, fv_off, fv_idx, n_fv);
+    orc_vocab_free(h);
+    return r;
 }
 
 }  // extern "C"
