@@ -185,6 +185,24 @@ __device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, con
     return pmax(mn9[0], (s16x2)(0) - mx9[0]) - (s16x2)(1);
 }
 
+// Compass pre-test for a pixel pair: every arc of 9 contains two compass taps 4 apart (0/4, 4/8, 8/12 or
+// 12/0), so "corner at t" (some arc with all d > t, or all d < -t) implies max over those four pairs of
+// min(d_k, d_k+4) > t, or min of max < -t.  A pixel failing it has s < t.  Returns 2 bits (pixel x, x+1).
+__device__ __forceinline__ int fast_pretest2(const uint32_t* __restrict__ E, const uint32_t* __restrict__ O, int y, int j,
+                                             int t) {
+    const uint32_t* eb = E + (y - 3) * kPairStride + j;
+    const uint32_t* ob = O + (y - 3) * kPairStride + j;
+    const s16x2 v = as_s2(ob[3 * kPairStride + 1]);
+    const s16x2 d0 = v - as_s2(ob[6 * kPairStride + 1]);      // ( 0,  3)
+    const s16x2 d4 = v - as_s2(eb[3 * kPairStride + 3]);      // ( 3,  0)
+    const s16x2 d8 = v - as_s2(ob[1]);                        // ( 0, -3)
+    const s16x2 d12 = v - as_s2(eb[3 * kPairStride + 0]);     // (-3,  0)
+    const s16x2 dk = pmax(pmax(pmin(d0, d4), pmin(d4, d8)), pmax(pmin(d8, d12), pmin(d12, d0)));
+    const s16x2 br = pmin(pmin(pmax(d0, d4), pmax(d4, d8)), pmin(pmax(d8, d12), pmax(d12, d0)));
+    const s16x2 m = pmax(dk, (s16x2)(0) - br);
+    return (m.x > t ? 1 : 0) | (m.y > t ? 2 : 0);
+}
+
 // OpenCV's NMS keeps a corner (s >= t) iff s > every neighbour's buffer value (s_n if s_n >= t, else
 // 0).  For s >= max(t, 1) a neighbour with s_n < t never blocks (s_n < t <= s, and 0 < s), so the rule
 // is: s >= max(t, 1) and s > max of the 8 raw neighbour scores -- one maximum serves both thresholds.
@@ -213,47 +231,55 @@ __device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, 
 }
 
 // One workgroup per (cell, image).  Cell geometry from ComputeKeyPointsOctTree (:784-807); FAST on the
-// ROI detects rows/cols [3, dim-3) of the ROI, NMS compares against the 8 neighbours' scores inside
-// the ROI's detection window (0 outside), strict '>' (OpenCV FAST_t).  Empty at iniTh -> minTh (:812-816).
+// ROI detects rows/cols [3, dim-3) of the ROI, NMS compares against the 8 neighbours' scores inside the
+// ROI's detection window (0 outside), strict '>' (OpenCV FAST_t).  Empty at iniTh -> minTh (:812-816).
 // Dynamic LDS: E and O pair images (max_rows x kPairStride dwords each) + padded int16 score map whose
-// pixel pairs are dword aligned (det column x at map column x + 2, pad ring at columns 1 and Wd + 2).
+// pixel pairs are dword aligned (det column x at map column x + 2, pad ring at columns 1 and Wd + 2) +
+// survivor list + kept-pixel key lists.  (A multi-cell workgroup that prefetches the next ROI into
+// registers while processing the current one measured 1.6x slower: 153 VGPRs, 3 waves per SIMD.)
+constexpr int kRoiRowsPerWave = kMaxRoi / 4;
+
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                     const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
                                                     int iniTh, int minTh, uint32_t* __restrict__ cand_xy,
                                                     uint8_t* __restrict__ cand_s, int cand_stride,
                                                     int* __restrict__ cell_cnt, int ncells, int stop_after, Src0 s0,
-                                                    int max_rows) {
+                                                    int max_rows, int max_cols) {
     extern __shared__ uint32_t fsm[];
-    __shared__ int red[8];
     uint32_t* E = fsm;
     uint32_t* O = fsm + max_rows * kPairStride;
     int16_t* sc = (int16_t*)(fsm + 2 * max_rows * kPairStride);
-    const int img = blockIdx.y, c = blockIdx.x, tid = threadIdx.x;
-    const int w = tid >> 6, nw = blockDim.x >> 6, ln = lane_id();
+    uint16_t* list = (uint16_t*)(fsm + 2 * max_rows * kPairStride + ((max_rows - 4) * max_cols + 1) / 2);
+    const int kmax = max_rows * max_cols / 4 + 32;           // >= strict-NMS bound ceil(wd/2)*ceil(hd/2)
+    uint16_t* kini = list + ((max_rows * max_cols / 2 + 65) & ~1);
+    uint16_t* kmin = kini + kmax;
+    __shared__ int nsurv, nki, nkm;
+    const int img = blockIdx.y, tid = threadIdx.x;
+    const int w = tid >> 6, ln = lane_id();
+    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
+    const int tp = min(T1, T2);
+    const int c = blockIdx.x;
     const CellDev cd = cells[c];
-    const LevelDev L = levels[cd.level];
-    int lstride;
-    const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
     const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
-    if (Wd <= 0 || Hd <= 0) {
-        if (tid == 0) cell_cnt[(size_t)img * ncells + c] = 0;
-        return;
-    }
-    // 1. every ROI byte loaded once (lane = column, one wave per row, all loads issued before the first
-    //    wait) and stored twice as u16: E at column q, O at column q - 1
+    const bool live = Wd > 0 && Hd > 0;                           // workgroup-uniform
     const int SW = (Wd + 5) & ~1;        // int16 per score-map row (even: rows stay dword aligned)
     {
-        constexpr int kRowsPerWave = kMaxRoi / 4;
+        // 1. every ROI byte loaded once (lane = column, one wave per row, all loads issued before the first
+        //    wait) and stored twice as u16: E at column q, O at column q - 1
+        const LevelDev L = levels[cd.level];
+        int lstride;
+        const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
+        const uint8_t* src0 = base + (size_t)cd.y0 * lstride + cd.x0;
         uint16_t* E16 = (uint16_t*)E;
         uint16_t* O16 = (uint16_t*)O;
-        const uint8_t* src0 = base + (size_t)cd.y0 * lstride + cd.x0;
-        for (int q0 = 0; q0 < W + 2; q0 += kWave) {
+        for (int q0 = 0; live && q0 < W + 2; q0 += kWave) {
             const int q = q0 + ln, qc = min(q, W - 1);
-            uint32_t v[kRowsPerWave];
+            uint32_t v[kRoiRowsPerWave];
+            const int kr = (H - w + 3) >> 2;   // rows w, w+4, ... below H (wave-uniform)
 #pragma unroll
-            for (int k = 0; k < kRowsPerWave; ++k) v[k] = src0[(size_t)min(w + 4 * k, H - 1) * lstride + qc];
+            for (int k = 0; k < kRoiRowsPerWave; ++k) v[k] = k < kr ? src0[(size_t)(w + 4 * k) * lstride + qc] : 0;
 #pragma unroll
-            for (int k = 0; k < kRowsPerWave; ++k) {
+            for (int k = 0; k < kRoiRowsPerWave; ++k) {
                 const int r = w + 4 * k;
                 if (r < H && q < W + 2) {
                     const uint16_t b = q < W ? (uint16_t)v[k] : 0;
@@ -262,60 +288,93 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                 }
             }
         }
-    }
-    for (int i = tid; i < SW; i += blockDim.x) { sc[i] = -1; sc[(Hd + 1) * SW + i] = -1; }
-    for (int r = tid; r < Hd + 2; r += blockDim.x) { sc[r * SW + 1] = -1; sc[r * SW + Wd + 2] = -1; }
-    __syncthreads();
-    if (stop_after == 1) { if (tid == 0) cell_cnt[(size_t)img * ncells + c] = (int)(E[tid] & 0); return; }
-    // 2. scores, two pixels per lane: pair q -> det row rr, pixels x = 3 + 2j, x + 1 (ROI coords)
-    const int PR = (Wd + 1) >> 1, NP = Hd * PR;
-    // pair q = tid + 256*it -> (row rr, pair column j), walked incrementally (no per-iteration division)
-    const int rr0 = tid / PR, j0 = tid - rr0 * PR;
-    const int dq = (int)blockDim.x / PR, dj = (int)blockDim.x - dq * PR;
-    auto next = [&](int& rr, int& j) { rr += dq; j += dj; if (j >= PR) { j -= PR; ++rr; } };
-    for (int q = tid, rr = rr0, j = j0; q < NP; q += blockDim.x, next(rr, j)) {
-        const s16x2 s2 = fast_score2(E, O, rr + 3, j);
-        *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
-    }
-    __syncthreads();
-    if (stop_after == 2) { if (tid == 0) cell_cnt[(size_t)img * ncells + c] = sc[tid * 5] & 0; return; }
-    // 3. NMS at iniTh and minTh in one pass from 3 x 3 aligned dwords per pair; 4 flag bits per pair
-    //    iteration kept in a register
-    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
-    uint32_t flags = 0;
-    int it = 0;
-    for (int q = tid, rr = rr0, j = j0; q < NP; q += blockDim.x, ++it, next(rr, j))
-        flags |= (uint32_t)nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd) << (4 * it);
-    const int any_ini = __syncthreads_or((flags & 0x33333333u) != 0);
-    const int sel = any_ini ? 0 : 2;          // cell empty at iniTh -> minTh (:812-816)
-    if (stop_after == 3) { if (tid == 0) cell_cnt[(size_t)img * ncells + c] = (int)(flags & 0); return; }
-    // 4. row-major compaction (OpenCV's output order) into the cell's slots
-    uint32_t* oxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
-    uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
-    int running = 0;
-    it = 0;
-    int rr = rr0, j = j0;
-    for (int b = 0; b < NP; b += blockDim.x, ++it, next(rr, j)) {
-        const int q = b + tid;
-        const bool f0 = q < NP && ((flags >> (4 * it + sel)) & 1u);
-        const bool f1 = q < NP && ((flags >> (4 * it + sel + 1)) & 1u);
-        const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
-        if (ln == 0) red[w] = __popcll(m0) + __popcll(m1);
-        __syncthreads();
-        int before = running, tot = 0;
-        for (int k = 0; k < nw; ++k) { before += (k < w) ? red[k] : 0; tot += red[k]; }
-        if (f0 || f1) {
-            const int16_t* cp = sc + (rr + 1) * SW + 2 + 2 * j;
-            int pos = before + lanes_below(m0) + lanes_below(m1);
-            const uint32_t yv = (uint32_t)(cd.y0 + rr + 3) << 16;
-            if (f0 && pos < cd.slot_cap) { oxy[pos] = (uint32_t)(cd.x0 + 3 + 2 * j) | yv; os[pos] = (uint8_t)cp[0]; }
-            pos += f0 ? 1 : 0;
-            if (f1 && pos < cd.slot_cap) { oxy[pos] = (uint32_t)(cd.x0 + 4 + 2 * j) | yv; os[pos] = (uint8_t)cp[1]; }
+        if (live) {
+            for (int i = tid; i < SW; i += blockDim.x) { sc[i] = -1; sc[(Hd + 1) * SW + i] = -1; }
+            for (int r = tid; r < Hd + 2; r += blockDim.x) { sc[r * SW + 1] = -1; sc[r * SW + Wd + 2] = -1; }
         }
-        running += tot;
+        if (tid == 0) { nsurv = 0; nki = 0; nkm = 0; }
         __syncthreads();
     }
-    if (tid == 0) cell_cnt[(size_t)img * ncells + c] = min(running, cd.slot_cap);
+    {
+        int count = 0;
+        if (live && stop_after != 1) {
+            // 2. compass pre-test for every pixel pair at tp = min(T1, T2); the score map gets 0 (< tp: never
+            //    kept, never blocks) and the surviving pairs go to an LDS list (order irrelevant)
+            const int PR = (Wd + 1) >> 1, NP = Hd * PR;
+            // pair q = tid + 256*it -> (row rr, pair column j), walked incrementally (no division per step)
+            const int rr0 = tid / PR, j0 = tid - rr0 * PR;
+            const int dq = (int)blockDim.x / PR, dj = (int)blockDim.x - dq * PR;
+            for (int q = tid, rr = rr0, j = j0; q < NP; q += blockDim.x) {
+                const bool two = 2 * j + 1 < Wd;
+                const int pt = fast_pretest2(E, O, rr + 3, j, tp) & (two ? 3 : 1);
+                *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
+                const uint64_t bm = __ballot(pt != 0);
+                int wbase = 0;
+                if (ln == 0 && bm) wbase = atomicAdd(&nsurv, __popcll(bm));
+                wbase = __shfl(wbase, 0, kWave);
+                if (pt) list[wbase + lanes_below(bm)] = (uint16_t)((rr << 8) | j);
+                rr += dq; j += dj;
+                if (j >= PR) { j -= PR; ++rr; }
+            }
+            __syncthreads();
+            const int ns = nsurv;
+            if (stop_after != 2) {
+                // 3. full closed-form scores of the surviving pairs only
+                for (int i = tid; i < ns; i += blockDim.x) {
+                    const int rr = list[i] >> 8, j = list[i] & 0xff;
+                    const s16x2 s2 = fast_score2(E, O, rr + 3, j);
+                    *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
+                }
+                __syncthreads();
+                // 4. NMS at iniTh and minTh in one pass from 3 x 3 aligned dwords per surviving pair (other
+                //    pairs have s < tp and keep nothing); kept pixels of each threshold appended to an LDS
+                //    key list (key = row * 128 + column: row-major order)
+                int any = 0;
+                for (int i0 = 0; i0 < ns; i0 += blockDim.x) {
+                    const int i = i0 + tid;
+                    int f = 0, key = 0;
+                    if (i < ns) {
+                        const int rr = list[i] >> 8, j = list[i] & 0xff;
+                        f = nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd);
+                        key = rr * 128 + 2 * j;
+                    }
+                    any |= f;
+#pragma unroll
+                    for (int bit = 0; bit < 4; ++bit) {
+                        const bool on = (f >> bit) & 1;
+                        const uint64_t bm = __ballot(on);
+                        if (!bm) continue;
+                        int base = 0;
+                        if (ln == 0) base = atomicAdd(bit < 2 ? &nki : &nkm, __popcll(bm));
+                        base = __shfl(base, 0, kWave);
+                        const int pos = base + lanes_below(bm);
+                        if (on && pos < kmax) (bit < 2 ? kini : kmin)[pos] = (uint16_t)(key + (bit & 1));
+                    }
+                }
+                const int any_ini = __syncthreads_or((any & 3) != 0);
+                if (stop_after != 3) {
+                    // 5. cell empty at iniTh -> minTh (:812-816); output in OpenCV's row-major order: each
+                    //    kept pixel's slot is its rank among the cell's keys (few per cell)
+                    const uint16_t* keys = any_ini ? kini : kmin;
+                    const int nk = min(any_ini ? nki : nkm, kmax);
+                    uint32_t* oxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
+                    uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
+                    for (int i = tid; i < nk; i += blockDim.x) {
+                        const int k = keys[i];
+                        int rank = 0;
+                        for (int m = 0; m < nk; ++m) rank += keys[m] < k;
+                        if (rank < cd.slot_cap) {
+                            const int rr = k >> 7, x = k & 127;
+                            oxy[rank] = (uint32_t)(cd.x0 + 3 + x) | ((uint32_t)(cd.y0 + rr + 3) << 16);
+                            os[rank] = (uint8_t)sc[(rr + 1) * SW + 2 + x];
+                        }
+                    }
+                    count = min(nk, cd.slot_cap);
+                }
+            }
+        }
+        if (tid == 0) cell_cnt[(size_t)img * ncells + c] = count;
+    }
 }
 
 // GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, integer separable path: taps {18,34,49,55,49,34,18},
@@ -989,7 +1048,10 @@ void Extractor::free_buffers() {
 
 static size_t qt_lds_bytes(int cap, int scan_cap);
 static size_t fast_lds_bytes(const Extractor* e) {
-    return (size_t)2 * e->cell_max_rows * kPairStride * 4 + (size_t)(e->cell_max_rows - 4) * (e->cell_max_cols) * 2 + 16;
+    // E + O pair images, int16 score map, u16 survivor list and two u16 kept-pixel key lists
+    const size_t R = e->cell_max_rows, Cc = e->cell_max_cols;
+    return 2 * R * kPairStride * 4 + 4 * (((R - 4) * Cc + 1) / 2) + 2 * ((R * Cc / 2 + 65) & ~(size_t)1) +
+           2 * 2 * (R * Cc / 4 + 32);
 }
 
 template <typename T>
@@ -1200,7 +1262,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         dim3 g(ncells, batch);
         hipLaunchKernelGGL(k_fast_cells, g, dim3(256), fast_lds_bytes(e), s, e->d_pyr, ps, e->d_levels, e->d_cells, e->iniTh, e->minTh,
                            e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, e->fast_stop_after, s0,
-                           e->cell_max_rows);
+                           e->cell_max_rows, e->cell_max_cols);
     }
     mark(2);
     {

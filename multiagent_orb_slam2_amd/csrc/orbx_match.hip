@@ -185,8 +185,7 @@ __global__ __launch_bounds__(256) void k_stereo(StereoArgs A) {
             best = min(best, key);
         }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+    best = wave_min_u32(best);
     if (ln == 0) {
         int d = (best == 0xffffffffu) ? kThHigh : (int)(best >> 20);
         d = min(d, kThHigh);                                                // init TH_HIGH, strict < (:522-547)
@@ -219,17 +218,14 @@ __device__ __forceinline__ int rot_bin(float a1, float a2) {   // src/ORBmatcher
 }
 
 // best (lowest position on ties) and multiset-second over one wave's candidates; values 256 = none
+// best distance, its (first) position, and the second-best distance of one value per lane, with the
+// reference's sequential update rule (ties for the best count as second).  Wave-uniform results.
 __device__ __forceinline__ void wave_best2(int d, int pos, int& b1, int& bpos, int& b2) {
-    uint32_t key = ((uint32_t)d << 20) | (uint32_t)pos;
-    uint32_t m = key;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, kWave));
+    const uint32_t key = ((uint32_t)d << 20) | (uint32_t)pos;
+    const uint32_t m = wave_min_u32(key);
     b1 = (int)(m >> 20);
     bpos = (int)(m & 0xfffff);
-    int s = (key == m) ? 256 : d;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s = min(s, __shfl_xor(s, o, kWave));
-    b2 = s;
+    b2 = (int)wave_min_u32((key == m) ? 256u : (uint32_t)d);
 }
 
 struct BowArgs {
@@ -248,72 +244,122 @@ struct BowArgs {
 };
 
 // One FeatureVector node of view 1 against the same node of view 2 (merge-join of :547-634 by binary
-// search), queries in node order with lanes over the candidates; the greedy "already matched" flags are
-// node-local (a feature belongs to exactly one node) and live in LDS.
-__device__ void bow_node(const BowArgs& A, int a, uint8_t* taken) {
+// search): queries in node order, lanes over the candidates.  Candidate descriptors of the first kBowRegChunks
+// 64-wide chunks stay in registers for the whole node, so the sequential (greedy) query loop only loads the
+// wave-uniform query descriptor; the "already matched" flags (vbMatched2 / vpMapPointMatches, node-local
+// because a feature belongs to exactly one node) are one bit per (lane, chunk) in a register.
+constexpr int kBowRegChunks = 2;
+
+// Position of node id in a FeatureVector's ascending node list, or -1: 64 ids per load round and a ballot
+// instead of a chain of dependent binary-search loads.
+__device__ __forceinline__ int fv_find_wave(const FvDev& f, uint32_t id) {
+    for (int base = 0; base < f.n; base += kWave) {
+        const int k = base + lane_id();
+        const uint32_t v = k < f.n ? f.node[k] : 0xffffffffu;
+        const uint64_t hit = __ballot(v == id);
+        if (hit) return base + (int)__builtin_ctzll(hit);
+        if (__builtin_amdgcn_readlane((int)(v >= id), kWave - 1)) return -1;   // ids ascending: passed it
+    }
+    return -1;
+}
+
+__device__ void bow_node(const BowArgs& A, int a) {
     const int ln = lane_id();
     const uint32_t id = A.f1.node[a];
-    const int b = fv_lower_bound(A.f2, id);
-    if (b >= A.f2.n || A.f2.node[b] != id) return;
+    const int b = fv_find_wave(A.f2, id);
+    if (b < 0) return;
     const int q0 = A.f1.off[a], q1 = A.f1.off[a + 1];
     const int c0 = A.f2.off[b], c1 = A.f2.off[b + 1];
     const int nc = min(c1 - c0, 4096);
-    for (int j = ln; j < nc; j += kWave) taken[j] = 0;
-    __syncthreads();
+    const int nch = (nc + kWave - 1) / kWave;
+    uint4 r0[kBowRegChunks], r1[kBowRegChunks];
+    bool rok[kBowRegChunks];
+#pragma unroll
+    for (int c = 0; c < kBowRegChunks; ++c) {
+        const int j = c * kWave + ln;
+        rok[c] = false;
+        r0[c] = r1[c] = make_uint4(0, 0, 0, 0);
+        if (j < nc) {
+            const int i2 = A.f2.idx[c0 + j];
+            rok[c] = A.kff ? true : (A.v2[i2] != 0);
+            if (rok[c]) load_desc(A.d2 + 32 * (size_t)i2, r0[c], r1[c]);
+        }
+    }
+    uint64_t taken = 0;   // bit c: candidate c*64 + lane already matched
     int local = 0;
-    for (int p = q0; p < q1; ++p) {
-        const int i1 = A.f1.idx[p];
-        if (!A.v1[i1]) continue;
-        uint4 x0, x1;
-        load_desc(A.d1 + 32 * (size_t)i1, x0, x1);
-        int b1 = 256, bp = 0xfffff, b2 = 256;
-        for (int base = 0; base < nc; base += kWave) {
-            const int j = base + ln;
-            int d = 256;
-            if (j < nc) {
-                const int i2 = A.f2.idx[c0 + j];
-                const bool ok = A.kff ? !taken[j] : (!taken[j] && A.v2[i2]);
-                if (ok) {
-                    uint4 y0, y1;
-                    load_desc(A.d2 + 32 * (size_t)i2, y0, y1);
-                    d = hamming256(x0, x1, y0, y1);
+    for (int qb = q0; qb < q1; qb += kWave) {
+        // 64 queries at a time: lane k holds query qb+k (index, MapPoint flag, descriptor); the sequential
+        // greedy loop below reads them with v_readlane, so it issues no memory loads of its own
+        const int nq = min(kWave, q1 - qb);
+        int qi = 0, qv = 0;
+        uint4 qx0 = make_uint4(0, 0, 0, 0), qx1 = qx0;
+        if (ln < nq) {
+            qi = A.f1.idx[qb + ln];
+            qv = A.v1[qi] != 0;
+            if (qv) load_desc(A.d1 + 32 * (size_t)qi, qx0, qx1);
+        }
+        for (int k = 0; k < nq; ++k) {
+            if (!__builtin_amdgcn_readlane(qv, k)) continue;
+            const int i1 = __builtin_amdgcn_readlane(qi, k);
+            uint4 x0, x1;
+            x0.x = __builtin_amdgcn_readlane(qx0.x, k); x0.y = __builtin_amdgcn_readlane(qx0.y, k);
+            x0.z = __builtin_amdgcn_readlane(qx0.z, k); x0.w = __builtin_amdgcn_readlane(qx0.w, k);
+            x1.x = __builtin_amdgcn_readlane(qx1.x, k); x1.y = __builtin_amdgcn_readlane(qx1.y, k);
+            x1.z = __builtin_amdgcn_readlane(qx1.z, k); x1.w = __builtin_amdgcn_readlane(qx1.w, k);
+            int b1 = 256, bp = 0xfffff, b2 = 256;
+            auto merge = [&](int d, int j) {   // chunks in candidate order
+                int cb1, cbp, cb2;
+                wave_best2(d, j < nc ? j : 0xfffff, cb1, cbp, cb2);
+                if (cb1 < b1) { b2 = min(b1, cb2); b1 = cb1; bp = cbp; }
+                else { b2 = min(b2, min(cb1, cb2)); }
+            };
+#pragma unroll
+            for (int c = 0; c < kBowRegChunks; ++c) {
+                if (c < nch) {
+                    const int j = c * kWave + ln;
+                    const int d = (rok[c] && !((taken >> c) & 1)) ? hamming256(x0, x1, r0[c], r1[c]) : 256;
+                    merge(d, j);
                 }
             }
-            int cb1, cbp, cb2;
-            wave_best2(d, j < nc ? j : 0xfffff, cb1, cbp, cb2);
-            // merge chunk result with the running one (chunks in candidate order)
-            if (cb1 < b1) { b2 = min(b1, cb2); b1 = cb1; bp = cbp; }
-            else { b2 = min(b2, min(cb1, cb2)); }
-        }
-        const bool pass = A.kff ? (b1 <= kThLow) : (b1 < kThLow);          // :230 vs :600
-        if (pass && (float)b1 < A.nnratio * (float)b2) {
-            const int i2 = A.f2.idx[c0 + bp];
-            if (ln == 0) {
-                taken[bp] = 1;
-                const int ridx = A.kff ? i2 : i1;
-                A.match[ridx] = A.kff ? i1 : i2;
-                if (A.checkOri) {
-                    const int bn = rot_bin(A.a1[(size_t)i1 * A.as1], A.a2[(size_t)i2 * A.as2]);
-                    A.bin[ridx] = bn;
-                    atomicAdd(&A.hist[bn], 1);
+            for (int c = kBowRegChunks; c < nch; ++c) {   // large nodes: the remaining chunks from memory
+                const int j = c * kWave + ln;
+                int d = 256;
+                if (j < nc && !((taken >> c) & 1)) {
+                    const int i2 = A.f2.idx[c0 + j];
+                    if (A.kff || A.v2[i2]) {
+                        uint4 y0, y1;
+                        load_desc(A.d2 + 32 * (size_t)i2, y0, y1);
+                        d = hamming256(x0, x1, y0, y1);
+                    }
                 }
+                merge(d, j);
             }
-            ++local;
+            const bool pass = A.kff ? (b1 <= kThLow) : (b1 < kThLow);          // :230 vs :600
+            if (pass && (float)b1 < A.nnratio * (float)b2) {
+                if (ln == (bp & (kWave - 1))) taken |= 1ull << (bp / kWave);
+                if (ln == 0) {
+                    const int i2 = A.f2.idx[c0 + bp];
+                    const int ridx = A.kff ? i2 : i1;
+                    A.match[ridx] = A.kff ? i1 : i2;
+                    if (A.checkOri) {
+                        const int bn = rot_bin(A.a1[(size_t)i1 * A.as1], A.a2[(size_t)i2 * A.as2]);
+                        A.bin[ridx] = bn;
+                        atomicAdd(&A.hist[bn], 1);
+                    }
+                }
+                ++local;
+            }
         }
-        __syncthreads();
     }
     if (ln == 0 && local) atomicAdd(A.nmatch, local);
 }
 
 // one wave per node of view 1
 __global__ __launch_bounds__(64) void k_bow(BowArgs A) {
-    __shared__ uint8_t taken[4096];
     if ((int)blockIdx.x >= A.f1.n) return;
-    bow_node(A, blockIdx.x, taken);
+    bow_node(A, blockIdx.x);
 }
 
-// Keyframe store on the device (extractor + vocabulary batch outputs, slot stride 'cap'): many
-// SearchByBoW(KF, KF) pairs in one launch -- MapFusion's cross-agent matches (src/MapFusion.cc:275, :849).
 template <typename T>
 __device__ __forceinline__ const T* slot_ptr(const T* base, size_t stride, int k) {
     return reinterpret_cast<const T*>(reinterpret_cast<const uint8_t*>(base) + (size_t)k * stride);
@@ -330,7 +376,6 @@ __device__ __forceinline__ FvDev store_fv(const orbx_kf_store& S, int k) {
 
 __global__ __launch_bounds__(64) void k_bow_pairs(orbx_kf_store S, const int32_t* __restrict__ pairs, float nnratio, int checkOri,
                                                   int32_t* match, int32_t* bin, int32_t* hist, int32_t* nmatch) {
-    __shared__ uint8_t taken[4096];
     const int pr = blockIdx.y;
     const int k1 = pairs[2 * pr], k2 = pairs[2 * pr + 1];
     BowArgs A;
@@ -343,7 +388,7 @@ __global__ __launch_bounds__(64) void k_bow_pairs(orbx_kf_store S, const int32_t
     A.nnratio = nnratio; A.checkOri = checkOri; A.kff = 0;
     A.match = match + (size_t)pr * S.capacity; A.bin = bin + (size_t)pr * S.capacity;
     A.hist = hist + (size_t)pr * 32; A.nmatch = nmatch + pr;
-    for (int a = blockIdx.x; a < A.f1.n; a += gridDim.x) bow_node(A, a, taken);   // grid.x is only a width hint
+    for (int a = blockIdx.x; a < A.f1.n; a += gridDim.x) bow_node(A, a);   // grid.x is only a width hint
 }
 
 struct TriArgs {
@@ -403,8 +448,7 @@ __global__ __launch_bounds__(64) void k_triangulate(TriArgs A) {
             const uint32_t key = ((uint32_t)(256 - d) << 20) | (uint32_t)(j - c0);
             bestkey = max(bestkey, key);
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) bestkey = max(bestkey, (uint32_t)__shfl_xor((int)bestkey, o, kWave));
+        bestkey = ~wave_min_u32(~bestkey);
         if (bestkey != 0) {
             const int i2 = A.f2.idx[c0 + (int)(bestkey & 0xfffff)];
             if (ln == 0) {

@@ -142,36 +142,64 @@ __global__ __launch_bounds__(kVocabAggThreads) void k_vocab_aggregate(const int3
     for (int i = tid; i < P2; i += T) flag[i] = (key[i] != ~0ull && (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32))) ? 1 : 0;
     __syncthreads();
     const int nwords = block_scan_array(flag, P2, tmp);
-    for (int i = tid; i < nv; i += T) {
+    // per word: its weight accumulated in feature order (addWeight: one += per further occurrence), kept in
+    // registers until every thread is done reading key[], then written over key[] as doubles
+    constexpr int kPer = kVocabMaxSet / kVocabAggThreads;
+    double myv[kPer];
+    int myslot[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+        const int i = tid + r * T;
+        myslot[r] = -1;
+        if (i >= nv) continue;
         const bool start = (i == 0) || (key[i] >> 32) != (key[i - 1] >> 32);
         if (!start) continue;
         const double w = wgt[o + (key[i] & 0xffffffffu)];
         double v = w;
-        if (weighting == W_TF_IDF || weighting == W_TF) {       // addWeight: one += per further occurrence
+        if (weighting == W_TF_IDF || weighting == W_TF) {
             for (int k = i + 1; k < nv && (key[k] >> 32) == (key[i] >> 32); ++k) v += w;
         }                                                        // IDF / BINARY: addIfNotExist keeps w
         out.words[o + flag[i]] = (uint32_t)(key[i] >> 32);
-        out.values[o + flag[i]] = v;
+        myv[r] = v;
+        myslot[r] = flag[i];
     }
     __syncthreads();
+    double* vals = reinterpret_cast<double*>(key);
+#pragma unroll
+    for (int r = 0; r < kPer; ++r)
+        if (myslot[r] >= 0) vals[myslot[r]] = myv[r];
+    __syncthreads();
+    // BowVector::normalize: the norm is a sequential sum in word order (bit-exact), read from LDS
+    __shared__ double norm_sh;
     if (tid == 0) {
-        out.n_words[img] = nwords;
-        // normalisation (BowVector::normalize): L1 when scoring is L1; TF/TF_IDF without normalisation
-        // divide by the number of words instead (:1160-1166)
-        double* vals = out.values + o;
-        const bool must = true;   // L1 / L2 scoring objects both normalise (ScoringObject mustNormalize)
-        if (must) {
-            double norm = 0.0;
-            if (scoring == S_L1) {
-                for (int k = 0; k < nwords; ++k) norm += fabs(vals[k]);
-            } else {
-                for (int k = 0; k < nwords; ++k) norm += vals[k] * vals[k];
-                norm = sqrt(norm);
+        double norm = 0.0;
+        int k = 0;
+        if (scoring == S_L1) {
+            for (; k + 8 <= nwords; k += 8) {
+                double x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = vals[k + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) norm += fabs(x[u]);
             }
-            if (norm > 0.0)
-                for (int k = 0; k < nwords; ++k) vals[k] /= norm;
+            for (; k < nwords; ++k) norm += fabs(vals[k]);
+        } else {
+            for (; k + 8 <= nwords; k += 8) {
+                double x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = vals[k + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) norm += x[u] * x[u];
+            }
+            for (; k < nwords; ++k) norm += vals[k] * vals[k];
+            norm = sqrt(norm);
         }
+        norm_sh = norm;
+        out.n_words[img] = nwords;
     }
+    __syncthreads();
+    const double norm = norm_sh;
+    for (int k = tid; k < nwords; k += T) out.values[o + k] = norm > 0.0 ? vals[k] / norm : vals[k];
 }
 
 struct Vocab {

@@ -33,6 +33,20 @@ def score_map(img: np.ndarray) -> np.ndarray:
     return out
 
 
+def pretest_map(img: np.ndarray, t: int) -> np.ndarray:
+    """k_fast_cells' compass pre-test: True where max over compass pairs (0,4),(4,8),(8,12),(12,0) of
+    min(d_k, d_k+4) > t, or min of max < -t (a necessary condition for 'corner at t')."""
+    h, w = img.shape
+    I = img.astype(np.int32)
+    v = I[3:h - 3, 3:w - 3]
+    d = [v - I[3 + dy:h - 3 + dy, 3 + dx:w - 3 + dx] for dx, dy in (CIRCLE[0], CIRCLE[4], CIRCLE[8], CIRCLE[12])]
+    dk = np.max([np.minimum(d[k], d[(k + 1) % 4]) for k in range(4)], axis=0)
+    br = np.min([np.maximum(d[k], d[(k + 1) % 4]) for k in range(4)], axis=0)
+    out = np.zeros((h, w), bool)
+    out[3:h - 3, 3:w - 3] = np.maximum(dk, -br) > t
+    return out
+
+
 def cells_of_level(h: int, w: int):
     """ComputeKeyPointsOctTree cell grid (src/ORBextractor.cc:773-807): list of (x0, y0, x1, y1, i, j)."""
     minB, maxBX, maxBY = 16, w - 16, h - 16
@@ -65,13 +79,16 @@ def fast_candidates(level: np.ndarray, ini_th=20, min_th=7):
     out = []
     for (x0, y0, x1, y1, i, j) in cells:
         roi = level[y0:y1, x0:x1]
-        s = score_map(roi)
         H, W = roi.shape
-        det = np.zeros_like(s, bool)
+        det = np.zeros((H, W), bool)
         det[3:H - 3, 3:W - 3] = True
-        for t in (ini_th, min_th):
-            m = np.where(det & (s >= t), s, 0)
-            pad = np.pad(m, 1)
+        T1, T2 = max(min(max(ini_th, 0), 255), 1), max(min(max(min_th, 0), 255), 1)
+        # kernel form: exact scores only where the compass pre-test at min(T1, T2) passes, 0 elsewhere;
+        # NMS against the raw 8 neighbours (-1 outside the detection window)
+        s = np.where(pretest_map(roi, min(T1, T2)), score_map(roi), 0)
+        s = np.where(det, s, -1)
+        for t in (T1, T2):
+            pad = np.pad(s, 1, constant_values=-1)
             keep = det & (s >= t)
             for dy in (-1, 0, 1):
                 for dx in (-1, 0, 1):
