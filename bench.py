@@ -50,11 +50,6 @@ def parse():
     return ap.parse_args()
 
 
-def level_pixels():
-    from multiagent_orb_slam2_amd.orbx import load_library  # noqa: F401  (geometry comes from the extractor)
-    return None
-
-
 def algorithmic_bytes(ex, mean_cand, mean_kps):
     """Compulsory HBM bytes per image for each stage."""
     sizes = ex.level_sizes(ROWS, COLS)

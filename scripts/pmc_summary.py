@@ -15,8 +15,10 @@ import os
 import shutil
 import sys
 
+R1A_CALIBRATION = 1.3265335392964581
 STAGE_OF = {"k_copy_level0": "copy_level0", "k_resize": "resize", "k_fast_cells": "fast_cells", "k_blur7": "blur7",
-            "k_quadtree": "quadtree", "k_describe": "describe", "k_stereo": "stereo_match"}
+            "k_quadtree": "quadtree", "k_describe": "describe", "k_stereo": "stereo_match",
+            "k_stereo_sad": "stereo_refine", "k_bow_pairs": "keyframe_bow_fusion"}
 
 
 def short(name):
@@ -40,8 +42,12 @@ def main():
     shutil.copy(os.path.join(prof, "kt", "run_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
     fetch = per_kernel(os.path.join(prof, "fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(prof, "write", "run_counter_collection.csv"))
-    known_read = batch * rows * cols
-    calib = known_read / (fetch["k_copy_level0"] * 1024.0)
+    if "k_copy_level0" in fetch:
+        calib = batch * rows * cols / (fetch["k_copy_level0"] * 1024.0)
+    else:
+        # level 0 is now read in place (no copy kernel): reuse the factor measured on k_copy_level0 in r1a
+        # (profiles/r1a_pmc_summary.json), the same byte-load pattern
+        calib = R1A_CALIBRATION
     stats = {}
     for r in csv.DictReader(open(os.path.join(prof, "kt", "run_kernel_stats.csv"))):
         stats[short(r["Name"])] = dict(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]), pct=float(r["Percentage"]))
