@@ -110,6 +110,18 @@ __device__ __forceinline__ int block_scan_array(int* a, int n, int* tmp) {
     return total;
 }
 
+// XCD-aware block -> work-item mapping.  Workgroups are dealt round-robin to the 8 XCDs (blocks b and
+// b + 8 share one XCD and its 4 MiB L2; MI355X_MICROARCH.md, workgroup dispatch), so with a 1-D grid of
+// 8 * chunk blocks XCD x gets the contiguous items [x * chunk, (x + 1) * chunk) in dispatch order:
+// neighbouring items (adjacent cells, keypoints of one image) share one L2 instead of being fetched by
+// all eight.  Placement is used for speed only; correctness never depends on it.
+constexpr int kXcds = 8;
+__host__ __device__ __forceinline__ int xcd_chunk(int total) { return (total + kXcds - 1) / kXcds; }
+__device__ __forceinline__ int xcd_item(int chunk) {
+    const int b = (int)blockIdx.x;
+    return (b % kXcds) * chunk + b / kXcds;
+}
+
 __device__ __forceinline__ int popc32(uint32_t v) { return __builtin_popcount(v); }
 
 // 256-bit Hamming distance (ORBmatcher::DescriptorDistance, src/ORBmatcher.cc:1649-1665): the

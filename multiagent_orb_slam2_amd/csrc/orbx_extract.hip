@@ -127,6 +127,84 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
     pyr[img * pyr_stride + dst_off + (size_t)y * dw + x] = (uint8_t)v;
 }
 
+// Vectorised form of the same arithmetic: one wave per (image, 8-row band, 256-column strip); lane l owns
+// the 4 output columns of group g = strip*64 + l.  The source bytes of a group's 8 taps lie in an 8-byte
+// window at column xb[g] (the host checks the span), so per source row a lane issues one 8-byte load, and
+// per column one v_perm_b32 (selector sel[g][k] = left and right tap offsets, as u16 lanes) and one
+// v_dot2_u32_u16 with the packed taps (a0 | a1 << 16) give the horizontal value exactly.  The row's
+// vertical taps are wave-uniform (scalar loads); the 4 output bytes leave as one dword store.
+constexpr int kResizeBand = 8, kResizeStrip = 256;
+struct ResizeVec {       // per level >= 1 with every group's span <= 8 bytes
+    const int* xb;       // [groups]
+    const uint4* sel;    // [groups] perm selectors of the 4 columns
+    const uint4* coef;   // [groups] a0 | a1 << 16 of the 4 columns
+    const int4* yrow;    // [h] y0, y1, b0, b1
+    int groups;
+};
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void resize_window(const uint8_t* __restrict__ row, int xb, int sw, bool fast, uint32_t& lo,
+                                              uint32_t& hi) {
+    if (fast) {
+        uint32_t v[2];
+        __builtin_memcpy(v, row + xb, 8);
+        lo = v[0]; hi = v[1];
+    } else {                      // window reaches past the row end: only bytes inside the row are ever selected
+        uint32_t v[2] = {0, 0};
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (xb + i < sw) v[i >> 2] |= (uint32_t)row[xb + i] << (8 * (i & 3));
+        lo = v[0]; hi = v[1];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
+                                                 size_t src_step, size_t src_istride, int sw, int dst_off, int dw, int dh,
+                                                 ResizeVec t, int nstrips, int nbands, int batch) {
+    const int nwaves = nstrips * nbands * batch;
+    const int nwg = (nwaves + 3) / 4;
+    const int wg = xcd_item(xcd_chunk(nwg));
+    const int wv = wg * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (wg >= nwg || wv >= nwaves) return;
+    const int img = wv / (nstrips * nbands);
+    const int rem = wv - img * nstrips * nbands;
+    const int band = rem / nstrips, strip = rem - band * nstrips;
+    const int g = strip * (kResizeStrip / 4) + lane_id();
+    if (g >= t.groups) return;
+    const int xb = t.xb[g];
+    const uint4 sel = t.sel[g], coef = t.coef[g];
+    const bool fast = xb + 8 <= sw;
+    const int x = 4 * g;
+    const bool full = x + 4 <= dw;
+    const uint8_t* S = src + img * src_istride;
+    uint8_t* D = pyr + img * pyr_stride + dst_off;
+    const int y1 = min((band + 1) * kResizeBand, dh);
+    for (int y = band * kResizeBand; y < y1; ++y) {
+        const int4 yr = t.yrow[y];
+        uint32_t l0, h0, l1, h1;
+        resize_window(S + (size_t)yr.x * src_step, xb, sw, fast, l0, h0);
+        resize_window(S + (size_t)yr.y * src_step, xb, sw, fast, l1, h1);
+        const uint32_t sl[4] = {sel.x, sel.y, sel.z, sel.w}, cf[4] = {coef.x, coef.y, coef.z, coef.w};
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u16x2 c = __builtin_bit_cast(u16x2, cf[k]);
+            const uint32_t hv0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(h0, l0, sl[k])), c, 0u, false);
+            const uint32_t hv1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(h1, l1, sl[k])), c, 0u, false);
+            const uint32_t v = min((hv0 * (uint32_t)yr.z + hv1 * (uint32_t)yr.w + (1u << 21)) >> 22, 255u);
+            packed |= v << (8 * k);
+        }
+        uint8_t* o = D + (size_t)y * dw + x;
+        if (full) {
+            __builtin_memcpy(o, &packed, 4);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (x + k < dw) o[k] = (uint8_t)(packed >> (8 * k));
+        }
+    }
+}
+
 // FAST-9/16 corner score in closed form.  For pixel value v and circle values p_k (Bresenham r=3,
 // OpenCV order), with d_k = v - p_k:  m_dark = max over the 16 arcs of 9 of min d, m_bright = max
 // over arcs of min(-d).  OpenCV's cornerScore<16> returns max(t, m_dark, m_bright) - 1 and the pixel
@@ -243,8 +321,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                                                     const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
                                                     int iniTh, int minTh, uint32_t* __restrict__ cand_xy,
                                                     uint8_t* __restrict__ cand_s, int cand_stride,
-                                                    int* __restrict__ cell_cnt, int ncells, int stop_after, Src0 s0,
-                                                    int max_rows, int max_cols) {
+                                                    int* __restrict__ cell_cnt, int ncells, int batch, int stop_after,
+                                                    Src0 s0, int max_rows, int max_cols) {
     extern __shared__ uint32_t fsm[];
     uint32_t* E = fsm;
     uint32_t* O = fsm + max_rows * kPairStride;
@@ -254,11 +332,12 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     uint16_t* kini = list + ((max_rows * max_cols / 2 + 65) & ~1);
     uint16_t* kmin = kini + kmax;
     __shared__ int nsurv, nki, nkm;
-    const int img = blockIdx.y, tid = threadIdx.x;
+    const int item = xcd_item(xcd_chunk(ncells * batch));    // (image, cell), cells of one image adjacent
+    if (item >= ncells * batch) return;                       // whole workgroup: no barrier is split
+    const int img = item / ncells, c = item - img * ncells, tid = threadIdx.x;
     const int w = tid >> 6, ln = lane_id();
     const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
     const int tp = min(T1, T2);
-    const int c = blockIdx.x;
     const CellDev cd = cells[c];
     const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
     const bool live = Wd > 0 && Hd > 0;                           // workgroup-uniform
@@ -391,27 +470,62 @@ __device__ __forceinline__ int refl101(int i, int n) {
 // output columns x0 = strip*256 + 4l .. x0+3, walks down the band's 38 input rows once, and keeps the
 // last 7 rows of horizontal sums in registers (a ring unrolled by 7, so no moves); no LDS, no
 // divisions.  Reflection only at the level borders (scalar for rows, per byte for edge lanes).
+// Per input row a lane issues one 12-byte load (x0-4 .. x0+7; global loads need no alignment on gfx950),
+// builds the 9 byte pairs (b[i], b[i+1]) with v_perm_b32 and forms the horizontal sums of its 4 columns
+// as two packed u16 pairs (v_pk_mad_u16: a row sum is at most 255 * 257 = 65535, exact in u16).  The
+// column pass widens to u32 and the 4 output bytes leave as one dword store.
 constexpr int kBlurBand = 32, kBlurStrip = 256;
 
-__device__ __forceinline__ void blur_hrow(const uint8_t* __restrict__ row, int x0, int w, bool interior, int h[4]) {
-    int b[10];
+// byte m of the 12-byte window (w0 | w1 << 32 | w2 << 64) and byte m+1, as u16 lanes (lo = m)
+template <int m>
+__device__ __forceinline__ u16x2 byte_pair(uint32_t w0, uint32_t w1, uint32_t w2) {
+    constexpr int q = m / 4, r = m % 4;
+    const uint32_t lo = q == 0 ? w0 : (q == 1 ? w1 : w2);
+    const uint32_t hi = q == 0 ? w1 : (q == 1 ? w2 : w2);
+    // v_perm_b32: selector byte k picks byte k' of {hi:lo} (0-3 lo, 4-7 hi); 0x0c gives 0
+    constexpr uint32_t sel = 0x0c000c00u | (uint32_t)r | ((uint32_t)(r + 1) << 16);
+    return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, sel));
+}
+
+struct BlurRow { u16x2 h01, h23; };   // horizontal sums of columns x0, x0+1 | x0+2, x0+3
+
+__device__ __forceinline__ BlurRow blur_hrow(const uint8_t* __restrict__ row, int x0, int w, bool interior) {
+    uint32_t w0, w1, w2;
     if (interior) {
-#pragma unroll
-        for (int i = 0; i < 10; ++i) b[i] = row[x0 - 3 + i];
+        uint32_t v[3];
+        __builtin_memcpy(v, row + x0 - 4, 12);
+        w0 = v[0]; w1 = v[1]; w2 = v[2];
     } else {
+        uint32_t v[3] = {0, 0, 0};
 #pragma unroll
-        for (int i = 0; i < 10; ++i) b[i] = row[refl101(x0 - 3 + i, w)];
+        for (int i = 1; i < 11; ++i) v[i >> 2] |= (uint32_t)row[refl101(x0 - 4 + i, w)] << (8 * (i & 3));
+        w0 = v[0]; w1 = v[1]; w2 = v[2];
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-        h[j] = 18 * (b[j] + b[j + 6]) + 34 * (b[j + 1] + b[j + 5]) + 49 * (b[j + 2] + b[j + 4]) + 55 * b[j + 3];
+    // b[i] = pixel x0 - 3 + i = window byte i + 1;  P_i = (b[i], b[i+1])
+    const u16x2 P0 = byte_pair<1>(w0, w1, w2), P1 = byte_pair<2>(w0, w1, w2), P2 = byte_pair<3>(w0, w1, w2);
+    const u16x2 P3 = byte_pair<4>(w0, w1, w2), P4 = byte_pair<5>(w0, w1, w2), P5 = byte_pair<6>(w0, w1, w2);
+    const u16x2 P6 = byte_pair<7>(w0, w1, w2), P7 = byte_pair<8>(w0, w1, w2), P8 = byte_pair<9>(w0, w1, w2);
+    const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
+    BlurRow o;
+    o.h01 = (P0 + P6) * k18 + (P1 + P5) * k34 + (P2 + P4) * k49 + P3 * k55;
+    o.h23 = (P2 + P8) * k18 + (P3 + P7) * k34 + (P4 + P6) * k49 + P5 * k55;
+    return o;
+}
+
+__device__ __forceinline__ uint32_t blur_col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t f,
+                                             uint32_t g) {
+    const uint32_t acc = 18u * (a + g) + 34u * (b + f) + 49u * (c + e) + 55u * d;
+    return min((acc + (1u << 15)) >> 16, 255u);
 }
 
 __global__ __launch_bounds__(256) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                size_t pyr_stride, const LevelDev* __restrict__ levels,
-                                               const BlurTile* __restrict__ tiles, int ntiles, Src0 s0) {
-    const int img = blockIdx.y;
-    const int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+                                               const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0) {
+    const int nbx = (ntiles + 3) / 4;                         // 4 tiles (waves) per workgroup
+    const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
+    if (item >= nbx * batch) return;
+    const int img = item / nbx;
+    const int t = (item - img * nbx) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (t >= ntiles) return;
     const BlurTile bt = tiles[t];
     const LevelDev L = levels[bt.level];
@@ -421,32 +535,41 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t* __restrict__ pyr, 
     const uint8_t* S = level_pixels(pyr, pyr_stride, L, bt.level, img, s0, sstride);
     uint8_t* D = blur + img * pyr_stride + L.pyr_off;
     const int y0 = bt.ty * kBlurBand, y1 = min(y0 + kBlurBand, L.h);
-    const bool interior = (x0 - 3 >= 0) && (x0 + 7 <= L.w);
-    int r0[4], r1[4], r2[4], r3[4], r4[4], r5[4], r6[4];
-#define ORBX_HROW(dst, yy) blur_hrow(S + (size_t)refl101((yy), L.h) * sstride, x0, L.w, interior, dst)
-    ORBX_HROW(r0, y0 - 3);
-    ORBX_HROW(r1, y0 - 2);
-    ORBX_HROW(r2, y0 - 1);
-    ORBX_HROW(r3, y0);
-    ORBX_HROW(r4, y0 + 1);
-    ORBX_HROW(r5, y0 + 2);
-    auto emit = [&](int y, const int* a, const int* b, const int* c, const int* d, const int* e, const int* f, const int* g) {
+    const bool interior = (x0 - 4 >= 0) && (x0 + 8 <= L.w);
+    const bool full = x0 + 4 <= L.w;
+    BlurRow r0, r1, r2, r3, r4, r5, r6;
+#define ORBX_HROW(yy) blur_hrow(S + (size_t)refl101((yy), L.h) * sstride, x0, L.w, interior)
+    r0 = ORBX_HROW(y0 - 3);
+    r1 = ORBX_HROW(y0 - 2);
+    r2 = ORBX_HROW(y0 - 1);
+    r3 = ORBX_HROW(y0);
+    r4 = ORBX_HROW(y0 + 1);
+    r5 = ORBX_HROW(y0 + 2);
+    auto emit = [&](int y, const BlurRow& a, const BlurRow& b, const BlurRow& c, const BlurRow& d, const BlurRow& e,
+                    const BlurRow& f, const BlurRow& g) {
+        const uint32_t o0 = blur_col(a.h01.x, b.h01.x, c.h01.x, d.h01.x, e.h01.x, f.h01.x, g.h01.x);
+        const uint32_t o1 = blur_col(a.h01.y, b.h01.y, c.h01.y, d.h01.y, e.h01.y, f.h01.y, g.h01.y);
+        const uint32_t o2 = blur_col(a.h23.x, b.h23.x, c.h23.x, d.h23.x, e.h23.x, f.h23.x, g.h23.x);
+        const uint32_t o3 = blur_col(a.h23.y, b.h23.y, c.h23.y, d.h23.y, e.h23.y, f.h23.y, g.h23.y);
+        const uint32_t packed = o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
         uint8_t* o = D + (size_t)y * L.w + x0;
+        if (full) {
+            __builtin_memcpy(o, &packed, 4);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int acc = 18 * (a[j] + g[j]) + 34 * (b[j] + f[j]) + 49 * (c[j] + e[j]) + 55 * d[j];
-            if (x0 + j < L.w) o[j] = (uint8_t)min(max((acc + (1 << 15)) >> 16, 0), 255);
+            for (int j = 0; j < 4; ++j)
+                if (x0 + j < L.w) o[j] = (uint8_t)(packed >> (8 * j));
         }
     };
     // ring of 7 row sums; each unrolled step loads row y+3 into the slot freed by row y-4
     for (int y = y0; y < y1; y += 7) {
-        ORBX_HROW(r6, y + 3); emit(y, r0, r1, r2, r3, r4, r5, r6); if (y + 1 >= y1) break;
-        ORBX_HROW(r0, y + 4); emit(y + 1, r1, r2, r3, r4, r5, r6, r0); if (y + 2 >= y1) break;
-        ORBX_HROW(r1, y + 5); emit(y + 2, r2, r3, r4, r5, r6, r0, r1); if (y + 3 >= y1) break;
-        ORBX_HROW(r2, y + 6); emit(y + 3, r3, r4, r5, r6, r0, r1, r2); if (y + 4 >= y1) break;
-        ORBX_HROW(r3, y + 7); emit(y + 4, r4, r5, r6, r0, r1, r2, r3); if (y + 5 >= y1) break;
-        ORBX_HROW(r4, y + 8); emit(y + 5, r5, r6, r0, r1, r2, r3, r4); if (y + 6 >= y1) break;
-        ORBX_HROW(r5, y + 9); emit(y + 6, r6, r0, r1, r2, r3, r4, r5);
+        r6 = ORBX_HROW(y + 3); emit(y, r0, r1, r2, r3, r4, r5, r6); if (y + 1 >= y1) break;
+        r0 = ORBX_HROW(y + 4); emit(y + 1, r1, r2, r3, r4, r5, r6, r0); if (y + 2 >= y1) break;
+        r1 = ORBX_HROW(y + 5); emit(y + 2, r2, r3, r4, r5, r6, r0, r1); if (y + 3 >= y1) break;
+        r2 = ORBX_HROW(y + 6); emit(y + 3, r3, r4, r5, r6, r0, r1, r2); if (y + 4 >= y1) break;
+        r3 = ORBX_HROW(y + 7); emit(y + 4, r4, r5, r6, r0, r1, r2, r3); if (y + 5 >= y1) break;
+        r4 = ORBX_HROW(y + 8); emit(y + 5, r5, r6, r0, r1, r2, r3, r4); if (y + 6 >= y1) break;
+        r5 = ORBX_HROW(y + 9); emit(y + 6, r6, r0, r1, r2, r3, r4, r5);
     }
 #undef ORBX_HROW
 }
@@ -818,9 +941,12 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                   const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
                                                   int out_stride, const int* __restrict__ level_cnt,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
-                                                  int capacity, int total_slots, Src0 s0) {
-    const int img = blockIdx.y;
-    const int slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+                                                  int capacity, int total_slots, int batch, Src0 s0) {
+    const int nbx = (total_slots + 3) / 4;                    // 4 slots (waves) per workgroup
+    const int item = xcd_item(xcd_chunk(nbx * batch));       // keypoints of one image on one XCD
+    if (item >= nbx * batch) return;
+    const int img = item / nbx;
+    const int slot = ((item - img * nbx) * blockDim.x + threadIdx.x) >> 6;
     const int ln = lane_id();
     if (slot >= total_slots) return;
     // slot -> (level, index)
@@ -948,6 +1074,7 @@ struct Extractor {
     CellDev* d_cells = nullptr;
     BlurTile* d_tiles = nullptr;
     std::vector<ResizeTab> rtab;
+    std::vector<ResizeVec> rvec;      // per level: vectorised tables (groups == 0 -> use rtab)
     std::vector<void*> rtab_mem;
     uint8_t* d_pyr = nullptr;
     uint8_t* d_blur = nullptr;
@@ -1042,6 +1169,7 @@ void Extractor::free_buffers() {
     for (void* p : rtab_mem) (void)hipFree(p);
     rtab_mem.clear();
     rtab.clear();
+    rvec.clear();
     rows = cols = max_batch = 0;
     in_bytes = 0;
 }
@@ -1166,6 +1294,7 @@ int Extractor::configure(int r, int c, int batch) {
 
     // ---- resize tables (pinned OpenCV 3.2 INTER_LINEAR fixed point), level l from level l-1
     rtab.assign(nlevels, ResizeTab{});
+    rvec.assign(nlevels, ResizeVec{});
     for (int l = 1; l < nlevels; ++l) {
         const int sw = lv[l - 1].w, sh = lv[l - 1].h, dw = lv[l].w, dh = lv[l].h;
         const double sxs = 1.0 / ((double)dw / sw), sys = 1.0 / ((double)dh / sh);
@@ -1206,6 +1335,37 @@ int Extractor::configure(int r, int c, int batch) {
         for (auto* v : {&hx0, &hx1, &ha0, &ha1, &hy0, &hy1, &hb0, &hb1}) host.insert(host.end(), v->begin(), v->end());
         ORBX_HIP(hipMemcpy(mem, host.data(), host.size() * sizeof(int), hipMemcpyHostToDevice));
         rtab[l] = t;
+        // vectorised tables: 4 columns per group, their taps inside an 8-byte window at xb
+        const int G = (dw + 3) / 4;
+        std::vector<int> vxb(G);
+        std::vector<uint32_t> vsel(4 * (size_t)G, 0), vcoef(4 * (size_t)G, 0);
+        bool fits = true;
+        for (int g = 0; g < G; ++g) {
+            vxb[g] = hx0[4 * g];
+            for (int k = 0; k < 4 && 4 * g + k < dw; ++k) {
+                const int x = 4 * g + k, oL = hx0[x] - vxb[g], oR = hx1[x] - vxb[g];
+                if (oL < 0 || oR < 0 || oL > 7 || oR > 7 || ha0[x] < 0 || ha1[x] < 0) fits = false;
+                vsel[4 * g + k] = (uint32_t)(oL & 7) | 0x0c00u | ((uint32_t)(oR & 7) << 16) | 0x0c000000u;
+                vcoef[4 * g + k] = (uint32_t)(ha0[x] & 0xffff) | ((uint32_t)(ha1[x] & 0xffff) << 16);
+            }
+        }
+        for (int y = 0; y < dh; ++y) if (hb0[y] < 0 || hb1[y] < 0) fits = false;
+        if (fits) {
+            uint8_t* vm;
+            const size_t bx = ((size_t)G * 4 + 15) & ~(size_t)15, bs = (size_t)G * 16, by = (size_t)dh * 16;
+            if ((st = dev_alloc(&vm, bx + 2 * bs + by))) return st;
+            rtab_mem.push_back(vm);
+            std::vector<int32_t> yr(4 * (size_t)dh);
+            for (int y = 0; y < dh; ++y) { yr[4 * y] = hy0[y]; yr[4 * y + 1] = hy1[y]; yr[4 * y + 2] = hb0[y]; yr[4 * y + 3] = hb1[y]; }
+            ORBX_HIP(hipMemcpy(vm, vxb.data(), (size_t)G * 4, hipMemcpyHostToDevice));
+            ORBX_HIP(hipMemcpy(vm + bx, vsel.data(), bs, hipMemcpyHostToDevice));
+            ORBX_HIP(hipMemcpy(vm + bx + bs, vcoef.data(), bs, hipMemcpyHostToDevice));
+            ORBX_HIP(hipMemcpy(vm + bx + 2 * bs, yr.data(), by, hipMemcpyHostToDevice));
+            ResizeVec rv;
+            rv.xb = (const int*)vm; rv.sel = (const uint4*)(vm + bx); rv.coef = (const uint4*)(vm + bx + bs);
+            rv.yrow = (const int4*)(vm + bx + 2 * bs); rv.groups = G;
+            rvec[l] = rv;
+        }
     }
 
     // ---- batch buffers (HBM): pyramid + blurred pyramid + candidates + quadtree scratch
@@ -1250,25 +1410,32 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     e->last_src0 = s0;
     mark(0);
     for (int l = 1; l < nl; ++l) {
-        dim3 g((e->lv[l].w + 255) / 256, e->lv[l].h, batch);
         const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
         const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
-        hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis, e->lv[l].pyr_off, e->lv[l].w,
-                           e->lv[l].h, e->rtab[l]);
+        const LevelDev& L = e->lv[l];
+        if (e->rvec[l].groups > 0) {
+            const int nstrips = (L.w + kResizeStrip - 1) / kResizeStrip, nbands = (L.h + kResizeBand - 1) / kResizeBand;
+            const int nwg = (nstrips * nbands * batch + 3) / 4;
+            hipLaunchKernelGGL(k_resize4, dim3(kXcds * xcd_chunk(nwg)), dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis,
+                               e->lv[l - 1].w, L.pyr_off, L.w, L.h, e->rvec[l], nstrips, nbands, batch);
+        } else {
+            dim3 g((L.w + 255) / 256, L.h, batch);
+            hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis, L.pyr_off, L.w, L.h, e->rtab[l]);
+        }
     }
     mark(1);
     const int ncells = (int)e->cellv.size();
     if (ncells > 0) {
-        dim3 g(ncells, batch);
+        dim3 g(kXcds * xcd_chunk(ncells * batch));
         hipLaunchKernelGGL(k_fast_cells, g, dim3(256), fast_lds_bytes(e), s, e->d_pyr, ps, e->d_levels, e->d_cells, e->iniTh, e->minTh,
-                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, e->fast_stop_after, s0,
-                           e->cell_max_rows, e->cell_max_cols);
+                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, batch, e->fast_stop_after,
+                           s0, e->cell_max_rows, e->cell_max_cols);
     }
     mark(2);
     {
         const int nt = (int)e->tilev.size();
-        dim3 g((nt + 3) / 4, batch);
-        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles, nt, s0);
+        dim3 g(kXcds * xcd_chunk((nt + 3) / 4 * batch));
+        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles, nt, batch, s0);
     }
     mark(3);
     {
@@ -1281,9 +1448,9 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     mark(4);
     {
         const int total_slots = e->out_stride;
-        dim3 g((total_slots * 64 + 255) / 256, batch);
+        dim3 g(kXcds * xcd_chunk((total_slots + 3) / 4 * batch));
         hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
-                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, total_slots, s0);
+                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, total_slots, batch, s0);
     }
     mark(5);
     ORBX_HIP(hipGetLastError());

@@ -126,6 +126,7 @@ struct StereoArgs {
     int32_t* row_start;     // [batch][rows + 1]  right keypoints bucketed by floor(y)
     int32_t* row_idx;       // [batch][capacity]
     int32_t* best_idx; int32_t* best_dist;
+    int batch, nbx;         // k_stereo: images, workgroups per image (XCD-aware 1-D grid)
 };
 
 // Counting sort of one image pair's right keypoints by row (the row table of Frame.cc:476-493, kept as
@@ -155,8 +156,10 @@ __global__ __launch_bounds__(1024) void k_stereo_rows(StereoArgs A) {
 }
 
 __global__ __launch_bounds__(256) void k_stereo(StereoArgs A) {
-    const int img = blockIdx.y;
-    const int iL = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int item = xcd_item(xcd_chunk(A.nbx * A.batch));   // left keypoints of one pair on one XCD
+    if (item >= A.nbx * A.batch) return;
+    const int img = item / A.nbx;
+    const int iL = ((item - img * A.nbx) * blockDim.x + threadIdx.x) >> 6;
     const int ln = lane_id();
     const int nl = A.nl ? A.nl[img] : A.nl_fixed;
     if (iL >= nl) return;
@@ -514,6 +517,7 @@ struct RefineArgs {
     int left_first, right_first;
     float bf, maxD;
     float* uright; float* depth; int32_t* sad;
+    int batch, nbx;         // k_stereo_sad: pairs, workgroups per pair (XCD-aware 1-D grid)
 };
 
 constexpr int kRefKp = 23;   // keypoints per 256-thread workgroup: 23 x 11 window shifts = 253 lanes
@@ -533,9 +537,11 @@ __device__ __forceinline__ const uint8_t* pyr_level(const orbx_pyramid& P, int i
 // disparity test) in float with the same operation order.
 __global__ __launch_bounds__(256) void k_stereo_sad(RefineArgs A) {
     __shared__ int dist[kRefKp][11];
-    const int img = blockIdx.y, t = threadIdx.x;
+    const int item = xcd_item(xcd_chunk(A.nbx * A.batch));   // keypoints of one pair on one XCD
+    if (item >= A.nbx * A.batch) return;
+    const int img = item / A.nbx, t = threadIdx.x;
     const int q = t / 11, inc = t % 11 - 5;
-    const int l = blockIdx.x * kRefKp + q;
+    const int l = (item - img * A.nbx) * kRefKp + q;
     if (q >= kRefKp || l >= A.capacity) return;          // whole keypoints only: no barrier below is split
     const int nl = A.nl ? A.nl[img] : A.nl_fixed;
     const size_t o = (size_t)img * A.capacity + l;
@@ -830,7 +836,9 @@ static int stereo_common(orbx_matcher* m, StereoArgs& A, const float* scale, int
 
 static int stereo_launch(StereoArgs& A, int batch, int nl_max, hipStream_t s) {
     hipLaunchKernelGGL(k_stereo_rows, dim3(batch), dim3(1024), (size_t)(A.rows + 1) * sizeof(int), s, A);
-    hipLaunchKernelGGL(k_stereo, dim3((nl_max * 64 + 255) / 256, batch), dim3(256), 0, s, A);
+    A.batch = batch;
+    A.nbx = (nl_max * 64 + 255) / 256;
+    hipLaunchKernelGGL(k_stereo, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }
@@ -905,7 +913,9 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
 }
 
 static int refine_launch(RefineArgs& A, int batch, hipStream_t s) {
-    hipLaunchKernelGGL(k_stereo_sad, dim3((A.capacity + kRefKp - 1) / kRefKp, batch), dim3(256), 0, s, A);
+    A.batch = batch;
+    A.nbx = (A.capacity + kRefKp - 1) / kRefKp;
+    hipLaunchKernelGGL(k_stereo_sad, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
     hipLaunchKernelGGL(k_stereo_median, dim3(batch), dim3(1024), 0, s, A);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
