@@ -57,6 +57,17 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return min(min(r0, r1), min(r2, r3));
 }
 
+// Wave-uniform sum by DPP inside each 16-lane row (no LDS traffic), then the four row sums as scalars.
+// Every lane must be active.
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);    // quad_perm 1,0,3,2
+    v += __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);    // quad_perm 2,3,0,1
+    v += __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false);   // row_mirror
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
+
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);

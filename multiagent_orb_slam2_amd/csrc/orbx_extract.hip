@@ -29,6 +29,7 @@
 
 #include "orbx_common.h"
 #include "orbx_pattern.h"
+#include "orbx_sincos.h"
 
 namespace orbx {
 
@@ -101,7 +102,7 @@ struct ResizeTab {       // per level >= 1, device arrays
     int* y0; int* y1; int* b0; int* b1;   // [h]
 };
 
-__constant__ signed char c_pattern[ORBX_PATTERN_TESTS * 4];
+__constant__ __attribute__((aligned(16))) signed char c_pattern[ORBX_PATTERN_TESTS * 4];
 // umax for HALF_PATCH_SIZE = 15 (ORBextractor ctor :454-469); the host recomputes it and checks equality
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
@@ -993,14 +994,15 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
             m01 += v * x;
         }
     }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
+    m10 = wave_sum_dpp(m10);
+    m01 = wave_sum_dpp(m01);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
 
     // --- computeOrbDescriptor (:108-147) on the blurred level
     const float toRad = (float)(M_PI / 180.f);
     const float ang = __fmul_rn(angle, toRad);
-    const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+    float a, b;
+    orbx_sincos_brief(ang, &a, &b);   // == (float)cos/sin((double)ang) for every possible ang (orbx_sincos.h)
     const uint8_t* B = blur + img * pyr_stride + L.pyr_off;
     const uint8_t* center = B + (size_t)cy * L.w + cx;
     const int step = L.w;
@@ -1008,11 +1010,11 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         const int t = g * 64 + ln;
-        const signed char* pp = c_pattern + 4 * t;
+        const uint32_t pw = reinterpret_cast<const uint32_t*>(c_pattern)[t];   // x0, y0, x1, y1 (signed bytes)
         int vals[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const float fx = (float)pp[2 * e], fy = (float)pp[2 * e + 1];
+            const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
             const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
             const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
             vals[e] = center[__float2int_rn(ry) * step + __float2int_rn(rx)];
