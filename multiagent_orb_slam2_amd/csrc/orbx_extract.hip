@@ -309,14 +309,31 @@ __device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, 
     return (g0 & (sv.x >= T1)) | ((g1 & (sv.y >= T1)) << 1) | ((g0 & (sv.x >= T2)) << 2) | ((g1 & (sv.y >= T2)) << 3);
 }
 
-// One workgroup per (cell, image).  Cell geometry from ComputeKeyPointsOctTree (:784-807); FAST on the
-// ROI detects rows/cols [3, dim-3) of the ROI, NMS compares against the 8 neighbours' scores inside the
-// ROI's detection window (0 outside), strict '>' (OpenCV FAST_t).  Empty at iniTh -> minTh (:812-816).
+// One workgroup per (image, cell) (XCD-aware order: the cells of one image share an L2).  Cell geometry from
+// ComputeKeyPointsOctTree (:784-807); FAST on the ROI detects rows/cols [3, dim-3) of the ROI, NMS compares
+// against the 8 neighbours' scores inside the ROI's detection window (0 outside), strict '>' (OpenCV
+// FAST_t).  Empty at iniTh -> minTh (:812-816).  (A persistent form -- each workgroup walking a range of
+// cells with the next ROI prefetched into registers -- measured 1.3x slower: fewer resident workgroups.)
 // Dynamic LDS: E and O pair images (max_rows x kPairStride dwords each) + padded int16 score map whose
 // pixel pairs are dword aligned (det column x at map column x + 2, pad ring at columns 1 and Wd + 2) +
-// survivor list + kept-pixel key lists.  (A multi-cell workgroup that prefetches the next ROI into
-// registers while processing the current one measured 1.6x slower: 153 VGPRs, 3 waves per SIMD.)
-constexpr int kRoiRowsPerWave = kMaxRoi / 4;
+// survivor list + kept-pixel key lists.
+constexpr int kFastPf = 6;        // row groups per wave held in flight (ROI <= 72 rows, chunks <= 19 per row)
+
+struct FastRoi {                  // lane mapping of one cell's ROI: lane -> (row in group, 4-column chunk)
+    int cpr, rpi, ngroups, rr, c;
+    bool lane_ok;
+};
+
+__device__ __forceinline__ FastRoi fast_roi(int W, int H, int ln) {
+    FastRoi f;
+    f.cpr = (W + 2 + 3) >> 2;
+    f.rpi = kWave / f.cpr;
+    f.ngroups = (H + f.rpi - 1) / f.rpi;
+    f.rr = ln / f.cpr;
+    f.c = ln - f.rr * f.cpr;
+    f.lane_ok = f.rr < f.rpi;
+    return f;
+}
 
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                     const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
@@ -333,49 +350,57 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     uint16_t* kini = list + ((max_rows * max_cols / 2 + 65) & ~1);
     uint16_t* kmin = kini + kmax;
     __shared__ int nsurv, nki, nkm;
+    const int tid = threadIdx.x, w = tid >> 6, ln = lane_id();
     const int item = xcd_item(xcd_chunk(ncells * batch));    // (image, cell), cells of one image adjacent
     if (item >= ncells * batch) return;                       // whole workgroup: no barrier is split
-    const int img = item / ncells, c = item - img * ncells, tid = threadIdx.x;
-    const int w = tid >> 6, ln = lane_id();
     const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
     const int tp = min(T1, T2);
-    const CellDev cd = cells[c];
-    const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
-    const bool live = Wd > 0 && Hd > 0;                           // workgroup-uniform
-    const int SW = (Wd + 5) & ~1;        // int16 per score-map row (even: rows stay dword aligned)
     {
-        // 1. every ROI byte loaded once (lane = column, one wave per row, all loads issued before the first
-        //    wait) and stored twice as u16: E at column q, O at column q - 1
-        const LevelDev L = levels[cd.level];
-        int lstride;
-        const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
-        const uint8_t* src0 = base + (size_t)cd.y0 * lstride + cd.x0;
-        uint16_t* E16 = (uint16_t*)E;
-        uint16_t* O16 = (uint16_t*)O;
-        for (int q0 = 0; live && q0 < W + 2; q0 += kWave) {
-            const int q = q0 + ln, qc = min(q, W - 1);
-            uint32_t v[kRoiRowsPerWave];
-            const int kr = (H - w + 3) >> 2;   // rows w, w+4, ... below H (wave-uniform)
+        const int img = item / ncells, c = item - img * ncells;
+        const CellDev cd = cells[c];
+        const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
+        const bool live = Wd > 0 && Hd > 0;                       // workgroup-uniform
+        const int SW = (Wd + 5) & ~1;        // int16 per score-map row (even: rows stay dword aligned)
+        {
+            // 1. ROI -> pair images: lanes are (row, 4-column chunk) pairs, one 8-byte load per lane and row
+            //    group (all issued before the first use), E[r][i] = (roi[2i], roi[2i+1]) and O[r][i] =
+            //    (roi[2i+1], roi[2i+2]) built with v_perm_b32 and stored as ds_write_b64; columns >= W read as 0
+            const LevelDev L = levels[cd.level];
+            int lstride;
+            const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
+            const FastRoi f = fast_roi(W, H, ln);
+            const uint8_t* src = base + (size_t)cd.y0 * lstride + cd.x0 + 4 * f.c;
+            uint32_t pf[2 * kFastPf];
 #pragma unroll
-            for (int k = 0; k < kRoiRowsPerWave; ++k) v[k] = k < kr ? src0[(size_t)(w + 4 * k) * lstride + qc] : 0;
+            for (int k = 0; k < kFastPf; ++k) {
+                const int r = (w + 4 * k) * f.rpi + f.rr;
+                pf[2 * k] = pf[2 * k + 1] = 0;
+                if (live && f.lane_ok && r < H) __builtin_memcpy(&pf[2 * k], src + (size_t)r * lstride, 8);
+            }
+            const int keep = W - 4 * f.c;                          // bytes of this chunk inside the ROI
 #pragma unroll
-            for (int k = 0; k < kRoiRowsPerWave; ++k) {
-                const int r = w + 4 * k;
-                if (r < H && q < W + 2) {
-                    const uint16_t b = q < W ? (uint16_t)v[k] : 0;
-                    E16[r * 2 * kPairStride + q] = b;
-                    if (q >= 1) O16[r * 2 * kPairStride + q - 1] = b;
+            for (int k = 0; k < kFastPf; ++k) {
+                const int r = (w + 4 * k) * f.rpi + f.rr;
+                if (live && f.lane_ok && r < H) {
+                    uint32_t lo = pf[2 * k], hi = pf[2 * k + 1];
+                    if (keep < 8) {
+                        const uint64_t m = keep <= 0 ? 0ull : ((1ull << (8 * keep)) - 1ull);
+                        const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
+                        lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+                    }
+                    const uint2 e = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u), __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
+                    const uint2 o = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c020c01u), __builtin_amdgcn_perm(hi, lo, 0x0c040c03u));
+                    *reinterpret_cast<uint2*>(E + r * kPairStride + 2 * f.c) = e;
+                    *reinterpret_cast<uint2*>(O + r * kPairStride + 2 * f.c) = o;
                 }
             }
+            if (live) {
+                for (int i = tid; i < SW; i += blockDim.x) { sc[i] = -1; sc[(Hd + 1) * SW + i] = -1; }
+                for (int r = tid; r < Hd + 2; r += blockDim.x) { sc[r * SW + 1] = -1; sc[r * SW + Wd + 2] = -1; }
+            }
+            if (tid == 0) { nsurv = 0; nki = 0; nkm = 0; }
+            __syncthreads();
         }
-        if (live) {
-            for (int i = tid; i < SW; i += blockDim.x) { sc[i] = -1; sc[(Hd + 1) * SW + i] = -1; }
-            for (int r = tid; r < Hd + 2; r += blockDim.x) { sc[r * SW + 1] = -1; sc[r * SW + Wd + 2] = -1; }
-        }
-        if (tid == 0) { nsurv = 0; nki = 0; nkm = 0; }
-        __syncthreads();
-    }
-    {
         int count = 0;
         if (live && stop_after != 1) {
             // 2. compass pre-test for every pixel pair at tp = min(T1, T2); the score map gets 0 (< tp: never
@@ -1070,6 +1095,7 @@ struct Extractor {
     int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
     int out_capacity = 0;     // max keypoints per image
+    int fast_resident = 0;    // k_fast_cells workgroups resident on the whole device (persistent grid)
 
     // device buffers
     LevelDev* d_levels = nullptr;
@@ -1278,6 +1304,15 @@ int Extractor::configure(int r, int c, int batch) {
         ORBX_REQUIRE(lds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "quadtree LDS %zu B exceeds 160 KiB", lds);
         if (lds > 64 * 1024)
             ORBX_HIP(hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
+    {
+        int per_cu = 0, cus = 0;
+        const size_t lds = fast_lds_bytes(this);
+        if (lds > 64 * 1024)
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        ORBX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_fast_cells, 256, lds));
+        ORBX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        fast_resident = std::max(per_cu, 1) * std::max(cus, 1);
     }
     pyr_size = (poff + 255) & ~(size_t)255;
     cand_stride = std::max(cand, 1);

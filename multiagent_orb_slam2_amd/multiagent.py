@@ -71,7 +71,7 @@ def pack_keyframes(kps, desc, counts, valid, agent: int, frames, capacity: int, 
     """Pack n keyframes into a (n, packet_bytes) uint8 tensor on the same device.
 
     kps: (n, capacity, 28) uint8, desc: (n, capacity, 32) uint8, counts: (n,) int32,
-    valid: (n, capacity) uint8 (keypoint has a MapPoint), frames: (n,) frame ids,
+    valid: (n, capacity) uint8 (keypoint has a MapPoint), frames: (n,) frame ids (device tensor or host list),
     fv: optional dict of the vocabulary batch outputs (fv_nodes (n, cap), fv_offsets (n, cap+1),
     fv_indices (n, cap), n_fv (n,)), as ORBVocabulary.transform_batch_device returns them."""
     import torch
@@ -80,8 +80,10 @@ def pack_keyframes(kps, desc, counts, valid, agent: int, frames, capacity: int, 
     lay = PacketLayout(capacity)
     out = torch.zeros((n, lay.bytes), dtype=torch.uint8, device=dev)
     n_fv = fv["n_fv"].to(torch.int32) if fv is not None else torch.zeros_like(counts, dtype=torch.int32)
+    if not torch.is_tensor(frames):   # a host list is staged once through pinned memory (no pageable copy,
+        frames = torch.as_tensor(frames, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)  # no stall)
     hdr = torch.stack([counts.to(torch.int32), torch.full_like(counts, agent, dtype=torch.int32),
-                       torch.as_tensor(frames, dtype=torch.int32, device=dev), n_fv], 1)
+                       frames.to(torch.int32), n_fv], 1)
     out[:, :HEADER] = hdr.contiguous().view(torch.uint8).view(n, HEADER)
 
     def put(name, t, nbytes):

@@ -11,6 +11,13 @@ __global__ void k_work(int* out, int iters) {
     if (v == 0x7fffffff) out[0] = v;
 }
 
+__global__ void k_lds(int* out, int n) {
+    extern __shared__ int sm[];
+    sm[threadIdx.x] = threadIdx.x;
+    __syncthreads();
+    if (sm[(threadIdx.x + 1) & 255] == n) out[0] = 1;
+}
+
 int main() {
     int* d;
     (void)hipMalloc(&d, 4);
@@ -30,6 +37,18 @@ int main() {
             (void)hipEventElapsedTime(&ms, a, b);
             printf("empty bs=%4d waves=%8d : %8.3f ms  %.3f waves/ns\n", bs, waves, ms, waves / (ms * 1e6));
         }
+    }
+    for (int lds : {0, 8192, 22528, 40960}) {
+        const int blocks = 150000;
+        for (int rep = 0; rep < 2; ++rep) {
+            (void)hipEventRecord(a);
+            hipLaunchKernelGGL(k_lds, dim3(blocks), dim3(256), lds + 1024, 0, d, -5);
+            (void)hipEventRecord(b);
+            (void)hipEventSynchronize(b);
+        }
+        float ms;
+        (void)hipEventElapsedTime(&ms, a, b);
+        printf("lds+barrier bs=256 blocks=%d lds=%d : %.3f ms\n", blocks, lds + 1024, ms);
     }
     for (int iters : {100, 1000}) {
         const int waves = 262144;
