@@ -251,6 +251,81 @@ int orbx_search_for_triangulation(orbx_matcher* m, const uint8_t* desc1, const o
                                   int only_stereo, int32_t* match12, int* n_matches);
 
 /* ------------------------------------------------------------------------------------------------
+ * Keypoint grid and the projection / radius matchers.
+ * The reference's callers project each MapPoint before searching (cv::Mat products, PredictScale,
+ * src/ORBmatcher.cc); a query carries what that projection hands to the search: the window of
+ * GetFeaturesInArea and the values the reference's inner loop tests.
+ * ---------------------------------------------------------------------------------------------- */
+/* Frame grid (FRAME_GRID_COLS 64 x FRAME_GRID_ROWS 48, include/Frame.h:37-38): image bounds and inverse
+ * cell size as the Frame constructor computes them (src/Frame.cc:99-104, :436-464). */
+typedef struct orbx_grid {
+    float min_x, min_y, max_x, max_y;
+    float inv_w, inv_h;          /* mfGridElementWidthInv, mfGridElementHeightInv */
+    int32_t cols, rows;
+} orbx_grid;
+
+enum {
+    ORBX_PROJ_MAPPOINTS = 0, /* SearchByProjection(Frame&, vpMapPoints, th)             src/ORBmatcher.cc:45-131 */
+    ORBX_PROJ_LASTFRAME = 1, /* SearchByProjection(Frame&, const Frame&, th, bMono)     :1330-1472 */
+    ORBX_PROJ_KEYFRAME = 2,  /* SearchByProjection(Frame&, KeyFrame*, sFound, th, ORBdist) :1474-1601 */
+    ORBX_PROJ_SIM3 = 3,      /* SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th) :292-405 */
+    ORBX_PROJ_FUSE = 4,      /* Fuse(KeyFrame*, vpMapPoints, th), its search             :894-951 */
+    ORBX_PROJ_BEST = 5,      /* Fuse(KeyFrame*, Scw, ...) :1053-1081; SearchBySim3's two searches :1193-1226, :1273-1306 */
+    ORBX_PROJ_INIT = 6       /* SearchForInitialization                                  :407-522 */
+};
+enum { ORBX_QF_SKIP = 1,     /* query absent (bad MapPoint, not in view, already found, level > 0 for INIT) */
+       ORBX_QF_BLOCKS = 2 }; /* an assignment by this query excludes the keypoint from later queries
+                                (MAPPOINTS/LASTFRAME: the MapPoint has Observations() > 0; KEYFRAME/SIM3: always) */
+
+/* One projected MapPoint (or, for INIT, one F1 keypoint). 40 bytes. */
+typedef struct orbx_proj_query {
+    float x, y, r;                /* GetFeaturesInArea(x, y, r, ...) window: projection u, v and radius */
+    int32_t min_level, max_level; /* Frame::GetFeaturesInArea level arguments (tested iff min > 0 || max >= 0) */
+    float ur, ur_tol;             /* MAPPOINTS/LASTFRAME: skip candidates with uright > 0 && |ur - uright| > ur_tol
+                                     (ur_tol < 0: off); FUSE: ur = u - bf/z for the stereo reprojection error */
+    float angle;                  /* the query keypoint's angle (rotation-consistency histogram) */
+    int32_t level;                /* reserved (predicted level) */
+    int32_t flags;                /* ORBX_QF_* */
+} orbx_proj_query;
+
+typedef struct orbx_proj_params {
+    int32_t mode;                 /* ORBX_PROJ_* */
+    int32_t accept_max;           /* accept if bestDist <= accept_max: TH_HIGH, TH_LOW or ORBdist */
+    float nnratio;                /* MAPPOINTS same-level ratio (:122) / INIT ratio (:463) */
+    int32_t check_ori;            /* rotation-consistency filter (LASTFRAME, KEYFRAME, INIT) */
+    int32_t nlevels;
+    float inv_sigma2[32];         /* mvInvLevelSigma2 of the target view (FUSE reprojection test :927, :938) */
+} orbx_proj_params;
+
+/* One search problem on the device: a query set against one target view with its grid (CSR cells
+ * from orbx_grid_build_device).  blocked[idx] != 0: the target keypoint already holds an excluding
+ * MapPoint (MAPPOINTS/LASTFRAME: Observations() > 0; KEYFRAME: any; SIM3: vpMatched[idx]); NULL = none.
+ * Outputs: q_idx/q_dist per query (accepted keypoint or -1; INIT: vnMatches12); owner[idx] for modes
+ * MAPPOINTS..SIM3 (-1 untouched, q = the MapPoint of query q, -2 = set to NULL by the rotation filter);
+ * *nmatches as the reference returns it. */
+typedef struct orbx_proj_problem {
+    const orbx_proj_query* queries; const uint8_t* qdesc; int32_t nq;
+    const orbx_keypoint* kps; const uint8_t* desc; const float* uright; const uint8_t* blocked; int32_t n;
+    const int32_t* cell_start; const int32_t* cell_idx;
+    int32_t* q_idx; int32_t* q_dist; int32_t* owner; int32_t* nmatches;
+} orbx_proj_problem;
+
+/* Frame::AssignFeaturesToGrid (src/Frame.cc:230-245) for 'batch' keypoint sets laid out like the
+ * orbx_extract_batch_device output: cell (ix, iy) -> CSR row ix*rows + iy at d_cell_start + i*(cols*rows+1),
+ * keypoint indices ascending inside a cell at d_cell_idx + i*capacity.  capacity <= 8192. */
+int orbx_grid_build_device(orbx_matcher* m, orbx_grid grid, const orbx_keypoint* d_kps, const int32_t* d_counts,
+                           int batch, int capacity, int32_t* d_cell_start, int32_t* d_cell_idx, void* stream);
+/* The searches of n_problems problems (device array) in one launch; max_n / max_nq bound the target
+ * keypoints / queries of any problem. */
+int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
+                                  const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq,
+                                  void* stream);
+/* Host form: one query set against one view (host buffers; uright / blocked / owner may be NULL). */
+int orbx_proj_search(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid, const orbx_proj_query* queries,
+                     const uint8_t* qdesc, int nq, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,
+                     const uint8_t* blocked, int n, int32_t* q_idx, int32_t* q_dist, int32_t* owner, int* n_matches);
+
+/* ------------------------------------------------------------------------------------------------
  * DBoW2 vocabulary — replaces TemplatedVocabulary<FORB>::transform (Thirdparty/DBoW2/DBoW2/
  * TemplatedVocabulary.h:1125-1259), i.e. Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:395-402),
  * which produce the FeatureVector that SearchByBoW buckets on.  Supported: L1/L2 scoring with any

@@ -16,6 +16,11 @@ namespace orbx {
 // ---------------------------------------------------------------------------------------------
 void set_error(const char* fmt, ...);
 
+// Matcher internals shared with orbx_proj.hip (defined in orbx_match.hip): the device a matcher is bound to,
+// and its growable scratch buffer + own stream for the host-form entry points.
+int matcher_device(const orbx_matcher* m);
+int matcher_scratch(orbx_matcher* m, size_t bytes, void** base, void** stream);
+
 #define ORBX_HIP(call)                                                                          \
     do {                                                                                        \
         hipError_t e_ = (call);                                                                 \

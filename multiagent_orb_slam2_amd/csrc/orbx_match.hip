@@ -721,6 +721,15 @@ static size_t bf_scratch(int nq, int nt) {
 using namespace orbx;
 struct orbx_matcher : public orbx::Matcher {};
 
+int orbx::matcher_device(const orbx_matcher* m) { return m->device; }
+int orbx::matcher_scratch(orbx_matcher* m, size_t bytes, void** base, void** stream) {
+    int st = m->reserve(bytes);
+    if (st) return st;
+    *base = m->scratch;
+    *stream = (void*)m->stream;
+    return ORBX_OK;
+}
+
 extern "C" {
 
 int orbx_th_high(void) { return kThHigh; }

@@ -1,0 +1,513 @@
+// =====================================================================================================
+// orbx_proj.hip — keypoint grid and the projection / radius matchers on gfx950.
+//
+//   k_grid_build   Frame::AssignFeaturesToGrid (src/Frame.cc:230-245, PosInGrid :382-392): one workgroup per
+//                  keypoint set; (cell, index) keys bitonic-sorted in LDS, cell starts by binary search ->
+//                  CSR cell lists with indices ascending inside a cell, the reference's mGrid[ix][iy] order.
+//   k_proj_search  the window search of SearchByProjection x4, Fuse x2 and SearchBySim3 (modes in
+//                  include/orbx.h): one workgroup per (query set, target view), one query per thread, the
+//                  candidate walk in GetFeaturesInArea order (src/Frame.cc:327-380) so the first-minimum tie
+//                  rule holds.  The assigning modes exclude keypoints that EARLIER queries of the same call
+//                  were assigned to (the reference's sequential mvpMapPoints check); that dependency is solved
+//                  exactly by a fixed-point iteration: every query re-evaluates its window with the keypoints
+//                  claimed by earlier accepted (blocking) queries of the previous round excluded, until no
+//                  choice changes.  Query 0 is final after one round and, by induction over the query order,
+//                  the unique fixed point is the sequential result; real calls settle in a few rounds.
+//   k_proj_init    SearchForInitialization (src/ORBmatcher.cc:407-522), whose exclusion depends on the distance
+//                  of the current owner (stealing): one wave walks the queries in order, lanes over candidates.
+// Float arithmetic is written with explicit __f*_rn (no contraction) in the reference's operation order.
+// =====================================================================================================
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <vector>
+
+#include "orbx_common.h"
+
+namespace orbx {
+
+constexpr int kProjThreads = 1024;
+constexpr int kGridMaxKps = 8192;          // keypoints per view (13-bit index in the sort key)
+constexpr int kGridMaxCells = (1 << 19) - 1;
+constexpr int kProjHisto = 30;             // HISTO_LENGTH (src/ORBmatcher.cc:39)
+
+__device__ __forceinline__ int grid_cell(const orbx_grid& g, float x, float y) {   // PosInGrid (:382-392)
+    const int px = (int)roundf(__fmul_rn(__fsub_rn(x, g.min_x), g.inv_w));
+    const int py = (int)roundf(__fmul_rn(__fsub_rn(y, g.min_y), g.inv_h));
+    if (px < 0 || px >= g.cols || py < 0 || py >= g.rows) return -1;
+    return px * g.rows + py;
+}
+
+__device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_t v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kProjThreads) void k_grid_build(const orbx_keypoint* __restrict__ kps, const int32_t* __restrict__ counts,
+                                                             int n_fixed, int capacity, orbx_grid g,
+                                                             int32_t* __restrict__ cell_start, int32_t* __restrict__ cell_idx) {
+    extern __shared__ uint32_t gkey[];
+    const int set = blockIdx.x, tid = threadIdx.x, T = blockDim.x;
+    const int n = min(counts ? counts[set] : n_fixed, capacity);
+    const int ncell = g.cols * g.rows;
+    const orbx_keypoint* K = kps + (size_t)set * capacity;
+    int32_t* cs = cell_start + (size_t)set * (ncell + 1);
+    int32_t* ci = cell_idx + (size_t)set * capacity;
+    int P2 = 1;
+    while (P2 < n) P2 <<= 1;
+    for (int i = tid; i < P2; i += T) {
+        uint32_t key = 0xffffffffu;
+        if (i < n) {
+            const int c = grid_cell(g, K[i].x, K[i].y);
+            if (c >= 0) key = ((uint32_t)c << 13) | (uint32_t)i;
+        }
+        gkey[i] = key;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < P2; i += T) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t a = gkey[i], b = gkey[ixj];
+                    if ((a > b) == ((i & k) == 0)) { gkey[i] = b; gkey[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    for (int c = tid; c <= ncell; c += T) cs[c] = lower_bound_u32(gkey, P2, (uint32_t)c << 13);
+    for (int i = tid; i < n; i += T)
+        if (gkey[i] != 0xffffffffu) ci[i] = (int32_t)(gkey[i] & 0x1fffu);
+}
+
+__device__ __forceinline__ int proj_rot_bin(float a1, float a2) {   // e.g. src/ORBmatcher.cc:1435-1440
+    float rot = __fsub_rn(a1, a2);
+    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+    int bin = (int)roundf(__fmul_rn(rot, 1.0f / kProjHisto));
+    if (bin == kProjHisto) bin = 0;
+    return bin;
+}
+
+// One query's window search in GetFeaturesInArea order.  claim[idx] < q: keypoint taken by an earlier
+// blocking query (assigning modes; nullptr otherwise).  Returns the accepted keypoint or -1.
+__device__ int proj_walk(const orbx_proj_params& P, const orbx_grid& g, const orbx_proj_problem& pb, int q,
+                         const orbx_proj_query& Q, const int* claim, int& out_dist) {
+    const int mode = P.mode;
+    const float x = Q.x, y = Q.y, r = Q.r;
+    const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, g.min_x), r), g.inv_w)));
+    if (nMinCellX >= g.cols) return -1;
+    const int nMaxCellX = min(g.cols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, g.min_x), r), g.inv_w)));
+    if (nMaxCellX < 0) return -1;
+    const int nMinCellY = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, g.min_y), r), g.inv_h)));
+    if (nMinCellY >= g.rows) return -1;
+    const int nMaxCellY = min(g.rows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, g.min_y), r), g.inv_h)));
+    if (nMaxCellY < 0) return -1;
+    const bool check = (Q.min_level > 0) || (Q.max_level >= 0);
+    const bool assigning = mode <= ORBX_PROJ_SIM3;
+    const bool stereo_tol = (mode == ORBX_PROJ_MAPPOINTS || mode == ORBX_PROJ_LASTFRAME) && pb.uright && Q.ur_tol >= 0.0f;
+    const uint4* qd = reinterpret_cast<const uint4*>(pb.qdesc + 32 * (size_t)q);
+    const uint4 a0 = qd[0], a1 = qd[1];
+    const int init = (mode == ORBX_PROJ_INIT || mode == ORBX_PROJ_BEST) ? INT_MAX : 256;
+    int bestDist = init, bestIdx = -1, bestLevel = -1, bestDist2 = init, bestLevel2 = -1;
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix)
+        for (int iy = nMinCellY; iy <= nMaxCellY; ++iy) {
+            const int c = ix * g.rows + iy;
+            const int j1 = pb.cell_start[c + 1];
+            for (int j = pb.cell_start[c]; j < j1; ++j) {
+                const int idx = pb.cell_idx[j];
+                const orbx_keypoint kp = pb.kps[idx];
+                if (check) {
+                    if (kp.octave < Q.min_level) continue;
+                    if (Q.max_level >= 0 && kp.octave > Q.max_level) continue;
+                }
+                if (!(fabsf(__fsub_rn(kp.x, x)) < r && fabsf(__fsub_rn(kp.y, y)) < r)) continue;
+                if (assigning) {
+                    if (pb.blocked && pb.blocked[idx]) continue;
+                    if (claim && claim[idx] < q) continue;
+                }
+                if (stereo_tol && pb.uright[idx] > 0.0f) {
+                    if (fabsf(__fsub_rn(Q.ur, pb.uright[idx])) > Q.ur_tol) continue;
+                }
+                if (mode == ORBX_PROJ_FUSE) {
+                    const float ex = __fsub_rn(Q.x, kp.x), ey = __fsub_rn(Q.y, kp.y);
+                    if (pb.uright && pb.uright[idx] >= 0.0f) {
+                        const float er = __fsub_rn(Q.ur, pb.uright[idx]);
+                        const float e2 = __fadd_rn(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), __fmul_rn(er, er));
+                        if ((double)__fmul_rn(e2, P.inv_sigma2[kp.octave]) > 7.8) continue;
+                    } else {
+                        const float e2 = __fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
+                        if ((double)__fmul_rn(e2, P.inv_sigma2[kp.octave]) > 5.99) continue;
+                    }
+                }
+                const uint4* kd = reinterpret_cast<const uint4*>(pb.desc + 32 * (size_t)idx);
+                const int dist = hamming256(a0, a1, kd[0], kd[1]);
+                if (dist < bestDist) {
+                    bestDist2 = bestDist;
+                    bestLevel2 = bestLevel;
+                    bestDist = dist;
+                    bestLevel = kp.octave;
+                    bestIdx = idx;
+                } else if (dist < bestDist2) {
+                    bestLevel2 = kp.octave;
+                    bestDist2 = dist;
+                }
+            }
+        }
+    if (bestIdx < 0 || bestDist > P.accept_max) return -1;
+    if (mode == ORBX_PROJ_MAPPOINTS && bestLevel == bestLevel2 && (float)bestDist > __fmul_rn(P.nnratio, (float)bestDist2))
+        return -1;
+    out_dist = bestDist;
+    return bestIdx;
+}
+
+// Modes MAPPOINTS .. BEST.  Dynamic LDS: claim[n] + own[n] (assigning modes).
+__global__ __launch_bounds__(kProjThreads) void k_proj_search(orbx_proj_params P, orbx_grid g,
+                                                              const orbx_proj_problem* __restrict__ probs) {
+    extern __shared__ int psm[];
+    __shared__ int changed, hist[32], keep[3], acc_sh, bad_sh;
+    const orbx_proj_problem pb = probs[blockIdx.x];
+    const int tid = threadIdx.x, T = blockDim.x, nq = pb.nq, n = pb.n;
+    const bool assigning = P.mode <= ORBX_PROJ_SIM3;
+    if (tid == 0) { acc_sh = 0; bad_sh = 0; }
+    if (tid < 32) hist[tid] = 0;
+    __syncthreads();
+    if (!assigning) {
+        int acc = 0;
+        for (int q = tid; q < nq; q += T) {
+            const orbx_proj_query Q = pb.queries[q];
+            int d = -1, r = -1;
+            if (!(Q.flags & ORBX_QF_SKIP)) r = proj_walk(P, g, pb, q, Q, nullptr, d);
+            pb.q_idx[q] = r;
+            pb.q_dist[q] = r >= 0 ? d : -1;
+            acc += r >= 0;
+        }
+        acc = wave_sum(acc);
+        if (lane_id() == 0 && acc) atomicAdd(&acc_sh, acc);
+        __syncthreads();
+        if (tid == 0) *pb.nmatches = acc_sh;
+        return;
+    }
+    int* claim = psm;
+    int* own = psm + n;
+    for (int i = tid; i < n; i += T) claim[i] = INT_MAX;
+    __syncthreads();
+    for (int round = 0; round <= nq; ++round) {       // at most nq + 1 rounds (query q is final after q + 1)
+        if (tid == 0) changed = 0;
+        __syncthreads();
+        int ch = 0;
+        for (int q = tid; q < nq; q += T) {
+            const orbx_proj_query Q = pb.queries[q];
+            int d = -1, r = -1;
+            if (!(Q.flags & ORBX_QF_SKIP)) r = proj_walk(P, g, pb, q, Q, claim, d);
+            if (round == 0 || r != pb.q_idx[q]) ch = 1;
+            pb.q_idx[q] = r;
+            pb.q_dist[q] = r >= 0 ? d : -1;
+        }
+        if (ch) changed = 1;
+        __syncthreads();
+        if (!changed) break;                           // workgroup-uniform
+        for (int i = tid; i < n; i += T) claim[i] = INT_MAX;
+        __syncthreads();
+        for (int q = tid; q < nq; q += T) {
+            const int r = pb.q_idx[q];
+            if (r >= 0 && (pb.queries[q].flags & ORBX_QF_BLOCKS)) atomicMin(&claim[r], q);
+        }
+        __syncthreads();
+    }
+    // final assignment: the last accepted query writes mvpMapPoints[idx] (src/ORBmatcher.cc:125, :1430, :1559, :398)
+    for (int i = tid; i < n; i += T) own[i] = -1;
+    __syncthreads();
+    const bool rot = P.check_ori && (P.mode == ORBX_PROJ_LASTFRAME || P.mode == ORBX_PROJ_KEYFRAME);
+    int acc = 0;
+    for (int q = tid; q < nq; q += T) {
+        const int r = pb.q_idx[q];
+        if (r < 0) continue;
+        ++acc;
+        atomicMax(&own[r], q);
+        if (rot) atomicAdd(&hist[proj_rot_bin(pb.queries[q].angle, pb.kps[r].angle)], 1);
+    }
+    acc = wave_sum(acc);
+    if (lane_id() == 0 && acc) atomicAdd(&acc_sh, acc);
+    __syncthreads();
+    if (rot) {
+        // ComputeThreeMaxima (:1603-1644), then every entry of the other bins sets mvpMapPoints[idx] = NULL
+        if (tid == 0) {
+            int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
+            for (int i = 0; i < kProjHisto; ++i) {
+                const int s = hist[i];
+                if (s > m1) { m3 = m2; m2 = m1; m1 = s; i3 = i2; i2 = i1; i1 = i; }
+                else if (s > m2) { m3 = m2; m2 = s; i3 = i2; i2 = i; }
+                else if (s > m3) { m3 = s; i3 = i; }
+            }
+            if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+            else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+            keep[0] = i1; keep[1] = i2; keep[2] = i3;
+        }
+        __syncthreads();
+        int bad = 0;
+        for (int q = tid; q < nq; q += T) {
+            const int r = pb.q_idx[q];
+            if (r < 0) continue;
+            const int b = proj_rot_bin(pb.queries[q].angle, pb.kps[r].angle);
+            if (b == keep[0] || b == keep[1] || b == keep[2]) continue;
+            own[r] = -2;
+            ++bad;
+        }
+        bad = wave_sum(bad);
+        if (lane_id() == 0 && bad) atomicAdd(&bad_sh, bad);
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += T) pb.owner[i] = own[i];
+    if (tid == 0) *pb.nmatches = acc_sh - bad_sh;
+}
+
+// SearchForInitialization: one wave per problem walks the queries in order.  Dynamic LDS: matchedDist[n],
+// m21[n] (vMatchedDistance / vnMatches21 of :417-418) and res[nq] (vnMatches12).
+constexpr int kInitNone = 1023;   // "INT_MAX" distance inside the packed (distance << 20 | position) key
+
+__global__ __launch_bounds__(64) void k_proj_init(orbx_proj_params P, orbx_grid g, const orbx_proj_problem* __restrict__ probs) {
+    extern __shared__ int ism[];
+    __shared__ int hist[32];
+    const orbx_proj_problem pb = probs[blockIdx.x];
+    const int ln = lane_id(), nq = pb.nq, n = pb.n;
+    int* mdist = ism;
+    int* m21 = ism + n;
+    int* res = ism + 2 * n;
+    for (int i = ln; i < n; i += kWave) { mdist[i] = INT_MAX; m21[i] = -1; }
+    for (int i = ln; i < nq; i += kWave) res[i] = -1;
+    if (ln < 32) hist[ln] = 0;
+    __syncthreads();
+    int nm = 0;
+    for (int q = 0; q < nq; ++q) {
+        const orbx_proj_query Q = pb.queries[q];
+        if (Q.flags & ORBX_QF_SKIP) continue;
+        const float x = Q.x, y = Q.y, r = Q.r;
+        const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, g.min_x), r), g.inv_w)));
+        if (nMinCellX >= g.cols) continue;
+        const int nMaxCellX = min(g.cols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, g.min_x), r), g.inv_w)));
+        if (nMaxCellX < 0) continue;
+        const int nMinCellY = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, g.min_y), r), g.inv_h)));
+        if (nMinCellY >= g.rows) continue;
+        const int nMaxCellY = min(g.rows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, g.min_y), r), g.inv_h)));
+        if (nMaxCellY < 0) continue;
+        const bool check = (Q.min_level > 0) || (Q.max_level >= 0);
+        const uint4* qd = reinterpret_cast<const uint4*>(pb.qdesc + 32 * (size_t)q);
+        const uint4 a0 = qd[0], a1 = qd[1];
+        // running best (b1, position bp, keypoint bi) and second b2 over the candidates in walk order; the
+        // sequential update rule keeps as second the smallest value among the non-best candidates
+        int b1 = kInitNone, b2 = kInitNone, bi = -1, pos = 0;
+        for (int ix = nMinCellX; ix <= nMaxCellX; ++ix)
+            for (int iy = nMinCellY; iy <= nMaxCellY; ++iy) {
+                const int c = ix * g.rows + iy;
+                const int j0 = pb.cell_start[c], j1 = pb.cell_start[c + 1];
+                for (int jb = j0; jb < j1; jb += kWave) {
+                    const int j = jb + ln;
+                    int d = kInitNone, idx = -1;
+                    if (j < j1) {
+                        idx = pb.cell_idx[j];
+                        const orbx_keypoint kp = pb.kps[idx];
+                        bool ok = true;
+                        if (check) {
+                            if (kp.octave < Q.min_level) ok = false;
+                            if (Q.max_level >= 0 && kp.octave > Q.max_level) ok = false;
+                        }
+                        if (!(fabsf(__fsub_rn(kp.x, x)) < r && fabsf(__fsub_rn(kp.y, y)) < r)) ok = false;
+                        if (ok) {
+                            const uint4* kd = reinterpret_cast<const uint4*>(pb.desc + 32 * (size_t)idx);
+                            const int dist = hamming256(a0, a1, kd[0], kd[1]);
+                            if (!(mdist[idx] <= dist)) d = dist;           // :446-447
+                        }
+                    }
+                    const uint32_t key = ((uint32_t)d << 20) | (uint32_t)(pos + ln);
+                    const uint32_t m = wave_min_u32(key);
+                    const int cb1 = (int)(m >> 20);
+                    const int cb2 = (int)wave_min_u32(key == m ? (uint32_t)kInitNone : (uint32_t)d);
+                    const int cidx = __builtin_amdgcn_readlane(idx, (int)(m & 0xfffff) - pos);
+                    if (cb1 < b1) { b2 = min(b1, cb2); b1 = cb1; bi = cidx; }
+                    else { b2 = min(b2, min(cb1, cb2)); }
+                    pos += min(kWave, j1 - jb);
+                }
+            }
+        if (bi < 0 || b1 == kInitNone || b1 > P.accept_max) continue;
+        const float second = b2 == kInitNone ? (float)INT_MAX : (float)b2;
+        if (!((float)b1 < __fmul_rn(second, P.nnratio))) continue;         // :463
+        if (ln == 0) {
+            if (m21[bi] >= 0) res[m21[bi]] = -1;                            // :465-469
+            res[q] = bi;
+            m21[bi] = q;
+            mdist[bi] = b1;
+            if (P.check_ori) hist[proj_rot_bin(Q.angle, pb.kps[bi].angle)] += 1;
+        }
+        nm += 1;
+        __syncthreads();
+    }
+    __syncthreads();
+    // nmatches = accepted - stolen - rotation-filtered (:461-514); stolen entries have res == -1 already
+    int owners = 0;
+    for (int q = ln; q < nq; q += kWave) owners += res[q] >= 0;
+    owners = wave_sum(owners);
+    int keep0 = -1, keep1 = -1, keep2 = -1;
+    if (P.check_ori) {
+        int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
+        for (int i = 0; i < kProjHisto; ++i) {
+            const int s = hist[i];
+            if (s > m1) { m3 = m2; m2 = m1; m1 = s; i3 = i2; i2 = i1; i1 = i; }
+            else if (s > m2) { m3 = m2; m2 = s; i3 = i2; i2 = i; }
+            else if (s > m3) { m3 = s; i3 = i; }
+        }
+        if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+        else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+        keep0 = i1; keep1 = i2; keep2 = i3;
+    }
+    int dropped = 0;
+    for (int q = ln; q < nq; q += kWave) {
+        int r = res[q];
+        if (r >= 0 && P.check_ori) {
+            const int b = proj_rot_bin(pb.queries[q].angle, pb.kps[r].angle);
+            if (b != keep0 && b != keep1 && b != keep2) { r = -1; ++dropped; }
+        }
+        pb.q_idx[q] = r;
+        pb.q_dist[q] = r >= 0 ? mdist[r] : -1;
+    }
+    dropped = wave_sum(dropped);
+    (void)nm;
+    if (ln == 0) *pb.nmatches = owners - dropped;
+}
+
+}  // namespace orbx
+
+using namespace orbx;
+
+static size_t a256p(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static int grid_check(const orbx_grid& g) {
+    ORBX_REQUIRE(g.cols > 0 && g.rows > 0 && (long long)g.cols * g.rows <= kGridMaxCells, ORBX_ERR_ARG, "bad grid %d x %d",
+                 g.cols, g.rows);
+    return ORBX_OK;
+}
+
+extern "C" {
+
+int orbx_grid_build_device(orbx_matcher* m, orbx_grid grid, const orbx_keypoint* d_kps, const int32_t* d_counts, int batch,
+                           int capacity, int32_t* d_cell_start, int32_t* d_cell_idx, void* stream) {
+    ORBX_REQUIRE(m && d_kps && d_counts && d_cell_start && d_cell_idx && batch >= 0 && capacity > 0, ORBX_ERR_ARG,
+                 "bad argument");
+    int st = grid_check(grid);
+    if (st) return st;
+    ORBX_REQUIRE(capacity <= kGridMaxKps, ORBX_ERR_UNSUPPORTED, "capacity %d > %d", capacity, kGridMaxKps);
+    if (batch == 0) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(matcher_device(m)));
+    int p2 = 1;
+    while (p2 < capacity) p2 <<= 1;
+    hipLaunchKernelGGL(k_grid_build, dim3(batch), dim3(kProjThreads), (size_t)p2 * 4, (hipStream_t)stream, d_kps, d_counts, 0,
+                       capacity, grid, d_cell_start, d_cell_idx);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
+                                  const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq, void* stream) {
+    ORBX_REQUIRE(m && params && d_problems && n_problems >= 0 && max_n >= 0 && max_nq >= 0, ORBX_ERR_ARG, "bad argument");
+    int st = grid_check(grid);
+    if (st) return st;
+    const orbx_proj_params& P = *params;
+    ORBX_REQUIRE(P.mode >= ORBX_PROJ_MAPPOINTS && P.mode <= ORBX_PROJ_INIT, ORBX_ERR_ARG, "bad mode %d", P.mode);
+    ORBX_REQUIRE(P.nlevels >= 1 && P.nlevels <= 32, ORBX_ERR_ARG, "bad nlevels %d", P.nlevels);
+    if (n_problems == 0) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(matcher_device(m)));
+    hipStream_t s = (hipStream_t)stream;
+    if (P.mode == ORBX_PROJ_INIT) {
+        const size_t lds = (size_t)(2 * std::max(max_n, 1) + std::max(max_nq, 1)) * 4;
+        ORBX_REQUIRE(lds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "too many keypoints for SearchForInitialization (%d, %d)", max_n,
+                     max_nq);
+        if (lds > 64 * 1024)
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_proj_init, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(k_proj_init, dim3(n_problems), dim3(64), lds, s, P, grid, d_problems);
+    } else {
+        const size_t lds = (size_t)2 * std::max(max_n, 1) * 4;
+        ORBX_REQUIRE(lds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "too many target keypoints (%d)", max_n);
+        if (lds > 64 * 1024)
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_proj_search, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(k_proj_search, dim3(n_problems), dim3(kProjThreads), lds, s, P, grid, d_problems);
+    }
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+// Host form: one query set against one view; builds the view's grid, runs the search, copies results back.
+int orbx_proj_search(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid, const orbx_proj_query* queries,
+                     const uint8_t* qdesc, int nq, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,
+                     const uint8_t* blocked, int n, int32_t* q_idx, int32_t* q_dist, int32_t* owner, int* n_matches) {
+    ORBX_REQUIRE(m && params && n_matches && nq >= 0 && n >= 0, ORBX_ERR_ARG, "bad argument");
+    ORBX_REQUIRE((nq == 0 || (queries && qdesc && q_idx && q_dist)) && (n == 0 || (kps && desc)), ORBX_ERR_ARG,
+                 "null buffers");
+    ORBX_REQUIRE(n <= kGridMaxKps, ORBX_ERR_UNSUPPORTED, "more than %d keypoints", kGridMaxKps);
+    int st = grid_check(grid);
+    if (st) return st;
+    *n_matches = 0;
+    const int ncell = grid.cols * grid.rows;
+    const size_t N = std::max(n, 1), NQ = std::max(nq, 1);
+    const size_t bytes = a256p(sizeof(orbx_proj_query) * NQ) + a256p(32 * NQ) + a256p(sizeof(orbx_keypoint) * N) +
+                         a256p(32 * N) + a256p(4 * N) + a256p(N) + a256p(4 * ((size_t)ncell + 1)) + a256p(4 * N) +
+                         3 * a256p(4 * NQ) + a256p(4 * N) + a256p(sizeof(orbx_proj_problem)) + 1024;
+    uint8_t* base = nullptr;
+    hipStream_t s = nullptr;
+    if ((st = matcher_scratch(m, bytes, (void**)&base, (void**)&s))) return st;
+    size_t off = 0;
+    auto take = [&](size_t b) { uint8_t* p = base + off; off += a256p(b); return p; };
+    orbx_proj_query* dq = (orbx_proj_query*)take(sizeof(orbx_proj_query) * NQ);
+    uint8_t* dqd = take(32 * NQ);
+    orbx_keypoint* dk = (orbx_keypoint*)take(sizeof(orbx_keypoint) * N);
+    uint8_t* dd = take(32 * N);
+    float* du = (float*)take(4 * N);
+    uint8_t* db = take(N);
+    int32_t* dcs = (int32_t*)take(4 * ((size_t)ncell + 1));
+    int32_t* dci = (int32_t*)take(4 * N);
+    int32_t* dqi = (int32_t*)take(4 * NQ);
+    int32_t* dqdist = (int32_t*)take(4 * NQ);
+    int32_t* dnm = (int32_t*)take(4 * NQ);
+    int32_t* down = (int32_t*)take(4 * N);
+    orbx_proj_problem* dpb = (orbx_proj_problem*)take(sizeof(orbx_proj_problem));
+    if (nq) {
+        ORBX_HIP(hipMemcpyAsync(dq, queries, sizeof(orbx_proj_query) * nq, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(dqd, qdesc, 32 * (size_t)nq, hipMemcpyHostToDevice, s));
+    }
+    if (n) {
+        ORBX_HIP(hipMemcpyAsync(dk, kps, sizeof(orbx_keypoint) * n, hipMemcpyHostToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(dd, desc, 32 * (size_t)n, hipMemcpyHostToDevice, s));
+        if (uright) ORBX_HIP(hipMemcpyAsync(du, uright, 4 * (size_t)n, hipMemcpyHostToDevice, s));
+        if (blocked) ORBX_HIP(hipMemcpyAsync(db, blocked, (size_t)n, hipMemcpyHostToDevice, s));
+    }
+    orbx_proj_problem pb{};
+    pb.queries = dq; pb.qdesc = dqd; pb.nq = nq;
+    pb.kps = dk; pb.desc = dd; pb.uright = uright ? du : nullptr; pb.blocked = blocked ? db : nullptr; pb.n = n;
+    pb.cell_start = dcs; pb.cell_idx = dci;
+    pb.q_idx = dqi; pb.q_dist = dqdist; pb.owner = down; pb.nmatches = dnm;
+    ORBX_HIP(hipMemcpyAsync(dpb, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
+    int p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(kProjThreads), (size_t)p2 * 4, s, dk, (const int32_t*)nullptr, n,
+                       std::max(n, 1), grid, dcs, dci);
+    ORBX_HIP(hipGetLastError());
+    if ((st = orbx_proj_search_batch_device(m, params, grid, dpb, 1, n, nq, s))) return st;
+    int nm = 0;
+    ORBX_HIP(hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, s));
+    if (nq) {
+        ORBX_HIP(hipMemcpyAsync(q_idx, dqi, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
+        ORBX_HIP(hipMemcpyAsync(q_dist, dqdist, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
+    }
+    if (owner && n && params->mode <= ORBX_PROJ_SIM3) ORBX_HIP(hipMemcpyAsync(owner, down, 4 * (size_t)n, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+    if (owner && n && params->mode > ORBX_PROJ_SIM3)
+        for (int i = 0; i < n; ++i) owner[i] = -1;
+    *n_matches = nm;
+    return ORBX_OK;
+}
+
+}  // extern "C"

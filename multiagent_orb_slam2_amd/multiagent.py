@@ -80,8 +80,9 @@ def pack_keyframes(kps, desc, counts, valid, agent: int, frames, capacity: int, 
     lay = PacketLayout(capacity)
     out = torch.zeros((n, lay.bytes), dtype=torch.uint8, device=dev)
     n_fv = fv["n_fv"].to(torch.int32) if fv is not None else torch.zeros_like(counts, dtype=torch.int32)
-    if not torch.is_tensor(frames):   # a host list is staged once through pinned memory (no pageable copy,
-        frames = torch.as_tensor(frames, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)  # no stall)
+    if not torch.is_tensor(frames):   # a host list goes through pinned memory on a GPU (a pageable copy stalls)
+        f = torch.as_tensor(frames, dtype=torch.int32)
+        frames = f.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else f.to(dev)
     hdr = torch.stack([counts.to(torch.int32), torch.full_like(counts, agent, dtype=torch.int32),
                        frames.to(torch.int32), n_fv], 1)
     out[:, :HEADER] = hdr.contiguous().view(torch.uint8).view(n, HEADER)

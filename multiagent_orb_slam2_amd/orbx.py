@@ -69,6 +69,50 @@ class Pyramid(C.Structure):
                 ("scale", C.c_float * 32), ("inv_scale", C.c_float * 32)]
 
 
+class Grid(C.Structure):
+    """orbx_grid (include/orbx.h): Frame grid bounds and inverse cell size."""
+    _fields_ = [("min_x", C.c_float), ("min_y", C.c_float), ("max_x", C.c_float), ("max_y", C.c_float),
+                ("inv_w", C.c_float), ("inv_h", C.c_float), ("cols", C.c_int32), ("rows", C.c_int32)]
+
+
+def frame_grid(min_x: float, min_y: float, max_x: float, max_y: float, cols: int = 64, rows: int = 48) -> Grid:
+    """The grid a Frame builds (src/Frame.cc:99-104: FRAME_GRID_COLS / (mnMaxX - mnMinX) in float)."""
+    f = np.float32
+    return Grid(f(min_x), f(min_y), f(max_x), f(max_y), f(cols) / (f(max_x) - f(min_x)),
+                f(rows) / (f(max_y) - f(min_y)), cols, rows)
+
+
+# orbx_proj_query (40 B)
+PROJ_QUERY_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("r", "<f4"), ("min_level", "<i4"), ("max_level", "<i4"),
+                             ("ur", "<f4"), ("ur_tol", "<f4"), ("angle", "<f4"), ("level", "<i4"), ("flags", "<i4")])
+PROJ_MAPPOINTS, PROJ_LASTFRAME, PROJ_KEYFRAME, PROJ_SIM3, PROJ_FUSE, PROJ_BEST, PROJ_INIT = range(7)
+QF_SKIP, QF_BLOCKS = 1, 2
+
+
+class ProjParams(C.Structure):
+    """orbx_proj_params (include/orbx.h)."""
+    _fields_ = [("mode", C.c_int32), ("accept_max", C.c_int32), ("nnratio", C.c_float), ("check_ori", C.c_int32),
+                ("nlevels", C.c_int32), ("inv_sigma2", C.c_float * 32)]
+
+    @classmethod
+    def make(cls, mode, accept_max, nnratio=0.6, check_ori=False, inv_sigma2=None):
+        p = cls()
+        p.mode, p.accept_max, p.nnratio, p.check_ori = int(mode), int(accept_max), float(nnratio), int(bool(check_ori))
+        sig = np.ones(8, np.float32) if inv_sigma2 is None else np.asarray(inv_sigma2, np.float32)
+        p.nlevels = len(sig)
+        for i, v in enumerate(sig):
+            p.inv_sigma2[i] = float(v)
+        return p
+
+
+class ProjProblem(C.Structure):
+    """orbx_proj_problem (include/orbx.h): device pointers of one query set against one view."""
+    _fields_ = [("queries", C.c_void_p), ("qdesc", C.c_void_p), ("nq", C.c_int32), ("kps", C.c_void_p),
+                ("desc", C.c_void_p), ("uright", C.c_void_p), ("blocked", C.c_void_p), ("n", C.c_int32),
+                ("cell_start", C.c_void_p), ("cell_idx", C.c_void_p), ("q_idx", C.c_void_p), ("q_dist", C.c_void_p),
+                ("owner", C.c_void_p), ("nmatches", C.c_void_p)]
+
+
 _lib = None
 
 
@@ -128,6 +172,10 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, i32, FeatVec, vp, vp, vp, vp, i32, FeatVec,
                                                   vp, vp, vp, i32, f32, f32, i32, vp, C.POINTER(i32)]
     lib.orbx_search_by_bow_kfkf_pairs_device.argtypes = [vp, C.POINTER(KfStore), vp, i32, i32, vp, vp, vp]
+    lib.orbx_grid_build_device.argtypes = [vp, Grid, vp, vp, i32, i32, vp, vp, vp]
+    lib.orbx_proj_search_batch_device.argtypes = [vp, C.POINTER(ProjParams), Grid, vp, i32, i32, i32, vp]
+    lib.orbx_proj_search.argtypes = [vp, C.POINTER(ProjParams), Grid, vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp,
+                                     C.POINTER(i32)]
     lib.orbx_vocab_load_text.argtypes = [C.c_char_p, i32, C.POINTER(vp)]
     lib.orbx_vocab_create.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, C.POINTER(vp)]
     lib.orbx_vocab_destroy.argtypes = [vp]
@@ -476,6 +524,86 @@ class ORBmatcher:
                                                        _p(s2), _p(sc2), len(s2), ex, ey, int(bOnlyStereo), _p(m),
                                                        C.byref(n)))
         return n.value, m
+
+
+    # ---- projection / radius matchers (src/ORBmatcher.cc) ------------------------------
+    def proj_search(self, params: ProjParams, grid: Grid, queries, qdesc, kps, desc, uright=None, blocked=None):
+        """Generic window search (include/orbx.h orbx_proj_search).  queries: PROJ_QUERY_DTYPE array.
+        Returns (nmatches, q_idx, q_dist, owner)."""
+        q = np.ascontiguousarray(queries, PROJ_QUERY_DTYPE)
+        qd = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+        k = np.ascontiguousarray(kps, KP_DTYPE)
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        ur = None if uright is None else np.ascontiguousarray(uright, np.float32)
+        bl = None if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+        nq, n = len(q), len(k)
+        qi, qdist = np.zeros(max(nq, 1), np.int32), np.zeros(max(nq, 1), np.int32)
+        own = np.zeros(max(n, 1), np.int32)
+        nm = C.c_int()
+        _check(self._lib.orbx_proj_search(self._h, C.byref(params), grid, _p(q), _p(qd), nq, _p(k), _p(d),
+                                          None if ur is None else _p(ur), None if bl is None else _p(bl), n, _p(qi),
+                                          _p(qdist), _p(own), C.byref(nm)))
+        return nm.value, qi[:nq], qdist[:nq], own[:n]
+
+    def SearchByProjection_MapPoints(self, grid, queries, qdesc, kps, desc, uright, blocked):
+        """SearchByProjection(Frame&, vpMapPoints, th) (src/ORBmatcher.cc:45-131): queries from isInFrustum
+        (Frame.cc:269-325): window r*scale[level] at (mTrackProjX, mTrackProjY), levels [level-1, level],
+        ur = mTrackProjXR, ur_tol = the window radius; flags BLOCKS when the MapPoint has observations."""
+        return self.proj_search(ProjParams.make(PROJ_MAPPOINTS, self.TH_HIGH, self.mfNNratio), grid, queries, qdesc, kps,
+                                desc, uright, blocked)
+
+    def SearchByProjection_LastFrame(self, grid, queries, qdesc, kps, desc, uright, blocked=None):
+        """SearchByProjection(Frame&, const Frame& LastFrame, th, bMono) (src/ORBmatcher.cc:1330-1472)."""
+        return self.proj_search(ProjParams.make(PROJ_LASTFRAME, self.TH_HIGH, self.mfNNratio, self.mbCheckOrientation),
+                                grid, queries, qdesc, kps, desc, uright, blocked)
+
+    def SearchByProjection_KeyFrame(self, grid, queries, qdesc, kps, desc, blocked, ORBdist):
+        """SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:1474-1601)."""
+        return self.proj_search(ProjParams.make(PROJ_KEYFRAME, ORBdist, self.mfNNratio, self.mbCheckOrientation), grid,
+                                queries, qdesc, kps, desc, None, blocked)
+
+    def SearchByProjection_Sim3(self, grid, queries, qdesc, kps, desc, matched):
+        """SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th) (src/ORBmatcher.cc:292-405)."""
+        return self.proj_search(ProjParams.make(PROJ_SIM3, self.TH_LOW), grid, queries, qdesc, kps, desc, None, matched)
+
+    def Fuse(self, grid, queries, qdesc, kps, desc, uright, inv_sigma2):
+        """The search of Fuse(KeyFrame*, vpMapPoints, th) (src/ORBmatcher.cc:827-977); the caller applies the
+        replace / add-observation step (:953-972) to the returned best matches in query order."""
+        return self.proj_search(ProjParams.make(PROJ_FUSE, self.TH_LOW, inv_sigma2=inv_sigma2), grid, queries, qdesc,
+                                kps, desc, uright, None)
+
+    def Fuse_Scw(self, grid, queries, qdesc, kps, desc):
+        """The search of Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint) (src/ORBmatcher.cc:979-1102)."""
+        return self.proj_search(ProjParams.make(PROJ_BEST, self.TH_LOW), grid, queries, qdesc, kps, desc)
+
+    def SearchBySim3_direction(self, grid, queries, qdesc, kps, desc):
+        """One direction of SearchBySim3 (src/ORBmatcher.cc:1150-1227 / 1230-1307); the caller keeps the
+        pairs both directions agree on (:1309-1325)."""
+        return self.proj_search(ProjParams.make(PROJ_BEST, self.TH_HIGH), grid, queries, qdesc, kps, desc)
+
+    def SearchForInitialization(self, grid, queries, qdesc, kps, desc):
+        """SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) (src/ORBmatcher.cc:407-522):
+        one query per F1 keypoint (window at vbPrevMatched, levels [0, 0], SKIP if its octave > 0)."""
+        return self.proj_search(ProjParams.make(PROJ_INIT, self.TH_LOW, self.mfNNratio, self.mbCheckOrientation), grid,
+                                queries, qdesc, kps, desc)
+
+    def grid_build_device(self, grid: Grid, kps, counts, stream=None):
+        """Frame::AssignFeaturesToGrid on (B, capacity, 28) device keypoints: (cell_start, cell_idx) tensors."""
+        import torch
+        B, cap = kps.shape[0], kps.shape[1]
+        ncell = grid.cols * grid.rows
+        cs = torch.empty((B, ncell + 1), dtype=torch.int32, device=kps.device)
+        ci = torch.empty((B, cap), dtype=torch.int32, device=kps.device)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(kps.device).cuda_stream)
+        _check(self._lib.orbx_grid_build_device(self._h, grid, _tp(kps), _tp(counts), B, cap, _tp(cs), _tp(ci), s))
+        return cs, ci
+
+    def proj_search_batch_device(self, params: ProjParams, grid: Grid, problems, max_n: int, max_nq: int, stream=None):
+        """problems: uint8 device tensor holding n ProjProblem structs (see ProjProblem)."""
+        import torch
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(problems.device).cuda_stream)
+        n = problems.numel() // C.sizeof(ProjProblem)
+        _check(self._lib.orbx_proj_search_batch_device(self._h, C.byref(params), grid, _tp(problems), n, max_n, max_nq, s))
 
 
 @dataclass

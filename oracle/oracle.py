@@ -278,3 +278,70 @@ def vocab_transform(voc, feats, levelsup):
                               C.byref(nf))
     return dict(bow_words=bw[:nw.value].copy(), bow_values=bv[:nw.value].copy(), fv_nodes=fn[:nf.value].copy(),
                 fv_offsets=fo[:nf.value + 1].copy(), fv_indices=fi[:fo[nf.value]].copy())
+
+
+# ---- keypoint grid + projection / radius matchers (oracle/proj_oracle.cpp) ----------------------------
+class OGrid(C.Structure):
+    _fields_ = [("min_x", C.c_float), ("min_y", C.c_float), ("max_x", C.c_float), ("max_y", C.c_float),
+                ("inv_w", C.c_float), ("inv_h", C.c_float), ("cols", C.c_int32), ("rows", C.c_int32)]
+
+
+class OParams(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("accept_max", C.c_int32), ("nnratio", C.c_float), ("check_ori", C.c_int32),
+                ("nlevels", C.c_int32), ("inv_sigma2", C.c_float * 32)]
+
+
+def _ogrid(g):
+    return OGrid(g.min_x, g.min_y, g.max_x, g.max_y, g.inv_w, g.inv_h, g.cols, g.rows)
+
+
+def grid_assign(kps, grid):
+    """Frame::AssignFeaturesToGrid -> (cell_start (cols*rows+1,), cell_idx (n,))."""
+    k = np.ascontiguousarray(kps, KP_DTYPE)
+    cs = np.zeros(grid.cols * grid.rows + 1, np.int32)
+    ci = np.zeros(max(len(k), 1), np.int32)
+    L = lib()
+    L.orc_grid_assign.argtypes = [C.c_void_p, C.c_int, OGrid, C.c_void_p, C.c_void_p]
+    n = L.orc_grid_assign(_p(k), len(k), _ogrid(grid), _p(cs), _p(ci))
+    return cs, ci[:n]
+
+
+def features_in_area(kps, cs, ci, grid, x, y, r, min_level=-1, max_level=-1):
+    k = np.ascontiguousarray(kps, KP_DTYPE)
+    cs = np.ascontiguousarray(cs, np.int32)
+    ci = np.ascontiguousarray(ci if len(ci) else np.zeros(1, np.int32), np.int32)
+    out = np.zeros(max(len(k), 1), np.int32)
+    L = lib()
+    L.orc_features_in_area.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, OGrid, C.c_float, C.c_float, C.c_float,
+                                       C.c_int, C.c_int, C.c_void_p, C.c_int]
+    m = L.orc_features_in_area(_p(k), _p(cs), _p(ci), _ogrid(grid), x, y, r, min_level, max_level, _p(out), len(out))
+    return out[:m]
+
+
+def proj_search(params, grid, queries, qdesc, kps, desc, uright=None, blocked=None):
+    """The sequential restatement of the projection matchers: (nmatches, q_idx, q_dist, owner)."""
+    q = np.ascontiguousarray(queries)
+    assert q.dtype.itemsize == 40
+    qd = np.ascontiguousarray(qdesc, np.uint8).reshape(-1, 32)
+    k = np.ascontiguousarray(kps, KP_DTYPE)
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    cs, ci = grid_assign(k, grid)
+    ci = np.ascontiguousarray(ci if len(ci) else np.zeros(1, np.int32), np.int32)
+    P = OParams()
+    P.mode, P.accept_max, P.nnratio, P.check_ori, P.nlevels = (params.mode, params.accept_max, params.nnratio,
+                                                                 params.check_ori, params.nlevels)
+    for i in range(32):
+        P.inv_sigma2[i] = params.inv_sigma2[i]
+    nq, n = len(q), len(k)
+    qi, qdist = np.zeros(max(nq, 1), np.int32), np.zeros(max(nq, 1), np.int32)
+    own = np.zeros(max(n, 1), np.int32)
+    ur = None if uright is None else np.ascontiguousarray(uright, np.float32)
+    bl = None if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+    L = lib()
+    L.orc_proj_search.argtypes = [OParams, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_int, OGrid, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    nm = L.orc_proj_search(P, _p(q), _p(qd), nq, _p(k), _p(d), None if ur is None else _p(ur),
+                           None if bl is None else _p(bl), n, _ogrid(grid), _p(cs), _p(ci), _p(qi), _p(qdist), _p(own))
+    if params.mode > 3:
+        own[:] = -1
+    return nm, qi[:nq], qdist[:nq], own[:n]

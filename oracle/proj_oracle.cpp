@@ -1,0 +1,265 @@
+// =====================================================================================================
+// proj_oracle.cpp — TEST INFRASTRUCTURE ONLY (the checker; never on the product path).
+//
+// Scalar restatement of the keypoint grid and the projection / radius matchers of the reference
+// (SURVEY §8f row 2), line by line in the reference's loop order, over flat arrays:
+//   Frame::AssignFeaturesToGrid / PosInGrid           src/Frame.cc:230-245, :382-392
+//   Frame::GetFeaturesInArea                          src/Frame.cc:327-380
+//   KeyFrame::GetFeaturesInArea                       src/KeyFrame.cc:589-628
+//   ORBmatcher::SearchByProjection(Frame&, vpMapPoints, th)            src/ORBmatcher.cc:45-131
+//   ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)    src/ORBmatcher.cc:1330-1472
+//   ORBmatcher::SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist) src/ORBmatcher.cc:1474-1601
+//   ORBmatcher::SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th) src/ORBmatcher.cc:292-405
+//   ORBmatcher::Fuse(KeyFrame*, vpMapPoints, th) — the search   src/ORBmatcher.cc:894-951
+//   ORBmatcher::Fuse(KeyFrame*, Scw, ...) — the search          src/ORBmatcher.cc:1053-1081
+//   ORBmatcher::SearchBySim3 — each direction's search          src/ORBmatcher.cc:1193-1226, 1273-1306
+//   ORBmatcher::SearchForInitialization                         src/ORBmatcher.cc:407-522
+// The projection arithmetic before each search (cv::Mat products, PredictScale) is the caller's: a query
+// carries the window the reference passes to GetFeaturesInArea and the values its inner loop tests.
+// Struct layouts are identical to orbx_grid / orbx_proj_query / orbx_proj_params (include/orbx.h).
+// Compiled with -ffp-contract=off (oracle/Makefile): float expressions evaluate as written.
+// =====================================================================================================
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+namespace {
+
+struct Kp { float x, y, size, angle, response; int32_t octave, class_id; };   // cv::KeyPoint (28 B)
+
+int hamming(const uint8_t* a, const uint8_t* b) {   // ORBmatcher::DescriptorDistance (ORBmatcher.cc:1649-1665)
+    int d = 0;
+    for (int i = 0; i < 8; ++i) {
+        uint32_t x, y;
+        std::memcpy(&x, a + 4 * i, 4);
+        std::memcpy(&y, b + 4 * i, 4);
+        uint32_t v = x ^ y;
+        v = v - ((v >> 1) & 0x55555555u);
+        v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
+        d += (int)((((v + (v >> 4)) & 0x0F0F0F0Fu) * 0x01010101u) >> 24);
+    }
+    return d;
+}
+
+void three_maxima(const int* h, int L, int& i1, int& i2, int& i3) {   // ORBmatcher.cc:1603-1644
+    int m1 = 0, m2 = 0, m3 = 0;
+    i1 = i2 = i3 = -1;
+    for (int i = 0; i < L; ++i) {
+        const int s = h[i];
+        if (s > m1) { m3 = m2; m2 = m1; m1 = s; i3 = i2; i2 = i1; i1 = i; }
+        else if (s > m2) { m3 = m2; m2 = s; i3 = i2; i2 = i; }
+        else if (s > m3) { m3 = s; i3 = i; }
+    }
+    if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+    else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+}
+
+int rot_bin(float a1, float a2) {   // e.g. ORBmatcher.cc:1435-1440 (factor = 1/HISTO_LENGTH)
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)std::round(rot * (1.0f / 30));
+    if (bin == 30) bin = 0;
+    return bin;
+}
+
+}  // namespace
+
+extern "C" {
+
+struct orc_grid { float min_x, min_y, max_x, max_y, inv_w, inv_h; int32_t cols, rows; };
+struct orc_proj_query {
+    float x, y, r;                 // GetFeaturesInArea(x, y, r, min_level, max_level)
+    int32_t min_level, max_level;
+    float ur, ur_tol, angle;       // stereo right coordinate + tolerance, query keypoint angle
+    int32_t level, flags;
+};
+struct orc_proj_params {
+    int32_t mode, accept_max;
+    float nnratio;
+    int32_t check_ori, nlevels;
+    float inv_sigma2[32];
+};
+enum { ORC_PROJ_MAPPOINTS = 0, ORC_PROJ_LASTFRAME, ORC_PROJ_KEYFRAME, ORC_PROJ_SIM3, ORC_PROJ_FUSE, ORC_PROJ_BEST,
+       ORC_PROJ_INIT };
+enum { ORC_QF_SKIP = 1, ORC_QF_BLOCKS = 2 };
+
+// Frame::AssignFeaturesToGrid with PosInGrid: cell (ix, iy) -> CSR row ix * rows + iy; indices ascending
+// inside a cell (push_back in index order).  Returns the number of keypoints placed.
+int orc_grid_assign(const Kp* k, int n, orc_grid g, int32_t* cell_start, int32_t* cell_idx) {
+    std::vector<std::vector<int>> cells((size_t)g.cols * g.rows);
+    for (int i = 0; i < n; ++i) {
+        const int px = (int)std::round((k[i].x - g.min_x) * g.inv_w);
+        const int py = (int)std::round((k[i].y - g.min_y) * g.inv_h);
+        if (px < 0 || px >= g.cols || py < 0 || py >= g.rows) continue;
+        cells[(size_t)px * g.rows + py].push_back(i);
+    }
+    int o = 0;
+    for (size_t c = 0; c < cells.size(); ++c) {
+        cell_start[c] = o;
+        for (int i : cells[c]) cell_idx[o++] = i;
+    }
+    cell_start[cells.size()] = o;
+    return o;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Frame::GetFeaturesInArea; the KeyFrame version walks the same cells without a level test, and its callers
+// test the level inside their own loop (same candidate order), so they pass their level range here.
+void features_in_area(const Kp* k, const int32_t* cs, const int32_t* ci, const orc_grid& g, float x, float y, float r,
+                      int minLevel, int maxLevel, std::vector<int>& out) {
+    out.clear();
+    const int nMinCellX = std::max(0, (int)std::floor((x - g.min_x - r) * g.inv_w));
+    if (nMinCellX >= g.cols) return;
+    const int nMaxCellX = std::min(g.cols - 1, (int)std::ceil((x - g.min_x + r) * g.inv_w));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = std::max(0, (int)std::floor((y - g.min_y - r) * g.inv_h));
+    if (nMinCellY >= g.rows) return;
+    const int nMaxCellY = std::min(g.rows - 1, (int)std::ceil((y - g.min_y + r) * g.inv_h));
+    if (nMaxCellY < 0) return;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix)
+        for (int iy = nMinCellY; iy <= nMaxCellY; ++iy) {
+            const int c = ix * g.rows + iy;
+            for (int j = cs[c]; j < cs[c + 1]; ++j) {
+                const Kp& kp = k[ci[j]];
+                if (bCheckLevels) {
+                    if (kp.octave < minLevel) continue;
+                    if (maxLevel >= 0 && kp.octave > maxLevel) continue;
+                }
+                const float distx = kp.x - x, disty = kp.y - y;
+                if (std::fabs(distx) < r && std::fabs(disty) < r) out.push_back(ci[j]);
+            }
+        }
+}
+
+}  // namespace
+
+extern "C" {
+
+int orc_features_in_area(const Kp* k, const int32_t* cs, const int32_t* ci, orc_grid g, float x, float y, float r,
+                         int minLevel, int maxLevel, int32_t* out, int cap) {
+    std::vector<int> v;
+    features_in_area(k, cs, ci, g, x, y, r, minLevel, maxLevel, v);
+    for (size_t i = 0; i < v.size() && (int)i < cap; ++i) out[i] = v[i];
+    return (int)v.size();
+}
+
+// All modes as one sequential walk over the queries in order.  blocked0[idx] != 0: the target keypoint
+// already holds a MapPoint that excludes it (MAPPOINTS/LASTFRAME: Observations() > 0; KEYFRAME: any MapPoint;
+// SIM3: vpMatched[idx]).  A query with ORC_QF_BLOCKS excludes the keypoint it is assigned to from later
+// queries (MAPPOINTS/LASTFRAME: the assigned MapPoint has observations; KEYFRAME/SIM3: always).
+// Outputs: q_idx/q_dist per query (accepted candidate, -1 if none; INIT: vnMatches12 after stealing and the
+// rotation filter); owner[idx] (modes MAPPOINTS..SIM3): -1 untouched, q = MapPoint of query q (last
+// writer), -2 = set to NULL by the rotation filter.  Returns nmatches as the reference counts it.
+int orc_proj_search(orc_proj_params P, const orc_proj_query* Q, const uint8_t* qd, int nq, const Kp* k,
+                    const uint8_t* kd, const float* uright, const uint8_t* blocked0, int n, orc_grid g,
+                    const int32_t* cs, const int32_t* ci, int32_t* q_idx, int32_t* q_dist, int32_t* owner) {
+    const int mode = P.mode;
+    const bool assigning = mode <= ORC_PROJ_SIM3;
+    const bool rot_mode = P.check_ori && (mode == ORC_PROJ_LASTFRAME || mode == ORC_PROJ_KEYFRAME || mode == ORC_PROJ_INIT);
+    std::vector<int> own(n, -1), ownBlocks(n, 0), matchedDist(n, INT_MAX), m21(n, -1);
+    std::vector<int> cand;
+    std::vector<std::pair<int, int>> rot;   // (bin, entry): rotHist[bin].push_back(entry) in acceptance order
+    int nm = 0;
+    for (int q = 0; q < nq; ++q) {
+        q_idx[q] = -1;
+        q_dist[q] = -1;
+    }
+    for (int q = 0; q < nq; ++q) {
+        const orc_proj_query& Qq = Q[q];
+        if (Qq.flags & ORC_QF_SKIP) continue;
+        features_in_area(k, cs, ci, g, Qq.x, Qq.y, Qq.r, Qq.min_level, Qq.max_level, cand);
+        if (cand.empty()) continue;
+        const uint8_t* d = qd + 32 * (size_t)q;
+        int bestDist = 256, bestIdx = -1, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1;
+        if (mode == ORC_PROJ_INIT || mode == ORC_PROJ_BEST) bestDist = bestDist2 = INT_MAX;
+        for (int idx : cand) {
+            const Kp& kp = k[idx];
+            if (assigning) {
+                if (blocked0 && blocked0[idx]) continue;
+                if (own[idx] >= 0 && ownBlocks[idx]) continue;
+            }
+            if ((mode == ORC_PROJ_MAPPOINTS || mode == ORC_PROJ_LASTFRAME) && uright && Qq.ur_tol >= 0 && uright[idx] > 0) {
+                const float er = std::fabs(Qq.ur - uright[idx]);   // :93-97, :1409-1415
+                if (er > Qq.ur_tol) continue;
+            }
+            if (mode == ORC_PROJ_FUSE) {                           // :916-940
+                const float ex = Qq.x - kp.x, ey = Qq.y - kp.y;
+                if (uright && uright[idx] >= 0) {
+                    const float er = Qq.ur - uright[idx];
+                    const float e2 = ex * ex + ey * ey + er * er;
+                    if (e2 * P.inv_sigma2[kp.octave] > 7.8) continue;
+                } else {
+                    const float e2 = ex * ex + ey * ey;
+                    if (e2 * P.inv_sigma2[kp.octave] > 5.99) continue;
+                }
+            }
+            const int dist = hamming(d, kd + 32 * (size_t)idx);
+            if (mode == ORC_PROJ_INIT && matchedDist[idx] <= dist) continue;   // :446-447
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestLevel2 = bestLevel;
+                bestDist = dist;
+                bestLevel = kp.octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = kp.octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestIdx < 0 || bestDist > P.accept_max) continue;
+        if (mode == ORC_PROJ_MAPPOINTS && bestLevel == bestLevel2 && (float)bestDist > P.nnratio * (float)bestDist2) continue;
+        if (mode == ORC_PROJ_INIT && !((float)bestDist < (float)bestDist2 * P.nnratio)) continue;
+        q_idx[q] = bestIdx;
+        q_dist[q] = bestDist;
+        ++nm;
+        if (assigning) {
+            own[bestIdx] = q;
+            ownBlocks[bestIdx] = (Qq.flags & ORC_QF_BLOCKS) ? 1 : 0;
+        }
+        if (mode == ORC_PROJ_INIT) {                               // :465-473
+            if (m21[bestIdx] >= 0) {
+                q_idx[m21[bestIdx]] = -1;
+                --nm;
+            }
+            m21[bestIdx] = q;
+            matchedDist[bestIdx] = bestDist;
+        }
+        if (rot_mode) rot.push_back({rot_bin(Qq.angle, k[bestIdx].angle), mode == ORC_PROJ_INIT ? q : bestIdx});
+    }
+    if (rot_mode) {                                                // :1449-1469, :1579-1598, :491-514
+        int hist[30] = {0};
+        for (auto& e : rot) hist[e.first]++;
+        int i1, i2, i3;
+        three_maxima(hist, 30, i1, i2, i3);
+        for (int b = 0; b < 30; ++b) {
+            if (b == i1 || b == i2 || b == i3) continue;
+            for (auto& e : rot) {
+                if (e.first != b) continue;
+                if (mode == ORC_PROJ_INIT) {
+                    if (q_idx[e.second] >= 0) {
+                        q_idx[e.second] = -1;
+                        --nm;
+                    }
+                } else {
+                    own[e.second] = -2;                            // CurrentFrame.mvpMapPoints[...] = NULL
+                    --nm;
+                }
+            }
+        }
+    }
+    for (int q = 0; q < nq; ++q)
+        if (q_idx[q] < 0) q_dist[q] = -1;   // stolen (INIT) or filtered entries carry no distance
+    if (owner)
+        for (int i = 0; i < n; ++i) owner[i] = own[i];
+    return nm;
+}
+
+}  // extern "C"

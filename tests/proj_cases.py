@@ -1,0 +1,263 @@
+"""Seeded test cases for the projection / radius matchers and a pure-Python
+restatement of the reference's sequential loops (src/ORBmatcher.cc, src/Frame.cc) used to check the
+C++ oracle on small cases.  No reference code or data is copied: cases are synthetic keypoint sets whose
+queries are perturbed copies of target keypoints (true matches), distractors, and dense conflicts."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from multiagent_orb_slam2_amd.orbx import (KP_DTYPE, PROJ_BEST, PROJ_FUSE, PROJ_INIT, PROJ_KEYFRAME, PROJ_LASTFRAME,
+                                           PROJ_MAPPOINTS, PROJ_QUERY_DTYPE, PROJ_SIM3, QF_BLOCKS, QF_SKIP, ProjParams,
+                                           frame_grid)
+
+SCALE = np.array([1.2 ** i for i in range(8)], np.float32)
+INV_SIGMA2 = (np.float32(1) / (SCALE * SCALE)).astype(np.float32)
+MODES = {"mappoints": PROJ_MAPPOINTS, "lastframe": PROJ_LASTFRAME, "keyframe": PROJ_KEYFRAME, "sim3": PROJ_SIM3,
+         "fuse": PROJ_FUSE, "best": PROJ_BEST, "init": PROJ_INIT}
+
+
+def make_case(seed: int, mode: int, n_target: int = 400, n_query: int = 300, W: int = 640, H: int = 480,
+              dense: bool = False, check_ori: bool = True):
+    """Target view (keypoints, descriptors, uright, blocked) + queries + params for one mode."""
+    rng = np.random.default_rng(seed)
+    if dense:
+        n_target = max(8, n_target // 6)
+    k = np.zeros(n_target, KP_DTYPE)
+    k["x"] = rng.uniform(-4, W + 4, n_target).astype(np.float32)        # a few fall outside the grid
+    k["y"] = rng.uniform(-4, H + 4, n_target).astype(np.float32)
+    k["octave"] = np.minimum(rng.geometric(0.45, n_target) - 1, 7)
+    k["angle"] = rng.uniform(0, 360, n_target).astype(np.float32)
+    k["size"] = 31 * SCALE[k["octave"]]
+    k["response"] = rng.integers(7, 120, n_target)
+    k["class_id"] = -1
+    if dense:   # many keypoints in a few places -> many queries per window
+        c = rng.integers(0, 6, n_target)
+        k["x"] = (W * (0.15 + 0.14 * c) + rng.normal(0, 6, n_target)).astype(np.float32)
+        k["y"] = (H * 0.5 + rng.normal(0, 6, n_target)).astype(np.float32)
+    desc = rng.integers(0, 256, (n_target, 32), dtype=np.uint8)
+    uright = np.where(rng.random(n_target) < 0.5, k["x"] - rng.uniform(0, 40, n_target), -1).astype(np.float32)
+    uright[rng.random(n_target) < 0.05] = 0.0                            # uright == 0: neither > 0 nor < 0
+    blocked = (rng.random(n_target) < 0.15).astype(np.uint8)
+
+    q = np.zeros(n_query, PROJ_QUERY_DTYPE)
+    qd = rng.integers(0, 256, (n_query, 32), dtype=np.uint8)
+    tgt = rng.integers(0, n_target, n_query)
+    true = rng.random(n_query) < (0.9 if dense else 0.7)
+    lvl = np.where(true, k["octave"][tgt], rng.integers(0, 8, n_query)).astype(np.int32)
+    lvl = np.clip(lvl + rng.integers(-1, 2, n_query) * (rng.random(n_query) < 0.2), 0, 7).astype(np.int32)
+    q["x"] = np.where(true, k["x"][tgt] + rng.normal(0, 2, n_query), rng.uniform(0, W, n_query)).astype(np.float32)
+    q["y"] = np.where(true, k["y"][tgt] + rng.normal(0, 2, n_query), rng.uniform(0, H, n_query)).astype(np.float32)
+    flips = (rng.random((n_query, 32)) < 0.03) * rng.integers(1, 256, (n_query, 32))
+    qd = np.where(true[:, None], desc[tgt] ^ flips.astype(np.uint8), qd).astype(np.uint8)
+    dup = rng.random(n_query) < 0.1                                      # exact duplicates -> ties
+    qd[dup] = desc[tgt[dup]]
+    q["angle"] = np.where(rng.random(n_query) < 0.8, k["angle"][tgt] + rng.normal(0, 4, n_query),
+                          rng.uniform(0, 360, n_query)).astype(np.float32) % np.float32(360)
+    q["ur"] = np.where(uright[tgt] > 0, uright[tgt] + rng.normal(0, 1.5, n_query), q["x"] - 10).astype(np.float32)
+    q["ur_tol"] = -1
+    q["level"] = lvl
+    flags = np.where(rng.random(n_query) < 0.08, QF_SKIP, 0) | np.where(rng.random(n_query) < 0.8, QF_BLOCKS, 0)
+    th = {PROJ_MAPPOINTS: 4.0, PROJ_LASTFRAME: 7.0, PROJ_KEYFRAME: 10.0, PROJ_SIM3: 10.0, PROJ_FUSE: 3.0,
+          PROJ_BEST: 7.5, PROJ_INIT: 30.0}[mode]
+    q["r"] = (np.float32(th) * SCALE[lvl]).astype(np.float32)
+    q["min_level"], q["max_level"] = lvl - 1, lvl
+    if mode == PROJ_MAPPOINTS:
+        q["ur_tol"] = q["r"]
+    elif mode == PROJ_LASTFRAME:
+        kind = rng.integers(0, 3, n_query)           # :1387-1392 forward / backward / both
+        q["min_level"] = np.where(kind == 0, lvl, np.where(kind == 1, 0, lvl - 1))
+        q["max_level"] = np.where(kind == 0, -1, np.where(kind == 1, lvl, lvl + 1))
+        q["ur_tol"] = q["r"]
+    elif mode == PROJ_KEYFRAME:
+        q["min_level"], q["max_level"] = lvl - 1, lvl + 1
+        flags |= QF_BLOCKS
+    elif mode == PROJ_SIM3:
+        flags |= QF_BLOCKS
+    elif mode == PROJ_INIT:
+        q["min_level"], q["max_level"] = 0, 0
+        q["r"] = np.float32(th)
+        flags = np.where(lvl > 0, QF_SKIP, 0)
+    q["flags"] = flags
+    accept = {PROJ_MAPPOINTS: 100, PROJ_LASTFRAME: 100, PROJ_KEYFRAME: 64, PROJ_SIM3: 50, PROJ_FUSE: 50,
+              PROJ_BEST: 100, PROJ_INIT: 50}[mode]
+    nnratio = {PROJ_MAPPOINTS: 0.8, PROJ_INIT: 0.9}.get(mode, 0.6)
+    params = ProjParams.make(mode, accept, nnratio, check_ori and mode in (PROJ_LASTFRAME, PROJ_KEYFRAME, PROJ_INIT),
+                             INV_SIGMA2)
+    grid = frame_grid(0.0, 0.0, float(W), float(H))
+    return dict(params=params, grid=grid, queries=q, qdesc=qd, kps=k, desc=desc, uright=uright,
+                blocked=blocked if mode <= PROJ_SIM3 else None)
+
+
+# --------------------------------------------------------------------------------------------------
+# pure-Python restatement (float32 arithmetic via numpy scalars), small cases only
+# --------------------------------------------------------------------------------------------------
+f32 = np.float32
+
+
+def _round_away(v) -> int:                   # std::round: half away from zero
+    v = float(v)
+    return int(math.floor(v + 0.5)) if v >= 0 else -int(math.floor(-v + 0.5))
+
+
+def py_grid(kps, g):
+    cells = [[] for _ in range(g.cols * g.rows)]
+    for i, kp in enumerate(kps):
+        px = _round_away(f32(f32(kp["x"]) - f32(g.min_x)) * f32(g.inv_w))
+        py = _round_away(f32(f32(kp["y"]) - f32(g.min_y)) * f32(g.inv_h))
+        if 0 <= px < g.cols and 0 <= py < g.rows:
+            cells[px * g.rows + py].append(i)
+    return cells
+
+
+def py_features_in_area(kps, cells, g, x, y, r, min_level, max_level):
+    x, y, r = f32(x), f32(y), f32(r)
+    nminx = max(0, int(math.floor(f32(f32(f32(x - f32(g.min_x)) - r) * f32(g.inv_w)))))
+    if nminx >= g.cols:
+        return []
+    nmaxx = min(g.cols - 1, int(math.ceil(f32(f32(f32(x - f32(g.min_x)) + r) * f32(g.inv_w)))))
+    if nmaxx < 0:
+        return []
+    nminy = max(0, int(math.floor(f32(f32(f32(y - f32(g.min_y)) - r) * f32(g.inv_h)))))
+    if nminy >= g.rows:
+        return []
+    nmaxy = min(g.rows - 1, int(math.ceil(f32(f32(f32(y - f32(g.min_y)) + r) * f32(g.inv_h)))))
+    if nmaxy < 0:
+        return []
+    check = min_level > 0 or max_level >= 0
+    out = []
+    for ix in range(nminx, nmaxx + 1):
+        for iy in range(nminy, nmaxy + 1):
+            for i in cells[ix * g.rows + iy]:
+                kp = kps[i]
+                if check:
+                    if kp["octave"] < min_level:
+                        continue
+                    if max_level >= 0 and kp["octave"] > max_level:
+                        continue
+                if abs(f32(f32(kp["x"]) - x)) < r and abs(f32(f32(kp["y"]) - y)) < r:
+                    out.append(i)
+    return out
+
+
+def _ham(a, b):
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+def _rot_bin(a1, a2):
+    rot = f32(f32(a1) - f32(a2))
+    if rot < 0:
+        rot = f32(rot + f32(360))
+    b = _round_away(f32(rot * f32(f32(1) / f32(30))))
+    return 0 if b == 30 else b
+
+
+def _three_maxima(h):
+    m1 = m2 = m3 = 0
+    i1 = i2 = i3 = -1
+    for i, s in enumerate(h):
+        if s > m1:
+            m3, m2, m1, i3, i2, i1 = m2, m1, s, i2, i1, i
+        elif s > m2:
+            m3, m2, i3, i2 = m2, s, i2, i
+        elif s > m3:
+            m3, i3 = s, i
+    if m2 < f32(0.1) * f32(m1):
+        i2 = i3 = -1
+    elif m3 < f32(0.1) * f32(m1):
+        i3 = -1
+    return i1, i2, i3
+
+
+def py_proj_search(c):
+    """The reference's loops (ORBmatcher.cc :45-131, :292-405, :407-522, :894-951, :1053-1081, :1330-1472,
+    :1474-1601) on a case from make_case."""
+    P, g, Q, qd, k, d = c["params"], c["grid"], c["queries"], c["qdesc"], c["kps"], c["desc"]
+    ur, bl = c["uright"], c["blocked"]
+    mode = P.mode
+    n, nq = len(k), len(Q)
+    cells = py_grid(k, g)
+    own, own_blocks = [-1] * n, [0] * n
+    mdist, m21 = [2 ** 31 - 1] * n, [-1] * n
+    q_idx, q_dist = [-1] * nq, [-1] * nq
+    rot_mode = P.check_ori and mode in (PROJ_LASTFRAME, PROJ_KEYFRAME, PROJ_INIT)
+    rot = []
+    nm = 0
+    big = 2 ** 31 - 1
+    for qi in range(nq):
+        q = Q[qi]
+        if q["flags"] & QF_SKIP:
+            continue
+        cand = py_features_in_area(k, cells, g, q["x"], q["y"], q["r"], int(q["min_level"]), int(q["max_level"]))
+        if not cand:
+            continue
+        init = big if mode in (PROJ_INIT, PROJ_BEST) else 256
+        bd, bi, bl1, bd2, bl2 = init, -1, -1, init, -1
+        for idx in cand:
+            kp = k[idx]
+            if mode <= PROJ_SIM3:
+                if bl is not None and bl[idx]:
+                    continue
+                if own[idx] >= 0 and own_blocks[idx]:
+                    continue
+            if mode in (PROJ_MAPPOINTS, PROJ_LASTFRAME) and ur is not None and q["ur_tol"] >= 0 and ur[idx] > 0:
+                if abs(f32(f32(q["ur"]) - f32(ur[idx]))) > f32(q["ur_tol"]):
+                    continue
+            if mode == PROJ_FUSE:
+                ex, ey = f32(f32(q["x"]) - f32(kp["x"])), f32(f32(q["y"]) - f32(kp["y"]))
+                if ur is not None and ur[idx] >= 0:
+                    er = f32(f32(q["ur"]) - f32(ur[idx]))
+                    e2 = f32(f32(f32(ex * ex) + f32(ey * ey)) + f32(er * er))
+                    if float(f32(e2 * f32(P.inv_sigma2[int(kp["octave"])]))) > 7.8:
+                        continue
+                else:
+                    e2 = f32(f32(ex * ex) + f32(ey * ey))
+                    if float(f32(e2 * f32(P.inv_sigma2[int(kp["octave"])]))) > 5.99:
+                        continue
+            dist = _ham(qd[qi], d[idx])
+            if mode == PROJ_INIT and mdist[idx] <= dist:
+                continue
+            if dist < bd:
+                bd2, bl2, bd, bl1, bi = bd, bl1, dist, int(kp["octave"]), idx
+            elif dist < bd2:
+                bl2, bd2 = int(kp["octave"]), dist
+        if bi < 0 or bd > P.accept_max:
+            continue
+        if mode == PROJ_MAPPOINTS and bl1 == bl2 and f32(bd) > f32(f32(P.nnratio) * f32(bd2)):
+            continue
+        if mode == PROJ_INIT and not (f32(bd) < f32(f32(bd2) * f32(P.nnratio))):
+            continue
+        q_idx[qi], q_dist[qi] = bi, bd
+        nm += 1
+        if mode <= PROJ_SIM3:
+            own[bi], own_blocks[bi] = qi, 1 if q["flags"] & QF_BLOCKS else 0
+        if mode == PROJ_INIT:
+            if m21[bi] >= 0:
+                q_idx[m21[bi]] = -1
+                nm -= 1
+            m21[bi], mdist[bi] = qi, bd
+        if rot_mode:
+            rot.append((_rot_bin(q["angle"], k[bi]["angle"]), qi if mode == PROJ_INIT else bi))
+    if rot_mode:
+        hist = [0] * 30
+        for b, _ in rot:
+            hist[b] += 1
+        keep = _three_maxima(hist)
+        for b in range(30):
+            if b in keep:
+                continue
+            for bb, e in rot:
+                if bb != b:
+                    continue
+                if mode == PROJ_INIT:
+                    if q_idx[e] >= 0:
+                        q_idx[e] = -1
+                        nm -= 1
+                else:
+                    own[e] = -2
+                    nm -= 1
+    if mode > PROJ_SIM3:
+        own = [-1] * n
+    q_dist = [dd if ii >= 0 else -1 for ii, dd in zip(q_idx, q_dist)]
+    return nm, np.array(q_idx, np.int32), np.array(q_dist, np.int32), np.array(own, np.int32)
