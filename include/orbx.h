@@ -360,6 +360,69 @@ int orbx_vocab_transform_batch_device(orbx_vocab* v, const uint8_t* d_desc, cons
                                       int32_t* d_n_words, uint32_t* d_fv_nodes, int32_t* d_fv_offsets,
                                       int32_t* d_fv_indices, int32_t* d_n_fv_nodes, void* stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * Keyframe database — replaces KeyFrameDatabase (src/KeyFrameDatabase.cc) and ORBVocabulary::score
+ * (DBoW2 L1Scoring, Thirdparty/DBoW2/DBoW2/ScoringObject.cpp:23-66).  SURVEY §8f row 4: the inverted-
+ * file candidate search that precedes every cross-agent SearchByBoW.
+ *
+ * A database is a table of max_slots keyframe slots.  A slot holds the keyframe's BowVector (word ids
+ * ascending, DBoW2 values), its GetBestCovisibilityKeyFrames(10) list (src/KeyFrame.cc:189-197) and, per
+ * query kind, the scratch fields the reference keeps on KeyFrame: mn*Query, mn*Words, m*Score
+ * (include/KeyFrame.h:155-163; the scores are never initialised by the reference: here they start at 0
+ * unless set with orbx_kfdb_set_state).  Membership (add / erase / clear) defines the inverted file.
+ * A query names a slot for its BowVector (a Frame's BowVector for relocalisation goes in a spare slot) and
+ * its id (KeyFrame::mnId / Frame::mnId).  Only L1 scoring is implemented (ORBvoc.txt: "10 6 0 0").
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct orbx_kfdb orbx_kfdb;
+
+enum {
+    ORBX_KFDB_LOOP = 0,   /* DetectLoopCandidates (src/KeyFrameDatabase.cc:76-197): exclusions = GetConnectedKeyFrames() */
+    ORBX_KFDB_COVIS = 1,  /* DetectCovisibilityCandidates (:199-308): exclusions = vpKFsToIgnore */
+    ORBX_KFDB_RELOC = 2   /* DetectRelocalizationCandidates (:310-420): no exclusions, no minScore */
+};
+
+/* KeyFrameDatabase(voc) (:33-37): n_vocab_words = voc.size(); max_words <= 4096 BowVector entries per slot. */
+int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device, orbx_kfdb** out);
+int orbx_kfdb_destroy(orbx_kfdb* db);
+int orbx_kfdb_info(const orbx_kfdb* db, int* n_vocab_words, int* max_slots, int* max_words, int* n_members);
+/* Store a slot's BowVector (KeyFrame::mBowVec); word ids strictly ascending and < n_vocab_words. */
+int orbx_kfdb_set_bow(orbx_kfdb* db, int slot, const uint32_t* words, const double* values, int n);
+/* Device form: BowVector i of an orbx_vocab_transform_batch_device output (words/values at i*stride,
+ * d_n_words[i]) into slot d_slots[i], for i < n.  Word ids must satisfy the rules above. */
+int orbx_kfdb_set_bow_device(orbx_kfdb* db, const int32_t* d_slots, int n, const uint32_t* d_words, const double* d_values,
+                             const int32_t* d_n_words, int stride, void* stream);
+/* GetBestCovisibilityKeyFrames(10) of slots[i]: best[i*10 .. i*10+9], best first, -1 padded. */
+int orbx_kfdb_set_covisibility(orbx_kfdb* db, const int32_t* slots, int n, const int32_t* best);
+/* KeyFrameDatabase::add (:40-46) in order (adding a slot already in the database is ORBX_ERR_ARG),
+ * erase (:48-67; slots not in the database are ignored), clear (:69-73). */
+int orbx_kfdb_add(orbx_kfdb* db, const int32_t* slots, int n);
+int orbx_kfdb_erase(orbx_kfdb* db, const int32_t* slots, int n);
+int orbx_kfdb_clear(orbx_kfdb* db);
+/* The scratch fields of one query kind for all max_slots slots. */
+int orbx_kfdb_get_state(orbx_kfdb* db, int kind, uint64_t* query, int32_t* words, float* score);
+int orbx_kfdb_set_state(orbx_kfdb* db, int kind, const uint64_t* query, const int32_t* words, const float* score);
+/* ORBVocabulary::score(bow[pairs[2i]], bow[pairs[2i+1]]) (first = v1), e.g. the minScore bound of
+ * src/MapFusion.cc:800-815 and src/LoopClosing.cc DetectLoop. */
+int orbx_kfdb_score(orbx_kfdb* db, const int32_t* pairs, int n, double* scores);
+int orbx_kfdb_score_device(orbx_kfdb* db, const int32_t* d_pairs, int n, double* d_scores, void* stream);
+/* nq queries of one kind, evaluated in order as the reference would evaluate them one after another.
+ * min_scores[q]: minScore (ignored for RELOC, may be NULL).  Exclusions of query q:
+ * excl_slots[excl_offsets[q] .. excl_offsets[q+1]) (excl_offsets NULL = none).  Candidates of query q:
+ * out[out_offsets[q] .. out_offsets[q+1]) in the reference's order; ORBX_ERR_CAPACITY if out_cap is too
+ * small or a query retains more than 2048 candidates. */
+int orbx_kfdb_detect(orbx_kfdb* db, int kind, const int32_t* query_slots, const uint64_t* query_ids, const float* min_scores,
+                     int nq, const int32_t* excl_offsets, const int32_t* excl_slots, int32_t* out_offsets, int32_t* out,
+                     int out_cap);
+/* Device form (device pointers, no synchronisation).  Outputs: d_out[q*out_stride ...], d_out_n[q];
+ * *d_status |= 2 when a query exceeds out_stride or 2048 retained candidates, |= 1 when the queries of the
+ * batch interact through the scratch fields (a query id equal to one already recorded in a slot another
+ * query of the batch updates, or repeated ids): then the results are not the sequential ones and the
+ * batch must be re-run one query at a time on restored state (orbx_kfdb_detect does this itself).
+ * Distinct, fresh query ids (monotonic mnId, as in the reference) never interact. */
+int orbx_kfdb_detect_device(orbx_kfdb* db, int kind, const int32_t* d_query_slots, const uint64_t* d_query_ids,
+                            const float* d_min_scores, int nq, const int32_t* d_excl_offsets, const int32_t* d_excl_slots,
+                            int32_t* d_out, int out_stride, int32_t* d_out_n, int32_t* d_status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,938 @@
+// =====================================================================================================
+// orbx_kfdb.hip — keyframe database (DBoW2 inverted file) queries on gfx950.
+//
+// Replaces KeyFrameDatabase (src/KeyFrameDatabase.cc): add / erase / clear (:40-73) and the three
+// candidate queries that precede every SearchByBoW of the cross-agent path:
+//   DetectLoopCandidates            :76-197   LoopClosing::DetectLoop (src/LoopClosing.cc:164),
+//                                             MapFusion's fusion detection (src/MapFusion.cc:133)
+//   DetectCovisibilityCandidates    :199-308  MapFusion covisibility discovery (src/MapFusion.cc:820)
+//   DetectRelocalizationCandidates  :310-420  Tracking::Relocalization (src/Tracking.cc:1366)
+// and ORBVocabulary::score (DBoW2 L1Scoring, Thirdparty/DBoW2/DBoW2/ScoringObject.cpp:23-66), which
+// the callers also use directly for the minimum-score bound (src/MapFusion.cc:800-815).
+//
+// The database is a table of keyframe slots.  A slot holds a BowVector (word ids ascending, double
+// values), its GetBestCovisibilityKeyFrames(10) list (src/KeyFrame.cc:189-197) and the per-keyframe
+// scratch fields the reference keeps on KeyFrame (mnLoopQuery/mnLoopWords/mLoopScore and the Covis /
+// Reloc triples, include/KeyFrame.h:155-163): results then equal the reference's even when a query
+// id repeats and stale fields are read (the reference reads mCovisScore, which nothing assigns).
+//
+// Reference order -> data-parallel form.  The reference walks the query's words in ascending order and,
+// per word, the inverted list in add order, pushing each keyframe at its first encounter.  The list
+// order is therefore the order of (position of the first shared query word, add sequence number), a
+// key every keyframe computes independently; all other steps are per-keyframe (word count, L1 score,
+// covisibility accumulation) or order-free reductions (max).  Kernels per query batch:
+//   k_kfdb_share    one thread per (query word): walk the word's inverted list, atomic word count and
+//                   atomic-min first position per keyframe slot
+//   k_kfdb_select   one workgroup per query: list membership from the scratch fields, max common words,
+//                   compaction of the keyframes to score
+//   k_kfdb_score    query BowVector staged in LDS; one wave per scored keyframe walks its words, finds
+//                   the common ones by binary search in LDS and adds the L1 terms in ascending word order
+//                   (sequential scalar double adds, exactly DBoW2's summation order)
+//   k_kfdb_accum    one workgroup per query: covisibility accumulation, best-score retention, LDS
+//                   bitonic sort by the reference's list key, first-occurrence de-duplication
+//   k_kfdb_state    one thread per slot: applies the queries' updates to the scratch fields in query
+//                   order and flags a batch whose queries interact through them (then the host form
+//                   re-runs the batch one query at a time)
+// The inverted file (CSR word -> slots) is rebuilt on the device when membership changed: count,
+// exclusive scan over the vocabulary, scatter.
+// =====================================================================================================
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "orbx_common.h"
+
+namespace orbx {
+
+constexpr int kKfdbCovis = 10;           // GetBestCovisibilityKeyFrames(10)
+constexpr int kKfdbMaxWords = 4096;      // BowVector entries per slot (<= features per keyframe)
+constexpr int kKfdbMaxRetained = 2048;   // retained candidates per query (LDS sort)
+constexpr int kScanChunk = 4096;         // vocabulary entries per scan workgroup (1024 threads x 4)
+constexpr uint32_t kNoSeq = 0xFFFFFFFFu;
+
+enum { KIND_LOOP = ORBX_KFDB_LOOP, KIND_COVIS = ORBX_KFDB_COVIS, KIND_RELOC = ORBX_KFDB_RELOC };
+
+// Per-query scratch, one row of S slots per query (see kfdb_scratch_layout).
+struct QScratch {
+    int32_t* cnt;        // words shared with the query (atomic)
+    int32_t* first;      // position of the first shared query word (atomic min; INT_MAX-ish when none)
+    uint8_t* excl;       // exclusion set of the query (connected / ignored keyframes)
+    float* si;           // L1 score of scored keyframes
+    int32_t* cand;       // compacted scored keyframes (any order)
+    float* acc;          // accumulated score of candidate i (by cand position)
+    int32_t* best;       // best keyframe of candidate i
+    int32_t* meta;       // per query: [0] npushed, [1] minCommon, [2] ncand
+};
+
+struct DbDev {
+    const uint32_t* bw;      // [S][maxw] word ids ascending
+    const double* bv;        // [S][maxw] values
+    const int32_t* bn;       // [S] BowVector sizes
+    const int32_t* covis;    // [S][10] best covisible slots, -1 padded
+    const uint32_t* seq;     // [S] add sequence number, kNoSeq when not in the database
+    const int32_t* if_off;   // [n_vocab + 1]
+    const int32_t* if_slot;  // inverted file entries
+    int S, maxw, n_vocab;
+};
+
+struct StateDev {
+    unsigned long long* q;
+    int32_t* w;
+    float* s;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Inverted file rebuild
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_if_count(DbDev D, const int32_t* __restrict__ members, int32_t* __restrict__ cnt) {
+    const int k = members[blockIdx.x];
+    const int n = D.bn[k];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t w = D.bw[(size_t)k * D.maxw + i];
+        if (w < (uint32_t)D.n_vocab) atomicAdd(&cnt[w], 1);
+    }
+}
+
+// Exclusive scan of n ints in place, pass 1: per-chunk totals.
+__global__ __launch_bounds__(1024) void k_scan_chunks(const int32_t* __restrict__ a, int n, int32_t* __restrict__ sums) {
+    __shared__ int tmp[1024 / kWave + 1];
+    const int b = blockIdx.x * kScanChunk + threadIdx.x * 4;
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += (b + j < n) ? a[b + j] : 0;
+    int total;
+    block_excl_scan(s, tmp, &total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+// Pass 2: one workgroup scans the chunk totals (in place, exclusive).
+__global__ __launch_bounds__(1024) void k_scan_top(int32_t* __restrict__ sums, int nb) {
+    __shared__ int tmp[1024 / kWave + 1];
+    int carry = 0;
+    for (int base = 0; base < nb; base += 1024) {
+        const int i = base + threadIdx.x;
+        const int v = i < nb ? sums[i] : 0;
+        int total;
+        const int ex = block_excl_scan(v, tmp, &total);
+        if (i < nb) sums[i] = carry + ex;
+        carry += total;
+        __syncthreads();
+    }
+}
+
+// Pass 3: chunk-local exclusive scan plus the chunk offset; also writes the scatter cursor.
+__global__ __launch_bounds__(1024) void k_scan_apply(int32_t* __restrict__ a, int n, const int32_t* __restrict__ sums,
+                                                     int32_t* __restrict__ cur) {
+    __shared__ int tmp[1024 / kWave + 1];
+    const int b = blockIdx.x * kScanChunk + threadIdx.x * 4;
+    int v[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = (b + j < n) ? a[b + j] : 0;
+        s += v[j];
+    }
+    int total;
+    int off = block_excl_scan(s, tmp, &total) + sums[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (b + j < n) {
+            a[b + j] = off;
+            if (cur) cur[b + j] = off;
+            off += v[j];
+        }
+}
+
+__global__ __launch_bounds__(256) void k_if_scatter(DbDev D, const int32_t* __restrict__ members, int32_t* __restrict__ cur,
+                                                    int32_t* __restrict__ slot_out) {
+    const int k = members[blockIdx.x];
+    const int n = D.bn[k];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t w = D.bw[(size_t)k * D.maxw + i];
+        if (w < (uint32_t)D.n_vocab) slot_out[atomicAdd(&cur[w], 1)] = k;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_set_bow(DbDev D, uint32_t* __restrict__ bw, double* __restrict__ bv, int32_t* __restrict__ bn,
+                                                 const int32_t* __restrict__ slots, const uint32_t* __restrict__ words,
+                                                 const double* __restrict__ values, const int32_t* __restrict__ n_words,
+                                                 int stride) {
+    const int i = blockIdx.x;
+    const int k = slots[i];
+    if (k < 0 || k >= D.S) return;
+    const int n = min(n_words[i], D.maxw);
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        bw[(size_t)k * D.maxw + j] = words[(size_t)i * stride + j];
+        bv[(size_t)k * D.maxw + j] = values[(size_t)i * stride + j];
+    }
+    if (threadIdx.x == 0) bn[k] = n;
+}
+
+// ---------------------------------------------------------------------------------------------
+// L1 score (DBoW2 L1Scoring::score): score = -(sum over common words, ascending id, of
+// |v - w| - |v| - |w|) / 2 with v from the first vector (the query) and w from the second.
+// One wave; 'q' (the first vector, usually staged in LDS) is searched, 'c' drives the lanes.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, l), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), l);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+__device__ double wave_l1_score(const uint32_t* qw, const double* qv, int nq, const uint32_t* cw, const double* cv, int nc) {
+    double score = 0.0;
+    for (int base = 0; base < nc; base += kWave) {
+        const int i = base + lane_id();
+        double term = 0.0;
+        bool found = false;
+        if (i < nc && nq > 0) {
+            const uint32_t w = cw[i];
+            int lo = 0, hi = nq;                 // lower_bound in the query's words
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (qw[mid] < w) lo = mid + 1; else hi = mid;
+            }
+            if (lo < nq && qw[lo] == w) {
+                const double vi = qv[lo], wi = cv[i];
+                term = __dsub_rn(__dsub_rn(fabs(__dsub_rn(vi, wi)), fabs(vi)), fabs(wi));
+                found = true;
+            }
+        }
+        uint64_t m = __ballot(found);
+        while (m) {
+            const int l = __builtin_ctzll(m);
+            score = __dadd_rn(score, readlane_f64(term, l));
+            m &= m - 1;
+        }
+    }
+    return -score / 2.0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Queries
+// ---------------------------------------------------------------------------------------------
+struct QueryIn {
+    const int32_t* slot;              // [nq] query slots
+    const unsigned long long* id;     // [nq] query ids (KeyFrame::mnId / Frame::mnId)
+    const float* min_score;           // [nq] (LOOP, COVIS)
+    const int32_t* excl_off;          // [nq + 1] or NULL
+    const int32_t* excl;
+};
+
+__global__ __launch_bounds__(256) void k_kfdb_mark_excl(QueryIn Q, QScratch X, int S) {
+    const int q = blockIdx.x;
+    if (!Q.excl_off) return;
+    for (int e = Q.excl_off[q] + threadIdx.x; e < Q.excl_off[q + 1]; e += blockDim.x) {
+        const int k = Q.excl[e];
+        if (k >= 0 && k < S) X.excl[(size_t)q * S + k] = 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_kfdb_share(DbDev D, QueryIn Q, QScratch X, int kind) {
+    const int q = blockIdx.y;
+    const int qs = Q.slot[q];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= D.bn[qs]) return;
+    const uint32_t w = D.bw[(size_t)qs * D.maxw + p];
+    if (w >= (uint32_t)D.n_vocab) return;
+    const size_t row = (size_t)q * D.S;
+    for (int e = D.if_off[w]; e < D.if_off[w + 1]; ++e) {
+        const int k = D.if_slot[e];
+        if (kind == KIND_COVIS && X.excl[row + k]) continue;   // :220 ignored keyframes are skipped
+        atomicAdd(&X.cnt[row + k], 1);
+        atomicMin(&X.first[row + k], p);
+    }
+}
+
+// A keyframe enters lKFsSharingWords when it shares a word, its query field is not already this id
+// (:93 / :221 / :325) and, for loop queries, it is not connected to the query (:96).
+__device__ __forceinline__ bool kf_pushed(int kind, int c, bool stale, bool ex) {
+    return c > 0 && !stale && !(kind == KIND_LOOP && ex);
+}
+
+__global__ __launch_bounds__(1024) void k_kfdb_select(DbDev D, QueryIn Q, QScratch X, StateDev St, int kind) {
+    __shared__ int s_max, s_np, s_nc;
+    const int q = blockIdx.x;
+    const unsigned long long id = Q.id[q];
+    const size_t row = (size_t)q * D.S;
+    if (threadIdx.x == 0) { s_max = 0; s_np = 0; s_nc = 0; }
+    __syncthreads();
+    int mx = 0, np = 0;
+    for (int k = threadIdx.x; k < D.S; k += blockDim.x) {
+        const int c = X.cnt[row + k];
+        if (kf_pushed(kind, c, St.q[k] == id, X.excl[row + k])) {
+            mx = max(mx, c);
+            ++np;
+        }
+    }
+    atomicMax(&s_max, mx);
+    atomicAdd(&s_np, np);
+    __syncthreads();
+    const int minCommon = (int)((float)s_max * 0.8f);          // int minCommonWords = maxCommonWords*0.8f
+    for (int k = threadIdx.x; k < D.S; k += blockDim.x) {
+        const int c = X.cnt[row + k];
+        if (kf_pushed(kind, c, St.q[k] == id, X.excl[row + k]) && c > minCommon) {
+            const int pos = atomicAdd(&s_nc, 1);
+            X.cand[row + pos] = k;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        X.meta[q * 4 + 0] = s_np;
+        X.meta[q * 4 + 1] = minCommon;
+        X.meta[q * 4 + 2] = s_np ? s_nc : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_kfdb_score(DbDev D, QueryIn Q, QScratch X) {
+    extern __shared__ unsigned char smem[];
+    double* qv = reinterpret_cast<double*>(smem);
+    uint32_t* qw = reinterpret_cast<uint32_t*>(qv + D.maxw);
+    const int q = blockIdx.y;
+    const int nc = X.meta[q * 4 + 2];
+    if (nc == 0) return;
+    const int qs = Q.slot[q];
+    const int nq = D.bn[qs];
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+        qw[i] = D.bw[(size_t)qs * D.maxw + i];
+        qv[i] = D.bv[(size_t)qs * D.maxw + i];
+    }
+    __syncthreads();
+    const int waves = blockDim.x / kWave;
+    const size_t row = (size_t)q * D.S;
+    for (int c = blockIdx.x * waves + (int)(threadIdx.x / kWave); c < nc; c += gridDim.x * waves) {
+        const int k = X.cand[row + c];
+        const double s = wave_l1_score(qw, qv, nq, D.bw + (size_t)k * D.maxw, D.bv + (size_t)k * D.maxw, D.bn[k]);
+        if (lane_id() == 0) X.si[row + k] = (float)s;
+    }
+}
+
+// The scratch fields of keyframe n as the reference sees them after this query's word counting.
+struct PostState {
+    bool is_query;   // mn*Query == query id
+    int words;
+    float score;
+};
+
+__device__ __forceinline__ PostState post_state(int kind, int n, unsigned long long id, const StateDev& St, const QScratch& X,
+                                                size_t row, int minCommon) {
+    const int c = X.cnt[row + n];
+    const bool stale = St.q[n] == id;
+    const bool ex = X.excl[row + n];
+    PostState p;
+    if (stale) {
+        p.is_query = true;
+        p.words = St.w[n] + c;
+        p.score = St.s[n];
+    } else if (kf_pushed(kind, c, false, ex)) {
+        p.is_query = true;
+        p.words = c;
+        p.score = (kind != KIND_COVIS && c > minCommon) ? X.si[row + n] : St.s[n];
+    } else {
+        p.is_query = false;
+        p.words = 0;
+        p.score = 0.f;
+    }
+    return p;
+}
+
+__device__ void bitonic_u64(unsigned long long* a, int P2) {
+    for (int k = 2; k <= P2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P2; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long x = a[i], y = a[ixj];
+                    if ((x > y) == ((i & k) == 0)) { a[i] = y; a[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+__global__ __launch_bounds__(256) void k_kfdb_accum(DbDev D, QueryIn Q, QScratch X, StateDev St, int kind, int32_t* __restrict__ out,
+                                                    int out_stride, int32_t* __restrict__ out_n, int32_t* __restrict__ status) {
+    __shared__ unsigned long long key[kKfdbMaxRetained];
+    __shared__ int rbest[kKfdbMaxRetained];
+    __shared__ int sbest[kKfdbMaxRetained];
+    __shared__ uint8_t keep[kKfdbMaxRetained];
+    __shared__ float s_part[256 / kWave];
+    __shared__ int s_nr, s_tmp[256 / kWave + 1];
+    const int q = blockIdx.x;
+    const int T = blockDim.x;
+    const unsigned long long id = Q.id[q];
+    const size_t row = (size_t)q * D.S;
+    const int minCommon = X.meta[q * 4 + 1];
+    const int nc = X.meta[q * 4 + 2];
+    const float minScore = Q.min_score ? Q.min_score[q] : 0.f;
+    const float init = kind == KIND_RELOC ? 0.f : minScore;
+
+    // accumulate by covisibility (:148-173 / :264-287 / :373-398); bestAcc: strict > from init = max
+    float part = init;
+    for (int c = threadIdx.x; c < nc; c += T) {
+        const int k = X.cand[row + c];
+        const float si = X.si[row + k];
+        if (kind != KIND_RELOC && !(si >= minScore)) {
+            X.acc[row + c] = 0.f;
+            X.best[row + c] = -1;
+            continue;
+        }
+        float best = si, acc = si;
+        int bk = k;
+        for (int j = 0; j < kKfdbCovis; ++j) {
+            const int n = D.covis[(size_t)k * kKfdbCovis + j];
+            if (n < 0) break;
+            const PostState p = post_state(kind, n, id, St, X, row, minCommon);
+            if (!p.is_query) continue;
+            if (kind != KIND_RELOC && !(p.words > minCommon)) continue;
+            acc = __fadd_rn(acc, p.score);
+            if (p.score > best) {
+                bk = n;
+                best = p.score;
+            }
+        }
+        X.acc[row + c] = acc;
+        X.best[row + c] = bk;
+        if (acc > part) part = acc;
+    }
+    // wave then block max with the same strict rule (partials are never NaN)
+    for (int o = 32; o > 0; o >>= 1) {
+        const float t = __shfl_xor(part, o, kWave);
+        if (t > part) part = t;
+    }
+    if (lane_id() == 0) s_part[threadIdx.x / kWave] = part;
+    if (threadIdx.x == 0) s_nr = 0;
+    __syncthreads();
+    float bestAcc = s_part[0];
+    for (int w = 1; w < T / kWave; ++w)
+        if (s_part[w] > bestAcc) bestAcc = s_part[w];
+    const float minRetain = 0.75f * bestAcc;
+
+    // retained candidates with the reference's list key (first shared query word, add order)
+    for (int c = threadIdx.x; c < nc; c += T) {
+        if (X.best[row + c] < 0) continue;
+        if (!(X.acc[row + c] > minRetain)) continue;
+        const int r = atomicAdd(&s_nr, 1);
+        if (r >= kKfdbMaxRetained) continue;
+        const int k = X.cand[row + c];
+        key[r] = ((unsigned long long)(uint32_t)X.first[row + k] << 44) | ((unsigned long long)D.seq[k] << 12) |
+                 (unsigned long long)r;
+        rbest[r] = X.best[row + c];
+    }
+    __syncthreads();
+    int R = s_nr;
+    if (R > kKfdbMaxRetained) {
+        if (threadIdx.x == 0) atomicOr(status, 2);
+        R = kKfdbMaxRetained;
+    }
+    int P2 = 1;
+    while (P2 < R) P2 <<= 1;
+    for (int i = R + threadIdx.x; i < P2; i += T) key[i] = ~0ull;
+    __syncthreads();
+    bitonic_u64(key, P2);
+    // sbest[pos] = best keyframe in list order; then sort (best, pos) to find first occurrences
+    for (int i = threadIdx.x; i < R; i += T) sbest[i] = rbest[key[i] & 0xFFF];
+    __syncthreads();
+    for (int i = threadIdx.x; i < P2; i += T) {
+        key[i] = i < R ? (((unsigned long long)(uint32_t)sbest[i] << 12) | (unsigned long long)i) : ~0ull;
+        if (i < R) keep[i] = 0;
+    }
+    __syncthreads();
+    bitonic_u64(key, P2);
+    for (int i = threadIdx.x; i < R; i += T)
+        if (i == 0 || (key[i] >> 12) != (key[i - 1] >> 12)) keep[key[i] & 0xFFF] = 1;
+    __syncthreads();
+    // ordered compaction of the kept positions
+    int written = 0;
+    for (int base = 0; base < R; base += T) {
+        const int i = base + threadIdx.x;
+        const int f = (i < R) ? keep[i] : 0;
+        int total;
+        const int pos = block_excl_scan(f, s_tmp, &total) + written;
+        if (f && pos < out_stride) out[(size_t)q * out_stride + pos] = sbest[i];
+        written += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out_n[q] = min(written, out_stride);
+        if (written > out_stride) atomicOr(status, 2);
+    }
+}
+
+// Apply the batch's updates to the scratch fields in query order (:93-102 / :220-227 / :325-331,
+// scores :135 / :361) and flag a batch whose queries see one another's updates: query j's results
+// assume the fields of every slot it reads are as at batch start whenever one equals its id.
+__global__ __launch_bounds__(256) void k_kfdb_state(DbDev D, QueryIn Q, QScratch X, StateDev St, int kind, int nq,
+                                                    int32_t* __restrict__ status) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= D.S) return;
+    const unsigned long long q0 = St.q[k];
+    unsigned long long qf = q0;
+    int wf = St.w[k];
+    float sf = St.s[k];
+    bool touched = false;
+    for (int j = 0; j < nq; ++j) {
+        const unsigned long long id = Q.id[j];
+        if (touched && (q0 == id || qf == id)) atomicOr(status, 1);
+        const size_t row = (size_t)j * D.S;
+        const int c = X.cnt[row + k];
+        if (c == 0) continue;                            // COVIS-ignored slots were never counted
+        const bool ex = X.excl[row + k];
+        touched = true;
+        if (qf == id) {
+            wf += c;
+        } else if (kind == KIND_LOOP && ex) {
+            wf = 1;
+        } else {
+            qf = id;
+            wf = c;
+            if (kind != KIND_COVIS && X.meta[j * 4 + 0] > 0 && c > X.meta[j * 4 + 1]) sf = X.si[row + k];
+        }
+    }
+    if (touched) {
+        St.q[k] = qf;
+        St.w[k] = wf;
+        St.s[k] = sf;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_kfdb_score_pairs(DbDev D, const int32_t* __restrict__ pairs, int n, double* __restrict__ out) {
+    const int p = blockIdx.x * (blockDim.x / kWave) + (int)(threadIdx.x / kWave);
+    if (p >= n) return;
+    const int a = pairs[2 * p], b = pairs[2 * p + 1];
+    if (a < 0 || a >= D.S || b < 0 || b >= D.S) {
+        if (lane_id() == 0) out[p] = 0.0;
+        return;
+    }
+    const double s = wave_l1_score(D.bw + (size_t)a * D.maxw, D.bv + (size_t)a * D.maxw, D.bn[a], D.bw + (size_t)b * D.maxw,
+                                   D.bv + (size_t)b * D.maxw, D.bn[b]);
+    if (lane_id() == 0) out[p] = s;
+}
+
+}  // namespace orbx
+
+using namespace orbx;
+
+struct orbx_kfdb {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int n_vocab = 0, S = 0, maxw = 0;
+    uint32_t* d_bw = nullptr;
+    double* d_bv = nullptr;
+    int32_t* d_bn = nullptr;
+    int32_t* d_covis = nullptr;
+    uint32_t* d_seq = nullptr;
+    int32_t* d_if_off = nullptr;
+    int32_t* d_if_cur = nullptr;
+    int32_t* d_if_slot = nullptr;
+    int32_t* d_scan = nullptr;
+    int32_t* d_members = nullptr;
+    unsigned long long* d_q[3] = {nullptr, nullptr, nullptr};
+    int32_t* d_w[3] = {nullptr, nullptr, nullptr};
+    float* d_s[3] = {nullptr, nullptr, nullptr};
+    void* scratch = nullptr;       // per-query rows + host-form staging
+    size_t scratch_bytes = 0;
+    std::vector<uint32_t> seq;     // host mirror of membership (add order)
+    std::vector<int32_t> members;
+    uint32_t next_seq = 0;
+    bool dirty = true;
+};
+
+namespace {
+
+DbDev dev_view(const orbx_kfdb* db) {
+    return DbDev{db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_slot, db->S, db->maxw, db->n_vocab};
+}
+
+int grow_scratch(orbx_kfdb* db, size_t bytes) {
+    if (bytes <= db->scratch_bytes) return ORBX_OK;
+    if (db->scratch) {
+        ORBX_HIP(hipStreamSynchronize(db->stream));
+        ORBX_HIP(hipFree(db->scratch));
+        db->scratch = nullptr;
+        db->scratch_bytes = 0;
+    }
+    ORBX_HIP(hipMalloc(&db->scratch, bytes));
+    db->scratch_bytes = bytes;
+    return ORBX_OK;
+}
+
+size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// Row layout of the query scratch for nq queries over S slots.
+size_t qscratch_layout(int nq, int S, unsigned char* base, QScratch* X) {
+    const size_t r = (size_t)nq * S;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { unsigned char* p = base ? base + o : nullptr; o += align_up(bytes); return p; };
+    QScratch x;
+    x.cnt = (int32_t*)take(4 * r);
+    x.first = (int32_t*)take(4 * r);
+    x.excl = (uint8_t*)take(r);
+    x.si = (float*)take(4 * r);
+    x.cand = (int32_t*)take(4 * r);
+    x.acc = (float*)take(4 * r);
+    x.best = (int32_t*)take(4 * r);
+    x.meta = (int32_t*)take(16 * (size_t)nq);
+    if (X) *X = x;
+    return o;
+}
+
+int rebuild_inverted_file(orbx_kfdb* db, hipStream_t s) {
+    if (!db->dirty) return ORBX_OK;
+    const int nm = (int)db->members.size();
+    ORBX_HIP(hipMemcpyAsync(db->d_seq, db->seq.data(), sizeof(uint32_t) * db->S, hipMemcpyHostToDevice, s));
+    if (nm) ORBX_HIP(hipMemcpyAsync(db->d_members, db->members.data(), sizeof(int32_t) * nm, hipMemcpyHostToDevice, s));
+    const int n = db->n_vocab + 1;
+    ORBX_HIP(hipMemsetAsync(db->d_if_off, 0, sizeof(int32_t) * n, s));
+    DbDev D = dev_view(db);
+    if (nm) hipLaunchKernelGGL(k_if_count, dim3(nm), dim3(256), 0, s, D, db->d_members, db->d_if_off);
+    const int nb = (n + kScanChunk - 1) / kScanChunk;
+    hipLaunchKernelGGL(k_scan_chunks, dim3(nb), dim3(1024), 0, s, db->d_if_off, n, db->d_scan);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, db->d_scan, nb);
+    hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(1024), 0, s, db->d_if_off, n, db->d_scan, db->d_if_cur);
+    if (nm) hipLaunchKernelGGL(k_if_scatter, dim3(nm), dim3(256), 0, s, D, db->d_members, db->d_if_cur, db->d_if_slot);
+    ORBX_HIP(hipGetLastError());
+    db->dirty = false;
+    return ORBX_OK;
+}
+
+// The query batch on stream s; d_* are device pointers.  Scratch rows at 'base' (nq x S).
+int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned char* base, int32_t* d_out, int out_stride,
+                 int32_t* d_out_n, int32_t* d_status, hipStream_t s) {
+    int st = rebuild_inverted_file(db, s);
+    if (st) return st;
+    QScratch X;
+    qscratch_layout(nq, db->S, base, &X);
+    const size_t r = (size_t)nq * db->S;
+    ORBX_HIP(hipMemsetAsync(X.cnt, 0, 4 * r, s));
+    ORBX_HIP(hipMemsetAsync(X.first, 0x7f, 4 * r, s));
+    ORBX_HIP(hipMemsetAsync(X.excl, 0, r, s));
+    DbDev D = dev_view(db);
+    StateDev St{db->d_q[kind], db->d_w[kind], db->d_s[kind]};
+    hipLaunchKernelGGL(k_kfdb_mark_excl, dim3(nq), dim3(256), 0, s, Q, X, db->S);
+    hipLaunchKernelGGL(k_kfdb_share, dim3((db->maxw + 255) / 256, nq), dim3(256), 0, s, D, Q, X, kind);
+    hipLaunchKernelGGL(k_kfdb_select, dim3(nq), dim3(1024), 0, s, D, Q, X, St, kind);
+    const size_t lds = (size_t)db->maxw * (sizeof(double) + sizeof(uint32_t));
+    hipLaunchKernelGGL(k_kfdb_score, dim3(32, nq), dim3(256), lds, s, D, Q, X);
+    hipLaunchKernelGGL(k_kfdb_accum, dim3(nq), dim3(256), 0, s, D, Q, X, St, kind, d_out, out_stride, d_out_n, d_status);
+    hipLaunchKernelGGL(k_kfdb_state, dim3((db->S + 255) / 256), dim3(256), 0, s, D, Q, X, St, kind, nq, d_status);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device, orbx_kfdb** out) {
+    ORBX_REQUIRE(out, ORBX_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    ORBX_REQUIRE(n_vocab_words >= 1 && max_slots >= 1 && max_slots <= (1 << 20), ORBX_ERR_ARG,
+                 "bad sizes (n_vocab_words %d, max_slots %d)", n_vocab_words, max_slots);
+    ORBX_REQUIRE(max_words >= 1 && max_words <= kKfdbMaxWords, ORBX_ERR_UNSUPPORTED, "max_words %d outside [1, %d]", max_words,
+                 kKfdbMaxWords);
+    int ndev = 0;
+    ORBX_HIP(hipGetDeviceCount(&ndev));
+    ORBX_REQUIRE(device >= 0 && device < ndev, ORBX_ERR_ARG, "device %d out of range (%d devices)", device, ndev);
+    orbx_kfdb* db = new orbx_kfdb();
+    db->device = device;
+    db->n_vocab = n_vocab_words;
+    db->S = max_slots;
+    db->maxw = max_words;
+    db->seq.assign(max_slots, kNoSeq);
+    const size_t S = max_slots, W = max_words;
+    hipError_t e = hipSetDevice(device);
+    auto alloc = [&](void** p, size_t bytes) {
+        if (e == hipSuccess) e = hipMalloc(p, bytes);
+        if (e == hipSuccess) e = hipMemset(*p, 0, bytes);
+    };
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&db->stream, hipStreamNonBlocking);
+    alloc((void**)&db->d_bw, 4 * S * W);
+    alloc((void**)&db->d_bv, 8 * S * W);
+    alloc((void**)&db->d_bn, 4 * S);
+    alloc((void**)&db->d_covis, 4 * S * kKfdbCovis);
+    if (e == hipSuccess) e = hipMemset(db->d_covis, 0xff, 4 * S * kKfdbCovis);
+    alloc((void**)&db->d_seq, 4 * S);
+    alloc((void**)&db->d_if_off, 4 * ((size_t)n_vocab_words + 1));
+    alloc((void**)&db->d_if_cur, 4 * ((size_t)n_vocab_words + 1));
+    alloc((void**)&db->d_if_slot, 4 * S * W);
+    alloc((void**)&db->d_scan, 4 * ((size_t)(n_vocab_words + 1 + kScanChunk - 1) / kScanChunk + 1));
+    alloc((void**)&db->d_members, 4 * S);
+    for (int k = 0; k < 3; ++k) {
+        alloc((void**)&db->d_q[k], 8 * S);
+        alloc((void**)&db->d_w[k], 4 * S);
+        alloc((void**)&db->d_s[k], 4 * S);
+    }
+    if (e != hipSuccess) {
+        set_error("kfdb create: %s", hipGetErrorString(e));
+        orbx_kfdb_destroy(db);
+        return ORBX_ERR_HIP;
+    }
+    *out = db;
+    return ORBX_OK;
+}
+
+int orbx_kfdb_destroy(orbx_kfdb* db) {
+    if (!db) return ORBX_OK;
+    (void)hipSetDevice(db->device);
+    if (db->stream) (void)hipStreamSynchronize(db->stream);
+    void* bufs[] = {db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_cur, db->d_if_slot,
+                    db->d_scan, db->d_members, db->scratch};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    for (int k = 0; k < 3; ++k) {
+        if (db->d_q[k]) (void)hipFree(db->d_q[k]);
+        if (db->d_w[k]) (void)hipFree(db->d_w[k]);
+        if (db->d_s[k]) (void)hipFree(db->d_s[k]);
+    }
+    if (db->stream) (void)hipStreamDestroy(db->stream);
+    delete db;
+    return ORBX_OK;
+}
+
+int orbx_kfdb_info(const orbx_kfdb* db, int* n_vocab_words, int* max_slots, int* max_words, int* n_members) {
+    ORBX_REQUIRE(db, ORBX_ERR_ARG, "db is NULL");
+    if (n_vocab_words) *n_vocab_words = db->n_vocab;
+    if (max_slots) *max_slots = db->S;
+    if (max_words) *max_words = db->maxw;
+    if (n_members) *n_members = (int)db->members.size();
+    return ORBX_OK;
+}
+
+int orbx_kfdb_set_bow(orbx_kfdb* db, int slot, const uint32_t* words, const double* values, int n) {
+    ORBX_REQUIRE(db && slot >= 0 && slot < db->S && n >= 0 && n <= db->maxw && (n == 0 || (words && values)), ORBX_ERR_ARG,
+                 "bad argument (slot %d, n %d)", slot, n);
+    for (int i = 0; i < n; ++i) {
+        ORBX_REQUIRE(words[i] < (uint32_t)db->n_vocab, ORBX_ERR_ARG, "word id %u >= vocabulary size %d", words[i], db->n_vocab);
+        ORBX_REQUIRE(i == 0 || words[i] > words[i - 1], ORBX_ERR_ARG, "BowVector word ids must ascend");
+    }
+    ORBX_HIP(hipSetDevice(db->device));
+    const size_t o = (size_t)slot * db->maxw;
+    if (n) {
+        ORBX_HIP(hipMemcpyAsync(db->d_bw + o, words, 4 * (size_t)n, hipMemcpyHostToDevice, db->stream));
+        ORBX_HIP(hipMemcpyAsync(db->d_bv + o, values, 8 * (size_t)n, hipMemcpyHostToDevice, db->stream));
+    }
+    ORBX_HIP(hipMemcpyAsync(db->d_bn + slot, &n, 4, hipMemcpyHostToDevice, db->stream));
+    ORBX_HIP(hipStreamSynchronize(db->stream));
+    if (db->seq[slot] != kNoSeq) db->dirty = true;
+    return ORBX_OK;
+}
+
+int orbx_kfdb_set_bow_device(orbx_kfdb* db, const int32_t* d_slots, int n, const uint32_t* d_words, const double* d_values,
+                             const int32_t* d_n_words, int stride, void* stream) {
+    ORBX_REQUIRE(db && n >= 0 && (n == 0 || (d_slots && d_words && d_values && d_n_words)) && stride >= 0, ORBX_ERR_ARG,
+                 "bad argument");
+    if (n == 0) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(db->device));
+    DbDev D = dev_view(db);
+    hipLaunchKernelGGL(k_set_bow, dim3(n), dim3(256), 0, (hipStream_t)stream, D, db->d_bw, db->d_bv, db->d_bn, d_slots, d_words,
+                       d_values, d_n_words, stride);
+    ORBX_HIP(hipGetLastError());
+    db->dirty = true;
+    return ORBX_OK;
+}
+
+int orbx_kfdb_set_covisibility(orbx_kfdb* db, const int32_t* slots, int n, const int32_t* best) {
+    ORBX_REQUIRE(db && n >= 0 && (n == 0 || (slots && best)), ORBX_ERR_ARG, "bad argument");
+    ORBX_HIP(hipSetDevice(db->device));
+    for (int i = 0; i < n; ++i) {
+        ORBX_REQUIRE(slots[i] >= 0 && slots[i] < db->S, ORBX_ERR_ARG, "slot %d out of range", slots[i]);
+        for (int j = 0; j < kKfdbCovis; ++j)
+            ORBX_REQUIRE(best[i * kKfdbCovis + j] >= -1 && best[i * kKfdbCovis + j] < db->S, ORBX_ERR_ARG,
+                         "covisible slot %d out of range", best[i * kKfdbCovis + j]);
+        ORBX_HIP(hipMemcpyAsync(db->d_covis + (size_t)slots[i] * kKfdbCovis, best + (size_t)i * kKfdbCovis,
+                                4 * kKfdbCovis, hipMemcpyHostToDevice, db->stream));
+    }
+    ORBX_HIP(hipStreamSynchronize(db->stream));
+    return ORBX_OK;
+}
+
+int orbx_kfdb_add(orbx_kfdb* db, const int32_t* slots, int n) {
+    ORBX_REQUIRE(db && n >= 0 && (n == 0 || slots), ORBX_ERR_ARG, "bad argument");
+    for (int i = 0; i < n; ++i) {
+        const int k = slots[i];
+        ORBX_REQUIRE(k >= 0 && k < db->S, ORBX_ERR_ARG, "slot %d out of range", k);
+        ORBX_REQUIRE(db->seq[k] == kNoSeq, ORBX_ERR_ARG, "slot %d is already in the database", k);
+        ORBX_REQUIRE(db->next_seq < kNoSeq, ORBX_ERR_CAPACITY, "add sequence exhausted");
+        db->seq[k] = db->next_seq++;
+        db->members.push_back(k);
+    }
+    if (n) db->dirty = true;
+    return ORBX_OK;
+}
+
+int orbx_kfdb_erase(orbx_kfdb* db, const int32_t* slots, int n) {
+    ORBX_REQUIRE(db && n >= 0 && (n == 0 || slots), ORBX_ERR_ARG, "bad argument");
+    bool any = false;
+    for (int i = 0; i < n; ++i) {
+        const int k = slots[i];
+        ORBX_REQUIRE(k >= 0 && k < db->S, ORBX_ERR_ARG, "slot %d out of range", k);
+        if (db->seq[k] == kNoSeq) continue;      // not in the database: the reference's erase finds nothing
+        db->seq[k] = kNoSeq;
+        db->members.erase(std::find(db->members.begin(), db->members.end(), k));
+        any = true;
+    }
+    if (any) db->dirty = true;
+    return ORBX_OK;
+}
+
+int orbx_kfdb_clear(orbx_kfdb* db) {
+    ORBX_REQUIRE(db, ORBX_ERR_ARG, "db is NULL");
+    std::fill(db->seq.begin(), db->seq.end(), kNoSeq);
+    db->members.clear();
+    db->dirty = true;
+    return ORBX_OK;
+}
+
+int orbx_kfdb_get_state(orbx_kfdb* db, int kind, uint64_t* query, int32_t* words, float* score) {
+    ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && query && words && score, ORBX_ERR_ARG, "bad argument");
+    ORBX_HIP(hipSetDevice(db->device));
+    ORBX_HIP(hipMemcpyAsync(query, db->d_q[kind], 8 * (size_t)db->S, hipMemcpyDeviceToHost, db->stream));
+    ORBX_HIP(hipMemcpyAsync(words, db->d_w[kind], 4 * (size_t)db->S, hipMemcpyDeviceToHost, db->stream));
+    ORBX_HIP(hipMemcpyAsync(score, db->d_s[kind], 4 * (size_t)db->S, hipMemcpyDeviceToHost, db->stream));
+    ORBX_HIP(hipStreamSynchronize(db->stream));
+    return ORBX_OK;
+}
+
+int orbx_kfdb_set_state(orbx_kfdb* db, int kind, const uint64_t* query, const int32_t* words, const float* score) {
+    ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && query && words && score, ORBX_ERR_ARG, "bad argument");
+    ORBX_HIP(hipSetDevice(db->device));
+    ORBX_HIP(hipMemcpyAsync(db->d_q[kind], query, 8 * (size_t)db->S, hipMemcpyHostToDevice, db->stream));
+    ORBX_HIP(hipMemcpyAsync(db->d_w[kind], words, 4 * (size_t)db->S, hipMemcpyHostToDevice, db->stream));
+    ORBX_HIP(hipMemcpyAsync(db->d_s[kind], score, 4 * (size_t)db->S, hipMemcpyHostToDevice, db->stream));
+    ORBX_HIP(hipStreamSynchronize(db->stream));
+    return ORBX_OK;
+}
+
+int orbx_kfdb_score_device(orbx_kfdb* db, const int32_t* d_pairs, int n, double* d_scores, void* stream) {
+    ORBX_REQUIRE(db && n >= 0 && (n == 0 || (d_pairs && d_scores)), ORBX_ERR_ARG, "bad argument");
+    if (n == 0) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(db->device));
+    hipLaunchKernelGGL(k_kfdb_score_pairs, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, dev_view(db), d_pairs, n,
+                       d_scores);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_kfdb_score(orbx_kfdb* db, const int32_t* pairs, int n, double* scores) {
+    ORBX_REQUIRE(db && n >= 0 && (n == 0 || (pairs && scores)), ORBX_ERR_ARG, "bad argument");
+    if (n == 0) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(db->device));
+    const size_t qb = qscratch_layout(0, db->S, nullptr, nullptr);
+    int st = grow_scratch(db, qb + align_up(8 * (size_t)n) + align_up(8 * (size_t)n));
+    if (st) return st;
+    int32_t* d_pairs = (int32_t*)((unsigned char*)db->scratch + qb);
+    double* d_out = (double*)((unsigned char*)d_pairs + align_up(8 * (size_t)n));
+    ORBX_HIP(hipMemcpyAsync(d_pairs, pairs, 8 * (size_t)n, hipMemcpyHostToDevice, db->stream));
+    st = orbx_kfdb_score_device(db, d_pairs, n, d_out, db->stream);
+    if (st) return st;
+    ORBX_HIP(hipMemcpyAsync(scores, d_out, 8 * (size_t)n, hipMemcpyDeviceToHost, db->stream));
+    ORBX_HIP(hipStreamSynchronize(db->stream));
+    return ORBX_OK;
+}
+
+int orbx_kfdb_detect_device(orbx_kfdb* db, int kind, const int32_t* d_query_slots, const uint64_t* d_query_ids,
+                            const float* d_min_scores, int nq, const int32_t* d_excl_offsets, const int32_t* d_excl_slots,
+                            int32_t* d_out, int out_stride, int32_t* d_out_n, int32_t* d_status, void* stream) {
+    ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && nq >= 0 && out_stride >= 0, ORBX_ERR_ARG, "bad argument");
+    ORBX_REQUIRE(nq == 0 || (d_query_slots && d_query_ids && d_out && d_out_n && d_status), ORBX_ERR_ARG, "null buffers");
+    ORBX_REQUIRE(kind == ORBX_KFDB_RELOC || nq == 0 || d_min_scores, ORBX_ERR_ARG, "min scores required for this query kind");
+    if (nq == 0) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(db->device));
+    const size_t qb = qscratch_layout(nq, db->S, nullptr, nullptr);
+    int st = grow_scratch(db, qb);
+    if (st) return st;
+    QueryIn Q{d_query_slots, (const unsigned long long*)d_query_ids, d_min_scores, d_excl_offsets, d_excl_slots};
+    return detect_batch(db, kind, Q, nq, (unsigned char*)db->scratch, d_out, out_stride, d_out_n, d_status,
+                        (hipStream_t)stream);
+}
+
+int orbx_kfdb_detect(orbx_kfdb* db, int kind, const int32_t* query_slots, const uint64_t* query_ids, const float* min_scores,
+                     int nq, const int32_t* excl_offsets, const int32_t* excl_slots, int32_t* out_offsets, int32_t* out,
+                     int out_cap) {
+    ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && nq >= 0 && out_cap >= 0, ORBX_ERR_ARG, "bad argument");
+    ORBX_REQUIRE(nq == 0 || (query_slots && query_ids && out_offsets), ORBX_ERR_ARG, "null buffers");
+    ORBX_REQUIRE(kind == ORBX_KFDB_RELOC || nq == 0 || min_scores, ORBX_ERR_ARG, "min scores required for this query kind");
+    if (out_offsets) out_offsets[0] = 0;
+    if (nq == 0) return ORBX_OK;
+    for (int q = 0; q < nq; ++q)
+        ORBX_REQUIRE(query_slots[q] >= 0 && query_slots[q] < db->S, ORBX_ERR_ARG, "query slot %d out of range", query_slots[q]);
+    const int n_excl = excl_offsets ? excl_offsets[nq] : 0;
+    ORBX_REQUIRE(!excl_offsets || (excl_offsets[0] == 0 && (n_excl == 0 || excl_slots)), ORBX_ERR_ARG, "bad exclusion lists");
+    ORBX_HIP(hipSetDevice(db->device));
+    const int S = db->S;
+    // device staging: [query scratch][slots][ids][min][excl_off][excl][out nq x S][out_n][status][state snapshot]
+    const size_t qb = qscratch_layout(nq, S, nullptr, nullptr);
+    size_t o = qb;
+    const size_t o_slot = o; o += align_up(4 * (size_t)nq);
+    const size_t o_id = o; o += align_up(8 * (size_t)nq);
+    const size_t o_min = o; o += align_up(4 * (size_t)nq);
+    const size_t o_eoff = o; o += align_up(4 * (size_t)(nq + 1));
+    const size_t o_excl = o; o += align_up(4 * (size_t)std::max(n_excl, 1));
+    const size_t o_out = o; o += align_up(4 * (size_t)nq * S);
+    const size_t o_outn = o; o += align_up(4 * (size_t)nq);
+    const size_t o_stat = o; o += align_up(4);
+    const size_t o_snap = o; o += align_up(16 * (size_t)S);
+    int st = grow_scratch(db, o);
+    if (st) return st;
+    unsigned char* b = (unsigned char*)db->scratch;
+    hipStream_t s = db->stream;
+    ORBX_HIP(hipMemcpyAsync(b + o_slot, query_slots, 4 * (size_t)nq, hipMemcpyHostToDevice, s));
+    ORBX_HIP(hipMemcpyAsync(b + o_id, query_ids, 8 * (size_t)nq, hipMemcpyHostToDevice, s));
+    if (min_scores) ORBX_HIP(hipMemcpyAsync(b + o_min, min_scores, 4 * (size_t)nq, hipMemcpyHostToDevice, s));
+    if (excl_offsets) {
+        ORBX_HIP(hipMemcpyAsync(b + o_eoff, excl_offsets, 4 * (size_t)(nq + 1), hipMemcpyHostToDevice, s));
+        if (n_excl) ORBX_HIP(hipMemcpyAsync(b + o_excl, excl_slots, 4 * (size_t)n_excl, hipMemcpyHostToDevice, s));
+    }
+    // snapshot of this kind's scratch fields, restored if the batch has to be re-run one query at a time
+    ORBX_HIP(hipMemcpyAsync(b + o_snap, db->d_q[kind], 8 * (size_t)S, hipMemcpyDeviceToDevice, s));
+    ORBX_HIP(hipMemcpyAsync(b + o_snap + 8 * (size_t)S, db->d_w[kind], 4 * (size_t)S, hipMemcpyDeviceToDevice, s));
+    ORBX_HIP(hipMemcpyAsync(b + o_snap + 12 * (size_t)S, db->d_s[kind], 4 * (size_t)S, hipMemcpyDeviceToDevice, s));
+    int32_t* d_status = (int32_t*)(b + o_stat);
+    ORBX_HIP(hipMemsetAsync(d_status, 0, 4, s));
+    QueryIn Q{(const int32_t*)(b + o_slot), (const unsigned long long*)(b + o_id), min_scores ? (const float*)(b + o_min) : nullptr,
+              excl_offsets ? (const int32_t*)(b + o_eoff) : nullptr, (const int32_t*)(b + o_excl)};
+    st = detect_batch(db, kind, Q, nq, b, (int32_t*)(b + o_out), S, (int32_t*)(b + o_outn), d_status, s);
+    if (st) return st;
+    int32_t status = 0;
+    ORBX_HIP(hipMemcpyAsync(&status, d_status, 4, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+    if ((status & 1) && nq > 1) {
+        // the queries interact through the scratch fields: restore them and run in order, one by one
+        ORBX_HIP(hipMemcpyAsync(db->d_q[kind], b + o_snap, 8 * (size_t)S, hipMemcpyDeviceToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(db->d_w[kind], b + o_snap + 8 * (size_t)S, 4 * (size_t)S, hipMemcpyDeviceToDevice, s));
+        ORBX_HIP(hipMemcpyAsync(db->d_s[kind], b + o_snap + 12 * (size_t)S, 4 * (size_t)S, hipMemcpyDeviceToDevice, s));
+        ORBX_HIP(hipMemsetAsync(d_status, 0, 4, s));
+        for (int q = 0; q < nq; ++q) {
+            QueryIn Q1{Q.slot + q, Q.id + q, Q.min_score ? Q.min_score + q : nullptr, Q.excl_off ? Q.excl_off + q : nullptr,
+                       Q.excl};
+            st = detect_batch(db, kind, Q1, 1, b, (int32_t*)(b + o_out) + (size_t)q * S, S, (int32_t*)(b + o_outn) + q, d_status,
+                              s);
+            if (st) return st;
+        }
+        ORBX_HIP(hipMemcpyAsync(&status, d_status, 4, hipMemcpyDeviceToHost, s));
+        ORBX_HIP(hipStreamSynchronize(s));
+        status &= ~1;
+    }
+    ORBX_REQUIRE(!(status & 2), ORBX_ERR_CAPACITY, "more than %d retained candidates in one query", kKfdbMaxRetained);
+    std::vector<int32_t> cnt(nq);
+    ORBX_HIP(hipMemcpyAsync(cnt.data(), b + o_outn, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+    int total = 0;
+    for (int q = 0; q < nq; ++q) {
+        out_offsets[q + 1] = out_offsets[q] + cnt[q];
+        total += cnt[q];
+    }
+    if (total > out_cap) {
+        set_error("output capacity %d < %d candidates", out_cap, total);
+        return ORBX_ERR_CAPACITY;
+    }
+    for (int q = 0; q < nq; ++q)
+        if (cnt[q]) ORBX_HIP(hipMemcpyAsync(out + out_offsets[q], (int32_t*)(b + o_out) + (size_t)q * S, 4 * (size_t)cnt[q],
+                                            hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+    return ORBX_OK;
+}
+
+}  // extern "C"

@@ -183,6 +183,21 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_vocab_transform.argtypes = [vp, vp, i32, i32, vp, vp, C.POINTER(i32), vp, vp, vp, C.POINTER(i32)]
     lib.orbx_vocab_words_device.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
     lib.orbx_vocab_transform_batch_device.argtypes = [vp, vp, vp, i32, i32, i32] + [vp] * 11
+    lib.orbx_kfdb_create.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
+    lib.orbx_kfdb_destroy.argtypes = [vp]
+    lib.orbx_kfdb_info.argtypes = [vp] + [C.POINTER(i32)] * 4
+    lib.orbx_kfdb_set_bow.argtypes = [vp, i32, vp, vp, i32]
+    lib.orbx_kfdb_set_bow_device.argtypes = [vp, vp, i32, vp, vp, vp, i32, vp]
+    lib.orbx_kfdb_set_covisibility.argtypes = [vp, vp, i32, vp]
+    for name in ("orbx_kfdb_add", "orbx_kfdb_erase"):
+        getattr(lib, name).argtypes = [vp, vp, i32]
+    lib.orbx_kfdb_clear.argtypes = [vp]
+    lib.orbx_kfdb_get_state.argtypes = [vp, i32, vp, vp, vp]
+    lib.orbx_kfdb_set_state.argtypes = [vp, i32, vp, vp, vp]
+    lib.orbx_kfdb_score.argtypes = [vp, vp, i32, vp]
+    lib.orbx_kfdb_score_device.argtypes = [vp, vp, i32, vp, vp]
+    lib.orbx_kfdb_detect.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, vp, i32]
+    lib.orbx_kfdb_detect_device.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp]
     _lib = lib
     return lib
 
@@ -587,13 +602,20 @@ class ORBmatcher:
         return self.proj_search(ProjParams.make(PROJ_INIT, self.TH_LOW, self.mfNNratio, self.mbCheckOrientation), grid,
                                 queries, qdesc, kps, desc)
 
-    def grid_build_device(self, grid: Grid, kps, counts, stream=None):
-        """Frame::AssignFeaturesToGrid on (B, capacity, 28) device keypoints: (cell_start, cell_idx) tensors."""
+    def grid_build_device(self, grid: Grid, kps, counts, stream=None, out=None):
+        """Frame::AssignFeaturesToGrid on (B, capacity, 28) device keypoints: (cell_start, cell_idx) tensors
+        (written into out = (cell_start, cell_idx) when given)."""
         import torch
         B, cap = kps.shape[0], kps.shape[1]
         ncell = grid.cols * grid.rows
-        cs = torch.empty((B, ncell + 1), dtype=torch.int32, device=kps.device)
-        ci = torch.empty((B, cap), dtype=torch.int32, device=kps.device)
+        if out is None:
+            cs = torch.empty((B, ncell + 1), dtype=torch.int32, device=kps.device)
+            ci = torch.empty((B, cap), dtype=torch.int32, device=kps.device)
+        else:
+            cs, ci = out
+            if tuple(cs.shape) != (B, ncell + 1) or tuple(ci.shape) != (B, cap) or cs.dtype != torch.int32 \
+                    or ci.dtype != torch.int32:
+                raise ValueError("grid_build_device: out tensors must be int32 (B, cells+1) and (B, capacity)")
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(kps.device).cuda_stream)
         _check(self._lib.orbx_grid_build_device(self._h, grid, _tp(kps), _tp(counts), B, cap, _tp(cs), _tp(ci), s))
         return cs, ci
@@ -686,3 +708,141 @@ class ORBVocabulary:
             _tp(out["bow_words"]), _tp(out["bow_values"]), _tp(out["n_words"]), _tp(out["fv_nodes"]),
             _tp(out["fv_offsets"]), _tp(out["fv_indices"]), _tp(out["n_fv"]), s))
         return out
+
+
+KFDB_LOOP, KFDB_COVIS, KFDB_RELOC = 0, 1, 2
+KFDB_COVIS_WIDTH = 10   # GetBestCovisibilityKeyFrames(10)
+
+
+class KeyFrameDatabase:
+    """KeyFrameDatabase (src/KeyFrameDatabase.cc) over a table of keyframe slots on a MI355X.
+
+    Keyframes are slot indices.  A slot carries its BowVector (set_bow), its best-10 covisibility list
+    (set_covisibility) and the KeyFrame scratch fields mn*Query / mn*Words / m*Score per query kind
+    (include/KeyFrame.h:155-163; get_state / set_state).  DetectLoopCandidates / DetectCovisibility-
+    Candidates / DetectRelocalizationCandidates return candidate slots in the reference's order."""
+
+    def __init__(self, n_vocab_words: int, max_slots: int, max_words: int = 4096, device: int = 0):
+        self._lib = load_library()
+        self._h = C.c_void_p()
+        _check(self._lib.orbx_kfdb_create(n_vocab_words, max_slots, max_words, device, C.byref(self._h)))
+        self.n_vocab_words, self.max_slots, self.max_words, self.device = n_vocab_words, max_slots, max_words, device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.orbx_kfdb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def n_members(self) -> int:
+        n = C.c_int()
+        _check(self._lib.orbx_kfdb_info(self._h, None, None, None, C.byref(n)))
+        return n.value
+
+    def set_bow(self, slot: int, words, values):
+        w = np.ascontiguousarray(words, np.uint32)
+        v = np.ascontiguousarray(values, np.float64)
+        if len(w) != len(v):
+            raise ValueError("words and values differ in length")
+        _check(self._lib.orbx_kfdb_set_bow(self._h, slot, _p(w), _p(v), len(w)))
+
+    def set_bow_device(self, slots, words, values, n_words, stream=None):
+        """BowVectors from orbx_vocab_transform_batch_device output (B, capacity) into device int32 slots."""
+        import torch
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(words.device).cuda_stream)
+        _check(self._lib.orbx_kfdb_set_bow_device(self._h, _tp(slots), slots.numel(), _tp(words), _tp(values),
+                                                  _tp(n_words), words.shape[1], s))
+
+    def set_covisibility(self, slot_lists: dict):
+        """{slot: [best covisible slots, best first]} (at most 10 each, KeyFrame::GetBestCovisibilityKeyFrames)."""
+        slots = np.array(list(slot_lists.keys()), np.int32)
+        best = np.full((len(slots), KFDB_COVIS_WIDTH), -1, np.int32)
+        for i, k in enumerate(slots):
+            lst = list(slot_lists[int(k)])[:KFDB_COVIS_WIDTH]
+            best[i, :len(lst)] = lst
+        _check(self._lib.orbx_kfdb_set_covisibility(self._h, _p(slots), len(slots), _p(best)))
+
+    def add(self, slots):
+        a = np.atleast_1d(np.ascontiguousarray(slots, np.int32))
+        _check(self._lib.orbx_kfdb_add(self._h, _p(a), len(a)))
+
+    def erase(self, slots):
+        a = np.atleast_1d(np.ascontiguousarray(slots, np.int32))
+        _check(self._lib.orbx_kfdb_erase(self._h, _p(a), len(a)))
+
+    def clear(self):
+        _check(self._lib.orbx_kfdb_clear(self._h))
+
+    def get_state(self, kind: int):
+        q = np.zeros(self.max_slots, np.uint64)
+        w = np.zeros(self.max_slots, np.int32)
+        sc = np.zeros(self.max_slots, np.float32)
+        _check(self._lib.orbx_kfdb_get_state(self._h, kind, _p(q), _p(w), _p(sc)))
+        return q, w, sc
+
+    def set_state(self, kind: int, query, words, score):
+        q = np.ascontiguousarray(query, np.uint64)
+        w = np.ascontiguousarray(words, np.int32)
+        sc = np.ascontiguousarray(score, np.float32)
+        if not (len(q) == len(w) == len(sc) == self.max_slots):
+            raise ValueError("state arrays must hold max_slots entries")
+        _check(self._lib.orbx_kfdb_set_state(self._h, kind, _p(q), _p(w), _p(sc)))
+
+    def score(self, pairs) -> np.ndarray:
+        """ORBVocabulary::score(bow[a], bow[b]) for (a, b) slot pairs (DBoW2 L1)."""
+        pr = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+        out = np.zeros(len(pr), np.float64)
+        _check(self._lib.orbx_kfdb_score(self._h, _p(pr), len(pr), _p(out)))
+        return out
+
+    def detect(self, kind: int, query_slots, query_ids, min_scores=None, exclusions=None):
+        """Batch of queries evaluated in order; returns a list of candidate-slot arrays."""
+        qs = np.atleast_1d(np.ascontiguousarray(query_slots, np.int32))
+        nq = len(qs)
+        ids = np.atleast_1d(np.ascontiguousarray(query_ids, np.uint64))
+        ms = None if min_scores is None else np.atleast_1d(np.ascontiguousarray(min_scores, np.float32))
+        eo = ex = None
+        if exclusions is not None:
+            lens = [len(e) for e in exclusions]
+            eo = np.zeros(nq + 1, np.int32)
+            eo[1:] = np.cumsum(lens)
+            ex = np.ascontiguousarray(np.concatenate([np.asarray(e, np.int32) for e in exclusions]) if sum(lens)
+                                      else np.zeros(1, np.int32), np.int32)
+        oo = np.zeros(nq + 1, np.int32)
+        cap = max(1, nq * self.max_slots)
+        out = np.zeros(cap, np.int32)
+        _check(self._lib.orbx_kfdb_detect(self._h, kind, _p(qs), _p(ids), None if ms is None else _p(ms), nq,
+                                          None if eo is None else _p(eo), None if ex is None else _p(ex), _p(oo),
+                                          _p(out), cap))
+        return [out[oo[i]:oo[i + 1]].copy() for i in range(nq)]
+
+    def detect_device(self, kind: int, query_slots, query_ids, min_scores=None, excl_offsets=None, excl_slots=None,
+                      out=None, out_n=None, status=None, stream=None):
+        """Device form: int32 slots, int64 ids, float32 min scores; returns (out, out_n, status) tensors."""
+        import torch
+        nq = query_slots.numel()
+        dev = query_slots.device
+        out = out if out is not None else torch.empty((nq, self.max_slots), dtype=torch.int32, device=dev)
+        out_n = out_n if out_n is not None else torch.empty((nq,), dtype=torch.int32, device=dev)
+        status = status if status is not None else torch.zeros((1,), dtype=torch.int32, device=dev)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream)
+        opt = lambda t: None if t is None else _tp(t)
+        _check(self._lib.orbx_kfdb_detect_device(self._h, kind, _tp(query_slots), _tp(query_ids), opt(min_scores), nq,
+                                                 opt(excl_offsets), opt(excl_slots), _tp(out), out.shape[1], _tp(out_n),
+                                                 _tp(status), s))
+        return out, out_n, status
+
+    # the reference's method names (one query each)
+    def DetectLoopCandidates(self, slot: int, query_id: int, minScore: float, connected=()):
+        return self.detect(KFDB_LOOP, [slot], [query_id], [minScore], [list(connected)])[0]
+
+    def DetectCovisibilityCandidates(self, slot: int, query_id: int, minScore: float, ignore=()):
+        return self.detect(KFDB_COVIS, [slot], [query_id], [minScore], [list(ignore)])[0]
+
+    def DetectRelocalizationCandidates(self, slot: int, query_id: int):
+        return self.detect(KFDB_RELOC, [slot], [query_id])[0]

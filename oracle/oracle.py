@@ -345,3 +345,78 @@ def proj_search(params, grid, queries, qdesc, kps, desc, uright=None, blocked=No
     if params.mode > 3:
         own[:] = -1
     return nm, qi[:nq], qdist[:nq], own[:n]
+
+
+# ---- keyframe database queries (oracle/kfdb_oracle.cpp) ---------------------------------------------
+class Kfdb:
+    """Sequential restatement of KeyFrameDatabase (src/KeyFrameDatabase.cc) over keyframe slots."""
+
+    def __init__(self, n_vocab_words, n_slots):
+        L = lib()
+        L.orc_kfdb_create.restype = C.c_void_p
+        L.orc_kfdb_create.argtypes = [C.c_int, C.c_int]
+        L.orc_kfdb_destroy.argtypes = [C.c_void_p]
+        L.orc_kfdb_set_bow.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_kfdb_set_covis.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int]
+        for n in ("orc_kfdb_add", "orc_kfdb_erase"):
+            getattr(L, n).argtypes = [C.c_void_p, C.c_int]
+        L.orc_kfdb_clear.argtypes = [C.c_void_p]
+        L.orc_kfdb_set_state.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_kfdb_get_state.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_kfdb_score.restype = C.c_double
+        L.orc_kfdb_score.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.orc_kfdb_detect.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.c_float, C.c_void_p, C.c_int,
+                                      C.c_void_p, C.c_int]
+        self._L = L
+        self.n_slots = n_slots
+        self._h = L.orc_kfdb_create(n_vocab_words, n_slots)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.orc_kfdb_destroy(self._h)
+            self._h = None
+
+    def set_bow(self, slot, words, values):
+        w = np.ascontiguousarray(words, np.uint32)
+        v = np.ascontiguousarray(values, np.float64)
+        self._L.orc_kfdb_set_bow(self._h, slot, _p(w), _p(v), len(w))
+
+    def set_covisibility(self, slot_lists):
+        for k, lst in slot_lists.items():
+            a = np.ascontiguousarray(list(lst)[:10], np.int32)
+            self._L.orc_kfdb_set_covis(self._h, int(k), _p(a), len(a))
+
+    def add(self, slots):
+        for k in np.atleast_1d(slots):
+            self._L.orc_kfdb_add(self._h, int(k))
+
+    def erase(self, slots):
+        for k in np.atleast_1d(slots):
+            self._L.orc_kfdb_erase(self._h, int(k))
+
+    def clear(self):
+        self._L.orc_kfdb_clear(self._h)
+
+    def get_state(self, kind):
+        q = np.zeros(self.n_slots, np.uint64)
+        w = np.zeros(self.n_slots, np.int32)
+        s = np.zeros(self.n_slots, np.float32)
+        self._L.orc_kfdb_get_state(self._h, kind, _p(q), _p(w), _p(s))
+        return q, w, s
+
+    def set_state(self, kind, q, w, s):
+        q, w, s = (np.ascontiguousarray(q, np.uint64), np.ascontiguousarray(w, np.int32),
+                   np.ascontiguousarray(s, np.float32))
+        self._L.orc_kfdb_set_state(self._h, kind, _p(q), _p(w), _p(s))
+
+    def score(self, a, b):
+        return self._L.orc_kfdb_score(self._h, int(a), int(b))
+
+    def detect(self, kind, slot, query_id, min_score=0.0, exclusions=()):
+        ex = np.ascontiguousarray(list(exclusions) or [0], np.int32)
+        out = np.zeros(self.n_slots, np.int32)
+        n = self._L.orc_kfdb_detect(self._h, kind, int(slot), int(query_id), float(min_score), _p(ex),
+                                    len(list(exclusions)), _p(out), len(out))
+        if n < 0:
+            raise RuntimeError("oracle candidate capacity")
+        return out[:n].copy()

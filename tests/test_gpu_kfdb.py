@@ -1,0 +1,106 @@
+"""GPU parity of the keyframe database queries against the oracle
+(oracle/kfdb_oracle.cpp): candidate lists in the reference's order, the KeyFrame scratch fields after
+every batch, and DBoW2 L1 scores bit for bit."""
+import numpy as np
+import pytest
+
+from kfdb_cases import COVIS, LOOP, RELOC, make_kfdb_case, setup_db
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_both(case, batched=True):
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    g = pkg.KeyFrameDatabase(case["n_vocab"], case["n_slots"], max_words=2048)
+    o = O.Kfdb(case["n_vocab"], case["n_slots"])
+    setup_db(case, g)
+    setup_db(case, o)
+    n_results = 0
+    for op, arg in case["ops"]:
+        if op in ("add", "erase"):
+            for k in arg:
+                getattr(g, op)([k])
+                getattr(o, op)([k])
+            continue
+        ref = [list(o.detect(kind, slot, qid, ms, excl)) for kind, slot, qid, ms, excl in arg]
+        got = [None] * len(arg)
+        for kind in (LOOP, COVIS, RELOC):        # kinds keep separate scratch fields: batch per kind, in order
+            idx = [i for i, a in enumerate(arg) if a[0] == kind]
+            if not idx:
+                continue
+            if batched:
+                res = g.detect(kind, [arg[i][1] for i in idx], [arg[i][2] for i in idx], [arg[i][3] for i in idx],
+                               [arg[i][4] for i in idx])
+            else:
+                res = [g.detect(kind, [arg[i][1]], [arg[i][2]], [arg[i][3]], [arg[i][4]])[0] for i in idx]
+            for i, r in zip(idx, res):
+                got[i] = list(r)
+        assert got == ref
+        n_results += sum(len(r) for r in ref)
+        for kind in (LOOP, COVIS, RELOC):
+            gq, gw, gs = g.get_state(kind)
+            oq, ow, os_ = o.get_state(kind)
+            assert np.array_equal(gq, oq) and np.array_equal(gw, ow), kind
+            assert np.array_equal(gs.view(np.uint32), os_.view(np.uint32)), kind
+    return n_results
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_detect_sequences(gpu, seed):
+    case = make_kfdb_case(100 + seed, n_slots=150, n_queries=48, words_hi=400)
+    assert _run_both(case) > 0
+
+
+def test_detect_one_by_one(gpu):
+    case = make_kfdb_case(200, n_slots=100, n_queries=30)
+    assert _run_both(case, batched=False) > 0
+
+
+def test_detect_fresh_ids_large(gpu):
+    """KITTI-like keyframes (1000-1500 words of a 1M-word vocabulary), 600 slots, fresh query ids only."""
+    case = make_kfdb_case(300, n_slots=600, n_vocab=1_000_000, n_places=30, words_lo=900, words_hi=1500,
+                          n_queries=40, repeat_ids=False)
+    assert _run_both(case) > 0
+
+
+def test_scores_bit_exact(gpu):
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    case = make_kfdb_case(400, n_slots=80, words_hi=1200)
+    g = pkg.KeyFrameDatabase(case["n_vocab"], case["n_slots"], max_words=2048)
+    o = O.Kfdb(case["n_vocab"], case["n_slots"])
+    setup_db(case, g)
+    setup_db(case, o)
+    rng = np.random.default_rng(2)
+    pairs = rng.integers(0, 80, (500, 2)).astype(np.int32)
+    got = g.score(pairs)
+    ref = np.array([o.score(a, b) for a, b in pairs])
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
+def test_edge_cases(gpu):
+    import multiagent_orb_slam2_amd as pkg
+    g = pkg.KeyFrameDatabase(16, 4, max_words=8)
+    g.set_bow(0, [1, 5, 9], [0.2, 0.3, 0.5])
+    g.set_bow(1, [1, 5, 10], [0.4, 0.4, 0.2])
+    g.set_bow(2, [5, 9], [0.5, 0.5])
+    g.set_bow(3, [], [])
+    assert g.DetectRelocalizationCandidates(0, 7).tolist() == []      # empty database
+    g.add([1, 2])
+    with pytest.raises(pkg.OrbxError):
+        g.add([1])                                                    # already in the database
+    with pytest.raises(pkg.OrbxError):
+        g.set_bow(3, [4, 2], [0.5, 0.5])                              # word ids must ascend
+    assert g.DetectRelocalizationCandidates(0, 8).tolist() == [2]
+    assert g.DetectLoopCandidates(0, 9, 0.0, connected=[2]).tolist() == [1]
+    assert g.DetectCovisibilityCandidates(0, 10, 0.9).tolist() == []
+    assert g.DetectRelocalizationCandidates(3, 11).tolist() == []     # query without words
+    g.set_covisibility({1: [2]})
+    assert g.DetectRelocalizationCandidates(0, 12).tolist() == [2]
+    g.erase([2, 3])
+    assert g.DetectRelocalizationCandidates(0, 13).tolist() == [1]
+    assert g.n_members() == 1
+    g.clear()
+    assert g.DetectRelocalizationCandidates(0, 14).tolist() == []
+    assert g.detect(RELOC, [], []) == []
