@@ -315,8 +315,23 @@ struct PostState {
     float score;
 };
 
-__device__ __forceinline__ PostState post_state(int kind, int n, unsigned long long id, const StateDev& St, const QScratch& X,
-                                                size_t row, int minCommon) {
+// m*Score of keyframe n before query q of the batch: written by the latest earlier query that scored it
+// (:135 / :361), else the value at batch start.  Relocalisation reads it for neighbours that share too
+// few words to be scored by this query (:384-387).
+__device__ float score_before(int kind, int n, int q, const QueryIn& Q, const QScratch& X, const StateDev& St, int S) {
+    if (kind != KIND_COVIS)
+        for (int i = q - 1; i >= 0; --i) {
+            const size_t r = (size_t)i * S;
+            const int c = X.cnt[r + n];
+            if (kf_pushed(kind, c, St.q[n] == Q.id[i], X.excl[r + n]) && c > X.meta[i * 4 + 1]) return X.si[r + n];
+        }
+    return St.s[n];
+}
+
+__device__ __forceinline__ PostState post_state(int kind, int n, int q, const QueryIn& Q, const StateDev& St, const QScratch& X,
+                                                int S, int minCommon) {
+    const unsigned long long id = Q.id[q];
+    const size_t row = (size_t)q * S;
     const int c = X.cnt[row + n];
     const bool stale = St.q[n] == id;
     const bool ex = X.excl[row + n];
@@ -328,7 +343,7 @@ __device__ __forceinline__ PostState post_state(int kind, int n, unsigned long l
     } else if (kf_pushed(kind, c, false, ex)) {
         p.is_query = true;
         p.words = c;
-        p.score = (kind != KIND_COVIS && c > minCommon) ? X.si[row + n] : St.s[n];
+        p.score = (kind != KIND_COVIS && c > minCommon) ? X.si[row + n] : score_before(kind, n, q, Q, X, St, S);
     } else {
         p.is_query = false;
         p.words = 0;
@@ -361,7 +376,6 @@ __global__ __launch_bounds__(256) void k_kfdb_accum(DbDev D, QueryIn Q, QScratch
     __shared__ int s_nr, s_tmp[256 / kWave + 1];
     const int q = blockIdx.x;
     const int T = blockDim.x;
-    const unsigned long long id = Q.id[q];
     const size_t row = (size_t)q * D.S;
     const int minCommon = X.meta[q * 4 + 1];
     const int nc = X.meta[q * 4 + 2];
@@ -383,7 +397,7 @@ __global__ __launch_bounds__(256) void k_kfdb_accum(DbDev D, QueryIn Q, QScratch
         for (int j = 0; j < kKfdbCovis; ++j) {
             const int n = D.covis[(size_t)k * kKfdbCovis + j];
             if (n < 0) break;
-            const PostState p = post_state(kind, n, id, St, X, row, minCommon);
+            const PostState p = post_state(kind, n, q, Q, St, X, D.S, minCommon);
             if (!p.is_query) continue;
             if (kind != KIND_RELOC && !(p.words > minCommon)) continue;
             acc = __fadd_rn(acc, p.score);
@@ -461,8 +475,10 @@ __global__ __launch_bounds__(256) void k_kfdb_accum(DbDev D, QueryIn Q, QScratch
 }
 
 // Apply the batch's updates to the scratch fields in query order (:93-102 / :220-227 / :325-331,
-// scores :135 / :361) and flag a batch whose queries see one another's updates: query j's results
-// assume the fields of every slot it reads are as at batch start whenever one equals its id.
+// scores :135 / :361) and flag a batch whose queries see one another's updates in a way the batched
+// kernels do not model: query j assumes the query id and word count of a slot are as at batch start
+// whenever the id equals its own (stale fields, repeated ids).  Scores written by earlier queries of the
+// batch are modelled (score_before).
 __global__ __launch_bounds__(256) void k_kfdb_state(DbDev D, QueryIn Q, QScratch X, StateDev St, int kind, int nq,
                                                     int32_t* __restrict__ status) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;

@@ -203,3 +203,91 @@ def setup_db(case, db, py_style: bool = False):
         n = case["n_slots"]
         for kind in range(3):
             db.set_state(kind, np.zeros(n, np.uint64), np.zeros(n, np.int32), case["init_scores"][kind])
+
+
+# --------------------------------------------------------------------------------------------------
+# numpy model of the GPU's batched reformulation (orbx_kfdb.hip): every query of a batch computed from
+# the scratch fields at batch start, list order from the (first shared word, add sequence) key, scores
+# written by earlier queries of the batch looked up (score_before), plus the interaction flag that
+# sends a batch back to one-query-at-a-time evaluation.  Must equal the sequential restatement on every
+# batch it does not flag.
+# --------------------------------------------------------------------------------------------------
+def batch_model(db: PyKfdb, kind, queries, seqs, members):
+    S = len(db.covis)
+    q0, w0, s0 = db.q[kind].copy(), db.w[kind].copy(), db.s[kind].copy()
+    sets = [set(db.bow[k][0].tolist()) if members[k] else set() for k in range(S)]
+    outs, hist = [], []
+    for qs, qid, ms, excl in queries:
+        ex = np.zeros(S, bool)
+        ex[list(excl)] = True
+        qwords = db.bow[qs][0].tolist()
+        pos = {w: p for p, w in enumerate(qwords)}
+        cnt = np.zeros(S, np.int64)
+        first = np.full(S, 1 << 30)
+        for k in range(S):
+            if kind == COVIS and ex[k]:
+                continue
+            common = sets[k].intersection(pos)
+            if common:
+                cnt[k] = len(common)
+                first[k] = min(pos[w] for w in common)
+        pushed = (cnt > 0) & (q0 != qid) & ~((kind == LOOP) & ex)
+        mx = int(cnt[pushed].max()) if pushed.any() else 0
+        mc = int(f32(mx) * f32(0.8))
+        cand = np.flatnonzero(pushed & (cnt > mc))
+        si = np.zeros(S, np.float32)
+        for k in cand:
+            si[k] = f32(l1_score(db.bow[qs], db.bow[k]))
+
+        def score_before(n):
+            if kind != COVIS:
+                for pc, pp, pm, ps in reversed(hist):
+                    if pp[n] and pc[n] > pm:
+                        return ps[n]
+            return s0[n]
+
+        def post(n):
+            if q0[n] == qid:
+                return True, w0[n] + cnt[n], s0[n]
+            if pushed[n]:
+                return True, cnt[n], (si[n] if kind != COVIS and cnt[n] > mc else score_before(n))
+            return False, 0, 0
+
+        best_acc = f32(0) if kind == RELOC else f32(ms)
+        accs = []
+        for k in cand:
+            if kind != RELOC and not (si[k] >= f32(ms)):
+                continue
+            acc, best, bk = si[k], si[k], int(k)
+            for n in db.covis[k]:
+                is_q, wp, sp = post(n)
+                if not is_q or (kind != RELOC and not wp > mc):
+                    continue
+                acc = f32(acc + sp)
+                if sp > best:
+                    bk, best = n, sp
+            accs.append(((first[k], seqs[k]), acc, bk))
+            if acc > best_acc:
+                best_acc = acc
+        retain = f32(0.75) * best_acc
+        out, seen = [], set()
+        for _, bk in sorted((key, bk) for key, acc, bk in accs if acc > retain):
+            if bk not in seen:
+                out.append(bk)
+                seen.add(bk)
+        outs.append(out)
+        hist.append((cnt, pushed, mc, si))
+    # interaction flag (k_kfdb_state)
+    flag = False
+    for k in range(S):
+        qf, touched = q0[k], False
+        for j, (qs, qid, ms, excl) in enumerate(queries):
+            if touched and (q0[k] == qid or qf == qid):
+                flag = True
+            c = hist[j][0][k]
+            if c == 0:
+                continue
+            touched = True
+            if qf != qid and not (kind == LOOP and k in set(excl)):
+                qf = qid
+    return outs, flag

@@ -59,3 +59,37 @@ def test_known_small_database():
     assert o.detect(RELOC, 0, 12).tolist() == [1]
     o.clear()
     assert o.detect(RELOC, 0, 13).tolist() == []
+
+
+@pytest.mark.parametrize("seed", range(100, 106))
+def test_batched_reformulation_matches_sequential(seed):
+    """The GPU's batched form (tests/kfdb_cases.batch_model) equals the sequential queries on every batch
+    it does not flag; flagged batches (repeated / stale ids) are re-run one by one by orbx_kfdb_detect."""
+    import copy
+
+    from kfdb_cases import batch_model
+    case = make_kfdb_case(seed, n_slots=150, n_queries=48, words_hi=400)
+    p = PyKfdb(case["n_vocab"], case["n_slots"])
+    setup_db(case, p, py_style=True)
+    members, seqs, nxt = [False] * case["n_slots"], [None] * case["n_slots"], 0
+    n_unflagged = 0
+    for op, arg in case["ops"]:
+        for k in (arg if op != "query" else []):
+            if op == "add":
+                p.add(k)
+                members[k], seqs[k], nxt = True, nxt, nxt + 1
+            else:
+                p.erase(k)
+                members[k], seqs[k] = False, None
+        if op != "query":
+            continue
+        for kind in (LOOP, COVIS, RELOC):
+            qsel = [a for a in arg if a[0] == kind]
+            if not qsel:
+                continue
+            model, flag = batch_model(copy.deepcopy(p), kind, [a[1:] for a in qsel], seqs, members)
+            ref = [p.detect(*a) for a in qsel]
+            if not flag:
+                assert model == ref
+                n_unflagged += 1
+    assert n_unflagged > 5
