@@ -9,9 +9,10 @@ and the keyframe path: every 5th left frame becomes a keyframe (MapPoint-valid =
 Tracking::CreateNewKeyFrame makes stereo MapPoints), its DBoW2 FeatureVector is computed on the GPU
 (KeyFrame::ComputeBoW, synthetic k=10 L=6 vocabulary of ORBvoc's shape), the keyframe packets are
 all-gathered over RCCL into every rank's MapFusion store (src/MapFusion.cc:83-88 replaced by
-ncclAllGather; a local insert at N=1) and each new keyframe is matched with SearchByBoW against 16
-candidate keyframes (other agents' at N>1 -- MapFusion.cc:275; the agent's own earlier ones at N=1 --
-LoopClosing.cc:288), so every rank does the same work at every N.  Inputs are resident in HBM before
+ncclAllGather; a local insert at N=1), each new keyframe queries the KeyFrameDatabase over the store
+(DetectLoopCandidates, src/MapFusion.cc:133) and is matched with SearchByBoW against its first 16
+candidates (other agents' at N>1 -- MapFusion.cc:136-144, :275; the agent's own earlier ones at N=1 --
+LoopClosing.cc:164, :288), so every rank does the same work at every N.  Inputs are resident in HBM before
 the timed region; weak scaling.
 
 Prints ONE JSON line on rank 0 (driver contract).  Run: python bench.py [--gpus N --steps K --warmup W]
@@ -66,11 +67,15 @@ def algorithmic_bytes(ex, mean_cand, mean_kps):
 
 def cpu_baseline(lefts, rights, tables, voc, seconds):
     """The same per-frame work on one host core with the oracle: extract L and R, ComputeStereoMatches
-    (band search + SAD refinement), and every KF_EVERY-th frame a keyframe: BoW transform + SearchByBoW
-    against the KF_CANDIDATES previous keyframes."""
+    (band search + SAD refinement), and every KF_EVERY-th frame a keyframe: BoW transform,
+    DetectLoopCandidates over a keyframe ring of the GPU store's size, SearchByBoW against the first
+    KF_CANDIDATES candidates, then the keyframe joins the database."""
     from oracle import oracle as O
     vocab = O.Vocabulary(voc)
-    kfs = []
+    ring = STORE_STEPS * max(1, 64 // KF_EVERY)
+    db = O.Kfdb(voc["n_words"] if "n_words" in voc else int(np.sum(voc["is_leaf"])), ring)
+    kfs = [None] * ring
+    n_kf = 0
     t0 = time.perf_counter()
     n = 0
     while True:
@@ -82,9 +87,14 @@ def cpu_baseline(lefts, rights, tables, voc, seconds):
             bow = vocab.transform(a["desc"], 4)
             kf = (a["desc"], a["kps"]["angle"], (depth > 0).astype(np.uint8),
                   (bow["fv_nodes"], bow["fv_offsets"], bow["fv_indices"]))
-            for c in kfs[-KF_CANDIDATES:]:
-                O.search_by_bow_kfkf(*kf, *c, 0.75, True)
-            kfs.append(kf)
+            slot = n_kf % ring
+            db.erase([slot])
+            db.set_bow(slot, bow["bow_words"], bow["bow_values"])
+            for c in db.detect(0, slot, n_kf + 1, 0.0)[:KF_CANDIDATES]:
+                O.search_by_bow_kfkf(*kf, *kfs[c], 0.75, True)
+            db.add([slot])
+            kfs[slot] = kf
+            n_kf += 1
         n += 1
         el = time.perf_counter() - t0
         if el >= seconds and n >= KF_EVERY:
@@ -209,7 +219,8 @@ def main():
         "config": {"workload": "C2+C3 stereo frame: ORBextractor x2 (1242x375, 8 levels, 2000 kpts) + stereo "
                                "L<->R 256-bit Hamming band match + SAD sub-pixel refinement; every 5th frame a keyframe: DBoW2 transform (k=10, "
                                "L=6) + " + ("RCCL all-gather of KF packets + " if world > 1 else "") +
-                               f"SearchByBoW vs {KF_CANDIDATES} candidate KFs",
+                               "KeyFrameDatabase DetectLoopCandidates over the KF store + "
+                               f"SearchByBoW vs the first {KF_CANDIDATES} candidates",
                    "keyframes_per_gpu_per_step": n_kf, "bow_pairs_per_gpu_per_step": n_kf * KF_CANDIDATES,
                    "global_batch": B * world, "frames_per_gpu_per_step": B, "image": [ROWS, COLS],
                    "nfeatures": NFEAT, "nlevels": NLEV, "parallelism": f"agent-per-gpu x{world}"},
@@ -257,9 +268,12 @@ def main():
         out["cpu_baseline"] = {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
                                "sample": f"{n} stereo frames of the same synthetic inputs and the same per-frame work "
                                          f"(2 extractions + ComputeStereoMatches; every {KF_EVERY}th frame BoW + "
-                                         f"SearchByBoW vs {KF_CANDIDATES} earlier keyframes), oracle/orb_oracle.cpp -O2, "
+                                         f"DetectLoopCandidates + SearchByBoW vs the first {KF_CANDIDATES} candidates), "
+                                         f"oracle/orb_oracle.cpp -O2, "
                                          f"1 thread, {secs:.1f} s"}
     out["fusion_gate_passed_per_step"] = round(int(gate.item()) / (args.steps + args.warmup + STORE_STEPS), 2)
+    if int(fusion.status.item()) & 2:
+        raise RuntimeError("KeyFrameDatabase query exceeded its candidate capacity")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -227,7 +227,8 @@ typedef struct orbx_kf_store {
 
 /* Many SearchByBoW(KeyFrame*, KeyFrame*) pairs in one launch over a device keyframe store — MapFusion's
  * cross-agent matches (src/MapFusion.cc:275 ComputeSim3, :849 CovisibilityDiscovery) and LoopClosing's
- * (src/LoopClosing.cc ComputeSim3).  d_pairs: n_pairs (kf1, kf2) slot pairs (int32); max_fv_nodes is the
+ * (src/LoopClosing.cc ComputeSim3).  d_pairs: n_pairs (kf1, kf2) slot pairs (int32; a pair with a negative
+ * slot is padding and gets no matches); max_fv_nodes is the
  * launch width per pair (workgroups stride over kf1's FeatureVector nodes, so any value >= 1 is correct; the
  * largest node count is the fastest).  Outputs: d_match12[p*capacity + i1] = KF2 index or -1, d_nmatches[p]. */
 int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const orbx_kf_store* store, const int32_t* d_pairs,
@@ -385,12 +386,21 @@ enum {
 int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device, orbx_kfdb** out);
 int orbx_kfdb_destroy(orbx_kfdb* db);
 int orbx_kfdb_info(const orbx_kfdb* db, int* n_vocab_words, int* max_slots, int* max_words, int* n_members);
+/* How a query finds the keyframes sharing its words (results are identical):
+ * ORBX_KFDB_INVERTED walks the inverted file (rebuilt on the device after membership changes), as the
+ * reference does; ORBX_KFDB_PAIRWISE intersects the query with every member's BowVector (no rebuild, cheaper
+ * for small databases); ORBX_KFDB_AUTO (default) picks pairwise up to 2048 members. */
+enum { ORBX_KFDB_AUTO = 0, ORBX_KFDB_INVERTED = 1, ORBX_KFDB_PAIRWISE = 2 };
+int orbx_kfdb_set_strategy(orbx_kfdb* db, int strategy);
 /* Store a slot's BowVector (KeyFrame::mBowVec); word ids strictly ascending and < n_vocab_words. */
 int orbx_kfdb_set_bow(orbx_kfdb* db, int slot, const uint32_t* words, const double* values, int n);
-/* Device form: BowVector i of an orbx_vocab_transform_batch_device output (words/values at i*stride,
- * d_n_words[i]) into slot d_slots[i], for i < n.  Word ids must satisfy the rules above. */
-int orbx_kfdb_set_bow_device(orbx_kfdb* db, const int32_t* d_slots, int n, const uint32_t* d_words, const double* d_values,
-                             const int32_t* d_n_words, int stride, void* stream);
+/* Device form: BowVector i (words at d_words + i*word_stride, values at d_values + i*value_stride, size
+ * d_n_words[i*n_stride]; strides in elements) into slot d_slots[i], for i < n: an
+ * orbx_vocab_transform_batch_device output (strides capacity, capacity, 1) or an array of exchanged
+ * keyframe packets.  Word ids must satisfy the rules above. */
+int orbx_kfdb_set_bow_device(orbx_kfdb* db, const int32_t* d_slots, int n, const uint32_t* d_words, long long word_stride,
+                             const double* d_values, long long value_stride, const int32_t* d_n_words, long long n_stride,
+                             void* stream);
 /* GetBestCovisibilityKeyFrames(10) of slots[i]: best[i*10 .. i*10+9], best first, -1 padded. */
 int orbx_kfdb_set_covisibility(orbx_kfdb* db, const int32_t* slots, int n, const int32_t* best);
 /* KeyFrameDatabase::add (:40-46) in order (adding a slot already in the database is ORBX_ERR_ARG),
@@ -422,6 +432,14 @@ int orbx_kfdb_detect(orbx_kfdb* db, int kind, const int32_t* query_slots, const 
 int orbx_kfdb_detect_device(orbx_kfdb* db, int kind, const int32_t* d_query_slots, const uint64_t* d_query_ids,
                             const float* d_min_scores, int nq, const int32_t* d_excl_offsets, const int32_t* d_excl_slots,
                             int32_t* d_out, int out_stride, int32_t* d_out_n, int32_t* d_status, void* stream);
+/* MapFusion's use of the candidates (src/MapFusion.cc:136-144, :275): for query q, the first k of its
+ * candidates d_cand[q*cand_stride ..+ d_n_cand[q]) whose map differs from the query's
+ * (d_slot_group[cand] != d_query_group[q]; both NULL = keep all, LoopClosing's own-map case) become
+ * SearchByBoW pairs d_pairs[(q*k + j)*2 ..] = (query slot, candidate slot), padded with (query slot, -1)
+ * (orbx_search_by_bow_kfkf_pairs_device skips those: no matches). */
+int orbx_kfdb_candidate_pairs_device(const int32_t* d_cand, int cand_stride, const int32_t* d_n_cand, const int32_t* d_query_slots,
+                                     int nq, const int32_t* d_slot_group, const int32_t* d_query_group, int k, int32_t* d_pairs,
+                                     void* stream);
 
 #ifdef __cplusplus
 }

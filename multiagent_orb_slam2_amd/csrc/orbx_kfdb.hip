@@ -58,13 +58,15 @@ enum { KIND_LOOP = ORBX_KFDB_LOOP, KIND_COVIS = ORBX_KFDB_COVIS, KIND_RELOC = OR
 struct QScratch {
     int32_t* cnt;        // words shared with the query (atomic)
     int32_t* first;      // position of the first shared query word (atomic min; INT_MAX-ish when none)
-    uint8_t* excl;       // exclusion set of the query (connected / ignored keyframes)
+    uint8_t* excl;       // exclusion set of the query (connected / ignored keyframes); NULL = none in the batch
     float* si;           // L1 score of scored keyframes
     int32_t* cand;       // compacted scored keyframes (any order)
     float* acc;          // accumulated score of candidate i (by cand position)
     int32_t* best;       // best keyframe of candidate i
     int32_t* meta;       // per query: [0] npushed, [1] minCommon, [2] ncand
 };
+
+__device__ __forceinline__ bool excl_at(const QScratch& X, size_t i) { return X.excl && X.excl[i]; }
 
 struct DbDev {
     const uint32_t* bw;      // [S][maxw] word ids ascending
@@ -155,18 +157,42 @@ __global__ __launch_bounds__(256) void k_if_scatter(DbDev D, const int32_t* __re
 }
 
 __global__ __launch_bounds__(256) void k_set_bow(DbDev D, uint32_t* __restrict__ bw, double* __restrict__ bv, int32_t* __restrict__ bn,
-                                                 const int32_t* __restrict__ slots, const uint32_t* __restrict__ words,
-                                                 const double* __restrict__ values, const int32_t* __restrict__ n_words,
-                                                 int stride) {
+                                                 const int32_t* __restrict__ slots, const uint32_t* __restrict__ words, long long word_stride,
+                                                 const double* __restrict__ values, long long value_stride,
+                                                 const int32_t* __restrict__ n_words, long long n_stride) {
     const int i = blockIdx.x;
     const int k = slots[i];
     if (k < 0 || k >= D.S) return;
-    const int n = min(n_words[i], D.maxw);
+    const int n = max(0, min(n_words[(size_t)i * n_stride], D.maxw));
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        bw[(size_t)k * D.maxw + j] = words[(size_t)i * stride + j];
-        bv[(size_t)k * D.maxw + j] = values[(size_t)i * stride + j];
+        bw[(size_t)k * D.maxw + j] = words[(size_t)i * word_stride + j];
+        bv[(size_t)k * D.maxw + j] = values[(size_t)i * value_stride + j];
     }
     if (threadIdx.x == 0) bn[k] = n;
+}
+
+// MapFusion keeps the first k candidates of another map (src/MapFusion.cc:136-144 drops same-map
+// candidates) and matches the query against each (:275).  One thread per query; pairs (query, cand) or
+// (query, -1) padding, k per query.
+__global__ __launch_bounds__(64) void k_kfdb_pairs(const int32_t* __restrict__ cand, int cand_stride, const int32_t* __restrict__ n_cand,
+                                                   const int32_t* __restrict__ qslots, int nq, const int32_t* __restrict__ slot_group,
+                                                   const int32_t* __restrict__ query_group, int k, int32_t* __restrict__ pairs) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    const int qs = qslots[q];
+    const int g = (slot_group && query_group) ? query_group[q] : 0;
+    int m = 0;
+    for (int i = 0; i < n_cand[q] && m < k; ++i) {
+        const int c = cand[(size_t)q * cand_stride + i];
+        if (slot_group && query_group && slot_group[c] == g) continue;
+        pairs[2 * ((size_t)q * k + m)] = qs;
+        pairs[2 * ((size_t)q * k + m) + 1] = c;
+        ++m;
+    }
+    for (; m < k; ++m) {
+        pairs[2 * ((size_t)q * k + m)] = qs;
+        pairs[2 * ((size_t)q * k + m) + 1] = -1;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -239,9 +265,70 @@ __global__ __launch_bounds__(256) void k_kfdb_share(DbDev D, QueryIn Q, QScratch
     const size_t row = (size_t)q * D.S;
     for (int e = D.if_off[w]; e < D.if_off[w + 1]; ++e) {
         const int k = D.if_slot[e];
-        if (kind == KIND_COVIS && X.excl[row + k]) continue;   // :220 ignored keyframes are skipped
+        if (kind == KIND_COVIS && excl_at(X, row + k)) continue;   // :220 ignored keyframes are skipped
         atomicAdd(&X.cnt[row + k], 1);
         atomicMin(&X.first[row + k], p);
+    }
+}
+
+// Small databases: no inverted file.  One wave per (query, slot) intersects the slot's BowVector with the
+// query's (staged in LDS, binary search per slot word) and produces the same word count and first shared
+// query word as k_kfdb_share -- plus the L1 score, summed in ascending word order as k_kfdb_score does.
+__global__ __launch_bounds__(512) void k_kfdb_pairwise(DbDev D, QueryIn Q, QScratch X, int kind) {
+    extern __shared__ unsigned char smem[];
+    double* qv = reinterpret_cast<double*>(smem);
+    uint32_t* qw = reinterpret_cast<uint32_t*>(qv + D.maxw);
+    const int q = blockIdx.y;
+    const int qs = Q.slot[q];
+    const int nq = D.bn[qs];
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+        qw[i] = D.bw[(size_t)qs * D.maxw + i];
+        qv[i] = D.bv[(size_t)qs * D.maxw + i];
+    }
+    __syncthreads();
+    const int waves = blockDim.x / kWave;
+    const size_t row = (size_t)q * D.S;
+    for (int k = blockIdx.x * waves + (int)(threadIdx.x / kWave); k < D.S; k += gridDim.x * waves) {
+        int c = 0, first = 0x7f7f7f7f;
+        double score = 0.0;
+        if (D.seq[k] != kNoSeq && !(kind == KIND_COVIS && excl_at(X, row + k))) {
+            const uint32_t* cw = D.bw + (size_t)k * D.maxw;
+            const double* cv = D.bv + (size_t)k * D.maxw;
+            const int nc = D.bn[k];
+            for (int base = 0; base < nc; base += kWave) {
+                const int i = base + lane_id();
+                double term = 0.0;
+                int pos = 0x7f7f7f7f;
+                bool found = false;
+                if (i < nc && nq > 0) {
+                    const uint32_t w = cw[i];
+                    int lo = 0, hi = nq;
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (qw[mid] < w) lo = mid + 1; else hi = mid;
+                    }
+                    if (lo < nq && qw[lo] == w) {
+                        const double vi = qv[lo], wi = cv[i];
+                        term = __dsub_rn(__dsub_rn(fabs(__dsub_rn(vi, wi)), fabs(vi)), fabs(wi));
+                        pos = lo;
+                        found = true;
+                    }
+                }
+                uint64_t m = __ballot(found);
+                c += __popcll(m);
+                first = min(first, (int)wave_min_u32((uint32_t)pos));
+                while (m) {
+                    const int l = __builtin_ctzll(m);
+                    score = __dadd_rn(score, readlane_f64(term, l));
+                    m &= m - 1;
+                }
+            }
+        }
+        if (lane_id() == 0) {
+            X.cnt[row + k] = c;
+            X.first[row + k] = first;
+            X.si[row + k] = (float)(-score / 2.0);
+        }
     }
 }
 
@@ -261,7 +348,7 @@ __global__ __launch_bounds__(1024) void k_kfdb_select(DbDev D, QueryIn Q, QScrat
     int mx = 0, np = 0;
     for (int k = threadIdx.x; k < D.S; k += blockDim.x) {
         const int c = X.cnt[row + k];
-        if (kf_pushed(kind, c, St.q[k] == id, X.excl[row + k])) {
+        if (kf_pushed(kind, c, St.q[k] == id, excl_at(X, row + k))) {
             mx = max(mx, c);
             ++np;
         }
@@ -272,7 +359,7 @@ __global__ __launch_bounds__(1024) void k_kfdb_select(DbDev D, QueryIn Q, QScrat
     const int minCommon = (int)((float)s_max * 0.8f);          // int minCommonWords = maxCommonWords*0.8f
     for (int k = threadIdx.x; k < D.S; k += blockDim.x) {
         const int c = X.cnt[row + k];
-        if (kf_pushed(kind, c, St.q[k] == id, X.excl[row + k]) && c > minCommon) {
+        if (kf_pushed(kind, c, St.q[k] == id, excl_at(X, row + k)) && c > minCommon) {
             const int pos = atomicAdd(&s_nc, 1);
             X.cand[row + pos] = k;
         }
@@ -323,7 +410,7 @@ __device__ float score_before(int kind, int n, int q, const QueryIn& Q, const QS
         for (int i = q - 1; i >= 0; --i) {
             const size_t r = (size_t)i * S;
             const int c = X.cnt[r + n];
-            if (kf_pushed(kind, c, St.q[n] == Q.id[i], X.excl[r + n]) && c > X.meta[i * 4 + 1]) return X.si[r + n];
+            if (kf_pushed(kind, c, St.q[n] == Q.id[i], excl_at(X, r + n)) && c > X.meta[i * 4 + 1]) return X.si[r + n];
         }
     return St.s[n];
 }
@@ -334,7 +421,7 @@ __device__ __forceinline__ PostState post_state(int kind, int n, int q, const Qu
     const size_t row = (size_t)q * S;
     const int c = X.cnt[row + n];
     const bool stale = St.q[n] == id;
-    const bool ex = X.excl[row + n];
+    const bool ex = excl_at(X, row + n);
     PostState p;
     if (stale) {
         p.is_query = true;
@@ -494,7 +581,7 @@ __global__ __launch_bounds__(256) void k_kfdb_state(DbDev D, QueryIn Q, QScratch
         const size_t row = (size_t)j * D.S;
         const int c = X.cnt[row + k];
         if (c == 0) continue;                            // COVIS-ignored slots were never counted
-        const bool ex = X.excl[row + k];
+        const bool ex = excl_at(X, row + k);
         touched = true;
         if (qf == id) {
             wf += c;
@@ -551,8 +638,13 @@ struct orbx_kfdb {
     size_t scratch_bytes = 0;
     std::vector<uint32_t> seq;     // host mirror of membership (add order)
     std::vector<int32_t> members;
+    uint32_t* h_stage = nullptr;   // 2 pinned staging buffers of seq + members (membership uploads never stall
+    hipEvent_t stage_done[2] = {nullptr, nullptr};   // on a pageable copy; each is reused two uploads later)
+    int stage_next = 0;
     uint32_t next_seq = 0;
-    bool dirty = true;
+    bool dirty = true;             // inverted file stale (membership or a member's BowVector changed)
+    bool seq_dirty = true;         // device membership (d_seq, d_members) stale
+    int strategy = ORBX_KFDB_AUTO;
 };
 
 namespace {
@@ -594,11 +686,27 @@ size_t qscratch_layout(int nq, int S, unsigned char* base, QScratch* X) {
     return o;
 }
 
+int upload_membership(orbx_kfdb* db, hipStream_t s) {
+    if (!db->seq_dirty) return ORBX_OK;
+    const int nm = (int)db->members.size();
+    const int b = db->stage_next;
+    db->stage_next ^= 1;
+    uint32_t* stage = db->h_stage + (size_t)b * 2 * db->S;
+    ORBX_HIP(hipEventSynchronize(db->stage_done[b]));       // the upload before last has left this buffer
+    std::memcpy(stage, db->seq.data(), sizeof(uint32_t) * db->S);
+    if (nm) std::memcpy(stage + db->S, db->members.data(), sizeof(int32_t) * nm);
+    ORBX_HIP(hipMemcpyAsync(db->d_seq, stage, sizeof(uint32_t) * db->S, hipMemcpyHostToDevice, s));
+    if (nm) ORBX_HIP(hipMemcpyAsync(db->d_members, stage + db->S, sizeof(int32_t) * nm, hipMemcpyHostToDevice, s));
+    ORBX_HIP(hipEventRecord(db->stage_done[b], s));
+    db->seq_dirty = false;
+    return ORBX_OK;
+}
+
 int rebuild_inverted_file(orbx_kfdb* db, hipStream_t s) {
+    int st = upload_membership(db, s);
+    if (st) return st;
     if (!db->dirty) return ORBX_OK;
     const int nm = (int)db->members.size();
-    ORBX_HIP(hipMemcpyAsync(db->d_seq, db->seq.data(), sizeof(uint32_t) * db->S, hipMemcpyHostToDevice, s));
-    if (nm) ORBX_HIP(hipMemcpyAsync(db->d_members, db->members.data(), sizeof(int32_t) * nm, hipMemcpyHostToDevice, s));
     const int n = db->n_vocab + 1;
     ORBX_HIP(hipMemsetAsync(db->d_if_off, 0, sizeof(int32_t) * n, s));
     DbDev D = dev_view(db);
@@ -613,24 +721,36 @@ int rebuild_inverted_file(orbx_kfdb* db, hipStream_t s) {
     return ORBX_OK;
 }
 
+constexpr int kPairwiseMaxMembers = 2048;   // auto strategy: below this, intersect pairwise (no inverted file)
+
 // The query batch on stream s; d_* are device pointers.  Scratch rows at 'base' (nq x S).
 int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned char* base, int32_t* d_out, int out_stride,
                  int32_t* d_out_n, int32_t* d_status, hipStream_t s) {
-    int st = rebuild_inverted_file(db, s);
+    const bool pairwise = db->strategy == ORBX_KFDB_PAIRWISE ||
+                          (db->strategy == ORBX_KFDB_AUTO && (int)db->members.size() <= kPairwiseMaxMembers);
+    int st = pairwise ? upload_membership(db, s) : rebuild_inverted_file(db, s);
     if (st) return st;
     QScratch X;
     qscratch_layout(nq, db->S, base, &X);
     const size_t r = (size_t)nq * db->S;
-    ORBX_HIP(hipMemsetAsync(X.cnt, 0, 4 * r, s));
-    ORBX_HIP(hipMemsetAsync(X.first, 0x7f, 4 * r, s));
-    ORBX_HIP(hipMemsetAsync(X.excl, 0, r, s));
+    if (!Q.excl_off) X.excl = nullptr;
     DbDev D = dev_view(db);
     StateDev St{db->d_q[kind], db->d_w[kind], db->d_s[kind]};
-    hipLaunchKernelGGL(k_kfdb_mark_excl, dim3(nq), dim3(256), 0, s, Q, X, db->S);
-    hipLaunchKernelGGL(k_kfdb_share, dim3((db->maxw + 255) / 256, nq), dim3(256), 0, s, D, Q, X, kind);
-    hipLaunchKernelGGL(k_kfdb_select, dim3(nq), dim3(1024), 0, s, D, Q, X, St, kind);
+    if (X.excl) {
+        ORBX_HIP(hipMemsetAsync(X.excl, 0, r, s));
+        hipLaunchKernelGGL(k_kfdb_mark_excl, dim3(nq), dim3(256), 0, s, Q, X, db->S);
+    }
     const size_t lds = (size_t)db->maxw * (sizeof(double) + sizeof(uint32_t));
-    hipLaunchKernelGGL(k_kfdb_score, dim3(32, nq), dim3(256), lds, s, D, Q, X);
+    if (pairwise) {
+        const int gx = std::min((db->S + 7) / 8, 64);
+        hipLaunchKernelGGL(k_kfdb_pairwise, dim3(gx, nq), dim3(512), lds, s, D, Q, X, kind);
+    } else {
+        ORBX_HIP(hipMemsetAsync(X.cnt, 0, 4 * r, s));
+        ORBX_HIP(hipMemsetAsync(X.first, 0x7f, 4 * r, s));
+        hipLaunchKernelGGL(k_kfdb_share, dim3((db->maxw + 255) / 256, nq), dim3(256), 0, s, D, Q, X, kind);
+    }
+    hipLaunchKernelGGL(k_kfdb_select, dim3(nq), dim3(1024), 0, s, D, Q, X, St, kind);
+    if (!pairwise) hipLaunchKernelGGL(k_kfdb_score, dim3(32, nq), dim3(256), lds, s, D, Q, X);
     hipLaunchKernelGGL(k_kfdb_accum, dim3(nq), dim3(256), 0, s, D, Q, X, St, kind, d_out, out_stride, d_out_n, d_status);
     hipLaunchKernelGGL(k_kfdb_state, dim3((db->S + 255) / 256), dim3(256), 0, s, D, Q, X, St, kind, nq, d_status);
     ORBX_HIP(hipGetLastError());
@@ -680,6 +800,11 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
         alloc((void**)&db->d_w[k], 4 * S);
         alloc((void**)&db->d_s[k], 4 * S);
     }
+    if (e == hipSuccess) e = hipHostMalloc((void**)&db->h_stage, 16 * S, hipHostMallocDefault);
+    for (int b = 0; b < 2; ++b) {
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&db->stage_done[b], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(db->stage_done[b], db->stream);
+    }
     if (e != hipSuccess) {
         set_error("kfdb create: %s", hipGetErrorString(e));
         orbx_kfdb_destroy(db);
@@ -702,6 +827,12 @@ int orbx_kfdb_destroy(orbx_kfdb* db) {
         if (db->d_w[k]) (void)hipFree(db->d_w[k]);
         if (db->d_s[k]) (void)hipFree(db->d_s[k]);
     }
+    for (int b = 0; b < 2; ++b)
+        if (db->stage_done[b]) {
+            (void)hipEventSynchronize(db->stage_done[b]);
+            (void)hipEventDestroy(db->stage_done[b]);
+        }
+    if (db->h_stage) (void)hipHostFree(db->h_stage);
     if (db->stream) (void)hipStreamDestroy(db->stream);
     delete db;
     return ORBX_OK;
@@ -713,6 +844,12 @@ int orbx_kfdb_info(const orbx_kfdb* db, int* n_vocab_words, int* max_slots, int*
     if (max_slots) *max_slots = db->S;
     if (max_words) *max_words = db->maxw;
     if (n_members) *n_members = (int)db->members.size();
+    return ORBX_OK;
+}
+
+int orbx_kfdb_set_strategy(orbx_kfdb* db, int strategy) {
+    ORBX_REQUIRE(db && strategy >= ORBX_KFDB_AUTO && strategy <= ORBX_KFDB_PAIRWISE, ORBX_ERR_ARG, "bad strategy");
+    db->strategy = strategy;
     return ORBX_OK;
 }
 
@@ -735,17 +872,30 @@ int orbx_kfdb_set_bow(orbx_kfdb* db, int slot, const uint32_t* words, const doub
     return ORBX_OK;
 }
 
-int orbx_kfdb_set_bow_device(orbx_kfdb* db, const int32_t* d_slots, int n, const uint32_t* d_words, const double* d_values,
-                             const int32_t* d_n_words, int stride, void* stream) {
-    ORBX_REQUIRE(db && n >= 0 && (n == 0 || (d_slots && d_words && d_values && d_n_words)) && stride >= 0, ORBX_ERR_ARG,
-                 "bad argument");
+int orbx_kfdb_set_bow_device(orbx_kfdb* db, const int32_t* d_slots, int n, const uint32_t* d_words, long long word_stride,
+                             const double* d_values, long long value_stride, const int32_t* d_n_words, long long n_stride,
+                             void* stream) {
+    ORBX_REQUIRE(db && n >= 0 && (n == 0 || (d_slots && d_words && d_values && d_n_words)) && word_stride >= 0 &&
+                     value_stride >= 0 && n_stride >= 0, ORBX_ERR_ARG, "bad argument");
     if (n == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(db->device));
     DbDev D = dev_view(db);
     hipLaunchKernelGGL(k_set_bow, dim3(n), dim3(256), 0, (hipStream_t)stream, D, db->d_bw, db->d_bv, db->d_bn, d_slots, d_words,
-                       d_values, d_n_words, stride);
+                       word_stride, d_values, value_stride, d_n_words, n_stride);
     ORBX_HIP(hipGetLastError());
     db->dirty = true;
+    return ORBX_OK;
+}
+
+int orbx_kfdb_candidate_pairs_device(const int32_t* d_cand, int cand_stride, const int32_t* d_n_cand, const int32_t* d_query_slots,
+                                     int nq, const int32_t* d_slot_group, const int32_t* d_query_group, int k, int32_t* d_pairs,
+                                     void* stream) {
+    ORBX_REQUIRE(nq >= 0 && k >= 0 && cand_stride >= 0, ORBX_ERR_ARG, "bad argument");
+    if (nq == 0 || k == 0) return ORBX_OK;
+    ORBX_REQUIRE(d_cand && d_n_cand && d_query_slots && d_pairs, ORBX_ERR_ARG, "null buffers");
+    hipLaunchKernelGGL(k_kfdb_pairs, dim3((nq + 63) / 64), dim3(64), 0, (hipStream_t)stream, d_cand, cand_stride, d_n_cand,
+                       d_query_slots, nq, d_slot_group, d_query_group, k, d_pairs);
+    ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }
 
@@ -774,7 +924,7 @@ int orbx_kfdb_add(orbx_kfdb* db, const int32_t* slots, int n) {
         db->seq[k] = db->next_seq++;
         db->members.push_back(k);
     }
-    if (n) db->dirty = true;
+    if (n) db->dirty = db->seq_dirty = true;
     return ORBX_OK;
 }
 
@@ -789,7 +939,7 @@ int orbx_kfdb_erase(orbx_kfdb* db, const int32_t* slots, int n) {
         db->members.erase(std::find(db->members.begin(), db->members.end(), k));
         any = true;
     }
-    if (any) db->dirty = true;
+    if (any) db->dirty = db->seq_dirty = true;
     return ORBX_OK;
 }
 
@@ -797,7 +947,7 @@ int orbx_kfdb_clear(orbx_kfdb* db) {
     ORBX_REQUIRE(db, ORBX_ERR_ARG, "db is NULL");
     std::fill(db->seq.begin(), db->seq.end(), kNoSeq);
     db->members.clear();
-    db->dirty = true;
+    db->dirty = db->seq_dirty = true;
     return ORBX_OK;
 }
 

@@ -381,6 +381,7 @@ __global__ __launch_bounds__(64) void k_bow_pairs(orbx_kf_store S, const int32_t
                                                   int32_t* match, int32_t* bin, int32_t* hist, int32_t* nmatch) {
     const int pr = blockIdx.y;
     const int k1 = pairs[2 * pr], k2 = pairs[2 * pr + 1];
+    if (k1 < 0 || k2 < 0) return;                       // padding pair: no matches
     BowArgs A;
     A.f1 = store_fv(S, k1);
     if ((int)blockIdx.x >= A.f1.n) return;

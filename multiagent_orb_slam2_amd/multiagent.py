@@ -20,7 +20,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-HEADER = 16        # int32 count, int32 agent, int32 frame, int32 n_fv (FeatureVector node count)
+HEADER = 32        # int32 count, agent, frame, n_fv (FeatureVector nodes), n_words (BowVector entries), 3 x pad
 KP_BYTES = 28
 DESC_BYTES = 32
 
@@ -47,17 +47,20 @@ class PacketLayout:
     """Byte layout of one keyframe packet (every field 16-byte aligned, so a packet array is directly an
     orbx_kf_store with all strides = packet bytes):
 
-        header 16 | kps cap*28 | desc cap*32 | fv_nodes cap*4 | fv_offsets (cap+1)*4 | fv_indices cap*4 | valid cap
+        header 32 | kps cap*28 | desc cap*32 | fv_nodes cap*4 | fv_offsets (cap+1)*4 | fv_indices cap*4 | valid cap
+        | bow_words cap*4 | bow_values cap*8
 
-    i.e. what KeyFrame carries into MapFusion for SearchByBoW: keypoints (angle), descriptors, the BoW
-    FeatureVector (KeyFrame::mFeatVec) and the MapPoint-valid flags (KeyFrame.h:171-185)."""
+    i.e. what KeyFrame carries into MapFusion: keypoints (angle), descriptors, the BoW FeatureVector
+    (KeyFrame::mFeatVec) and MapPoint-valid flags for SearchByBoW (KeyFrame.h:171-185), and the BowVector
+    (KeyFrame::mBowVec) for the KeyFrameDatabase query that picks the candidates (src/MapFusion.cc:133)."""
 
     def __init__(self, capacity: int):
         self.capacity = capacity
         o = HEADER
         self.offsets = {}
         for name, size in (("kps", capacity * KP_BYTES), ("desc", capacity * DESC_BYTES), ("fv_nodes", capacity * 4),
-                           ("fv_offsets", (capacity + 1) * 4), ("fv_indices", capacity * 4), ("valid", capacity)):
+                           ("fv_offsets", (capacity + 1) * 4), ("fv_indices", capacity * 4), ("valid", capacity),
+                           ("bow_words", capacity * 4), ("bow_values", capacity * 8)):
             self.offsets[name] = o
             o = _a16(o + size)
         self.bytes = o
@@ -73,18 +76,21 @@ def pack_keyframes(kps, desc, counts, valid, agent: int, frames, capacity: int, 
     kps: (n, capacity, 28) uint8, desc: (n, capacity, 32) uint8, counts: (n,) int32,
     valid: (n, capacity) uint8 (keypoint has a MapPoint), frames: (n,) frame ids (device tensor or host list),
     fv: optional dict of the vocabulary batch outputs (fv_nodes (n, cap), fv_offsets (n, cap+1),
-    fv_indices (n, cap), n_fv (n,)), as ORBVocabulary.transform_batch_device returns them."""
+    fv_indices (n, cap), n_fv (n,), bow_words / bow_values (n, cap), n_words (n,)), as
+    ORBVocabulary.transform_batch_device returns them."""
     import torch
     n = kps.shape[0]
     dev = kps.device
     lay = PacketLayout(capacity)
     out = torch.zeros((n, lay.bytes), dtype=torch.uint8, device=dev)
     n_fv = fv["n_fv"].to(torch.int32) if fv is not None else torch.zeros_like(counts, dtype=torch.int32)
+    n_words = fv["n_words"].to(torch.int32) if fv is not None and "n_words" in fv else torch.zeros_like(n_fv)
     if not torch.is_tensor(frames):   # a host list goes through pinned memory on a GPU (a pageable copy stalls)
         f = torch.as_tensor(frames, dtype=torch.int32)
         frames = f.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else f.to(dev)
+    z = torch.zeros_like(n_fv)
     hdr = torch.stack([counts.to(torch.int32), torch.full_like(counts, agent, dtype=torch.int32),
-                       frames.to(torch.int32), n_fv], 1)
+                       frames.to(torch.int32), n_fv, n_words, z, z, z], 1)
     out[:, :HEADER] = hdr.contiguous().view(torch.uint8).view(n, HEADER)
 
     def put(name, t, nbytes):
@@ -98,6 +104,9 @@ def pack_keyframes(kps, desc, counts, valid, agent: int, frames, capacity: int, 
         put("fv_nodes", fv["fv_nodes"], capacity * 4)
         put("fv_offsets", fv["fv_offsets"], (capacity + 1) * 4)
         put("fv_indices", fv["fv_indices"], capacity * 4)
+        if "bow_words" in fv:
+            put("bow_words", fv["bow_words"], capacity * 4)
+            put("bow_values", fv["bow_values"], capacity * 8)
     return out
 
 
@@ -110,6 +119,7 @@ class KeyframeView:
     desc: np.ndarray     # (count, 32) uint8
     valid: np.ndarray    # (count,) uint8
     featvec: tuple = None  # (node ids uint32, offsets int32, indices int32) or None
+    bow: tuple = None      # BowVector (word ids uint32 ascending, values float64) or None
 
 
 def unpack_keyframes(packets, capacity: int) -> list[KeyframeView]:
@@ -119,7 +129,7 @@ def unpack_keyframes(packets, capacity: int) -> list[KeyframeView]:
     o = lay.offsets
     out = []
     for row in p:
-        cnt, agent, frame, n_fv = row[:HEADER].view(np.int32)
+        cnt, agent, frame, n_fv, n_words = row[:HEADER].view(np.int32)[:5]
         kp = row[o["kps"]:o["kps"] + capacity * KP_BYTES].view(KP_DTYPE)[:cnt].copy()
         d = row[o["desc"]:o["desc"] + capacity * DESC_BYTES].reshape(capacity, DESC_BYTES)[:cnt].copy()
         v = row[o["valid"]:o["valid"] + capacity][:cnt].copy()
@@ -129,7 +139,11 @@ def unpack_keyframes(packets, capacity: int) -> list[KeyframeView]:
             offs = row[o["fv_offsets"]:o["fv_offsets"] + 4 * (capacity + 1)].view(np.int32)[:n_fv + 1].copy()
             idx = row[o["fv_indices"]:o["fv_indices"] + 4 * capacity].view(np.int32)[:offs[-1]].copy()
             fv = (nodes, offs, idx)
-        out.append(KeyframeView(int(cnt), int(agent), int(frame), kp, d, v, fv))
+        bow = None
+        if n_words > 0:
+            bow = (row[o["bow_words"]:o["bow_words"] + 4 * capacity].view(np.uint32)[:n_words].copy(),
+                   row[o["bow_values"]:o["bow_values"] + 8 * capacity].view(np.float64)[:n_words].copy())
+        out.append(KeyframeView(int(cnt), int(agent), int(frame), kp, d, v, fv, bow))
     return out
 
 
@@ -272,46 +286,90 @@ class DeviceKeyframeStore:
 class KeyframeFusion:
     """The per-agent keyframe path after the front-end, all on the device:
 
-        new keyframes (extractor batch rows) -> ORBVocabulary::transform (BoW FeatureVector, level L-4,
-        src/KeyFrame.cc ComputeBoW) -> packets -> all-gather into every rank's DeviceKeyframeStore
-        (MapFusion ingress, src/MapFusion.cc:83-88) -> SearchByBoW(new KF, candidate KF) for this rank's
-        new keyframes only (sharded by query keyframe) -> MapFusion's 20-match gate (src/MapFusion.cc:275-281).
+        new keyframes (extractor batch rows) -> ORBVocabulary::transform (BowVector + FeatureVector at level
+        L-4, src/KeyFrame.cc ComputeBoW) -> packets -> all-gather into every rank's DeviceKeyframeStore
+        (MapFusion ingress, src/MapFusion.cc:83-88) -> KeyFrameDatabase::DetectLoopCandidates for this rank's
+        new keyframes (src/MapFusion.cc:133; sharded by query keyframe) -> first k candidates of another map
+        (:136-144) -> SearchByBoW(new KF, candidate) (:275) -> the 20-match gate (:275-281) -> the new
+        keyframes join the database (:149 / :222).
 
-    With one agent (no exchange) the candidates are the agent's own earlier keyframes, as LoopClosing's
-    ComputeSim3 matches them (src/LoopClosing.cc), so every rank does the same work at every N."""
+    The database covers the store ring: a slot leaves it when the ring overwrites it.  There is no
+    covisibility graph in this front-end-only pipeline, so queries exclude nothing and use minScore 0
+    (the reference bounds it by the scores of the query's covisible keyframes, :100-131).  With one agent
+    (no exchange) candidates may come from the agent's own map, as LoopClosing's (src/LoopClosing.cc:164)."""
 
     def __init__(self, matcher, vocab, capacity: int, slots: int, device, agent: int = 0, exchange=None,
                  candidates: int = 16, levelsup: int = 4, min_matches: int = 20):
+        import torch
+
+        from .orbx import KeyFrameDatabase
         self.matcher, self.vocab, self.capacity = matcher, vocab, capacity
         self.store = DeviceKeyframeStore(capacity, slots, device)
         self.agent, self.exchange = agent, exchange
         self.k, self.levelsup, self.min_matches = candidates, levelsup, min_matches
         info = vocab.info()
         self.max_fv_nodes = min(capacity, info["k"] ** max(info["L"] - levelsup, 0) + 1)   # launch width hint
-        self._pairs = {}
+        self.db = KeyFrameDatabase(info["n_words"], slots, max_words=min(capacity, 4096), device=device.index or 0)
+        self.device = device
+        self._slot_tensors = {}
+        self._next_id = 1
+        self.slot_group = torch.full((slots,), -1, dtype=torch.int32, device=device)   # map (agent) of each slot
+        self.status = torch.zeros((1,), dtype=torch.int32, device=device)             # orbx_kfdb_detect_device flags
 
-    def _device_pairs(self, pairs: np.ndarray, device):
+    def _slots(self, r: range):
         import torch
-        key = pairs.tobytes()
-        t = self._pairs.get(key)
+        key = (r.start, r.stop)
+        t = self._slot_tensors.get(key)
         if t is None:
-            t = torch.from_numpy(pairs).to(device)
-            self._pairs[key] = t
+            t = torch.arange(r.start, r.stop, dtype=torch.int32, device=self.device)
+            self._slot_tensors[key] = t
         return t
 
     def step(self, kps, desc, counts, valid, frames, stream=None):
         """kps (n, cap, 28) u8, desc (n, cap, 32) u8, counts (n,), valid (n, cap) u8: this agent's new
-        keyframes.  Returns (pairs (P, 2) device, match12 (P, cap), nmatches (P,), passed (P,) bool)."""
+        keyframes.  Returns (pairs (n*k, 2) device, match12 (n*k, cap), nmatches (n*k,), passed (n*k,) bool);
+        pairs (query, -1) are padding (fewer than k candidates) with no matches."""
+        import torch
         n = kps.shape[0]
         fv = self.vocab.transform_batch_device(desc.contiguous(), counts.contiguous(), self.levelsup, stream=stream)
         pk = pack_keyframes(kps, desc, counts, valid, self.agent, frames, self.capacity, fv)
         multi = self.exchange is not None and self.exchange.world > 1
         if multi:
-            slots = self.store.exchange_into(self.exchange, pk)
-            mine = slots[self.agent * n:(self.agent + 1) * n]
+            new = self.store.exchange_into(self.exchange, pk)
+            mine = range(new.start + self.agent * n, new.start + (self.agent + 1) * n)
+            w = self.exchange.world
+            grp = self._slot_tensors.get(("group", w, n))
+            if grp is None:
+                grp = torch.arange(w * n, dtype=torch.int32, device=self.device) // n
+                self._slot_tensors[("group", w, n)] = grp
+            self.slot_group[new.start:new.stop].copy_(grp)
         else:
-            mine = self.store.insert(pk, self.agent)
-        pairs = self.store.candidate_pairs(mine, self.agent, self.k, other_agents_only=multi)
-        pr = self._device_pairs(pairs, kps.device)
+            new = self.store.insert(pk, self.agent)
+            mine = new
+            self.slot_group[new.start:new.stop].fill_(self.agent)
+        # the ring overwrote these slots: they leave the database, take the new BowVectors, and join it after
+        # this step's queries (MapFusion adds the query keyframe after detection, src/MapFusion.cc:149, :222)
+        self.db.erase(list(new))
+        P, o = self.store.layout.bytes, self.store.layout.offsets
+        rows = self.store.buf[new.start:new.stop]
+        self.db.set_bow_device(self._slots(new), rows[:, o["bow_words"]:], rows[:, o["bow_values"]:], rows[:, 16:],
+                               strides=(P // 4, P // 8, P // 4), stream=stream)
+        q = self._slots(mine)
+        ids = torch.arange(self._next_id, self._next_id + n, dtype=torch.int64, device=self.device)
+        self._next_id += n
+        zeros = self._slot_tensors.get(("zeros", n))
+        if zeros is None:
+            zeros = torch.zeros((n,), dtype=torch.float32, device=self.device)
+            self._slot_tensors[("zeros", n)] = zeros
+        cand, n_cand, _ = self.db.detect_device(0, q, ids, zeros, status=self.status, stream=stream)
+        if multi:
+            qg = self._slot_tensors.get(("qgroup", n))
+            if qg is None:
+                qg = torch.full((n,), self.agent, dtype=torch.int32, device=self.device)
+                self._slot_tensors[("qgroup", n)] = qg
+            pr = self.db.candidate_pairs_device(cand, n_cand, q, self.k, self.slot_group, qg, stream=stream)
+        else:
+            pr = self.db.candidate_pairs_device(cand, n_cand, q, self.k, stream=stream)
+        self.db.add(list(new))
         m12, nm = self.matcher.SearchByBoW_pairs_device(self.store.kf_store(), pr, self.max_fv_nodes, stream=stream)
         return pr, m12, nm, nm >= self.min_matches

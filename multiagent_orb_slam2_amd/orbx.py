@@ -186,8 +186,11 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_kfdb_create.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
     lib.orbx_kfdb_destroy.argtypes = [vp]
     lib.orbx_kfdb_info.argtypes = [vp] + [C.POINTER(i32)] * 4
+    lib.orbx_kfdb_set_strategy.argtypes = [vp, i32]
     lib.orbx_kfdb_set_bow.argtypes = [vp, i32, vp, vp, i32]
-    lib.orbx_kfdb_set_bow_device.argtypes = [vp, vp, i32, vp, vp, vp, i32, vp]
+    ll = C.c_longlong
+    lib.orbx_kfdb_set_bow_device.argtypes = [vp, vp, i32, vp, ll, vp, ll, vp, ll, vp]
+    lib.orbx_kfdb_candidate_pairs_device.argtypes = [vp, i32, vp, vp, i32, vp, vp, i32, vp, vp]
     lib.orbx_kfdb_set_covisibility.argtypes = [vp, vp, i32, vp]
     for name in ("orbx_kfdb_add", "orbx_kfdb_erase"):
         getattr(lib, name).argtypes = [vp, vp, i32]
@@ -711,6 +714,7 @@ class ORBVocabulary:
 
 
 KFDB_LOOP, KFDB_COVIS, KFDB_RELOC = 0, 1, 2
+KFDB_AUTO, KFDB_INVERTED, KFDB_PAIRWISE = 0, 1, 2   # how a query finds the keyframes sharing its words
 KFDB_COVIS_WIDTH = 10   # GetBestCovisibilityKeyFrames(10)
 
 
@@ -739,6 +743,11 @@ class KeyFrameDatabase:
         except Exception:
             pass
 
+    def set_strategy(self, strategy: int):
+        """KFDB_INVERTED (inverted file, as the reference), KFDB_PAIRWISE (intersect with every member) or
+        KFDB_AUTO; results are identical."""
+        _check(self._lib.orbx_kfdb_set_strategy(self._h, strategy))
+
     def n_members(self) -> int:
         n = C.c_int()
         _check(self._lib.orbx_kfdb_info(self._h, None, None, None, C.byref(n)))
@@ -751,12 +760,16 @@ class KeyFrameDatabase:
             raise ValueError("words and values differ in length")
         _check(self._lib.orbx_kfdb_set_bow(self._h, slot, _p(w), _p(v), len(w)))
 
-    def set_bow_device(self, slots, words, values, n_words, stream=None):
-        """BowVectors from orbx_vocab_transform_batch_device output (B, capacity) into device int32 slots."""
+    def set_bow_device(self, slots, words, values, n_words, strides=None, stream=None):
+        """BowVectors into device int32 slots: words/values/n_words device tensors, BowVector i at
+        words[i], values[i], n_words[i] (strides = element strides (word, value, n) if given, e.g. for a
+        packet ring; default: row strides of (B, capacity) vocabulary outputs)."""
         import torch
+        if strides is None:
+            strides = (words.shape[1], values.shape[1], 1)
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(words.device).cuda_stream)
-        _check(self._lib.orbx_kfdb_set_bow_device(self._h, _tp(slots), slots.numel(), _tp(words), _tp(values),
-                                                  _tp(n_words), words.shape[1], s))
+        _check(self._lib.orbx_kfdb_set_bow_device(self._h, _tp(slots), slots.numel(), _tp(words), strides[0],
+                                                  _tp(values), strides[1], _tp(n_words), strides[2], s))
 
     def set_covisibility(self, slot_lists: dict):
         """{slot: [best covisible slots, best first]} (at most 10 each, KeyFrame::GetBestCovisibilityKeyFrames)."""
@@ -836,6 +849,20 @@ class KeyFrameDatabase:
                                                  opt(excl_offsets), opt(excl_slots), _tp(out), out.shape[1], _tp(out_n),
                                                  _tp(status), s))
         return out, out_n, status
+
+    @staticmethod
+    def candidate_pairs_device(cand, n_cand, query_slots, k: int, slot_group=None, query_group=None, out=None,
+                               stream=None):
+        """MapFusion's candidate use (src/MapFusion.cc:136-144, :275): first k candidates of another map per
+        query as (query, candidate) SearchByBoW pairs, (query, -1) padded; (nq*k, 2) int32 device tensor."""
+        import torch
+        nq = query_slots.numel()
+        out = out if out is not None else torch.empty((nq * k, 2), dtype=torch.int32, device=cand.device)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(cand.device).cuda_stream)
+        opt = lambda t: None if t is None else _tp(t)
+        _check(load_library().orbx_kfdb_candidate_pairs_device(_tp(cand), cand.shape[1], _tp(n_cand), _tp(query_slots), nq,
+                                                               opt(slot_group), opt(query_group), k, _tp(out), s))
+        return out
 
     # the reference's method names (one query each)
     def DetectLoopCandidates(self, slot: int, query_id: int, minScore: float, connected=()):

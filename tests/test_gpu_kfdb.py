@@ -9,10 +9,11 @@ from kfdb_cases import COVIS, LOOP, RELOC, make_kfdb_case, setup_db
 pytestmark = pytest.mark.gpu
 
 
-def _run_both(case, batched=True):
+def _run_both(case, batched=True, strategy=0):
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
     g = pkg.KeyFrameDatabase(case["n_vocab"], case["n_slots"], max_words=2048)
+    g.set_strategy(strategy)
     o = O.Kfdb(case["n_vocab"], case["n_slots"])
     setup_db(case, g)
     setup_db(case, o)
@@ -46,22 +47,28 @@ def _run_both(case, batched=True):
     return n_results
 
 
+INVERTED, PAIRWISE = 1, 2
+
+
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
 @pytest.mark.parametrize("seed", range(8))
-def test_detect_sequences(gpu, seed):
+def test_detect_sequences(gpu, seed, strategy):
     case = make_kfdb_case(100 + seed, n_slots=150, n_queries=48, words_hi=400)
-    assert _run_both(case) > 0
+    assert _run_both(case, strategy=strategy) > 0
 
 
-def test_detect_one_by_one(gpu):
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
+def test_detect_one_by_one(gpu, strategy):
     case = make_kfdb_case(200, n_slots=100, n_queries=30)
-    assert _run_both(case, batched=False) > 0
+    assert _run_both(case, batched=False, strategy=strategy) > 0
 
 
-def test_detect_fresh_ids_large(gpu):
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
+def test_detect_fresh_ids_large(gpu, strategy):
     """KITTI-like keyframes (1000-1500 words of a 1M-word vocabulary), 600 slots, fresh query ids only."""
     case = make_kfdb_case(300, n_slots=600, n_vocab=1_000_000, n_places=30, words_lo=900, words_hi=1500,
                           n_queries=40, repeat_ids=False)
-    assert _run_both(case) > 0
+    assert _run_both(case, strategy=strategy) > 0
 
 
 def test_scores_bit_exact(gpu):
@@ -79,9 +86,11 @@ def test_scores_bit_exact(gpu):
     assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
 
 
-def test_edge_cases(gpu):
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
+def test_edge_cases(gpu, strategy):
     import multiagent_orb_slam2_amd as pkg
     g = pkg.KeyFrameDatabase(16, 4, max_words=8)
+    g.set_strategy(strategy)
     g.set_bow(0, [1, 5, 9], [0.2, 0.3, 0.5])
     g.set_bow(1, [1, 5, 10], [0.4, 0.4, 0.2])
     g.set_bow(2, [5, 9], [0.5, 0.5])

@@ -240,8 +240,10 @@ def test_two_agent_store_exchange_gloo():
 
 @pytest.mark.gpu
 def test_gpu_keyframe_fusion_store_vs_oracle(gpu):
-    """Extractor -> stereo valid flags -> vocabulary -> packets -> device store -> batched SearchByBoW,
-    every (query, candidate) pair checked against the oracle on the unpacked host keyframes."""
+    """Extractor -> stereo valid flags -> vocabulary -> packets -> device store -> KeyFrameDatabase
+    DetectLoopCandidates -> batched SearchByBoW: the candidates of every query checked against the oracle's
+    database fed the same BowVectors in the same order, every (query, candidate) pair against the oracle's
+    SearchByBoW on the unpacked host keyframes."""
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
     dev = torch.device("cuda", 0)
@@ -250,27 +252,43 @@ def test_gpu_keyframe_fusion_store_vs_oracle(gpu):
     ex = pkg.ORBextractor(1200, 1.2, 8, 20, 7)
     m = pkg.ORBmatcher(0.75, True)
     base = S.kitti_like_image(77)
-    imgs = np.stack([base] + [S.shifted_right_view(base, 3 + i, max_disp=12) for i in range(5)])
+    imgs = np.stack([base] + [S.shifted_right_view(base, 3 + i, max_disp=12) for i in range(8)])
     kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).to(dev))
     cap = kps.shape[1]
     valid = (torch.arange(cap, device=dev)[None, :] < cnt[:, None]).to(torch.uint8)
     valid[:, ::4] = 0                                   # a quarter without MapPoints
-    fus = MA.KeyframeFusion(m, v, cap, slots=6, device=dev, candidates=4, levelsup=2)
-    out = []
-    for step in range(2):
+    K = 2
+    fus = MA.KeyframeFusion(m, v, cap, slots=6, device=dev, candidates=K, levelsup=2)
+    odb = O.Kfdb(v.info()["n_words"], 6)
+    total = n_real = 0
+    qid = 1
+    for step in range(3):                               # 3 keyframes per step into a 6-slot ring: wraps once
         r = slice(3 * step, 3 * step + 3)
-        out.append(fus.step(kps[r], desc[r], cnt[r], valid[r], frames=[3 * step, 3 * step + 1, 3 * step + 2]))
-    torch.cuda.synchronize()
-    views = MA.unpack_keyframes(fus.store.buf, cap)
-    total = 0
-    for pr, m12, nm, passed in out:
+        pr, m12, nm, passed = fus.step(kps[r], desc[r], cnt[r], valid[r], frames=[3 * step + i for i in range(3)])
+        torch.cuda.synchronize()
+        views = MA.unpack_keyframes(fus.store.buf, cap)
+        new = list(range((3 * step) % 6, (3 * step) % 6 + 3))
+        odb.erase(new)
+        for k in new:
+            odb.set_bow(k, *views[k].bow)
+        expect = []
+        for k in new:
+            c = odb.detect(0, k, qid, 0.0)[:K].tolist()
+            qid += 1
+            expect += [[k, x] for x in c] + [[k, -1]] * (K - len(c))
+        odb.add(new)
         prh, m12h, nmh = pr.cpu().numpy(), m12.cpu().numpy(), nm.cpu().numpy()
-        assert len(prh) > 0
+        assert prh.tolist() == expect, step
         for p, (a, b) in enumerate(prh):
+            if b < 0:
+                assert nmh[p] == 0 and (m12h[p] == -1).all()
+                continue
             A, B = views[a], views[b]
             rn, rm = O.search_by_bow_kfkf(A.desc, A.kps["angle"], A.valid, A.featvec, B.desc, B.kps["angle"], B.valid,
                                           B.featvec, 0.75, True)
             assert nmh[p] == rn and np.array_equal(m12h[p, :A.count], rm), (p, a, b)
             total += rn
+            n_real += 1
         assert np.array_equal(passed.cpu().numpy(), nmh >= 20)
-    assert total > 100
+    assert fus.status.item() == 0
+    assert n_real >= 6 and total > 100
