@@ -29,6 +29,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Hardware queues per process (HIP's default is 4).  The bench drives 8 streams (front-end, keyframe path,
+# the extractor's blur side stream, and the library objects' own queues); with 4 queues, round-robin puts
+# the front-end and keyframe streams on one queue and serialises them.  Read by the HIP runtime at init.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ORBX_HW_QUEUES", "8")
 
 METRIC = "frames/sec ORB extract+match, KITTI 1242×375 @2000 kpts, 1/2/4/8 GPU"
 ROWS, COLS, NFEAT, NLEV, SCALE, INI, MINTH = 375, 1242, 2000, 8, 1.2, 20, 7
@@ -135,8 +139,12 @@ def main():
     kps = torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev)
     desc = torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev)
     cnt = torch.empty((2 * B,), dtype=torch.int32, device=dev)
-    stream = torch.cuda.Stream(dev)                    # one queue for extractor, matchers and RCCL
+    stream = torch.cuda.Stream(dev)                    # front-end queue: extractor + stereo matcher
     torch.cuda.set_stream(stream)
+    # keyframe queue: BoW, RCCL exchange, KeyFrameDatabase, SearchByBoW.  As in the reference, where MapFusion
+    # and LoopClosing run in their own threads beside Tracking, step k's keyframe work overlaps step k+1's
+    # extraction; it reads private copies of the keyframe rows taken on the front-end queue.
+    kf_stream = torch.cuda.Stream(dev)
     n_kf = max(1, B // KF_EVERY)
     kf_rows = torch.arange(0, KF_EVERY * n_kf, KF_EVERY, device=dev)
     voc = S.synthetic_vocabulary(2024, k=10, L=6)      # ORBvoc.txt's shape ("10 6 0 0"); the file is absent
@@ -168,19 +176,26 @@ def main():
             e1.record(stream)
             stereo_ms.append((e0, e1))
         # keyframe path: BoW -> packets -> all-gather (N>1) into the store -> batched SearchByBoW
-        if time_stereo:
-            e2 = torch.cuda.Event(enable_timing=True)
-            e2.record(stream)
         valid = (depth.index_select(0, kf_rows) > 0).to(torch.uint8)   # stereo keypoints get MapPoints
         frames = kf_rows.to(torch.int32) + frame_no[0]          # device-side frame ids (no host->device copy)
         frame_no[0] += B
-        _, _, nm, passed = fusion.step(kps.index_select(0, kf_rows), desc.index_select(0, kf_rows),
-                                       cnt.index_select(0, kf_rows), valid, frames, stream=stream)
-        gate.add_(passed.sum())
-        if time_stereo:
-            e3 = torch.cuda.Event(enable_timing=True)
-            e3.record(stream)
-            kf_ms.append((e2, e3))
+        kf_in = (kps.index_select(0, kf_rows), desc.index_select(0, kf_rows), cnt.index_select(0, kf_rows), valid,
+                 frames)
+        handoff = torch.cuda.Event()
+        handoff.record(stream)
+        kf_stream.wait_event(handoff)
+        for t in kf_in:
+            t.record_stream(kf_stream)
+        with torch.cuda.stream(kf_stream):
+            if time_stereo:
+                e2 = torch.cuda.Event(enable_timing=True)
+                e2.record(kf_stream)
+            _, _, nm, passed = fusion.step(*kf_in, stream=kf_stream)
+            gate.add_(passed.sum())
+            if time_stereo:
+                e3 = torch.cuda.Event(enable_timing=True)
+                e3.record(kf_stream)
+                kf_ms.append((e2, e3))
         return bi, bd
 
     for _ in range(STORE_STEPS):                       # fill the keyframe store ring (setup, untimed)

@@ -1081,6 +1081,11 @@ struct Extractor {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    // k_blur7 runs on a side stream, concurrently with k_quadtree (a latency-bound grid of one workgroup per
+    // (level, image)): fork after k_fast_cells (or after the pyramid, ORBX_BLUR_FORK=0), join before k_describe
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int blur_fork = 1;
 
     // geometry for the reserved size
     int rows = 0, cols = 0, max_batch = 0;
@@ -1125,8 +1130,12 @@ struct Extractor {
     int last_batch = 0;
     Src0 last_src0{nullptr, 0, 0};   // level 0 of the last device call = the caller's images
 
-    // timing: a pool of event sets recorded on the launch stream, resolved lazily (no host sync per call)
-    struct EventSet { hipEvent_t ev[ST_COUNT + 1]; bool pending; };
+    // timing: a pool of event sets recorded on the launch streams, resolved lazily (no host sync per call).
+    // Events: 0 start, 1 pyramid done, 2 FAST done, 3 quadtree done, 4 describe start (after the join),
+    // 5 describe done (all on the launch stream); 6/7 blur start/done on the side stream.
+    static constexpr int kEvents = 8;
+    static constexpr int kStageEv[ST_COUNT][2] = {{0, 1}, {1, 2}, {6, 7}, {2, 3}, {4, 5}};
+    struct EventSet { hipEvent_t ev[kEvents]; bool pending; };
     bool timing = false;
     std::vector<EventSet> tpool;
     size_t tnext = 0;
@@ -1134,10 +1143,11 @@ struct Extractor {
     int timed_calls = 0;
     int resolve(EventSet& es) {
         if (!es.pending) return ORBX_OK;
-        ORBX_HIP(hipEventSynchronize(es.ev[ST_COUNT]));
+        ORBX_HIP(hipEventSynchronize(es.ev[5]));
+        ORBX_HIP(hipEventSynchronize(es.ev[7]));
         for (int k = 0; k < ST_COUNT; ++k) {
             float ms = 0;
-            ORBX_HIP(hipEventElapsedTime(&ms, es.ev[k], es.ev[k + 1]));
+            ORBX_HIP(hipEventElapsedTime(&ms, es.ev[kStageEv[k][0]], es.ev[kStageEv[k][1]]));
             stage_ms[k] += ms;
         }
         es.pending = false;
@@ -1220,6 +1230,7 @@ int Extractor::configure(int r, int c, int batch) {
     if (r == rows && c == cols && batch <= max_batch) return ORBX_OK;
     ORBX_HIP(hipSetDevice(device));
     if (stream) ORBX_HIP(hipStreamSynchronize(stream));
+    if (side) ORBX_HIP(hipStreamSynchronize(side));
     const int keep_batch = std::max(batch, (r == rows && c == cols) ? max_batch : 0);
     free_buffers();
     ORBX_REQUIRE(r > 0 && c > 0 && batch > 0, ORBX_ERR_ARG, "configure: bad size %dx%d batch %d", r, c, batch);
@@ -1442,9 +1453,20 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         if (st) return st;
         es->pending = true;
     }
-    auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], s); };
     const Src0 s0{d_images, step, istride};
     e->last_src0 = s0;
+    auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], k >= 6 ? e->side : s); };
+    auto launch_blur = [&]() -> int {
+        ORBX_HIP(hipEventRecord(e->ev_fork, s));
+        ORBX_HIP(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+        mark(6);
+        const int nt = (int)e->tilev.size();
+        dim3 g(kXcds * xcd_chunk((nt + 3) / 4 * batch));
+        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, e->side, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles, nt, batch, s0);
+        mark(7);
+        ORBX_HIP(hipEventRecord(e->ev_join, e->side));
+        return ORBX_OK;
+    };
     mark(0);
     for (int l = 1; l < nl; ++l) {
         const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
@@ -1461,6 +1483,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         }
     }
     mark(1);
+    int st;
+    if (e->blur_fork == 0 && (st = launch_blur())) return st;
     const int ncells = (int)e->cellv.size();
     if (ncells > 0) {
         dim3 g(kXcds * xcd_chunk(ncells * batch));
@@ -1469,12 +1493,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
                            s0, e->cell_max_rows, e->cell_max_cols);
     }
     mark(2);
-    {
-        const int nt = (int)e->tilev.size();
-        dim3 g(kXcds * xcd_chunk((nt + 3) / 4 * batch));
-        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles, nt, batch, s0);
-    }
-    mark(3);
+    if (e->blur_fork != 0 && (st = launch_blur())) return st;
     {
         QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
         dim3 g(nl, batch);
@@ -1482,6 +1501,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
                            e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
                            e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err);
     }
+    mark(3);
+    ORBX_HIP(hipStreamWaitEvent(s, e->ev_join, 0));
     mark(4);
     {
         const int total_slots = e->out_stride;
@@ -1543,18 +1564,21 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     e->device = device;
     compute_tables(e);
     hipError_t he = hipSetDevice(device);
+    e->own_stream = true;
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
     if (he != hipSuccess) {
         set_error("stream create: %s", hipGetErrorString(he));
-        delete e;
+        orbx_extractor_destroy(e);
         return ORBX_ERR_HIP;
     }
-    e->own_stream = true;
     if (const char* ab = std::getenv("ORBX_FAST_ABLATE")) e->fast_stop_after = std::atoi(ab);
+    if (const char* bf = std::getenv("ORBX_BLUR_FORK")) e->blur_fork = std::atoi(bf);
     std::call_once(g_const_once, [&] { g_const_status = upload_constants(e); });
     if (g_const_status != ORBX_OK) {
-        (void)hipStreamDestroy(e->stream);
-        delete e;
+        orbx_extractor_destroy(e);
         return g_const_status;
     }
     *out = e;
@@ -1565,10 +1589,14 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     if (!e) return ORBX_OK;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->side) (void)hipStreamSynchronize(e->side);
     e->free_buffers();
     for (auto& es : e->tpool)
         for (auto& ev : es.ev) (void)hipEventDestroy(ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->side) (void)hipStreamDestroy(e->side);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     delete e;
     return ORBX_OK;
 }

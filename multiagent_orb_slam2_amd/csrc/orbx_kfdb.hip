@@ -617,6 +617,8 @@ __global__ __launch_bounds__(256) void k_kfdb_score_pairs(DbDev D, const int32_t
 
 using namespace orbx;
 
+constexpr int kKfdbStages = 4;
+
 struct orbx_kfdb {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -638,8 +640,9 @@ struct orbx_kfdb {
     size_t scratch_bytes = 0;
     std::vector<uint32_t> seq;     // host mirror of membership (add order)
     std::vector<int32_t> members;
-    uint32_t* h_stage = nullptr;   // 2 pinned staging buffers of seq + members (membership uploads never stall
-    hipEvent_t stage_done[2] = {nullptr, nullptr};   // on a pageable copy; each is reused two uploads later)
+    uint32_t* h_stage = nullptr;   // kKfdbStages pinned staging buffers of seq + members (membership uploads never
+    hipEvent_t stage_done[kKfdbStages] = {};   // stall on a pageable copy; each is reused kKfdbStages uploads later,
+                                               // so the host may run that many uploads ahead of the stream)
     int stage_next = 0;
     uint32_t next_seq = 0;
     bool dirty = true;             // inverted file stale (membership or a member's BowVector changed)
@@ -690,7 +693,7 @@ int upload_membership(orbx_kfdb* db, hipStream_t s) {
     if (!db->seq_dirty) return ORBX_OK;
     const int nm = (int)db->members.size();
     const int b = db->stage_next;
-    db->stage_next ^= 1;
+    db->stage_next = (b + 1) % kKfdbStages;
     uint32_t* stage = db->h_stage + (size_t)b * 2 * db->S;
     ORBX_HIP(hipEventSynchronize(db->stage_done[b]));       // the upload before last has left this buffer
     std::memcpy(stage, db->seq.data(), sizeof(uint32_t) * db->S);
@@ -800,8 +803,8 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
         alloc((void**)&db->d_w[k], 4 * S);
         alloc((void**)&db->d_s[k], 4 * S);
     }
-    if (e == hipSuccess) e = hipHostMalloc((void**)&db->h_stage, 16 * S, hipHostMallocDefault);
-    for (int b = 0; b < 2; ++b) {
+    if (e == hipSuccess) e = hipHostMalloc((void**)&db->h_stage, 8 * (size_t)kKfdbStages * S, hipHostMallocDefault);
+    for (int b = 0; b < kKfdbStages; ++b) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&db->stage_done[b], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventRecord(db->stage_done[b], db->stream);
     }
@@ -827,7 +830,7 @@ int orbx_kfdb_destroy(orbx_kfdb* db) {
         if (db->d_w[k]) (void)hipFree(db->d_w[k]);
         if (db->d_s[k]) (void)hipFree(db->d_s[k]);
     }
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < kKfdbStages; ++b)
         if (db->stage_done[b]) {
             (void)hipEventSynchronize(db->stage_done[b]);
             (void)hipEventDestroy(db->stage_done[b]);
