@@ -9,11 +9,15 @@ and the keyframe path: every 5th left frame becomes a keyframe (MapPoint-valid =
 Tracking::CreateNewKeyFrame makes stereo MapPoints), its DBoW2 FeatureVector is computed on the GPU
 (KeyFrame::ComputeBoW, synthetic k=10 L=6 vocabulary of ORBvoc's shape), the keyframe packets are
 all-gathered over RCCL into every rank's MapFusion store (src/MapFusion.cc:83-88 replaced by
-ncclAllGather; a local insert at N=1), each new keyframe queries the KeyFrameDatabase over the store
-(DetectLoopCandidates, src/MapFusion.cc:133) and is matched with SearchByBoW against its first 16
-candidates (other agents' at N>1 -- MapFusion.cc:136-144, :275; the agent's own earlier ones at N=1 --
-LoopClosing.cc:164, :288), so every rank does the same work at every N.  Inputs are resident in HBM before
-the timed region; weak scaling.
+ncclAllGather; a local insert at N=1), each exchanged keyframe in turn queries the KeyFrameDatabase over
+the store (DetectLoopCandidates, src/MapFusion.cc:133) and then joins it (:149 / :222) -- each rank answers
+its own keyframes' queries -- and is matched with SearchByBoW against its first 16 candidates (other
+agents' at N>1 -- MapFusion.cc:136-144, :275; the agent's own earlier ones at N=1 -- LoopClosing.cc:164,
+:288), so every rank does the same work at every N.  Inputs are resident in HBM before the timed region;
+weak scaling.  Rank r's frames are its contiguous chunk of one synthetic sequence, split as the reference's
+multi-agent driver splits a sequence (Examples/MultiAgent/generic_split_seq.cc:543-589).
+
+--config kitti (C2/C5: 1242x375, 2000 kpts, KITTI00-02.yaml) or euroc (C4: 752x480, 1200 kpts, EuRoC.yaml:88).
 
 Prints ONE JSON line on rank 0 (driver contract).  Run: python bench.py [--gpus N --steps K --warmup W]
 """
@@ -23,6 +27,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -35,12 +40,19 @@ sys.path.insert(0, ROOT)
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ORBX_HW_QUEUES", "8")
 
 METRIC = "frames/sec ORB extract+match, KITTI 1242×375 @2000 kpts, 1/2/4/8 GPU"
-ROWS, COLS, NFEAT, NLEV, SCALE, INI, MINTH = 375, 1242, 2000, 8, 1.2, 20, 7
-BF, BASELINE_B = 386.1448, 0.537165          # KITTI stereo (Examples/Stereo/KITTI00-02.yaml)
 HBM_PEAK_GBS = 8000.0                         # MI355X HBM3E peak (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12     # 256 CU x 4 SIMD-32 x 2.4 GHz lane-ops (MI355X_MICROARCH.md)
+NLEV, SCALE, INI, MINTH = 8, 1.2, 20, 7
 KF_EVERY = 5
 KF_CANDIDATES = 16
 STORE_STEPS = 3                               # keyframe store ring = 3 steps of every agent's keyframes
+# Camera.bf and Camera.fx of the reference's stereo settings (baseline b = bf / fx, Frame.cc mb)
+CONFIGS = {
+    "kitti": dict(rows=375, cols=1242, nfeatures=2000, bf=386.1448, fx=718.856, seq_frames=4541,
+                  source="Examples/Stereo/KITTI00-02.yaml (1242x375 synthetic, BASELINE C2/C5)"),
+    "euroc": dict(rows=480, cols=752, nfeatures=1200, bf=47.90639384423901, fx=435.2046959714599, seq_frames=3682,
+                  source="Examples/Stereo/EuRoC.yaml:18-19,25,88 (752x480, 1200 kpts, BASELINE C4)"),
+}
 
 
 def parse():
@@ -48,70 +60,171 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--batch", type=int, default=64, help="stereo frames per GPU per step")
-    ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic stereo pairs (tiled to batch)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--distinct", type=int, default=64, help="distinct synthetic stereo pairs per rank (tiled to batch)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage event timing")
     return ap.parse_args()
 
 
-def algorithmic_bytes(ex, mean_cand, mean_kps):
-    """Compulsory HBM bytes per image for each stage."""
-    sizes = ex.level_sizes(ROWS, COLS)
-    px = [h * w for h, w in sizes]
-    P = sum(px)
-    return {
-        "resize": sum(px[l - 1] + px[l] for l in range(1, len(px))),
-        "fast_cells": P + 5 * mean_cand,                 # read every level once, write candidates (xy + score)
-        "blur7": 2 * P,                                  # read + write every level
-        "quadtree": 2 * 5 * mean_cand + 5 * mean_kps,     # read slots, write compacted keys, write kept keys
-        "describe": mean_kps * (749 + 512 + 28 + 32 + 5),  # IC disc + 512 BRIEF samples + outputs
-    }
+def compulsory_bytes(cfg):
+    """SURVEY §8(d) algorithmic bytes: one extraction reads the image once and writes nfeatures x (28 B keypoint +
+    32 B descriptor); one stereo descriptor match reads both descriptor sets and writes (index, distance)."""
+    img = cfg["rows"] * cfg["cols"]
+    n = cfg["nfeatures"]
+    return {"extraction": img + n * (28 + 32), "stereo_match": 2 * n * 32 + n * 8}
 
 
-def cpu_baseline(lefts, rights, tables, voc, seconds):
-    """The same per-frame work on one host core with the oracle: extract L and R, ComputeStereoMatches
-    (band search + SAD refinement), and every KF_EVERY-th frame a keyframe: BoW transform,
-    DetectLoopCandidates over a keyframe ring of the GPU store's size, SearchByBoW against the first
-    KF_CANDIDATES candidates, then the keyframe joins the database."""
-    from oracle import oracle as O
-    vocab = O.Vocabulary(voc)
-    ring = STORE_STEPS * max(1, 64 // KF_EVERY)
-    db = O.Kfdb(voc["n_words"] if "n_words" in voc else int(np.sum(voc["is_leaf"])), ring)
-    kfs = [None] * ring
-    n_kf = 0
-    t0 = time.perf_counter()
-    n = 0
-    while True:
-        l, r = lefts[n % len(lefts)], rights[n % len(rights)]
-        a = O.extract(l, nfeatures=NFEAT, want_pyramid=True)
-        b = O.extract(r, nfeatures=NFEAT, want_pyramid=True)
-        _, depth = O.compute_stereo_matches(a, b, tables["scale"], tables["inv_scale"], ROWS, BF, BASELINE_B)
-        if n % KF_EVERY == 0:
-            bow = vocab.transform(a["desc"], 4)
+def cpu_threads():
+    n = os.environ.get("OMP_NUM_THREADS")
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return max(1, min(int(n) if n and n.isdigit() else avail, avail, 16))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+class CpuAgent:
+    """The per-frame work on host cores with the oracle (oracle/orb_oracle.cpp -O3, same FP pins): extract L and R,
+    ComputeStereoMatches (band search + SAD refinement), and every KF_EVERY-th frame a keyframe: BoW transform,
+    DetectLoopCandidates over a keyframe ring of the GPU store's size, SearchByBoW against the first KF_CANDIDATES
+    candidates, then the keyframe joins the database (MapFusion's query-then-add).  One per thread, as one
+    extractor per agent (Tracking.cc:119-125)."""
+
+    def __init__(self, O, cfg, tables, voc, n_kf_step):
+        self.O, self.cfg, self.tables = O, cfg, tables
+        self.vocab = O.Vocabulary(voc)
+        self.ring = STORE_STEPS * max(1, n_kf_step)
+        self.db = O.Kfdb(int(np.sum(voc["is_leaf"])), self.ring)
+        self.kfs = [None] * self.ring
+        self.n_kf = 0
+        self.n = 0
+
+    def frame(self, left, right):
+        O, c = self.O, self.cfg
+        a = O.extract(left, nfeatures=c["nfeatures"], want_pyramid=True)
+        b = O.extract(right, nfeatures=c["nfeatures"], want_pyramid=True)
+        _, depth = O.compute_stereo_matches(a, b, self.tables["scale"], self.tables["inv_scale"], c["rows"], c["bf"],
+                                            c["bf"] / c["fx"])
+        if self.n % KF_EVERY == 0:
+            bow = self.vocab.transform(a["desc"], 4)
             kf = (a["desc"], a["kps"]["angle"], (depth > 0).astype(np.uint8),
                   (bow["fv_nodes"], bow["fv_offsets"], bow["fv_indices"]))
-            slot = n_kf % ring
-            db.erase([slot])
-            db.set_bow(slot, bow["bow_words"], bow["bow_values"])
-            for c in db.detect(0, slot, n_kf + 1, 0.0)[:KF_CANDIDATES]:
-                O.search_by_bow_kfkf(*kf, *kfs[c], 0.75, True)
-            db.add([slot])
-            kfs[slot] = kf
-            n_kf += 1
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and n >= KF_EVERY:
+            slot = self.n_kf % self.ring
+            self.db.erase([slot])
+            self.db.set_bow(slot, bow["bow_words"], bow["bow_values"])
+            for cand in self.db.detect(0, slot, self.n_kf + 1, 0.0)[:KF_CANDIDATES]:
+                O.search_by_bow_kfkf(*kf, *self.kfs[cand], 0.75, True)
+            self.db.add([slot])
+            self.kfs[slot] = kf
+            self.n_kf += 1
+        self.n += 1
+
+
+def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds):
+    """1-thread latency per stereo frame (median / p95) and T-thread throughput with one agent per thread on
+    independent frames -- the reference drivers' timing pattern (generic_split_seq.cc:277-314, :369-379: per-frame
+    steady_clock around TrackStereo, median and mean reported)."""
+    from oracle import oracle as O
+    tables = O.tables(cfg["nfeatures"])
+    nd = len(lefts)
+    # (i) latency, one thread
+    ag = CpuAgent(O, cfg, tables, voc, n_kf_step)
+    lat = []
+    t_end = time.perf_counter() + 0.4 * seconds
+    while True:
+        t0 = time.perf_counter()
+        ag.frame(lefts[ag.n % nd], rights[ag.n % nd])
+        lat.append(time.perf_counter() - t0)
+        if time.perf_counter() >= t_end and ag.n >= 2 * KF_EVERY:
             break
-    return n / el, n, el
+    lat_ms = np.array(lat[1:] if len(lat) > 1 else lat) * 1e3
+    # (ii) throughput, T threads (ctypes releases the GIL inside the oracle's C++)
+    T = cpu_threads()
+    agents = [CpuAgent(O, cfg, tables, voc, n_kf_step) for _ in range(T)]
+    stop = threading.Event()
+
+    def run(i):
+        a = agents[i]
+        while not stop.is_set():
+            k = (a.n * T + i) % nd
+            a.frame(lefts[k], rights[k])
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(T)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    time.sleep(0.6 * seconds)
+    stop.set()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    done = sum(a.n for a in agents)
+    return {"value": round(done / el, 3), "unit": "frames/s", "cores": T, "kind": "port",
+            "cpu_model": cpu_model(),
+            "latency_ms_1thread": {"median": round(float(np.median(lat_ms)), 2),
+                                   "p95": round(float(np.percentile(lat_ms, 95)), 2), "frames": len(lat_ms)},
+            "throughput_1thread_fps": round(1e3 / float(np.mean(lat_ms)), 3),
+            "sample": f"{done} stereo frames on {T} threads in {el:.1f} s (+ {len(lat)} on 1 thread for latency) of the "
+                      f"same synthetic inputs and the same per-frame work (2 extractions + ComputeStereoMatches; every "
+                      f"{KF_EVERY}th frame BoW + DetectLoopCandidates + SearchByBoW vs the first {KF_CANDIDATES} "
+                      f"candidates), oracle/orb_oracle.cpp -O3 -ffp-contract=off, one agent per thread"}
+
+
+def host_api_rate(pkg, cfg, lefts, rights, n_frames, device):
+    """The per-call drop-in path: orbx_extract on host images (left, right) + orbx_compute_stereo_matches, host
+    keypoints / descriptors / depths out -- what an unchanged Frame constructor pays per stereo frame (PCIe
+    included, one frame at a time, as the reference calls it)."""
+    ex_l = pkg.ORBextractor(cfg["nfeatures"], SCALE, NLEV, INI, MINTH, device=device)
+    ex_r = pkg.ORBextractor(cfg["nfeatures"], SCALE, NLEV, INI, MINTH, device=device)
+    m = pkg.ORBmatcher(0.75, True, device=device)
+    b = cfg["bf"] / cfg["fx"]
+    lat = []
+    for i in range(n_frames + 3):
+        t0 = time.perf_counter()
+        kl, dl = ex_l(lefts[i % len(lefts)])
+        kr, dr = ex_r(rights[i % len(rights)])
+        m.ComputeStereoMatches(ex_l, ex_r, kl, dl, kr, dr, cfg["bf"], b)
+        if i >= 3:
+            lat.append(time.perf_counter() - t0)
+    lat_ms = np.array(lat) * 1e3
+    return {"frames_per_s": round(1e3 / float(np.mean(lat_ms)), 1), "latency_ms_median": round(float(np.median(lat_ms)), 3),
+            "latency_ms_p95": round(float(np.percentile(lat_ms, 95)), 3), "frames": len(lat),
+            "path": "orbx_extract(L) + orbx_extract(R) + orbx_compute_stereo_matches, host buffers, one frame per call"}
+
+
+def load_profile(name):
+    p = os.path.join(ROOT, "profiles", name)
+    if os.path.exists(p):
+        try:
+            return json.load(open(p))
+        except (OSError, ValueError):
+            return None
+    return None
 
 
 def main():
     args = parse()
+    cfg = dict(CONFIGS[args.config])
+    ROWS, COLS, NFEAT, BF = cfg["rows"], cfg["cols"], cfg["nfeatures"], cfg["bf"]
+    BASELINE_B = BF / cfg["fx"]
     import torch
     import torch.distributed as dist
 
     import multiagent_orb_slam2_amd as pkg
+    from multiagent_orb_slam2_amd import multiagent as MA
     from multiagent_orb_slam2_amd import synthetic as S
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,9 +238,13 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     B = args.batch
-    nd = min(args.distinct, B)
-    lefts = [S.kitti_like_image(1000 * rank + i) for i in range(nd)]
-    rights = [S.shifted_right_view(l, 1000 * rank + i) for i, l in enumerate(lefts)]
+    nd = max(1, min(args.distinct, B))
+    # this agent's contiguous chunk of one synthetic sequence (generic_split_seq.cc:543-589); frame f of the
+    # sequence is the synthetic stereo pair of seed f
+    chunk = MA.split_sequence(cfg["seq_frames"], world)[rank]
+    seeds = [chunk.start + (i % max(len(chunk), 1)) for i in range(nd)]
+    lefts = [S.kitti_like_image(s, rows=ROWS, cols=COLS) for s in seeds]
+    rights = [S.shifted_right_view(l, s) for s, l in zip(seeds, lefts)]
     host = np.stack([lefts[i % nd] for i in range(B)] + [rights[i % nd] for i in range(B)])
     imgs = torch.from_numpy(host).to(dev)               # resident in HBM before timing
 
@@ -149,12 +266,11 @@ def main():
     kf_rows = torch.arange(0, KF_EVERY * n_kf, KF_EVERY, device=dev)
     voc = S.synthetic_vocabulary(2024, k=10, L=6)      # ORBvoc.txt's shape ("10 6 0 0"); the file is absent
     vocab = pkg.ORBVocabulary.from_arrays(voc, device=dev.index)
-    del voc
-    from multiagent_orb_slam2_amd import multiagent as MA
+    exchange = MA.KeyframeExchange(timed=not args.no_timing) if world > 1 else None
     fusion = MA.KeyframeFusion(pkg.ORBmatcher(0.75, True, device=dev.index), vocab, cap,
-                               slots=STORE_STEPS * world * n_kf, device=dev, agent=rank,
-                               exchange=MA.KeyframeExchange() if world > 1 else None, candidates=KF_CANDIDATES)
-    frame_no = [0]
+                               slots=STORE_STEPS * world * n_kf, device=dev, agent=rank, exchange=exchange,
+                               candidates=KF_CANDIDATES)
+    frame_no = [chunk.start]
     gate = torch.zeros((), dtype=torch.int64, device=dev)
 
     stereo_ms = []
@@ -206,6 +322,8 @@ def main():
     torch.cuda.synchronize()
     if not args.no_timing:
         ex.enable_timing(True)
+    if exchange is not None:
+        exchange.reset_stats()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -231,14 +349,17 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "host_enqueue_ms_per_step": round(1000 * host_s / args.steps, 3),
-        "config": {"workload": "C2+C3 stereo frame: ORBextractor x2 (1242x375, 8 levels, 2000 kpts) + stereo "
-                               "L<->R 256-bit Hamming band match + SAD sub-pixel refinement; every 5th frame a keyframe: DBoW2 transform (k=10, "
-                               "L=6) + " + ("RCCL all-gather of KF packets + " if world > 1 else "") +
-                               "KeyFrameDatabase DetectLoopCandidates over the KF store + "
+        "config": {"workload": f"{args.config}: stereo frame = ORBextractor x2 ({COLS}x{ROWS}, 8 levels, {NFEAT} kpts) + "
+                               "stereo L<->R 256-bit Hamming band match + SAD sub-pixel refinement; every 5th frame a "
+                               "keyframe: DBoW2 transform (k=10, L=6) + " + ("RCCL all-gather of KF packets + " if world > 1 else "") +
+                               "KeyFrameDatabase DetectLoopCandidates (query, then add) over the KF store + "
                                f"SearchByBoW vs the first {KF_CANDIDATES} candidates",
+                   "settings": cfg["source"],
                    "keyframes_per_gpu_per_step": n_kf, "bow_pairs_per_gpu_per_step": n_kf * KF_CANDIDATES,
                    "global_batch": B * world, "frames_per_gpu_per_step": B, "image": [ROWS, COLS],
-                   "nfeatures": NFEAT, "nlevels": NLEV, "parallelism": f"agent-per-gpu x{world}"},
+                   "nfeatures": NFEAT, "nlevels": NLEV, "distinct_stereo_pairs_per_gpu": nd,
+                   "sequence_chunk": [chunk.start, chunk.stop],
+                   "parallelism": f"agent-per-gpu x{world}"},
     }
 
     if not args.no_timing:
@@ -248,47 +369,49 @@ def main():
         per_call["stereo_match"] = float(np.mean(sms)) if sms else 0.0
         kms = [a.elapsed_time(b) for a, b in kf_ms]
         per_call["keyframe_bow_fusion"] = float(np.mean(kms)) if kms else 0.0
-        counts = cnt.cpu().numpy()
-        mean_kps = float(counts.mean())
-        mean_cand = float(mean_kps * 4)   # replaced below by the measured candidate count if available
-        try:
-            from oracle import oracle as O  # candidate count of the synthetic inputs (geometry only)
-            mean_cand = float(np.mean([sum(len(c) for c in O.level_candidates(lefts[i])) for i in range(min(2, nd))]))
-        except Exception:
-            pass
-        alg = algorithmic_bytes(ex, mean_cand, mean_kps)
-        alg["stereo_match"] = 2 * cap * 0 + 2 * mean_kps * 60 + mean_kps * 8
-        dom = max((k for k in per_call if k in alg), key=per_call.get)
-        n_units = 2 * B if dom != "stereo_match" else B
-        bytes_launch = alg[dom] * n_units
-        achieved = bytes_launch / (per_call[dom] * 1e-3) / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                d = json.load(open(pmc))
-                if d.get("kernel_stage") == dom and d.get("batch_images") == n_units:
-                    traffic = d.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": dom,
-                           "kernel_ms_per_launch": round(per_call[dom], 4), "algorithmic_bytes_per_launch": bytes_launch}
         out["stage_ms_per_step"] = {k: round(v, 4) for k, v in per_call.items()}
+        # roofline of the dominant extractor kernel (each stage below is one kernel launch over the whole batch)
+        kernel_of = {"fast_cells": "k_fast_cells", "blur7": "k_blur7", "describe": "k_describe", "quadtree": "k_quadtree"}
+        dom = max(kernel_of, key=lambda k: per_call.get(k, 0.0))
+        units = 2 * B                                    # extractions per launch
+        cb = compulsory_bytes(cfg)
+        bytes_launch = cb["extraction"] * units
+        t_ms = per_call[dom]
+        achieved = bytes_launch / (t_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = load_profile("pmc_traffic.json")
+        if pmc and pmc.get("kernel") == kernel_of[dom] and pmc.get("batch_images") == units \
+                and pmc.get("config", "kitti") == args.config:
+            traffic = pmc.get("hbm_bytes_per_launch")
+        out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": kernel_of[dom],
+                           "kernel_ms_per_launch": round(t_ms, 4), "algorithmic_bytes_per_launch": bytes_launch,
+                           "algorithmic_bytes_per_unit": cb["extraction"], "units_per_launch": units,
+                           "unit_of_work": "one extraction (SURVEY §8d: image in + nfeatures x 60 B out)"}
+        sq = load_profile("sq_summary.json")
+        if sq and sq.get("config", "kitti") == args.config and sq.get("batch_images") == units:
+            k = sq["kernels"].get(kernel_of[dom])
+            if k:
+                ops = k["valu_lane_ops"]
+                out["roofline_valu"] = {"bound": "valu", "achieved": round(ops / (t_ms * 1e-3) / 1e12, 3),
+                                        "peak": round(VALU_PEAK_TOPS, 2), "unit": "Tlane-op/s",
+                                        "frac": round(ops / (t_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
+                                        "kernel": kernel_of[dom], "valu_lane_ops_per_launch": ops,
+                                        "source": "SQ_INSTS_VALU x 64 per launch from profiles/sq_summary.json "
+                                                  f"({sq.get('tag')}), time measured live"}
+    if exchange is not None:
+        xs = exchange.stats()
+        if xs:
+            out["exchange"] = dict(xs, collective="all_gather_into_tensor (RCCL over xGMI)",
+                                   packet_bytes=fusion.store.layout.bytes, keyframes_per_rank=n_kf)
 
+    if rank == 0 and world == 1 and args.host_api_frames > 0:
+        out["host_api"] = host_api_rate(pkg, cfg, lefts, rights, args.host_api_frames, dev.index)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        from oracle import oracle as O
-        fps, n, secs = cpu_baseline(lefts, rights, O.tables(NFEAT), S.synthetic_vocabulary(2024, k=10, L=6),
-                                    args.cpu_seconds)
-        out["cpu_baseline"] = {"value": round(fps, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": f"{n} stereo frames of the same synthetic inputs and the same per-frame work "
-                                         f"(2 extractions + ComputeStereoMatches; every {KF_EVERY}th frame BoW + "
-                                         f"DetectLoopCandidates + SearchByBoW vs the first {KF_CANDIDATES} candidates), "
-                                         f"oracle/orb_oracle.cpp -O2, "
-                                         f"1 thread, {secs:.1f} s"}
+        out["cpu_baseline"] = cpu_baseline(lefts[:16], rights[:16], cfg, S.synthetic_vocabulary(2024, k=10, L=6), n_kf,
+                                           args.cpu_seconds)
     out["fusion_gate_passed_per_step"] = round(int(gate.item()) / (args.steps + args.warmup + STORE_STEPS), 2)
-    if int(fusion.status.item()) & 2:
-        raise RuntimeError("KeyFrameDatabase query exceeded its candidate capacity")
+    fusion.check()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -426,12 +426,25 @@ int orbx_kfdb_detect(orbx_kfdb* db, int kind, const int32_t* query_slots, const 
 /* Device form (device pointers, no synchronisation).  Outputs: d_out[q*out_stride ...], d_out_n[q];
  * *d_status |= 2 when a query exceeds out_stride or 2048 retained candidates, |= 1 when the queries of the
  * batch interact through the scratch fields (a query id equal to one already recorded in a slot another
- * query of the batch updates, or repeated ids): then the results are not the sequential ones and the
- * batch must be re-run one query at a time on restored state (orbx_kfdb_detect does this itself).
+ * query of the batch updates, or repeated ids): then the results are not the sequential ones, the scratch
+ * fields hold the batched (not the sequential) updates, and the caller must treat the batch as failed (a
+ * device caller cannot restore them; orbx_kfdb_detect snapshots and re-runs one query at a time itself).
  * Distinct, fresh query ids (monotonic mnId, as in the reference) never interact. */
 int orbx_kfdb_detect_device(orbx_kfdb* db, int kind, const int32_t* d_query_slots, const uint64_t* d_query_ids,
                             const float* d_min_scores, int nq, const int32_t* d_excl_offsets, const int32_t* d_excl_slots,
                             int32_t* d_out, int out_stride, int32_t* d_out_n, int32_t* d_status, void* stream);
+/* MapFusion's query-then-add order (src/MapFusion.cc:133 DetectFusionCandidates, then the keyframe is added to the
+ * database, :149 / :222) for a whole batch in one call: the caller first adds the query slots with orbx_kfdb_add in
+ * query order; query q then sees only the members added before its own slot (its own slot and every later query
+ * slot are invisible to it), so the results equal detect(q0); add(q0); detect(q1); add(q1); ...  A query slot that
+ * is not a member sees every member.  Otherwise as orbx_kfdb_detect / orbx_kfdb_detect_device. */
+int orbx_kfdb_detect_sequential(orbx_kfdb* db, int kind, const int32_t* query_slots, const uint64_t* query_ids,
+                                const float* min_scores, int nq, const int32_t* excl_offsets, const int32_t* excl_slots,
+                                int32_t* out_offsets, int32_t* out, int out_cap);
+int orbx_kfdb_detect_sequential_device(orbx_kfdb* db, int kind, const int32_t* d_query_slots, const uint64_t* d_query_ids,
+                                       const float* d_min_scores, int nq, const int32_t* d_excl_offsets,
+                                       const int32_t* d_excl_slots, int32_t* d_out, int out_stride, int32_t* d_out_n,
+                                       int32_t* d_status, void* stream);
 /* MapFusion's use of the candidates (src/MapFusion.cc:136-144, :275): for query q, the first k of its
  * candidates d_cand[q*cand_stride ..+ d_n_cand[q]) whose map differs from the query's
  * (d_slot_group[cand] != d_query_group[q]; both NULL = keep all, LoopClosing's own-map case) become

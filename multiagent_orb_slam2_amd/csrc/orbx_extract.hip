@@ -102,7 +102,9 @@ struct ResizeTab {       // per level >= 1, device arrays
     int* y0; int* y1; int* b0; int* b1;   // [h]
 };
 
-__constant__ __attribute__((aligned(16))) signed char c_pattern[ORBX_PATTERN_TESTS * 4];
+// Initialised in its declaration: the table is part of the code object, so every device the module is loaded on
+// holds it (an uninitialised __constant__ filled by hipMemcpyToSymbol is written on the current device only).
+__constant__ __attribute__((aligned(16))) signed char c_pattern[ORBX_PATTERN_TESTS * 4] = ORBX_PATTERN_INIT;
 // umax for HALF_PATCH_SIZE = 15 (ORBextractor ctor :454-469); the host recomputes it and checks equality
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
@@ -1516,12 +1518,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     return ORBX_OK;
 }
 
-static std::once_flag g_const_once;
-static int g_const_status = ORBX_OK;
-
-static int upload_constants(const Extractor* e) {
-    // pattern is a fixed table; umax is the same for every extractor (depends only on HALF_PATCH_SIZE)
-    ORBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), ORBX_PATTERN, sizeof(ORBX_PATTERN)));
+static int check_constants(const Extractor* e) {
+    // umax is the same for every extractor (depends only on HALF_PATCH_SIZE); the kernels use kUmax
     for (int v = 0; v < 16; ++v)
         ORBX_REQUIRE(e->umax[v] == kUmax[v], ORBX_ERR_UNSUPPORTED, "umax table mismatch at %d", v);
     return ORBX_OK;
@@ -1576,10 +1574,9 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     }
     if (const char* ab = std::getenv("ORBX_FAST_ABLATE")) e->fast_stop_after = std::atoi(ab);
     if (const char* bf = std::getenv("ORBX_BLUR_FORK")) e->blur_fork = std::atoi(bf);
-    std::call_once(g_const_once, [&] { g_const_status = upload_constants(e); });
-    if (g_const_status != ORBX_OK) {
+    if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
-        return g_const_status;
+        return st;
     }
     *out = e;
     return ORBX_OK;

@@ -244,7 +244,17 @@ struct QueryIn {
     const float* min_score;           // [nq] (LOOP, COVIS)
     const int32_t* excl_off;          // [nq + 1] or NULL
     const int32_t* excl;
+    int seq_bounded;                  // query q sees only the members added before its own slot (MapFusion's
+                                      // query-then-add order, src/MapFusion.cc:133, :149 / :222)
 };
+
+// Membership of slot k for query q: in the database and, for a sequentially bounded batch, added before the
+// query's own slot (a query slot that is not a member sees every member).
+__device__ __forceinline__ bool kf_visible(const DbDev& D, const QueryIn& Q, int q, int k) {
+    const uint32_t sk = D.seq[k];
+    if (sk == kNoSeq) return false;
+    return !Q.seq_bounded || sk < D.seq[Q.slot[q]];
+}
 
 __global__ __launch_bounds__(256) void k_kfdb_mark_excl(QueryIn Q, QScratch X, int S) {
     const int q = blockIdx.x;
@@ -263,9 +273,11 @@ __global__ __launch_bounds__(256) void k_kfdb_share(DbDev D, QueryIn Q, QScratch
     const uint32_t w = D.bw[(size_t)qs * D.maxw + p];
     if (w >= (uint32_t)D.n_vocab) return;
     const size_t row = (size_t)q * D.S;
+    const uint32_t bound = Q.seq_bounded ? D.seq[qs] : kNoSeq;
     for (int e = D.if_off[w]; e < D.if_off[w + 1]; ++e) {
         const int k = D.if_slot[e];
         if (kind == KIND_COVIS && excl_at(X, row + k)) continue;   // :220 ignored keyframes are skipped
+        if (D.seq[k] >= bound) continue;                           // added after the query (sequential batch)
         atomicAdd(&X.cnt[row + k], 1);
         atomicMin(&X.first[row + k], p);
     }
@@ -291,7 +303,7 @@ __global__ __launch_bounds__(512) void k_kfdb_pairwise(DbDev D, QueryIn Q, QScra
     for (int k = blockIdx.x * waves + (int)(threadIdx.x / kWave); k < D.S; k += gridDim.x * waves) {
         int c = 0, first = 0x7f7f7f7f;
         double score = 0.0;
-        if (D.seq[k] != kNoSeq && !(kind == KIND_COVIS && excl_at(X, row + k))) {
+        if (kf_visible(D, Q, q, k) && !(kind == KIND_COVIS && excl_at(X, row + k))) {
             const uint32_t* cw = D.bw + (size_t)k * D.maxw;
             const double* cv = D.bv + (size_t)k * D.maxw;
             const int nc = D.bn[k];
@@ -638,6 +650,9 @@ struct orbx_kfdb {
     float* d_s[3] = {nullptr, nullptr, nullptr};
     void* scratch = nullptr;       // per-query rows + host-form staging
     size_t scratch_bytes = 0;
+    hipEvent_t scratch_used = nullptr;   // recorded on the stream of the last detect that used 'scratch'
+    void* score_stage = nullptr;   // orbx_kfdb_score's own staging (never shared with a detect in flight elsewhere)
+    size_t score_stage_bytes = 0;
     std::vector<uint32_t> seq;     // host mirror of membership (add order)
     std::vector<int32_t> members;
     uint32_t* h_stage = nullptr;   // kKfdbStages pinned staging buffers of seq + members (membership uploads never
@@ -659,6 +674,8 @@ DbDev dev_view(const orbx_kfdb* db) {
 int grow_scratch(orbx_kfdb* db, size_t bytes) {
     if (bytes <= db->scratch_bytes) return ORBX_OK;
     if (db->scratch) {
+        // the last detect may have run on a caller's stream: wait for it before the buffer goes away
+        ORBX_HIP(hipEventSynchronize(db->scratch_used));
         ORBX_HIP(hipStreamSynchronize(db->stream));
         ORBX_HIP(hipFree(db->scratch));
         db->scratch = nullptr;
@@ -757,6 +774,7 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
     hipLaunchKernelGGL(k_kfdb_accum, dim3(nq), dim3(256), 0, s, D, Q, X, St, kind, d_out, out_stride, d_out_n, d_status);
     hipLaunchKernelGGL(k_kfdb_state, dim3((db->S + 255) / 256), dim3(256), 0, s, D, Q, X, St, kind, nq, d_status);
     ORBX_HIP(hipGetLastError());
+    ORBX_HIP(hipEventRecord(db->scratch_used, s));
     return ORBX_OK;
 }
 
@@ -803,6 +821,8 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
         alloc((void**)&db->d_w[k], 4 * S);
         alloc((void**)&db->d_s[k], 4 * S);
     }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&db->scratch_used, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(db->scratch_used, db->stream);
     if (e == hipSuccess) e = hipHostMalloc((void**)&db->h_stage, 8 * (size_t)kKfdbStages * S, hipHostMallocDefault);
     for (int b = 0; b < kKfdbStages; ++b) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&db->stage_done[b], hipEventDisableTiming);
@@ -821,8 +841,9 @@ int orbx_kfdb_destroy(orbx_kfdb* db) {
     if (!db) return ORBX_OK;
     (void)hipSetDevice(db->device);
     if (db->stream) (void)hipStreamSynchronize(db->stream);
+    if (db->scratch_used) (void)hipEventSynchronize(db->scratch_used);   // a detect on a caller's stream
     void* bufs[] = {db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_cur, db->d_if_slot,
-                    db->d_scan, db->d_members, db->scratch};
+                    db->d_scan, db->d_members, db->scratch, db->score_stage};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (int k = 0; k < 3; ++k) {
@@ -835,6 +856,7 @@ int orbx_kfdb_destroy(orbx_kfdb* db) {
             (void)hipEventSynchronize(db->stage_done[b]);
             (void)hipEventDestroy(db->stage_done[b]);
         }
+    if (db->scratch_used) (void)hipEventDestroy(db->scratch_used);
     if (db->h_stage) (void)hipHostFree(db->h_stage);
     if (db->stream) (void)hipStreamDestroy(db->stream);
     delete db;
@@ -988,10 +1010,17 @@ int orbx_kfdb_score(orbx_kfdb* db, const int32_t* pairs, int n, double* scores) 
     ORBX_REQUIRE(db && n >= 0 && (n == 0 || (pairs && scores)), ORBX_ERR_ARG, "bad argument");
     if (n == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(db->device));
-    const size_t qb = qscratch_layout(0, db->S, nullptr, nullptr);
-    int st = grow_scratch(db, qb + align_up(8 * (size_t)n) + align_up(8 * (size_t)n));
-    if (st) return st;
-    int32_t* d_pairs = (int32_t*)((unsigned char*)db->scratch + qb);
+    const size_t need = align_up(8 * (size_t)n) + align_up(8 * (size_t)n);
+    if (need > db->score_stage_bytes) {          // db->stream is the only user of this buffer
+        ORBX_HIP(hipStreamSynchronize(db->stream));
+        if (db->score_stage) ORBX_HIP(hipFree(db->score_stage));
+        db->score_stage = nullptr;
+        db->score_stage_bytes = 0;
+        ORBX_HIP(hipMalloc(&db->score_stage, need));
+        db->score_stage_bytes = need;
+    }
+    int st;
+    int32_t* d_pairs = (int32_t*)db->score_stage;
     double* d_out = (double*)((unsigned char*)d_pairs + align_up(8 * (size_t)n));
     ORBX_HIP(hipMemcpyAsync(d_pairs, pairs, 8 * (size_t)n, hipMemcpyHostToDevice, db->stream));
     st = orbx_kfdb_score_device(db, d_pairs, n, d_out, db->stream);
@@ -1001,9 +1030,13 @@ int orbx_kfdb_score(orbx_kfdb* db, const int32_t* pairs, int n, double* scores) 
     return ORBX_OK;
 }
 
-int orbx_kfdb_detect_device(orbx_kfdb* db, int kind, const int32_t* d_query_slots, const uint64_t* d_query_ids,
-                            const float* d_min_scores, int nq, const int32_t* d_excl_offsets, const int32_t* d_excl_slots,
-                            int32_t* d_out, int out_stride, int32_t* d_out_n, int32_t* d_status, void* stream) {
+}  // extern "C"
+
+namespace {
+
+int detect_device_impl(orbx_kfdb* db, int kind, const int32_t* d_query_slots, const uint64_t* d_query_ids,
+                       const float* d_min_scores, int nq, const int32_t* d_excl_offsets, const int32_t* d_excl_slots,
+                       int32_t* d_out, int out_stride, int32_t* d_out_n, int32_t* d_status, void* stream, int seq_bounded) {
     ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && nq >= 0 && out_stride >= 0, ORBX_ERR_ARG, "bad argument");
     ORBX_REQUIRE(nq == 0 || (d_query_slots && d_query_ids && d_out && d_out_n && d_status), ORBX_ERR_ARG, "null buffers");
     ORBX_REQUIRE(kind == ORBX_KFDB_RELOC || nq == 0 || d_min_scores, ORBX_ERR_ARG, "min scores required for this query kind");
@@ -1012,14 +1045,37 @@ int orbx_kfdb_detect_device(orbx_kfdb* db, int kind, const int32_t* d_query_slot
     const size_t qb = qscratch_layout(nq, db->S, nullptr, nullptr);
     int st = grow_scratch(db, qb);
     if (st) return st;
-    QueryIn Q{d_query_slots, (const unsigned long long*)d_query_ids, d_min_scores, d_excl_offsets, d_excl_slots};
+    QueryIn Q{d_query_slots, (const unsigned long long*)d_query_ids, d_min_scores, d_excl_offsets, d_excl_slots, seq_bounded};
     return detect_batch(db, kind, Q, nq, (unsigned char*)db->scratch, d_out, out_stride, d_out_n, d_status,
                         (hipStream_t)stream);
 }
 
-int orbx_kfdb_detect(orbx_kfdb* db, int kind, const int32_t* query_slots, const uint64_t* query_ids, const float* min_scores,
+}  // namespace
+
+extern "C" {
+
+int orbx_kfdb_detect_device(orbx_kfdb* db, int kind, const int32_t* d_query_slots, const uint64_t* d_query_ids,
+                            const float* d_min_scores, int nq, const int32_t* d_excl_offsets, const int32_t* d_excl_slots,
+                            int32_t* d_out, int out_stride, int32_t* d_out_n, int32_t* d_status, void* stream) {
+    return detect_device_impl(db, kind, d_query_slots, d_query_ids, d_min_scores, nq, d_excl_offsets, d_excl_slots, d_out,
+                              out_stride, d_out_n, d_status, stream, 0);
+}
+
+int orbx_kfdb_detect_sequential_device(orbx_kfdb* db, int kind, const int32_t* d_query_slots, const uint64_t* d_query_ids,
+                                       const float* d_min_scores, int nq, const int32_t* d_excl_offsets,
+                                       const int32_t* d_excl_slots, int32_t* d_out, int out_stride, int32_t* d_out_n,
+                                       int32_t* d_status, void* stream) {
+    return detect_device_impl(db, kind, d_query_slots, d_query_ids, d_min_scores, nq, d_excl_offsets, d_excl_slots, d_out,
+                              out_stride, d_out_n, d_status, stream, 1);
+}
+
+}  // extern "C"
+
+namespace {
+
+int detect_host_impl(orbx_kfdb* db, int kind, const int32_t* query_slots, const uint64_t* query_ids, const float* min_scores,
                      int nq, const int32_t* excl_offsets, const int32_t* excl_slots, int32_t* out_offsets, int32_t* out,
-                     int out_cap) {
+                     int out_cap, int seq_bounded) {
     ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && nq >= 0 && out_cap >= 0, ORBX_ERR_ARG, "bad argument");
     ORBX_REQUIRE(nq == 0 || (query_slots && query_ids && out_offsets), ORBX_ERR_ARG, "null buffers");
     ORBX_REQUIRE(kind == ORBX_KFDB_RELOC || nq == 0 || min_scores, ORBX_ERR_ARG, "min scores required for this query kind");
@@ -1061,7 +1117,7 @@ int orbx_kfdb_detect(orbx_kfdb* db, int kind, const int32_t* query_slots, const 
     int32_t* d_status = (int32_t*)(b + o_stat);
     ORBX_HIP(hipMemsetAsync(d_status, 0, 4, s));
     QueryIn Q{(const int32_t*)(b + o_slot), (const unsigned long long*)(b + o_id), min_scores ? (const float*)(b + o_min) : nullptr,
-              excl_offsets ? (const int32_t*)(b + o_eoff) : nullptr, (const int32_t*)(b + o_excl)};
+              excl_offsets ? (const int32_t*)(b + o_eoff) : nullptr, (const int32_t*)(b + o_excl), seq_bounded};
     st = detect_batch(db, kind, Q, nq, b, (int32_t*)(b + o_out), S, (int32_t*)(b + o_outn), d_status, s);
     if (st) return st;
     int32_t status = 0;
@@ -1075,7 +1131,7 @@ int orbx_kfdb_detect(orbx_kfdb* db, int kind, const int32_t* query_slots, const 
         ORBX_HIP(hipMemsetAsync(d_status, 0, 4, s));
         for (int q = 0; q < nq; ++q) {
             QueryIn Q1{Q.slot + q, Q.id + q, Q.min_score ? Q.min_score + q : nullptr, Q.excl_off ? Q.excl_off + q : nullptr,
-                       Q.excl};
+                       Q.excl, seq_bounded};
             st = detect_batch(db, kind, Q1, 1, b, (int32_t*)(b + o_out) + (size_t)q * S, S, (int32_t*)(b + o_outn) + q, d_status,
                               s);
             if (st) return st;
@@ -1102,6 +1158,24 @@ int orbx_kfdb_detect(orbx_kfdb* db, int kind, const int32_t* query_slots, const 
                                             hipMemcpyDeviceToHost, s));
     ORBX_HIP(hipStreamSynchronize(s));
     return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orbx_kfdb_detect(orbx_kfdb* db, int kind, const int32_t* query_slots, const uint64_t* query_ids, const float* min_scores,
+                     int nq, const int32_t* excl_offsets, const int32_t* excl_slots, int32_t* out_offsets, int32_t* out,
+                     int out_cap) {
+    return detect_host_impl(db, kind, query_slots, query_ids, min_scores, nq, excl_offsets, excl_slots, out_offsets, out,
+                            out_cap, 0);
+}
+
+int orbx_kfdb_detect_sequential(orbx_kfdb* db, int kind, const int32_t* query_slots, const uint64_t* query_ids,
+                                const float* min_scores, int nq, const int32_t* excl_offsets, const int32_t* excl_slots,
+                                int32_t* out_offsets, int32_t* out, int out_cap) {
+    return detect_host_impl(db, kind, query_slots, query_ids, min_scores, nq, excl_offsets, excl_slots, out_offsets, out,
+                            out_cap, 1);
 }
 
 }  // extern "C"

@@ -150,9 +150,11 @@ def unpack_keyframes(packets, capacity: int) -> list[KeyframeView]:
 class KeyframeExchange:
     """All-gather of keyframe packets: the MapFusion ingress (src/MapFusion.cc:83-88) as one collective.
 
-    Works with the ``nccl`` (RCCL over xGMI) and ``gloo`` backends."""
+    Works with the ``nccl`` (RCCL over xGMI) and ``gloo`` backends.  With timed=True (GPU tensors) every call is
+    bracketed by HIP events on the current stream, so stats() reports the time from the stream reaching the
+    collective to its completion, per call, and the rate at which each rank receives the other ranks' bytes."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, timed: bool = False):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -160,6 +162,8 @@ class KeyframeExchange:
         self.rank = dist.get_rank(group)
         self.bytes_moved = 0
         self.calls = 0
+        self.timed = timed
+        self._events = []
 
     def exchange(self, packets, out=None):
         """packets: (n, P) uint8 on this rank (same n and P on every rank) -> (world*n, P), rank-major
@@ -168,14 +172,37 @@ class KeyframeExchange:
         n, P = packets.shape
         if out is None:
             out = torch.empty((self.world * n, P), dtype=torch.uint8, device=packets.device)
+        ev = None
+        if self.timed and packets.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         if hasattr(self.dist, "all_gather_into_tensor") and packets.is_cuda:
             self.dist.all_gather_into_tensor(out, packets.contiguous(), group=self.group)
         else:
             parts = list(out.chunk(self.world, 0))
             self.dist.all_gather(parts, packets.contiguous(), group=self.group)
+        if ev is not None:
+            ev[1].record()
+            self._events.append((ev, out.numel()))
         self.bytes_moved += out.numel()
         self.calls += 1
         return out
+
+    def reset_stats(self):
+        self._events = []
+
+    def stats(self):
+        """Timed calls since reset_stats(): mean microseconds per all-gather, bytes gathered per call (all ranks'
+        packets), bytes received per rank per call ((world-1)/world of them) and that received rate in GB/s."""
+        if not self._events:
+            return None
+        us = [a.elapsed_time(b) * 1e3 for (a, b), _ in self._events]
+        nbytes = float(np.mean([nb for _, nb in self._events]))
+        recv = nbytes * (self.world - 1) / self.world
+        mean_us = float(np.mean(us))
+        return {"calls": len(us), "us_per_allgather": round(mean_us, 2), "us_min": round(float(np.min(us)), 2),
+                "bytes_per_allgather": int(nbytes), "bytes_received_per_rank": int(recv),
+                "recv_GBps": round(recv / (mean_us * 1e-6) / 1e9, 3) if mean_us > 0 else None}
 
 
 class MapFusionStore:
@@ -254,6 +281,19 @@ class DeviceKeyframeStore:
         self._record(base, [r for r in range(w) for _ in range(n)])
         return range(base, base + w * n)
 
+    def ingest(self, packets, agent: int, exchange: "KeyframeExchange" = None):
+        """This step's keyframes into the ring: all-gathered from every rank when an exchange with world > 1 is
+        given (rank-major), else inserted locally.  Returns (new slots, this agent's slots among them, the agent
+        of every new slot).  The slot order is the order MapFusion processes them in (query, then add)."""
+        n = packets.shape[0]
+        if exchange is not None and exchange.world > 1:
+            new = self.exchange_into(exchange, packets)
+            mine = range(new.start + exchange.rank * n, new.start + (exchange.rank + 1) * n)
+        else:
+            new = self.insert(packets, agent)
+            mine = new
+        return new, mine, [self.agent_of[s] for s in new]
+
     def kf_store(self):
         """orbx_kf_store over the ring (pointers are fixed for the store's lifetime)."""
         if self._store is None:
@@ -288,42 +328,54 @@ class KeyframeFusion:
 
         new keyframes (extractor batch rows) -> ORBVocabulary::transform (BowVector + FeatureVector at level
         L-4, src/KeyFrame.cc ComputeBoW) -> packets -> all-gather into every rank's DeviceKeyframeStore
-        (MapFusion ingress, src/MapFusion.cc:83-88) -> KeyFrameDatabase::DetectLoopCandidates for this rank's
-        new keyframes (src/MapFusion.cc:133; sharded by query keyframe) -> first k candidates of another map
-        (:136-144) -> SearchByBoW(new KF, candidate) (:275) -> the 20-match gate (:275-281) -> the new
-        keyframes join the database (:149 / :222).
+        (MapFusion ingress, src/MapFusion.cc:83-88) -> for every exchanged keyframe in order: DetectLoopCandidates
+        (src/MapFusion.cc:133), then the keyframe joins the database (:149 / :222) -- queries sharded by keyframe:
+        each rank answers its own keyframes' queries on its replica of the database -> first k candidates of
+        another map (:136-144) -> SearchByBoW(new KF, candidate) (:275) -> the 20-match gate (:275-281).
 
-    The database covers the store ring: a slot leaves it when the ring overwrites it.  There is no
-    covisibility graph in this front-end-only pipeline, so queries exclude nothing and use minScore 0
-    (the reference bounds it by the scores of the query's covisible keyframes, :100-131).  With one agent
-    (no exchange) candidates may come from the agent's own map, as LoopClosing's (src/LoopClosing.cc:164)."""
+    The database covers the store ring: a slot leaves it when the ring overwrites it.  The query-then-add order
+    is one sequential detect per step (orbx_kfdb_detect_sequential_device): the step's slots are added in
+    processing order (rank-major) and each query sees only what was added before it, so a later keyframe of
+    the step -- also another agent's -- can be a candidate of the next one, exactly as in MapFusion's loop.
+    Query ids are global keyframe sequence numbers (KeyFrame::mnId), fresh per keyframe.  There is no
+    covisibility graph in this front-end-only pipeline, so queries exclude nothing and use minScore 0 (the
+    reference bounds it by the scores of the query's covisible keyframes, :100-131).  With one agent (no
+    exchange) candidates may come from the agent's own map, as LoopClosing's (src/LoopClosing.cc:164).
+
+    vocab / matcher / db are the library objects (ORBVocabulary, ORBmatcher, KeyFrameDatabase); tests on CPU
+    pass oracle-backed doubles with the same methods."""
 
     def __init__(self, matcher, vocab, capacity: int, slots: int, device, agent: int = 0, exchange=None,
-                 candidates: int = 16, levelsup: int = 4, min_matches: int = 20):
+                 candidates: int = 16, levelsup: int = 4, min_matches: int = 20, db=None):
         import torch
 
-        from .orbx import KeyFrameDatabase
         self.matcher, self.vocab, self.capacity = matcher, vocab, capacity
         self.store = DeviceKeyframeStore(capacity, slots, device)
         self.agent, self.exchange = agent, exchange
         self.k, self.levelsup, self.min_matches = candidates, levelsup, min_matches
         info = vocab.info()
         self.max_fv_nodes = min(capacity, info["k"] ** max(info["L"] - levelsup, 0) + 1)   # launch width hint
-        self.db = KeyFrameDatabase(info["n_words"], slots, max_words=min(capacity, 4096), device=device.index or 0)
+        if db is None:
+            from .orbx import KeyFrameDatabase
+            dev_index = device.index if getattr(device, "index", None) is not None else 0
+            db = KeyFrameDatabase(info["n_words"], slots, max_words=min(capacity, 4096), device=dev_index)
+        self.db = db
         self.device = device
         self._slot_tensors = {}
         self._next_id = 1
         self.slot_group = torch.full((slots,), -1, dtype=torch.int32, device=device)   # map (agent) of each slot
         self.status = torch.zeros((1,), dtype=torch.int32, device=device)             # orbx_kfdb_detect_device flags
 
-    def _slots(self, r: range):
-        import torch
-        key = (r.start, r.stop)
+    def _cached(self, key, make):
         t = self._slot_tensors.get(key)
         if t is None:
-            t = torch.arange(r.start, r.stop, dtype=torch.int32, device=self.device)
+            t = make()
             self._slot_tensors[key] = t
         return t
+
+    def _slots(self, r: range):
+        import torch
+        return self._cached((r.start, r.stop), lambda: torch.arange(r.start, r.stop, dtype=torch.int32, device=self.device))
 
     def step(self, kps, desc, counts, valid, frames, stream=None):
         """kps (n, cap, 28) u8, desc (n, cap, 32) u8, counts (n,), valid (n, cap) u8: this agent's new
@@ -333,43 +385,37 @@ class KeyframeFusion:
         n = kps.shape[0]
         fv = self.vocab.transform_batch_device(desc.contiguous(), counts.contiguous(), self.levelsup, stream=stream)
         pk = pack_keyframes(kps, desc, counts, valid, self.agent, frames, self.capacity, fv)
-        multi = self.exchange is not None and self.exchange.world > 1
+        new, mine, agents = self.store.ingest(pk, self.agent, self.exchange)
+        multi = len(new) != len(mine)
+        w = len(new) // max(n, 1)
+        grp = self._cached(("group", w, n), lambda: torch.arange(w * n, dtype=torch.int32, device=self.device) // n)
         if multi:
-            new = self.store.exchange_into(self.exchange, pk)
-            mine = range(new.start + self.agent * n, new.start + (self.agent + 1) * n)
-            w = self.exchange.world
-            grp = self._slot_tensors.get(("group", w, n))
-            if grp is None:
-                grp = torch.arange(w * n, dtype=torch.int32, device=self.device) // n
-                self._slot_tensors[("group", w, n)] = grp
             self.slot_group[new.start:new.stop].copy_(grp)
         else:
-            new = self.store.insert(pk, self.agent)
-            mine = new
             self.slot_group[new.start:new.stop].fill_(self.agent)
-        # the ring overwrote these slots: they leave the database, take the new BowVectors, and join it after
-        # this step's queries (MapFusion adds the query keyframe after detection, src/MapFusion.cc:149, :222)
+        # the ring overwrote these slots: they leave the database and take the new BowVectors; then they join it
+        # in processing order, and the sequential detect answers each query as if it ran before its own add
         self.db.erase(list(new))
         P, o = self.store.layout.bytes, self.store.layout.offsets
         rows = self.store.buf[new.start:new.stop]
         self.db.set_bow_device(self._slots(new), rows[:, o["bow_words"]:], rows[:, o["bow_values"]:], rows[:, 16:],
                                strides=(P // 4, P // 8, P // 4), stream=stream)
+        self.db.add(list(new))
         q = self._slots(mine)
-        ids = torch.arange(self._next_id, self._next_id + n, dtype=torch.int64, device=self.device)
-        self._next_id += n
-        zeros = self._slot_tensors.get(("zeros", n))
-        if zeros is None:
-            zeros = torch.zeros((n,), dtype=torch.float32, device=self.device)
-            self._slot_tensors[("zeros", n)] = zeros
-        cand, n_cand, _ = self.db.detect_device(0, q, ids, zeros, status=self.status, stream=stream)
+        first = self._next_id + (mine.start - new.start)       # global keyframe ids in processing order
+        ids = torch.arange(first, first + n, dtype=torch.int64, device=self.device)
+        self._next_id += len(new)
+        zeros = self._cached(("zeros", n), lambda: torch.zeros((n,), dtype=torch.float32, device=self.device))
+        cand, n_cand, _ = self.db.detect_device(0, q, ids, zeros, status=self.status, stream=stream, sequential=True)
         if multi:
-            qg = self._slot_tensors.get(("qgroup", n))
-            if qg is None:
-                qg = torch.full((n,), self.agent, dtype=torch.int32, device=self.device)
-                self._slot_tensors[("qgroup", n)] = qg
+            qg = self._cached(("qgroup", n), lambda: torch.full((n,), self.agent, dtype=torch.int32, device=self.device))
             pr = self.db.candidate_pairs_device(cand, n_cand, q, self.k, self.slot_group, qg, stream=stream)
         else:
             pr = self.db.candidate_pairs_device(cand, n_cand, q, self.k, stream=stream)
-        self.db.add(list(new))
         m12, nm = self.matcher.SearchByBoW_pairs_device(self.store.kf_store(), pr, self.max_fv_nodes, stream=stream)
         return pr, m12, nm, nm >= self.min_matches
+
+    def check(self):
+        """Raise if any detect so far reported interacting queries or exceeded capacity (synchronises)."""
+        from .orbx import KeyFrameDatabase
+        KeyFrameDatabase.check_status(self.status)

@@ -201,6 +201,8 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_kfdb_score_device.argtypes = [vp, vp, i32, vp, vp]
     lib.orbx_kfdb_detect.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, vp, i32]
     lib.orbx_kfdb_detect_device.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp]
+    lib.orbx_kfdb_detect_sequential.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, vp, i32]
+    lib.orbx_kfdb_detect_sequential_device.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp]
     _lib = lib
     return lib
 
@@ -813,8 +815,10 @@ class KeyFrameDatabase:
         _check(self._lib.orbx_kfdb_score(self._h, _p(pr), len(pr), _p(out)))
         return out
 
-    def detect(self, kind: int, query_slots, query_ids, min_scores=None, exclusions=None):
-        """Batch of queries evaluated in order; returns a list of candidate-slot arrays."""
+    def detect(self, kind: int, query_slots, query_ids, min_scores=None, exclusions=None, sequential=False):
+        """Batch of queries evaluated in order; returns a list of candidate-slot arrays.  sequential=True: the
+        query slots were added in query order and query q sees only the members added before its own slot
+        (MapFusion's query-then-add order, orbx_kfdb_detect_sequential)."""
         qs = np.atleast_1d(np.ascontiguousarray(query_slots, np.int32))
         nq = len(qs)
         ids = np.atleast_1d(np.ascontiguousarray(query_ids, np.uint64))
@@ -829,14 +833,16 @@ class KeyFrameDatabase:
         oo = np.zeros(nq + 1, np.int32)
         cap = max(1, nq * self.max_slots)
         out = np.zeros(cap, np.int32)
-        _check(self._lib.orbx_kfdb_detect(self._h, kind, _p(qs), _p(ids), None if ms is None else _p(ms), nq,
-                                          None if eo is None else _p(eo), None if ex is None else _p(ex), _p(oo),
-                                          _p(out), cap))
+        fn = self._lib.orbx_kfdb_detect_sequential if sequential else self._lib.orbx_kfdb_detect
+        _check(fn(self._h, kind, _p(qs), _p(ids), None if ms is None else _p(ms), nq, None if eo is None else _p(eo),
+                  None if ex is None else _p(ex), _p(oo), _p(out), cap))
         return [out[oo[i]:oo[i + 1]].copy() for i in range(nq)]
 
     def detect_device(self, kind: int, query_slots, query_ids, min_scores=None, excl_offsets=None, excl_slots=None,
-                      out=None, out_n=None, status=None, stream=None):
-        """Device form: int32 slots, int64 ids, float32 min scores; returns (out, out_n, status) tensors."""
+                      out=None, out_n=None, status=None, stream=None, sequential=False):
+        """Device form: int32 slots, int64 ids, float32 min scores; returns (out, out_n, status) tensors.
+        status bit 1: the queries interacted through the scratch fields (results not sequential); bit 2:
+        candidate capacity exceeded -- check_status() raises on either."""
         import torch
         nq = query_slots.numel()
         dev = query_slots.device
@@ -845,10 +851,20 @@ class KeyFrameDatabase:
         status = status if status is not None else torch.zeros((1,), dtype=torch.int32, device=dev)
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream)
         opt = lambda t: None if t is None else _tp(t)
-        _check(self._lib.orbx_kfdb_detect_device(self._h, kind, _tp(query_slots), _tp(query_ids), opt(min_scores), nq,
-                                                 opt(excl_offsets), opt(excl_slots), _tp(out), out.shape[1], _tp(out_n),
-                                                 _tp(status), s))
+        fn = self._lib.orbx_kfdb_detect_sequential_device if sequential else self._lib.orbx_kfdb_detect_device
+        _check(fn(self._h, kind, _tp(query_slots), _tp(query_ids), opt(min_scores), nq, opt(excl_offsets),
+                  opt(excl_slots), _tp(out), out.shape[1], _tp(out_n), _tp(status), s))
         return out, out_n, status
+
+    @staticmethod
+    def check_status(status):
+        """Raise if a detect_device status word reports interacting queries (1) or exceeded capacity (2)."""
+        v = int(status.reshape(-1)[0].item())
+        if v & 1:
+            raise OrbxError(ORBX_ERR_ARG, "KeyFrameDatabase batch queries interacted through the scratch fields "
+                                          "(repeated or stale query ids): results are not the sequential ones")
+        if v & 2:
+            raise OrbxError(ORBX_ERR_CAPACITY, "KeyFrameDatabase query exceeded its candidate capacity")
 
     @staticmethod
     def candidate_pairs_device(cand, n_cand, query_slots, k: int, slot_group=None, query_group=None, out=None,

@@ -113,3 +113,42 @@ def test_edge_cases(gpu, strategy):
     g.clear()
     assert g.DetectRelocalizationCandidates(0, 14).tolist() == []
     assert g.detect(RELOC, [], []) == []
+
+
+@pytest.mark.parametrize("kind", [LOOP, COVIS, RELOC])
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
+def test_detect_sequential_batch(gpu, kind, strategy):
+    """orbx_kfdb_detect_sequential: a batch of new keyframes added in order and queried in one call equals
+    MapFusion's loop detect(k0); add(k0); detect(k1); add(k1); ... (src/MapFusion.cc:133, :149 / :222) --
+    candidate lists and scratch fields -- with the database's earlier members and the new ones sharing places."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    case = make_kfdb_case(500 + kind, n_slots=120, n_queries=4, words_hi=500)
+    g = pkg.KeyFrameDatabase(case["n_vocab"], case["n_slots"], max_words=2048)
+    g.set_strategy(strategy)
+    o = O.Kfdb(case["n_vocab"], case["n_slots"])
+    setup_db(case, g)
+    setup_db(case, o)
+    rng = np.random.default_rng(kind)
+    order = rng.permutation(case["n_slots"])
+    old, new = order[:80].tolist(), order[80:104].tolist()
+    g.add(old)
+    o.add(old)
+    ids = list(range(1000, 1000 + len(new)))
+    ms = [0.01 * (i % 3) for i in range(len(new))]
+    excl = [order[104 + (i % 16):106 + (i % 16)].tolist() + old[i:i + 2] for i in range(len(new))]
+    g.add(new)
+    got = [list(r) for r in g.detect(kind, new, ids, ms, excl, sequential=True)]
+    ref = []
+    for i, k in enumerate(new):
+        ref.append(list(o.detect(kind, k, ids[i], ms[i], excl[i])))
+        o.add([k])
+    assert got == ref
+    assert sum(len(r) for r in ref) > 0
+    assert any(c in new for r in ref for c in r)        # a new keyframe is a candidate of a later one
+    gq, gw, gs = g.get_state(kind)
+    oq, ow, os_ = o.get_state(kind)
+    assert np.array_equal(gq, oq) and np.array_equal(gw, ow)
+    assert np.array_equal(gs.view(np.uint32), os_.view(np.uint32))
+    # the query slots are members afterwards, in the same order as the oracle's
+    assert g.n_members() == len(old) + len(new)

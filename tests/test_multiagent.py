@@ -272,11 +272,11 @@ def test_gpu_keyframe_fusion_store_vs_oracle(gpu):
         for k in new:
             odb.set_bow(k, *views[k].bow)
         expect = []
-        for k in new:
+        for k in new:                                   # MapFusion: query, then add (src/MapFusion.cc:133, :149)
             c = odb.detect(0, k, qid, 0.0)[:K].tolist()
             qid += 1
             expect += [[k, x] for x in c] + [[k, -1]] * (K - len(c))
-        odb.add(new)
+            odb.add([k])
         prh, m12h, nmh = pr.cpu().numpy(), m12.cpu().numpy(), nm.cpu().numpy()
         assert prh.tolist() == expect, step
         for p, (a, b) in enumerate(prh):
@@ -292,3 +292,225 @@ def test_gpu_keyframe_fusion_store_vs_oracle(gpu):
         assert np.array_equal(passed.cpu().numpy(), nmh >= 20)
     assert fus.status.item() == 0
     assert n_real >= 6 and total > 100
+
+
+class _FakeExchange:
+    """One GPU standing in for two agents: exchange() writes every agent's packets of this step rank-major, as
+    the RCCL all-gather would (the packets of all agents are prepared beforehand)."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+        self.packets = None
+
+    def exchange(self, packets, out=None):
+        assert torch.equal(packets, self.packets[self.rank])
+        g = torch.cat(self.packets, 0)
+        if out is None:
+            return g
+        out.copy_(g)
+        return out
+
+
+@pytest.mark.gpu
+def test_gpu_keyframe_fusion_two_agents_one_gpu(gpu):
+    """KeyframeFusion.step's multi-rank branch on the GPU, two agents emulated on one device: the exchanged ring,
+    slot groups, orbx_kfdb_detect_sequential_device and orbx_kfdb_candidate_pairs_device with slot/query groups
+    (the same-map discard of src/MapFusion.cc:136-144) and the batched SearchByBoW, against the oracle running
+    MapFusion's loop over the same keyframes (every exchanged keyframe queried then added, in order)."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    dev = torch.device("cuda", 0)
+    voc = S.synthetic_vocabulary(31, k=10, L=4)
+    v = pkg.ORBVocabulary.from_arrays(voc)
+    ex = pkg.ORBextractor(1200, 1.2, 8, 20, 7)
+    base = S.kitti_like_image(91)
+    # agents 0 and 1 revisit the same place: 2 keyframes per agent per step, 3 steps
+    imgs = np.stack([S.shifted_right_view(base, 5 + i, max_disp=10) for i in range(12)])
+    kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).to(dev))
+    cap = kps.shape[1]
+    valid = (torch.arange(cap, device=dev)[None, :] < cnt[:, None]).to(torch.uint8)
+    valid[:, 1::3] = 0
+    n, K, W, SLOTS = 2, 3, 2, 8
+    fx = [_FakeExchange(r, W) for r in range(W)]
+    fus = [MA.KeyframeFusion(pkg.ORBmatcher(0.75, True), v, cap, slots=SLOTS, device=dev, agent=r, exchange=fx[r],
+                             candidates=K, levelsup=2) for r in range(W)]
+    odb = O.Kfdb(v.info()["n_words"], SLOTS)
+    kf_id, n_real, n_cross_same_step = 1, 0, 0
+    for step in range(3):
+        rows = [list(range(4 * step + 2 * r, 4 * step + 2 * r + 2)) for r in range(W)]
+        pk = []
+        for r in range(W):
+            ix = torch.tensor(rows[r], device=dev)
+            fv = v.transform_batch_device(desc[ix].contiguous(), cnt[ix].contiguous(), 2)
+            pk.append(MA.pack_keyframes(kps[ix], desc[ix], cnt[ix], valid[ix], r, [10 * step + i for i in range(n)], cap,
+                                        fv))
+        for f in fx:
+            f.packets = pk
+        outs = []
+        for r in range(W):
+            ix = torch.tensor(rows[r], device=dev)
+            outs.append(fus[r].step(kps[ix], desc[ix], cnt[ix], valid[ix], frames=[10 * step + i for i in range(n)]))
+        torch.cuda.synchronize()
+        views = MA.unpack_keyframes(fus[0].store.buf, cap)
+        assert torch.equal(fus[0].store.buf, fus[1].store.buf)
+        new = list(range((4 * step) % SLOTS, (4 * step) % SLOTS + 4))
+        agent = {k: views[k].agent for k in range(SLOTS) if views[k].count > 0}
+        assert [agent[k] for k in new] == [0, 0, 1, 1]
+        for r in range(W):
+            assert fus[r].slot_group[new].tolist() == [0, 0, 1, 1]
+        odb.erase(new)
+        for k in new:
+            odb.set_bow(k, *views[k].bow)
+        expect = {0: [], 1: []}
+        for k in new:
+            a = agent[k]
+            c = [x for x in odb.detect(0, k, kf_id, 0.0).tolist() if agent[x] != a][:K]
+            kf_id += 1
+            n_cross_same_step += sum(1 for x in c if x in new)
+            expect[a] += [[k, x] for x in c] + [[k, -1]] * (K - len(c))
+            odb.add([k])
+        for r in range(W):
+            pr, m12, nm, passed = outs[r]
+            prh, m12h, nmh = pr.cpu().numpy(), m12.cpu().numpy(), nm.cpu().numpy()
+            assert prh.tolist() == expect[r], (step, r)
+            for p, (a, b) in enumerate(prh):
+                if b < 0:
+                    assert nmh[p] == 0 and (m12h[p] == -1).all()
+                    continue
+                A, B = views[a], views[b]
+                rn, rm = O.search_by_bow_kfkf(A.desc, A.kps["angle"], A.valid, A.featvec, B.desc, B.kps["angle"],
+                                              B.valid, B.featvec, 0.75, True)
+                assert nmh[p] == rn and np.array_equal(m12h[p, :A.count], rm), (step, r, p)
+                n_real += 1
+            assert np.array_equal(passed.cpu().numpy(), nmh >= 20)
+            fus[r].check()
+    assert n_real >= 10 and n_cross_same_step >= 1
+
+
+# ---- KeyframeFusion.step on CPU over gloo: ring, exchange, slot groups, query-then-add order ---------------
+_FUS_CAP, _FUS_SLOTS, _FUS_K, _FUS_STEPS, _FUS_N = 320, 8, 3, 3, 2
+
+
+def _fusion_inputs(rank, step):
+    kps, desc, valid, counts = _keyframes(rank, 4, _FUS_CAP)
+    # rotate the views per step so each step's keyframes differ
+    sel = [(step + i) % 4 for i in range(_FUS_N)]
+    return kps[sel], desc[sel], valid[sel], counts[sel]
+
+
+def _fusion_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from fusion_doubles import OracleKfdb, OracleMatcher, OracleVocab
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    voc = S.synthetic_vocabulary(31, k=10, L=4)
+    vocab = OracleVocab(voc)
+    m = OracleMatcher(0.75, True)
+    fus = MA.KeyframeFusion(m, vocab, _FUS_CAP, slots=_FUS_SLOTS, device=torch.device("cpu"), agent=rank,
+                            exchange=MA.KeyframeExchange(), candidates=_FUS_K, levelsup=2,
+                            db=OracleKfdb(vocab.n_words, _FUS_SLOTS))
+    m.fusion = fus
+    outs = []
+    for step in range(_FUS_STEPS):
+        kps, desc, valid, counts = _fusion_inputs(rank, step)
+        pr, m12, nm, passed = fus.step(torch.from_numpy(kps.view(np.uint8).reshape(_FUS_N, _FUS_CAP, 28)),
+                                       torch.from_numpy(desc), torch.from_numpy(counts), torch.from_numpy(valid),
+                                       frames=[10 * step + i for i in range(_FUS_N)])
+        outs.append((pr.tolist(), nm.tolist(), m12.tolist(), passed.tolist(), fus.slot_group.tolist()))
+    fus.check()
+    objs = [None] * world
+    dist.all_gather_object(objs, outs)
+    if rank == 0:
+        q.put(objs)
+    dist.destroy_process_group()
+
+
+def _fusion_expected(world):
+    """MapFusion's server loop (src/MapFusion.cc:51-81) over the same keyframes in processing order: every
+    exchanged keyframe in turn is queried (DetectLoopCandidates, :133), its first K other-map candidates
+    (:136-144) are matched (SearchByBoW, :275), then it joins the database (:149 / :222)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from oracle import oracle as O
+    voc = S.synthetic_vocabulary(31, k=10, L=4)
+    vocab = O.Vocabulary(voc)
+    db = O.Kfdb(int(np.sum(voc["is_leaf"])), _FUS_SLOTS)
+    ring = {}
+    expect = {r: [] for r in range(world)}
+    pos, kf_id = 0, 1
+    for step in range(_FUS_STEPS):
+        n_new = world * _FUS_N
+        if pos + n_new > _FUS_SLOTS:
+            pos = 0
+        slots = list(range(pos, pos + n_new))
+        pos += n_new
+        db.erase(slots)
+        for r in range(world):
+            kps, desc, valid, counts = _fusion_inputs(r, step)
+            for i in range(_FUS_N):
+                s = slots[r * _FUS_N + i]
+                c = counts[i]
+                bow = vocab.transform(desc[i, :c], 2)
+                ring[s] = dict(agent=r, desc=desc[i, :c], angle=kps[i, :c]["angle"], valid=valid[i, :c],
+                               fv=(bow["fv_nodes"], bow["fv_offsets"], bow["fv_indices"]))
+                db.set_bow(s, bow["bow_words"], bow["bow_values"])
+        step_out = {r: ([], [], []) for r in range(world)}
+        for s in slots:
+            r = ring[s]["agent"]
+            cands = [c for c in db.detect(0, s, kf_id, 0.0).tolist() if ring[c]["agent"] != r][:_FUS_K]
+            kf_id += 1
+            for c in cands + [-1] * (_FUS_K - len(cands)):
+                step_out[r][0].append([s, c])
+                if c < 0:
+                    step_out[r][1].append(0)
+                    step_out[r][2].append(None)
+                    continue
+                A, B = ring[s], ring[c]
+                nm, m12 = O.search_by_bow_kfkf(A["desc"], A["angle"], A["valid"], A["fv"], B["desc"], B["angle"],
+                                               B["valid"], B["fv"], 0.75, True)
+                step_out[r][1].append(int(nm))
+                step_out[r][2].append(np.asarray(m12).tolist())
+            db.add([s])
+        for r in range(world):
+            expect[r].append(step_out[r])
+    return expect
+
+
+def test_keyframe_fusion_step_two_agents_gloo():
+    """KeyframeFusion.step's multi-rank branch on CPU (gloo, world 2) with oracle-backed vocabulary, database and
+    matcher: the exchanged ring, the slot groups, the sequential query-then-add order and the same-map discard
+    must give exactly MapFusion's single-server results, split by the agent that owns each query."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fusion_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    objs = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    expect = _fusion_expected(world)
+    n_real = 0
+    for r in range(world):
+        for step in range(_FUS_STEPS):
+            pr, nm, m12, passed, groups = objs[r][step]
+            epr, enm, em12 = expect[r][step]
+            assert pr == epr, (r, step)
+            assert nm == enm, (r, step)
+            for p, e in enumerate(em12):
+                if e is None:
+                    assert all(v == -1 for v in m12[p])
+                else:
+                    assert m12[p][:len(e)] == e
+                    n_real += 1
+            assert passed == [v >= 20 for v in nm]
+            # ring slots of this step carry their agent
+            assert sorted(set(g for g in groups if g >= 0)) == [0, 1]
+    assert n_real >= 6
+    # sequential adds: in the first step (empty ring before it) agent 1's keyframes (slots 2, 3) already see agent
+    # 0's keyframes of the same exchange (slots 0, 1), which MapFusion added before them
+    assert any(c in (0, 1) for _, c in objs[1][0][0])
+    assert max(v for r in range(world) for st in objs[r] for v in st[1]) >= 20
