@@ -234,6 +234,24 @@ typedef struct orbx_kf_store {
 int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const orbx_kf_store* store, const int32_t* d_pairs,
                                          int n_pairs, int max_fv_nodes, int32_t* d_match12, int32_t* d_nmatches,
                                          void* stream);
+/* orbx_distinctive_descriptors over a keyframe store (see above): observation o = (slot d_obs[2o], keypoint
+ * d_obs[2o+1]). */
+int orbx_distinctive_descriptors_store_device(orbx_matcher* m, const orbx_kf_store* store, const int32_t* d_obs,
+                                              const int32_t* d_offsets, int n_mappoints, int32_t* d_best,
+                                              uint8_t* d_out_desc, void* stream);
+
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:246-311) for n_mappoints MapPoints at once.  MapPoint p's
+ * observed descriptors -- the rows of its non-bad observing keyframes, in mObservations order (the caller
+ * flattens them) -- are desc[offsets[p] .. offsets[p+1]) (32 B each).  best[p] = the index, within p's list, of
+ * the descriptor with the least median distance to the others (the reference's first strict minimum of
+ * vDists[(size_t)(0.5*(N-1))] over rows of the all-pairs Hamming table), -1 for a MapPoint without observations
+ * (the reference returns, leaving mDescriptor unchanged).  out_desc[p] (may be NULL) = that descriptor
+ * (mDescriptor).  Host form and device forms; the _store_ form reads observation o as keypoint obs[2o+1] of
+ * keyframe slot obs[2o] of a device keyframe store (e.g. MapFusion's packet ring). */
+int orbx_distinctive_descriptors(orbx_matcher* m, const uint8_t* desc, const int32_t* offsets, int n_mappoints, int32_t* best,
+                                 uint8_t* out_desc);
+int orbx_distinctive_descriptors_device(orbx_matcher* m, const uint8_t* d_desc, const int32_t* d_offsets, int n_mappoints,
+                                        int32_t* d_best, uint8_t* d_out_desc, void* stream);
 
 /* ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (src/ORBmatcher.cc:161-290).
  * validk[i] != 0 when KF keypoint i has a non-bad MapPoint.  matchf[j] = KF index or -1. */

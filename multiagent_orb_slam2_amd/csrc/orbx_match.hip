@@ -658,6 +658,82 @@ __global__ __launch_bounds__(1024) void k_stereo_median(RefineArgs A) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:246-311), batched over MapPoints
+// ---------------------------------------------------------------------------------------------
+// The reference fills the N x N distance table, sorts each row and takes element (size_t)(0.5*(N-1)) =
+// (N-1)/2 as the row's median, keeping the first row with the strictly smallest median.  Here one wave per
+// MapPoint, lane = row: the median of row i is the smallest v with #{j : d(i, j) <= v} >= (N-1)/2 + 1 (d(i, i) = 0
+// included, as in the table), found by a 9-step binary search over v in [0, 256] -- each step counts the row
+// against every descriptor of the MapPoint, broadcast from registers (v_readlane), so nothing is sorted and
+// nothing goes through LDS.  (median << 20 | row) wave minimum = first row with the smallest median.
+struct DistinctArgs {
+    const uint8_t* desc;      // flat observation descriptors [total][32] (store == 0)
+    const int32_t* obs;       // (slot, keypoint index) per observation (store == 1)
+    orbx_kf_store S;
+    int store;
+    const int32_t* off;       // [M + 1]
+    int M;
+    int32_t* best;            // [M] index in the MapPoint's observation list, -1 when it has none
+    uint8_t* out;             // [M][32] the chosen descriptor (mDescriptor), or NULL
+    int nbx;
+};
+
+__device__ __forceinline__ const uint8_t* obs_desc(const DistinctArgs& A, int o) {
+    if (!A.store) return A.desc + 32 * (size_t)o;
+    const int slot = A.obs[2 * (size_t)o], idx = A.obs[2 * (size_t)o + 1];
+    return A.S.desc + (size_t)slot * A.S.desc_stride + 32 * (size_t)idx;
+}
+
+__global__ __launch_bounds__(256) void k_distinctive(DistinctArgs A) {
+    const int item = xcd_item(xcd_chunk(A.nbx));
+    if (item >= A.nbx) return;
+    const int mp = item * 4 + (int)(threadIdx.x >> 6);
+    if (mp >= A.M) return;
+    const int ln = lane_id();
+    const int o0 = A.off[mp], N = A.off[mp + 1] - o0;
+    if (N <= 0) {
+        if (ln == 0) A.best[mp] = -1;
+        return;
+    }
+    const int need = (N - 1) / 2 + 1;          // rank of vDists[(size_t)(0.5 * (N - 1))], 1-based
+    uint32_t bestkey = 0xffffffffu;
+    for (int rc = 0; rc < N; rc += kWave) {
+        const int i = rc + ln;
+        uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+        if (i < N) load_desc(obs_desc(A, o0 + i), a0, a1);
+        int lo = 0, hi = 256;
+#pragma unroll 1
+        for (int it = 0; it < 9; ++it) {
+            const int mid = (lo + hi) >> 1;
+            int cnt = 0;
+            for (int cc = 0; cc < N; cc += kWave) {
+                const int j = cc + ln;
+                uint4 b0 = make_uint4(0, 0, 0, 0), b1 = b0;
+                if (j < N) load_desc(obs_desc(A, o0 + j), b0, b1);
+                const int nc = min(kWave, N - cc);
+                for (int t = 0; t < nc; ++t) {
+                    uint4 x0, x1;
+                    x0.x = __builtin_amdgcn_readlane(b0.x, t); x0.y = __builtin_amdgcn_readlane(b0.y, t);
+                    x0.z = __builtin_amdgcn_readlane(b0.z, t); x0.w = __builtin_amdgcn_readlane(b0.w, t);
+                    x1.x = __builtin_amdgcn_readlane(b1.x, t); x1.y = __builtin_amdgcn_readlane(b1.y, t);
+                    x1.z = __builtin_amdgcn_readlane(b1.z, t); x1.w = __builtin_amdgcn_readlane(b1.w, t);
+                    cnt += hamming256(a0, a1, x0, x1) <= mid;
+                }
+            }
+            if (cnt >= need) hi = mid; else lo = mid + 1;
+        }
+        const uint32_t key = (i < N) ? (((uint32_t)lo << 20) | (uint32_t)i) : 0xffffffffu;
+        bestkey = min(bestkey, wave_min_u32(key));
+    }
+    const int bi = (int)(bestkey & 0xfffff);
+    if (ln == 0) A.best[mp] = bi;
+    if (A.out && ln < 8) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(obs_desc(A, o0 + bi));
+        reinterpret_cast<uint32_t*>(A.out + 32 * (size_t)mp)[ln] = src[ln];
+    }
+}
+
 // =============================================================================================
 // host side
 // =============================================================================================
@@ -1158,6 +1234,67 @@ int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const orbx_kf_store* s
     if (m->checkOri)
         hipLaunchKernelGGL(k_rot_filter, dim3(n_pairs), dim3(256), 0, s, d_match12, bin, S.capacity, hist, d_nmatches, S.capacity);
     ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+static int distinct_launch(DistinctArgs& A, hipStream_t s) {
+    if (A.M == 0) return ORBX_OK;
+    A.nbx = (A.M + 3) / 4;
+    hipLaunchKernelGGL(k_distinctive, dim3(kXcds * xcd_chunk(A.nbx)), dim3(256), 0, s, A);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_distinctive_descriptors_device(orbx_matcher* m, const uint8_t* d_desc, const int32_t* d_offsets, int n_mappoints,
+                                        int32_t* d_best, uint8_t* d_out_desc, void* stream) {
+    ORBX_REQUIRE(m && n_mappoints >= 0 && (n_mappoints == 0 || (d_desc && d_offsets && d_best)), ORBX_ERR_ARG, "bad argument");
+    ORBX_HIP(hipSetDevice(m->device));
+    DistinctArgs A{};
+    A.desc = d_desc; A.store = 0; A.off = d_offsets; A.M = n_mappoints; A.best = d_best; A.out = d_out_desc;
+    return distinct_launch(A, (hipStream_t)stream);
+}
+
+int orbx_distinctive_descriptors_store_device(orbx_matcher* m, const orbx_kf_store* store, const int32_t* d_obs,
+                                              const int32_t* d_offsets, int n_mappoints, int32_t* d_best, uint8_t* d_out_desc,
+                                              void* stream) {
+    ORBX_REQUIRE(m && store && n_mappoints >= 0 && (n_mappoints == 0 || (d_obs && d_offsets && d_best)), ORBX_ERR_ARG,
+                 "bad argument");
+    ORBX_REQUIRE(store->desc && ((uintptr_t)store->desc % 16) == 0 && store->desc_stride % 16 == 0, ORBX_ERR_ARG,
+                 "misaligned keyframe store");
+    ORBX_HIP(hipSetDevice(m->device));
+    DistinctArgs A{};
+    A.obs = d_obs; A.S = *store; A.store = 1; A.off = d_offsets; A.M = n_mappoints; A.best = d_best; A.out = d_out_desc;
+    return distinct_launch(A, (hipStream_t)stream);
+}
+
+int orbx_distinctive_descriptors(orbx_matcher* m, const uint8_t* desc, const int32_t* offsets, int n_mappoints, int32_t* best,
+                                 uint8_t* out_desc) {
+    ORBX_REQUIRE(m && n_mappoints >= 0 && (n_mappoints == 0 || (offsets && best)), ORBX_ERR_ARG, "bad argument");
+    if (n_mappoints == 0) return ORBX_OK;
+    ORBX_REQUIRE(offsets[0] == 0, ORBX_ERR_ARG, "offsets[0] must be 0");
+    for (int i = 0; i < n_mappoints; ++i)
+        ORBX_REQUIRE(offsets[i + 1] >= offsets[i], ORBX_ERR_ARG, "offsets not monotone at %d", i);
+    const int total = offsets[n_mappoints];
+    ORBX_REQUIRE(total == 0 || desc, ORBX_ERR_ARG, "null descriptors");
+    ORBX_REQUIRE(total < (1 << 30) / 32, ORBX_ERR_UNSUPPORTED, "too many observations");
+    ORBX_HIP(hipSetDevice(m->device));
+    const size_t M = (size_t)n_mappoints;
+    int st = m->reserve(a256(32 * (size_t)std::max(total, 1)) + a256(4 * (M + 1)) + a256(4 * M) + a256(32 * M));
+    if (st) return st;
+    Bump bp{(uint8_t*)m->scratch};
+    uint8_t* dd = bp.take<uint8_t>(32 * (size_t)std::max(total, 1));
+    int32_t* doff = bp.take<int32_t>(M + 1);
+    int32_t* dbest = bp.take<int32_t>(M);
+    uint8_t* dout = bp.take<uint8_t>(32 * M);
+    hipStream_t s = m->stream;
+    if (total) ORBX_HIP(hipMemcpyAsync(dd, desc, 32 * (size_t)total, hipMemcpyHostToDevice, s));
+    ORBX_HIP(hipMemcpyAsync(doff, offsets, 4 * (M + 1), hipMemcpyHostToDevice, s));
+    DistinctArgs A{};
+    A.desc = dd; A.store = 0; A.off = doff; A.M = n_mappoints; A.best = dbest; A.out = out_desc ? dout : nullptr;
+    if ((st = distinct_launch(A, s))) return st;
+    ORBX_HIP(hipMemcpyAsync(best, dbest, 4 * M, hipMemcpyDeviceToHost, s));
+    if (out_desc) ORBX_HIP(hipMemcpyAsync(out_desc, dout, 32 * M, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
     return ORBX_OK;
 }
 

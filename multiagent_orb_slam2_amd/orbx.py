@@ -172,6 +172,9 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, i32, FeatVec, vp, vp, vp, vp, i32, FeatVec,
                                                   vp, vp, vp, i32, f32, f32, i32, vp, C.POINTER(i32)]
     lib.orbx_search_by_bow_kfkf_pairs_device.argtypes = [vp, C.POINTER(KfStore), vp, i32, i32, vp, vp, vp]
+    lib.orbx_distinctive_descriptors.argtypes = [vp, vp, vp, i32, vp, vp]
+    lib.orbx_distinctive_descriptors_device.argtypes = [vp, vp, vp, i32, vp, vp, vp]
+    lib.orbx_distinctive_descriptors_store_device.argtypes = [vp, C.POINTER(KfStore), vp, vp, i32, vp, vp, vp]
     lib.orbx_grid_build_device.argtypes = [vp, Grid, vp, vp, i32, i32, vp, vp, vp]
     lib.orbx_proj_search_batch_device.argtypes = [vp, C.POINTER(ProjParams), Grid, vp, i32, i32, i32, vp]
     lib.orbx_proj_search.argtypes = [vp, C.POINTER(ProjParams), Grid, vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp,
@@ -545,6 +548,41 @@ class ORBmatcher:
                                                        C.byref(n)))
         return n.value, m
 
+
+    # ---- MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:246-311) ----------------------------------
+    def ComputeDistinctiveDescriptors(self, descriptor_lists):
+        """For each MapPoint, its observed descriptors (an (N, 32) uint8 array, in mObservations order, bad
+        keyframes skipped): returns (best index per MapPoint, -1 if it has none; (M, 32) chosen descriptors)."""
+        lists = [np.ascontiguousarray(d, np.uint8).reshape(-1, 32) for d in descriptor_lists]
+        M = len(lists)
+        off = np.zeros(M + 1, np.int32)
+        off[1:] = np.cumsum([len(d) for d in lists])
+        flat = np.ascontiguousarray(np.concatenate(lists) if off[-1] else np.zeros((1, 32), np.uint8))
+        best = np.zeros(max(M, 1), np.int32)
+        out = np.zeros((max(M, 1), 32), np.uint8)
+        _check(self._lib.orbx_distinctive_descriptors(self._h, _p(flat), _p(off), M, _p(best), _p(out)))
+        return best[:M], out[:M]
+
+    def distinctive_descriptors_device(self, desc, offsets, out_desc=None, stream=None):
+        """Device form: desc (total, 32) uint8, offsets (M+1,) int32 device tensors -> (best (M,), out (M, 32))."""
+        import torch
+        M = offsets.numel() - 1
+        best = torch.empty((max(M, 1),), dtype=torch.int32, device=offsets.device)
+        out = out_desc if out_desc is not None else torch.empty((max(M, 1), 32), dtype=torch.uint8, device=offsets.device)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(offsets.device).cuda_stream)
+        _check(self._lib.orbx_distinctive_descriptors_device(self._h, _tp(desc), _tp(offsets), M, _tp(best), _tp(out), s))
+        return best[:M], out[:M]
+
+    def distinctive_descriptors_store_device(self, store: "KfStore", obs, offsets, stream=None):
+        """Over a device keyframe store: obs (total, 2) int32 (slot, keypoint index), offsets (M+1,) int32."""
+        import torch
+        M = offsets.numel() - 1
+        best = torch.empty((max(M, 1),), dtype=torch.int32, device=offsets.device)
+        out = torch.empty((max(M, 1), 32), dtype=torch.uint8, device=offsets.device)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(offsets.device).cuda_stream)
+        _check(self._lib.orbx_distinctive_descriptors_store_device(self._h, C.byref(store), _tp(obs), _tp(offsets), M,
+                                                                   _tp(best), _tp(out), s))
+        return best[:M], out[:M]
 
     # ---- projection / radius matchers (src/ORBmatcher.cc; SURVEY §8f row 2) ------------------------------
     def proj_search(self, params: ProjParams, grid: Grid, queries, qdesc, kps, desc, uright=None, blocked=None):

@@ -130,6 +130,18 @@ def bf_match(q, t):
     return bi, b1, b2
 
 
+def distinctive_descriptors(lists):
+    """MapPoint::ComputeDistinctiveDescriptors restated (oracle/orb_oracle.cpp orc_distinctive): best index per
+    descriptor list (-1 for an empty list)."""
+    lists = [np.ascontiguousarray(d, np.uint8).reshape(-1, 32) for d in lists]
+    off = np.zeros(len(lists) + 1, np.int32)
+    off[1:] = np.cumsum([len(d) for d in lists])
+    flat = np.ascontiguousarray(np.concatenate(lists) if off[-1] else np.zeros((1, 32), np.uint8))
+    best = np.zeros(max(len(lists), 1), np.int32)
+    lib().orc_distinctive(_p(flat), _p(off), len(lists), _p(best))
+    return best[:len(lists)]
+
+
 def stereo_match(kl, dl, kr, dr, scale, rows, bf, b):
     kl, kr = np.ascontiguousarray(kl, KP_DTYPE), np.ascontiguousarray(kr, KP_DTYPE)
     dl, dr = np.ascontiguousarray(dl, np.uint8), np.ascontiguousarray(dr, np.uint8)

@@ -23,6 +23,7 @@
 //      larger key), i.e. a stable sort by size.
 // =====================================================================================================
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -285,6 +286,24 @@ void split4(const QNode& n, QNode c[4]) {
         if (c[q].keys.size() == 1) c[q].leaf = true;
 }
 
+// Phase-2 tie study: the reference orders equal-size nodes by heap address (:681-684), i.e. an
+// allocator-dependent permutation of each tie group.  tie_mode 0 is the pinned rule (creation order, later-created
+// first, as the HIP path); 1 = earlier-created first; 2 = a seeded pseudo-random permutation of every tie group.
+// The counters record how often a phase-2 pass splits equal-size nodes and how often its >=N break falls inside
+// a run of equal sizes (only then can the keypoint SET depend on the tie order).
+struct TieStats {
+    long levels = 0, levels_phase2 = 0, passes_phase2 = 0, passes_with_tie_split = 0, breaks_inside_tie = 0;
+};
+static thread_local int g_tie_mode = 0;
+static thread_local unsigned g_tie_salt = 0;
+static thread_local TieStats g_tie_stats;
+
+static unsigned tie_hash(long seq) {
+    unsigned x = (unsigned)seq * 2654435761u ^ g_tie_salt;
+    x ^= x >> 15; x *= 2246822519u; x ^= x >> 13; x *= 3266489917u; x ^= x >> 16;
+    return x;
+}
+
 std::vector<Kp> distribute_octtree(const std::vector<Kp>& cand, int minX, int maxX, int minY, int maxY, int N) {
     // A level whose detection window is empty has no candidates; the reference would divide by zero
     // here (undefined behaviour) — both this oracle and the HIP path return no keypoints.
@@ -331,6 +350,8 @@ std::vector<Kp> distribute_octtree(const std::vector<Kp>& cand, int minX, int ma
     };
 
     bool done = false;
+    bool level_phase2 = false;
+    g_tie_stats.levels++;
     while (!done) {
         const int before = (int)nodes.size();
         int nToExpand = 0;
@@ -349,15 +370,32 @@ std::vector<Kp> distribute_octtree(const std::vector<Kp>& cand, int minX, int ma
                 const int before2 = (int)nodes.size();
                 std::vector<Expandable> prev = expandable;
                 expandable.clear();
-                std::sort(prev.begin(), prev.end(),
-                          [](const Expandable& a, const Expandable& b) { return a.first < b.first; });
+                if (g_tie_mode == 0) {
+                    std::sort(prev.begin(), prev.end(),
+                              [](const Expandable& a, const Expandable& b) { return a.first < b.first; });
+                } else {
+                    std::sort(prev.begin(), prev.end(), [](const Expandable& a, const Expandable& b) {
+                        if (a.first.first != b.first.first) return a.first.first < b.first.first;
+                        if (g_tie_mode == 1) return a.first.second > b.first.second;
+                        return tie_hash(a.first.second) < tie_hash(b.first.second);
+                    });
+                }
+                if (!level_phase2) { level_phase2 = true; g_tie_stats.levels_phase2++; }
+                g_tie_stats.passes_phase2++;
+                int j_last = -1;
                 for (int j = (int)prev.size() - 1; j >= 0; --j) {
                     QNode c[4];
                     split4(*prev[j].second, c);
                     emit_children(c, &expandable);
                     nodes.erase(prev[j].second);
+                    j_last = j;
                     if ((int)nodes.size() >= N) break;
                 }
+                bool tie_split = false;
+                for (int j = (int)prev.size() - 1; j > j_last && j > 0; --j)
+                    if (prev[j].first.first == prev[j - 1].first.first && j - 1 >= j_last) tie_split = true;
+                if (tie_split) g_tie_stats.passes_with_tie_split++;
+                if (j_last > 0 && prev[j_last].first.first == prev[j_last - 1].first.first) g_tie_stats.breaks_inside_tie++;
                 if ((int)nodes.size() >= N || (int)nodes.size() == before2) done = true;
             }
         }
@@ -706,6 +744,14 @@ int orc_level_candidates(int nfeatures, float scaleFactor, int nlevels, int iniT
 
 // DistributeOctTree on given window-relative candidates (x, y, response) — returns kept count and the
 // kept keys (x, y, response) in list order.
+// Tie-rule study hooks (test infrastructure): set the phase-2 tie mode of this thread, read / reset its counters.
+void orc_set_tie_mode(int mode, unsigned salt) { g_tie_mode = mode; g_tie_salt = salt; }
+void orc_tie_stats(long* out5) {
+    out5[0] = g_tie_stats.levels; out5[1] = g_tie_stats.levels_phase2; out5[2] = g_tie_stats.passes_phase2;
+    out5[3] = g_tie_stats.passes_with_tie_split; out5[4] = g_tie_stats.breaks_inside_tie;
+    g_tie_stats = TieStats();
+}
+
 int orc_distribute(const float* xyr, int n, int minX, int maxX, int minY, int maxY, int N, float* out, int cap) {
     std::vector<Kp> cand(n);
     for (int i = 0; i < n; ++i) cand[i] = Kp{xyr[3 * i], xyr[3 * i + 1], 7.f, -1.f, xyr[3 * i + 2], 0, -1};
@@ -733,6 +779,35 @@ int orc_blur7(const uint8_t* src, int w, int h, uint8_t* dst) {
 float orc_fast_atan2(float y, float x) { return fast_atan2_deg(y, x); }
 
 int orc_descriptor_distance(const uint8_t* a, const uint8_t* b) { return hamming(a, b); }
+
+// MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:246-311) per MapPoint p over its observed descriptors
+// desc[offsets[p] .. offsets[p+1]): float distance table, each row copied into a vector<int>, sorted, element
+// 0.5*(N-1) (converted to size_t) as the median; the first row with a strictly smaller median wins.  best[p] = -1
+// when p has no descriptors (the reference returns early).
+void orc_distinctive(const uint8_t* desc, const int32_t* offsets, int M, int32_t* best) {
+    for (int p = 0; p < M; ++p) {
+        const size_t N = (size_t)(offsets[p + 1] - offsets[p]);
+        const uint8_t* d = desc + 32 * (size_t)offsets[p];
+        if (N == 0) { best[p] = -1; continue; }
+        std::vector<float> D(N * N);
+        for (size_t i = 0; i < N; i++) {
+            D[i * N + i] = 0;
+            for (size_t j = i + 1; j < N; j++) {
+                const int dij = hamming(d + 32 * i, d + 32 * j);
+                D[i * N + j] = (float)dij;
+                D[j * N + i] = (float)dij;
+            }
+        }
+        int bestMedian = INT_MAX, bestIdx = 0;
+        for (size_t i = 0; i < N; i++) {
+            std::vector<int> v(D.begin() + i * N, D.begin() + (i + 1) * N);
+            std::sort(v.begin(), v.end());
+            const int median = v[(size_t)(0.5 * (double)(N - 1))];
+            if (median < bestMedian) { bestMedian = median; bestIdx = (int)i; }
+        }
+        best[p] = bestIdx;
+    }
+}
 
 // Brute force: per query, min distance, lowest index achieving it, second smallest distance (multiset),
 // with the reference's "init 256, strict <" update rule (ORBmatcher.cc:568-598).

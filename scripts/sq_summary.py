@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel SQ counter summary of a scripts/prof_sq.sh run (kernel trace + two --pmc passes).
 
-usage: scripts/sq_summary.py gpurun_out/<TAG> <out.json>
+usage: scripts/sq_summary.py gpurun_out/<TAG> <out.json> [config batch_images]
 
 Derived per kernel (averages per dispatch):
   valu_lane_ops      = SQ_INSTS_VALU * 64 (wave instructions x lanes; an upper bound: exec-masked lanes count)
@@ -66,7 +66,12 @@ def main():
         if d.get("SQ_ACTIVE_INST_LDS"):
             e["lds_conflict_frac"] = round(d.get("SQ_LDS_BANK_CONFLICT", 0) / (d["SQ_ACTIVE_INST_LDS"] * 4), 4)
         res[k] = e
-    json.dump({"peak_valu_tops": PEAK_VALU_TOPS, "kernels": res}, open(out, "w"), indent=1)
+    tag = base.rstrip("/").split("/")[-1]
+    meta = {"tag": tag, "config": sys.argv[3] if len(sys.argv) > 3 else "kitti",
+            "batch_images": int(sys.argv[4]) if len(sys.argv) > 4 else 128,
+            "note": "per-dispatch averages of a short bench run (scripts/prof_sq.sh); SQ_* wave counters summed over "
+                    "the chip by rocprofv3; valu_lane_ops = SQ_INSTS_VALU x 64"}
+    json.dump(dict(meta, peak_valu_tops=PEAK_VALU_TOPS, kernels=res), open(out, "w"), indent=1)
     for k, e in list(res.items())[:14]:
         print(f"{k:24s} {e['avg_ns']/1e3:8.1f}us {e['pct']:5.1f}% valu {e['valu_tops']:6.2f}T ({100*e['valu_frac']:4.1f}%) "
               f"clk {e.get('clock_ghz', 0):.2f} occ {e.get('occupancy_waves_per_cu', 0):5.1f} issue {e.get('valu_issue_frac', 0):.3f} "
