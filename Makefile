@@ -5,7 +5,7 @@ PKG := multiagent_orb_slam2_amd
 SRC := $(PKG)/csrc
 HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result
 HDRS := include/orbx.h $(SRC)/orbx_common.h $(SRC)/orbx_pattern.h $(SRC)/orbx_sincos.h
-OBJS := $(SRC)/orbx_extract.o $(SRC)/orbx_match.o $(SRC)/orbx_vocab.o $(SRC)/orbx_proj.o $(SRC)/orbx_kfdb.o
+OBJS := $(SRC)/orbx_extract.o $(SRC)/orbx_match.o $(SRC)/orbx_vocab.o $(SRC)/orbx_proj.o $(SRC)/orbx_kfdb.o $(SRC)/orbx_fusion.o
 
 all: $(PKG)/liborbx.so oracle
 
@@ -13,7 +13,7 @@ $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(PKG)/liborbx.so: $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -ldl
 
 oracle:
 	$(MAKE) -s -C oracle

@@ -253,31 +253,43 @@ def main():
     m = pkg.ORBmatcher(0.6, True, device=dev.index)
     scale = ex.GetScaleFactors()
     cap = ex.max_keypoints(ROWS, COLS)
-    kps = torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev)
-    desc = torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev)
-    cnt = torch.empty((2 * B,), dtype=torch.int32, device=dev)
+    # two sets of extractor outputs: step k's keyframe path (on its own queue) reads set k % 2 while step k+1's
+    # front-end writes the other set; the front-end waits for the keyframe path of step k-1 before reusing a set
+    outs = [(torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev),
+             torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev),
+             torch.empty((2 * B,), dtype=torch.int32, device=dev)) for _ in range(2)]
     stream = torch.cuda.Stream(dev)                    # front-end queue: extractor + stereo matcher
     torch.cuda.set_stream(stream)
-    # keyframe queue: BoW, RCCL exchange, KeyFrameDatabase, SearchByBoW.  As in the reference, where MapFusion
-    # and LoopClosing run in their own threads beside Tracking, step k's keyframe work overlaps step k+1's
-    # extraction; it reads private copies of the keyframe rows taken on the front-end queue.
+    # keyframe queue: BoW, packets, exchange, KeyFrameDatabase, SearchByBoW -- the native orbx_fusion object.  As in
+    # the reference, where LoopClosing and MapFusion run in their own threads beside Tracking, step k's keyframe work
+    # overlaps step k+1's extraction.
     kf_stream = torch.cuda.Stream(dev)
+    kf_done = [None, None]
     n_kf = max(1, B // KF_EVERY)
-    kf_rows = torch.arange(0, KF_EVERY * n_kf, KF_EVERY, device=dev)
     voc = S.synthetic_vocabulary(2024, k=10, L=6)      # ORBvoc.txt's shape ("10 6 0 0"); the file is absent
     vocab = pkg.ORBVocabulary.from_arrays(voc, device=dev.index)
     exchange = MA.KeyframeExchange(timed=not args.no_timing) if world > 1 else None
-    fusion = MA.KeyframeFusion(pkg.ORBmatcher(0.75, True, device=dev.index), vocab, cap,
-                               slots=STORE_STEPS * world * n_kf, device=dev, agent=rank, exchange=exchange,
-                               candidates=KF_CANDIDATES)
+    engine = pkg.KeyframeFusionEngine(vocab, pkg.ORBmatcher(0.75, True, device=dev.index), cap,
+                                      slots=STORE_STEPS * world * n_kf, max_keyframes=n_kf, candidates=KF_CANDIDATES,
+                                      agent=rank, world=world, device=dev.index)
+    kf_rows = range(0, KF_EVERY * n_kf, KF_EVERY)      # every 5th left frame of the batch becomes a keyframe
+    if world > 1:
+        send = torch.empty((n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
+        gathered = torch.empty((world * n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
     frame_no = [chunk.start]
-    gate = torch.zeros((), dtype=torch.int64, device=dev)
+    n_step = [0]
 
     stereo_ms = []
     kf_ms = []
     pyr = []
+    host_split = [0.0, 0.0]                            # host enqueue seconds: front-end, keyframe path
 
     def step(time_stereo=False):
+        h0 = time.perf_counter()
+        buf = n_step[0] % 2
+        kps, desc, cnt = outs[buf]
+        if kf_done[buf] is not None:
+            stream.wait_event(kf_done[buf])            # the keyframe path of two steps ago has read this set
         ex.extract_batch_device(imgs, kps, desc, cnt, stream=stream)
         if time_stereo:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -291,27 +303,35 @@ def main():
         if time_stereo:
             e1.record(stream)
             stereo_ms.append((e0, e1))
-        # keyframe path: BoW -> packets -> all-gather (N>1) into the store -> batched SearchByBoW
-        valid = (depth.index_select(0, kf_rows) > 0).to(torch.uint8)   # stereo keypoints get MapPoints
-        frames = kf_rows.to(torch.int32) + frame_no[0]          # device-side frame ids (no host->device copy)
-        frame_no[0] += B
-        kf_in = (kps.index_select(0, kf_rows), desc.index_select(0, kf_rows), cnt.index_select(0, kf_rows), valid,
-                 frames)
         handoff = torch.cuda.Event()
         handoff.record(stream)
+        h1 = time.perf_counter()
+        # keyframe path: rows of this step's batch -> BoW -> packets -> all-gather (N>1) into the ring -> sequential
+        # DetectLoopCandidates -> batched SearchByBoW; MapPoint-valid = stereo depth > 0
         kf_stream.wait_event(handoff)
-        for t in kf_in:
-            t.record_stream(kf_stream)
-        with torch.cuda.stream(kf_stream):
-            if time_stereo:
-                e2 = torch.cuda.Event(enable_timing=True)
-                e2.record(kf_stream)
-            _, _, nm, passed = fusion.step(*kf_in, stream=kf_stream)
-            gate.add_(passed.sum())
-            if time_stereo:
-                e3 = torch.cuda.Event(enable_timing=True)
-                e3.record(kf_stream)
-                kf_ms.append((e2, e3))
+        depth.record_stream(kf_stream)
+        if time_stereo:
+            e2 = torch.cuda.Event(enable_timing=True)
+            e2.record(kf_stream)
+        if world == 1:
+            engine.step(kps, desc, cnt, kf_rows, frame_no[0], KF_EVERY, depth=depth, stream=kf_stream)
+        else:
+            engine.pack(kps, desc, cnt, kf_rows, frame_no[0], KF_EVERY, depth=depth, send=send, stream=kf_stream)
+            with torch.cuda.stream(kf_stream):
+                exchange.exchange(send, out=gathered)
+            engine.commit(gathered, stream=kf_stream)
+        done = torch.cuda.Event()
+        done.record(kf_stream)
+        kf_done[buf] = done
+        if time_stereo:
+            e3 = torch.cuda.Event(enable_timing=True)
+            e3.record(kf_stream)
+            kf_ms.append((e2, e3))
+        frame_no[0] += B
+        n_step[0] += 1
+        h2 = time.perf_counter()
+        host_split[0] += h1 - h0
+        host_split[1] += h2 - h1
         return bi, bd
 
     for _ in range(STORE_STEPS):                       # fill the keyframe store ring (setup, untimed)
@@ -329,6 +349,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     host_s = 0.0
+    host_split[0] = host_split[1] = 0.0
     for _ in range(args.steps):
         th = time.perf_counter()
         step(time_stereo=not args.no_timing)
@@ -349,6 +370,8 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "host_enqueue_ms_per_step": round(1000 * host_s / args.steps, 3),
+        "host_enqueue_split_ms": {"front_end": round(1000 * host_split[0] / args.steps, 3),
+                                  "keyframe_path": round(1000 * host_split[1] / args.steps, 3)},
         "config": {"workload": f"{args.config}: stereo frame = ORBextractor x2 ({COLS}x{ROWS}, 8 levels, {NFEAT} kpts) + "
                                "stereo L<->R 256-bit Hamming band match + SAD sub-pixel refinement; every 5th frame a "
                                "keyframe: DBoW2 transform (k=10, L=6) + " + ("RCCL all-gather of KF packets + " if world > 1 else "") +
@@ -403,15 +426,16 @@ def main():
         xs = exchange.stats()
         if xs:
             out["exchange"] = dict(xs, collective="all_gather_into_tensor (RCCL over xGMI)",
-                                   packet_bytes=fusion.store.layout.bytes, keyframes_per_rank=n_kf)
+                                   packet_bytes=engine.packet_bytes, keyframes_per_rank=n_kf)
 
     if rank == 0 and world == 1 and args.host_api_frames > 0:
         out["host_api"] = host_api_rate(pkg, cfg, lefts, rights, args.host_api_frames, dev.index)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(lefts[:16], rights[:16], cfg, S.synthetic_vocabulary(2024, k=10, L=6), n_kf,
                                            args.cpu_seconds)
-    out["fusion_gate_passed_per_step"] = round(int(gate.item()) / (args.steps + args.warmup + STORE_STEPS), 2)
-    fusion.check()
+    gate, _ = engine.stats()
+    out["fusion_gate_passed_per_step"] = round(gate / (args.steps + args.warmup + STORE_STEPS), 2)
+    engine.check()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -472,6 +472,71 @@ int orbx_kfdb_candidate_pairs_device(const int32_t* d_cand, int cand_stride, con
                                      int nq, const int32_t* d_slot_group, const int32_t* d_query_group, int k, int32_t* d_pairs,
                                      void* stream);
 
+
+/* ------------------------------------------------------------------------------------------------
+ * Keyframe fusion — one agent's keyframe path into MapFusion as one native object:
+ * KeyFrame::ComputeBoW, the LoopClosing -> MultiAgentServer::InsertKeyFrame -> MapFusion::InsertKeyFrame hand-off
+ * (src/LoopClosing.cc:83-94, src/MultiAgentServer.cc:78-80, src/MapFusion.cc:83-88), DetectLoopCandidates then
+ * add (src/MapFusion.cc:133, :149 / :222), the same-map discard (:136-144) and SearchByBoW with the 20-match gate
+ * (:275-281).  A keyframe is a fixed-size packet (orbx_packet_layout) in a device ring of 'slots' packets that the
+ * agents' packets are all-gathered into (rank-major: the order MapFusion processes them in); each agent answers
+ * its own keyframes' queries on its replica of the database.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct orbx_fusion orbx_fusion;
+typedef struct orbx_exchange orbx_exchange;
+
+/* Packet byte layout for 'capacity' keypoints: offsets of kps, desc, fv_nodes, fv_offsets, fv_indices, valid,
+ * bow_words, bow_values (8 entries, after a 32-byte header: int32 count, agent, frame, n_fv, n_words) and the
+ * packet size. */
+int orbx_packet_layout(int capacity, size_t* offsets, size_t* bytes);
+
+/* vocab / matcher stay owned by the caller (the matcher's nnratio / checkOri are MapFusion's 0.75 / true); the
+ * fusion owns its KeyFrameDatabase over the ring.  max_keyframes: keyframes per agent per step; slots >=
+ * world * max_keyframes; candidates: SearchByBoW pairs per query (first k other-map candidates). */
+int orbx_fusion_create(orbx_vocab* vocab, orbx_matcher* matcher, int capacity, int slots, int max_keyframes, int candidates,
+                       int levelsup, int min_matches, int agent, int world, int device, orbx_fusion** out);
+int orbx_fusion_destroy(orbx_fusion* f);
+/* Packet size, ring slots, ring base pointer and the ring as an orbx_kf_store (any may be NULL). */
+int orbx_fusion_info(const orbx_fusion* f, size_t* packet_bytes, int* slots, void** d_ring, orbx_kf_store* store);
+/* Phase 1: this agent's n new keyframes are rows first_row + j*row_step of an orbx_extract_batch_device output
+ * (d_kps / d_desc at row*capacity, d_counts[row]); MapPoint-valid = d_valid[row*capacity+i] != 0, else
+ * d_depth[row*capacity+i] > 0 (stereo keypoints get MapPoints, Tracking::CreateNewKeyFrame), else all; frame id of
+ * keyframe j = frame_base + j*frame_step.  BoW + packets.  With world == 1 the packets go straight into the ring;
+ * otherwise into d_send_out (n packets; NULL = an internal buffer), returned in *d_send, which the caller
+ * all-gathers (world*n packets, rank-major) into *d_exchange_dst -- this exchange's ring slots -- or elsewhere and
+ * hands to phase 2 as d_exchanged. */
+int orbx_fusion_pack_device(orbx_fusion* f, const orbx_keypoint* d_kps, const uint8_t* d_desc, const int32_t* d_counts,
+                            const float* d_depth, const uint8_t* d_valid, int capacity, int first_row, int row_step, int n,
+                            long long frame_base, int frame_step, void* d_send_out, void** d_exchange_dst, void** d_send,
+                            void* stream);
+/* Phase 2: (d_exchanged: the gathered packets when they were not gathered into the ring, else NULL) ring slots leave
+ * and rejoin the database in processing order, the sequential DetectLoopCandidates of this agent's keyframes, the
+ * first k other-map candidates as SearchByBoW pairs ((query, -1) padded), the batched SearchByBoW.  Outputs, each
+ * optional (NULL = not returned): d_pairs [n*k][2] slot pairs, d_match12 [n*k][capacity] (KF2 index or -1),
+ * d_nmatches [n*k]. */
+int orbx_fusion_commit_device(orbx_fusion* f, const void* d_exchanged, int32_t* d_pairs, int32_t* d_match12,
+                              int32_t* d_nmatches, void* stream);
+/* Both phases with the all-gather over a native exchange in between (x = NULL for a single agent). */
+int orbx_fusion_step_device(orbx_fusion* f, orbx_exchange* x, const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                            const int32_t* d_counts, const float* d_depth, const uint8_t* d_valid, int capacity, int first_row,
+                            int row_step, int n, long long frame_base, int frame_step, int32_t* d_pairs, int32_t* d_match12,
+                            int32_t* d_nmatches, void* stream);
+/* Host copy of the whole ring (slots x packet bytes; synchronises). */
+int orbx_fusion_read_ring(orbx_fusion* f, uint8_t* host_dst);
+/* Ring slots of the last commit: the new slots [first_slot, first_slot + n_new) and this agent's queries. */
+int orbx_fusion_last_step(const orbx_fusion* f, int* first_slot, int* n_new, int* query_first, int* n_queries);
+/* Synchronises the device; candidates that passed the 20-match gate so far, and the database status word (bit 1:
+ * queries interacted, bit 2: candidate capacity exceeded -- either means the results are not the reference's). */
+int orbx_fusion_stats(orbx_fusion* f, long long* gate_passed, int* status);
+
+/* RCCL communicator for the keyframe all-gather (librccl opened at run time; ncclUniqueId is 128 bytes: rank 0
+ * creates it and the caller distributes it to every rank, e.g. over the process launcher). */
+int orbx_exchange_unique_id(void* id128);
+int orbx_exchange_create(const void* id128, int world, int rank, int device, orbx_exchange** out);
+int orbx_exchange_destroy(orbx_exchange* x);
+/* ncclAllGather of 'bytes' per rank: d_recv receives world * bytes, rank-major. */
+int orbx_exchange_allgather_device(orbx_exchange* x, const void* d_send, size_t bytes, void* d_recv, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

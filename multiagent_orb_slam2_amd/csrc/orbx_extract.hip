@@ -1123,9 +1123,13 @@ struct Extractor {
     uint8_t* d_lvl_r = nullptr;
     int* d_lvl_cnt = nullptr;
     int* d_err = nullptr;
-    // host-API staging
+    // host-API staging: the image is packed into pinned host memory and goes over PCIe as one DMA (a pageable
+    // 2-D copy of an odd-width image falls back to per-row transfers); results come back through pinned memory
     uint8_t* d_in = nullptr;
     size_t in_bytes = 0;
+    uint8_t* h_in = nullptr;
+    uint8_t* h_out = nullptr;      // pinned: count | keypoints | descriptors of one image
+    size_t h_out_bytes = 0;
     orbx_keypoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
     int32_t* d_cnt = nullptr;
@@ -1206,6 +1210,9 @@ void Extractor::free_buffers() {
     F(d_levels); F(d_cells); F(d_tiles); F(d_pyr); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
     F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
     F(d_kps); F(d_desc); F(d_cnt);
+    if (h_in) { (void)hipHostFree(h_in); h_in = nullptr; }
+    if (h_out) { (void)hipHostFree(h_out); h_out = nullptr; }
+    h_out_bytes = 0;
     for (void* p : rtab_mem) (void)hipFree(p);
     rtab_mem.clear();
     rtab.clear();
@@ -1671,8 +1678,12 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     const size_t nb = (size_t)rows * cols;
     if (e->in_bytes < nb) {
         if (e->d_in) (void)hipFree(e->d_in);
+        if (e->h_in) (void)hipHostFree(e->h_in);
         e->d_in = nullptr;
+        e->h_in = nullptr;
+        e->in_bytes = 0;
         if ((st = dev_alloc(&e->d_in, nb))) return st;
+        ORBX_HIP(hipHostMalloc((void**)&e->h_in, nb, hipHostMallocDefault));
         e->in_bytes = nb;
     }
     if (!e->d_kps) {
@@ -1680,13 +1691,34 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
         if ((st = dev_alloc(&e->d_desc, (size_t)e->out_capacity * 32))) return st;
         if ((st = dev_alloc(&e->d_cnt, 1))) return st;
     }
-    ORBX_HIP(hipMemcpy2DAsync(e->d_in, cols, image, step, cols, rows, hipMemcpyHostToDevice, e->stream));
+    const size_t ob = 64 + (size_t)e->out_capacity * (sizeof(orbx_keypoint) + 32);
+    if (e->h_out_bytes < ob) {
+        if (e->h_out) (void)hipHostFree(e->h_out);
+        e->h_out = nullptr;
+        e->h_out_bytes = 0;
+        ORBX_HIP(hipHostMalloc((void**)&e->h_out, ob, hipHostMallocDefault));
+        e->h_out_bytes = ob;
+    }
+    // the previous call's transfers out of h_in / h_out completed before it returned (stream synchronised)
+    if (step == (size_t)cols) {
+        std::memcpy(e->h_in, image, nb);
+    } else {
+        for (int r = 0; r < rows; ++r) std::memcpy(e->h_in + (size_t)r * cols, image + (size_t)r * step, (size_t)cols);
+    }
+    ORBX_HIP(hipMemcpyAsync(e->d_in, e->h_in, nb, hipMemcpyHostToDevice, e->stream));
     st = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, e->stream);
     if (st) return st;
-    int n = 0, err = 0;
-    ORBX_HIP(hipMemcpyAsync(&n, e->d_cnt, sizeof(int), hipMemcpyDeviceToHost, e->stream));
-    ORBX_HIP(hipMemcpyAsync(&err, e->d_err, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    int32_t* h_cnt = (int32_t*)e->h_out;
+    orbx_keypoint* h_kps = (orbx_keypoint*)(e->h_out + 64);
+    uint8_t* h_desc = e->h_out + 64 + (size_t)e->out_capacity * sizeof(orbx_keypoint);
+    ORBX_HIP(hipMemcpyAsync(h_cnt, e->d_cnt, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    ORBX_HIP(hipMemcpyAsync(h_cnt + 1, e->d_err, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    // keypoints and descriptors of the whole capacity in the same round trip (a count-sized copy would need a
+    // second synchronisation); only the first n are read
+    ORBX_HIP(hipMemcpyAsync(h_kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)e->out_capacity, hipMemcpyDeviceToHost, e->stream));
+    ORBX_HIP(hipMemcpyAsync(h_desc, e->d_desc, (size_t)e->out_capacity * 32, hipMemcpyDeviceToHost, e->stream));
     ORBX_HIP(hipStreamSynchronize(e->stream));
+    const int n = h_cnt[0], err = h_cnt[1];
     ORBX_REQUIRE(err == 0, ORBX_ERR_UNSUPPORTED, "quadtree node capacity exceeded (err=%d)", err);
     *n_out = n;
     if (n > capacity) {
@@ -1695,9 +1727,8 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     }
     if (n > 0) {
         ORBX_REQUIRE(kps && desc, ORBX_ERR_ARG, "null output buffers");
-        ORBX_HIP(hipMemcpyAsync(kps, e->d_kps, sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, e->stream));
-        ORBX_HIP(hipMemcpyAsync(desc, e->d_desc, (size_t)n * 32, hipMemcpyDeviceToHost, e->stream));
-        ORBX_HIP(hipStreamSynchronize(e->stream));
+        std::memcpy(kps, h_kps, sizeof(orbx_keypoint) * (size_t)n);
+        std::memcpy(desc, h_desc, (size_t)n * 32);
     }
     return ORBX_OK;
 }

@@ -206,6 +206,22 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_kfdb_detect_device.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp]
     lib.orbx_kfdb_detect_sequential.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, vp, i32]
     lib.orbx_kfdb_detect_sequential_device.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp]
+    ll = C.c_longlong
+    lib.orbx_packet_layout.argtypes = [i32, vp, C.POINTER(C.c_size_t)]
+    lib.orbx_fusion_create.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp)]
+    lib.orbx_fusion_destroy.argtypes = [vp]
+    lib.orbx_fusion_info.argtypes = [vp, C.POINTER(C.c_size_t), C.POINTER(i32), C.POINTER(vp), C.POINTER(KfStore)]
+    lib.orbx_fusion_pack_device.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, ll, i32, vp, C.POINTER(vp),
+                                            C.POINTER(vp), vp]
+    lib.orbx_fusion_commit_device.argtypes = [vp, vp, vp, vp, vp, vp]
+    lib.orbx_fusion_step_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, ll, i32, vp, vp, vp, vp]
+    lib.orbx_fusion_last_step.argtypes = [vp] + [C.POINTER(i32)] * 4
+    lib.orbx_fusion_stats.argtypes = [vp, C.POINTER(ll), C.POINTER(i32)]
+    lib.orbx_fusion_read_ring.argtypes = [vp, vp]
+    lib.orbx_exchange_unique_id.argtypes = [vp]
+    lib.orbx_exchange_create.argtypes = [vp, i32, i32, i32, C.POINTER(vp)]
+    lib.orbx_exchange_destroy.argtypes = [vp]
+    lib.orbx_exchange_allgather_device.argtypes = [vp, vp, C.c_size_t, vp, vp]
     _lib = lib
     return lib
 
@@ -927,3 +943,155 @@ class KeyFrameDatabase:
 
     def DetectRelocalizationCandidates(self, slot: int, query_id: int):
         return self.detect(KFDB_RELOC, [slot], [query_id])[0]
+
+
+PACKET_FIELDS = ("kps", "desc", "fv_nodes", "fv_offsets", "fv_indices", "valid", "bow_words", "bow_values")
+
+
+def packet_layout(capacity: int):
+    """orbx_packet_layout: {field: byte offset}, packet bytes."""
+    off = (C.c_size_t * 8)()
+    nb = C.c_size_t()
+    _check(load_library().orbx_packet_layout(capacity, off, C.byref(nb)))
+    return dict(zip(PACKET_FIELDS, list(off))), nb.value
+
+
+def _stream_ptr(stream, device):
+    import torch
+    return C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(device).cuda_stream)
+
+
+class KeyframeExchangeRCCL:
+    """orbx_exchange: the keyframe all-gather through a native RCCL communicator (liborbx dlopens librccl).
+    unique_id() on one rank, distributed by the caller (e.g. torch.distributed.broadcast_object_list)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        _check(load_library().orbx_exchange_unique_id(buf))
+        return buf.raw
+
+    def __init__(self, uid: bytes, world: int, rank: int, device: int = 0):
+        self._lib = load_library()
+        self._h = C.c_void_p()
+        b = C.create_string_buffer(bytes(uid), 128)
+        _check(self._lib.orbx_exchange_create(b, world, rank, device, C.byref(self._h)))
+        self.world, self.rank, self.device = world, rank, device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.orbx_exchange_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def allgather(self, send, recv, stream=None):
+        """send (n, P) uint8 device tensor -> recv (world*n, P), rank-major."""
+        _check(self._lib.orbx_exchange_allgather_device(self._h, _tp(send), send.numel(), _tp(recv),
+                                                        _stream_ptr(stream, send.device)))
+        return recv
+
+
+class KeyframeFusionEngine:
+    """orbx_fusion: one agent's keyframe path into MapFusion in native code (include/orbx.h, "Keyframe fusion") --
+    BoW, packets, the exchange into the ring, the sequential DetectLoopCandidates, the other-map candidate pairs
+    and the batched SearchByBoW (src/MapFusion.cc:83-88, :133-149, :275-281).  vocab / matcher are kept alive
+    here; the matcher is MapFusion's ORBmatcher(0.75, true)."""
+
+    def __init__(self, vocab: "ORBVocabulary", matcher: ORBmatcher, capacity: int, slots: int, max_keyframes: int,
+                 candidates: int = 16, levelsup: int = 4, min_matches: int = 20, agent: int = 0, world: int = 1,
+                 device: int = 0):
+        self._lib = load_library()
+        self.vocab, self.matcher = vocab, matcher
+        self._h = C.c_void_p()
+        _check(self._lib.orbx_fusion_create(vocab._h, matcher._h, capacity, slots, max_keyframes, candidates, levelsup,
+                                            min_matches, agent, world, device, C.byref(self._h)))
+        self.capacity, self.slots, self.k, self.agent, self.world, self.device = capacity, slots, candidates, agent, world, device
+        pb, ns, ring, st = C.c_size_t(), C.c_int(), C.c_void_p(), KfStore()
+        _check(self._lib.orbx_fusion_info(self._h, C.byref(pb), C.byref(ns), C.byref(ring), C.byref(st)))
+        self.packet_bytes = pb.value
+        self.store = st
+        self._pending = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.orbx_fusion_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _src(self, kps, desc, counts, depth, valid):
+        return (_tp(kps), _tp(desc), _tp(counts), None if depth is None else _tp(depth), None if valid is None else _tp(valid))
+
+    def pack(self, kps, desc, counts, rows: range, frame_base: int, frame_step: int = 1, depth=None, valid=None, send=None,
+             stream=None):
+        """Phase 1 over extractor batch rows rows.start + j*rows.step (kps (B, cap, 28), desc (B, cap, 32), counts (B,)
+        device tensors; depth / valid (B, cap)).  send: (n, P) uint8 tensor for the packets when world > 1."""
+        n = len(rows)
+        dst, snd = C.c_void_p(), C.c_void_p()
+        _check(self._lib.orbx_fusion_pack_device(self._h, *self._src(kps, desc, counts, depth, valid), kps.shape[1],
+                                                 rows.start, rows.step, n, frame_base, frame_step,
+                                                 None if send is None else _tp(send), C.byref(dst), C.byref(snd),
+                                                 _stream_ptr(stream, kps.device)))
+        self._pending = n
+        return n
+
+    def commit(self, exchanged=None, outputs=None, stream=None):
+        """Phase 2.  exchanged: (world*n, P) uint8 tensor of the gathered packets (world > 1).  outputs: optional
+        (pairs (n*k, 2), match12 (n*k, cap), nmatches (n*k,)) int32 tensors to fill."""
+        o = outputs or (None, None, None)
+        dev = exchanged.device if exchanged is not None else (o[0].device if o[0] is not None else None)
+        _check(self._lib.orbx_fusion_commit_device(self._h, None if exchanged is None else _tp(exchanged),
+                                                   *[None if t is None else _tp(t) for t in o],
+                                                   _stream_ptr(stream, dev if dev is not None else self.device)))
+        return outputs
+
+    def step(self, kps, desc, counts, rows: range, frame_base: int, frame_step: int = 1, depth=None, valid=None,
+             exchange: "KeyframeExchangeRCCL" = None, outputs=None, stream=None):
+        """Both phases (native exchange in between when world > 1)."""
+        o = outputs or (None, None, None)
+        _check(self._lib.orbx_fusion_step_device(self._h, None if exchange is None else exchange._h,
+                                                 *self._src(kps, desc, counts, depth, valid), kps.shape[1], rows.start,
+                                                 rows.step, len(rows), frame_base, frame_step,
+                                                 *[None if t is None else _tp(t) for t in o],
+                                                 _stream_ptr(stream, kps.device)))
+        return outputs
+
+    def new_outputs(self, n: int):
+        import torch
+        dev = torch.device("cuda", self.device)
+        return (torch.empty((n * self.k, 2), dtype=torch.int32, device=dev),
+                torch.empty((n * self.k, self.capacity), dtype=torch.int32, device=dev),
+                torch.empty((n * self.k,), dtype=torch.int32, device=dev))
+
+    def last_step(self):
+        v = [C.c_int() for _ in range(4)]
+        _check(self._lib.orbx_fusion_last_step(self._h, *[C.byref(x) for x in v]))
+        first, n_new, qfirst, nq = (x.value for x in v)
+        return range(first, first + n_new), range(qfirst, qfirst + nq)
+
+    def stats(self):
+        """(keyframe candidates that passed the 20-match gate so far, database status word); synchronises."""
+        g, st = C.c_longlong(), C.c_int()
+        _check(self._lib.orbx_fusion_stats(self._h, C.byref(g), C.byref(st)))
+        return g.value, st.value
+
+    def check(self):
+        _, st = self.stats()
+        if st & 1:
+            raise OrbxError(ORBX_ERR_ARG, "KeyFrameDatabase batch queries interacted through the scratch fields")
+        if st & 2:
+            raise OrbxError(ORBX_ERR_CAPACITY, "KeyFrameDatabase query exceeded its candidate capacity")
+
+    def read_ring(self) -> np.ndarray:
+        out = np.zeros((self.slots, self.packet_bytes), np.uint8)
+        _check(self._lib.orbx_fusion_read_ring(self._h, _p(out)))
+        return out

@@ -70,3 +70,13 @@ def test_header_compiles_as_c():
 def test_keypoint_layout_matches_cv_keypoint():
     assert pkg.KP_DTYPE.itemsize == 28
     assert list(pkg.KP_DTYPE.names) == ["x", "y", "size", "angle", "response", "octave", "class_id"]
+
+
+def test_packet_layout_matches_python():
+    """The native keyframe packet layout (orbx_packet_layout) equals multiagent.PacketLayout byte for byte."""
+    from multiagent_orb_slam2_amd import multiagent as MA
+    from multiagent_orb_slam2_amd.orbx import packet_layout
+    for cap in (1, 64, 320, 1203, 2045, 4096):
+        off, nbytes = packet_layout(cap)
+        lay = MA.PacketLayout(cap)
+        assert nbytes == lay.bytes and off == lay.offsets, cap
