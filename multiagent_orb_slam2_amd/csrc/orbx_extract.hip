@@ -319,6 +319,12 @@ __device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, 
 // Dynamic LDS: E and O pair images (max_rows x kPairStride dwords each) + padded int16 score map whose
 // pixel pairs are dword aligned (det column x at map column x + 2, pad ring at columns 1 and Wd + 2) +
 // survivor list + kept-pixel key lists.
+// Byte offset of the three counters after the dynamic LDS arrays of k_fast_cells (16-byte aligned).
+__host__ __device__ __forceinline__ int fast_counter_off(int R, int Cc) {
+    const int b = 2 * R * kPairStride * 4 + 4 * (((R - 4) * Cc + 1) / 2) + 2 * ((R * Cc / 2 + 65) & ~1) + 2 * 2 * (R * Cc / 4 + 32);
+    return (b + 15) & ~15;
+}
+
 constexpr int kFastPf = 6;        // row groups per wave held in flight (ROI <= 72 rows, chunks <= 19 per row)
 
 struct FastRoi {                  // lane mapping of one cell's ROI: lane -> (row in group, 4-column chunk)
@@ -343,7 +349,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                                                     uint8_t* __restrict__ cand_s, int cand_stride,
                                                     int* __restrict__ cell_cnt, int ncells, int batch, int stop_after,
                                                     Src0 s0, int max_rows, int max_cols) {
-    extern __shared__ uint32_t fsm[];
+    // counters at the tail of the dynamic region (no static __shared__: it would shift the dynamic base off 16-byte
+    // alignment and the ds_write_b64 of the pair images would replay, cdna_hip_programming.md Guideline 17)
+    extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
     uint32_t* E = fsm;
     uint32_t* O = fsm + max_rows * kPairStride;
     int16_t* sc = (int16_t*)(fsm + 2 * max_rows * kPairStride);
@@ -351,7 +359,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     const int kmax = max_rows * max_cols / 4 + 32;           // >= strict-NMS bound ceil(wd/2)*ceil(hd/2)
     uint16_t* kini = list + ((max_rows * max_cols / 2 + 65) & ~1);
     uint16_t* kmin = kini + kmax;
-    __shared__ int nsurv, nki, nkm;
+    int* counters = reinterpret_cast<int*>(fsm) + fast_counter_off(max_rows, max_cols) / 4;
+    int& nsurv = counters[0];
+    int& nki = counters[1];
+    int& nkm = counters[2];
     const int tid = threadIdx.x, w = tid >> 6, ln = lane_id();
     const int item = xcd_item(xcd_chunk(ncells * batch));    // (image, cell), cells of one image adjacent
     if (item >= ncells * batch) return;                       // whole workgroup: no barrier is split
@@ -602,6 +613,7 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t* __restrict__ pyr, 
 #undef ORBX_HROW
 }
 
+
 // ---------------------------------------------------------------------------------------------
 // Quadtree: DistributeOctTree (:539-763) as data-parallel passes.
 //
@@ -659,7 +671,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                                                          QtScratch qs, uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r,
                                                          int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
                                                          int scan_cap, int* __restrict__ err) {
-    extern __shared__ int smem[];
+    extern __shared__ __attribute__((aligned(16))) int smem[];
     const int lvl = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
     const LevelDev L = levels[lvl];
     // LDS layout
@@ -1087,7 +1099,7 @@ struct Extractor {
     // (level, image)): fork after k_fast_cells (or after the pyramid, ORBX_BLUR_FORK=0), join before k_describe
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int blur_fork = 1;
+    int blur_fork = 1;        // ORBX_BLUR_FORK: 1 after FAST, 0 after the pyramid, -1 on the launch stream (serial)
 
     // geometry for the reserved size
     int rows = 0, cols = 0, max_batch = 0;
@@ -1101,6 +1113,7 @@ struct Extractor {
     int cell_max_rows = 0, cell_max_cols = 0;
     int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
+    size_t qt_lds = 0;        // k_quadtree dynamic LDS bytes
     int out_capacity = 0;     // max keypoints per image
     int fast_resident = 0;    // k_fast_cells workgroups resident on the whole device (persistent grid)
 
@@ -1222,11 +1235,10 @@ void Extractor::free_buffers() {
 }
 
 static size_t qt_lds_bytes(int cap, int scan_cap);
+
 static size_t fast_lds_bytes(const Extractor* e) {
-    // E + O pair images, int16 score map, u16 survivor list and two u16 kept-pixel key lists
-    const size_t R = e->cell_max_rows, Cc = e->cell_max_cols;
-    return 2 * R * kPairStride * 4 + 4 * (((R - 4) * Cc + 1) / 2) + 2 * ((R * Cc / 2 + 65) & ~(size_t)1) +
-           2 * 2 * (R * Cc / 4 + 32);
+    // E + O pair images, int16 score map, u16 survivor list, two u16 kept-pixel key lists, 3 counters
+    return (size_t)fast_counter_off(e->cell_max_rows, e->cell_max_cols) + 16;
 }
 
 template <typename T>
@@ -1322,6 +1334,7 @@ int Extractor::configure(int r, int c, int batch) {
     {
         const size_t lds = qt_lds_bytes(cap, scan_cap);
         ORBX_REQUIRE(lds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "quadtree LDS %zu B exceeds 160 KiB", lds);
+        qt_lds = lds;
         if (lds > 64 * 1024)
             ORBX_HIP(hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     }
@@ -1451,6 +1464,7 @@ static size_t qt_lds_bytes(int cap, int scan_cap) {
     return ints * 4 + (size_t)p2 * 8;
 }
 
+
 static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t step, size_t istride,
                      orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int capacity, hipStream_t s) {
     const int nl = e->nlevels;
@@ -1466,14 +1480,17 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     e->last_src0 = s0;
     auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], k >= 6 ? e->side : s); };
     auto launch_blur = [&]() -> int {
-        ORBX_HIP(hipEventRecord(e->ev_fork, s));
-        ORBX_HIP(hipStreamWaitEvent(e->side, e->ev_fork, 0));
-        mark(6);
+        hipStream_t bs = e->blur_fork < 0 ? s : e->side;
+        if (bs != s) {
+            ORBX_HIP(hipEventRecord(e->ev_fork, s));
+            ORBX_HIP(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+        }
+        if (es) (void)hipEventRecord(es->ev[6], bs);
         const int nt = (int)e->tilev.size();
         dim3 g(kXcds * xcd_chunk((nt + 3) / 4 * batch));
-        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, e->side, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles, nt, batch, s0);
-        mark(7);
-        ORBX_HIP(hipEventRecord(e->ev_join, e->side));
+        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, bs, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles, nt, batch, s0);
+        if (es) (void)hipEventRecord(es->ev[7], bs);
+        ORBX_HIP(hipEventRecord(e->ev_join, bs));
         return ORBX_OK;
     };
     mark(0);
@@ -1506,9 +1523,9 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     {
         QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
         dim3 g(nl, batch);
-        hipLaunchKernelGGL(k_quadtree, g, dim3(kQtThreads), qt_lds_bytes(e->node_cap, e->scan_cap), s, e->d_levels, e->d_cells,
-                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
-                           e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err);
+        hipLaunchKernelGGL(k_quadtree, g, dim3(kQtThreads), e->qt_lds, s, e->d_levels, e->d_cells, e->d_cand_xy, e->d_cand_s,
+                           e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy, e->d_lvl_r, e->out_stride,
+                           e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err);
     }
     mark(3);
     ORBX_HIP(hipStreamWaitEvent(s, e->ev_join, 0));

@@ -91,7 +91,7 @@ def test_gpu_distinctive_over_keyframe_store(gpu):
     M = 150
     obs, lists = [], []
     for p in range(M):
-        n = int(rng.integers(0, 14))
+        n = int(rng.integers(0, slots + 1))
         ks = rng.choice(slots, n, replace=False)
         idx = p % cap
         base = desc[ks[0], idx] if n else None
