@@ -66,6 +66,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage event timing")
+    ap.add_argument("--no-c3", dest="c3", action="store_false", help="skip the C3 2000x2000 all-pairs block")
     return ap.parse_args()
 
 
@@ -203,6 +204,40 @@ def host_api_rate(pkg, cfg, lefts, rights, n_frames, device):
     return {"frames_per_s": round(1e3 / float(np.mean(lat_ms)), 1), "latency_ms_median": round(float(np.median(lat_ms)), 3),
             "latency_ms_p95": round(float(np.percentile(lat_ms, 95)), 3), "frames": len(lat),
             "path": "orbx_extract(L) + orbx_extract(R) + orbx_compute_stereo_matches, host buffers, one frame per call"}
+
+
+def c3_bench(pkg, dev, n_problems=64, reps=30):
+    """BASELINE config C3: brute-force 256-bit Hamming match of 2000 x 2000 descriptors (pair-index exact in the
+    tests).  The reference has no unconstrained all-pairs matcher; its best/second loop is ORBmatcher.cc:568-598 and
+    the stereo search of Frame.cc:528-548 without the band.  Timed with HIP events on the launch stream: one match per
+    launch (latency) and n_problems matches per launch (throughput, e.g. every stereo pair of a bench step)."""
+    import torch
+    from multiagent_orb_slam2_amd import synthetic as S
+    m = pkg.ORBmatcher(0.6, True, device=dev.index)
+    qs, ts = zip(*[S.planted_pairs(7 + z, 2000, 2000) for z in range(8)])
+    q1, t1 = torch.from_numpy(qs[0]).to(dev), torch.from_numpy(ts[0]).to(dev)
+    qb = torch.from_numpy(np.stack([qs[z % 8] for z in range(n_problems)])).to(dev)
+    tb = torch.from_numpy(np.stack([ts[z % 8] for z in range(n_problems)])).to(dev)
+    s = torch.cuda.current_stream(dev)
+    out = {}
+    for name, fn, nprob in (("single", lambda: m.bf_match_device(q1, t1, stream=s), 1),
+                            ("batched", lambda: m.bf_match_batch_device(qb, tb, stream=s), n_problems)):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        pairs = 2000 * 2000 * nprob
+        alg = 144000 * nprob                       # SURVEY §8(d): 2 x 2000 x 32 B in + 2000 x 8 B out per match
+        out[name] = {"problems": nprob, "us_per_launch": round(us, 2), "matches_per_s": round(nprob / (us * 1e-6), 1),
+                     "pair_distances_per_s": round(pairs / (us * 1e-6), 1),
+                     "algorithmic_GBps": round(alg / (us * 1e-6) / 1e9, 2)}
+    out["kernels"] = "k_bf_tile (256 queries per workgroup, one per lane, train rows staged in LDS) + k_bf_merge"
+    return out
 
 
 def load_profile(name):
@@ -430,6 +465,8 @@ def main():
             out["exchange"] = dict(xs, collective="all_gather_into_tensor (RCCL over xGMI)",
                                    packet_bytes=engine.packet_bytes, keyframes_per_rank=n_kf)
 
+    if rank == 0 and world == 1 and args.c3:
+        out["c3_bruteforce"] = c3_bench(pkg, dev)
     if rank == 0 and world == 1 and args.host_api_frames > 0:
         out["host_api"] = host_api_rate(pkg, cfg, lefts, rights, args.host_api_frames, dev.index)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -154,6 +154,13 @@ int orbx_bf_match(orbx_matcher* m, const uint8_t* query, int nq, const uint8_t* 
                   int32_t* best_idx, int32_t* best_dist, int32_t* second_dist);
 int orbx_bf_match_device(orbx_matcher* m, const uint8_t* d_query, int nq, const uint8_t* d_train, int nt,
                          int32_t* d_best_idx, int32_t* d_best_dist, int32_t* d_second_dist, void* stream);
+/* n_problems independent all-pairs matches in one launch (e.g. the L x R descriptor sets of a batch of stereo pairs,
+ * or a query keyframe against many candidates): problem z reads nq queries at d_query + z*query_stride and nt train
+ * rows at d_train + z*train_stride (bytes, multiples of 16) and writes outputs at z*nq.  nt = 0: every query gets
+ * (-1, 256, 256). */
+int orbx_bf_match_batch_device(orbx_matcher* m, const uint8_t* d_query, int nq, size_t query_stride, const uint8_t* d_train,
+                               int nt, size_t train_stride, int n_problems, int32_t* d_best_idx, int32_t* d_best_dist,
+                               int32_t* d_second_dist, void* stream);
 
 /* Stereo L<->R descriptor search of Frame::ComputeStereoMatches (src/Frame.cc:466-552): for each left
  * keypoint, the right keypoint in the row band of (int)vL (+-2*scale[octave] rows), octave within +-1

@@ -49,12 +49,16 @@ __global__ __launch_bounds__(256) void k_hamming_pairs(const uint8_t* __restrict
 constexpr int kBfQ = 256;      // queries per workgroup (4 waves, one query per lane)
 constexpr int kBfStage = 256;  // train rows staged in LDS per step (8 KB)
 
-// partial record: best (dist << 20 | train idx), second dist
-__global__ __launch_bounds__(256) void k_bf_tile(const uint8_t* __restrict__ q, int nq, const uint8_t* __restrict__ t, int nt,
-                                                 int chunk, uint32_t* __restrict__ pbest, int32_t* __restrict__ psecond) {
+// partial record: best (dist << 20 | train idx), second dist.  blockIdx.z = problem: query set z at q + z*q_stride,
+// train set z at t + z*t_stride (bytes), partials at z * nchunks * nq.
+__global__ __launch_bounds__(256) void k_bf_tile(const uint8_t* __restrict__ q, int nq, size_t q_stride, const uint8_t* __restrict__ t,
+                                                 int nt, size_t t_stride, int chunk, uint32_t* __restrict__ pbest,
+                                                 int32_t* __restrict__ psecond) {
     __shared__ uint4 tile[kBfStage * 2];
     const int qi = blockIdx.x * kBfQ + threadIdx.x;
-    const int c = blockIdx.y;
+    const int c = blockIdx.y, z = blockIdx.z, nch = gridDim.y;
+    q += (size_t)z * q_stride;
+    t += (size_t)z * t_stride;
     const int t0 = c * chunk, t1 = min(nt, t0 + chunk);
     uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
     if (qi < nq) load_desc(q + 32 * (size_t)qi, a0, a1);
@@ -81,16 +85,19 @@ __global__ __launch_bounds__(256) void k_bf_tile(const uint8_t* __restrict__ q, 
         }
     }
     if (qi < nq) {
-        pbest[(size_t)c * nq + qi] = best;
-        psecond[(size_t)c * nq + qi] = second;
+        const size_t o = ((size_t)z * nch + c) * nq + qi;
+        pbest[o] = best;
+        psecond[o] = second;
     }
 }
 
 __global__ __launch_bounds__(256) void k_bf_merge(const uint32_t* __restrict__ pbest, const int32_t* __restrict__ psecond,
                                                   int nq, int nchunks, int32_t* __restrict__ best_idx,
                                                   int32_t* __restrict__ best_dist, int32_t* __restrict__ second_dist) {
-    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+    const int qi = blockIdx.x * blockDim.x + threadIdx.x, z = blockIdx.y;
     if (qi >= nq) return;
+    pbest += (size_t)z * nchunks * nq;
+    psecond += (size_t)z * nchunks * nq;
     uint32_t best = 256u << 20;
     int second = 256;
     for (int c = 0; c < nchunks; ++c) {   // chunks in ascending train order: same rule as a sequential scan
@@ -106,9 +113,20 @@ __global__ __launch_bounds__(256) void k_bf_merge(const uint32_t* __restrict__ p
         }
     }
     const int bd = (int)(best >> 20);
-    best_dist[qi] = bd;
-    best_idx[qi] = bd < 256 ? (int)(best & 0xfffff) : -1;
-    second_dist[qi] = second;
+    const size_t o = (size_t)z * nq + qi;
+    best_dist[o] = bd;
+    best_idx[o] = bd < 256 ? (int)(best & 0xfffff) : -1;
+    second_dist[o] = second;
+}
+
+// No train rows: every query keeps the reference's initial state (no match, distances 256).
+__global__ __launch_bounds__(256) void k_bf_empty(int n, int32_t* __restrict__ best_idx, int32_t* __restrict__ best_dist,
+                                                  int32_t* __restrict__ second_dist) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    best_idx[i] = -1;
+    best_dist[i] = 256;
+    second_dist[i] = 256;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -773,24 +791,36 @@ struct Bump {
 };
 static size_t a256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-static int bf_launch(Matcher* m, const uint8_t* dq, int nq, const uint8_t* dt, int nt, int32_t* bi, int32_t* bd, int32_t* sd,
-                     hipStream_t s, void* scratch) {
-    // chunk the train set so that the grid fills the chip (>= ~1024 workgroups when possible)
+// Grid: 256 queries per workgroup x train chunks x problems.  The train set of a problem is split into chunks so that
+// the whole launch has >= ~2048 workgroups when the problems are few (a single 2000 x 2000 match is 8 query blocks:
+// 64 chunks of 32 rows fill the chip; at many problems one chunk per problem suffices).
+static int bf_chunks(int nq, int nt, int nprob) {
     const int qb = (nq + kBfQ - 1) / kBfQ;
-    int nch = std::max(1, std::min((nt + kBfStage - 1) / kBfStage, (2048 + qb - 1) / qb));
+    const int want = (2048 + qb * nprob - 1) / (qb * nprob);
+    return std::max(1, std::min(want, (nt + 31) / 32));
+}
+static size_t bf_scratch(int nq, int nt, int nprob) {
+    const int nch = bf_chunks(nq, nt, nprob);
+    return 2 * a256((size_t)nch * nq * nprob * 4) + 256;
+}
+static int bf_launch(Matcher* m, const uint8_t* dq, int nq, size_t qs, const uint8_t* dt, int nt, size_t ts, int nprob, int32_t* bi,
+                     int32_t* bd, int32_t* sd, hipStream_t s, void* scratch) {
+    (void)m;
+    if (nt == 0) {
+        hipLaunchKernelGGL(k_bf_empty, dim3(((size_t)nq * nprob + 255) / 256), dim3(256), 0, s, nq * nprob, bi, bd, sd);
+        ORBX_HIP(hipGetLastError());
+        return ORBX_OK;
+    }
+    const int qb = (nq + kBfQ - 1) / kBfQ;
+    int nch = bf_chunks(nq, nt, nprob);
     const int chunk = (nt + nch - 1) / nch;
     nch = (nt + chunk - 1) / chunk;
     uint32_t* pb = (uint32_t*)scratch;
-    int32_t* ps = (int32_t*)((uint8_t*)scratch + a256((size_t)nch * nq * 4));
-    hipLaunchKernelGGL(k_bf_tile, dim3(qb, nch), dim3(256), 0, s, dq, nq, dt, nt, chunk, pb, ps);
-    hipLaunchKernelGGL(k_bf_merge, dim3((nq + 255) / 256), dim3(256), 0, s, pb, ps, nq, nch, bi, bd, sd);
+    int32_t* ps = (int32_t*)((uint8_t*)scratch + a256((size_t)nch * nq * nprob * 4));
+    hipLaunchKernelGGL(k_bf_tile, dim3(qb, nch, nprob), dim3(256), 0, s, dq, nq, qs, dt, nt, ts, chunk, pb, ps);
+    hipLaunchKernelGGL(k_bf_merge, dim3((nq + 255) / 256, nprob), dim3(256), 0, s, pb, ps, nq, nch, bi, bd, sd);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
-}
-static size_t bf_scratch(int nq, int nt) {
-    const int qb = (nq + kBfQ - 1) / kBfQ;
-    int nch = std::max(1, std::min((nt + kBfStage - 1) / kBfStage, (2048 + qb - 1) / qb));
-    return 2 * a256((size_t)nch * nq * 4) + 256;
 }
 
 }  // namespace orbx
@@ -856,23 +886,23 @@ int orbx_descriptor_distance_device(orbx_matcher* m, const uint8_t* a, const uin
 
 int orbx_bf_match_device(orbx_matcher* m, const uint8_t* dq, int nq, const uint8_t* dt, int nt, int32_t* bi, int32_t* bd,
                          int32_t* sd, void* stream) {
-    ORBX_REQUIRE(m && nq >= 0 && nt >= 0, ORBX_ERR_ARG, "bad argument");
+    return orbx_bf_match_batch_device(m, dq, nq, 0, dt, nt, 0, 1, bi, bd, sd, stream);
+}
+
+int orbx_bf_match_batch_device(orbx_matcher* m, const uint8_t* dq, int nq, size_t query_stride, const uint8_t* dt, int nt,
+                               size_t train_stride, int n_problems, int32_t* bi, int32_t* bd, int32_t* sd, void* stream) {
+    ORBX_REQUIRE(m && nq >= 0 && nt >= 0 && n_problems >= 0, ORBX_ERR_ARG, "bad argument");
     ORBX_REQUIRE(nt < (1 << 20), ORBX_ERR_UNSUPPORTED, "train set too large (%d)", nt);
-    if (nq == 0) return ORBX_OK;
+    ORBX_REQUIRE(n_problems <= 65535, ORBX_ERR_UNSUPPORTED, "too many problems (%d)", n_problems);
+    if (nq == 0 || n_problems == 0) return ORBX_OK;
     ORBX_REQUIRE(dq && bi && bd && sd && (nt == 0 || dt), ORBX_ERR_ARG, "null pointer");
+    ORBX_REQUIRE(n_problems == 1 || ((query_stride % 16) == 0 && (train_stride % 16) == 0), ORBX_ERR_ARG,
+                 "problem strides must be multiples of 16 bytes");
     ORBX_HIP(hipSetDevice(m->device));
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
-    int st = m->reserve_on(bf_scratch(nq, std::max(nt, 1)), s);
+    int st = m->reserve_on(bf_scratch(nq, std::max(nt, 1), n_problems), s);
     if (st) return st;
-    if (nt == 0) {
-        std::vector<int32_t> neg(nq, -1), d256(nq, 256);
-        ORBX_HIP(hipMemcpyAsync(bi, neg.data(), 4 * (size_t)nq, hipMemcpyHostToDevice, s));
-        ORBX_HIP(hipMemcpyAsync(bd, d256.data(), 4 * (size_t)nq, hipMemcpyHostToDevice, s));
-        ORBX_HIP(hipMemcpyAsync(sd, d256.data(), 4 * (size_t)nq, hipMemcpyHostToDevice, s));
-        ORBX_HIP(hipStreamSynchronize(s));
-        return ORBX_OK;
-    }
-    return bf_launch(m, dq, nq, dt, nt, bi, bd, sd, s, m->scratch);
+    return bf_launch(m, dq, nq, query_stride, dt, nt, train_stride, n_problems, bi, bd, sd, s, m->scratch);
 }
 
 int orbx_bf_match(orbx_matcher* m, const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* bi, int32_t* bd, int32_t* sd) {
@@ -882,7 +912,7 @@ int orbx_bf_match(orbx_matcher* m, const uint8_t* q, int nq, const uint8_t* t, i
     ORBX_REQUIRE(nt < (1 << 20), ORBX_ERR_UNSUPPORTED, "train set too large (%d)", nt);
     ORBX_HIP(hipSetDevice(m->device));
     const size_t io = a256((size_t)nq * 32) + a256((size_t)std::max(nt, 1) * 32) + 3 * a256((size_t)nq * 4);
-    int st = m->reserve(io + bf_scratch(nq, std::max(nt, 1)));
+    int st = m->reserve(io + bf_scratch(nq, std::max(nt, 1), 1));
     if (st) return st;
     Bump bp{(uint8_t*)m->scratch};
     uint8_t* dq = bp.take<uint8_t>((size_t)nq * 32);
@@ -894,7 +924,7 @@ int orbx_bf_match(orbx_matcher* m, const uint8_t* q, int nq, const uint8_t* t, i
     ORBX_HIP(hipMemcpyAsync(dq, q, (size_t)nq * 32, hipMemcpyHostToDevice, s));
     if (nt > 0) {
         ORBX_HIP(hipMemcpyAsync(dt, t, (size_t)nt * 32, hipMemcpyHostToDevice, s));
-        st = bf_launch(m, dq, nq, dt, nt, dbi, dbd, dsd, s, (uint8_t*)m->scratch + bp.off);
+        st = bf_launch(m, dq, nq, 0, dt, nt, 0, 1, dbi, dbd, dsd, s, (uint8_t*)m->scratch + bp.off);
         if (st) return st;
         ORBX_HIP(hipMemcpyAsync(bi, dbi, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
         ORBX_HIP(hipMemcpyAsync(bd, dbd, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));

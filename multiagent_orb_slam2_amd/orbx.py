@@ -159,6 +159,7 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_descriptor_distance_device.argtypes = [vp, vp, vp, i32, vp, vp]
     lib.orbx_bf_match.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp]
     lib.orbx_bf_match_device.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, vp]
+    lib.orbx_bf_match_batch_device.argtypes = [vp, vp, i32, C.c_size_t, vp, i32, C.c_size_t, i32, vp, vp, vp, vp]
     lib.orbx_stereo_match.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, i32, i32, f32, f32, vp, vp, C.POINTER(i32)]
     lib.orbx_stereo_match_batch_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, f32, f32, vp,
                                                    vp, vp]
@@ -455,6 +456,19 @@ class ORBmatcher:
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(query.device).cuda_stream)
         _check(self._lib.orbx_bf_match_device(self._h, _tp(query), n, _tp(train), train.shape[0], _tp(bi), _tp(bd),
                                               _tp(sd), s))
+        return bi, bd, sd
+
+    def bf_match_batch_device(self, query, train, stream=None, out=None):
+        """query (P, nq, 32), train (P, nt, 32) uint8 device tensors (rows contiguous within a problem) -> best_idx,
+        best_dist, second_dist (P, nq) int32: P independent all-pairs matches in one launch."""
+        import torch
+        P, nq, nt = query.shape[0], query.shape[1], train.shape[1]
+        assert query.stride(1) == 32 and train.stride(1) == 32 and query.stride(2) == 1 and train.stride(2) == 1
+        bi, bd, sd = out if out is not None else \
+            (torch.empty((P, nq), dtype=torch.int32, device=query.device) for _ in range(3))
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(query.device).cuda_stream)
+        _check(self._lib.orbx_bf_match_batch_device(self._h, _tp(query), nq, query.stride(0), _tp(train), nt, train.stride(0),
+                                                    P, _tp(bi), _tp(bd), _tp(sd), s))
         return bi, bd, sd
 
     def stereo_descriptor_search(self, kps_left, desc_left, kps_right, desc_right, scale_factors, rows, bf, b):

@@ -45,6 +45,28 @@ def test_bf_match_c3(gpu, nq, nt):
         assert np.array_equal(g, r), name
 
 
+@pytest.mark.parametrize("P,nq,nt", [(1, 2000, 2000), (16, 2000, 2000), (5, 300, 17), (3, 64, 0), (70, 33, 1200)])
+def test_bf_match_batch_device(gpu, P, nq, nt):
+    """orbx_bf_match_batch_device: P independent all-pairs problems in one launch, each equal to the oracle's."""
+    import torch
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    qs, ts = [], []
+    for z in range(P):
+        q, t = S.planted_pairs(100 + z, nq, max(nt, 1))
+        qs.append(q)
+        ts.append(t[:nt])
+    dev = torch.device("cuda", 0)
+    qd = torch.from_numpy(np.stack(qs)).to(dev)
+    td = torch.from_numpy(np.stack(ts).reshape(P, nt, 32)).to(dev)
+    bi, bd, sd = pkg.ORBmatcher().bf_match_batch_device(qd, td)
+    bi, bd, sd = bi.cpu().numpy(), bd.cpu().numpy(), sd.cpu().numpy()
+    for z in range(P):
+        ref = O.bf_match(qs[z], ts[z])
+        for g, r, name in zip((bi[z], bd[z], sd[z]), ref, ("best_idx", "best_dist", "second_dist")):
+            assert np.array_equal(g, r), (z, name)
+
+
 def test_bf_match_ties_and_full_distance(gpu):
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
