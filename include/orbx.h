@@ -336,6 +336,20 @@ typedef struct orbx_proj_problem {
     int32_t* q_idx; int32_t* q_dist; int32_t* owner; int32_t* nmatches;
 } orbx_proj_problem;
 
+/* Frame::UndistortKeyPoints (src/Frame.cc:404-434): mvKeysUn = mvKeys with pt replaced by cv::undistortPoints(pt, K,
+ * DistCoef, R = I, P = K), pinned to OpenCV 3.2's cvUndistortPoints (double precision, five fixed iterations; the
+ * oracle restates it).  K: 3x3 row-major float (mK); dist: n_dist = 0, 4, 5, 8 or 12 coefficients (k1 k2 p1 p2 [k3
+ * [k4 k5 k6 [s1..s4]]]); dist[0] == 0 copies the keypoints unchanged (:406-410), as the reference does. */
+int orbx_undistort_keypoints(orbx_matcher* m, const orbx_keypoint* kps, int n, const float* K, const float* dist, int n_dist,
+                             orbx_keypoint* out);
+/* Device form over an extractor batch (keypoints at i*capacity, d_counts[i]); K / dist are host arrays. */
+int orbx_undistort_keypoints_device(orbx_matcher* m, const orbx_keypoint* d_kps, const int32_t* d_counts, int batch, int capacity,
+                                    const float* K, const float* dist, int n_dist, orbx_keypoint* d_out, void* stream);
+/* Frame::ComputeImageBounds (src/Frame.cc:436-464): bounds = {mnMinX, mnMaxX, mnMinY, mnMaxY} of the undistorted image
+ * corners (or the image rectangle when dist[0] == 0). */
+int orbx_compute_image_bounds(orbx_matcher* m, const float* K, const float* dist, int n_dist, int cols, int rows,
+                              float* bounds);
+
 /* Frame::AssignFeaturesToGrid (src/Frame.cc:230-245) for 'batch' keypoint sets laid out like the
  * orbx_extract_batch_device output: cell (ix, iy) -> CSR row ix*rows + iy at d_cell_start + i*(cols*rows+1),
  * keypoint indices ascending inside a cell at d_cell_idx + i*capacity.  capacity <= 8192. */

@@ -380,6 +380,63 @@ __global__ __launch_bounds__(64) void k_proj_init(orbx_proj_params P, orbx_grid 
     if (ln == 0) *pb.nmatches = owners - dropped;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Frame::UndistortKeyPoints (src/Frame.cc:404-434) and ComputeImageBounds (:436-464): cv::undistortPoints(pts,
+// K, DistCoef, R = I, P = K), pinned to OpenCV 3.2's cvUndistortPoints (README.md:68 "Tested with ... OpenCV 3.2"):
+// double precision, normalise with 1/fx, 1/fy, five fixed iterations of
+//   icdist = (1 + ((k7 r2 + k6) r2 + k5) r2) / (1 + ((k4 r2 + k1) r2 + k0) r2)
+//   dx = 2 k2 x y + k3 (r2 + 2 x^2) + k8 r2 + k9 r2^2,   dy = k2 (r2 + 2 y^2) + 2 k3 x y + k10 r2 + k11 r2^2
+//   x = (x0 - dx) icdist,  y = (y0 - dy) icdist
+// then P = K: u = fx x + 0 y + cx, v = 0 x + fy y + cy, w = 1 / (0 x + 0 y + 1).  No FMA (explicit __d*_rn), so the
+// oracle's plain C++ gives the same bits.  Thin-prism / tilt terms (k12, k13) are not supported (ORB-SLAM2 reads at
+// most k1 k2 p1 p2 k3, Tracking.cc).
+// ---------------------------------------------------------------------------------------------
+struct Undist {
+    double fx, fy, cx, cy, ifx, ify, k[12];
+    double r[9];         // RR = P * I = K in double (cvMatMul with the identity is exact)
+};
+
+__device__ __forceinline__ void undistort_point(const Undist& U, float fu, float fv, float& ou, float& ov) {
+    double x = __dmul_rn(__dsub_rn((double)fu, U.cx), U.ifx);
+    double y = __dmul_rn(__dsub_rn((double)fv, U.cy), U.ify);
+    const double x0 = x, y0 = y;
+    const double* k = U.k;
+    for (int j = 0; j < 5; ++j) {
+        const double r2 = __dadd_rn(__dmul_rn(x, x), __dmul_rn(y, y));
+        const double num = __dadd_rn(1.0, __dmul_rn(__dadd_rn(__dmul_rn(__dadd_rn(__dmul_rn(k[7], r2), k[6]), r2), k[5]), r2));
+        const double den = __dadd_rn(1.0, __dmul_rn(__dadd_rn(__dmul_rn(__dadd_rn(__dmul_rn(k[4], r2), k[1]), r2), k[0]), r2));
+        const double icdist = __ddiv_rn(num, den);
+        const double dx = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(__dmul_rn(__dmul_rn(2.0, k[2]), x), y),
+                                                        __dmul_rn(k[3], __dadd_rn(r2, __dmul_rn(__dmul_rn(2.0, x), x)))),
+                                              __dmul_rn(k[8], r2)),
+                                    __dmul_rn(__dmul_rn(k[9], r2), r2));
+        const double dy = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(k[2], __dadd_rn(r2, __dmul_rn(__dmul_rn(2.0, y), y))),
+                                                        __dmul_rn(__dmul_rn(__dmul_rn(2.0, k[3]), x), y)),
+                                              __dmul_rn(k[10], r2)),
+                                    __dmul_rn(__dmul_rn(k[11], r2), r2));
+        x = __dmul_rn(__dsub_rn(x0, dx), icdist);
+        y = __dmul_rn(__dsub_rn(y0, dy), icdist);
+    }
+    const double* R = U.r;
+    const double xx = __dadd_rn(__dadd_rn(__dmul_rn(R[0], x), __dmul_rn(R[1], y)), R[2]);
+    const double yy = __dadd_rn(__dadd_rn(__dmul_rn(R[3], x), __dmul_rn(R[4], y)), R[5]);
+    const double ww = __ddiv_rn(1.0, __dadd_rn(__dadd_rn(__dmul_rn(R[6], x), __dmul_rn(R[7], y)), R[8]));
+    ou = (float)__dmul_rn(xx, ww);
+    ov = (float)__dmul_rn(yy, ww);
+}
+
+// One thread per keypoint of 'batch' sets (extractor batch layout); a zero first coefficient copies (Frame.cc:406-410).
+__global__ __launch_bounds__(256) void k_undistort(Undist U, int copy_only, const orbx_keypoint* __restrict__ kps,
+                                                   const int32_t* __restrict__ counts, int n_fixed, int capacity,
+                                                   orbx_keypoint* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
+    const int n = counts ? counts[b] : n_fixed;
+    if (i >= n || i >= capacity) return;
+    orbx_keypoint kp = kps[(size_t)b * capacity + i];
+    if (!copy_only) undistort_point(U, kp.x, kp.y, kp.x, kp.y);
+    out[(size_t)b * capacity + i] = kp;
+}
+
 }  // namespace orbx
 
 using namespace orbx;
@@ -392,7 +449,84 @@ static int grid_check(const orbx_grid& g) {
     return ORBX_OK;
 }
 
+
+static int make_undist(const float* K, const float* dist, int n_dist, Undist* U, int* copy_only) {
+    ORBX_REQUIRE(K && (n_dist == 0 || dist) && (n_dist == 0 || n_dist == 4 || n_dist == 5 || n_dist == 8 || n_dist == 12),
+                 ORBX_ERR_ARG, "distortion coefficients: 0, 4, 5, 8 or 12 expected (got %d)", n_dist);
+    std::memset(U, 0, sizeof(*U));
+    for (int i = 0; i < n_dist; ++i) U->k[i] = (double)dist[i];
+    U->fx = K[0]; U->fy = K[4]; U->cx = K[2]; U->cy = K[5];
+    ORBX_REQUIRE(U->fx != 0.0 && U->fy != 0.0, ORBX_ERR_ARG, "bad camera matrix");
+    U->ifx = 1.0 / U->fx;
+    U->ify = 1.0 / U->fy;
+    for (int i = 0; i < 9; ++i) U->r[i] = (double)K[i];
+    *copy_only = n_dist == 0 || dist[0] == 0.0f;       // mDistCoef.at<float>(0) == 0.0 (Frame.cc:406)
+    return ORBX_OK;
+}
+
 extern "C" {
+
+int orbx_undistort_keypoints_device(orbx_matcher* m, const orbx_keypoint* d_kps, const int32_t* d_counts, int batch, int capacity,
+                                    const float* K, const float* dist, int n_dist, orbx_keypoint* d_out, void* stream) {
+    ORBX_REQUIRE(m && d_kps && d_counts && d_out && batch >= 0 && capacity > 0, ORBX_ERR_ARG, "bad argument");
+    Undist U;
+    int copy_only = 0;
+    int st = make_undist(K, dist, n_dist, &U, &copy_only);
+    if (st) return st;
+    if (batch == 0) return ORBX_OK;
+    ORBX_REQUIRE(batch <= 65535, ORBX_ERR_UNSUPPORTED, "batch too large");
+    ORBX_HIP(hipSetDevice(matcher_device(m)));
+    hipLaunchKernelGGL(k_undistort, dim3((capacity + 255) / 256, batch), dim3(256), 0, (hipStream_t)stream, U, copy_only, d_kps,
+                       d_counts, 0, capacity, d_out);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_undistort_keypoints(orbx_matcher* m, const orbx_keypoint* kps, int n, const float* K, const float* dist, int n_dist,
+                             orbx_keypoint* out) {
+    ORBX_REQUIRE(m && n >= 0 && (n == 0 || (kps && out)), ORBX_ERR_ARG, "bad argument");
+    Undist U;
+    int copy_only = 0;
+    int st = make_undist(K, dist, n_dist, &U, &copy_only);
+    if (st) return st;
+    if (n == 0) return ORBX_OK;
+    uint8_t* base = nullptr;
+    hipStream_t s = nullptr;
+    const size_t b = a256p(sizeof(orbx_keypoint) * (size_t)n);
+    if ((st = matcher_scratch(m, 2 * b, (void**)&base, (void**)&s))) return st;
+    ORBX_HIP(hipSetDevice(matcher_device(m)));
+    orbx_keypoint* din = (orbx_keypoint*)base;
+    orbx_keypoint* dout = (orbx_keypoint*)(base + b);
+    ORBX_HIP(hipMemcpyAsync(din, kps, sizeof(orbx_keypoint) * (size_t)n, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_undistort, dim3((n + 255) / 256, 1), dim3(256), 0, s, U, copy_only, din, nullptr, n, n, dout);
+    ORBX_HIP(hipGetLastError());
+    ORBX_HIP(hipMemcpyAsync(out, dout, sizeof(orbx_keypoint) * (size_t)n, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
+    return ORBX_OK;
+}
+
+int orbx_compute_image_bounds(orbx_matcher* m, const float* K, const float* dist, int n_dist, int cols, int rows,
+                              float* bounds) {
+    ORBX_REQUIRE(m && bounds && cols > 0 && rows > 0, ORBX_ERR_ARG, "bad argument");
+    Undist U;
+    int copy_only = 0;
+    int st = make_undist(K, dist, n_dist, &U, &copy_only);
+    if (st) return st;
+    if (copy_only) {   // Frame.cc:457-463
+        bounds[0] = 0.0f; bounds[1] = (float)cols; bounds[2] = 0.0f; bounds[3] = (float)rows;
+        return ORBX_OK;
+    }
+    orbx_keypoint c[4] = {};
+    c[0].x = 0.0f; c[0].y = 0.0f; c[1].x = (float)cols; c[1].y = 0.0f;
+    c[2].x = 0.0f; c[2].y = (float)rows; c[3].x = (float)cols; c[3].y = (float)rows;
+    orbx_keypoint u[4];
+    if ((st = orbx_undistort_keypoints(m, c, 4, K, dist, n_dist, u))) return st;
+    bounds[0] = std::min(u[0].x, u[2].x);   // mnMinX, mnMaxX, mnMinY, mnMaxY (:451-454)
+    bounds[1] = std::max(u[1].x, u[3].x);
+    bounds[2] = std::min(u[0].y, u[1].y);
+    bounds[3] = std::max(u[2].y, u[3].y);
+    return ORBX_OK;
+}
 
 int orbx_grid_build_device(orbx_matcher* m, orbx_grid grid, const orbx_keypoint* d_kps, const int32_t* d_counts, int batch,
                            int capacity, int32_t* d_cell_start, int32_t* d_cell_idx, void* stream) {

@@ -177,6 +177,9 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_distinctive_descriptors_device.argtypes = [vp, vp, vp, i32, vp, vp, vp]
     lib.orbx_distinctive_descriptors_store_device.argtypes = [vp, C.POINTER(KfStore), vp, vp, i32, vp, vp, vp]
     lib.orbx_grid_build_device.argtypes = [vp, Grid, vp, vp, i32, i32, vp, vp, vp]
+    lib.orbx_undistort_keypoints.argtypes = [vp, vp, i32, vp, vp, i32, vp]
+    lib.orbx_undistort_keypoints_device.argtypes = [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]
+    lib.orbx_compute_image_bounds.argtypes = [vp, vp, vp, i32, i32, i32, vp]
     lib.orbx_proj_search_batch_device.argtypes = [vp, C.POINTER(ProjParams), Grid, vp, i32, i32, i32, vp]
     lib.orbx_proj_search.argtypes = [vp, C.POINTER(ProjParams), Grid, vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp,
                                      C.POINTER(i32)]
@@ -463,12 +466,13 @@ class ORBmatcher:
         best_dist, second_dist (P, nq) int32: P independent all-pairs matches in one launch."""
         import torch
         P, nq, nt = query.shape[0], query.shape[1], train.shape[1]
-        assert query.stride(1) == 32 and train.stride(1) == 32 and query.stride(2) == 1 and train.stride(2) == 1
+        assert query.stride(1) == 32 and query.stride(2) == 1 and (nt == 0 or (train.stride(1) == 32 and train.stride(2) == 1))
         bi, bd, sd = out if out is not None else \
             (torch.empty((P, nq), dtype=torch.int32, device=query.device) for _ in range(3))
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(query.device).cuda_stream)
-        _check(self._lib.orbx_bf_match_batch_device(self._h, _tp(query), nq, query.stride(0), _tp(train), nt, train.stride(0),
-                                                    P, _tp(bi), _tp(bd), _tp(sd), s))
+        _check(self._lib.orbx_bf_match_batch_device(self._h, _tp(query), nq, query.stride(0),
+                                                    _tp(train) if nt else None, nt, train.stride(0) if nt else 0, P,
+                                                    _tp(bi), _tp(bd), _tp(sd), s))
         return bi, bd, sd
 
     def stereo_descriptor_search(self, kps_left, desc_left, kps_right, desc_right, scale_factors, rows, bf, b):
@@ -578,6 +582,37 @@ class ORBmatcher:
                                                        C.byref(n)))
         return n.value, m
 
+
+    # ---- Frame::UndistortKeyPoints / ComputeImageBounds (src/Frame.cc:404-464) ---------------------------------
+    def UndistortKeyPoints(self, kps, K, dist_coef):
+        """mvKeysUn from mvKeys: K 3x3 float, dist_coef (k1, k2, p1, p2[, k3]); a zero first coefficient copies."""
+        k = np.ascontiguousarray(kps, KP_DTYPE)
+        Km = np.ascontiguousarray(K, np.float32).reshape(9)
+        d = np.ascontiguousarray(dist_coef, np.float32).reshape(-1)
+        out = np.zeros_like(k)
+        _check(self._lib.orbx_undistort_keypoints(self._h, _p(k), len(k), _p(Km), _p(d) if len(d) else None, len(d),
+                                                   _p(out)))
+        return out
+
+    def undistort_keypoints_device(self, kps, counts, K, dist_coef, out=None, stream=None):
+        """(B, cap, 28) device keypoints of an extractor batch -> undistorted copy (same layout)."""
+        import torch
+        B, cap = kps.shape[0], kps.shape[1]
+        Km = np.ascontiguousarray(K, np.float32).reshape(9)
+        d = np.ascontiguousarray(dist_coef, np.float32).reshape(-1)
+        out = out if out is not None else torch.empty_like(kps)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(kps.device).cuda_stream)
+        _check(self._lib.orbx_undistort_keypoints_device(self._h, _tp(kps), _tp(counts), B, cap, _p(Km),
+                                                          _p(d) if len(d) else None, len(d), _tp(out), s))
+        return out
+
+    def ComputeImageBounds(self, K, dist_coef, cols, rows):
+        """(mnMinX, mnMaxX, mnMinY, mnMaxY) of Frame::ComputeImageBounds."""
+        Km = np.ascontiguousarray(K, np.float32).reshape(9)
+        d = np.ascontiguousarray(dist_coef, np.float32).reshape(-1)
+        b = np.zeros(4, np.float32)
+        _check(self._lib.orbx_compute_image_bounds(self._h, _p(Km), _p(d) if len(d) else None, len(d), cols, rows, _p(b)))
+        return tuple(float(v) for v in b)
 
     # ---- MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:246-311) ----------------------------------
     def ComputeDistinctiveDescriptors(self, descriptor_lists):

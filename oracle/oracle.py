@@ -359,6 +359,18 @@ def proj_search(params, grid, queries, qdesc, kps, desc, uright=None, blocked=No
     return nm, qi[:nq], qdist[:nq], own[:n]
 
 
+def undistort_points(xy, K, dist):
+    """Frame::UndistortKeyPoints' cv::undistortPoints(K, D, R=I, P=K), OpenCV 3.2 semantics restated."""
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    Km = np.ascontiguousarray(K, np.float32).reshape(9)
+    d = np.ascontiguousarray(dist if len(dist) else [0.0], np.float32)
+    out = np.zeros_like(xy)
+    L = lib()
+    L.orc_undistort_points.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    L.orc_undistort_points(_p(xy), len(xy), _p(Km), _p(d), len(dist), _p(out))
+    return out
+
+
 # ---- keyframe database queries (oracle/kfdb_oracle.cpp) ---------------------------------------------
 class Kfdb:
     """Sequential restatement of KeyFrameDatabase (src/KeyFrameDatabase.cc) over keyframe slots."""

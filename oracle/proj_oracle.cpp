@@ -262,4 +262,36 @@ int orc_proj_search(orc_proj_params P, const orc_proj_query* Q, const uint8_t* q
     return nm;
 }
 
+
+// Frame::UndistortKeyPoints / ComputeImageBounds (src/Frame.cc:404-464) via OpenCV 3.2 cvUndistortPoints(src, dst, K,
+// D, R = I, P = K) restated: double precision, 5 fixed iterations (test infrastructure; -ffp-contract=off).
+void orc_undistort_points(const float* xy, int n, const float* K, const float* dist, int n_dist, float* out) {
+    double k[14] = {0};
+    for (int i = 0; i < n_dist; ++i) k[i] = dist[i];
+    const double fx = K[0], fy = K[4], cx = K[2], cy = K[5], ifx = 1. / fx, ify = 1. / fy;
+    double RR[3][3];
+    for (int i = 0; i < 9; ++i) RR[i / 3][i % 3] = K[i];
+    const bool copy = n_dist == 0 || dist[0] == 0.0f;
+    for (int i = 0; i < n; ++i) {
+        if (copy) { out[2 * i] = xy[2 * i]; out[2 * i + 1] = xy[2 * i + 1]; continue; }
+        double x = xy[2 * i], y = xy[2 * i + 1];
+        x = (x - cx) * ifx;
+        y = (y - cy) * ify;
+        const double x0 = x, y0 = y;
+        for (int j = 0; j < 5; j++) {
+            double r2 = x * x + y * y;
+            double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+            double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+            double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+            x = (x0 - deltaX) * icdist;
+            y = (y0 - deltaY) * icdist;
+        }
+        double xx = RR[0][0] * x + RR[0][1] * y + RR[0][2];
+        double yy = RR[1][0] * x + RR[1][1] * y + RR[1][2];
+        double ww = 1. / (RR[2][0] * x + RR[2][1] * y + RR[2][2]);
+        out[2 * i] = (float)(xx * ww);
+        out[2 * i + 1] = (float)(yy * ww);
+    }
+}
+
 }  // extern "C"
