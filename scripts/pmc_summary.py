@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 kernel-trace/stats run and its separate FETCH_SIZE / WRITE_SIZE PMC passes
-into profiles/<tag>_*.  Traffic correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE/WRITE_SIZE are KiB;
-on gfx950 FETCH_SIZE under-reports wide coalesced reads by 2x and is uncalibrated for other widths, so
-the read side is calibrated on k_copy_level0, whose bytes are known exactly (it reads every input image
-once with coalesced byte loads: batch x rows x cols bytes), and the same factor is applied to the other
-kernels (all of them read bytes or dwords, never 16-B vectors).
+"""Summarise a rocprofv3 kernel-trace run and its separate FETCH_SIZE / WRITE_SIZE PMC passes (scripts/prof_round.sh)
+into profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc_summary.json and profiles/pmc_traffic.json.
 
-usage: scripts/pmc_summary.py <prof_dir> <tag> <batch_images> <rows> <cols> [dominant_stage]
+Only the bench's batch launches are summarised (the extractor launches over all 2 x batch images: the largest grid of
+each kernel).  Traffic correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE are KiB per dispatch; on gfx950
+FETCH_SIZE under-reports wide coalesced reads and is uncalibrated for other widths, so the read side is calibrated on
+the first k_resize4 launch of the batch (level 0 -> level 1): it reads every level-0 byte of the batch from HBM once
+(batch x rows x cols; its 8-byte window loads overlap only inside L2), with the same 8-byte load pattern k_fast_cells
+uses.  WRITE_SIZE is taken as reported.
+
+usage: scripts/pmc_summary.py <prof_dir> <tag> <batch_images> <rows> <cols> [dominant_kernel]
 """
 import collections
 import csv
@@ -15,61 +18,65 @@ import os
 import shutil
 import sys
 
-R1A_CALIBRATION = 1.3265335392964581
-STAGE_OF = {"k_copy_level0": "copy_level0", "k_resize": "resize", "k_fast_cells": "fast_cells", "k_blur7": "blur7",
-            "k_quadtree": "quadtree", "k_describe": "describe", "k_stereo": "stereo_match",
-            "k_stereo_sad": "stereo_refine", "k_bow_pairs": "keyframe_bow_fusion"}
-
 
 def short(name):
-    n = name.split("(")[0]
-    return n.split("::")[-1]
+    return name.split("(")[0].split("::")[-1]
 
 
-def per_kernel(path):
-    agg = collections.defaultdict(list)
+def launches(path, value_col=None):
+    """{(kernel, grid_x, grid_y): [values]} with durations (kernel trace) or counter values (PMC)."""
+    out = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+        gx = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
+        gy = int(r.get("Grid_Size_Y", 1) or 1)
+        v = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) if value_col is None else float(r[value_col])
+        out[(short(r["Kernel_Name"]), gx, gy)].append(v)
+    return out
+
+
+def biggest(d):
+    """kernel -> values of its largest-grid launches (the batch launches; resize: per level, keep all)."""
+    best = {}
+    for (k, gx, gy), v in d.items():
+        if k not in best or gx * gy > best[k][0]:
+            best[k] = (gx * gy, v)
+    return {k: v for k, (_, v) in best.items()}
 
 
 def main():
     prof, tag, batch, rows, cols = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
-    dom = sys.argv[6] if len(sys.argv) > 6 else None
+    dom = sys.argv[6] if len(sys.argv) > 6 else "k_fast_cells"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = os.path.join(root, "profiles")
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(prof, "kt", "run_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
-    fetch = per_kernel(os.path.join(prof, "fetch", "run_counter_collection.csv"))
-    write = per_kernel(os.path.join(prof, "write", "run_counter_collection.csv"))
-    if "k_copy_level0" in fetch:
-        calib = batch * rows * cols / (fetch["k_copy_level0"] * 1024.0)
-    else:
-        # level 0 is now read in place (no copy kernel): reuse the factor measured on k_copy_level0 in r1a
-        # (profiles/r1a_pmc_summary.json), the same byte-load pattern
-        calib = R1A_CALIBRATION
-    stats = {}
-    for r in csv.DictReader(open(os.path.join(prof, "kt", "run_kernel_stats.csv"))):
-        stats[short(r["Name"])] = dict(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]), pct=float(r["Percentage"]))
+    dur = biggest(launches(os.path.join(prof, "kt", "run_kernel_trace.csv")))
+    fetch = biggest(launches(os.path.join(prof, "fetch", "run_counter_collection.csv"), "Counter_Value"))
+    write = biggest(launches(os.path.join(prof, "write", "run_counter_collection.csv"), "Counter_Value"))
+    calib = batch * rows * cols / (sum(fetch["k_resize4"]) / len(fetch["k_resize4"]) * 1024.0)
     summary = {"tag": tag, "batch_images": batch, "image": [rows, cols], "fetch_calibration": calib,
-               "note": "bytes per dispatch; read = FETCH_SIZE*1024*calibration, write = WRITE_SIZE*1024",
+               "calibration_kernel": "k_resize4 (level 0 -> 1): reads batch x rows x cols bytes once",
+               "note": "bytes per batch launch; read = FETCH_SIZE*1024*calibration, write = WRITE_SIZE*1024",
                "kernels": {}}
     for k in sorted(fetch):
         if not k.startswith("k_"):
             continue
-        rd, wr = fetch[k] * 1024.0 * calib, write.get(k, 0.0) * 1024.0
-        summary["kernels"][k] = dict(stage=STAGE_OF.get(k), read_bytes=rd, write_bytes=wr, hbm_bytes=rd + wr,
-                                     **stats.get(k, {}))
+        f = sum(fetch[k]) / len(fetch[k])
+        w = sum(write.get(k, [0.0])) / max(len(write.get(k, [])), 1)
+        t = dur.get(k)
+        rd, wr = f * 1024.0 * calib, w * 1024.0
+        summary["kernels"][k] = dict(read_bytes=rd, write_bytes=wr, hbm_bytes=rd + wr,
+                                     avg_ns=(sum(t) / len(t)) if t else None,
+                                     hbm_GBps=((rd + wr) / (sum(t) / len(t))) if t else None)
     json.dump(summary, open(os.path.join(out, f"{tag}_pmc_summary.json"), "w"), indent=1)
-    if dom is None:
-        dom_k = max((k for k in stats if k.startswith("k_") and k != "k_resize"), key=lambda k: stats[k]["pct"])
-    else:
-        dom_k = [k for k, s in STAGE_OF.items() if s == dom][0]
-    d = summary["kernels"][dom_k]
-    json.dump({"tag": tag, "kernel": dom_k, "kernel_stage": d["stage"], "batch_images": batch,
-               "hbm_bytes_per_launch": d["hbm_bytes"], "avg_ns": d.get("avg_ns")},
+    d = summary["kernels"][dom]
+    json.dump({"tag": tag, "kernel": dom, "batch_images": batch, "config": "kitti" if cols == 1242 else "euroc",
+               "hbm_bytes_per_launch": d["hbm_bytes"], "avg_ns": d["avg_ns"],
+               "source": f"profiles/{tag}_pmc_summary.json"},
               open(os.path.join(out, "pmc_traffic.json"), "w"), indent=1)
-    print(json.dumps(summary, indent=1))
+    for k, v in sorted(summary["kernels"].items(), key=lambda kv: -(kv[1]["avg_ns"] or 0))[:14]:
+        print(f"{k:24s} {v['avg_ns'] / 1e3 if v['avg_ns'] else 0:8.1f} us  read {v['read_bytes'] / 1e6:8.2f} MB  "
+              f"write {v['write_bytes'] / 1e6:8.2f} MB  {v['hbm_GBps'] or 0:7.1f} GB/s")
 
 
 if __name__ == "__main__":

@@ -35,11 +35,13 @@ def counters(path):
 
 def main():
     base, out = sys.argv[1], sys.argv[2]
+    import os
+    sep = "/" if os.path.isdir(base + "/kt") else "_"      # prof_round.sh (TAG/kt) or prof_sq.sh (TAG_kt) layout
     stats = {}
-    for r in csv.DictReader(open(base + "_kt/run_kernel_stats.csv")):
+    for r in csv.DictReader(open(base + sep + "kt/run_kernel_stats.csv")):
         stats[short(r["Name"])] = dict(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]), pct=float(r["Percentage"]))
-    c = counters(base + "_sqa/run_counter_collection.csv")
-    for k, d in counters(base + "_sqb/run_counter_collection.csv").items():
+    c = counters(base + sep + "sqa/run_counter_collection.csv")
+    for k, d in counters(base + sep + "sqb/run_counter_collection.csv").items():
         c.setdefault(k, {}).update(d)
     res = {}
     for k, s in sorted(stats.items(), key=lambda kv: -kv[1]["pct"]):
