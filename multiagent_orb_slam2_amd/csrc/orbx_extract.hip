@@ -348,7 +348,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                                                     int iniTh, int minTh, uint32_t* __restrict__ cand_xy,
                                                     uint8_t* __restrict__ cand_s, int cand_stride,
                                                     int* __restrict__ cell_cnt, int ncells, int batch, int stop_after,
-                                                    Src0 s0, int max_rows, int max_cols) {
+                                                    Src0 s0, int max_rows, int max_cols, int cell0, int ncell_sub) {
     // counters at the tail of the dynamic region (no static __shared__: it would shift the dynamic base off 16-byte
     // alignment and the ds_write_b64 of the pair images would replay, cdna_hip_programming.md Guideline 17)
     extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
@@ -364,12 +364,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     int& nki = counters[1];
     int& nkm = counters[2];
     const int tid = threadIdx.x, w = tid >> 6, ln = lane_id();
-    const int item = xcd_item(xcd_chunk(ncells * batch));    // (image, cell), cells of one image adjacent
-    if (item >= ncells * batch) return;                       // whole workgroup: no barrier is split
+    // cells [cell0, cell0 + ncell_sub) of every image (a level range: cells are level-major)
+    const int item = xcd_item(xcd_chunk(ncell_sub * batch));  // (image, cell), cells of one image adjacent
+    if (item >= ncell_sub * batch) return;                    // whole workgroup: no barrier is split
     const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
     const int tp = min(T1, T2);
     {
-        const int img = item / ncells, c = item - img * ncells;
+        const int img = item / ncell_sub, c = cell0 + (item - img * ncell_sub);
         const CellDev cd = cells[c];
         const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
         const bool live = Wd > 0 && Hd > 0;                       // workgroup-uniform
@@ -559,13 +560,15 @@ __device__ __forceinline__ uint32_t blur_col(uint32_t a, uint32_t b, uint32_t c,
 
 __global__ __launch_bounds__(256) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                size_t pyr_stride, const LevelDev* __restrict__ levels,
-                                               const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0) {
+                                               const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
+    // tiles [tile0, tile0 + ntiles) of every image (a level range: tiles are level-major)
     const int nbx = (ntiles + 3) / 4;                         // 4 tiles (waves) per workgroup
     const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
     if (item >= nbx * batch) return;
     const int img = item / nbx;
-    const int t = (item - img * nbx) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (t >= ntiles) return;
+    const int tl = (item - img * nbx) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (tl >= ntiles) return;
+    const int t = tile0 + tl;
     const BlurTile bt = tiles[t];
     const LevelDev L = levels[bt.level];
     const int x0 = bt.tx * kBlurStrip + 4 * lane_id();
@@ -670,9 +673,9 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                                                          int cand_stride, const int* __restrict__ cell_cnt, int ncells,
                                                          QtScratch qs, uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r,
                                                          int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
-                                                         int scan_cap, int* __restrict__ err) {
+                                                         int scan_cap, int* __restrict__ err, int lvl0) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
-    const int lvl = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
+    const int lvl = lvl0 + (int)blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
     const LevelDev L = levels[lvl];
     // LDS layout
     int* A_xr = smem;              // x0 | x1 << 16
@@ -1082,8 +1085,9 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
 static int round_even_f(float v) { return (int)std::nearbyintf(v); }
 static int round_even_d(double v) { return (int)std::nearbyint(v); }
 
-enum Stage { ST_RESIZE = 0, ST_FAST, ST_BLUR, ST_QUADTREE, ST_DESCRIBE, ST_COUNT };
-static const char* kStageNames[ST_COUNT] = {"resize", "fast_cells", "blur7", "quadtree", "describe"};
+enum Stage { ST_RESIZE = 0, ST_FAST, ST_BLUR, ST_QUADTREE, ST_DESCRIBE, ST_FAST_L0, ST_QUADTREE_L0, ST_COUNT };
+static const char* kStageNames[ST_COUNT] = {"resize", "fast_cells", "blur7", "quadtree", "describe", "fast_cells_l0",
+                                            "quadtree_l0"};
 
 struct Extractor {
     // ORBextractor parameters and tables (:410-470)
@@ -1095,11 +1099,13 @@ struct Extractor {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    // k_blur7 runs on a side stream, concurrently with k_quadtree (a latency-bound grid of one workgroup per
-    // (level, image)): fork after k_fast_cells (or after the pyramid, ORBX_BLUR_FORK=0), join before k_describe
+    // Two-stream schedule (run_batch).  Level 0 of the pyramid is the caller's image, so FAST, DistributeOctTree
+    // and the blur of level 0 need nothing from the resize chain: they run on a side stream while the launch stream
+    // builds levels 1..7 (seven dependent, latency-bound resize launches) and runs FAST / DistributeOctTree on them.
+    // The side stream then blurs levels 1..7 once the pyramid is done; k_describe joins both.
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int blur_fork = 1;        // ORBX_BLUR_FORK: 1 after FAST, 0 after the pyramid, -1 on the launch stream (serial)
+    hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_join = nullptr;
+    int pipeline = 1;         // ORBX_PIPELINE: 1 two streams (above), 0 every launch in order on the launch stream
 
     // geometry for the reserved size
     int rows = 0, cols = 0, max_batch = 0;
@@ -1150,10 +1156,11 @@ struct Extractor {
     Src0 last_src0{nullptr, 0, 0};   // level 0 of the last device call = the caller's images
 
     // timing: a pool of event sets recorded on the launch streams, resolved lazily (no host sync per call).
-    // Events: 0 start, 1 pyramid done, 2 FAST done, 3 quadtree done, 4 describe start (after the join),
-    // 5 describe done (all on the launch stream); 6/7 blur start/done on the side stream.
-    static constexpr int kEvents = 8;
-    static constexpr int kStageEv[ST_COUNT][2] = {{0, 1}, {1, 2}, {6, 7}, {2, 3}, {4, 5}};
+    // Launch stream: 0 start, 1 pyramid done, 10 FAST (levels >= 1) start, 2 its end, 3 quadtree (levels >= 1) done,
+    // 4 describe start (after the join), 5 describe done.  Side stream: 6 start, 7 FAST level 0 done, 8 quadtree
+    // level 0 done, 9 blur done (level 0, the wait for the pyramid, levels >= 1; pure blur time when serial).
+    static constexpr int kEvents = 11;
+    static constexpr int kStageEv[ST_COUNT][2] = {{0, 1}, {10, 2}, {8, 9}, {2, 3}, {4, 5}, {6, 7}, {7, 8}};
     struct EventSet { hipEvent_t ev[kEvents]; bool pending; };
     bool timing = false;
     std::vector<EventSet> tpool;
@@ -1163,7 +1170,7 @@ struct Extractor {
     int resolve(EventSet& es) {
         if (!es.pending) return ORBX_OK;
         ORBX_HIP(hipEventSynchronize(es.ev[5]));
-        ORBX_HIP(hipEventSynchronize(es.ev[7]));
+        ORBX_HIP(hipEventSynchronize(es.ev[9]));
         for (int k = 0; k < ST_COUNT; ++k) {
             float ms = 0;
             ORBX_HIP(hipEventElapsedTime(&ms, es.ev[kStageEv[k][0]], es.ev[kStageEv[k][1]]));
@@ -1478,23 +1485,40 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     }
     const Src0 s0{d_images, step, istride};
     e->last_src0 = s0;
-    auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], k >= 6 ? e->side : s); };
-    auto launch_blur = [&]() -> int {
-        hipStream_t bs = e->blur_fork < 0 ? s : e->side;
-        if (bs != s) {
-            ORBX_HIP(hipEventRecord(e->ev_fork, s));
-            ORBX_HIP(hipStreamWaitEvent(e->side, e->ev_fork, 0));
-        }
-        if (es) (void)hipEventRecord(es->ev[6], bs);
-        const int nt = (int)e->tilev.size();
-        dim3 g(kXcds * xcd_chunk((nt + 3) / 4 * batch));
-        hipLaunchKernelGGL(k_blur7, g, dim3(256), 0, bs, e->d_pyr, e->d_blur, ps, e->d_levels, e->d_tiles, nt, batch, s0);
-        if (es) (void)hipEventRecord(es->ev[7], bs);
-        ORBX_HIP(hipEventRecord(e->ev_join, bs));
-        return ORBX_OK;
+    hipStream_t side = e->pipeline ? e->side : s;
+    auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : s); };
+    const int ncells = (int)e->cellv.size();
+    const int c0 = nl > 0 ? e->lv[0].cell_end : 0;                 // cells of level 0: [0, c0)
+    int t0 = 0;                                                     // blur tiles of level 0: [0, t0)
+    while (t0 < (int)e->tilev.size() && e->tilev[t0].level == 0) ++t0;
+    const int nt = (int)e->tilev.size();
+    QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
+    auto fast = [&](hipStream_t q, int cell0, int n) {
+        if (n <= 0) return;
+        hipLaunchKernelGGL(k_fast_cells, dim3(kXcds * xcd_chunk(n * batch)), dim3(256), fast_lds_bytes(e), q, e->d_pyr, ps,
+                           e->d_levels, e->d_cells, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s, e->cand_stride,
+                           e->d_cell_cnt, ncells, batch, e->fast_stop_after, s0, e->cell_max_rows, e->cell_max_cols,
+                           cell0, n);
     };
+    auto quadtree = [&](hipStream_t q, int lvl0, int n) {
+        if (n <= 0) return;
+        hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds, q, e->d_levels, e->d_cells, e->d_cand_xy,
+                           e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy, e->d_lvl_r,
+                           e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err, lvl0);
+    };
+    auto blur = [&](hipStream_t q, int tile0, int n) {
+        if (n <= 0) return;
+        hipLaunchKernelGGL(k_blur7, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur, ps,
+                           e->d_levels, e->d_tiles, n, batch, s0, tile0);
+    };
+
     mark(0);
-    for (int l = 1; l < nl; ++l) {
+    if (side != s) {
+        ORBX_HIP(hipEventRecord(e->ev_fork, s));
+        ORBX_HIP(hipStreamWaitEvent(side, e->ev_fork, 0));
+    }
+    auto resize_chain = [&]() {
+      for (int l = 1; l < nl; ++l) {
         const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
         const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
         const LevelDev& L = e->lv[l];
@@ -1507,28 +1531,31 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
             dim3 g((L.w + 255) / 256, L.h, batch);
             hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis, L.pyr_off, L.w, L.h, e->rtab[l]);
         }
+      }
+      mark(1);
+    };
+    if (side == s) resize_chain();                                  // serial: every stage contiguous on one stream
+    // side stream, level 0 (reads only the caller's images)
+    mark(6);
+    fast(side, 0, c0);
+    mark(7);
+    quadtree(side, 0, nl > 0 ? 1 : 0);
+    mark(8);
+    blur(side, 0, t0);
+    if (side != s) {
+        resize_chain();                                             // launch stream: levels 1..nl-1 of the pyramid
+        ORBX_HIP(hipEventRecord(e->ev_pyr, s));
+        ORBX_HIP(hipStreamWaitEvent(side, e->ev_pyr, 0));
     }
-    mark(1);
-    int st;
-    if (e->blur_fork == 0 && (st = launch_blur())) return st;
-    const int ncells = (int)e->cellv.size();
-    if (ncells > 0) {
-        dim3 g(kXcds * xcd_chunk(ncells * batch));
-        hipLaunchKernelGGL(k_fast_cells, g, dim3(256), fast_lds_bytes(e), s, e->d_pyr, ps, e->d_levels, e->d_cells, e->iniTh, e->minTh,
-                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, batch, e->fast_stop_after,
-                           s0, e->cell_max_rows, e->cell_max_cols);
-    }
+    blur(side, t0, nt - t0);                                        // side: levels 1..nl-1 once the pyramid exists
+    mark(9);
+    if (side != s) ORBX_HIP(hipEventRecord(e->ev_join, side));
+    mark(10);                                                       // launch stream: FAST, DistributeOctTree 1..nl-1
+    fast(s, c0, ncells - c0);
     mark(2);
-    if (e->blur_fork != 0 && (st = launch_blur())) return st;
-    {
-        QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
-        dim3 g(nl, batch);
-        hipLaunchKernelGGL(k_quadtree, g, dim3(kQtThreads), e->qt_lds, s, e->d_levels, e->d_cells, e->d_cand_xy, e->d_cand_s,
-                           e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy, e->d_lvl_r, e->out_stride,
-                           e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err);
-    }
+    quadtree(s, 1, nl - 1);
     mark(3);
-    ORBX_HIP(hipStreamWaitEvent(s, e->ev_join, 0));
+    if (side != s) ORBX_HIP(hipStreamWaitEvent(s, e->ev_join, 0));
     mark(4);
     {
         const int total_slots = e->out_stride;
@@ -1588,8 +1615,11 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     hipError_t he = hipSetDevice(device);
     e->own_stream = true;
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
+    // ORBX_SIDE_PRIORITY (A/B only): HIP priority of the side stream; default normal
+    const int side_prio = std::getenv("ORBX_SIDE_PRIORITY") ? std::atoi(std::getenv("ORBX_SIDE_PRIORITY")) : 0;
+    if (he == hipSuccess) he = hipStreamCreateWithPriority(&e->side, hipStreamNonBlocking, side_prio);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pyr, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
     if (he != hipSuccess) {
         set_error("stream create: %s", hipGetErrorString(he));
@@ -1597,7 +1627,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
         return ORBX_ERR_HIP;
     }
     if (const char* ab = std::getenv("ORBX_FAST_ABLATE")) e->fast_stop_after = std::atoi(ab);
-    if (const char* bf = std::getenv("ORBX_BLUR_FORK")) e->blur_fork = std::atoi(bf);
+    if (const char* pl = std::getenv("ORBX_PIPELINE")) e->pipeline = std::atoi(pl) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
         return st;
@@ -1617,6 +1647,7 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->side) (void)hipStreamDestroy(e->side);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_pyr) (void)hipEventDestroy(e->ev_pyr);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     delete e;
     return ORBX_OK;
