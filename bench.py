@@ -293,8 +293,12 @@ def main():
     outs = [(torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev),
              torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev),
              torch.empty((2 * B,), dtype=torch.int32, device=dev)) for _ in range(2)]
-    stream = torch.cuda.Stream(dev)                    # front-end queue: extractor + stereo matcher
+    stream = torch.cuda.Stream(dev)                    # front-end queue: the extractor
     torch.cuda.set_stream(stream)
+    # stereo queue: step k's ComputeStereoMatches (band match + SAD refinement on step k's pyramids) runs beside
+    # step k+1's extraction; the extractor cycles two pyramid sets so that step k+1 does not overwrite step k's
+    stereo_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("ORBX_STEREO_PRIORITY", "0")))
+    ex.set_pyramid_ring(2)
     # keyframe queue: BoW, packets, exchange, KeyFrameDatabase, SearchByBoW -- the native orbx_fusion object.  As in
     # the reference, where LoopClosing and MapFusion run in their own threads beside Tracking, step k's keyframe work
     # overlaps step k+1's extraction.
@@ -318,7 +322,6 @@ def main():
 
     stereo_ms = []
     kf_ms = []
-    pyr = []
     host_split = [0.0, 0.0]                            # host enqueue seconds: front-end, keyframe path
 
     def step(time_stereo=False):
@@ -328,20 +331,23 @@ def main():
         if kf_done[buf] is not None:
             stream.wait_event(kf_done[buf])            # the keyframe path of two steps ago has read this set
         ex.extract_batch_device(imgs, kps, desc, cnt, stream=stream)
-        if time_stereo:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        bi, bd = m.stereo_match_batch_device(kps[:B], desc[:B], cnt[:B], kps[B:], desc[B:], cnt[B:], cap, scale,
-                                             ROWS, BF, BASELINE_B, stream=stream)
-        if not pyr:
-            pyr.append(ex.pyramid_device())            # device pointers are fixed for this input / config
-        ur, depth = m.stereo_refine_batch_device(kps[:B], cnt[:B], kps[B:], bi, pyr[0], 0, pyr[0], B, BF, BASELINE_B,
-                                                 stream=stream)
-        if time_stereo:
-            e1.record(stream)
-            stereo_ms.append((e0, e1))
+        extracted = torch.cuda.Event()
+        extracted.record(stream)
+        pyr = ex.pyramid_device()                      # this call's pyramid set (a slot of the ring of 2)
+        stereo_stream.wait_event(extracted)
+        with torch.cuda.stream(stereo_stream):         # outputs allocated on (and owned by) the stereo queue
+            if time_stereo:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stereo_stream)
+            bi, bd = m.stereo_match_batch_device(kps[:B], desc[:B], cnt[:B], kps[B:], desc[B:], cnt[B:], cap, scale,
+                                                 ROWS, BF, BASELINE_B, stream=stereo_stream)
+            ur, depth = m.stereo_refine_batch_device(kps[:B], cnt[:B], kps[B:], bi, pyr, 0, pyr, B, BF, BASELINE_B,
+                                                     stream=stereo_stream)
+            if time_stereo:
+                e1.record(stereo_stream)
+                stereo_ms.append((e0, e1))
         handoff = torch.cuda.Event()
-        handoff.record(stream)
+        handoff.record(stereo_stream)
         h1 = time.perf_counter()
         # keyframe path: rows of this step's batch -> BoW -> packets -> all-gather (N>1) into the ring -> sequential
         # DetectLoopCandidates -> batched SearchByBoW; MapPoint-valid = stereo depth > 0

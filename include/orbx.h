@@ -100,7 +100,8 @@ int orbx_extract_batch_device(orbx_extractor* ex, const uint8_t* d_images, int b
  * ORBextractor::mvImagePyramid exposes, include/ORBextractor.h:85): level 0 of image i is the caller's
  * image at level0 + i*level0_image_stride (row step level0_step); level l >= 1 of image i is at
  * levels + i*image_stride + offset[l] with row step cols[l].  scale / inv_scale: mvScaleFactor /
- * mvInvScaleFactor.  Valid until the next call on the extractor (and while the caller keeps level 0). */
+ * mvInvScaleFactor.  Valid until the next call on the extractor (and while the caller keeps level 0);
+ * with a pyramid ring of n sets (orbx_extractor_set_pyramid_ring), until the n-th next call. */
 #define ORBX_MAX_LEVELS 32
 typedef struct orbx_pyramid {
     int nlevels, batch;
@@ -113,6 +114,12 @@ typedef struct orbx_pyramid {
     float scale[ORBX_MAX_LEVELS], inv_scale[ORBX_MAX_LEVELS];
 } orbx_pyramid;
 int orbx_extractor_pyramid_device(const orbx_extractor* ex, orbx_pyramid* out);
+
+/* Number of pyramid sets the extractor cycles through (1..8, default 1).  In the reference each Frame
+ * owns its extractor's mvImagePyramid until the next Frame is built (src/Frame.cc:78-81, used by
+ * ComputeStereoMatches :598-640); a ring of 2 lets the caller run step k's stereo SAD refinement on
+ * another stream while step k+1 extracts.  Reallocates the extractor's buffers. */
+int orbx_extractor_set_pyramid_ring(orbx_extractor* ex, int n);
 
 /* Device pointer and row step of pyramid level 'level' of image 'index' of the last call.  Level 0 is
  * the caller's input image itself (read in place, never copied): valid while the caller keeps it. */

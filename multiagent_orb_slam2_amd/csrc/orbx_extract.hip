@@ -528,19 +528,42 @@ __device__ __forceinline__ u16x2 byte_pair(uint32_t w0, uint32_t w1, uint32_t w2
 }
 
 struct BlurRow { u16x2 h01, h23; };   // horizontal sums of columns x0, x0+1 | x0+2, x0+3
+struct BlurWin { uint32_t w0, w1, w2; };   // 12 input bytes x0-4 .. x0+7 of one row
 
-__device__ __forceinline__ BlurRow blur_hrow(const uint8_t* __restrict__ row, int x0, int w, bool interior) {
-    uint32_t w0, w1, w2;
-    if (interior) {
+// Row window loads.  kMode 0: interior lane, one 12-byte load.  kMode 1: a lane within 8 columns of a level edge
+// (level at least 12 wide): one 12-byte load clamped inside the row, then the reflected bytes are picked out of it
+// (every reflected column x0-3 .. x0+6 falls inside the clamped window).  kMode 2: tiny level, per-byte loads.
+template <int kMode>
+__device__ __forceinline__ BlurWin blur_load(const uint8_t* __restrict__ row, int x0, int w) {
+    BlurWin o;
+    if (kMode == 0) {
         uint32_t v[3];
         __builtin_memcpy(v, row + x0 - 4, 12);
-        w0 = v[0]; w1 = v[1]; w2 = v[2];
+        o.w0 = v[0]; o.w1 = v[1]; o.w2 = v[2];
+    } else if (kMode == 1) {
+        const int xs = min(max(x0 - 4, 0), w - 12);
+        uint32_t v[3];
+        __builtin_memcpy(v, row + xs, 12);
+        uint32_t r[3] = {0, 0, 0};
+#pragma unroll
+        for (int i = 1; i < 11; ++i) {
+            const int x = x0 - 4 + i;
+            const int k = (x < 0 ? -x : (x >= w ? 2 * w - 2 - x : x)) - xs;     // 0 <= k < 12
+            const uint32_t d = k < 4 ? v[0] : (k < 8 ? v[1] : v[2]);
+            r[i >> 2] |= ((d >> (8 * (k & 3))) & 0xffu) << (8 * (i & 3));
+        }
+        o.w0 = r[0]; o.w1 = r[1]; o.w2 = r[2];
     } else {
         uint32_t v[3] = {0, 0, 0};
 #pragma unroll
         for (int i = 1; i < 11; ++i) v[i >> 2] |= (uint32_t)row[refl101(x0 - 4 + i, w)] << (8 * (i & 3));
-        w0 = v[0]; w1 = v[1]; w2 = v[2];
+        o.w0 = v[0]; o.w1 = v[1]; o.w2 = v[2];
     }
+    return o;
+}
+
+__device__ __forceinline__ BlurRow blur_hrow(const BlurWin& v) {
+    const uint32_t w0 = v.w0, w1 = v.w1, w2 = v.w2;
     // b[i] = pixel x0 - 3 + i = window byte i + 1;  P_i = (b[i], b[i+1])
     const u16x2 P0 = byte_pair<1>(w0, w1, w2), P1 = byte_pair<2>(w0, w1, w2), P2 = byte_pair<3>(w0, w1, w2);
     const u16x2 P3 = byte_pair<4>(w0, w1, w2), P4 = byte_pair<5>(w0, w1, w2), P5 = byte_pair<6>(w0, w1, w2);
@@ -558,7 +581,58 @@ __device__ __forceinline__ uint32_t blur_col(uint32_t a, uint32_t b, uint32_t c,
     return min((acc + (1u << 15)) >> 16, 255u);
 }
 
-__global__ __launch_bounds__(256) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+// One wave's band: outputs rows [y0, y1) of columns x0 .. x0+3 (per lane).  Every load of a step is issued before
+// any of its rows is used, so the band costs ~6 memory round trips per wave, not one per input row; row indices are
+// reflected branch-free (|overhang| <= 3 < h), so loads past the band's end stay in bounds.
+template <int kMode>
+__device__ __forceinline__ void blur_band(const uint8_t* __restrict__ S, int sstride, uint8_t* __restrict__ D,
+                                          const LevelDev& L, int x0, int y0, int y1) {
+    const int h = L.h, w = L.w;
+    auto row_ptr = [&](int yy) {
+        const int r = h >= 4 ? (yy < 0 ? -yy : (yy >= h ? 2 * h - 2 - yy : yy)) : refl101(yy, h);
+        return S + (size_t)r * sstride;
+    };
+    const bool full = x0 + 4 <= w;
+    BlurRow r0, r1, r2, r3, r4, r5, r6;
+    {
+        BlurWin p[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) p[k] = blur_load<kMode>(row_ptr(y0 - 3 + k), x0, w);
+        r0 = blur_hrow(p[0]); r1 = blur_hrow(p[1]); r2 = blur_hrow(p[2]);
+        r3 = blur_hrow(p[3]); r4 = blur_hrow(p[4]); r5 = blur_hrow(p[5]);
+    }
+    auto emit = [&](int y, const BlurRow& a, const BlurRow& b, const BlurRow& c, const BlurRow& d, const BlurRow& e,
+                    const BlurRow& f, const BlurRow& g) {
+        const uint32_t o0 = blur_col(a.h01.x, b.h01.x, c.h01.x, d.h01.x, e.h01.x, f.h01.x, g.h01.x);
+        const uint32_t o1 = blur_col(a.h01.y, b.h01.y, c.h01.y, d.h01.y, e.h01.y, f.h01.y, g.h01.y);
+        const uint32_t o2 = blur_col(a.h23.x, b.h23.x, c.h23.x, d.h23.x, e.h23.x, f.h23.x, g.h23.x);
+        const uint32_t o3 = blur_col(a.h23.y, b.h23.y, c.h23.y, d.h23.y, e.h23.y, f.h23.y, g.h23.y);
+        const uint32_t packed = o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
+        uint8_t* o = D + (size_t)y * w + x0;
+        if (kMode == 0 || full) {
+            __builtin_memcpy(o, &packed, 4);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (x0 + j < w) o[j] = (uint8_t)(packed >> (8 * j));
+        }
+    };
+    // ring of 7 row sums; each step loads input rows y+3 .. y+9 at once, then emits outputs y .. y+6
+    for (int y = y0; y < y1; y += 7) {
+        BlurWin p[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) p[k] = blur_load<kMode>(row_ptr(y + 3 + k), x0, w);
+        r6 = blur_hrow(p[0]); emit(y, r0, r1, r2, r3, r4, r5, r6); if (y + 1 >= y1) break;
+        r0 = blur_hrow(p[1]); emit(y + 1, r1, r2, r3, r4, r5, r6, r0); if (y + 2 >= y1) break;
+        r1 = blur_hrow(p[2]); emit(y + 2, r2, r3, r4, r5, r6, r0, r1); if (y + 3 >= y1) break;
+        r2 = blur_hrow(p[3]); emit(y + 3, r3, r4, r5, r6, r0, r1, r2); if (y + 4 >= y1) break;
+        r3 = blur_hrow(p[4]); emit(y + 4, r4, r5, r6, r0, r1, r2, r3); if (y + 5 >= y1) break;
+        r4 = blur_hrow(p[5]); emit(y + 5, r5, r6, r0, r1, r2, r3, r4); if (y + 6 >= y1) break;
+        r5 = blur_hrow(p[6]); emit(y + 6, r6, r0, r1, r2, r3, r4, r5);
+    }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                size_t pyr_stride, const LevelDev* __restrict__ levels,
                                                const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
     // tiles [tile0, tile0 + ntiles) of every image (a level range: tiles are level-major)
@@ -578,42 +652,13 @@ __global__ __launch_bounds__(256) void k_blur7(const uint8_t* __restrict__ pyr, 
     uint8_t* D = blur + img * pyr_stride + L.pyr_off;
     const int y0 = bt.ty * kBlurBand, y1 = min(y0 + kBlurBand, L.h);
     const bool interior = (x0 - 4 >= 0) && (x0 + 8 <= L.w);
-    const bool full = x0 + 4 <= L.w;
-    BlurRow r0, r1, r2, r3, r4, r5, r6;
-#define ORBX_HROW(yy) blur_hrow(S + (size_t)refl101((yy), L.h) * sstride, x0, L.w, interior)
-    r0 = ORBX_HROW(y0 - 3);
-    r1 = ORBX_HROW(y0 - 2);
-    r2 = ORBX_HROW(y0 - 1);
-    r3 = ORBX_HROW(y0);
-    r4 = ORBX_HROW(y0 + 1);
-    r5 = ORBX_HROW(y0 + 2);
-    auto emit = [&](int y, const BlurRow& a, const BlurRow& b, const BlurRow& c, const BlurRow& d, const BlurRow& e,
-                    const BlurRow& f, const BlurRow& g) {
-        const uint32_t o0 = blur_col(a.h01.x, b.h01.x, c.h01.x, d.h01.x, e.h01.x, f.h01.x, g.h01.x);
-        const uint32_t o1 = blur_col(a.h01.y, b.h01.y, c.h01.y, d.h01.y, e.h01.y, f.h01.y, g.h01.y);
-        const uint32_t o2 = blur_col(a.h23.x, b.h23.x, c.h23.x, d.h23.x, e.h23.x, f.h23.x, g.h23.x);
-        const uint32_t o3 = blur_col(a.h23.y, b.h23.y, c.h23.y, d.h23.y, e.h23.y, f.h23.y, g.h23.y);
-        const uint32_t packed = o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
-        uint8_t* o = D + (size_t)y * L.w + x0;
-        if (full) {
-            __builtin_memcpy(o, &packed, 4);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (x0 + j < L.w) o[j] = (uint8_t)(packed >> (8 * j));
-        }
-    };
-    // ring of 7 row sums; each unrolled step loads row y+3 into the slot freed by row y-4
-    for (int y = y0; y < y1; y += 7) {
-        r6 = ORBX_HROW(y + 3); emit(y, r0, r1, r2, r3, r4, r5, r6); if (y + 1 >= y1) break;
-        r0 = ORBX_HROW(y + 4); emit(y + 1, r1, r2, r3, r4, r5, r6, r0); if (y + 2 >= y1) break;
-        r1 = ORBX_HROW(y + 5); emit(y + 2, r2, r3, r4, r5, r6, r0, r1); if (y + 3 >= y1) break;
-        r2 = ORBX_HROW(y + 6); emit(y + 3, r3, r4, r5, r6, r0, r1, r2); if (y + 4 >= y1) break;
-        r3 = ORBX_HROW(y + 7); emit(y + 4, r4, r5, r6, r0, r1, r2, r3); if (y + 5 >= y1) break;
-        r4 = ORBX_HROW(y + 8); emit(y + 5, r5, r6, r0, r1, r2, r3, r4); if (y + 6 >= y1) break;
-        r5 = ORBX_HROW(y + 9); emit(y + 6, r6, r0, r1, r2, r3, r4, r5);
-    }
-#undef ORBX_HROW
+    // wave-uniform choice of the load form (strips touching a level's left/right edge pick reflected bytes)
+    if (__builtin_amdgcn_read_exec() == __ballot(interior))
+        blur_band<0>(S, sstride, D, L, x0, y0, y1);
+    else if (L.w >= 12)
+        blur_band<1>(S, sstride, D, L, x0, y0, y1);
+    else
+        blur_band<2>(S, sstride, D, L, x0, y0, y1);
 }
 
 
@@ -979,22 +1024,26 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {   // OpenCV 
     return a;
 }
 
+struct SlotTable { int out_off[kMaxLevels]; };   // LevelDev::out_off per level, as a kernel argument
+
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   size_t pyr_stride, const LevelDev* __restrict__ levels, int nlevels,
                                                   const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
                                                   int out_stride, const int* __restrict__ level_cnt,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
-                                                  int capacity, int total_slots, int batch, Src0 s0) {
+                                                  int capacity, int total_slots, int batch, Src0 s0, SlotTable tab) {
     const int nbx = (total_slots + 3) / 4;                    // 4 slots (waves) per workgroup
     const int item = xcd_item(xcd_chunk(nbx * batch));       // keypoints of one image on one XCD
     if (item >= nbx * batch) return;
     const int img = item / nbx;
-    const int slot = ((item - img * nbx) * blockDim.x + threadIdx.x) >> 6;
+    // wave-uniform (one wave per slot): kept in SGPRs, so the level lookup below is scalar, from the kernel arguments
+    const int slot = __builtin_amdgcn_readfirstlane(((item - img * nbx) * blockDim.x + threadIdx.x) >> 6);
     const int ln = lane_id();
     if (slot >= total_slots) return;
     // slot -> (level, index)
     int lvl = 0;
-    while (lvl + 1 < nlevels && slot >= levels[lvl + 1].out_off) ++lvl;
+#pragma unroll
+    for (int l = 1; l < kMaxLevels; ++l) lvl += (l < nlevels && slot >= tab.out_off[l]) ? 1 : 0;
     const LevelDev L = levels[lvl];
     const int i = slot - L.out_off;
     const int* lc = level_cnt + img * nlevels;
@@ -1130,7 +1179,10 @@ struct Extractor {
     std::vector<ResizeTab> rtab;
     std::vector<ResizeVec> rvec;      // per level: vectorised tables (groups == 0 -> use rtab)
     std::vector<void*> rtab_mem;
-    uint8_t* d_pyr = nullptr;
+    uint8_t* d_pyr = nullptr;         // pyramid set of the current / last call (a slot of d_pyr_ring)
+    uint8_t* d_pyr_ring = nullptr;    // pyr_ring sets of max_batch pyramids: a caller that reads the pyramid of call
+    int pyr_ring = 1;                 // k (Frame::ComputeStereoMatches' SAD step) on another stream can overlap call
+    unsigned long long ncalls = 0;    // k+1, which writes the next set
     uint8_t* d_blur = nullptr;
     uint32_t* d_cand_xy = nullptr;
     uint8_t* d_cand_s = nullptr;
@@ -1227,7 +1279,7 @@ static void level_dims(const Extractor* e, int rows, int cols, int l, int* w, in
 
 void Extractor::free_buffers() {
     auto F = [](auto*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } };
-    F(d_levels); F(d_cells); F(d_tiles); F(d_pyr); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
+    F(d_levels); F(d_cells); F(d_tiles); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
     F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
     F(d_kps); F(d_desc); F(d_cnt);
     if (h_in) { (void)hipHostFree(h_in); h_in = nullptr; }
@@ -1239,6 +1291,7 @@ void Extractor::free_buffers() {
     rvec.clear();
     rows = cols = max_batch = 0;
     in_bytes = 0;
+    d_pyr = nullptr;
 }
 
 static size_t qt_lds_bytes(int cap, int scan_cap);
@@ -1447,7 +1500,9 @@ int Extractor::configure(int r, int c, int batch) {
 
     // ---- batch buffers (HBM): pyramid + blurred pyramid + candidates + quadtree scratch
     const size_t B = (size_t)batch;
-    if ((st = dev_alloc(&d_pyr, B * pyr_size))) return st;
+    if ((st = dev_alloc(&d_pyr_ring, (size_t)pyr_ring * B * pyr_size))) return st;
+    d_pyr = d_pyr_ring;
+    ncalls = 0;
     if ((st = dev_alloc(&d_blur, B * pyr_size))) return st;
     if ((st = dev_alloc(&d_cand_xy, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_cand_s, B * cand_stride))) return st;
@@ -1485,6 +1540,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     }
     const Src0 s0{d_images, step, istride};
     e->last_src0 = s0;
+    e->d_pyr = e->d_pyr_ring + (size_t)(e->ncalls++ % (unsigned long long)e->pyr_ring) * e->max_batch * ps;
     hipStream_t side = e->pipeline ? e->side : s;
     auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : s); };
     const int ncells = (int)e->cellv.size();
@@ -1560,8 +1616,10 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     {
         const int total_slots = e->out_stride;
         dim3 g(kXcds * xcd_chunk((total_slots + 3) / 4 * batch));
+        SlotTable tab{};
+        for (int l = 0; l < nl; ++l) tab.out_off[l] = e->lv[l].out_off;
         hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
-                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, total_slots, batch, s0);
+                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, total_slots, batch, s0, tab);
     }
     mark(5);
     ORBX_HIP(hipGetLastError());
@@ -1686,6 +1744,18 @@ int orbx_extractor_get_features_per_level(const orbx_extractor* e, int* out) {
 int orbx_extractor_reserve(orbx_extractor* e, int rows, int cols, int max_batch) {
     ORBX_REQUIRE(e, ORBX_ERR_ARG, "null extractor");
     return e->configure(rows, cols, max_batch);
+}
+
+int orbx_extractor_set_pyramid_ring(orbx_extractor* e, int n) {
+    ORBX_REQUIRE(e && n >= 1 && n <= 8, ORBX_ERR_ARG, "pyramid ring must be 1..8");
+    if (n == e->pyr_ring) return ORBX_OK;
+    const int r = e->rows, c = e->cols, b = e->max_batch;
+    ORBX_HIP(hipSetDevice(e->device));
+    if (e->stream) ORBX_HIP(hipStreamSynchronize(e->stream));
+    if (e->side) ORBX_HIP(hipStreamSynchronize(e->side));
+    e->free_buffers();
+    e->pyr_ring = n;
+    return (r > 0 && c > 0 && b > 0) ? e->configure(r, c, b) : ORBX_OK;
 }
 
 int orbx_extractor_max_keypoints(orbx_extractor* e, int rows, int cols) {

@@ -145,6 +145,7 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_extract.argtypes = [vp, vp, i32, i32, C.c_size_t, vp, vp, i32, C.POINTER(i32)]
     lib.orbx_extract_batch_device.argtypes = [vp, vp, i32, i32, i32, C.c_size_t, C.c_size_t, vp, vp, vp, i32, vp]
     lib.orbx_extractor_reserve.argtypes = [vp, i32, i32, i32]
+    lib.orbx_extractor_set_pyramid_ring.argtypes = [vp, i32]
     lib.orbx_extractor_max_keypoints.argtypes = [vp, i32, i32]
     lib.orbx_extractor_level_sizes.argtypes = [vp, i32, i32, vp, vp]
     lib.orbx_extractor_copy_level.argtypes = [vp, i32, i32, vp, C.c_size_t]
@@ -326,6 +327,10 @@ class ORBextractor:
         c = np.zeros(self.nlevels, np.int32)
         _check(self._lib.orbx_extractor_level_sizes(self._h, rows, cols, _p(r), _p(c)))
         return list(zip(r.tolist(), c.tolist()))
+
+    def set_pyramid_ring(self, n: int):
+        """Cycle through n pyramid sets: pyramid_device() of call k stays valid until call k+n."""
+        _check(self._lib.orbx_extractor_set_pyramid_ring(self._h, n))
 
     def reserve(self, rows: int, cols: int, max_batch: int):
         _check(self._lib.orbx_extractor_reserve(self._h, rows, cols, max_batch))

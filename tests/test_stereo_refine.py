@@ -129,3 +129,36 @@ def test_gpu_stereo_refine_batch_device(gpu):
         rur, rdp = O.compute_stereo_matches(a, b, t["scale"], t["inv_scale"], 375, BF, B)
         assert urh[i, :ch[i]].tobytes() == rur.tobytes() and dph[i, :ch[i]].tobytes() == rdp.tobytes()
         assert (urh[i, ch[i]:] == -1).all()
+
+
+@pytest.mark.gpu
+def test_gpu_stereo_refine_pyramid_ring(gpu):
+    """Pyramid ring of 2 (orbx_extractor_set_pyramid_ring): step k's pyramid stays intact while step k+1 extracts
+    other images, so step k's SAD refinement run after step k+1 still equals the oracle's (the bench runs it on its
+    own stream beside the next extraction)."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    n = 2
+    lefts = [S.kitti_like_image(310 + i) for i in range(n)]
+    rights = [S.shifted_right_view(x, 310 + i) for i, x in enumerate(lefts)]
+    imgs = torch.from_numpy(np.stack(lefts + rights)).cuda()
+    other = torch.from_numpy(np.stack([S.kitti_like_image(400 + i) for i in range(2 * n)])).cuda()
+    ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    ex.set_pyramid_ring(2)
+    kps, desc, cnt = ex.extract_batch_device(imgs)
+    pyr = ex.pyramid_device()
+    ex.extract_batch_device(other)                                 # writes the other pyramid set
+    assert ex.pyramid_device().levels != pyr.levels
+    cap = kps.shape[1]
+    m = pkg.ORBmatcher()
+    scale = ex.GetScaleFactors()
+    bi, bd = m.stereo_match_batch_device(kps[:n], desc[:n], cnt[:n], kps[n:], desc[n:], cnt[n:], cap, scale, 375, BF, B)
+    ur, dp = m.stereo_refine_batch_device(kps[:n], cnt[:n], kps[n:], bi, pyr, 0, pyr, n, BF, B)
+    torch.cuda.synchronize()
+    urh, dph, ch = ur.cpu().numpy(), dp.cpu().numpy(), cnt.cpu().numpy()
+    t = O.tables(2000)
+    for i in range(n):
+        a, b = O.extract(lefts[i], want_pyramid=True), O.extract(rights[i], want_pyramid=True)
+        rur, rdp = O.compute_stereo_matches(a, b, t["scale"], t["inv_scale"], 375, BF, B)
+        assert urh[i, :ch[i]].tobytes() == rur.tobytes() and dph[i, :ch[i]].tobytes() == rdp.tobytes()
