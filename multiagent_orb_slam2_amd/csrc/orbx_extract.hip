@@ -161,6 +161,17 @@ __device__ __forceinline__ void resize_window(const uint8_t* __restrict__ row, i
     }
 }
 
+// Branch-free form for rows of >= 8 bytes: one 8-byte load clamped inside the row, shifted so that byte i is column
+// xb + i (columns past the row end read as 0 and are never selected).  Every lane loads, so a wave's loads for
+// several rows issue back to back instead of one divergent branch (and one wait) per row.
+__device__ __forceinline__ void resize_window8(const uint8_t* __restrict__ row, int xb, int sw, uint32_t& lo, uint32_t& hi) {
+    const int xc = min(xb, sw - 8);
+    uint64_t v;
+    __builtin_memcpy(&v, row + xc, 8);
+    v >>= 8 * (xb - xc);
+    lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+}
+
 __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
                                                  size_t src_step, size_t src_istride, int sw, int dst_off, int dw, int dh,
                                                  ResizeVec t, int nstrips, int nbands, int batch) {
@@ -181,8 +192,46 @@ __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size
     const bool full = x + 4 <= dw;
     const uint8_t* S = src + img * src_istride;
     uint8_t* D = pyr + img * pyr_stride + dst_off;
-    const int y1 = min((band + 1) * kResizeBand, dh);
-    for (int y = band * kResizeBand; y < y1; ++y) {
+    const int y0 = band * kResizeBand, y1 = min(y0 + kResizeBand, dh);
+    if (sw >= 8) {
+        // every source window of the band's rows first (one memory round trip per wave), then the arithmetic
+        const int ny = y1 - y0;
+        int4 yr[kResizeBand];
+        uint32_t lo[2 * kResizeBand], hi[2 * kResizeBand];
+#pragma unroll
+        for (int r = 0; r < kResizeBand; ++r) yr[r] = t.yrow[y0 + min(r, ny - 1)];
+#pragma unroll
+        for (int r = 0; r < kResizeBand; ++r) {
+            resize_window8(S + (size_t)yr[r].x * src_step, xb, sw, lo[2 * r], hi[2 * r]);
+            resize_window8(S + (size_t)yr[r].y * src_step, xb, sw, lo[2 * r + 1], hi[2 * r + 1]);
+        }
+        const uint32_t sl[4] = {sel.x, sel.y, sel.z, sel.w}, cf[4] = {coef.x, coef.y, coef.z, coef.w};
+#pragma unroll
+        for (int r = 0; r < kResizeBand; ++r) {
+            if (r >= ny) break;
+            uint32_t packed = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const u16x2 c = __builtin_bit_cast(u16x2, cf[k]);
+                const uint32_t hv0 = __builtin_amdgcn_udot2(
+                    __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi[2 * r], lo[2 * r], sl[k])), c, 0u, false);
+                const uint32_t hv1 = __builtin_amdgcn_udot2(
+                    __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi[2 * r + 1], lo[2 * r + 1], sl[k])), c, 0u, false);
+                const uint32_t v = min((hv0 * (uint32_t)yr[r].z + hv1 * (uint32_t)yr[r].w + (1u << 21)) >> 22, 255u);
+                packed |= v << (8 * k);
+            }
+            uint8_t* o = D + (size_t)(y0 + r) * dw + x;
+            if (full) {
+                __builtin_memcpy(o, &packed, 4);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (x + k < dw) o[k] = (uint8_t)(packed >> (8 * k));
+            }
+        }
+        return;
+    }
+    for (int y = y0; y < y1; ++y) {          // source rows narrower than 8 bytes
         const int4 yr = t.yrow[y];
         uint32_t l0, h0, l1, h1;
         resize_window(S + (size_t)yr.x * src_step, xb, sw, fast, l0, h0);
@@ -219,7 +268,10 @@ __device__ __forceinline__ s16x2 as_s2(uint32_t v) { return __builtin_bit_cast(s
 __device__ __forceinline__ s16x2 pmin(s16x2 a, s16x2 b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ s16x2 pmax(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
 
-constexpr int kPairStride = 48;   // dwords per LDS pair-image row (== 16 mod 32: rows 16 pairs apart hit other banks)
+// Dwords per LDS pair-image row, per launch (template): 24 when the launch's widest cell ROI fits (the KITTI/EuRoC
+// case: ROI <= 46 columns), else 48.  A 32-lane half of a ds_read_b32 covers two ROI rows of 16 pairs; with 64 banks
+// any stride in [16, 48] mod 64 keeps the two rows on disjoint banks.  The narrow form cuts the workgroup's LDS from
+// ~25 KB to ~16 KB: 8 resident workgroups per CU (32 waves) instead of 6.
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
@@ -231,6 +283,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // a 4-byte-aligned ds_read_b32 with a compile-time offset (2-byte-misaligned 32-bit LDS reads measured
 // ~2x slower on gfx950).  The reads are explicit (inline asm) so the compiler does not merge neighbours
 // into misaligned b64/b128 reads.
+template <int kPairStride>
 __device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, const uint32_t* __restrict__ O, int y, int j) {
     const uint32_t* eb = E + (y - 3) * kPairStride + j;   // row y-3, pair index j; offsets >= 0
     const uint32_t* ob = O + (y - 3) * kPairStride + j;
@@ -269,6 +322,7 @@ __device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, con
 // Compass pre-test for a pixel pair: every arc of 9 contains two compass taps 4 apart (0/4, 4/8, 8/12 or
 // 12/0), so "corner at t" (some arc with all d > t, or all d < -t) implies max over those four pairs of
 // min(d_k, d_k+4) > t, or min of max < -t.  A pixel failing it has s < t.  Returns 2 bits (pixel x, x+1).
+template <int kPairStride>
 __device__ __forceinline__ int fast_pretest2(const uint32_t* __restrict__ E, const uint32_t* __restrict__ O, int y, int j,
                                              int t) {
     const uint32_t* eb = E + (y - 3) * kPairStride + j;
@@ -320,7 +374,7 @@ __device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, 
 // pixel pairs are dword aligned (det column x at map column x + 2, pad ring at columns 1 and Wd + 2) +
 // survivor list + kept-pixel key lists.
 // Byte offset of the three counters after the dynamic LDS arrays of k_fast_cells (16-byte aligned).
-__host__ __device__ __forceinline__ int fast_counter_off(int R, int Cc) {
+__host__ __device__ __forceinline__ int fast_counter_off(int R, int Cc, int kPairStride) {
     const int b = 2 * R * kPairStride * 4 + 4 * (((R - 4) * Cc + 1) / 2) + 2 * ((R * Cc / 2 + 65) & ~1) + 2 * 2 * (R * Cc / 4 + 32);
     return (b + 15) & ~15;
 }
@@ -343,6 +397,7 @@ __device__ __forceinline__ FastRoi fast_roi(int W, int H, int ln) {
     return f;
 }
 
+template <int kPairStride>
 __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                     const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
                                                     int iniTh, int minTh, uint32_t* __restrict__ cand_xy,
@@ -359,7 +414,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     const int kmax = max_rows * max_cols / 4 + 32;           // >= strict-NMS bound ceil(wd/2)*ceil(hd/2)
     uint16_t* kini = list + ((max_rows * max_cols / 2 + 65) & ~1);
     uint16_t* kmin = kini + kmax;
-    int* counters = reinterpret_cast<int*>(fsm) + fast_counter_off(max_rows, max_cols) / 4;
+    int* counters = reinterpret_cast<int*>(fsm) + fast_counter_off(max_rows, max_cols, kPairStride) / 4;
     int& nsurv = counters[0];
     int& nki = counters[1];
     int& nkm = counters[2];
@@ -425,7 +480,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
             const int dq = (int)blockDim.x / PR, dj = (int)blockDim.x - dq * PR;
             for (int q = tid, rr = rr0, j = j0; q < NP; q += blockDim.x) {
                 const bool two = 2 * j + 1 < Wd;
-                const int pt = fast_pretest2(E, O, rr + 3, j, tp) & (two ? 3 : 1);
+                const int pt = fast_pretest2<kPairStride>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
                 *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
                 const uint64_t bm = __ballot(pt != 0);
                 int wbase = 0;
@@ -441,7 +496,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
                 // 3. full closed-form scores of the surviving pairs only
                 for (int i = tid; i < ns; i += blockDim.x) {
                     const int rr = list[i] >> 8, j = list[i] & 0xff;
-                    const s16x2 s2 = fast_score2(E, O, rr + 3, j);
+                    const s16x2 s2 = fast_score2<kPairStride>(E, O, rr + 3, j);
                     *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
                 }
                 __syncthreads();
@@ -1025,6 +1080,9 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {   // OpenCV 
 }
 
 struct SlotTable { int out_off[kMaxLevels]; };   // LevelDev::out_off per level, as a kernel argument
+constexpr int kBriefR = 18;                      // max |rotated pattern offset|: round(hypot(-13, -13)) = 18
+constexpr int kBriefRow = 40;                    // LDS bytes per window row (5 x 8-byte chunks)
+constexpr int kBriefWin = (2 * kBriefR + 1) * kBriefRow;
 
 __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                   size_t pyr_stride, const LevelDev* __restrict__ levels, int nlevels,
@@ -1032,6 +1090,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                   int out_stride, const int* __restrict__ level_cnt,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
                                                   int capacity, int total_slots, int batch, Src0 s0, SlotTable tab) {
+    __shared__ __attribute__((aligned(16))) uint8_t brief_lds[4 * kBriefWin];
     const int nbx = (total_slots + 3) / 4;                    // 4 slots (waves) per workgroup
     const int item = xcd_item(xcd_chunk(nbx * batch));       // keypoints of one image on one XCD
     if (item >= nbx * batch) return;
@@ -1059,6 +1118,22 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
 
     const uint32_t xy = lvl_xy[(size_t)img * out_stride + L.out_off + i];
     const int cx = (int)(xy & 0xffff), cy = (int)(xy >> 16);
+    // --- the blurred 37 x 37 window the BRIEF tests can touch (|rotated offset| <= 18), loaded now, beside the
+    //     IC_Angle loads, into this wave's LDS slice (rows of kBriefRow bytes): the tests then read LDS, so the
+    //     angle -> BRIEF dependency costs no second memory round trip.  Keypoints lie >= 19 px inside the level
+    //     (FAST window :789-797), so rows cy-18 .. cy+18 exist; a row's bytes past cx+18 are never read.
+    const uint8_t* B = blur + img * pyr_stride + L.pyr_off;
+    const int step = L.w;
+    uint8_t* win = brief_lds + (threadIdx.x >> 6) * kBriefWin;
+    uint64_t wv[3];
+    {
+        const uint8_t* w0 = B + (size_t)(cy - kBriefR) * step + (cx - kBriefR);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int q = ln + 64 * k, r = min(q / 5, 2 * kBriefR), c = q - (q / 5) * 5;   // 37 rows x 5 chunks
+            __builtin_memcpy(&wv[k], w0 + (size_t)r * step + 8 * c, 8);
+        }
+    }
     // --- IC_Angle (:77-104): m10 = sum u*I, m01 = sum v*I over the radius-15 disc
     int pstride;
     const uint8_t* P = level_pixels(pyr, pyr_stride, L, lvl, img, s0, pstride);
@@ -1085,6 +1160,12 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
             m01 += v * x;
         }
     }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int q = ln + 64 * k;
+        if (q < 5 * (2 * kBriefR + 1)) *reinterpret_cast<uint64_t*>(win + (q / 5) * kBriefRow + 8 * (q % 5)) = wv[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");         // other lanes' window bytes before the tests read
     m10 = wave_sum_dpp(m10);
     m01 = wave_sum_dpp(m01);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
@@ -1094,9 +1175,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     const float ang = __fmul_rn(angle, toRad);
     float a, b;
     orbx_sincos_brief(ang, &a, &b);   // == (float)cos/sin((double)ang) for every possible ang (orbx_sincos.h)
-    const uint8_t* B = blur + img * pyr_stride + L.pyr_off;
-    const uint8_t* center = B + (size_t)cy * L.w + cx;
-    const int step = L.w;
+    const uint8_t* center = win + kBriefR * kBriefRow + kBriefR;    // LDS written by this wave (in-order LDS queue)
     uint64_t bits[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -1108,7 +1187,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
             const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
             const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
             const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
-            vals[e] = center[__float2int_rn(ry) * step + __float2int_rn(rx)];
+            vals[e] = center[__float2int_rn(ry) * kBriefRow + __float2int_rn(rx)];
         }
         bits[g] = __ballot(vals[0] < vals[1]);
     }
@@ -1155,6 +1234,8 @@ struct Extractor {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_join = nullptr;
     int pipeline = 1;         // ORBX_PIPELINE: 1 two streams (above), 0 every launch in order on the launch stream
+    int qt_split = 1;         // ORBX_QT_SPLIT: 1 level-0 quadtree on the side stream, 0 one quadtree launch (all levels)
+    hipEvent_t ev_fast0 = nullptr;   // side: FAST level 0 done (qt_split 0: the launch stream's quadtree waits on it)
 
     // geometry for the reserved size
     int rows = 0, cols = 0, max_batch = 0;
@@ -1165,12 +1246,12 @@ struct Extractor {
     int cand_stride = 0;      // candidate slots per image
     int out_stride = 0;       // quadtree output slots per image
     int node_cap = 0;
-    int cell_max_rows = 0, cell_max_cols = 0;
+    struct FastLaunch { int cell0, n, R, C, ps; size_t lds; };
+    FastLaunch fast_launch[2] = {};   // k_fast_cells over level 0 / levels >= 1
     int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
     size_t qt_lds = 0;        // k_quadtree dynamic LDS bytes
     int out_capacity = 0;     // max keypoints per image
-    int fast_resident = 0;    // k_fast_cells workgroups resident on the whole device (persistent grid)
 
     // device buffers
     LevelDev* d_levels = nullptr;
@@ -1296,9 +1377,9 @@ void Extractor::free_buffers() {
 
 static size_t qt_lds_bytes(int cap, int scan_cap);
 
-static size_t fast_lds_bytes(const Extractor* e) {
+static size_t fast_lds_bytes(int R, int C, int ps) {
     // E + O pair images, int16 score map, u16 survivor list, two u16 kept-pixel key lists, 3 counters
-    return (size_t)fast_counter_off(e->cell_max_rows, e->cell_max_cols) + 16;
+    return (size_t)fast_counter_off(R, C, ps) + 16;
 }
 
 template <typename T>
@@ -1385,9 +1466,21 @@ int Extractor::configure(int r, int c, int batch) {
             for (int tx = 0; tx < (L.w + kBlurStrip - 1) / kBlurStrip; ++tx) tilev.push_back(BlurTile{l, tx, ty, 0});
     }
     ORBX_REQUIRE(cap < 32768 && cap < (1 << 20), ORBX_ERR_UNSUPPORTED, "node capacity %d too large", cap);
-    cell_max_rows = 8; cell_max_cols = 8;
-    for (const CellDev& cd : cellv) { cell_max_rows = std::max(cell_max_rows, cd.H); cell_max_cols = std::max(cell_max_cols, cd.W); }
-    ORBX_REQUIRE((cell_max_cols + 2) / 2 <= kPairStride, ORBX_ERR_UNSUPPORTED, "cell too wide");
+    // k_fast_cells launches: level 0 (side stream) and levels 1..n-1, each sized for its own widest / tallest ROI
+    for (int k = 0; k < 2; ++k) {
+        FastLaunch& f = fast_launch[k];
+        f.cell0 = k == 0 ? 0 : lv[0].cell_end;
+        f.n = k == 0 ? lv[0].cell_end : (int)cellv.size() - lv[0].cell_end;
+        f.R = 8; f.C = 8;
+        for (int i = f.cell0; i < f.cell0 + f.n; ++i) { f.R = std::max(f.R, cellv[i].H); f.C = std::max(f.C, cellv[i].W); }
+        const int pairs = 2 * ((f.C + 5) / 4);                // E/O dwords one ROI row writes (8-byte chunks)
+        ORBX_REQUIRE(pairs <= 48, ORBX_ERR_UNSUPPORTED, "cell too wide");
+        f.ps = pairs <= 24 ? 24 : 48;
+        f.lds = fast_lds_bytes(f.R, f.C, f.ps);
+        if (f.lds > 64 * 1024)
+            ORBX_HIP(hipFuncSetAttribute(f.ps == 24 ? (const void*)k_fast_cells<24> : (const void*)k_fast_cells<48>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.lds));
+    }
     int scap = cap;
     for (const LevelDev& L : lv) scap = std::max(scap, std::max(L.cell_end - L.cell_begin, L.nIni));
     scan_cap = scap + 1;
@@ -1397,15 +1490,6 @@ int Extractor::configure(int r, int c, int batch) {
         qt_lds = lds;
         if (lds > 64 * 1024)
             ORBX_HIP(hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    }
-    {
-        int per_cu = 0, cus = 0;
-        const size_t lds = fast_lds_bytes(this);
-        if (lds > 64 * 1024)
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        ORBX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_fast_cells, 256, lds));
-        ORBX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        fast_resident = std::max(per_cu, 1) * std::max(cus, 1);
     }
     pyr_size = (poff + 255) & ~(size_t)255;
     cand_stride = std::max(cand, 1);
@@ -1544,17 +1628,16 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     hipStream_t side = e->pipeline ? e->side : s;
     auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : s); };
     const int ncells = (int)e->cellv.size();
-    const int c0 = nl > 0 ? e->lv[0].cell_end : 0;                 // cells of level 0: [0, c0)
     int t0 = 0;                                                     // blur tiles of level 0: [0, t0)
     while (t0 < (int)e->tilev.size() && e->tilev[t0].level == 0) ++t0;
     const int nt = (int)e->tilev.size();
     QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
-    auto fast = [&](hipStream_t q, int cell0, int n) {
-        if (n <= 0) return;
-        hipLaunchKernelGGL(k_fast_cells, dim3(kXcds * xcd_chunk(n * batch)), dim3(256), fast_lds_bytes(e), q, e->d_pyr, ps,
+    auto fast = [&](hipStream_t q, const Extractor::FastLaunch& f) {
+        if (f.n <= 0) return;
+        auto kern = f.ps == 24 ? k_fast_cells<24> : k_fast_cells<48>;
+        hipLaunchKernelGGL(kern, dim3(kXcds * xcd_chunk(f.n * batch)), dim3(256), f.lds, q, e->d_pyr, ps,
                            e->d_levels, e->d_cells, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s, e->cand_stride,
-                           e->d_cell_cnt, ncells, batch, e->fast_stop_after, s0, e->cell_max_rows, e->cell_max_cols,
-                           cell0, n);
+                           e->d_cell_cnt, ncells, batch, e->fast_stop_after, s0, f.R, f.C, f.cell0, f.n);
     };
     auto quadtree = [&](hipStream_t q, int lvl0, int n) {
         if (n <= 0) return;
@@ -1593,9 +1676,11 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     if (side == s) resize_chain();                                  // serial: every stage contiguous on one stream
     // side stream, level 0 (reads only the caller's images)
     mark(6);
-    fast(side, 0, c0);
+    fast(side, e->fast_launch[0]);
     mark(7);
-    quadtree(side, 0, nl > 0 ? 1 : 0);
+    const bool split = e->qt_split || side == s;
+    if (split) quadtree(side, 0, nl > 0 ? 1 : 0);
+    else ORBX_HIP(hipEventRecord(e->ev_fast0, side));
     mark(8);
     blur(side, 0, t0);
     if (side != s) {
@@ -1607,9 +1692,14 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     mark(9);
     if (side != s) ORBX_HIP(hipEventRecord(e->ev_join, side));
     mark(10);                                                       // launch stream: FAST, DistributeOctTree 1..nl-1
-    fast(s, c0, ncells - c0);
+    fast(s, e->fast_launch[1]);
     mark(2);
-    quadtree(s, 1, nl - 1);
+    if (split) {
+        quadtree(s, 1, nl - 1);
+    } else {
+        ORBX_HIP(hipStreamWaitEvent(s, e->ev_fast0, 0));
+        quadtree(s, 0, nl);
+    }
     mark(3);
     if (side != s) ORBX_HIP(hipStreamWaitEvent(s, e->ev_join, 0));
     mark(4);
@@ -1673,11 +1763,13 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     hipError_t he = hipSetDevice(device);
     e->own_stream = true;
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-    // ORBX_SIDE_PRIORITY (A/B only): HIP priority of the side stream; default normal
-    const int side_prio = std::getenv("ORBX_SIDE_PRIORITY") ? std::atoi(std::getenv("ORBX_SIDE_PRIORITY")) : 0;
+    // High priority for the side stream: its level-0 quadtree (128 long-lived workgroups) must not queue behind the
+    // launch stream's FAST grid (measured: 35.1k -> 37.6k frames/s).  ORBX_SIDE_PRIORITY overrides (A/B).
+    const int side_prio = std::getenv("ORBX_SIDE_PRIORITY") ? std::atoi(std::getenv("ORBX_SIDE_PRIORITY")) : -1;
     if (he == hipSuccess) he = hipStreamCreateWithPriority(&e->side, hipStreamNonBlocking, side_prio);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pyr, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fast0, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
     if (he != hipSuccess) {
         set_error("stream create: %s", hipGetErrorString(he));
@@ -1686,6 +1778,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     }
     if (const char* ab = std::getenv("ORBX_FAST_ABLATE")) e->fast_stop_after = std::atoi(ab);
     if (const char* pl = std::getenv("ORBX_PIPELINE")) e->pipeline = std::atoi(pl) != 0;
+    if (const char* qs = std::getenv("ORBX_QT_SPLIT")) e->qt_split = std::atoi(qs) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
         return st;
@@ -1706,6 +1799,7 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     if (e->side) (void)hipStreamDestroy(e->side);
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
     if (e->ev_pyr) (void)hipEventDestroy(e->ev_pyr);
+    if (e->ev_fast0) (void)hipEventDestroy(e->ev_fast0);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     delete e;
     return ORBX_OK;
