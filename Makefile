@@ -23,3 +23,10 @@ clean:
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean
+
+# Diagnostics build: k_quadtree stage stamps (orbx_debug_qt_prof), scripts/qt_prof.py.  Not the product library.
+qtprof: $(OBJS)
+	mkdir -p build/qtprof
+	$(HIPCC) $(HIPFLAGS) -DORBX_QT_PROF -c $(SRC)/orbx_extract.hip -o build/qtprof/orbx_extract.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/qtprof/liborbx.so build/qtprof/orbx_extract.o $(filter-out $(SRC)/orbx_extract.o,$(OBJS)) -ldl
+.PHONY: qtprof

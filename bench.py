@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage event timing")
     ap.add_argument("--no-c3", dest="c3", action="store_false", help="skip the C3 2000x2000 all-pairs block")
+    ap.add_argument("--sync-each", action="store_true",
+                    help="diagnostics: synchronise after every timed step (host_enqueue_* = pure host cost, no back-pressure)")
     return ap.parse_args()
 
 
@@ -397,6 +399,8 @@ def main():
         th = time.perf_counter()
         step(time_stereo=not args.no_timing)
         host_s += time.perf_counter() - th               # host time to enqueue one step (no sync inside)
+        if args.sync_each:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -768,14 +768,35 @@ __device__ __forceinline__ int rank_asc(const int* cc, int q) {
     return r;
 }
 
+#ifdef ORBX_QT_PROF
+// Diagnostics build only (make qtprof): wall-clock stamps of thread 0 of the (first level, image 0) workgroup at the
+// stage boundaries of k_quadtree, read back by orbx_debug_qt_prof.
+__device__ unsigned long long g_qtprof[2][64];
+#define QTP(tag)                                                                                                     \
+    do {                                                                                                             \
+        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && qtp_n < 32) {                                 \
+            g_qtprof[lvl0 ? 1 : 0][2 * qtp_n] = wall_clock64();                                                      \
+            g_qtprof[lvl0 ? 1 : 0][2 * qtp_n + 1] = (tag);                                                           \
+        }                                                                                                            \
+        ++qtp_n;                                                                                                     \
+    } while (0)
+#else
+#define QTP(tag) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
                                                          const uint32_t* __restrict__ cand_xy, const uint8_t* __restrict__ cand_s,
                                                          int cand_stride, const int* __restrict__ cell_cnt, int ncells,
                                                          QtScratch qs, uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r,
                                                          int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
-                                                         int scan_cap, int* __restrict__ err, int lvl0) {
+                                                         int scan_cap, int* __restrict__ err, int lvl0, int key_lds_off,
+                                                         int key_lds_cap) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int lvl = lvl0 + (int)blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
+#ifdef ORBX_QT_PROF
+    int qtp_n = 0;
+#endif
+    QTP(0);
     const LevelDev L = levels[lvl];
     // LDS layout
     int* A_xr = smem;              // x0 | x1 << 16
@@ -796,29 +817,64 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
     const int ncl = L.cell_end - L.cell_begin;
 
     // ---- 1. compact the level's cell candidates into reference order (cell row-major, then FAST order)
-    for (int i = tid; i < ncl; i += T) sa[i] = cell_cnt[(size_t)img * ncells + L.cell_begin + i];
+    // (per cell: count -> sa, slot offset -> sb; all loads independent)
+    for (int i = tid; i < ncl; i += T) {
+        sa[i] = cell_cnt[(size_t)img * ncells + L.cell_begin + i];
+        sb[i] = cells[L.cell_begin + i].slot_off;
+    }
     __syncthreads();
     const int K = block_scan_array(sa, ncl, tmp);
-    uint32_t* kxy = qs.key_xy + (size_t)img * cand_stride + L.cand_off;
+    // Every pass walks all K keys two or three times: they live in LDS when the level's keys fit the launch's key
+    // region (the common case: ~2-4k keys at level 0 of a KITTI frame), in the HBM scratch otherwise.  The pointers
+    // are generic, so one code path serves both (flat loads resolve to LDS or global at run time).
+    uint32_t* kxy;
+    int16_t* kn;
+    if (K <= key_lds_cap) {
+        kxy = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(smem) + key_lds_off);
+        kn = reinterpret_cast<int16_t*>(kxy + key_lds_cap);
+    } else {
+        kxy = qs.key_xy + (size_t)img * cand_stride + L.cand_off;
+        kn = qs.key_node + (size_t)img * cand_stride + L.cand_off;
+    }
     uint8_t* kr = qs.key_r + (size_t)img * cand_stride + L.cand_off;
-    int16_t* kn = qs.key_node + (size_t)img * cand_stride + L.cand_off;
     const int minB = kEdge - 3;
+    // owner cell of every key (LDS / scratch writes only), then one flat gather over the keys with every load
+    // independent: a walk cell by cell chains three dependent HBM loads per cell (~150 us at level 0)
+    for (int c = tid; c < ncl; c += T) {
+        const int b = sa[c], e = (c + 1 < ncl) ? sa[c + 1] : K;
+        for (int k = b; k < e; ++k) kn[k] = (int16_t)c;
+    }
+    __syncthreads();
     {
-        const int w = tid >> 6, nw = T >> 6, ln = lane_id();
-        for (int c = w; c < ncl; c += nw) {
-            const CellDev cd = cells[L.cell_begin + c];
-            const int n = cell_cnt[(size_t)img * ncells + L.cell_begin + c];
-            const uint32_t* sxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
-            const uint8_t* ss = cand_s + (size_t)img * cand_stride + cd.slot_off;
-            for (int e = ln; e < n; e += kWave) {
-                const uint32_t xy = sxy[e];
-                kxy[sa[c] + e] = ((xy & 0xffff) - minB) | (((xy >> 16) - minB) << 16);
-                kr[sa[c] + e] = ss[e];
+        const uint32_t* sxy = cand_xy + (size_t)img * cand_stride;
+        const uint8_t* ss = cand_s + (size_t)img * cand_stride;
+        constexpr int U = 4;
+        for (int k0 = tid; k0 < K; k0 += U * T) {
+            uint32_t xy[U];
+            uint8_t r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = k0 + u * T;
+                if (k < K) {
+                    const int c = kn[k];
+                    const int src = sb[c] + (k - sa[c]);
+                    xy[u] = sxy[src];
+                    r[u] = ss[src];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = k0 + u * T;
+                if (k < K) {
+                    kxy[k] = ((xy[u] & 0xffff) - minB) | (((xy[u] >> 16) - minB) << 16);
+                    kr[k] = r[u];
+                }
             }
         }
     }
     __syncthreads();
 
+    QTP(1);
     // ---- 2. root nodes (:543-585)
     const int nIni = L.nIni;
     const float hX = L.hX;
@@ -855,8 +911,10 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
 
     const int N = L.N;
     bool phase2 = false, finished = false;
+    QTP(2);
     while (!finished) {
         const int prev = n;
+        QTP(10 + phase2);
         // -- child counts of every expandable node (phase 1 splits all of them, phase 2 needs their sizes)
         for (int i = tid; i < 4 * n; i += T) cc[i] = 0;
         __syncthreads();
@@ -868,6 +926,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             }
         }
         __syncthreads();
+        QTP(20);
 
         if (!phase2) {
             // ---------------- phase 1 pass (:606-665)
@@ -895,6 +954,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             const int U = block_scan_array(sb, n, tmp);     // sb = survivors before node i
             const int nToExpand = misc[0];
             const int nn = C + U;
+            QTP(30);
             if (nn > cap) { if (tid == 0) atomicOr(err, 1); finished = true; break; }
             for (int i = tid; i < n; i += T) {
                 const int nch = base[i];
@@ -933,6 +993,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             for (int i = tid; i < nn; i += T) { A_xr[i] = B_xr[i]; A_yr[i] = B_yr[i]; A_cnt[i] = B_cnt[i]; A_seq[i] = B_seq[i]; }
             n = nn;
             __syncthreads();
+            QTP(50);
             if (n >= N || n == prev) finished = true;              // :669-672
             else if (n + nToExpand * 3 > N) phase2 = true;         // :673
         } else {
@@ -964,6 +1025,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                 }
             }
             // processing order p = 0.. is descending key order; delta_p = children_p - 1
+            QTP(31);
             for (int p = tid; p < nV; p += T) {
                 const int i = (int)(sk[nV - 1 - p] & 0xfffff);
                 const int* c4 = cc + 4 * i;
@@ -995,6 +1057,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             __syncthreads();
             const int U = block_scan_array(sb, n, tmp);
             const int nn = Cn + U;
+            QTP(32);
             if (nn > cap) { if (tid == 0) atomicOr(err, 1); finished = true; break; }
             for (int i = tid; i < n; i += T) {
                 if (base[i] >= 0) {
@@ -1031,10 +1094,12 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             for (int i = tid; i < nn; i += T) { A_xr[i] = B_xr[i]; A_yr[i] = B_yr[i]; A_cnt[i] = B_cnt[i]; A_seq[i] = B_seq[i]; }
             n = nn;
             __syncthreads();
+            QTP(51);
             if (n >= N || n == prev) finished = true;              // :734-735
         }
     }
 
+    QTP(80);
     // ---- retain the first maximum-response key of every node (:742-760)
     for (int i = tid; i < n; i += T) sk[i] = 0ull;
     __syncthreads();
@@ -1053,6 +1118,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
         orr[i] = kr[k];
     }
     if (tid == 0) level_cnt[img * nlevels + lvl] = nout;
+    QTP(90);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1250,7 +1316,8 @@ struct Extractor {
     FastLaunch fast_launch[2] = {};   // k_fast_cells over level 0 / levels >= 1
     int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
-    size_t qt_lds = 0;        // k_quadtree dynamic LDS bytes
+    size_t qt_lds = 0;        // k_quadtree dynamic LDS bytes of the node arrays (the key region follows at this offset)
+    int qt_keys[2] = {0, 0};  // LDS-resident key capacity of the level-0 launch / the levels 1..n-1 launch
     int out_capacity = 0;     // max keypoints per image
 
     // device buffers
@@ -1485,11 +1552,24 @@ int Extractor::configure(int r, int c, int batch) {
     for (const LevelDev& L : lv) scap = std::max(scap, std::max(L.cell_end - L.cell_begin, L.nIni));
     scan_cap = scap + 1;
     {
-        const size_t lds = qt_lds_bytes(cap, scan_cap);
+        const size_t lds = (qt_lds_bytes(cap, scan_cap) + 15) & ~(size_t)15;
         ORBX_REQUIRE(lds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "quadtree LDS %zu B exceeds 160 KiB", lds);
         qt_lds = lds;
-        if (lds > 64 * 1024)
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        // LDS key region (6 B per key: xy + node) per launch: level 0 (one workgroup per image, ~2-4k keys on a
+        // KITTI frame) and levels >= 1 (seven workgroups per image, ~1-1.5k keys at level 1), each bounded by the
+        // largest candidate count its levels can produce; levels whose keys overflow it use the HBM scratch
+        int lcap[2] = {0, 0};
+        for (int l = 0; l < nlevels; ++l) lcap[l ? 1 : 0] = std::max(lcap[l ? 1 : 0], lv[l].cand_cap);
+        const int want[2] = {8192, 2048};
+        size_t maxl = lds;
+        for (int k = 0; k < 2; ++k) {
+            int kc = std::min(want[k], lcap[k]);
+            kc = (int)std::min<size_t>((size_t)kc, (160 * 1024 - lds) / 6) & ~7;
+            qt_keys[k] = std::max(kc, 0);
+            maxl = std::max(maxl, lds + 6 * (size_t)qt_keys[k]);
+        }
+        if (maxl > 64 * 1024)
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxl));
     }
     pyr_size = (poff + 255) & ~(size_t)255;
     cand_stride = std::max(cand, 1);
@@ -1641,9 +1721,13 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     };
     auto quadtree = [&](hipStream_t q, int lvl0, int n) {
         if (n <= 0) return;
-        hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds, q, e->d_levels, e->d_cells, e->d_cand_xy,
-                           e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy, e->d_lvl_r,
-                           e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err, lvl0);
+        // key capacity: the level-0 region when the launch covers level 0 alone, else the levels >= 1 region (a launch
+        // over every level, qt_split 0, takes the smaller one; level 0 then overflows to HBM as before)
+        const int kc = (lvl0 == 0 && n == 1) ? e->qt_keys[0] : e->qt_keys[1];
+        hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds + 6 * (size_t)kc, q, e->d_levels, e->d_cells,
+                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
+                           e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err, lvl0,
+                           (int)e->qt_lds, kc);
     };
     auto blur = [&](hipStream_t q, int tile0, int n) {
         if (n <= 0) return;
@@ -2014,6 +2098,14 @@ int orbx_extractor_enable_timing(orbx_extractor* e, int enable) {
 }
 int orbx_extractor_stage_count(void) { return ST_COUNT; }
 const char* orbx_extractor_stage_name(int s) { return (s >= 0 && s < ST_COUNT) ? kStageNames[s] : ""; }
+#ifdef ORBX_QT_PROF
+int orbx_debug_qt_prof(unsigned long long* out) {   // 2 x 64 stamps (diagnostics build only)
+    ORBX_HIP(hipDeviceSynchronize());
+    ORBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_qtprof), sizeof(orbx::g_qtprof)));
+    return ORBX_OK;
+}
+#endif
+
 int orbx_extractor_stage_times(orbx_extractor* e, double* ms, int* calls) {
     ORBX_REQUIRE(e && ms, ORBX_ERR_ARG, "null argument");
     ORBX_HIP(hipSetDevice(e->device));
