@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage event timing")
     ap.add_argument("--no-c3", dest="c3", action="store_false", help="skip the C3 2000x2000 all-pairs block")
+    ap.add_argument("--diag-skip", default="", help="diagnostics only (not the metric): comma list of stereo,keyframes "
+                                                     "to leave out of the step")
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostics: synchronise after every timed step (host_enqueue_* = pure host cost, no back-pressure)")
     return ap.parse_args()
@@ -322,6 +324,7 @@ def main():
     frame_no = [chunk.start]
     n_step = [0]
 
+    skip = set(filter(None, args.diag_skip.split(",")))
     stereo_ms = []
     kf_ms = []
     host_split = [0.0, 0.0]                            # host enqueue seconds: front-end, keyframe path
@@ -336,6 +339,9 @@ def main():
         extracted = torch.cuda.Event()
         extracted.record(stream)
         pyr = ex.pyramid_device()                      # this call's pyramid set (a slot of the ring of 2)
+        if "stereo" in skip:
+            n_step[0] += 1
+            return None, None
         stereo_stream.wait_event(extracted)
         with torch.cuda.stream(stereo_stream):         # outputs allocated on (and owned by) the stereo queue
             if time_stereo:
@@ -351,6 +357,9 @@ def main():
         handoff = torch.cuda.Event()
         handoff.record(stereo_stream)
         h1 = time.perf_counter()
+        if "keyframes" in skip:
+            n_step[0] += 1
+            return bi, bd
         # keyframe path: rows of this step's batch -> BoW -> packets -> all-gather (N>1) into the ring -> sequential
         # DetectLoopCandidates -> batched SearchByBoW; MapPoint-valid = stereo depth > 0
         kf_stream.wait_event(handoff)
@@ -485,6 +494,8 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(lefts[:16], rights[:16], cfg, S.synthetic_vocabulary(2024, k=10, L=6), n_kf,
                                            args.cpu_seconds)
+    if skip:
+        out["diag_skip"] = sorted(skip)
     gate, _ = engine.stats()
     out["fusion_gate_passed_per_step"] = round(gate / (args.steps + args.warmup + STORE_STEPS), 2)
     engine.check()

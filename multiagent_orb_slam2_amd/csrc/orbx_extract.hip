@@ -551,6 +551,248 @@ __global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Band form of the cell FAST: one workgroup per (image, band), a band = up to G consecutive cells of one cell row
+// of a level (same iniY / ROI height).  The cells' ROIs overlap by 6 columns, so the band loads ONE ROI (x0 of the
+// first cell .. end of the last) into the pair images; pre-test and closed-form scores run over the band's whole
+// detection width, which is the concatenation of the cells' detection windows ([iniX+3, iniX+wCell+3) each).
+// Scores are position independent; only the NMS sees the cell: OpenCV's FAST on a cell ROI treats pixels outside
+// that cell's detection window as 0, so a neighbour across a cell boundary is masked out (-1 never blocks a kept
+// score s >= 1).  Kept pixels go to their own cell's key lists; the iniTh -> minTh fallback and the row-major
+// output order are per cell, as in k_fast_cells.  G cells share the load latency and the five barriers.
+// ---------------------------------------------------------------------------------------------
+struct BandDev {
+    int level, cell0, ncell;   // cells [cell0, cell0 + ncell) of one cell row, left to right
+    int x0, y0, W, H;          // band ROI in level coordinates (first cell's iniX / iniY, width to the last cell's end)
+    int wcell;                 // detection width of every cell but possibly the last (ceil(width / nCols))
+};
+constexpr int kBandMaxCells = 8;
+
+struct BandLds {               // byte offsets inside the dynamic LDS of k_fast_band
+    int o_sc, o_list, o_keys, o_meta, o_cnt, bytes;
+};
+// rows: max ROI rows; sw: max score-map row (int16); np: max pairs; kmax: max keys per cell and threshold; ps: dwords
+// per pair-image row
+__host__ __device__ __forceinline__ BandLds band_lds(int rows, int sw, int np, int kmax, int ps, int gmax) {
+    BandLds b;
+    int o = 2 * rows * ps * 4;                                  // E, O
+    b.o_sc = o;   o += ((rows - 4) * sw * 2 + 15) & ~15;        // score map (Hd + 2 rows)
+    b.o_list = o; o += (np * 2 + 15) & ~15;                     // survivor pairs
+    b.o_keys = o; o += (2 * gmax * kmax * 2 + 15) & ~15;        // per cell: iniTh keys, minTh keys
+    b.o_meta = o; o += (2 * sw + 15) & ~15;                     // per detection column: cell index, boundary flag
+    b.o_cnt = o;  o += 16 * (2 * kBandMaxCells + 1);
+    b.bytes = o;
+    return b;
+}
+
+// NMS of a pixel pair of the band score map with cell-boundary masks.  P1 = (full column x-1, full column x),
+// P2 = (column x above/below, column x+1 above/below), P3 = (full column x+1, full column x+2); keep1 / keep3 hold
+// 0xffff in the 16-bit lanes whose column lies in the pixel's own cell.  Result bits as nms_pair.
+__device__ __forceinline__ int nms_pair_band(const int16_t* __restrict__ sc, int SW, int rr, int j, int T1, int T2, bool second,
+                                             uint32_t keep1, uint32_t keep3) {
+    const uint32_t* r0 = (const uint32_t*)(sc + rr * SW + 2 * j);
+    const uint32_t* r1 = r0 + (SW >> 1);
+    const uint32_t* r2 = r1 + (SW >> 1);
+    const uint32_t a0 = r0[0], a1 = r0[1], a2 = r0[2];
+    const uint32_t b0 = r1[0], b1 = r1[1], b2 = r1[2];
+    const uint32_t c0 = r2[0], c1 = r2[1], c2 = r2[2];
+    s16x2 p1 = pmax(pmax(as_s2(align16(a1, a0)), as_s2(align16(b1, b0))), as_s2(align16(c1, c0)));
+    const s16x2 p2 = pmax(as_s2(a1), as_s2(c1));
+    s16x2 p3 = pmax(pmax(as_s2(align16(a2, a1)), as_s2(align16(b2, b1))), as_s2(align16(c2, c1)));
+    p1 = as_s2(__builtin_bit_cast(uint32_t, p1) | ~keep1);
+    p3 = as_s2(__builtin_bit_cast(uint32_t, p3) | ~keep3);
+    const s16x2 m = pmax(pmax(p1, p2), p3);
+    const s16x2 sv = as_s2(b1);
+    const int g0 = sv.x > m.x, g1 = second && (sv.y > m.y);
+    return (g0 & (sv.x >= T1)) | ((g1 & (sv.y >= T1)) << 1) | ((g0 & (sv.x >= T2)) << 2) | ((g1 & (sv.y >= T2)) << 3);
+}
+
+constexpr int kBandPf = 6;     // ROI loads per thread held in flight per round
+
+#ifdef ORBX_QT_PROF
+__device__ unsigned long long g_fbprof[2][16];
+#define FBP(k)                                                                                                       \
+    do {                                                                                                             \
+        if (threadIdx.x == 0 && item == 8 * 37 + 3) g_fbprof[band0 ? 1 : 0][k] = wall_clock64();                    \
+    } while (0)
+#else
+#define FBP(k) do {} while (0)
+#endif
+
+template <int kPairStride>
+__global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                   const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
+                                                   const BandDev* __restrict__ bands, int band0, int nband, int iniTh, int minTh,
+                                                   uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s, int cand_stride,
+                                                   int* __restrict__ cell_cnt, int ncells, int batch, Src0 s0, BandLds lay,
+                                                   int kmax) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
+    char* lds = reinterpret_cast<char*>(fsm);
+    uint32_t* E = fsm;
+    uint32_t* O = nullptr;       // set below (row count of the launch is in lay: O = E + rows * PS)
+    int16_t* sc = reinterpret_cast<int16_t*>(lds + lay.o_sc);
+    uint16_t* list = reinterpret_cast<uint16_t*>(lds + lay.o_list);
+    uint16_t* keys = reinterpret_cast<uint16_t*>(lds + lay.o_keys);
+    uint8_t* cidx = reinterpret_cast<uint8_t*>(lds + lay.o_meta);
+    int* counters = reinterpret_cast<int*>(lds + lay.o_cnt);      // [0] survivors, [1 + 2c + t] keys of cell c
+    O = E + lay.o_sc / 8;                                        // o_sc = 2 * rows * PS * 4 bytes
+    const int tid = threadIdx.x;
+    const int item = xcd_item(xcd_chunk(nband * batch));
+    if (item >= nband * batch) return;                          // whole workgroup
+    FBP(0);
+    const int img = item / nband;
+    const BandDev bd = bands[band0 + (item - img * nband)];
+    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
+    const int tp = min(T1, T2);
+    const int W = bd.W, H = bd.H, Wd = W - 6, Hd = H - 6;
+    const bool live = Wd > 0 && Hd > 0;                         // workgroup-uniform (one row of cells)
+    const int SW = (Wd + 5) & ~1;
+    const int wc = bd.wcell, nc = bd.ncell;
+    {
+        // 1. band ROI -> pair images; lanes walk (row, 4-column chunk) items, kBandPf 8-byte loads in flight
+        const LevelDev L = levels[bd.level];
+        int lstride;
+        const uint8_t* base = level_pixels(pyr, pyr_stride, L, bd.level, img, s0, lstride);
+        const int cpr = (W + 2 + 3) >> 2;
+        const int NQ = live ? H * cpr : 0;
+        const uint8_t* src0 = base + (size_t)bd.y0 * lstride + bd.x0;
+        const int dq = 256 / cpr, dc = 256 - dq * cpr;
+        int r = tid / cpr, c = tid - r * cpr;
+        for (int q0 = tid; q0 < NQ; q0 += kBandPf * 256) {
+            uint32_t pf[2 * kBandPf];
+            int rs[kBandPf], cs[kBandPf];
+#pragma unroll
+            for (int k = 0; k < kBandPf; ++k) {
+                rs[k] = r; cs[k] = c;
+                pf[2 * k] = pf[2 * k + 1] = 0;
+                if (q0 + k * 256 < NQ) __builtin_memcpy(&pf[2 * k], src0 + (size_t)r * lstride + 4 * c, 8);
+                r += dq; c += dc;
+                if (c >= cpr) { c -= cpr; ++r; }
+            }
+#pragma unroll
+            for (int k = 0; k < kBandPf; ++k) {
+                if (q0 + k * 256 < NQ) {
+                    uint32_t lo = pf[2 * k], hi = pf[2 * k + 1];
+                    const int keep = W - 4 * cs[k];
+                    if (keep < 8) {
+                        const uint64_t m = keep <= 0 ? 0ull : ((1ull << (8 * keep)) - 1ull);
+                        const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
+                        lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+                    }
+                    const uint2 e = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u), __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
+                    const uint2 o = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c020c01u), __builtin_amdgcn_perm(hi, lo, 0x0c040c03u));
+                    *reinterpret_cast<uint2*>(E + rs[k] * kPairStride + 2 * cs[k]) = e;
+                    *reinterpret_cast<uint2*>(O + rs[k] * kPairStride + 2 * cs[k]) = o;
+                }
+            }
+        }
+        if (live) {
+            for (int i = tid; i < SW; i += 256) { sc[i] = -1; sc[(Hd + 1) * SW + i] = -1; }
+            for (int rr = tid; rr < Hd + 2; rr += 256) { sc[rr * SW + 1] = -1; sc[rr * SW + Wd + 2] = -1; }
+            // per detection column x in [0, Wd + 2): cell index (low 7 bits) | left-boundary flag (bit 7: x starts a
+            // cell, so x - 1 is in another cell's window or outside the band)
+            for (int x = tid; x < Wd + 2; x += 256) {
+                const int cx = min(x / wc, nc - 1);
+                cidx[x] = (uint8_t)(cx | ((x == cx * wc || x >= Wd) ? 0x80 : 0));
+            }
+        }
+        if (tid < 1 + 2 * kBandMaxCells) counters[tid] = 0;
+        __syncthreads();
+    }
+    FBP(1);
+    if (live) {
+        // 2. compass pre-test over the band's pixel pairs at tp (as k_fast_cells); each thread keeps a bit per pair
+        //    it tested (NP <= 32 * 256, checked on the host), one block scan places every thread's survivors
+        const int PR = (Wd + 1) >> 1, NP = Hd * PR;
+        const int rr0 = tid / PR, j0 = tid - rr0 * PR;
+        const int dq = 256 / PR, dj = 256 - dq * PR;
+        uint32_t sm = 0;
+        for (int q = tid, it = 0, rr = rr0, j = j0; q < NP; q += 256, ++it) {
+            const bool two = 2 * j + 1 < Wd;
+            const int pt = fast_pretest2<kPairStride>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
+            *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
+            sm |= (pt ? 1u : 0u) << it;
+            rr += dq; j += dj;
+            if (j >= PR) { j -= PR; ++rr; }
+        }
+        int ns;
+        int pos = block_excl_scan(__builtin_popcount(sm), counters + 1 + 2 * kBandMaxCells, &ns);
+        for (int it = 0, rr = rr0, j = j0; sm >> it; ++it) {
+            if ((sm >> it) & 1) list[pos++] = (uint16_t)((rr << 8) | j);
+            rr += dq; j += dj;
+            if (j >= PR) { j -= PR; ++rr; }
+        }
+        __syncthreads();
+        FBP(2);
+        // 3. closed-form scores of the survivors
+        for (int i = tid; i < ns; i += 256) {
+            const int rr = list[i] >> 8, j = list[i] & 0xff;
+            const s16x2 s2 = fast_score2<kPairStride>(E, O, rr + 3, j);
+            *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
+        }
+        __syncthreads();
+        FBP(3);
+        // 4. masked NMS at iniTh and minTh; kept pixels appended to their cell's lists (key = row * 128 + column in
+        //    the cell's window: row-major order)
+        for (int i = tid; i < ns; i += 256) {
+            const int rr = list[i] >> 8, j = list[i] & 0xff;
+            const int x = 2 * j;
+            const uint32_t m01 = *reinterpret_cast<const uint16_t*>(cidx + x);   // columns x, x + 1
+            const uint32_t m2 = cidx[x + 2];
+            const bool bx = m01 & 0x80, bx1 = m01 & 0x8000, bx2 = m2 & 0x80;
+            const uint32_t keep1 = (bx ? 0u : 0xffffu) | (bx1 ? 0u : 0xffff0000u);
+            const uint32_t keep3 = (bx1 ? 0u : 0xffffu) | (bx2 ? 0u : 0xffff0000u);
+            const int f = nms_pair_band(sc, SW, rr, j, T1, T2, x + 1 < Wd, keep1, keep3);
+            if (f) {
+                const int c0 = m01 & 0x7f, c1 = (m01 >> 8) & 0x7f;
+#pragma unroll
+                for (int bit = 0; bit < 4; ++bit) {
+                    if (!((f >> bit) & 1)) continue;
+                    const int px = x + (bit & 1), cc = (bit & 1) ? c1 : c0, t = bit >> 1;
+                    const int pos = atomicAdd(&counters[1 + 2 * cc + t], 1);
+                    if (pos < kmax) keys[(2 * cc + t) * kmax + pos] = (uint16_t)(rr * 128 + (px - cc * wc));
+                }
+            }
+        }
+        __syncthreads();
+        FBP(4);
+#ifdef ORBX_QT_PROF
+        if (tid == 0 && item == 8 * 37 + 3) { g_fbprof[band0 ? 1 : 0][8] = ns; g_fbprof[band0 ? 1 : 0][9] = NP; }
+#endif
+    }
+    // 5. per cell: iniTh keys, or minTh keys when the cell has none (:812-816); slot = rank in row-major order.
+    //    The keys of all the band's cells are ranked in one pass (thread -> (cell, key)).
+    // (chosen list of cell c: t = 0 iniTh when it kept any, else 1; its size from the LDS counters)
+    auto chosen = [&](int cc, int& t) {
+        t = counters[1 + 2 * cc] > 0 ? 0 : 1;
+        return min(counters[1 + 2 * cc + t], kmax);
+    };
+    int tot = 0;
+    if (live)
+        for (int cc = 0; cc < nc; ++cc) { int t; tot += chosen(cc, t); }
+    for (int g = tid; g < tot; g += 256) {
+        int cc = 0, i = g, t, nk;
+        while (i >= (nk = chosen(cc, t))) { i -= nk; ++cc; }
+        const uint16_t* ks = keys + (2 * cc + t) * kmax;
+        const CellDev cd = cells[bd.cell0 + cc];
+        const int k = ks[i];
+        int rank = 0;
+        for (int m = 0; m < nk; ++m) rank += ks[m] < k;
+        if (rank < cd.slot_cap) {
+            const int rr = k >> 7, xl = k & 127;
+            const size_t o = (size_t)img * cand_stride + cd.slot_off + rank;
+            cand_xy[o] = (uint32_t)(cd.x0 + 3 + xl) | ((uint32_t)(cd.y0 + rr + 3) << 16);
+            cand_s[o] = (uint8_t)sc[(rr + 1) * SW + 2 + cc * wc + xl];
+        }
+    }
+    if (tid < nc) {
+        int t;
+        const int cnt = live ? min(chosen(tid, t), cells[bd.cell0 + tid].slot_cap) : 0;
+        cell_cnt[(size_t)img * ncells + bd.cell0 + tid] = cnt;
+    }
+    FBP(5);
+}
+
 // GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, integer separable path: taps {18,34,49,55,49,34,18},
 // column pass (acc + 2^15) >> 16 saturated.  Tile 64 x 16 per workgroup; tiles of all levels in one grid.
 struct BlurTile { int level, tx, ty, pad; };
@@ -1314,6 +1556,13 @@ struct Extractor {
     int node_cap = 0;
     struct FastLaunch { int cell0, n, R, C, ps; size_t lds; };
     FastLaunch fast_launch[2] = {};   // k_fast_cells over level 0 / levels >= 1
+    // k_fast_band (default; ORBX_FAST_BAND=0 selects k_fast_cells): bands of up to band_g cells, level 0 / levels >= 1
+    struct BandLaunch { int band0, n, kmax; BandLds lay; };
+    BandLaunch band_launch[2] = {};
+    std::vector<BandDev> bandv;
+    BandDev* d_bands = nullptr;
+    int fast_band = 1;
+    int band_g = 4;
     int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
     size_t qt_lds = 0;        // k_quadtree dynamic LDS bytes of the node arrays (the key region follows at this offset)
@@ -1427,7 +1676,7 @@ static void level_dims(const Extractor* e, int rows, int cols, int l, int* w, in
 
 void Extractor::free_buffers() {
     auto F = [](auto*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } };
-    F(d_levels); F(d_cells); F(d_tiles); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
+    F(d_levels); F(d_cells); F(d_tiles); F(d_bands); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
     F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
     F(d_kps); F(d_desc); F(d_cnt);
     if (h_in) { (void)hipHostFree(h_in); h_in = nullptr; }
@@ -1548,6 +1797,41 @@ int Extractor::configure(int r, int c, int batch) {
             ORBX_HIP(hipFuncSetAttribute(f.ps == 24 ? (const void*)k_fast_cells<24> : (const void*)k_fast_cells<48>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.lds));
     }
+    // k_fast_band: runs of up to band_g cells of one cell row (same level and iniY), the band ROI at most 139 columns
+    // (2 * cpr <= 72 pair dwords per row); level 0 / levels >= 1 as the two launches above
+    bandv.clear();
+    for (int k = 0; k < 2; ++k) {
+        BandLaunch& b = band_launch[k];
+        b.band0 = (int)bandv.size();
+        const FastLaunch& f = fast_launch[k];
+        int rows = 8, sw = 8, np = 1, kmax = 1, gmax = 1;
+        for (int i = f.cell0; i < f.cell0 + f.n;) {
+            const CellDev& c0 = cellv[i];
+            const int wc = c0.W - 6;                        // every cell but a row's last: wCell
+            const int g = std::max(1, std::min({band_g, kBandMaxCells, (139 - 6) / std::max(wc, 1)}));
+            int n = 1;
+            while (n < g && i + n < f.cell0 + f.n && cellv[i + n].level == c0.level && cellv[i + n].y0 == c0.y0 &&
+                   cellv[i + n].x0 == c0.x0 + n * wc && cellv[i + n - 1].W == wc + 6)
+                ++n;
+            const CellDev& cl = cellv[i + n - 1];
+            BandDev bd{c0.level, i, n, c0.x0, c0.y0, cl.x0 + cl.W - c0.x0, c0.H, wc};
+            ORBX_REQUIRE(bd.W <= 139 && bd.H <= kMaxRoi && (bd.H - 6) * ((bd.W - 5) / 2) <= 32 * 256, ORBX_ERR_UNSUPPORTED,
+                         "FAST band too large");
+            bandv.push_back(bd);
+            const int Wd = bd.W - 6, Hd = bd.H - 6;
+            rows = std::max(rows, bd.H);
+            sw = std::max(sw, (Wd + 5) & ~1);
+            np = std::max(np, std::max(Hd, 0) * ((std::max(Wd, 0) + 1) >> 1));
+            for (int m = 0; m < n; ++m) kmax = std::max(kmax, cellv[i + m].slot_cap);
+            gmax = std::max(gmax, n);
+            i += n;
+        }
+        b.n = (int)bandv.size() - b.band0;
+        b.kmax = kmax;
+        b.lay = band_lds(rows, sw, np, kmax, 72, gmax);
+        if (b.lay.bytes > 64 * 1024)
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_band<72>, hipFuncAttributeMaxDynamicSharedMemorySize, b.lay.bytes));
+    }
     int scap = cap;
     for (const LevelDev& L : lv) scap = std::max(scap, std::max(L.cell_end - L.cell_begin, L.nIni));
     scan_cap = scap + 1;
@@ -1560,7 +1844,9 @@ int Extractor::configure(int r, int c, int batch) {
         // largest candidate count its levels can produce; levels whose keys overflow it use the HBM scratch
         int lcap[2] = {0, 0};
         for (int l = 0; l < nlevels; ++l) lcap[l ? 1 : 0] = std::max(lcap[l ? 1 : 0], lv[l].cand_cap);
-        const int want[2] = {8192, 2048};
+        int want[2] = {6144, 2048};
+        if (const char* v = std::getenv("ORBX_QT_KEYS0")) want[0] = std::atoi(v);   // diagnostics
+        if (const char* v = std::getenv("ORBX_QT_KEYS1")) want[1] = std::atoi(v);
         size_t maxl = lds;
         for (int k = 0; k < 2; ++k) {
             int kc = std::min(want[k], lcap[k]);
@@ -1585,6 +1871,8 @@ int Extractor::configure(int r, int c, int batch) {
     ORBX_HIP(hipMemcpy(d_levels, lv.data(), sizeof(LevelDev) * nlevels, hipMemcpyHostToDevice));
     if (!cellv.empty()) ORBX_HIP(hipMemcpy(d_cells, cellv.data(), sizeof(CellDev) * cellv.size(), hipMemcpyHostToDevice));
     ORBX_HIP(hipMemcpy(d_tiles, tilev.data(), sizeof(BlurTile) * tilev.size(), hipMemcpyHostToDevice));
+    if ((st = dev_alloc(&d_bands, bandv.size()))) return st;
+    if (!bandv.empty()) ORBX_HIP(hipMemcpy(d_bands, bandv.data(), sizeof(BandDev) * bandv.size(), hipMemcpyHostToDevice));
 
     // ---- resize tables (pinned OpenCV 3.2 INTER_LINEAR fixed point), level l from level l-1
     rtab.assign(nlevels, ResizeTab{});
@@ -1714,6 +2002,13 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
     auto fast = [&](hipStream_t q, const Extractor::FastLaunch& f) {
         if (f.n <= 0) return;
+        if (e->fast_band && !e->fast_stop_after) {
+            const Extractor::BandLaunch& b = e->band_launch[&f == &e->fast_launch[0] ? 0 : 1];
+            hipLaunchKernelGGL(k_fast_band<72>, dim3(kXcds * xcd_chunk(b.n * batch)), dim3(256), b.lay.bytes, q, e->d_pyr, ps,
+                               e->d_levels, e->d_cells, e->d_bands, b.band0, b.n, e->iniTh, e->minTh, e->d_cand_xy,
+                               e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, batch, s0, b.lay, b.kmax);
+            return;
+        }
         auto kern = f.ps == 24 ? k_fast_cells<24> : k_fast_cells<48>;
         hipLaunchKernelGGL(kern, dim3(kXcds * xcd_chunk(f.n * batch)), dim3(256), f.lds, q, e->d_pyr, ps,
                            e->d_levels, e->d_cells, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s, e->cand_stride,
@@ -1721,9 +2016,9 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     };
     auto quadtree = [&](hipStream_t q, int lvl0, int n) {
         if (n <= 0) return;
-        // key capacity: the level-0 region when the launch covers level 0 alone, else the levels >= 1 region (a launch
-        // over every level, qt_split 0, takes the smaller one; level 0 then overflows to HBM as before)
-        const int kc = (lvl0 == 0 && n == 1) ? e->qt_keys[0] : e->qt_keys[1];
+        // key capacity: the level-0 region when the launch covers level 0 (alone, or every level with qt_split 0),
+        // else the levels >= 1 region
+        const int kc = lvl0 == 0 ? e->qt_keys[0] : e->qt_keys[1];
         hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds + 6 * (size_t)kc, q, e->d_levels, e->d_cells,
                            e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
                            e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err, lvl0,
@@ -1862,6 +2157,8 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     }
     if (const char* ab = std::getenv("ORBX_FAST_ABLATE")) e->fast_stop_after = std::atoi(ab);
     if (const char* pl = std::getenv("ORBX_PIPELINE")) e->pipeline = std::atoi(pl) != 0;
+    if (const char* fb = std::getenv("ORBX_FAST_BAND")) e->fast_band = std::atoi(fb) != 0;
+    if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
     if (const char* qs = std::getenv("ORBX_QT_SPLIT")) e->qt_split = std::atoi(qs) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
@@ -2102,6 +2399,7 @@ const char* orbx_extractor_stage_name(int s) { return (s >= 0 && s < ST_COUNT) ?
 int orbx_debug_qt_prof(unsigned long long* out) {   // 2 x 64 stamps (diagnostics build only)
     ORBX_HIP(hipDeviceSynchronize());
     ORBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_qtprof), sizeof(orbx::g_qtprof)));
+    ORBX_HIP(hipMemcpyFromSymbol(out + 128, HIP_SYMBOL(orbx::g_fbprof), sizeof(orbx::g_fbprof)));
     return ORBX_OK;
 }
 #endif

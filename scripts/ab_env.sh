@@ -1,17 +1,9 @@
-# A/B of extractor variants selected by environment (one bench run each, short, no CPU baseline).
-# usage: bash scripts/ab_env.sh TAG "ENV1" "ENV2" ...   (each ENV a space-separated list of VAR=VALUE)
+# A/B of environment settings on the default bench (no CPU / C3 / host-API legs): scripts/ab_env.sh "A=1" "A=0 B=2" ...
 set -o pipefail
-R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
-TAG=$1; shift
+cd ${GRAFT_REPO_ROOT:-.}; mkdir -p gpurun_out
 i=0
 for cfg in "$@"; do
   i=$((i+1))
-  env $cfg timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --cpu-seconds 0 --host-api-frames 0 \
-      > gpurun_out/${TAG}_ab$i.log 2>&1 || { echo "run $i ($cfg) failed"; tail -5 gpurun_out/${TAG}_ab$i.log; exit 1; }
-  python3 - "$cfg" gpurun_out/${TAG}_ab$i.log <<'PY'
-import json, sys
-d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
-print(f"{sys.argv[1]:50s} {d['value']:9.0f} fps {d['ms_per_step']:.3f} ms/step host {d['host_enqueue_ms_per_step']:.3f} " +
-      " ".join(f"{k}={v:.3f}" for k, v in d.get("stage_ms_per_step", {}).items()))
-PY
+  env $cfg timeout -k 10 200 python bench.py --cpu-seconds 0 --no-c3 --host-api-frames 0 > gpurun_out/ab_$i.log 2>&1 || { echo "[$cfg] failed"; tail -3 gpurun_out/ab_$i.log; exit 1; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/ab_$i.log').read().strip().splitlines()[-1]); print('[$cfg]', d['value'], d['ms_per_step'], {k: round(v, 3) for k, v in d['stage_ms_per_step'].items()})"
 done

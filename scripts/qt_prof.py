@@ -31,7 +31,7 @@ s = torch.cuda.current_stream(dev)
 for _ in range(3):
     ex.extract_batch_device(imgs, kps, desc, cnt, stream=s)
 torch.cuda.synchronize()
-buf = (C.c_ulonglong * 128)()
+buf = (C.c_ulonglong * 160)()
 assert lib.orbx_debug_qt_prof(buf) == 0
 for row in range(2):
     v = list(buf)[64 * row: 64 * row + 64]
@@ -43,3 +43,7 @@ for row in range(2):
             break
         out.append(f"{tag}:{(t - t0) / 100:.1f}")
     print(("level0 " if row == 0 else "level1 ") + " ".join(out))
+for row in range(2):
+    v = list(buf)[128 + 16 * row: 128 + 16 * row + 16]
+    print(("fast band l0 " if row == 0 else "fast band l1+ ") + " ".join(f"{k}:{(v[k] - v[0]) / 100:.1f}" for k in range(6)),
+          "survivors", v[8], "of", v[9])
