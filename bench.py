@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--batch", type=int, default=64, help="stereo frames per GPU per step")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="extractor contexts used in turn (step k on context k %% n, each on its own queue), so step k+1's "
+                         "extraction can start while step k's tail runs")
     ap.add_argument("--distinct", type=int, default=64, help="distinct synthetic stereo pairs per rank (tiled to batch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
@@ -287,8 +290,11 @@ def main():
     host = np.stack([lefts[i % nd] for i in range(B)] + [rights[i % nd] for i in range(B)])
     imgs = torch.from_numpy(host).to(dev)               # resident in HBM before timing
 
-    ex = pkg.ORBextractor(NFEAT, SCALE, NLEV, INI, MINTH, device=dev.index)
-    ex.reserve(ROWS, COLS, 2 * B)
+    n_ctx = max(1, args.inflight)
+    exs = [pkg.ORBextractor(NFEAT, SCALE, NLEV, INI, MINTH, device=dev.index) for _ in range(n_ctx)]
+    for e_ in exs:
+        e_.reserve(ROWS, COLS, 2 * B)
+    ex = exs[0]
     m = pkg.ORBmatcher(0.6, True, device=dev.index)
     scale = ex.GetScaleFactors()
     cap = ex.max_keypoints(ROWS, COLS)
@@ -297,12 +303,13 @@ def main():
     outs = [(torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev),
              torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev),
              torch.empty((2 * B,), dtype=torch.int32, device=dev)) for _ in range(2)]
-    stream = torch.cuda.Stream(dev)                    # front-end queue: the extractor
-    torch.cuda.set_stream(stream)
+    streams = [torch.cuda.Stream(dev) for _ in range(n_ctx)]   # front-end queues: one per extractor context
+    torch.cuda.set_stream(streams[0])
     # stereo queue: step k's ComputeStereoMatches (band match + SAD refinement on step k's pyramids) runs beside
     # step k+1's extraction; the extractor cycles two pyramid sets so that step k+1 does not overwrite step k's
     stereo_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("ORBX_STEREO_PRIORITY", "0")))
-    ex.set_pyramid_ring(2)
+    for e_ in exs:
+        e_.set_pyramid_ring(2)
     # keyframe queue: BoW, packets, exchange, KeyFrameDatabase, SearchByBoW -- the native orbx_fusion object.  As in
     # the reference, where LoopClosing and MapFusion run in their own threads beside Tracking, step k's keyframe work
     # overlaps step k+1's extraction.
@@ -332,6 +339,8 @@ def main():
     def step(time_stereo=False):
         h0 = time.perf_counter()
         buf = n_step[0] % 2
+        ex = exs[n_step[0] % n_ctx]
+        stream = streams[n_step[0] % n_ctx]
         kps, desc, cnt = outs[buf]
         if kf_done[buf] is not None:
             stream.wait_event(kf_done[buf])            # the keyframe path of two steps ago has read this set
@@ -395,7 +404,8 @@ def main():
         step()
     torch.cuda.synchronize()
     if not args.no_timing:
-        ex.enable_timing(True)
+        for e_ in exs:
+            e_.enable_timing(True)
     if exchange is not None:
         exchange.reset_stats()
     if world > 1:
@@ -442,7 +452,12 @@ def main():
     }
 
     if not args.no_timing:
-        st, calls = ex.stage_times()
+        st, calls = {}, 0
+        for e_ in exs:
+            s_, c_ = e_.stage_times()
+            calls += c_
+            for k, v in s_.items():
+                st[k] = st.get(k, 0.0) + v
         per_call = {k: v / max(calls, 1) for k, v in st.items()}
         sms = [a.elapsed_time(b) for a, b in stereo_ms]
         per_call["stereo_match"] = float(np.mean(sms)) if sms else 0.0

@@ -569,8 +569,9 @@ struct BandDev {
 constexpr int kBandMaxCells = 8;
 
 struct BandLds {               // byte offsets inside the dynamic LDS of k_fast_band
-    int o_sc, o_list, o_keys, o_meta, o_cnt, bytes;
+    int o_sc, o_list, o_keys, o_meta, o_cnt, o_bm, bytes;
 };
+constexpr int kBandMaxIt = 32;   // pre-test iterations per thread (NP <= 32 * 256)
 // rows: max ROI rows; sw: max score-map row (int16); np: max pairs; kmax: max keys per cell and threshold; ps: dwords
 // per pair-image row
 __host__ __device__ __forceinline__ BandLds band_lds(int rows, int sw, int np, int kmax, int ps, int gmax) {
@@ -581,6 +582,7 @@ __host__ __device__ __forceinline__ BandLds band_lds(int rows, int sw, int np, i
     b.o_keys = o; o += (2 * gmax * kmax * 2 + 15) & ~15;        // per cell: iniTh keys, minTh keys
     b.o_meta = o; o += (2 * sw + 15) & ~15;                     // per detection column: cell index, boundary flag
     b.o_cnt = o;  o += 16 * (2 * kBandMaxCells + 1);
+    b.o_bm = o;   o += kBandMaxIt * 4 * (8 + 4);                 // per (iteration, wave): survivor ballot, list base
     b.bytes = o;
     return b;
 }
@@ -701,24 +703,45 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
     }
     FBP(1);
     if (live) {
-        // 2. compass pre-test over the band's pixel pairs at tp (as k_fast_cells); each thread keeps a bit per pair
-        //    it tested (NP <= 32 * 256, checked on the host), one block scan places every thread's survivors
+        // 2. compass pre-test over the band's pixel pairs at tp (as k_fast_cells).  The survivor list keeps pair
+        //    order (row-major: the score and NMS passes then read neighbouring LDS words lane by lane, no bank
+        //    conflicts): per (iteration, wave) the ballot goes to LDS, wave 0 scans the counts, every lane places
+        //    its survivors at base + rank in its wave's ballot (NP <= 32 * 256, checked on the host)
         const int PR = (Wd + 1) >> 1, NP = Hd * PR;
         const int rr0 = tid / PR, j0 = tid - rr0 * PR;
         const int dq = 256 / PR, dj = 256 - dq * PR;
+        const int w = tid >> 6, ln = lane_id();
+        uint64_t* bmt = reinterpret_cast<uint64_t*>(lds + lay.o_bm);          // [it][wave]
+        int* bbase = reinterpret_cast<int*>(lds + lay.o_bm + kBandMaxIt * 4 * 8);
+        const int nit = (NP + 255) >> 8;
         uint32_t sm = 0;
-        for (int q = tid, it = 0, rr = rr0, j = j0; q < NP; q += 256, ++it) {
-            const bool two = 2 * j + 1 < Wd;
-            const int pt = fast_pretest2<kPairStride>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
-            *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
+        for (int q = tid, it = 0, rr = rr0, j = j0; it < nit; q += 256, ++it) {
+            int pt = 0;
+            if (q < NP) {
+                const bool two = 2 * j + 1 < Wd;
+                pt = fast_pretest2<kPairStride>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
+                *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
+            }
+            const uint64_t bm = __ballot(pt != 0);
+            if (ln == 0) bmt[it * 4 + w] = bm;
             sm |= (pt ? 1u : 0u) << it;
             rr += dq; j += dj;
             if (j >= PR) { j -= PR; ++rr; }
         }
-        int ns;
-        int pos = block_excl_scan(__builtin_popcount(sm), counters + 1 + 2 * kBandMaxCells, &ns);
-        for (int it = 0, rr = rr0, j = j0; sm >> it; ++it) {
-            if ((sm >> it) & 1) list[pos++] = (uint16_t)((rr << 8) | j);
+        __syncthreads();
+        if (w == 0) {   // exclusive prefix over (iteration, wave) of the survivor counts: 2 entries per lane
+            const int e0 = 2 * ln, e1 = 2 * ln + 1, ne = 4 * nit;
+            const int c0 = e0 < ne ? __popcll(bmt[e0]) : 0, c1 = e1 < ne ? __popcll(bmt[e1]) : 0;
+            const int inc = wave_incl_scan(c0 + c1);
+            if (e0 < ne) bbase[e0] = inc - c0 - c1;
+            if (e1 < ne) bbase[e1] = inc - c1;
+            if (ln == kWave - 1) counters[0] = inc;
+        }
+        __syncthreads();
+        const int ns = counters[0];
+        const uint64_t below = (1ull << ln) - 1ull;
+        for (int it = 0, rr = rr0, j = j0; it < nit; ++it) {   // (it < 32: no shift by >= 32)
+            if ((sm >> it) & 1) list[bbase[it * 4 + w] + __popcll(bmt[it * 4 + w] & below)] = (uint16_t)((rr << 8) | j);
             rr += dq; j += dj;
             if (j >= PR) { j -= PR; ++rr; }
         }
@@ -1447,25 +1470,34 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     const uint8_t* P = level_pixels(pyr, pyr_stride, L, lvl, img, s0, pstride);
     int m10 = 0, m01 = 0;
     {
-        // lane: column u = (ln & 31) - 15, row parity h = ln >> 5; rows v = -15 + 2*it + h.  All 16 loads
-        // are issued unconditionally (row clamped to the disc) and masked afterwards.
-        const int h = ln >> 5, u = (ln & 31) - kHalfPatch;
-        const int au = u < 0 ? -u : u;
-        const uint8_t* col = P + (size_t)cy * pstride + cx + min(u, kHalfPatch);
-        int val[16];
+        // The 31 x 32 box around the disc as 124 (row, 8-byte chunk) items, two per lane, two 8-byte loads per lane
+        // (instead of one byte load per lane and disc row pair: 16 memory instructions).  Per chunk at row v and
+        // columns u0 .. u0+7: the bytes outside the disc (|u| > umax[|v|]) are masked off, then
+        // sum (u+16)*I and sum I come from v_dot4_u32_u8 against packed weights: m10 += that - 16 * sum I,
+        // m01 += v * sum I (integer, exact).
+        const uint8_t* p0 = P + (size_t)(cy - kHalfPatch) * pstride + (cx - kHalfPatch);
+        uint64_t ic[2];
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int v = min(-kHalfPatch + 2 * it + h, kHalfPatch);
-            val[it] = col[v * pstride];
+        for (int k = 0; k < 2; ++k) {
+            const int q = ln + 64 * k, r = min(q >> 2, 2 * kHalfPatch);
+            __builtin_memcpy(&ic[k], p0 + (size_t)r * pstride + 8 * (q & 3), 8);
         }
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int v = -kHalfPatch + 2 * it + h;
-            const int av = v < 0 ? -v : v;
-            const bool in = (v <= kHalfPatch) && ((ln & 31) <= 30) && (au <= kUmax[av > 15 ? 15 : av]);
-            const int x = in ? val[it] : 0;
-            m10 += u * x;
-            m01 += v * x;
+        for (int k = 0; k < 2; ++k) {
+            const int q = ln + 64 * k;
+            const int v = (q >> 2) - kHalfPatch, av = v < 0 ? -v : v;
+            const int um = kUmax[av > 15 ? 15 : av];
+            const int u0 = 8 * (q & 3) - kHalfPatch;
+            const int lo = max(0, -um - u0), hi = min(7, um - u0);          // bytes lo..hi lie in the disc
+            uint64_t m = 0;
+            if (q < 124 && lo <= hi) m = (hi >= 7 ? ~0ull : ((1ull << (8 * hi + 8)) - 1ull)) & (~0ull << (8 * lo));
+            const uint64_t px = ic[k] & m;
+            const uint32_t a = (uint32_t)px, b = (uint32_t)(px >> 32);
+            const uint32_t wa = (uint32_t)(u0 + 16) * 0x01010101u + 0x03020100u, wb = wa + 0x04040404u;
+            const int dot = (int)__builtin_amdgcn_udot4(b, wb, __builtin_amdgcn_udot4(a, wa, 0u, false), false);
+            const int sum = (int)__builtin_amdgcn_udot4(b, 0x01010101u, __builtin_amdgcn_udot4(a, 0x01010101u, 0u, false), false);
+            m10 += dot - 16 * sum;
+            m01 += v * sum;
         }
     }
 #pragma unroll
