@@ -30,3 +30,10 @@ qtprof: $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -DORBX_QT_PROF -c $(SRC)/orbx_extract.hip -o build/qtprof/orbx_extract.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/qtprof/liborbx.so build/qtprof/orbx_extract.o $(filter-out $(SRC)/orbx_extract.o,$(OBJS)) -ldl
 .PHONY: qtprof
+
+# A/B builds of compile-time variants: make variant V=name D="-DORBX_X=1" -> build/<name>/liborbx.so (ORBX_LIB=...)
+variant: $(OBJS)
+	mkdir -p build/$(V)
+	$(HIPCC) $(HIPFLAGS) $(D) -c $(SRC)/orbx_extract.hip -o build/$(V)/orbx_extract.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/$(V)/liborbx.so build/$(V)/orbx_extract.o $(filter-out $(SRC)/orbx_extract.o,$(OBJS)) -ldl
+.PHONY: variant

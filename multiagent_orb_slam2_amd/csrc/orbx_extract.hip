@@ -300,23 +300,26 @@ __device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, con
     s16x2 d[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) d[k] = v - as_s2(r[k]);
-    s16x2 mn2[16], mx2[16];
+    // The 16 arcs pair up as OpenCV's cornerScore walks them: for even k the arcs starting at k and k+1 share the
+    // 8 taps k+1..k+8 (m8), so max(min arc_k, min arc_k+1) = min(m8, max(d[k], d[k+9])); m8 comes from pair and
+    // quad minima over odd starts.  Likewise for the bright side with min/max swapped.  (112 packed ops, was 176.)
+    s16x2 a2[8], b2[8], a4[8], b4[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { mn2[k] = pmin(d[k], d[(k + 1) & 15]); mx2[k] = pmax(d[k], d[(k + 1) & 15]); }
-    s16x2 mn4[16], mx4[16];
+    for (int m = 0; m < 8; ++m) { a2[m] = pmin(d[2 * m + 1], d[(2 * m + 2) & 15]); b2[m] = pmax(d[2 * m + 1], d[(2 * m + 2) & 15]); }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { mn4[k] = pmin(mn2[k], mn2[(k + 2) & 15]); mx4[k] = pmax(mx2[k], mx2[(k + 2) & 15]); }
-    s16x2 mn9[16], mx9[16];
+    for (int m = 0; m < 8; ++m) { a4[m] = pmin(a2[m], a2[(m + 1) & 7]); b4[m] = pmax(b2[m], b2[(m + 1) & 7]); }
+    s16x2 dk[8], br[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn9[k] = pmin(pmin(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        mx9[k] = pmax(pmax(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+    for (int m = 0; m < 8; ++m) {
+        const s16x2 e0 = d[2 * m], e9 = d[(2 * m + 9) & 15];
+        dk[m] = pmin(pmin(a4[m], a4[(m + 2) & 7]), pmax(e0, e9));   // max over arcs 2m, 2m+1 of min d
+        br[m] = pmax(pmax(b4[m], b4[(m + 2) & 7]), pmin(e0, e9));   // min over arcs 2m, 2m+1 of max d
     }
 #pragma unroll
-    for (int w = 8; w > 0; w >>= 1)      // balanced reductions (short dependency chains)
+    for (int w = 4; w > 0; w >>= 1)      // balanced reductions (short dependency chains)
 #pragma unroll
-        for (int k = 0; k < w; ++k) { mn9[k] = pmax(mn9[k], mn9[k + w]); mx9[k] = pmin(mx9[k], mx9[k + w]); }
-    return pmax(mn9[0], (s16x2)(0) - mx9[0]) - (s16x2)(1);
+        for (int k = 0; k < w; ++k) { dk[k] = pmax(dk[k], dk[k + w]); br[k] = pmin(br[k], br[k + w]); }
+    return pmax(dk[0], (s16x2)(0) - br[0]) - (s16x2)(1);
 }
 
 // Compass pre-test for a pixel pair: every arc of 9 contains two compass taps 4 apart (0/4, 4/8, 8/12 or
@@ -834,7 +837,10 @@ __device__ __forceinline__ int refl101(int i, int n) {
 // builds the 9 byte pairs (b[i], b[i+1]) with v_perm_b32 and forms the horizontal sums of its 4 columns
 // as two packed u16 pairs (v_pk_mad_u16: a row sum is at most 255 * 257 = 65535, exact in u16).  The
 // column pass widens to u32 and the 4 output bytes leave as one dword store.
-constexpr int kBlurBand = 32, kBlurStrip = 256;
+#ifndef ORBX_BLUR_BAND
+#define ORBX_BLUR_BAND 32
+#endif
+constexpr int kBlurBand = ORBX_BLUR_BAND, kBlurStrip = 256;
 
 // byte m of the 12-byte window (w0 | w1 << 32 | w2 << 64) and byte m+1, as u16 lanes (lo = m)
 template <int m>

@@ -16,7 +16,7 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liborbx.so")
+LIB_PATH = os.environ.get("ORBX_LIB") or os.path.join(HERE, "liborbx.so")   # ORBX_LIB: A/B of diagnostic builds
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "orbx.h")
 
 ORBX_OK, ORBX_ERR_ARG, ORBX_ERR_HIP, ORBX_ERR_CAPACITY, ORBX_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
