@@ -1582,6 +1582,13 @@ struct Extractor {
     int pipeline = 1;         // ORBX_PIPELINE: 1 two streams (above), 0 every launch in order on the launch stream
     int qt_split = 1;         // ORBX_QT_SPLIT: 1 level-0 quadtree on the side stream, 0 one quadtree launch (all levels)
     hipEvent_t ev_fast0 = nullptr;   // side: FAST level 0 done (qt_split 0: the launch stream's quadtree waits on it)
+    // Per-level FAST (fast_split, ORBX_FAST_SPLIT): FAST of level l >= 1 runs on its own stream as soon as the resize
+    // chain has produced level l (ev_lvl[l]), so the latency-bound chain of seven resizes overlaps the FAST work of
+    // the levels it has finished; the launch stream's DistributeOctTree waits for ev_fast1.
+    hipStream_t fastq = nullptr;
+    hipEvent_t ev_lvl[kMaxLevels] = {};
+    hipEvent_t ev_fast1 = nullptr;
+    int fast_split = 0;
 
     // geometry for the reserved size
     int rows = 0, cols = 0, max_batch = 0;
@@ -1597,6 +1604,7 @@ struct Extractor {
     // k_fast_band (default; ORBX_FAST_BAND=0 selects k_fast_cells): bands of up to band_g cells, level 0 / levels >= 1
     struct BandLaunch { int band0, n, kmax; BandLds lay; };
     BandLaunch band_launch[2] = {};
+    int band_lvl0[kMaxLevels] = {}, band_lvln[kMaxLevels] = {};   // bands of level l: [band_lvl0[l], + band_lvln[l])
     std::vector<BandDev> bandv;
     BandDev* d_bands = nullptr;
     int fast_band = 1;
@@ -1747,6 +1755,7 @@ int Extractor::configure(int r, int c, int batch) {
     ORBX_HIP(hipSetDevice(device));
     if (stream) ORBX_HIP(hipStreamSynchronize(stream));
     if (side) ORBX_HIP(hipStreamSynchronize(side));
+    if (fastq) ORBX_HIP(hipStreamSynchronize(fastq));
     const int keep_batch = std::max(batch, (r == rows && c == cols) ? max_batch : 0);
     free_buffers();
     ORBX_REQUIRE(r > 0 && c > 0 && batch > 0, ORBX_ERR_ARG, "configure: bad size %dx%d batch %d", r, c, batch);
@@ -1838,6 +1847,7 @@ int Extractor::configure(int r, int c, int batch) {
     // k_fast_band: runs of up to band_g cells of one cell row (same level and iniY), the band ROI at most 139 columns
     // (2 * cpr <= 72 pair dwords per row); level 0 / levels >= 1 as the two launches above
     bandv.clear();
+    for (int l = 0; l < kMaxLevels; ++l) band_lvl0[l] = band_lvln[l] = 0;
     for (int k = 0; k < 2; ++k) {
         BandLaunch& b = band_launch[k];
         b.band0 = (int)bandv.size();
@@ -1865,6 +1875,11 @@ int Extractor::configure(int r, int c, int batch) {
             i += n;
         }
         b.n = (int)bandv.size() - b.band0;
+        for (int q = b.band0; q < b.band0 + b.n; ++q) {
+            const int l = bandv[q].level;
+            if (band_lvln[l] == 0) band_lvl0[l] = q;
+            ++band_lvln[l];
+        }
         b.kmax = kmax;
         b.lay = band_lds(rows, sw, np, kmax, 72, gmax);
         if (b.lay.bytes > 64 * 1024)
@@ -2073,7 +2088,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         ORBX_HIP(hipEventRecord(e->ev_fork, s));
         ORBX_HIP(hipStreamWaitEvent(side, e->ev_fork, 0));
     }
-    auto resize_chain = [&]() {
+    const bool split_fast = side != s && e->fast_split && e->fast_band && !e->fast_stop_after && e->fastq;
+    auto resize_chain = [&]() -> int {
       for (int l = 1; l < nl; ++l) {
         const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
         const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
@@ -2087,10 +2103,12 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
             dim3 g((L.w + 255) / 256, L.h, batch);
             hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis, L.pyr_off, L.w, L.h, e->rtab[l]);
         }
+        if (split_fast) ORBX_HIP(hipEventRecord(e->ev_lvl[l], s));
       }
       mark(1);
+      return ORBX_OK;
     };
-    if (side == s) resize_chain();                                  // serial: every stage contiguous on one stream
+    if (side == s) { int st = resize_chain(); if (st) return st; }  // serial: every stage contiguous on one stream
     // side stream, level 0 (reads only the caller's images)
     mark(6);
     fast(side, e->fast_launch[0]);
@@ -2101,7 +2119,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     mark(8);
     blur(side, 0, t0);
     if (side != s) {
-        resize_chain();                                             // launch stream: levels 1..nl-1 of the pyramid
+        int st = resize_chain();                                    // launch stream: levels 1..nl-1 of the pyramid
+        if (st) return st;
         ORBX_HIP(hipEventRecord(e->ev_pyr, s));
         ORBX_HIP(hipStreamWaitEvent(side, e->ev_pyr, 0));
     }
@@ -2109,7 +2128,20 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     mark(9);
     if (side != s) ORBX_HIP(hipEventRecord(e->ev_join, side));
     mark(10);                                                       // launch stream: FAST, DistributeOctTree 1..nl-1
-    fast(s, e->fast_launch[1]);
+    if (split_fast) {
+        const Extractor::BandLaunch& b = e->band_launch[1];
+        for (int l = 1; l < nl; ++l) {
+            if (e->band_lvln[l] <= 0) continue;
+            ORBX_HIP(hipStreamWaitEvent(e->fastq, e->ev_lvl[l], 0));
+            hipLaunchKernelGGL(k_fast_band<72>, dim3(kXcds * xcd_chunk(e->band_lvln[l] * batch)), dim3(256), b.lay.bytes, e->fastq,
+                               e->d_pyr, ps, e->d_levels, e->d_cells, e->d_bands, e->band_lvl0[l], e->band_lvln[l], e->iniTh,
+                               e->minTh, e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, batch, s0, b.lay, b.kmax);
+        }
+        ORBX_HIP(hipEventRecord(e->ev_fast1, e->fastq));
+        ORBX_HIP(hipStreamWaitEvent(s, e->ev_fast1, 0));
+    } else {
+        fast(s, e->fast_launch[1]);
+    }
     mark(2);
     if (split) {
         quadtree(s, 1, nl - 1);
@@ -2188,6 +2220,12 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pyr, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fast0, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
+    // (every stream holds a hardware queue: streams beyond GPU_MAX_HW_QUEUES share queues and serialise, so the
+    // per-level FAST stream exists only when that schedule is on)
+    if (const char* fs = std::getenv("ORBX_FAST_SPLIT")) e->fast_split = std::atoi(fs) != 0;
+    if (he == hipSuccess && e->fast_split) he = hipStreamCreateWithFlags(&e->fastq, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fast1, hipEventDisableTiming);
+    for (int l = 0; l < kMaxLevels && he == hipSuccess; ++l) he = hipEventCreateWithFlags(&e->ev_lvl[l], hipEventDisableTiming);
     if (he != hipSuccess) {
         set_error("stream create: %s", hipGetErrorString(he));
         orbx_extractor_destroy(e);
@@ -2211,6 +2249,7 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->side) (void)hipStreamSynchronize(e->side);
+    if (e->fastq) (void)hipStreamSynchronize(e->fastq);
     e->free_buffers();
     for (auto& es : e->tpool)
         for (auto& ev : es.ev) (void)hipEventDestroy(ev);
@@ -2220,6 +2259,10 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     if (e->ev_pyr) (void)hipEventDestroy(e->ev_pyr);
     if (e->ev_fast0) (void)hipEventDestroy(e->ev_fast0);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->fastq) (void)hipStreamDestroy(e->fastq);
+    if (e->ev_fast1) (void)hipEventDestroy(e->ev_fast1);
+    for (auto& ev : e->ev_lvl)
+        if (ev) (void)hipEventDestroy(ev);
     delete e;
     return ORBX_OK;
 }
@@ -2266,6 +2309,7 @@ int orbx_extractor_set_pyramid_ring(orbx_extractor* e, int n) {
     ORBX_HIP(hipSetDevice(e->device));
     if (e->stream) ORBX_HIP(hipStreamSynchronize(e->stream));
     if (e->side) ORBX_HIP(hipStreamSynchronize(e->side));
+    if (e->fastq) ORBX_HIP(hipStreamSynchronize(e->fastq));
     e->free_buffers();
     e->pyr_ring = n;
     return (r > 0 && c > 0 && b > 0) ? e->configure(r, c, b) : ORBX_OK;
