@@ -5,11 +5,26 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
 #include <string>
 
 #include "../../include/orbx.h"
 
 namespace orbx {
+
+// An object's own stream (the queue of its host-API entry points), created on first use: an object driven only
+// through the device API (caller's streams) never creates one, so it holds no hardware queue -- streams beyond
+// GPU_MAX_HW_QUEUES share queues, and two busy streams on one queue serialise.
+inline hipStream_t lazy_stream(hipStream_t& s, std::once_flag& once, int device) {
+    std::call_once(once, [&] {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+        (void)hipSetDevice(cur);
+    });
+    return s;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Error reporting: every C-ABI entry returns a status and leaves a message for orbx_last_error().

@@ -1571,7 +1571,9 @@ struct Extractor {
     std::vector<int> nPerLevel;
     int umax[16];
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;    // own stream of the host API, created on first use (lazy_stream)
+    std::once_flag stream_once;
+    hipStream_t own() { return lazy_stream(stream, stream_once, device); }
     bool own_stream = false;
     // Two-stream schedule (run_batch).  Level 0 of the pyramid is the caller's image, so FAST, DistributeOctTree
     // and the blur of level 0 need nothing from the resize chain: they run on a side stream while the launch stream
@@ -2211,7 +2213,6 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     compute_tables(e);
     hipError_t he = hipSetDevice(device);
     e->own_stream = true;
-    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     // High priority for the side stream: its level-0 quadtree (128 long-lived workgroups) must not queue behind the
     // launch stream's FAST grid (measured: 35.1k -> 37.6k frames/s).  ORBX_SIDE_PRIORITY overrides (A/B).
     const int side_prio = std::getenv("ORBX_SIDE_PRIORITY") ? std::atoi(std::getenv("ORBX_SIDE_PRIORITY")) : -1;
@@ -2380,19 +2381,19 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     } else {
         for (int r = 0; r < rows; ++r) std::memcpy(e->h_in + (size_t)r * cols, image + (size_t)r * step, (size_t)cols);
     }
-    ORBX_HIP(hipMemcpyAsync(e->d_in, e->h_in, nb, hipMemcpyHostToDevice, e->stream));
-    st = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, e->stream);
+    ORBX_HIP(hipMemcpyAsync(e->d_in, e->h_in, nb, hipMemcpyHostToDevice, e->own()));
+    st = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, e->own());
     if (st) return st;
     int32_t* h_cnt = (int32_t*)e->h_out;
     orbx_keypoint* h_kps = (orbx_keypoint*)(e->h_out + 64);
     uint8_t* h_desc = e->h_out + 64 + (size_t)e->out_capacity * sizeof(orbx_keypoint);
-    ORBX_HIP(hipMemcpyAsync(h_cnt, e->d_cnt, sizeof(int), hipMemcpyDeviceToHost, e->stream));
-    ORBX_HIP(hipMemcpyAsync(h_cnt + 1, e->d_err, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    ORBX_HIP(hipMemcpyAsync(h_cnt, e->d_cnt, sizeof(int), hipMemcpyDeviceToHost, e->own()));
+    ORBX_HIP(hipMemcpyAsync(h_cnt + 1, e->d_err, sizeof(int), hipMemcpyDeviceToHost, e->own()));
     // keypoints and descriptors of the whole capacity in the same round trip (a count-sized copy would need a
     // second synchronisation); only the first n are read
-    ORBX_HIP(hipMemcpyAsync(h_kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)e->out_capacity, hipMemcpyDeviceToHost, e->stream));
-    ORBX_HIP(hipMemcpyAsync(h_desc, e->d_desc, (size_t)e->out_capacity * 32, hipMemcpyDeviceToHost, e->stream));
-    ORBX_HIP(hipStreamSynchronize(e->stream));
+    ORBX_HIP(hipMemcpyAsync(h_kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)e->out_capacity, hipMemcpyDeviceToHost, e->own()));
+    ORBX_HIP(hipMemcpyAsync(h_desc, e->d_desc, (size_t)e->out_capacity * 32, hipMemcpyDeviceToHost, e->own()));
+    ORBX_HIP(hipStreamSynchronize(e->own()));
     const int n = h_cnt[0], err = h_cnt[1];
     ORBX_REQUIRE(err == 0, ORBX_ERR_UNSUPPORTED, "quadtree node capacity exceeded (err=%d)", err);
     *n_out = n;
@@ -2454,8 +2455,8 @@ int orbx_extractor_copy_level(orbx_extractor* e, int index, int level, uint8_t* 
     if (st) return st;
     ORBX_REQUIRE(dst && dst_step >= (size_t)c, ORBX_ERR_ARG, "bad destination");
     ORBX_HIP(hipSetDevice(e->device));
-    ORBX_HIP(hipMemcpy2DAsync(dst, dst_step, p, sp, c, r, hipMemcpyDeviceToHost, e->stream));
-    ORBX_HIP(hipStreamSynchronize(e->stream));
+    ORBX_HIP(hipMemcpy2DAsync(dst, dst_step, p, sp, c, r, hipMemcpyDeviceToHost, e->own()));
+    ORBX_HIP(hipStreamSynchronize(e->own()));
     return ORBX_OK;
 }
 

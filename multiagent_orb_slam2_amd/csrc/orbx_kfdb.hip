@@ -633,7 +633,9 @@ constexpr int kKfdbStages = 4;
 
 struct orbx_kfdb {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // lazy: own() on first host-API use
+    std::once_flag stream_once;
+    hipStream_t own() { return lazy_stream(stream, stream_once, device); }
     int n_vocab = 0, S = 0, maxw = 0;
     uint32_t* d_bw = nullptr;
     double* d_bv = nullptr;
@@ -676,7 +678,7 @@ int grow_scratch(orbx_kfdb* db, size_t bytes) {
     if (db->scratch) {
         // the last detect may have run on a caller's stream: wait for it before the buffer goes away
         ORBX_HIP(hipEventSynchronize(db->scratch_used));
-        ORBX_HIP(hipStreamSynchronize(db->stream));
+        if (db->stream) ORBX_HIP(hipStreamSynchronize(db->stream));
         ORBX_HIP(hipFree(db->scratch));
         db->scratch = nullptr;
         db->scratch_bytes = 0;
@@ -804,7 +806,6 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
         if (e == hipSuccess) e = hipMalloc(p, bytes);
         if (e == hipSuccess) e = hipMemset(*p, 0, bytes);
     };
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&db->stream, hipStreamNonBlocking);
     alloc((void**)&db->d_bw, 4 * S * W);
     alloc((void**)&db->d_bv, 8 * S * W);
     alloc((void**)&db->d_bn, 4 * S);
@@ -822,11 +823,9 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
         alloc((void**)&db->d_s[k], 4 * S);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&db->scratch_used, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(db->scratch_used, db->stream);
     if (e == hipSuccess) e = hipHostMalloc((void**)&db->h_stage, 8 * (size_t)kKfdbStages * S, hipHostMallocDefault);
     for (int b = 0; b < kKfdbStages; ++b) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&db->stage_done[b], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventRecord(db->stage_done[b], db->stream);
     }
     if (e != hipSuccess) {
         set_error("kfdb create: %s", hipGetErrorString(e));
@@ -888,11 +887,11 @@ int orbx_kfdb_set_bow(orbx_kfdb* db, int slot, const uint32_t* words, const doub
     ORBX_HIP(hipSetDevice(db->device));
     const size_t o = (size_t)slot * db->maxw;
     if (n) {
-        ORBX_HIP(hipMemcpyAsync(db->d_bw + o, words, 4 * (size_t)n, hipMemcpyHostToDevice, db->stream));
-        ORBX_HIP(hipMemcpyAsync(db->d_bv + o, values, 8 * (size_t)n, hipMemcpyHostToDevice, db->stream));
+        ORBX_HIP(hipMemcpyAsync(db->d_bw + o, words, 4 * (size_t)n, hipMemcpyHostToDevice, db->own()));
+        ORBX_HIP(hipMemcpyAsync(db->d_bv + o, values, 8 * (size_t)n, hipMemcpyHostToDevice, db->own()));
     }
-    ORBX_HIP(hipMemcpyAsync(db->d_bn + slot, &n, 4, hipMemcpyHostToDevice, db->stream));
-    ORBX_HIP(hipStreamSynchronize(db->stream));
+    ORBX_HIP(hipMemcpyAsync(db->d_bn + slot, &n, 4, hipMemcpyHostToDevice, db->own()));
+    ORBX_HIP(hipStreamSynchronize(db->own()));
     if (db->seq[slot] != kNoSeq) db->dirty = true;
     return ORBX_OK;
 }
@@ -933,9 +932,9 @@ int orbx_kfdb_set_covisibility(orbx_kfdb* db, const int32_t* slots, int n, const
             ORBX_REQUIRE(best[i * kKfdbCovis + j] >= -1 && best[i * kKfdbCovis + j] < db->S, ORBX_ERR_ARG,
                          "covisible slot %d out of range", best[i * kKfdbCovis + j]);
         ORBX_HIP(hipMemcpyAsync(db->d_covis + (size_t)slots[i] * kKfdbCovis, best + (size_t)i * kKfdbCovis,
-                                4 * kKfdbCovis, hipMemcpyHostToDevice, db->stream));
+                                4 * kKfdbCovis, hipMemcpyHostToDevice, db->own()));
     }
-    ORBX_HIP(hipStreamSynchronize(db->stream));
+    ORBX_HIP(hipStreamSynchronize(db->own()));
     return ORBX_OK;
 }
 
@@ -979,20 +978,20 @@ int orbx_kfdb_clear(orbx_kfdb* db) {
 int orbx_kfdb_get_state(orbx_kfdb* db, int kind, uint64_t* query, int32_t* words, float* score) {
     ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && query && words && score, ORBX_ERR_ARG, "bad argument");
     ORBX_HIP(hipSetDevice(db->device));
-    ORBX_HIP(hipMemcpyAsync(query, db->d_q[kind], 8 * (size_t)db->S, hipMemcpyDeviceToHost, db->stream));
-    ORBX_HIP(hipMemcpyAsync(words, db->d_w[kind], 4 * (size_t)db->S, hipMemcpyDeviceToHost, db->stream));
-    ORBX_HIP(hipMemcpyAsync(score, db->d_s[kind], 4 * (size_t)db->S, hipMemcpyDeviceToHost, db->stream));
-    ORBX_HIP(hipStreamSynchronize(db->stream));
+    ORBX_HIP(hipMemcpyAsync(query, db->d_q[kind], 8 * (size_t)db->S, hipMemcpyDeviceToHost, db->own()));
+    ORBX_HIP(hipMemcpyAsync(words, db->d_w[kind], 4 * (size_t)db->S, hipMemcpyDeviceToHost, db->own()));
+    ORBX_HIP(hipMemcpyAsync(score, db->d_s[kind], 4 * (size_t)db->S, hipMemcpyDeviceToHost, db->own()));
+    ORBX_HIP(hipStreamSynchronize(db->own()));
     return ORBX_OK;
 }
 
 int orbx_kfdb_set_state(orbx_kfdb* db, int kind, const uint64_t* query, const int32_t* words, const float* score) {
     ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && query && words && score, ORBX_ERR_ARG, "bad argument");
     ORBX_HIP(hipSetDevice(db->device));
-    ORBX_HIP(hipMemcpyAsync(db->d_q[kind], query, 8 * (size_t)db->S, hipMemcpyHostToDevice, db->stream));
-    ORBX_HIP(hipMemcpyAsync(db->d_w[kind], words, 4 * (size_t)db->S, hipMemcpyHostToDevice, db->stream));
-    ORBX_HIP(hipMemcpyAsync(db->d_s[kind], score, 4 * (size_t)db->S, hipMemcpyHostToDevice, db->stream));
-    ORBX_HIP(hipStreamSynchronize(db->stream));
+    ORBX_HIP(hipMemcpyAsync(db->d_q[kind], query, 8 * (size_t)db->S, hipMemcpyHostToDevice, db->own()));
+    ORBX_HIP(hipMemcpyAsync(db->d_w[kind], words, 4 * (size_t)db->S, hipMemcpyHostToDevice, db->own()));
+    ORBX_HIP(hipMemcpyAsync(db->d_s[kind], score, 4 * (size_t)db->S, hipMemcpyHostToDevice, db->own()));
+    ORBX_HIP(hipStreamSynchronize(db->own()));
     return ORBX_OK;
 }
 
@@ -1011,8 +1010,8 @@ int orbx_kfdb_score(orbx_kfdb* db, const int32_t* pairs, int n, double* scores) 
     if (n == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(db->device));
     const size_t need = align_up(8 * (size_t)n) + align_up(8 * (size_t)n);
-    if (need > db->score_stage_bytes) {          // db->stream is the only user of this buffer
-        ORBX_HIP(hipStreamSynchronize(db->stream));
+    if (need > db->score_stage_bytes) {          // the db's own stream is the only user of this buffer
+        ORBX_HIP(hipStreamSynchronize(db->own()));
         if (db->score_stage) ORBX_HIP(hipFree(db->score_stage));
         db->score_stage = nullptr;
         db->score_stage_bytes = 0;
@@ -1022,11 +1021,11 @@ int orbx_kfdb_score(orbx_kfdb* db, const int32_t* pairs, int n, double* scores) 
     int st;
     int32_t* d_pairs = (int32_t*)db->score_stage;
     double* d_out = (double*)((unsigned char*)d_pairs + align_up(8 * (size_t)n));
-    ORBX_HIP(hipMemcpyAsync(d_pairs, pairs, 8 * (size_t)n, hipMemcpyHostToDevice, db->stream));
-    st = orbx_kfdb_score_device(db, d_pairs, n, d_out, db->stream);
+    ORBX_HIP(hipMemcpyAsync(d_pairs, pairs, 8 * (size_t)n, hipMemcpyHostToDevice, db->own()));
+    st = orbx_kfdb_score_device(db, d_pairs, n, d_out, db->own());
     if (st) return st;
-    ORBX_HIP(hipMemcpyAsync(scores, d_out, 8 * (size_t)n, hipMemcpyDeviceToHost, db->stream));
-    ORBX_HIP(hipStreamSynchronize(db->stream));
+    ORBX_HIP(hipMemcpyAsync(scores, d_out, 8 * (size_t)n, hipMemcpyDeviceToHost, db->own()));
+    ORBX_HIP(hipStreamSynchronize(db->own()));
     return ORBX_OK;
 }
 
@@ -1102,7 +1101,7 @@ int detect_host_impl(orbx_kfdb* db, int kind, const int32_t* query_slots, const 
     int st = grow_scratch(db, o);
     if (st) return st;
     unsigned char* b = (unsigned char*)db->scratch;
-    hipStream_t s = db->stream;
+    hipStream_t s = db->own();
     ORBX_HIP(hipMemcpyAsync(b + o_slot, query_slots, 4 * (size_t)nq, hipMemcpyHostToDevice, s));
     ORBX_HIP(hipMemcpyAsync(b + o_id, query_ids, 8 * (size_t)nq, hipMemcpyHostToDevice, s));
     if (min_scores) ORBX_HIP(hipMemcpyAsync(b + o_min, min_scores, 4 * (size_t)nq, hipMemcpyHostToDevice, s));

@@ -759,16 +759,18 @@ struct Matcher {
     float nnratio;
     int checkOri;
     int device;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // lazy: own() on first host-API use
+    std::once_flag stream_once;
+    hipStream_t own() { return lazy_stream(stream, stream_once, device); }
     // growable device scratch
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
-    int reserve(size_t bytes) { return reserve_on(bytes, stream); }
+    int reserve(size_t bytes) { return reserve_on(bytes, own()); }
     // grow the scratch buffer; work already queued on 'on' (and on the own stream) may still use the old one
     int reserve_on(size_t bytes, hipStream_t on) {
         if (bytes <= scratch_bytes) return ORBX_OK;
         if (scratch) {
-            (void)hipStreamSynchronize(stream);
+            if (stream) (void)hipStreamSynchronize(stream);
             (void)hipStreamSynchronize(on);
             (void)hipFree(scratch);
             scratch = nullptr;
@@ -833,7 +835,7 @@ int orbx::matcher_scratch(orbx_matcher* m, size_t bytes, void** base, void** str
     int st = m->reserve(bytes);
     if (st) return st;
     *base = m->scratch;
-    *stream = (void*)m->stream;
+    *stream = (void*)m->own();
     return ORBX_OK;
 }
 
@@ -854,7 +856,6 @@ int orbx_matcher_create(float nnratio, int checkOri, int device, orbx_matcher** 
     m->checkOri = checkOri;
     m->device = device;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         set_error("stream create: %s", hipGetErrorString(e));
         delete m;
@@ -920,7 +921,7 @@ int orbx_bf_match(orbx_matcher* m, const uint8_t* q, int nq, const uint8_t* t, i
     int32_t* dbi = bp.take<int32_t>(nq);
     int32_t* dbd = bp.take<int32_t>(nq);
     int32_t* dsd = bp.take<int32_t>(nq);
-    hipStream_t s = m->stream;
+    hipStream_t s = m->own();
     ORBX_HIP(hipMemcpyAsync(dq, q, (size_t)nq * 32, hipMemcpyHostToDevice, s));
     if (nt > 0) {
         ORBX_HIP(hipMemcpyAsync(dt, t, (size_t)nt * 32, hipMemcpyHostToDevice, s));
@@ -1008,7 +1009,7 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
     int32_t* dbd = bp.take<int32_t>(cap);
     A.row_start = bp.take<int32_t>((size_t)rows + 1);
     A.row_idx = bp.take<int32_t>(cap);
-    hipStream_t s = m->stream;
+    hipStream_t s = m->own();
     ORBX_HIP(hipMemcpyAsync(dkl, kpl, 28 * (size_t)nl, hipMemcpyHostToDevice, s));
     ORBX_HIP(hipMemcpyAsync(ddl, desc_l, 32 * (size_t)nl, hipMemcpyHostToDevice, s));
     if (nr > 0) {
@@ -1099,7 +1100,7 @@ int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, con
     float* dur = bp.take<float>(cap);
     float* ddp = bp.take<float>(cap);
     int32_t* dsad = bp.take<int32_t>(cap);
-    hipStream_t s = m->stream;
+    hipStream_t s = m->own();
     ORBX_HIP(hipMemcpyAsync(dkl, kpl, 28 * (size_t)nl, hipMemcpyHostToDevice, s));
     ORBX_HIP(hipMemcpyAsync(ddl, desc_l, 32 * (size_t)nl, hipMemcpyHostToDevice, s));
     if (nr > 0) {
@@ -1172,7 +1173,7 @@ static int run_bow(orbx_matcher* m, int kff, const uint8_t* d1, const float* a1,
     const size_t bytes = a256(32 * N1) + a256(4 * N1) + a256(N1) + a256(32 * N2) + a256(4 * N2) + a256(N2) + fv_bytes(fv1) +
                          fv_bytes(fv2) + 2 * a256(4 * NR) + a256(4 * 32) + 256;
     if ((st = m->reserve(bytes))) return st;
-    hipStream_t s = m->stream;
+    hipStream_t s = m->own();
     Bump bp{(uint8_t*)m->scratch};
     uint8_t* dd1 = bp.take<uint8_t>(32 * N1);
     float* da1 = bp.take<float>(N1);
@@ -1316,7 +1317,7 @@ int orbx_distinctive_descriptors(orbx_matcher* m, const uint8_t* desc, const int
     int32_t* doff = bp.take<int32_t>(M + 1);
     int32_t* dbest = bp.take<int32_t>(M);
     uint8_t* dout = bp.take<uint8_t>(32 * M);
-    hipStream_t s = m->stream;
+    hipStream_t s = m->own();
     if (total) ORBX_HIP(hipMemcpyAsync(dd, desc, 32 * (size_t)total, hipMemcpyHostToDevice, s));
     ORBX_HIP(hipMemcpyAsync(doff, offsets, 4 * (M + 1), hipMemcpyHostToDevice, s));
     DistinctArgs A{};
@@ -1345,7 +1346,7 @@ int orbx_search_for_triangulation(orbx_matcher* m, const uint8_t* desc1, const o
     const size_t bytes = a256(32 * N1) + a256(28 * N1) + a256(N1) + a256(4 * N1) + a256(32 * N2) + a256(28 * N2) + a256(N2) +
                          a256(4 * N2) + fv_bytes(fv1) + fv_bytes(fv2) + 2 * a256(4 * N1) + a256(4 * 32) + 256;
     if ((st = m->reserve(bytes))) return st;
-    hipStream_t s = m->stream;
+    hipStream_t s = m->own();
     Bump bp{(uint8_t*)m->scratch};
     uint8_t* dd1 = bp.take<uint8_t>(32 * N1);
     orbx_keypoint* dk1 = bp.take<orbx_keypoint>(N1);

@@ -205,7 +205,9 @@ __global__ __launch_bounds__(kVocabAggThreads) void k_vocab_aggregate(const int3
 struct Vocab {
     int k = 0, L = 0, scoring = 0, weighting = 0, device = 0;
     int n_nodes = 0, n_words = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // lazy: own() on first host-API use
+    std::once_flag stream_once;
+    hipStream_t own() { return lazy_stream(stream, stream_once, device); }
     void* mem = nullptr;
     VocabDev dev{};
     // scratch for the host API
@@ -274,7 +276,6 @@ static int vocab_new(int k, int L, int scoring, int weighting, int device, orbx_
     orbx_vocab* v = new orbx_vocab();
     v->k = k; v->L = L; v->scoring = scoring; v->weighting = weighting; v->device = device;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         set_error("stream create: %s", hipGetErrorString(e));
         delete v;
@@ -426,7 +427,7 @@ int orbx_vocab_transform(orbx_vocab* v, const uint8_t* desc, int n, int levelsup
     int32_t* dfo = (int32_t*)take(4 * (N + 1));
     int32_t* dfi = (int32_t*)take(4 * N);
     int32_t* dcnt = (int32_t*)take(64);
-    hipStream_t s = v->stream;
+    hipStream_t s = v->own();
     int32_t hn[3] = {n, 0, 0};
     ORBX_HIP(hipMemcpyAsync(dd, desc, 32 * N, hipMemcpyHostToDevice, s));
     ORBX_HIP(hipMemcpyAsync(dcnt, hn, 4, hipMemcpyHostToDevice, s));
