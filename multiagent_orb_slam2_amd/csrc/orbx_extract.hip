@@ -283,13 +283,21 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // a 4-byte-aligned ds_read_b32 with a compile-time offset (2-byte-misaligned 32-bit LDS reads measured
 // ~2x slower on gfx950).  The reads are explicit (inline asm) so the compiler does not merge neighbours
 // into misaligned b64/b128 reads.
-template <int kPairStride>
+// kOE: no O image in LDS; O[i] = (E[i] hi, E[i+1] lo) = v_alignbit(E[i+1], E[i], 16) from two aligned E reads (half
+// the pair-image LDS, so more resident workgroups; neighbouring taps share their E reads).
+template <bool kOE>
+__device__ __forceinline__ uint32_t o_at(const uint32_t* __restrict__ ob, const uint32_t* __restrict__ eb, int i) {
+    if (kOE) return __builtin_amdgcn_alignbit(eb[i + 1], eb[i], 16);
+    return ob[i];
+}
+
+template <int kPairStride, bool kOE = false>
 __device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, const uint32_t* __restrict__ O, int y, int j) {
     const uint32_t* eb = E + (y - 3) * kPairStride + j;   // row y-3, pair index j; offsets >= 0
-    const uint32_t* ob = O + (y - 3) * kPairStride + j;
+    const uint32_t* ob = kOE ? eb : O + (y - 3) * kPairStride + j;
     uint32_t r[17];
 #define ORBX_TAP(k, dx, dy) \
-    r[k] = ((dx) & 1) ? eb[((dy) + 3) * kPairStride + (3 + (dx)) / 2] : ob[((dy) + 3) * kPairStride + 1 + (dx) / 2]
+    r[k] = ((dx) & 1) ? eb[((dy) + 3) * kPairStride + (3 + (dx)) / 2] : o_at<kOE>(ob, eb, ((dy) + 3) * kPairStride + 1 + (dx) / 2)
     ORBX_TAP(16, 0, 0);
     ORBX_TAP(0, 0, 3);    ORBX_TAP(1, 1, 3);    ORBX_TAP(2, 2, 2);    ORBX_TAP(3, 3, 1);
     ORBX_TAP(4, 3, 0);    ORBX_TAP(5, 3, -1);   ORBX_TAP(6, 2, -2);   ORBX_TAP(7, 1, -3);
@@ -325,15 +333,15 @@ __device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, con
 // Compass pre-test for a pixel pair: every arc of 9 contains two compass taps 4 apart (0/4, 4/8, 8/12 or
 // 12/0), so "corner at t" (some arc with all d > t, or all d < -t) implies max over those four pairs of
 // min(d_k, d_k+4) > t, or min of max < -t.  A pixel failing it has s < t.  Returns 2 bits (pixel x, x+1).
-template <int kPairStride>
+template <int kPairStride, bool kOE = false>
 __device__ __forceinline__ int fast_pretest2(const uint32_t* __restrict__ E, const uint32_t* __restrict__ O, int y, int j,
                                              int t) {
     const uint32_t* eb = E + (y - 3) * kPairStride + j;
-    const uint32_t* ob = O + (y - 3) * kPairStride + j;
-    const s16x2 v = as_s2(ob[3 * kPairStride + 1]);
-    const s16x2 d0 = v - as_s2(ob[6 * kPairStride + 1]);      // ( 0,  3)
+    const uint32_t* ob = kOE ? eb : O + (y - 3) * kPairStride + j;
+    const s16x2 v = as_s2(o_at<kOE>(ob, eb, 3 * kPairStride + 1));
+    const s16x2 d0 = v - as_s2(o_at<kOE>(ob, eb, 6 * kPairStride + 1));      // ( 0,  3)
     const s16x2 d4 = v - as_s2(eb[3 * kPairStride + 3]);      // ( 3,  0)
-    const s16x2 d8 = v - as_s2(ob[1]);                        // ( 0, -3)
+    const s16x2 d8 = v - as_s2(o_at<kOE>(ob, eb, 1));         // ( 0, -3)
     const s16x2 d12 = v - as_s2(eb[3 * kPairStride + 0]);     // (-3,  0)
     const s16x2 dk = pmax(pmax(pmin(d0, d4), pmin(d4, d8)), pmax(pmin(d8, d12), pmin(d12, d0)));
     const s16x2 br = pmin(pmin(pmax(d0, d4), pmax(d4, d8)), pmin(pmax(d8, d12), pmax(d12, d0)));
@@ -577,9 +585,9 @@ struct BandLds {               // byte offsets inside the dynamic LDS of k_fast_
 constexpr int kBandMaxIt = 32;   // pre-test iterations per thread (NP <= 32 * 256)
 // rows: max ROI rows; sw: max score-map row (int16); np: max pairs; kmax: max keys per cell and threshold; ps: dwords
 // per pair-image row
-__host__ __device__ __forceinline__ BandLds band_lds(int rows, int sw, int np, int kmax, int ps, int gmax) {
+__host__ __device__ __forceinline__ BandLds band_lds(int rows, int sw, int np, int kmax, int ps, int gmax, bool oe) {
     BandLds b;
-    int o = 2 * rows * ps * 4;                                  // E, O
+    int o = (oe ? 1 : 2) * rows * ps * 4;                       // E (and O)
     b.o_sc = o;   o += ((rows - 4) * sw * 2 + 15) & ~15;        // score map (Hd + 2 rows)
     b.o_list = o; o += (np * 2 + 15) & ~15;                     // survivor pairs
     b.o_keys = o; o += (2 * gmax * kmax * 2 + 15) & ~15;        // per cell: iniTh keys, minTh keys
@@ -624,7 +632,7 @@ __device__ unsigned long long g_fbprof[2][16];
 #define FBP(k) do {} while (0)
 #endif
 
-template <int kPairStride>
+template <int kPairStride, bool kOE>
 __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                    const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
                                                    const BandDev* __restrict__ bands, int band0, int nband, int iniTh, int minTh,
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
     uint16_t* keys = reinterpret_cast<uint16_t*>(lds + lay.o_keys);
     uint8_t* cidx = reinterpret_cast<uint8_t*>(lds + lay.o_meta);
     int* counters = reinterpret_cast<int*>(lds + lay.o_cnt);      // [0] survivors, [1 + 2c + t] keys of cell c
-    O = E + lay.o_sc / 8;                                        // o_sc = 2 * rows * PS * 4 bytes
+    if (!kOE) O = E + lay.o_sc / 8;                              // o_sc = 2 * rows * PS * 4 bytes
     const int tid = threadIdx.x;
     const int item = xcd_item(xcd_chunk(nband * batch));
     if (item >= nband * batch) return;                          // whole workgroup
@@ -687,7 +695,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
                     const uint2 e = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u), __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
                     const uint2 o = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c020c01u), __builtin_amdgcn_perm(hi, lo, 0x0c040c03u));
                     *reinterpret_cast<uint2*>(E + rs[k] * kPairStride + 2 * cs[k]) = e;
-                    *reinterpret_cast<uint2*>(O + rs[k] * kPairStride + 2 * cs[k]) = o;
+                    if (!kOE) *reinterpret_cast<uint2*>(O + rs[k] * kPairStride + 2 * cs[k]) = o;
                 }
             }
         }
@@ -722,7 +730,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
             int pt = 0;
             if (q < NP) {
                 const bool two = 2 * j + 1 < Wd;
-                pt = fast_pretest2<kPairStride>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
+                pt = fast_pretest2<kPairStride, kOE>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
                 *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
             }
             const uint64_t bm = __ballot(pt != 0);
@@ -753,7 +761,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
         // 3. closed-form scores of the survivors
         for (int i = tid; i < ns; i += 256) {
             const int rr = list[i] >> 8, j = list[i] & 0xff;
-            const s16x2 s2 = fast_score2<kPairStride>(E, O, rr + 3, j);
+            const s16x2 s2 = fast_score2<kPairStride, kOE>(E, O, rr + 3, j);
             *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
         }
         __syncthreads();
@@ -1611,6 +1619,7 @@ struct Extractor {
     BandDev* d_bands = nullptr;
     int fast_band = 1;
     int band_g = 4;
+    int fast_oe = 1;          // ORBX_FAST_OE: E-only pair image (O taps by v_alignbit), 0 = E and O images
     int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
     size_t qt_lds = 0;        // k_quadtree dynamic LDS bytes of the node arrays (the key region follows at this offset)
@@ -1883,9 +1892,11 @@ int Extractor::configure(int r, int c, int batch) {
             ++band_lvln[l];
         }
         b.kmax = kmax;
-        b.lay = band_lds(rows, sw, np, kmax, 72, gmax);
-        if (b.lay.bytes > 64 * 1024)
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_band<72>, hipFuncAttributeMaxDynamicSharedMemorySize, b.lay.bytes));
+        b.lay = band_lds(rows, sw, np, kmax, 72, gmax, fast_oe != 0);
+        if (b.lay.bytes > 64 * 1024) {
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_band<72, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b.lay.bytes));
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_band<72, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b.lay.bytes));
+        }
     }
     int scap = cap;
     for (const LevelDev& L : lv) scap = std::max(scap, std::max(L.cell_end - L.cell_begin, L.nIni));
@@ -2059,7 +2070,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         if (f.n <= 0) return;
         if (e->fast_band && !e->fast_stop_after) {
             const Extractor::BandLaunch& b = e->band_launch[&f == &e->fast_launch[0] ? 0 : 1];
-            hipLaunchKernelGGL(k_fast_band<72>, dim3(kXcds * xcd_chunk(b.n * batch)), dim3(256), b.lay.bytes, q, e->d_pyr, ps,
+            auto kb = e->fast_oe ? k_fast_band<72, true> : k_fast_band<72, false>;
+            hipLaunchKernelGGL(kb, dim3(kXcds * xcd_chunk(b.n * batch)), dim3(256), b.lay.bytes, q, e->d_pyr, ps,
                                e->d_levels, e->d_cells, e->d_bands, b.band0, b.n, e->iniTh, e->minTh, e->d_cand_xy,
                                e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, batch, s0, b.lay, b.kmax);
             return;
@@ -2135,7 +2147,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         for (int l = 1; l < nl; ++l) {
             if (e->band_lvln[l] <= 0) continue;
             ORBX_HIP(hipStreamWaitEvent(e->fastq, e->ev_lvl[l], 0));
-            hipLaunchKernelGGL(k_fast_band<72>, dim3(kXcds * xcd_chunk(e->band_lvln[l] * batch)), dim3(256), b.lay.bytes, e->fastq,
+            auto kb = e->fast_oe ? k_fast_band<72, true> : k_fast_band<72, false>;
+            hipLaunchKernelGGL(kb, dim3(kXcds * xcd_chunk(e->band_lvln[l] * batch)), dim3(256), b.lay.bytes, e->fastq,
                                e->d_pyr, ps, e->d_levels, e->d_cells, e->d_bands, e->band_lvl0[l], e->band_lvln[l], e->iniTh,
                                e->minTh, e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, batch, s0, b.lay, b.kmax);
         }
@@ -2236,6 +2249,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* pl = std::getenv("ORBX_PIPELINE")) e->pipeline = std::atoi(pl) != 0;
     if (const char* fb = std::getenv("ORBX_FAST_BAND")) e->fast_band = std::atoi(fb) != 0;
     if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
+    if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;
     if (const char* qs = std::getenv("ORBX_QT_SPLIT")) e->qt_split = std::atoi(qs) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
