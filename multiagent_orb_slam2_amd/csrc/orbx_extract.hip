@@ -1434,16 +1434,20 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                   const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
                                                   int out_stride, const int* __restrict__ level_cnt,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
-                                                  int capacity, int total_slots, int batch, Src0 s0, SlotTable tab) {
+                                                  int capacity, int slot0, int nslots, int write_count, int batch, Src0 s0,
+                                                  SlotTable tab) {
+    // slots [slot0, slot0 + nslots) of every image (a level range: slots are level-major); the launch that covers
+    // the last levels writes the per-image counts (it runs once every level's count is known)
     __shared__ __attribute__((aligned(16))) uint8_t brief_lds[4 * kBriefWin];
-    const int nbx = (total_slots + 3) / 4;                    // 4 slots (waves) per workgroup
+    const int nbx = (nslots + 3) / 4;                         // 4 slots (waves) per workgroup
     const int item = xcd_item(xcd_chunk(nbx * batch));       // keypoints of one image on one XCD
     if (item >= nbx * batch) return;
     const int img = item / nbx;
     // wave-uniform (one wave per slot): kept in SGPRs, so the level lookup below is scalar, from the kernel arguments
-    const int slot = __builtin_amdgcn_readfirstlane(((item - img * nbx) * blockDim.x + threadIdx.x) >> 6);
+    const int rel = __builtin_amdgcn_readfirstlane(((item - img * nbx) * blockDim.x + threadIdx.x) >> 6);
+    const int slot = slot0 + rel;
     const int ln = lane_id();
-    if (slot >= total_slots) return;
+    if (rel >= nslots) return;
     // slot -> (level, index)
     int lvl = 0;
 #pragma unroll
@@ -1451,12 +1455,13 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     const LevelDev L = levels[lvl];
     const int i = slot - L.out_off;
     const int* lc = level_cnt + img * nlevels;
-    int off = 0, total = 0;
-    for (int l = 0; l < nlevels; ++l) {
-        off += (l < lvl) ? lc[l] : 0;
-        total += lc[l];
+    int off = 0;
+    for (int l = 0; l < lvl; ++l) off += lc[l];
+    if (write_count && rel == 0 && ln == 0) {
+        int total = 0;
+        for (int l = 0; l < nlevels; ++l) total += lc[l];
+        counts[img] = min(total, capacity);
     }
-    if (slot == 0 && ln == 0) counts[img] = min(total, capacity);
     if (i >= lc[lvl]) return;
     const int o = off + i;
     if (o >= capacity) return;
@@ -1599,6 +1604,7 @@ struct Extractor {
     hipEvent_t ev_lvl[kMaxLevels] = {};
     hipEvent_t ev_fast1 = nullptr;
     int fast_split = 0;
+    int desc_split = 0;       // ORBX_DESC_SPLIT=1: level-0 describe on the side stream (measured 1.29 vs 1.26 ms/step)
 
     // geometry for the reserved size
     int rows = 0, cols = 0, max_batch = 0;
@@ -2132,6 +2138,20 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     else ORBX_HIP(hipEventRecord(e->ev_fast0, side));
     mark(8);
     blur(side, 0, t0);
+    // describe: slot table of the levels; level 0's keypoints on the side stream as soon as its quadtree and blur are
+    // done (beside the launch stream's FAST of levels 1..n-1), the rest on the launch stream after the join
+    SlotTable tab{};
+    for (int l = 0; l < nl; ++l) tab.out_off[l] = e->lv[l].out_off;
+    auto describe = [&](hipStream_t q, int slot0, int nslots, int write_count) {
+        if (nslots <= 0) return;
+        dim3 g(kXcds * xcd_chunk((nslots + 3) / 4 * batch));
+        hipLaunchKernelGGL(k_describe, g, dim3(256), 0, q, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
+                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, slot0, nslots, write_count, batch, s0,
+                           tab);
+    };
+    const bool split_desc = side != s && split && e->desc_split && nl > 1;
+    const int d0_slots = split_desc ? e->lv[1].out_off : 0;           // level 0 = slots [0, out_off[1])
+    if (split_desc) describe(side, 0, d0_slots, 0);
     if (side != s) {
         int st = resize_chain();                                    // launch stream: levels 1..nl-1 of the pyramid
         if (st) return st;
@@ -2167,14 +2187,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     mark(3);
     if (side != s) ORBX_HIP(hipStreamWaitEvent(s, e->ev_join, 0));
     mark(4);
-    {
-        const int total_slots = e->out_stride;
-        dim3 g(kXcds * xcd_chunk((total_slots + 3) / 4 * batch));
-        SlotTable tab{};
-        for (int l = 0; l < nl; ++l) tab.out_off[l] = e->lv[l].out_off;
-        hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
-                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, total_slots, batch, s0, tab);
-    }
+    describe(s, d0_slots, e->out_stride - d0_slots, 1);
     mark(5);
     ORBX_HIP(hipGetLastError());
     e->last_batch = batch;
@@ -2250,6 +2263,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* fb = std::getenv("ORBX_FAST_BAND")) e->fast_band = std::atoi(fb) != 0;
     if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
     if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;
+    if (const char* ds = std::getenv("ORBX_DESC_SPLIT")) e->desc_split = std::atoi(ds) != 0;
     if (const char* qs = std::getenv("ORBX_QT_SPLIT")) e->qt_split = std::atoi(qs) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
