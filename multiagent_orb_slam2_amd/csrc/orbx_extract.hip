@@ -172,17 +172,10 @@ __device__ __forceinline__ void resize_window8(const uint8_t* __restrict__ row, 
     lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
 }
 
-__global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
-                                                 size_t src_step, size_t src_istride, int sw, int dst_off, int dw, int dh,
-                                                 ResizeVec t, int nstrips, int nbands, int batch) {
-    const int nwaves = nstrips * nbands * batch;
-    const int nwg = (nwaves + 3) / 4;
-    const int wg = xcd_item(xcd_chunk(nwg));
-    const int wv = wg * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (wg >= nwg || wv >= nwaves) return;
-    const int img = wv / (nstrips * nbands);
-    const int rem = wv - img * nstrips * nbands;
-    const int band = rem / nstrips, strip = rem - band * nstrips;
+// One wave's work item of the vectorised resize: (256-column strip, 8-row band) of one image's level.
+__device__ __forceinline__ void resize4_item(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
+                                             size_t src_step, size_t src_istride, int sw, int dst_off, int dw, int dh,
+                                             const ResizeVec& t, int strip, int band, int img) {
     const int g = strip * (kResizeStrip / 4) + lane_id();
     if (g >= t.groups) return;
     const int xb = t.xb[g];
@@ -254,6 +247,47 @@ __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size
             for (int k = 0; k < 4; ++k)
                 if (x + k < dw) o[k] = (uint8_t)(packed >> (8 * k));
         }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
+                                                 size_t src_step, size_t src_istride, int sw, int dst_off, int dw, int dh,
+                                                 ResizeVec t, int nstrips, int nbands, int batch) {
+    const int nwaves = nstrips * nbands * batch;
+    const int nwg = (nwaves + 3) / 4;
+    const int wg = xcd_item(xcd_chunk(nwg));
+    const int wv = wg * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (wg >= nwg || wv >= nwaves) return;
+    const int img = wv / (nstrips * nbands);
+    const int rem = wv - img * nstrips * nbands;
+    const int band = rem / nstrips, strip = rem - band * nstrips;
+    resize4_item(pyr, pyr_stride, src, src_step, src_istride, sw, dst_off, dw, dh, t, strip, band, img);
+}
+
+// The small levels of the chain in ONE launch: one 1024-thread workgroup per image walks levels lt .. nl-1, each
+// level's (strip, band) items spread over its 16 waves, a workgroup barrier between levels (the next level reads
+// what other waves of the workgroup stored).  Seven dependent launches of shrinking grids were launch- and
+// tail-latency bound (the last ones 10-20 us for a few hundred kilobytes); here the tail levels cost one launch.
+struct ResizeTail {
+    ResizeVec t[kMaxLevels];
+    int sw[kMaxLevels], sh[kMaxLevels], src_off[kMaxLevels], dst_off[kMaxLevels], dw[kMaxLevels], dh[kMaxLevels];
+    int nstrips[kMaxLevels], nbands[kMaxLevels];
+};
+__global__ __launch_bounds__(1024) void k_resize_tail(uint8_t* __restrict__ pyr, size_t pyr_stride, int lt, int nl,
+                                                      const ResizeTail* __restrict__ tail) {
+    const int img = blockIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), nw = blockDim.x >> 6;
+    for (int l = lt; l < nl; ++l) {
+        const ResizeVec t = tail->t[l];
+        const int ns = tail->nstrips[l], nitems = ns * tail->nbands[l];
+        const uint8_t* src = pyr + tail->src_off[l];
+        for (int it = w; it < nitems; it += nw) {
+            const int band = it / ns, strip = it - band * ns;
+            resize4_item(pyr, pyr_stride, src, (size_t)tail->sw[l], pyr_stride, tail->sw[l], tail->dst_off[l], tail->dw[l],
+                         tail->dh[l], t, strip, band, img);
+        }
+        __syncthreads();   // workgroup-scope release/acquire: the waves of one workgroup share the CU's L1 (an agent-scope
+                           // fence here writes back L2 per wave, measured 4x slower than the separate launches)
     }
 }
 
@@ -1638,6 +1672,9 @@ struct Extractor {
     BlurTile* d_tiles = nullptr;
     std::vector<ResizeTab> rtab;
     std::vector<ResizeVec> rvec;      // per level: vectorised tables (groups == 0 -> use rtab)
+    ResizeTail* d_tail = nullptr;     // k_resize_tail tables (device)
+    int tail_from = 0;                // ORBX_RESIZE_TAIL=l: levels >= l in one k_resize_tail launch (0 = off: measured slower)
+    int tail_lt = 0;                  // level the tail launch starts at for the reserved size (nlevels = none)
     std::vector<void*> rtab_mem;
     uint8_t* d_pyr = nullptr;         // pyramid set of the current / last call (a slot of d_pyr_ring)
     uint8_t* d_pyr_ring = nullptr;    // pyr_ring sets of max_batch pyramids: a caller that reads the pyramid of call
@@ -1739,7 +1776,7 @@ static void level_dims(const Extractor* e, int rows, int cols, int l, int* w, in
 
 void Extractor::free_buffers() {
     auto F = [](auto*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } };
-    F(d_levels); F(d_cells); F(d_tiles); F(d_bands); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
+    F(d_levels); F(d_cells); F(d_tiles); F(d_bands); F(d_tail); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
     F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
     F(d_kps); F(d_desc); F(d_cnt);
     if (h_in) { (void)hipHostFree(h_in); h_in = nullptr; }
@@ -2022,6 +2059,27 @@ int Extractor::configure(int r, int c, int batch) {
         }
     }
 
+    // ---- k_resize_tail: levels tail_from .. nlevels-1 in one launch when every one has vectorised tables
+    tail_lt = nlevels;
+    if (tail_from >= 2 && tail_from < nlevels) {
+        bool ok = true;
+        for (int l = tail_from; l < nlevels; ++l) ok = ok && rvec[l].groups > 0;
+        if (ok) {
+            ResizeTail h{};
+            for (int l = tail_from; l < nlevels; ++l) {
+                h.t[l] = rvec[l];
+                h.sw[l] = lv[l - 1].w; h.sh[l] = lv[l - 1].h;
+                h.src_off[l] = lv[l - 1].pyr_off; h.dst_off[l] = lv[l].pyr_off;
+                h.dw[l] = lv[l].w; h.dh[l] = lv[l].h;
+                h.nstrips[l] = (lv[l].w + kResizeStrip - 1) / kResizeStrip;
+                h.nbands[l] = (lv[l].h + kResizeBand - 1) / kResizeBand;
+            }
+            if ((st = dev_alloc(&d_tail, 1))) return st;
+            ORBX_HIP(hipMemcpy(d_tail, &h, sizeof(h), hipMemcpyHostToDevice));
+            tail_lt = tail_from;
+        }
+    }
+
     // ---- batch buffers (HBM): pyramid + blurred pyramid + candidates + quadtree scratch
     const size_t B = (size_t)batch;
     if ((st = dev_alloc(&d_pyr_ring, (size_t)pyr_ring * B * pyr_size))) return st;
@@ -2111,6 +2169,12 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     const bool split_fast = side != s && e->fast_split && e->fast_band && !e->fast_stop_after && e->fastq;
     auto resize_chain = [&]() -> int {
       for (int l = 1; l < nl; ++l) {
+        if (l >= e->tail_lt) {                                      // the small levels: one launch
+            hipLaunchKernelGGL(k_resize_tail, dim3(batch), dim3(1024), 0, s, e->d_pyr, ps, e->tail_lt, nl, e->d_tail);
+            if (split_fast)
+                for (int m = l; m < nl; ++m) ORBX_HIP(hipEventRecord(e->ev_lvl[m], s));
+            break;
+        }
         const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
         const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
         const LevelDev& L = e->lv[l];
@@ -2264,6 +2328,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
     if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;
     if (const char* ds = std::getenv("ORBX_DESC_SPLIT")) e->desc_split = std::atoi(ds) != 0;
+    if (const char* rt = std::getenv("ORBX_RESIZE_TAIL")) e->tail_from = std::atoi(rt);
     if (const char* qs = std::getenv("ORBX_QT_SPLIT")) e->qt_split = std::atoi(qs) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
