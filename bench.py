@@ -61,11 +61,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
-    ap.add_argument("--batch", type=int, default=64, help="stereo frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=128, help="stereo frames per GPU per step (256 images per extractor launch)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="extractor contexts used in turn (step k on context k %% n, each on its own queue), so step k+1's "
                          "extraction can start while step k's tail runs")
-    ap.add_argument("--distinct", type=int, default=64, help="distinct synthetic stereo pairs per rank (tiled to batch)")
+    ap.add_argument("--distinct", type=int, default=128, help="distinct synthetic stereo pairs per rank (tiled to batch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage event timing")

@@ -1000,7 +1000,10 @@ __device__ __forceinline__ void blur_band(const uint8_t* __restrict__ S, int sst
     }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+#ifndef ORBX_BLUR_WPE
+#define ORBX_BLUR_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_WPE))) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                size_t pyr_stride, const LevelDev* __restrict__ levels,
                                                const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
     // tiles [tile0, tile0 + ntiles) of every image (a level range: tiles are level-major)
