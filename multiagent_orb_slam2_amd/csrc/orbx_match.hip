@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -143,6 +144,8 @@ struct StereoArgs {
     float maxD;             // bf / b (Frame.cc:496-498)
     int32_t* row_start;     // [batch][rows + 1]  right keypoints bucketed by floor(y)
     int32_t* row_idx;       // [batch][capacity]
+    int32_t* lrow_start;    // [batch][rows + 1]  left keypoints bucketed by vRowIndices row (int)y (k_stereo_blk)
+    int32_t* lrow_idx;      // [batch][capacity]
     int32_t* best_idx; int32_t* best_dist;
     int batch, nbx;         // k_stereo: images, workgroups per image (XCD-aware 1-D grid)
 };
@@ -170,6 +173,113 @@ __global__ __launch_bounds__(1024) void k_stereo_rows(StereoArgs A) {
     for (int i = tid; i < nr; i += blockDim.x) {
         const int r = min(max((int)floorf(A.kr[ob + i].y), 0), A.rows - 1);
         A.row_idx[ob + atomicAdd(&cnt[r], 1)] = i;
+    }
+    if (!A.lrow_start) return;
+    // the left keypoints by their own row (vRowIndices index (int)y, :511); rows outside the image go to the last
+    // bucket and find nothing (the search re-checks the row)
+    __syncthreads();
+    const int nl = A.nl ? A.nl[img] : A.nl_fixed;
+    for (int r = tid; r <= A.rows; r += blockDim.x) cnt[r] = 0;
+    __syncthreads();
+    for (int i = tid; i < nl; i += blockDim.x) atomicAdd(&cnt[min(max((int)A.kl[ob + i].y, 0), A.rows - 1)], 1);
+    __syncthreads();
+    block_scan_array(cnt, A.rows + 1, tmp);
+    int32_t* ls = A.lrow_start + (size_t)img * (A.rows + 1);
+    for (int r = tid; r <= A.rows; r += blockDim.x) ls[r] = cnt[r];
+    __syncthreads();
+    for (int i = tid; i < nl; i += blockDim.x)
+        A.lrow_idx[ob + atomicAdd(&cnt[min(max((int)A.kl[ob + i].y, 0), A.rows - 1)], 1)] = i;
+}
+
+// Row-block form of the search: one workgroup per (image pair, kStereoRows rows of left keypoints).  The right
+// keypoints of every bucket the block's rows can reach ([r0 - band, r1 - 1 + band], a superset of each left
+// keypoint's own [vrow - band, vrow + band]) are staged in LDS once -- descriptor, x, the octave and the row band
+// [floor(y - 2s), ceil(y + 2s)] of :487-492 -- and each wave takes left keypoints of the block with lanes over the
+// staged candidates.  The per-candidate tests are the reference's (row band, octave +-1, disparity window), so the
+// candidate set and the (distance, index) minimum are exactly k_stereo's; a candidate outside a left keypoint's own
+// bucket window never passes its row test.  Replaces ~8 dependent HBM round trips per left keypoint by one staged
+// load per block.
+constexpr int kStereoRows = 8, kStereoRC = 512, kStereoLC = 128;
+__global__ __launch_bounds__(256) void k_stereo_blk(StereoArgs A, int nblk) {
+    __shared__ uint4 rd[2 * kStereoRC];
+    __shared__ float rx[kStereoRC];
+    __shared__ int rband[kStereoRC];     // minr (low 16, signed) | maxr (high 16, signed)
+    __shared__ int rmeta[kStereoRC];     // index << 8 | octave
+    __shared__ uint4 ldsc[2 * kStereoLC];
+    __shared__ float lx[kStereoLC];
+    __shared__ int lmeta[kStereoLC];     // vrow << 8 | octave (vrow clamped to 16 bits)
+    __shared__ int lidx[kStereoLC];
+    __shared__ uint32_t lbest[kStereoLC];
+    const int item = xcd_item(xcd_chunk(nblk * A.batch));   // row blocks of one pair on one XCD
+    if (item >= nblk * A.batch) return;
+    const int img = item / nblk, blk = item - img * nblk;
+    const int tid = threadIdx.x, w = tid >> 6, ln = lane_id();
+    const size_t ob = (size_t)img * A.capacity;
+    const int r0 = blk * kStereoRows, r1 = min(r0 + kStereoRows, A.rows);
+    const int32_t* lrs = A.lrow_start + (size_t)img * (A.rows + 1);
+    const int32_t* rrs = A.row_start + (size_t)img * (A.rows + 1);
+    const int ls = lrs[r0], le = lrs[r1];
+    const int rs0 = rrs[max(r0 - A.band, 0)], rs1 = rrs[min(r1 - 1 + A.band, A.rows - 1) + 1];
+    for (int lc = ls; lc < le; lc += kStereoLC) {
+        const int nL = min(kStereoLC, le - lc);
+        __syncthreads();
+        for (int t = tid; t < nL; t += 256) {
+            const int iL = A.lrow_idx[ob + lc + t];
+            const orbx_keypoint k = A.kl[ob + iL];
+            const int vrow = (int)k.y;
+            lx[t] = k.x;
+            lmeta[t] = (min(max(vrow, -32768), 32767) << 8) | (k.octave & 0xff);
+            lidx[t] = iL;
+            lbest[t] = 0xffffffffu;
+            load_desc(A.dl + 32 * (ob + iL), ldsc[2 * t], ldsc[2 * t + 1]);
+        }
+        for (int rc = rs0; rc < rs1; rc += kStereoRC) {
+            const int nR = min(kStereoRC, rs1 - rc);
+            __syncthreads();
+            for (int t = tid; t < nR; t += 256) {
+                const int iR = A.row_idx[ob + rc + t];
+                const orbx_keypoint k = A.kr[ob + iR];
+                const float r = 2.0f * A.scale[k.octave];                               // :487
+                const int maxr = (int)ceilf(k.y + r), minr = (int)floorf(k.y - r);
+                rx[t] = k.x;
+                rband[t] = (min(max(minr, -32768), 32767) & 0xffff) | (min(max(maxr, -32768), 32767) << 16);
+                rmeta[t] = (iR << 8) | (k.octave & 0xff);
+                load_desc(A.dr + 32 * (ob + iR), rd[2 * t], rd[2 * t + 1]);
+            }
+            __syncthreads();
+            for (int j = w; j < nL; j += 4) {
+                const int lm = lmeta[j];
+                const int vrow = lm >> 8, octL = (int)(signed char)(lm & 0xff);
+                const float uL = lx[j];
+                const float minU = uL - A.maxD, maxU = uL - 0.0f;
+                if (vrow < 0 || vrow >= A.rows || maxU < 0) continue;                 // wave-uniform
+                const uint4 a0 = ldsc[2 * j], a1 = ldsc[2 * j + 1];
+                uint32_t best = 0xffffffffu;
+                for (int c = ln; c < nR; c += kWave) {
+                    const int rb = rband[c];
+                    const int minr = (int)(short)(rb & 0xffff), maxr = rb >> 16;
+                    if (vrow < minr || vrow > maxr) continue;                          // row band (:491-492)
+                    const int rm = rmeta[c];
+                    const int octR = (int)(signed char)(rm & 0xff);
+                    if (octR < octL - 1 || octR > octL + 1) continue;                  // :533
+                    const float xr = rx[c];
+                    if (!(xr >= minU && xr <= maxU)) continue;                         // :538
+                    const uint32_t key = ((uint32_t)hamming256(a0, a1, rd[2 * c], rd[2 * c + 1]) << 20) | (uint32_t)(rm >> 8);
+                    best = min(best, key);
+                }
+                best = wave_min_u32(best);
+                if (ln == 0) lbest[j] = min(lbest[j], best);
+            }
+        }
+        __syncthreads();
+        for (int t = tid; t < nL; t += 256) {
+            const uint32_t best = lbest[t];
+            int d = (best == 0xffffffffu) ? kThHigh : (int)(best >> 20);
+            d = min(d, kThHigh);                                                        // init TH_HIGH, strict <
+            const int thOrb = (kThHigh + kThLow) / 2;                                   // :471
+            A.best_dist[ob + lidx[t]] = d;
+            A.best_idx[ob + lidx[t]] = (d < thOrb) ? (int)(best & 0xfffff) : -1;        // :552
+        }
     }
 }
 
@@ -954,14 +1064,24 @@ static int stereo_common(orbx_matcher* m, StereoArgs& A, const float* scale, int
 static int stereo_launch(StereoArgs& A, int batch, int nl_max, hipStream_t s) {
     hipLaunchKernelGGL(k_stereo_rows, dim3(batch), dim3(1024), (size_t)(A.rows + 1) * sizeof(int), s, A);
     A.batch = batch;
-    A.nbx = (nl_max * 64 + 255) / 256;
-    hipLaunchKernelGGL(k_stereo, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
+    if (A.lrow_start) {                                   // row-block search (default)
+        const int nblk = (A.rows + kStereoRows - 1) / kStereoRows;
+        hipLaunchKernelGGL(k_stereo_blk, dim3(kXcds * xcd_chunk(nblk * batch)), dim3(256), 0, s, A, nblk);
+    } else {
+        A.nbx = (nl_max * 64 + 255) / 256;
+        hipLaunchKernelGGL(k_stereo, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
+    }
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }
 
+static bool stereo_blocks() {   // ORBX_STEREO_BLK=0 selects the wave-per-keypoint k_stereo (A/B)
+    static const bool on = !(std::getenv("ORBX_STEREO_BLK") && std::atoi(std::getenv("ORBX_STEREO_BLK")) == 0);
+    return on;
+}
+
 static size_t stereo_scratch(int batch, int rows, int capacity) {
-    return a256((size_t)batch * (rows + 1) * 4) + a256((size_t)batch * capacity * 4);
+    return 2 * (a256((size_t)batch * (rows + 1) * 4) + a256((size_t)batch * capacity * 4));
 }
 
 int orbx_stereo_match_batch_device(orbx_matcher* m, const orbx_keypoint* kl, const uint8_t* dl, const int32_t* nl,
@@ -979,6 +1099,10 @@ int orbx_stereo_match_batch_device(orbx_matcher* m, const orbx_keypoint* kl, con
     Bump bp{(uint8_t*)m->scratch};
     A.row_start = bp.take<int32_t>((size_t)batch * (rows + 1));
     A.row_idx = bp.take<int32_t>((size_t)batch * capacity);
+    if (stereo_blocks()) {
+        A.lrow_start = bp.take<int32_t>((size_t)batch * (rows + 1));
+        A.lrow_idx = bp.take<int32_t>((size_t)batch * capacity);
+    }
     A.kl = kl; A.dl = dl; A.nl = nl; A.kr = kr; A.dr = dr; A.nr = nr; A.capacity = capacity;
     A.best_idx = bi; A.best_dist = bd;
     return stereo_launch(A, batch, capacity, s);
@@ -1009,6 +1133,10 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
     int32_t* dbd = bp.take<int32_t>(cap);
     A.row_start = bp.take<int32_t>((size_t)rows + 1);
     A.row_idx = bp.take<int32_t>(cap);
+    if (stereo_blocks()) {
+        A.lrow_start = bp.take<int32_t>((size_t)rows + 1);
+        A.lrow_idx = bp.take<int32_t>(cap);
+    }
     hipStream_t s = m->own();
     ORBX_HIP(hipMemcpyAsync(dkl, kpl, 28 * (size_t)nl, hipMemcpyHostToDevice, s));
     ORBX_HIP(hipMemcpyAsync(ddl, desc_l, 32 * (size_t)nl, hipMemcpyHostToDevice, s));
