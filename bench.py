@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--no-c3", dest="c3", action="store_false", help="skip the C3 2000x2000 all-pairs block")
     ap.add_argument("--diag-skip", default="", help="diagnostics only (not the metric): comma list of stereo,keyframes "
                                                      "to leave out of the step")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 process group: nccl (RCCL over xGMI, the measured path) or gloo (rehearsal: several ranks "
+                         "sharing one GPU, packets staged through host memory)")
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostics: synchronise after every timed step (host_enqueue_* = pure host cost, no back-pressure)")
     return ap.parse_args()
@@ -273,8 +276,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        local = local % max(1, torch.cuda.device_count())   # (rehearsal: more ranks than GPUs share them)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -284,7 +291,10 @@ def main():
     # this agent's contiguous chunk of one synthetic sequence (generic_split_seq.cc:543-589); frame f of the
     # sequence is the synthetic stereo pair of seed f
     chunk = MA.split_sequence(cfg["seq_frames"], world)[rank]
-    seeds = [chunk.start + (i % max(len(chunk), 1)) for i in range(nd)]
+    # frame f of the sequence shows synthetic scene f mod nd: every agent's chunk revisits the same nd scenes (in its
+    # own order), as agents exploring one area do -- MapFusion's cross-agent candidates exist at every N, so the
+    # keyframe path does the same matching work per rank at N > 1 as at N = 1 (where the agent revisits its own)
+    seeds = [(chunk.start + i) % nd for i in range(nd)]
     lefts = [S.kitti_like_image(s, rows=ROWS, cols=COLS) for s in seeds]
     rights = [S.shifted_right_view(l, s) for s, l in zip(seeds, lefts)]
     host = np.stack([lefts[i % nd] for i in range(B)] + [rights[i % nd] for i in range(B)])
@@ -425,7 +435,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
@@ -499,7 +509,8 @@ def main():
     if exchange is not None:
         xs = exchange.stats()
         if xs:
-            out["exchange"] = dict(xs, collective="all_gather_into_tensor (RCCL over xGMI)",
+            out["exchange"] = dict(xs, collective="all_gather_into_tensor (RCCL over xGMI)" if args.dist_backend == "nccl"
+                                   else "all_gather (gloo, staged through host memory: rehearsal, not xGMI)",
                                    packet_bytes=engine.packet_bytes, keyframes_per_rank=n_kf)
 
     if rank == 0 and world == 1 and args.c3:

@@ -176,7 +176,12 @@ class KeyframeExchange:
         if self.timed and packets.is_cuda:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if hasattr(self.dist, "all_gather_into_tensor") and packets.is_cuda:
+        if packets.is_cuda and self.dist.get_backend(self.group) == "gloo":
+            # gloo gathers host tensors only: stage through host memory (rehearsal of the N>1 path on one GPU)
+            host = [torch.empty((n, P), dtype=torch.uint8) for _ in range(self.world)]
+            self.dist.all_gather(host, packets.cpu(), group=self.group)
+            out.copy_(torch.cat(host, 0).to(out.device))
+        elif hasattr(self.dist, "all_gather_into_tensor") and packets.is_cuda:
             self.dist.all_gather_into_tensor(out, packets.contiguous(), group=self.group)
         else:
             parts = list(out.chunk(self.world, 0))
