@@ -740,6 +740,132 @@ __global__ __launch_bounds__(256) void k_stereo_sad(RefineArgs A) {
     A.sad[o] = sd;
 }
 
+// Row-parallel form: lane (keypoint k of 5 per wave, window row y of 11) loads its row of the left 11 x 11 window
+// (11 bytes) and of the right strip that every shift touches (21 bytes: columns iuR0 - 10 .. iuR0 + 10), once, and
+// computes its row's share of all 11 SADs -- |(L - cL) - (R - cR(inc))| = |(L + 512 - d) - (R + 512)| with
+// d = cL - cR(inc), two pixels per v_sad_u16 -- instead of one lane per (keypoint, shift) re-reading 242 single
+// bytes.  Row shares are summed through LDS; the tail (first minimum, parabola, disparity test) is k_stereo_sad's.
+constexpr int kSadKpWave = 5;
+__device__ __forceinline__ uint32_t pair16(uint32_t lo4, uint32_t hi4, int b) {   // bytes b, b+1 of (hi4:lo4) as u16x2
+    return __builtin_amdgcn_perm(hi4, lo4, 0x0c000c00u | (uint32_t)b | ((uint32_t)(b + 1) << 16));
+}
+__global__ __launch_bounds__(256) void k_stereo_sad_rows(RefineArgs A) {
+    constexpr int w = 5, W = 2 * w + 1, Ls = 5, KP = 4 * kSadKpWave;
+    __shared__ int part[KP][W][W + 1];      // [keypoint][shift][row]
+    __shared__ int dist[KP][W];
+    const int item = xcd_item(xcd_chunk(A.nbx * A.batch));
+    if (item >= A.nbx * A.batch) return;
+    const int img = item / A.nbx, t = threadIdx.x, wv = t >> 6, ln = lane_id();
+    const int kq = ln / W, y = ln - kq * W;                    // lanes 55..63: kq = 5 (idle)
+    const int q = wv * kSadKpWave + kq;                        // keypoint of the workgroup
+    const int l = (item - img * A.nbx) * KP + q;
+    const bool lane_kp = kq < kSadKpWave && l < A.capacity;
+    const int nl = A.nl ? A.nl[img] : A.nl_fixed;
+    const size_t o = (size_t)img * A.capacity + (lane_kp ? l : 0);
+    const int bi = (lane_kp && l < nl) ? A.best_idx[o] : -1;
+    int oct = 0, ivL = 0, iuL = 0;
+    float suR0 = 0.f, uL = 0.f;
+    bool ok = bi >= 0;
+    int iuR0 = 0;
+    if (ok) {
+        const orbx_keypoint kp = A.kl[o];
+        oct = kp.octave;
+        uL = kp.x;
+        const float sf = A.L.inv_scale[oct];
+        const float uR0 = A.kr[(size_t)img * A.capacity + bi].x;
+        const float suL = __builtin_roundf(__fmul_rn(kp.x, sf)), svL = __builtin_roundf(__fmul_rn(kp.y, sf));
+        suR0 = __builtin_roundf(__fmul_rn(uR0, sf));
+        iuL = (int)suL; ivL = (int)svL; iuR0 = (int)suR0;
+        ok = !(ivL - w < 0 || ivL + w >= A.L.rows[oct] || iuL - w < 0 || iuL + w >= A.L.cols[oct] ||
+               ivL + w >= A.R.rows[oct] || iuR0 - Ls - w < 0);
+        const float endu = suR0 + (float)(Ls + w + 1);
+        ok = ok && !(suR0 < 0.f || endu >= (float)A.R.cols[oct]);   // iniu = scaleduR0 + L - w
+    }
+    uint32_t lw[3] = {0, 0, 0}, rw[6] = {0, 0, 0, 0, 0, 0};
+    if (ok) {
+        int sl, sr;
+        const uint8_t* IL = pyr_level(A.L, A.left_first + img, oct, sl) + (size_t)(ivL - w + y) * sl + (iuL - w);
+        const uint8_t* IR = pyr_level(A.R, A.right_first + img, oct, sr) + (size_t)(ivL - w + y) * sr + (iuR0 - Ls - w);
+        __builtin_memcpy(lw, IL, 11);                          // exact widths: never past the window
+        __builtin_memcpy(rw, IR, 21);
+    }
+    // centre values from row 5's lane of the keypoint: cL = L[5][5], cR(inc) = strip[5][10 + inc]
+    const int src = kq * W + w;
+    const uint32_t cl1 = __shfl(lw[1], src, kWave);
+    const uint32_t cr1 = __shfl(rw[1], src, kWave), cr2 = __shfl(rw[2], src, kWave), cr3 = __shfl(rw[3], src, kWave);
+    const int cL = (int)((cl1 >> 8) & 0xff);                   // byte 5
+    // left pixels as u16 pairs (x, x+1), x = 0, 2, .., 10 (the last pair's high half is masked off below)
+    uint32_t Lp[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int b = 2 * i;
+        Lp[i] = pair16(b < 4 ? lw[0] : (b < 8 ? lw[1] : lw[2]), b < 4 ? lw[1] : (b < 8 ? lw[2] : 0u), b & 3);
+    }
+    Lp[5] &= 0xffffu;                                          // x = 11 does not exist
+    int acc[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {                              // shift inc = k - 5: strip columns x + k, x = 0..10
+        const int cb = 5 + k;                                   // strip byte of cR(inc)
+        const uint32_t cw = cb < 8 ? cr1 : (cb < 12 ? cr2 : cr3);
+        const int cR = (int)((cw >> (8 * (cb & 3))) & 0xff);
+        const uint32_t off = (uint32_t)(512 - (cL - cR)) * 0x00010001u;
+        uint32_t a = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int b = k + 2 * i;                            // strip bytes b, b+1
+            const uint32_t lo4 = rw[b >> 2], hi4 = (b >> 2) + 1 < 6 ? rw[(b >> 2) + 1] : 0u;
+            uint32_t rp = pair16(lo4, hi4, b & 3) + 0x02000200u;   // R + 512
+            uint32_t lp = Lp[i] + off;                          // L + 512 - d
+            if (i == 5) { rp &= 0xffffu; lp &= 0xffffu; }       // (x = 11)
+            a = __builtin_amdgcn_sad_u16(lp, rp, a);
+        }
+        acc[k] = (int)a;
+    }
+    if (kq < kSadKpWave) {
+#pragma unroll
+        for (int k = 0; k < W; ++k) part[q][k][y] = acc[k];
+    }
+    __syncthreads();
+    if (kq < kSadKpWave && y < W) {                            // lane (keypoint, shift = y - 5): sum the 11 rows
+        int d = 0;
+#pragma unroll
+        for (int r = 0; r < W; ++r) d += part[q][y][r];
+        dist[q][y] = d;
+    }
+    __syncthreads();
+    if (!lane_kp || y != 0) return;
+    float ur = -1.0f, dp = -1.0f;
+    int sd = -1;
+    if (ok) {
+        int best = 0x7fffffff, binc = 0;
+        for (int k = -Ls; k <= Ls; ++k) {
+            const int d = dist[q][k + Ls];
+            if ((float)d < (float)best) { best = d; binc = k; }
+        }
+        if (binc != -Ls && binc != Ls) {
+            const float d1 = (float)dist[q][Ls + binc - 1], d2 = (float)dist[q][Ls + binc], d3 = (float)dist[q][Ls + binc + 1];
+            const float den = __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2)));
+            const float deltaR = __fdiv_rn(__fsub_rn(d1, d3), den);
+            if (!(deltaR < -1.f || deltaR > 1.f)) {
+                float bestuR = __fmul_rn(A.L.scale[oct], __fadd_rn(__fadd_rn(suR0, (float)binc), deltaR));
+                float disparity = __fsub_rn(uL, bestuR);
+                if (disparity >= 0.f && disparity < A.maxD) {
+                    if (disparity <= 0.f) {
+                        disparity = 0.01f;
+                        bestuR = (float)((double)uL - 0.01);
+                    }
+                    dp = __fdiv_rn(A.bf, disparity);
+                    ur = bestuR;
+                    sd = best;
+                }
+            }
+        }
+    }
+    A.uright[o] = ur;
+    A.depth[o] = dp;
+    A.sad[o] = sd;
+}
+
 // Median-SAD outlier rejection of one stereo pair (src/Frame.cc:627-639): sort the accepted SAD values,
 // median = element n/2, reject every match with SAD >= 1.5*1.4*median (the reference's backward loop
 // stops at the first value below the threshold of an ascending list).
@@ -1159,8 +1285,14 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
 
 static int refine_launch(RefineArgs& A, int batch, hipStream_t s) {
     A.batch = batch;
-    A.nbx = (A.capacity + kRefKp - 1) / kRefKp;
-    hipLaunchKernelGGL(k_stereo_sad, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
+    static const bool rows = !(std::getenv("ORBX_SAD_ROWS") && std::atoi(std::getenv("ORBX_SAD_ROWS")) == 0);
+    if (rows) {
+        A.nbx = (A.capacity + 4 * kSadKpWave - 1) / (4 * kSadKpWave);
+        hipLaunchKernelGGL(k_stereo_sad_rows, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
+    } else {
+        A.nbx = (A.capacity + kRefKp - 1) / kRefKp;
+        hipLaunchKernelGGL(k_stereo_sad, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
+    }
     hipLaunchKernelGGL(k_stereo_median, dim3(batch), dim3(1024), 0, s, A);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
