@@ -870,38 +870,63 @@ __global__ __launch_bounds__(256) void k_stereo_sad_rows(RefineArgs A) {
 // median = element n/2, reject every match with SAD >= 1.5*1.4*median (the reference's backward loop
 // stops at the first value below the threshold of an ascending list).
 __global__ __launch_bounds__(1024) void k_stereo_median(RefineArgs A) {
-    __shared__ uint32_t key[4096];
-    __shared__ int cnt;
+    // element n/2 of the ascending accepted SADs (0 <= SAD <= 121 * 510 < 2^16) by a two-digit radix select: a
+    // histogram of the high bytes finds the bin holding rank n/2, a histogram of the low bytes inside that bin finds
+    // the value (two passes over the pair's keypoints, no sort)
+    __shared__ int hist[256];
+    __shared__ int sel[4];                 // n, high byte, rank left inside the bin, low byte
     const int img = blockIdx.x, tid = threadIdx.x;
     const int nl = min(A.nl ? A.nl[img] : A.nl_fixed, A.capacity);
     const size_t o = (size_t)img * A.capacity;
-    int P2 = 1;
-    while (P2 < nl) P2 <<= 1;
-    if (tid == 0) cnt = 0;
+    if (tid < 256) hist[tid] = 0;
+    if (tid < 4) sel[tid] = 0;
     __syncthreads();
     int c = 0;
-    for (int i = tid; i < P2; i += blockDim.x) {
-        const int v = i < nl ? A.sad[o + i] : -1;
-        key[i] = v >= 0 ? (uint32_t)v : 0xffffffffu;
-        c += v >= 0;
+    for (int i = tid; i < nl; i += blockDim.x) {
+        const int v = A.sad[o + i];
+        if (v >= 0) { atomicAdd(&hist[(v >> 8) & 0xff], 1); ++c; }
     }
     c = wave_sum(c);
-    if (lane_id() == 0 && c) atomicAdd(&cnt, c);
-    for (int k = 2; k <= P2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            __syncthreads();
-            for (int i = tid; i < P2; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint32_t x = key[i], y = key[ixj];
-                    if ((x > y) == ((i & k) == 0)) { key[i] = y; key[ixj] = x; }
-                }
-            }
-        }
+    if (lane_id() == 0 && c) atomicAdd(&sel[0], c);
     __syncthreads();
-    const int n = cnt;
+    const int n = sel[0];
     if (n == 0) return;
-    const float median = (float)key[n / 2];
+    const int k = n / 2;
+    if (tid < kWave) {                     // wave 0: inclusive scan of the 256 bins, 4 per lane
+        const int b0 = 4 * tid;
+        const int h0 = hist[b0], h1 = hist[b0 + 1], h2 = hist[b0 + 2], h3 = hist[b0 + 3];
+        const int inc = wave_incl_scan(h0 + h1 + h2 + h3);
+        int before = inc - (h0 + h1 + h2 + h3);
+        const int hh[4] = {h0, h1, h2, h3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (before <= k && k < before + hh[j]) { sel[1] = b0 + j; sel[2] = k - before; }
+            before += hh[j];
+        }
+    }
+    __syncthreads();
+    const int hb = sel[1], kk = sel[2];
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < nl; i += blockDim.x) {
+        const int v = A.sad[o + i];
+        if (v >= 0 && ((v >> 8) & 0xff) == hb) atomicAdd(&hist[v & 0xff], 1);
+    }
+    __syncthreads();
+    if (tid < kWave) {
+        const int b0 = 4 * tid;
+        const int h0 = hist[b0], h1 = hist[b0 + 1], h2 = hist[b0 + 2], h3 = hist[b0 + 3];
+        const int inc = wave_incl_scan(h0 + h1 + h2 + h3);
+        int before = inc - (h0 + h1 + h2 + h3);
+        const int hh[4] = {h0, h1, h2, h3};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (before <= kk && kk < before + hh[j]) sel[3] = b0 + j;
+            before += hh[j];
+        }
+    }
+    __syncthreads();
+    const float median = (float)((hb << 8) | sel[3]);
     const float thDist = __fmul_rn(__fmul_rn(1.5f, 1.4f), median);
     for (int i = tid; i < nl; i += blockDim.x) {
         const int v = A.sad[o + i];
