@@ -119,6 +119,34 @@ def test_stereo_batch_device(gpu):
         assert np.array_equal(bi[i, :nl], idx) and np.array_equal(bd[i, :nl], dist)
 
 
+def _dense_rows_kps(seed, n, y0, y1, xmax=1200.0):
+    import multiagent_orb_slam2_amd as pkg
+    rng = np.random.default_rng(seed)
+    k = np.zeros(n, pkg.KP_DTYPE)
+    k["x"] = rng.uniform(20.0, xmax, n).astype(np.float32)
+    k["y"] = rng.uniform(y0, y1, n).astype(np.float32)
+    k["octave"] = rng.integers(0, 8, n)
+    k["size"] = 31.0
+    return k
+
+
+@pytest.mark.parametrize("nl,nr,band", [(3000, 3000, (100.0, 104.0)), (700, 4000, (0.0, 12.0)), (2500, 10, (360.0, 375.0))])
+def test_stereo_dense_rows(gpu, nl, nr, band):
+    """Keypoints crowded into a few rows: the row-block search stages more right keypoints than one LDS chunk
+    (512) and more left keypoints than one left chunk (128) per block, plus rows at the image edges."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    q, t = S.planted_pairs(11 + nl, nl, nr, frac=0.6, flip_p=0.03)
+    kl = _dense_rows_kps(1, nl, *band)
+    kr = _dense_rows_kps(2, nr, band[0] - 2.0, band[1] + 2.0)
+    kr["x"] = np.clip(kr["x"], 0, 1241)
+    scale = pkg.ORBextractor(2000, 1.2, 8, 20, 7).GetScaleFactors()
+    res = pkg.ORBmatcher().stereo_descriptor_search(kl, q, kr, t, scale, 375, BF, B)
+    n, idx, dist = O.stereo_match(kl, q, kr, t, scale, 375, BF, B)
+    assert np.array_equal(res.best_idx, idx) and np.array_equal(res.best_dist, dist)
+    assert n > 0 or nr < 100
+
+
 def _kf(seed, n_nodes=60):
     import multiagent_orb_slam2_amd as pkg
     img = S.kitti_like_image(seed)
