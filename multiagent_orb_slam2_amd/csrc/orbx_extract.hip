@@ -50,7 +50,10 @@ void set_error(const char* fmt, ...) {
 constexpr int kEdge = 19;          // EDGE_THRESHOLD (src/ORBextractor.cc:74)
 constexpr int kHalfPatch = 15;     // HALF_PATCH_SIZE (:73)
 constexpr int kMaxRoi = 72;        // cell ROI side bound: wCell < 60 (+6)
-constexpr int kQtThreads = 256;
+#ifndef ORBX_QT_THREADS
+#define ORBX_QT_THREADS 256
+#endif
+constexpr int kQtThreads = ORBX_QT_THREADS;
 constexpr int kMaxLevels = 32;
 
 // ---------------------------------------------------------------------------------------------
