@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--batch", type=int, default=128, help="stereo frames per GPU per step (256 images per extractor launch)")
+    ap.add_argument("--desc-stream", type=int, default=0,
+                    help="1: the extractor's descriptor stage on the stereo stream (orbx_extract_batch_device_split), "
+                         "so step k+1's front end overlaps step k's descriptor stage; 2: on a stream of its own; 0: on "
+                         "the launch stream")
     ap.add_argument("--inflight", type=int, default=1,
                     help="extractor contexts used in turn (step k on context k %% n, each on its own queue), so step k+1's "
                          "extraction can start while step k's tail runs")
@@ -318,6 +322,10 @@ def main():
     # stereo queue: step k's ComputeStereoMatches (band match + SAD refinement on step k's pyramids) runs beside
     # step k+1's extraction; the extractor cycles two pyramid sets so that step k+1 does not overwrite step k's
     stereo_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("ORBX_STEREO_PRIORITY", "0")))
+    # descriptor stage: on the stereo queue by default (stereo k needs describe k anyway).  A fifth busy queue is
+    # starved by the hardware scheduler (measured: the keyframe path's small kernels then wait 0.1-0.3 ms each)
+    desc_streams = ([stereo_stream] * n_ctx if args.desc_stream == 1 else
+                    [torch.cuda.Stream(dev) for _ in range(n_ctx)] if args.desc_stream == 2 else [None] * n_ctx)
     for e_ in exs:
         e_.set_pyramid_ring(2)
     # keyframe queue: BoW, packets, exchange, KeyFrameDatabase, SearchByBoW -- the native orbx_fusion object.  As in
@@ -351,12 +359,18 @@ def main():
         buf = n_step[0] % 2
         ex = exs[n_step[0] % n_ctx]
         stream = streams[n_step[0] % n_ctx]
+        dstream = desc_streams[n_step[0] % n_ctx]       # the descriptor stage (writes the outputs)
+        ostream = dstream if dstream is not None else stream
         kps, desc, cnt = outs[buf]
         if kf_done[buf] is not None:
-            stream.wait_event(kf_done[buf])            # the keyframe path of two steps ago has read this set
-        ex.extract_batch_device(imgs, kps, desc, cnt, stream=stream)
+            # the keyframe path of two steps ago has read this output set (written by the descriptor stage), and the
+            # stereo step before it the pyramid set this call's resize chain overwrites
+            stream.wait_event(kf_done[buf])
+            if dstream is not None:
+                dstream.wait_event(kf_done[buf])
+        ex.extract_batch_device(imgs, kps, desc, cnt, stream=stream, out_stream=dstream)
         extracted = torch.cuda.Event()
-        extracted.record(stream)
+        extracted.record(ostream)
         pyr = ex.pyramid_device()                      # this call's pyramid set (a slot of the ring of 2)
         if "stereo" in skip:
             n_step[0] += 1

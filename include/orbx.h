@@ -95,6 +95,17 @@ int orbx_extractor_copy_level(orbx_extractor* ex, int index, int level, uint8_t*
 int orbx_extract_batch_device(orbx_extractor* ex, const uint8_t* d_images, int batch, int rows, int cols,
                               size_t step, size_t image_stride, orbx_keypoint* d_keypoints,
                               uint8_t* d_descriptors, int32_t* d_counts, int capacity, void* stream);
+/* The same with two streams: the inputs are read in in_stream order and the outputs (keypoints, descriptors,
+ * counts) are complete in out_stream order.  Everything up to DistributeOctTree runs on in_stream (and the
+ * extractor's side stream); the descriptor stage runs on out_stream, so a caller that issues call k+1 on
+ * in_stream overlaps it with call k's descriptor stage.  The extractor orders its own buffer reuse across calls
+ * (call k+1's quadtree / blur wait for call k's descriptor stage; a pyramid set's resize waits for the last
+ * descriptor stage that read it); the pyramid of the call (orbx_extractor_pyramid_device) is complete in
+ * out_stream order too.  out_stream == in_stream is orbx_extract_batch_device. */
+int orbx_extract_batch_device_split(orbx_extractor* ex, const uint8_t* d_images, int batch, int rows, int cols,
+                                    size_t step, size_t image_stride, orbx_keypoint* d_keypoints,
+                                    uint8_t* d_descriptors, int32_t* d_counts, int capacity, void* in_stream,
+                                    void* out_stream);
 
 /* The image pyramids of the last extraction call, as one device-side description (what
  * ORBextractor::mvImagePyramid exposes, include/ORBextractor.h:85): level 0 of image i is the caller's

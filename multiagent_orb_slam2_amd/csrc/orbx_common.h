@@ -141,6 +141,32 @@ __device__ __forceinline__ int block_scan_array(int* a, int n, int* tmp) {
     return total;
 }
 
+// Bitonic sort (ascending) of P2 (a power of two) 64-bit keys in LDS by the whole block (blockDim a multiple of 64).
+// Thread t takes compare pairs p = t, t + T, ...: pair p of stage j is (i, i | j) with i = p with a zero bit inserted at
+// log2(j), so the 64 pairs of a wave span 128 consecutive keys and every stage with j <= 64 stays inside one wave: those
+// stages need only a wave-level fence; only the stages with j >= 128 (10 of 66 at P2 = 2048) take a block barrier.
+// Every thread must call it; it ends with a block barrier.
+__device__ __forceinline__ void block_bitonic_u64(unsigned long long* a, int P2) {
+    const int half = P2 >> 1;
+    for (int k = 2; k <= P2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int p = threadIdx.x; p < half; p += blockDim.x) {
+                const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), ixj = i | j;
+                const unsigned long long x = a[i], y = a[ixj];
+                if ((x > y) == ((i & k) == 0)) { a[i] = y; a[ixj] = x; }
+            }
+            const int nj = j > 1 ? j >> 1 : k;                   // the next stage's j
+            if (j >= 128 || nj >= 128) {
+                __syncthreads();
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+    __syncthreads();
+}
+
 // XCD-aware block -> work-item mapping.  Workgroups are dealt round-robin to the 8 XCDs (blocks b and
 // b + 8 share one XCD and its 4 MiB L2; MI355X_MICROARCH.md, workgroup dispatch), so with a 1-D grid of
 // 8 * chunk blocks XCD x gets the contiguous items [x * chunk, (x + 1) * chunk) in dispatch order:

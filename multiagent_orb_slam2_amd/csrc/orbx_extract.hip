@@ -1645,6 +1645,14 @@ struct Extractor {
     hipEvent_t ev_fast1 = nullptr;
     int fast_split = 0;
     int desc_split = 0;       // ORBX_DESC_SPLIT=1: level-0 describe on the side stream (measured 1.29 vs 1.26 ms/step)
+    // Describe stream (orbx_extract_batch_device_split): k_describe runs on the caller's output stream, so the next
+    // call's front half (resize chain, FAST) on the input stream overlaps this call's describe.  What the next call
+    // overwrites that describe reads is ordered by events: the kept keypoints and the blurred pyramid (its quadtree
+    // and blur wait for ev_desc_last) and its pyramid set (the resize chain waits for that set's last describe).
+    hipEvent_t ev_front = nullptr;                  // launch stream: quadtree of levels >= 1 done
+    hipEvent_t ev_desc[8] = {};                     // per pyramid set: describe of the last call on it done
+    bool desc_pending[8] = {};
+    int desc_last = -1;                             // set of the previous call (its describe event), -1 none
 
     // geometry for the reserved size
     int rows = 0, cols = 0, max_batch = 0;
@@ -2116,7 +2124,8 @@ static size_t qt_lds_bytes(int cap, int scan_cap) {
 
 
 static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t step, size_t istride,
-                     orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int capacity, hipStream_t s) {
+                     orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int capacity, hipStream_t s,
+                     hipStream_t so) {
     const int nl = e->nlevels;
     const size_t ps = e->pyr_size;
     Extractor::EventSet* es = nullptr;
@@ -2128,9 +2137,18 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     }
     const Src0 s0{d_images, step, istride};
     e->last_src0 = s0;
-    e->d_pyr = e->d_pyr_ring + (size_t)(e->ncalls++ % (unsigned long long)e->pyr_ring) * e->max_batch * ps;
+    const int slot = (int)(e->ncalls++ % (unsigned long long)e->pyr_ring);
+    e->d_pyr = e->d_pyr_ring + (size_t)slot * e->max_batch * ps;
     hipStream_t side = e->pipeline ? e->side : s;
-    auto mark = [&](int k) { if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : s); };
+    if (!e->pipeline) so = s;
+    auto mark = [&](int k) {
+        if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : (k == 4 || k == 5) ? so : s);
+    };
+    // the previous call's describe (possibly on another stream) reads the kept keypoints and the blurred pyramid
+    auto after_prev_describe = [&](hipStream_t q) -> int {
+        if (e->desc_last >= 0) ORBX_HIP(hipStreamWaitEvent(q, e->ev_desc[e->desc_last], 0));
+        return ORBX_OK;
+    };
     const int ncells = (int)e->cellv.size();
     int t0 = 0;                                                     // blur tiles of level 0: [0, t0)
     while (t0 < (int)e->tilev.size() && e->tilev[t0].level == 0) ++t0;
@@ -2174,6 +2192,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     }
     const bool split_fast = side != s && e->fast_split && e->fast_band && !e->fast_stop_after && e->fastq;
     auto resize_chain = [&]() -> int {
+      if (e->desc_pending[slot]) ORBX_HIP(hipStreamWaitEvent(s, e->ev_desc[slot], 0));   // this set's last reader
       for (int l = 1; l < nl; ++l) {
         if (l >= e->tail_lt) {                                      // the small levels: one launch
             hipLaunchKernelGGL(k_resize_tail, dim3(batch), dim3(1024), 0, s, e->d_pyr, ps, e->tail_lt, nl, e->d_tail);
@@ -2204,6 +2223,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     fast(side, e->fast_launch[0]);
     mark(7);
     const bool split = e->qt_split || side == s;
+    if (int st = after_prev_describe(side)) return st;
     if (split) quadtree(side, 0, nl > 0 ? 1 : 0);
     else ORBX_HIP(hipEventRecord(e->ev_fast0, side));
     mark(8);
@@ -2248,6 +2268,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         fast(s, e->fast_launch[1]);
     }
     mark(2);
+    if (int st = after_prev_describe(s)) return st;
     if (split) {
         quadtree(s, 1, nl - 1);
     } else {
@@ -2255,10 +2276,17 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         quadtree(s, 0, nl);
     }
     mark(3);
-    if (side != s) ORBX_HIP(hipStreamWaitEvent(s, e->ev_join, 0));
+    if (so != s) {
+        ORBX_HIP(hipEventRecord(e->ev_front, s));
+        ORBX_HIP(hipStreamWaitEvent(so, e->ev_front, 0));
+    }
+    if (side != so) ORBX_HIP(hipStreamWaitEvent(so, e->ev_join, 0));
     mark(4);
-    describe(s, d0_slots, e->out_stride - d0_slots, 1);
+    describe(so, d0_slots, e->out_stride - d0_slots, 1);
     mark(5);
+    ORBX_HIP(hipEventRecord(e->ev_desc[slot], so));
+    e->desc_pending[slot] = true;
+    e->desc_last = slot;
     ORBX_HIP(hipGetLastError());
     e->last_batch = batch;
     return ORBX_OK;
@@ -2317,6 +2345,8 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pyr, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fast0, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_front, hipEventDisableTiming);
+    for (int k = 0; k < 8 && he == hipSuccess; ++k) he = hipEventCreateWithFlags(&e->ev_desc[k], hipEventDisableTiming);
     // (every stream holds a hardware queue: streams beyond GPU_MAX_HW_QUEUES share queues and serialise, so the
     // per-level FAST stream exists only when that schedule is on)
     if (const char* fs = std::getenv("ORBX_FAST_SPLIT")) e->fast_split = std::atoi(fs) != 0;
@@ -2350,6 +2380,8 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->side) (void)hipStreamSynchronize(e->side);
     if (e->fastq) (void)hipStreamSynchronize(e->fastq);
+    for (int k = 0; k < 8; ++k)
+        if (e->desc_pending[k]) (void)hipEventSynchronize(e->ev_desc[k]);   // a describe on the caller's stream
     e->free_buffers();
     for (auto& es : e->tpool)
         for (auto& ev : es.ev) (void)hipEventDestroy(ev);
@@ -2359,6 +2391,9 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     if (e->ev_pyr) (void)hipEventDestroy(e->ev_pyr);
     if (e->ev_fast0) (void)hipEventDestroy(e->ev_fast0);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->ev_front) (void)hipEventDestroy(e->ev_front);
+    for (auto& ev : e->ev_desc)
+        if (ev) (void)hipEventDestroy(ev);
     if (e->fastq) (void)hipStreamDestroy(e->fastq);
     if (e->ev_fast1) (void)hipEventDestroy(e->ev_fast1);
     for (auto& ev : e->ev_lvl)
@@ -2410,7 +2445,11 @@ int orbx_extractor_set_pyramid_ring(orbx_extractor* e, int n) {
     if (e->stream) ORBX_HIP(hipStreamSynchronize(e->stream));
     if (e->side) ORBX_HIP(hipStreamSynchronize(e->side));
     if (e->fastq) ORBX_HIP(hipStreamSynchronize(e->fastq));
+    for (int k = 0; k < 8; ++k)
+        if (e->desc_pending[k]) ORBX_HIP(hipEventSynchronize(e->ev_desc[k]));
     e->free_buffers();
+    for (int k = 0; k < 8; ++k) e->desc_pending[k] = false;
+    e->desc_last = -1;
     e->pyr_ring = n;
     return (r > 0 && c > 0 && b > 0) ? e->configure(r, c, b) : ORBX_OK;
 }
@@ -2438,7 +2477,20 @@ int orbx_extract_batch_device(orbx_extractor* e, const uint8_t* d_images, int ba
     if (st) return st;
     ORBX_REQUIRE(capacity >= e->out_capacity, ORBX_ERR_CAPACITY, "capacity %d < required %d", capacity, e->out_capacity);
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
-    return run_batch(e, d_images, batch, step, image_stride, d_keypoints, d_descriptors, d_counts, capacity, s);
+    return run_batch(e, d_images, batch, step, image_stride, d_keypoints, d_descriptors, d_counts, capacity, s, s);
+}
+
+int orbx_extract_batch_device_split(orbx_extractor* e, const uint8_t* d_images, int batch, int rows, int cols, size_t step,
+                                    size_t image_stride, orbx_keypoint* d_keypoints, uint8_t* d_descriptors,
+                                    int32_t* d_counts, int capacity, void* in_stream, void* out_stream) {
+    ORBX_REQUIRE(e && d_images && d_keypoints && d_descriptors && d_counts, ORBX_ERR_ARG, "null argument");
+    ORBX_REQUIRE(batch > 0 && rows > 0 && cols > 0 && step >= (size_t)cols, ORBX_ERR_ARG, "bad batch geometry");
+    ORBX_HIP(hipSetDevice(e->device));
+    int st = e->configure(rows, cols, batch);
+    if (st) return st;
+    ORBX_REQUIRE(capacity >= e->out_capacity, ORBX_ERR_CAPACITY, "capacity %d < required %d", capacity, e->out_capacity);
+    return run_batch(e, d_images, batch, step, image_stride, d_keypoints, d_descriptors, d_counts, capacity,
+                     (hipStream_t)in_stream, (hipStream_t)out_stream);
 }
 
 int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, size_t step, orbx_keypoint* kps,
@@ -2481,7 +2533,7 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
         for (int r = 0; r < rows; ++r) std::memcpy(e->h_in + (size_t)r * cols, image + (size_t)r * step, (size_t)cols);
     }
     ORBX_HIP(hipMemcpyAsync(e->d_in, e->h_in, nb, hipMemcpyHostToDevice, e->own()));
-    st = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, e->own());
+    st = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, e->own(), e->own());
     if (st) return st;
     int32_t* h_cnt = (int32_t*)e->h_out;
     orbx_keypoint* h_kps = (orbx_keypoint*)(e->h_out + 64);

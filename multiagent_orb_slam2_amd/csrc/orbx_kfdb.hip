@@ -451,20 +451,6 @@ __device__ __forceinline__ PostState post_state(int kind, int n, int q, const Qu
     return p;
 }
 
-__device__ void bitonic_u64(unsigned long long* a, int P2) {
-    for (int k = 2; k <= P2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < P2; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long x = a[i], y = a[ixj];
-                    if ((x > y) == ((i & k) == 0)) { a[i] = y; a[ixj] = x; }
-                }
-            }
-            __syncthreads();
-        }
-}
-
 __global__ __launch_bounds__(256) void k_kfdb_accum(DbDev D, QueryIn Q, QScratch X, StateDev St, int kind, int32_t* __restrict__ out,
                                                     int out_stride, int32_t* __restrict__ out_n, int32_t* __restrict__ status) {
     __shared__ unsigned long long key[kKfdbMaxRetained];
@@ -543,7 +529,7 @@ __global__ __launch_bounds__(256) void k_kfdb_accum(DbDev D, QueryIn Q, QScratch
     while (P2 < R) P2 <<= 1;
     for (int i = R + threadIdx.x; i < P2; i += T) key[i] = ~0ull;
     __syncthreads();
-    bitonic_u64(key, P2);
+    block_bitonic_u64(key, P2);
     // sbest[pos] = best keyframe in list order; then sort (best, pos) to find first occurrences
     for (int i = threadIdx.x; i < R; i += T) sbest[i] = rbest[key[i] & 0xFFF];
     __syncthreads();
@@ -552,7 +538,7 @@ __global__ __launch_bounds__(256) void k_kfdb_accum(DbDev D, QueryIn Q, QScratch
         if (i < R) keep[i] = 0;
     }
     __syncthreads();
-    bitonic_u64(key, P2);
+    block_bitonic_u64(key, P2);
     for (int i = threadIdx.x; i < R; i += T)
         if (i == 0 || (key[i] >> 12) != (key[i - 1] >> 12)) keep[key[i] & 0xFFF] = 1;
     __syncthreads();

@@ -416,8 +416,73 @@ __device__ void bow_node(const BowArgs& A, int a) {
             if (rok[c]) load_desc(A.d2 + 32 * (size_t)i2, r0[c], r1[c]);
         }
     }
-    uint64_t taken = 0;   // bit c: candidate c*64 + lane already matched
     int local = 0;
+    if (nc <= kWave) {
+        // Small node (the common case): lanes = 64 queries compute their best / second-best over ALL candidates at
+        // once (candidate descriptors broadcast by v_readlane), then the greedy loop walks the queries in order with
+        // the "already matched" set as one scalar bit mask over candidate positions.  A query's precomputed result is
+        // the exact one unless its best position bp or a position j2 (!= bp) holding its second-best value has been
+        // taken: without them removed the minimum and its first position are unchanged, and the second-best over
+        // the remaining positions is still reached at j2.  Only then is the query redone over the untaken candidates.
+        const uint64_t rokm = __ballot(rok[0]);
+        uint64_t taken = 0;
+        for (int qb = q0; qb < q1; qb += kWave) {
+            const int nq = min(kWave, q1 - qb);
+            int qi = 0, qv = 0;
+            uint4 qx0 = make_uint4(0, 0, 0, 0), qx1 = qx0;
+            if (ln < nq) {
+                qi = A.f1.idx[qb + ln];
+                qv = A.v1[qi] != 0;
+                if (qv) load_desc(A.d1 + 32 * (size_t)qi, qx0, qx1);
+            }
+            int b1 = 256, bp = -1, b2 = 256, j2 = -1;          // the reference's sequential rule, candidate order
+            for (int j = 0; j < nc; ++j) {
+                if (!((rokm >> j) & 1)) continue;
+                uint4 y0, y1;
+                y0.x = __builtin_amdgcn_readlane(r0[0].x, j); y0.y = __builtin_amdgcn_readlane(r0[0].y, j);
+                y0.z = __builtin_amdgcn_readlane(r0[0].z, j); y0.w = __builtin_amdgcn_readlane(r0[0].w, j);
+                y1.x = __builtin_amdgcn_readlane(r1[0].x, j); y1.y = __builtin_amdgcn_readlane(r1[0].y, j);
+                y1.z = __builtin_amdgcn_readlane(r1[0].z, j); y1.w = __builtin_amdgcn_readlane(r1[0].w, j);
+                const int d = hamming256(qx0, qx1, y0, y1);
+                if (d < b1) { b2 = b1; j2 = bp; b1 = d; bp = j; }
+                else if (d < b2) { b2 = d; j2 = j; }
+            }
+            for (int k = 0; k < nq; ++k) {
+                if (!__builtin_amdgcn_readlane(qv, k)) continue;
+                int kb1 = __builtin_amdgcn_readlane(b1, k), kbp = __builtin_amdgcn_readlane(bp, k);
+                int kb2 = __builtin_amdgcn_readlane(b2, k);
+                const int kj2 = __builtin_amdgcn_readlane(j2, k);
+                if ((kbp >= 0 && ((taken >> kbp) & 1)) || (kj2 >= 0 && ((taken >> kj2) & 1))) {
+                    uint4 x0, x1;
+                    x0.x = __builtin_amdgcn_readlane(qx0.x, k); x0.y = __builtin_amdgcn_readlane(qx0.y, k);
+                    x0.z = __builtin_amdgcn_readlane(qx0.z, k); x0.w = __builtin_amdgcn_readlane(qx0.w, k);
+                    x1.x = __builtin_amdgcn_readlane(qx1.x, k); x1.y = __builtin_amdgcn_readlane(qx1.y, k);
+                    x1.z = __builtin_amdgcn_readlane(qx1.z, k); x1.w = __builtin_amdgcn_readlane(qx1.w, k);
+                    const int d = (rok[0] && !((taken >> ln) & 1)) ? hamming256(x0, x1, r0[0], r1[0]) : 256;
+                    wave_best2(d, ln < nc ? ln : 0xfffff, kb1, kbp, kb2);
+                }
+                const bool pass = A.kff ? (kb1 <= kThLow) : (kb1 < kThLow);      // :230 vs :600
+                if (pass && (float)kb1 < A.nnratio * (float)kb2) {
+                    taken |= 1ull << kbp;
+                    if (ln == 0) {
+                        const int i1 = __builtin_amdgcn_readlane(qi, k);
+                        const int i2 = A.f2.idx[c0 + kbp];
+                        const int ridx = A.kff ? i2 : i1;
+                        A.match[ridx] = A.kff ? i1 : i2;
+                        if (A.checkOri) {
+                            const int bn = rot_bin(A.a1[(size_t)i1 * A.as1], A.a2[(size_t)i2 * A.as2]);
+                            A.bin[ridx] = bn;
+                            atomicAdd(&A.hist[bn], 1);
+                        }
+                    }
+                    ++local;
+                }
+            }
+        }
+        if (ln == 0 && local) atomicAdd(A.nmatch, local);
+        return;
+    }
+    uint64_t taken = 0;   // bit c: candidate c*64 + lane already matched
     for (int qb = q0; qb < q1; qb += kWave) {
         // 64 queries at a time: lane k holds query qb+k (index, MapPoint flag, descriptor); the sequential
         // greedy loop below reads them with v_readlane, so it issues no memory loads of its own

@@ -9,7 +9,7 @@
 //   k_vocab_words      one thread per descriptor: descend the k-ary tree, at each level the child with
 //                      the smallest Hamming distance (first minimum, strict <, :1244), record the node
 //                      at level L - levelsup, return the leaf's word id and weight.
-//   k_vocab_aggregate  one workgroup per descriptor set: FeatureVector = (node, feature) pairs sorted
+//   k_vocab_aggregate  two workgroups per descriptor set: FeatureVector = (node, feature) pairs sorted
 //                      (bitonic, LDS) and run-length grouped; BowVector = (word) sorted, TF-IDF weights
 //                      accumulated in feature order per word (BowVector::addWeight), L1 norm summed
 //                      sequentially in word order (BowVector::normalize) so doubles match bit for bit.
@@ -74,20 +74,6 @@ __global__ __launch_bounds__(256) void k_vocab_words(VocabDev V, const uint8_t* 
     node[o] = nid;
 }
 
-__device__ void bitonic64(unsigned long long* a, int P2) {
-    for (int k = 2; k <= P2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < P2; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long x = a[i], y = a[ixj];
-                    if ((x > y) == ((i & k) == 0)) { a[i] = y; a[ixj] = x; }
-                }
-            }
-            __syncthreads();
-        }
-}
-
 struct BowOut {
     uint32_t* words; double* values; int32_t* n_words;
     uint32_t* fv_nodes; int32_t* fv_off; int32_t* fv_idx; int32_t* n_fv;
@@ -97,6 +83,7 @@ __global__ __launch_bounds__(kVocabAggThreads) void k_vocab_aggregate(const int3
                                                                       const int32_t* __restrict__ word, const double* __restrict__ wgt,
                                                                       const int32_t* __restrict__ node, int weighting, int scoring,
                                                                       BowOut out) {
+    // blockIdx.y = 0: FeatureVector of set blockIdx.x; 1: its BowVector (independent, so two workgroups per set)
     __shared__ unsigned long long key[kVocabMaxSet];
     __shared__ int flag[kVocabMaxSet + 1];
     __shared__ int tmp[64];
@@ -105,11 +92,13 @@ __global__ __launch_bounds__(kVocabAggThreads) void k_vocab_aggregate(const int3
     const size_t o = (size_t)img * stride;
     int P2 = 1;
     while (P2 < n) P2 <<= 1;
-    // ---- FeatureVector: (node, feature) for features whose word is not stopped (w > 0)
+    const bool fv = blockIdx.y == 0;
+    // (node or word, feature) for features whose word is not stopped (w > 0)
+    const int32_t* kv = fv ? node : word;
     for (int i = tid; i < P2; i += T)
-        key[i] = (i < n && wgt[o + i] > 0) ? ((unsigned long long)(uint32_t)node[o + i] << 32) | (uint32_t)i : ~0ull;
+        key[i] = (i < n && wgt[o + i] > 0) ? ((unsigned long long)(uint32_t)kv[o + i] << 32) | (uint32_t)i : ~0ull;
     __syncthreads();
-    bitonic64(key, P2);
+    block_bitonic_u64(key, P2);
     for (int i = tid; i < P2; i += T) flag[i] = (key[i] != ~0ull && (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32))) ? 1 : 0;
     __syncthreads();
     int nv = 0;   // number of valid entries
@@ -120,27 +109,24 @@ __global__ __launch_bounds__(kVocabAggThreads) void k_vocab_aggregate(const int3
     nv = 0;
     for (int wv = 0; wv < (T >> 6); ++wv) nv += tmp[32 + wv];
     __syncthreads();
-    const int nnodes = block_scan_array(flag, P2, tmp);   // flag[i] = index of i's group if it starts one
-    for (int i = tid; i < nv; i += T) {
-        out.fv_idx[o + i] = (int32_t)(key[i] & 0xffffffffu);
-        const bool start = (i == 0) || (key[i] >> 32) != (key[i - 1] >> 32);
-        if (start) {
-            out.fv_nodes[o + flag[i]] = (uint32_t)(key[i] >> 32);
-            out.fv_off[o + img + flag[i]] = i;   // offsets array has stride + 1 per image: index o + img
+    if (fv) {
+        // ---- FeatureVector: node groups of the sorted (node, feature) list
+        const int nnodes = block_scan_array(flag, P2, tmp);   // flag[i] = index of i's group if it starts one
+        for (int i = tid; i < nv; i += T) {
+            out.fv_idx[o + i] = (int32_t)(key[i] & 0xffffffffu);
+            const bool start = (i == 0) || (key[i] >> 32) != (key[i - 1] >> 32);
+            if (start) {
+                out.fv_nodes[o + flag[i]] = (uint32_t)(key[i] >> 32);
+                out.fv_off[o + img + flag[i]] = i;   // offsets array has stride + 1 per image: index o + img
+            }
         }
+        if (tid == 0) {
+            out.fv_off[o + img + nnodes] = nv;
+            out.n_fv[img] = nnodes;
+        }
+        return;
     }
-    if (tid == 0) {
-        out.fv_off[o + img + nnodes] = nv;
-        out.n_fv[img] = nnodes;
-    }
-    __syncthreads();
-    // ---- BowVector: (word, feature) sorted; one value per word
-    for (int i = tid; i < P2; i += T)
-        key[i] = (i < n && wgt[o + i] > 0) ? ((unsigned long long)(uint32_t)word[o + i] << 32) | (uint32_t)i : ~0ull;
-    __syncthreads();
-    bitonic64(key, P2);
-    for (int i = tid; i < P2; i += T) flag[i] = (key[i] != ~0ull && (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32))) ? 1 : 0;
-    __syncthreads();
+    // ---- BowVector: one value per word of the sorted (word, feature) list
     const int nwords = block_scan_array(flag, P2, tmp);
     // per word: its weight accumulated in feature order (addWeight: one += per further occurrence), kept in
     // registers until every thread is done reading key[], then written over key[] as doubles
@@ -293,7 +279,7 @@ static int vocab_launch(orbx_vocab* v, const uint8_t* d_desc, const int32_t* d_c
     hipLaunchKernelGGL(k_vocab_words, dim3((stride + 255) / 256, batch), dim3(256), 0, s, v->dev, d_desc, d_counts, n_fixed,
                        stride, nid_level > 0 ? nid_level : -1, d_word, d_wgt, d_node);
     if (aggregate)
-        hipLaunchKernelGGL(k_vocab_aggregate, dim3(batch), dim3(kVocabAggThreads), 0, s, d_counts, n_fixed, stride, d_word,
+        hipLaunchKernelGGL(k_vocab_aggregate, dim3(batch, 2), dim3(kVocabAggThreads), 0, s, d_counts, n_fixed, stride, d_word,
                            d_wgt, d_node, v->weighting, v->scoring, out);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;

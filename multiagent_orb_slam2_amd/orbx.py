@@ -144,6 +144,7 @@ def load_library(path: str = LIB_PATH):
         getattr(lib, name).argtypes = [vp]
     lib.orbx_extract.argtypes = [vp, vp, i32, i32, C.c_size_t, vp, vp, i32, C.POINTER(i32)]
     lib.orbx_extract_batch_device.argtypes = [vp, vp, i32, i32, i32, C.c_size_t, C.c_size_t, vp, vp, vp, i32, vp]
+    lib.orbx_extract_batch_device_split.argtypes = [vp, vp, i32, i32, i32, C.c_size_t, C.c_size_t, vp, vp, vp, i32, vp, vp]
     lib.orbx_extractor_reserve.argtypes = [vp, i32, i32, i32]
     lib.orbx_extractor_set_pyramid_ring.argtypes = [vp, i32]
     lib.orbx_extractor_max_keypoints.argtypes = [vp, i32, i32]
@@ -372,9 +373,11 @@ class ORBextractor:
         return out
 
     # --- batched device path (torch tensors on cuda:device)
-    def extract_batch_device(self, images, kps=None, desc=None, counts=None, stream=None):
+    def extract_batch_device(self, images, kps=None, desc=None, counts=None, stream=None, out_stream=None):
         """images: uint8 tensor (B, rows, cols) on the GPU.  Returns (kps (B, cap, 28) uint8 view-able as
-        KP_DTYPE, desc (B, cap, 32) uint8, counts (B,) int32), all device tensors."""
+        KP_DTYPE, desc (B, cap, 32) uint8, counts (B,) int32), all device tensors.  With out_stream the descriptor
+        stage runs there and the outputs are complete in out_stream order (orbx_extract_batch_device_split): the
+        next call on `stream` overlaps this call's descriptor stage."""
         import torch
         B, rows, cols = images.shape
         cap = self.max_keypoints(rows, cols)
@@ -386,8 +389,13 @@ class ORBextractor:
         if counts is None:
             counts = torch.empty((B,), dtype=torch.int32, device=dev)
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream)
-        _check(self._lib.orbx_extract_batch_device(self._h, _tp(images), B, rows, cols, images.stride(1),
-                                                   images.stride(0), _tp(kps), _tp(desc), _tp(counts), cap, s))
+        if out_stream is None:
+            _check(self._lib.orbx_extract_batch_device(self._h, _tp(images), B, rows, cols, images.stride(1),
+                                                       images.stride(0), _tp(kps), _tp(desc), _tp(counts), cap, s))
+        else:
+            _check(self._lib.orbx_extract_batch_device_split(self._h, _tp(images), B, rows, cols, images.stride(1),
+                                                             images.stride(0), _tp(kps), _tp(desc), _tp(counts), cap, s,
+                                                             C.c_void_p(out_stream.cuda_stream)))
         return kps, desc, counts
 
     def enable_timing(self, on: bool = True):

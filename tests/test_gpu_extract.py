@@ -116,3 +116,32 @@ def test_batch_device_equals_single(gpu):
         kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
         assert n == len(k1)
         assert np.array_equal(kb, k1) and np.array_equal(desc[i, :n], d1)
+
+
+@pytest.mark.parametrize("ring", [1, 2])
+def test_split_streams_back_to_back(gpu, ring):
+    """orbx_extract_batch_device_split: calls issued back to back without a host sync, the descriptor stage on a
+    second stream, so call k+1's front half overlaps call k's descriptor stage.  Every call must equal the
+    single-image host API (the extractor orders its own buffer reuse across calls)."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    batches = [np.stack([S.kitti_like_image(300 + 7 * b + i) for i in range(3)]) for b in range(4)]
+    ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    ex.set_pyramid_ring(ring)
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+    ts = [torch.from_numpy(b).cuda() for b in batches]
+    torch.cuda.synchronize()
+    outs = []
+    for t in ts:
+        outs.append(ex.extract_batch_device(t, stream=s_in, out_stream=s_out))
+    torch.cuda.synchronize()
+    ex1 = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    for b, (kps, desc, cnt) in zip(batches, outs):
+        kps, desc, cnt = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+        for i in range(len(b)):
+            k1, d1 = ex1(b[i])
+            n = int(cnt[i])
+            kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
+            assert n == len(k1)
+            assert np.array_equal(kb, k1) and np.array_equal(desc[i, :n], d1)
