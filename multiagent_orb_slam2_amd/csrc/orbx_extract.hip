@@ -669,6 +669,20 @@ __device__ unsigned long long g_fbprof[2][16];
 #define FBP(k) do {} while (0)
 #endif
 
+// Diagnostics build only (make variant D=-DORBX_FAST_STOP=k): the workgroup stops after phase k (1 ROI load, 2 pre-test
+// and survivor list, 3 scores, 4 NMS) and reports empty cells -- the time of the phases before k, for ablation.
+#ifdef ORBX_FAST_STOP
+#define FAST_STOP(k)                                                                                                 \
+    do {                                                                                                             \
+        if ((k) == ORBX_FAST_STOP) {                                                                                 \
+            if (tid < nc) cell_cnt[(size_t)img * ncells + bd.cell0 + tid] = 0;                                       \
+            return;                                                                                                  \
+        }                                                                                                            \
+    } while (0)
+#else
+#define FAST_STOP(k) do {} while (0)
+#endif
+
 template <int kPairStride, bool kOE>
 __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                    const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
@@ -750,6 +764,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
         __syncthreads();
     }
     FBP(1);
+    FAST_STOP(1);
     if (live) {
         // 2. compass pre-test over the band's pixel pairs at tp (as k_fast_cells).  The survivor list keeps pair
         //    order (row-major: the score and NMS passes then read neighbouring LDS words lane by lane, no bank
@@ -795,6 +810,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
         }
         __syncthreads();
         FBP(2);
+        FAST_STOP(2);
         // 3. closed-form scores of the survivors
         for (int i = tid; i < ns; i += 256) {
             const int rr = list[i] >> 8, j = list[i] & 0xff;
@@ -803,6 +819,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
         }
         __syncthreads();
         FBP(3);
+        FAST_STOP(3);
         // 4. masked NMS at iniTh and minTh; kept pixels appended to their cell's lists (key = row * 128 + column in
         //    the cell's window: row-major order)
         for (int i = tid; i < ns; i += 256) {
@@ -827,6 +844,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
         }
         __syncthreads();
         FBP(4);
+        FAST_STOP(4);
 #ifdef ORBX_QT_PROF
         if (tid == 0 && item == 8 * 37 + 3) { g_fbprof[band0 ? 1 : 0][8] = ns; g_fbprof[band0 ? 1 : 0][9] = NP; }
 #endif
@@ -1606,6 +1624,168 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     }
 }
 
+// Sum of v over the kLp-lane group of each lane (groups of 16, 32 or 64 lanes), in every lane of the group.
+template <int kLp>
+__device__ __forceinline__ int group_sum(int v, int sub) {
+    v += __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);    // quad_perm 1,0,3,2
+    v += __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);    // quad_perm 2,3,0,1
+    v += __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false);   // row_mirror: row sum in every lane of the row
+    if (kLp == 16) return v;
+    const int r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const int r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    if (kLp == 32) return sub == 0 ? r0 + r1 : r2 + r3;
+    return r0 + r1 + r2 + r3;
+}
+
+// k_describe with kKpw keypoints per wave (kLp = 64 / kKpw lanes each): the wave-uniform part of a keypoint (level
+// lookup, moment reductions, fastAtan2, the double sin/cos, the keypoint record) is paid once per kKpw keypoints,
+// and each lane loads kKpw times as many window chunks and runs kKpw times as many BRIEF tests.  The keypoints of a
+// wave can straddle a level boundary, so the level is per lane.  Same results as k_describe, bit for bit.
+template <int kKpw>
+__global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                                                    size_t pyr_stride, const LevelDev* __restrict__ levels, int nlevels,
+                                                    const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
+                                                    int out_stride, const int* __restrict__ level_cnt,
+                                                    orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                    int32_t* __restrict__ counts, int capacity, int slot0, int nslots,
+                                                    int write_count, int batch, Src0 s0, SlotTable tab) {
+    constexpr int kLp = kWave / kKpw;
+    constexpr int kWinItems = 5 * (2 * kBriefR + 1);             // 37 rows x 5 chunks of 8 bytes
+    constexpr int kNW = (kWinItems + kLp - 1) / kLp;             // window chunks per lane
+    constexpr int kIcItems = 4 * (2 * kHalfPatch + 1);           // 31 rows x 4 chunks (124)
+    constexpr int kNI = (kIcItems + kLp - 1) / kLp;              // IC chunks per lane
+    constexpr int kNT = 256 / kLp;                               // BRIEF tests per lane
+    static_assert(kKpw == 2 || kKpw == 4, "2 or 4 keypoints per wave");
+    __shared__ __attribute__((aligned(16))) uint8_t brief_lds[4 * kKpw * kBriefWin];
+    const int per_wg = 4 * kKpw;
+    const int nbx = (nslots + per_wg - 1) / per_wg;
+    const int item = xcd_item(xcd_chunk(nbx * batch));
+    if (item >= nbx * batch) return;
+    const int img = item / nbx;
+    const int wrel = __builtin_amdgcn_readfirstlane(((item - img * nbx) * blockDim.x + threadIdx.x) >> 6);
+    if (wrel * kKpw >= nslots) return;                           // whole wave
+    const int ln = lane_id();
+    const int sub = ln / kLp, lk = ln - sub * kLp;
+    const int rel = wrel * kKpw + sub;
+    const int slot = slot0 + rel;
+    int lvl = 0;
+#pragma unroll
+    for (int l = 1; l < kMaxLevels; ++l) lvl += (l < nlevels && slot >= tab.out_off[l]) ? 1 : 0;
+    const int* lc = level_cnt + img * nlevels;
+    int off = 0, total = 0;
+    for (int l = 0; l < nlevels; ++l) {
+        const int c = lc[l];
+        off += l < lvl ? c : 0;
+        total += c;
+    }
+    if (write_count && wrel == 0 && ln == 0) counts[img] = min(total, capacity);
+    const LevelDev& L = levels[lvl];
+    const int lw = L.w, lpo = L.pyr_off, loo = L.out_off;
+    const int i = slot - loo;
+    const int o = off + i;
+    const bool valid = rel < nslots && i < lc[lvl] && o < capacity;
+    if (__ballot(valid) == 0) return;                            // whole wave
+
+    const uint32_t xy = valid ? lvl_xy[(size_t)img * out_stride + loo + i] : 0u;
+    const int cx = (int)(xy & 0xffff), cy = (int)(xy >> 16);
+    const uint8_t* B = blur + img * pyr_stride + lpo;
+    uint8_t* win = brief_lds + ((threadIdx.x >> 6) * kKpw + sub) * kBriefWin;
+    uint64_t wv[kNW];
+    if (valid) {
+        const uint8_t* w0 = B + (size_t)(cy - kBriefR) * lw + (cx - kBriefR);
+#pragma unroll
+        for (int k = 0; k < kNW; ++k) {
+            const int q = lk + kLp * k, r = min(q / 5, 2 * kBriefR), c = q - (q / 5) * 5;
+            __builtin_memcpy(&wv[k], w0 + (size_t)r * lw + 8 * c, 8);
+        }
+    }
+    int pstride;
+    const uint8_t* P = lvl == 0 ? s0.p + img * s0.istride : pyr + img * pyr_stride + lpo;
+    pstride = lvl == 0 ? (int)s0.step : lw;
+    int m10 = 0, m01 = 0;
+    {
+        uint64_t ic[kNI];
+        const uint8_t* p0 = P + (size_t)(cy - kHalfPatch) * pstride + (cx - kHalfPatch);
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < kNI; ++k) {
+                const int q = lk + kLp * k, r = min(q >> 2, 2 * kHalfPatch);
+                __builtin_memcpy(&ic[k], p0 + (size_t)r * pstride + 8 * (q & 3), 8);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kNI; ++k) {
+            const int q = lk + kLp * k;
+            const int v = (q >> 2) - kHalfPatch, av = v < 0 ? -v : v;
+            const int um = kUmax[av > 15 ? 15 : av];
+            const int u0 = 8 * (q & 3) - kHalfPatch;
+            const int lo = max(0, -um - u0), hi = min(7, um - u0);
+            uint64_t m = 0;
+            if (valid && q < kIcItems && lo <= hi) m = (hi >= 7 ? ~0ull : ((1ull << (8 * hi + 8)) - 1ull)) & (~0ull << (8 * lo));
+            const uint64_t px = ic[k] & m;
+            const uint32_t a = (uint32_t)px, b = (uint32_t)(px >> 32);
+            const uint32_t wa = (uint32_t)(u0 + 16) * 0x01010101u + 0x03020100u, wb = wa + 0x04040404u;
+            const int dot = (int)__builtin_amdgcn_udot4(b, wb, __builtin_amdgcn_udot4(a, wa, 0u, false), false);
+            const int sum = (int)__builtin_amdgcn_udot4(b, 0x01010101u, __builtin_amdgcn_udot4(a, 0x01010101u, 0u, false), false);
+            m10 += dot - 16 * sum;
+            m01 += v * sum;
+        }
+    }
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < kNW; ++k) {
+            const int q = lk + kLp * k;
+            if (q < kWinItems) *reinterpret_cast<uint64_t*>(win + (q / 5) * kBriefRow + 8 * (q % 5)) = wv[k];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    m10 = group_sum<kLp>(m10, sub);
+    m01 = group_sum<kLp>(m01, sub);
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    const float ang = __fmul_rn(angle, (float)(M_PI / 180.f));
+    float a, b;
+    orbx_sincos_brief(ang, &a, &b);
+    const uint8_t* center = win + kBriefR * kBriefRow + kBriefR;
+    uint32_t words[kNT];                                          // this lane's keypoint: tests g*kLp .. g*kLp+kLp-1
+#pragma unroll
+    for (int g = 0; g < kNT; ++g) {
+        const int t = g * kLp + lk;
+        const uint32_t pw = reinterpret_cast<const uint32_t*>(c_pattern)[t];
+        int vals[2] = {0, 0};
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
+            const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
+            const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
+            if (valid) vals[e] = center[__float2int_rn(ry) * kBriefRow + __float2int_rn(rx)];
+        }
+        const uint64_t bm = __ballot(vals[0] < vals[1]);
+        words[g] = (uint32_t)(bm >> (sub * kLp)) & (uint32_t)((1ull << kLp) - 1ull);
+    }
+    if (!valid) return;
+    // descriptor dword j (j < 8) of this lane's keypoint, written by lane lk = j
+    uint32_t dw = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t w = kLp == 32 ? words[j] : (words[2 * j] | (words[2 * j + 1] << 16));
+        dw = lk == j ? w : dw;
+    }
+    if (lk < 8) reinterpret_cast<uint32_t*>(desc + ((size_t)img * capacity + o) * 32)[lk] = dw;
+    if (lk == 0) {
+        orbx_keypoint k;
+        float x = (float)cx, y = (float)cy;
+        if (lvl != 0) { x = __fmul_rn(x, L.scale); y = __fmul_rn(y, L.scale); }
+        k.x = x; k.y = y;
+        k.size = (float)L.patch;
+        k.angle = angle;
+        k.response = (float)lvl_r[(size_t)img * out_stride + loo + i];
+        k.octave = lvl;
+        k.class_id = -1;
+        kps[(size_t)img * capacity + o] = k;
+    }
+}
+
 // =============================================================================================
 // host side
 // =============================================================================================
@@ -1644,6 +1824,7 @@ struct Extractor {
     hipEvent_t ev_lvl[kMaxLevels] = {};
     hipEvent_t ev_fast1 = nullptr;
     int fast_split = 0;
+    int desc_kpw = 2;         // keypoints per k_describe wave (ORBX_DESC_KPW = 1, 2 or 4)
     int desc_split = 0;       // ORBX_DESC_SPLIT=1: level-0 describe on the side stream (measured 1.29 vs 1.26 ms/step)
     // Describe stream (orbx_extract_batch_device_split): k_describe runs on the caller's output stream, so the next
     // call's front half (resize chain, FAST) on the input stream overlaps this call's describe.  What the next call
@@ -2234,8 +2415,10 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     for (int l = 0; l < nl; ++l) tab.out_off[l] = e->lv[l].out_off;
     auto describe = [&](hipStream_t q, int slot0, int nslots, int write_count) {
         if (nslots <= 0) return;
-        dim3 g(kXcds * xcd_chunk((nslots + 3) / 4 * batch));
-        hipLaunchKernelGGL(k_describe, g, dim3(256), 0, q, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
+        const int kpw = e->desc_kpw;                                // keypoints per wave (1, 2 or 4)
+        dim3 g(kXcds * xcd_chunk((nslots + 4 * kpw - 1) / (4 * kpw) * batch));
+        auto kern = kpw == 4 ? k_describe_m<4> : kpw == 2 ? k_describe_m<2> : k_describe;
+        hipLaunchKernelGGL(kern, g, dim3(256), 0, q, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
                            e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, slot0, nslots, write_count, batch, s0,
                            tab);
     };
@@ -2364,6 +2547,10 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
     if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;
     if (const char* ds = std::getenv("ORBX_DESC_SPLIT")) e->desc_split = std::atoi(ds) != 0;
+    if (const char* dk = std::getenv("ORBX_DESC_KPW")) {
+        const int v = std::atoi(dk);
+        e->desc_kpw = v == 4 ? 4 : v == 1 ? 1 : 2;
+    }
     if (const char* rt = std::getenv("ORBX_RESIZE_TAIL")) e->tail_from = std::atoi(rt);
     if (const char* qs = std::getenv("ORBX_QT_SPLIT")) e->qt_split = std::atoi(qs) != 0;
     if (int st = check_constants(e)) {

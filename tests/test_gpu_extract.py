@@ -145,3 +145,27 @@ def test_split_streams_back_to_back(gpu, ring):
             kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
             assert n == len(k1)
             assert np.array_equal(kb, k1) and np.array_equal(desc[i, :n], d1)
+
+
+@pytest.mark.parametrize("kpw", [1, 2, 4])
+def test_describe_keypoints_per_wave(gpu, monkeypatch, kpw):
+    """k_describe (one keypoint per wave) and k_describe_m (2 or 4 per wave, levels straddling a wave) give the same
+    bits: ORBX_DESC_KPW picks the form at extractor creation.  Batched, so waves also straddle images' slot ends."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    monkeypatch.setenv("ORBX_DESC_KPW", str(kpw))
+    imgs = np.stack([S.kitti_like_image(400 + i) for i in range(3)])
+    ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).cuda())
+    torch.cuda.synchronize()
+    kps, desc, cnt = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+    for i in range(len(imgs)):
+        ref = O.extract(imgs[i])
+        n = int(cnt[i])
+        kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
+        assert np.array_equal(kb, ref["kps"]) and np.array_equal(desc[i, :n], ref["desc"]), _diff_report(
+            kb, desc[i, :n], ref["kps"], ref["desc"])
+    # odd feature budget and level count: level slot ranges of odd lengths
+    _check(S.kitti_like_image(410, rows=240, cols=333), nfeatures=777, nlevels=5, scale=1.3)
