@@ -683,6 +683,9 @@ __device__ unsigned long long g_fbprof[2][16];
 #define FAST_STOP(k) do {} while (0)
 #endif
 
+#ifndef ORBX_FAST_QUAD
+#define ORBX_FAST_QUAD 1
+#endif
 template <int kPairStride, bool kOE>
 __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                    const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
@@ -770,44 +773,121 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
         //    order (row-major: the score and NMS passes then read neighbouring LDS words lane by lane, no bank
         //    conflicts): per (iteration, wave) the ballot goes to LDS, wave 0 scans the counts, every lane places
         //    its survivors at base + rank in its wave's ballot (NP <= 32 * 256, checked on the host)
-        const int PR = (Wd + 1) >> 1, NP = Hd * PR;
-        const int rr0 = tid / PR, j0 = tid - rr0 * PR;
-        const int dq = 256 / PR, dj = 256 - dq * PR;
         const int w = tid >> 6, ln = lane_id();
-        uint64_t* bmt = reinterpret_cast<uint64_t*>(lds + lay.o_bm);          // [it][wave]
         int* bbase = reinterpret_cast<int*>(lds + lay.o_bm + kBandMaxIt * 4 * 8);
-        const int nit = (NP + 255) >> 8;
-        uint32_t sm = 0;
-        for (int q = tid, it = 0, rr = rr0, j = j0; it < nit; q += 256, ++it) {
-            int pt = 0;
-            if (q < NP) {
-                const bool two = 2 * j + 1 < Wd;
-                pt = fast_pretest2<kPairStride, kOE>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
-                *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
-            }
-            const uint64_t bm = __ballot(pt != 0);
-            if (ln == 0) bmt[it * 4 + w] = bm;
-            sm |= (pt ? 1u : 0u) << it;
-            rr += dq; j += dj;
-            if (j >= PR) { j -= PR; ++rr; }
-        }
-        __syncthreads();
-        if (w == 0) {   // exclusive prefix over (iteration, wave) of the survivor counts: 2 entries per lane
-            const int e0 = 2 * ln, e1 = 2 * ln + 1, ne = 4 * nit;
-            const int c0 = e0 < ne ? __popcll(bmt[e0]) : 0, c1 = e1 < ne ? __popcll(bmt[e1]) : 0;
-            const int inc = wave_incl_scan(c0 + c1);
-            if (e0 < ne) bbase[e0] = inc - c0 - c1;
-            if (e1 < ne) bbase[e1] = inc - c1;
-            if (ln == kWave - 1) counters[0] = inc;
-        }
-        __syncthreads();
-        const int ns = counters[0];
         const uint64_t below = (1ull << ln) - 1ull;
-        for (int it = 0, rr = rr0, j = j0; it < nit; ++it) {   // (it < 32: no shift by >= 32)
-            if ((sm >> it) & 1) list[bbase[it * 4 + w] + __popcll(bmt[it * 4 + w] & below)] = (uint16_t)((rr << 8) | j);
-            rr += dq; j += dj;
-            if (j >= PR) { j -= PR; ++rr; }
+        if constexpr (kOE && ORBX_FAST_QUAD) {
+            // Quad form: a lane tests 4 consecutive pairs of one row (pairs 4u .. 4u+3), reading the 7 E words of row y
+            // and the 5 of rows y-3 / y+3 with 16/8-byte LDS reads (9 reads per 4 pairs instead of 32) and forming the
+            // O words by v_alignbit.  Per (iteration, wave) the survivor-pair count goes to LDS (3 ballots of the
+            // per-lane counts 0..4), wave 0 scans them, and the placement pass keeps pair order (lane-major within
+            // a wave, then its pairs).
+            const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
+            int* cnt_t = reinterpret_cast<int*>(lds + lay.o_bm);             // [it][wave] survivor pairs
+            const int nit = (NQ4 + 255) >> 8;                                // <= 16 (host: NP <= 8192, Hd <= 66)
+            const int rq0 = tid / QR, u0 = tid - rq0 * QR;
+            const int dq = 256 / QR, du = 256 - dq * QR;
+            uint64_t sm = 0;                                                 // 4 bits (surviving pairs) per iteration
+            for (int it = 0, rr = rq0, u = u0; it < nit; ++it) {
+                uint32_t mq = 0;
+                if (rr < Hd) {
+                    const uint32_t* e0 = E + rr * kPairStride + 4 * u;       // row y-3 (16-byte aligned)
+                    const uint32_t* e1 = e0 + 3 * kPairStride;               // row y
+                    const uint32_t* e2 = e0 + 6 * kPairStride;               // row y+3
+                    uint32_t A[7], U[6], D[6];
+                    {
+                        const uint4 a = *reinterpret_cast<const uint4*>(e1);
+                        const uint2 b = *reinterpret_cast<const uint2*>(e1 + 4);
+                        A[0] = a.x; A[1] = a.y; A[2] = a.z; A[3] = a.w; A[4] = b.x; A[5] = b.y; A[6] = e1[6];
+                        const uint2 u23 = *reinterpret_cast<const uint2*>(e0 + 2), u45 = *reinterpret_cast<const uint2*>(e0 + 4);
+                        U[0] = 0; U[1] = e0[1]; U[2] = u23.x; U[3] = u23.y; U[4] = u45.x; U[5] = u45.y;
+                        const uint2 d23 = *reinterpret_cast<const uint2*>(e2 + 2), d45 = *reinterpret_cast<const uint2*>(e2 + 4);
+                        D[0] = 0; D[1] = e2[1]; D[2] = d23.x; D[3] = d23.y; D[4] = d45.x; D[5] = d45.y;
+                    }
+                    int16_t* srow = sc + (rr + 1) * SW + 2 + 8 * u;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int j = 4 * u + k;
+                        const s16x2 v = as_s2(align16(A[k + 2], A[k + 1]));             // O[y][j+1]: pixels of pair j
+                        const s16x2 d0 = v - as_s2(align16(D[k + 2], D[k + 1]));        // ( 0,  3)
+                        const s16x2 d4 = v - as_s2(A[k + 3]);                           // ( 3,  0)
+                        const s16x2 d8 = v - as_s2(align16(U[k + 2], U[k + 1]));        // ( 0, -3)
+                        const s16x2 d12 = v - as_s2(A[k]);                              // (-3,  0)
+                        const s16x2 dk = pmax(pmax(pmin(d0, d4), pmin(d4, d8)), pmax(pmin(d8, d12), pmin(d12, d0)));
+                        const s16x2 br = pmin(pmin(pmax(d0, d4), pmax(d4, d8)), pmin(pmax(d8, d12), pmax(d12, d0)));
+                        const s16x2 m = pmax(dk, (s16x2)(0) - br);
+                        const bool two = 2 * j + 1 < Wd;
+                        const int pm = j < PR ? (two ? 3 : 1) : 0;
+                        const int pt = ((m.x > tp ? 1 : 0) | (m.y > tp ? 2 : 0)) & pm;
+                        mq |= (pt != 0 ? 1u : 0u) << k;
+                        if (j < PR) *reinterpret_cast<s16x2*>(srow + 2 * k) = (s16x2){0, (short)(two ? 0 : -1)};
+                    }
+                }
+                const int c = __builtin_popcount(mq);
+                const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+                if (ln == 0) cnt_t[it * 4 + w] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+                sm |= (uint64_t)mq << (4 * it);
+                rr += dq; u += du;
+                if (u >= QR) { u -= QR; ++rr; }
+            }
+            __syncthreads();
+            if (w == 0) {
+                const int e0 = 2 * ln, e1 = 2 * ln + 1, ne = 4 * nit;
+                const int c0 = e0 < ne ? cnt_t[e0] : 0, c1 = e1 < ne ? cnt_t[e1] : 0;
+                const int inc = wave_incl_scan(c0 + c1);
+                if (e0 < ne) bbase[e0] = inc - c0 - c1;
+                if (e1 < ne) bbase[e1] = inc - c1;
+                if (ln == kWave - 1) counters[0] = inc;
+            }
+            __syncthreads();
+            for (int it = 0, rr = rq0, u = u0; it < nit; ++it) {
+                const uint32_t mq = (uint32_t)(sm >> (4 * it)) & 15u;
+                const int c = __builtin_popcount(mq);
+                const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+                int pos = bbase[it * 4 + w] + __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if ((mq >> k) & 1u) list[pos++] = (uint16_t)((rr << 8) | (4 * u + k));
+                rr += dq; u += du;
+                if (u >= QR) { u -= QR; ++rr; }
+            }
+        } else {
+            const int PR = (Wd + 1) >> 1, NP = Hd * PR;
+            const int rr0 = tid / PR, j0 = tid - rr0 * PR;
+            const int dq = 256 / PR, dj = 256 - dq * PR;
+            uint64_t* bmt = reinterpret_cast<uint64_t*>(lds + lay.o_bm);          // [it][wave]
+            const int nit = (NP + 255) >> 8;
+            uint32_t sm = 0;
+            for (int q = tid, it = 0, rr = rr0, j = j0; it < nit; q += 256, ++it) {
+                int pt = 0;
+                if (q < NP) {
+                    const bool two = 2 * j + 1 < Wd;
+                    pt = fast_pretest2<kPairStride, kOE>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
+                    *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
+                }
+                const uint64_t bm = __ballot(pt != 0);
+                if (ln == 0) bmt[it * 4 + w] = bm;
+                sm |= (pt ? 1u : 0u) << it;
+                rr += dq; j += dj;
+                if (j >= PR) { j -= PR; ++rr; }
+            }
+            __syncthreads();
+            if (w == 0) {   // exclusive prefix over (iteration, wave) of the survivor counts: 2 entries per lane
+                const int e0 = 2 * ln, e1 = 2 * ln + 1, ne = 4 * nit;
+                const int c0 = e0 < ne ? __popcll(bmt[e0]) : 0, c1 = e1 < ne ? __popcll(bmt[e1]) : 0;
+                const int inc = wave_incl_scan(c0 + c1);
+                if (e0 < ne) bbase[e0] = inc - c0 - c1;
+                if (e1 < ne) bbase[e1] = inc - c1;
+                if (ln == kWave - 1) counters[0] = inc;
+            }
+            __syncthreads();
+            for (int it = 0, rr = rr0, j = j0; it < nit; ++it) {   // (it < 32: no shift by >= 32)
+                if ((sm >> it) & 1) list[bbase[it * 4 + w] + __popcll(bmt[it * 4 + w] & below)] = (uint16_t)((rr << 8) | j);
+                rr += dq; j += dj;
+                if (j >= PR) { j -= PR; ++rr; }
+            }
         }
+        const int ns = counters[0];
         __syncthreads();
         FBP(2);
         FAST_STOP(2);
