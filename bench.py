@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--inflight", type=int, default=1,
                     help="extractor contexts used in turn (step k on context k %% n, each on its own queue), so step k+1's "
                          "extraction can start while step k's tail runs")
+    ap.add_argument("--cu-exclude", type=int, default=int(os.environ.get("ORBX_CU_EXCLUDE", "0")),
+                    help="front-end and stereo streams leave this many CUs out of their CU mask (the keyframe stream keeps "
+                         "every CU), so the keyframe path's small kernels are not starved; 0 = plain streams")
     ap.add_argument("--distinct", type=int, default=128, help="distinct synthetic stereo pairs per rank (tiled to batch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
@@ -267,6 +270,7 @@ def load_profile(name):
 def main():
     args = parse()
     cfg = dict(CONFIGS[args.config])
+    os.environ["ORBX_CU_EXCLUDE"] = str(max(args.cu_exclude, 0))   # the extractors' side streams (read at creation)
     ROWS, COLS, NFEAT, BF = cfg["rows"], cfg["cols"], cfg["nfeatures"], cfg["bf"]
     BASELINE_B = BF / cfg["fx"]
     import torch
@@ -317,15 +321,17 @@ def main():
     outs = [(torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev),
              torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev),
              torch.empty((2 * B,), dtype=torch.int32, device=dev)) for _ in range(2)]
-    streams = [torch.cuda.Stream(dev) for _ in range(n_ctx)]   # front-end queues: one per extractor context
+    mk = (lambda prio=0: pkg.orbx.create_stream(dev.index, prio, args.cu_exclude)) if args.cu_exclude > 0 else \
+        (lambda prio=0: torch.cuda.Stream(dev, priority=prio))
+    streams = [mk() for _ in range(n_ctx)]                     # front-end queues: one per extractor context
     torch.cuda.set_stream(streams[0])
     # stereo queue: step k's ComputeStereoMatches (band match + SAD refinement on step k's pyramids) runs beside
     # step k+1's extraction; the extractor cycles two pyramid sets so that step k+1 does not overwrite step k's
-    stereo_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("ORBX_STEREO_PRIORITY", "0")))
+    stereo_stream = mk(int(os.environ.get("ORBX_STEREO_PRIORITY", "0")))
     # descriptor stage: on the stereo queue by default (stereo k needs describe k anyway).  A fifth busy queue is
     # starved by the hardware scheduler (measured: the keyframe path's small kernels then wait 0.1-0.3 ms each)
     desc_streams = ([stereo_stream] * n_ctx if args.desc_stream == 1 else
-                    [torch.cuda.Stream(dev) for _ in range(n_ctx)] if args.desc_stream == 2 else [None] * n_ctx)
+                    [mk() for _ in range(n_ctx)] if args.desc_stream == 2 else [None] * n_ctx)
     for e_ in exs:
         e_.set_pyramid_ring(2)
     # keyframe queue: BoW, packets, exchange, KeyFrameDatabase, SearchByBoW -- the native orbx_fusion object.  As in

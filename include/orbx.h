@@ -46,6 +46,13 @@ const char* orbx_version(void);
 /* Number of visible HIP devices (0 when none; never fails). */
 int orbx_device_count(void);
 
+/* A non-blocking stream on `device` (no reference counterpart: scheduling plumbing for device-API callers).
+ * cu_exclude > 0 leaves that many compute units out of the stream's CU mask (spread over the device), so that
+ * streams without a mask keep free CUs for latency-bound work; cu_exclude <= 0: a plain stream of `priority`.
+ * *out receives the hipStream_t. */
+int orbx_stream_create(int device, int priority, int cu_exclude, void** out);
+int orbx_stream_destroy(void* stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Extractor — replaces ORBextractor (src/ORBextractor.cc:410-1132)
  * ---------------------------------------------------------------------------------------------- */

@@ -15,6 +15,29 @@ namespace orbx {
 // An object's own stream (the queue of its host-API entry points), created on first use: an object driven only
 // through the device API (caller's streams) never creates one, so it holds no hardware queue -- streams beyond
 // GPU_MAX_HW_QUEUES share queues, and two busy streams on one queue serialise.
+// A non-blocking stream that may not use every compute unit: cu_exclude > 0 leaves that many CUs (every k-th of the
+// device's CU enumeration, so the excluded ones spread over the shader engines) out of its CU mask, so that work on
+// streams without the mask (the keyframe path's chain of small kernels) finds free CUs while the front end fills the
+// rest.  CU masks carry no priority; cu_exclude <= 0 gives a plain stream of the given priority.
+inline hipError_t create_stream_masked(hipStream_t* s, int priority, int cu_exclude) {
+    if (cu_exclude <= 0) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, priority);
+    int dev = 0, n = 0;
+    hipError_t he = hipGetDevice(&dev);
+    if (he == hipSuccess) he = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (he != hipSuccess) return he;
+    if (cu_exclude >= n) return hipErrorInvalidValue;
+    const int k = n / cu_exclude;
+    uint32_t mask[32] = {};
+    int words = (n + 31) / 32, dropped = 0;
+    if (words > 32) return hipErrorInvalidValue;
+    for (int i = 0; i < n; ++i) {
+        const bool drop = dropped < cu_exclude && (i % k) == k - 1;
+        dropped += drop ? 1 : 0;
+        if (!drop) mask[i >> 5] |= 1u << (i & 31);
+    }
+    return hipExtStreamCreateWithCUMask(s, (uint32_t)words, mask);
+}
+
 inline hipStream_t lazy_stream(hipStream_t& s, std::once_flag& once, int device) {
     std::call_once(once, [&] {
         int cur = 0;

@@ -139,6 +139,8 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_extractor_get_scale_factor.restype = f32
     lib.orbx_extractor_get_scale_factor.argtypes = [vp]
     lib.orbx_extractor_create.argtypes = [i32, f32, i32, i32, i32, i32, C.POINTER(vp)]
+    lib.orbx_stream_create.argtypes = [i32, i32, i32, C.POINTER(vp)]
+    lib.orbx_stream_destroy.argtypes = [vp]
     lib.orbx_matcher_create.argtypes = [f32, i32, i32, C.POINTER(vp)]
     for name in ("orbx_extractor_destroy", "orbx_matcher_destroy", "orbx_extractor_get_levels"):
         getattr(lib, name).argtypes = [vp]
@@ -254,6 +256,15 @@ def _tp(t):
 
 def device_count() -> int:
     return load_library().orbx_device_count()
+
+
+def create_stream(device: int = 0, priority: int = 0, cu_exclude: int = 0):
+    """A torch ExternalStream over orbx_stream_create: cu_exclude > 0 leaves that many CUs out of its CU mask (so
+    unmasked streams -- the keyframe path -- keep free CUs).  The stream lives as long as the process."""
+    import torch
+    h = C.c_void_p()
+    _check(load_library().orbx_stream_create(device, priority, cu_exclude, C.byref(h)))
+    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", device))
 
 
 def _featvec(fv):
