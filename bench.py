@@ -62,10 +62,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--batch", type=int, default=128, help="stereo frames per GPU per step (256 images per extractor launch)")
-    ap.add_argument("--desc-stream", type=int, default=0,
+    ap.add_argument("--desc-stream", type=int, default=1,
                     help="1: the extractor's descriptor stage on the stereo stream (orbx_extract_batch_device_split), "
                          "so step k+1's front end overlaps step k's descriptor stage; 2: on a stream of its own; 0: on "
                          "the launch stream")
+    ap.add_argument("--sets", type=int, default=3,
+                    help="output / pyramid sets in flight: step k's stereo and keyframe path read set k %% sets while later "
+                         "steps' front ends write the others (2: the front end of step k+2 waits for keyframe path k)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="extractor contexts used in turn (step k on context k %% n, each on its own queue), so step k+1's "
                          "extraction can start while step k's tail runs")
@@ -316,11 +319,12 @@ def main():
     m = pkg.ORBmatcher(0.6, True, device=dev.index)
     scale = ex.GetScaleFactors()
     cap = ex.max_keypoints(ROWS, COLS)
-    # two sets of extractor outputs: step k's keyframe path (on its own queue) reads set k % 2 while step k+1's
+    # NS sets of extractor outputs: step k's keyframe path (on its own queue) reads set k % NS while later steps'
     # front-end writes the other set; the front-end waits for the keyframe path of step k-1 before reusing a set
+    NS = max(2, args.sets)
     outs = [(torch.empty((2 * B, cap, 28), dtype=torch.uint8, device=dev),
              torch.empty((2 * B, cap, 32), dtype=torch.uint8, device=dev),
-             torch.empty((2 * B,), dtype=torch.int32, device=dev)) for _ in range(2)]
+             torch.empty((2 * B,), dtype=torch.int32, device=dev)) for _ in range(NS)]
     mk = (lambda prio=0: pkg.orbx.create_stream(dev.index, prio, args.cu_exclude)) if args.cu_exclude > 0 else \
         (lambda prio=0: torch.cuda.Stream(dev, priority=prio))
     streams = [mk() for _ in range(n_ctx)]                     # front-end queues: one per extractor context
@@ -328,19 +332,21 @@ def main():
     # stereo queue: step k's ComputeStereoMatches (band match + SAD refinement on step k's pyramids) runs beside
     # step k+1's extraction; the extractor cycles two pyramid sets so that step k+1 does not overwrite step k's
     stereo_stream = mk(int(os.environ.get("ORBX_STEREO_PRIORITY", "0")))
-    # descriptor stage: on the stereo queue by default (stereo k needs describe k anyway).  A fifth busy queue is
-    # starved by the hardware scheduler (measured: the keyframe path's small kernels then wait 0.1-0.3 ms each)
+    # descriptor stage: on the stereo queue by default (stereo k needs describe k anyway), so that step k+1's resize
+    # chain and level-0 FAST run beside step k's describe (2.115 -> 2.019 ms/step with 3 sets and an unthrottled
+    # host; on the launch stream the describe ran alone).  A fifth busy queue (--desc-stream 2) is starved by the
+    # hardware scheduler (measured: the keyframe path's small kernels then wait 0.1-0.3 ms each; 2.57 ms/step)
     desc_streams = ([stereo_stream] * n_ctx if args.desc_stream == 1 else
                     [mk() for _ in range(n_ctx)] if args.desc_stream == 2 else [None] * n_ctx)
     for e_ in exs:
-        e_.set_pyramid_ring(2)
+        e_.set_pyramid_ring(NS)
     # keyframe queue: BoW, packets, exchange, KeyFrameDatabase, SearchByBoW -- the native orbx_fusion object.  As in
     # the reference, where LoopClosing and MapFusion run in their own threads beside Tracking, step k's keyframe work
     # overlaps step k+1's extraction.
     # A stream of another priority gets a hardware queue of its own: two same-priority streams can land on one HW
     # queue (observed in a kernel trace: front-end and keyframe kernels then serialise, +0.5 ms per step).
     kf_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("ORBX_KF_PRIORITY", "-1")))
-    kf_done = [None, None]
+    kf_done = [None] * NS
     n_kf = max(1, B // KF_EVERY)
     voc = S.synthetic_vocabulary(2024, k=10, L=6)      # ORBvoc.txt's shape ("10 6 0 0"); the file is absent
     vocab = pkg.ORBVocabulary.from_arrays(voc, device=dev.index)
@@ -362,7 +368,7 @@ def main():
 
     def step(time_stereo=False):
         h0 = time.perf_counter()
-        buf = n_step[0] % 2
+        buf = n_step[0] % NS
         ex = exs[n_step[0] % n_ctx]
         stream = streams[n_step[0] % n_ctx]
         dstream = desc_streams[n_step[0] % n_ctx]       # the descriptor stage (writes the outputs)
@@ -454,12 +460,14 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     host_s = 0.0
+    split0 = list(host_split)
     for _ in range(args.steps):
         th = time.perf_counter()
         step(time_stereo=not args.no_timing)
         host_s += time.perf_counter() - th               # host time to enqueue one step (no sync inside)
         if args.sync_each:
             torch.cuda.synchronize()
+    split1 = list(host_split)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -481,6 +489,8 @@ def main():
         "host_enqueue_split_ms": {"front_end": round(1000 * pure_split[0], 3) if pure_n else None,
                                   "keyframe_path": round(1000 * pure_split[1], 3) if pure_n else None},
         "host_wall_ms_per_timed_step": round(1000 * host_s / args.steps, 3),
+        "host_wall_split_ms_per_timed_step": {"front_end": round(1000 * (split1[0] - split0[0]) / args.steps, 3),
+                                              "keyframe_path": round(1000 * (split1[1] - split0[1]) / args.steps, 3)},
         "config": {"workload": f"{args.config}: stereo frame = ORBextractor x2 ({COLS}x{ROWS}, 8 levels, {NFEAT} kpts) + "
                                "stereo L<->R 256-bit Hamming band match + SAD sub-pixel refinement; every 5th frame a "
                                "keyframe: DBoW2 transform (k=10, L=6) + " + ("RCCL all-gather of KF packets + " if world > 1 else "") +
@@ -510,8 +520,10 @@ def main():
         # Roofline of the extractor kernel launched ONCE over the whole batch: k_describe.  FAST, DistributeOctTree and
         # the blur are each split into a level-0 launch (side stream, concurrent with the resize chain) and a levels
         # 1..7 launch, so their event spans hold concurrent work and neither launch covers whole extractions;
-        # k_describe runs alone after the join, so its event span is its kernel duration (rocprof agrees).
-        kernel_of = {"describe": "k_describe"}
+        # k_describe is one launch over the whole batch (on the stereo queue, beside the next step's resize chain and
+        # level-0 FAST: its event span is its kernel duration under that overlap, as rocprof's).
+        kpw = int(os.environ.get("ORBX_DESC_KPW", "2"))
+        kernel_of = {"describe": "k_describe" if kpw == 1 else f"k_describe_m<{4 if kpw == 4 else 2}>"}
         dom = max(kernel_of, key=lambda k: per_call.get(k, 0.0))
         units = 2 * B                                    # extractions per launch
         cb = compulsory_bytes(cfg)

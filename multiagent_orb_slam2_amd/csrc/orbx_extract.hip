@@ -686,6 +686,10 @@ __device__ unsigned long long g_fbprof[2][16];
 #ifndef ORBX_FAST_QUAD
 #define ORBX_FAST_QUAD 1
 #endif
+#ifndef ORBX_FAST_ONEPASS
+#define ORBX_FAST_ONEPASS 1     // 0: iniTh pre-test first, minTh re-test of the cells left empty (bit-exact; measured
+                                // slower: serial FAST 0.930 -> 0.971 ms, the re-test phases cost more than the scores saved)
+#endif
 template <int kPairStride, bool kOE>
 __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                    const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
@@ -763,7 +767,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
                 cidx[x] = (uint8_t)(cx | ((x == cx * wc || x >= Wd) ? 0x80 : 0));
             }
         }
-        if (tid < 1 + 2 * kBandMaxCells) counters[tid] = 0;
+        if (tid < 24) counters[tid] = 0;                         // [20]: minTh re-test survivors
         __syncthreads();
     }
     FBP(1);
@@ -776,53 +780,60 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
         const int w = tid >> 6, ln = lane_id();
         int* bbase = reinterpret_cast<int*>(lds + lay.o_bm + kBandMaxIt * 4 * 8);
         const uint64_t below = (1ull << ln) - 1ull;
-        if constexpr (kOE && ORBX_FAST_QUAD) {
-            // Quad form: a lane tests 4 consecutive pairs of one row (pairs 4u .. 4u+3), reading the 7 E words of row y
-            // and the 5 of rows y-3 / y+3 with 16/8-byte LDS reads (9 reads per 4 pairs instead of 32) and forming the
-            // O words by v_alignbit.  Per (iteration, wave) the survivor-pair count goes to LDS (3 ballots of the
-            // per-lane counts 0..4), wave 0 scans them, and the placement pass keeps pair order (lane-major within
-            // a wave, then its pairs).
-            const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
-            int* cnt_t = reinterpret_cast<int*>(lds + lay.o_bm);             // [it][wave] survivor pairs
-            const int nit = (NQ4 + 255) >> 8;                                // <= 16 (host: NP <= 8192, Hd <= 66)
-            const int rq0 = tid / QR, u0 = tid - rq0 * QR;
-            const int dq = 256 / QR, du = 256 - dq * QR;
-            uint64_t sm = 0;                                                 // 4 bits (surviving pairs) per iteration
-            for (int it = 0, rr = rq0, u = u0; it < nit; ++it) {
-                uint32_t mq = 0;
-                if (rr < Hd) {
-                    const uint32_t* e0 = E + rr * kPairStride + 4 * u;       // row y-3 (16-byte aligned)
-                    const uint32_t* e1 = e0 + 3 * kPairStride;               // row y
-                    const uint32_t* e2 = e0 + 6 * kPairStride;               // row y+3
-                    uint32_t A[7], U[6], D[6];
-                    {
-                        const uint4 a = *reinterpret_cast<const uint4*>(e1);
-                        const uint2 b = *reinterpret_cast<const uint2*>(e1 + 4);
-                        A[0] = a.x; A[1] = a.y; A[2] = a.z; A[3] = a.w; A[4] = b.x; A[5] = b.y; A[6] = e1[6];
-                        const uint2 u23 = *reinterpret_cast<const uint2*>(e0 + 2), u45 = *reinterpret_cast<const uint2*>(e0 + 4);
-                        U[0] = 0; U[1] = e0[1]; U[2] = u23.x; U[3] = u23.y; U[4] = u45.x; U[5] = u45.y;
-                        const uint2 d23 = *reinterpret_cast<const uint2*>(e2 + 2), d45 = *reinterpret_cast<const uint2*>(e2 + 4);
-                        D[0] = 0; D[1] = e2[1]; D[2] = d23.x; D[3] = d23.y; D[4] = d45.x; D[5] = d45.y;
-                    }
-                    int16_t* srow = sc + (rr + 1) * SW + 2 + 8 * u;
+        // Quad form (kOE): a lane tests 4 consecutive pairs of one row (pairs 4u .. 4u+3), reading the 7 E words of row y
+        // and the 5 of rows y-3 / y+3 with 16/8-byte LDS reads (9 reads per 4 pairs instead of 32) and forming the O
+        // words by v_alignbit.  Per (iteration, wave) the survivor-pair count goes to LDS (3 ballots of the per-lane
+        // counts 0..4), wave 0 scans them, and the placement pass keeps pair order (lane-major within a wave, then its
+        // pairs).  With minTh < iniTh the pre-test runs at iniTh first (half the survivors to score on textured
+        // cells); the cells left without an iniTh corner are re-tested at minTh after the NMS (step 4b).
+        constexpr bool kQuad = kOE && ORBX_FAST_QUAD;
+        const bool two_pass = kQuad && !ORBX_FAST_ONEPASS && T2 < T1;  // workgroup-uniform
+        const int tA = two_pass ? T1 : tp;
+        const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
+        const int nit = (NQ4 + 255) >> 8;                                    // <= 16 (host: NP <= 8192, Hd <= 66)
+        const int rq0 = tid / QR, u0 = tid - rq0 * QR;
+        const int dq = 256 / QR, du = 256 - dq * QR;
+        uint64_t sm = 0;                                                     // 4 bits (surviving pairs) per iteration
+        // pre-test of quad (rr, u) at threshold t: bit k = pair 4u+k has a pixel with compass value > t
+        auto quad_test = [&](int rr, int u, int t, bool init_scores) -> uint32_t {
+            const uint32_t* e0 = E + rr * kPairStride + 4 * u;               // row y-3 (16-byte aligned)
+            const uint32_t* e1 = e0 + 3 * kPairStride;                       // row y
+            const uint32_t* e2 = e0 + 6 * kPairStride;                       // row y+3
+            uint32_t A[7], U[6], D[6];
+            {
+                const uint4 a = *reinterpret_cast<const uint4*>(e1);
+                const uint2 b = *reinterpret_cast<const uint2*>(e1 + 4);
+                A[0] = a.x; A[1] = a.y; A[2] = a.z; A[3] = a.w; A[4] = b.x; A[5] = b.y; A[6] = e1[6];
+                const uint2 u23 = *reinterpret_cast<const uint2*>(e0 + 2), u45 = *reinterpret_cast<const uint2*>(e0 + 4);
+                U[0] = 0; U[1] = e0[1]; U[2] = u23.x; U[3] = u23.y; U[4] = u45.x; U[5] = u45.y;
+                const uint2 d23 = *reinterpret_cast<const uint2*>(e2 + 2), d45 = *reinterpret_cast<const uint2*>(e2 + 4);
+                D[0] = 0; D[1] = e2[1]; D[2] = d23.x; D[3] = d23.y; D[4] = d45.x; D[5] = d45.y;
+            }
+            int16_t* srow = sc + (rr + 1) * SW + 2 + 8 * u;
+            uint32_t mq = 0;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const int j = 4 * u + k;
-                        const s16x2 v = as_s2(align16(A[k + 2], A[k + 1]));             // O[y][j+1]: pixels of pair j
-                        const s16x2 d0 = v - as_s2(align16(D[k + 2], D[k + 1]));        // ( 0,  3)
-                        const s16x2 d4 = v - as_s2(A[k + 3]);                           // ( 3,  0)
-                        const s16x2 d8 = v - as_s2(align16(U[k + 2], U[k + 1]));        // ( 0, -3)
-                        const s16x2 d12 = v - as_s2(A[k]);                              // (-3,  0)
-                        const s16x2 dk = pmax(pmax(pmin(d0, d4), pmin(d4, d8)), pmax(pmin(d8, d12), pmin(d12, d0)));
-                        const s16x2 br = pmin(pmin(pmax(d0, d4), pmax(d4, d8)), pmin(pmax(d8, d12), pmax(d12, d0)));
-                        const s16x2 m = pmax(dk, (s16x2)(0) - br);
-                        const bool two = 2 * j + 1 < Wd;
-                        const int pm = j < PR ? (two ? 3 : 1) : 0;
-                        const int pt = ((m.x > tp ? 1 : 0) | (m.y > tp ? 2 : 0)) & pm;
-                        mq |= (pt != 0 ? 1u : 0u) << k;
-                        if (j < PR) *reinterpret_cast<s16x2*>(srow + 2 * k) = (s16x2){0, (short)(two ? 0 : -1)};
-                    }
-                }
+            for (int k = 0; k < 4; ++k) {
+                const int j = 4 * u + k;
+                const s16x2 v = as_s2(align16(A[k + 2], A[k + 1]));             // O[y][j+1]: pixels of pair j
+                const s16x2 d0 = v - as_s2(align16(D[k + 2], D[k + 1]));        // ( 0,  3)
+                const s16x2 d4 = v - as_s2(A[k + 3]);                           // ( 3,  0)
+                const s16x2 d8 = v - as_s2(align16(U[k + 2], U[k + 1]));        // ( 0, -3)
+                const s16x2 d12 = v - as_s2(A[k]);                              // (-3,  0)
+                const s16x2 dk = pmax(pmax(pmin(d0, d4), pmin(d4, d8)), pmax(pmin(d8, d12), pmin(d12, d0)));
+                const s16x2 br = pmin(pmin(pmax(d0, d4), pmax(d4, d8)), pmin(pmax(d8, d12), pmax(d12, d0)));
+                const s16x2 m = pmax(dk, (s16x2)(0) - br);
+                const bool two = 2 * j + 1 < Wd;
+                const int pm = j < PR ? (two ? 3 : 1) : 0;
+                const int pt = ((m.x > t ? 1 : 0) | (m.y > t ? 2 : 0)) & pm;
+                mq |= (pt != 0 ? 1u : 0u) << k;
+                if (init_scores && j < PR) *reinterpret_cast<s16x2*>(srow + 2 * k) = (s16x2){0, (short)(two ? 0 : -1)};
+            }
+            return mq;
+        };
+        if constexpr (kQuad) {
+            int* cnt_t = reinterpret_cast<int*>(lds + lay.o_bm);             // [it][wave] survivor pairs
+            for (int it = 0, rr = rq0, u = u0; it < nit; ++it) {
+                const uint32_t mq = rr < Hd ? quad_test(rr, u, tA, true) : 0u;
                 const int c = __builtin_popcount(mq);
                 const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
                 if (ln == 0) cnt_t[it * 4 + w] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
@@ -852,13 +863,13 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
                 if (u >= QR) { u -= QR; ++rr; }
             }
         } else {
-            const int PR = (Wd + 1) >> 1, NP = Hd * PR;
+            const int NP = Hd * PR;
             const int rr0 = tid / PR, j0 = tid - rr0 * PR;
-            const int dq = 256 / PR, dj = 256 - dq * PR;
+            const int dqp = 256 / PR, dj = 256 - dqp * PR;
             uint64_t* bmt = reinterpret_cast<uint64_t*>(lds + lay.o_bm);          // [it][wave]
-            const int nit = (NP + 255) >> 8;
-            uint32_t sm = 0;
-            for (int q = tid, it = 0, rr = rr0, j = j0; it < nit; q += 256, ++it) {
+            const int nitp = (NP + 255) >> 8;
+            uint32_t smp = 0;
+            for (int q = tid, it = 0, rr = rr0, j = j0; it < nitp; q += 256, ++it) {
                 int pt = 0;
                 if (q < NP) {
                     const bool two = 2 * j + 1 < Wd;
@@ -867,13 +878,13 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
                 }
                 const uint64_t bm = __ballot(pt != 0);
                 if (ln == 0) bmt[it * 4 + w] = bm;
-                sm |= (pt ? 1u : 0u) << it;
-                rr += dq; j += dj;
+                smp |= (pt ? 1u : 0u) << it;
+                rr += dqp; j += dj;
                 if (j >= PR) { j -= PR; ++rr; }
             }
             __syncthreads();
             if (w == 0) {   // exclusive prefix over (iteration, wave) of the survivor counts: 2 entries per lane
-                const int e0 = 2 * ln, e1 = 2 * ln + 1, ne = 4 * nit;
+                const int e0 = 2 * ln, e1 = 2 * ln + 1, ne = 4 * nitp;
                 const int c0 = e0 < ne ? __popcll(bmt[e0]) : 0, c1 = e1 < ne ? __popcll(bmt[e1]) : 0;
                 const int inc = wave_incl_scan(c0 + c1);
                 if (e0 < ne) bbase[e0] = inc - c0 - c1;
@@ -881,9 +892,9 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
                 if (ln == kWave - 1) counters[0] = inc;
             }
             __syncthreads();
-            for (int it = 0, rr = rr0, j = j0; it < nit; ++it) {   // (it < 32: no shift by >= 32)
-                if ((sm >> it) & 1) list[bbase[it * 4 + w] + __popcll(bmt[it * 4 + w] & below)] = (uint16_t)((rr << 8) | j);
-                rr += dq; j += dj;
+            for (int it = 0, rr = rr0, j = j0; it < nitp; ++it) {   // (it < 32: no shift by >= 32)
+                if ((smp >> it) & 1) list[bbase[it * 4 + w] + __popcll(bmt[it * 4 + w] & below)] = (uint16_t)((rr << 8) | j);
+                rr += dqp; j += dj;
                 if (j >= PR) { j -= PR; ++rr; }
             }
         }
@@ -910,7 +921,7 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
             const bool bx = m01 & 0x80, bx1 = m01 & 0x8000, bx2 = m2 & 0x80;
             const uint32_t keep1 = (bx ? 0u : 0xffffu) | (bx1 ? 0u : 0xffff0000u);
             const uint32_t keep3 = (bx1 ? 0u : 0xffffu) | (bx2 ? 0u : 0xffff0000u);
-            const int f = nms_pair_band(sc, SW, rr, j, T1, T2, x + 1 < Wd, keep1, keep3);
+            const int f = nms_pair_band(sc, SW, rr, j, T1, T2, x + 1 < Wd, keep1, keep3) & (two_pass ? 3 : 15);
             if (f) {
                 const int c0 = m01 & 0x7f, c1 = (m01 >> 8) & 0x7f;
 #pragma unroll
@@ -923,10 +934,68 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
             }
         }
         __syncthreads();
+        if (two_pass) {
+            // 4b. cells without an iniTh corner (:812-816): pre-test at minTh the pairs touching them that did not pass at
+            //     iniTh (appended to the list), score those, then NMS at minTh over both lists for the pixels of these
+            //     cells.  Pixels of these cells passing at minTh are all scored now; neighbours in other cells are
+            //     masked, so the minTh keys are those of the one-pass form.
+            uint32_t fb = 0;
+            for (int cc = 0; cc < nc; ++cc) fb |= (counters[1 + 2 * cc] == 0 ? 1u : 0u) << cc;
+            if (fb) {
+                auto in_fb = [&](int x) { return (fb >> (cidx[x] & 0x7f)) & 1u; };
+                for (int it = 0, rr = rq0, u = u0; it < nit; ++it) {
+                    if (rr < Hd && (in_fb(8 * u) | in_fb(min(8 * u + 7, Wd - 1)))) {
+                        uint32_t mq = quad_test(rr, u, T2, false) & ~(uint32_t)(sm >> (4 * it)) & 15u;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const int x = 8 * u + 2 * k;
+                            if (((mq >> k) & 1u) && !(in_fb(x) | (x + 1 < Wd ? in_fb(x + 1) : 0u))) mq &= ~(1u << k);
+                        }
+                        if (mq) {
+                            int pos = ns + atomicAdd(&counters[20], __builtin_popcount(mq));
+#pragma unroll
+                            for (int k = 0; k < 4; ++k)
+                                if ((mq >> k) & 1u) list[pos++] = (uint16_t)((rr << 8) | (4 * u + k));
+                        }
+                    }
+                    rr += dq; u += du;
+                    if (u >= QR) { u -= QR; ++rr; }
+                }
+                __syncthreads();
+                const int ns2 = counters[20];
+                for (int i = ns + tid; i < ns + ns2; i += 256) {
+                    const int rr = list[i] >> 8, j = list[i] & 0xff;
+                    const s16x2 s2 = fast_score2<kPairStride, kOE>(E, O, rr + 3, j);
+                    *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
+                }
+                __syncthreads();
+                for (int i = tid; i < ns + ns2; i += 256) {
+                    const int rr = list[i] >> 8, j = list[i] & 0xff;
+                    const int x = 2 * j;
+                    const uint32_t m01 = *reinterpret_cast<const uint16_t*>(cidx + x);
+                    const uint32_t m2 = cidx[x + 2];
+                    const int c0 = m01 & 0x7f, c1 = (m01 >> 8) & 0x7f;
+                    if (!(((fb >> c0) & 1u) | (x + 1 < Wd ? (fb >> c1) & 1u : 0u))) continue;
+                    const bool bx = m01 & 0x80, bx1 = m01 & 0x8000, bx2 = m2 & 0x80;
+                    const uint32_t keep1 = (bx ? 0u : 0xffffu) | (bx1 ? 0u : 0xffff0000u);
+                    const uint32_t keep3 = (bx1 ? 0u : 0xffffu) | (bx2 ? 0u : 0xffff0000u);
+                    const int f = nms_pair_band(sc, SW, rr, j, T1, T2, x + 1 < Wd, keep1, keep3) >> 2;
+#pragma unroll
+                    for (int bit = 0; bit < 2; ++bit) {
+                        if (!((f >> bit) & 1)) continue;
+                        const int px = x + bit, cc = bit ? c1 : c0;
+                        if (!((fb >> cc) & 1u)) continue;
+                        const int pos = atomicAdd(&counters[1 + 2 * cc + 1], 1);
+                        if (pos < kmax) keys[(2 * cc + 1) * kmax + pos] = (uint16_t)(rr * 128 + (px - cc * wc));
+                    }
+                }
+                __syncthreads();
+            }
+        }
         FBP(4);
         FAST_STOP(4);
 #ifdef ORBX_QT_PROF
-        if (tid == 0 && item == 8 * 37 + 3) { g_fbprof[band0 ? 1 : 0][8] = ns; g_fbprof[band0 ? 1 : 0][9] = NP; }
+        if (tid == 0 && item == 8 * 37 + 3) { g_fbprof[band0 ? 1 : 0][8] = ns; g_fbprof[band0 ? 1 : 0][9] = Hd * PR; }
 #endif
     }
     // 5. per cell: iniTh keys, or minTh keys when the cell has none (:812-816); slot = rank in row-major order.
@@ -1904,6 +1973,7 @@ struct Extractor {
     hipEvent_t ev_lvl[kMaxLevels] = {};
     hipEvent_t ev_fast1 = nullptr;
     int fast_split = 0;
+    int desc_side = 0;        // ORBX_DESC_SIDE=1: describe at the end of the side stream (split entry point only)
     int desc_kpw = 2;         // keypoints per k_describe wave (ORBX_DESC_KPW = 1, 2 or 4)
     int desc_split = 0;       // ORBX_DESC_SPLIT=1: level-0 describe on the side stream (measured 1.29 vs 1.26 ms/step)
     // Describe stream (orbx_extract_batch_device_split): k_describe runs on the caller's output stream, so the next
@@ -2403,7 +2473,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     hipStream_t side = e->pipeline ? e->side : s;
     if (!e->pipeline) so = s;
     auto mark = [&](int k) {
-        if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : (k == 4 || k == 5) ? so : s);
+        const hipStream_t dq = (e->desc_side && side != s && so != s) ? side : so;
+        if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : (k == 4 || k == 5) ? dq : s);
     };
     // the previous call's describe (possibly on another stream) reads the kept keypoints and the blurred pyramid
     auto after_prev_describe = [&](hipStream_t q) -> int {
@@ -2539,15 +2610,20 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         quadtree(s, 0, nl);
     }
     mark(3);
-    if (so != s) {
+    // the descriptor stage: on the output stream, or (desc_side, with an output stream other than the launch stream)
+    // at the end of the side stream, so that the launch stream's next call (its resize chain) runs beside it without
+    // a further busy queue; the output stream then waits for it
+    const hipStream_t dq = (e->desc_side && side != s && so != s) ? side : so;
+    if (dq != s) {
         ORBX_HIP(hipEventRecord(e->ev_front, s));
-        ORBX_HIP(hipStreamWaitEvent(so, e->ev_front, 0));
+        ORBX_HIP(hipStreamWaitEvent(dq, e->ev_front, 0));
     }
-    if (side != so) ORBX_HIP(hipStreamWaitEvent(so, e->ev_join, 0));
+    if (side != dq) ORBX_HIP(hipStreamWaitEvent(dq, e->ev_join, 0));
     mark(4);
-    describe(so, d0_slots, e->out_stride - d0_slots, 1);
+    describe(dq, d0_slots, e->out_stride - d0_slots, 1);
     mark(5);
-    ORBX_HIP(hipEventRecord(e->ev_desc[slot], so));
+    ORBX_HIP(hipEventRecord(e->ev_desc[slot], dq));
+    if (dq != so) ORBX_HIP(hipStreamWaitEvent(so, e->ev_desc[slot], 0));
     e->desc_pending[slot] = true;
     e->desc_last = slot;
     ORBX_HIP(hipGetLastError());
@@ -2651,6 +2727,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
     if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;
     if (const char* ds = std::getenv("ORBX_DESC_SPLIT")) e->desc_split = std::atoi(ds) != 0;
+    if (const char* dsd = std::getenv("ORBX_DESC_SIDE")) e->desc_side = std::atoi(dsd) != 0;
     if (const char* dk = std::getenv("ORBX_DESC_KPW")) {
         const int v = std::atoi(dk);
         e->desc_kpw = v == 4 ? 4 : v == 1 ? 1 : 2;

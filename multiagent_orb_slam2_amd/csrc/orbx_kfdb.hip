@@ -615,7 +615,10 @@ __global__ __launch_bounds__(256) void k_kfdb_score_pairs(DbDev D, const int32_t
 
 using namespace orbx;
 
-constexpr int kKfdbStages = 4;
+#ifndef ORBX_KFDB_STAGES
+#define ORBX_KFDB_STAGES 16      // 4 throttled the bench host to the keyframe stream (1.54 of 2.1 ms per step blocked here)
+#endif
+constexpr int kKfdbStages = ORBX_KFDB_STAGES;
 
 struct orbx_kfdb {
     int device = 0;

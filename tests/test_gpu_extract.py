@@ -118,14 +118,16 @@ def test_batch_device_equals_single(gpu):
         assert np.array_equal(kb, k1) and np.array_equal(desc[i, :n], d1)
 
 
-@pytest.mark.parametrize("ring", [1, 2])
-def test_split_streams_back_to_back(gpu, ring):
+@pytest.mark.parametrize("ring,desc_side", [(1, 0), (2, 0), (2, 1)])
+def test_split_streams_back_to_back(gpu, monkeypatch, ring, desc_side):
     """orbx_extract_batch_device_split: calls issued back to back without a host sync, the descriptor stage on a
     second stream, so call k+1's front half overlaps call k's descriptor stage.  Every call must equal the
-    single-image host API (the extractor orders its own buffer reuse across calls)."""
+    single-image host API (the extractor orders its own buffer reuse across calls).  desc_side: the descriptor stage
+    at the end of the extractor's side stream (ORBX_DESC_SIDE=1), the output stream waiting for it."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
+    monkeypatch.setenv("ORBX_DESC_SIDE", str(desc_side))
     batches = [np.stack([S.kitti_like_image(300 + 7 * b + i) for i in range(3)]) for b in range(4)]
     ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
     ex.set_pyramid_ring(ring)
