@@ -120,6 +120,59 @@ __global__ __launch_bounds__(256) void k_bf_merge(const uint32_t* __restrict__ p
     second_dist[o] = second;
 }
 
+// k_bf_merge with the chunk walk split over 8 lanes per query (32 queries per workgroup): the (best key, second
+// distance) pair of a chunk range is a top-2 reduction -- best = the smallest (distance, index) key, second = the
+// second order statistic of the distances -- so partial pairs combine in any order: (k1, s1) + (k2, s2) =
+// k1 < k2 ? (k1, min(s1, d2)) : (k2, min(s2, d1)).  Each lane walks every 8th chunk (independent, coalesced
+// loads), the 8 partials meet in LDS.  Same results as the sequential chunk order of k_bf_merge.
+constexpr int kBfMergeG = 8;
+__global__ __launch_bounds__(256) void k_bf_merge_g(const uint32_t* __restrict__ pbest, const int32_t* __restrict__ psecond,
+                                                    int nq, int nchunks, int32_t* __restrict__ best_idx,
+                                                    int32_t* __restrict__ best_dist, int32_t* __restrict__ second_dist) {
+    constexpr int kQ = 256 / kBfMergeG;
+    __shared__ uint32_t sb[kBfMergeG][kQ];
+    __shared__ int32_t ss[kBfMergeG][kQ];
+    const int ql = threadIdx.x % kQ, g = threadIdx.x / kQ;
+    const int qi = blockIdx.x * kQ + ql, z = blockIdx.y;
+    uint32_t best = 256u << 20;
+    int second = 256;
+    if (qi < nq) {
+        const uint32_t* pb = pbest + (size_t)z * nchunks * nq + qi;
+        const int32_t* pss = psecond + (size_t)z * nchunks * nq + qi;
+#pragma unroll 4
+        for (int c = g; c < nchunks; c += kBfMergeG) {
+            const uint32_t b = pb[(size_t)c * nq];
+            const int sc = pss[(size_t)c * nq];
+            if (b < best) {
+                second = min(sc, (int)(best >> 20));
+                best = b;
+            } else {
+                second = min(second, (int)(b >> 20));
+            }
+        }
+    }
+    sb[g][ql] = best;
+    ss[g][ql] = second;
+    __syncthreads();
+    if (g != 0 || qi >= nq) return;
+#pragma unroll
+    for (int h = 1; h < kBfMergeG; ++h) {
+        const uint32_t b = sb[h][ql];
+        const int sc = ss[h][ql];
+        if (b < best) {
+            second = min(sc, (int)(best >> 20));
+            best = b;
+        } else {
+            second = min(second, (int)(b >> 20));
+        }
+    }
+    const int bd = (int)(best >> 20);
+    const size_t o = (size_t)z * nq + qi;
+    best_dist[o] = bd;
+    best_idx[o] = bd < 256 ? (int)(best & 0xfffff) : -1;
+    second_dist[o] = second;
+}
+
 // No train rows: every query keeps the reference's initial state (no match, distances 256).
 __global__ __launch_bounds__(256) void k_bf_empty(int n, int32_t* __restrict__ best_idx, int32_t* __restrict__ best_dist,
                                                   int32_t* __restrict__ second_dist) {
@@ -1146,7 +1199,11 @@ static int bf_launch(Matcher* m, const uint8_t* dq, int nq, size_t qs, const uin
     uint32_t* pb = (uint32_t*)scratch;
     int32_t* ps = (int32_t*)((uint8_t*)scratch + a256((size_t)nch * nq * nprob * 4));
     hipLaunchKernelGGL(k_bf_tile, dim3(qb, nch, nprob), dim3(256), 0, s, dq, nq, qs, dt, nt, ts, chunk, pb, ps);
-    hipLaunchKernelGGL(k_bf_merge, dim3((nq + 255) / 256, nprob), dim3(256), 0, s, pb, ps, nq, nch, bi, bd, sd);
+    if (nch >= 2 * kBfMergeG)   // a long chunk walk: split it over 8 lanes per query
+        hipLaunchKernelGGL(k_bf_merge_g, dim3((nq + 256 / kBfMergeG - 1) / (256 / kBfMergeG), nprob), dim3(256), 0, s, pb, ps,
+                           nq, nch, bi, bd, sd);
+    else
+        hipLaunchKernelGGL(k_bf_merge, dim3((nq + 255) / 256, nprob), dim3(256), 0, s, pb, ps, nq, nch, bi, bd, sd);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }

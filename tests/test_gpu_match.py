@@ -228,3 +228,21 @@ def test_search_for_triangulation(gpu, only_stereo):
     rn, rm = O.search_for_triangulation(d1, k1, mp1, ur1, fv1, d2, k2, mp2, ur2, fv1, F12, sigma2, scale, 600.0,
                                         180.0, only_stereo, True)
     assert n == rn and np.array_equal(m12, rm)
+
+
+def test_bf_match_ties_across_chunks(gpu):
+    """Long train sets split into many chunks (the grouped merge): equal distances in different chunks keep the first
+    train index, and the second distance counts the tie (strict '<' of ORBmatcher.cc:568-598)."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    rng = np.random.Generator(np.random.PCG64(5))
+    q = rng.integers(0, 256, (40, 32), dtype=np.uint8)
+    t = np.repeat(rng.integers(0, 256, (3, 32), dtype=np.uint8), 1500, axis=0)   # 4500 rows, three distinct values
+    t[4000:] = q[0]                                                                 # exact matches of query 0 late
+    t[100] = ~q[1]                                                                  # distance 256 for query 1
+    m = pkg.ORBmatcher()
+    got = m.bf_match(q, t)
+    ref = O.bf_match(q, t)
+    for g, r, name in zip(got, ref, ("best_idx", "best_dist", "second_dist")):
+        assert np.array_equal(g, r), name
+    assert got[0][0] == 4000 and got[1][0] == 0 and got[2][0] == 0
