@@ -333,7 +333,7 @@ def main():
              torch.empty((2 * B,), dtype=torch.int32, device=dev)) for _ in range(NS)]
     mk = (lambda prio=0: pkg.orbx.create_stream(dev.index, prio, args.cu_exclude)) if args.cu_exclude > 0 else \
         (lambda prio=0: torch.cuda.Stream(dev, priority=prio))
-    streams = [mk() for _ in range(n_ctx)]                     # front-end queues: one per extractor context
+    streams = [mk(int(os.environ.get("ORBX_MAIN_PRIORITY", "0"))) for _ in range(n_ctx)]   # front-end queues
     torch.cuda.set_stream(streams[0])
     # stereo queue: step k's ComputeStereoMatches (band match + SAD refinement on step k's pyramids) runs beside
     # step k+1's extraction; the extractor cycles two pyramid sets so that step k+1 does not overwrite step k's
