@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--sets", type=int, default=3,
                     help="output / pyramid sets in flight: step k's stereo and keyframe path read set k %% sets while later "
                          "steps' front ends write the others (2: the front end of step k+2 waits for keyframe path k)")
+    ap.add_argument("--pyr-sets", type=int, default=0,
+                    help="pyramid sets of the extractor ring (0 = --sets): step k's stereo SAD reads set k %% pyr-sets; "
+                         "the front end of step k + pyr-sets waits for that stereo step")
     ap.add_argument("--inflight", type=int, default=1,
                     help="extractor contexts used in turn (step k on context k %% n, each on its own queue), so step k+1's "
                          "extraction can start while step k's tail runs")
@@ -344,8 +347,10 @@ def main():
     # hardware scheduler (measured: the keyframe path's small kernels then wait 0.1-0.3 ms each; 2.57 ms/step)
     desc_streams = ([stereo_stream] * n_ctx if args.desc_stream == 1 else
                     [mk() for _ in range(n_ctx)] if args.desc_stream == 2 else [None] * n_ctx)
+    NP = args.pyr_sets if args.pyr_sets > 0 else NS
     for e_ in exs:
-        e_.set_pyramid_ring(NS)
+        e_.set_pyramid_ring(NP)
+    stereo_done = [None] * NP                          # per pyramid set: the stereo step that last read it
     # keyframe queue: BoW, packets, exchange, KeyFrameDatabase, SearchByBoW -- the native orbx_fusion object.  As in
     # the reference, where LoopClosing and MapFusion run in their own threads beside Tracking, step k's keyframe work
     # overlaps step k+1's extraction.
@@ -386,6 +391,9 @@ def main():
             stream.wait_event(kf_done[buf])
             if dstream is not None:
                 dstream.wait_event(kf_done[buf])
+        pslot = n_step[0] % NP
+        if stereo_done[pslot] is not None:
+            stream.wait_event(stereo_done[pslot])     # the resize chain overwrites the set that stereo step read
         ex.extract_batch_device(imgs, kps, desc, cnt, stream=stream, out_stream=dstream)
         extracted = torch.cuda.Event()
         extracted.record(ostream)
@@ -407,6 +415,7 @@ def main():
                 stereo_ms.append((e0, e1))
         handoff = torch.cuda.Event()
         handoff.record(stereo_stream)
+        stereo_done[pslot] = handoff
         h1 = time.perf_counter()
         if "keyframes" in skip:
             n_step[0] += 1
