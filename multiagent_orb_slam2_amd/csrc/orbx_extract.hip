@@ -367,6 +367,59 @@ __device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, con
     return pmax(dk[0], (s16x2)(0) - br[0]) - (s16x2)(1);
 }
 
+// fast_score2 on an f16-biased pair image (k_fast_band with ORBX_FAST_F16): every u16 lane holds the f16 value
+// 1024 + pixel (bits 0x6400 | pixel), so tap differences are exact f16 subtractions and the arc minima / maxima use
+// gfx950's 3-input packed f16 min / max (20 % fewer VALU operations than the i16 form).  Scores below 0 are raised to
+// -1 (never a corner, never blocks a neighbour in the NMS -- the same keypoints); the result is i16 like fast_score2.
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h16x2 as_h2(uint32_t v) { return __builtin_bit_cast(h16x2, v); }
+__device__ __forceinline__ h16x2 hmin(h16x2 a, h16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ h16x2 hmax(h16x2 a, h16x2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ h16x2 hmin3(h16x2 a, h16x2 b, h16x2 c) {
+    uint32_t r;
+    asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return as_h2(r);
+}
+__device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
+    uint32_t r;
+    asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return as_h2(r);
+}
+template <int kPairStride>
+__device__ __forceinline__ s16x2 fast_score2_f16(const uint32_t* __restrict__ E, int y, int j) {
+    const uint32_t* eb = E + (y - 3) * kPairStride + j;
+    uint32_t r[17];
+#define ORBX_TAP(k, dx, dy) \
+    r[k] = ((dx) & 1) ? eb[((dy) + 3) * kPairStride + (3 + (dx)) / 2] : o_at<true>(eb, eb, ((dy) + 3) * kPairStride + 1 + (dx) / 2)
+    ORBX_TAP(16, 0, 0);
+    ORBX_TAP(0, 0, 3);    ORBX_TAP(1, 1, 3);    ORBX_TAP(2, 2, 2);    ORBX_TAP(3, 3, 1);
+    ORBX_TAP(4, 3, 0);    ORBX_TAP(5, 3, -1);   ORBX_TAP(6, 2, -2);   ORBX_TAP(7, 1, -3);
+    ORBX_TAP(8, 0, -3);   ORBX_TAP(9, -1, -3);  ORBX_TAP(10, -2, -2); ORBX_TAP(11, -3, -1);
+    ORBX_TAP(12, -3, 0);  ORBX_TAP(13, -3, 1);  ORBX_TAP(14, -2, 2);  ORBX_TAP(15, -1, 3);
+#undef ORBX_TAP
+    const h16x2 v = as_h2(r[16]);
+    h16x2 d[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = v - as_h2(r[k]);
+    h16x2 a2[8], b2[8], a4[8], b4[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) { a2[m] = hmin(d[2 * m + 1], d[(2 * m + 2) & 15]); b2[m] = hmax(d[2 * m + 1], d[(2 * m + 2) & 15]); }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) { a4[m] = hmin(a2[m], a2[(m + 1) & 7]); b4[m] = hmax(b2[m], b2[(m + 1) & 7]); }
+    h16x2 dk[8], br[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const h16x2 e0 = d[2 * m], e9 = d[(2 * m + 9) & 15];
+        dk[m] = hmin3(a4[m], a4[(m + 2) & 7], hmax(e0, e9));
+        br[m] = hmax3(b4[m], b4[(m + 2) & 7], hmin(e0, e9));
+    }
+    const h16x2 dmax = hmax3(hmax3(dk[0], dk[1], dk[2]), hmax3(dk[3], dk[4], dk[5]), hmax(dk[6], dk[7]));
+    const h16x2 bmin = hmin3(hmin3(br[0], br[1], br[2]), hmin3(br[3], br[4], br[5]), hmin(br[6], br[7]));
+    const h16x2 zero = {(_Float16)0, (_Float16)0}, bias = {(_Float16)1024, (_Float16)1024};
+    const h16x2 m = hmax3(dmax, -bmin, zero) + bias;                // 1024 + max(m, 0): bits 0x6400 + value
+    return as_s2(__builtin_bit_cast(uint32_t, m)) - (s16x2){0x6401, 0x6401};
+}
+
 // Compass pre-test for a pixel pair: every arc of 9 contains two compass taps 4 apart (0/4, 4/8, 8/12 or
 // 12/0), so "corner at t" (some arc with all d > t, or all d < -t) implies max over those four pairs of
 // min(d_k, d_k+4) > t, or min of max < -t.  A pixel failing it has s < t.  Returns 2 bits (pixel x, x+1).
@@ -686,6 +739,9 @@ __device__ unsigned long long g_fbprof[2][16];
 #ifndef ORBX_FAST_QUAD
 #define ORBX_FAST_QUAD 1
 #endif
+#ifndef ORBX_FAST_F16
+#define ORBX_FAST_F16 1         // 0: i16 pair image and scores (fast_score2)
+#endif
 #ifndef ORBX_FAST_ONEPASS
 #define ORBX_FAST_ONEPASS 1     // 0: iniTh pre-test first, minTh re-test of the cells left empty (bit-exact; measured
                                 // slower: serial FAST 0.930 -> 0.971 ms, the re-test phases cost more than the scores saved)
@@ -750,8 +806,9 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
                         const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
                         lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
                     }
-                    const uint2 e = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u), __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
+                    uint2 e = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u), __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
                     const uint2 o = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c020c01u), __builtin_amdgcn_perm(hi, lo, 0x0c040c03u));
+                    if (kOE && ORBX_FAST_F16) { e.x |= 0x64006400u; e.y |= 0x64006400u; }   // f16 1024 + pixel
                     *reinterpret_cast<uint2*>(E + rs[k] * kPairStride + 2 * cs[k]) = e;
                     if (!kOE) *reinterpret_cast<uint2*>(O + rs[k] * kPairStride + 2 * cs[k]) = o;
                 }
@@ -905,7 +962,8 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
         // 3. closed-form scores of the survivors
         for (int i = tid; i < ns; i += 256) {
             const int rr = list[i] >> 8, j = list[i] & 0xff;
-            const s16x2 s2 = fast_score2<kPairStride, kOE>(E, O, rr + 3, j);
+            const s16x2 s2 = (kOE && ORBX_FAST_F16) ? fast_score2_f16<kPairStride>(E, rr + 3, j)
+                                                    : fast_score2<kPairStride, kOE>(E, O, rr + 3, j);
             *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
         }
         __syncthreads();
@@ -965,7 +1023,8 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
                 const int ns2 = counters[20];
                 for (int i = ns + tid; i < ns + ns2; i += 256) {
                     const int rr = list[i] >> 8, j = list[i] & 0xff;
-                    const s16x2 s2 = fast_score2<kPairStride, kOE>(E, O, rr + 3, j);
+                    const s16x2 s2 = (kOE && ORBX_FAST_F16) ? fast_score2_f16<kPairStride>(E, rr + 3, j)
+                                                    : fast_score2<kPairStride, kOE>(E, O, rr + 3, j);
                     *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
                 }
                 __syncthreads();
@@ -1962,10 +2021,11 @@ struct Extractor {
     // builds levels 1..7 (seven dependent, latency-bound resize launches) and runs FAST / DistributeOctTree on them.
     // The side stream then blurs levels 1..7 once the pyramid is done; k_describe joins both.
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_pyr = nullptr, ev_join = nullptr;
+    // Per-call events come from a pool (CallEvents below): an event is recorded again only 32 calls later, never
+    // while a wait on its previous record may still be in flight.
     int pipeline = 1;         // ORBX_PIPELINE: 1 two streams (above), 0 every launch in order on the launch stream
     int qt_split = 1;         // ORBX_QT_SPLIT: 1 level-0 quadtree on the side stream, 0 one quadtree launch (all levels)
-    hipEvent_t ev_fast0 = nullptr;   // side: FAST level 0 done (qt_split 0: the launch stream's quadtree waits on it)
+    // (fast0 in CallEvents: side FAST level 0 done -- with qt_split 0 the launch stream's quadtree waits on it)
     // Per-level FAST (fast_split, ORBX_FAST_SPLIT): FAST of level l >= 1 runs on its own stream as soon as the resize
     // chain has produced level l (ev_lvl[l]), so the latency-bound chain of seven resizes overlaps the FAST work of
     // the levels it has finished; the launch stream's DistributeOctTree waits for ev_fast1.
@@ -1979,11 +2039,22 @@ struct Extractor {
     // Describe stream (orbx_extract_batch_device_split): k_describe runs on the caller's output stream, so the next
     // call's front half (resize chain, FAST) on the input stream overlaps this call's describe.  What the next call
     // overwrites that describe reads is ordered by events: the kept keypoints and the blurred pyramid (its quadtree
-    // and blur wait for ev_desc_last) and its pyramid set (the resize chain waits for that set's last describe).
-    hipEvent_t ev_front = nullptr;                  // launch stream: quadtree of levels >= 1 done
-    hipEvent_t ev_desc[8] = {};                     // per pyramid set: describe of the last call on it done
-    bool desc_pending[8] = {};
-    int desc_last = -1;                             // set of the previous call (its describe event), -1 none
+    // and blur wait for the previous call's describe) and its pyramid set (the resize chain waits for that set's last
+    // describe).
+    static constexpr int kCallEv = 32;
+    struct CallEvents {
+        hipEvent_t fork, pyr, fast0, join, front, desc;   // fork from the caller, pyramid built, side FAST level 0,
+        bool used;                                         // side join, launch-stream quadtree, describe done
+    };
+    CallEvents cev[kCallEv] = {};
+    unsigned long long cev_next = 0;
+    int slot_call[8] = {-1, -1, -1, -1, -1, -1, -1, -1};   // per pyramid set: pool index of its last describe
+    int last_call = -1;                                    // pool index of the previous call, -1 none
+    int sync_calls() {                                     // every describe issued so far is done
+        for (auto& c : cev)
+            if (c.used) ORBX_HIP(hipEventSynchronize(c.desc));
+        return ORBX_OK;
+    }
 
     // geometry for the reserved size
     int rows = 0, cols = 0, max_batch = 0;
@@ -2155,6 +2226,9 @@ int Extractor::configure(int r, int c, int batch) {
     if (stream) ORBX_HIP(hipStreamSynchronize(stream));
     if (side) ORBX_HIP(hipStreamSynchronize(side));
     if (fastq) ORBX_HIP(hipStreamSynchronize(fastq));
+    if (int st0 = sync_calls()) return st0;                 // a describe still running on a caller's output stream
+    for (int& k : slot_call) k = -1;
+    last_call = -1;
     const int keep_batch = std::max(batch, (r == rows && c == cols) ? max_batch : 0);
     free_buffers();
     ORBX_REQUIRE(r > 0 && c > 0 && batch > 0, ORBX_ERR_ARG, "configure: bad size %dx%d batch %d", r, c, batch);
@@ -2470,6 +2544,10 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     e->last_src0 = s0;
     const int slot = (int)(e->ncalls++ % (unsigned long long)e->pyr_ring);
     e->d_pyr = e->d_pyr_ring + (size_t)slot * e->max_batch * ps;
+    // this call's events: the pool entry of 32 calls ago, whose describe (and every wait on its events) is long done
+    const int ci = (int)(e->cev_next++ % Extractor::kCallEv);
+    Extractor::CallEvents& ce = e->cev[ci];
+    if (ce.used) ORBX_HIP(hipEventSynchronize(ce.desc));
     hipStream_t side = e->pipeline ? e->side : s;
     if (!e->pipeline) so = s;
     auto mark = [&](int k) {
@@ -2478,7 +2556,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     };
     // the previous call's describe (possibly on another stream) reads the kept keypoints and the blurred pyramid
     auto after_prev_describe = [&](hipStream_t q) -> int {
-        if (e->desc_last >= 0) ORBX_HIP(hipStreamWaitEvent(q, e->ev_desc[e->desc_last], 0));
+        if (e->last_call >= 0) ORBX_HIP(hipStreamWaitEvent(q, e->cev[e->last_call].desc, 0));
         return ORBX_OK;
     };
     const int ncells = (int)e->cellv.size();
@@ -2519,12 +2597,13 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
 
     mark(0);
     if (side != s) {
-        ORBX_HIP(hipEventRecord(e->ev_fork, s));
-        ORBX_HIP(hipStreamWaitEvent(side, e->ev_fork, 0));
+        ORBX_HIP(hipEventRecord(ce.fork, s));
+        ORBX_HIP(hipStreamWaitEvent(side, ce.fork, 0));
     }
     const bool split_fast = side != s && e->fast_split && e->fast_band && !e->fast_stop_after && e->fastq;
     auto resize_chain = [&]() -> int {
-      if (e->desc_pending[slot]) ORBX_HIP(hipStreamWaitEvent(s, e->ev_desc[slot], 0));   // this set's last reader
+      if (e->slot_call[slot] >= 0)                                  // this set's last reader
+          ORBX_HIP(hipStreamWaitEvent(s, e->cev[e->slot_call[slot]].desc, 0));
       for (int l = 1; l < nl; ++l) {
         if (l >= e->tail_lt) {                                      // the small levels: one launch
             hipLaunchKernelGGL(k_resize_tail, dim3(batch), dim3(1024), 0, s, e->d_pyr, ps, e->tail_lt, nl, e->d_tail);
@@ -2557,7 +2636,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     const bool split = e->qt_split || side == s;
     if (int st = after_prev_describe(side)) return st;
     if (split) quadtree(side, 0, nl > 0 ? 1 : 0);
-    else ORBX_HIP(hipEventRecord(e->ev_fast0, side));
+    else ORBX_HIP(hipEventRecord(ce.fast0, side));
     mark(8);
     blur(side, 0, t0);
     // describe: slot table of the levels; level 0's keypoints on the side stream as soon as its quadtree and blur are
@@ -2579,12 +2658,12 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     if (side != s) {
         int st = resize_chain();                                    // launch stream: levels 1..nl-1 of the pyramid
         if (st) return st;
-        ORBX_HIP(hipEventRecord(e->ev_pyr, s));
-        ORBX_HIP(hipStreamWaitEvent(side, e->ev_pyr, 0));
+        ORBX_HIP(hipEventRecord(ce.pyr, s));
+        ORBX_HIP(hipStreamWaitEvent(side, ce.pyr, 0));
     }
     blur(side, t0, nt - t0);                                        // side: levels 1..nl-1 once the pyramid exists
     mark(9);
-    if (side != s) ORBX_HIP(hipEventRecord(e->ev_join, side));
+    if (side != s) ORBX_HIP(hipEventRecord(ce.join, side));
     mark(10);                                                       // launch stream: FAST, DistributeOctTree 1..nl-1
     if (split_fast) {
         const Extractor::BandLaunch& b = e->band_launch[1];
@@ -2606,7 +2685,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     if (split) {
         quadtree(s, 1, nl - 1);
     } else {
-        ORBX_HIP(hipStreamWaitEvent(s, e->ev_fast0, 0));
+        ORBX_HIP(hipStreamWaitEvent(s, ce.fast0, 0));
         quadtree(s, 0, nl);
     }
     mark(3);
@@ -2615,17 +2694,18 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     // a further busy queue; the output stream then waits for it
     const hipStream_t dq = (e->desc_side && side != s && so != s) ? side : so;
     if (dq != s) {
-        ORBX_HIP(hipEventRecord(e->ev_front, s));
-        ORBX_HIP(hipStreamWaitEvent(dq, e->ev_front, 0));
+        ORBX_HIP(hipEventRecord(ce.front, s));
+        ORBX_HIP(hipStreamWaitEvent(dq, ce.front, 0));
     }
-    if (side != dq) ORBX_HIP(hipStreamWaitEvent(dq, e->ev_join, 0));
+    if (side != dq) ORBX_HIP(hipStreamWaitEvent(dq, ce.join, 0));
     mark(4);
     describe(dq, d0_slots, e->out_stride - d0_slots, 1);
     mark(5);
-    ORBX_HIP(hipEventRecord(e->ev_desc[slot], dq));
-    if (dq != so) ORBX_HIP(hipStreamWaitEvent(so, e->ev_desc[slot], 0));
-    e->desc_pending[slot] = true;
-    e->desc_last = slot;
+    ORBX_HIP(hipEventRecord(ce.desc, dq));
+    if (dq != so) ORBX_HIP(hipStreamWaitEvent(so, ce.desc, 0));
+    ce.used = true;
+    e->slot_call[slot] = ci;
+    e->last_call = ci;
     ORBX_HIP(hipGetLastError());
     e->last_batch = batch;
     return ORBX_OK;
@@ -2704,12 +2784,9 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     const int side_prio = std::getenv("ORBX_SIDE_PRIORITY") ? std::atoi(std::getenv("ORBX_SIDE_PRIORITY")) : -1;
     const int cu_ex = std::getenv("ORBX_CU_EXCLUDE") ? std::atoi(std::getenv("ORBX_CU_EXCLUDE")) : 0;
     if (he == hipSuccess) he = create_stream_masked(&e->side, side_prio, cu_ex);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pyr, hipEventDisableTiming);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fast0, hipEventDisableTiming);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_front, hipEventDisableTiming);
-    for (int k = 0; k < 8 && he == hipSuccess; ++k) he = hipEventCreateWithFlags(&e->ev_desc[k], hipEventDisableTiming);
+    for (auto& c : e->cev)
+        for (hipEvent_t* ev : {&c.fork, &c.pyr, &c.fast0, &c.join, &c.front, &c.desc})
+            if (he == hipSuccess) he = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     // (every stream holds a hardware queue: streams beyond GPU_MAX_HW_QUEUES share queues and serialise, so the
     // per-level FAST stream exists only when that schedule is on)
     if (const char* fs = std::getenv("ORBX_FAST_SPLIT")) e->fast_split = std::atoi(fs) != 0;
@@ -2748,20 +2825,15 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->side) (void)hipStreamSynchronize(e->side);
     if (e->fastq) (void)hipStreamSynchronize(e->fastq);
-    for (int k = 0; k < 8; ++k)
-        if (e->desc_pending[k]) (void)hipEventSynchronize(e->ev_desc[k]);   // a describe on the caller's stream
+    (void)e->sync_calls();                                  // a describe on the caller's stream
     e->free_buffers();
     for (auto& es : e->tpool)
         for (auto& ev : es.ev) (void)hipEventDestroy(ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->side) (void)hipStreamDestroy(e->side);
-    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-    if (e->ev_pyr) (void)hipEventDestroy(e->ev_pyr);
-    if (e->ev_fast0) (void)hipEventDestroy(e->ev_fast0);
-    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
-    if (e->ev_front) (void)hipEventDestroy(e->ev_front);
-    for (auto& ev : e->ev_desc)
-        if (ev) (void)hipEventDestroy(ev);
+    for (auto& c : e->cev)
+        for (hipEvent_t ev : {c.fork, c.pyr, c.fast0, c.join, c.front, c.desc})
+            if (ev) (void)hipEventDestroy(ev);
     if (e->fastq) (void)hipStreamDestroy(e->fastq);
     if (e->ev_fast1) (void)hipEventDestroy(e->ev_fast1);
     for (auto& ev : e->ev_lvl)
@@ -2813,11 +2885,10 @@ int orbx_extractor_set_pyramid_ring(orbx_extractor* e, int n) {
     if (e->stream) ORBX_HIP(hipStreamSynchronize(e->stream));
     if (e->side) ORBX_HIP(hipStreamSynchronize(e->side));
     if (e->fastq) ORBX_HIP(hipStreamSynchronize(e->fastq));
-    for (int k = 0; k < 8; ++k)
-        if (e->desc_pending[k]) ORBX_HIP(hipEventSynchronize(e->ev_desc[k]));
+    if (int st = e->sync_calls()) return st;
     e->free_buffers();
-    for (int k = 0; k < 8; ++k) e->desc_pending[k] = false;
-    e->desc_last = -1;
+    for (int& k : e->slot_call) k = -1;
+    e->last_call = -1;
     e->pyr_ring = n;
     return (r > 0 && c > 0 && b > 0) ? e->configure(r, c, b) : ORBX_OK;
 }
