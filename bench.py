@@ -247,16 +247,19 @@ def c3_bench(pkg, dev, n_problems=64, reps=30):
                             ("batched", lambda: m.bf_match_batch_device(qb, tb, stream=s), n_problems)):
         for _ in range(3):
             fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(reps):
-            fn()
-        e1.record(s)
-        e1.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / reps
+        rounds = []                                # median of 5 windows of `reps` launches (one window once read
+        for _ in range(5):                         # 6x slow right after the bench step: a clock / power transient)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(reps):
+                fn()
+            e1.record(s)
+            e1.synchronize()
+            rounds.append(e0.elapsed_time(e1) * 1e3 / reps)
+        us = float(np.median(rounds))
         pairs = 2000 * 2000 * nprob
         alg = 144000 * nprob                       # 2 x 2000 x 32 B in + 2000 x 8 B out per match
-        out[name] = {"problems": nprob, "us_per_launch": round(us, 2), "matches_per_s": round(nprob / (us * 1e-6), 1),
+        out[name] = {"problems": nprob, "us_per_launch": round(us, 2), "us_per_launch_windows": [round(r, 2) for r in rounds], "matches_per_s": round(nprob / (us * 1e-6), 1),
                      "pair_distances_per_s": round(pairs / (us * 1e-6), 1),
                      "algorithmic_GBps": round(alg / (us * 1e-6) / 1e9, 2)}
     out["kernels"] = ("k_bf_tile (256 queries per workgroup, one per lane, train rows staged in LDS) + k_bf_merge_g "
