@@ -264,11 +264,11 @@ def c3_bench(pkg, dev, n_problems=64, reps=30):
                      "algorithmic_GBps": round(alg / (us * 1e-6) / 1e9, 2)}
     out["kernels"] = ("k_bf_tile (256 queries per workgroup, one per lane, train rows staged in LDS) + k_bf_merge_g "
                       "(chunk walk split over 8 lanes per query; k_bf_merge for short walks)")
-    c3p = load_profile("r2v_c3_summary.json")
+    c3p = load_profile("r2w_c3_summary.json")
     if c3p:   # VALU fraction of the tile kernel per launch shape (SQ_INSTS_VALU x 64 / profiled duration / peak)
         out["valu_frac_profiled"] = {("batched" if e["grid"] >= 524288 else "single"): e["valu_frac"]
                                      for e in c3p["launches"].values() if e["kernel"] == "k_bf_tile"}
-        out["profile"] = "profiles/r2v_c3_summary.json"
+        out["profile"] = "profiles/r2w_c3_summary.json"
     return out
 
 
