@@ -125,7 +125,10 @@ __global__ __launch_bounds__(256) void k_bf_merge(const uint32_t* __restrict__ p
 // second order statistic of the distances -- so partial pairs combine in any order: (k1, s1) + (k2, s2) =
 // k1 < k2 ? (k1, min(s1, d2)) : (k2, min(s2, d1)).  Each lane walks every 8th chunk (independent, coalesced
 // loads), the 8 partials meet in LDS.  Same results as the sequential chunk order of k_bf_merge.
-constexpr int kBfMergeG = 8;
+#ifndef ORBX_BF_MERGE_G
+#define ORBX_BF_MERGE_G 16
+#endif
+constexpr int kBfMergeG = ORBX_BF_MERGE_G;   // lanes per query (8: 7.4 us merge for one 2000x2000 problem)
 __global__ __launch_bounds__(256) void k_bf_merge_g(const uint32_t* __restrict__ pbest, const int32_t* __restrict__ psecond,
                                                     int nq, int nchunks, int32_t* __restrict__ best_idx,
                                                     int32_t* __restrict__ best_dist, int32_t* __restrict__ second_dist) {
