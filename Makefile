@@ -37,3 +37,15 @@ variant: $(OBJS)
 	$(HIPCC) $(HIPFLAGS) $(D) -c $(SRC)/orbx_extract.hip -o build/$(V)/orbx_extract.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/$(V)/liborbx.so build/$(V)/orbx_extract.o $(filter-out $(SRC)/orbx_extract.o,$(OBJS)) -ldl
 .PHONY: variant
+
+# ThreadSanitizer on the host code of liborbx and the native concurrency driver (tests/native/concurrency.cpp):
+# host-only instrumentation (-Xarch_host), device code untouched.  Run on a GPU box: scripts/tsan_gpu.sh
+TSAN := build/tsan
+tsan:
+	mkdir -p $(TSAN)
+	for f in orbx_extract orbx_match orbx_vocab orbx_proj orbx_kfdb orbx_fusion; do \
+	  $(HIPCC) $(HIPFLAGS) -Xarch_host -fsanitize=thread -Xarch_host -g -c $(SRC)/$$f.hip -o $(TSAN)/$$f.o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -fsanitize=thread -fno-gpu-sanitize -o $(TSAN)/liborbx.so $(TSAN)/*.o -ldl
+	$(HIPCC) -O1 -g -std=c++17 -fsanitize=thread -fno-gpu-sanitize -o $(TSAN)/concurrency tests/native/concurrency.cpp \
+	  -L$(TSAN) -lorbx -Wl,-rpath,'$$ORIGIN' -lpthread
+.PHONY: tsan
