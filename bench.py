@@ -268,7 +268,7 @@ def c3_bench(pkg, dev, n_problems=64, reps=30):
                      "pair_distances_per_s": round(pairs / (us * 1e-6), 1),
                      "algorithmic_GBps": round(alg / (us * 1e-6) / 1e9, 2)}
     out["kernels"] = ("k_bf_tile (256 queries per workgroup, one per lane, train rows staged in LDS) + k_bf_merge_g "
-                      "(chunk walk split over 8 lanes per query; k_bf_merge for short walks)")
+                      "(chunk walk split over 16 lanes per query; k_bf_merge for short walks)")
     c3p = load_profile("r2w_c3_summary.json")
     if c3p:   # VALU fraction of the tile kernel per launch shape (SQ_INSTS_VALU x 64 / profiled duration / peak)
         out["valu_frac_profiled"] = {("batched" if e["grid"] >= 524288 else "single"): e["valu_frac"]
