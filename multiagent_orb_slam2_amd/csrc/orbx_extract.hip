@@ -2,17 +2,20 @@
 // orbx_extract.hip — MI355X (gfx950) ORB extractor: the hot path of ORBextractor::operator()
 // (reference src/ORBextractor.cc:1043-1105) as batched HIP kernels behind the C-ABI of include/orbx.h.
 //
-// Per device call over a batch of B images (all rows x cols), one stream, 4 + (nlevels-1) launches:
+// Per device call over a batch of B images (all rows x cols), two streams (run_batch; §7 of DESIGN.md):
 //   (level 0 is read in place from the caller's images: no copy)   (ComputePyramid :1127)
-//   k_resize        level l-1 -> level l, l = 1..L-1 (chained)       (ComputePyramid :1120)
-//   k_fast_cells    one workgroup per (30-px grid cell, image): FAST-9 score map in LDS, 3x3 strict
-//                   NMS at iniThFAST, fallback to minThFAST when the cell is empty, row-major
-//                   compaction into per-cell candidate slots          (ComputeKeyPointsOctTree :789-829)
-//   k_blur7         7x7 sigma-2 Gaussian on every level (REFLECT_101), register-streaming (:1085-1086)
+//   k_resize4       level l-1 -> level l, l = 1..L-1 (chained, launch stream)      (ComputePyramid :1120)
+//   k_fast_band     one workgroup per (band of <= 4 cells of one cell row, image): the band ROI as an f16-biased
+//                   u16 pair image in LDS, compass pre-test in quads, closed-form FAST scores of the survivors,
+//                   cell-masked strict 3x3 NMS at iniThFAST / minThFAST, per-cell fallback and row-major slots
+//                   (level 0 on the side stream, levels 1..L-1 on the launch stream)   (:789-829)
+//   k_blur7         7x7 sigma-2 Gaussian on every level (REFLECT_101), register-streaming, side stream (:1085-1086)
 //   k_quadtree      one workgroup per (level, image): DistributeOctTree's list/quadtree as data-parallel
 //                   passes over LDS node arrays                     (:539-763, :834-847)
-//   k_describe      one wave per keypoint: IC angle on the level, steered BRIEF on the blurred level,
-//                   level-major output with coordinates scaled to level 0   (:77-147, :851-852, :1075-1104)
+//   k_describe_m    two keypoints per wave: IC angle on the level, steered BRIEF on the blurred level,
+//                   level-major output with coordinates scaled to level 0 (on the caller's output stream with
+//                   the split entry point)                            (:77-147, :851-852, :1075-1104)
+// Cross-call reuse of every buffer is ordered by events from a pool of per-call sets (Extractor::CallEvents).
 // Pinned arithmetic (identical to oracle/orb_oracle.cpp): fixed-point resize and blur,
 // round-half-even, no FMA contraction (-ffp-contract=off + explicit __f*_rn), correctly rounded
 // float cos/sin of the BRIEF angle, quadtree phase-2 ties in creation order.
