@@ -177,3 +177,25 @@ def test_oracle_regression_fixtures():
         assert r["ncand"].tolist() == case["ncand"]
         k0 = r["kps"][:8]
         assert [[float(v) for v in row] for row in k0.tolist()] == case["first_kps"]
+
+
+def test_model_f16_score_form():
+    """k_fast_band's f16 score form (orbx_extract.hip fast_score2_f16): pixels stored as f16 1024 + value, differences,
+    arc minima / maxima and the final max in f16, the score raised to -1 when below.  Every intermediate is an integer
+    below 2048, so f16 is exact; the only change is max(s, -1), which alters no corner (s >= T >= 1) and no NMS
+    outcome (a neighbour below T never blocks).  Checked against the integer score map on textured and noise images."""
+    import gpu_model as M
+    from multiagent_orb_slam2_amd import synthetic as S
+    for img in (S.kitti_like_image(5, rows=120, cols=200), S.uniform_noise_image(7, rows=96, cols=160)):
+        ref = M.score_map(img)[3:-3, 3:-3]
+        h, w = img.shape
+        I = (1024 + img.astype(np.int32)).astype(np.float16)          # exact: integers < 2048
+        v = I[3:h - 3, 3:w - 3]
+        d = np.stack([v - I[3 + dy:h - 3 + dy, 3 + dx:w - 3 + dx] for dx, dy in M.CIRCLE]).astype(np.float16)
+        dd = np.concatenate([d, d[:9]], axis=0)
+        mins = np.stack([dd[k:k + 9].min(axis=0) for k in range(16)])
+        maxs = np.stack([dd[k:k + 9].max(axis=0) for k in range(16)])
+        m = np.maximum(np.maximum(mins.max(axis=0), -maxs.min(axis=0)), np.float16(0)) + np.float16(1024)
+        bits = m.view(np.uint16).astype(np.int32)
+        s16 = bits - 0x6401                                             # i16 subtraction of the kernel
+        assert np.array_equal(s16, np.maximum(ref, -1))
