@@ -1178,9 +1178,13 @@ static size_t a256(size_t b) { return (b + 255) & ~(size_t)255; }
 // Grid: 256 queries per workgroup x train chunks x problems.  The train set of a problem is split into chunks so that
 // the whole launch has >= ~2048 workgroups when the problems are few (a single 2000 x 2000 match is 8 query blocks:
 // 64 chunks of 32 rows fill the chip; at many problems one chunk per problem suffices).
+static int bf_target_wgs() {   // workgroups the train chunking aims for (ORBX_BF_WGS, diagnostics)
+    static const int v = [] { const char* e = std::getenv("ORBX_BF_WGS"); return e ? std::max(1, std::atoi(e)) : 2048; }();
+    return v;
+}
 static int bf_chunks(int nq, int nt, int nprob) {
     const int qb = (nq + kBfQ - 1) / kBfQ;
-    const int want = (2048 + qb * nprob - 1) / (qb * nprob);
+    const int want = (bf_target_wgs() + qb * nprob - 1) / (qb * nprob);
     return std::max(1, std::min(want, (nt + 31) / 32));
 }
 static size_t bf_scratch(int nq, int nt, int nprob) {
