@@ -142,7 +142,10 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
 // per column one v_perm_b32 (selector sel[g][k] = left and right tap offsets, as u16 lanes) and one
 // v_dot2_u32_u16 with the packed taps (a0 | a1 << 16) give the horizontal value exactly.  The row's
 // vertical taps are wave-uniform (scalar loads); the 4 output bytes leave as one dword store.
-constexpr int kResizeBand = 8, kResizeStrip = 256;
+#ifndef ORBX_RESIZE_BAND
+#define ORBX_RESIZE_BAND 8      // output rows per wave (r2z A/B: 4 is 1 % slower, 16 is 29 % slower)
+#endif
+constexpr int kResizeBand = ORBX_RESIZE_BAND, kResizeStrip = 256;
 struct ResizeVec {       // per level >= 1 with every group's span <= 8 bytes
     const int* xb;       // [groups]
     const uint4* sel;    // [groups] perm selectors of the 4 columns
