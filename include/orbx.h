@@ -144,6 +144,16 @@ int orbx_extractor_set_pyramid_ring(orbx_extractor* ex, int n);
 int orbx_extractor_level_device(orbx_extractor* ex, int index, int level, const uint8_t** d_level,
                                 int* rows, int* cols, size_t* step);
 
+/* Device-side error word of the extractor, after every call issued so far has finished (waits for them).
+ * Bits: 1 = a level's quadtree exceeded its node capacity; 4 = ordering canary -- a descriptor stage found another
+ * call's kept-keypoint stamp (a missing cross-call ordering edge; the host API returns ORBX_ERR_HIP for it).  The
+ * device entry points cannot return these; a device-API caller polls them here.  reset != 0 clears the word. */
+int orbx_extractor_status(orbx_extractor* ex, int* flags, int reset);
+
+/* Diagnostics: a kernel occupying 'stream' for about 'ms' milliseconds (<= 2000), used by the ordering tests to
+ * delay one stream so that a missing cross-stream edge shows deterministically. */
+int orbx_debug_spin_device(void* stream, double ms);
+
 /* Optional per-stage timing of device calls (HIP events on the launch stream).  When enabled, each
  * orbx_extract_batch_device records events around every stage; orbx_extractor_stage_times returns
  * the accumulated milliseconds per stage and the number of recorded calls.  Stage names via

@@ -38,6 +38,16 @@ inline hipError_t create_stream_masked(hipStream_t* s, int priority, int cu_excl
     return hipExtStreamCreateWithCUMask(s, (uint32_t)words, mask);
 }
 
+// Device-memory initialisation (hipMalloc'd tables and counters filled with hipMemset / hipMemcpy on the null stream)
+// is complete only after this returns.  hipMemset returns before the device has done it, and the null stream does not
+// order the non-blocking streams every kernel of this library runs on (scripts/micro/stream_order.hip, case A): the
+// first kernel after an initialisation could otherwise run before it, or have its results overwritten by it.
+inline hipError_t init_done() { return hipStreamSynchronize(nullptr); }
+
+// Diagnostics: a kernel that occupies `stream` for about `ms` milliseconds (bounded spin on the 100 MHz constant
+// clock), used by tests to delay one stream and expose a missing ordering edge deterministically.
+hipError_t debug_spin(hipStream_t stream, double ms);
+
 inline hipStream_t lazy_stream(hipStream_t& s, std::once_flag& once, int device) {
     std::call_once(once, [&] {
         int cur = 0;

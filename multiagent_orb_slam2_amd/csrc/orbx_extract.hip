@@ -1279,6 +1279,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_W
 // permutations computable with prefix sums: node arrays live in LDS (double-buffered, list order),
 // each key carries the list position of its node (key_node), child counts come from LDS atomics.
 // ---------------------------------------------------------------------------------------------
+// bits of the extractor's device error word (orbx_extractor_status)
+constexpr int kErrQtCap = 1, kErrStale = 4;
+
 struct QtScratch {
     uint32_t* key_xy;    // window-relative (x | y << 16), reference order
     uint8_t* key_r;      // FAST response
@@ -1341,7 +1344,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                                                          QtScratch qs, uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r,
                                                          int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
                                                          int scan_cap, int* __restrict__ err, int lvl0, int key_lds_off,
-                                                         int key_lds_cap) {
+                                                         int key_lds_cap, unsigned seq) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int lvl = lvl0 + (int)blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
 #ifdef ORBX_QT_PROF
@@ -1506,7 +1509,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             const int nToExpand = misc[0];
             const int nn = C + U;
             QTP(30);
-            if (nn > cap) { if (tid == 0) atomicOr(err, 1); finished = true; break; }
+            if (nn > cap) { if (tid == 0) atomicOr(err, kErrQtCap); finished = true; break; }
             for (int i = tid; i < n; i += T) {
                 const int nch = base[i];
                 if (A_cnt[i] > 1) {
@@ -1609,7 +1612,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             const int U = block_scan_array(sb, n, tmp);
             const int nn = Cn + U;
             QTP(32);
-            if (nn > cap) { if (tid == 0) atomicOr(err, 1); finished = true; break; }
+            if (nn > cap) { if (tid == 0) atomicOr(err, kErrQtCap); finished = true; break; }
             for (int i = tid; i < n; i += T) {
                 if (base[i] >= 0) {
                     const int gb = base[i];
@@ -1668,7 +1671,8 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
         oxy[i] = ((xy & 0xffff) + minB) | (((xy >> 16) + minB) << 16);
         orr[i] = kr[k];
     }
-    if (tid == 0) level_cnt[img * nlevels + lvl] = nout;
+    // count | call sequence number << 16: the describe that reads this level checks the stamp (ordering canary)
+    if (tid == 0) level_cnt[img * nlevels + lvl] = nout | (int)((seq & 0x7fffu) << 16);
     QTP(90);
 }
 
@@ -1697,6 +1701,13 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x) {   // OpenCV 
 }
 
 struct SlotTable { int out_off[kMaxLevels]; };   // LevelDev::out_off per level, as a kernel argument
+
+// Ordering canary.  k_quadtree stamps each level count with the low 15 bits of the call's sequence number; the
+// describe of that call finds another call's stamp only if some edge that orders the kept-keypoint buffers across
+// calls is missing, and then raises kErrStale in the extractor's error word instead of returning wrong keypoints.
+__device__ __forceinline__ bool lvl_stale(int packed, unsigned seq) {
+    return (((unsigned)packed >> 16) & 0x7fffu) != (seq & 0x7fffu);
+}
 constexpr int kBriefR = 18;                      // max |rotated pattern offset|: round(hypot(-13, -13)) = 18
 constexpr int kBriefRow = 40;                    // LDS bytes per window row (5 x 8-byte chunks)
 constexpr int kBriefWin = (2 * kBriefR + 1) * kBriefRow;
@@ -1707,7 +1718,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
                                                   int out_stride, const int* __restrict__ level_cnt,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
                                                   int capacity, int slot0, int nslots, int write_count, int batch, Src0 s0,
-                                                  SlotTable tab) {
+                                                  SlotTable tab, unsigned seq, int* __restrict__ err) {
     // slots [slot0, slot0 + nslots) of every image (a level range: slots are level-major); the launch that covers
     // the last levels writes the per-image counts (it runs once every level's count is known)
     __shared__ __attribute__((aligned(16))) uint8_t brief_lds[4 * kBriefWin];
@@ -1726,15 +1737,19 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     for (int l = 1; l < kMaxLevels; ++l) lvl += (l < nlevels && slot >= tab.out_off[l]) ? 1 : 0;
     const LevelDev L = levels[lvl];
     const int i = slot - L.out_off;
-    const int* lc = level_cnt + img * nlevels;
-    int off = 0;
-    for (int l = 0; l < lvl; ++l) off += lc[l];
-    if (write_count && rel == 0 && ln == 0) {
-        int total = 0;
-        for (int l = 0; l < nlevels; ++l) total += lc[l];
-        counts[img] = min(total, capacity);
+    const int* lcs = level_cnt + img * nlevels;
+    int off = 0, total = 0, ci = 0;
+    bool stale = false;
+    for (int l = 0; l < nlevels; ++l) {
+        const int c = lcs[l] & 0xffff;
+        stale |= (l <= lvl || write_count) && lvl_stale(lcs[l], seq);   // only the levels this launch reads
+        off += l < lvl ? c : 0;
+        ci = l == lvl ? c : ci;
+        total += c;
     }
-    if (i >= lc[lvl]) return;
+    if (__ballot(stale) && ln == 0) atomicOr(err, kErrStale);
+    if (write_count && rel == 0 && ln == 0) counts[img] = min(total, capacity);
+    if (i >= ci) return;
     const int o = off + i;
     if (o >= capacity) return;
 
@@ -1863,7 +1878,8 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
                                                     int out_stride, const int* __restrict__ level_cnt,
                                                     orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                     int32_t* __restrict__ counts, int capacity, int slot0, int nslots,
-                                                    int write_count, int batch, Src0 s0, SlotTable tab) {
+                                                    int write_count, int batch, Src0 s0, SlotTable tab, unsigned seq,
+                                                    int* __restrict__ err) {
     constexpr int kLp = kWave / kKpw;
     constexpr int kWinItems = 5 * (2 * kBriefR + 1);             // 37 rows x 5 chunks of 8 bytes
     constexpr int kNW = (kWinItems + kLp - 1) / kLp;             // window chunks per lane
@@ -1886,19 +1902,23 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
     int lvl = 0;
 #pragma unroll
     for (int l = 1; l < kMaxLevels; ++l) lvl += (l < nlevels && slot >= tab.out_off[l]) ? 1 : 0;
-    const int* lc = level_cnt + img * nlevels;
-    int off = 0, total = 0;
+    const int* lcs = level_cnt + img * nlevels;
+    int off = 0, total = 0, ci = 0;
+    bool stale = false;
     for (int l = 0; l < nlevels; ++l) {
-        const int c = lc[l];
+        const int c = lcs[l] & 0xffff;
+        stale |= (l <= lvl || write_count) && lvl_stale(lcs[l], seq);   // only the levels this launch reads
         off += l < lvl ? c : 0;
+        ci = l == lvl ? c : ci;
         total += c;
     }
+    if (__ballot(stale) && ln == 0) atomicOr(err, kErrStale);
     if (write_count && wrel == 0 && ln == 0) counts[img] = min(total, capacity);
     const LevelDev& L = levels[lvl];
     const int lw = L.w, lpo = L.pyr_off, loo = L.out_off;
     const int i = slot - loo;
     const int o = off + i;
-    const bool valid = rel < nslots && i < lc[lvl] && o < capacity;
+    const bool valid = rel < nslots && i < ci && o < capacity;
     if (__ballot(valid) == 0) return;                            // whole wave
 
     const uint32_t xy = valid ? lvl_xy[(size_t)img * out_stride + loo + i] : 0u;
@@ -2003,6 +2023,18 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
 // =============================================================================================
 // host side
 // =============================================================================================
+__global__ void k_debug_spin(unsigned long long ticks) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+
+hipError_t debug_spin(hipStream_t stream, double ms) {
+    ms = std::min(std::max(ms, 0.0), 2000.0);
+    hipLaunchKernelGGL(k_debug_spin, dim3(1), dim3(64), 0, stream, (unsigned long long)(ms * 1e5));
+    return hipGetLastError();
+}
+
 static int round_even_f(float v) { return (int)std::nearbyintf(v); }
 static int round_even_d(double v) { return (int)std::nearbyint(v); }
 
@@ -2054,6 +2086,9 @@ struct Extractor {
     };
     CallEvents cev[kCallEv] = {};
     unsigned long long cev_next = 0;
+    unsigned call_seq = 0;                                 // per-call stamp of the ordering canary (lvl_stale)
+    int dbg_skip_desc_wait = 0;   // ORBX_DEBUG_SKIP_DESC_WAIT=1 (tests only): drop the quadtree's wait for the previous
+                                  // describe, i.e. remove an ordering edge on purpose so the canary must fire
     int slot_call[8] = {-1, -1, -1, -1, -1, -1, -1, -1};   // per pyramid set: pool index of its last describe
     int last_call = -1;                                    // pool index of the previous call, -1 none
     int sync_calls() {                                     // every describe issued so far is done
@@ -2521,8 +2556,16 @@ int Extractor::configure(int r, int c, int batch) {
     if ((st = dev_alloc(&d_lvl_r, B * out_stride))) return st;
     if ((st = dev_alloc(&d_lvl_cnt, B * nlevels))) return st;
     if ((st = dev_alloc(&d_err, 1))) return st;
+    // diagnostics: delay the null stream right before the counter initialisation (tests/test_gpu_ordering.py)
+    if (const char* dl = std::getenv("ORBX_DEBUG_UPLOAD_DELAY_MS")) ORBX_HIP(debug_spin(nullptr, std::atof(dl)));
     ORBX_HIP(hipMemset(d_err, 0, sizeof(int)));
     ORBX_HIP(hipMemset(d_cell_cnt, 0, sizeof(int) * B * std::max<size_t>(cellv.size(), 1)));
+#ifndef ORBX_LEGACY_UPLOADS
+    // The first call's FAST runs on the non-blocking side stream right after this returns; the null-stream uploads
+    // above must be complete by then (until r2 they were not waited for: the delayed memset could zero cell counts
+    // FAST had already stored -- the intermittent cross-call mismatch of DESIGN §7, reproduced by the test above).
+    ORBX_HIP(init_done());
+#endif
     return ORBX_OK;
 }
 
@@ -2548,6 +2591,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     }
     const Src0 s0{d_images, step, istride};
     e->last_src0 = s0;
+    const unsigned seq = ++e->call_seq;                             // ordering canary stamp (k_quadtree -> describe)
     const int slot = (int)(e->ncalls++ % (unsigned long long)e->pyr_ring);
     e->d_pyr = e->d_pyr_ring + (size_t)slot * e->max_batch * ps;
     // this call's events: the pool entry of 32 calls ago, whose describe (and every wait on its events) is long done
@@ -2562,7 +2606,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     };
     // the previous call's describe (possibly on another stream) reads the kept keypoints and the blurred pyramid
     auto after_prev_describe = [&](hipStream_t q) -> int {
-        if (e->last_call >= 0) ORBX_HIP(hipStreamWaitEvent(q, e->cev[e->last_call].desc, 0));
+        if (e->last_call >= 0 && !e->dbg_skip_desc_wait) ORBX_HIP(hipStreamWaitEvent(q, e->cev[e->last_call].desc, 0));
         return ORBX_OK;
     };
     const int ncells = (int)e->cellv.size();
@@ -2593,7 +2637,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds + 6 * (size_t)kc, q, e->d_levels, e->d_cells,
                            e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
                            e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err, lvl0,
-                           (int)e->qt_lds, kc);
+                           (int)e->qt_lds, kc, seq);
     };
     auto blur = [&](hipStream_t q, int tile0, int n) {
         if (n <= 0) return;
@@ -2656,7 +2700,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         auto kern = kpw == 4 ? k_describe_m<4> : kpw == 2 ? k_describe_m<2> : k_describe;
         hipLaunchKernelGGL(kern, g, dim3(256), 0, q, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
                            e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, slot0, nslots, write_count, batch, s0,
-                           tab);
+                           tab, seq, e->d_err);
     };
     const bool split_desc = side != s && split && e->desc_split && nl > 1;
     const int d0_slots = split_desc ? e->lv[1].out_off : 0;           // level 0 = slots [0, out_off[1])
@@ -2817,6 +2861,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     }
     if (const char* rt = std::getenv("ORBX_RESIZE_TAIL")) e->tail_from = std::atoi(rt);
     if (const char* qs = std::getenv("ORBX_QT_SPLIT")) e->qt_split = std::atoi(qs) != 0;
+    if (const char* sw = std::getenv("ORBX_DEBUG_SKIP_DESC_WAIT")) e->dbg_skip_desc_wait = std::atoi(sw) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
         return st;
@@ -2991,6 +3036,7 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     ORBX_HIP(hipMemcpyAsync(h_desc, e->d_desc, (size_t)e->out_capacity * 32, hipMemcpyDeviceToHost, e->own()));
     ORBX_HIP(hipStreamSynchronize(e->own()));
     const int n = h_cnt[0], err = h_cnt[1];
+    ORBX_REQUIRE(!(err & kErrStale), ORBX_ERR_HIP, "ordering canary: a describe read another call's keypoints (err=%d)", err);
     ORBX_REQUIRE(err == 0, ORBX_ERR_UNSUPPORTED, "quadtree node capacity exceeded (err=%d)", err);
     *n_out = n;
     if (n > capacity) {
@@ -3002,6 +3048,29 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
         std::memcpy(kps, h_kps, sizeof(orbx_keypoint) * (size_t)n);
         std::memcpy(desc, h_desc, (size_t)n * 32);
     }
+    return ORBX_OK;
+}
+
+int orbx_extractor_status(orbx_extractor* e, int* flags, int reset) {
+    ORBX_REQUIRE(e && flags, ORBX_ERR_ARG, "null argument");
+    *flags = 0;
+    if (!e->d_err) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(e->device));
+    if (e->stream) ORBX_HIP(hipStreamSynchronize(e->stream));
+    if (e->side) ORBX_HIP(hipStreamSynchronize(e->side));
+    if (e->fastq) ORBX_HIP(hipStreamSynchronize(e->fastq));
+    if (int st = e->sync_calls()) return st;
+    hipStream_t q = e->side ? e->side : e->own();
+    int h = 0;
+    ORBX_HIP(hipMemcpyAsync(&h, e->d_err, sizeof(int), hipMemcpyDeviceToHost, q));
+    if (reset) ORBX_HIP(hipMemsetAsync(e->d_err, 0, sizeof(int), q));
+    ORBX_HIP(hipStreamSynchronize(q));
+    *flags = h;
+    return ORBX_OK;
+}
+
+int orbx_debug_spin_device(void* stream, double ms) {
+    ORBX_HIP(debug_spin((hipStream_t)stream, ms));
     return ORBX_OK;
 }
 

@@ -262,7 +262,8 @@ int orbx_fusion_create(orbx_vocab* vocab, orbx_matcher* matcher, int capacity, i
         (st = falloc(&f->nm, N * std::max(candidates, 1))) || (st = falloc(&f->gate, 1)))
         return fail(st);
     if (hipMemset(f->ring, 0, S * f->lay.bytes) != hipSuccess || hipMemset(f->slot_group, 0xff, 4 * S) != hipSuccess ||
-        hipMemset(f->status, 0, 4) != hipSuccess || hipMemset(f->gate, 0, 8) != hipSuccess) {
+        hipMemset(f->status, 0, 4) != hipSuccess || hipMemset(f->gate, 0, 8) != hipSuccess ||
+        init_done() != hipSuccess) {   // complete before the first kernel on a caller's (non-blocking) stream
         set_error("fusion init memset failed");
         return fail(ORBX_ERR_HIP);
     }

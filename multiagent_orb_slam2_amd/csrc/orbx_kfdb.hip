@@ -811,6 +811,7 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
         alloc((void**)&db->d_w[k], 4 * S);
         alloc((void**)&db->d_s[k], 4 * S);
     }
+    if (e == hipSuccess) e = init_done();   // the null-stream memsets above, before any kernel on a caller's stream
     if (e == hipSuccess) e = hipEventCreateWithFlags(&db->scratch_used, hipEventDisableTiming);
     if (e == hipSuccess) e = hipHostMalloc((void**)&db->h_stage, 8 * (size_t)kKfdbStages * S, hipHostMallocDefault);
     for (int b = 0; b < kKfdbStages; ++b) {

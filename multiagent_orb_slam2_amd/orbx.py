@@ -155,6 +155,8 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_extractor_level_device.argtypes = [vp, i32, i32, C.POINTER(vp), C.POINTER(i32), C.POINTER(i32),
                                                 C.POINTER(C.c_size_t)]
     lib.orbx_extractor_enable_timing.argtypes = [vp, i32]
+    lib.orbx_extractor_status.argtypes = [vp, C.POINTER(i32), i32]
+    lib.orbx_debug_spin_device.argtypes = [vp, C.c_double]
     lib.orbx_extractor_stage_times.argtypes = [vp, vp, C.POINTER(i32)]
     for name in ("orbx_extractor_get_scale_factors", "orbx_extractor_get_inverse_scale_factors",
                  "orbx_extractor_get_scale_sigma_squares", "orbx_extractor_get_inverse_scale_sigma_squares",
@@ -256,6 +258,12 @@ def _tp(t):
 
 def device_count() -> int:
     return load_library().orbx_device_count()
+
+
+def debug_spin(stream, ms: float):
+    """Diagnostics: occupy a torch stream (or raw hipStream_t int, 0 = null stream) for about ms milliseconds."""
+    ptr = stream if isinstance(stream, int) else stream.cuda_stream
+    _check(load_library().orbx_debug_spin_device(C.c_void_p(ptr), float(ms)))
 
 
 def create_stream(device: int = 0, priority: int = 0, cu_exclude: int = 0):
@@ -408,6 +416,13 @@ class ORBextractor:
                                                              images.stride(0), _tp(kps), _tp(desc), _tp(counts), cap, s,
                                                              C.c_void_p(out_stream.cuda_stream)))
         return kps, desc, counts
+
+    def status(self, reset: bool = False) -> int:
+        """Device error word after every call issued so far (orbx_extractor_status): 1 = quadtree node capacity,
+        4 = ordering canary (a descriptor stage read another call's keypoints)."""
+        f = C.c_int()
+        _check(self._lib.orbx_extractor_status(self._h, C.byref(f), int(reset)))
+        return f.value
 
     def enable_timing(self, on: bool = True):
         _check(self._lib.orbx_extractor_enable_timing(self._h, int(on)))

@@ -1,0 +1,118 @@
+"""Cross-call and cross-stream ordering of the extractor, made deterministic.
+
+The split entry point (orbx_extract_batch_device_split) runs call k's descriptor stage on the caller's output stream
+while call k+1's front half runs on the input stream; call k+1 overwrites the kept keypoints, the blurred pyramid and
+(ring 1) the pyramid set that call k's describe reads.  Each of those buffers is ordered by an event edge
+(orbx_extract.hip run_batch).  These tests stall one stream with a spin kernel so that a missing edge corrupts the
+results every time instead of once in ten suite runs, and check the device-side ordering canary
+(orbx_extractor_status bit 4: k_quadtree stamps each level count with the call number, the describe checks it).
+
+Background: the intermittent mismatch of round 2 came from the extractor's configure(), whose
+null-stream hipMemset of the per-cell FAST counts could land after the first call's FAST on a non-blocking stream
+(scripts/micro/stream_order.hip shows the runtime behaviour); configure now waits for its uploads."""
+import numpy as np
+import pytest
+
+from multiagent_orb_slam2_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _batches(n=4, per=3, seed0=500):
+    return [np.stack([S.kitti_like_image(seed0 + 7 * b + i) for i in range(per)]) for b in range(n)]
+
+
+def _reference(batches):
+    import multiagent_orb_slam2_amd as pkg
+    ex1 = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    return [[ex1(b[i]) for i in range(len(b))] for b in batches]
+
+
+def _mismatches(outs, ref):
+    import multiagent_orb_slam2_amd as pkg
+    bad = []
+    for bi, (kps, desc, cnt) in enumerate(outs):
+        kps, desc, cnt = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+        for i, (k1, d1) in enumerate(ref[bi]):
+            n = int(cnt[i])
+            kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
+            if n != len(k1) or not (np.array_equal(kb, k1) and np.array_equal(desc[i, :n], d1)):
+                bad.append((bi, i, n, len(k1)))
+    return bad
+
+
+@pytest.mark.parametrize("ring,desc_side", [(1, 0), (2, 0), (2, 1)])
+def test_stalled_describe_orders_next_call(gpu, monkeypatch, ring, desc_side):
+    """A 15 ms spin on the output stream right before each call: call k's describe starts long after call k+1's
+    quadtree, blur and (ring 1) resize were enqueued.  Every result must equal the host API and the canary must stay
+    clear -- i.e. every cross-call buffer reuse waits for the describe that reads it."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    monkeypatch.setenv("ORBX_DESC_SIDE", str(desc_side))
+    batches = _batches()
+    ref = _reference(batches)
+    ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    ex.set_pyramid_ring(ring)
+    ex.reserve(batches[0].shape[1], batches[0].shape[2], len(batches[0]))
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+    ts = [torch.from_numpy(b).cuda() for b in batches]
+    torch.cuda.synchronize()
+    outs = []
+    for t in ts:
+        pkg.orbx.debug_spin(s_out, 15.0)
+        outs.append(ex.extract_batch_device(t, stream=s_in, out_stream=s_out))
+    torch.cuda.synchronize()
+    assert ex.status() == 0
+    assert _mismatches(outs, ref) == []
+
+
+def test_canary_fires_when_an_edge_is_missing(gpu, monkeypatch):
+    """Negative control: with the quadtree's wait for the previous describe removed on purpose
+    (ORBX_DEBUG_SKIP_DESC_WAIT), the same stall makes call k+1's quadtree overwrite call k's kept keypoints before
+    call k's describe reads them.  The canary must report it (bit 4), and the outputs are wrong -- which shows the
+    positive test above would catch a missing edge."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    monkeypatch.setenv("ORBX_DEBUG_SKIP_DESC_WAIT", "1")
+    batches = _batches(n=3)
+    ref = _reference(batches)
+    ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    ex.set_pyramid_ring(2)
+    ex.reserve(batches[0].shape[1], batches[0].shape[2], len(batches[0]))
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+    ts = [torch.from_numpy(b).cuda() for b in batches]
+    torch.cuda.synchronize()
+    outs = []
+    for t in ts:
+        pkg.orbx.debug_spin(s_out, 15.0)
+        outs.append(ex.extract_batch_device(t, stream=s_in, out_stream=s_out))
+    torch.cuda.synchronize()
+    flags = ex.status(reset=True)
+    assert flags & 4, f"canary did not fire (flags {flags})"
+    assert _mismatches(outs, ref), "outputs unexpectedly correct without the edge"
+    assert ex.status() == 0   # reset
+
+
+@pytest.mark.parametrize("delay_ms", [0.0, 0.03, 0.1, 0.3, 1.0])
+def test_configure_uploads_complete_before_first_call(gpu, monkeypatch, delay_ms):
+    """configure() initialises the per-cell FAST counts with a null-stream hipMemset; the null stream is delayed by
+    `delay_ms` right before it (ORBX_DEBUG_UPLOAD_DELAY_MS) and the first call follows at once on non-blocking
+    streams.  configure waits for its uploads, so every delay gives the host API's results."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    batches = _batches(n=2, seed0=600)
+    ref = _reference(batches)
+    ts = [torch.from_numpy(b).cuda() for b in batches]
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    monkeypatch.setenv("ORBX_DEBUG_UPLOAD_DELAY_MS", str(delay_ms))
+    ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    ex.set_pyramid_ring(2)
+    ex.reserve(batches[0].shape[1], batches[0].shape[2], len(batches[0]))
+    outs = [ex.extract_batch_device(t, stream=s_in, out_stream=s_out) for t in ts]
+    torch.cuda.synchronize()
+    assert ex.status() == 0
+    assert _mismatches(outs, ref) == []
