@@ -7,9 +7,15 @@
  * signatures; their bodies call the functions below (adapter in INTEGRATION.md).  Plain pointers and
  * sizes only; every function returns an int status (ORBX_OK = 0, < 0 on error; text via
  * orbx_last_error()) and never throws.  Host buffers are owned by the caller, device buffers made by
- * a context are owned by the context.  A context is used by one host thread at a time (the reference
- * constructs one ORBextractor per camera per agent, Tracking.cc:119-125, and stack ORBmatchers per
- * thread); distinct contexts may be used concurrently from different threads.
+ * a context are owned by the context.  Threads:
+ *   - an extractor or a fusion object is used by one host thread at a time (the reference constructs one
+ *     ORBextractor per camera per agent, Tracking.cc:119-125);
+ *   - a matcher and a keyframe database may be shared by any number of threads, like the reference's
+ *     KeyFrameDatabase (its mMutex, KeyFrameDatabase.cc:42-316): each call holds the object's lock while it
+ *     runs, and a call's stream is ordered after the previous call's device work on the object's state
+ *     (matcher scratch; database BowVectors, membership, scratch fields), whatever stream that ran on -- so
+ *     operations take effect in the order their calls took the lock;
+ *   - distinct objects may be used concurrently from different threads.
  *
  * "_device" entry points take device pointers and a hipStream_t (passed as void*; NULL = the HIP
  * null stream, as in the HIP API) and do not synchronise; all other entry points take host pointers,

@@ -68,6 +68,21 @@ void set_error(const char* fmt, ...);
 // and its growable scratch buffer + own stream for the host-form entry points.
 int matcher_device(const orbx_matcher* m);
 int matcher_scratch(orbx_matcher* m, size_t bytes, void** base, void** stream);
+// One call's hold on a matcher's scratch / own stream: the matcher's lock for the call's duration, and (used = true)
+// the call's stream recorded as the last scratch user, which the next call's stream waits for (Matcher::reserve_on).
+void matcher_acquire(orbx_matcher* m);
+void matcher_release(orbx_matcher* m, hipStream_t s, bool used);
+struct MatcherLease {
+    orbx_matcher* m;
+    hipStream_t s = nullptr;
+    bool used = false;   // set once s is the stream the call's scratch work runs on
+    MatcherLease(orbx_matcher* mm, hipStream_t st) : m(mm), s(st), used(true) { matcher_acquire(m); }
+    explicit MatcherLease(orbx_matcher* mm) : m(mm) { matcher_acquire(m); }
+    void on(hipStream_t st) { s = st; used = true; }
+    ~MatcherLease() { matcher_release(m, s, used); }
+    MatcherLease(const MatcherLease&) = delete;
+    MatcherLease& operator=(const MatcherLease&) = delete;
+};
 
 #define ORBX_HIP(call)                                                                          \
     do {                                                                                        \

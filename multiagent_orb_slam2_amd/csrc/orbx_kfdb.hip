@@ -641,7 +641,14 @@ struct orbx_kfdb {
     float* d_s[3] = {nullptr, nullptr, nullptr};
     void* scratch = nullptr;       // per-query rows + host-form staging
     size_t scratch_bytes = 0;
-    hipEvent_t scratch_used = nullptr;   // recorded on the stream of the last detect that used 'scratch'
+    // Thread and stream contract (KeyFrameDatabase.cc:42,50,84,210,316 lock mMutex in add / erase / every Detect*):
+    // every entry point holds 'mtx' while it runs, and every one that enqueues device work on the database's state
+    // (BowVectors, membership, inverted file, scratch fields, 'scratch') first makes its stream wait for 'last_op' and
+    // re-records it after -- so operations take effect in the order their calls took the lock, whatever threads and
+    // streams they come from (DbOp below).
+    std::recursive_mutex mtx;
+    hipEvent_t last_op = nullptr;        // the last enqueue on database state, on its caller's stream
+    bool last_op_set = false;
     void* score_stage = nullptr;   // orbx_kfdb_score's own staging (never shared with a detect in flight elsewhere)
     size_t score_stage_bytes = 0;
     std::vector<uint32_t> seq;     // host mirror of membership (add order)
@@ -658,6 +665,25 @@ struct orbx_kfdb {
 
 namespace {
 
+// One database operation: the lock for its duration; its stream (if any) ordered after the previous operation.
+struct DbOp {
+    orbx_kfdb* db;
+    hipStream_t s;
+    bool on_stream;
+    std::unique_lock<std::recursive_mutex> lk;
+    hipError_t err = hipSuccess;
+    DbOp(orbx_kfdb* d, hipStream_t st, bool uses_stream) : db(d), s(st), on_stream(uses_stream), lk(d->mtx) {
+        if (on_stream && db->last_op_set) err = hipStreamWaitEvent(s, db->last_op, 0);
+    }
+    ~DbOp() {
+        if (on_stream && hipEventRecord(db->last_op, s) == hipSuccess) db->last_op_set = true;
+    }
+};
+#define ORBX_DBOP(db, stream)                                                                                          \
+    DbOp op_((db), (stream), true);                                                                                  \
+    ORBX_HIP(op_.err)
+#define ORBX_DBLOCK(db) std::lock_guard<std::recursive_mutex> lock_((db)->mtx)
+
 DbDev dev_view(const orbx_kfdb* db) {
     return DbDev{db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_slot, db->S, db->maxw, db->n_vocab};
 }
@@ -665,8 +691,8 @@ DbDev dev_view(const orbx_kfdb* db) {
 int grow_scratch(orbx_kfdb* db, size_t bytes) {
     if (bytes <= db->scratch_bytes) return ORBX_OK;
     if (db->scratch) {
-        // the last detect may have run on a caller's stream: wait for it before the buffer goes away
-        ORBX_HIP(hipEventSynchronize(db->scratch_used));
+        // the last operation may have run on a caller's stream: wait for it before the buffer goes away
+        if (db->last_op_set) ORBX_HIP(hipEventSynchronize(db->last_op));
         if (db->stream) ORBX_HIP(hipStreamSynchronize(db->stream));
         ORBX_HIP(hipFree(db->scratch));
         db->scratch = nullptr;
@@ -765,7 +791,6 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
     hipLaunchKernelGGL(k_kfdb_accum, dim3(nq), dim3(256), 0, s, D, Q, X, St, kind, d_out, out_stride, d_out_n, d_status);
     hipLaunchKernelGGL(k_kfdb_state, dim3((db->S + 255) / 256), dim3(256), 0, s, D, Q, X, St, kind, nq, d_status);
     ORBX_HIP(hipGetLastError());
-    ORBX_HIP(hipEventRecord(db->scratch_used, s));
     return ORBX_OK;
 }
 
@@ -812,7 +837,7 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
         alloc((void**)&db->d_s[k], 4 * S);
     }
     if (e == hipSuccess) e = init_done();   // the null-stream memsets above, before any kernel on a caller's stream
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&db->scratch_used, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&db->last_op, hipEventDisableTiming);
     if (e == hipSuccess) e = hipHostMalloc((void**)&db->h_stage, 8 * (size_t)kKfdbStages * S, hipHostMallocDefault);
     for (int b = 0; b < kKfdbStages; ++b) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&db->stage_done[b], hipEventDisableTiming);
@@ -830,7 +855,7 @@ int orbx_kfdb_destroy(orbx_kfdb* db) {
     if (!db) return ORBX_OK;
     (void)hipSetDevice(db->device);
     if (db->stream) (void)hipStreamSynchronize(db->stream);
-    if (db->scratch_used) (void)hipEventSynchronize(db->scratch_used);   // a detect on a caller's stream
+    if (db->last_op && db->last_op_set) (void)hipEventSynchronize(db->last_op);   // an operation on a caller's stream
     void* bufs[] = {db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_cur, db->d_if_slot,
                     db->d_scan, db->d_members, db->scratch, db->score_stage};
     for (void* p : bufs)
@@ -845,7 +870,7 @@ int orbx_kfdb_destroy(orbx_kfdb* db) {
             (void)hipEventSynchronize(db->stage_done[b]);
             (void)hipEventDestroy(db->stage_done[b]);
         }
-    if (db->scratch_used) (void)hipEventDestroy(db->scratch_used);
+    if (db->last_op) (void)hipEventDestroy(db->last_op);
     if (db->h_stage) (void)hipHostFree(db->h_stage);
     if (db->stream) (void)hipStreamDestroy(db->stream);
     delete db;
@@ -854,6 +879,7 @@ int orbx_kfdb_destroy(orbx_kfdb* db) {
 
 int orbx_kfdb_info(const orbx_kfdb* db, int* n_vocab_words, int* max_slots, int* max_words, int* n_members) {
     ORBX_REQUIRE(db, ORBX_ERR_ARG, "db is NULL");
+    ORBX_DBLOCK(const_cast<orbx_kfdb*>(db));
     if (n_vocab_words) *n_vocab_words = db->n_vocab;
     if (max_slots) *max_slots = db->S;
     if (max_words) *max_words = db->maxw;
@@ -863,6 +889,7 @@ int orbx_kfdb_info(const orbx_kfdb* db, int* n_vocab_words, int* max_slots, int*
 
 int orbx_kfdb_set_strategy(orbx_kfdb* db, int strategy) {
     ORBX_REQUIRE(db && strategy >= ORBX_KFDB_AUTO && strategy <= ORBX_KFDB_PAIRWISE, ORBX_ERR_ARG, "bad strategy");
+    ORBX_DBLOCK(db);
     db->strategy = strategy;
     return ORBX_OK;
 }
@@ -875,6 +902,7 @@ int orbx_kfdb_set_bow(orbx_kfdb* db, int slot, const uint32_t* words, const doub
         ORBX_REQUIRE(i == 0 || words[i] > words[i - 1], ORBX_ERR_ARG, "BowVector word ids must ascend");
     }
     ORBX_HIP(hipSetDevice(db->device));
+    ORBX_DBOP(db, db->own());
     const size_t o = (size_t)slot * db->maxw;
     if (n) {
         ORBX_HIP(hipMemcpyAsync(db->d_bw + o, words, 4 * (size_t)n, hipMemcpyHostToDevice, db->own()));
@@ -893,6 +921,7 @@ int orbx_kfdb_set_bow_device(orbx_kfdb* db, const int32_t* d_slots, int n, const
                      value_stride >= 0 && n_stride >= 0, ORBX_ERR_ARG, "bad argument");
     if (n == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(db->device));
+    ORBX_DBOP(db, (hipStream_t)stream);
     DbDev D = dev_view(db);
     hipLaunchKernelGGL(k_set_bow, dim3(n), dim3(256), 0, (hipStream_t)stream, D, db->d_bw, db->d_bv, db->d_bn, d_slots, d_words,
                        word_stride, d_values, value_stride, d_n_words, n_stride);
@@ -916,6 +945,7 @@ int orbx_kfdb_candidate_pairs_device(const int32_t* d_cand, int cand_stride, con
 int orbx_kfdb_set_covisibility(orbx_kfdb* db, const int32_t* slots, int n, const int32_t* best) {
     ORBX_REQUIRE(db && n >= 0 && (n == 0 || (slots && best)), ORBX_ERR_ARG, "bad argument");
     ORBX_HIP(hipSetDevice(db->device));
+    ORBX_DBOP(db, db->own());
     for (int i = 0; i < n; ++i) {
         ORBX_REQUIRE(slots[i] >= 0 && slots[i] < db->S, ORBX_ERR_ARG, "slot %d out of range", slots[i]);
         for (int j = 0; j < kKfdbCovis; ++j)
@@ -930,6 +960,7 @@ int orbx_kfdb_set_covisibility(orbx_kfdb* db, const int32_t* slots, int n, const
 
 int orbx_kfdb_add(orbx_kfdb* db, const int32_t* slots, int n) {
     ORBX_REQUIRE(db && n >= 0 && (n == 0 || slots), ORBX_ERR_ARG, "bad argument");
+    ORBX_DBLOCK(db);   // membership: host mirror only, uploaded by the next detect on that detect's stream
     for (int i = 0; i < n; ++i) {
         const int k = slots[i];
         ORBX_REQUIRE(k >= 0 && k < db->S, ORBX_ERR_ARG, "slot %d out of range", k);
@@ -944,6 +975,7 @@ int orbx_kfdb_add(orbx_kfdb* db, const int32_t* slots, int n) {
 
 int orbx_kfdb_erase(orbx_kfdb* db, const int32_t* slots, int n) {
     ORBX_REQUIRE(db && n >= 0 && (n == 0 || slots), ORBX_ERR_ARG, "bad argument");
+    ORBX_DBLOCK(db);
     bool any = false;
     for (int i = 0; i < n; ++i) {
         const int k = slots[i];
@@ -959,6 +991,7 @@ int orbx_kfdb_erase(orbx_kfdb* db, const int32_t* slots, int n) {
 
 int orbx_kfdb_clear(orbx_kfdb* db) {
     ORBX_REQUIRE(db, ORBX_ERR_ARG, "db is NULL");
+    ORBX_DBLOCK(db);
     std::fill(db->seq.begin(), db->seq.end(), kNoSeq);
     db->members.clear();
     db->dirty = db->seq_dirty = true;
@@ -968,6 +1001,7 @@ int orbx_kfdb_clear(orbx_kfdb* db) {
 int orbx_kfdb_get_state(orbx_kfdb* db, int kind, uint64_t* query, int32_t* words, float* score) {
     ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && query && words && score, ORBX_ERR_ARG, "bad argument");
     ORBX_HIP(hipSetDevice(db->device));
+    ORBX_DBOP(db, db->own());
     ORBX_HIP(hipMemcpyAsync(query, db->d_q[kind], 8 * (size_t)db->S, hipMemcpyDeviceToHost, db->own()));
     ORBX_HIP(hipMemcpyAsync(words, db->d_w[kind], 4 * (size_t)db->S, hipMemcpyDeviceToHost, db->own()));
     ORBX_HIP(hipMemcpyAsync(score, db->d_s[kind], 4 * (size_t)db->S, hipMemcpyDeviceToHost, db->own()));
@@ -978,6 +1012,7 @@ int orbx_kfdb_get_state(orbx_kfdb* db, int kind, uint64_t* query, int32_t* words
 int orbx_kfdb_set_state(orbx_kfdb* db, int kind, const uint64_t* query, const int32_t* words, const float* score) {
     ORBX_REQUIRE(db && kind >= 0 && kind <= 2 && query && words && score, ORBX_ERR_ARG, "bad argument");
     ORBX_HIP(hipSetDevice(db->device));
+    ORBX_DBOP(db, db->own());
     ORBX_HIP(hipMemcpyAsync(db->d_q[kind], query, 8 * (size_t)db->S, hipMemcpyHostToDevice, db->own()));
     ORBX_HIP(hipMemcpyAsync(db->d_w[kind], words, 4 * (size_t)db->S, hipMemcpyHostToDevice, db->own()));
     ORBX_HIP(hipMemcpyAsync(db->d_s[kind], score, 4 * (size_t)db->S, hipMemcpyHostToDevice, db->own()));
@@ -989,6 +1024,7 @@ int orbx_kfdb_score_device(orbx_kfdb* db, const int32_t* d_pairs, int n, double*
     ORBX_REQUIRE(db && n >= 0 && (n == 0 || (d_pairs && d_scores)), ORBX_ERR_ARG, "bad argument");
     if (n == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(db->device));
+    ORBX_DBOP(db, (hipStream_t)stream);
     hipLaunchKernelGGL(k_kfdb_score_pairs, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, dev_view(db), d_pairs, n,
                        d_scores);
     ORBX_HIP(hipGetLastError());
@@ -999,6 +1035,7 @@ int orbx_kfdb_score(orbx_kfdb* db, const int32_t* pairs, int n, double* scores) 
     ORBX_REQUIRE(db && n >= 0 && (n == 0 || (pairs && scores)), ORBX_ERR_ARG, "bad argument");
     if (n == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(db->device));
+    ORBX_DBOP(db, db->own());
     const size_t need = align_up(8 * (size_t)n) + align_up(8 * (size_t)n);
     if (need > db->score_stage_bytes) {          // the db's own stream is the only user of this buffer
         ORBX_HIP(hipStreamSynchronize(db->own()));
@@ -1031,6 +1068,7 @@ int detect_device_impl(orbx_kfdb* db, int kind, const int32_t* d_query_slots, co
     ORBX_REQUIRE(kind == ORBX_KFDB_RELOC || nq == 0 || d_min_scores, ORBX_ERR_ARG, "min scores required for this query kind");
     if (nq == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(db->device));
+    ORBX_DBOP(db, (hipStream_t)stream);
     const size_t qb = qscratch_layout(nq, db->S, nullptr, nullptr);
     int st = grow_scratch(db, qb);
     if (st) return st;
@@ -1075,6 +1113,7 @@ int detect_host_impl(orbx_kfdb* db, int kind, const int32_t* query_slots, const 
     const int n_excl = excl_offsets ? excl_offsets[nq] : 0;
     ORBX_REQUIRE(!excl_offsets || (excl_offsets[0] == 0 && (n_excl == 0 || excl_slots)), ORBX_ERR_ARG, "bad exclusion lists");
     ORBX_HIP(hipSetDevice(db->device));
+    ORBX_DBOP(db, db->own());
     const int S = db->S;
     // device staging: [query scratch][slots][ids][min][excl_off][excl][out nq x S][out_n][status][state snapshot]
     const size_t qb = qscratch_layout(nq, S, nullptr, nullptr);

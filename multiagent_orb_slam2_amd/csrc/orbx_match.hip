@@ -1144,14 +1144,21 @@ struct Matcher {
     hipStream_t stream = nullptr;      // lazy: own() on first host-API use
     std::once_flag stream_once;
     hipStream_t own() { return lazy_stream(stream, stream_once, device); }
-    // growable device scratch
+    // growable device scratch.  Contract: one call at a time holds the matcher ('mtx', MatcherLease), and a call's
+    // stream waits for the previous scratch user ('last_op', recorded on that call's stream) before its own kernels
+    // touch the scratch -- device calls on different streams are ordered, not racing on one buffer.
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
+    std::recursive_mutex mtx;
+    hipEvent_t last_op = nullptr;
+    bool last_op_set = false;
     int reserve(size_t bytes) { return reserve_on(bytes, own()); }
-    // grow the scratch buffer; work already queued on 'on' (and on the own stream) may still use the old one
+    // order 'on' after the previous scratch user; grow the buffer (after that user has finished) if needed
     int reserve_on(size_t bytes, hipStream_t on) {
+        if (last_op_set) ORBX_HIP(hipStreamWaitEvent(on, last_op, 0));
         if (bytes <= scratch_bytes) return ORBX_OK;
         if (scratch) {
+            if (last_op_set) ORBX_HIP(hipEventSynchronize(last_op));
             if (stream) (void)hipStreamSynchronize(stream);
             (void)hipStreamSynchronize(on);
             (void)hipFree(scratch);
@@ -1221,8 +1228,13 @@ using namespace orbx;
 struct orbx_matcher : public orbx::Matcher {};
 
 int orbx::matcher_device(const orbx_matcher* m) { return m->device; }
+void orbx::matcher_acquire(orbx_matcher* m) { m->mtx.lock(); }
+void orbx::matcher_release(orbx_matcher* m, hipStream_t s, bool used) {
+    if (used && m->last_op && hipEventRecord(m->last_op, s) == hipSuccess) m->last_op_set = true;
+    m->mtx.unlock();
+}
 int orbx::matcher_scratch(orbx_matcher* m, size_t bytes, void** base, void** stream) {
-    int st = m->reserve(bytes);
+    int st = m->reserve(bytes);   // (the caller holds a MatcherLease)
     if (st) return st;
     *base = m->scratch;
     *stream = (void*)m->own();
@@ -1246,6 +1258,7 @@ int orbx_matcher_create(float nnratio, int checkOri, int device, orbx_matcher** 
     m->checkOri = checkOri;
     m->device = device;
     hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&m->last_op, hipEventDisableTiming);
     if (e != hipSuccess) {
         set_error("stream create: %s", hipGetErrorString(e));
         delete m;
@@ -1259,6 +1272,8 @@ int orbx_matcher_destroy(orbx_matcher* m) {
     if (!m) return ORBX_OK;
     (void)hipSetDevice(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
+    if (m->last_op_set) (void)hipEventSynchronize(m->last_op);   // a device call on a caller's stream
+    if (m->last_op) (void)hipEventDestroy(m->last_op);
     if (m->scratch) (void)hipFree(m->scratch);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
@@ -1291,6 +1306,7 @@ int orbx_bf_match_batch_device(orbx_matcher* m, const uint8_t* dq, int nq, size_
                  "problem strides must be multiples of 16 bytes");
     ORBX_HIP(hipSetDevice(m->device));
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
+    MatcherLease lease_(m, s);
     int st = m->reserve_on(bf_scratch(nq, std::max(nt, 1), n_problems), s);
     if (st) return st;
     return bf_launch(m, dq, nq, query_stride, dt, nt, train_stride, n_problems, bi, bd, sd, s, m->scratch);
@@ -1303,6 +1319,7 @@ int orbx_bf_match(orbx_matcher* m, const uint8_t* q, int nq, const uint8_t* t, i
     ORBX_REQUIRE(nt < (1 << 20), ORBX_ERR_UNSUPPORTED, "train set too large (%d)", nt);
     ORBX_HIP(hipSetDevice(m->device));
     const size_t io = a256((size_t)nq * 32) + a256((size_t)std::max(nt, 1) * 32) + 3 * a256((size_t)nq * 4);
+    MatcherLease lease_(m, m->own());
     int st = m->reserve(io + bf_scratch(nq, std::max(nt, 1), 1));
     if (st) return st;
     Bump bp{(uint8_t*)m->scratch};
@@ -1375,6 +1392,7 @@ int orbx_stereo_match_batch_device(orbx_matcher* m, const orbx_keypoint* kl, con
     if (st) return st;
     ORBX_HIP(hipSetDevice(m->device));
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
+    MatcherLease lease_(m, s);
     if ((st = m->reserve_on(stereo_scratch(batch, rows, capacity), s))) return st;
     Bump bp{(uint8_t*)m->scratch};
     A.row_start = bp.take<int32_t>((size_t)batch * (rows + 1));
@@ -1403,6 +1421,7 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
     const int cap = std::max(nl, std::max(nr, 1));
     const size_t bytes = a256(28 * (size_t)cap) * 2 + a256(32 * (size_t)cap) * 2 + 2 * a256(4 * (size_t)cap) +
                          stereo_scratch(1, rows, cap);
+    MatcherLease lease_(m, m->own());
     if ((st = m->reserve(bytes))) return st;
     Bump bp{(uint8_t*)m->scratch};
     orbx_keypoint* dkl = bp.take<orbx_keypoint>(cap);
@@ -1473,6 +1492,7 @@ int orbx_stereo_refine_batch_device(orbx_matcher* m, const orbx_keypoint* kl, co
     ORBX_REQUIRE(left->nlevels == right->nlevels, ORBX_ERR_ARG, "left/right pyramids differ in levels");
     ORBX_HIP(hipSetDevice(m->device));
     hipStream_t s = (hipStream_t)stream;
+    MatcherLease lease_(m, s);
     if ((st = m->reserve_on(a256((size_t)batch * capacity * 4), s))) return st;
     RefineArgs A{};
     A.kl = kl; A.nl = nl; A.kr = kr; A.best_idx = best_idx; A.capacity = capacity;
@@ -1501,6 +1521,7 @@ int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, con
     const int cap = std::max(nl, std::max(nr, 1));
     const size_t bytes = a256(28 * (size_t)cap) * 2 + a256(32 * (size_t)cap) * 2 + 2 * a256(4 * (size_t)cap) +
                          stereo_scratch(1, PL.rows[0], cap) + 3 * a256(4 * (size_t)cap);
+    MatcherLease lease_(m, m->own());
     if ((st = m->reserve(bytes))) return st;
     Bump bp{(uint8_t*)m->scratch};
     orbx_keypoint* dkl = bp.take<orbx_keypoint>(cap);
@@ -1586,6 +1607,7 @@ static int run_bow(orbx_matcher* m, int kff, const uint8_t* d1, const float* a1,
     const size_t N1 = std::max(n1, 1), N2 = std::max(n2, 1), NR = std::max(nres, 1);
     const size_t bytes = a256(32 * N1) + a256(4 * N1) + a256(N1) + a256(32 * N2) + a256(4 * N2) + a256(N2) + fv_bytes(fv1) +
                          fv_bytes(fv2) + 2 * a256(4 * NR) + a256(4 * 32) + 256;
+    MatcherLease lease_(m, m->own());
     if ((st = m->reserve(bytes))) return st;
     hipStream_t s = m->own();
     Bump bp{(uint8_t*)m->scratch};
@@ -1669,6 +1691,7 @@ int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const orbx_kf_store* s
     const size_t cap = (size_t)S.capacity;
     ORBX_HIP(hipMemsetAsync(d_match12, 0xff, (size_t)n_pairs * cap * 4, s));
     ORBX_HIP(hipMemsetAsync(d_nmatches, 0, (size_t)n_pairs * 4, s));
+    MatcherLease lease_(m, s);
     int st = m->reserve_on(a256((size_t)n_pairs * cap * 4) + a256((size_t)n_pairs * 32 * 4), s);
     if (st) return st;
     int32_t* bin = (int32_t*)m->scratch;
@@ -1724,6 +1747,7 @@ int orbx_distinctive_descriptors(orbx_matcher* m, const uint8_t* desc, const int
     ORBX_REQUIRE(total < (1 << 30) / 32, ORBX_ERR_UNSUPPORTED, "too many observations");
     ORBX_HIP(hipSetDevice(m->device));
     const size_t M = (size_t)n_mappoints;
+    MatcherLease lease_(m, m->own());
     int st = m->reserve(a256(32 * (size_t)std::max(total, 1)) + a256(4 * (M + 1)) + a256(4 * M) + a256(32 * M));
     if (st) return st;
     Bump bp{(uint8_t*)m->scratch};
@@ -1759,6 +1783,7 @@ int orbx_search_for_triangulation(orbx_matcher* m, const uint8_t* desc1, const o
     const size_t N1 = std::max(n1, 1), N2 = std::max(n2, 1);
     const size_t bytes = a256(32 * N1) + a256(28 * N1) + a256(N1) + a256(4 * N1) + a256(32 * N2) + a256(28 * N2) + a256(N2) +
                          a256(4 * N2) + fv_bytes(fv1) + fv_bytes(fv2) + 2 * a256(4 * N1) + a256(4 * 32) + 256;
+    MatcherLease lease_(m, m->own());
     if ((st = m->reserve(bytes))) return st;
     hipStream_t s = m->own();
     Bump bp{(uint8_t*)m->scratch};

@@ -493,7 +493,9 @@ int orbx_undistort_keypoints(orbx_matcher* m, const orbx_keypoint* kps, int n, c
     uint8_t* base = nullptr;
     hipStream_t s = nullptr;
     const size_t b = a256p(sizeof(orbx_keypoint) * (size_t)n);
+    MatcherLease lease_(m);
     if ((st = matcher_scratch(m, 2 * b, (void**)&base, (void**)&s))) return st;
+    lease_.on(s);
     ORBX_HIP(hipSetDevice(matcher_device(m)));
     orbx_keypoint* din = (orbx_keypoint*)base;
     orbx_keypoint* dout = (orbx_keypoint*)(base + b);
@@ -592,7 +594,9 @@ int orbx_proj_search(orbx_matcher* m, const orbx_proj_params* params, orbx_grid 
                          3 * a256p(4 * NQ) + a256p(4 * N) + a256p(sizeof(orbx_proj_problem)) + 1024;
     uint8_t* base = nullptr;
     hipStream_t s = nullptr;
+    MatcherLease lease_(m);
     if ((st = matcher_scratch(m, bytes, (void**)&base, (void**)&s))) return st;
+    lease_.on(s);
     size_t off = 0;
     auto take = [&](size_t b) { uint8_t* p = base + off; off += a256p(b); return p; };
     orbx_proj_query* dq = (orbx_proj_query*)take(sizeof(orbx_proj_query) * NQ);

@@ -3,9 +3,13 @@
 // their own threads).  Two extractors on two threads and four matchers on four threads, each repeating its call and
 // comparing every result with its single-threaded first result (bit-exact).  Built with ThreadSanitizer on the host
 // code (make tsan; scripts/tsan_gpu.sh runs it on the GPU box); exit status = number of mismatches.
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -47,6 +51,124 @@ int extract(orbx_extractor* ex, const std::vector<uint8_t>& im, int rows, int co
 bool same(const Extraction& a, const Extraction& b) {
     return a.n == b.n && std::memcmp(a.kps.data(), b.kps.data(), sizeof(orbx_keypoint) * a.n) == 0 &&
            std::memcmp(a.desc.data(), b.desc.data(), (size_t)a.n * 32) == 0;
+}
+
+// ---- KeyFrameDatabase: one database shared by the reference's threads (KeyFrameDatabase.cc:42-316 lock mMutex).
+// Tracking's relocalisation queries (Tracking.cc:1366), LoopClosing's detect-then-add (LoopClosing.cc:164,169) and
+// KeyFrame::SetBadFlag's erase (KeyFrame.cc:564) each run on their own thread; a test-side ticket lock records the
+// order in which the calls reached the library, a fourth thread reads (info, score) without it.  The log is replayed
+// on a second database single-threaded: every candidate list must match.
+struct KfdbSetup {
+    int n_vocab = 4000, S = 160;
+    std::vector<std::vector<uint32_t>> words;
+    std::vector<std::vector<double>> values;
+    std::vector<std::vector<int32_t>> covis;
+};
+
+KfdbSetup make_kfdb(uint32_t seed) {
+    KfdbSetup k;
+    uint32_t s = seed * 2654435761u + 7u;
+    auto rnd = [&]() { s = s * 1664525u + 1013904223u; return s >> 8; };
+    k.words.resize(k.S); k.values.resize(k.S); k.covis.resize(k.S);
+    for (int i = 0; i < k.S; ++i) {
+        const int place = i % 8;
+        std::vector<uint32_t> w;
+        const int m = 60 + (int)(rnd() % 120);
+        for (int j = 0; j < m; ++j) w.push_back(rnd() % 3 ? (uint32_t)(place * 400 + rnd() % 400) : (uint32_t)(rnd() % k.n_vocab));
+        std::sort(w.begin(), w.end());
+        w.erase(std::unique(w.begin(), w.end()), w.end());
+        std::vector<double> v(w.size());
+        double t = 0;
+        for (auto& x : v) { x = 1.0 + (rnd() % 1000); t += x; }
+        for (auto& x : v) x /= t;
+        k.words[i] = w; k.values[i] = v;
+        for (int j = 1; j <= 10; ++j) k.covis[i].push_back((i + 8 * j) % k.S);
+    }
+    return k;
+}
+
+int kfdb_init(orbx_kfdb** db, const KfdbSetup& k) {
+    int st = orbx_kfdb_create(k.n_vocab, k.S, 512, 0, db);
+    for (int i = 0; i < k.S && !st; ++i) st = orbx_kfdb_set_bow(*db, i, k.words[i].data(), k.values[i].data(), (int)k.words[i].size());
+    std::vector<int32_t> slots(k.S), best((size_t)k.S * 10);
+    for (int i = 0; i < k.S; ++i) { slots[i] = i; std::copy(k.covis[i].begin(), k.covis[i].end(), best.begin() + 10 * i); }
+    if (!st) st = orbx_kfdb_set_covisibility(*db, slots.data(), k.S, best.data());
+    std::vector<int32_t> init;
+    for (int i = 0; i < 80; ++i) init.push_back(i);
+    if (!st) st = orbx_kfdb_add(*db, init.data(), (int)init.size());
+    return st;
+}
+
+struct KfOp { int kind, slot; uint64_t id; float min_score; std::vector<int32_t> excl, result; };  // kind -1 add, -2 erase
+
+int kfdb_apply(orbx_kfdb* db, KfOp& op) {
+    if (op.kind == -1) return orbx_kfdb_add(db, &op.slot, 1);
+    if (op.kind == -2) return orbx_kfdb_erase(db, &op.slot, 1);
+    int32_t eo[2] = {0, (int32_t)op.excl.size()}, oo[2] = {0, 0};
+    std::vector<int32_t> out(160);
+    const int st = orbx_kfdb_detect(db, op.kind, &op.slot, &op.id, op.kind == ORBX_KFDB_RELOC ? nullptr : &op.min_score, 1,
+                                    op.kind == ORBX_KFDB_RELOC ? nullptr : eo, op.excl.empty() ? nullptr : op.excl.data(), oo,
+                                    out.data(), (int)out.size());
+    op.result.assign(out.begin(), out.begin() + oo[1]);
+    return st;
+}
+
+int kfdb_concurrency(int reps) {
+    const KfdbSetup k = make_kfdb(11);
+    orbx_kfdb *db = nullptr, *db2 = nullptr;
+    if (kfdb_init(&db, k) || kfdb_init(&db2, k)) { std::fprintf(stderr, "%s\n", orbx_last_error()); return 100; }
+    std::mutex ticket;
+    std::vector<KfOp> log;
+    int errors = 0;
+    auto run = [&](KfOp op) {
+        std::lock_guard<std::mutex> g(ticket);
+        if (kfdb_apply(db, op)) ++errors;
+        log.push_back(std::move(op));
+    };
+    std::vector<std::pair<int32_t, int32_t>> pairs;
+    for (int i = 0; i < 64; ++i) pairs.push_back({i, (i * 7 + 3) % k.S});
+    std::vector<double> sref(pairs.size());
+    if (orbx_kfdb_score(db2, &pairs[0].first, (int)pairs.size(), sref.data())) return 100;
+    std::atomic<bool> stop{false};
+    int reader_bad = 0;
+    std::vector<std::thread> th;
+    th.emplace_back([&] {   // Tracking: relocalisation queries from frames (spare slots 150..159)
+        for (int r = 0; r < 4 * reps; ++r) run(KfOp{ORBX_KFDB_RELOC, 150 + r % 10, 1000000ull + r, 0.f, {}, {}});
+    });
+    th.emplace_back([&] {   // LoopClosing: DetectLoopCandidates, then the keyframe joins the database
+        for (int i = 0; i < 40; ++i) {
+            const int slot = 80 + i;
+            run(KfOp{ORBX_KFDB_LOOP, slot, 2000000ull + i, 0.01f, k.covis[slot], {}});
+            run(KfOp{-1, slot, 0, 0.f, {}, {}});
+        }
+    });
+    th.emplace_back([&] {   // KeyFrame::SetBadFlag: erase
+        for (int i = 0; i < 30; ++i) { run(KfOp{-2, i, 0, 0.f, {}, {}}); std::this_thread::yield(); }
+    });
+    std::thread reader([&] {   // no ticket: the database's own lock orders these against the writers
+        std::vector<double> sc(pairs.size());
+        while (!stop.load()) {
+            int nm = 0;
+            if (orbx_kfdb_info(db, nullptr, nullptr, nullptr, &nm) || nm < 0 || nm > k.S) ++reader_bad;
+            if (orbx_kfdb_score(db, &pairs[0].first, (int)pairs.size(), sc.data()) || sc != sref) ++reader_bad;
+        }
+    });
+    for (auto& t : th) t.join();
+    stop = true;
+    reader.join();
+    int mismatch = 0;
+    for (auto& op : log) {   // single-threaded replay in ticket order
+        KfOp r = op;
+        if (kfdb_apply(db2, r)) ++errors;
+        if (r.result != op.result) ++mismatch;
+    }
+    int nres = 0;
+    for (auto& op : log) nres += (int)op.result.size();
+    std::printf("kfdb concurrency: %zu operations on 3 threads + reader, %d candidates, %d replay mismatches, %d errors, %d reader "
+                "errors\n", log.size(), nres, mismatch, errors, reader_bad);
+    orbx_kfdb_destroy(db);
+    orbx_kfdb_destroy(db2);
+    return mismatch + errors + reader_bad;
 }
 
 }  // namespace
@@ -104,5 +226,5 @@ int main(int argc, char** argv) {
                 2 * reps, ref[0].n, ref[1].n, 4 * reps, total);
     for (auto& m : mt) orbx_matcher_destroy(m);
     for (auto& e : ex) orbx_extractor_destroy(e);
-    return total;
+    return total + kfdb_concurrency(reps);
 }
