@@ -354,6 +354,10 @@ class KeyframeFusion:
                  candidates: int = 16, levelsup: int = 4, min_matches: int = 20, db=None):
         import torch
 
+        if exchange is not None and getattr(exchange, "world", 1) > 1 and agent != exchange.rank:
+            # the slot groups of a step are rank-major (rank r's packets are group r) and the query group is the
+            # agent: they must be one number, or the same-map discard (MapFusion.cc:136-144) compares different ids
+            raise ValueError(f"agent {agent} != exchange rank {exchange.rank}: one agent per rank")
         self.matcher, self.vocab, self.capacity = matcher, vocab, capacity
         self.store = DeviceKeyframeStore(capacity, slots, device)
         self.agent, self.exchange = agent, exchange

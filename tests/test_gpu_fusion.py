@@ -155,3 +155,80 @@ def test_native_rccl_exchange_world1(gpu):
     torch.cuda.synchronize()
     assert torch.equal(send, recv)
     x.close()
+
+
+@pytest.mark.parametrize("config", ["C4", "C5"])
+def test_native_fusion_agents_one_gpu(gpu, config):
+    """The native engine (orbx_fusion) at C4's (4 agents, 752x480 / 1200) and C5's (8 agents, KITTI 1242x375 / 2000,
+    seq 00 split 8-way) agent counts on one GPU: W engines, the test all-gathers their packets rank-major and hands them
+    to phase 2 -- ring replicas, slot groups, the sequential DetectLoopCandidates, the same-map discard and the batched
+    SearchByBoW against the oracle's MapFusion loop."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    from test_multiagent import AGENT_CONFIGS, agent_images
+    cfg = AGENT_CONFIGS[config]
+    W, n, K, STEPS = cfg["W"], 2, 3, 3
+    SLOTS = 2 * W * n
+    dev = torch.device("cuda", 0)
+    voc = S.synthetic_vocabulary(37, k=10, L=5)
+    v = pkg.ORBVocabulary.from_arrays(voc)
+    ex = pkg.ORBextractor(cfg["nfeat"], 1.2, 8, 20, 7)
+    imgs, frames = agent_images(cfg, STEPS, n, seed=760)
+    flat = np.stack([im for st in imgs for ag in st for im in ag])
+    kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(flat).to(dev))
+    cap = kps.shape[1]
+    depth = torch.rand((len(flat), cap), device=dev) - 0.3
+    eng = [pkg.KeyframeFusionEngine(v, pkg.ORBmatcher(0.75, True), cap, SLOTS, max_keyframes=n, candidates=K, levelsup=3,
+                                    agent=r, world=W) for r in range(W)]
+    odb = O.Kfdb(v.info()["n_words"], SLOTS)
+    kf_id, total_real, cross = 1, 0, 0
+    for step in range(STEPS):
+        sends = []
+        for r in range(W):
+            send = torch.empty((n, eng[r].packet_bytes), dtype=torch.uint8, device=dev)
+            first = (step * W + r) * n
+            eng[r].pack(kps, desc, cnt, range(first, first + n), frame_base=frames[step][r][0], frame_step=5, depth=depth,
+                        send=send)
+            sends.append(send)
+        gathered = torch.cat(sends, 0)
+        outs = []
+        for r in range(W):
+            o = eng[r].new_outputs(n)
+            eng[r].commit(gathered, o)
+            outs.append(o)
+        torch.cuda.synchronize()
+        rings = [e.read_ring() for e in eng]
+        new, _ = eng[0].last_step()
+        for r in range(1, W):
+            assert np.array_equal(rings[0][new.start:new.stop], rings[r][new.start:new.stop])
+        views = MA.unpack_keyframes(rings[0], cap)
+        agent_of = {k: views[k].agent for k in range(SLOTS)}
+        assert [agent_of[k] for k in new] == [r for r in range(W) for _ in range(n)]
+        assert [views[k].frame for k in new] == [f for r in range(W) for f in frames[step][r]]
+        odb.erase(list(new))
+        for k in new:
+            odb.set_bow(k, *views[k].bow)
+        expect = {}
+        for k in new:
+            c = [x for x in odb.detect(0, k, kf_id, 0.0).tolist() if agent_of[x] != agent_of[k]][:K]
+            cross += sum(1 for x in c if x in new)
+            kf_id += 1
+            expect[k] = c + [-1] * (K - len(c))
+            odb.add([k])
+        for r in range(W):
+            _, queries = eng[r].last_step()
+            assert list(queries) == list(range(new.start + r * n, new.start + (r + 1) * n))
+            pr, m12, nm = outs[r]
+            assert pr.cpu().numpy().tolist() == [[q, c] for q in queries for c in expect[q]], (step, r)
+            for p, (a, b) in enumerate(pr.cpu().numpy()):
+                if b < 0:
+                    continue
+                assert agent_of[b] != r
+                A, B = views[a], views[b]
+                rn, rm = O.search_by_bow_kfkf(A.desc, A.kps["angle"], A.valid, A.featvec, B.desc, B.kps["angle"],
+                                              B.valid, B.featvec, 0.75, True)
+                assert int(nm[p]) == rn and np.array_equal(m12[p, :A.count].cpu().numpy(), rm)
+                total_real += 1
+    for e in eng:
+        e.check()
+    assert total_real >= W * n and cross >= 1

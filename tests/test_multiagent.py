@@ -516,3 +516,116 @@ def test_keyframe_fusion_step_two_agents_gloo():
     # 0's keyframes of the same exchange (slots 0, 1), which MapFusion added before them
     assert any(c in (0, 1) for _, c in objs[1][0][0])
     assert max(v for r in range(world) for st in objs[r] for v in st[1]) >= 20
+
+
+# ---- configs C4 / C5 at their agent counts, emulated on one GPU ------------------------------------------------
+# C4: 4 agents on EuRoC MH01-MH04 (752x480, 1200 kpts, Examples/Stereo/EuRoC.yaml:88) -- one sequence per agent;
+# C5: 8 agents on KITTI seq 00 (1242x375, 2000 kpts) split 8-way (generic_split_seq.cc:543-589, 4541 frames).
+AGENT_CONFIGS = {
+    "C4": dict(W=4, rows=480, cols=752, nfeat=1200, chunks=[range(0, 3682), range(0, 3040), range(0, 2700), range(0, 2033)]),
+    "C5": dict(W=8, rows=375, cols=1242, nfeat=2000, chunks=MA.split_sequence(4541, 8)),
+}
+
+
+def agent_images(cfg, steps, n, places=3, seed=700):
+    """Keyframe j of agent r at step s shows place (r + s + j) % places, shifted: every agent revisits the places
+    the others see, so MapFusion finds cross-agent candidates.  Returns (images [steps][W][n], frame ids)."""
+    bases = [S.kitti_like_image(seed + p, rows=cfg["rows"], cols=cfg["cols"]) for p in range(places)]
+    imgs, frames = [], []
+    for s in range(steps):
+        imgs.append([[S.shifted_right_view(bases[(r + s + j) % places], 3 + 5 * r + j, max_disp=10) for j in range(n)]
+                     for r in range(cfg["W"])])
+        frames.append([[cfg["chunks"][r].start + 5 * (s * n + j) for j in range(n)] for r in range(cfg["W"])])
+    return imgs, frames
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["C4", "C5"])
+def test_gpu_keyframe_fusion_agents_one_gpu(gpu, config):
+    """KeyframeFusion.step's multi-rank branch at C4's / C5's agent count on one GPU: every agent's packets
+    exchanged rank-major (the RCCL all-gather's order), W replicas of the ring, slot groups, the sequential
+    DetectLoopCandidates, the same-map discard (src/MapFusion.cc:136-144) and SearchByBoW, against the oracle running
+    MapFusion's single-server loop over the same keyframes."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    cfg = AGENT_CONFIGS[config]
+    W, n, K, STEPS = cfg["W"], 2, 3, 3
+    SLOTS = 2 * W * n
+    dev = torch.device("cuda", 0)
+    voc = S.synthetic_vocabulary(31, k=10, L=5)
+    v = pkg.ORBVocabulary.from_arrays(voc)
+    ex = pkg.ORBextractor(cfg["nfeat"], 1.2, 8, 20, 7)
+    imgs, frames = agent_images(cfg, STEPS, n)
+    flat = np.stack([im for st in imgs for ag in st for im in ag])
+    kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(flat).to(dev))
+    cap = kps.shape[1]
+    valid = (torch.arange(cap, device=dev)[None, :] < cnt[:, None]).to(torch.uint8)
+    valid[:, 2::5] = 0
+    fx = [_FakeExchange(r, W) for r in range(W)]
+    fus = [MA.KeyframeFusion(pkg.ORBmatcher(0.75, True), v, cap, slots=SLOTS, device=dev, agent=r, exchange=fx[r],
+                             candidates=K, levelsup=3) for r in range(W)]
+    odb = O.Kfdb(v.info()["n_words"], SLOTS)
+    kf_id, n_real, n_cross, n_gate = 1, 0, 0, 0
+    for step in range(STEPS):
+        rows = [[(step * W + r) * n + j for j in range(n)] for r in range(W)]
+        pk = []
+        for r in range(W):
+            ix = torch.tensor(rows[r], device=dev)
+            fv = v.transform_batch_device(desc[ix].contiguous(), cnt[ix].contiguous(), 3)
+            pk.append(MA.pack_keyframes(kps[ix], desc[ix], cnt[ix], valid[ix], r, frames[step][r], cap, fv))
+        for f in fx:
+            f.packets = pk
+        outs = []
+        for r in range(W):
+            ix = torch.tensor(rows[r], device=dev)
+            outs.append(fus[r].step(kps[ix], desc[ix], cnt[ix], valid[ix], frames=frames[step][r]))
+        torch.cuda.synchronize()
+        views = MA.unpack_keyframes(fus[0].store.buf, cap)
+        for r in range(1, W):   # every rank's ring holds the same keyframes
+            for a, b in zip(views, MA.unpack_keyframes(fus[r].store.buf, cap)):
+                assert (a.count, a.agent, a.frame) == (b.count, b.agent, b.frame)
+                assert np.array_equal(a.desc, b.desc) and np.array_equal(a.valid, b.valid)
+        base = (step * W * n) % SLOTS
+        new = list(range(base, base + W * n))
+        agent = {k: views[k].agent for k in range(SLOTS) if views[k].count > 0}
+        assert [agent[k] for k in new] == [r for r in range(W) for _ in range(n)]
+        assert [views[k].frame for k in new] == [f for r in range(W) for f in frames[step][r]]
+        for r in range(W):
+            assert fus[r].slot_group[new].tolist() == [r for r in range(W) for _ in range(n)]
+        odb.erase(new)
+        for k in new:
+            odb.set_bow(k, *views[k].bow)
+        expect = {r: [] for r in range(W)}
+        for k in new:   # MapFusion's loop: query, drop same-map candidates, first K, then add
+            a = agent[k]
+            c = [x for x in odb.detect(0, k, kf_id, 0.0).tolist() if agent[x] != a][:K]
+            kf_id += 1
+            n_cross += sum(1 for x in c if x in new)
+            expect[a] += [[k, x] for x in c] + [[k, -1]] * (K - len(c))
+            odb.add([k])
+        for r in range(W):
+            pr, m12, nm, passed = outs[r]
+            prh, m12h, nmh = pr.cpu().numpy(), m12.cpu().numpy(), nm.cpu().numpy()
+            assert prh.tolist() == expect[r], (step, r)
+            for p, (a, b) in enumerate(prh):
+                if b < 0:
+                    assert nmh[p] == 0 and (m12h[p] == -1).all()
+                    continue
+                assert agent[b] != r                                   # same-map discard
+                A, B = views[a], views[b]
+                rn, rm = O.search_by_bow_kfkf(A.desc, A.kps["angle"], A.valid, A.featvec, B.desc, B.kps["angle"],
+                                              B.valid, B.featvec, 0.75, True)
+                assert nmh[p] == rn and np.array_equal(m12h[p, :A.count], rm), (step, r, p)
+                n_real += 1
+                n_gate += int(rn >= 20)
+            assert np.array_equal(passed.cpu().numpy(), nmh >= 20)
+            fus[r].check()
+    assert n_real >= W * n and n_cross >= 1 and n_gate >= 1
+
+
+def test_keyframe_fusion_agent_must_be_rank():
+    """the same-map discard compares slot groups (rank-major) with the query group (the agent)."""
+    class X:
+        world, rank = 4, 2
+    with pytest.raises(ValueError):
+        MA.KeyframeFusion(None, None, 64, slots=8, device=torch.device("cpu"), agent=1, exchange=X())
