@@ -81,8 +81,12 @@ def parse():
     ap.add_argument("--distinct", type=int, default=128, help="distinct synthetic stereo pairs per rank (tiled to batch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
+    ap.add_argument("--host-fed-steps", type=int, default=10,
+                    help="steps of the host-fed block: the batch's images copied H2D from pinned host memory every step on a "
+                         "copy stream, overlapped with the previous step (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage event timing")
     ap.add_argument("--no-c3", dest="c3", action="store_false", help="skip the C3 2000x2000 all-pairs block")
+    ap.add_argument("--no-cd", dest="cd", action="store_false", help="skip the CovisibilityDiscovery-shaped block")
     ap.add_argument("--diag-skip", default="", help="diagnostics only (not the metric): comma list of stereo,keyframes "
                                                      "to leave out of the step")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -102,12 +106,27 @@ def compulsory_bytes(cfg):
 
 
 def cpu_threads():
-    n = os.environ.get("OMP_NUM_THREADS")
+    """Every core this process may use, as SURVEY §8(d) asks (T = nproc): the CPUs of sched_getaffinity, bounded by the
+    cgroup CPU quota when there is one (the GPU box shows 256 CPUs but grants 16: 256 threads there measured 238
+    frames/s against 285 on 16).  ORBX_CPU_THREADS overrides (diagnostics)."""
+    n = os.environ.get("ORBX_CPU_THREADS")
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    return max(1, min(int(n) if n and n.isdigit() else avail, avail, 16))
+    q = cpu_quota()
+    if q:
+        avail = min(avail, max(1, int(np.ceil(q))))
+    return max(1, int(n)) if n and n.isdigit() else avail
+
+
+def cpu_quota():
+    """The cgroup CPU quota in CPUs (cgroup v2 cpu.max), None when unlimited or unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_model():
@@ -197,7 +216,8 @@ def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds):
     el = time.perf_counter() - t0
     done = sum(a.n for a in agents)
     return {"value": round(done / el, 3), "unit": "frames/s", "cores": T, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": cpu_quota(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "latency_ms_1thread": {"median": round(float(np.median(lat_ms)), 2),
                                    "p95": round(float(np.percentile(lat_ms, 95)), 2), "frames": len(lat_ms)},
             "throughput_1thread_fps": round(1e3 / float(np.mean(lat_ms)), 3),
@@ -232,6 +252,105 @@ def host_api_rate(pkg, cfg, lefts, rights, n_frames, device):
             "latency_ms_p95": round(float(np.percentile(lat_ms, 95)), 3), "frames": len(lat),
             "path": "orbx_extract(L) and orbx_extract(R) on two threads (Frame.cc:78-81) + orbx_compute_stereo_matches, "
                     "host buffers, one frame per call"}
+
+
+def host_fed_block(step, last_handoff, host, stream, B, steps, dev):
+    """The same step with its 2B input images arriving from host memory every step, as Frame's constructor receives
+    host images (Frame.cc:61-117): a pinned host batch (a camera ring would fill it) is copied H2D on a copy stream into
+    a ring of 3 device batches; step k's extraction waits for its copy, and the copy of step k+1 overlaps step k.  A
+    slot is rewritten only after the stereo step that last read it (level 0 of the pyramid is the input image itself)."""
+    import torch
+    pinned = torch.from_numpy(host).pin_memory()
+    nbytes = pinned.numel()
+    ring = [torch.empty_like(pinned, device=dev) for _ in range(3)]
+    consumed = [None] * 3
+    cs = torch.cuda.Stream(dev)
+    # PCIe H2D alone, for the ceiling
+    for _ in range(2):
+        with torch.cuda.stream(cs):
+            ring[0].copy_(pinned, non_blocking=True)
+    cs.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(cs)
+    for i in range(5):
+        with torch.cuda.stream(cs):
+            ring[i % 3].copy_(pinned, non_blocking=True)
+    e1.record(cs)
+    e1.synchronize()
+    h2d_gbs = 5 * nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+    def fed_step(i):
+        k = i % 3
+        if consumed[k] is not None:
+            cs.wait_event(consumed[k])
+        with torch.cuda.stream(cs):
+            ring[k].copy_(pinned, non_blocking=True)
+        ready = torch.cuda.Event()
+        ready.record(cs)
+        stream.wait_event(ready)
+        step(src=ring[k])
+        consumed[k] = last_handoff[0]
+
+    for i in range(3):
+        fed_step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        fed_step(i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    fps = B * steps / el
+    return {"frames_per_s": round(fps, 1), "ms_per_step": round(1e3 * el / steps, 3), "steps": steps,
+            "input_bytes_per_step": nbytes, "h2d_GBps_needed": round(nbytes * steps / el / 1e9, 2),
+            "h2d_GBps_alone": round(h2d_gbs, 2),
+            "pcie_bound_frames_per_s": round(B * h2d_gbs * 1e9 / nbytes, 1),
+            "path": "pinned host batch -> H2D on a copy stream into a 3-slot device ring, overlapped with the previous "
+                    "step; the same step as `value` otherwise (stereo + keyframe path)"}
+
+
+def cd_block(pkg, MA, kps, desc, cnt, vocab, B, reps=3):
+    """A CovisibilityDiscovery-shaped batch (MapFusion.cc:774-885): the last step's B left keyframes are the matched
+    map (in its KeyFrameDatabase), its B right keyframes the absorbed map; every absorbed keyframe computes minScore
+    over its 10 covisible keyframes (the 5 before and after it), queries DetectCovisibilityCandidates ignoring the
+    absorbed map, and runs SearchByBoW against every candidate (15-match gate).  Wall time per pass with the
+    candidate-count readback it needs (the Fuse step after it is out of scope).  The reference's published CD stage
+    (which also fuses MapPoints and stops / releases LocalMapping) is printed beside it as context only."""
+    import torch
+    dev = kps.device
+    cap = kps.shape[1]
+    fv = vocab.transform_batch_device(desc, cnt, 4)
+    valid = (torch.arange(cap, device=dev)[None, :] < cnt[:, None]).to(torch.uint8)
+    valid[:, 2::3] = 0                                         # ~2/3 of keypoints carry a MapPoint
+    store = pkg.KfStore.from_fields(cap, desc=(desc, cap * 32), kps=(kps, cap * 28), valid=(valid, cap),
+                                    fv_nodes=(fv["fv_nodes"], cap * 4), fv_offsets=(fv["fv_offsets"], (cap + 1) * 4),
+                                    fv_indices=(fv["fv_indices"], cap * 4), n_fv=(fv["n_fv"], 4))
+    db = pkg.KeyFrameDatabase(vocab.info()["n_words"], 2 * B, max_words=min(cap, 4096), device=dev.index)
+    db.set_bow_device(torch.arange(2 * B, dtype=torch.int32, device=dev), fv["bow_words"], fv["bow_values"], fv["n_words"])
+    db.add(list(range(B)))
+    queries = list(range(B, 2 * B))
+    covis = [[c for c in range(q - 5, q + 6) if c != q and B <= c < 2 * B] for q in queries]
+    cd = MA.CovisibilityDiscovery(pkg.ORBmatcher(0.75, True, device=dev.index), db, store,
+                                  max_fv_nodes=min(cap, 10 ** 2 + 1))
+    times, last = [], None
+    for r in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = cd.run(queries, [10_000_000 + r * B + i for i in range(B)], covis, queries)
+        torch.cuda.synchronize()
+        if r:
+            times.append(time.perf_counter() - t0)
+        last = res
+    pr, m12, nm, passed, n_cand = last
+    ms = 1e3 * float(np.median(times))
+    real = int((pr[:, 1] >= 0).sum().item())
+    return {"absorbed_keyframes": B, "matched_map_keyframes": B, "ms_per_pass": round(ms, 3),
+            "ms_per_keyframe": round(ms / B, 4), "passes": [round(1e3 * t, 3) for t in times],
+            "candidates_per_keyframe": round(float(np.mean(n_cand)), 2), "searchbybow_pairs": real,
+            "pairs_passing_15": int(passed.sum().item()),
+            "reference_cd_stage_ms (context: includes Fuse + LocalMapping stop/release, hardware unstated)":
+                {"KITTI 00 (mkf 136.2)": 1850.51, "KITTI 02": 15297.20, "EuRoC MH01": 7362.53},
+            "path": "multiagent.CovisibilityDiscovery: orbx_kfdb_score_device (minScore), orbx_kfdb_detect_device COVIS, "
+                    "one candidate-count readback, orbx_kfdb_candidate_pairs_device, orbx_search_by_bow_kfkf_pairs_device"}
 
 
 def c3_bench(pkg, dev, n_problems=64, reps=30):
@@ -285,6 +404,96 @@ def load_profile(name):
         except (OSError, ValueError):
             return None
     return None
+
+
+# Live stage timers (orbx_extractor_stage_times: HIP events on the stream each launch is issued on) that time a
+# kernel's launches over the whole batch: k_fast_band is two launches per call (level 0 on the extractor's side stream,
+# levels 1..7 on the launch stream), each timed by its own event pair; k_describe_m is one launch on the output stream.
+LIVE_STAGES = {"k_fast_band": ("fast_cells", "fast_cells_l0"), "k_describe_m": ("describe",), "k_describe": ("describe",),
+               "k_quadtree": ("quadtree", "quadtree_l0")}
+
+
+def kernel_family(name):
+    return name.split("<")[0]
+
+
+def source_sha16():
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from kernel_share import source_sha16 as f
+    return f(ROOT)
+
+
+def roofline_lines(per_call, cfg, units, config):
+    """Roofline of the dominant kernel -- the one with the largest share of GPU time in the committed kernel trace of
+    the bench command (profiles/kernel_share.json, scripts/kernel_share.py) -- and of the describe as a secondary
+    line.  achieved = SURVEY §8(d) algorithmic bytes of the extractions the kernel's launches cover per step (one
+    extraction = image in + nfeatures x 60 B out; every launch family covers all 2B images once) / the kernel's live
+    time per step (sum of its launches' event spans)."""
+    share = load_profile("kernel_share.json")
+    cb = compulsory_bytes(cfg)["extraction"]
+    dom = "k_fast_band"
+    prof_ms, stale, tag = None, None, None
+    if share and share.get("config", "kitti") == config and share.get("batch_images") == units:
+        dom = kernel_family(share["dominant"])
+        tag = share.get("tag")
+        stale = share.get("source_sha16") != source_sha16()
+        prof_ms = sum(k["ms_per_step"] for k in share["kernels"] if kernel_family(k["kernel"]) == dom)
+
+    def line(fam, kernel_name):
+        stages = LIVE_STAGES.get(fam)
+        if not stages or any(st not in per_call for st in stages):
+            return None
+        t_ms = sum(per_call[st] for st in stages)
+        bytes_step = cb * units
+        achieved = bytes_step / (t_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = load_profile("pmc_traffic.json")
+        if pmc and kernel_family(pmc.get("kernel", "")) == fam and pmc.get("batch_images") == units \
+                and pmc.get("config", "kitti") == config:
+            traffic = pmc.get("hbm_bytes_per_step", pmc.get("hbm_bytes_per_launch"))
+        return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": kernel_name,
+                "launches_per_step": len(stages), "live_stages": list(stages),
+                "kernel_ms_per_step": round(t_ms, 4), "algorithmic_bytes_per_step": bytes_step,
+                "algorithmic_bytes_per_unit": cb, "units_per_step": units,
+                "traffic_ratio": round(traffic / bytes_step, 2) if traffic else None,
+                "unit_of_work": "one extraction (SURVEY §8d: image in + nfeatures x 60 B out); the kernel's launches of a "
+                                "step together cover every image of the batch once"}
+    kpw = int(os.environ.get("ORBX_DESC_KPW", "2"))
+    desc_name = "k_describe" if kpw == 1 else f"k_describe_m<{4 if kpw == 4 else 2}>"
+    names = {"k_fast_band": "k_fast_band<72, true>", "k_describe_m": desc_name, "k_describe": desc_name,
+             "k_quadtree": "k_quadtree"}
+    main_line = line(dom, names.get(dom, dom)) or line("k_fast_band", names["k_fast_band"])
+    if main_line is not None:
+        main_line["selected_by"] = (f"largest share of GPU time in profiles/kernel_share.json ({tag})" if tag else
+                                    "default (no kernel_share.json for this config)")
+        if prof_ms is not None:
+            main_line["rocprof_ms_per_step"] = round(prof_ms, 4)
+            main_line["profile_stale"] = stale
+    sec = line(kernel_family(desc_name), desc_name) if kernel_family(desc_name) != dom else None
+    return main_line, sec
+
+
+def valu_line(roof, config, units):
+    """VALU roofline of the same kernel: SQ_INSTS_VALU x 64 lane-ops per step from the committed SQ pass
+    (profiles/sq_summary.json), over the live time; dropped when the SQ profile was taken on other sources."""
+    sq = load_profile("sq_summary.json")
+    if not (roof and sq and sq.get("config", "kitti") == config and sq.get("batch_images") == units):
+        return None
+    if sq.get("source_sha16") != source_sha16():
+        return None
+    fam = kernel_family(roof["kernel"])
+    ks = [(k, v) for k, v in sq["kernels"].items() if kernel_family(k) == fam]
+    if not ks:
+        return None
+    ops = sum(v["valu_lane_ops"] * v.get("launches_per_step", 1) for _, v in ks)
+    t_ms = roof["kernel_ms_per_step"]
+    tops = ops / (t_ms * 1e-3) / 1e12
+    return {"bound": "valu", "achieved": round(tops, 3), "peak": round(VALU_PEAK_TOPS, 2), "unit": "Tlane-op/s",
+            "frac": round(tops / VALU_PEAK_TOPS, 4), "kernel": roof["kernel"], "valu_lane_ops_per_step": ops,
+            "profiled_valu_frac": {k: v.get("valu_frac") for k, v in ks},
+            "source": f"SQ_INSTS_VALU x 64 per launch from profiles/sq_summary.json ({sq.get('tag')}, sources "
+                      f"{sq.get('source_sha16')}), time measured live"}
 
 
 def main():
@@ -385,7 +594,9 @@ def main():
     kf_ms = []
     host_split = [0.0, 0.0]                            # host enqueue seconds: front-end, keyframe path
 
-    def step(time_stereo=False):
+    last_handoff = [None]
+
+    def step(time_stereo=False, src=None):
         h0 = time.perf_counter()
         buf = n_step[0] % NS
         ex = exs[n_step[0] % n_ctx]
@@ -402,7 +613,7 @@ def main():
         pslot = n_step[0] % NP
         if stereo_done[pslot] is not None:
             stream.wait_event(stereo_done[pslot])     # the resize chain overwrites the set that stereo step read
-        ex.extract_batch_device(imgs, kps, desc, cnt, stream=stream, out_stream=dstream)
+        ex.extract_batch_device(imgs if src is None else src, kps, desc, cnt, stream=stream, out_stream=dstream)
         extracted = torch.cuda.Event()
         extracted.record(ostream)
         pyr = ex.pyramid_device()                      # this call's pyramid set (a slot of the ring of 2)
@@ -424,6 +635,7 @@ def main():
         handoff = torch.cuda.Event()
         handoff.record(stereo_stream)
         stereo_done[pslot] = handoff
+        last_handoff[0] = handoff
         h1 = time.perf_counter()
         if "keyframes" in skip:
             n_step[0] += 1
@@ -502,6 +714,8 @@ def main():
 
     frames = B * args.steps * world
     value = frames / el
+    collective = ("RCCL all-gather (torch.distributed nccl, xGMI)" if args.dist_backend == "nccl" else
+                  "gloo all-gather staged through host memory (rehearsal, not xGMI)")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True,
@@ -516,9 +730,12 @@ def main():
                                               "keyframe_path": round(1000 * (split1[1] - split0[1]) / args.steps, 3)},
         "config": {"workload": f"{args.config}: stereo frame = ORBextractor x2 ({COLS}x{ROWS}, 8 levels, {NFEAT} kpts) + "
                                "stereo L<->R 256-bit Hamming band match + SAD sub-pixel refinement; every 5th frame a "
-                               "keyframe: DBoW2 transform (k=10, L=6) + " + ("RCCL all-gather of KF packets + " if world > 1 else "") +
+                               "keyframe: DBoW2 transform (k=10, L=6) + " + (f"{collective} of KF packets + " if world > 1 else "") +
                                "KeyFrameDatabase DetectLoopCandidates (query, then add) over the KF store + "
-                               f"SearchByBoW vs the first {KF_CANDIDATES} candidates",
+                               f"SearchByBoW vs the first {KF_CANDIDATES} candidates" +
+                               (" of other agents' maps (MapFusion.cc:136-144)" if world > 1 else
+                                " of the agent's own map with minScore 0 (LoopClosing-like: N=1 has no other map, so these "
+                                "pairs are work MapFusion itself would not do)"),
                    "settings": cfg["source"],
                    "keyframes_per_gpu_per_step": n_kf, "bow_pairs_per_gpu_per_step": n_kf * KF_CANDIDATES,
                    "global_batch": B * world, "frames_per_gpu_per_step": B, "image": [ROWS, COLS],
@@ -540,49 +757,28 @@ def main():
         kms = [a.elapsed_time(b) for a, b in kf_ms]
         per_call["keyframe_bow_fusion"] = float(np.mean(kms)) if kms else 0.0
         out["stage_ms_per_step"] = {k: round(v, 4) for k, v in per_call.items()}
-        # Roofline of the extractor kernel launched ONCE over the whole batch: k_describe.  FAST, DistributeOctTree and
-        # the blur are each split into a level-0 launch (side stream, concurrent with the resize chain) and a levels
-        # 1..7 launch, so their event spans hold concurrent work and neither launch covers whole extractions;
-        # k_describe is one launch over the whole batch (on the stereo queue, beside the next step's resize chain and
-        # level-0 FAST: its event span is its kernel duration under that overlap, as rocprof's).
-        kpw = int(os.environ.get("ORBX_DESC_KPW", "2"))
-        kernel_of = {"describe": "k_describe" if kpw == 1 else f"k_describe_m<{4 if kpw == 4 else 2}>"}
-        dom = max(kernel_of, key=lambda k: per_call.get(k, 0.0))
-        units = 2 * B                                    # extractions per launch
-        cb = compulsory_bytes(cfg)
-        bytes_launch = cb["extraction"] * units
-        t_ms = per_call[dom]
-        achieved = bytes_launch / (t_ms * 1e-3) / 1e9
-        traffic = None
-        pmc = load_profile("pmc_traffic.json")
-        if pmc and pmc.get("kernel") == kernel_of[dom] and pmc.get("batch_images") == units \
-                and pmc.get("config", "kitti") == args.config:
-            traffic = pmc.get("hbm_bytes_per_launch")
-        out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": kernel_of[dom],
-                           "kernel_ms_per_launch": round(t_ms, 4), "algorithmic_bytes_per_launch": bytes_launch,
-                           "algorithmic_bytes_per_unit": cb["extraction"], "units_per_launch": units,
-                           "unit_of_work": "one extraction (SURVEY §8d: image in + nfeatures x 60 B out)"}
-        sq = load_profile("sq_summary.json")
-        if sq and sq.get("config", "kitti") == args.config and sq.get("batch_images") == units:
-            k = sq["kernels"].get(kernel_of[dom])
-            if k:
-                ops = k["valu_lane_ops"]
-                out["roofline_valu"] = {"bound": "valu", "achieved": round(ops / (t_ms * 1e-3) / 1e12, 3),
-                                        "peak": round(VALU_PEAK_TOPS, 2), "unit": "Tlane-op/s",
-                                        "frac": round(ops / (t_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4),
-                                        "kernel": kernel_of[dom], "valu_lane_ops_per_launch": ops,
-                                        "source": "SQ_INSTS_VALU x 64 per launch from profiles/sq_summary.json "
-                                                  f"({sq.get('tag')}), time measured live"}
+        out["roofline"], sec = roofline_lines(per_call, cfg, 2 * B, args.config)
+        if sec:
+            out["roofline_secondary"] = sec
+        v = valu_line(out["roofline"], args.config, 2 * B)
+        if v:
+            out["roofline_valu"] = v
     if exchange is not None:
         xs = exchange.stats()
         if xs:
-            out["exchange"] = dict(xs, collective="all_gather_into_tensor (RCCL over xGMI)" if args.dist_backend == "nccl"
-                                   else "all_gather (gloo, staged through host memory: rehearsal, not xGMI)",
+            out["exchange"] = dict(xs, collective=collective,
                                    packet_bytes=engine.packet_bytes, keyframes_per_rank=n_kf)
 
     if rank == 0 and world == 1 and args.c3:
         out["c3_bruteforce"] = c3_bench(pkg, dev)
+    gate, _ = engine.stats()
+    out["fusion_gate_passed_per_step"] = round(gate / (args.steps + args.warmup + STORE_STEPS), 2)
+    if rank == 0 and world == 1 and args.host_fed_steps > 0:
+        out["host_fed"] = host_fed_block(step, last_handoff, host, streams[0], B, args.host_fed_steps, dev)
+    if rank == 0 and world == 1 and args.cd:
+        torch.cuda.synchronize()
+        kps_l, desc_l, cnt_l = outs[(n_step[0] - 1) % NS]
+        out["covisibility_discovery"] = cd_block(pkg, MA, kps_l, desc_l, cnt_l, vocab, B)
     if rank == 0 and world == 1 and args.host_api_frames > 0:
         out["host_api"] = host_api_rate(pkg, cfg, lefts, rights, args.host_api_frames, dev.index)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -590,8 +786,6 @@ def main():
                                            args.cpu_seconds)
     if skip:
         out["diag_skip"] = sorted(skip)
-    gate, _ = engine.stats()
-    out["fusion_gate_passed_per_step"] = round(gate / (args.steps + args.warmup + STORE_STEPS), 2)
     engine.check()
     if rank == 0:
         print(json.dumps(out), flush=True)

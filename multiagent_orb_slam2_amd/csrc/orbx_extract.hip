@@ -1096,6 +1096,266 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
     FBP(5);
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_fast_rows: FAST-9 scores, cell-masked strict 3x3 NMS at iniThFAST and minThFAST, and row-major candidate slots for
+// one cell row of up to 8 cells (<= 248 detection columns) per WAVE, with the image held in registers.
+//
+// Lane l owns the 4 level columns X .. X+3, X = first detection column - 4 + 4l (lanes 0 and 63 are the +-3 halo;
+// ComputeKeyPointsOctTree's cell ROI is the detection window + 3, :789-806).  The wave walks the group's ROI rows
+// once, top to bottom.  Each row is one 4-byte load per lane; its left / right neighbours' bytes come by DPP
+// (wave_shr / wave_shl), and the row is kept as f16-biased pixel pairs (1024 + value: exact differences, gfx950's
+// packed 3-input f16 min / max, as k_fast_band) -- even starts E(-2,0,2,4) and odd starts O(-3,-1,1,3,5) relative to X
+// -- in a ring of 7 rows (the FAST circle spans rows y-3 .. y+3; the ring index is static in the 7-way unrolled loop).
+// Every pixel of the window is scored (OpenCV's cornerScore in closed form, the same arithmetic as fast_score2_f16):
+// no pre-test, no survivor list, no LDS image and no barrier -- the scores of a whole cell row cost less than the
+// compaction they used to avoid.  NMS of row y runs once row y+1 is scored (neighbour columns across lanes by DPP,
+// columns of another cell masked: OpenCV's FAST runs on the cell ROI, :809-816); the kept pixels of both thresholds
+// are ranked in row-major order per cell (wave ballots + a per-cell row base in LDS) and written to the cell's two
+// candidate lists (iniTh -> cand, minTh -> cand2).  The cell's count word says which list DistributeOctTree uses:
+// the iniTh list, or the minTh list when the cell kept nothing at iniTh (:812-816) -- bit 30 set.
+// ---------------------------------------------------------------------------------------------
+constexpr int kCntMinList = 1 << 30;   // cell count word: the cell's candidates are its minTh list (cand2)
+
+__device__ __forceinline__ uint32_t dpp_from_left(uint32_t v) {    // lane l <- lane l-1 (lane 0 <- 0)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t dpp_from_right(uint32_t v) {   // lane l <- lane l+1 (lane 63 <- 0)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+
+// cornerScore of the pixel pair whose 16 circle taps are t[0..15] (circle order of fast_score2) and centre v, all
+// f16-biased pairs; result i16 pair, -1 for "not a corner at any threshold >= 1"
+__device__ __forceinline__ s16x2 fast_score_taps_f16(const uint32_t (&t)[16], uint32_t vc) {
+    const h16x2 v = as_h2(vc);
+    h16x2 d[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = v - as_h2(t[k]);
+    h16x2 a2[8], b2[8], a4[8], b4[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) { a2[m] = hmin(d[2 * m + 1], d[(2 * m + 2) & 15]); b2[m] = hmax(d[2 * m + 1], d[(2 * m + 2) & 15]); }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) { a4[m] = hmin(a2[m], a2[(m + 1) & 7]); b4[m] = hmax(b2[m], b2[(m + 1) & 7]); }
+    h16x2 dk[8], br[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const h16x2 e0 = d[2 * m], e9 = d[(2 * m + 9) & 15];
+        dk[m] = hmin3(a4[m], a4[(m + 2) & 7], hmax(e0, e9));
+        br[m] = hmax3(b4[m], b4[(m + 2) & 7], hmin(e0, e9));
+    }
+    const h16x2 dmax = hmax3(hmax3(dk[0], dk[1], dk[2]), hmax3(dk[3], dk[4], dk[5]), hmax(dk[6], dk[7]));
+    const h16x2 bmin = hmin3(hmin3(br[0], br[1], br[2]), hmin3(br[3], br[4], br[5]), hmin(br[6], br[7]));
+    const h16x2 zero = {(_Float16)0, (_Float16)0}, bias = {(_Float16)1024, (_Float16)1024};
+    const h16x2 m = hmax3(dmax, -bmin, zero) + bias;
+    return as_s2(__builtin_bit_cast(uint32_t, m)) - (s16x2){0x6401, 0x6401};
+}
+
+struct FastRowSc {            // one scored row, as the NMS reads it: (x,x+1), (x+2,x+3), (x-1,x), (x+1,x+2), (x+3,x+4)
+    uint32_t s0, s1, l0, mid, r1;
+};
+
+__device__ __forceinline__ uint32_t pmax_u(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, pmax(as_s2(a), as_s2(b)));
+}
+
+template <int kDummy>
+__global__ __launch_bounds__(256) void k_fast_rows(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                   const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
+                                                   const BandDev* __restrict__ groups, int g0, int ngroup, int iniTh,
+                                                   int minTh, uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
+                                                   uint32_t* __restrict__ cand2_xy, uint8_t* __restrict__ cand2_s,
+                                                   int cand_stride, int* __restrict__ cell_cnt, int ncells, int batch, Src0 s0) {
+    const int wv = threadIdx.x >> 6, ln = lane_id();
+    const int nitems = ngroup * batch;
+    const int item = xcd_item(xcd_chunk((nitems + 3) / 4)) * 4 + wv;
+    if (item >= nitems) return;                                   // whole wave (no block barriers below)
+    const int img = item / ngroup;
+    const BandDev g = groups[g0 + (item - img * ngroup)];
+    const int nc = g.ncell, wc = g.wcell;
+    const int DW = g.W - 6, H = g.H;
+    const int D0 = g.x0 + 3;                                      // first detection column
+    if (DW <= 0 || H - 6 <= 0) {                                  // no detection window: empty cells
+        if (ln < nc) cell_cnt[(size_t)img * ncells + g.cell0 + ln] = 0;
+        return;
+    }
+    const LevelDev L = levels[g.level];
+    int lstride;
+    const uint8_t* base = level_pixels(pyr, pyr_stride, L, g.level, img, s0, lstride);
+    const int X = D0 - 4 + 4 * ln;                                // this lane's first column
+    const bool ld_ok = X + 3 < L.w;
+    const uint8_t* src = base + (size_t)g.y0 * lstride + X;
+    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
+    const uint32_t t1p = (uint32_t)(T1 & 0xffff) * 0x10001u, t2p = (uint32_t)(T2 & 0xffff) * 0x10001u;
+    // per pixel k of the lane: detection column?  cell index, left / right neighbour in the same cell?
+    uint32_t det_mask[2], mL[2], mR[2];                           // 0xffff halves = "force -1"
+    int cidx[4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) { det_mask[j] = 0; mL[j] = 0; mR[j] = 0; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int rel = X + k - D0;
+        const bool det = rel >= 0 && rel < DW;
+        const int c = det ? min(rel / wc, nc - 1) : 0;
+        cidx[k] = c;
+        const bool lin = det && rel % wc != 0;                    // column x-1 in the same cell's window
+        const bool rin = det && rel + 1 < DW && (rel + 1) % wc != 0;
+        const uint32_t half = 0xffffu << (16 * (k & 1));
+        if (!det) det_mask[k >> 1] |= half;
+        if (!lin) mL[k >> 1] |= half;
+        if (!rin) mR[k >> 1] |= half;
+    }
+    // The lane's pixels lie in at most two cells: ca = the cell of its first pixel and ca + 1 (every cell but a row's
+    // last is wCell >= 30 columns wide).  A cell's row base (kept pixels of the row before its first column) is published by the lane holding
+    // that column (my_off = its offset in the lane) and fetched by ds_bpermute; each lane tracks the running kept
+    // counts of ca and ca + 1 itself (every lane of a cell computes the same numbers), so ranking needs no LDS.
+    const int ca = cidx[0] < nc ? cidx[0] : 0;
+    int my_off = -1;                                              // offset of a cell's first column in this lane
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+        const int rel = X + k - D0;
+        if (rel >= 0 && rel < DW && rel % wc == 0) my_off = k;
+    }
+    auto start_lane = [&](int c) { return 1 + (c * wc) / 4; };   // lane holding cell c's first column
+    const bool hasB = ca + 1 < nc, hasC = ca + 2 < nc;
+    const int addrA = 4 * start_lane(ca), addrB = 4 * start_lane(hasB ? ca + 1 : ca), addrC = 4 * start_lane(hasC ? ca + 2 : ca);
+    const CellDev cellA = cells[g.cell0 + ca], cellB = cells[g.cell0 + (hasB ? ca + 1 : ca)];
+    int cntA[2] = {0, 0}, cntB[2] = {0, 0};                      // kept pixels of cells ca / ca + 1 in earlier rows
+    const uint64_t below = (1ull << ln) - 1ull;
+    uint32_t* cxy[2] = {cand_xy + (size_t)img * cand_stride, cand2_xy + (size_t)img * cand_stride};
+    uint8_t* cs[2] = {cand_s + (size_t)img * cand_stride, cand2_s + (size_t)img * cand_stride};
+
+    // rank and store the kept pixels of one row (bits k of kb[t]: pixel X + k kept at threshold t)
+    auto emit = [&](int row, const int (&kb)[2], uint32_t sc0, uint32_t sc1) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int n = __builtin_popcount(kb[t]);
+            const uint64_t b0 = __ballot(n & 1), b1 = __ballot(n & 2), b2 = __ballot(n & 4);
+            const int tot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+            if (tot == 0) continue;                              // wave-uniform
+            const int pre = __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
+            const int pub = pre + __builtin_popcount(kb[t] & ((1u << (my_off & 3)) - 1u));   // row base if a cell starts here
+            // every lane takes part in every bpermute (a source lane must be active), then selects
+            const int rbA = __builtin_amdgcn_ds_bpermute(addrA, pub);
+            const int pB = __builtin_amdgcn_ds_bpermute(addrB, pub);
+            const int pC = __builtin_amdgcn_ds_bpermute(addrC, pub);
+            const int rbB = hasB ? pB : tot, rbC = hasC ? pC : tot;
+            int m = kb[t];
+            while (m) {
+                const int k = __builtin_ctz(m);
+                m &= m - 1;
+                const bool inA = cidx[k] == ca;
+                const int q = pre + __builtin_popcount(kb[t] & ((1u << k) - 1u));
+                const int rank = inA ? cntA[t] + q - rbA : cntB[t] + q - rbB;
+                const CellDev& cd = inA ? cellA : cellB;
+                if (rank < cd.slot_cap) {
+                    const size_t o = (size_t)cd.slot_off + rank;
+                    cxy[t][o] = (uint32_t)(X + k) | ((uint32_t)(g.y0 + row) << 16);
+                    const uint32_t sw = (k >> 1) ? sc1 : sc0;
+                    cs[t][o] = (uint8_t)(sw >> (16 * (k & 1)));
+                }
+            }
+            cntA[t] += rbB - rbA;
+            cntB[t] += rbC - rbB;
+        }
+    };
+    int dbg_acc = 0;
+    // strict 3x3 NMS of row c (scores of rows c-1, c, c+1) at both thresholds
+    auto nms = [&](int row, const FastRowSc& U, const FastRowSc& C, const FastRowSc& D) {
+        const uint32_t lm0 = pmax_u(pmax_u(U.l0, C.l0), D.l0) | mL[0];
+        const uint32_t mm = pmax_u(pmax_u(U.mid, C.mid), D.mid);
+        const uint32_t rm1 = pmax_u(pmax_u(U.r1, C.r1), D.r1) | mR[1];
+        const uint32_t m0 = pmax_u(pmax_u(lm0, pmax_u(U.s0, D.s0)), mm | mR[0]);
+        const uint32_t m1 = pmax_u(pmax_u(mm | mL[1], pmax_u(U.s1, D.s1)), rm1);
+        // kept at t: s > m (m - s < 0) and s >= T (s - T >= 0): sign bits
+        const uint32_t g0 = __builtin_bit_cast(uint32_t, as_s2(m0) - as_s2(C.s0));
+        const uint32_t g1 = __builtin_bit_cast(uint32_t, as_s2(m1) - as_s2(C.s1));
+        int kb[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const uint32_t tp = t ? t2p : t1p;
+            const uint32_t a0 = g0 & ~__builtin_bit_cast(uint32_t, as_s2(C.s0) - as_s2(tp));
+            const uint32_t a1 = g1 & ~__builtin_bit_cast(uint32_t, as_s2(C.s1) - as_s2(tp));
+            kb[t] = (int)(((a0 >> 15) & 1u) | ((a0 >> 30) & 2u) | ((a1 >> 13) & 4u) | ((a1 >> 28) & 8u));
+        }
+        if (__ballot((kb[0] | kb[1]) != 0) == 0) return;         // wave-uniform
+#ifdef ORBX_ROWS_NOEMIT
+        dbg_acc += kb[0] * 3 + kb[1] + row;                       // diagnostics: scores and NMS only (kept observable)
+#else
+        emit(row, kb, C.s0, C.s1);
+#endif
+    };
+
+    const uint32_t K64 = 0x64646464u;
+    uint32_t E[7][4], O[7][5], raw[7];
+#ifndef ORBX_ROWS_PF
+#define ORBX_ROWS_PF 3
+#endif
+    constexpr int kPf = ORBX_ROWS_PF;                             // rows loaded ahead (<= 6)
+#pragma unroll
+    for (int p = 0; p < kPf; ++p) raw[p] = (p < H && ld_ok) ? *reinterpret_cast<const uint32_t*>(src + (size_t)p * lstride) : 0u;
+    const FastRowSc none{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    FastRowSc sa = none, sb = none;                               // scores of rows r-5, r-4 (the NMS window)
+    for (int r0 = 0; r0 < H; r0 += 7) {
+#pragma unroll
+        for (int p = 0; p < 7; ++p) {
+            const int r = r0 + p;
+            if (r >= H) break;                                    // wave-uniform
+            if (r + kPf < H) raw[(p + kPf) % 7] = ld_ok ? *reinterpret_cast<const uint32_t*>(src + (size_t)(r + kPf) * lstride) : 0u;
+            // row r -> slot p: E(-2), E(0), E(2), E(4); O(-3), O(-1), O(1), O(3), O(5)
+            const uint32_t C = raw[p], Lw = dpp_from_left(C), Rw = dpp_from_right(C);
+            E[p][0] = __builtin_amdgcn_perm(K64, Lw, 0x04030402u);
+            E[p][1] = __builtin_amdgcn_perm(K64, C, 0x04010400u);
+            E[p][2] = __builtin_amdgcn_perm(K64, C, 0x04030402u);
+            E[p][3] = __builtin_amdgcn_perm(K64, Rw, 0x04010400u);
+            O[p][0] = __builtin_amdgcn_perm(K64, Lw, 0x04020401u);
+            O[p][1] = __builtin_amdgcn_alignbit(E[p][1], E[p][0], 16);
+            O[p][2] = __builtin_amdgcn_perm(K64, C, 0x04020401u);
+            O[p][3] = __builtin_amdgcn_alignbit(E[p][3], E[p][2], 16);
+            O[p][4] = __builtin_amdgcn_perm(K64, Rw, 0x04020401u);
+            if (r < 6) continue;                                  // wave-uniform
+            // score row r-3: circle taps (dx, dy) at rows (p + dy) mod 7 (row r-3+dy), pair start 2j + dx
+            FastRowSc sc;
+            s16x2 sp[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                // tap (dx, dy): start s = 2j + dx in [-3, 5]; even -> E[(s + 2) / 2], odd -> O[(s + 3) / 2]
+#define ORBX_RT(dx, dy) ((((2 * j + (dx)) & 1) != 0) ? O[(p + 4 + (dy)) % 7][(2 * j + (dx) + 3) / 2] \
+                                                   : E[(p + 4 + (dy)) % 7][(2 * j + (dx) + 2) / 2])
+                const uint32_t t[16] = {ORBX_RT(0, 3),  ORBX_RT(1, 3),   ORBX_RT(2, 2),   ORBX_RT(3, 1),
+                                        ORBX_RT(3, 0),  ORBX_RT(3, -1),  ORBX_RT(2, -2),  ORBX_RT(1, -3),
+                                        ORBX_RT(0, -3), ORBX_RT(-1, -3), ORBX_RT(-2, -2), ORBX_RT(-3, -1),
+                                        ORBX_RT(-3, 0), ORBX_RT(-3, 1),  ORBX_RT(-2, 2),  ORBX_RT(-1, 3)};
+                sp[j] = fast_score_taps_f16(t, ORBX_RT(0, 0));
+#undef ORBX_RT
+            }
+            sc.s0 = __builtin_bit_cast(uint32_t, sp[0]) | det_mask[0];
+            sc.s1 = __builtin_bit_cast(uint32_t, sp[1]) | det_mask[1];
+            sc.l0 = __builtin_amdgcn_alignbit(sc.s0, dpp_from_left(sc.s1), 16);
+            sc.mid = __builtin_amdgcn_alignbit(sc.s1, sc.s0, 16);
+            sc.r1 = __builtin_amdgcn_alignbit(dpp_from_right(sc.s0), sc.s1, 16);
+#ifdef ORBX_ROWS_SCOREONLY
+            dbg_acc += (int)(sc.s0 ^ sc.s1 ^ sc.l0 ^ sc.mid ^ sc.r1);
+#else
+            if (r - 3 >= 4) nms(r - 4, sa, sb, sc);
+#endif
+            sa = sb;
+            sb = sc;
+        }
+    }
+    if (H - 4 >= 3) nms(H - 4, sa, sb, none);                     // last detection row: nothing below
+#if defined(ORBX_ROWS_NOEMIT) || defined(ORBX_ROWS_SCOREONLY)
+    if (dbg_acc == 0x7fffffff) cand_s[0] = 1;
+#endif
+    // per cell (written by the lane holding its first column): the iniTh list, or the minTh list when the cell kept
+    // nothing at iniTh
+    if (my_off >= 0) {
+        const bool a = cidx[my_off] == ca;
+        const int ci = a ? cntA[0] : cntB[0], cm = a ? cntA[1] : cntB[1];
+        const int use_min = ci == 0;
+        const int n = min(use_min ? cm : ci, (a ? cellA : cellB).slot_cap);
+        cell_cnt[(size_t)img * ncells + g.cell0 + cidx[my_off]] = n | (use_min && n > 0 ? kCntMinList : 0);
+    }
+}
+
 // GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, integer separable path: taps {18,34,49,55,49,34,18},
 // column pass (acc + 2^15) >> 16 saturated.  Tile 64 x 16 per workgroup; tiles of all levels in one grid.
 struct BlurTile { int level, tx, ty, pad; };
@@ -1340,6 +1600,7 @@ __device__ unsigned long long g_qtprof[2][64];
 
 __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
                                                          const uint32_t* __restrict__ cand_xy, const uint8_t* __restrict__ cand_s,
+                                                         const uint32_t* __restrict__ cand2_xy, const uint8_t* __restrict__ cand2_s,
                                                          int cand_stride, const int* __restrict__ cell_cnt, int ncells,
                                                          QtScratch qs, uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r,
                                                          int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
@@ -1373,8 +1634,9 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
     // ---- 1. compact the level's cell candidates into reference order (cell row-major, then FAST order)
     // (per cell: count -> sa, slot offset -> sb; all loads independent)
     for (int i = tid; i < ncl; i += T) {
-        sa[i] = cell_cnt[(size_t)img * ncells + L.cell_begin + i];
-        sb[i] = cells[L.cell_begin + i].slot_off;
+        const int cw = cell_cnt[(size_t)img * ncells + L.cell_begin + i];
+        sa[i] = cw & ~kCntMinList;
+        sb[i] = cells[L.cell_begin + i].slot_off | (cw & kCntMinList ? (int)0x80000000u : 0);   // list: iniTh / minTh
     }
     __syncthreads();
     const int K = block_scan_array(sa, ncl, tmp);
@@ -1400,8 +1662,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
     }
     __syncthreads();
     {
-        const uint32_t* sxy = cand_xy + (size_t)img * cand_stride;
-        const uint8_t* ss = cand_s + (size_t)img * cand_stride;
+        const size_t io = (size_t)img * cand_stride;
         constexpr int U = 4;
         for (int k0 = tid; k0 < K; k0 += U * T) {
             uint32_t xy[U];
@@ -1411,9 +1672,10 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                 const int k = k0 + u * T;
                 if (k < K) {
                     const int c = kn[k];
-                    const int src = sb[c] + (k - sa[c]);
-                    xy[u] = sxy[src];
-                    r[u] = ss[src];
+                    const int sbc = sb[c];
+                    const size_t src = io + (size_t)(sbc & 0x7fffffff) + (k - sa[c]);
+                    xy[u] = sbc < 0 ? cand2_xy[src] : cand_xy[src];
+                    r[u] = sbc < 0 ? cand2_s[src] : cand_s[src];
                 }
             }
 #pragma unroll
@@ -1738,17 +2000,15 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
     const LevelDev L = levels[lvl];
     const int i = slot - L.out_off;
     const int* lcs = level_cnt + img * nlevels;
-    int off = 0, total = 0, ci = 0;
-    bool stale = false;
-    for (int l = 0; l < nlevels; ++l) {
-        const int c = lcs[l] & 0xffff;
-        stale |= (l <= lvl || write_count) && lvl_stale(lcs[l], seq);   // only the levels this launch reads
-        off += l < lvl ? c : 0;
-        ci = l == lvl ? c : ci;
-        total += c;
+    int off = 0;
+    for (int l = 0; l < lvl; ++l) off += lcs[l] & 0xffff;
+    if (write_count && rel == 0 && ln == 0) {
+        int total = 0;
+        for (int l = 0; l < nlevels; ++l) total += lcs[l] & 0xffff;
+        counts[img] = min(total, capacity);
     }
-    if (__ballot(stale) && ln == 0) atomicOr(err, kErrStale);
-    if (write_count && rel == 0 && ln == 0) counts[img] = min(total, capacity);
+    const int craw = lcs[lvl], ci = craw & 0xffff;
+    if (lvl_stale(craw, seq) && ln == 0) atomicOr(err, kErrStale);   // this call's stamp on the level read
     if (i >= ci) return;
     const int o = off + i;
     if (o >= capacity) return;
@@ -1903,16 +2163,15 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
 #pragma unroll
     for (int l = 1; l < kMaxLevels; ++l) lvl += (l < nlevels && slot >= tab.out_off[l]) ? 1 : 0;
     const int* lcs = level_cnt + img * nlevels;
-    int off = 0, total = 0, ci = 0;
-    bool stale = false;
+    int off = 0, total = 0;
     for (int l = 0; l < nlevels; ++l) {
         const int c = lcs[l] & 0xffff;
-        stale |= (l <= lvl || write_count) && lvl_stale(lcs[l], seq);   // only the levels this launch reads
         off += l < lvl ? c : 0;
-        ci = l == lvl ? c : ci;
         total += c;
     }
-    if (__ballot(stale) && ln == 0) atomicOr(err, kErrStale);
+    const int craw = lcs[lvl], ci = craw & 0xffff;
+    // the level this lane reads must carry this call's stamp
+    if (__ballot(lvl_stale(craw, seq)) && ln == 0) atomicOr(err, kErrStale);
     if (write_count && wrel == 0 && ln == 0) counts[img] = min(total, capacity);
     const LevelDev& L = levels[lvl];
     const int lw = L.w, lpo = L.pyr_off, loo = L.out_off;
@@ -2115,6 +2374,13 @@ struct Extractor {
     std::vector<BandDev> bandv;
     BandDev* d_bands = nullptr;
     int fast_band = 1;
+    // k_fast_rows (default; ORBX_FAST_ROWS=0 selects k_fast_band): one wave per group of <= 8 cells of one cell row
+    // (<= 248 detection columns); level 0 / levels >= 1 as the two launches above
+    struct RowsLaunch { int g0, n; };
+    RowsLaunch rows_launch[2] = {};
+    std::vector<BandDev> rowgv;
+    BandDev* d_rowg = nullptr;
+    int fast_rows = 0;   // (default off until it measures faster than k_fast_band in the full step)
     int band_g = 4;
     int fast_oe = 1;          // ORBX_FAST_OE: E-only pair image (O taps by v_alignbit), 0 = E and O images
     int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
@@ -2140,6 +2406,8 @@ struct Extractor {
     uint8_t* d_blur = nullptr;
     uint32_t* d_cand_xy = nullptr;
     uint8_t* d_cand_s = nullptr;
+    uint32_t* d_cand2_xy = nullptr;   // k_fast_rows: the cells' minTh lists (the iniTh lists are d_cand_*)
+    uint8_t* d_cand2_s = nullptr;
     int* d_cell_cnt = nullptr;
     uint32_t* d_key_xy = nullptr;
     uint8_t* d_key_r = nullptr;
@@ -2233,7 +2501,8 @@ static void level_dims(const Extractor* e, int rows, int cols, int l, int* w, in
 
 void Extractor::free_buffers() {
     auto F = [](auto*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } };
-    F(d_levels); F(d_cells); F(d_tiles); F(d_bands); F(d_tail); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
+    F(d_levels); F(d_cells); F(d_tiles); F(d_bands); F(d_rowg); F(d_tail); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s);
+    F(d_cand2_xy); F(d_cand2_s); F(d_cell_cnt);
     F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
     F(d_kps); F(d_desc); F(d_cnt);
     if (h_in) { (void)hipHostFree(h_in); h_in = nullptr; }
@@ -2401,6 +2670,29 @@ int Extractor::configure(int r, int c, int batch) {
             ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_band<72, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b.lay.bytes));
         }
     }
+    // k_fast_rows groups: runs of consecutive cells of one cell row (same level and iniY, abutting), <= 8 cells and
+    // <= 248 detection columns (lanes 1..62 of a wave; lanes 0 and 63 hold the +-3 halo)
+    rowgv.clear();
+    for (int k = 0; k < 2; ++k) {
+        RowsLaunch& rl = rows_launch[k];
+        rl.g0 = (int)rowgv.size();
+        const FastLaunch& f = fast_launch[k];
+        for (int i = f.cell0; i < f.cell0 + f.n;) {
+            const CellDev& c0 = cellv[i];
+            const int wc = c0.W - 6;
+            int n = 1;
+            while (n < 8 && i + n < f.cell0 + f.n && cellv[i + n].level == c0.level && cellv[i + n].y0 == c0.y0 &&
+                   cellv[i + n].x0 == c0.x0 + n * wc && cellv[i + n - 1].W == wc + 6 &&
+                   cellv[i + n].x0 + cellv[i + n].W - c0.x0 - 6 <= 248)
+                ++n;
+            const CellDev& cl = cellv[i + n - 1];
+            BandDev gd{c0.level, i, n, c0.x0, c0.y0, cl.x0 + cl.W - c0.x0, c0.H, std::max(wc, 1)};
+            ORBX_REQUIRE(gd.W - 6 <= 248 && gd.H <= 1024, ORBX_ERR_UNSUPPORTED, "FAST row group too large");
+            rowgv.push_back(gd);
+            i += n;
+        }
+        rl.n = (int)rowgv.size() - rl.g0;
+    }
     int scap = cap;
     for (const LevelDev& L : lv) scap = std::max(scap, std::max(L.cell_end - L.cell_begin, L.nIni));
     scan_cap = scap + 1;
@@ -2442,6 +2734,8 @@ int Extractor::configure(int r, int c, int batch) {
     ORBX_HIP(hipMemcpy(d_tiles, tilev.data(), sizeof(BlurTile) * tilev.size(), hipMemcpyHostToDevice));
     if ((st = dev_alloc(&d_bands, bandv.size()))) return st;
     if (!bandv.empty()) ORBX_HIP(hipMemcpy(d_bands, bandv.data(), sizeof(BandDev) * bandv.size(), hipMemcpyHostToDevice));
+    if ((st = dev_alloc(&d_rowg, rowgv.size()))) return st;
+    if (!rowgv.empty()) ORBX_HIP(hipMemcpy(d_rowg, rowgv.data(), sizeof(BandDev) * rowgv.size(), hipMemcpyHostToDevice));
 
     // ---- resize tables (pinned OpenCV 3.2 INTER_LINEAR fixed point), level l from level l-1
     rtab.assign(nlevels, ResizeTab{});
@@ -2548,6 +2842,8 @@ int Extractor::configure(int r, int c, int batch) {
     if ((st = dev_alloc(&d_blur, B * pyr_size))) return st;
     if ((st = dev_alloc(&d_cand_xy, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_cand_s, B * cand_stride))) return st;
+    if ((st = dev_alloc(&d_cand2_xy, B * cand_stride))) return st;
+    if ((st = dev_alloc(&d_cand2_s, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_cell_cnt, B * std::max<size_t>(cellv.size(), 1)))) return st;
     if ((st = dev_alloc(&d_key_xy, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_key_r, B * cand_stride))) return st;
@@ -2616,6 +2912,14 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
     auto fast = [&](hipStream_t q, const Extractor::FastLaunch& f) {
         if (f.n <= 0) return;
+        if (e->fast_rows && !e->fast_stop_after) {
+            const Extractor::RowsLaunch& rl = e->rows_launch[&f == &e->fast_launch[0] ? 0 : 1];
+            if (rl.n <= 0) return;
+            hipLaunchKernelGGL(k_fast_rows<0>, dim3(kXcds * xcd_chunk((rl.n * batch + 3) / 4)), dim3(256), 0, q, e->d_pyr, ps,
+                               e->d_levels, e->d_cells, e->d_rowg, rl.g0, rl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s,
+                               e->d_cand2_xy, e->d_cand2_s, e->cand_stride, e->d_cell_cnt, ncells, batch, s0);
+            return;
+        }
         if (e->fast_band && !e->fast_stop_after) {
             const Extractor::BandLaunch& b = e->band_launch[&f == &e->fast_launch[0] ? 0 : 1];
             auto kb = e->fast_oe ? k_fast_band<72, true> : k_fast_band<72, false>;
@@ -2635,7 +2939,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         // else the levels >= 1 region
         const int kc = lvl0 == 0 ? e->qt_keys[0] : e->qt_keys[1];
         hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds + 6 * (size_t)kc, q, e->d_levels, e->d_cells,
-                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
+                           e->d_cand_xy, e->d_cand_s, e->d_cand2_xy, e->d_cand2_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
                            e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err, lvl0,
                            (int)e->qt_lds, kc, seq);
     };
@@ -2851,6 +3155,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* ab = std::getenv("ORBX_FAST_ABLATE")) e->fast_stop_after = std::atoi(ab);
     if (const char* pl = std::getenv("ORBX_PIPELINE")) e->pipeline = std::atoi(pl) != 0;
     if (const char* fb = std::getenv("ORBX_FAST_BAND")) e->fast_band = std::atoi(fb) != 0;
+    if (const char* fr = std::getenv("ORBX_FAST_ROWS")) e->fast_rows = std::atoi(fr) != 0;
     if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
     if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;
     if (const char* ds = std::getenv("ORBX_DESC_SPLIT")) e->desc_split = std::atoi(ds) != 0;

@@ -428,3 +428,50 @@ class KeyframeFusion:
         """Raise if any detect so far reported interacting queries or exceeded capacity (synchronises)."""
         from .orbx import KeyFrameDatabase
         KeyFrameDatabase.check_status(self.status)
+
+
+class CovisibilityDiscovery:
+    """MapFusion::CovisibilityDiscovery's detection and matching (src/MapFusion.cc:774-885) over device keyframes.
+
+    For every keyframe of the absorbed map (query slots, processed in order as the reference's loop does): minScore =
+    the smallest ORBVocabulary::score against its covisible keyframes, starting at 1 and kept in a float (:801-816);
+    DetectCovisibilityCandidates(KF, minScore, vpCurrentMapKFs) on the matched map's database (:819-820, the whole
+    absorbed map ignored); SearchByBoW(KF, candidate) with ORBmatcher(0.75, true) for every candidate (:840-856), a
+    candidate kept with >= 15 matches.  The queries use fresh keyframe ids and the COVIS scratch fields only, so the
+    batch equals the sequential loop (the database reports any interaction in its status word).  The Fuse step that
+    follows (:903-910: projection search and map edits on the CPU's map) is outside the hot path.
+
+    db: KeyFrameDatabase holding the matched map's keyframes as members; store: orbx_kf_store (KfStore) over every
+    slot (both maps); matcher: ORBmatcher(0.75, True).  Runs on the current torch stream."""
+
+    def __init__(self, matcher, db, store, max_fv_nodes: int, min_matches: int = 15):
+        self.matcher, self.db, self.store = matcher, db, store
+        self.max_fv_nodes, self.min_matches = max_fv_nodes, min_matches
+
+    def run(self, query_slots, query_ids, covisible, ignore):
+        """query_slots / query_ids: the absorbed map's keyframes (lists); covisible[i]: slots of query i's covisible
+        keyframes (GetVectorCovisibleKeyFrames); ignore: vpCurrentMapKFs.  Returns (pairs (P, 2), match12 (P, cap),
+        nmatches (P,), passed (P,)) device tensors and the per-query candidate counts (host; one synchronisation)."""
+        import torch
+
+        from .orbx import KFDB_COVIS, KeyFrameDatabase
+        dev = self.store._keep[0].device
+        nq = len(query_slots)
+        q = torch.tensor(query_slots, dtype=torch.int32, device=dev)
+        ids = torch.tensor(query_ids, dtype=torch.int64, device=dev)
+        ms = torch.ones((nq,), dtype=torch.float32, device=dev)          # float minScore = 1 (:805)
+        sp = [(query_slots[i], c) for i in range(nq) for c in covisible[i]]
+        if sp:
+            sc = self.db.score_device(torch.tensor(sp, dtype=torch.int32, device=dev))
+            owner = torch.tensor([i for i in range(nq) for _ in covisible[i]], dtype=torch.int64, device=dev)
+            ms.scatter_reduce_(0, owner, sc.to(torch.float32), reduce="amin", include_self=True)
+        n_ign = len(ignore)
+        excl_slots = torch.tensor(list(ignore) * nq if n_ign else [0], dtype=torch.int32, device=dev)
+        excl_off = torch.arange(0, nq + 1, dtype=torch.int32, device=dev) * n_ign
+        cand, n_cand, status = self.db.detect_device(KFDB_COVIS, q, ids, ms, excl_off, excl_slots)
+        n_host = n_cand.cpu().numpy()
+        KeyFrameDatabase.check_status(status)
+        k = max(1, int(n_host.max()) if nq else 1)
+        pr = KeyFrameDatabase.candidate_pairs_device(cand, n_cand, q, k)
+        m12, nm = self.matcher.SearchByBoW_pairs_device(self.store, pr, self.max_fv_nodes)
+        return pr, m12, nm, nm >= self.min_matches, n_host

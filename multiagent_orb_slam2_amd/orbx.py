@@ -950,6 +950,14 @@ class KeyFrameDatabase:
             raise ValueError("state arrays must hold max_slots entries")
         _check(self._lib.orbx_kfdb_set_state(self._h, kind, _p(q), _p(w), _p(sc)))
 
+    def score_device(self, pairs, out=None, stream=None):
+        """ORBVocabulary::score for (P, 2) int32 device slot pairs; (P,) float64 device tensor."""
+        import torch
+        out = out if out is not None else torch.empty((pairs.shape[0],), dtype=torch.float64, device=pairs.device)
+        _check(self._lib.orbx_kfdb_score_device(self._h, _tp(pairs), pairs.shape[0], _tp(out),
+                                                _stream_ptr(stream, pairs.device)))
+        return out
+
     def score(self, pairs) -> np.ndarray:
         """ORBVocabulary::score(bow[a], bow[b]) for (a, b) slot pairs (DBoW2 L1)."""
         pr = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel SQ counter summary of a scripts/prof_sq.sh run (kernel trace + two --pmc passes).
 
-usage: scripts/sq_summary.py gpurun_out/<TAG> <out.json> [config batch_images]
+usage: scripts/sq_summary.py gpurun_out/<TAG> <out.json> [config batch_images steps_traced]
 
 Derived per kernel (averages per dispatch):
   valu_lane_ops      = SQ_INSTS_VALU * 64 (wave instructions x lanes; an upper bound: exec-masked lanes count)
@@ -69,7 +69,13 @@ def main():
             e["lds_conflict_frac"] = round(d.get("SQ_LDS_BANK_CONFLICT", 0) / (d["SQ_ACTIVE_INST_LDS"] * 4), 4)
         res[k] = e
     tag = base.rstrip("/").split("/")[-1]
-    meta = {"tag": tag, "config": sys.argv[3] if len(sys.argv) > 3 else "kitti",
+    steps = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    if steps:
+        for k, e in res.items():
+            e["launches_per_step"] = round(e["calls"] / steps, 3)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from kernel_share import source_sha16
+    meta = {"tag": tag, "config": sys.argv[3] if len(sys.argv) > 3 else "kitti", "source_sha16": source_sha16(),
             "batch_images": int(sys.argv[4]) if len(sys.argv) > 4 else 128,
             "note": "per-dispatch averages of a short bench run (scripts/prof_sq.sh); SQ_* wave counters summed over "
                     "the chip by rocprofv3; valu_lane_ops = SQ_INSTS_VALU x 64"}

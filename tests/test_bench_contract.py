@@ -33,7 +33,7 @@ def test_defaults_and_compulsory_bytes(monkeypatch):
 def test_bench_json_line(gpu, capsys, monkeypatch):
     b = _bench()
     monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "2", "--warmup", "3", "--batch", "16", "--cpu-seconds", "0",
-                                      "--host-api-frames", "0", "--no-c3"])
+                                      "--host-api-frames", "0", "--no-c3", "--host-fed-steps", "2"])
     import torch
     prev = torch.cuda.current_stream()
     try:
@@ -49,6 +49,12 @@ def test_bench_json_line(gpu, capsys, monkeypatch):
     assert d["unit"] == "frames/s" and d["scaling"] == "weak" and d["vs_baseline"] is None and d["dtype"] == "u8"
     assert d["value"] > 0 and abs(d["value"] - 16 * 1000.0 / d["ms_per_step"]) / d["value"] < 0.01
     r = d["roofline"]
-    assert r["algorithmic_bytes_per_launch"] == 585750 * 32 and r["units_per_launch"] == 32
+    assert r["algorithmic_bytes_per_step"] == 585750 * 32 and r["units_per_step"] == 32
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-4
+    # achieved = algorithmic bytes per step / the kernel's live time per step (its launches' event spans summed)
+    assert abs(r["achieved"] - r["algorithmic_bytes_per_step"] / (r["kernel_ms_per_step"] * 1e-3) / 1e9) / r["achieved"] < 1e-3
+    assert r["kernel"].startswith("k_fast_band") and r["launches_per_step"] == 2
+    assert d["host_fed"]["frames_per_s"] > 0 and d["host_fed"]["input_bytes_per_step"] == 32 * 375 * 1242
+    cd = d["covisibility_discovery"]
+    assert cd["absorbed_keyframes"] == 16 and cd["searchbybow_pairs"] >= 1
     assert d["config"]["frames_per_gpu_per_step"] == 16 and d["config"]["keyframes_per_gpu_per_step"] == 3

@@ -171,3 +171,29 @@ def test_describe_keypoints_per_wave(gpu, monkeypatch, kpw):
             kb, desc[i, :n], ref["kps"], ref["desc"])
     # odd feature budget and level count: level slot ranges of odd lengths
     _check(S.kitti_like_image(410, rows=240, cols=333), nfeatures=777, nlevels=5, scale=1.3)
+
+
+@pytest.mark.parametrize("rows", [0, 1])
+def test_fast_kernels_bit_exact(gpu, monkeypatch, rows):
+    """Both FAST forms -- k_fast_band (LDS band image, pre-test and survivor list) and k_fast_rows (one wave per cell
+    row in registers, every pixel scored, both thresholds' lists) -- are bit-exact against the oracle: KITTI size,
+    odd sizes and another parameter set, batched."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    monkeypatch.setenv("ORBX_FAST_ROWS", str(rows))
+    for shape, nf, kw in (((375, 1242), 2000, {}), ((377, 1243), 800, {}), ((120, 160), 300, {}),
+                          ((480, 752), 1500, dict(nlevels=5, scale=1.3, ini=25, mn=10))):
+        imgs = np.stack([S.kitti_like_image(900 + i, rows=shape[0], cols=shape[1]) for i in range(3)])
+        ex = pkg.ORBextractor(nf, kw.get("scale", 1.2), kw.get("nlevels", 8), kw.get("ini", 20), kw.get("mn", 7))
+        kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).cuda())
+        torch.cuda.synchronize()
+        kps, desc, cnt = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+        for i in range(len(imgs)):
+            ref = O.extract(imgs[i], nfeatures=nf, scale_factor=kw.get("scale", 1.2), nlevels=kw.get("nlevels", 8),
+                            ini_th=kw.get("ini", 20), min_th=kw.get("mn", 7))
+            n = int(cnt[i])
+            kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
+            assert np.array_equal(kb, ref["kps"]) and np.array_equal(desc[i, :n], ref["desc"]), _diff_report(
+                kb, desc[i, :n], ref["kps"], ref["desc"])
