@@ -1377,7 +1377,12 @@ __device__ __forceinline__ int refl101(int i, int n) {
 #ifndef ORBX_BLUR_BAND
 #define ORBX_BLUR_BAND 16     // rows per wave (r2y A/B: 16 ≈ +0.6 % over 32; 8 and 64 slower)
 #endif
-constexpr int kBlurBand = ORBX_BLUR_BAND, kBlurStrip = 256;
+#ifndef ORBX_BLUR_DPP
+#define ORBX_BLUR_DPP 0       // 1: interior strips load one dword per lane and row, neighbours' bytes by DPP (r3l A/B: serial blur 0.476 -> 0.561 ms, slower)
+#endif
+// strip = output columns of one wave: 256 (every lane loads its own 12-byte window), or 248 with the DPP form
+// (lanes 1..62 output, lanes 0 and 63 load the +-4 halo)
+constexpr int kBlurBand = ORBX_BLUR_BAND, kBlurStrip = ORBX_BLUR_DPP ? 248 : 256;
 
 // byte m of the 12-byte window (w0 | w1 << 32 | w2 << 64) and byte m+1, as u16 lanes (lo = m)
 template <int m>
@@ -1399,7 +1404,13 @@ struct BlurWin { uint32_t w0, w1, w2; };   // 12 input bytes x0-4 .. x0+7 of one
 template <int kMode>
 __device__ __forceinline__ BlurWin blur_load(const uint8_t* __restrict__ row, int x0, int w) {
     BlurWin o;
-    if (kMode == 0) {
+    if (kMode == 3) {            // DPP form: every lane active, all loads in bounds (interior strip)
+        uint32_t c;
+        __builtin_memcpy(&c, row + x0, 4);
+        o.w0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x138, 0xF, 0xF, false);   // lane l-1 (wave_shr:1)
+        o.w1 = c;
+        o.w2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x130, 0xF, 0xF, false);   // lane l+1 (wave_shl:1)
+    } else if (kMode == 0) {
         uint32_t v[3];
         __builtin_memcpy(v, row + x0 - 4, 12);
         o.w0 = v[0]; o.w1 = v[1]; o.w2 = v[2];
@@ -1449,7 +1460,7 @@ __device__ __forceinline__ uint32_t blur_col(uint32_t a, uint32_t b, uint32_t c,
 // reflected branch-free (|overhang| <= 3 < h), so loads past the band's end stay in bounds.
 template <int kMode>
 __device__ __forceinline__ void blur_band(const uint8_t* __restrict__ S, int sstride, uint8_t* __restrict__ D,
-                                          const LevelDev& L, int x0, int y0, int y1) {
+                                          const LevelDev& L, int x0, int y0, int y1, bool store_lane = true) {
     const int h = L.h, w = L.w;
     auto row_ptr = [&](int yy) {
         const int r = h >= 4 ? (yy < 0 ? -yy : (yy >= h ? 2 * h - 2 - yy : yy)) : refl101(yy, h);
@@ -1472,7 +1483,9 @@ __device__ __forceinline__ void blur_band(const uint8_t* __restrict__ S, int sst
         const uint32_t o3 = blur_col(a.h23.y, b.h23.y, c.h23.y, d.h23.y, e.h23.y, f.h23.y, g.h23.y);
         const uint32_t packed = o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
         uint8_t* o = D + (size_t)y * w + x0;
-        if (kMode == 0 || full) {
+        if (kMode == 3) {
+            if (store_lane) __builtin_memcpy(o, &packed, 4);
+        } else if (kMode == 0 || full) {
             __builtin_memcpy(o, &packed, 4);
         } else {
 #pragma unroll
@@ -1511,12 +1524,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_W
     const int t = tile0 + tl;
     const BlurTile bt = tiles[t];
     const LevelDev L = levels[bt.level];
-    const int x0 = bt.tx * kBlurStrip + 4 * lane_id();
-    if (x0 >= L.w) return;
     int sstride;
     const uint8_t* S = level_pixels(pyr, pyr_stride, L, bt.level, img, s0, sstride);
     uint8_t* D = blur + img * pyr_stride + L.pyr_off;
     const int y0 = bt.ty * kBlurBand, y1 = min(y0 + kBlurBand, L.h);
+#if ORBX_BLUR_DPP
+    {
+        const int ln = lane_id(), sx = bt.tx * kBlurStrip;
+        const int x0 = sx - 4 + 4 * ln;                           // lanes 1..62 output columns x0 .. x0+3
+        if (sx - 4 >= 0 && sx + 252 <= L.w) {                     // interior strip (wave-uniform): DPP form
+            blur_band<3>(S, sstride, D, L, x0, y0, y1, ln >= 1 && ln <= 62);
+            return;
+        }
+        if (ln == 0 || ln == 63 || x0 >= L.w) return;             // edge strip: per-lane windows
+        const bool interior = (x0 - 4 >= 0) && (x0 + 8 <= L.w);
+        if (__builtin_amdgcn_read_exec() == __ballot(interior))
+            blur_band<0>(S, sstride, D, L, x0, y0, y1);
+        else if (L.w >= 12)
+            blur_band<1>(S, sstride, D, L, x0, y0, y1);
+        else
+            blur_band<2>(S, sstride, D, L, x0, y0, y1);
+        return;
+    }
+#endif
+    const int x0 = bt.tx * kBlurStrip + 4 * lane_id();
+    if (x0 >= L.w) return;
     const bool interior = (x0 - 4 >= 0) && (x0 + 8 <= L.w);
     // wave-uniform choice of the load form (strips touching a level's left/right edge pick reflected bytes)
     if (__builtin_amdgcn_read_exec() == __ballot(interior))
