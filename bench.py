@@ -45,6 +45,7 @@ VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12     # 256 CU x 4 SIMD-32 x 2.4 GHz lan
 NLEV, SCALE, INI, MINTH = 8, 1.2, 20, 7
 KF_EVERY = 5
 KF_CANDIDATES = 16
+TRI_NEIGHBOURS = 10                           # CreateNewMapPoints' neighbours of a stereo keyframe (LocalMapping.cc:216)
 STORE_STEPS = 3                               # keyframe store ring = 3 steps of every agent's keyframes
 # Camera.bf and Camera.fx of the reference's stereo settings (baseline b = bf / fx, Frame.cc mb)
 CONFIGS = {
@@ -86,6 +87,9 @@ def parse():
                          "copy stream, overlapped with the previous step (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-stage event timing")
     ap.add_argument("--no-c3", dest="c3", action="store_false", help="skip the C3 2000x2000 all-pairs block")
+    ap.add_argument("--no-tri", dest="tri", action="store_false",
+                    help="leave CreateNewMapPoints' matching (SearchForTriangulation vs 10 neighbours + distinctive "
+                         "descriptors) out of the keyframe path")
     ap.add_argument("--no-cd", dest="cd", action="store_false", help="skip the CovisibilityDiscovery-shaped block")
     ap.add_argument("--diag-skip", default="", help="diagnostics only (not the metric): comma list of stereo,keyframes "
                                                      "to leave out of the step")
@@ -103,6 +107,24 @@ def compulsory_bytes(cfg):
     img = cfg["rows"] * cfg["cols"]
     n = cfg["nfeatures"]
     return {"extraction": img + n * (28 + 32), "stereo_match": 2 * n * 32 + n * 8}
+
+
+def tri_geometry_rows(cfg):
+    """F12 and epipole rows for a keyframe and its d-th previous keyframe, d = 1..TRI_NEIGHBOURS: a synthetic
+    trajectory of 0.8 m forward and 0.01 rad of yaw per keyframe (baseline > the stereo baseline, so
+    LocalMapping.cc:252-256 keeps every neighbour).  (TRI_NEIGHBOURS, 12) float32 tensor on the CPU."""
+    import torch
+    from multiagent_orb_slam2_amd import multiagent as MA
+    n = TRI_NEIGHBOURS + 1
+    K = torch.tensor([[cfg["fx"], 0, cfg["cols"] / 2], [0, cfg["fx"], cfg["rows"] / 2], [0, 0, 1]], dtype=torch.float64)
+    yaw = 0.01 * torch.arange(n, dtype=torch.float64)
+    R = torch.zeros((n, 3, 3), dtype=torch.float64)
+    R[:, 0, 0], R[:, 0, 2], R[:, 1, 1], R[:, 2, 0], R[:, 2, 2] = yaw.cos(), -yaw.sin(), 1, yaw.sin(), yaw.cos()
+    Ow = torch.stack([0.05 * torch.sin(0.3 * torch.arange(n, dtype=torch.float64)), torch.zeros(n),
+                      0.8 * torch.arange(n, dtype=torch.float64)], 1)
+    t = -(R @ Ow[:, :, None])[:, :, 0]
+    pairs = torch.tensor([[n - 1, n - 1 - d] for d in range(1, n)])
+    return MA.triangulation_geometry(K, R, t, pairs)
 
 
 def cpu_threads():
@@ -146,12 +168,14 @@ class CpuAgent:
     candidates, then the keyframe joins the database (MapFusion's query-then-add).  One per thread, as one
     extractor per agent (Tracking.cc:119-125)."""
 
-    def __init__(self, O, cfg, tables, voc, n_kf_step):
+    def __init__(self, O, cfg, tables, voc, n_kf_step, tri=None):
         self.O, self.cfg, self.tables = O, cfg, tables
+        self.tri = tri                                 # (TRI_NEIGHBOURS, 12) geometry rows, None = no triangulation
         self.vocab = O.Vocabulary(voc)
         self.ring = STORE_STEPS * max(1, n_kf_step)
         self.db = O.Kfdb(int(np.sum(voc["is_leaf"])), self.ring)
         self.kfs = [None] * self.ring
+        self.kps = [None] * self.ring
         self.n_kf = 0
         self.n = 0
 
@@ -166,25 +190,54 @@ class CpuAgent:
             kf = (a["desc"], a["kps"]["angle"], (depth > 0).astype(np.uint8),
                   (bow["fv_nodes"], bow["fv_offsets"], bow["fv_indices"]))
             slot = self.n_kf % self.ring
+            if self.tri is not None:
+                self.new_mappoints(a, kf)
             self.db.erase([slot])
             self.db.set_bow(slot, bow["bow_words"], bow["bow_values"])
             for cand in self.db.detect(0, slot, self.n_kf + 1, 0.0)[:KF_CANDIDATES]:
                 O.search_by_bow_kfkf(*kf, *self.kfs[cand], 0.75, True)
             self.db.add([slot])
             self.kfs[slot] = kf
+            self.kps[slot] = a["kps"]
             self.n_kf += 1
         self.n += 1
 
+    def new_mappoints(self, a, kf):
+        """SearchForTriangulation against the previous TRI_NEIGHBOURS keyframes with ORBmatcher(0.6, false), then the
+        distinctive descriptor of every keypoint's observation list (itself + its matches), as the GPU stage."""
+        O, n = self.O, len(a["desc"])
+        d1, mp1, fv1 = kf[0], kf[2], kf[3]
+        ur = np.full(n, -1, np.float32)
+        rows, m12s = [], []
+        for d in range(1, TRI_NEIGHBOURS + 1):
+            if self.n_kf - d < 0:
+                break
+            s2 = (self.n_kf - d) % self.ring
+            d2, _, mp2, fv2 = self.kfs[s2]
+            g = self.tri[d - 1]
+            _, m12 = O.search_for_triangulation(d1, a["kps"], mp1, ur, fv1, d2, self.kps[s2], mp2,
+                                                np.full(len(d2), -1, np.float32), fv2, g[:9].reshape(3, 3),
+                                                self.tables["sigma2"], self.tables["scale"], float(g[9]), float(g[10]),
+                                                False, False)
+            rows.append(d2)
+            m12s.append(m12)
+        hit = np.stack([np.ones(n, bool)] + [m >= 0 for m in m12s], 1)
+        parts = np.stack([d1] + [r[np.maximum(m, 0)] for r, m in zip(rows, m12s)], 1)   # (n, 1 + k, 32)
+        off = np.zeros(n + 1, np.int32)
+        off[1:] = np.cumsum(hit.sum(1))
+        O.distinctive_descriptors_flat(parts[hit], off)
 
-def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds):
+
+def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds, tri=True):
     """1-thread latency per stereo frame (median / p95) and T-thread throughput with one agent per thread on
     independent frames -- the reference drivers' timing pattern (generic_split_seq.cc:277-314, :369-379: per-frame
     steady_clock around TrackStereo, median and mean reported)."""
     from oracle import oracle as O
     tables = O.tables(cfg["nfeatures"])
     nd = len(lefts)
+    geo = tri_geometry_rows(cfg).numpy() if tri else None
     # (i) latency, one thread
-    ag = CpuAgent(O, cfg, tables, voc, n_kf_step)
+    ag = CpuAgent(O, cfg, tables, voc, n_kf_step, geo)
     lat = []
     t_end = time.perf_counter() + 0.4 * seconds
     while True:
@@ -196,7 +249,7 @@ def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds):
     lat_ms = np.array(lat[1:] if len(lat) > 1 else lat) * 1e3
     # (ii) throughput, T threads (ctypes releases the GIL inside the oracle's C++)
     T = cpu_threads()
-    agents = [CpuAgent(O, cfg, tables, voc, n_kf_step) for _ in range(T)]
+    agents = [CpuAgent(O, cfg, tables, voc, n_kf_step, geo) for _ in range(T)]
     stop = threading.Event()
 
     def run(i):
@@ -583,6 +636,26 @@ def main():
                                       slots=STORE_STEPS * world * n_kf, max_keyframes=n_kf, candidates=KF_CANDIDATES,
                                       agent=rank, world=world, device=dev.index)
     kf_rows = range(0, KF_EVERY * n_kf, KF_EVERY)      # every 5th left frame of the batch becomes a keyframe
+    # CreateNewMapPoints' matching per new keyframe: SearchForTriangulation vs its TRI_NEIGHBOURS previous keyframes of
+    # this agent (all pairs in one launch; MapPoint flags = the store's valid field, i.e. stereo depth > 0), then
+    # the distinctive descriptors of its keypoints' observation lists.  FeatureVector nodes at levelsup 4 of a k=10,
+    # L=6 tree: at most 10^2 per keyframe
+    tri, tri_pat = None, {}
+    if args.tri:
+        tri = MA.NewMapPoints(engine.store, 100, ex.GetScaleSigmaSquares(), ex.GetScaleFactors(),
+                              matcher=pkg.ORBmatcher(0.6, False, device=dev.index))
+        tri_geom = tri_geometry_rows(cfg).float().to(dev).view(1, TRI_NEIGHBOURS, 12).expand(n_kf, -1, -1).contiguous()
+
+        def tri_pattern(q):
+            """(new slots, neighbour slots) of this agent's keyframes q (a slot range): the d-th previous keyframe of
+            keyframe j sits (j - d) keyframes back in this agent's ring order."""
+            if q.start not in tri_pat:
+                nq, per = len(q), world * n_kf
+                nb = [[(q.start + ((j - d) // nq) * per + (j - d) % nq) % engine.slots for d in range(1, TRI_NEIGHBOURS + 1)]
+                      for j in range(nq)]
+                tri_pat[q.start] = (torch.tensor(list(q), dtype=torch.int32, device=dev),
+                                    torch.tensor(nb, dtype=torch.int32, device=dev))
+            return tri_pat[q.start]
     if world > 1:
         send = torch.empty((n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
         gathered = torch.empty((world * n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
@@ -592,6 +665,7 @@ def main():
     skip = set(filter(None, args.diag_skip.split(",")))
     stereo_ms = []
     kf_ms = []
+    tri_ms = []
     host_split = [0.0, 0.0]                            # host enqueue seconds: front-end, keyframe path
 
     last_handoff = [None]
@@ -654,6 +728,17 @@ def main():
             with torch.cuda.stream(kf_stream):
                 exchange.exchange(send, out=gathered)
             engine.commit(gathered, stream=kf_stream)
+        if tri is not None:
+            ns, nb = tri_pattern(engine.last_step()[1])
+            if time_stereo:
+                e4 = torch.cuda.Event(enable_timing=True)
+                e4.record(kf_stream)
+            with torch.cuda.stream(kf_stream):
+                tri.run(ns, nb, tri_geom)
+            if time_stereo:
+                e5 = torch.cuda.Event(enable_timing=True)
+                e5.record(kf_stream)
+                tri_ms.append((e4, e5))
         done = torch.cuda.Event()
         done.record(kf_stream)
         kf_done[buf] = done
@@ -733,6 +818,9 @@ def main():
                                "keyframe: DBoW2 transform (k=10, L=6) + " + (f"{collective} of KF packets + " if world > 1 else "") +
                                "KeyFrameDatabase DetectLoopCandidates (query, then add) over the KF store + "
                                f"SearchByBoW vs the first {KF_CANDIDATES} candidates" +
+                               (f"; CreateNewMapPoints matching: SearchForTriangulation vs {TRI_NEIGHBOURS} neighbour "
+                                "keyframes + distinctive descriptors of the new keyframes' observation lists"
+                                if args.tri else "") +
                                (" of other agents' maps (MapFusion.cc:136-144)" if world > 1 else
                                 " of the agent's own map with minScore 0 (LoopClosing-like: N=1 has no other map, so these "
                                 "pairs are work MapFusion itself would not do)"),
@@ -756,6 +844,9 @@ def main():
         per_call["stereo_match"] = float(np.mean(sms)) if sms else 0.0
         kms = [a.elapsed_time(b) for a, b in kf_ms]
         per_call["keyframe_bow_fusion"] = float(np.mean(kms)) if kms else 0.0
+        tms = [a.elapsed_time(b) for a, b in tri_ms]
+        if tms:
+            per_call["keyframe_new_mappoints"] = float(np.mean(tms))   # part of keyframe_bow_fusion
         out["stage_ms_per_step"] = {k: round(v, 4) for k, v in per_call.items()}
         out["roofline"], sec = roofline_lines(per_call, cfg, 2 * B, args.config)
         if sec:
@@ -783,7 +874,7 @@ def main():
         out["host_api"] = host_api_rate(pkg, cfg, lefts, rights, args.host_api_frames, dev.index)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(lefts[:16], rights[:16], cfg, S.synthetic_vocabulary(2024, k=10, L=6), n_kf,
-                                           args.cpu_seconds)
+                                           args.cpu_seconds, tri=args.tri)
     if skip:
         out["diag_skip"] = sorted(skip)
     engine.check()

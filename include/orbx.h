@@ -317,6 +317,33 @@ int orbx_search_for_triangulation(orbx_matcher* m, const uint8_t* desc1, const o
                                   const float* sigma2_2, const float* scale_2, int nlevels, float ex, float ey,
                                   int only_stereo, int32_t* match12, int* n_matches);
 
+/* SearchForTriangulation for many (kf1, kf2) slot pairs of a device keyframe store in one launch -- LocalMapping::
+ * CreateNewMapPoints' loop over the new keyframe's best covisible neighbours (src/LocalMapping.cc:243-274).
+ * d_has_mp: per-slot "keypoint already has a MapPoint" rows at d_has_mp + k*has_mp_stride bytes (NULL = the store's
+ * valid field; stride 0 = one row for every slot); d_uright: per-slot mvuRight rows likewise (NULL = no stereo keypoints); d_geom[p]: F12 (row-major) and the epipole of KF1 in KF2 for pair p; sigma2_2 / scale_2: KF2's
+ * level tables (host).  Outputs d_match12[p*capacity + i1] = KF2 index or -1, d_nmatches[p]; the matcher's
+ * checkOri applies (CreateNewMapPoints uses ORBmatcher(0.6, false)). */
+typedef struct orbx_tri_geom {
+    float F12[9];
+    float ex, ey;
+    float pad;
+} orbx_tri_geom;
+int orbx_search_for_triangulation_pairs_device(orbx_matcher* m, const orbx_kf_store* store, const uint8_t* d_has_mp,
+                                               size_t has_mp_stride, const float* d_uright, size_t uright_stride, const int32_t* d_pairs, const orbx_tri_geom* d_geom,
+                                               int n_pairs, int max_fv_nodes, const float* sigma2_2, const float* scale_2,
+                                               int nlevels, int only_stereo, int32_t* d_match12, int32_t* d_nmatches,
+                                               void* stream);
+
+/* orbx_distinctive_descriptors for the MapPoints of new keyframes after the batched SearchForTriangulation above
+ * (LocalMapping.cc:440-448 and the fused points of SearchInNeighbors, :528-533), lists read from the match table
+ * itself: MapPoint j*capacity + i = keypoint i of keyframe d_new_slots[j], observed there first and then at
+ * d_match12[(j*n_neighbours + k)*capacity + i] of slot d_neighbours[j*n_neighbours + k] for every k in order with a
+ * neighbour (>= 0) and a match (>= 0).  n_neighbours <= 63.  d_best[mp] = list index; d_out_desc[mp] (or NULL). */
+int orbx_distinctive_descriptors_neighbours_device(orbx_matcher* m, const orbx_kf_store* store, const int32_t* d_new_slots,
+                                                   const int32_t* d_neighbours, int n_new, int n_neighbours,
+                                                   const int32_t* d_match12, int32_t* d_best, uint8_t* d_out_desc,
+                                                   void* stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Keypoint grid and the projection / radius matchers.
  * The reference's callers project each MapPoint before searching (cv::Mat products, PredictScale,

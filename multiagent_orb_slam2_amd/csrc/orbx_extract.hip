@@ -1257,7 +1257,7 @@ __global__ __launch_bounds__(256) void k_fast_rows(const uint8_t* __restrict__ p
             cntB[t] += rbC - rbB;
         }
     };
-    int dbg_acc = 0;
+    [[maybe_unused]] int dbg_acc = 0;
     // strict 3x3 NMS of row c (scores of rows c-1, c, c+1) at both thresholds
     auto nms = [&](int row, const FastRowSc& U, const FastRowSc& C, const FastRowSc& D) {
         const uint32_t lm0 = pmax_u(pmax_u(U.l0, C.l0), D.l0) | mL[0];

@@ -657,65 +657,147 @@ struct TriArgs {
 // SearchForTriangulation: no greedy coupling between queries (vbMatched2 is never set, :679,727), so
 // the result of a query is the LAST candidate (in node order) among those with the minimum distance
 // that pass the epipole and epipolar tests (dist <= TH_LOW, ties replace: :740).
-__global__ __launch_bounds__(64) void k_triangulate(TriArgs A) {
-    const int a = blockIdx.x, ln = lane_id();
-    if (a >= A.f1.n) return;
+// One wave per node: up to 64 queries and 64 candidates of the node are staged in lanes at once (all loads issued
+// together), then each query is broadcast to the wave with v_readlane and tested against every candidate lane,
+// so the inner loop touches no memory.  s_sig2 / s_sc2: KF2's level tables in LDS.
+__device__ __forceinline__ void tri_node(const TriArgs& A, const float* s_sig2, const float* s_sc2, int a) {
+    const int ln = lane_id();
     const uint32_t id = A.f1.node[a];
     const int b = fv_lower_bound(A.f2, id);
     if (b >= A.f2.n || A.f2.node[b] != id) return;
     const int q0 = A.f1.off[a], q1 = A.f1.off[a + 1];
     const int c0 = A.f2.off[b], c1 = A.f2.off[b + 1];
     int local = 0;
-    for (int p = q0; p < q1; ++p) {
-        const int i1 = A.f1.idx[p];
-        if (A.mp1[i1]) continue;
-        const bool st1 = A.ur1[i1] >= 0;
-        if (A.onlyStereo && !st1) continue;
-        const orbx_keypoint kp1 = A.k1[i1];
-        uint4 x0, x1;
-        load_desc(A.d1 + 32 * (size_t)i1, x0, x1);
-        // CheckDistEpipolarLine (:142-159) line coefficients
-        const float la = __fadd_rn(__fadd_rn(__fmul_rn(kp1.x, A.F[0]), __fmul_rn(kp1.y, A.F[3])), A.F[6]);
-        const float lb = __fadd_rn(__fadd_rn(__fmul_rn(kp1.x, A.F[1]), __fmul_rn(kp1.y, A.F[4])), A.F[7]);
-        const float lc = __fadd_rn(__fadd_rn(__fmul_rn(kp1.x, A.F[2]), __fmul_rn(kp1.y, A.F[5])), A.F[8]);
+    for (int qb = q0; qb < q1; qb += kWave) {
+        // this lane's query (node position qb + ln)
+        const bool qin = qb + ln < q1;
+        const int i1 = qin ? A.f1.idx[qb + ln] : 0;
+        bool qok = qin && !A.mp1[i1];
+        const bool st1 = qok && A.ur1[i1] >= 0;
+        if (A.onlyStereo && !st1) qok = false;
+        uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0;
+        float la = 0.0f, lb = 0.0f, lc = 0.0f;
+        if (qok) {
+            const orbx_keypoint kp1 = A.k1[i1];
+            load_desc(A.d1 + 32 * (size_t)i1, x0, x1);
+            // CheckDistEpipolarLine (:142-159) line coefficients
+            la = __fadd_rn(__fadd_rn(__fmul_rn(kp1.x, A.F[0]), __fmul_rn(kp1.y, A.F[3])), A.F[6]);
+            lb = __fadd_rn(__fadd_rn(__fmul_rn(kp1.x, A.F[1]), __fmul_rn(kp1.y, A.F[4])), A.F[7]);
+            lc = __fadd_rn(__fadd_rn(__fmul_rn(kp1.x, A.F[2]), __fmul_rn(kp1.y, A.F[5])), A.F[8]);
+        }
         const float den = __fadd_rn(__fmul_rn(la, la), __fmul_rn(lb, lb));
-        uint32_t bestkey = 0;   // ((256 - d) << 20 | pos): max -> min distance, last position
-        for (int j = c0 + ln; j < c1; j += kWave) {
-            const int i2 = A.f2.idx[j];
-            if (A.mp2[i2]) continue;
-            const bool st2 = A.ur2[i2] >= 0;
-            if (A.onlyStereo && !st2) continue;
-            uint4 y0, y1;
-            load_desc(A.d2 + 32 * (size_t)i2, y0, y1);
-            const int d = hamming256(x0, x1, y0, y1);
-            if (d > kThLow) continue;
-            const orbx_keypoint kp2 = A.k2[i2];
-            if (!st1 && !st2) {
+        const uint64_t qmask = __ballot(qok);
+        if (!qmask) continue;
+        uint32_t mybest = 0;    // ((256 - d) << 20 | pos): max -> min distance, last position
+        for (int cb = c0; cb < c1; cb += kWave) {
+            // this lane's candidate (node position cb + ln)
+            const bool cin = cb + ln < c1;
+            const int i2 = cin ? A.f2.idx[cb + ln] : 0;
+            bool cok = cin && !A.mp2[i2];
+            const bool st2 = cok && A.ur2[i2] >= 0;
+            if (A.onlyStereo && !st2) cok = false;
+            uint4 y0 = make_uint4(0, 0, 0, 0), y1 = y0;
+            float x2 = 0.0f, y2 = 0.0f, sig2 = 0.0f;
+            bool near_epi = false;
+            if (cok) {
+                const orbx_keypoint kp2 = A.k2[i2];
+                load_desc(A.d2 + 32 * (size_t)i2, y0, y1);
+                x2 = kp2.x; y2 = kp2.y;
+                sig2 = s_sig2[kp2.octave];
                 const float dx = __fsub_rn(A.ex, kp2.x), dy = __fsub_rn(A.ey, kp2.y);
-                if (__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < __fmul_rn(100.0f, A.scale2[kp2.octave])) continue;
+                near_epi = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)) < __fmul_rn(100.0f, s_sc2[kp2.octave]);
             }
-            if (den == 0.0f) continue;
-            const float num = __fadd_rn(__fadd_rn(__fmul_rn(la, kp2.x), __fmul_rn(lb, kp2.y)), lc);
-            const float dsqr = __fdiv_rn(__fmul_rn(num, num), den);
-            if (!((double)dsqr < 3.84 * (double)A.sigma2[kp2.octave])) continue;
-            const uint32_t key = ((uint32_t)(256 - d) << 20) | (uint32_t)(j - c0);
-            bestkey = max(bestkey, key);
-        }
-        bestkey = ~wave_min_u32(~bestkey);
-        if (bestkey != 0) {
-            const int i2 = A.f2.idx[c0 + (int)(bestkey & 0xfffff)];
-            if (ln == 0) {
-                A.match[i1] = i2;
-                if (A.checkOri) {
-                    const int bn = rot_bin(kp1.angle, A.k2[i2].angle);
-                    A.bin[i1] = bn;
-                    atomicAdd(&A.hist[bn], 1);
+            if (!__ballot(cok)) continue;
+            const uint32_t pos = (uint32_t)(cb + ln - c0);
+            for (uint64_t mq = qmask; mq; mq &= mq - 1) {
+                const int k = __builtin_ctzll(mq);
+                uint4 q0v, q1v;
+                q0v.x = __builtin_amdgcn_readlane(x0.x, k); q0v.y = __builtin_amdgcn_readlane(x0.y, k);
+                q0v.z = __builtin_amdgcn_readlane(x0.z, k); q0v.w = __builtin_amdgcn_readlane(x0.w, k);
+                q1v.x = __builtin_amdgcn_readlane(x1.x, k); q1v.y = __builtin_amdgcn_readlane(x1.y, k);
+                q1v.z = __builtin_amdgcn_readlane(x1.z, k); q1v.w = __builtin_amdgcn_readlane(x1.w, k);
+                const float qa = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, la), k));
+                const float qb_ = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lb), k));
+                const float qc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lc), k));
+                const float qd = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, den), k));
+                const bool qst = __builtin_amdgcn_readlane((int)st1, k) != 0;
+                uint32_t key = 0;
+                if (cok) {
+                    const int d = hamming256(q0v, q1v, y0, y1);
+                    bool pass = d <= kThLow && !(!qst && !st2 && near_epi) && qd != 0.0f;
+                    if (pass) {
+                        const float num = __fadd_rn(__fadd_rn(__fmul_rn(qa, x2), __fmul_rn(qb_, y2)), qc);
+                        const float dsqr = __fdiv_rn(__fmul_rn(num, num), qd);
+                        pass = (double)dsqr < 3.84 * (double)sig2;
+                    }
+                    if (pass) key = ((uint32_t)(256 - d) << 20) | pos;
                 }
+                const uint32_t best = ~wave_min_u32(~key);
+                if (ln == k) mybest = max(mybest, best);
             }
-            ++local;
         }
+        const bool hit = mybest != 0;
+        if (hit) {
+            const int j2 = A.f2.idx[c0 + (int)(mybest & 0xfffff)];
+            A.match[i1] = j2;
+            if (A.checkOri) {
+                const int bn = rot_bin(A.k1[i1].angle, A.k2[j2].angle);
+                A.bin[i1] = bn;
+                atomicAdd(&A.hist[bn], 1);
+            }
+        }
+        local += __builtin_popcountll(__ballot(hit));
     }
     if (ln == 0 && local) atomicAdd(A.nmatch, local);
+}
+
+// KF2's level tables into LDS (byval kernel-argument arrays indexed with constants only)
+__device__ __forceinline__ void tri_tables(const float (&sig2)[32], const float (&sc2)[32], float* s_sig2, float* s_sc2) {
+#pragma unroll
+    for (int l = 0; l < 32; ++l)
+        if (lane_id() == l) { s_sig2[l] = sig2[l]; s_sc2[l] = sc2[l]; }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void k_triangulate(TriArgs A) {
+    __shared__ float s_sig2[32], s_sc2[32];
+    if ((int)blockIdx.x >= A.f1.n) return;
+    tri_tables(A.sigma2, A.scale2, s_sig2, s_sc2);
+    tri_node(A, s_sig2, s_sc2, blockIdx.x);
+}
+
+// SearchForTriangulation over (kf1, kf2) slot pairs of a device keyframe store (LocalMapping::CreateNewMapPoints'
+// loop over the new keyframe's neighbours, LocalMapping.cc:243-274): MapPoint flags = the store's valid field,
+// uright per slot (optional), F12 and the epipole per pair, the level tables of KF2 shared (one extractor).
+struct TriTables { float sigma2[32], scale2[32]; };
+
+__global__ __launch_bounds__(64) void k_triangulate_pairs(orbx_kf_store S, const uint8_t* __restrict__ has_mp, size_t mp_stride,
+                                                          const float* __restrict__ uright, size_t ur_stride,
+                                                          const int32_t* __restrict__ pairs, const orbx_tri_geom* __restrict__ geom,
+                                                          TriTables T, int onlyStereo, int checkOri, const float* __restrict__ no_ur,
+                                                          int32_t* match, int32_t* bin, int32_t* hist, int32_t* nmatch) {
+    __shared__ float s_sig2[32], s_sc2[32];
+    const int pr = blockIdx.y;
+    const int k1 = pairs[2 * pr], k2 = pairs[2 * pr + 1];
+    if (k1 < 0 || k2 < 0) return;                       // padding pair: no matches
+    TriArgs A;
+    A.f1 = store_fv(S, k1);
+    if ((int)blockIdx.x >= A.f1.n) return;
+    A.f2 = store_fv(S, k2);
+    A.d1 = slot_ptr(S.desc, S.desc_stride, k1); A.d2 = slot_ptr(S.desc, S.desc_stride, k2);
+    A.k1 = slot_ptr(S.kps, S.kps_stride, k1); A.k2 = slot_ptr(S.kps, S.kps_stride, k2);
+    A.mp1 = has_mp ? slot_ptr(has_mp, mp_stride, k1) : slot_ptr(S.valid, S.valid_stride, k1);
+    A.mp2 = has_mp ? slot_ptr(has_mp, mp_stride, k2) : slot_ptr(S.valid, S.valid_stride, k2);
+    A.ur1 = uright ? slot_ptr(uright, ur_stride, k1) : no_ur;
+    A.ur2 = uright ? slot_ptr(uright, ur_stride, k2) : no_ur;
+    const orbx_tri_geom g = geom[pr];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) A.F[i] = g.F12[i];
+    A.ex = g.ex; A.ey = g.ey; A.onlyStereo = onlyStereo; A.checkOri = checkOri;
+    A.match = match + (size_t)pr * S.capacity; A.bin = bin + (size_t)pr * S.capacity;
+    A.hist = hist + (size_t)pr * 32; A.nmatch = nmatch + pr;
+    tri_tables(T.sigma2, T.scale2, s_sig2, s_sc2);
+    for (int a = blockIdx.x; a < A.f1.n; a += gridDim.x) tri_node(A, s_sig2, s_sc2, a);   // grid.x: a width hint
 }
 
 // rotation-consistency filter: keep matches whose bin is one of the three largest bins
@@ -1130,6 +1212,74 @@ __global__ __launch_bounds__(256) void k_distinctive(DistinctArgs A) {
     if (ln == 0) A.best[mp] = bi;
     if (A.out && ln < 8) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(obs_desc(A, o0 + bi));
+        reinterpret_cast<uint32_t*>(A.out + 32 * (size_t)mp)[ln] = src[ln];
+    }
+}
+
+// The MapPoints of new keyframes with observation lists read straight from CreateNewMapPoints' match tables
+// (no CSR built): MapPoint (j, i) = keypoint i of new keyframe j, observed there (lane 0) and at match12[j][k][i] of
+// neighbour k (lane 1 + k) when matched -- multiagent.neighbour_observations' list order.  One wave per MapPoint;
+// lane t holds observation t, list position = its rank among the observing lanes.  N <= 2: every row's median is its
+// own zero distance, so the first row wins without a distance (MapPoint.cc:296-306).
+struct DistinctNbArgs {
+    orbx_kf_store S;
+    const int32_t* new_slots;   // [n]
+    const int32_t* nb;          // [n][nn] neighbour slots, -1 = none
+    const int32_t* m12;         // [n][nn][capacity]
+    int n, nn, M;
+    int32_t* best;              // [M] list index
+    uint8_t* out;               // [M][32] or NULL
+    int nbx;
+};
+
+__global__ __launch_bounds__(256) void k_distinctive_nb(DistinctNbArgs A) {
+    const int item = xcd_item(xcd_chunk(A.nbx));
+    if (item >= A.nbx) return;
+    const int mp = item * 4 + (int)(threadIdx.x >> 6);
+    if (mp >= A.M) return;
+    const int ln = lane_id(), cap = A.S.capacity;
+    const int j = mp / cap, i = mp - j * cap;
+    int slot = -1, kp = -1;
+    if (ln == 0) { slot = A.new_slots[j]; kp = i; }
+    else if (ln <= A.nn) {
+        const int nbk = A.nb[j * A.nn + ln - 1];
+        if (nbk >= 0) {
+            const int m = A.m12[((size_t)j * A.nn + ln - 1) * cap + i];
+            if (m >= 0) { slot = nbk; kp = m; }
+        }
+    }
+    const bool has = kp >= 0;
+    const uint64_t mask = __ballot(has);
+    const int N = __builtin_popcountll(mask);
+    const int pos = __builtin_popcountll(mask & ((1ull << ln) - 1ull));
+    int win = 0;                                           // lane of the chosen observation
+    if (N > 2) {
+        uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+        if (has) load_desc(A.S.desc + (size_t)slot * A.S.desc_stride + 32 * (size_t)kp, a0, a1);
+        const int need = (N - 1) / 2 + 1;
+        int lo = 0, hi = 256;
+#pragma unroll 1
+        for (int it = 0; it < 9; ++it) {
+            const int mid = (lo + hi) >> 1;
+            int cnt = 0;
+            for (uint64_t mq = mask; mq; mq &= mq - 1) {
+                const int t = __builtin_ctzll(mq);
+                uint4 x0, x1;
+                x0.x = __builtin_amdgcn_readlane(a0.x, t); x0.y = __builtin_amdgcn_readlane(a0.y, t);
+                x0.z = __builtin_amdgcn_readlane(a0.z, t); x0.w = __builtin_amdgcn_readlane(a0.w, t);
+                x1.x = __builtin_amdgcn_readlane(a1.x, t); x1.y = __builtin_amdgcn_readlane(a1.y, t);
+                x1.z = __builtin_amdgcn_readlane(a1.z, t); x1.w = __builtin_amdgcn_readlane(a1.w, t);
+                cnt += hamming256(a0, a1, x0, x1) <= mid;
+            }
+            if (cnt >= need) hi = mid; else lo = mid + 1;
+        }
+        const uint32_t key = has ? (((uint32_t)lo << 20) | ((uint32_t)pos << 8) | (uint32_t)ln) : 0xffffffffu;
+        win = (int)(wave_min_u32(key) & 0xff);
+    }
+    const int wslot = __builtin_amdgcn_readlane(slot, win), wkp = __builtin_amdgcn_readlane(kp, win);
+    if (ln == 0) A.best[mp] = __builtin_amdgcn_readlane(pos, win);
+    if (A.out && ln < 8) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(A.S.desc + (size_t)wslot * A.S.desc_stride + 32 * (size_t)wkp);
         reinterpret_cast<uint32_t*>(A.out + 32 * (size_t)mp)[ln] = src[ln];
     }
 }
@@ -1705,6 +1855,46 @@ int orbx_search_by_bow_kfkf_pairs_device(orbx_matcher* m, const orbx_kf_store* s
     return ORBX_OK;
 }
 
+int orbx_search_for_triangulation_pairs_device(orbx_matcher* m, const orbx_kf_store* store, const uint8_t* d_has_mp,
+                                               size_t has_mp_stride, const float* d_uright, size_t uright_stride, const int32_t* d_pairs, const orbx_tri_geom* d_geom,
+                                               int n_pairs, int max_fv_nodes, const float* sigma2_2, const float* scale_2,
+                                               int nlevels, int only_stereo, int32_t* d_match12, int32_t* d_nmatches,
+                                               void* stream) {
+    ORBX_REQUIRE(m && store && d_pairs && d_geom && d_match12 && d_nmatches && n_pairs >= 0 && max_fv_nodes >= 0 && sigma2_2 &&
+                     scale_2 && nlevels >= 1 && nlevels <= 32, ORBX_ERR_ARG, "bad argument");
+    const orbx_kf_store& S = *store;
+    ORBX_REQUIRE(S.desc && S.kps && S.valid && S.fv_nodes && S.fv_offsets && S.fv_indices && S.n_fv && S.capacity > 0,
+                 ORBX_ERR_ARG, "incomplete keyframe store");
+    ORBX_REQUIRE(((uintptr_t)S.desc % 16) == 0 && S.desc_stride % 16 == 0 && ((uintptr_t)S.kps % 4) == 0 &&
+                     S.kps_stride % 4 == 0 && S.fv_nodes_stride % 4 == 0 && S.fv_offsets_stride % 4 == 0 &&
+                     S.fv_indices_stride % 4 == 0 && S.n_fv_stride % 4 == 0 && (!d_uright || uright_stride % 4 == 0),
+                 ORBX_ERR_ARG, "misaligned keyframe store");
+    if (n_pairs == 0) return ORBX_OK;
+    ORBX_REQUIRE(n_pairs <= 65535, ORBX_ERR_UNSUPPORTED, "too many pairs (%d)", n_pairs);
+    ORBX_HIP(hipSetDevice(m->device));
+    hipStream_t s = (hipStream_t)stream;
+    const size_t cap = (size_t)S.capacity;
+    ORBX_HIP(hipMemsetAsync(d_match12, 0xff, (size_t)n_pairs * cap * 4, s));
+    ORBX_HIP(hipMemsetAsync(d_nmatches, 0, (size_t)n_pairs * 4, s));
+    MatcherLease lease_(m, s);
+    // scratch: bins, histograms, and (no uright given) one row of -1 = "no stereo keypoint"
+    int st = m->reserve_on(a256((size_t)n_pairs * cap * 4) + a256((size_t)n_pairs * 32 * 4) + a256(cap * 4), s);
+    if (st) return st;
+    int32_t* bin = (int32_t*)m->scratch;
+    int32_t* hist = (int32_t*)((uint8_t*)m->scratch + a256((size_t)n_pairs * cap * 4));
+    float* no_ur = (float*)((uint8_t*)hist + a256((size_t)n_pairs * 32 * 4));
+    ORBX_HIP(hipMemsetAsync(hist, 0, (size_t)n_pairs * 32 * 4, s));
+    if (!d_uright) ORBX_HIP(hipMemsetAsync(no_ur, 0xff, cap * 4, s));   // 0xffffffff = NaN: "ur >= 0" false
+    TriTables T{};
+    for (int l = 0; l < nlevels; ++l) { T.sigma2[l] = sigma2_2[l]; T.scale2[l] = scale_2[l]; }
+    hipLaunchKernelGGL(k_triangulate_pairs, dim3(std::max(1, std::min(max_fv_nodes, 4096)), n_pairs), dim3(64), 0, s, S, d_has_mp, has_mp_stride, d_uright,
+                       uright_stride, d_pairs, d_geom, T, only_stereo, m->checkOri, no_ur, d_match12, bin, hist, d_nmatches);
+    if (m->checkOri)
+        hipLaunchKernelGGL(k_rot_filter, dim3(n_pairs), dim3(256), 0, s, d_match12, bin, S.capacity, hist, d_nmatches, S.capacity);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
 static int distinct_launch(DistinctArgs& A, hipStream_t s) {
     if (A.M == 0) return ORBX_OK;
     A.nbx = (A.M + 3) / 4;
@@ -1733,6 +1923,26 @@ int orbx_distinctive_descriptors_store_device(orbx_matcher* m, const orbx_kf_sto
     DistinctArgs A{};
     A.obs = d_obs; A.S = *store; A.store = 1; A.off = d_offsets; A.M = n_mappoints; A.best = d_best; A.out = d_out_desc;
     return distinct_launch(A, (hipStream_t)stream);
+}
+
+int orbx_distinctive_descriptors_neighbours_device(orbx_matcher* m, const orbx_kf_store* store, const int32_t* d_new_slots,
+                                                   const int32_t* d_neighbours, int n_new, int n_neighbours,
+                                                   const int32_t* d_match12, int32_t* d_best, uint8_t* d_out_desc,
+                                                   void* stream) {
+    ORBX_REQUIRE(m && store && n_new >= 0 && n_neighbours >= 0 && n_neighbours < kWave &&
+                     (n_new == 0 || (d_new_slots && d_best && (n_neighbours == 0 || (d_neighbours && d_match12)))),
+                 ORBX_ERR_ARG, "bad argument");
+    ORBX_REQUIRE(store->desc && ((uintptr_t)store->desc % 16) == 0 && store->desc_stride % 16 == 0 && store->capacity > 0,
+                 ORBX_ERR_ARG, "misaligned keyframe store");
+    ORBX_REQUIRE((size_t)n_new * store->capacity < (1u << 31), ORBX_ERR_UNSUPPORTED, "too many MapPoints");
+    if (n_new == 0) return ORBX_OK;
+    ORBX_HIP(hipSetDevice(m->device));
+    DistinctNbArgs A{};
+    A.S = *store; A.new_slots = d_new_slots; A.nb = d_neighbours; A.m12 = d_match12; A.n = n_new; A.nn = n_neighbours;
+    A.M = n_new * store->capacity; A.best = d_best; A.out = d_out_desc; A.nbx = (A.M + 3) / 4;
+    hipLaunchKernelGGL(k_distinctive_nb, dim3(kXcds * xcd_chunk(A.nbx)), dim3(256), 0, (hipStream_t)stream, A);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
 }
 
 int orbx_distinctive_descriptors(orbx_matcher* m, const uint8_t* desc, const int32_t* offsets, int n_mappoints, int32_t* best,

@@ -475,3 +475,93 @@ class CovisibilityDiscovery:
         pr = KeyFrameDatabase.candidate_pairs_device(cand, n_cand, q, k)
         m12, nm = self.matcher.SearchByBoW_pairs_device(self.store, pr, self.max_fv_nodes)
         return pr, m12, nm, nm >= self.min_matches, n_host
+
+
+def triangulation_geometry(K, Rcw, tcw, pairs):
+    """F12 = K1^-T [t12]x R12 K2^-1 with R12 = R1w R2w^T, t12 = -R12 t2w + t1w (LocalMapping::ComputeF12,
+    src/LocalMapping.cc:542-557) and the epipole of KF1's centre in KF2 (ORBmatcher.cc:666-672) for (kf1, kf2) index
+    pairs into per-keyframe poses.  K (3, 3), Rcw (N, 3, 3), tcw (N, 3), pairs (P, 2) integer tensors (any device, one
+    intrinsics for all keyframes); float32 arithmetic.  Returns (P, 12) rows [F12 row-major, ex, ey, 0] for
+    ORBmatcher.SearchForTriangulation_pairs_device; rows of pairs with a negative index are zero."""
+    import torch
+    K = K.to(torch.float32)
+    p = pairs.long().clamp(min=0)
+    R1, t1 = Rcw[p[:, 0]].float(), tcw[p[:, 0]].float()
+    R2, t2 = Rcw[p[:, 1]].float(), tcw[p[:, 1]].float()
+    R12 = R1 @ R2.transpose(1, 2)
+    t12 = -(R12 @ t2[:, :, None])[:, :, 0] + t1
+    z = torch.zeros_like(t12[:, 0])
+    tx = torch.stack([z, -t12[:, 2], t12[:, 1], t12[:, 2], z, -t12[:, 0], -t12[:, 1], t12[:, 0], z], 1).view(-1, 3, 3)
+    Kinv = torch.linalg.inv(K)
+    F = Kinv.T[None] @ tx @ R12 @ Kinv[None]
+    C1 = -(R1.transpose(1, 2) @ t1[:, :, None])[:, :, 0]                   # Ow1 = -R1w^T t1w
+    C2 = (R2 @ C1[:, :, None])[:, :, 0] + t2
+    iz = 1.0 / C2[:, 2]
+    ex = K[0, 0] * C2[:, 0] * iz + K[0, 2]
+    ey = K[1, 1] * C2[:, 1] * iz + K[1, 2]
+    g = torch.cat([F.reshape(-1, 9), ex[:, None], ey[:, None], z[:, None]], 1).contiguous()
+    return torch.where((pairs.long() >= 0).all(1)[:, None], g, torch.zeros_like(g))
+
+
+def neighbour_observations(new_slots, neighbours, match12):
+    """Observation lists of the MapPoints of new keyframes, built on the device without a host round trip: MapPoint
+    (j, i) = keypoint i of new keyframe j, observed there and at every neighbour keypoint it matched
+    (match12[j, k, i] >= 0, neighbours in order).  new_slots (n,), neighbours (n, nn) slots (-1 = none), match12
+    (n, nn, capacity).  Returns (obs (n*capacity*(nn+1), 2) int32 -- the first offsets[-1] rows used, offsets
+    (n*capacity + 1,) int32) for ORBmatcher.distinctive_descriptors_store_device."""
+    import torch
+    n, nn, cap = match12.shape
+    dev = match12.device
+    hit = torch.cat([torch.ones((n, cap, 1), dtype=torch.bool, device=dev), (match12 >= 0).permute(0, 2, 1)], 2)
+    slot = torch.cat([new_slots.view(n, 1).expand(n, cap)[:, :, None].int(),
+                      neighbours.view(n, 1, nn).expand(n, cap, nn).int()], 2)
+    kp = torch.cat([torch.arange(cap, dtype=torch.int32, device=dev).view(1, cap, 1).expand(n, cap, 1),
+                    match12.permute(0, 2, 1).int()], 2)
+    cnt = hit.sum(2, dtype=torch.int32).view(-1)
+    offsets = torch.zeros((n * cap + 1,), dtype=torch.int32, device=dev)
+    offsets[1:] = torch.cumsum(cnt, 0)
+    rank = torch.cumsum(hit.int(), 2) - 1                                   # position inside the MapPoint's list
+    pos = (offsets[:-1].view(n, cap, 1) + rank).long()
+    tot = n * cap * (nn + 1)
+    pos = torch.where(hit, pos, torch.full_like(pos, tot))                  # unmatched -> the spill row
+    obs = torch.zeros((tot + 1, 2), dtype=torch.int32, device=dev)
+    obs.index_copy_(0, pos.view(-1), torch.stack([slot, kp], 3).view(-1, 2))
+    return obs[:tot], offsets
+
+
+class NewMapPoints:
+    """LocalMapping::CreateNewMapPoints' matching for a batch of new keyframes (src/LocalMapping.cc:213-274): every new
+    keyframe against its best covisible neighbours with ORBmatcher(0.6, false).SearchForTriangulation, all pairs in
+    one launch, then ComputeDistinctiveDescriptors for the new keyframes' MapPoints (ProcessNewKeyFrame :150-160 and
+    the new points :440-448) over the observation lists of neighbour_observations, read from the match table in
+    place (orbx_distinctive_descriptors_neighbours_device).
+
+    The reference visits the neighbours of one keyframe in turn and a keypoint triangulated with neighbour k is
+    skipped for neighbours k' > k; here every pair reads the MapPoint flags given (has_mp) and the pair results are
+    exactly those of SearchForTriangulation on that state -- the pose checks, SVD triangulation and map insertion
+    that decide which matches become MapPoints run on the map side (out of the hot path)."""
+
+    def __init__(self, store, max_fv_nodes: int, sigma2, scale, matcher=None, only_stereo: bool = False):
+        from .orbx import ORBmatcher
+        self.store, self.max_fv_nodes = store, max_fv_nodes
+        self.sigma2 = np.ascontiguousarray(sigma2, np.float32)
+        self.scale = np.ascontiguousarray(scale, np.float32)
+        self.matcher = matcher if matcher is not None else ORBmatcher(0.6, False)
+        self.only_stereo = only_stereo
+
+    def run(self, new_slots, neighbours, geom, has_mp=None, uright=None):
+        """new_slots (n,), neighbours (n, nn) int32 device tensors (-1 = no neighbour), geom (n, nn, 12) rows from
+        triangulation_geometry.  Returns (match12 (n, nn, cap), nmatches (n, nn), best, descriptors): best[j*cap + i] =
+        index in neighbour_observations' list of MapPoint (j, i), descriptors its distinctive descriptor."""
+        import torch
+        n, nn = neighbours.shape
+        cap = self.store.capacity
+        k1 = new_slots.view(n, 1).expand(n, nn).int()
+        pairs = torch.stack([torch.where(neighbours >= 0, k1, torch.full_like(k1, -1)), neighbours.int()], 2)
+        m12, nm = self.matcher.SearchForTriangulation_pairs_device(
+            self.store, pairs.view(-1, 2).contiguous(), geom.reshape(-1, 12).contiguous(), self.sigma2, self.scale,
+            self.max_fv_nodes, has_mp=has_mp, uright=uright, bOnlyStereo=self.only_stereo)
+        m12 = m12.view(n, nn, cap)
+        best, desc = self.matcher.distinctive_descriptors_neighbours_device(self.store, new_slots.int().contiguous(),
+                                                                           neighbours.int().contiguous(), m12)
+        return m12, nm.view(n, nn), best, desc

@@ -179,9 +179,13 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, i32, FeatVec, vp, vp, vp, vp, i32, FeatVec,
                                                   vp, vp, vp, i32, f32, f32, i32, vp, C.POINTER(i32)]
     lib.orbx_search_by_bow_kfkf_pairs_device.argtypes = [vp, C.POINTER(KfStore), vp, i32, i32, vp, vp, vp]
+    lib.orbx_search_for_triangulation_pairs_device.argtypes = [vp, C.POINTER(KfStore), vp, C.c_size_t, vp, C.c_size_t, vp,
+                                                               vp, i32, i32, vp,
+                                                               vp, i32, i32, vp, vp, vp]
     lib.orbx_distinctive_descriptors.argtypes = [vp, vp, vp, i32, vp, vp]
     lib.orbx_distinctive_descriptors_device.argtypes = [vp, vp, vp, i32, vp, vp, vp]
     lib.orbx_distinctive_descriptors_store_device.argtypes = [vp, C.POINTER(KfStore), vp, vp, i32, vp, vp, vp]
+    lib.orbx_distinctive_descriptors_neighbours_device.argtypes = [vp, C.POINTER(KfStore), vp, vp, i32, i32, vp, vp, vp, vp]
     lib.orbx_grid_build_device.argtypes = [vp, Grid, vp, vp, i32, i32, vp, vp, vp]
     lib.orbx_undistort_keypoints.argtypes = [vp, vp, i32, vp, vp, i32, vp]
     lib.orbx_undistort_keypoints_device.argtypes = [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]
@@ -593,6 +597,35 @@ class ORBmatcher:
                                                               _tp(m12), _tp(nm), s))
         return m12, nm
 
+    def SearchForTriangulation_pairs_device(self, store: "KfStore", pairs, geom, sigma2_2, scale_2, max_fv_nodes,
+                                            has_mp=None, uright=None, bOnlyStereo=False, stream=None):
+        """SearchForTriangulation for many (kf1, kf2) slot pairs of a device keyframe store in one launch
+        (LocalMapping::CreateNewMapPoints' neighbour loop, src/LocalMapping.cc:243-274).  pairs: (P, 2) int32; geom:
+        (P, 12) float32 rows = F12 (row-major 3x3), epipole ex, ey, pad; has_mp / uright: (slots, capacity) uint8 /
+        float32 device tensors, or (1, capacity) for one row shared by all slots (None = the store's valid field / no
+        stereo).  Returns (match12 (P, capacity) int32, nmatches (P,) int32) device tensors."""
+        import torch
+        P, cap = pairs.shape[0], store.capacity
+        dev = pairs.device
+        assert geom.shape == (P, 12) and geom.dtype == torch.float32 and geom.is_contiguous()
+        m12 = torch.empty((P, cap), dtype=torch.int32, device=dev)
+        nm = torch.empty((P,), dtype=torch.int32, device=dev)
+        s2 = np.ascontiguousarray(sigma2_2, np.float32)
+        sc = np.ascontiguousarray(scale_2, np.float32)
+
+        def rows(t, dt):
+            if t is None:
+                return None, 0
+            assert t.dtype == dt and t.is_contiguous() and t.shape[-1] >= cap
+            return t, (0 if t.shape[0] == 1 else t.stride(0) * t.element_size())
+        mp, mps = rows(has_mp, torch.uint8)
+        ur, urs = rows(uright, torch.float32)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream)
+        _check(self._lib.orbx_search_for_triangulation_pairs_device(
+            self._h, C.byref(store), _tp(mp) if mp is not None else None, mps, _tp(ur) if ur is not None else None, urs,
+            _tp(pairs), _tp(geom), P, int(max_fv_nodes), _p(s2), _p(sc), len(s2), int(bOnlyStereo), _tp(m12), _tp(nm), s))
+        return m12, nm
+
     def SearchByBoW_KF_F(self, desck, anglek, validk, fvk, descf, anglef, fvf):
         """ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) (src/ORBmatcher.cc:161-290).  Returns
         (nmatches, matchF) with matchF[iF] = KF index or -1."""
@@ -686,6 +719,24 @@ class ORBmatcher:
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(offsets.device).cuda_stream)
         _check(self._lib.orbx_distinctive_descriptors_store_device(self._h, C.byref(store), _tp(obs), _tp(offsets), M,
                                                                    _tp(best), _tp(out), s))
+        return best[:M], out[:M]
+
+    def distinctive_descriptors_neighbours_device(self, store: "KfStore", new_slots, neighbours, match12, stream=None):
+        """MapPoints of new keyframes, lists = multiagent.neighbour_observations' (read from match12 in place):
+        new_slots (n,), neighbours (n, nn), match12 (n, nn, capacity) int32 device tensors.  Returns (best (n*cap,),
+        descriptors (n*cap, 32))."""
+        import torch
+        n, nn = neighbours.shape
+        M = n * store.capacity
+        for t in (new_slots, neighbours, match12):
+            assert t.dtype == torch.int32 and t.is_contiguous()
+        assert match12.shape == (n, nn, store.capacity)
+        best = torch.empty((max(M, 1),), dtype=torch.int32, device=new_slots.device)
+        out = torch.empty((max(M, 1), 32), dtype=torch.uint8, device=new_slots.device)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(new_slots.device).cuda_stream)
+        _check(self._lib.orbx_distinctive_descriptors_neighbours_device(self._h, C.byref(store), _tp(new_slots),
+                                                                        _tp(neighbours), n, nn, _tp(match12), _tp(best),
+                                                                        _tp(out), s))
         return best[:M], out[:M]
 
     # ---- projection / radius matchers (src/ORBmatcher.cc; SURVEY §8f row 2) ------------------------------

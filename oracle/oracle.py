@@ -130,6 +130,17 @@ def bf_match(q, t):
     return bi, b1, b2
 
 
+def distinctive_descriptors_flat(flat, off):
+    """distinctive_descriptors over a flat (total, 32) descriptor array and (M+1,) list offsets."""
+    flat = np.ascontiguousarray(flat, np.uint8).reshape(-1, 32)
+    off = np.ascontiguousarray(off, np.int32)
+    if not len(flat):
+        flat = np.zeros((1, 32), np.uint8)
+    best = np.zeros(max(len(off) - 1, 1), np.int32)
+    lib().orc_distinctive(_p(flat), _p(off), len(off) - 1, _p(best))
+    return best[:len(off) - 1]
+
+
 def distinctive_descriptors(lists):
     """MapPoint::ComputeDistinctiveDescriptors restated (oracle/orb_oracle.cpp orc_distinctive): best index per
     descriptor list (-1 for an empty list)."""

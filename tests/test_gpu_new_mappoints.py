@@ -1,0 +1,104 @@
+"""Batched CreateNewMapPoints matching (multiagent.NewMapPoints; src/LocalMapping.cc:213-274 and :440-448) on the
+device against the oracle: every (new keyframe, neighbour) pair equals ORBmatcher::SearchForTriangulation
+(src/ORBmatcher.cc:659-825) run on that pair alone with ORBmatcher(0.6, false), and the distinctive descriptors of the
+new keyframes' MapPoints equal MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:257-317) over the same
+observation lists.  Keyframes: extracted left / shifted-right views of synthetic scenes, poses with a stereo-like
+baseline and small rotations, random MapPoint flags and right coordinates."""
+import numpy as np
+import pytest
+import torch
+
+from multiagent_orb_slam2_amd import multiagent as MA
+from multiagent_orb_slam2_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _rot(w):
+    th = float(np.linalg.norm(w))
+    k = w / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+
+
+@pytest.mark.parametrize("mode", ["flags", "store_valid", "only_stereo"])
+def test_new_mappoints_vs_oracle(gpu, mode):
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    n, rows, cols = 6, 240, 480
+    left = [S.kitti_like_image(70 + i, rows=rows, cols=cols) for i in range(n)]
+    right = [S.shifted_right_view(l, 70 + i, max_disp=16) for i, l in enumerate(left)]
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7)
+    kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(np.stack(left + right)).cuda())
+    cap, dev = kps.shape[1], kps.device
+    voc = S.synthetic_vocabulary(17, k=10, L=4)
+    v = pkg.ORBVocabulary.from_arrays(voc)
+    fv = v.transform_batch_device(desc, cnt, 2)
+    rng = np.random.default_rng(5)
+    valid = (torch.arange(cap, device=dev)[None, :] < cnt[:, None]).to(torch.uint8)
+    if mode == "store_valid":
+        valid &= torch.from_numpy((rng.random((2 * n, cap)) < 0.3).astype(np.uint8)).to(dev)
+    store = pkg.KfStore.from_fields(cap, desc=(desc, cap * 32), kps=(kps, cap * 28), valid=(valid, cap),
+                                    fv_nodes=(fv["fv_nodes"], cap * 4), fv_offsets=(fv["fv_offsets"], (cap + 1) * 4),
+                                    fv_indices=(fv["fv_indices"], cap * 4), n_fv=(fv["n_fv"], 4))
+    has_mp = None if mode == "store_valid" else \
+        torch.from_numpy((rng.random((2 * n, cap)) < 0.3).astype(np.uint8)).to(dev)
+    ur = torch.from_numpy(np.where(rng.random((2 * n, cap)) < 0.6, rng.uniform(0, cols, (2 * n, cap)), -1)
+                          .astype(np.float32)).to(dev)
+    # poses: left view s at (0.4 s, 0, 0.8 s), right view 0.54 m to its right; small rotations
+    K = np.array([[718.856, 0, 240.0], [0, 718.856, 120.0], [0, 0, 1]])
+    R = np.stack([_rot(rng.normal(0, 0.02, 3) + 1e-9) for _ in range(2 * n)])
+    Ow = np.array([[0.4 * s, 0.0, 0.8 * s] for s in range(n)] + [[0.4 * s + 0.54, 0.01, 0.8 * s] for s in range(n)])
+    t = -np.einsum("kij,kj->ki", R, Ow)
+    new = torch.tensor([n + s for s in range(4)], dtype=torch.int32, device=dev)       # right views 0..3 are new
+    nb = torch.tensor([[s, (s + 1) % n, n + (s + 1) % n, (s + 2) % n, -1] for s in range(4)], dtype=torch.int32,
+                      device=dev)
+    k1 = new.view(-1, 1).expand_as(nb)
+    geom = MA.triangulation_geometry(torch.tensor(K, device=dev), torch.tensor(R, device=dev),
+                                     torch.tensor(t, device=dev), torch.stack([k1, nb], 2).view(-1, 2)).view(4, 5, 12)
+    scale = np.array([1.2 ** i for i in range(8)], np.float32)
+    sigma2 = (scale * scale).astype(np.float32)
+    stage = MA.NewMapPoints(store, cap, sigma2, scale, only_stereo=(mode == "only_stereo"))
+    m12, nm, best, bdesc = stage.run(new, nb, geom, has_mp=has_mp, uright=ur)
+    # the same lists materialised (CSR on the device) through the generic store path
+    obs, off = MA.neighbour_observations(new, nb, m12)
+    best2, bdesc2 = stage.matcher.distinctive_descriptors_store_device(store, obs, off)
+    torch.cuda.synchronize()
+    assert torch.equal(best, best2) and torch.equal(bdesc, bdesc2)
+
+    kh, dh, ch = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+    mph = (has_mp if has_mp is not None else valid).cpu().numpy()
+    urh, gh = ur.cpu().numpy(), geom.cpu().numpy()
+    fvh = {k: t_.cpu().numpy() for k, t_ in fv.items()}
+
+    def view(s):
+        c = int(ch[s])
+        nf = int(fvh["n_fv"][s])
+        offs = fvh["fv_offsets"][s, :nf + 1]
+        f = (fvh["fv_nodes"][s, :nf].astype(np.uint32), offs, fvh["fv_indices"][s, :offs[-1]])
+        return dh[s, :c], kh[s, :c].copy().view(pkg.KP_DTYPE).reshape(-1), mph[s, :c], urh[s, :c], f
+
+    m12h, nmh, nbh = m12.cpu().numpy(), nm.cpu().numpy(), nb.cpu().numpy()
+    total, lists = 0, []
+    for j in range(4):
+        q = n + j
+        for k in range(5):
+            c = int(nbh[j, k])
+            if c < 0:
+                assert nmh[j, k] == 0 and (m12h[j, k] == -1).all()
+                continue
+            F = gh[j, k, :9].reshape(3, 3)
+            rn, rm = O.search_for_triangulation(*view(q), *view(c), F, sigma2, scale, float(gh[j, k, 9]),
+                                                float(gh[j, k, 10]), mode == "only_stereo", False)
+            assert nmh[j, k] == rn and np.array_equal(m12h[j, k, :int(ch[q])], rm), (q, c)
+            assert (m12h[j, k, int(ch[q]):] == -1).all()
+            total += rn
+        for i in range(cap):
+            rows_ = [dh[q, i]] + [dh[int(nbh[j, k]), m12h[j, k, i]] for k in range(5) if m12h[j, k, i] >= 0]
+            lists.append(np.stack(rows_))
+    assert total >= 20, total
+    ref = O.distinctive_descriptors(lists)
+    assert np.array_equal(best.cpu().numpy(), ref)
+    bd = bdesc.cpu().numpy()
+    for p, l in enumerate(lists):
+        assert np.array_equal(bd[p], l[ref[p]])
