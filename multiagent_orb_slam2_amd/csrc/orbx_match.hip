@@ -208,13 +208,35 @@ struct StereoArgs {
 
 // Counting sort of one image pair's right keypoints by row (the row table of Frame.cc:476-493, kept as
 // a bucket per floor(y) instead of one list per covered row); order inside a bucket is irrelevant
-// because the search below reduces with a (distance, index) minimum.
-__global__ __launch_bounds__(1024) void k_stereo_rows(StereoArgs A) {
+// because the search below reduces with a (distance, index) minimum.  blockIdx.y = 1: the left keypoints'
+// buckets, in a workgroup of their own.
+#ifndef ORBX_STEREO_ROWS_T
+#define ORBX_STEREO_ROWS_T 256
+#endif
+constexpr int kStereoRowsThreads = ORBX_STEREO_ROWS_T;
+__global__ __launch_bounds__(kStereoRowsThreads) void k_stereo_rows(StereoArgs A) {
     extern __shared__ int cnt[];   // rows + 1
     __shared__ int tmp[40];
     const int img = blockIdx.x, tid = threadIdx.x;
-    const int nr = A.nr ? A.nr[img] : A.nr_fixed;
     const size_t ob = (size_t)img * A.capacity;
+    if (blockIdx.y == 1) {
+        if (!A.lrow_start) return;
+        // the left keypoints by their own row (vRowIndices index (int)y, :511); rows outside the image go to the last
+        // bucket and find nothing (the search re-checks the row)
+        const int nl = A.nl ? A.nl[img] : A.nl_fixed;
+        for (int r = tid; r <= A.rows; r += blockDim.x) cnt[r] = 0;
+        __syncthreads();
+        for (int i = tid; i < nl; i += blockDim.x) atomicAdd(&cnt[min(max((int)A.kl[ob + i].y, 0), A.rows - 1)], 1);
+        __syncthreads();
+        block_scan_array(cnt, A.rows + 1, tmp);
+        int32_t* ls = A.lrow_start + (size_t)img * (A.rows + 1);
+        for (int r = tid; r <= A.rows; r += blockDim.x) ls[r] = cnt[r];
+        __syncthreads();
+        for (int i = tid; i < nl; i += blockDim.x)
+            A.lrow_idx[ob + atomicAdd(&cnt[min(max((int)A.kl[ob + i].y, 0), A.rows - 1)], 1)] = i;
+        return;
+    }
+    const int nr = A.nr ? A.nr[img] : A.nr_fixed;
     for (int r = tid; r <= A.rows; r += blockDim.x) cnt[r] = 0;
     __syncthreads();
     for (int i = tid; i < nr; i += blockDim.x) {
@@ -230,21 +252,6 @@ __global__ __launch_bounds__(1024) void k_stereo_rows(StereoArgs A) {
         const int r = min(max((int)floorf(A.kr[ob + i].y), 0), A.rows - 1);
         A.row_idx[ob + atomicAdd(&cnt[r], 1)] = i;
     }
-    if (!A.lrow_start) return;
-    // the left keypoints by their own row (vRowIndices index (int)y, :511); rows outside the image go to the last
-    // bucket and find nothing (the search re-checks the row)
-    __syncthreads();
-    const int nl = A.nl ? A.nl[img] : A.nl_fixed;
-    for (int r = tid; r <= A.rows; r += blockDim.x) cnt[r] = 0;
-    __syncthreads();
-    for (int i = tid; i < nl; i += blockDim.x) atomicAdd(&cnt[min(max((int)A.kl[ob + i].y, 0), A.rows - 1)], 1);
-    __syncthreads();
-    block_scan_array(cnt, A.rows + 1, tmp);
-    int32_t* ls = A.lrow_start + (size_t)img * (A.rows + 1);
-    for (int r = tid; r <= A.rows; r += blockDim.x) ls[r] = cnt[r];
-    __syncthreads();
-    for (int i = tid; i < nl; i += blockDim.x)
-        A.lrow_idx[ob + atomicAdd(&cnt[min(max((int)A.kl[ob + i].y, 0), A.rows - 1)], 1)] = i;
 }
 
 // Row-block form of the search: one workgroup per (image pair, kStereoRows rows of left keypoints).  The right
@@ -1509,7 +1516,8 @@ static int stereo_common(orbx_matcher* m, StereoArgs& A, const float* scale, int
 }
 
 static int stereo_launch(StereoArgs& A, int batch, int nl_max, hipStream_t s) {
-    hipLaunchKernelGGL(k_stereo_rows, dim3(batch), dim3(1024), (size_t)(A.rows + 1) * sizeof(int), s, A);
+    hipLaunchKernelGGL(k_stereo_rows, dim3(batch, A.lrow_start ? 2 : 1), dim3(kStereoRowsThreads),
+                       (size_t)(A.rows + 1) * sizeof(int), s, A);
     A.batch = batch;
     if (A.lrow_start) {                                   // row-block search (default)
         const int nblk = (A.rows + kStereoRows - 1) / kStereoRows;

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -74,21 +75,80 @@ __global__ __launch_bounds__(256) void k_vocab_words(VocabDev V, const uint8_t* 
     node[o] = nid;
 }
 
+// The same descent with 16 lanes per descriptor (4 per wave; branching factor k <= 16): lane j of a group scores
+// child j, and the group's (distance, j) minimum -- the first minimum, as the sequential strict '<' -- picks the
+// next node.  One level costs one round of independent loads (CSR row, child id, child descriptor) instead of k
+// dependent ones.
+__device__ __forceinline__ uint32_t group16_min(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_vocab_words16(VocabDev V, const uint8_t* __restrict__ desc,
+                                                       const int32_t* __restrict__ counts, int n_fixed, int stride,
+                                                       int nid_level, int32_t* __restrict__ word, double* __restrict__ wgt,
+                                                       int32_t* __restrict__ node) {
+    const int img = blockIdx.y;
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) >> 4, j = (int)threadIdx.x & 15;
+    const int n = counts ? counts[img] : n_fixed;
+    if (__builtin_amdgcn_read_exec() == 0) return;
+    const bool live = i < n;
+    const size_t o = (size_t)img * stride + (live ? i : 0);
+    const uint4* dp = reinterpret_cast<const uint4*>(desc + 32 * o);
+    const uint4 a0 = dp[0], a1 = dp[1];
+    int cur = 0, level = 0, nid = 0;
+    // every group of the wave walks the same number of levels only if the tree is balanced; groups that reached a
+    // leaf idle (their lanes keep the wave's DPP reductions well defined)
+    bool done = !live;
+    for (;;) {
+        int c0 = 0, c1 = 0;
+        if (!done) { c0 = V.child_off[cur]; c1 = V.child_off[cur + 1]; }
+        if (!done && c1 <= c0) done = true;                      // isLeaf
+        if (__builtin_amdgcn_read_exec() == __ballot(done)) break;
+        uint32_t key = 0xffffffffu;
+        int id = 0;
+        if (!done && c0 + j < c1) {
+            id = V.child[c0 + j];
+            key = ((uint32_t)hamming256(a0, a1, V.desc[2 * id], V.desc[2 * id + 1]) << 8) | (uint32_t)j;
+        }
+        const uint32_t best = group16_min(key);
+        const int bj = (int)(best & 0xff);
+        const int bid = __builtin_amdgcn_ds_bpermute(((int)(threadIdx.x & ~15u) + bj) << 2, id);
+        if (!done) {
+            ++level;
+            cur = bid;
+            if (level == nid_level) nid = cur;
+        }
+    }
+    if (live && j == 0) {
+        word[o] = V.word_id[cur];
+        wgt[o] = V.weight[cur];
+        node[o] = nid;
+    }
+}
+
 struct BowOut {
     uint32_t* words; double* values; int32_t* n_words;
     uint32_t* fv_nodes; int32_t* fv_off; int32_t* fv_idx; int32_t* n_fv;
 };
 
-__global__ __launch_bounds__(kVocabAggThreads) void k_vocab_aggregate(const int32_t* __restrict__ counts, int n_fixed, int stride,
+// kT threads, sets of <= kMaxSet descriptors: <1024, 4096> (49 KB of LDS) or, for sets of <= 2048, <256, 2048> (24 KB)
+// -- a workgroup the size of a FAST band's, so the keyframe batch's 2 x 25 workgroups find CU room beside the front
+// end instead of waiting for a CU with 1024 free lanes and 49 KB of LDS.
+template <int kT, int kMaxSet>
+__global__ __launch_bounds__(kT) void k_vocab_aggregate(const int32_t* __restrict__ counts, int n_fixed, int stride,
                                                                       const int32_t* __restrict__ word, const double* __restrict__ wgt,
                                                                       const int32_t* __restrict__ node, int weighting, int scoring,
                                                                       BowOut out) {
     // blockIdx.y = 0: FeatureVector of set blockIdx.x; 1: its BowVector (independent, so two workgroups per set)
-    __shared__ unsigned long long key[kVocabMaxSet];
-    __shared__ int flag[kVocabMaxSet + 1];
+    __shared__ unsigned long long key[kMaxSet];
+    __shared__ int flag[kMaxSet + 1];
     __shared__ int tmp[64];
     const int img = blockIdx.x, tid = threadIdx.x, T = blockDim.x;
-    const int n = min(counts ? counts[img] : n_fixed, kVocabMaxSet);
+    const int n = min(counts ? counts[img] : n_fixed, kMaxSet);
     const size_t o = (size_t)img * stride;
     int P2 = 1;
     while (P2 < n) P2 <<= 1;
@@ -130,7 +190,7 @@ __global__ __launch_bounds__(kVocabAggThreads) void k_vocab_aggregate(const int3
     const int nwords = block_scan_array(flag, P2, tmp);
     // per word: its weight accumulated in feature order (addWeight: one += per further occurrence), kept in
     // registers until every thread is done reading key[], then written over key[] as doubles
-    constexpr int kPer = kVocabMaxSet / kVocabAggThreads;
+    constexpr int kPer = kMaxSet / kT;
     double myv[kPer];
     int myslot[kPer];
 #pragma unroll
@@ -191,6 +251,9 @@ __global__ __launch_bounds__(kVocabAggThreads) void k_vocab_aggregate(const int3
 struct Vocab {
     int k = 0, L = 0, scoring = 0, weighting = 0, device = 0;
     int n_nodes = 0, n_words = 0;
+    bool agg_wide = std::getenv("ORBX_VOCAB_AGG_WIDE") != nullptr;   // diagnostics: 1024-thread aggregation always
+    int max_children = 0;              // the descent uses 16-lane groups when every node has <= 16 children
+    bool words_scalar = std::getenv("ORBX_VOCAB_SCALAR") != nullptr;   // diagnostics: one thread per descriptor
     hipStream_t stream = nullptr;      // lazy: own() on first host-API use
     std::once_flag stream_once;
     hipStream_t own() { return lazy_stream(stream, stream_once, device); }
@@ -227,6 +290,8 @@ static int vocab_build(Vocab* v, int n_lines, const int32_t* parent, const uint8
         ch.insert(ch.end(), children[id].begin(), children[id].end());
     }
     off[N] = (int)ch.size();
+    v->max_children = 0;
+    for (int id = 0; id < N; ++id) v->max_children = std::max(v->max_children, (int)children[id].size());
     const size_t bd = (size_t)N * 32, bo = 4 * ((size_t)N + 1), bc = 4 * std::max<size_t>(ch.size(), 1), bw = 8 * (size_t)N,
                  bwi = 4 * (size_t)N;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -276,11 +341,19 @@ static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 static int vocab_launch(orbx_vocab* v, const uint8_t* d_desc, const int32_t* d_counts, int n_fixed, int batch, int stride,
                         int levelsup, int32_t* d_word, double* d_wgt, int32_t* d_node, BowOut out, hipStream_t s, bool aggregate) {
     const int nid_level = v->L - levelsup;   // nid_level <= 0 -> root (node 0), as :1226
-    hipLaunchKernelGGL(k_vocab_words, dim3((stride + 255) / 256, batch), dim3(256), 0, s, v->dev, d_desc, d_counts, n_fixed,
-                       stride, nid_level > 0 ? nid_level : -1, d_word, d_wgt, d_node);
+    if (v->max_children <= 16 && !v->words_scalar)
+        hipLaunchKernelGGL(k_vocab_words16, dim3((stride + 15) / 16, batch), dim3(256), 0, s, v->dev, d_desc, d_counts, n_fixed,
+                           stride, nid_level > 0 ? nid_level : -1, d_word, d_wgt, d_node);
+    else
+        hipLaunchKernelGGL(k_vocab_words, dim3((stride + 255) / 256, batch), dim3(256), 0, s, v->dev, d_desc, d_counts, n_fixed,
+                           stride, nid_level > 0 ? nid_level : -1, d_word, d_wgt, d_node);
     if (aggregate)
-        hipLaunchKernelGGL(k_vocab_aggregate, dim3(batch, 2), dim3(kVocabAggThreads), 0, s, d_counts, n_fixed, stride, d_word,
+    {
+        const bool small = stride <= 2048 && !v->agg_wide;
+        auto kagg = small ? k_vocab_aggregate<256, 2048> : k_vocab_aggregate<kVocabAggThreads, kVocabMaxSet>;
+        hipLaunchKernelGGL(kagg, dim3(batch, 2), dim3(small ? 256 : kVocabAggThreads), 0, s, d_counts, n_fixed, stride, d_word,
                            d_wgt, d_node, v->weighting, v->scoring, out);
+    }
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }
