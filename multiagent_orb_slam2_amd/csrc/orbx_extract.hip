@@ -391,10 +391,10 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
     asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return as_h2(r);
 }
+// the 16 circle taps + centre of a pixel pair on the f16-biased pair image (pair words; odd offsets by v_alignbit)
 template <int kPairStride>
-__device__ __forceinline__ s16x2 fast_score2_f16(const uint32_t* __restrict__ E, int y, int j) {
+__device__ __forceinline__ void fast_taps_f16(const uint32_t* __restrict__ E, int y, int j, uint32_t (&r)[17]) {
     const uint32_t* eb = E + (y - 3) * kPairStride + j;
-    uint32_t r[17];
 #define ORBX_TAP(k, dx, dy) \
     r[k] = ((dx) & 1) ? eb[((dy) + 3) * kPairStride + (3 + (dx)) / 2] : o_at<true>(eb, eb, ((dy) + 3) * kPairStride + 1 + (dx) / 2)
     ORBX_TAP(16, 0, 0);
@@ -403,6 +403,17 @@ __device__ __forceinline__ s16x2 fast_score2_f16(const uint32_t* __restrict__ E,
     ORBX_TAP(8, 0, -3);   ORBX_TAP(9, -1, -3);  ORBX_TAP(10, -2, -2); ORBX_TAP(11, -3, -1);
     ORBX_TAP(12, -3, 0);  ORBX_TAP(13, -3, 1);  ORBX_TAP(14, -2, 2);  ORBX_TAP(15, -1, 3);
 #undef ORBX_TAP
+}
+__device__ __forceinline__ s16x2 fast_score_from_taps_f16(const uint32_t (&r)[17]);
+
+template <int kPairStride>
+__device__ __forceinline__ s16x2 fast_score2_f16(const uint32_t* __restrict__ E, int y, int j) {
+    uint32_t r[17];
+    fast_taps_f16<kPairStride>(E, y, j, r);
+    return fast_score_from_taps_f16(r);
+}
+
+__device__ __forceinline__ s16x2 fast_score_from_taps_f16(const uint32_t (&r)[17]) {
     const h16x2 v = as_h2(r[16]);
     h16x2 d[16];
 #pragma unroll
@@ -1094,6 +1105,237 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ p
         cell_cnt[(size_t)img * ncells + bd.cell0 + tid] = cnt;
     }
     FBP(5);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_fast_wave: one WAVE per (image, cell) -- ComputeKeyPointsOctTree's per-cell FAST (:789-829) with no workgroup
+// barrier.  OpenCV's FAST runs on the cell ROI, so a cell is self-contained: its ROI (detection window + 3) goes into the
+// wave's own LDS slice as the f16-biased pair image of k_fast_band, the compass pre-test runs in quads (4 pixel pairs per
+// lane), the survivors are compacted in row-major order by wave ballots (no atomics), scored in closed form, and the
+// strict 3x3 NMS at iniThFAST and minThFAST appends the kept pixels to two key lists by ballot rank -- so the lists are
+// already in OpenCV's row-major output order and a kept pixel's slot is its list index (no rank pass).  The cell's
+// count selects the iniTh list, or the minTh list when nothing was kept at iniTh (:812-816).  Phases of one wave are
+// ordered by the in-order LDS queue (wavefront fences keep the compiler from reordering across them); the waves of a
+// workgroup never wait for each other.
+// ---------------------------------------------------------------------------------------------
+struct WaveLds {               // per-wave slice of k_fast_wave's dynamic LDS (byte offsets inside the slice)
+    int o_sc, o_list, bytes;   // E pair image at 0 (the NMS key lists reuse it), score map, survivor list; slice size
+};
+// rows: max ROI rows; sw: max score-map row (int16); np: max pixel pairs; ps: dwords per pair-image row
+__host__ __device__ __forceinline__ WaveLds wave_lds(int rows, int sw, int np, int ps) {
+    WaveLds b;
+    int o = rows * ps * 4;
+    b.o_sc = o;   o += ((rows - 4) * sw * 2 + 15) & ~15;
+    b.o_list = o; o += (np * 2 + 15) & ~15;
+    b.bytes = o;
+    return b;
+}
+
+// Compass pre-test of quad (rr, u) of a cell (pairs 4u .. 4u+3 of detection row rr) at threshold t; also writes the
+// quad's score-map words (0, or -1 for the missing second pixel of an odd-width row).  As k_fast_band's quad_test.
+struct QuadTaps { uint32_t A[7], U[6], D[6]; };   // E words of rows y (7), y-3 and y+3 (5 each) of one quad
+
+template <int kPS>
+__device__ __forceinline__ QuadTaps fastw_quad_load(const uint32_t* __restrict__ E, int rr, int u) {
+    const uint32_t* e0 = E + rr * kPS + 4 * u;                       // row y-3 (16-byte aligned)
+    const uint32_t* e1 = e0 + 3 * kPS;                               // row y
+    const uint32_t* e2 = e0 + 6 * kPS;                               // row y+3
+    QuadTaps q;
+    const uint4 a = *reinterpret_cast<const uint4*>(e1);
+    const uint2 b = *reinterpret_cast<const uint2*>(e1 + 4);
+    q.A[0] = a.x; q.A[1] = a.y; q.A[2] = a.z; q.A[3] = a.w; q.A[4] = b.x; q.A[5] = b.y; q.A[6] = e1[6];
+    const uint2 u23 = *reinterpret_cast<const uint2*>(e0 + 2), u45 = *reinterpret_cast<const uint2*>(e0 + 4);
+    q.U[0] = 0; q.U[1] = e0[1]; q.U[2] = u23.x; q.U[3] = u23.y; q.U[4] = u45.x; q.U[5] = u45.y;
+    const uint2 d23 = *reinterpret_cast<const uint2*>(e2 + 2), d45 = *reinterpret_cast<const uint2*>(e2 + 4);
+    q.D[0] = 0; q.D[1] = e2[1]; q.D[2] = d23.x; q.D[3] = d23.y; q.D[4] = d45.x; q.D[5] = d45.y;
+    return q;
+}
+
+// test of a loaded quad
+__device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, int t, int PR, int Wd) {
+    const uint32_t *A = q.A, *U = q.U, *D = q.D;
+    uint32_t mq = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 4 * u + k;
+        const s16x2 v = as_s2(align16(A[k + 2], A[k + 1]));             // pixels of pair j
+        const s16x2 d0 = v - as_s2(align16(D[k + 2], D[k + 1]));        // ( 0,  3)
+        const s16x2 d4 = v - as_s2(A[k + 3]);                           // ( 3,  0)
+        const s16x2 d8 = v - as_s2(align16(U[k + 2], U[k + 1]));        // ( 0, -3)
+        const s16x2 d12 = v - as_s2(A[k]);                              // (-3,  0)
+        const s16x2 dk = pmax(pmax(pmin(d0, d4), pmin(d4, d8)), pmax(pmin(d8, d12), pmin(d12, d0)));
+        const s16x2 br = pmin(pmin(pmax(d0, d4), pmax(d4, d8)), pmin(pmax(d8, d12), pmax(d12, d0)));
+        const s16x2 m = pmax(dk, (s16x2)(0) - br);
+        const bool two = 2 * j + 1 < Wd;
+        const int pm = j < PR ? (two ? 3 : 1) : 0;
+        const int pt = ((m.x > t ? 1 : 0) | (m.y > t ? 2 : 0)) & pm;
+        mq |= (pt != 0 ? 1u : 0u) << k;
+    }
+    return mq;
+}
+
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
+// score-map row stride (int16) per pair stride: >= (Wd + 5) & ~1 for every cell the pair stride admits
+__host__ __device__ constexpr int fastw_sw(int ps) { return ps == 20 ? 36 : ps == 24 ? 44 : 76; }
+
+template <int kPS, int kWpg>
+__global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                         const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
+                                                         int cell0, int ncell, int iniTh, int minTh,
+                                                         uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
+                                                         int cand_stride, int* __restrict__ cell_cnt, int ncells, int batch,
+                                                         Src0 s0, WaveLds lay, int kcap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
+    const int w = threadIdx.x >> 6, ln = lane_id();
+    const int total = ncell * batch, nwg = (total + kWpg - 1) / kWpg;
+    const int wg = xcd_item(xcd_chunk(nwg));                        // cells of one image on one XCD
+    const int item = __builtin_amdgcn_readfirstlane(wg * kWpg + w);
+    if (wg >= nwg || item >= total) return;                         // whole wave (no barrier in this kernel)
+    const int img = item / ncell, c = cell0 + (item - img * ncell);
+    char* lds = reinterpret_cast<char*>(fsm) + w * lay.bytes;
+    uint32_t* E = reinterpret_cast<uint32_t*>(lds);
+    int16_t* sc = reinterpret_cast<int16_t*>(lds + lay.o_sc);
+    uint16_t* list = reinterpret_cast<uint16_t*>(lds + lay.o_list);
+    const CellDev cd = cells[c];
+    const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
+    int* cnt_out = cell_cnt + (size_t)img * ncells + c;
+    if (Wd <= 0 || Hd <= 0) {
+        if (ln == 0) *cnt_out = 0;
+        return;
+    }
+    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
+    const int tp = min(T1, T2);
+    constexpr int SW = fastw_sw(kPS);
+    {
+        // 1. cell ROI -> f16-biased pair image: lane items (row, 8-column chunk), one 8-byte load each, all of a round
+        //    issued before the first use; bytes past the ROI's width read as 0
+        const LevelDev& L = levels[cd.level];
+        int lstride;
+        const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
+        const uint8_t* src0 = base + (size_t)cd.y0 * lstride + cd.x0;
+        const int cpr = (W + 7) >> 3, NQ = H * cpr;
+        const int dr = kWave / cpr, dc = kWave - dr * cpr;          // item q -> q + 64 (no division per item)
+        int r = ln / cpr, cc = ln - r * cpr;
+        constexpr int kPf = 6;
+        for (int q0 = 0; q0 < NQ; q0 += kPf * kWave) {
+            uint32_t pf[2 * kPf];
+            int rs[kPf], cs[kPf];
+#pragma unroll
+            for (int k = 0; k < kPf; ++k) {
+                const int q = q0 + ln + k * kWave;
+                rs[k] = r; cs[k] = cc;
+                r += dr; cc += dc;
+                if (cc >= cpr) { cc -= cpr; ++r; }
+                pf[2 * k] = pf[2 * k + 1] = 0;
+                if (q < NQ) __builtin_memcpy(&pf[2 * k], src0 + (size_t)rs[k] * lstride + 8 * cs[k], 8);
+            }
+#pragma unroll
+            for (int k = 0; k < kPf; ++k) {
+                if (q0 + ln + k * kWave < NQ) {
+                    uint32_t lo = pf[2 * k], hi = pf[2 * k + 1];
+                    const int keep = W - 8 * cs[k];
+                    if (keep < 8) {
+                        const uint64_t m = (1ull << (8 * keep)) - 1ull;        // keep >= 1
+                        const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
+                        lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+                    }
+                    const uint4 e = make_uint4(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u) | 0x64006400u,
+                                               __builtin_amdgcn_perm(hi, lo, 0x0c030c02u) | 0x64006400u,
+                                               __builtin_amdgcn_perm(hi, lo, 0x0c050c04u) | 0x64006400u,
+                                               __builtin_amdgcn_perm(hi, lo, 0x0c070c06u) | 0x64006400u);
+                    *reinterpret_cast<uint4*>(E + rs[k] * kPS + 4 * cs[k]) = e;
+                }
+            }
+        }
+        // score map cleared to 0: pixels that fail the pre-test and the pad ring (a 0 never blocks a kept score >= 1)
+        const int n16 = ((Hd + 2) * SW * 2 + 15) >> 4;
+        for (int i = ln; i < n16; i += kWave) reinterpret_cast<uint4*>(sc)[i] = make_uint4(0, 0, 0, 0);
+    }
+    wave_fence();
+    const uint64_t below = (1ull << ln) - 1ull;
+    // 2. compass pre-test at min(iniTh, minTh) in quads; survivors compacted in row-major order
+    const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
+    int ns = 0;                                                       // wave-uniform
+    {
+        // quad q -> (row q / QR, column q % QR), walked incrementally; two quads per lane per round (q, q + 64), both
+        // read before either is tested.  Survivors are appended in quad order (row-major).
+        const int dr = kWave / QR, du = kWave - dr * QR;
+        int rr = ln / QR, u = ln - rr * QR;
+        auto step = [&](int& r0, int& u0) { r0 += dr; u0 += du; if (u0 >= QR) { u0 -= QR; ++r0; } };
+        auto emit = [&](uint32_t mq, int r0, int u0) {
+            const int cq = __builtin_popcount(mq);
+            const uint64_t b0 = __ballot(cq & 1), b1 = __ballot(cq & 2), b2 = __ballot(cq & 4);
+            int pos = ns + __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((mq >> k) & 1u) list[pos++] = (uint16_t)((r0 << 8) | (4 * u0 + k));
+            ns += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+        };
+        for (int q0 = 0; q0 < NQ4; q0 += 2 * kWave) {
+            const int qa = q0 + ln, qb = qa + kWave;
+            const int ra = rr, ua = u;
+            step(rr, u);
+            const int rb = rr, ub = u;
+            step(rr, u);
+            const bool va = qa < NQ4, vb = qb < NQ4;
+            const QuadTaps ta = fastw_quad_load<kPS>(E, va ? ra : 0, va ? ua : 0);
+            const QuadTaps tb = fastw_quad_load<kPS>(E, vb ? rb : 0, vb ? ub : 0);
+            const uint32_t ma = va ? fastw_quad_test(ta, ua, tp, PR, Wd) : 0u;
+            const uint32_t mb = vb ? fastw_quad_test(tb, ub, tp, PR, Wd) : 0u;
+            emit(ma, ra, ua);
+            emit(mb, rb, ub);
+        }
+    }
+    wave_fence();
+    // 3. closed-form scores of the survivors, two per lane per round (both tap sets read before either is scored)
+    for (int i = ln; i < ns; i += 2 * kWave) {
+        const int i2 = i + kWave;
+        const uint32_t e1 = list[i], e2 = i2 < ns ? list[i2] : e1;
+        const int rr1 = e1 >> 8, j1 = e1 & 0xff, rr2 = e2 >> 8, j2 = e2 & 0xff;
+        uint32_t t1[17], t2[17];
+        fast_taps_f16<kPS>(E, rr1 + 3, j1, t1);
+        fast_taps_f16<kPS>(E, rr2 + 3, j2, t2);
+        const s16x2 s1 = fast_score_from_taps_f16(t1), s2 = fast_score_from_taps_f16(t2);
+        *(s16x2*)(sc + (rr1 + 1) * SW + 2 + 2 * j1) = (2 * j1 + 1 < Wd) ? s1 : (s16x2){s1.x, (short)-1};
+        if (i2 < ns) *(s16x2*)(sc + (rr2 + 1) * SW + 2 + 2 * j2) = (2 * j2 + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
+    }
+    wave_fence();
+    // 4. strict 3x3 NMS at iniTh (bits 0, 1) and minTh (bits 2, 3); kept pixels appended in list order (= row-major)
+    //    to the two key lists, which take over the pair image's LDS (key = row * 128 + column in the detection window)
+    uint16_t* k1 = reinterpret_cast<uint16_t*>(E);
+    uint16_t* k2 = k1 + kcap;
+    int n1 = 0, n2 = 0;                                               // wave-uniform
+    for (int i0 = 0; i0 < ns; i0 += kWave) {
+        const int i = i0 + ln;
+        int f = 0, key = 0;
+        if (i < ns) {
+            const int rr = list[i] >> 8, j = list[i] & 0xff;
+            f = nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd);
+            key = rr * 128 + 2 * j;
+        }
+        const uint64_t a0 = __ballot(f & 1), a1 = __ballot(f & 2), c0 = __ballot(f & 4), c1 = __ballot(f & 8);
+        int p1 = n1 + __popcll(a0 & below) + __popcll(a1 & below);
+        int p2 = n2 + __popcll(c0 & below) + __popcll(c1 & below);
+        if (f & 1) { if (p1 < kcap) k1[p1] = (uint16_t)key; ++p1; }
+        if ((f & 2) && p1 < kcap) k1[p1] = (uint16_t)(key + 1);
+        if (f & 4) { if (p2 < kcap) k2[p2] = (uint16_t)key; ++p2; }
+        if ((f & 8) && p2 < kcap) k2[p2] = (uint16_t)(key + 1);
+        n1 += __popcll(a0) + __popcll(a1);
+        n2 += __popcll(c0) + __popcll(c1);
+    }
+    wave_fence();
+    // 5. the cell's list (iniTh, or minTh when iniTh kept nothing: :812-816) -> its candidate slots, coalesced
+    const uint16_t* ks = n1 > 0 ? k1 : k2;
+    const int n = min(n1 > 0 ? n1 : n2, min(kcap, cd.slot_cap));
+    uint32_t* oxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
+    uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
+    for (int i = ln; i < n; i += kWave) {
+        const int k = ks[i], rr = k >> 7, x = k & 127;
+        oxy[i] = (uint32_t)(cd.x0 + 3 + x) | ((uint32_t)(cd.y0 + rr + 3) << 16);
+        os[i] = (uint8_t)sc[(rr + 1) * SW + 2 + x];
+    }
+    if (ln == 0) *cnt_out = n;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2311,6 +2553,213 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_describe_fb: k_describe_m<2> with the GaussianBlur (:1085-1086) done per keypoint in LDS -- no blurred pyramid.
+//
+// A keypoint's BRIEF tests read the blurred level only inside the 37 x 37 window around it (|rotated offset| <= 18), and
+// those blurred pixels depend on the raw level inside a 43 x 43 window (7 x 7 kernel).  Each keypoint's 32 lanes load
+// the raw rows cy-21 .. cy+21, columns cx-23 .. cx+24 (6 chunks of 8 bytes per row, the IC_Angle box cx-15 .. cx+16 =
+// chunks 1..4 of rows 6..36, so the moments come straight from the loaded registers), store them in the keypoint's LDS
+// slice, and blur them there with the pinned arithmetic of k_blur7 (horizontal sums as packed u16, column pass
+// (acc + 2^15) >> 16 saturated; REFLECT_101 applied to the raw coordinates of windows that cross the level border,
+// which is the same as reflecting per axis): 30 lanes each own 4 output columns x 12-13 output rows.  The BRIEF tests
+// then read the blurred window exactly as k_describe_m does.  Bit-identical to k_blur7 + k_describe_m; the blurred
+// pyramid's HBM write and the describe's gather of it are gone (one raw window per keypoint is read instead).
+// ---------------------------------------------------------------------------------------------
+constexpr int kFbRows = 2 * kBriefR + 7;          // 43 raw rows: cy-21 .. cy+21
+constexpr int kFbRow = 48;                        // raw bytes per row: cx-23 .. cx+24
+constexpr int kFbChunks = kFbRows * (kFbRow / 8); // 258 8-byte chunks
+constexpr int kFbRaw = kFbRows * kFbRow;          // 2064 bytes
+
+// horizontal sums of the 4 output columns whose 12-byte window starts one byte before blur_hrow's (x0 - 5)
+__device__ __forceinline__ BlurRow blur_hrow5(uint32_t w0, uint32_t w1, uint32_t w2) {
+    const u16x2 P0 = byte_pair<2>(w0, w1, w2), P1 = byte_pair<3>(w0, w1, w2), P2 = byte_pair<4>(w0, w1, w2);
+    const u16x2 P3 = byte_pair<5>(w0, w1, w2), P4 = byte_pair<6>(w0, w1, w2), P5 = byte_pair<7>(w0, w1, w2);
+    const u16x2 P6 = byte_pair<8>(w0, w1, w2), P7 = byte_pair<9>(w0, w1, w2), P8 = byte_pair<10>(w0, w1, w2);
+    const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
+    BlurRow o;
+    o.h01 = (P0 + P6) * k18 + (P1 + P5) * k34 + (P2 + P4) * k49 + P3 * k55;
+    o.h23 = (P2 + P8) * k18 + (P3 + P7) * k34 + (P4 + P6) * k49 + P5 * k55;
+    return o;
+}
+
+__device__ __forceinline__ uint32_t blur_emit4(const BlurRow& a, const BlurRow& b, const BlurRow& c, const BlurRow& d,
+                                               const BlurRow& e, const BlurRow& f, const BlurRow& g) {
+    const uint32_t o0 = blur_col(a.h01.x, b.h01.x, c.h01.x, d.h01.x, e.h01.x, f.h01.x, g.h01.x);
+    const uint32_t o1 = blur_col(a.h01.y, b.h01.y, c.h01.y, d.h01.y, e.h01.y, f.h01.y, g.h01.y);
+    const uint32_t o2 = blur_col(a.h23.x, b.h23.x, c.h23.x, d.h23.x, e.h23.x, f.h23.x, g.h23.x);
+    const uint32_t o3 = blur_col(a.h23.y, b.h23.y, c.h23.y, d.h23.y, e.h23.y, f.h23.y, g.h23.y);
+    return o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
+}
+
+__global__ __launch_bounds__(256) void k_describe_fb(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                     const LevelDev* __restrict__ levels, int nlevels,
+                                                     const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
+                                                     int out_stride, const int* __restrict__ level_cnt,
+                                                     orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                     int32_t* __restrict__ counts, int capacity, int slot0, int nslots,
+                                                     int write_count, int batch, Src0 s0, SlotTable tab, unsigned seq,
+                                                     int* __restrict__ err) {
+    constexpr int kKpw = 2, kLp = kWave / kKpw;
+    constexpr int kNW = (kFbChunks + kLp - 1) / kLp;             // 9 raw chunks per lane
+    constexpr int kNT = 256 / kLp;                               // BRIEF tests per lane
+    __shared__ __attribute__((aligned(16))) uint8_t raw_lds[4 * kKpw * kFbRaw];
+    __shared__ __attribute__((aligned(16))) uint8_t brief_lds[4 * kKpw * kBriefWin];
+    const int per_wg = 4 * kKpw;
+    const int nbx = (nslots + per_wg - 1) / per_wg;
+    const int item = xcd_item(xcd_chunk(nbx * batch));
+    if (item >= nbx * batch) return;
+    const int img = item / nbx;
+    const int wrel = __builtin_amdgcn_readfirstlane(((item - img * nbx) * blockDim.x + threadIdx.x) >> 6);
+    if (wrel * kKpw >= nslots) return;                           // whole wave
+    const int ln = lane_id();
+    const int sub = ln / kLp, lk = ln - sub * kLp;
+    const int rel = wrel * kKpw + sub;
+    const int slot = slot0 + rel;
+    int lvl = 0;
+#pragma unroll
+    for (int l = 1; l < kMaxLevels; ++l) lvl += (l < nlevels && slot >= tab.out_off[l]) ? 1 : 0;
+    const int* lcs = level_cnt + img * nlevels;
+    int off = 0, total = 0;
+    for (int l = 0; l < nlevels; ++l) {
+        const int c = lcs[l] & 0xffff;
+        off += l < lvl ? c : 0;
+        total += c;
+    }
+    const int craw = lcs[lvl], ci = craw & 0xffff;
+    if (__ballot(lvl_stale(craw, seq)) && ln == 0) atomicOr(err, kErrStale);
+    if (write_count && wrel == 0 && ln == 0) counts[img] = min(total, capacity);
+    const LevelDev& L = levels[lvl];
+    const int lw = L.w, lh = L.h, lpo = L.pyr_off, loo = L.out_off;
+    const int i = slot - loo;
+    const int o = off + i;
+    const bool valid = rel < nslots && i < ci && o < capacity;
+    if (__ballot(valid) == 0) return;                            // whole wave
+
+    const uint32_t xy = valid ? lvl_xy[(size_t)img * out_stride + loo + i] : 0u;
+    const int cx = (int)(xy & 0xffff), cy = (int)(xy >> 16);
+    const uint8_t* P = lvl == 0 ? s0.p + img * s0.istride : pyr + img * pyr_stride + lpo;
+    const int pstride = lvl == 0 ? (int)s0.step : lw;
+    const int wx0 = cx - 23, wy0 = cy - 21;                      // raw window origin
+    // windows crossing the level border (keypoints lie >= 19 px inside, so by at most 4 columns / 2 rows): bytes by
+    // REFLECT_101 coordinates, one byte load each (uniform per keypoint)
+    const bool inside = wx0 >= 0 && wx0 + kFbRow <= lw && wy0 >= 0 && wy0 + kFbRows <= lh;
+    uint64_t wv[kNW];
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < kNW; ++k) {
+            const int q = min(lk + kLp * k, kFbChunks - 1), r = q / 6, c = q - r * 6;
+            if (inside) {
+                __builtin_memcpy(&wv[k], P + (size_t)(wy0 + r) * pstride + wx0 + 8 * c, 8);
+            } else {
+                const int y = refl101(wy0 + r, lh);
+                const uint8_t* row = P + (size_t)y * pstride;
+                uint64_t v = 0;
+#pragma unroll
+                for (int b = 0; b < 8; ++b) v |= (uint64_t)row[refl101(wx0 + 8 * c + b, lw)] << (8 * b);
+                wv[k] = v;
+            }
+        }
+    }
+    uint8_t* raw = raw_lds + ((threadIdx.x >> 6) * kKpw + sub) * kFbRaw;
+    uint8_t* win = brief_lds + ((threadIdx.x >> 6) * kKpw + sub) * kBriefWin;
+    // --- IC_Angle (:77-104) from the loaded chunks: the 31 x 32 box is chunks 1..4 of window rows 6..36
+    int m10 = 0, m01 = 0;
+#pragma unroll
+    for (int k = 0; k < kNW; ++k) {
+        const int q = lk + kLp * k, r = q / 6, c = q - r * 6;
+        const int v = r - 21, av = v < 0 ? -v : v;
+        const int um = kUmax[av > 15 ? 15 : av];
+        const int u0 = 8 * c - 23;                                // column offset of the chunk's first byte
+        const int lo = max(0, -um - u0), hi = min(7, um - u0);
+        uint64_t m = 0;
+        if (valid && q < kFbChunks && av <= kHalfPatch && c >= 1 && c <= 4 && lo <= hi)
+            m = (hi >= 7 ? ~0ull : ((1ull << (8 * hi + 8)) - 1ull)) & (~0ull << (8 * lo));
+        const uint64_t px = wv[k] & m;
+        const uint32_t a = (uint32_t)px, b = (uint32_t)(px >> 32);
+        const uint32_t wa = (uint32_t)(u0 + 16) * 0x01010101u + 0x03020100u, wb = wa + 0x04040404u;
+        const int dot = (int)__builtin_amdgcn_udot4(b, wb, __builtin_amdgcn_udot4(a, wa, 0u, false), false);
+        const int sum = (int)__builtin_amdgcn_udot4(b, 0x01010101u, __builtin_amdgcn_udot4(a, 0x01010101u, 0u, false), false);
+        m10 += dot - 16 * sum;
+        m01 += v * sum;
+    }
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < kNW; ++k) {
+            const int q = lk + kLp * k;
+            if (q < kFbChunks) *reinterpret_cast<uint64_t*>(raw + 8 * q) = wv[k];   // row q / 6, chunk q % 6
+        }
+    }
+    m10 = group_sum<kLp>(m10, sub);
+    m01 = group_sum<kLp>(m01, sub);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");       // other lanes' raw chunks before the blur reads
+    // --- GaussianBlur of the 37 x 37 window: lane lk < 30 owns output columns 4g .. 4g+3 (g = lk % 10; blurred column
+    //     c <-> x = cx - 18 + c <-> raw byte c + 5) and output rows [13s, min(13s + 13, 37)) (s = lk / 10); output row
+    //     r needs raw rows r .. r + 6
+    {
+        const int g = lk % 10, s = lk / 10;
+        const bool act = valid && lk < 30;
+        const int y0 = 13 * s, y1 = min(y0 + 13, 2 * kBriefR + 1);
+        const uint8_t* rb = raw + 4 * g;
+        auto ld = [&](int r) -> BlurRow {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(rb + r * kFbRow);
+            return blur_hrow5(p[0], p[1], p[2]);
+        };
+        if (act) {
+            BlurRow r0 = ld(y0), r1 = ld(y0 + 1), r2 = ld(y0 + 2), r3 = ld(y0 + 3), r4 = ld(y0 + 4), r5 = ld(y0 + 5), r6;
+            uint32_t* wo = reinterpret_cast<uint32_t*>(win + 4 * g);
+            for (int y = y0; y < y1; y += 7) {
+                r6 = ld(y + 6); wo[y * (kBriefRow / 4)] = blur_emit4(r0, r1, r2, r3, r4, r5, r6); if (y + 1 >= y1) break;
+                r0 = ld(y + 7); wo[(y + 1) * (kBriefRow / 4)] = blur_emit4(r1, r2, r3, r4, r5, r6, r0); if (y + 2 >= y1) break;
+                r1 = ld(y + 8); wo[(y + 2) * (kBriefRow / 4)] = blur_emit4(r2, r3, r4, r5, r6, r0, r1); if (y + 3 >= y1) break;
+                r2 = ld(y + 9); wo[(y + 3) * (kBriefRow / 4)] = blur_emit4(r3, r4, r5, r6, r0, r1, r2); if (y + 4 >= y1) break;
+                r3 = ld(y + 10); wo[(y + 4) * (kBriefRow / 4)] = blur_emit4(r4, r5, r6, r0, r1, r2, r3); if (y + 5 >= y1) break;
+                r4 = ld(y + 11); wo[(y + 5) * (kBriefRow / 4)] = blur_emit4(r5, r6, r0, r1, r2, r3, r4); if (y + 6 >= y1) break;
+                r5 = ld(y + 12); wo[(y + 6) * (kBriefRow / 4)] = blur_emit4(r6, r0, r1, r2, r3, r4, r5);
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");       // blurred window before the tests read it
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    const float ang = __fmul_rn(angle, (float)(M_PI / 180.f));
+    float a, b;
+    orbx_sincos_brief(ang, &a, &b);
+    const uint8_t* center = win + kBriefR * kBriefRow + kBriefR;
+    uint32_t words[kNT];
+#pragma unroll
+    for (int gt = 0; gt < kNT; ++gt) {
+        const int t = gt * kLp + lk;
+        const uint32_t pw = reinterpret_cast<const uint32_t*>(c_pattern)[t];
+        int vals[2] = {0, 0};
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
+            const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
+            const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
+            if (valid) vals[e] = center[__float2int_rn(ry) * kBriefRow + __float2int_rn(rx)];
+        }
+        const uint64_t bm = __ballot(vals[0] < vals[1]);
+        words[gt] = (uint32_t)(bm >> (sub * kLp)) & (uint32_t)((1ull << kLp) - 1ull);
+    }
+    if (!valid) return;
+    uint32_t dw = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dw = lk == j ? words[j] : dw;
+    if (lk < 8) reinterpret_cast<uint32_t*>(desc + ((size_t)img * capacity + o) * 32)[lk] = dw;
+    if (lk == 0) {
+        orbx_keypoint k;
+        float x = (float)cx, y = (float)cy;
+        if (lvl != 0) { x = __fmul_rn(x, L.scale); y = __fmul_rn(y, L.scale); }
+        k.x = x; k.y = y;
+        k.size = (float)L.patch;
+        k.angle = angle;
+        k.response = (float)lvl_r[(size_t)img * out_stride + loo + i];
+        k.octave = lvl;
+        k.class_id = -1;
+        kps[(size_t)img * capacity + o] = k;
+    }
+}
+
 // =============================================================================================
 // host side
 // =============================================================================================
@@ -2413,6 +2862,13 @@ struct Extractor {
     std::vector<BandDev> rowgv;
     BandDev* d_rowg = nullptr;
     int fast_rows = 0;   // (default off until it measures faster than k_fast_band in the full step)
+    // k_fast_wave (ORBX_FAST_WAVE): one wave per (cell, image), wave_wpg waves per workgroup; level 0 / levels >= 1
+    struct WaveLaunch { int cell0, n, ps, kcap; WaveLds lay; };
+    WaveLaunch wave_launch[2] = {};
+    int fast_wave = 0;
+    int wave_wpg = 4;
+    int wave_psmin = 0;
+    int desc_fb = 0;          // ORBX_DESC_FB: k_describe_fb (blur per keypoint in LDS, no k_blur7 / blurred pyramid)
     int band_g = 4;
     int fast_oe = 1;          // ORBX_FAST_OE: E-only pair image (O taps by v_alignbit), 0 = E and O images
     int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
@@ -2658,6 +3114,39 @@ int Extractor::configure(int r, int c, int batch) {
         if (f.lds > 64 * 1024)
             ORBX_HIP(hipFuncSetAttribute(f.ps == 24 ? (const void*)k_fast_cells<24> : (const void*)k_fast_cells<48>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.lds));
+    }
+    // k_fast_wave launches: the same cell ranges, each wave's LDS slice sized for the launch's largest cell
+    for (int k = 0; k < 2; ++k) {
+        WaveLaunch& wl = wave_launch[k];
+        const FastLaunch& f = fast_launch[k];
+        wl.cell0 = f.cell0;
+        wl.n = f.n;
+        int rows = 8, sw = 8, np = 1, kcap = 1, psn = 4;
+        for (int i = f.cell0; i < f.cell0 + f.n; ++i) {
+            const CellDev& cd = cellv[i];
+            const int Wd = std::max(cd.W - 6, 0), Hd = std::max(cd.H - 6, 0);
+            const int PR = (Wd + 1) / 2, QR = (PR + 3) / 4;
+            rows = std::max(rows, cd.H);
+            sw = std::max(sw, (Wd + 5) & ~1);
+            np = std::max(np, Hd * PR);
+            kcap = std::max(kcap, cd.slot_cap);
+            psn = std::max({psn, 4 * ((cd.W + 7) / 8), 4 * QR + 3});   // ROI chunk words; quad reads up to 4 * QR + 2
+        }
+        ORBX_REQUIRE(psn <= 40, ORBX_ERR_UNSUPPORTED, "cell too wide for k_fast_wave");
+        psn = std::max(psn, wave_psmin);                    // ORBX_FAST_PSMIN (A/B of the pair stride)
+        wl.ps = psn <= 20 ? 20 : psn <= 24 ? 24 : 40;
+        ORBX_REQUIRE(sw <= fastw_sw(wl.ps), ORBX_ERR_UNSUPPORTED, "k_fast_wave score-map row");
+        sw = fastw_sw(wl.ps);
+        wl.kcap = kcap;                                     // two u16 key lists inside the pair image: 4 * kcap bytes
+        ORBX_REQUIRE(4 * kcap <= rows * wl.ps * 4, ORBX_ERR_UNSUPPORTED, "k_fast_wave key lists exceed the pair image");
+        wl.lay = wave_lds(rows, sw, np, wl.ps);
+        const int bytes = wave_wpg * wl.lay.bytes;
+        ORBX_REQUIRE(bytes <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "k_fast_wave LDS %d B", bytes);
+        if (bytes > 64 * 1024) {
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<20, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<24, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<40, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+        }
     }
     // k_fast_band: runs of up to band_g cells of one cell row (same level and iniY), the band ROI at most 139 columns
     // (2 * cpr <= 72 pair dwords per row); level 0 / levels >= 1 as the two launches above
@@ -2944,6 +3433,18 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
     auto fast = [&](hipStream_t q, const Extractor::FastLaunch& f) {
         if (f.n <= 0) return;
+        if (e->fast_wave && !e->fast_stop_after) {
+            const Extractor::WaveLaunch& wl = e->wave_launch[&f == &e->fast_launch[0] ? 0 : 1];
+            if (wl.n <= 0) return;
+            const int wpg = e->wave_wpg, nwg = (wl.n * batch + wpg - 1) / wpg;
+            auto kw = wl.ps == 20 ? (wpg == 4 ? k_fast_wave<20, 4> : wpg == 2 ? k_fast_wave<20, 2> : k_fast_wave<20, 1>)
+                    : wl.ps == 24 ? (wpg == 4 ? k_fast_wave<24, 4> : wpg == 2 ? k_fast_wave<24, 2> : k_fast_wave<24, 1>)
+                                  : (wpg == 4 ? k_fast_wave<40, 4> : wpg == 2 ? k_fast_wave<40, 2> : k_fast_wave<40, 1>);
+            hipLaunchKernelGGL(kw, dim3(kXcds * xcd_chunk(nwg)), dim3(64 * wpg), (size_t)wpg * wl.lay.bytes, q, e->d_pyr, ps,
+                               e->d_levels, e->d_cells, wl.cell0, wl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s,
+                               e->cand_stride, e->d_cell_cnt, ncells, batch, s0, wl.lay, wl.kcap);
+            return;
+        }
         if (e->fast_rows && !e->fast_stop_after) {
             const Extractor::RowsLaunch& rl = e->rows_launch[&f == &e->fast_launch[0] ? 0 : 1];
             if (rl.n <= 0) return;
@@ -2976,7 +3477,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
                            (int)e->qt_lds, kc, seq);
     };
     auto blur = [&](hipStream_t q, int tile0, int n) {
-        if (n <= 0) return;
+        if (n <= 0 || e->desc_fb) return;                           // k_describe_fb blurs per keypoint
         hipLaunchKernelGGL(k_blur7, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur, ps,
                            e->d_levels, e->d_tiles, n, batch, s0, tile0);
     };
@@ -3031,8 +3532,14 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     for (int l = 0; l < nl; ++l) tab.out_off[l] = e->lv[l].out_off;
     auto describe = [&](hipStream_t q, int slot0, int nslots, int write_count) {
         if (nslots <= 0) return;
-        const int kpw = e->desc_kpw;                                // keypoints per wave (1, 2 or 4)
+        const int kpw = e->desc_fb ? 2 : e->desc_kpw;               // keypoints per wave (1, 2 or 4)
         dim3 g(kXcds * xcd_chunk((nslots + 4 * kpw - 1) / (4 * kpw) * batch));
+        if (e->desc_fb) {
+            hipLaunchKernelGGL(k_describe_fb, g, dim3(256), 0, q, e->d_pyr, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
+                               e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, slot0, nslots, write_count,
+                               batch, s0, tab, seq, e->d_err);
+            return;
+        }
         auto kern = kpw == 4 ? k_describe_m<4> : kpw == 2 ? k_describe_m<2> : k_describe;
         hipLaunchKernelGGL(kern, g, dim3(256), 0, q, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
                            e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, slot0, nslots, write_count, batch, s0,
@@ -3188,6 +3695,10 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* pl = std::getenv("ORBX_PIPELINE")) e->pipeline = std::atoi(pl) != 0;
     if (const char* fb = std::getenv("ORBX_FAST_BAND")) e->fast_band = std::atoi(fb) != 0;
     if (const char* fr = std::getenv("ORBX_FAST_ROWS")) e->fast_rows = std::atoi(fr) != 0;
+    if (const char* fw = std::getenv("ORBX_FAST_WAVE")) e->fast_wave = std::atoi(fw) != 0;
+    if (const char* fb = std::getenv("ORBX_DESC_FB")) e->desc_fb = std::atoi(fb) != 0;
+    if (const char* pm = std::getenv("ORBX_FAST_PSMIN")) e->wave_psmin = std::atoi(pm);
+    if (const char* fp = std::getenv("ORBX_FAST_WPG")) e->wave_wpg = std::atoi(fp) == 1 ? 1 : std::atoi(fp) == 2 ? 2 : 4;
     if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
     if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;
     if (const char* ds = std::getenv("ORBX_DESC_SPLIT")) e->desc_split = std::atoi(ds) != 0;

@@ -1,0 +1,24 @@
+# k_fast_wave (one wave per cell) A/B: parity of every FAST form, then serial and pipelined bench, band vs wave (4 and 1
+# waves per workgroup)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${TAG:-r3u}
+timeout -k 10 400 python -u -m pytest tests/test_gpu_extract.py -k "fast_kernels or kitti_c2 or fused_blur" -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc $(tail -1 gpurun_out/${TAG}_pytest.log)"; [ $rc -eq 0 ] || { tail -40 gpurun_out/${TAG}_pytest.log; exit $rc; }
+B="--cpu-seconds 0 --host-api-frames 0 --no-c3 --no-cd --host-fed-steps 0 --steps 30"
+for v in ${FORMS:-band wave wave2 wave1 wave}; do
+  E="ORBX_FAST_WAVE=0"; [ $v = wave ] && E="ORBX_FAST_WAVE=1"; [ $v = wave1 ] && E="ORBX_FAST_WAVE=1 ORBX_FAST_WPG=1"; [ $v = wave2 ] && E="ORBX_FAST_WAVE=1 ORBX_FAST_WPG=2"; [ $v = fb ] && E="ORBX_FAST_WAVE=1 ORBX_DESC_FB=1"; [ $v = wave24 ] && E="ORBX_FAST_WAVE=1 ORBX_FAST_PSMIN=24"
+  env $E ORBX_PIPELINE=0 timeout -k 10 300 python -u bench.py $B > gpurun_out/${TAG}_${v}_s.log 2>&1 || exit $?
+  env $E timeout -k 10 300 python -u bench.py $B > gpurun_out/${TAG}_${v}_p.log 2>&1 || exit $?
+  python3 -c "
+import json
+s=json.loads(open('gpurun_out/${TAG}_${v}_s.log').read().strip().splitlines()[-1]); p=json.loads(open('gpurun_out/${TAG}_${v}_p.log').read().strip().splitlines()[-1])
+st=s['stage_ms_per_step']
+print('$v serial fast %.3f (l0 %.3f) blur %.3f desc %.3f value %s | pipelined %s %s ms' % (st['fast_cells']+st['fast_cells_l0'], st['fast_cells_l0'], st.get('blur7', 0), st.get('describe', 0), s['value'], p['value'], p['ms_per_step']))"
+done
+# SQ counters of the serial step with k_fast_wave (one --pmc pass per counter set)
+if [ -n "$SQ" ]; then
+  export ORBX_FAST_WAVE=1 ORBX_PIPELINE=0 ORBX_FAST_WPG=${SQ}
+  bash scripts/prof_sq.sh ${TAG}_sq --steps 5 --warmup 2 --no-c3 --no-cd --host-fed-steps 0 --host-api-frames 0 || exit $?
+  python3 scripts/sq_summary.py gpurun_out/${TAG}_sq gpurun_out/${TAG}_sq_summary.json | head -8
+fi

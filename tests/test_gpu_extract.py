@@ -173,19 +173,28 @@ def test_describe_keypoints_per_wave(gpu, monkeypatch, kpw):
     _check(S.kitti_like_image(410, rows=240, cols=333), nfeatures=777, nlevels=5, scale=1.3)
 
 
-@pytest.mark.parametrize("rows", [0, 1])
-def test_fast_kernels_bit_exact(gpu, monkeypatch, rows):
-    """Both FAST forms -- k_fast_band (LDS band image, pre-test and survivor list) and k_fast_rows (one wave per cell
-    row in registers, every pixel scored, both thresholds' lists) -- are bit-exact against the oracle: KITTI size,
-    odd sizes and another parameter set, batched."""
+@pytest.mark.parametrize("form", ["band", "rows", "wave", "wave24", "wave2", "wave1"])
+def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
+    """Every FAST form -- k_fast_band (LDS band image, pre-test and survivor list), k_fast_rows (one wave per cell
+    row in registers, every pixel scored, both thresholds' lists) and k_fast_wave (one wave per cell, no barrier; 4, 2
+    or 1 waves per workgroup) -- is bit-exact against the oracle: KITTI size, odd, tall and tiny sizes, uniform noise (most
+    pixels survive the pre-test) and another parameter set, batched."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
-    monkeypatch.setenv("ORBX_FAST_ROWS", str(rows))
+    monkeypatch.setenv("ORBX_FAST_ROWS", "1" if form == "rows" else "0")
+    monkeypatch.setenv("ORBX_FAST_WAVE", "1" if form.startswith("wave") else "0")
+    monkeypatch.setenv("ORBX_FAST_WPG", {"wave1": "1", "wave2": "2"}.get(form, "4"))
+    monkeypatch.setenv("ORBX_FAST_PSMIN", "24" if form == "wave24" else "0")   # pair stride 24 on KITTI-size cells
     for shape, nf, kw in (((375, 1242), 2000, {}), ((377, 1243), 800, {}), ((120, 160), 300, {}),
-                          ((480, 752), 1500, dict(nlevels=5, scale=1.3, ini=25, mn=10))):
-        imgs = np.stack([S.kitti_like_image(900 + i, rows=shape[0], cols=shape[1]) for i in range(3)])
+                          ((1000, 200), 800, {}), ((40, 40), 100, {}), ((500, 500), 1000, {}),
+                          ((480, 752), 1500, dict(nlevels=5, scale=1.3, ini=25, mn=10)),
+                          ((375, 1242), 2000, dict(noise=True)), ((375, 1242), 2000, dict(ini=5, mn=12))):
+        if kw.get("noise"):
+            imgs = np.stack([S.uniform_noise_image(950 + i) for i in range(3)])
+        else:
+            imgs = np.stack([S.kitti_like_image(900 + i, rows=shape[0], cols=shape[1]) for i in range(3)])
         ex = pkg.ORBextractor(nf, kw.get("scale", 1.2), kw.get("nlevels", 8), kw.get("ini", 20), kw.get("mn", 7))
         kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).cuda())
         torch.cuda.synchronize()
@@ -197,3 +206,39 @@ def test_fast_kernels_bit_exact(gpu, monkeypatch, rows):
             kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
             assert np.array_equal(kb, ref["kps"]) and np.array_equal(desc[i, :n], ref["desc"]), _diff_report(
                 kb, desc[i, :n], ref["kps"], ref["desc"])
+
+
+@pytest.mark.parametrize("fast_wave", [0, 1])
+def test_describe_fused_blur_bit_exact(gpu, monkeypatch, fast_wave):
+    """k_describe_fb (the 7x7 GaussianBlur done per keypoint on its raw 43x48 window in LDS, no blurred pyramid) gives
+    the oracle's descriptors bit for bit: windows that cross the level border (REFLECT_101 on the raw coordinates) occur
+    on every level of these images; small and odd sizes, uniform noise, another parameter set, batched."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    monkeypatch.setenv("ORBX_DESC_FB", "1")
+    monkeypatch.setenv("ORBX_FAST_WAVE", str(fast_wave))
+    for shape, nf, kw in (((375, 1242), 2000, {}), ((377, 1243), 800, {}), ((40, 40), 100, {}), ((120, 160), 300, {}),
+                          ((1000, 200), 800, {}), ((480, 752), 1500, dict(nlevels=5, scale=1.3, ini=25, mn=10)),
+                          ((375, 1242), 2000, dict(noise=True))):
+        if kw.get("noise"):
+            imgs = np.stack([S.uniform_noise_image(960 + i) for i in range(3)])
+        else:
+            imgs = np.stack([S.kitti_like_image(920 + i, rows=shape[0], cols=shape[1]) for i in range(3)])
+        ex = pkg.ORBextractor(nf, kw.get("scale", 1.2), kw.get("nlevels", 8), kw.get("ini", 20), kw.get("mn", 7))
+        kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).cuda())
+        torch.cuda.synchronize()
+        kps, desc, cnt = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+        for i in range(len(imgs)):
+            ref = O.extract(imgs[i], nfeatures=nf, scale_factor=kw.get("scale", 1.2), nlevels=kw.get("nlevels", 8),
+                            ini_th=kw.get("ini", 20), min_th=kw.get("mn", 7))
+            n = int(cnt[i])
+            kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
+            assert np.array_equal(kb, ref["kps"]) and np.array_equal(desc[i, :n], ref["desc"]), _diff_report(
+                kb, desc[i, :n], ref["kps"], ref["desc"])
+        # the host API (one image per call) takes the same path
+        k1, d1 = ex(imgs[0])
+        ref = O.extract(imgs[0], nfeatures=nf, scale_factor=kw.get("scale", 1.2), nlevels=kw.get("nlevels", 8),
+                        ini_th=kw.get("ini", 20), min_th=kw.get("mn", 7))
+        assert np.array_equal(k1, ref["kps"]) and np.array_equal(d1, ref["desc"])
