@@ -466,8 +466,9 @@ def load_profile(name):
 # Live stage timers (orbx_extractor_stage_times: HIP events on the stream each launch is issued on) that time a
 # kernel's launches over the whole batch: k_fast_band is two launches per call (level 0 on the extractor's side stream,
 # levels 1..7 on the launch stream), each timed by its own event pair; k_describe_m is one launch on the output stream.
-LIVE_STAGES = {"k_fast_band": ("fast_cells", "fast_cells_l0"), "k_describe_m": ("describe",), "k_describe": ("describe",),
-               "k_quadtree": ("quadtree", "quadtree_l0")}
+LIVE_STAGES = {"k_fast_band": ("fast_cells", "fast_cells_l0"), "k_fast_wave": ("fast_cells", "fast_cells_l0"),
+               "k_describe_m": ("describe",), "k_describe": ("describe",), "k_describe_fb": ("describe",),
+               "k_quadtree": ("quadtree", "quadtree_l0"), "k_blur7": ("blur7",)}
 
 
 def kernel_family(name):
@@ -480,6 +481,26 @@ def source_sha16():
     return f(ROOT)
 
 
+def active_kernel_names():
+    """Names (as rocprofv3 prints them) of the extractor kernels this process runs, from the same environment switches
+    liborbx reads at extractor creation (csrc/orbx_extract.hip, orbx_extractor_create)."""
+    env = os.environ.get
+    if env("ORBX_FAST_WAVE", "1") != "0":
+        wpg = {"1": 1, "2": 2}.get(env("ORBX_FAST_WPG", "4"), 4)
+        psmin = int(env("ORBX_FAST_PSMIN", "24"))               # KITTI / EuRoC cells need a pair stride of 20
+        fast = f"k_fast_wave<{20 if psmin <= 20 else 24 if psmin <= 24 else 40}, {wpg}>"
+    else:
+        fast = "k_fast_band<72, true>"
+    if env("ORBX_DESC_FB", "0") != "0":
+        desc = "k_describe_fb"
+    else:
+        kpw = int(env("ORBX_DESC_KPW", "2"))
+        desc = "k_describe" if kpw == 1 else f"k_describe_m<{4 if kpw == 4 else 2}>"
+    blur = "k_blur7<false>" if env("ORBX_BLUR_DOT2", "1") == "0" else "k_blur7<true>"
+    return {"fast": fast, "describe": desc, "blur": blur,
+            "families": {kernel_family(fast), kernel_family(desc), "k_quadtree", "k_blur7", "k_resize4"}}
+
+
 def roofline_lines(per_call, cfg, units, config):
     """Roofline of the dominant kernel -- the one with the largest share of GPU time in the committed kernel trace of
     the bench command (profiles/kernel_share.json, scripts/kernel_share.py) -- and of the describe as a secondary
@@ -488,9 +509,12 @@ def roofline_lines(per_call, cfg, units, config):
     time per step (sum of its launches' event spans)."""
     share = load_profile("kernel_share.json")
     cb = compulsory_bytes(cfg)["extraction"]
-    dom = "k_fast_band"
+    names = active_kernel_names()
+    fast_fam = kernel_family(names["fast"])
+    dom = fast_fam
     prof_ms, stale, tag = None, None, None
-    if share and share.get("config", "kitti") == config and share.get("batch_images") == units:
+    if share and share.get("config", "kitti") == config and share.get("batch_images") == units \
+            and kernel_family(share["dominant"]) in names["families"]:       # a profile of the kernels that run
         dom = kernel_family(share["dominant"])
         tag = share.get("tag")
         stale = share.get("source_sha16") != source_sha16()
@@ -516,11 +540,9 @@ def roofline_lines(per_call, cfg, units, config):
                 "traffic_ratio": round(traffic / bytes_step, 2) if traffic else None,
                 "unit_of_work": "one extraction (SURVEY §8d: image in + nfeatures x 60 B out); the kernel's launches of a "
                                 "step together cover every image of the batch once"}
-    kpw = int(os.environ.get("ORBX_DESC_KPW", "2"))
-    desc_name = "k_describe" if kpw == 1 else f"k_describe_m<{4 if kpw == 4 else 2}>"
-    names = {"k_fast_band": "k_fast_band<72, true>", "k_describe_m": desc_name, "k_describe": desc_name,
-             "k_quadtree": "k_quadtree"}
-    main_line = line(dom, names.get(dom, dom)) or line("k_fast_band", names["k_fast_band"])
+    desc_name = names["describe"]
+    full = {kernel_family(n): n for n in (names["fast"], desc_name, "k_quadtree", names["blur"])}
+    main_line = line(dom, full.get(dom, dom)) or line(fast_fam, names["fast"])
     if main_line is not None:
         main_line["selected_by"] = (f"largest share of GPU time in profiles/kernel_share.json ({tag})" if tag else
                                     "default (no kernel_share.json for this config)")

@@ -1151,27 +1151,36 @@ __device__ __forceinline__ QuadTaps fastw_quad_load(const uint32_t* __restrict__
     return q;
 }
 
-// test of a loaded quad
+// Test of a loaded quad at threshold t: bit k = pair 4u+k has a pixel inside the detection window (column < Wd) whose
+// compass value exceeds t.  f16 form of the compass test (the pair image is f16-biased: differences are exact): per
+// pair 4 packed differences, dk / br by 3-input packed min / max, m = max(dk, -br); z = m - (t + 1) has its sign bit
+// set iff m <= t, and the 8 sign bits of the quad (2 per pair) are gathered by two v_perm into one byte each.
 __device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, int t, int PR, int Wd) {
+    (void)PR;
     const uint32_t *A = q.A, *U = q.U, *D = q.D;
-    uint32_t mq = 0;
+    const h16x2 tq = {(_Float16)(t + 1), (_Float16)(t + 1)};
+    uint32_t z[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int j = 4 * u + k;
-        const s16x2 v = as_s2(align16(A[k + 2], A[k + 1]));             // pixels of pair j
-        const s16x2 d0 = v - as_s2(align16(D[k + 2], D[k + 1]));        // ( 0,  3)
-        const s16x2 d4 = v - as_s2(A[k + 3]);                           // ( 3,  0)
-        const s16x2 d8 = v - as_s2(align16(U[k + 2], U[k + 1]));        // ( 0, -3)
-        const s16x2 d12 = v - as_s2(A[k]);                              // (-3,  0)
-        const s16x2 dk = pmax(pmax(pmin(d0, d4), pmin(d4, d8)), pmax(pmin(d8, d12), pmin(d12, d0)));
-        const s16x2 br = pmin(pmin(pmax(d0, d4), pmax(d4, d8)), pmin(pmax(d8, d12), pmax(d12, d0)));
-        const s16x2 m = pmax(dk, (s16x2)(0) - br);
-        const bool two = 2 * j + 1 < Wd;
-        const int pm = j < PR ? (two ? 3 : 1) : 0;
-        const int pt = ((m.x > t ? 1 : 0) | (m.y > t ? 2 : 0)) & pm;
-        mq |= (pt != 0 ? 1u : 0u) << k;
+        const h16x2 v = as_h2(align16(A[k + 2], A[k + 1]));             // pixels of pair 4u+k
+        const h16x2 d0 = v - as_h2(align16(D[k + 2], D[k + 1]));        // ( 0,  3)
+        const h16x2 d4 = v - as_h2(A[k + 3]);                           // ( 3,  0)
+        const h16x2 d8 = v - as_h2(align16(U[k + 2], U[k + 1]));        // ( 0, -3)
+        const h16x2 d12 = v - as_h2(A[k]);                              // (-3,  0)
+        const h16x2 dk = hmax(hmax3(hmin(d0, d4), hmin(d4, d8), hmin(d8, d12)), hmin(d12, d0));
+        const h16x2 br = hmin(hmin3(hmax(d0, d4), hmax(d4, d8), hmax(d8, d12)), hmax(d12, d0));
+        const h16x2 m = hmax(dk, -br);
+        z[k] = __builtin_bit_cast(uint32_t, m - tq);
     }
-    return mq;
+    // sign bytes: pixel 2k at byte 2k, pixel 2k+1 at byte 2k+1 of the 8-byte (lo | hi << 32) pack
+    const uint32_t lo = __builtin_amdgcn_perm(z[1], z[0], 0x07050301u), hi = __builtin_amdgcn_perm(z[3], z[2], 0x07050301u);
+    const int nv = min(max(Wd - 8 * u, 0), 8);                         // pixels of the quad inside the window
+    const uint64_t inv = nv >= 8 ? 0ull : (0x8080808080808080ull << (8 * nv));
+    const uint64_t f = ((((uint64_t)hi << 32) | lo) | inv) & 0x8080808080808080ull;   // 0x80: pixel fails
+    const uint64_t g = f & (f >> 8) & 0x0080008000800080ull;          // bit 7 of byte 2k: both pixels of pair k fail
+    const uint32_t gl = (uint32_t)g, gh = (uint32_t)(g >> 32);
+    const uint32_t failq = ((gl >> 7) & 1u) | ((gl >> 22) & 2u) | ((gh >> 5) & 4u) | ((gh >> 20) & 8u);
+    return ~failq & 15u;
 }
 
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
@@ -1185,7 +1194,7 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
                                                          int cell0, int ncell, int iniTh, int minTh,
                                                          uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
                                                          int cand_stride, int* __restrict__ cell_cnt, int ncells, int batch,
-                                                         Src0 s0, WaveLds lay, int kcap) {
+                                                         Src0 s0, WaveLds lay, int kcap, int two_pass) {
     extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
     const int w = threadIdx.x >> 6, ln = lane_id();
     const int total = ncell * batch, nwg = (total + kWpg - 1) / kWpg;
@@ -1214,39 +1223,77 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
         int lstride;
         const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
         const uint8_t* src0 = base + (size_t)cd.y0 * lstride + cd.x0;
-        const int cpr = (W + 7) >> 3, NQ = H * cpr;
-        const int dr = kWave / cpr, dc = kWave - dr * cpr;          // item q -> q + 64 (no division per item)
-        int r = ln / cpr, cc = ln - r * cpr;
-        constexpr int kPf = 6;
-        for (int q0 = 0; q0 < NQ; q0 += kPf * kWave) {
-            uint32_t pf[2 * kPf];
-            int rs[kPf], cs[kPf];
+        if constexpr (kPS % 8 == 0) {
+            // 16-byte chunks (8 pair words each): a KITTI cell ROI (<= 38 x 38) is one round of <= 2 loads per lane.  The
+            // bytes past the ROI's width (< 16, inside the level row: the ROI ends >= 16 px before the level's edge) only
+            // reach pixels outside the detection window, which are masked.
+            const int cpr = (W + 15) >> 4, NQ = H * cpr;
+            const int dr = kWave / cpr, dc = kWave - dr * cpr;      // item q -> q + 64 (no division per item)
+            int r = ln / cpr, cc = ln - r * cpr;
+            constexpr int kPf = 2;
+            for (int q0 = 0; q0 < NQ; q0 += kPf * kWave) {
+                uint4 pf[kPf];
+                int rs[kPf], cs[kPf];
 #pragma unroll
-            for (int k = 0; k < kPf; ++k) {
-                const int q = q0 + ln + k * kWave;
-                rs[k] = r; cs[k] = cc;
-                r += dr; cc += dc;
-                if (cc >= cpr) { cc -= cpr; ++r; }
-                pf[2 * k] = pf[2 * k + 1] = 0;
-                if (q < NQ) __builtin_memcpy(&pf[2 * k], src0 + (size_t)rs[k] * lstride + 8 * cs[k], 8);
-            }
+                for (int k = 0; k < kPf; ++k) {
+                    rs[k] = r; cs[k] = cc;
+                    r += dr; cc += dc;
+                    if (cc >= cpr) { cc -= cpr; ++r; }
+                    if (q0 + ln + k * kWave < NQ) __builtin_memcpy(&pf[k], src0 + (size_t)rs[k] * lstride + 16 * cs[k], 16);
+                }
 #pragma unroll
-            for (int k = 0; k < kPf; ++k) {
-                if (q0 + ln + k * kWave < NQ) {
-                    uint32_t lo = pf[2 * k], hi = pf[2 * k + 1];
-                    const int keep = W - 8 * cs[k];
-                    if (keep < 8) {
-                        const uint64_t m = (1ull << (8 * keep)) - 1ull;        // keep >= 1
-                        const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
-                        lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+                for (int k = 0; k < kPf; ++k) {
+                    if (q0 + ln + k * kWave < NQ) {
+                        const uint4 a = pf[k];
+                        const uint4 e0 = make_uint4(__builtin_amdgcn_perm(a.y, a.x, 0x0c010c00u) | 0x64006400u,
+                                                    __builtin_amdgcn_perm(a.y, a.x, 0x0c030c02u) | 0x64006400u,
+                                                    __builtin_amdgcn_perm(a.y, a.x, 0x0c050c04u) | 0x64006400u,
+                                                    __builtin_amdgcn_perm(a.y, a.x, 0x0c070c06u) | 0x64006400u);
+                        const uint4 e1 = make_uint4(__builtin_amdgcn_perm(a.w, a.z, 0x0c010c00u) | 0x64006400u,
+                                                    __builtin_amdgcn_perm(a.w, a.z, 0x0c030c02u) | 0x64006400u,
+                                                    __builtin_amdgcn_perm(a.w, a.z, 0x0c050c04u) | 0x64006400u,
+                                                    __builtin_amdgcn_perm(a.w, a.z, 0x0c070c06u) | 0x64006400u);
+                        uint4* dst = reinterpret_cast<uint4*>(E + rs[k] * kPS + 8 * cs[k]);
+                        dst[0] = e0;
+                        dst[1] = e1;
                     }
-                    const uint4 e = make_uint4(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u) | 0x64006400u,
-                                               __builtin_amdgcn_perm(hi, lo, 0x0c030c02u) | 0x64006400u,
-                                               __builtin_amdgcn_perm(hi, lo, 0x0c050c04u) | 0x64006400u,
-                                               __builtin_amdgcn_perm(hi, lo, 0x0c070c06u) | 0x64006400u);
-                    *reinterpret_cast<uint4*>(E + rs[k] * kPS + 4 * cs[k]) = e;
                 }
             }
+        } else {
+            const int cpr = (W + 7) >> 3, NQ = H * cpr;
+            const int dr = kWave / cpr, dc = kWave - dr * cpr;          // item q -> q + 64 (no division per item)
+            int r = ln / cpr, cc = ln - r * cpr;
+            constexpr int kPf = 6;
+            for (int q0 = 0; q0 < NQ; q0 += kPf * kWave) {
+                uint32_t pf[2 * kPf];
+                int rs[kPf], cs[kPf];
+#pragma unroll
+                for (int k = 0; k < kPf; ++k) {
+                    const int q = q0 + ln + k * kWave;
+                    rs[k] = r; cs[k] = cc;
+                    r += dr; cc += dc;
+                    if (cc >= cpr) { cc -= cpr; ++r; }
+                    pf[2 * k] = pf[2 * k + 1] = 0;
+                    if (q < NQ) __builtin_memcpy(&pf[2 * k], src0 + (size_t)rs[k] * lstride + 8 * cs[k], 8);
+                }
+#pragma unroll
+                for (int k = 0; k < kPf; ++k) {
+                    if (q0 + ln + k * kWave < NQ) {
+                        uint32_t lo = pf[2 * k], hi = pf[2 * k + 1];
+                        const int keep = W - 8 * cs[k];
+                        if (keep < 8) {
+                            const uint64_t m = (1ull << (8 * keep)) - 1ull;        // keep >= 1
+                            const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
+                            lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+                        }
+                        const uint4 e = make_uint4(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u) | 0x64006400u,
+                                                   __builtin_amdgcn_perm(hi, lo, 0x0c030c02u) | 0x64006400u,
+                                                   __builtin_amdgcn_perm(hi, lo, 0x0c050c04u) | 0x64006400u,
+                                                   __builtin_amdgcn_perm(hi, lo, 0x0c070c06u) | 0x64006400u);
+                        *reinterpret_cast<uint4*>(E + rs[k] * kPS + 4 * cs[k]) = e;
+                    }
+                }
+        }
         }
         // score map cleared to 0: pixels that fail the pre-test and the pad ring (a 0 never blocks a kept score >= 1)
         const int n16 = ((Hd + 2) * SW * 2 + 15) >> 4;
@@ -1256,10 +1303,21 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
     const uint64_t below = (1ull << ln) - 1ull;
     // 2. compass pre-test at min(iniTh, minTh) in quads; survivors compacted in row-major order
     const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
+    // With minThFAST < iniThFAST the cell runs at iniThFAST first (fewer survivors to score); only a cell that kept
+    // nothing there -- a wave-uniform branch, no barrier -- runs again at minThFAST over all its pairs (:812-816).  The
+    // second pass finds every minTh survivor (a superset of the first pass's, whose scores it rewrites with the same
+    // values) and starts its list afresh.  Otherwise one pass at min(iniTh, minTh) keeps both thresholds' pixels.
+    const bool two = two_pass && T2 < T1;
+    uint16_t* k1 = reinterpret_cast<uint16_t*>(E);                  // key lists over the pair image (dead after scoring)
+    uint16_t* k2 = k1 + kcap;
+    int n1 = 0, n2 = 0;                                               // wave-uniform
+    for (int pass = 0; pass < 2; ++pass) {
+    const int tpre = two ? (pass == 0 ? T1 : T2) : tp;
+    const int fmask = two ? (pass == 0 ? 3 : 12) : 15;
     int ns = 0;                                                       // wave-uniform
     {
-        // quad q -> (row q / QR, column q % QR), walked incrementally; two quads per lane per round (q, q + 64), both
-        // read before either is tested.  Survivors are appended in quad order (row-major).
+        // 2. compass pre-test in quads: quad q -> (row q / QR, column q % QR), walked incrementally; two quads per lane
+        // per round (q, q + 64), both read before either is tested.  Survivors are appended in quad order (row-major).
         const int dr = kWave / QR, du = kWave - dr * QR;
         int rr = ln / QR, u = ln - rr * QR;
         auto step = [&](int& r0, int& u0) { r0 += dr; u0 += du; if (u0 >= QR) { u0 -= QR; ++r0; } };
@@ -1281,8 +1339,8 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
             const bool va = qa < NQ4, vb = qb < NQ4;
             const QuadTaps ta = fastw_quad_load<kPS>(E, va ? ra : 0, va ? ua : 0);
             const QuadTaps tb = fastw_quad_load<kPS>(E, vb ? rb : 0, vb ? ub : 0);
-            const uint32_t ma = va ? fastw_quad_test(ta, ua, tp, PR, Wd) : 0u;
-            const uint32_t mb = vb ? fastw_quad_test(tb, ub, tp, PR, Wd) : 0u;
+            const uint32_t ma = va ? fastw_quad_test(ta, ua, tpre, PR, Wd) : 0u;
+            const uint32_t mb = vb ? fastw_quad_test(tb, ub, tpre, PR, Wd) : 0u;
             emit(ma, ra, ua);
             emit(mb, rb, ub);
         }
@@ -1303,15 +1361,12 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
     wave_fence();
     // 4. strict 3x3 NMS at iniTh (bits 0, 1) and minTh (bits 2, 3); kept pixels appended in list order (= row-major)
     //    to the two key lists, which take over the pair image's LDS (key = row * 128 + column in the detection window)
-    uint16_t* k1 = reinterpret_cast<uint16_t*>(E);
-    uint16_t* k2 = k1 + kcap;
-    int n1 = 0, n2 = 0;                                               // wave-uniform
     for (int i0 = 0; i0 < ns; i0 += kWave) {
         const int i = i0 + ln;
         int f = 0, key = 0;
         if (i < ns) {
             const int rr = list[i] >> 8, j = list[i] & 0xff;
-            f = nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd);
+            f = nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
             key = rr * 128 + 2 * j;
         }
         const uint64_t a0 = __ballot(f & 1), a1 = __ballot(f & 2), c0 = __ballot(f & 4), c1 = __ballot(f & 8);
@@ -1325,6 +1380,8 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
         n2 += __popcll(c0) + __popcll(c1);
     }
     wave_fence();
+    if (!two || n1 > 0) break;                                        // wave-uniform
+    }
     // 5. the cell's list (iniTh, or minTh when iniTh kept nothing: :812-816) -> its candidate slots, coalesced
     const uint16_t* ks = n1 > 0 ? k1 : k2;
     const int n = min(n1 > 0 ? n1 : n2, min(kcap, cd.slot_cap));
@@ -1750,9 +1807,105 @@ __device__ __forceinline__ void blur_band(const uint8_t* __restrict__ S, int sst
     }
 }
 
+// Vertical-pair form (k_blur7<true>): two input rows at a time.  V_m = (row a byte m, row b byte m) as u16x2 (one
+// v_perm each), so the horizontal sums of 4 columns come out vertically packed -- H_c = (row a sum, row b sum) -- and
+// the column pass of an output pixel is 4 v_dot2_u32_u16 over 4 such pairs (weights (18,34), (49,55), (49,34), (18,0)
+// for an output row aligned with a pair start, (0,18), (34,49), (55,49), (34,18) for the next row) with the rounding
+// constant 2^15 as the first accumulator: no unpacking of u16 halves.  Same integers as blur_hrow + blur_col.
+struct BlurPair { u16x2 h[4]; };   // columns x0 .. x0+3: (row a, row b) horizontal sums
+
+template <int m>
+__device__ __forceinline__ u16x2 vpair(const BlurWin& a, const BlurWin& b) {
+    constexpr int q = m / 4, r = m % 4;
+    const uint32_t lo = q == 0 ? a.w0 : (q == 1 ? a.w1 : a.w2);
+    const uint32_t hi = q == 0 ? b.w0 : (q == 1 ? b.w1 : b.w2);
+    constexpr uint32_t sel = 0x0c000c00u | (uint32_t)r | ((uint32_t)(r + 4) << 16);
+    return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, sel));
+}
+
+__device__ __forceinline__ BlurPair blur_hpair(const BlurWin& a, const BlurWin& b) {
+    // window byte m = pixel x0 - 4 + m; output column x0 + c uses bytes c+1 .. c+7
+    const u16x2 V1 = vpair<1>(a, b), V2 = vpair<2>(a, b), V3 = vpair<3>(a, b), V4 = vpair<4>(a, b), V5 = vpair<5>(a, b);
+    const u16x2 V6 = vpair<6>(a, b), V7 = vpair<7>(a, b), V8 = vpair<8>(a, b), V9 = vpair<9>(a, b), V10 = vpair<10>(a, b);
+    const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
+    BlurPair o;
+    o.h[0] = (V1 + V7) * k18 + (V2 + V6) * k34 + (V3 + V5) * k49 + V4 * k55;
+    o.h[1] = (V2 + V8) * k18 + (V3 + V7) * k34 + (V4 + V6) * k49 + V5 * k55;
+    o.h[2] = (V3 + V9) * k18 + (V4 + V8) * k34 + (V5 + V7) * k49 + V6 * k55;
+    o.h[3] = (V4 + V10) * k18 + (V5 + V9) * k34 + (V6 + V8) * k49 + V7 * k55;
+    return o;
+}
+
+// output rows y (pairs a..d = rows y-3 .. y+4) and y+1, 4 columns each, packed bytes
+__device__ __forceinline__ void blur_emit2(const BlurPair& a, const BlurPair& b, const BlurPair& c, const BlurPair& d,
+                                           uint32_t& oe, uint32_t& oo) {
+    const u16x2 e0 = {18, 34}, e1 = {49, 55}, e2 = {49, 34}, e3 = {18, 0};
+    const u16x2 o0 = {0, 18}, o1 = {34, 49}, o2 = {55, 49}, o3 = {34, 18};
+    oe = 0; oo = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t ae = __builtin_amdgcn_udot2(d.h[k], e3, 1u << 15, false);
+        ae = __builtin_amdgcn_udot2(c.h[k], e2, ae, false);
+        ae = __builtin_amdgcn_udot2(b.h[k], e1, ae, false);
+        ae = __builtin_amdgcn_udot2(a.h[k], e0, ae, false);
+        uint32_t ao = __builtin_amdgcn_udot2(d.h[k], o3, 1u << 15, false);
+        ao = __builtin_amdgcn_udot2(c.h[k], o2, ao, false);
+        ao = __builtin_amdgcn_udot2(b.h[k], o1, ao, false);
+        ao = __builtin_amdgcn_udot2(a.h[k], o0, ao, false);
+        oe |= min(ae >> 16, 255u) << (8 * k);
+        oo |= min(ao >> 16, 255u) << (8 * k);
+    }
+}
+
+template <int kMode>
+__device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int sstride, uint8_t* __restrict__ D,
+                                           const LevelDev& L, int x0, int y0, int y1) {
+    const int h = L.h, w = L.w;
+    auto row_ptr = [&](int yy) {
+        const int r = h >= 16 ? (yy < 0 ? -yy : (yy >= h ? 2 * h - 2 - yy : yy)) : refl101(yy, h);
+        return S + (size_t)r * sstride;
+    };
+    const bool full = x0 + 4 <= w;
+    auto store = [&](int y, uint32_t packed) {
+        uint8_t* o = D + (size_t)y * w + x0;
+        if (kMode == 0 || full) {
+            __builtin_memcpy(o, &packed, 4);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (x0 + j < w) o[j] = (uint8_t)(packed >> (8 * j));
+        }
+    };
+    BlurPair q0, q1, q2, q3;
+    {
+        BlurWin p[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) p[k] = blur_load<kMode>(row_ptr(y0 - 3 + k), x0, w);
+        q0 = blur_hpair(p[0], p[1]); q1 = blur_hpair(p[2], p[3]); q2 = blur_hpair(p[4], p[5]);
+    }
+    // ring of 4 row pairs; 8 output rows per iteration, input rows loaded 4 at a time (8 in flight spill at 128 VGPRs)
+    for (int y = y0; y < y1; y += 8) {
+        BlurWin p[4];
+        uint32_t oe, oo;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[k] = blur_load<kMode>(row_ptr(y + 3 + k), x0, w);
+        q3 = blur_hpair(p[0], p[1]); blur_emit2(q0, q1, q2, q3, oe, oo);
+        store(y, oe); if (y + 1 >= y1) break; store(y + 1, oo); if (y + 2 >= y1) break;
+        q0 = blur_hpair(p[2], p[3]); blur_emit2(q1, q2, q3, q0, oe, oo);
+        store(y + 2, oe); if (y + 3 >= y1) break; store(y + 3, oo); if (y + 4 >= y1) break;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[k] = blur_load<kMode>(row_ptr(y + 7 + k), x0, w);
+        q1 = blur_hpair(p[0], p[1]); blur_emit2(q2, q3, q0, q1, oe, oo);
+        store(y + 4, oe); if (y + 5 >= y1) break; store(y + 5, oo); if (y + 6 >= y1) break;
+        q2 = blur_hpair(p[2], p[3]); blur_emit2(q3, q0, q1, q2, oe, oo);
+        store(y + 6, oe); if (y + 7 >= y1) break; store(y + 7, oo);
+    }
+}
+
 #ifndef ORBX_BLUR_WPE
 #define ORBX_BLUR_WPE 4
 #endif
+template <bool kDot2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_WPE))) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                size_t pyr_stride, const LevelDev* __restrict__ levels,
                                                const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
@@ -1792,6 +1945,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_W
     const int x0 = bt.tx * kBlurStrip + 4 * lane_id();
     if (x0 >= L.w) return;
     const bool interior = (x0 - 4 >= 0) && (x0 + 8 <= L.w);
+    if constexpr (kDot2) {
+        if (__builtin_amdgcn_read_exec() == __ballot(interior))
+            blur_band2<0>(S, sstride, D, L, x0, y0, y1);
+        else if (L.w >= 12)
+            blur_band2<1>(S, sstride, D, L, x0, y0, y1);
+        else
+            blur_band2<2>(S, sstride, D, L, x0, y0, y1);
+        return;
+    }
     // wave-uniform choice of the load form (strips touching a level's left/right edge pick reflected bytes)
     if (__builtin_amdgcn_read_exec() == __ballot(interior))
         blur_band<0>(S, sstride, D, L, x0, y0, y1);
@@ -2865,10 +3027,13 @@ struct Extractor {
     // k_fast_wave (ORBX_FAST_WAVE): one wave per (cell, image), wave_wpg waves per workgroup; level 0 / levels >= 1
     struct WaveLaunch { int cell0, n, ps, kcap; WaveLds lay; };
     WaveLaunch wave_launch[2] = {};
-    int fast_wave = 0;
+    int fast_wave = 1;        // default (r3x: 62.5k -> 67.1k frames/s with the pair-row blur); 0 = k_fast_band
     int wave_wpg = 4;
-    int wave_psmin = 0;
+    int wave_twopass = 1;     // ORBX_FAST_TWOPASS: iniTh first, minTh only for the cells left empty (0: one pass)
+    int wave_psmin = 24;      // pair stride >= 24: fewer resident FAST waves leave CUs to the overlapped stages (r3x:
+                              // stride 20 is faster alone, 0.772 vs 0.825 ms serial, but 66.6k vs 67.1k frames/s)
     int desc_fb = 0;          // ORBX_DESC_FB: k_describe_fb (blur per keypoint in LDS, no k_blur7 / blurred pyramid)
+    int blur_dot2 = 1;        // ORBX_BLUR_DOT2: k_blur7 in vertical row pairs with v_dot2 column sums (0: one row at a time)
     int band_g = 4;
     int fast_oe = 1;          // ORBX_FAST_OE: E-only pair image (O taps by v_alignbit), 0 = E and O images
     int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
@@ -3442,7 +3607,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
                                   : (wpg == 4 ? k_fast_wave<40, 4> : wpg == 2 ? k_fast_wave<40, 2> : k_fast_wave<40, 1>);
             hipLaunchKernelGGL(kw, dim3(kXcds * xcd_chunk(nwg)), dim3(64 * wpg), (size_t)wpg * wl.lay.bytes, q, e->d_pyr, ps,
                                e->d_levels, e->d_cells, wl.cell0, wl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s,
-                               e->cand_stride, e->d_cell_cnt, ncells, batch, s0, wl.lay, wl.kcap);
+                               e->cand_stride, e->d_cell_cnt, ncells, batch, s0, wl.lay, wl.kcap, e->wave_twopass);
             return;
         }
         if (e->fast_rows && !e->fast_stop_after) {
@@ -3478,7 +3643,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     };
     auto blur = [&](hipStream_t q, int tile0, int n) {
         if (n <= 0 || e->desc_fb) return;                           // k_describe_fb blurs per keypoint
-        hipLaunchKernelGGL(k_blur7, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur, ps,
+        hipLaunchKernelGGL(e->blur_dot2 ? k_blur7<true> : k_blur7<false>, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur, ps,
                            e->d_levels, e->d_tiles, n, batch, s0, tile0);
     };
 
@@ -3697,7 +3862,9 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* fr = std::getenv("ORBX_FAST_ROWS")) e->fast_rows = std::atoi(fr) != 0;
     if (const char* fw = std::getenv("ORBX_FAST_WAVE")) e->fast_wave = std::atoi(fw) != 0;
     if (const char* fb = std::getenv("ORBX_DESC_FB")) e->desc_fb = std::atoi(fb) != 0;
+    if (const char* bd = std::getenv("ORBX_BLUR_DOT2")) e->blur_dot2 = std::atoi(bd) != 0;
     if (const char* pm = std::getenv("ORBX_FAST_PSMIN")) e->wave_psmin = std::atoi(pm);
+    if (const char* tp = std::getenv("ORBX_FAST_TWOPASS")) e->wave_twopass = std::atoi(tp) != 0;
     if (const char* fp = std::getenv("ORBX_FAST_WPG")) e->wave_wpg = std::atoi(fp) == 1 ? 1 : std::atoi(fp) == 2 ? 2 : 4;
     if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
     if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;

@@ -20,7 +20,8 @@ run write --pmc WRITE_SIZE
 run sqa --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT
 run sqb --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE
 python3 scripts/kernel_share.py $O/kt/run_kernel_trace.csv $TAG $STEPS --config $CFG --out $O/kernel_share.json || exit 1
-python3 scripts/pmc_summary.py $O $TAG 256 $ROWS $COLS k_fast_band $STEPS $O || exit 1
+DOM=$(python3 -c "import json; print(json.load(open('$O/kernel_share.json'))['dominant'].split('<')[0])") || exit 1
+python3 scripts/pmc_summary.py $O $TAG 256 $ROWS $COLS $DOM $STEPS $O || exit 1
 python3 scripts/sq_summary.py $O $O/sq_summary.json $CFG 256 $STEPS || exit 1
 cp $O/kt/run_kernel_stats.csv $O/${TAG}_kernel_stats.csv
 grep -o '"stage_ms_per_step": {[^}]*}' $O/kt.log > $O/live_stages_under_rocprof.txt || true
