@@ -1883,21 +1883,25 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
         for (int k = 0; k < 6; ++k) p[k] = blur_load<kMode>(row_ptr(y0 - 3 + k), x0, w);
         q0 = blur_hpair(p[0], p[1]); q1 = blur_hpair(p[2], p[3]); q2 = blur_hpair(p[4], p[5]);
     }
-    // ring of 4 row pairs; 8 output rows per iteration, input rows loaded 4 at a time (8 in flight spill at 128 VGPRs)
+    // ring of 4 row pairs; 8 output rows per iteration.  Interior strips (kMode 0) load the iteration's 8 input rows at
+    // once; the edge forms, whose per-byte reflection needs more registers, 4 at a time (8 spilled at 128 VGPRs)
     for (int y = y0; y < y1; y += 8) {
-        BlurWin p[4];
+        constexpr int kB = kMode == 0 ? 8 : 4;
+        BlurWin p[kB];
         uint32_t oe, oo;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) p[k] = blur_load<kMode>(row_ptr(y + 3 + k), x0, w);
+        for (int k = 0; k < kB; ++k) p[k] = blur_load<kMode>(row_ptr(y + 3 + k), x0, w);
         q3 = blur_hpair(p[0], p[1]); blur_emit2(q0, q1, q2, q3, oe, oo);
         store(y, oe); if (y + 1 >= y1) break; store(y + 1, oo); if (y + 2 >= y1) break;
         q0 = blur_hpair(p[2], p[3]); blur_emit2(q1, q2, q3, q0, oe, oo);
         store(y + 2, oe); if (y + 3 >= y1) break; store(y + 3, oo); if (y + 4 >= y1) break;
+        if constexpr (kB == 4) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) p[k] = blur_load<kMode>(row_ptr(y + 7 + k), x0, w);
-        q1 = blur_hpair(p[0], p[1]); blur_emit2(q2, q3, q0, q1, oe, oo);
+            for (int k = 0; k < 4; ++k) p[k] = blur_load<kMode>(row_ptr(y + 7 + k), x0, w);
+        }
+        q1 = blur_hpair(p[kB - 4], p[kB - 3]); blur_emit2(q2, q3, q0, q1, oe, oo);
         store(y + 4, oe); if (y + 5 >= y1) break; store(y + 5, oo); if (y + 6 >= y1) break;
-        q2 = blur_hpair(p[2], p[3]); blur_emit2(q3, q0, q1, q2, oe, oo);
+        q2 = blur_hpair(p[kB - 2], p[kB - 1]); blur_emit2(q3, q0, q1, q2, oe, oo);
         store(y + 6, oe); if (y + 7 >= y1) break; store(y + 7, oo);
     }
 }
@@ -1963,6 +1967,133 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_W
         blur_band<2>(S, sstride, D, L, x0, y0, y1);
 }
 
+
+// LDS-staged form (k_blur7_lds): each wave (one tile = level, 256-column strip, 16-row band) issues every load of its
+// tile at once -- input rows y0-3 .. y1+2 (REFLECT_101 rows) x columns sx-4 .. sx+267 as 16-byte chunks; a chunk that
+// crosses the level's left or right edge is assembled byte by byte with REFLECT_101 columns -- into its own LDS slice,
+// then runs the pair-row blur of blur_band2 on 12-byte windows read from LDS.  One memory round trip per band instead
+// of one per batch of 4 rows, and the reflection lives in the fill, so the blur itself has a single form.  The waves of
+// a workgroup are independent (wavefront fences only).
+constexpr int kBlurTileRow = 272;                                // 17 chunks of 16 bytes: columns sx-4 .. sx+267
+#ifndef ORBX_BLUR_LDS_ROWS
+#define ORBX_BLUR_LDS_ROWS 16                                    // output rows per LDS pass (r3ae: 8 -> 14-row slices, slower)
+#endif
+constexpr int kBlurLdsRows = ORBX_BLUR_LDS_ROWS;
+constexpr int kBlurTileBytes = (kBlurLdsRows + 6) * kBlurTileRow;
+
+__global__ __launch_bounds__(256) void k_blur7_lds(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                   size_t pyr_stride, const LevelDev* __restrict__ levels,
+                                                   const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0,
+                                                   int tile0) {
+    __shared__ __attribute__((aligned(16))) uint8_t tile_lds[4 * kBlurTileBytes];
+    static_assert(kBlurStrip == 256, "k_blur7_lds: 4 output columns per lane");
+    static_assert(kBlurBand % kBlurLdsRows == 0 && kBlurLdsRows % 8 == 0, "whole passes of 8 rows");
+    const int nbx = (ntiles + 3) / 4;                         // 4 tiles (waves) per workgroup
+    const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
+    if (item >= nbx * batch) return;
+    const int img = item / nbx;
+    const int tl = (item - img * nbx) * 4 + (threadIdx.x >> 6);
+    if (tl >= ntiles) return;                                 // whole wave
+    const BlurTile bt = tiles[tile0 + tl];
+    const LevelDev L = levels[bt.level];
+    int sstride;
+    const uint8_t* S = level_pixels(pyr, pyr_stride, L, bt.level, img, s0, sstride);
+    uint8_t* D = blur + img * pyr_stride + L.pyr_off;
+    const int h = L.h, w = L.w;
+    const int sx = bt.tx * kBlurStrip;
+    uint8_t* T = tile_lds + (threadIdx.x >> 6) * kBlurTileBytes;
+    const int ln = lane_id();
+    const int x0 = sx + 4 * ln;
+    const bool full = x0 + 4 <= w;
+    const uint8_t* tb = T + 4 * ln;                           // tile byte 4 ln = column x0 - 4
+    // chunk c holds columns xs = sx - 4 + 16c .. xs + 15.  Full chunks [c0, c1) lie inside the level row (one 16-byte
+    // load); chunk 0 of a left-edge strip and the chunks of a right-edge strip that reach past the row are built byte by
+    // byte (REFLECT_101 columns) in a second, short pass; chunks starting at or past column w + 3 are never read (the
+    // last output column w - 1 reads up to w + 2) and are skipped.
+    constexpr int kCh = kBlurTileRow / 16;                    // 17
+    const int c0 = sx - 4 < 0 ? 1 : 0;
+    const int c1 = max(c0, min(kCh, (w - (sx - 4)) / 16));
+    const int c2 = max(c1, min(kCh, (w + 3 - (sx - 4) + 15) / 16));
+    const int nfc = c1 - c0, nsc = c0 + (c2 - c1);
+    for (int ya = bt.ty * kBlurBand; ya < min(bt.ty * kBlurBand + kBlurBand, h); ya += kBlurLdsRows) {
+        const int y0 = ya, y1 = min(ya + kBlurLdsRows, h), R = y1 - y0 + 6;
+        auto row_of = [&](int r) {
+            const int yy = y0 - 3 + r;
+            return S + (size_t)(h >= 4 ? (yy < 0 ? -yy : (yy >= h ? 2 * h - 2 - yy : yy)) : refl101(yy, h)) * sstride;
+        };
+        const int NF = R * nfc;
+        if (nfc > 0) {
+            constexpr int kPf = ((kBlurLdsRows + 6) * kCh + kWave - 1) / kWave;
+            const int dr = kWave / nfc, dc = kWave - dr * nfc;
+            int r = ln / nfc, c = ln - r * nfc;
+            for (int q0 = 0; q0 < NF; q0 += kPf * kWave) {
+                uint32_t v[4 * kPf];
+                int rs[kPf], cs[kPf];
+#pragma unroll
+                for (int k = 0; k < kPf; ++k) {
+                    rs[k] = r; cs[k] = c0 + c;
+                    r += dr; c += dc;
+                    if (c >= nfc) { c -= nfc; ++r; }
+                    v[4 * k] = v[4 * k + 1] = v[4 * k + 2] = v[4 * k + 3] = 0;
+                    if (q0 + ln + k * kWave < NF) __builtin_memcpy(&v[4 * k], row_of(rs[k]) + sx - 4 + 16 * cs[k], 16);
+                }
+#pragma unroll
+                for (int k = 0; k < kPf; ++k)
+                    if (q0 + ln + k * kWave < NF)
+                        *reinterpret_cast<uint4*>(T + rs[k] * kBlurTileRow + 16 * cs[k]) =
+                            make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            }
+        }
+        const int NS = R * nsc;
+        for (int q = ln; q < NS; q += kWave) {
+            const int r = q / nsc, k = q - r * nsc;
+            const int c = k < c0 ? 0 : c1 + (k - c0);
+            const uint8_t* row = row_of(r);
+            const int xs = sx - 4 + 16 * c;
+            uint32_t b4[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {
+                const int x = xs + b;
+                const int xr = w >= 4 ? (x < 0 ? -x : (x >= w ? 2 * w - 2 - x : x)) : refl101(x, w);
+                if (x < w + 3) b4[b >> 2] |= (uint32_t)row[xr] << (8 * (b & 3));
+            }
+            *reinterpret_cast<uint4*>(T + r * kBlurTileRow + 16 * c) = make_uint4(b4[0], b4[1], b4[2], b4[3]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // the tile before any lane's window reads
+        if (x0 < w) {
+            auto win = [&](int tr) -> BlurWin {
+                const uint32_t* p = reinterpret_cast<const uint32_t*>(tb + tr * kBlurTileRow);
+                BlurWin o; o.w0 = p[0]; o.w1 = p[1]; o.w2 = p[2];
+                return o;
+            };
+            auto store = [&](int y, uint32_t packed) {
+                uint8_t* o = D + (size_t)y * w + x0;
+                if (full) {
+                    __builtin_memcpy(o, &packed, 4);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (x0 + j < w) o[j] = (uint8_t)(packed >> (8 * j));
+                }
+            };
+            // tile row t = input row y0 - 3 + t; output row y needs tile rows y - y0 .. y - y0 + 6
+            BlurPair q0 = blur_hpair(win(0), win(1)), q1 = blur_hpair(win(2), win(3)), q2 = blur_hpair(win(4), win(5)), q3;
+            for (int y = y0; y < y1; y += 8) {
+                const int t = y - y0 + 6;
+                uint32_t oe, oo;
+                q3 = blur_hpair(win(t), win(t + 1)); blur_emit2(q0, q1, q2, q3, oe, oo);
+                store(y, oe); if (y + 1 >= y1) break; store(y + 1, oo); if (y + 2 >= y1) break;
+                q0 = blur_hpair(win(t + 2), win(t + 3)); blur_emit2(q1, q2, q3, q0, oe, oo);
+                store(y + 2, oe); if (y + 3 >= y1) break; store(y + 3, oo); if (y + 4 >= y1) break;
+                q1 = blur_hpair(win(t + 4), win(t + 5)); blur_emit2(q2, q3, q0, q1, oe, oo);
+                store(y + 4, oe); if (y + 5 >= y1) break; store(y + 5, oo); if (y + 6 >= y1) break;
+                q2 = blur_hpair(win(t + 6), win(t + 7)); blur_emit2(q3, q0, q1, q2, oe, oo);
+                store(y + 6, oe); if (y + 7 >= y1) break; store(y + 7, oo);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // window reads before the next pass refills
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // Quadtree: DistributeOctTree (:539-763) as data-parallel passes.
@@ -3033,6 +3164,7 @@ struct Extractor {
     int wave_psmin = 24;      // pair stride >= 24: fewer resident FAST waves leave CUs to the overlapped stages (r3x:
                               // stride 20 is faster alone, 0.772 vs 0.825 ms serial, but 66.6k vs 67.1k frames/s)
     int desc_fb = 0;          // ORBX_DESC_FB: k_describe_fb (blur per keypoint in LDS, no k_blur7 / blurred pyramid)
+    int blur_lds = 0;         // ORBX_BLUR_LDS: k_blur7_lds (one load round per band, the blur from LDS)
     int blur_dot2 = 1;        // ORBX_BLUR_DOT2: k_blur7 in vertical row pairs with v_dot2 column sums (0: one row at a time)
     int band_g = 4;
     int fast_oe = 1;          // ORBX_FAST_OE: E-only pair image (O taps by v_alignbit), 0 = E and O images
@@ -3643,7 +3775,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     };
     auto blur = [&](hipStream_t q, int tile0, int n) {
         if (n <= 0 || e->desc_fb) return;                           // k_describe_fb blurs per keypoint
-        hipLaunchKernelGGL(e->blur_dot2 ? k_blur7<true> : k_blur7<false>, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur, ps,
+        hipLaunchKernelGGL(e->blur_lds ? k_blur7_lds : e->blur_dot2 ? k_blur7<true> : k_blur7<false>, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur, ps,
                            e->d_levels, e->d_tiles, n, batch, s0, tile0);
     };
 
@@ -3863,6 +3995,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* fw = std::getenv("ORBX_FAST_WAVE")) e->fast_wave = std::atoi(fw) != 0;
     if (const char* fb = std::getenv("ORBX_DESC_FB")) e->desc_fb = std::atoi(fb) != 0;
     if (const char* bd = std::getenv("ORBX_BLUR_DOT2")) e->blur_dot2 = std::atoi(bd) != 0;
+    if (const char* bl = std::getenv("ORBX_BLUR_LDS")) e->blur_lds = std::atoi(bl) != 0;
     if (const char* pm = std::getenv("ORBX_FAST_PSMIN")) e->wave_psmin = std::atoi(pm);
     if (const char* tp = std::getenv("ORBX_FAST_TWOPASS")) e->wave_twopass = std::atoi(tp) != 0;
     if (const char* fp = std::getenv("ORBX_FAST_WPG")) e->wave_wpg = std::atoi(fp) == 1 ? 1 : std::atoi(fp) == 2 ? 2 : 4;

@@ -173,12 +173,12 @@ def test_describe_keypoints_per_wave(gpu, monkeypatch, kpw):
     _check(S.kitti_like_image(410, rows=240, cols=333), nfeatures=777, nlevels=5, scale=1.3)
 
 
-@pytest.mark.parametrize("form", ["band", "band_blur1row", "rows", "wave", "wave_1pass", "wave20", "wave2", "wave1"])
+@pytest.mark.parametrize("form", ["band", "band_blur1row", "rows", "wave", "wave_blurlds", "wave_1pass", "wave20", "wave2", "wave1"])
 def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
     """Every FAST form -- k_fast_band (LDS band image, pre-test and survivor list), k_fast_rows (one wave per cell
     row in registers, every pixel scored, both thresholds' lists) and k_fast_wave (one wave per cell, no barrier; 4, 2
     or 1 waves per workgroup) -- is bit-exact against the oracle (and so is k_blur7 in both forms: vertical row pairs with
-    v_dot2 column sums, the default, and one row at a time): KITTI size, odd, tall and tiny sizes, uniform noise (most
+    v_dot2 column sums, the default, one row at a time, and k_blur7_lds staged through LDS): KITTI size, odd, tall and tiny sizes, uniform noise (most
     pixels survive the pre-test) and another parameter set, batched."""
     import torch
 
@@ -190,6 +190,7 @@ def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
     monkeypatch.setenv("ORBX_FAST_PSMIN", "20" if form == "wave20" else "24")   # pair stride 20 on KITTI-size cells
     monkeypatch.setenv("ORBX_FAST_TWOPASS", "0" if form == "wave_1pass" else "1")   # iniTh and minTh in one pass
     monkeypatch.setenv("ORBX_BLUR_DOT2", "0" if form == "band_blur1row" else "1")   # k_blur7 one row at a time
+    monkeypatch.setenv("ORBX_BLUR_LDS", "1" if form == "wave_blurlds" else "0")     # k_blur7_lds
     for shape, nf, kw in (((375, 1242), 2000, {}), ((377, 1243), 800, {}), ((120, 160), 300, {}),
                           ((1000, 200), 800, {}), ((40, 40), 100, {}), ((500, 500), 1000, {}),
                           ((480, 752), 1500, dict(nlevels=5, scale=1.3, ini=25, mn=10)),
