@@ -2189,8 +2189,9 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
     int* B_yr = B_xr + cap;
     int* B_cnt = B_yr + cap;
     int* B_seq = B_cnt + cap;
-    int* cc = B_seq + cap;         // [cap][4] child counts
-    int* base = cc + 4 * cap;      // new list position (unsplit) / group base (split)
+    int* cc = B_seq + cap;         // [cap][4] child counts of the current list
+    int* cc2 = cc + 4 * cap;       // [cap][4] child counts of the list being built (counted while keys move)
+    int* base = cc2 + 4 * cap;     // new list position (unsplit) / group base (split)
     int* sa = base + cap;          // scan array [scan_cap]
     int* sb = sa + scan_cap;       // scan array [scan_cap]
     int* tmp = sb + scan_cap;      // 32 ints
@@ -2258,6 +2259,21 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
     __syncthreads();
 
     QTP(1);
+#ifdef ORBX_QT_TRIVIAL
+    {   // diagnostics build only (upper bound of a faster DistributeOctTree): the level's first N keys, no quadtree --
+        // wrong keypoints, the same amount of work downstream
+        uint32_t* oxy = out_xy + (size_t)img * out_stride + L.out_off;
+        uint8_t* orr = out_r + (size_t)img * out_stride + L.out_off;
+        const int nout = min(min(K, L.N), L.out_cap);
+        for (int i = tid; i < nout; i += T) {
+            const uint32_t xy = kxy[i];
+            oxy[i] = ((xy & 0xffff) + minB) | (((xy >> 16) + minB) << 16);
+            orr[i] = kr[i];
+        }
+        if (tid == 0) level_cnt[img * nlevels + lvl] = nout | (int)((seq & 0x7fffu) << 16);
+        return;
+    }
+#endif
     // ---- 2. root nodes (:543-585)
     const int nIni = L.nIni;
     const float hX = L.hX;
@@ -2290,15 +2306,27 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
     __syncthreads();
     for (int k = tid; k < K; k += T) kn[k] = (int16_t)sa[kn[k]];
     for (int i = tid; i < n; i += T) { A_xr[i] = B_xr[i]; A_yr[i] = B_yr[i]; A_cnt[i] = B_cnt[i]; A_seq[i] = B_seq[i]; }
+    if (tid == 0) misc[0] = 0;                               // phase 1's count of nodes to expand
     __syncthreads();
 
     const int N = L.N;
-    bool phase2 = false, finished = false;
+    // A = the node list of the current pass, B = the list it builds; after a pass the two swap roles
+    auto swap_nodes = [&]() {
+        int* t;
+        t = cc; cc = cc2; cc2 = t;
+        t = A_xr; A_xr = B_xr; B_xr = t;
+        t = A_yr; A_yr = B_yr; B_yr = t;
+        t = A_cnt; A_cnt = B_cnt; B_cnt = t;
+        t = A_seq; A_seq = B_seq; B_seq = t;
+    };
+    bool phase2 = false, finished = false, counted = false;
     QTP(2);
     while (!finished) {
         const int prev = n;
         QTP(10 + phase2);
-        // -- child counts of every expandable node (phase 1 splits all of them, phase 2 needs their sizes)
+        // -- child counts of every expandable node (phase 1 splits all of them, phase 2 needs their sizes); after the
+        //    first pass they were counted while the previous pass moved the keys (cc2, now cc)
+        if (!counted) {
         for (int i = tid; i < 4 * n; i += T) cc[i] = 0;
         __syncthreads();
         for (int k = tid; k < K; k += T) {
@@ -2309,32 +2337,28 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             }
         }
         __syncthreads();
+        }
         QTP(20);
 
         if (!phase2) {
             // ---------------- phase 1 pass (:606-665)
+            // per node: children (split) or 1 survivor, packed as children << 16 | survivor so that ONE scan gives both
+            // prefixes (children before node i in the high half, survivors before it in the low half; totals < 2^15);
+            // base = the node's children count; nodes of >1 key to expand next (misc[0], zeroed in the last pass)
+            int nexp = 0;
             for (int i = tid; i < n; i += T) {
                 const int* c4 = cc + 4 * i;
                 const bool split = A_cnt[i] > 1;
-                sa[i] = split ? (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0) : 0;   // children
-                sb[i] = split ? 0 : 1;                                                       // survivors
-            }
-            if (tid == 0) misc[0] = 0;
-            __syncthreads();
-            int nexp = 0;
-            for (int i = tid; i < n; i += T) {
-                if (A_cnt[i] > 1) {
-                    const int* c4 = cc + 4 * i;
-                    nexp += (c4[0] > 1) + (c4[1] > 1) + (c4[2] > 1) + (c4[3] > 1);
-                }
+                const int nch = split ? (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0) : 0;
+                sa[i] = split ? (nch << 16) : 1;
+                base[i] = nch;
+                if (split) nexp += (c4[0] > 1) + (c4[1] > 1) + (c4[2] > 1) + (c4[3] > 1);
             }
             nexp = wave_sum(nexp);
             if (lane_id() == 0) atomicAdd(&misc[0], nexp);
-            // keep children counts before the scan overwrites sa
-            for (int i = tid; i < n; i += T) base[i] = sa[i];
             __syncthreads();
-            const int C = block_scan_array(sa, n, tmp);     // sa = children before node i (creation order)
-            const int U = block_scan_array(sb, n, tmp);     // sb = survivors before node i
+            const int CU = block_scan_array(sa, n, tmp);
+            const int C = CU >> 16, U = CU & 0xffff;
             const int nToExpand = misc[0];
             const int nn = C + U;
             QTP(30);
@@ -2342,7 +2366,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             for (int i = tid; i < n; i += T) {
                 const int nch = base[i];
                 if (A_cnt[i] > 1) {
-                    const int gb = C - sa[i] - nch;
+                    const int gb = C - (sa[i] >> 16) - nch;
                     base[i] = gb;
                     const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
                     const int* c4 = cc + 4 * i;
@@ -2354,28 +2378,41 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                         B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
                         B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
                         B_cnt[p] = c4[q];
-                        B_seq[p] = sa[i] + rank_asc(c4, q);
+                        B_seq[p] = (sa[i] >> 16) + rank_asc(c4, q);
+                        reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
                     }
                 } else {
-                    const int p = C + sb[i];
+                    const int p = C + (sa[i] & 0xffff);
                     base[i] = p;
                     B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
+                    reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
                 }
             }
             __syncthreads();
+            if (tid == 0) misc[0] = 0;                           // every thread has read nToExpand
             for (int k = tid; k < K; k += T) {
                 const int i = kn[k];
+                const uint32_t xy = kxy[k];
+                int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
+                int p, c;                                        // new list position, its key count
                 if (A_cnt[i] > 1) {
-                    const int q = quadrant(kxy[k], A_xr[i] & 0xffff, A_xr[i] >> 16, A_yr[i] & 0xffff, A_yr[i] >> 16);
-                    kn[k] = (int16_t)(base[i] + rank_desc(cc + 4 * i, q));
+                    const int q = quadrant(xy, x0, x1, y0, y1);
+                    p = base[i] + rank_desc(cc + 4 * i, q);
+                    c = cc[4 * i + q];
+                    int cx0, cx1, cy0, cy1;
+                    child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
+                    x0 = cx0; x1 = cx1; y0 = cy0; y1 = cy1;
                 } else {
-                    kn[k] = (int16_t)base[i];
+                    p = base[i];
+                    c = A_cnt[i];
                 }
+                kn[k] = (int16_t)p;
+                if (c > 1) atomicAdd(&cc2[4 * p + quadrant(xy, x0, x1, y0, y1)], 1);   // the next pass's counts
             }
             __syncthreads();
-            for (int i = tid; i < nn; i += T) { A_xr[i] = B_xr[i]; A_yr[i] = B_yr[i]; A_cnt[i] = B_cnt[i]; A_seq[i] = B_seq[i]; }
+            swap_nodes();                                        // the new list becomes A (no copy, no barrier)
+            counted = true;
             n = nn;
-            __syncthreads();
             QTP(50);
             if (n >= N || n == prev) finished = true;              // :669-672
             else if (n + nToExpand * 3 > N) phase2 = true;         // :673
@@ -2393,24 +2430,15 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                 if (A_cnt[i] > 1)
                     sk[sa[i]] = ((unsigned long long)A_cnt[i] << 40) | ((unsigned long long)A_seq[i] << 20) | (unsigned long long)i;
             __syncthreads();
-            // bitonic sort ascending
-            for (int kk = 2; kk <= P2; kk <<= 1) {
-                for (int j = kk >> 1; j > 0; j >>= 1) {
-                    for (int i = tid; i < P2; i += T) {
-                        const int ixj = i ^ j;
-                        if (ixj > i) {
-                            const unsigned long long a = sk[i], b = sk[ixj];
-                            const bool up = (i & kk) == 0;
-                            if ((a > b) == up) { sk[i] = b; sk[ixj] = a; }
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-            // processing order p = 0.. is descending key order; delta_p = children_p - 1
+            // bitonic sort ascending (keys are unique: node index in the low bits); stages inside a wave's 128 keys
+            // need only a wave-level fence (block_bitonic_u64).  (Ranking each key by counting the smaller ones, no
+            // dependent stages, measured slower: 9 -> 15.7 us per level-0 pass, r3am.)
+            if (P2 >= 2) block_bitonic_u64(sk, P2);
+            auto key_at = [&](int p) { return sk[nV - 1 - p]; };     // processing order: descending keys
+            // delta_p = children_p - 1
             QTP(31);
             for (int p = tid; p < nV; p += T) {
-                const int i = (int)(sk[nV - 1 - p] & 0xfffff);
+                const int i = (int)(key_at(p) & 0xfffff);
                 const int* c4 = cc + 4 * i;
                 sb[p] = (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0);
             }
@@ -2431,7 +2459,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             for (int i = tid; i < n; i += T) base[i] = -1;
             __syncthreads();
             for (int p = tid; p < nproc; p += T) {
-                const int i = (int)(sk[nV - 1 - p] & 0xfffff);
+                const int i = (int)(key_at(p) & 0xfffff);
                 base[i] = Cn - sa[p] - sb[p];
                 A_seq[i] = -1 - sa[p];           // stash creation prefix (node is erased anyway)
             }
@@ -2457,26 +2485,38 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                         B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
                         B_cnt[p] = c4[q];
                         B_seq[p] = cre + rank_asc(c4, q);
+                        reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
                     }
                 } else {
                     const int p = Cn + sb[i];
                     B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
+                    reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
                 }
             }
             __syncthreads();
             for (int k = tid; k < K; k += T) {
                 const int i = kn[k];
+                const uint32_t xy = kxy[k];
+                int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
+                int p, c;
                 if (base[i] >= 0) {
-                    const int q = quadrant(kxy[k], A_xr[i] & 0xffff, A_xr[i] >> 16, A_yr[i] & 0xffff, A_yr[i] >> 16);
-                    kn[k] = (int16_t)(base[i] + rank_desc(cc + 4 * i, q));
+                    const int q = quadrant(xy, x0, x1, y0, y1);
+                    p = base[i] + rank_desc(cc + 4 * i, q);
+                    c = cc[4 * i + q];
+                    int cx0, cx1, cy0, cy1;
+                    child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
+                    x0 = cx0; x1 = cx1; y0 = cy0; y1 = cy1;
                 } else {
-                    kn[k] = (int16_t)(Cn + sb[i]);
+                    p = Cn + sb[i];
+                    c = A_cnt[i];
                 }
+                kn[k] = (int16_t)p;
+                if (c > 1) atomicAdd(&cc2[4 * p + quadrant(xy, x0, x1, y0, y1)], 1);   // the next pass's counts
             }
             __syncthreads();
-            for (int i = tid; i < nn; i += T) { A_xr[i] = B_xr[i]; A_yr[i] = B_yr[i]; A_cnt[i] = B_cnt[i]; A_seq[i] = B_seq[i]; }
+            swap_nodes();
+            counted = true;
             n = nn;
-            __syncthreads();
             QTP(51);
             if (n >= N || n == prev) finished = true;              // :734-735
         }
@@ -3686,7 +3726,7 @@ int Extractor::configure(int r, int c, int batch) {
 static size_t qt_lds_bytes(int cap, int scan_cap) {
     int p2 = 1;
     while (p2 < cap) p2 <<= 1;
-    const size_t ints = 8 * (size_t)cap + 4 * (size_t)cap + (size_t)cap + 2 * (size_t)scan_cap + 32 + 16 + 2;
+    const size_t ints = 8 * (size_t)cap + 8 * (size_t)cap + (size_t)cap + 2 * (size_t)scan_cap + 32 + 16 + 2;
     return ints * 4 + (size_t)p2 * 8;
 }
 
