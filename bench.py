@@ -909,6 +909,10 @@ def main():
     engine.check()
     if rank == 0:
         print(json.dumps(out), flush=True)
+    # ordered teardown while the runtime is up: every queue drained, then the library objects destroyed newest first
+    torch.cuda.synchronize()
+    pkg.orbx.close_all()
+    torch.cuda.synchronize()
     if world > 1:
         dist.destroy_process_group()
 

@@ -8,9 +8,11 @@ GPU is missing the constructors raise.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
 import re
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -30,6 +32,31 @@ class OrbxError(RuntimeError):
     def __init__(self, code: int, what: str):
         super().__init__(f"orbx error {code}: {what}")
         self.code = code
+
+
+# Every live library object, in creation order.  At interpreter exit they are destroyed newest first by close_all
+# (registered with atexit after torch's own handlers, so it runs before them): each destroy waits for its own streams
+# and events and then frees its device memory while the HIP runtime is fully up, instead of in whatever order module
+# teardown and garbage collection reach them.
+_LIVE: list = []
+
+
+def _register(obj):
+    _LIVE.append(weakref.ref(obj))
+
+
+def close_all():
+    """Destroy every live library object (newest first).  Called at exit; callable earlier."""
+    while _LIVE:
+        o = _LIVE.pop()()
+        if o is not None:
+            try:
+                o.close()
+            except Exception:
+                pass
+
+
+atexit.register(close_all)
 
 
 class FeatVec(C.Structure):
@@ -300,6 +327,7 @@ class ORBextractor:
                                                C.byref(h)))
         self._h = h
         self.nfeatures, self.nlevels, self.device = nfeatures, nlevels, device
+        _register(self)
         self._last_shape = None
 
     def close(self):
@@ -460,6 +488,7 @@ class ORBmatcher:
         _check(self._lib.orbx_matcher_create(nnratio, int(checkOri), device, C.byref(h)))
         self._h = h
         self.mfNNratio, self.mbCheckOrientation, self.device = nnratio, checkOri, device
+        _register(self)
         assert self._lib.orbx_th_high() == self.TH_HIGH and self._lib.orbx_th_low() == self.TH_LOW
 
     def close(self):
@@ -841,6 +870,7 @@ class ORBVocabulary:
         self._lib = load_library()
         self._h = handle
         self.device = device
+        _register(self)
 
     @classmethod
     def load_text(cls, path: str, device: int = 0):
@@ -926,6 +956,7 @@ class KeyFrameDatabase:
         self._h = C.c_void_p()
         _check(self._lib.orbx_kfdb_create(n_vocab_words, max_slots, max_words, device, C.byref(self._h)))
         self.n_vocab_words, self.max_slots, self.max_words, self.device = n_vocab_words, max_slots, max_words, device
+        _register(self)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -1123,6 +1154,7 @@ class KeyframeExchangeRCCL:
         self._h = C.c_void_p()
         b = C.create_string_buffer(bytes(uid), 128)
         _check(self._lib.orbx_exchange_create(b, world, rank, device, C.byref(self._h)))
+        _register(self)
         self.world, self.rank, self.device = world, rank, device
 
     def close(self):
@@ -1158,6 +1190,7 @@ class KeyframeFusionEngine:
         _check(self._lib.orbx_fusion_create(vocab._h, matcher._h, capacity, slots, max_keyframes, candidates, levelsup,
                                             min_matches, agent, world, device, C.byref(self._h)))
         self.capacity, self.slots, self.k, self.agent, self.world, self.device = capacity, slots, candidates, agent, world, device
+        _register(self)
         pb, ns, ring, st = C.c_size_t(), C.c_int(), C.c_void_p(), KfStore()
         _check(self._lib.orbx_fusion_info(self._h, C.byref(pb), C.byref(ns), C.byref(ring), C.byref(st)))
         self.packet_bytes = pb.value
