@@ -21,7 +21,7 @@ def test_defaults_and_compulsory_bytes(monkeypatch):
     b = _bench()
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = b.parse()
-    assert (a.gpus, a.steps, a.warmup, a.config, a.batch) == (1, 20, 5, "kitti", 128)
+    assert (a.gpus, a.steps, a.warmup, a.config, a.batch) == (1, 20, 5, "kitti", 256)
     assert a.desc_stream == 1 and a.sets == 3          # the measured schedule
     cb = b.compulsory_bytes(b.CONFIGS["kitti"])
     assert cb["extraction"] == 375 * 1242 + 2000 * 60 == 585750
