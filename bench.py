@@ -89,6 +89,8 @@ def parse():
                          "re-read every step)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
+    ap.add_argument("--alone-reps", type=int, default=5,
+                    help="calls of the roofline_alone block (the extraction alone, one stream); 0 skips it")
     ap.add_argument("--host-fed-steps", type=int, default=10,
                     help="steps of the host-fed block: the batch's images copied H2D from pinned host memory every step on a "
                          "copy stream, overlapped with the previous step (0 = skip)")
@@ -411,6 +413,36 @@ def cd_block(pkg, MA, kps, desc, cnt, vocab, B, reps=3):
                 {"KITTI 00 (mkf 136.2)": 1850.51, "KITTI 02": 15297.20, "EuRoC MH01": 7362.53},
             "path": "multiagent.CovisibilityDiscovery: orbx_kfdb_score_device (minScore), orbx_kfdb_detect_device COVIS, "
                     "one candidate-count readback, orbx_kfdb_candidate_pairs_device, orbx_search_by_bow_kfkf_pairs_device"}
+
+
+def alone_block(pkg, cfg, imgs, dev, reps=5):
+    """The extraction of one step's batch with every stage on one stream (ORBX_PIPELINE=0) and nothing else on the GPU:
+    per-stage spans of HIP events around each kernel, so each span is that kernel's own duration (plus launch gaps).
+    `roofline_alone` divides the dominant kernel's algorithmic bytes by its span here; the contract's
+    `roofline` uses the spans of the overlapped step, where every kernel shares the CUs with four other queues."""
+    import torch
+    saved = os.environ.get("ORBX_PIPELINE")
+    os.environ["ORBX_PIPELINE"] = "0"                  # read at extractor creation
+    try:
+        ex = pkg.ORBextractor(cfg["nfeatures"], SCALE, NLEV, INI, MINTH, device=dev.index)
+    finally:
+        if saved is None:
+            os.environ.pop("ORBX_PIPELINE")
+        else:
+            os.environ["ORBX_PIPELINE"] = saved
+    s = torch.cuda.current_stream(dev)
+    outs = ex.extract_batch_device(imgs, stream=s)
+    for _ in range(2):
+        ex.extract_batch_device(imgs, *outs, stream=s)
+    torch.cuda.synchronize()
+    ex.enable_timing(True)
+    for _ in range(reps):
+        ex.extract_batch_device(imgs, *outs, stream=s)
+    torch.cuda.synchronize()
+    st, calls = ex.stage_times()
+    ex.close()
+    per = {k: round(v / max(calls, 1), 4) for k, v in st.items()}
+    return per, calls
 
 
 def c3_bench(pkg, dev, n_problems=64, reps=30):
@@ -894,6 +926,18 @@ def main():
 
     if rank == 0 and world == 1 and args.c3:
         out["c3_bruteforce"] = c3_bench(pkg, dev)
+    if rank == 0 and world == 1 and not args.no_timing and args.alone_reps > 0:
+        per, calls = alone_block(pkg, cfg, img_sets[0], dev, args.alone_reps)
+        fam = kernel_family(active_kernel_names()["fast"])
+        t_ms = sum(per.get(st_, 0.0) for st_ in LIVE_STAGES[fam])
+        cb = compulsory_bytes(cfg)["extraction"] * 2 * B
+        ach = cb / (t_ms * 1e-3) / 1e9 if t_ms > 0 else 0.0
+        out["roofline_alone"] = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(ach / HBM_PEAK_GBS, 6), "kernel": active_kernel_names()["fast"],
+                                 "kernel_ms_per_step": round(t_ms, 4), "algorithmic_bytes_per_step": cb,
+                                 "stage_ms_alone": per, "calls": calls,
+                                 "schedule": "the step's extraction only, every stage on one stream (ORBX_PIPELINE=0), "
+                                             "HIP events around each kernel: each kernel's own duration"}
     gate, _ = engine.stats()
     out["fusion_gate_passed_per_step"] = round(gate / (args.steps + args.warmup + STORE_STEPS), 2)
     if rank == 0 and world == 1 and args.host_fed_steps > 0:
