@@ -1188,6 +1188,109 @@ __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_A
 // score-map row stride (int16) per pair stride: >= (Wd + 5) & ~1 for every cell the pair stride admits
 __host__ __device__ constexpr int fastw_sw(int ps) { return ps == 20 ? 36 : ps == 24 ? 44 : 76; }
 
+// The part of a cell after its ROI is in LDS: pre-test, scores, NMS at both thresholds, the cell's candidate slots.
+template <int kPS>
+__device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __restrict__ sc, uint16_t* __restrict__ list,
+                                           const CellDev& cd, int img, int* __restrict__ cnt_out, int Wd, int Hd, int T1,
+                                           int T2, int tp, uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
+                                           int cand_stride, int kcap, int two_pass, int ln) {
+    constexpr int SW = fastw_sw(kPS);
+    wave_fence();
+    const uint64_t below = (1ull << ln) - 1ull;
+    // 2. compass pre-test at min(iniTh, minTh) in quads; survivors compacted in row-major order
+    const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
+    // With minThFAST < iniThFAST the cell runs at iniThFAST first (fewer survivors to score); only a cell that kept
+    // nothing there -- a wave-uniform branch, no barrier -- runs again at minThFAST over all its pairs (:812-816).  The
+    // second pass finds every minTh survivor (a superset of the first pass's, whose scores it rewrites with the same
+    // values) and starts its list afresh.  Otherwise one pass at min(iniTh, minTh) keeps both thresholds' pixels.
+    const bool two = two_pass && T2 < T1;
+    uint16_t* k1 = reinterpret_cast<uint16_t*>(E);                  // key lists over the pair image (dead after scoring)
+    uint16_t* k2 = k1 + kcap;
+    int n1 = 0, n2 = 0;                                               // wave-uniform
+    for (int pass = 0; pass < 2; ++pass) {
+    const int tpre = two ? (pass == 0 ? T1 : T2) : tp;
+    const int fmask = two ? (pass == 0 ? 3 : 12) : 15;
+    int ns = 0;                                                       // wave-uniform
+    {
+        // 2. compass pre-test in quads: quad q -> (row q / QR, column q % QR), walked incrementally; two quads per lane
+        // per round (q, q + 64), both read before either is tested.  Survivors are appended in quad order (row-major).
+        const int dr = kWave / QR, du = kWave - dr * QR;
+        int rr = ln / QR, u = ln - rr * QR;
+        auto step = [&](int& r0, int& u0) { r0 += dr; u0 += du; if (u0 >= QR) { u0 -= QR; ++r0; } };
+        auto emit = [&](uint32_t mq, int r0, int u0) {
+            const int cq = __builtin_popcount(mq);
+            const uint64_t b0 = __ballot(cq & 1), b1 = __ballot(cq & 2), b2 = __ballot(cq & 4);
+            int pos = ns + __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((mq >> k) & 1u) list[pos++] = (uint16_t)((r0 << 8) | (4 * u0 + k));
+            ns += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+        };
+        for (int q0 = 0; q0 < NQ4; q0 += 2 * kWave) {
+            const int qa = q0 + ln, qb = qa + kWave;
+            const int ra = rr, ua = u;
+            step(rr, u);
+            const int rb = rr, ub = u;
+            step(rr, u);
+            const bool va = qa < NQ4, vb = qb < NQ4;
+            const QuadTaps ta = fastw_quad_load<kPS>(E, va ? ra : 0, va ? ua : 0);
+            const QuadTaps tb = fastw_quad_load<kPS>(E, vb ? rb : 0, vb ? ub : 0);
+            const uint32_t ma = va ? fastw_quad_test(ta, ua, tpre, PR, Wd) : 0u;
+            const uint32_t mb = vb ? fastw_quad_test(tb, ub, tpre, PR, Wd) : 0u;
+            emit(ma, ra, ua);
+            emit(mb, rb, ub);
+        }
+    }
+    wave_fence();
+    // 3. closed-form scores of the survivors, two per lane per round (both tap sets read before either is scored)
+    for (int i = ln; i < ns; i += 2 * kWave) {
+        const int i2 = i + kWave;
+        const uint32_t e1 = list[i], e2 = i2 < ns ? list[i2] : e1;
+        const int rr1 = e1 >> 8, j1 = e1 & 0xff, rr2 = e2 >> 8, j2 = e2 & 0xff;
+        uint32_t t1[17], t2[17];
+        fast_taps_f16<kPS>(E, rr1 + 3, j1, t1);
+        fast_taps_f16<kPS>(E, rr2 + 3, j2, t2);
+        const s16x2 s1 = fast_score_from_taps_f16(t1), s2 = fast_score_from_taps_f16(t2);
+        *(s16x2*)(sc + (rr1 + 1) * SW + 2 + 2 * j1) = (2 * j1 + 1 < Wd) ? s1 : (s16x2){s1.x, (short)-1};
+        if (i2 < ns) *(s16x2*)(sc + (rr2 + 1) * SW + 2 + 2 * j2) = (2 * j2 + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
+    }
+    wave_fence();
+    // 4. strict 3x3 NMS at iniTh (bits 0, 1) and minTh (bits 2, 3); kept pixels appended in list order (= row-major)
+    //    to the two key lists, which take over the pair image's LDS (key = row * 128 + column in the detection window)
+    for (int i0 = 0; i0 < ns; i0 += kWave) {
+        const int i = i0 + ln;
+        int f = 0, key = 0;
+        if (i < ns) {
+            const int rr = list[i] >> 8, j = list[i] & 0xff;
+            f = nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
+            key = rr * 128 + 2 * j;
+        }
+        const uint64_t a0 = __ballot(f & 1), a1 = __ballot(f & 2), c0 = __ballot(f & 4), c1 = __ballot(f & 8);
+        int p1 = n1 + __popcll(a0 & below) + __popcll(a1 & below);
+        int p2 = n2 + __popcll(c0 & below) + __popcll(c1 & below);
+        if (f & 1) { if (p1 < kcap) k1[p1] = (uint16_t)key; ++p1; }
+        if ((f & 2) && p1 < kcap) k1[p1] = (uint16_t)(key + 1);
+        if (f & 4) { if (p2 < kcap) k2[p2] = (uint16_t)key; ++p2; }
+        if ((f & 8) && p2 < kcap) k2[p2] = (uint16_t)(key + 1);
+        n1 += __popcll(a0) + __popcll(a1);
+        n2 += __popcll(c0) + __popcll(c1);
+    }
+    wave_fence();
+    if (!two || n1 > 0) break;                                        // wave-uniform
+    }
+    // 5. the cell's list (iniTh, or minTh when iniTh kept nothing: :812-816) -> its candidate slots, coalesced
+    const uint16_t* ks = n1 > 0 ? k1 : k2;
+    const int n = min(n1 > 0 ? n1 : n2, min(kcap, cd.slot_cap));
+    uint32_t* oxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
+    uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
+    for (int i = ln; i < n; i += kWave) {
+        const int k = ks[i], rr = k >> 7, x = k & 127;
+        oxy[i] = (uint32_t)(cd.x0 + 3 + x) | ((uint32_t)(cd.y0 + rr + 3) << 16);
+        os[i] = (uint8_t)sc[(rr + 1) * SW + 2 + x];
+    }
+    if (ln == 0) *cnt_out = n;
+}
+
 template <int kPS, int kWpg>
 __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                          const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
@@ -1299,100 +1402,101 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
         const int n16 = ((Hd + 2) * SW * 2 + 15) >> 4;
         for (int i = ln; i < n16; i += kWave) reinterpret_cast<uint4*>(sc)[i] = make_uint4(0, 0, 0, 0);
     }
-    wave_fence();
-    const uint64_t below = (1ull << ln) - 1ull;
-    // 2. compass pre-test at min(iniTh, minTh) in quads; survivors compacted in row-major order
-    const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
-    // With minThFAST < iniThFAST the cell runs at iniThFAST first (fewer survivors to score); only a cell that kept
-    // nothing there -- a wave-uniform branch, no barrier -- runs again at minThFAST over all its pairs (:812-816).  The
-    // second pass finds every minTh survivor (a superset of the first pass's, whose scores it rewrites with the same
-    // values) and starts its list afresh.  Otherwise one pass at min(iniTh, minTh) keeps both thresholds' pixels.
-    const bool two = two_pass && T2 < T1;
-    uint16_t* k1 = reinterpret_cast<uint16_t*>(E);                  // key lists over the pair image (dead after scoring)
-    uint16_t* k2 = k1 + kcap;
-    int n1 = 0, n2 = 0;                                               // wave-uniform
-    for (int pass = 0; pass < 2; ++pass) {
-    const int tpre = two ? (pass == 0 ? T1 : T2) : tp;
-    const int fmask = two ? (pass == 0 ? 3 : 12) : 15;
-    int ns = 0;                                                       // wave-uniform
-    {
-        // 2. compass pre-test in quads: quad q -> (row q / QR, column q % QR), walked incrementally; two quads per lane
-        // per round (q, q + 64), both read before either is tested.  Survivors are appended in quad order (row-major).
-        const int dr = kWave / QR, du = kWave - dr * QR;
-        int rr = ln / QR, u = ln - rr * QR;
-        auto step = [&](int& r0, int& u0) { r0 += dr; u0 += du; if (u0 >= QR) { u0 -= QR; ++r0; } };
-        auto emit = [&](uint32_t mq, int r0, int u0) {
-            const int cq = __builtin_popcount(mq);
-            const uint64_t b0 = __ballot(cq & 1), b1 = __ballot(cq & 2), b2 = __ballot(cq & 4);
-            int pos = ns + __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
+    fastw_body<kPS>(E, sc, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
+}
+
+// k_fast_wave_p: k_fast_wave with each wave walking kCells consecutive (image, cell) items, the next cell's ROI loaded into
+// registers (its cell record first, a scalar load) while the current cell is processed, so the dependent chain cell
+// record -> level record -> ROI rows of a wave's start is paid once per kCells cells.  Pair stride 24 (16-byte chunks,
+// ROI <= 48 x 72: <= 4 load rounds of 64 lanes).
+constexpr int kRoiPf = 4;
+struct FastwRoi { uint32_t v[4 * kRoiPf]; int rs[kRoiPf], cs[kRoiPf]; int nq; };
+
+__device__ __forceinline__ void fastw_roi_issue(FastwRoi& R, const uint8_t* __restrict__ src0, int lstride, int W, int H,
+                                                int ln) {
+    const int cpr = (W + 15) >> 4;
+    R.nq = H * cpr;
+    const int dr = kWave / cpr, dc = kWave - dr * cpr;
+    int r = ln / cpr, cc = ln - r * cpr;
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if ((mq >> k) & 1u) list[pos++] = (uint16_t)((r0 << 8) | (4 * u0 + k));
-            ns += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-        };
-        for (int q0 = 0; q0 < NQ4; q0 += 2 * kWave) {
-            const int qa = q0 + ln, qb = qa + kWave;
-            const int ra = rr, ua = u;
-            step(rr, u);
-            const int rb = rr, ub = u;
-            step(rr, u);
-            const bool va = qa < NQ4, vb = qb < NQ4;
-            const QuadTaps ta = fastw_quad_load<kPS>(E, va ? ra : 0, va ? ua : 0);
-            const QuadTaps tb = fastw_quad_load<kPS>(E, vb ? rb : 0, vb ? ub : 0);
-            const uint32_t ma = va ? fastw_quad_test(ta, ua, tpre, PR, Wd) : 0u;
-            const uint32_t mb = vb ? fastw_quad_test(tb, ub, tpre, PR, Wd) : 0u;
-            emit(ma, ra, ua);
-            emit(mb, rb, ub);
+    for (int k = 0; k < kRoiPf; ++k) {
+        R.rs[k] = r; R.cs[k] = cc;
+        r += dr; cc += dc;
+        if (cc >= cpr) { cc -= cpr; ++r; }
+        if (ln + k * kWave < R.nq) __builtin_memcpy(&R.v[4 * k], src0 + (size_t)R.rs[k] * lstride + 16 * R.cs[k], 16);
+    }
+}
+
+template <int kPS>
+__device__ __forceinline__ void fastw_roi_store(const FastwRoi& R, uint32_t* __restrict__ E, int ln) {
+#pragma unroll
+    for (int k = 0; k < kRoiPf; ++k) {
+        if (ln + k * kWave < R.nq) {
+            const uint32_t x = R.v[4 * k], y = R.v[4 * k + 1], z = R.v[4 * k + 2], w = R.v[4 * k + 3];
+            uint4* dst = reinterpret_cast<uint4*>(E + R.rs[k] * kPS + 8 * R.cs[k]);
+            dst[0] = make_uint4(__builtin_amdgcn_perm(y, x, 0x0c010c00u) | 0x64006400u, __builtin_amdgcn_perm(y, x, 0x0c030c02u) | 0x64006400u,
+                                __builtin_amdgcn_perm(y, x, 0x0c050c04u) | 0x64006400u, __builtin_amdgcn_perm(y, x, 0x0c070c06u) | 0x64006400u);
+            dst[1] = make_uint4(__builtin_amdgcn_perm(w, z, 0x0c010c00u) | 0x64006400u, __builtin_amdgcn_perm(w, z, 0x0c030c02u) | 0x64006400u,
+                                __builtin_amdgcn_perm(w, z, 0x0c050c04u) | 0x64006400u, __builtin_amdgcn_perm(w, z, 0x0c070c06u) | 0x64006400u);
         }
     }
-    wave_fence();
-    // 3. closed-form scores of the survivors, two per lane per round (both tap sets read before either is scored)
-    for (int i = ln; i < ns; i += 2 * kWave) {
-        const int i2 = i + kWave;
-        const uint32_t e1 = list[i], e2 = i2 < ns ? list[i2] : e1;
-        const int rr1 = e1 >> 8, j1 = e1 & 0xff, rr2 = e2 >> 8, j2 = e2 & 0xff;
-        uint32_t t1[17], t2[17];
-        fast_taps_f16<kPS>(E, rr1 + 3, j1, t1);
-        fast_taps_f16<kPS>(E, rr2 + 3, j2, t2);
-        const s16x2 s1 = fast_score_from_taps_f16(t1), s2 = fast_score_from_taps_f16(t2);
-        *(s16x2*)(sc + (rr1 + 1) * SW + 2 + 2 * j1) = (2 * j1 + 1 < Wd) ? s1 : (s16x2){s1.x, (short)-1};
-        if (i2 < ns) *(s16x2*)(sc + (rr2 + 1) * SW + 2 + 2 * j2) = (2 * j2 + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
-    }
-    wave_fence();
-    // 4. strict 3x3 NMS at iniTh (bits 0, 1) and minTh (bits 2, 3); kept pixels appended in list order (= row-major)
-    //    to the two key lists, which take over the pair image's LDS (key = row * 128 + column in the detection window)
-    for (int i0 = 0; i0 < ns; i0 += kWave) {
-        const int i = i0 + ln;
-        int f = 0, key = 0;
-        if (i < ns) {
-            const int rr = list[i] >> 8, j = list[i] & 0xff;
-            f = nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
-            key = rr * 128 + 2 * j;
+}
+
+template <int kWpg, int kCells>
+__global__ __launch_bounds__(64 * kWpg) void k_fast_wave_p(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                           const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
+                                                           int cell0, int ncell, int iniTh, int minTh,
+                                                           uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
+                                                           int cand_stride, int* __restrict__ cell_cnt, int ncells, int batch,
+                                                           Src0 s0, WaveLds lay, int kcap, int two_pass) {
+    constexpr int kPS = 24, SW = fastw_sw(kPS);
+    extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
+    const int w = threadIdx.x >> 6, ln = lane_id();
+    const int total = ncell * batch, nwv = (total + kCells - 1) / kCells, nwg = (nwv + kWpg - 1) / kWpg;
+    const int wg = xcd_item(xcd_chunk(nwg));                        // consecutive cells of one image on one XCD
+    const int wv = __builtin_amdgcn_readfirstlane(wg * kWpg + w);
+    if (wg >= nwg || wv >= nwv) return;                             // whole wave (no barrier in this kernel)
+    const int first = wv * kCells, last = min(first + kCells, total);
+    char* lds = reinterpret_cast<char*>(fsm) + w * lay.bytes;
+    uint32_t* E = reinterpret_cast<uint32_t*>(lds);
+    int16_t* sc = reinterpret_cast<int16_t*>(lds + lay.o_sc);
+    uint16_t* list = reinterpret_cast<uint16_t*>(lds + lay.o_list);
+    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
+    const int tp = min(T1, T2);
+    FastwRoi R;
+    auto prep = [&](int item, CellDev& cd, int& img, int& c) {   // the item's cell record, then its ROI loads
+        img = item / ncell;
+        c = cell0 + (item - img * ncell);
+        cd = cells[c];
+        if (cd.W > 6 && cd.H > 6) {
+            const LevelDev& L = levels[cd.level];
+            int lstride;
+            const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
+            fastw_roi_issue(R, base + (size_t)cd.y0 * lstride + cd.x0, lstride, cd.W, cd.H, ln);
         }
-        const uint64_t a0 = __ballot(f & 1), a1 = __ballot(f & 2), c0 = __ballot(f & 4), c1 = __ballot(f & 8);
-        int p1 = n1 + __popcll(a0 & below) + __popcll(a1 & below);
-        int p2 = n2 + __popcll(c0 & below) + __popcll(c1 & below);
-        if (f & 1) { if (p1 < kcap) k1[p1] = (uint16_t)key; ++p1; }
-        if ((f & 2) && p1 < kcap) k1[p1] = (uint16_t)(key + 1);
-        if (f & 4) { if (p2 < kcap) k2[p2] = (uint16_t)key; ++p2; }
-        if ((f & 8) && p2 < kcap) k2[p2] = (uint16_t)(key + 1);
-        n1 += __popcll(a0) + __popcll(a1);
-        n2 += __popcll(c0) + __popcll(c1);
+    };
+    CellDev cd;
+    int img, c;
+    prep(first, cd, img, c);
+    for (int item = first; item < last; ++item) {
+        const int Wd = cd.W - 6, Hd = cd.H - 6;
+        int* cnt_out = cell_cnt + (size_t)img * ncells + c;
+        const bool live = Wd > 0 && Hd > 0;
+        wave_fence();                                                // the previous cell's LDS reads before these writes
+        if (live) {
+            fastw_roi_store<kPS>(R, E, ln);
+            const int n16 = ((Hd + 2) * SW * 2 + 15) >> 4;
+            for (int i = ln; i < n16; i += kWave) reinterpret_cast<uint4*>(sc)[i] = make_uint4(0, 0, 0, 0);
+        }
+        CellDev cdn = cd;
+        int imgn = img, cn = c;
+        if (item + 1 < last) prep(item + 1, cdn, imgn, cn);          // next ROI in flight during this cell
+        if (live)
+            fastw_body<kPS>(E, sc, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
+        else if (ln == 0)
+            *cnt_out = 0;
+        cd = cdn; img = imgn; c = cn;
     }
-    wave_fence();
-    if (!two || n1 > 0) break;                                        // wave-uniform
-    }
-    // 5. the cell's list (iniTh, or minTh when iniTh kept nothing: :812-816) -> its candidate slots, coalesced
-    const uint16_t* ks = n1 > 0 ? k1 : k2;
-    const int n = min(n1 > 0 ? n1 : n2, min(kcap, cd.slot_cap));
-    uint32_t* oxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
-    uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
-    for (int i = ln; i < n; i += kWave) {
-        const int k = ks[i], rr = k >> 7, x = k & 127;
-        oxy[i] = (uint32_t)(cd.x0 + 3 + x) | ((uint32_t)(cd.y0 + rr + 3) << 16);
-        os[i] = (uint8_t)sc[(rr + 1) * SW + 2 + x];
-    }
-    if (ln == 0) *cnt_out = n;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3200,7 +3304,8 @@ struct Extractor {
     WaveLaunch wave_launch[2] = {};
     int fast_wave = 1;        // default (r3x: 62.5k -> 67.1k frames/s with the pair-row blur); 0 = k_fast_band
     int wave_wpg = 4;
-    int wave_twopass = 1;     // ORBX_FAST_TWOPASS: iniTh first, minTh only for the cells left empty (0: one pass)
+    int wave_twopass = 1;
+    int wave_cells = 1;       // ORBX_FAST_CELLS = 2 / 4: k_fast_wave_p (a wave walks that many cells, next ROI prefetched)     // ORBX_FAST_TWOPASS: iniTh first, minTh only for the cells left empty (0: one pass)
     int wave_psmin = 24;      // pair stride >= 24: fewer resident FAST waves leave CUs to the overlapped stages (r3x:
                               // stride 20 is faster alone, 0.772 vs 0.825 ms serial, but 66.6k vs 67.1k frames/s)
     int desc_fb = 0;          // ORBX_DESC_FB: k_describe_fb (blur per keypoint in LDS, no k_blur7 / blurred pyramid)
@@ -3774,6 +3879,15 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
             const Extractor::WaveLaunch& wl = e->wave_launch[&f == &e->fast_launch[0] ? 0 : 1];
             if (wl.n <= 0) return;
             const int wpg = e->wave_wpg, nwg = (wl.n * batch + wpg - 1) / wpg;
+            if (wl.ps == 24 && wpg == 4 && (e->wave_cells == 2 || e->wave_cells == 4)) {   // ORBX_FAST_CELLS
+                const int nwv = (wl.n * batch + e->wave_cells - 1) / e->wave_cells, nwgp = (nwv + 3) / 4;
+                auto kp = e->wave_cells == 2 ? k_fast_wave_p<4, 2> : k_fast_wave_p<4, 4>;
+                hipLaunchKernelGGL(kp, dim3(kXcds * xcd_chunk(nwgp)),
+                                   dim3(256), (size_t)4 * wl.lay.bytes, q, e->d_pyr, ps, e->d_levels, e->d_cells, wl.cell0,
+                                   wl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt,
+                                   ncells, batch, s0, wl.lay, wl.kcap, e->wave_twopass);
+                return;
+            }
             auto kw = wl.ps == 20 ? (wpg == 4 ? k_fast_wave<20, 4> : wpg == 2 ? k_fast_wave<20, 2> : k_fast_wave<20, 1>)
                     : wl.ps == 24 ? (wpg == 4 ? k_fast_wave<24, 4> : wpg == 2 ? k_fast_wave<24, 2> : k_fast_wave<24, 1>)
                                   : (wpg == 4 ? k_fast_wave<40, 4> : wpg == 2 ? k_fast_wave<40, 2> : k_fast_wave<40, 1>);
@@ -4038,6 +4152,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* bl = std::getenv("ORBX_BLUR_LDS")) e->blur_lds = std::atoi(bl) != 0;
     if (const char* pm = std::getenv("ORBX_FAST_PSMIN")) e->wave_psmin = std::atoi(pm);
     if (const char* tp = std::getenv("ORBX_FAST_TWOPASS")) e->wave_twopass = std::atoi(tp) != 0;
+    if (const char* fc = std::getenv("ORBX_FAST_CELLS")) e->wave_cells = std::atoi(fc);
     if (const char* fp = std::getenv("ORBX_FAST_WPG")) e->wave_wpg = std::atoi(fp) == 1 ? 1 : std::atoi(fp) == 2 ? 2 : 4;
     if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
     if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;

@@ -173,7 +173,8 @@ def test_describe_keypoints_per_wave(gpu, monkeypatch, kpw):
     _check(S.kitti_like_image(410, rows=240, cols=333), nfeatures=777, nlevels=5, scale=1.3)
 
 
-@pytest.mark.parametrize("form", ["band", "band_blur1row", "rows", "wave", "wave_blurlds", "wave_1pass", "wave20", "wave2", "wave1"])
+@pytest.mark.parametrize("form", ["band", "band_blur1row", "rows", "wave", "wave_blurlds", "wave_1pass", "wave20", "wave2",
+                                  "wave1", "wave_cells2", "wave_cells4"])
 def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
     """Every FAST form -- k_fast_band (LDS band image, pre-test and survivor list), k_fast_rows (one wave per cell
     row in registers, every pixel scored, both thresholds' lists) and k_fast_wave (one wave per cell, no barrier; 4, 2
@@ -191,6 +192,7 @@ def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
     monkeypatch.setenv("ORBX_FAST_TWOPASS", "0" if form == "wave_1pass" else "1")   # iniTh and minTh in one pass
     monkeypatch.setenv("ORBX_BLUR_DOT2", "0" if form == "band_blur1row" else "1")   # k_blur7 one row at a time
     monkeypatch.setenv("ORBX_BLUR_LDS", "1" if form == "wave_blurlds" else "0")     # k_blur7_lds
+    monkeypatch.setenv("ORBX_FAST_CELLS", {"wave_cells2": "2", "wave_cells4": "4"}.get(form, "1"))   # k_fast_wave_p
     for shape, nf, kw in (((375, 1242), 2000, {}), ((377, 1243), 800, {}), ((120, 160), 300, {}),
                           ((1000, 200), 800, {}), ((40, 40), 100, {}), ((500, 500), 1000, {}),
                           ((480, 752), 1500, dict(nlevels=5, scale=1.3, ini=25, mn=10)),
