@@ -1785,6 +1785,9 @@ __device__ __forceinline__ int refl101(int i, int n) {
 #endif
 // strip = output columns of one wave: 256 (every lane loads its own 12-byte window), or 248 with the DPP form
 // (lanes 1..62 output, lanes 0 and 63 load the +-4 halo)
+#ifndef ORBX_BLUR_SEL
+#define ORBX_BLUR_SEL 1         // edge strips of k_blur7<true>: per-band REFLECT_101 byte selectors (0: per-byte loop)
+#endif
 constexpr int kBlurBand = ORBX_BLUR_BAND, kBlurStrip = ORBX_BLUR_DPP ? 248 : 256;
 
 // byte m of the 12-byte window (w0 | w1 << 32 | w2 << 64) and byte m+1, as u16 lanes (lo = m)
@@ -1961,6 +1964,36 @@ __device__ __forceinline__ void blur_emit2(const BlurPair& a, const BlurPair& b,
     }
 }
 
+// Edge-strip window of blur_load<1> as byte selectors: which byte of the clamped 12-byte load each window byte
+// 1..10 takes depends on the lane's column only, so the REFLECT_101 picks are computed once per band and every row
+// then costs two v_perm_b32 and one OR per window dword (the per-byte loop of blur_load<1> was ~80 VALU per row).
+struct ReflSel { uint32_t a[3], b[3]; int xs; };
+__device__ __forceinline__ ReflSel refl_sel(int x0, int w) {
+    ReflSel s;
+    s.xs = min(max(x0 - 4, 0), w - 12);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { s.a[j] = 0x0c0c0c0cu; s.b[j] = 0x0c0c0c0cu; }   // 0x0c selects a zero byte
+#pragma unroll
+    for (int i = 1; i < 11; ++i) {
+        const int x = x0 - 4 + i;
+        const int k = (x < 0 ? -x : (x >= w ? 2 * w - 2 - x : x)) - s.xs;          // 0 <= k < 12
+        const int sh = 8 * (i & 3);
+        const uint32_t clr = ~(0xffu << sh);
+        if (k < 8) s.a[i >> 2] = (s.a[i >> 2] & clr) | ((uint32_t)k << sh);        // byte k of {v1:v0}
+        else s.b[i >> 2] = (s.b[i >> 2] & clr) | ((uint32_t)(k - 8) << sh);       // byte k-8 of v2
+    }
+    return s;
+}
+__device__ __forceinline__ BlurWin blur_load_sel(const uint8_t* __restrict__ row, const ReflSel& s) {
+    uint32_t v[3];
+    __builtin_memcpy(v, row + s.xs, 12);
+    BlurWin o;
+    o.w0 = __builtin_amdgcn_perm(v[1], v[0], s.a[0]) | __builtin_amdgcn_perm(v[2], v[2], s.b[0]);
+    o.w1 = __builtin_amdgcn_perm(v[1], v[0], s.a[1]) | __builtin_amdgcn_perm(v[2], v[2], s.b[1]);
+    o.w2 = __builtin_amdgcn_perm(v[1], v[0], s.a[2]) | __builtin_amdgcn_perm(v[2], v[2], s.b[2]);
+    return o;
+}
+
 template <int kMode>
 __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int sstride, uint8_t* __restrict__ D,
                                            const LevelDev& L, int x0, int y0, int y1) {
@@ -1969,6 +2002,13 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
         const int r = h >= 16 ? (yy < 0 ? -yy : (yy >= h ? 2 * h - 2 - yy : yy)) : refl101(yy, h);
         return S + (size_t)r * sstride;
     };
+#if ORBX_BLUR_SEL
+    ReflSel rs;
+    if constexpr (kMode == 1) rs = refl_sel(x0, w);
+    auto load = [&](const uint8_t* row) { return kMode == 1 ? blur_load_sel(row, rs) : blur_load<kMode>(row, x0, w); };
+#else
+    auto load = [&](const uint8_t* row) { return blur_load<kMode>(row, x0, w); };
+#endif
     const bool full = x0 + 4 <= w;
     auto store = [&](int y, uint32_t packed) {
         uint8_t* o = D + (size_t)y * w + x0;
@@ -1984,24 +2024,24 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
     {
         BlurWin p[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) p[k] = blur_load<kMode>(row_ptr(y0 - 3 + k), x0, w);
+        for (int k = 0; k < 6; ++k) p[k] = load(row_ptr(y0 - 3 + k));
         q0 = blur_hpair(p[0], p[1]); q1 = blur_hpair(p[2], p[3]); q2 = blur_hpair(p[4], p[5]);
     }
     // ring of 4 row pairs; 8 output rows per iteration.  Interior strips (kMode 0) load the iteration's 8 input rows at
     // once; the edge forms, whose per-byte reflection needs more registers, 4 at a time (8 spilled at 128 VGPRs)
     for (int y = y0; y < y1; y += 8) {
-        constexpr int kB = kMode == 0 ? 8 : 4;
+        constexpr int kB = (kMode == 0 || (ORBX_BLUR_SEL && kMode == 1)) ? 8 : 4;
         BlurWin p[kB];
         uint32_t oe, oo;
 #pragma unroll
-        for (int k = 0; k < kB; ++k) p[k] = blur_load<kMode>(row_ptr(y + 3 + k), x0, w);
+        for (int k = 0; k < kB; ++k) p[k] = load(row_ptr(y + 3 + k));
         q3 = blur_hpair(p[0], p[1]); blur_emit2(q0, q1, q2, q3, oe, oo);
         store(y, oe); if (y + 1 >= y1) break; store(y + 1, oo); if (y + 2 >= y1) break;
         q0 = blur_hpair(p[2], p[3]); blur_emit2(q1, q2, q3, q0, oe, oo);
         store(y + 2, oe); if (y + 3 >= y1) break; store(y + 3, oo); if (y + 4 >= y1) break;
         if constexpr (kB == 4) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) p[k] = blur_load<kMode>(row_ptr(y + 7 + k), x0, w);
+            for (int k = 0; k < 4; ++k) p[k] = load(row_ptr(y + 7 + k));
         }
         q1 = blur_hpair(p[kB - 4], p[kB - 3]); blur_emit2(q2, q3, q0, q1, oe, oo);
         store(y + 4, oe); if (y + 5 >= y1) break; store(y + 5, oo); if (y + 6 >= y1) break;
