@@ -181,6 +181,19 @@ __device__ __forceinline__ void resize_window8(const uint8_t* __restrict__ row, 
     lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
 }
 
+// Vertical step of one output pixel, exact under the table conditions the host checks for the vectorised form (every
+// tap >= 0, a0 + a1 <= 2049, b0 + b1 <= 2049): hv <= 255 * 2049 < 2^24, so both products are 24-bit multiplies
+// (v_mad_u32_u24, full rate; the u32 form is a quarter-rate v_mul_lo_u32), and with b scaled by 4
+// acc = 4 * (hv0 * b0 + hv1 * b1 + 2^21) < 2^32, whose byte 3 is (hv0 * b0 + hv1 * b1 + 2^21) >> 22 <= 255 (the
+// saturation of the generic path cannot bite).
+__device__ __forceinline__ uint32_t resize_acc(uint32_t hv0, uint32_t hv1, int b0, int b1) {
+    return __umul24(hv0, (uint32_t)b0 << 2) + __umul24(hv1, (uint32_t)b1 << 2) + (1u << 23);
+}
+// byte 3 of four accumulators -> the 4 output bytes (two v_perm_b32 and an OR)
+__device__ __forceinline__ uint32_t resize_pack(const uint32_t* acc) {
+    return __builtin_amdgcn_perm(acc[1], acc[0], 0x0c0c0703u) | __builtin_amdgcn_perm(acc[3], acc[2], 0x07030c0cu);
+}
+
 // One wave's work item of the vectorised resize: (256-column strip, 8-row band) of one image's level.
 __device__ __forceinline__ void resize4_item(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
                                              size_t src_step, size_t src_istride, int sw, int dst_off, int dw, int dh,
@@ -211,7 +224,7 @@ __device__ __forceinline__ void resize4_item(uint8_t* __restrict__ pyr, size_t p
 #pragma unroll
         for (int r = 0; r < kResizeBand; ++r) {
             if (r >= ny) break;
-            uint32_t packed = 0;
+            uint32_t acc[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const u16x2 c = __builtin_bit_cast(u16x2, cf[k]);
@@ -219,9 +232,9 @@ __device__ __forceinline__ void resize4_item(uint8_t* __restrict__ pyr, size_t p
                     __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi[2 * r], lo[2 * r], sl[k])), c, 0u, false);
                 const uint32_t hv1 = __builtin_amdgcn_udot2(
                     __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi[2 * r + 1], lo[2 * r + 1], sl[k])), c, 0u, false);
-                const uint32_t v = min((hv0 * (uint32_t)yr[r].z + hv1 * (uint32_t)yr[r].w + (1u << 21)) >> 22, 255u);
-                packed |= v << (8 * k);
+                acc[k] = resize_acc(hv0, hv1, yr[r].z, yr[r].w);
             }
+            const uint32_t packed = resize_pack(acc);
             uint8_t* o = D + (size_t)(y0 + r) * dw + x;
             if (full) {
                 __builtin_memcpy(o, &packed, 4);
@@ -239,15 +252,15 @@ __device__ __forceinline__ void resize4_item(uint8_t* __restrict__ pyr, size_t p
         resize_window(S + (size_t)yr.x * src_step, xb, sw, fast, l0, h0);
         resize_window(S + (size_t)yr.y * src_step, xb, sw, fast, l1, h1);
         const uint32_t sl[4] = {sel.x, sel.y, sel.z, sel.w}, cf[4] = {coef.x, coef.y, coef.z, coef.w};
-        uint32_t packed = 0;
+        uint32_t acc[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const u16x2 c = __builtin_bit_cast(u16x2, cf[k]);
             const uint32_t hv0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(h0, l0, sl[k])), c, 0u, false);
             const uint32_t hv1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(h1, l1, sl[k])), c, 0u, false);
-            const uint32_t v = min((hv0 * (uint32_t)yr.z + hv1 * (uint32_t)yr.w + (1u << 21)) >> 22, 255u);
-            packed |= v << (8 * k);
+            acc[k] = resize_acc(hv0, hv1, yr.z, yr.w);
         }
+        const uint32_t packed = resize_pack(acc);
         uint8_t* o = D + (size_t)y * dw + x;
         if (full) {
             __builtin_memcpy(o, &packed, 4);
@@ -1785,6 +1798,9 @@ __device__ __forceinline__ int refl101(int i, int n) {
 #endif
 // strip = output columns of one wave: 256 (every lane loads its own 12-byte window), or 248 with the DPP form
 // (lanes 1..62 output, lanes 0 and 63 load the +-4 halo)
+#ifndef ORBX_BLUR_PK
+#define ORBX_BLUR_PK 1          // k_blur7<true> output packing: v_perm + v_pk_min_u16 (0: shift, min, OR per pixel)
+#endif
 #ifndef ORBX_BLUR_SEL
 #define ORBX_BLUR_SEL 1         // edge strips of k_blur7<true>: per-band REFLECT_101 byte selectors (0: per-byte loop)
 #endif
@@ -1948,20 +1964,38 @@ __device__ __forceinline__ void blur_emit2(const BlurPair& a, const BlurPair& b,
                                            uint32_t& oe, uint32_t& oo) {
     const u16x2 e0 = {18, 34}, e1 = {49, 55}, e2 = {49, 34}, e3 = {18, 0};
     const u16x2 o0 = {0, 18}, o1 = {34, 49}, o2 = {55, 49}, o3 = {34, 18};
+    // acc < 2^25, so (acc + 2^15) >> 16 is the u16 in bytes 2-3 of acc: one v_perm_b32 gathers it for two columns as
+    // u16x2, one v_pk_min_u16 saturates both, one more v_perm_b32 packs four columns (5 VALU per 4 pixels instead of a
+    // shift, a min and an OR per pixel)
+    uint32_t ae[4], ao[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        ae[k] = __builtin_amdgcn_udot2(d.h[k], e3, 1u << 15, false);
+        ae[k] = __builtin_amdgcn_udot2(c.h[k], e2, ae[k], false);
+        ae[k] = __builtin_amdgcn_udot2(b.h[k], e1, ae[k], false);
+        ae[k] = __builtin_amdgcn_udot2(a.h[k], e0, ae[k], false);
+        ao[k] = __builtin_amdgcn_udot2(d.h[k], o3, 1u << 15, false);
+        ao[k] = __builtin_amdgcn_udot2(c.h[k], o2, ao[k], false);
+        ao[k] = __builtin_amdgcn_udot2(b.h[k], o1, ao[k], false);
+        ao[k] = __builtin_amdgcn_udot2(a.h[k], o0, ao[k], false);
+    }
+    const u16x2 k255 = {255, 255};
+    auto pack4 = [&](const uint32_t* v) {
+        const u16x2 lo = __builtin_elementwise_min(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(v[1], v[0], 0x07060302u)), k255);
+        const u16x2 hi = __builtin_elementwise_min(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(v[3], v[2], 0x07060302u)), k255);
+        return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x06040200u);
+    };
+#if ORBX_BLUR_PK
+    oe = pack4(ae);
+    oo = pack4(ao);
+#else
     oe = 0; oo = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        uint32_t ae = __builtin_amdgcn_udot2(d.h[k], e3, 1u << 15, false);
-        ae = __builtin_amdgcn_udot2(c.h[k], e2, ae, false);
-        ae = __builtin_amdgcn_udot2(b.h[k], e1, ae, false);
-        ae = __builtin_amdgcn_udot2(a.h[k], e0, ae, false);
-        uint32_t ao = __builtin_amdgcn_udot2(d.h[k], o3, 1u << 15, false);
-        ao = __builtin_amdgcn_udot2(c.h[k], o2, ao, false);
-        ao = __builtin_amdgcn_udot2(b.h[k], o1, ao, false);
-        ao = __builtin_amdgcn_udot2(a.h[k], o0, ao, false);
-        oe |= min(ae >> 16, 255u) << (8 * k);
-        oo |= min(ao >> 16, 255u) << (8 * k);
+        oe |= min(ae[k] >> 16, 255u) << (8 * k);
+        oo |= min(ao[k] >> 16, 255u) << (8 * k);
     }
+#endif
 }
 
 // Edge-strip window of blur_load<1> as byte selectors: which byte of the clamped 12-byte load each window byte
@@ -2844,7 +2878,7 @@ __global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ py
             const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
             const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
             const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
-            vals[e] = center[__float2int_rn(ry) * kBriefRow + __float2int_rn(rx)];
+            vals[e] = center[__mul24(__float2int_rn(ry), kBriefRow) + __float2int_rn(rx)];
         }
         bits[g] = __ballot(vals[0] < vals[1]);
     }
@@ -2936,12 +2970,15 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
     const uint8_t* B = blur + img * pyr_stride + lpo;
     uint8_t* win = brief_lds + ((threadIdx.x >> 6) * kKpw + sub) * kBriefWin;
     uint64_t wv[kNW];
-    if (valid) {
-        const uint8_t* w0 = B + (size_t)(cy - kBriefR) * lw + (cx - kBriefR);
+    int woff[kNW];                                               // LDS offset of chunk q = lk + kLp * k (row q / 5, chunk q % 5)
+    {
+        int wr = lk / 5, wc = lk - 5 * wr;                       // one division; later chunks step by kLp = 5 A + B
 #pragma unroll
         for (int k = 0; k < kNW; ++k) {
-            const int q = lk + kLp * k, r = min(q / 5, 2 * kBriefR), c = q - (q / 5) * 5;
-            __builtin_memcpy(&wv[k], w0 + (size_t)r * lw + 8 * c, 8);
+            woff[k] = __mul24(wr, kBriefRow) + 8 * wc;
+            if (valid) __builtin_memcpy(&wv[k], B + (size_t)(cy - kBriefR + min(wr, 2 * kBriefR)) * lw + (cx - kBriefR + 8 * wc), 8);
+            wc += kLp % 5; wr += kLp / 5;
+            if (wc >= 5) { wc -= 5; ++wr; }
         }
     }
     int pstride;
@@ -2980,7 +3017,7 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
 #pragma unroll
         for (int k = 0; k < kNW; ++k) {
             const int q = lk + kLp * k;
-            if (q < kWinItems) *reinterpret_cast<uint64_t*>(win + (q / 5) * kBriefRow + 8 * (q % 5)) = wv[k];
+            if (q < kWinItems) *reinterpret_cast<uint64_t*>(win + woff[k]) = wv[k];
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -3002,7 +3039,7 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
             const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
             const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
             const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
-            if (valid) vals[e] = center[__float2int_rn(ry) * kBriefRow + __float2int_rn(rx)];
+            if (valid) vals[e] = center[__mul24(__float2int_rn(ry), kBriefRow) + __float2int_rn(rx)];
         }
         const uint64_t bm = __ballot(vals[0] < vals[1]);
         words[g] = (uint32_t)(bm >> (sub * kLp)) & (uint32_t)((1ull << kLp) - 1ull);
@@ -3213,7 +3250,7 @@ __global__ __launch_bounds__(256) void k_describe_fb(const uint8_t* __restrict__
             const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
             const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
             const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
-            if (valid) vals[e] = center[__float2int_rn(ry) * kBriefRow + __float2int_rn(rx)];
+            if (valid) vals[e] = center[__mul24(__float2int_rn(ry), kBriefRow) + __float2int_rn(rx)];
         }
         const uint64_t bm = __ballot(vals[0] < vals[1]);
         words[gt] = (uint32_t)(bm >> (sub * kLp)) & (uint32_t)((1ull << kLp) - 1ull);
@@ -3792,12 +3829,12 @@ int Extractor::configure(int r, int c, int batch) {
             vxb[g] = hx0[4 * g];
             for (int k = 0; k < 4 && 4 * g + k < dw; ++k) {
                 const int x = 4 * g + k, oL = hx0[x] - vxb[g], oR = hx1[x] - vxb[g];
-                if (oL < 0 || oR < 0 || oL > 7 || oR > 7 || ha0[x] < 0 || ha1[x] < 0) fits = false;
+                if (oL < 0 || oR < 0 || oL > 7 || oR > 7 || ha0[x] < 0 || ha1[x] < 0 || ha0[x] + ha1[x] > 2049) fits = false;
                 vsel[4 * g + k] = (uint32_t)(oL & 7) | 0x0c00u | ((uint32_t)(oR & 7) << 16) | 0x0c000000u;
                 vcoef[4 * g + k] = (uint32_t)(ha0[x] & 0xffff) | ((uint32_t)(ha1[x] & 0xffff) << 16);
             }
         }
-        for (int y = 0; y < dh; ++y) if (hb0[y] < 0 || hb1[y] < 0) fits = false;
+        for (int y = 0; y < dh; ++y) if (hb0[y] < 0 || hb1[y] < 0 || hb0[y] + hb1[y] > 2049) fits = false;   // resize_acc
         if (fits) {
             uint8_t* vm;
             const size_t bx = ((size_t)G * 4 + 15) & ~(size_t)15, bs = (size_t)G * 16, by = (size_t)dh * 16;
