@@ -1180,8 +1180,12 @@ __device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, in
         const h16x2 d4 = v - as_h2(A[k + 3]);                           // ( 3,  0)
         const h16x2 d8 = v - as_h2(align16(U[k + 2], U[k + 1]));        // ( 0, -3)
         const h16x2 d12 = v - as_h2(A[k]);                              // (-3,  0)
-        const h16x2 dk = hmax(hmax3(hmin(d0, d4), hmin(d4, d8), hmin(d8, d12)), hmin(d12, d0));
-        const h16x2 br = hmin(hmin3(hmax(d0, d4), hmax(d4, d8), hmax(d8, d12)), hmax(d12, d0));
+        // on the 4-cycle 0-4-8-12 the largest adjacent minimum equals the smaller of the two opposite maxima (lattice
+        // identity: the taps at or below any level must cover every edge, i.e. contain {0, 8} or {4, 12}), so
+        // max(min(d0,d4), min(d4,d8), min(d8,d12), min(d12,d0)) = min(max(d0,d8), max(d4,d12)), and dually for br:
+        // the same values as the 6-op forms in 3 ops each
+        const h16x2 dk = hmin(hmax(d0, d8), hmax(d4, d12));
+        const h16x2 br = hmax(hmin(d0, d8), hmin(d4, d12));
         const h16x2 m = hmax(dk, -br);
         z[k] = __builtin_bit_cast(uint32_t, m - tq);
     }
