@@ -150,6 +150,13 @@ int orbx_extractor_set_pyramid_ring(orbx_extractor* ex, int n);
 int orbx_extractor_level_device(orbx_extractor* ex, int index, int level, const uint8_t** d_level,
                                 int* rows, int* cols, size_t* step);
 
+/* Diagnostics: host copy of the GaussianBlur'd level 'level' of image 'index' of the last call -- the whole level,
+ * borders (REFLECT_101) included: what computeDescriptors reads (src/ORBextractor.cc:1085-1086 blurs a clone of
+ * mvImagePyramid[level] with GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101)).  The reference keeps it internal; the
+ * parity tests read it to check every blurred pixel, not only those around keypoints.  Waits for the extractor's
+ * work.  ORBX_ERR_ARG when the extractor blurs per keypoint (ORBX_DESC_FB=1: no blurred pyramid exists). */
+int orbx_extractor_copy_blurred_level(orbx_extractor* ex, int index, int level, uint8_t* dst, size_t dst_step);
+
 /* Device-side error word of the extractor, after every call issued so far has finished (waits for them).
  * Bits: 1 = a level's quadtree exceeded its node capacity; 4 = ordering canary -- a descriptor stage found another
  * call's kept-keypoint stamp (a missing cross-call ordering edge; the host API returns ORBX_ERR_HIP for it).  The

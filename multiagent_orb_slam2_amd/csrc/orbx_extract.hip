@@ -4496,6 +4496,20 @@ int orbx_extractor_level_device(orbx_extractor* e, int index, int level, const u
     return ORBX_OK;
 }
 
+int orbx_extractor_copy_blurred_level(orbx_extractor* e, int index, int level, uint8_t* dst, size_t dst_step) {
+    ORBX_REQUIRE(e && dst, ORBX_ERR_ARG, "null argument");
+    ORBX_REQUIRE(e->d_blur && !e->desc_fb && e->last_src0.p && level >= 0 && level < e->nlevels && index >= 0 &&
+                     index < e->last_batch,
+                 ORBX_ERR_ARG, "no blurred level for index %d level %d", index, level);
+    const int w = e->lv[level].w, h = e->lv[level].h;
+    ORBX_REQUIRE(dst_step >= (size_t)w, ORBX_ERR_ARG, "bad destination");
+    ORBX_HIP(hipSetDevice(e->device));
+    ORBX_HIP(hipDeviceSynchronize());                                  // the last call's blur may run on any of its streams
+    const uint8_t* p = e->d_blur + (size_t)index * e->pyr_size + e->lv[level].pyr_off;   // as k_blur7 writes it
+    ORBX_HIP(hipMemcpy2D(dst, dst_step, p, (size_t)w, (size_t)w, (size_t)h, hipMemcpyDeviceToHost));
+    return ORBX_OK;
+}
+
 int orbx_extractor_copy_level(orbx_extractor* e, int index, int level, uint8_t* dst, size_t dst_step) {
     const uint8_t* p;
     int r, c;

@@ -179,6 +179,7 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_extractor_max_keypoints.argtypes = [vp, i32, i32]
     lib.orbx_extractor_level_sizes.argtypes = [vp, i32, i32, vp, vp]
     lib.orbx_extractor_copy_level.argtypes = [vp, i32, i32, vp, C.c_size_t]
+    lib.orbx_extractor_copy_blurred_level.argtypes = [vp, i32, i32, vp, C.c_size_t]
     lib.orbx_extractor_level_device.argtypes = [vp, i32, i32, C.POINTER(vp), C.POINTER(i32), C.POINTER(i32),
                                                 C.POINTER(C.c_size_t)]
     lib.orbx_extractor_enable_timing.argtypes = [vp, i32]
@@ -420,6 +421,20 @@ class ORBextractor:
         for l, (h, w) in enumerate(self.level_sizes(*self._last_shape)):
             a = np.zeros((h, w), np.uint8)
             _check(self._lib.orbx_extractor_copy_level(self._h, 0, l, _p(a), w))
+            out.append(a)
+        return out
+
+    def blurred_levels(self, index: int = 0, shape=None):
+        """Diagnostics: host copies of the GaussianBlur'd pyramid levels of image 'index' of the last call (the
+        images computeDescriptors reads, src/ORBextractor.cc:1085-1086), borders included.  shape = (rows, cols) of
+        the call's images (default: the last host-API image)."""
+        shape = shape or self._last_shape
+        if shape is None:
+            return []
+        out = []
+        for l, (h, w) in enumerate(self.level_sizes(*shape)):
+            a = np.zeros((h, w), np.uint8)
+            _check(self._lib.orbx_extractor_copy_blurred_level(self._h, index, l, _p(a), w))
             out.append(a)
         return out
 

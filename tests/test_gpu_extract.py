@@ -173,6 +173,40 @@ def test_describe_keypoints_per_wave(gpu, monkeypatch, kpw):
     _check(S.kitti_like_image(410, rows=240, cols=333), nfeatures=777, nlevels=5, scale=1.3)
 
 
+@pytest.mark.parametrize("form", ["dot2", "row", "lds"])
+def test_blurred_pyramid_bit_exact(gpu, monkeypatch, form):
+    """Every pixel of every blurred level -- not only the windows around keypoints that the descriptor tests see --
+    equals the oracle's GaussianBlur(7x7, sigma 2, REFLECT_101) of the oracle's pyramid level
+    (ORBextractor.cc:1085-1086): interior strips, strips at a level's left / right edge (REFLECT_101 columns by byte
+    selectors in k_blur7<true>), levels under 12 columns, bottom rows, saturation (a constant 255 image blurs to 255 with
+    taps summing to 257), batched (image index > 0).  Forms: k_blur7 in vertical row pairs (default), one row at a time,
+    and k_blur7_lds."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    monkeypatch.setenv("ORBX_BLUR_DOT2", "0" if form == "row" else "1")
+    monkeypatch.setenv("ORBX_BLUR_LDS", "1" if form == "lds" else "0")
+    monkeypatch.setenv("ORBX_DESC_FB", "0")
+    for shape in ((375, 1242), (377, 1243), (480, 752), (1000, 200), (40, 40), (61, 97)):
+        imgs = np.stack([S.kitti_like_image(700 + shape[1], rows=shape[0], cols=shape[1]),
+                         S.uniform_noise_image(701, rows=shape[0], cols=shape[1]) if shape == (375, 1242)
+                         else S.kitti_like_image(701, rows=shape[0], cols=shape[1]),
+                         np.full(shape, 255, np.uint8)])
+        ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7)
+        ex.extract_batch_device(torch.from_numpy(imgs).cuda())
+        torch.cuda.synchronize()
+        for i in range(len(imgs)):
+            ref = O.extract(imgs[i], nfeatures=1000, want_pyramid=True)["pyramid"]
+            got = ex.blurred_levels(i, shape)
+            assert len(got) == len(ref)
+            for l, (a, lv) in enumerate(zip(got, ref)):
+                b = O.blur7(lv)
+                bad = np.argwhere(a != b)
+                assert a.shape == b.shape and len(bad) == 0, (
+                    f"shape {shape} image {i} level {l} ({lv.shape}): {len(bad)} pixels differ, first {bad[:3].tolist()}")
+
+
 @pytest.mark.parametrize("form", ["band", "band_blur1row", "rows", "wave", "wave_blurlds", "wave_1pass", "wave20", "wave2",
                                   "wave1", "wave_cells2", "wave_cells4"])
 def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
