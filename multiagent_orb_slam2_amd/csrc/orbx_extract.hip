@@ -1201,6 +1201,11 @@ __device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, in
 }
 
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+// acc + number of set bits of b below this lane: v_mbcnt_lo + v_mbcnt_hi (the compiler turns popcount(b & below) into
+// two ANDs and two v_bcnt)
+__device__ __forceinline__ int rank_below(uint64_t b, int acc = 0) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, (uint32_t)acc));
+}
 
 // score-map row stride (int16) per pair stride: >= (Wd + 5) & ~1 for every cell the pair stride admits
 __host__ __device__ constexpr int fastw_sw(int ps) { return ps == 20 ? 36 : ps == 24 ? 44 : 76; }
@@ -1213,7 +1218,6 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
                                            int cand_stride, int kcap, int two_pass, int ln) {
     constexpr int SW = fastw_sw(kPS);
     wave_fence();
-    const uint64_t below = (1ull << ln) - 1ull;
     // 2. compass pre-test at min(iniTh, minTh) in quads; survivors compacted in row-major order
     const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
     // With minThFAST < iniThFAST the cell runs at iniThFAST first (fewer survivors to score); only a cell that kept
@@ -1237,7 +1241,7 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
         auto emit = [&](uint32_t mq, int r0, int u0) {
             const int cq = __builtin_popcount(mq);
             const uint64_t b0 = __ballot(cq & 1), b1 = __ballot(cq & 2), b2 = __ballot(cq & 4);
-            int pos = ns + __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
+            int pos = rank_below(b0, ns) + 2 * rank_below(b1) + 4 * rank_below(b2);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if ((mq >> k) & 1u) list[pos++] = (uint16_t)((r0 << 8) | (4 * u0 + k));
@@ -1283,8 +1287,8 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
             key = rr * 128 + 2 * j;
         }
         const uint64_t a0 = __ballot(f & 1), a1 = __ballot(f & 2), c0 = __ballot(f & 4), c1 = __ballot(f & 8);
-        int p1 = n1 + __popcll(a0 & below) + __popcll(a1 & below);
-        int p2 = n2 + __popcll(c0 & below) + __popcll(c1 & below);
+        int p1 = rank_below(a1, rank_below(a0, n1));
+        int p2 = rank_below(c1, rank_below(c0, n2));
         if (f & 1) { if (p1 < kcap) k1[p1] = (uint16_t)key; ++p1; }
         if ((f & 2) && p1 < kcap) k1[p1] = (uint16_t)(key + 1);
         if (f & 4) { if (p2 < kcap) k2[p2] = (uint16_t)key; ++p2; }
