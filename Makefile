@@ -7,7 +7,12 @@ HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -fno-f
 HDRS := include/orbx.h $(SRC)/orbx_common.h $(SRC)/orbx_pattern.h $(SRC)/orbx_sincos.h
 OBJS := $(SRC)/orbx_extract.o $(SRC)/orbx_match.o $(SRC)/orbx_vocab.o $(SRC)/orbx_proj.o $(SRC)/orbx_kfdb.o $(SRC)/orbx_fusion.o
 
-all: $(PKG)/liborbx.so oracle
+all: $(PKG)/liborbx.so oracle build/host_api_bench
+
+# native per-call latency driver (bench.py host_api.native; dlopens a liborbx.so by path)
+build/host_api_bench: scripts/micro/host_api_bench.cpp include/orbx.h
+	mkdir -p build
+	g++ -O2 -std=c++17 -pthread $< -ldl -o $@
 
 $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

@@ -88,7 +88,7 @@ def parse():
                          "exceeds the 256 MB Infinity Cache, so every step's level-0 reads come from HBM (1 = one batch "
                          "re-read every step)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
-    ap.add_argument("--host-api-frames", type=int, default=32, help="stereo frames through the host C-ABI (0 = skip)")
+    ap.add_argument("--host-api-frames", type=int, default=200, help="stereo frames through the host C-ABI (0 = skip)")
     ap.add_argument("--alone-reps", type=int, default=5,
                     help="calls of the roofline_alone block (the extraction alone, one stream); 0 skips it")
     ap.add_argument("--host-fed-steps", type=int, default=10,
@@ -310,10 +310,28 @@ def host_api_rate(pkg, cfg, lefts, rights, n_frames, device):
             lat.append(time.perf_counter() - t0)
     pool.shutdown()
     lat_ms = np.array(lat) * 1e3
-    return {"frames_per_s": round(1e3 / float(np.mean(lat_ms)), 1), "latency_ms_median": round(float(np.median(lat_ms)), 3),
-            "latency_ms_p95": round(float(np.percentile(lat_ms, 95)), 3), "frames": len(lat),
-            "path": "orbx_extract(L) and orbx_extract(R) on two threads (Frame.cc:78-81) + orbx_compute_stereo_matches, "
-                    "host buffers, one frame per call"}
+    out = {"frames_per_s": round(1e3 / float(np.mean(lat_ms)), 1), "latency_ms_median": round(float(np.median(lat_ms)), 3),
+           "latency_ms_p95": round(float(np.percentile(lat_ms, 95)), 3), "latency_ms_max": round(float(np.max(lat_ms)), 3),
+           "frames": len(lat),
+           "path": "Python ctypes: orbx_extract(L) and orbx_extract(R) on two threads (Frame.cc:78-81) + "
+                   "orbx_compute_stereo_matches, host buffers, one frame per call"}
+    # the same per-call path from a C++ caller (the reference's own language): scripts/micro/host_api_bench.cpp, built
+    # by build() into build/host_api_bench, run as a child process on the same GPU
+    exe = os.path.join(ROOT, "build", "host_api_bench")
+    lib = os.path.join(ROOT, "multiagent_orb_slam2_amd", "liborbx.so")
+    if os.path.exists(exe):
+        import subprocess
+        try:
+            r = subprocess.run([exe, lib, str(max(n_frames, 200)), str(cfg["rows"]), str(cfg["cols"]), str(cfg["nfeatures"])],
+                               capture_output=True, text=True, timeout=120)
+            if r.returncode == 0:
+                out["native"] = json.loads(r.stdout.strip().splitlines()[-1])
+                out["native"]["path"] = "C++ std::threads + dlopen'ed liborbx (scripts/micro/host_api_bench.cpp)"
+            else:
+                out["native_error"] = (r.stdout + r.stderr)[-500:]
+        except (OSError, subprocess.TimeoutExpired, ValueError) as e:
+            out["native_error"] = str(e)[:300]
+    return out
 
 
 def host_fed_block(step, last_handoff, host, stream, B, steps, dev):
@@ -498,12 +516,14 @@ def load_profile(name):
     return None
 
 
-# Live stage timers (orbx_extractor_stage_times: HIP events on the stream each launch is issued on) that time a
-# kernel's launches over the whole batch: k_fast_band is two launches per call (level 0 on the extractor's side stream,
-# levels 1..7 on the launch stream), each timed by its own event pair; k_describe_m is one launch on the output stream.
-LIVE_STAGES = {"k_fast_band": ("fast_cells", "fast_cells_l0"), "k_fast_wave": ("fast_cells", "fast_cells_l0"),
-               "k_describe_m": ("describe",), "k_describe": ("describe",), "k_describe_fb": ("describe",),
-               "k_quadtree": ("quadtree", "quadtree_l0"), "k_blur7": ("blur7",)}
+# Live stage timers (orbx_extractor_stage_times: HIP events on the stream each launch is issued on) of a kernel family's
+# launches over the whole batch: (launch spans, busy stage).  k_fast_wave and k_quadtree are two launches per call
+# (level 0 on the extractor's side stream, levels 1..7 on the launch stream) that overlap each other; the busy stage is
+# the union of the two spans (the wall time during which the kernel runs), which the roofline divides by.
+# k_describe_m is one launch on the output stream, k_blur7 two launches in order on the side stream.
+LIVE_STAGES = {"k_fast_wave": (("fast_cells", "fast_cells_l0"), "fast_busy"),
+               "k_quadtree": (("quadtree", "quadtree_l0"), "quadtree_busy"),
+               "k_describe_m": (("describe",), "describe"), "k_blur7": (("blur7",), "blur7")}
 
 
 def kernel_family(name):
@@ -517,23 +537,10 @@ def source_sha16():
 
 
 def active_kernel_names():
-    """Names (as rocprofv3 prints them) of the extractor kernels this process runs, from the same environment switches
-    liborbx reads at extractor creation (csrc/orbx_extract.hip, orbx_extractor_create)."""
-    env = os.environ.get
-    if env("ORBX_FAST_WAVE", "1") != "0":
-        wpg = {"1": 1, "2": 2}.get(env("ORBX_FAST_WPG", "4"), 4)
-        psmin = int(env("ORBX_FAST_PSMIN", "24"))               # KITTI / EuRoC cells need a pair stride of 20
-        fast = f"k_fast_wave<{20 if psmin <= 20 else 24 if psmin <= 24 else 40}, {wpg}>"
-    else:
-        fast = "k_fast_band<72, true>"
-    if env("ORBX_DESC_FB", "0") != "0":
-        desc = "k_describe_fb"
-    else:
-        kpw = int(env("ORBX_DESC_KPW", "2"))
-        desc = "k_describe" if kpw == 1 else f"k_describe_m<{4 if kpw == 4 else 2}>"
-    blur = "k_blur7<false>" if env("ORBX_BLUR_DOT2", "1") == "0" else "k_blur7<true>"
-    return {"fast": fast, "describe": desc, "blur": blur,
-            "families": {kernel_family(fast), kernel_family(desc), "k_quadtree", "k_blur7", "k_resize4"}}
+    """Names (as rocprofv3 prints them) of the extractor kernels this process runs (csrc/orbx_extract.hip run_batch):
+    k_fast_wave's pair stride is 24 for every cell of the KITTI / EuRoC configs (40 only for cells wider than 46)."""
+    return {"fast": "k_fast_wave<24, 4>", "describe": "k_describe_m<2>", "blur": "k_blur7",
+            "families": {"k_fast_wave", "k_describe_m", "k_quadtree", "k_blur7", "k_resize4"}}
 
 
 def roofline_lines(per_call, cfg, units, config):
@@ -541,25 +548,30 @@ def roofline_lines(per_call, cfg, units, config):
     the bench command (profiles/kernel_share.json, scripts/kernel_share.py) -- and of the describe as a secondary
     line.  achieved = SURVEY §8(d) algorithmic bytes of the extractions the kernel's launches cover per step (one
     extraction = image in + nfeatures x 60 B out; every launch family covers all 2B images once) / the kernel's live
-    time per step (sum of its launches' event spans)."""
+    busy time per step (the union of its launches' event spans: the two FAST launches run at once on two streams, so
+    the sum of their spans counts the overlap twice).  The committed profile's figures sit beside it:
+    rocprof_busy_ms_per_step (the union of the traced launch intervals per step) and rocprof_launch_avg_us (the
+    average duration of each of the two launch grids); frac_rocprof = bytes / the traced busy time."""
     share = load_profile("kernel_share.json")
     cb = compulsory_bytes(cfg)["extraction"]
     names = active_kernel_names()
     fast_fam = kernel_family(names["fast"])
     dom = fast_fam
-    prof_ms, stale, tag = None, None, None
+    prof, stale, tag = None, None, None
     if share and share.get("config", "kitti") == config and share.get("batch_images") == units \
             and kernel_family(share["dominant"]) in names["families"]:       # a profile of the kernels that run
         dom = kernel_family(share["dominant"])
         tag = share.get("tag")
         stale = share.get("source_sha16") != source_sha16()
-        prof_ms = sum(k["ms_per_step"] for k in share["kernels"] if kernel_family(k["kernel"]) == dom)
+        prof = [k for k in share["kernels"] if kernel_family(k["kernel"]) == dom]
 
     def line(fam, kernel_name):
-        stages = LIVE_STAGES.get(fam)
-        if not stages or any(st not in per_call for st in stages):
+        if fam not in LIVE_STAGES:
             return None
-        t_ms = sum(per_call[st] for st in stages)
+        stages, busy = LIVE_STAGES[fam]
+        if busy not in per_call or any(st not in per_call for st in stages):
+            return None
+        t_ms = per_call[busy]
         bytes_step = cb * units
         achieved = bytes_step / (t_ms * 1e-3) / 1e9
         traffic = None
@@ -569,8 +581,10 @@ def roofline_lines(per_call, cfg, units, config):
             traffic = pmc.get("hbm_bytes_per_step", pmc.get("hbm_bytes_per_launch"))
         return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": kernel_name,
-                "launches_per_step": len(stages), "live_stages": list(stages),
-                "kernel_ms_per_step": round(t_ms, 4), "algorithmic_bytes_per_step": bytes_step,
+                "launches_per_step": len(stages), "live_stages": list(stages), "live_busy_stage": busy,
+                "kernel_ms_per_step": round(t_ms, 4),
+                "launch_span_ms": {st: round(per_call[st], 4) for st in stages},
+                "algorithmic_bytes_per_step": bytes_step,
                 "algorithmic_bytes_per_unit": cb, "units_per_step": units,
                 "traffic_ratio": round(traffic / bytes_step, 2) if traffic else None,
                 "unit_of_work": "one extraction (SURVEY §8d: image in + nfeatures x 60 B out); the kernel's launches of a "
@@ -581,8 +595,15 @@ def roofline_lines(per_call, cfg, units, config):
     if main_line is not None:
         main_line["selected_by"] = (f"largest share of GPU time in profiles/kernel_share.json ({tag})" if tag else
                                     "default (no kernel_share.json for this config)")
-        if prof_ms is not None:
-            main_line["rocprof_ms_per_step"] = round(prof_ms, 4)
+        if prof:
+            k0 = prof[0]
+            main_line["rocprof_busy_ms_per_step"] = k0.get("busy_ms_per_step")
+            main_line["rocprof_launches_per_step"] = k0.get("launches_per_step")
+            main_line["rocprof_launch_avg_us"] = [g["avg_us"] for g in k0.get("grids", [])]
+            if k0.get("busy_ms_per_step"):
+                main_line["frac_rocprof"] = round(main_line["algorithmic_bytes_per_step"] /
+                                                  (k0["busy_ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
+            main_line["profile"] = f"profiles/kernel_share.json ({tag})"
             main_line["profile_stale"] = stale
     sec = line(kernel_family(desc_name), desc_name) if kernel_family(desc_name) != dom else None
     return main_line, sec
@@ -929,7 +950,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_timing and args.alone_reps > 0:
         per, calls = alone_block(pkg, cfg, img_sets[0], dev, args.alone_reps)
         fam = kernel_family(active_kernel_names()["fast"])
-        t_ms = sum(per.get(st_, 0.0) for st_ in LIVE_STAGES[fam])
+        t_ms = sum(per.get(st_, 0.0) for st_ in LIVE_STAGES[fam][0])            # serial: the spans do not overlap
         cb = compulsory_bytes(cfg)["extraction"] * 2 * B
         ach = cb / (t_ms * 1e-3) / 1e9 if t_ms > 0 else 0.0
         out["roofline_alone"] = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -959,7 +980,7 @@ def main():
     # ordered teardown while the runtime is up: every queue drained, then the library objects destroyed newest first
     torch.cuda.synchronize()
     pkg.orbx.close_all()
-    torch.cuda.synchronize()
+    pkg.orbx.device_check(dev.index)                   # raises (exit status 1) on a pending device error
     if world > 1:
         dist.destroy_process_group()
 

@@ -51,6 +51,10 @@ const char* orbx_last_error(void);
 const char* orbx_version(void);
 /* Number of visible HIP devices (0 when none; never fails). */
 int orbx_device_count(void);
+/* Waits for every stream of `device` and returns ORBX_ERR_HIP (message in orbx_last_error) if the device holds a
+ * pending error -- a kernel fault, an illegal address.  For a caller's shutdown path: a fault after the last result
+ * must not end in exit status 0. */
+int orbx_device_check(int device);
 
 /* A non-blocking stream on `device` (no reference counterpart: scheduling plumbing for device-API callers).
  * cu_exclude > 0 leaves that many compute units out of the stream's CU mask (spread over the device), so that
@@ -154,7 +158,7 @@ int orbx_extractor_level_device(orbx_extractor* ex, int index, int level, const 
  * borders (REFLECT_101) included: what computeDescriptors reads (src/ORBextractor.cc:1085-1086 blurs a clone of
  * mvImagePyramid[level] with GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101)).  The reference keeps it internal; the
  * parity tests read it to check every blurred pixel, not only those around keypoints.  Waits for the extractor's
- * work.  ORBX_ERR_ARG when the extractor blurs per keypoint (ORBX_DESC_FB=1: no blurred pyramid exists). */
+ * work.  ORBX_ERR_ARG before the first call. */
 int orbx_extractor_copy_blurred_level(orbx_extractor* ex, int index, int level, uint8_t* dst, size_t dst_step);
 
 /* Device-side error word of the extractor, after every call issued so far has finished (waits for them).

@@ -5,9 +5,9 @@
 // Per device call over a batch of B images (all rows x cols), two streams (run_batch; §7 of DESIGN.md):
 //   (level 0 is read in place from the caller's images: no copy)   (ComputePyramid :1127)
 //   k_resize4       level l-1 -> level l, l = 1..L-1 (chained, launch stream)      (ComputePyramid :1120)
-//   k_fast_band     one workgroup per (band of <= 4 cells of one cell row, image): the band ROI as an f16-biased
-//                   u16 pair image in LDS, compass pre-test in quads, closed-form FAST scores of the survivors,
-//                   cell-masked strict 3x3 NMS at iniThFAST / minThFAST, per-cell fallback and row-major slots
+//   k_fast_wave     one wave per (cell, image): the cell ROI as an f16-biased u16 pair image in the wave's LDS
+//                   slice, compass pre-test in quads, closed-form FAST scores of the survivors, strict 3x3 NMS at
+//                   iniThFAST / minThFAST, per-cell fallback, row-major slots by wave ballots (no barrier)
 //                   (level 0 on the side stream, levels 1..L-1 on the launch stream)   (:789-829)
 //   k_blur7         7x7 sigma-2 Gaussian on every level (REFLECT_101), register-streaming, side stream (:1085-1086)
 //   k_quadtree      one workgroup per (level, image): DistributeOctTree's list/quadtree as data-parallel
@@ -286,110 +286,22 @@ __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size
     resize4_item(pyr, pyr_stride, src, src_step, src_istride, sw, dst_off, dw, dh, t, strip, band, img);
 }
 
-// The small levels of the chain in ONE launch: one 1024-thread workgroup per image walks levels lt .. nl-1, each
-// level's (strip, band) items spread over its 16 waves, a workgroup barrier between levels (the next level reads
-// what other waves of the workgroup stored).  Seven dependent launches of shrinking grids were launch- and
-// tail-latency bound (the last ones 10-20 us for a few hundred kilobytes); here the tail levels cost one launch.
-struct ResizeTail {
-    ResizeVec t[kMaxLevels];
-    int sw[kMaxLevels], sh[kMaxLevels], src_off[kMaxLevels], dst_off[kMaxLevels], dw[kMaxLevels], dh[kMaxLevels];
-    int nstrips[kMaxLevels], nbands[kMaxLevels];
-};
-__global__ __launch_bounds__(1024) void k_resize_tail(uint8_t* __restrict__ pyr, size_t pyr_stride, int lt, int nl,
-                                                      const ResizeTail* __restrict__ tail) {
-    const int img = blockIdx.x;
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), nw = blockDim.x >> 6;
-    for (int l = lt; l < nl; ++l) {
-        const ResizeVec t = tail->t[l];
-        const int ns = tail->nstrips[l], nitems = ns * tail->nbands[l];
-        const uint8_t* src = pyr + tail->src_off[l];
-        for (int it = w; it < nitems; it += nw) {
-            const int band = it / ns, strip = it - band * ns;
-            resize4_item(pyr, pyr_stride, src, (size_t)tail->sw[l], pyr_stride, tail->sw[l], tail->dst_off[l], tail->dw[l],
-                         tail->dh[l], t, strip, band, img);
-        }
-        __syncthreads();   // workgroup-scope release/acquire: the waves of one workgroup share the CU's L1 (an agent-scope
-                           // fence here writes back L2 per wave, measured 4x slower than the separate launches)
-    }
-}
-
 // FAST-9/16 corner score in closed form.  For pixel value v and circle values p_k (Bresenham r=3,
 // OpenCV order), with d_k = v - p_k:  m_dark = max over the 16 arcs of 9 of min d, m_bright = max
 // over arcs of min(-d).  OpenCV's cornerScore<16> returns max(t, m_dark, m_bright) - 1 and the pixel
 // is a corner at threshold t iff max(m_dark, m_bright) > t; hence s = max(m_dark, m_bright) - 1 is
 // threshold independent and "corner at t" <=> s >= t.  Computed for two horizontally
-// adjacent pixels at once in packed 16-bit lanes (v_pk_sub/min/max_i16).
+// adjacent pixels at once in packed 16-bit lanes.
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s16x2 as_s2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
-__device__ __forceinline__ s16x2 pmin(s16x2 a, s16x2 b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ s16x2 pmax(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ uint32_t align16(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbit(hi, lo, 16); }
 
-// Dwords per LDS pair-image row, per launch (template): 24 when the launch's widest cell ROI fits (the KITTI/EuRoC
-// case: ROI <= 46 columns), else 48.  A 32-lane half of a ds_read_b32 covers two ROI rows of 16 pairs; with 64 banks
-// any stride in [16, 48] mod 64 keeps the two rows on disjoint banks.  The narrow form cuts the workgroup's LDS from
-// ~25 KB to ~16 KB: 8 resident workgroups per CU (32 waves) instead of 6.
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// The ROI lives in LDS as two pair images of 2 x u16 per dword:  E[r][i] = (roi[r][2i], roi[r][2i+1])
-// and O[r][i] = (roi[r][2i+1], roi[r][2i+2]).  The pixel pair (x, x+1) at odd x is O[r][(x-1)/2]; a tap
-// at horizontal offset dx reads O (dx even) or E (dx odd) -- every one of the 17 reads for two pixels is
-// a 4-byte-aligned ds_read_b32 with a compile-time offset (2-byte-misaligned 32-bit LDS reads measured
-// ~2x slower on gfx950).  The reads are explicit (inline asm) so the compiler does not merge neighbours
-// into misaligned b64/b128 reads.
-// kOE: no O image in LDS; O[i] = (E[i] hi, E[i+1] lo) = v_alignbit(E[i+1], E[i], 16) from two aligned E reads (half
-// the pair-image LDS, so more resident workgroups; neighbouring taps share their E reads).
-template <bool kOE>
-__device__ __forceinline__ uint32_t o_at(const uint32_t* __restrict__ ob, const uint32_t* __restrict__ eb, int i) {
-    if (kOE) return __builtin_amdgcn_alignbit(eb[i + 1], eb[i], 16);
-    return ob[i];
-}
-
-template <int kPairStride, bool kOE = false>
-__device__ __forceinline__ s16x2 fast_score2(const uint32_t* __restrict__ E, const uint32_t* __restrict__ O, int y, int j) {
-    const uint32_t* eb = E + (y - 3) * kPairStride + j;   // row y-3, pair index j; offsets >= 0
-    const uint32_t* ob = kOE ? eb : O + (y - 3) * kPairStride + j;
-    uint32_t r[17];
-#define ORBX_TAP(k, dx, dy) \
-    r[k] = ((dx) & 1) ? eb[((dy) + 3) * kPairStride + (3 + (dx)) / 2] : o_at<kOE>(ob, eb, ((dy) + 3) * kPairStride + 1 + (dx) / 2)
-    ORBX_TAP(16, 0, 0);
-    ORBX_TAP(0, 0, 3);    ORBX_TAP(1, 1, 3);    ORBX_TAP(2, 2, 2);    ORBX_TAP(3, 3, 1);
-    ORBX_TAP(4, 3, 0);    ORBX_TAP(5, 3, -1);   ORBX_TAP(6, 2, -2);   ORBX_TAP(7, 1, -3);
-    ORBX_TAP(8, 0, -3);   ORBX_TAP(9, -1, -3);  ORBX_TAP(10, -2, -2); ORBX_TAP(11, -3, -1);
-    ORBX_TAP(12, -3, 0);  ORBX_TAP(13, -3, 1);  ORBX_TAP(14, -2, 2);  ORBX_TAP(15, -1, 3);
-#undef ORBX_TAP
-    const s16x2 v = as_s2(r[16]);
-    s16x2 d[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) d[k] = v - as_s2(r[k]);
-    // The 16 arcs pair up as OpenCV's cornerScore walks them: for even k the arcs starting at k and k+1 share the
-    // 8 taps k+1..k+8 (m8), so max(min arc_k, min arc_k+1) = min(m8, max(d[k], d[k+9])); m8 comes from pair and
-    // quad minima over odd starts.  Likewise for the bright side with min/max swapped.  (112 packed ops, was 176.)
-    s16x2 a2[8], b2[8], a4[8], b4[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) { a2[m] = pmin(d[2 * m + 1], d[(2 * m + 2) & 15]); b2[m] = pmax(d[2 * m + 1], d[(2 * m + 2) & 15]); }
-#pragma unroll
-    for (int m = 0; m < 8; ++m) { a4[m] = pmin(a2[m], a2[(m + 1) & 7]); b4[m] = pmax(b2[m], b2[(m + 1) & 7]); }
-    s16x2 dk[8], br[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        const s16x2 e0 = d[2 * m], e9 = d[(2 * m + 9) & 15];
-        dk[m] = pmin(pmin(a4[m], a4[(m + 2) & 7]), pmax(e0, e9));   // max over arcs 2m, 2m+1 of min d
-        br[m] = pmax(pmax(b4[m], b4[(m + 2) & 7]), pmin(e0, e9));   // min over arcs 2m, 2m+1 of max d
-    }
-#pragma unroll
-    for (int w = 4; w > 0; w >>= 1)      // balanced reductions (short dependency chains)
-#pragma unroll
-        for (int k = 0; k < w; ++k) { dk[k] = pmax(dk[k], dk[k + w]); br[k] = pmin(br[k], br[k + w]); }
-    return pmax(dk[0], (s16x2)(0) - br[0]) - (s16x2)(1);
-}
-
-// fast_score2 on an f16-biased pair image (k_fast_band with ORBX_FAST_F16): every u16 lane holds the f16 value
-// 1024 + pixel (bits 0x6400 | pixel), so tap differences are exact f16 subtractions and the arc minima / maxima use
-// gfx950's 3-input packed f16 min / max (20 % fewer VALU operations than the i16 form).  Scores below 0 are raised to
-// -1 (never a corner, never blocks a neighbour in the NMS -- the same keypoints); the result is i16 like fast_score2.
+// The cell ROI lives in LDS as an f16-biased pair image E of 2 x u16 per dword: E[r][i] = (roi[r][2i], roi[r][2i+1]),
+// every u16 lane holding the f16 value 1024 + pixel (bits 0x6400 | pixel), so tap differences are exact f16
+// subtractions and the arc minima / maxima use gfx950's 3-input packed f16 min / max.  The pair starting at an odd
+// column, (roi[2i+1], roi[2i+2]), is v_alignbit(E[i+1], E[i], 16) of two aligned reads.  Scores below 0 are raised to
+// -1 (never a corner, never blocks a neighbour in the NMS -- the same keypoints); the result is i16.
 typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h16x2 as_h2(uint32_t v) { return __builtin_bit_cast(h16x2, v); }
 __device__ __forceinline__ h16x2 hmin(h16x2 a, h16x2 b) { return __builtin_elementwise_min(a, b); }
@@ -409,7 +321,8 @@ template <int kPairStride>
 __device__ __forceinline__ void fast_taps_f16(const uint32_t* __restrict__ E, int y, int j, uint32_t (&r)[17]) {
     const uint32_t* eb = E + (y - 3) * kPairStride + j;
 #define ORBX_TAP(k, dx, dy) \
-    r[k] = ((dx) & 1) ? eb[((dy) + 3) * kPairStride + (3 + (dx)) / 2] : o_at<true>(eb, eb, ((dy) + 3) * kPairStride + 1 + (dx) / 2)
+    r[k] = ((dx) & 1) ? eb[((dy) + 3) * kPairStride + (3 + (dx)) / 2] \
+                      : align16(eb[((dy) + 3) * kPairStride + 2 + (dx) / 2], eb[((dy) + 3) * kPairStride + 1 + (dx) / 2])
     ORBX_TAP(16, 0, 0);
     ORBX_TAP(0, 0, 3);    ORBX_TAP(1, 1, 3);    ORBX_TAP(2, 2, 2);    ORBX_TAP(3, 3, 1);
     ORBX_TAP(4, 3, 0);    ORBX_TAP(5, 3, -1);   ORBX_TAP(6, 2, -2);   ORBX_TAP(7, 1, -3);
@@ -417,15 +330,6 @@ __device__ __forceinline__ void fast_taps_f16(const uint32_t* __restrict__ E, in
     ORBX_TAP(12, -3, 0);  ORBX_TAP(13, -3, 1);  ORBX_TAP(14, -2, 2);  ORBX_TAP(15, -1, 3);
 #undef ORBX_TAP
 }
-__device__ __forceinline__ s16x2 fast_score_from_taps_f16(const uint32_t (&r)[17]);
-
-template <int kPairStride>
-__device__ __forceinline__ s16x2 fast_score2_f16(const uint32_t* __restrict__ E, int y, int j) {
-    uint32_t r[17];
-    fast_taps_f16<kPairStride>(E, y, j, r);
-    return fast_score_from_taps_f16(r);
-}
-
 __device__ __forceinline__ s16x2 fast_score_from_taps_f16(const uint32_t (&r)[17]) {
     const h16x2 v = as_h2(r[16]);
     h16x2 d[16];
@@ -450,31 +354,11 @@ __device__ __forceinline__ s16x2 fast_score_from_taps_f16(const uint32_t (&r)[17
     return as_s2(__builtin_bit_cast(uint32_t, m)) - (s16x2){0x6401, 0x6401};
 }
 
-// Compass pre-test for a pixel pair: every arc of 9 contains two compass taps 4 apart (0/4, 4/8, 8/12 or
-// 12/0), so "corner at t" (some arc with all d > t, or all d < -t) implies max over those four pairs of
-// min(d_k, d_k+4) > t, or min of max < -t.  A pixel failing it has s < t.  Returns 2 bits (pixel x, x+1).
-template <int kPairStride, bool kOE = false>
-__device__ __forceinline__ int fast_pretest2(const uint32_t* __restrict__ E, const uint32_t* __restrict__ O, int y, int j,
-                                             int t) {
-    const uint32_t* eb = E + (y - 3) * kPairStride + j;
-    const uint32_t* ob = kOE ? eb : O + (y - 3) * kPairStride + j;
-    const s16x2 v = as_s2(o_at<kOE>(ob, eb, 3 * kPairStride + 1));
-    const s16x2 d0 = v - as_s2(o_at<kOE>(ob, eb, 6 * kPairStride + 1));      // ( 0,  3)
-    const s16x2 d4 = v - as_s2(eb[3 * kPairStride + 3]);      // ( 3,  0)
-    const s16x2 d8 = v - as_s2(o_at<kOE>(ob, eb, 1));         // ( 0, -3)
-    const s16x2 d12 = v - as_s2(eb[3 * kPairStride + 0]);     // (-3,  0)
-    const s16x2 dk = pmax(pmax(pmin(d0, d4), pmin(d4, d8)), pmax(pmin(d8, d12), pmin(d12, d0)));
-    const s16x2 br = pmin(pmin(pmax(d0, d4), pmax(d4, d8)), pmin(pmax(d8, d12), pmax(d12, d0)));
-    const s16x2 m = pmax(dk, (s16x2)(0) - br);
-    return (m.x > t ? 1 : 0) | (m.y > t ? 2 : 0);
-}
-
 // OpenCV's NMS keeps a corner (s >= t) iff s > every neighbour's buffer value (s_n if s_n >= t, else
 // 0).  For s >= max(t, 1) a neighbour with s_n < t never blocks (s_n < t <= s, and 0 < s), so the rule
 // is: s >= max(t, 1) and s > max of the 8 raw neighbour scores -- one maximum serves both thresholds.
 // For a pixel pair the 8 neighbour pairs come from 3 aligned dwords per row (v_alignbit for the odd
 // shifts) and 7 v_pk_max_i16.
-__device__ __forceinline__ uint32_t align16(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbit(hi, lo, 16); }
 
 __device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, int rr, int j, int T1, int T2,
                                         bool second) {
@@ -496,634 +380,10 @@ __device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, 
     return (g0 & (sv.x >= T1)) | ((g1 & (sv.y >= T1)) << 1) | ((g0 & (sv.x >= T2)) << 2) | ((g1 & (sv.y >= T2)) << 3);
 }
 
-// One workgroup per (image, cell) (XCD-aware order: the cells of one image share an L2).  Cell geometry from
-// ComputeKeyPointsOctTree (:784-807); FAST on the ROI detects rows/cols [3, dim-3) of the ROI, NMS compares
-// against the 8 neighbours' scores inside the ROI's detection window (0 outside), strict '>' (OpenCV
-// FAST_t).  Empty at iniTh -> minTh (:812-816).  (A persistent form -- each workgroup walking a range of
-// cells with the next ROI prefetched into registers -- measured 1.3x slower: fewer resident workgroups.)
-// Dynamic LDS: E and O pair images (max_rows x kPairStride dwords each) + padded int16 score map whose
-// pixel pairs are dword aligned (det column x at map column x + 2, pad ring at columns 1 and Wd + 2) +
-// survivor list + kept-pixel key lists.
-// Byte offset of the three counters after the dynamic LDS arrays of k_fast_cells (16-byte aligned).
-__host__ __device__ __forceinline__ int fast_counter_off(int R, int Cc, int kPairStride) {
-    const int b = 2 * R * kPairStride * 4 + 4 * (((R - 4) * Cc + 1) / 2) + 2 * ((R * Cc / 2 + 65) & ~1) + 2 * 2 * (R * Cc / 4 + 32);
-    return (b + 15) & ~15;
-}
-
-constexpr int kFastPf = 6;        // row groups per wave held in flight (ROI <= 72 rows, chunks <= 19 per row)
-
-struct FastRoi {                  // lane mapping of one cell's ROI: lane -> (row in group, 4-column chunk)
-    int cpr, rpi, ngroups, rr, c;
-    bool lane_ok;
-};
-
-__device__ __forceinline__ FastRoi fast_roi(int W, int H, int ln) {
-    FastRoi f;
-    f.cpr = (W + 2 + 3) >> 2;
-    f.rpi = kWave / f.cpr;
-    f.ngroups = (H + f.rpi - 1) / f.rpi;
-    f.rr = ln / f.cpr;
-    f.c = ln - f.rr * f.cpr;
-    f.lane_ok = f.rr < f.rpi;
-    return f;
-}
-
-template <int kPairStride>
-__global__ __launch_bounds__(256) void k_fast_cells(const uint8_t* __restrict__ pyr, size_t pyr_stride,
-                                                    const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
-                                                    int iniTh, int minTh, uint32_t* __restrict__ cand_xy,
-                                                    uint8_t* __restrict__ cand_s, int cand_stride,
-                                                    int* __restrict__ cell_cnt, int ncells, int batch, int stop_after,
-                                                    Src0 s0, int max_rows, int max_cols, int cell0, int ncell_sub) {
-    // counters at the tail of the dynamic region (no static __shared__: it would shift the dynamic base off 16-byte
-    // alignment and the ds_write_b64 of the pair images would replay, cdna_hip_programming.md Guideline 17)
-    extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
-    uint32_t* E = fsm;
-    uint32_t* O = fsm + max_rows * kPairStride;
-    int16_t* sc = (int16_t*)(fsm + 2 * max_rows * kPairStride);
-    uint16_t* list = (uint16_t*)(fsm + 2 * max_rows * kPairStride + ((max_rows - 4) * max_cols + 1) / 2);
-    const int kmax = max_rows * max_cols / 4 + 32;           // >= strict-NMS bound ceil(wd/2)*ceil(hd/2)
-    uint16_t* kini = list + ((max_rows * max_cols / 2 + 65) & ~1);
-    uint16_t* kmin = kini + kmax;
-    int* counters = reinterpret_cast<int*>(fsm) + fast_counter_off(max_rows, max_cols, kPairStride) / 4;
-    int& nsurv = counters[0];
-    int& nki = counters[1];
-    int& nkm = counters[2];
-    const int tid = threadIdx.x, w = tid >> 6, ln = lane_id();
-    // cells [cell0, cell0 + ncell_sub) of every image (a level range: cells are level-major)
-    const int item = xcd_item(xcd_chunk(ncell_sub * batch));  // (image, cell), cells of one image adjacent
-    if (item >= ncell_sub * batch) return;                    // whole workgroup: no barrier is split
-    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
-    const int tp = min(T1, T2);
-    {
-        const int img = item / ncell_sub, c = cell0 + (item - img * ncell_sub);
-        const CellDev cd = cells[c];
-        const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
-        const bool live = Wd > 0 && Hd > 0;                       // workgroup-uniform
-        const int SW = (Wd + 5) & ~1;        // int16 per score-map row (even: rows stay dword aligned)
-        {
-            // 1. ROI -> pair images: lanes are (row, 4-column chunk) pairs, one 8-byte load per lane and row
-            //    group (all issued before the first use), E[r][i] = (roi[2i], roi[2i+1]) and O[r][i] =
-            //    (roi[2i+1], roi[2i+2]) built with v_perm_b32 and stored as ds_write_b64; columns >= W read as 0
-            const LevelDev L = levels[cd.level];
-            int lstride;
-            const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
-            const FastRoi f = fast_roi(W, H, ln);
-            const uint8_t* src = base + (size_t)cd.y0 * lstride + cd.x0 + 4 * f.c;
-            uint32_t pf[2 * kFastPf];
-#pragma unroll
-            for (int k = 0; k < kFastPf; ++k) {
-                const int r = (w + 4 * k) * f.rpi + f.rr;
-                pf[2 * k] = pf[2 * k + 1] = 0;
-                if (live && f.lane_ok && r < H) __builtin_memcpy(&pf[2 * k], src + (size_t)r * lstride, 8);
-            }
-            const int keep = W - 4 * f.c;                          // bytes of this chunk inside the ROI
-#pragma unroll
-            for (int k = 0; k < kFastPf; ++k) {
-                const int r = (w + 4 * k) * f.rpi + f.rr;
-                if (live && f.lane_ok && r < H) {
-                    uint32_t lo = pf[2 * k], hi = pf[2 * k + 1];
-                    if (keep < 8) {
-                        const uint64_t m = keep <= 0 ? 0ull : ((1ull << (8 * keep)) - 1ull);
-                        const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
-                        lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
-                    }
-                    const uint2 e = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u), __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
-                    const uint2 o = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c020c01u), __builtin_amdgcn_perm(hi, lo, 0x0c040c03u));
-                    *reinterpret_cast<uint2*>(E + r * kPairStride + 2 * f.c) = e;
-                    *reinterpret_cast<uint2*>(O + r * kPairStride + 2 * f.c) = o;
-                }
-            }
-            if (live) {
-                for (int i = tid; i < SW; i += blockDim.x) { sc[i] = -1; sc[(Hd + 1) * SW + i] = -1; }
-                for (int r = tid; r < Hd + 2; r += blockDim.x) { sc[r * SW + 1] = -1; sc[r * SW + Wd + 2] = -1; }
-            }
-            if (tid == 0) { nsurv = 0; nki = 0; nkm = 0; }
-            __syncthreads();
-        }
-        int count = 0;
-        if (live && stop_after != 1) {
-            // 2. compass pre-test for every pixel pair at tp = min(T1, T2); the score map gets 0 (< tp: never
-            //    kept, never blocks) and the surviving pairs go to an LDS list (order irrelevant)
-            const int PR = (Wd + 1) >> 1, NP = Hd * PR;
-            // pair q = tid + 256*it -> (row rr, pair column j), walked incrementally (no division per step)
-            const int rr0 = tid / PR, j0 = tid - rr0 * PR;
-            const int dq = (int)blockDim.x / PR, dj = (int)blockDim.x - dq * PR;
-            for (int q = tid, rr = rr0, j = j0; q < NP; q += blockDim.x) {
-                const bool two = 2 * j + 1 < Wd;
-                const int pt = fast_pretest2<kPairStride>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
-                *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
-                const uint64_t bm = __ballot(pt != 0);
-                int wbase = 0;
-                if (ln == 0 && bm) wbase = atomicAdd(&nsurv, __popcll(bm));
-                wbase = __shfl(wbase, 0, kWave);
-                if (pt) list[wbase + lanes_below(bm)] = (uint16_t)((rr << 8) | j);
-                rr += dq; j += dj;
-                if (j >= PR) { j -= PR; ++rr; }
-            }
-            __syncthreads();
-            const int ns = nsurv;
-            if (stop_after != 2) {
-                // 3. full closed-form scores of the surviving pairs only
-                for (int i = tid; i < ns; i += blockDim.x) {
-                    const int rr = list[i] >> 8, j = list[i] & 0xff;
-                    const s16x2 s2 = fast_score2<kPairStride>(E, O, rr + 3, j);
-                    *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
-                }
-                __syncthreads();
-                // 4. NMS at iniTh and minTh in one pass from 3 x 3 aligned dwords per surviving pair (other
-                //    pairs have s < tp and keep nothing); kept pixels of each threshold appended to an LDS
-                //    key list (key = row * 128 + column: row-major order)
-                int any = 0;
-                for (int i0 = 0; i0 < ns; i0 += blockDim.x) {
-                    const int i = i0 + tid;
-                    int f = 0, key = 0;
-                    if (i < ns) {
-                        const int rr = list[i] >> 8, j = list[i] & 0xff;
-                        f = nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd);
-                        key = rr * 128 + 2 * j;
-                    }
-                    any |= f;
-#pragma unroll
-                    for (int bit = 0; bit < 4; ++bit) {
-                        const bool on = (f >> bit) & 1;
-                        const uint64_t bm = __ballot(on);
-                        if (!bm) continue;
-                        int base = 0;
-                        if (ln == 0) base = atomicAdd(bit < 2 ? &nki : &nkm, __popcll(bm));
-                        base = __shfl(base, 0, kWave);
-                        const int pos = base + lanes_below(bm);
-                        if (on && pos < kmax) (bit < 2 ? kini : kmin)[pos] = (uint16_t)(key + (bit & 1));
-                    }
-                }
-                const int any_ini = __syncthreads_or((any & 3) != 0);
-                if (stop_after != 3) {
-                    // 5. cell empty at iniTh -> minTh (:812-816); output in OpenCV's row-major order: each
-                    //    kept pixel's slot is its rank among the cell's keys (few per cell)
-                    const uint16_t* keys = any_ini ? kini : kmin;
-                    const int nk = min(any_ini ? nki : nkm, kmax);
-                    uint32_t* oxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
-                    uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
-                    for (int i = tid; i < nk; i += blockDim.x) {
-                        const int k = keys[i];
-                        int rank = 0;
-                        for (int m = 0; m < nk; ++m) rank += keys[m] < k;
-                        if (rank < cd.slot_cap) {
-                            const int rr = k >> 7, x = k & 127;
-                            oxy[rank] = (uint32_t)(cd.x0 + 3 + x) | ((uint32_t)(cd.y0 + rr + 3) << 16);
-                            os[rank] = (uint8_t)sc[(rr + 1) * SW + 2 + x];
-                        }
-                    }
-                    count = min(nk, cd.slot_cap);
-                }
-            }
-        }
-        if (tid == 0) cell_cnt[(size_t)img * ncells + c] = count;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Band form of the cell FAST: one workgroup per (image, band), a band = up to G consecutive cells of one cell row
-// of a level (same iniY / ROI height).  The cells' ROIs overlap by 6 columns, so the band loads ONE ROI (x0 of the
-// first cell .. end of the last) into the pair images; pre-test and closed-form scores run over the band's whole
-// detection width, which is the concatenation of the cells' detection windows ([iniX+3, iniX+wCell+3) each).
-// Scores are position independent; only the NMS sees the cell: OpenCV's FAST on a cell ROI treats pixels outside
-// that cell's detection window as 0, so a neighbour across a cell boundary is masked out (-1 never blocks a kept
-// score s >= 1).  Kept pixels go to their own cell's key lists; the iniTh -> minTh fallback and the row-major
-// output order are per cell, as in k_fast_cells.  G cells share the load latency and the five barriers.
-// ---------------------------------------------------------------------------------------------
-struct BandDev {
-    int level, cell0, ncell;   // cells [cell0, cell0 + ncell) of one cell row, left to right
-    int x0, y0, W, H;          // band ROI in level coordinates (first cell's iniX / iniY, width to the last cell's end)
-    int wcell;                 // detection width of every cell but possibly the last (ceil(width / nCols))
-};
-constexpr int kBandMaxCells = 8;
-
-struct BandLds {               // byte offsets inside the dynamic LDS of k_fast_band
-    int o_sc, o_list, o_keys, o_meta, o_cnt, o_bm, bytes;
-};
-constexpr int kBandMaxIt = 32;   // pre-test iterations per thread (NP <= 32 * 256)
-// rows: max ROI rows; sw: max score-map row (int16); np: max pairs; kmax: max keys per cell and threshold; ps: dwords
-// per pair-image row
-__host__ __device__ __forceinline__ BandLds band_lds(int rows, int sw, int np, int kmax, int ps, int gmax, bool oe) {
-    BandLds b;
-    int o = (oe ? 1 : 2) * rows * ps * 4;                       // E (and O)
-    b.o_sc = o;   o += ((rows - 4) * sw * 2 + 15) & ~15;        // score map (Hd + 2 rows)
-    b.o_list = o; o += (np * 2 + 15) & ~15;                     // survivor pairs
-    b.o_keys = o; o += (2 * gmax * kmax * 2 + 15) & ~15;        // per cell: iniTh keys, minTh keys
-    b.o_meta = o; o += (2 * sw + 15) & ~15;                     // per detection column: cell index, boundary flag
-    b.o_cnt = o;  o += 16 * (2 * kBandMaxCells + 1);
-    b.o_bm = o;   o += kBandMaxIt * 4 * (8 + 4);                 // per (iteration, wave): survivor ballot, list base
-    b.bytes = o;
-    return b;
-}
-
-// NMS of a pixel pair of the band score map with cell-boundary masks.  P1 = (full column x-1, full column x),
-// P2 = (column x above/below, column x+1 above/below), P3 = (full column x+1, full column x+2); keep1 / keep3 hold
-// 0xffff in the 16-bit lanes whose column lies in the pixel's own cell.  Result bits as nms_pair.
-__device__ __forceinline__ int nms_pair_band(const int16_t* __restrict__ sc, int SW, int rr, int j, int T1, int T2, bool second,
-                                             uint32_t keep1, uint32_t keep3) {
-    const uint32_t* r0 = (const uint32_t*)(sc + rr * SW + 2 * j);
-    const uint32_t* r1 = r0 + (SW >> 1);
-    const uint32_t* r2 = r1 + (SW >> 1);
-    const uint32_t a0 = r0[0], a1 = r0[1], a2 = r0[2];
-    const uint32_t b0 = r1[0], b1 = r1[1], b2 = r1[2];
-    const uint32_t c0 = r2[0], c1 = r2[1], c2 = r2[2];
-    s16x2 p1 = pmax(pmax(as_s2(align16(a1, a0)), as_s2(align16(b1, b0))), as_s2(align16(c1, c0)));
-    const s16x2 p2 = pmax(as_s2(a1), as_s2(c1));
-    s16x2 p3 = pmax(pmax(as_s2(align16(a2, a1)), as_s2(align16(b2, b1))), as_s2(align16(c2, c1)));
-    p1 = as_s2(__builtin_bit_cast(uint32_t, p1) | ~keep1);
-    p3 = as_s2(__builtin_bit_cast(uint32_t, p3) | ~keep3);
-    const s16x2 m = pmax(pmax(p1, p2), p3);
-    const s16x2 sv = as_s2(b1);
-    const int g0 = sv.x > m.x, g1 = second && (sv.y > m.y);
-    return (g0 & (sv.x >= T1)) | ((g1 & (sv.y >= T1)) << 1) | ((g0 & (sv.x >= T2)) << 2) | ((g1 & (sv.y >= T2)) << 3);
-}
-
-constexpr int kBandPf = 6;     // ROI loads per thread held in flight per round
-
-#ifdef ORBX_QT_PROF
-__device__ unsigned long long g_fbprof[2][16];
-#define FBP(k)                                                                                                       \
-    do {                                                                                                             \
-        if (threadIdx.x == 0 && item == 8 * 37 + 3) g_fbprof[band0 ? 1 : 0][k] = wall_clock64();                    \
-    } while (0)
-#else
-#define FBP(k) do {} while (0)
-#endif
-
-// Diagnostics build only (make variant D=-DORBX_FAST_STOP=k): the workgroup stops after phase k (1 ROI load, 2 pre-test
-// and survivor list, 3 scores, 4 NMS) and reports empty cells -- the time of the phases before k, for ablation.
-#ifdef ORBX_FAST_STOP
-#define FAST_STOP(k)                                                                                                 \
-    do {                                                                                                             \
-        if ((k) == ORBX_FAST_STOP) {                                                                                 \
-            if (tid < nc) cell_cnt[(size_t)img * ncells + bd.cell0 + tid] = 0;                                       \
-            return;                                                                                                  \
-        }                                                                                                            \
-    } while (0)
-#else
-#define FAST_STOP(k) do {} while (0)
-#endif
-
-#ifndef ORBX_FAST_QUAD
-#define ORBX_FAST_QUAD 1
-#endif
-#ifndef ORBX_FAST_F16
-#define ORBX_FAST_F16 1         // 0: i16 pair image and scores (fast_score2)
-#endif
-#ifndef ORBX_FAST_ONEPASS
-#define ORBX_FAST_ONEPASS 1     // 0: iniTh pre-test first, minTh re-test of the cells left empty (bit-exact; measured
-                                // slower: serial FAST 0.930 -> 0.971 ms, the re-test phases cost more than the scores saved)
-#endif
-template <int kPairStride, bool kOE>
-__global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ pyr, size_t pyr_stride,
-                                                   const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
-                                                   const BandDev* __restrict__ bands, int band0, int nband, int iniTh, int minTh,
-                                                   uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s, int cand_stride,
-                                                   int* __restrict__ cell_cnt, int ncells, int batch, Src0 s0, BandLds lay,
-                                                   int kmax) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
-    char* lds = reinterpret_cast<char*>(fsm);
-    uint32_t* E = fsm;
-    uint32_t* O = nullptr;       // set below (row count of the launch is in lay: O = E + rows * PS)
-    int16_t* sc = reinterpret_cast<int16_t*>(lds + lay.o_sc);
-    uint16_t* list = reinterpret_cast<uint16_t*>(lds + lay.o_list);
-    uint16_t* keys = reinterpret_cast<uint16_t*>(lds + lay.o_keys);
-    uint8_t* cidx = reinterpret_cast<uint8_t*>(lds + lay.o_meta);
-    int* counters = reinterpret_cast<int*>(lds + lay.o_cnt);      // [0] survivors, [1 + 2c + t] keys of cell c
-    if (!kOE) O = E + lay.o_sc / 8;                              // o_sc = 2 * rows * PS * 4 bytes
-    const int tid = threadIdx.x;
-    const int item = xcd_item(xcd_chunk(nband * batch));
-    if (item >= nband * batch) return;                          // whole workgroup
-    FBP(0);
-    const int img = item / nband;
-    const BandDev bd = bands[band0 + (item - img * nband)];
-    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
-    const int tp = min(T1, T2);
-    const int W = bd.W, H = bd.H, Wd = W - 6, Hd = H - 6;
-    const bool live = Wd > 0 && Hd > 0;                         // workgroup-uniform (one row of cells)
-    const int SW = (Wd + 5) & ~1;
-    const int wc = bd.wcell, nc = bd.ncell;
-    {
-        // 1. band ROI -> pair images; lanes walk (row, 4-column chunk) items, kBandPf 8-byte loads in flight
-        const LevelDev L = levels[bd.level];
-        int lstride;
-        const uint8_t* base = level_pixels(pyr, pyr_stride, L, bd.level, img, s0, lstride);
-        const int cpr = (W + 2 + 3) >> 2;
-        const int NQ = live ? H * cpr : 0;
-        const uint8_t* src0 = base + (size_t)bd.y0 * lstride + bd.x0;
-        const int dq = 256 / cpr, dc = 256 - dq * cpr;
-        int r = tid / cpr, c = tid - r * cpr;
-        for (int q0 = tid; q0 < NQ; q0 += kBandPf * 256) {
-            uint32_t pf[2 * kBandPf];
-            int rs[kBandPf], cs[kBandPf];
-#pragma unroll
-            for (int k = 0; k < kBandPf; ++k) {
-                rs[k] = r; cs[k] = c;
-                pf[2 * k] = pf[2 * k + 1] = 0;
-                if (q0 + k * 256 < NQ) __builtin_memcpy(&pf[2 * k], src0 + (size_t)r * lstride + 4 * c, 8);
-                r += dq; c += dc;
-                if (c >= cpr) { c -= cpr; ++r; }
-            }
-#pragma unroll
-            for (int k = 0; k < kBandPf; ++k) {
-                if (q0 + k * 256 < NQ) {
-                    uint32_t lo = pf[2 * k], hi = pf[2 * k + 1];
-                    const int keep = W - 4 * cs[k];
-                    if (keep < 8) {
-                        const uint64_t m = keep <= 0 ? 0ull : ((1ull << (8 * keep)) - 1ull);
-                        const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
-                        lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
-                    }
-                    uint2 e = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u), __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
-                    const uint2 o = make_uint2(__builtin_amdgcn_perm(hi, lo, 0x0c020c01u), __builtin_amdgcn_perm(hi, lo, 0x0c040c03u));
-                    if (kOE && ORBX_FAST_F16) { e.x |= 0x64006400u; e.y |= 0x64006400u; }   // f16 1024 + pixel
-                    *reinterpret_cast<uint2*>(E + rs[k] * kPairStride + 2 * cs[k]) = e;
-                    if (!kOE) *reinterpret_cast<uint2*>(O + rs[k] * kPairStride + 2 * cs[k]) = o;
-                }
-            }
-        }
-        if (live) {
-            for (int i = tid; i < SW; i += 256) { sc[i] = -1; sc[(Hd + 1) * SW + i] = -1; }
-            for (int rr = tid; rr < Hd + 2; rr += 256) { sc[rr * SW + 1] = -1; sc[rr * SW + Wd + 2] = -1; }
-            // per detection column x in [0, Wd + 2): cell index (low 7 bits) | left-boundary flag (bit 7: x starts a
-            // cell, so x - 1 is in another cell's window or outside the band)
-            for (int x = tid; x < Wd + 2; x += 256) {
-                const int cx = min(x / wc, nc - 1);
-                cidx[x] = (uint8_t)(cx | ((x == cx * wc || x >= Wd) ? 0x80 : 0));
-            }
-        }
-        if (tid < 24) counters[tid] = 0;                         // [20]: minTh re-test survivors
-        __syncthreads();
-    }
-    FBP(1);
-    FAST_STOP(1);
-    if (live) {
-        // 2. compass pre-test over the band's pixel pairs at tp (as k_fast_cells).  The survivor list keeps pair
-        //    order (row-major: the score and NMS passes then read neighbouring LDS words lane by lane, no bank
-        //    conflicts): per (iteration, wave) the ballot goes to LDS, wave 0 scans the counts, every lane places
-        //    its survivors at base + rank in its wave's ballot (NP <= 32 * 256, checked on the host)
-        const int w = tid >> 6, ln = lane_id();
-        int* bbase = reinterpret_cast<int*>(lds + lay.o_bm + kBandMaxIt * 4 * 8);
-        const uint64_t below = (1ull << ln) - 1ull;
-        // Quad form (kOE): a lane tests 4 consecutive pairs of one row (pairs 4u .. 4u+3), reading the 7 E words of row y
-        // and the 5 of rows y-3 / y+3 with 16/8-byte LDS reads (9 reads per 4 pairs instead of 32) and forming the O
-        // words by v_alignbit.  Per (iteration, wave) the survivor-pair count goes to LDS (3 ballots of the per-lane
-        // counts 0..4), wave 0 scans them, and the placement pass keeps pair order (lane-major within a wave, then its
-        // pairs).  With minTh < iniTh the pre-test runs at iniTh first (half the survivors to score on textured
-        // cells); the cells left without an iniTh corner are re-tested at minTh after the NMS (step 4b).
-        constexpr bool kQuad = kOE && ORBX_FAST_QUAD;
-        const bool two_pass = kQuad && !ORBX_FAST_ONEPASS && T2 < T1;  // workgroup-uniform
-        const int tA = two_pass ? T1 : tp;
-        const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
-        const int nit = (NQ4 + 255) >> 8;                                    // <= 16 (host: NP <= 8192, Hd <= 66)
-        const int rq0 = tid / QR, u0 = tid - rq0 * QR;
-        const int dq = 256 / QR, du = 256 - dq * QR;
-        uint64_t sm = 0;                                                     // 4 bits (surviving pairs) per iteration
-        // pre-test of quad (rr, u) at threshold t: bit k = pair 4u+k has a pixel with compass value > t
-        auto quad_test = [&](int rr, int u, int t, bool init_scores) -> uint32_t {
-            const uint32_t* e0 = E + rr * kPairStride + 4 * u;               // row y-3 (16-byte aligned)
-            const uint32_t* e1 = e0 + 3 * kPairStride;                       // row y
-            const uint32_t* e2 = e0 + 6 * kPairStride;                       // row y+3
-            uint32_t A[7], U[6], D[6];
-            {
-                const uint4 a = *reinterpret_cast<const uint4*>(e1);
-                const uint2 b = *reinterpret_cast<const uint2*>(e1 + 4);
-                A[0] = a.x; A[1] = a.y; A[2] = a.z; A[3] = a.w; A[4] = b.x; A[5] = b.y; A[6] = e1[6];
-                const uint2 u23 = *reinterpret_cast<const uint2*>(e0 + 2), u45 = *reinterpret_cast<const uint2*>(e0 + 4);
-                U[0] = 0; U[1] = e0[1]; U[2] = u23.x; U[3] = u23.y; U[4] = u45.x; U[5] = u45.y;
-                const uint2 d23 = *reinterpret_cast<const uint2*>(e2 + 2), d45 = *reinterpret_cast<const uint2*>(e2 + 4);
-                D[0] = 0; D[1] = e2[1]; D[2] = d23.x; D[3] = d23.y; D[4] = d45.x; D[5] = d45.y;
-            }
-            int16_t* srow = sc + (rr + 1) * SW + 2 + 8 * u;
-            uint32_t mq = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int j = 4 * u + k;
-                const s16x2 v = as_s2(align16(A[k + 2], A[k + 1]));             // O[y][j+1]: pixels of pair j
-                const s16x2 d0 = v - as_s2(align16(D[k + 2], D[k + 1]));        // ( 0,  3)
-                const s16x2 d4 = v - as_s2(A[k + 3]);                           // ( 3,  0)
-                const s16x2 d8 = v - as_s2(align16(U[k + 2], U[k + 1]));        // ( 0, -3)
-                const s16x2 d12 = v - as_s2(A[k]);                              // (-3,  0)
-                const s16x2 dk = pmax(pmax(pmin(d0, d4), pmin(d4, d8)), pmax(pmin(d8, d12), pmin(d12, d0)));
-                const s16x2 br = pmin(pmin(pmax(d0, d4), pmax(d4, d8)), pmin(pmax(d8, d12), pmax(d12, d0)));
-                const s16x2 m = pmax(dk, (s16x2)(0) - br);
-                const bool two = 2 * j + 1 < Wd;
-                const int pm = j < PR ? (two ? 3 : 1) : 0;
-                const int pt = ((m.x > t ? 1 : 0) | (m.y > t ? 2 : 0)) & pm;
-                mq |= (pt != 0 ? 1u : 0u) << k;
-                if (init_scores && j < PR) *reinterpret_cast<s16x2*>(srow + 2 * k) = (s16x2){0, (short)(two ? 0 : -1)};
-            }
-            return mq;
-        };
-        if constexpr (kQuad) {
-            int* cnt_t = reinterpret_cast<int*>(lds + lay.o_bm);             // [it][wave] survivor pairs
-            for (int it = 0, rr = rq0, u = u0; it < nit; ++it) {
-                const uint32_t mq = rr < Hd ? quad_test(rr, u, tA, true) : 0u;
-                const int c = __builtin_popcount(mq);
-                const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
-                if (ln == 0) cnt_t[it * 4 + w] = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-                sm |= (uint64_t)mq << (4 * it);
-                rr += dq; u += du;
-                if (u >= QR) { u -= QR; ++rr; }
-            }
-            __syncthreads();
-            if (w == 0) {
-                const int e0 = 2 * ln, e1 = 2 * ln + 1, ne = 4 * nit;
-                const int c0 = e0 < ne ? cnt_t[e0] : 0, c1 = e1 < ne ? cnt_t[e1] : 0;
-                const int inc = wave_incl_scan(c0 + c1);
-                if (e0 < ne) bbase[e0] = inc - c0 - c1;
-                if (e1 < ne) bbase[e1] = inc - c1;
-                if (ln == kWave - 1) counters[0] = inc;
-            }
-            __syncthreads();
-            for (int it = 0, rr = rq0, u = u0; it < nit; ++it) {
-                const uint32_t mq = (uint32_t)(sm >> (4 * it)) & 15u;
-                const int c = __builtin_popcount(mq);
-                const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
-                int pos = bbase[it * 4 + w] + __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if ((mq >> k) & 1u) list[pos++] = (uint16_t)((rr << 8) | (4 * u + k));
-                rr += dq; u += du;
-                if (u >= QR) { u -= QR; ++rr; }
-            }
-        } else {
-            const int NP = Hd * PR;
-            const int rr0 = tid / PR, j0 = tid - rr0 * PR;
-            const int dqp = 256 / PR, dj = 256 - dqp * PR;
-            uint64_t* bmt = reinterpret_cast<uint64_t*>(lds + lay.o_bm);          // [it][wave]
-            const int nitp = (NP + 255) >> 8;
-            uint32_t smp = 0;
-            for (int q = tid, it = 0, rr = rr0, j = j0; it < nitp; q += 256, ++it) {
-                int pt = 0;
-                if (q < NP) {
-                    const bool two = 2 * j + 1 < Wd;
-                    pt = fast_pretest2<kPairStride, kOE>(E, O, rr + 3, j, tp) & (two ? 3 : 1);
-                    *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (s16x2){0, (short)(two ? 0 : -1)};
-                }
-                const uint64_t bm = __ballot(pt != 0);
-                if (ln == 0) bmt[it * 4 + w] = bm;
-                smp |= (pt ? 1u : 0u) << it;
-                rr += dqp; j += dj;
-                if (j >= PR) { j -= PR; ++rr; }
-            }
-            __syncthreads();
-            if (w == 0) {   // exclusive prefix over (iteration, wave) of the survivor counts: 2 entries per lane
-                const int e0 = 2 * ln, e1 = 2 * ln + 1, ne = 4 * nitp;
-                const int c0 = e0 < ne ? __popcll(bmt[e0]) : 0, c1 = e1 < ne ? __popcll(bmt[e1]) : 0;
-                const int inc = wave_incl_scan(c0 + c1);
-                if (e0 < ne) bbase[e0] = inc - c0 - c1;
-                if (e1 < ne) bbase[e1] = inc - c1;
-                if (ln == kWave - 1) counters[0] = inc;
-            }
-            __syncthreads();
-            for (int it = 0, rr = rr0, j = j0; it < nitp; ++it) {   // (it < 32: no shift by >= 32)
-                if ((smp >> it) & 1) list[bbase[it * 4 + w] + __popcll(bmt[it * 4 + w] & below)] = (uint16_t)((rr << 8) | j);
-                rr += dqp; j += dj;
-                if (j >= PR) { j -= PR; ++rr; }
-            }
-        }
-        const int ns = counters[0];
-        __syncthreads();
-        FBP(2);
-        FAST_STOP(2);
-        // 3. closed-form scores of the survivors
-        for (int i = tid; i < ns; i += 256) {
-            const int rr = list[i] >> 8, j = list[i] & 0xff;
-            const s16x2 s2 = (kOE && ORBX_FAST_F16) ? fast_score2_f16<kPairStride>(E, rr + 3, j)
-                                                    : fast_score2<kPairStride, kOE>(E, O, rr + 3, j);
-            *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
-        }
-        __syncthreads();
-        FBP(3);
-        FAST_STOP(3);
-        // 4. masked NMS at iniTh and minTh; kept pixels appended to their cell's lists (key = row * 128 + column in
-        //    the cell's window: row-major order)
-        for (int i = tid; i < ns; i += 256) {
-            const int rr = list[i] >> 8, j = list[i] & 0xff;
-            const int x = 2 * j;
-            const uint32_t m01 = *reinterpret_cast<const uint16_t*>(cidx + x);   // columns x, x + 1
-            const uint32_t m2 = cidx[x + 2];
-            const bool bx = m01 & 0x80, bx1 = m01 & 0x8000, bx2 = m2 & 0x80;
-            const uint32_t keep1 = (bx ? 0u : 0xffffu) | (bx1 ? 0u : 0xffff0000u);
-            const uint32_t keep3 = (bx1 ? 0u : 0xffffu) | (bx2 ? 0u : 0xffff0000u);
-            const int f = nms_pair_band(sc, SW, rr, j, T1, T2, x + 1 < Wd, keep1, keep3) & (two_pass ? 3 : 15);
-            if (f) {
-                const int c0 = m01 & 0x7f, c1 = (m01 >> 8) & 0x7f;
-#pragma unroll
-                for (int bit = 0; bit < 4; ++bit) {
-                    if (!((f >> bit) & 1)) continue;
-                    const int px = x + (bit & 1), cc = (bit & 1) ? c1 : c0, t = bit >> 1;
-                    const int pos = atomicAdd(&counters[1 + 2 * cc + t], 1);
-                    if (pos < kmax) keys[(2 * cc + t) * kmax + pos] = (uint16_t)(rr * 128 + (px - cc * wc));
-                }
-            }
-        }
-        __syncthreads();
-        if (two_pass) {
-            // 4b. cells without an iniTh corner (:812-816): pre-test at minTh the pairs touching them that did not pass at
-            //     iniTh (appended to the list), score those, then NMS at minTh over both lists for the pixels of these
-            //     cells.  Pixels of these cells passing at minTh are all scored now; neighbours in other cells are
-            //     masked, so the minTh keys are those of the one-pass form.
-            uint32_t fb = 0;
-            for (int cc = 0; cc < nc; ++cc) fb |= (counters[1 + 2 * cc] == 0 ? 1u : 0u) << cc;
-            if (fb) {
-                auto in_fb = [&](int x) { return (fb >> (cidx[x] & 0x7f)) & 1u; };
-                for (int it = 0, rr = rq0, u = u0; it < nit; ++it) {
-                    if (rr < Hd && (in_fb(8 * u) | in_fb(min(8 * u + 7, Wd - 1)))) {
-                        uint32_t mq = quad_test(rr, u, T2, false) & ~(uint32_t)(sm >> (4 * it)) & 15u;
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const int x = 8 * u + 2 * k;
-                            if (((mq >> k) & 1u) && !(in_fb(x) | (x + 1 < Wd ? in_fb(x + 1) : 0u))) mq &= ~(1u << k);
-                        }
-                        if (mq) {
-                            int pos = ns + atomicAdd(&counters[20], __builtin_popcount(mq));
-#pragma unroll
-                            for (int k = 0; k < 4; ++k)
-                                if ((mq >> k) & 1u) list[pos++] = (uint16_t)((rr << 8) | (4 * u + k));
-                        }
-                    }
-                    rr += dq; u += du;
-                    if (u >= QR) { u -= QR; ++rr; }
-                }
-                __syncthreads();
-                const int ns2 = counters[20];
-                for (int i = ns + tid; i < ns + ns2; i += 256) {
-                    const int rr = list[i] >> 8, j = list[i] & 0xff;
-                    const s16x2 s2 = (kOE && ORBX_FAST_F16) ? fast_score2_f16<kPairStride>(E, rr + 3, j)
-                                                    : fast_score2<kPairStride, kOE>(E, O, rr + 3, j);
-                    *(s16x2*)(sc + (rr + 1) * SW + 2 + 2 * j) = (2 * j + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
-                }
-                __syncthreads();
-                for (int i = tid; i < ns + ns2; i += 256) {
-                    const int rr = list[i] >> 8, j = list[i] & 0xff;
-                    const int x = 2 * j;
-                    const uint32_t m01 = *reinterpret_cast<const uint16_t*>(cidx + x);
-                    const uint32_t m2 = cidx[x + 2];
-                    const int c0 = m01 & 0x7f, c1 = (m01 >> 8) & 0x7f;
-                    if (!(((fb >> c0) & 1u) | (x + 1 < Wd ? (fb >> c1) & 1u : 0u))) continue;
-                    const bool bx = m01 & 0x80, bx1 = m01 & 0x8000, bx2 = m2 & 0x80;
-                    const uint32_t keep1 = (bx ? 0u : 0xffffu) | (bx1 ? 0u : 0xffff0000u);
-                    const uint32_t keep3 = (bx1 ? 0u : 0xffffu) | (bx2 ? 0u : 0xffff0000u);
-                    const int f = nms_pair_band(sc, SW, rr, j, T1, T2, x + 1 < Wd, keep1, keep3) >> 2;
-#pragma unroll
-                    for (int bit = 0; bit < 2; ++bit) {
-                        if (!((f >> bit) & 1)) continue;
-                        const int px = x + bit, cc = bit ? c1 : c0;
-                        if (!((fb >> cc) & 1u)) continue;
-                        const int pos = atomicAdd(&counters[1 + 2 * cc + 1], 1);
-                        if (pos < kmax) keys[(2 * cc + 1) * kmax + pos] = (uint16_t)(rr * 128 + (px - cc * wc));
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        FBP(4);
-        FAST_STOP(4);
-#ifdef ORBX_QT_PROF
-        if (tid == 0 && item == 8 * 37 + 3) { g_fbprof[band0 ? 1 : 0][8] = ns; g_fbprof[band0 ? 1 : 0][9] = Hd * PR; }
-#endif
-    }
-    // 5. per cell: iniTh keys, or minTh keys when the cell has none (:812-816); slot = rank in row-major order.
-    //    The keys of all the band's cells are ranked in one pass (thread -> (cell, key)).
-    // (chosen list of cell c: t = 0 iniTh when it kept any, else 1; its size from the LDS counters)
-    auto chosen = [&](int cc, int& t) {
-        t = counters[1 + 2 * cc] > 0 ? 0 : 1;
-        return min(counters[1 + 2 * cc + t], kmax);
-    };
-    int tot = 0;
-    if (live)
-        for (int cc = 0; cc < nc; ++cc) { int t; tot += chosen(cc, t); }
-    for (int g = tid; g < tot; g += 256) {
-        int cc = 0, i = g, t, nk;
-        while (i >= (nk = chosen(cc, t))) { i -= nk; ++cc; }
-        const uint16_t* ks = keys + (2 * cc + t) * kmax;
-        const CellDev cd = cells[bd.cell0 + cc];
-        const int k = ks[i];
-        int rank = 0;
-        for (int m = 0; m < nk; ++m) rank += ks[m] < k;
-        if (rank < cd.slot_cap) {
-            const int rr = k >> 7, xl = k & 127;
-            const size_t o = (size_t)img * cand_stride + cd.slot_off + rank;
-            cand_xy[o] = (uint32_t)(cd.x0 + 3 + xl) | ((uint32_t)(cd.y0 + rr + 3) << 16);
-            cand_s[o] = (uint8_t)sc[(rr + 1) * SW + 2 + cc * wc + xl];
-        }
-    }
-    if (tid < nc) {
-        int t;
-        const int cnt = live ? min(chosen(tid, t), cells[bd.cell0 + tid].slot_cap) : 0;
-        cell_cnt[(size_t)img * ncells + bd.cell0 + tid] = cnt;
-    }
-    FBP(5);
-}
-
 // ---------------------------------------------------------------------------------------------
 // k_fast_wave: one WAVE per (image, cell) -- ComputeKeyPointsOctTree's per-cell FAST (:789-829) with no workgroup
 // barrier.  OpenCV's FAST runs on the cell ROI, so a cell is self-contained: its ROI (detection window + 3) goes into the
-// wave's own LDS slice as the f16-biased pair image of k_fast_band, the compass pre-test runs in quads (4 pixel pairs per
+// wave's own LDS slice as the f16-biased pair image, the compass pre-test runs in quads (4 pixel pairs per
 // lane), the survivors are compacted in row-major order by wave ballots (no atomics), scored in closed form, and the
 // strict 3x3 NMS at iniThFAST and minThFAST appends the kept pixels to two key lists by ballot rank -- so the lists are
 // already in OpenCV's row-major output order and a kept pixel's slot is its list index (no rank pass).  The cell's
@@ -1145,7 +405,8 @@ __host__ __device__ __forceinline__ WaveLds wave_lds(int rows, int sw, int np, i
 }
 
 // Compass pre-test of quad (rr, u) of a cell (pairs 4u .. 4u+3 of detection row rr) at threshold t; also writes the
-// quad's score-map words (0, or -1 for the missing second pixel of an odd-width row).  As k_fast_band's quad_test.
+// quad's score-map words (0, or -1 for the missing second pixel of an odd-width row).  A lane reads the 7 E words of
+// row y and the 5 of rows y-3 / y+3 of its 4 pixel pairs with 16 / 8-byte LDS reads (9 reads per 4 pairs, not 32).
 struct QuadTaps { uint32_t A[7], U[6], D[6]; };   // E words of rows y (7), y-3 and y+3 (5 each) of one quad
 
 template <int kPS>
@@ -1426,360 +687,6 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
     fastw_body<kPS>(E, sc, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
 }
 
-// k_fast_wave_p: k_fast_wave with each wave walking kCells consecutive (image, cell) items, the next cell's ROI loaded into
-// registers (its cell record first, a scalar load) while the current cell is processed, so the dependent chain cell
-// record -> level record -> ROI rows of a wave's start is paid once per kCells cells.  Pair stride 24 (16-byte chunks,
-// ROI <= 48 x 72: <= 4 load rounds of 64 lanes).
-constexpr int kRoiPf = 4;
-struct FastwRoi { uint32_t v[4 * kRoiPf]; int rs[kRoiPf], cs[kRoiPf]; int nq; };
-
-__device__ __forceinline__ void fastw_roi_issue(FastwRoi& R, const uint8_t* __restrict__ src0, int lstride, int W, int H,
-                                                int ln) {
-    const int cpr = (W + 15) >> 4;
-    R.nq = H * cpr;
-    const int dr = kWave / cpr, dc = kWave - dr * cpr;
-    int r = ln / cpr, cc = ln - r * cpr;
-#pragma unroll
-    for (int k = 0; k < kRoiPf; ++k) {
-        R.rs[k] = r; R.cs[k] = cc;
-        r += dr; cc += dc;
-        if (cc >= cpr) { cc -= cpr; ++r; }
-        if (ln + k * kWave < R.nq) __builtin_memcpy(&R.v[4 * k], src0 + (size_t)R.rs[k] * lstride + 16 * R.cs[k], 16);
-    }
-}
-
-template <int kPS>
-__device__ __forceinline__ void fastw_roi_store(const FastwRoi& R, uint32_t* __restrict__ E, int ln) {
-#pragma unroll
-    for (int k = 0; k < kRoiPf; ++k) {
-        if (ln + k * kWave < R.nq) {
-            const uint32_t x = R.v[4 * k], y = R.v[4 * k + 1], z = R.v[4 * k + 2], w = R.v[4 * k + 3];
-            uint4* dst = reinterpret_cast<uint4*>(E + R.rs[k] * kPS + 8 * R.cs[k]);
-            dst[0] = make_uint4(__builtin_amdgcn_perm(y, x, 0x0c010c00u) | 0x64006400u, __builtin_amdgcn_perm(y, x, 0x0c030c02u) | 0x64006400u,
-                                __builtin_amdgcn_perm(y, x, 0x0c050c04u) | 0x64006400u, __builtin_amdgcn_perm(y, x, 0x0c070c06u) | 0x64006400u);
-            dst[1] = make_uint4(__builtin_amdgcn_perm(w, z, 0x0c010c00u) | 0x64006400u, __builtin_amdgcn_perm(w, z, 0x0c030c02u) | 0x64006400u,
-                                __builtin_amdgcn_perm(w, z, 0x0c050c04u) | 0x64006400u, __builtin_amdgcn_perm(w, z, 0x0c070c06u) | 0x64006400u);
-        }
-    }
-}
-
-template <int kWpg, int kCells>
-__global__ __launch_bounds__(64 * kWpg) void k_fast_wave_p(const uint8_t* __restrict__ pyr, size_t pyr_stride,
-                                                           const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
-                                                           int cell0, int ncell, int iniTh, int minTh,
-                                                           uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
-                                                           int cand_stride, int* __restrict__ cell_cnt, int ncells, int batch,
-                                                           Src0 s0, WaveLds lay, int kcap, int two_pass) {
-    constexpr int kPS = 24, SW = fastw_sw(kPS);
-    extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
-    const int w = threadIdx.x >> 6, ln = lane_id();
-    const int total = ncell * batch, nwv = (total + kCells - 1) / kCells, nwg = (nwv + kWpg - 1) / kWpg;
-    const int wg = xcd_item(xcd_chunk(nwg));                        // consecutive cells of one image on one XCD
-    const int wv = __builtin_amdgcn_readfirstlane(wg * kWpg + w);
-    if (wg >= nwg || wv >= nwv) return;                             // whole wave (no barrier in this kernel)
-    const int first = wv * kCells, last = min(first + kCells, total);
-    char* lds = reinterpret_cast<char*>(fsm) + w * lay.bytes;
-    uint32_t* E = reinterpret_cast<uint32_t*>(lds);
-    int16_t* sc = reinterpret_cast<int16_t*>(lds + lay.o_sc);
-    uint16_t* list = reinterpret_cast<uint16_t*>(lds + lay.o_list);
-    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
-    const int tp = min(T1, T2);
-    FastwRoi R;
-    auto prep = [&](int item, CellDev& cd, int& img, int& c) {   // the item's cell record, then its ROI loads
-        img = item / ncell;
-        c = cell0 + (item - img * ncell);
-        cd = cells[c];
-        if (cd.W > 6 && cd.H > 6) {
-            const LevelDev& L = levels[cd.level];
-            int lstride;
-            const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
-            fastw_roi_issue(R, base + (size_t)cd.y0 * lstride + cd.x0, lstride, cd.W, cd.H, ln);
-        }
-    };
-    CellDev cd;
-    int img, c;
-    prep(first, cd, img, c);
-    for (int item = first; item < last; ++item) {
-        const int Wd = cd.W - 6, Hd = cd.H - 6;
-        int* cnt_out = cell_cnt + (size_t)img * ncells + c;
-        const bool live = Wd > 0 && Hd > 0;
-        wave_fence();                                                // the previous cell's LDS reads before these writes
-        if (live) {
-            fastw_roi_store<kPS>(R, E, ln);
-            const int n16 = ((Hd + 2) * SW * 2 + 15) >> 4;
-            for (int i = ln; i < n16; i += kWave) reinterpret_cast<uint4*>(sc)[i] = make_uint4(0, 0, 0, 0);
-        }
-        CellDev cdn = cd;
-        int imgn = img, cn = c;
-        if (item + 1 < last) prep(item + 1, cdn, imgn, cn);          // next ROI in flight during this cell
-        if (live)
-            fastw_body<kPS>(E, sc, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
-        else if (ln == 0)
-            *cnt_out = 0;
-        cd = cdn; img = imgn; c = cn;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// k_fast_rows: FAST-9 scores, cell-masked strict 3x3 NMS at iniThFAST and minThFAST, and row-major candidate slots for
-// one cell row of up to 8 cells (<= 248 detection columns) per WAVE, with the image held in registers.
-//
-// Lane l owns the 4 level columns X .. X+3, X = first detection column - 4 + 4l (lanes 0 and 63 are the +-3 halo;
-// ComputeKeyPointsOctTree's cell ROI is the detection window + 3, :789-806).  The wave walks the group's ROI rows
-// once, top to bottom.  Each row is one 4-byte load per lane; its left / right neighbours' bytes come by DPP
-// (wave_shr / wave_shl), and the row is kept as f16-biased pixel pairs (1024 + value: exact differences, gfx950's
-// packed 3-input f16 min / max, as k_fast_band) -- even starts E(-2,0,2,4) and odd starts O(-3,-1,1,3,5) relative to X
-// -- in a ring of 7 rows (the FAST circle spans rows y-3 .. y+3; the ring index is static in the 7-way unrolled loop).
-// Every pixel of the window is scored (OpenCV's cornerScore in closed form, the same arithmetic as fast_score2_f16):
-// no pre-test, no survivor list, no LDS image and no barrier -- the scores of a whole cell row cost less than the
-// compaction they used to avoid.  NMS of row y runs once row y+1 is scored (neighbour columns across lanes by DPP,
-// columns of another cell masked: OpenCV's FAST runs on the cell ROI, :809-816); the kept pixels of both thresholds
-// are ranked in row-major order per cell (wave ballots + a per-cell row base in LDS) and written to the cell's two
-// candidate lists (iniTh -> cand, minTh -> cand2).  The cell's count word says which list DistributeOctTree uses:
-// the iniTh list, or the minTh list when the cell kept nothing at iniTh (:812-816) -- bit 30 set.
-// ---------------------------------------------------------------------------------------------
-constexpr int kCntMinList = 1 << 30;   // cell count word: the cell's candidates are its minTh list (cand2)
-
-__device__ __forceinline__ uint32_t dpp_from_left(uint32_t v) {    // lane l <- lane l-1 (lane 0 <- 0)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
-}
-__device__ __forceinline__ uint32_t dpp_from_right(uint32_t v) {   // lane l <- lane l+1 (lane 63 <- 0)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
-}
-
-// cornerScore of the pixel pair whose 16 circle taps are t[0..15] (circle order of fast_score2) and centre v, all
-// f16-biased pairs; result i16 pair, -1 for "not a corner at any threshold >= 1"
-__device__ __forceinline__ s16x2 fast_score_taps_f16(const uint32_t (&t)[16], uint32_t vc) {
-    const h16x2 v = as_h2(vc);
-    h16x2 d[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) d[k] = v - as_h2(t[k]);
-    h16x2 a2[8], b2[8], a4[8], b4[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) { a2[m] = hmin(d[2 * m + 1], d[(2 * m + 2) & 15]); b2[m] = hmax(d[2 * m + 1], d[(2 * m + 2) & 15]); }
-#pragma unroll
-    for (int m = 0; m < 8; ++m) { a4[m] = hmin(a2[m], a2[(m + 1) & 7]); b4[m] = hmax(b2[m], b2[(m + 1) & 7]); }
-    h16x2 dk[8], br[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        const h16x2 e0 = d[2 * m], e9 = d[(2 * m + 9) & 15];
-        dk[m] = hmin3(a4[m], a4[(m + 2) & 7], hmax(e0, e9));
-        br[m] = hmax3(b4[m], b4[(m + 2) & 7], hmin(e0, e9));
-    }
-    const h16x2 dmax = hmax3(hmax3(dk[0], dk[1], dk[2]), hmax3(dk[3], dk[4], dk[5]), hmax(dk[6], dk[7]));
-    const h16x2 bmin = hmin3(hmin3(br[0], br[1], br[2]), hmin3(br[3], br[4], br[5]), hmin(br[6], br[7]));
-    const h16x2 zero = {(_Float16)0, (_Float16)0}, bias = {(_Float16)1024, (_Float16)1024};
-    const h16x2 m = hmax3(dmax, -bmin, zero) + bias;
-    return as_s2(__builtin_bit_cast(uint32_t, m)) - (s16x2){0x6401, 0x6401};
-}
-
-struct FastRowSc {            // one scored row, as the NMS reads it: (x,x+1), (x+2,x+3), (x-1,x), (x+1,x+2), (x+3,x+4)
-    uint32_t s0, s1, l0, mid, r1;
-};
-
-__device__ __forceinline__ uint32_t pmax_u(uint32_t a, uint32_t b) {
-    return __builtin_bit_cast(uint32_t, pmax(as_s2(a), as_s2(b)));
-}
-
-template <int kDummy>
-__global__ __launch_bounds__(256) void k_fast_rows(const uint8_t* __restrict__ pyr, size_t pyr_stride,
-                                                   const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
-                                                   const BandDev* __restrict__ groups, int g0, int ngroup, int iniTh,
-                                                   int minTh, uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
-                                                   uint32_t* __restrict__ cand2_xy, uint8_t* __restrict__ cand2_s,
-                                                   int cand_stride, int* __restrict__ cell_cnt, int ncells, int batch, Src0 s0) {
-    const int wv = threadIdx.x >> 6, ln = lane_id();
-    const int nitems = ngroup * batch;
-    const int item = xcd_item(xcd_chunk((nitems + 3) / 4)) * 4 + wv;
-    if (item >= nitems) return;                                   // whole wave (no block barriers below)
-    const int img = item / ngroup;
-    const BandDev g = groups[g0 + (item - img * ngroup)];
-    const int nc = g.ncell, wc = g.wcell;
-    const int DW = g.W - 6, H = g.H;
-    const int D0 = g.x0 + 3;                                      // first detection column
-    if (DW <= 0 || H - 6 <= 0) {                                  // no detection window: empty cells
-        if (ln < nc) cell_cnt[(size_t)img * ncells + g.cell0 + ln] = 0;
-        return;
-    }
-    const LevelDev L = levels[g.level];
-    int lstride;
-    const uint8_t* base = level_pixels(pyr, pyr_stride, L, g.level, img, s0, lstride);
-    const int X = D0 - 4 + 4 * ln;                                // this lane's first column
-    const bool ld_ok = X + 3 < L.w;
-    const uint8_t* src = base + (size_t)g.y0 * lstride + X;
-    const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
-    const uint32_t t1p = (uint32_t)(T1 & 0xffff) * 0x10001u, t2p = (uint32_t)(T2 & 0xffff) * 0x10001u;
-    // per pixel k of the lane: detection column?  cell index, left / right neighbour in the same cell?
-    uint32_t det_mask[2], mL[2], mR[2];                           // 0xffff halves = "force -1"
-    int cidx[4];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) { det_mask[j] = 0; mL[j] = 0; mR[j] = 0; }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int rel = X + k - D0;
-        const bool det = rel >= 0 && rel < DW;
-        const int c = det ? min(rel / wc, nc - 1) : 0;
-        cidx[k] = c;
-        const bool lin = det && rel % wc != 0;                    // column x-1 in the same cell's window
-        const bool rin = det && rel + 1 < DW && (rel + 1) % wc != 0;
-        const uint32_t half = 0xffffu << (16 * (k & 1));
-        if (!det) det_mask[k >> 1] |= half;
-        if (!lin) mL[k >> 1] |= half;
-        if (!rin) mR[k >> 1] |= half;
-    }
-    // The lane's pixels lie in at most two cells: ca = the cell of its first pixel and ca + 1 (every cell but a row's
-    // last is wCell >= 30 columns wide).  A cell's row base (kept pixels of the row before its first column) is published by the lane holding
-    // that column (my_off = its offset in the lane) and fetched by ds_bpermute; each lane tracks the running kept
-    // counts of ca and ca + 1 itself (every lane of a cell computes the same numbers), so ranking needs no LDS.
-    const int ca = cidx[0] < nc ? cidx[0] : 0;
-    int my_off = -1;                                              // offset of a cell's first column in this lane
-#pragma unroll
-    for (int k = 3; k >= 0; --k) {
-        const int rel = X + k - D0;
-        if (rel >= 0 && rel < DW && rel % wc == 0) my_off = k;
-    }
-    auto start_lane = [&](int c) { return 1 + (c * wc) / 4; };   // lane holding cell c's first column
-    const bool hasB = ca + 1 < nc, hasC = ca + 2 < nc;
-    const int addrA = 4 * start_lane(ca), addrB = 4 * start_lane(hasB ? ca + 1 : ca), addrC = 4 * start_lane(hasC ? ca + 2 : ca);
-    const CellDev cellA = cells[g.cell0 + ca], cellB = cells[g.cell0 + (hasB ? ca + 1 : ca)];
-    int cntA[2] = {0, 0}, cntB[2] = {0, 0};                      // kept pixels of cells ca / ca + 1 in earlier rows
-    const uint64_t below = (1ull << ln) - 1ull;
-    uint32_t* cxy[2] = {cand_xy + (size_t)img * cand_stride, cand2_xy + (size_t)img * cand_stride};
-    uint8_t* cs[2] = {cand_s + (size_t)img * cand_stride, cand2_s + (size_t)img * cand_stride};
-
-    // rank and store the kept pixels of one row (bits k of kb[t]: pixel X + k kept at threshold t)
-    auto emit = [&](int row, const int (&kb)[2], uint32_t sc0, uint32_t sc1) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int n = __builtin_popcount(kb[t]);
-            const uint64_t b0 = __ballot(n & 1), b1 = __ballot(n & 2), b2 = __ballot(n & 4);
-            const int tot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-            if (tot == 0) continue;                              // wave-uniform
-            const int pre = __popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below);
-            const int pub = pre + __builtin_popcount(kb[t] & ((1u << (my_off & 3)) - 1u));   // row base if a cell starts here
-            // every lane takes part in every bpermute (a source lane must be active), then selects
-            const int rbA = __builtin_amdgcn_ds_bpermute(addrA, pub);
-            const int pB = __builtin_amdgcn_ds_bpermute(addrB, pub);
-            const int pC = __builtin_amdgcn_ds_bpermute(addrC, pub);
-            const int rbB = hasB ? pB : tot, rbC = hasC ? pC : tot;
-            int m = kb[t];
-            while (m) {
-                const int k = __builtin_ctz(m);
-                m &= m - 1;
-                const bool inA = cidx[k] == ca;
-                const int q = pre + __builtin_popcount(kb[t] & ((1u << k) - 1u));
-                const int rank = inA ? cntA[t] + q - rbA : cntB[t] + q - rbB;
-                const CellDev& cd = inA ? cellA : cellB;
-                if (rank < cd.slot_cap) {
-                    const size_t o = (size_t)cd.slot_off + rank;
-                    cxy[t][o] = (uint32_t)(X + k) | ((uint32_t)(g.y0 + row) << 16);
-                    const uint32_t sw = (k >> 1) ? sc1 : sc0;
-                    cs[t][o] = (uint8_t)(sw >> (16 * (k & 1)));
-                }
-            }
-            cntA[t] += rbB - rbA;
-            cntB[t] += rbC - rbB;
-        }
-    };
-    [[maybe_unused]] int dbg_acc = 0;
-    // strict 3x3 NMS of row c (scores of rows c-1, c, c+1) at both thresholds
-    auto nms = [&](int row, const FastRowSc& U, const FastRowSc& C, const FastRowSc& D) {
-        const uint32_t lm0 = pmax_u(pmax_u(U.l0, C.l0), D.l0) | mL[0];
-        const uint32_t mm = pmax_u(pmax_u(U.mid, C.mid), D.mid);
-        const uint32_t rm1 = pmax_u(pmax_u(U.r1, C.r1), D.r1) | mR[1];
-        const uint32_t m0 = pmax_u(pmax_u(lm0, pmax_u(U.s0, D.s0)), mm | mR[0]);
-        const uint32_t m1 = pmax_u(pmax_u(mm | mL[1], pmax_u(U.s1, D.s1)), rm1);
-        // kept at t: s > m (m - s < 0) and s >= T (s - T >= 0): sign bits
-        const uint32_t g0 = __builtin_bit_cast(uint32_t, as_s2(m0) - as_s2(C.s0));
-        const uint32_t g1 = __builtin_bit_cast(uint32_t, as_s2(m1) - as_s2(C.s1));
-        int kb[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const uint32_t tp = t ? t2p : t1p;
-            const uint32_t a0 = g0 & ~__builtin_bit_cast(uint32_t, as_s2(C.s0) - as_s2(tp));
-            const uint32_t a1 = g1 & ~__builtin_bit_cast(uint32_t, as_s2(C.s1) - as_s2(tp));
-            kb[t] = (int)(((a0 >> 15) & 1u) | ((a0 >> 30) & 2u) | ((a1 >> 13) & 4u) | ((a1 >> 28) & 8u));
-        }
-        if (__ballot((kb[0] | kb[1]) != 0) == 0) return;         // wave-uniform
-#ifdef ORBX_ROWS_NOEMIT
-        dbg_acc += kb[0] * 3 + kb[1] + row;                       // diagnostics: scores and NMS only (kept observable)
-#else
-        emit(row, kb, C.s0, C.s1);
-#endif
-    };
-
-    const uint32_t K64 = 0x64646464u;
-    uint32_t E[7][4], O[7][5], raw[7];
-#ifndef ORBX_ROWS_PF
-#define ORBX_ROWS_PF 3
-#endif
-    constexpr int kPf = ORBX_ROWS_PF;                             // rows loaded ahead (<= 6)
-#pragma unroll
-    for (int p = 0; p < kPf; ++p) raw[p] = (p < H && ld_ok) ? *reinterpret_cast<const uint32_t*>(src + (size_t)p * lstride) : 0u;
-    const FastRowSc none{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-    FastRowSc sa = none, sb = none;                               // scores of rows r-5, r-4 (the NMS window)
-    for (int r0 = 0; r0 < H; r0 += 7) {
-#pragma unroll
-        for (int p = 0; p < 7; ++p) {
-            const int r = r0 + p;
-            if (r >= H) break;                                    // wave-uniform
-            if (r + kPf < H) raw[(p + kPf) % 7] = ld_ok ? *reinterpret_cast<const uint32_t*>(src + (size_t)(r + kPf) * lstride) : 0u;
-            // row r -> slot p: E(-2), E(0), E(2), E(4); O(-3), O(-1), O(1), O(3), O(5)
-            const uint32_t C = raw[p], Lw = dpp_from_left(C), Rw = dpp_from_right(C);
-            E[p][0] = __builtin_amdgcn_perm(K64, Lw, 0x04030402u);
-            E[p][1] = __builtin_amdgcn_perm(K64, C, 0x04010400u);
-            E[p][2] = __builtin_amdgcn_perm(K64, C, 0x04030402u);
-            E[p][3] = __builtin_amdgcn_perm(K64, Rw, 0x04010400u);
-            O[p][0] = __builtin_amdgcn_perm(K64, Lw, 0x04020401u);
-            O[p][1] = __builtin_amdgcn_alignbit(E[p][1], E[p][0], 16);
-            O[p][2] = __builtin_amdgcn_perm(K64, C, 0x04020401u);
-            O[p][3] = __builtin_amdgcn_alignbit(E[p][3], E[p][2], 16);
-            O[p][4] = __builtin_amdgcn_perm(K64, Rw, 0x04020401u);
-            if (r < 6) continue;                                  // wave-uniform
-            // score row r-3: circle taps (dx, dy) at rows (p + dy) mod 7 (row r-3+dy), pair start 2j + dx
-            FastRowSc sc;
-            s16x2 sp[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                // tap (dx, dy): start s = 2j + dx in [-3, 5]; even -> E[(s + 2) / 2], odd -> O[(s + 3) / 2]
-#define ORBX_RT(dx, dy) ((((2 * j + (dx)) & 1) != 0) ? O[(p + 4 + (dy)) % 7][(2 * j + (dx) + 3) / 2] \
-                                                   : E[(p + 4 + (dy)) % 7][(2 * j + (dx) + 2) / 2])
-                const uint32_t t[16] = {ORBX_RT(0, 3),  ORBX_RT(1, 3),   ORBX_RT(2, 2),   ORBX_RT(3, 1),
-                                        ORBX_RT(3, 0),  ORBX_RT(3, -1),  ORBX_RT(2, -2),  ORBX_RT(1, -3),
-                                        ORBX_RT(0, -3), ORBX_RT(-1, -3), ORBX_RT(-2, -2), ORBX_RT(-3, -1),
-                                        ORBX_RT(-3, 0), ORBX_RT(-3, 1),  ORBX_RT(-2, 2),  ORBX_RT(-1, 3)};
-                sp[j] = fast_score_taps_f16(t, ORBX_RT(0, 0));
-#undef ORBX_RT
-            }
-            sc.s0 = __builtin_bit_cast(uint32_t, sp[0]) | det_mask[0];
-            sc.s1 = __builtin_bit_cast(uint32_t, sp[1]) | det_mask[1];
-            sc.l0 = __builtin_amdgcn_alignbit(sc.s0, dpp_from_left(sc.s1), 16);
-            sc.mid = __builtin_amdgcn_alignbit(sc.s1, sc.s0, 16);
-            sc.r1 = __builtin_amdgcn_alignbit(dpp_from_right(sc.s0), sc.s1, 16);
-#ifdef ORBX_ROWS_SCOREONLY
-            dbg_acc += (int)(sc.s0 ^ sc.s1 ^ sc.l0 ^ sc.mid ^ sc.r1);
-#else
-            if (r - 3 >= 4) nms(r - 4, sa, sb, sc);
-#endif
-            sa = sb;
-            sb = sc;
-        }
-    }
-    if (H - 4 >= 3) nms(H - 4, sa, sb, none);                     // last detection row: nothing below
-#if defined(ORBX_ROWS_NOEMIT) || defined(ORBX_ROWS_SCOREONLY)
-    if (dbg_acc == 0x7fffffff) cand_s[0] = 1;
-#endif
-    // per cell (written by the lane holding its first column): the iniTh list, or the minTh list when the cell kept
-    // nothing at iniTh
-    if (my_off >= 0) {
-        const bool a = cidx[my_off] == ca;
-        const int ci = a ? cntA[0] : cntB[0], cm = a ? cntA[1] : cntB[1];
-        const int use_min = ci == 0;
-        const int n = min(use_min ? cm : ci, (a ? cellA : cellB).slot_cap);
-        cell_cnt[(size_t)img * ncells + g.cell0 + cidx[my_off]] = n | (use_min && n > 0 ? kCntMinList : 0);
-    }
-}
-
 // GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, integer separable path: taps {18,34,49,55,49,34,18},
 // column pass (acc + 2^15) >> 16 saturated.  Tile 64 x 16 per workgroup; tiles of all levels in one grid.
 struct BlurTile { int level, tx, ty, pad; };
@@ -1790,73 +697,28 @@ __device__ __forceinline__ int refl101(int i, int n) {
     return i;
 }
 
-// Register-streaming form: one wave per (level, 256-column strip, 32-row band).  Lane l owns the 4
-// output columns x0 = strip*256 + 4l .. x0+3, walks down the band's 38 input rows once, and keeps the
-// last 7 rows of horizontal sums in registers (a ring unrolled by 7, so no moves); no LDS, no
-// divisions.  Reflection only at the level borders (scalar for rows, per byte for edge lanes).
-// Per input row a lane issues one 12-byte load (x0-4 .. x0+7; global loads need no alignment on gfx950),
-// builds the 9 byte pairs (b[i], b[i+1]) with v_perm_b32 and forms the horizontal sums of its 4 columns
-// as two packed u16 pairs (v_pk_mad_u16: a row sum is at most 255 * 257 = 65535, exact in u16).  The
-// column pass widens to u32 and the 4 output bytes leave as one dword store.
+// Register-streaming form: one wave per (level, 256-column strip, 16-row band).  Lane l owns the 4
+// output columns x0 = strip*256 + 4l .. x0+3, walks down the band's 22 input rows once, and keeps the
+// last 4 row pairs of horizontal sums in registers (a ring unrolled by 4, so no moves); no LDS, no
+// divisions.  Reflection only at the level borders (scalar for rows, byte selectors for edge lanes).
+// Per input row a lane issues one 12-byte load (x0-4 .. x0+7; global loads need no alignment on gfx950);
+// a horizontal row sum is at most 255 * 257 = 65535, exact in u16.  The 4 output bytes leave as one dword store.
 #ifndef ORBX_BLUR_BAND
 #define ORBX_BLUR_BAND 16     // rows per wave (r2y A/B: 16 ≈ +0.6 % over 32; 8 and 64 slower)
 #endif
-#ifndef ORBX_BLUR_DPP
-#define ORBX_BLUR_DPP 0       // 1: interior strips load one dword per lane and row, neighbours' bytes by DPP (r3l A/B: serial blur 0.476 -> 0.561 ms, slower)
-#endif
-// strip = output columns of one wave: 256 (every lane loads its own 12-byte window), or 248 with the DPP form
-// (lanes 1..62 output, lanes 0 and 63 load the +-4 halo)
-#ifndef ORBX_BLUR_PK
-#define ORBX_BLUR_PK 1          // k_blur7<true> output packing: v_perm + v_pk_min_u16 (0: shift, min, OR per pixel)
-#endif
-#ifndef ORBX_BLUR_SEL
-#define ORBX_BLUR_SEL 1         // edge strips of k_blur7<true>: per-band REFLECT_101 byte selectors (0: per-byte loop)
-#endif
-constexpr int kBlurBand = ORBX_BLUR_BAND, kBlurStrip = ORBX_BLUR_DPP ? 248 : 256;
+constexpr int kBlurBand = ORBX_BLUR_BAND, kBlurStrip = 256;
 
-// byte m of the 12-byte window (w0 | w1 << 32 | w2 << 64) and byte m+1, as u16 lanes (lo = m)
-template <int m>
-__device__ __forceinline__ u16x2 byte_pair(uint32_t w0, uint32_t w1, uint32_t w2) {
-    constexpr int q = m / 4, r = m % 4;
-    const uint32_t lo = q == 0 ? w0 : (q == 1 ? w1 : w2);
-    const uint32_t hi = q == 0 ? w1 : (q == 1 ? w2 : w2);
-    // v_perm_b32: selector byte k picks byte k' of {hi:lo} (0-3 lo, 4-7 hi); 0x0c gives 0
-    constexpr uint32_t sel = 0x0c000c00u | (uint32_t)r | ((uint32_t)(r + 1) << 16);
-    return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, sel));
-}
-
-struct BlurRow { u16x2 h01, h23; };   // horizontal sums of columns x0, x0+1 | x0+2, x0+3
 struct BlurWin { uint32_t w0, w1, w2; };   // 12 input bytes x0-4 .. x0+7 of one row
 
-// Row window loads.  kMode 0: interior lane, one 12-byte load.  kMode 1: a lane within 8 columns of a level edge
-// (level at least 12 wide): one 12-byte load clamped inside the row, then the reflected bytes are picked out of it
-// (every reflected column x0-3 .. x0+6 falls inside the clamped window).  kMode 2: tiny level, per-byte loads.
+// Row window loads.  kMode 0: interior lane, one 12-byte load.  kMode 2: a level under 12 columns, per-byte loads
+// with REFLECT_101 columns.  (A lane within 8 columns of the edge of a wider level uses blur_load_sel below.)
 template <int kMode>
 __device__ __forceinline__ BlurWin blur_load(const uint8_t* __restrict__ row, int x0, int w) {
     BlurWin o;
-    if (kMode == 3) {            // DPP form: every lane active, all loads in bounds (interior strip)
-        uint32_t c;
-        __builtin_memcpy(&c, row + x0, 4);
-        o.w0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x138, 0xF, 0xF, false);   // lane l-1 (wave_shr:1)
-        o.w1 = c;
-        o.w2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x130, 0xF, 0xF, false);   // lane l+1 (wave_shl:1)
-    } else if (kMode == 0) {
+    if (kMode == 0) {
         uint32_t v[3];
         __builtin_memcpy(v, row + x0 - 4, 12);
         o.w0 = v[0]; o.w1 = v[1]; o.w2 = v[2];
-    } else if (kMode == 1) {
-        const int xs = min(max(x0 - 4, 0), w - 12);
-        uint32_t v[3];
-        __builtin_memcpy(v, row + xs, 12);
-        uint32_t r[3] = {0, 0, 0};
-#pragma unroll
-        for (int i = 1; i < 11; ++i) {
-            const int x = x0 - 4 + i;
-            const int k = (x < 0 ? -x : (x >= w ? 2 * w - 2 - x : x)) - xs;     // 0 <= k < 12
-            const uint32_t d = k < 4 ? v[0] : (k < 8 ? v[1] : v[2]);
-            r[i >> 2] |= ((d >> (8 * (k & 3))) & 0xffu) << (8 * (i & 3));
-        }
-        o.w0 = r[0]; o.w1 = r[1]; o.w2 = r[2];
     } else {
         uint32_t v[3] = {0, 0, 0};
 #pragma unroll
@@ -1866,83 +728,12 @@ __device__ __forceinline__ BlurWin blur_load(const uint8_t* __restrict__ row, in
     return o;
 }
 
-__device__ __forceinline__ BlurRow blur_hrow(const BlurWin& v) {
-    const uint32_t w0 = v.w0, w1 = v.w1, w2 = v.w2;
-    // b[i] = pixel x0 - 3 + i = window byte i + 1;  P_i = (b[i], b[i+1])
-    const u16x2 P0 = byte_pair<1>(w0, w1, w2), P1 = byte_pair<2>(w0, w1, w2), P2 = byte_pair<3>(w0, w1, w2);
-    const u16x2 P3 = byte_pair<4>(w0, w1, w2), P4 = byte_pair<5>(w0, w1, w2), P5 = byte_pair<6>(w0, w1, w2);
-    const u16x2 P6 = byte_pair<7>(w0, w1, w2), P7 = byte_pair<8>(w0, w1, w2), P8 = byte_pair<9>(w0, w1, w2);
-    const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
-    BlurRow o;
-    o.h01 = (P0 + P6) * k18 + (P1 + P5) * k34 + (P2 + P4) * k49 + P3 * k55;
-    o.h23 = (P2 + P8) * k18 + (P3 + P7) * k34 + (P4 + P6) * k49 + P5 * k55;
-    return o;
-}
-
-__device__ __forceinline__ uint32_t blur_col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t f,
-                                             uint32_t g) {
-    const uint32_t acc = 18u * (a + g) + 34u * (b + f) + 49u * (c + e) + 55u * d;
-    return min((acc + (1u << 15)) >> 16, 255u);
-}
-
-// One wave's band: outputs rows [y0, y1) of columns x0 .. x0+3 (per lane).  Every load of a step is issued before
-// any of its rows is used, so the band costs ~6 memory round trips per wave, not one per input row; row indices are
-// reflected branch-free (|overhang| <= 3 < h), so loads past the band's end stay in bounds.
-template <int kMode>
-__device__ __forceinline__ void blur_band(const uint8_t* __restrict__ S, int sstride, uint8_t* __restrict__ D,
-                                          const LevelDev& L, int x0, int y0, int y1, bool store_lane = true) {
-    const int h = L.h, w = L.w;
-    auto row_ptr = [&](int yy) {
-        const int r = h >= 4 ? (yy < 0 ? -yy : (yy >= h ? 2 * h - 2 - yy : yy)) : refl101(yy, h);
-        return S + (size_t)r * sstride;
-    };
-    const bool full = x0 + 4 <= w;
-    BlurRow r0, r1, r2, r3, r4, r5, r6;
-    {
-        BlurWin p[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) p[k] = blur_load<kMode>(row_ptr(y0 - 3 + k), x0, w);
-        r0 = blur_hrow(p[0]); r1 = blur_hrow(p[1]); r2 = blur_hrow(p[2]);
-        r3 = blur_hrow(p[3]); r4 = blur_hrow(p[4]); r5 = blur_hrow(p[5]);
-    }
-    auto emit = [&](int y, const BlurRow& a, const BlurRow& b, const BlurRow& c, const BlurRow& d, const BlurRow& e,
-                    const BlurRow& f, const BlurRow& g) {
-        const uint32_t o0 = blur_col(a.h01.x, b.h01.x, c.h01.x, d.h01.x, e.h01.x, f.h01.x, g.h01.x);
-        const uint32_t o1 = blur_col(a.h01.y, b.h01.y, c.h01.y, d.h01.y, e.h01.y, f.h01.y, g.h01.y);
-        const uint32_t o2 = blur_col(a.h23.x, b.h23.x, c.h23.x, d.h23.x, e.h23.x, f.h23.x, g.h23.x);
-        const uint32_t o3 = blur_col(a.h23.y, b.h23.y, c.h23.y, d.h23.y, e.h23.y, f.h23.y, g.h23.y);
-        const uint32_t packed = o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
-        uint8_t* o = D + (size_t)y * w + x0;
-        if (kMode == 3) {
-            if (store_lane) __builtin_memcpy(o, &packed, 4);
-        } else if (kMode == 0 || full) {
-            __builtin_memcpy(o, &packed, 4);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (x0 + j < w) o[j] = (uint8_t)(packed >> (8 * j));
-        }
-    };
-    // ring of 7 row sums; each step loads input rows y+3 .. y+9 at once, then emits outputs y .. y+6
-    for (int y = y0; y < y1; y += 7) {
-        BlurWin p[7];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) p[k] = blur_load<kMode>(row_ptr(y + 3 + k), x0, w);
-        r6 = blur_hrow(p[0]); emit(y, r0, r1, r2, r3, r4, r5, r6); if (y + 1 >= y1) break;
-        r0 = blur_hrow(p[1]); emit(y + 1, r1, r2, r3, r4, r5, r6, r0); if (y + 2 >= y1) break;
-        r1 = blur_hrow(p[2]); emit(y + 2, r2, r3, r4, r5, r6, r0, r1); if (y + 3 >= y1) break;
-        r2 = blur_hrow(p[3]); emit(y + 3, r3, r4, r5, r6, r0, r1, r2); if (y + 4 >= y1) break;
-        r3 = blur_hrow(p[4]); emit(y + 4, r4, r5, r6, r0, r1, r2, r3); if (y + 5 >= y1) break;
-        r4 = blur_hrow(p[5]); emit(y + 5, r5, r6, r0, r1, r2, r3, r4); if (y + 6 >= y1) break;
-        r5 = blur_hrow(p[6]); emit(y + 6, r6, r0, r1, r2, r3, r4, r5);
-    }
-}
-
-// Vertical-pair form (k_blur7<true>): two input rows at a time.  V_m = (row a byte m, row b byte m) as u16x2 (one
+// Vertical-pair form: two input rows at a time.  V_m = (row a byte m, row b byte m) as u16x2 (one
 // v_perm each), so the horizontal sums of 4 columns come out vertically packed -- H_c = (row a sum, row b sum) -- and
 // the column pass of an output pixel is 4 v_dot2_u32_u16 over 4 such pairs (weights (18,34), (49,55), (49,34), (18,0)
 // for an output row aligned with a pair start, (0,18), (34,49), (55,49), (34,18) for the next row) with the rounding
-// constant 2^15 as the first accumulator: no unpacking of u16 halves.  Same integers as blur_hrow + blur_col.
+// constant 2^15 as the first accumulator: no unpacking of u16 halves.  Same integers as the separable
+// integer path (horizontal sums, then (column sum + 2^15) >> 16 saturated).
 struct BlurPair { u16x2 h[4]; };   // columns x0 .. x0+3: (row a, row b) horizontal sums
 
 template <int m>
@@ -1993,17 +784,8 @@ __device__ __forceinline__ void blur_emit2(const BlurPair& a, const BlurPair& b,
         const u16x2 hi = __builtin_elementwise_min(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(v[3], v[2], 0x07060302u)), k255);
         return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x06040200u);
     };
-#if ORBX_BLUR_PK
     oe = pack4(ae);
     oo = pack4(ao);
-#else
-    oe = 0; oo = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        oe |= min(ae[k] >> 16, 255u) << (8 * k);
-        oo |= min(ao[k] >> 16, 255u) << (8 * k);
-    }
-#endif
 }
 
 // Edge-strip window of blur_load<1> as byte selectors: which byte of the clamped 12-byte load each window byte
@@ -2044,13 +826,9 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
         const int r = h >= 16 ? (yy < 0 ? -yy : (yy >= h ? 2 * h - 2 - yy : yy)) : refl101(yy, h);
         return S + (size_t)r * sstride;
     };
-#if ORBX_BLUR_SEL
     ReflSel rs;
     if constexpr (kMode == 1) rs = refl_sel(x0, w);
     auto load = [&](const uint8_t* row) { return kMode == 1 ? blur_load_sel(row, rs) : blur_load<kMode>(row, x0, w); };
-#else
-    auto load = [&](const uint8_t* row) { return blur_load<kMode>(row, x0, w); };
-#endif
     const bool full = x0 + 4 <= w;
     auto store = [&](int y, uint32_t packed) {
         uint8_t* o = D + (size_t)y * w + x0;
@@ -2069,10 +847,10 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
         for (int k = 0; k < 6; ++k) p[k] = load(row_ptr(y0 - 3 + k));
         q0 = blur_hpair(p[0], p[1]); q1 = blur_hpair(p[2], p[3]); q2 = blur_hpair(p[4], p[5]);
     }
-    // ring of 4 row pairs; 8 output rows per iteration.  Interior strips (kMode 0) load the iteration's 8 input rows at
-    // once; the edge forms, whose per-byte reflection needs more registers, 4 at a time (8 spilled at 128 VGPRs)
+    // ring of 4 row pairs; 8 output rows per iteration.  Interior and edge strips load the iteration's 8 input rows at
+    // once; tiny levels (per-byte loads, more registers) 4 at a time (8 spilled at 128 VGPRs)
     for (int y = y0; y < y1; y += 8) {
-        constexpr int kB = (kMode == 0 || (ORBX_BLUR_SEL && kMode == 1)) ? 8 : 4;
+        constexpr int kB = kMode <= 1 ? 8 : 4;
         BlurWin p[kB];
         uint32_t oe, oo;
 #pragma unroll
@@ -2095,10 +873,9 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
 #ifndef ORBX_BLUR_WPE
 #define ORBX_BLUR_WPE 4
 #endif
-template <bool kDot2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_WPE))) void k_blur7(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                               size_t pyr_stride, const LevelDev* __restrict__ levels,
-                                               const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_WPE))) void k_blur7(
+    const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride, const LevelDev* __restrict__ levels,
+    const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
     // tiles [tile0, tile0 + ntiles) of every image (a level range: tiles are level-major)
     const int nbx = (ntiles + 3) / 4;                         // 4 tiles (waves) per workgroup
     const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
@@ -2113,172 +890,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_W
     const uint8_t* S = level_pixels(pyr, pyr_stride, L, bt.level, img, s0, sstride);
     uint8_t* D = blur + img * pyr_stride + L.pyr_off;
     const int y0 = bt.ty * kBlurBand, y1 = min(y0 + kBlurBand, L.h);
-#if ORBX_BLUR_DPP
-    {
-        const int ln = lane_id(), sx = bt.tx * kBlurStrip;
-        const int x0 = sx - 4 + 4 * ln;                           // lanes 1..62 output columns x0 .. x0+3
-        if (sx - 4 >= 0 && sx + 252 <= L.w) {                     // interior strip (wave-uniform): DPP form
-            blur_band<3>(S, sstride, D, L, x0, y0, y1, ln >= 1 && ln <= 62);
-            return;
-        }
-        if (ln == 0 || ln == 63 || x0 >= L.w) return;             // edge strip: per-lane windows
-        const bool interior = (x0 - 4 >= 0) && (x0 + 8 <= L.w);
-        if (__builtin_amdgcn_read_exec() == __ballot(interior))
-            blur_band<0>(S, sstride, D, L, x0, y0, y1);
-        else if (L.w >= 12)
-            blur_band<1>(S, sstride, D, L, x0, y0, y1);
-        else
-            blur_band<2>(S, sstride, D, L, x0, y0, y1);
-        return;
-    }
-#endif
     const int x0 = bt.tx * kBlurStrip + 4 * lane_id();
     if (x0 >= L.w) return;
     const bool interior = (x0 - 4 >= 0) && (x0 + 8 <= L.w);
-    if constexpr (kDot2) {
-        if (__builtin_amdgcn_read_exec() == __ballot(interior))
-            blur_band2<0>(S, sstride, D, L, x0, y0, y1);
-        else if (L.w >= 12)
-            blur_band2<1>(S, sstride, D, L, x0, y0, y1);
-        else
-            blur_band2<2>(S, sstride, D, L, x0, y0, y1);
-        return;
-    }
     // wave-uniform choice of the load form (strips touching a level's left/right edge pick reflected bytes)
     if (__builtin_amdgcn_read_exec() == __ballot(interior))
-        blur_band<0>(S, sstride, D, L, x0, y0, y1);
+        blur_band2<0>(S, sstride, D, L, x0, y0, y1);
     else if (L.w >= 12)
-        blur_band<1>(S, sstride, D, L, x0, y0, y1);
+        blur_band2<1>(S, sstride, D, L, x0, y0, y1);
     else
-        blur_band<2>(S, sstride, D, L, x0, y0, y1);
-}
-
-
-// LDS-staged form (k_blur7_lds): each wave (one tile = level, 256-column strip, 16-row band) issues every load of its
-// tile at once -- input rows y0-3 .. y1+2 (REFLECT_101 rows) x columns sx-4 .. sx+267 as 16-byte chunks; a chunk that
-// crosses the level's left or right edge is assembled byte by byte with REFLECT_101 columns -- into its own LDS slice,
-// then runs the pair-row blur of blur_band2 on 12-byte windows read from LDS.  One memory round trip per band instead
-// of one per batch of 4 rows, and the reflection lives in the fill, so the blur itself has a single form.  The waves of
-// a workgroup are independent (wavefront fences only).
-constexpr int kBlurTileRow = 272;                                // 17 chunks of 16 bytes: columns sx-4 .. sx+267
-#ifndef ORBX_BLUR_LDS_ROWS
-#define ORBX_BLUR_LDS_ROWS 16                                    // output rows per LDS pass (r3ae: 8 -> 14-row slices, slower)
-#endif
-constexpr int kBlurLdsRows = ORBX_BLUR_LDS_ROWS;
-constexpr int kBlurTileBytes = (kBlurLdsRows + 6) * kBlurTileRow;
-
-__global__ __launch_bounds__(256) void k_blur7_lds(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                   size_t pyr_stride, const LevelDev* __restrict__ levels,
-                                                   const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0,
-                                                   int tile0) {
-    __shared__ __attribute__((aligned(16))) uint8_t tile_lds[4 * kBlurTileBytes];
-    static_assert(kBlurStrip == 256, "k_blur7_lds: 4 output columns per lane");
-    static_assert(kBlurBand % kBlurLdsRows == 0 && kBlurLdsRows % 8 == 0, "whole passes of 8 rows");
-    const int nbx = (ntiles + 3) / 4;                         // 4 tiles (waves) per workgroup
-    const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
-    if (item >= nbx * batch) return;
-    const int img = item / nbx;
-    const int tl = (item - img * nbx) * 4 + (threadIdx.x >> 6);
-    if (tl >= ntiles) return;                                 // whole wave
-    const BlurTile bt = tiles[tile0 + tl];
-    const LevelDev L = levels[bt.level];
-    int sstride;
-    const uint8_t* S = level_pixels(pyr, pyr_stride, L, bt.level, img, s0, sstride);
-    uint8_t* D = blur + img * pyr_stride + L.pyr_off;
-    const int h = L.h, w = L.w;
-    const int sx = bt.tx * kBlurStrip;
-    uint8_t* T = tile_lds + (threadIdx.x >> 6) * kBlurTileBytes;
-    const int ln = lane_id();
-    const int x0 = sx + 4 * ln;
-    const bool full = x0 + 4 <= w;
-    const uint8_t* tb = T + 4 * ln;                           // tile byte 4 ln = column x0 - 4
-    // chunk c holds columns xs = sx - 4 + 16c .. xs + 15.  Full chunks [c0, c1) lie inside the level row (one 16-byte
-    // load); chunk 0 of a left-edge strip and the chunks of a right-edge strip that reach past the row are built byte by
-    // byte (REFLECT_101 columns) in a second, short pass; chunks starting at or past column w + 3 are never read (the
-    // last output column w - 1 reads up to w + 2) and are skipped.
-    constexpr int kCh = kBlurTileRow / 16;                    // 17
-    const int c0 = sx - 4 < 0 ? 1 : 0;
-    const int c1 = max(c0, min(kCh, (w - (sx - 4)) / 16));
-    const int c2 = max(c1, min(kCh, (w + 3 - (sx - 4) + 15) / 16));
-    const int nfc = c1 - c0, nsc = c0 + (c2 - c1);
-    for (int ya = bt.ty * kBlurBand; ya < min(bt.ty * kBlurBand + kBlurBand, h); ya += kBlurLdsRows) {
-        const int y0 = ya, y1 = min(ya + kBlurLdsRows, h), R = y1 - y0 + 6;
-        auto row_of = [&](int r) {
-            const int yy = y0 - 3 + r;
-            return S + (size_t)(h >= 4 ? (yy < 0 ? -yy : (yy >= h ? 2 * h - 2 - yy : yy)) : refl101(yy, h)) * sstride;
-        };
-        const int NF = R * nfc;
-        if (nfc > 0) {
-            constexpr int kPf = ((kBlurLdsRows + 6) * kCh + kWave - 1) / kWave;
-            const int dr = kWave / nfc, dc = kWave - dr * nfc;
-            int r = ln / nfc, c = ln - r * nfc;
-            for (int q0 = 0; q0 < NF; q0 += kPf * kWave) {
-                uint32_t v[4 * kPf];
-                int rs[kPf], cs[kPf];
-#pragma unroll
-                for (int k = 0; k < kPf; ++k) {
-                    rs[k] = r; cs[k] = c0 + c;
-                    r += dr; c += dc;
-                    if (c >= nfc) { c -= nfc; ++r; }
-                    v[4 * k] = v[4 * k + 1] = v[4 * k + 2] = v[4 * k + 3] = 0;
-                    if (q0 + ln + k * kWave < NF) __builtin_memcpy(&v[4 * k], row_of(rs[k]) + sx - 4 + 16 * cs[k], 16);
-                }
-#pragma unroll
-                for (int k = 0; k < kPf; ++k)
-                    if (q0 + ln + k * kWave < NF)
-                        *reinterpret_cast<uint4*>(T + rs[k] * kBlurTileRow + 16 * cs[k]) =
-                            make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-            }
-        }
-        const int NS = R * nsc;
-        for (int q = ln; q < NS; q += kWave) {
-            const int r = q / nsc, k = q - r * nsc;
-            const int c = k < c0 ? 0 : c1 + (k - c0);
-            const uint8_t* row = row_of(r);
-            const int xs = sx - 4 + 16 * c;
-            uint32_t b4[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int b = 0; b < 16; ++b) {
-                const int x = xs + b;
-                const int xr = w >= 4 ? (x < 0 ? -x : (x >= w ? 2 * w - 2 - x : x)) : refl101(x, w);
-                if (x < w + 3) b4[b >> 2] |= (uint32_t)row[xr] << (8 * (b & 3));
-            }
-            *reinterpret_cast<uint4*>(T + r * kBlurTileRow + 16 * c) = make_uint4(b4[0], b4[1], b4[2], b4[3]);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // the tile before any lane's window reads
-        if (x0 < w) {
-            auto win = [&](int tr) -> BlurWin {
-                const uint32_t* p = reinterpret_cast<const uint32_t*>(tb + tr * kBlurTileRow);
-                BlurWin o; o.w0 = p[0]; o.w1 = p[1]; o.w2 = p[2];
-                return o;
-            };
-            auto store = [&](int y, uint32_t packed) {
-                uint8_t* o = D + (size_t)y * w + x0;
-                if (full) {
-                    __builtin_memcpy(o, &packed, 4);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (x0 + j < w) o[j] = (uint8_t)(packed >> (8 * j));
-                }
-            };
-            // tile row t = input row y0 - 3 + t; output row y needs tile rows y - y0 .. y - y0 + 6
-            BlurPair q0 = blur_hpair(win(0), win(1)), q1 = blur_hpair(win(2), win(3)), q2 = blur_hpair(win(4), win(5)), q3;
-            for (int y = y0; y < y1; y += 8) {
-                const int t = y - y0 + 6;
-                uint32_t oe, oo;
-                q3 = blur_hpair(win(t), win(t + 1)); blur_emit2(q0, q1, q2, q3, oe, oo);
-                store(y, oe); if (y + 1 >= y1) break; store(y + 1, oo); if (y + 2 >= y1) break;
-                q0 = blur_hpair(win(t + 2), win(t + 3)); blur_emit2(q1, q2, q3, q0, oe, oo);
-                store(y + 2, oe); if (y + 3 >= y1) break; store(y + 3, oo); if (y + 4 >= y1) break;
-                q1 = blur_hpair(win(t + 4), win(t + 5)); blur_emit2(q2, q3, q0, q1, oe, oo);
-                store(y + 4, oe); if (y + 5 >= y1) break; store(y + 5, oo); if (y + 6 >= y1) break;
-                q2 = blur_hpair(win(t + 6), win(t + 7)); blur_emit2(q3, q0, q1, q2, oe, oo);
-                store(y + 6, oe); if (y + 7 >= y1) break; store(y + 7, oo);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");   // window reads before the next pass refills
-    }
+        blur_band2<2>(S, sstride, D, L, x0, y0, y1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2353,7 +974,6 @@ __device__ unsigned long long g_qtprof[2][64];
 
 __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
                                                          const uint32_t* __restrict__ cand_xy, const uint8_t* __restrict__ cand_s,
-                                                         const uint32_t* __restrict__ cand2_xy, const uint8_t* __restrict__ cand2_s,
                                                          int cand_stride, const int* __restrict__ cell_cnt, int ncells,
                                                          QtScratch qs, uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r,
                                                          int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
@@ -2389,8 +1009,8 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
     // (per cell: count -> sa, slot offset -> sb; all loads independent)
     for (int i = tid; i < ncl; i += T) {
         const int cw = cell_cnt[(size_t)img * ncells + L.cell_begin + i];
-        sa[i] = cw & ~kCntMinList;
-        sb[i] = cells[L.cell_begin + i].slot_off | (cw & kCntMinList ? (int)0x80000000u : 0);   // list: iniTh / minTh
+        sa[i] = cw;
+        sb[i] = cells[L.cell_begin + i].slot_off;
     }
     __syncthreads();
     const int K = block_scan_array(sa, ncl, tmp);
@@ -2427,9 +1047,9 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                 if (k < K) {
                     const int c = kn[k];
                     const int sbc = sb[c];
-                    const size_t src = io + (size_t)(sbc & 0x7fffffff) + (k - sa[c]);
-                    xy[u] = sbc < 0 ? cand2_xy[src] : cand_xy[src];
-                    r[u] = sbc < 0 ? cand2_s[src] : cand_s[src];
+                    const size_t src = io + (size_t)sbc + (k - sa[c]);
+                    xy[u] = cand_xy[src];
+                    r[u] = cand_s[src];
                 }
             }
 #pragma unroll
@@ -2732,7 +1352,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
 }
 
 // ---------------------------------------------------------------------------------------------
-// IC angle + steered BRIEF + output assembly: one wave per keypoint slot.
+// IC angle + steered BRIEF + output assembly (k_describe_m).
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ float fast_atan2_deg(float y, float x) {   // OpenCV fastAtan2 (pinned, :103)
     const float k = (float)(180.0 / M_PI);
@@ -2767,145 +1387,6 @@ constexpr int kBriefR = 18;                      // max |rotated pattern offset|
 constexpr int kBriefRow = 40;                    // LDS bytes per window row (5 x 8-byte chunks)
 constexpr int kBriefWin = (2 * kBriefR + 1) * kBriefRow;
 
-__global__ __launch_bounds__(256) void k_describe(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
-                                                  size_t pyr_stride, const LevelDev* __restrict__ levels, int nlevels,
-                                                  const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
-                                                  int out_stride, const int* __restrict__ level_cnt,
-                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int32_t* __restrict__ counts,
-                                                  int capacity, int slot0, int nslots, int write_count, int batch, Src0 s0,
-                                                  SlotTable tab, unsigned seq, int* __restrict__ err) {
-    // slots [slot0, slot0 + nslots) of every image (a level range: slots are level-major); the launch that covers
-    // the last levels writes the per-image counts (it runs once every level's count is known)
-    __shared__ __attribute__((aligned(16))) uint8_t brief_lds[4 * kBriefWin];
-    const int nbx = (nslots + 3) / 4;                         // 4 slots (waves) per workgroup
-    const int item = xcd_item(xcd_chunk(nbx * batch));       // keypoints of one image on one XCD
-    if (item >= nbx * batch) return;
-    const int img = item / nbx;
-    // wave-uniform (one wave per slot): kept in SGPRs, so the level lookup below is scalar, from the kernel arguments
-    const int rel = __builtin_amdgcn_readfirstlane(((item - img * nbx) * blockDim.x + threadIdx.x) >> 6);
-    const int slot = slot0 + rel;
-    const int ln = lane_id();
-    if (rel >= nslots) return;
-    // slot -> (level, index)
-    int lvl = 0;
-#pragma unroll
-    for (int l = 1; l < kMaxLevels; ++l) lvl += (l < nlevels && slot >= tab.out_off[l]) ? 1 : 0;
-    const LevelDev L = levels[lvl];
-    const int i = slot - L.out_off;
-    const int* lcs = level_cnt + img * nlevels;
-    int off = 0;
-    for (int l = 0; l < lvl; ++l) off += lcs[l] & 0xffff;
-    if (write_count && rel == 0 && ln == 0) {
-        int total = 0;
-        for (int l = 0; l < nlevels; ++l) total += lcs[l] & 0xffff;
-        counts[img] = min(total, capacity);
-    }
-    const int craw = lcs[lvl], ci = craw & 0xffff;
-    if (lvl_stale(craw, seq) && ln == 0) atomicOr(err, kErrStale);   // this call's stamp on the level read
-    if (i >= ci) return;
-    const int o = off + i;
-    if (o >= capacity) return;
-
-    const uint32_t xy = lvl_xy[(size_t)img * out_stride + L.out_off + i];
-    const int cx = (int)(xy & 0xffff), cy = (int)(xy >> 16);
-    // --- the blurred 37 x 37 window the BRIEF tests can touch (|rotated offset| <= 18), loaded now, beside the
-    //     IC_Angle loads, into this wave's LDS slice (rows of kBriefRow bytes): the tests then read LDS, so the
-    //     angle -> BRIEF dependency costs no second memory round trip.  Keypoints lie >= 19 px inside the level
-    //     (FAST window :789-797), so rows cy-18 .. cy+18 exist; a row's bytes past cx+18 are never read.
-    const uint8_t* B = blur + img * pyr_stride + L.pyr_off;
-    const int step = L.w;
-    uint8_t* win = brief_lds + (threadIdx.x >> 6) * kBriefWin;
-    uint64_t wv[3];
-    {
-        const uint8_t* w0 = B + (size_t)(cy - kBriefR) * step + (cx - kBriefR);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int q = ln + 64 * k, r = min(q / 5, 2 * kBriefR), c = q - (q / 5) * 5;   // 37 rows x 5 chunks
-            __builtin_memcpy(&wv[k], w0 + (size_t)r * step + 8 * c, 8);
-        }
-    }
-    // --- IC_Angle (:77-104): m10 = sum u*I, m01 = sum v*I over the radius-15 disc
-    int pstride;
-    const uint8_t* P = level_pixels(pyr, pyr_stride, L, lvl, img, s0, pstride);
-    int m10 = 0, m01 = 0;
-    {
-        // The 31 x 32 box around the disc as 124 (row, 8-byte chunk) items, two per lane, two 8-byte loads per lane
-        // (instead of one byte load per lane and disc row pair: 16 memory instructions).  Per chunk at row v and
-        // columns u0 .. u0+7: the bytes outside the disc (|u| > umax[|v|]) are masked off, then
-        // sum (u+16)*I and sum I come from v_dot4_u32_u8 against packed weights: m10 += that - 16 * sum I,
-        // m01 += v * sum I (integer, exact).
-        const uint8_t* p0 = P + (size_t)(cy - kHalfPatch) * pstride + (cx - kHalfPatch);
-        uint64_t ic[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int q = ln + 64 * k, r = min(q >> 2, 2 * kHalfPatch);
-            __builtin_memcpy(&ic[k], p0 + (size_t)r * pstride + 8 * (q & 3), 8);
-        }
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int q = ln + 64 * k;
-            const int v = (q >> 2) - kHalfPatch, av = v < 0 ? -v : v;
-            const int um = kUmax[av > 15 ? 15 : av];
-            const int u0 = 8 * (q & 3) - kHalfPatch;
-            const int lo = max(0, -um - u0), hi = min(7, um - u0);          // bytes lo..hi lie in the disc
-            uint64_t m = 0;
-            if (q < 124 && lo <= hi) m = (hi >= 7 ? ~0ull : ((1ull << (8 * hi + 8)) - 1ull)) & (~0ull << (8 * lo));
-            const uint64_t px = ic[k] & m;
-            const uint32_t a = (uint32_t)px, b = (uint32_t)(px >> 32);
-            const uint32_t wa = (uint32_t)(u0 + 16) * 0x01010101u + 0x03020100u, wb = wa + 0x04040404u;
-            const int dot = (int)__builtin_amdgcn_udot4(b, wb, __builtin_amdgcn_udot4(a, wa, 0u, false), false);
-            const int sum = (int)__builtin_amdgcn_udot4(b, 0x01010101u, __builtin_amdgcn_udot4(a, 0x01010101u, 0u, false), false);
-            m10 += dot - 16 * sum;
-            m01 += v * sum;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int q = ln + 64 * k;
-        if (q < 5 * (2 * kBriefR + 1)) *reinterpret_cast<uint64_t*>(win + (q / 5) * kBriefRow + 8 * (q % 5)) = wv[k];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");         // other lanes' window bytes before the tests read
-    m10 = wave_sum_dpp(m10);
-    m01 = wave_sum_dpp(m01);
-    const float angle = fast_atan2_deg((float)m01, (float)m10);
-
-    // --- computeOrbDescriptor (:108-147) on the blurred level
-    const float toRad = (float)(M_PI / 180.f);
-    const float ang = __fmul_rn(angle, toRad);
-    float a, b;
-    orbx_sincos_brief(ang, &a, &b);   // == (float)cos/sin((double)ang) for every possible ang (orbx_sincos.h)
-    const uint8_t* center = win + kBriefR * kBriefRow + kBriefR;    // LDS written by this wave (in-order LDS queue)
-    uint64_t bits[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const int t = g * 64 + ln;
-        const uint32_t pw = reinterpret_cast<const uint32_t*>(c_pattern)[t];   // x0, y0, x1, y1 (signed bytes)
-        int vals[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
-            const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
-            const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
-            vals[e] = center[__mul24(__float2int_rn(ry), kBriefRow) + __float2int_rn(rx)];
-        }
-        bits[g] = __ballot(vals[0] < vals[1]);
-    }
-    uint64_t* drow = reinterpret_cast<uint64_t*>(desc + ((size_t)img * capacity + o) * 32);
-    if (ln < 4) drow[ln] = bits[0] * (ln == 0) + bits[1] * (ln == 1) + bits[2] * (ln == 2) + bits[3] * (ln == 3);
-    if (ln == 0) {
-        orbx_keypoint k;
-        float x = (float)cx, y = (float)cy;
-        if (lvl != 0) { x = __fmul_rn(x, L.scale); y = __fmul_rn(y, L.scale); }
-        k.x = x; k.y = y;
-        k.size = (float)L.patch;
-        k.angle = angle;
-        k.response = (float)lvl_r[(size_t)img * out_stride + L.out_off + i];
-        k.octave = lvl;
-        k.class_id = -1;
-        kps[(size_t)img * capacity + o] = k;
-    }
-}
-
 // Sum of v over the kLp-lane group of each lane (groups of 16, 32 or 64 lanes), in every lane of the group.
 template <int kLp>
 __device__ __forceinline__ int group_sum(int v, int sub) {
@@ -2920,10 +1401,17 @@ __device__ __forceinline__ int group_sum(int v, int sub) {
     return r0 + r1 + r2 + r3;
 }
 
-// k_describe with kKpw keypoints per wave (kLp = 64 / kKpw lanes each): the wave-uniform part of a keypoint (level
+// IC angle + steered BRIEF + output assembly, kKpw keypoints per wave (kLp = 64 / kKpw lanes each; the shipped form is
+// 2 -- one keypoint per wave measured 449 vs 444 us serial, 4 no faster): the wave-uniform part of a keypoint (level
 // lookup, moment reductions, fastAtan2, the double sin/cos, the keypoint record) is paid once per kKpw keypoints,
 // and each lane loads kKpw times as many window chunks and runs kKpw times as many BRIEF tests.  The keypoints of a
-// wave can straddle a level boundary, so the level is per lane.  Same results as k_describe, bit for bit.
+// wave can straddle a level boundary, so the level is per lane.
+//   The blurred 37 x 37 window the BRIEF tests can touch (|rotated offset| <= 18) is loaded beside the IC_Angle loads
+// into the keypoint's LDS slice (rows of kBriefRow bytes): the tests then read LDS, so the angle -> BRIEF dependency
+// costs no second memory round trip.  Keypoints lie >= 19 px inside the level (FAST window :789-797), so rows
+// cy-18 .. cy+18 exist; a row's bytes past cx+18 are never read.  IC_Angle (:77-104): the 31 x 32 box around the
+// disc as 124 (row, 8-byte chunk) items; per chunk the bytes outside the disc (|u| > umax[|v|]) are masked off, then
+// sum (u+16)*I and sum I come from v_dot4_u32_u8 against packed weights: m10 += that - 16 * sum I, m01 += v * sum I.
 template <int kKpw>
 __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                                                     size_t pyr_stride, const LevelDev* __restrict__ levels, int nlevels,
@@ -2963,8 +1451,8 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
         total += c;
     }
     const int craw = lcs[lvl], ci = craw & 0xffff;
-    // the level this lane reads must carry this call's stamp
-    if (__ballot(lvl_stale(craw, seq)) && ln == 0) atomicOr(err, kErrStale);
+    // the level this lane reads must carry this call's stamp (lanes past the launch's slots read nothing)
+    if (__ballot(rel < nslots && lvl_stale(craw, seq)) && ln == 0) atomicOr(err, kErrStale);
     if (write_count && wrel == 0 && ln == 0) counts[img] = min(total, capacity);
     const LevelDev& L = levels[lvl];
     const int lw = L.w, lpo = L.pyr_off, loo = L.out_off;
@@ -3075,213 +1563,6 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_describe_fb: k_describe_m<2> with the GaussianBlur (:1085-1086) done per keypoint in LDS -- no blurred pyramid.
-//
-// A keypoint's BRIEF tests read the blurred level only inside the 37 x 37 window around it (|rotated offset| <= 18), and
-// those blurred pixels depend on the raw level inside a 43 x 43 window (7 x 7 kernel).  Each keypoint's 32 lanes load
-// the raw rows cy-21 .. cy+21, columns cx-23 .. cx+24 (6 chunks of 8 bytes per row, the IC_Angle box cx-15 .. cx+16 =
-// chunks 1..4 of rows 6..36, so the moments come straight from the loaded registers), store them in the keypoint's LDS
-// slice, and blur them there with the pinned arithmetic of k_blur7 (horizontal sums as packed u16, column pass
-// (acc + 2^15) >> 16 saturated; REFLECT_101 applied to the raw coordinates of windows that cross the level border,
-// which is the same as reflecting per axis): 30 lanes each own 4 output columns x 12-13 output rows.  The BRIEF tests
-// then read the blurred window exactly as k_describe_m does.  Bit-identical to k_blur7 + k_describe_m; the blurred
-// pyramid's HBM write and the describe's gather of it are gone (one raw window per keypoint is read instead).
-// ---------------------------------------------------------------------------------------------
-constexpr int kFbRows = 2 * kBriefR + 7;          // 43 raw rows: cy-21 .. cy+21
-constexpr int kFbRow = 48;                        // raw bytes per row: cx-23 .. cx+24
-constexpr int kFbChunks = kFbRows * (kFbRow / 8); // 258 8-byte chunks
-constexpr int kFbRaw = kFbRows * kFbRow;          // 2064 bytes
-
-// horizontal sums of the 4 output columns whose 12-byte window starts one byte before blur_hrow's (x0 - 5)
-__device__ __forceinline__ BlurRow blur_hrow5(uint32_t w0, uint32_t w1, uint32_t w2) {
-    const u16x2 P0 = byte_pair<2>(w0, w1, w2), P1 = byte_pair<3>(w0, w1, w2), P2 = byte_pair<4>(w0, w1, w2);
-    const u16x2 P3 = byte_pair<5>(w0, w1, w2), P4 = byte_pair<6>(w0, w1, w2), P5 = byte_pair<7>(w0, w1, w2);
-    const u16x2 P6 = byte_pair<8>(w0, w1, w2), P7 = byte_pair<9>(w0, w1, w2), P8 = byte_pair<10>(w0, w1, w2);
-    const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
-    BlurRow o;
-    o.h01 = (P0 + P6) * k18 + (P1 + P5) * k34 + (P2 + P4) * k49 + P3 * k55;
-    o.h23 = (P2 + P8) * k18 + (P3 + P7) * k34 + (P4 + P6) * k49 + P5 * k55;
-    return o;
-}
-
-__device__ __forceinline__ uint32_t blur_emit4(const BlurRow& a, const BlurRow& b, const BlurRow& c, const BlurRow& d,
-                                               const BlurRow& e, const BlurRow& f, const BlurRow& g) {
-    const uint32_t o0 = blur_col(a.h01.x, b.h01.x, c.h01.x, d.h01.x, e.h01.x, f.h01.x, g.h01.x);
-    const uint32_t o1 = blur_col(a.h01.y, b.h01.y, c.h01.y, d.h01.y, e.h01.y, f.h01.y, g.h01.y);
-    const uint32_t o2 = blur_col(a.h23.x, b.h23.x, c.h23.x, d.h23.x, e.h23.x, f.h23.x, g.h23.x);
-    const uint32_t o3 = blur_col(a.h23.y, b.h23.y, c.h23.y, d.h23.y, e.h23.y, f.h23.y, g.h23.y);
-    return o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
-}
-
-__global__ __launch_bounds__(256) void k_describe_fb(const uint8_t* __restrict__ pyr, size_t pyr_stride,
-                                                     const LevelDev* __restrict__ levels, int nlevels,
-                                                     const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
-                                                     int out_stride, const int* __restrict__ level_cnt,
-                                                     orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                     int32_t* __restrict__ counts, int capacity, int slot0, int nslots,
-                                                     int write_count, int batch, Src0 s0, SlotTable tab, unsigned seq,
-                                                     int* __restrict__ err) {
-    constexpr int kKpw = 2, kLp = kWave / kKpw;
-    constexpr int kNW = (kFbChunks + kLp - 1) / kLp;             // 9 raw chunks per lane
-    constexpr int kNT = 256 / kLp;                               // BRIEF tests per lane
-    __shared__ __attribute__((aligned(16))) uint8_t raw_lds[4 * kKpw * kFbRaw];
-    __shared__ __attribute__((aligned(16))) uint8_t brief_lds[4 * kKpw * kBriefWin];
-    const int per_wg = 4 * kKpw;
-    const int nbx = (nslots + per_wg - 1) / per_wg;
-    const int item = xcd_item(xcd_chunk(nbx * batch));
-    if (item >= nbx * batch) return;
-    const int img = item / nbx;
-    const int wrel = __builtin_amdgcn_readfirstlane(((item - img * nbx) * blockDim.x + threadIdx.x) >> 6);
-    if (wrel * kKpw >= nslots) return;                           // whole wave
-    const int ln = lane_id();
-    const int sub = ln / kLp, lk = ln - sub * kLp;
-    const int rel = wrel * kKpw + sub;
-    const int slot = slot0 + rel;
-    int lvl = 0;
-#pragma unroll
-    for (int l = 1; l < kMaxLevels; ++l) lvl += (l < nlevels && slot >= tab.out_off[l]) ? 1 : 0;
-    const int* lcs = level_cnt + img * nlevels;
-    int off = 0, total = 0;
-    for (int l = 0; l < nlevels; ++l) {
-        const int c = lcs[l] & 0xffff;
-        off += l < lvl ? c : 0;
-        total += c;
-    }
-    const int craw = lcs[lvl], ci = craw & 0xffff;
-    if (__ballot(lvl_stale(craw, seq)) && ln == 0) atomicOr(err, kErrStale);
-    if (write_count && wrel == 0 && ln == 0) counts[img] = min(total, capacity);
-    const LevelDev& L = levels[lvl];
-    const int lw = L.w, lh = L.h, lpo = L.pyr_off, loo = L.out_off;
-    const int i = slot - loo;
-    const int o = off + i;
-    const bool valid = rel < nslots && i < ci && o < capacity;
-    if (__ballot(valid) == 0) return;                            // whole wave
-
-    const uint32_t xy = valid ? lvl_xy[(size_t)img * out_stride + loo + i] : 0u;
-    const int cx = (int)(xy & 0xffff), cy = (int)(xy >> 16);
-    const uint8_t* P = lvl == 0 ? s0.p + img * s0.istride : pyr + img * pyr_stride + lpo;
-    const int pstride = lvl == 0 ? (int)s0.step : lw;
-    const int wx0 = cx - 23, wy0 = cy - 21;                      // raw window origin
-    // windows crossing the level border (keypoints lie >= 19 px inside, so by at most 4 columns / 2 rows): bytes by
-    // REFLECT_101 coordinates, one byte load each (uniform per keypoint)
-    const bool inside = wx0 >= 0 && wx0 + kFbRow <= lw && wy0 >= 0 && wy0 + kFbRows <= lh;
-    uint64_t wv[kNW];
-    if (valid) {
-#pragma unroll
-        for (int k = 0; k < kNW; ++k) {
-            const int q = min(lk + kLp * k, kFbChunks - 1), r = q / 6, c = q - r * 6;
-            if (inside) {
-                __builtin_memcpy(&wv[k], P + (size_t)(wy0 + r) * pstride + wx0 + 8 * c, 8);
-            } else {
-                const int y = refl101(wy0 + r, lh);
-                const uint8_t* row = P + (size_t)y * pstride;
-                uint64_t v = 0;
-#pragma unroll
-                for (int b = 0; b < 8; ++b) v |= (uint64_t)row[refl101(wx0 + 8 * c + b, lw)] << (8 * b);
-                wv[k] = v;
-            }
-        }
-    }
-    uint8_t* raw = raw_lds + ((threadIdx.x >> 6) * kKpw + sub) * kFbRaw;
-    uint8_t* win = brief_lds + ((threadIdx.x >> 6) * kKpw + sub) * kBriefWin;
-    // --- IC_Angle (:77-104) from the loaded chunks: the 31 x 32 box is chunks 1..4 of window rows 6..36
-    int m10 = 0, m01 = 0;
-#pragma unroll
-    for (int k = 0; k < kNW; ++k) {
-        const int q = lk + kLp * k, r = q / 6, c = q - r * 6;
-        const int v = r - 21, av = v < 0 ? -v : v;
-        const int um = kUmax[av > 15 ? 15 : av];
-        const int u0 = 8 * c - 23;                                // column offset of the chunk's first byte
-        const int lo = max(0, -um - u0), hi = min(7, um - u0);
-        uint64_t m = 0;
-        if (valid && q < kFbChunks && av <= kHalfPatch && c >= 1 && c <= 4 && lo <= hi)
-            m = (hi >= 7 ? ~0ull : ((1ull << (8 * hi + 8)) - 1ull)) & (~0ull << (8 * lo));
-        const uint64_t px = wv[k] & m;
-        const uint32_t a = (uint32_t)px, b = (uint32_t)(px >> 32);
-        const uint32_t wa = (uint32_t)(u0 + 16) * 0x01010101u + 0x03020100u, wb = wa + 0x04040404u;
-        const int dot = (int)__builtin_amdgcn_udot4(b, wb, __builtin_amdgcn_udot4(a, wa, 0u, false), false);
-        const int sum = (int)__builtin_amdgcn_udot4(b, 0x01010101u, __builtin_amdgcn_udot4(a, 0x01010101u, 0u, false), false);
-        m10 += dot - 16 * sum;
-        m01 += v * sum;
-    }
-    if (valid) {
-#pragma unroll
-        for (int k = 0; k < kNW; ++k) {
-            const int q = lk + kLp * k;
-            if (q < kFbChunks) *reinterpret_cast<uint64_t*>(raw + 8 * q) = wv[k];   // row q / 6, chunk q % 6
-        }
-    }
-    m10 = group_sum<kLp>(m10, sub);
-    m01 = group_sum<kLp>(m01, sub);
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");       // other lanes' raw chunks before the blur reads
-    // --- GaussianBlur of the 37 x 37 window: lane lk < 30 owns output columns 4g .. 4g+3 (g = lk % 10; blurred column
-    //     c <-> x = cx - 18 + c <-> raw byte c + 5) and output rows [13s, min(13s + 13, 37)) (s = lk / 10); output row
-    //     r needs raw rows r .. r + 6
-    {
-        const int g = lk % 10, s = lk / 10;
-        const bool act = valid && lk < 30;
-        const int y0 = 13 * s, y1 = min(y0 + 13, 2 * kBriefR + 1);
-        const uint8_t* rb = raw + 4 * g;
-        auto ld = [&](int r) -> BlurRow {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(rb + r * kFbRow);
-            return blur_hrow5(p[0], p[1], p[2]);
-        };
-        if (act) {
-            BlurRow r0 = ld(y0), r1 = ld(y0 + 1), r2 = ld(y0 + 2), r3 = ld(y0 + 3), r4 = ld(y0 + 4), r5 = ld(y0 + 5), r6;
-            uint32_t* wo = reinterpret_cast<uint32_t*>(win + 4 * g);
-            for (int y = y0; y < y1; y += 7) {
-                r6 = ld(y + 6); wo[y * (kBriefRow / 4)] = blur_emit4(r0, r1, r2, r3, r4, r5, r6); if (y + 1 >= y1) break;
-                r0 = ld(y + 7); wo[(y + 1) * (kBriefRow / 4)] = blur_emit4(r1, r2, r3, r4, r5, r6, r0); if (y + 2 >= y1) break;
-                r1 = ld(y + 8); wo[(y + 2) * (kBriefRow / 4)] = blur_emit4(r2, r3, r4, r5, r6, r0, r1); if (y + 3 >= y1) break;
-                r2 = ld(y + 9); wo[(y + 3) * (kBriefRow / 4)] = blur_emit4(r3, r4, r5, r6, r0, r1, r2); if (y + 4 >= y1) break;
-                r3 = ld(y + 10); wo[(y + 4) * (kBriefRow / 4)] = blur_emit4(r4, r5, r6, r0, r1, r2, r3); if (y + 5 >= y1) break;
-                r4 = ld(y + 11); wo[(y + 5) * (kBriefRow / 4)] = blur_emit4(r5, r6, r0, r1, r2, r3, r4); if (y + 6 >= y1) break;
-                r5 = ld(y + 12); wo[(y + 6) * (kBriefRow / 4)] = blur_emit4(r6, r0, r1, r2, r3, r4, r5);
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");       // blurred window before the tests read it
-    const float angle = fast_atan2_deg((float)m01, (float)m10);
-    const float ang = __fmul_rn(angle, (float)(M_PI / 180.f));
-    float a, b;
-    orbx_sincos_brief(ang, &a, &b);
-    const uint8_t* center = win + kBriefR * kBriefRow + kBriefR;
-    uint32_t words[kNT];
-#pragma unroll
-    for (int gt = 0; gt < kNT; ++gt) {
-        const int t = gt * kLp + lk;
-        const uint32_t pw = reinterpret_cast<const uint32_t*>(c_pattern)[t];
-        int vals[2] = {0, 0};
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
-            const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
-            const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
-            if (valid) vals[e] = center[__mul24(__float2int_rn(ry), kBriefRow) + __float2int_rn(rx)];
-        }
-        const uint64_t bm = __ballot(vals[0] < vals[1]);
-        words[gt] = (uint32_t)(bm >> (sub * kLp)) & (uint32_t)((1ull << kLp) - 1ull);
-    }
-    if (!valid) return;
-    uint32_t dw = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dw = lk == j ? words[j] : dw;
-    if (lk < 8) reinterpret_cast<uint32_t*>(desc + ((size_t)img * capacity + o) * 32)[lk] = dw;
-    if (lk == 0) {
-        orbx_keypoint k;
-        float x = (float)cx, y = (float)cy;
-        if (lvl != 0) { x = __fmul_rn(x, L.scale); y = __fmul_rn(y, L.scale); }
-        k.x = x; k.y = y;
-        k.size = (float)L.patch;
-        k.angle = angle;
-        k.response = (float)lvl_r[(size_t)img * out_stride + loo + i];
-        k.octave = lvl;
-        k.class_id = -1;
-        kps[(size_t)img * capacity + o] = k;
-    }
-}
-
 // =============================================================================================
 // host side
 // =============================================================================================
@@ -3300,9 +1581,14 @@ hipError_t debug_spin(hipStream_t stream, double ms) {
 static int round_even_f(float v) { return (int)std::nearbyintf(v); }
 static int round_even_d(double v) { return (int)std::nearbyint(v); }
 
-enum Stage { ST_RESIZE = 0, ST_FAST, ST_BLUR, ST_QUADTREE, ST_DESCRIBE, ST_FAST_L0, ST_QUADTREE_L0, ST_COUNT };
+// Stage spans per call (HIP events on the stream each launch is issued on).  The *_busy entries are the union of a
+// kernel family's two launches (level 0 on the side stream, levels >= 1 on the launch stream), which overlap each
+// other: the wall time during which that kernel is running, <= the sum of the two spans.
+enum Stage { ST_RESIZE = 0, ST_FAST, ST_BLUR, ST_QUADTREE, ST_DESCRIBE, ST_FAST_L0, ST_QUADTREE_L0, ST_FAST_BUSY,
+             ST_QUADTREE_BUSY, ST_COUNT };
 static const char* kStageNames[ST_COUNT] = {"resize", "fast_cells", "blur7", "quadtree", "describe", "fast_cells_l0",
-                                            "quadtree_l0"};
+                                            "quadtree_l0", "fast_busy", "quadtree_busy"};
+constexpr int kSpanStages = ST_FAST_BUSY;   // stages [0, kSpanStages) are single event pairs
 
 struct Extractor {
     // ORBextractor parameters and tables (:410-470)
@@ -3324,18 +1610,6 @@ struct Extractor {
     // Per-call events come from a pool (CallEvents below): an event is recorded again only 32 calls later, never
     // while a wait on its previous record may still be in flight.
     int pipeline = 1;         // ORBX_PIPELINE: 1 two streams (above), 0 every launch in order on the launch stream
-    int qt_split = 1;         // ORBX_QT_SPLIT: 1 level-0 quadtree on the side stream, 0 one quadtree launch (all levels)
-    // (fast0 in CallEvents: side FAST level 0 done -- with qt_split 0 the launch stream's quadtree waits on it)
-    // Per-level FAST (fast_split, ORBX_FAST_SPLIT): FAST of level l >= 1 runs on its own stream as soon as the resize
-    // chain has produced level l (ev_lvl[l]), so the latency-bound chain of seven resizes overlaps the FAST work of
-    // the levels it has finished; the launch stream's DistributeOctTree waits for ev_fast1.
-    hipStream_t fastq = nullptr;
-    hipEvent_t ev_lvl[kMaxLevels] = {};
-    hipEvent_t ev_fast1 = nullptr;
-    int fast_split = 0;
-    int desc_side = 0;        // ORBX_DESC_SIDE=1: describe at the end of the side stream (split entry point only)
-    int desc_kpw = 2;         // keypoints per k_describe wave (ORBX_DESC_KPW = 1, 2 or 4)
-    int desc_split = 0;       // ORBX_DESC_SPLIT=1: level-0 describe on the side stream (measured 1.29 vs 1.26 ms/step)
     // Describe stream (orbx_extract_batch_device_split): k_describe runs on the caller's output stream, so the next
     // call's front half (resize chain, FAST) on the input stream overlaps this call's describe.  What the next call
     // overwrites that describe reads is ordered by events: the kept keypoints and the blurred pyramid (its quadtree
@@ -3343,8 +1617,8 @@ struct Extractor {
     // describe).
     static constexpr int kCallEv = 32;
     struct CallEvents {
-        hipEvent_t fork, pyr, fast0, join, front, desc;   // fork from the caller, pyramid built, side FAST level 0,
-        bool used;                                         // side join, launch-stream quadtree, describe done
+        hipEvent_t fork, pyr, join, front, desc;          // fork from the caller, pyramid built, side join,
+        bool used;                                         // launch-stream quadtree, describe done
     };
     CallEvents cev[kCallEv] = {};
     unsigned long long cev_next = 0;
@@ -3368,37 +1642,12 @@ struct Extractor {
     int cand_stride = 0;      // candidate slots per image
     int out_stride = 0;       // quadtree output slots per image
     int node_cap = 0;
-    struct FastLaunch { int cell0, n, R, C, ps; size_t lds; };
-    FastLaunch fast_launch[2] = {};   // k_fast_cells over level 0 / levels >= 1
-    // k_fast_band (default; ORBX_FAST_BAND=0 selects k_fast_cells): bands of up to band_g cells, level 0 / levels >= 1
-    struct BandLaunch { int band0, n, kmax; BandLds lay; };
-    BandLaunch band_launch[2] = {};
-    int band_lvl0[kMaxLevels] = {}, band_lvln[kMaxLevels] = {};   // bands of level l: [band_lvl0[l], + band_lvln[l])
-    std::vector<BandDev> bandv;
-    BandDev* d_bands = nullptr;
-    int fast_band = 1;
-    // k_fast_rows (default; ORBX_FAST_ROWS=0 selects k_fast_band): one wave per group of <= 8 cells of one cell row
-    // (<= 248 detection columns); level 0 / levels >= 1 as the two launches above
-    struct RowsLaunch { int g0, n; };
-    RowsLaunch rows_launch[2] = {};
-    std::vector<BandDev> rowgv;
-    BandDev* d_rowg = nullptr;
-    int fast_rows = 0;   // (default off until it measures faster than k_fast_band in the full step)
-    // k_fast_wave (ORBX_FAST_WAVE): one wave per (cell, image), wave_wpg waves per workgroup; level 0 / levels >= 1
+    // k_fast_wave: one wave per (cell, image), 4 waves per workgroup; launch 0 = level 0, launch 1 = levels >= 1, each
+    // wave's LDS slice sized for its launch's largest cell
     struct WaveLaunch { int cell0, n, ps, kcap; WaveLds lay; };
     WaveLaunch wave_launch[2] = {};
-    int fast_wave = 1;        // default (r3x: 62.5k -> 67.1k frames/s with the pair-row blur); 0 = k_fast_band
-    int wave_wpg = 4;
-    int wave_twopass = 1;
-    int wave_cells = 1;       // ORBX_FAST_CELLS = 2 / 4: k_fast_wave_p (a wave walks that many cells, next ROI prefetched)     // ORBX_FAST_TWOPASS: iniTh first, minTh only for the cells left empty (0: one pass)
-    int wave_psmin = 24;      // pair stride >= 24: fewer resident FAST waves leave CUs to the overlapped stages (r3x:
-                              // stride 20 is faster alone, 0.772 vs 0.825 ms serial, but 66.6k vs 67.1k frames/s)
-    int desc_fb = 0;          // ORBX_DESC_FB: k_describe_fb (blur per keypoint in LDS, no k_blur7 / blurred pyramid)
-    int blur_lds = 0;         // ORBX_BLUR_LDS: k_blur7_lds (one load round per band, the blur from LDS)
-    int blur_dot2 = 1;        // ORBX_BLUR_DOT2: k_blur7 in vertical row pairs with v_dot2 column sums (0: one row at a time)
-    int band_g = 4;
-    int fast_oe = 1;          // ORBX_FAST_OE: E-only pair image (O taps by v_alignbit), 0 = E and O images
-    int fast_stop_after = 0;  // diagnostics only (ORBX_FAST_ABLATE): stop k_fast_cells after phase 1/2/3
+    static constexpr int kWaveWpg = 4;   // (1 or 2 waves per workgroup: faster alone, slower in the step)
+    int wave_twopass = 1;     // iniTh first, minTh only for the cells left empty (0: one pass at min(iniTh, minTh))
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
     size_t qt_lds = 0;        // k_quadtree dynamic LDS bytes of the node arrays (the key region follows at this offset)
     int qt_keys[2] = {0, 0};  // LDS-resident key capacity of the level-0 launch / the levels 1..n-1 launch
@@ -3410,9 +1659,6 @@ struct Extractor {
     BlurTile* d_tiles = nullptr;
     std::vector<ResizeTab> rtab;
     std::vector<ResizeVec> rvec;      // per level: vectorised tables (groups == 0 -> use rtab)
-    ResizeTail* d_tail = nullptr;     // k_resize_tail tables (device)
-    int tail_from = 0;                // ORBX_RESIZE_TAIL=l: levels >= l in one k_resize_tail launch (0 = off: measured slower)
-    int tail_lt = 0;                  // level the tail launch starts at for the reserved size (nlevels = none)
     std::vector<void*> rtab_mem;
     uint8_t* d_pyr = nullptr;         // pyramid set of the current / last call (a slot of d_pyr_ring)
     uint8_t* d_pyr_ring = nullptr;    // pyr_ring sets of max_batch pyramids: a caller that reads the pyramid of call
@@ -3421,8 +1667,6 @@ struct Extractor {
     uint8_t* d_blur = nullptr;
     uint32_t* d_cand_xy = nullptr;
     uint8_t* d_cand_s = nullptr;
-    uint32_t* d_cand2_xy = nullptr;   // k_fast_rows: the cells' minTh lists (the iniTh lists are d_cand_*)
-    uint8_t* d_cand2_s = nullptr;
     int* d_cell_cnt = nullptr;
     uint32_t* d_key_xy = nullptr;
     uint8_t* d_key_r = nullptr;
@@ -3449,7 +1693,7 @@ struct Extractor {
     // 4 describe start (after the join), 5 describe done.  Side stream: 6 start, 7 FAST level 0 done, 8 quadtree
     // level 0 done, 9 blur done (level 0, the wait for the pyramid, levels >= 1; pure blur time when serial).
     static constexpr int kEvents = 11;
-    static constexpr int kStageEv[ST_COUNT][2] = {{0, 1}, {10, 2}, {8, 9}, {2, 3}, {4, 5}, {6, 7}, {7, 8}};
+    static constexpr int kStageEv[kSpanStages][2] = {{0, 1}, {10, 2}, {8, 9}, {2, 3}, {4, 5}, {6, 7}, {7, 8}};
     struct EventSet { hipEvent_t ev[kEvents]; bool pending; };
     bool timing = false;
     std::vector<EventSet> tpool;
@@ -3460,11 +1704,23 @@ struct Extractor {
         if (!es.pending) return ORBX_OK;
         ORBX_HIP(hipEventSynchronize(es.ev[5]));
         ORBX_HIP(hipEventSynchronize(es.ev[9]));
-        for (int k = 0; k < ST_COUNT; ++k) {
+        for (int k = 0; k < kSpanStages; ++k) {
             float ms = 0;
             ORBX_HIP(hipEventElapsedTime(&ms, es.ev[kStageEv[k][0]], es.ev[kStageEv[k][1]]));
             stage_ms[k] += ms;
         }
+        // union of two spans [a, b] (level 0) and [c, d] (levels >= 1), all relative to a
+        auto busy = [&](int a, int b, int c, int d, double& acc) -> int {
+            float tb = 0, tc = 0, td = 0;
+            ORBX_HIP(hipEventElapsedTime(&tb, es.ev[a], es.ev[b]));
+            ORBX_HIP(hipEventElapsedTime(&tc, es.ev[a], es.ev[c]));
+            ORBX_HIP(hipEventElapsedTime(&td, es.ev[a], es.ev[d]));
+            const double overlap = std::max(0.0, (double)std::min(tb, td) - (double)std::max(0.f, tc));
+            acc += (double)tb + ((double)td - (double)tc) - overlap;
+            return ORBX_OK;
+        };
+        if (int st = busy(6, 7, 10, 2, stage_ms[ST_FAST_BUSY])) return st;
+        if (int st = busy(7, 8, 2, 3, stage_ms[ST_QUADTREE_BUSY])) return st;
         es.pending = false;
         timed_calls++;
         return ORBX_OK;
@@ -3516,8 +1772,7 @@ static void level_dims(const Extractor* e, int rows, int cols, int l, int* w, in
 
 void Extractor::free_buffers() {
     auto F = [](auto*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } };
-    F(d_levels); F(d_cells); F(d_tiles); F(d_bands); F(d_rowg); F(d_tail); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s);
-    F(d_cand2_xy); F(d_cand2_s); F(d_cell_cnt);
+    F(d_levels); F(d_cells); F(d_tiles); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
     F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
     F(d_kps); F(d_desc); F(d_cnt);
     if (h_in) { (void)hipHostFree(h_in); h_in = nullptr; }
@@ -3534,11 +1789,6 @@ void Extractor::free_buffers() {
 
 static size_t qt_lds_bytes(int cap, int scan_cap);
 
-static size_t fast_lds_bytes(int R, int C, int ps) {
-    // E + O pair images, int16 score map, u16 survivor list, two u16 kept-pixel key lists, 3 counters
-    return (size_t)fast_counter_off(R, C, ps) + 16;
-}
-
 template <typename T>
 static int dev_alloc(T** p, size_t count) {
     ORBX_HIP(hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T)));
@@ -3548,10 +1798,7 @@ static int dev_alloc(T** p, size_t count) {
 int Extractor::configure(int r, int c, int batch) {
     if (r == rows && c == cols && batch <= max_batch) return ORBX_OK;
     ORBX_HIP(hipSetDevice(device));
-    if (stream) ORBX_HIP(hipStreamSynchronize(stream));
-    if (side) ORBX_HIP(hipStreamSynchronize(side));
-    if (fastq) ORBX_HIP(hipStreamSynchronize(fastq));
-    if (int st0 = sync_calls()) return st0;                 // a describe still running on a caller's output stream
+    ORBX_HIP(hipDeviceSynchronize());                       // callers' streams may still read the buffers freed below
     for (int& k : slot_call) k = -1;
     last_call = -1;
     const int keep_batch = std::max(batch, (r == rows && c == cols) ? max_batch : 0);
@@ -3627,29 +1874,15 @@ int Extractor::configure(int r, int c, int batch) {
             for (int tx = 0; tx < (L.w + kBlurStrip - 1) / kBlurStrip; ++tx) tilev.push_back(BlurTile{l, tx, ty, 0});
     }
     ORBX_REQUIRE(cap < 32768 && cap < (1 << 20), ORBX_ERR_UNSUPPORTED, "node capacity %d too large", cap);
-    // k_fast_cells launches: level 0 (side stream) and levels 1..n-1, each sized for its own widest / tallest ROI
-    for (int k = 0; k < 2; ++k) {
-        FastLaunch& f = fast_launch[k];
-        f.cell0 = k == 0 ? 0 : lv[0].cell_end;
-        f.n = k == 0 ? lv[0].cell_end : (int)cellv.size() - lv[0].cell_end;
-        f.R = 8; f.C = 8;
-        for (int i = f.cell0; i < f.cell0 + f.n; ++i) { f.R = std::max(f.R, cellv[i].H); f.C = std::max(f.C, cellv[i].W); }
-        const int pairs = 2 * ((f.C + 5) / 4);                // E/O dwords one ROI row writes (8-byte chunks)
-        ORBX_REQUIRE(pairs <= 48, ORBX_ERR_UNSUPPORTED, "cell too wide");
-        f.ps = pairs <= 24 ? 24 : 48;
-        f.lds = fast_lds_bytes(f.R, f.C, f.ps);
-        if (f.lds > 64 * 1024)
-            ORBX_HIP(hipFuncSetAttribute(f.ps == 24 ? (const void*)k_fast_cells<24> : (const void*)k_fast_cells<48>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.lds));
-    }
-    // k_fast_wave launches: the same cell ranges, each wave's LDS slice sized for the launch's largest cell
+    // k_fast_wave launches: level 0 (side stream) and levels 1..n-1, each wave's LDS slice sized for the launch's
+    // largest cell.  Pair stride >= 24: fewer resident FAST waves leave CUs to the overlapped stages (r3x: stride 20 is
+    // faster alone, 0.772 vs 0.825 ms serial, but 66.6k vs 67.1k frames/s in the step)
     for (int k = 0; k < 2; ++k) {
         WaveLaunch& wl = wave_launch[k];
-        const FastLaunch& f = fast_launch[k];
-        wl.cell0 = f.cell0;
-        wl.n = f.n;
-        int rows = 8, sw = 8, np = 1, kcap = 1, psn = 4;
-        for (int i = f.cell0; i < f.cell0 + f.n; ++i) {
+        wl.cell0 = k == 0 ? 0 : lv[0].cell_end;
+        wl.n = k == 0 ? lv[0].cell_end : (int)cellv.size() - lv[0].cell_end;
+        int rows = 8, sw = 8, np = 1, kcap = 1, psn = 24;
+        for (int i = wl.cell0; i < wl.cell0 + wl.n; ++i) {
             const CellDev& cd = cellv[i];
             const int Wd = std::max(cd.W - 6, 0), Hd = std::max(cd.H - 6, 0);
             const int PR = (Wd + 1) / 2, QR = (PR + 3) / 4;
@@ -3660,86 +1893,18 @@ int Extractor::configure(int r, int c, int batch) {
             psn = std::max({psn, 4 * ((cd.W + 7) / 8), 4 * QR + 3});   // ROI chunk words; quad reads up to 4 * QR + 2
         }
         ORBX_REQUIRE(psn <= 40, ORBX_ERR_UNSUPPORTED, "cell too wide for k_fast_wave");
-        psn = std::max(psn, wave_psmin);                    // ORBX_FAST_PSMIN (A/B of the pair stride)
-        wl.ps = psn <= 20 ? 20 : psn <= 24 ? 24 : 40;
+        wl.ps = psn <= 24 ? 24 : 40;
         ORBX_REQUIRE(sw <= fastw_sw(wl.ps), ORBX_ERR_UNSUPPORTED, "k_fast_wave score-map row");
         sw = fastw_sw(wl.ps);
         wl.kcap = kcap;                                     // two u16 key lists inside the pair image: 4 * kcap bytes
         ORBX_REQUIRE(4 * kcap <= rows * wl.ps * 4, ORBX_ERR_UNSUPPORTED, "k_fast_wave key lists exceed the pair image");
         wl.lay = wave_lds(rows, sw, np, wl.ps);
-        const int bytes = wave_wpg * wl.lay.bytes;
+        const int bytes = kWaveWpg * wl.lay.bytes;
         ORBX_REQUIRE(bytes <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "k_fast_wave LDS %d B", bytes);
         if (bytes > 64 * 1024) {
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<20, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<24, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<40, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<24, kWaveWpg>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<40, kWaveWpg>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
         }
-    }
-    // k_fast_band: runs of up to band_g cells of one cell row (same level and iniY), the band ROI at most 139 columns
-    // (2 * cpr <= 72 pair dwords per row); level 0 / levels >= 1 as the two launches above
-    bandv.clear();
-    for (int l = 0; l < kMaxLevels; ++l) band_lvl0[l] = band_lvln[l] = 0;
-    for (int k = 0; k < 2; ++k) {
-        BandLaunch& b = band_launch[k];
-        b.band0 = (int)bandv.size();
-        const FastLaunch& f = fast_launch[k];
-        int rows = 8, sw = 8, np = 1, kmax = 1, gmax = 1;
-        for (int i = f.cell0; i < f.cell0 + f.n;) {
-            const CellDev& c0 = cellv[i];
-            const int wc = c0.W - 6;                        // every cell but a row's last: wCell
-            const int g = std::max(1, std::min({band_g, kBandMaxCells, (139 - 6) / std::max(wc, 1)}));
-            int n = 1;
-            while (n < g && i + n < f.cell0 + f.n && cellv[i + n].level == c0.level && cellv[i + n].y0 == c0.y0 &&
-                   cellv[i + n].x0 == c0.x0 + n * wc && cellv[i + n - 1].W == wc + 6)
-                ++n;
-            const CellDev& cl = cellv[i + n - 1];
-            BandDev bd{c0.level, i, n, c0.x0, c0.y0, cl.x0 + cl.W - c0.x0, c0.H, wc};
-            ORBX_REQUIRE(bd.W <= 139 && bd.H <= kMaxRoi && (bd.H - 6) * ((bd.W - 5) / 2) <= 32 * 256, ORBX_ERR_UNSUPPORTED,
-                         "FAST band too large");
-            bandv.push_back(bd);
-            const int Wd = bd.W - 6, Hd = bd.H - 6;
-            rows = std::max(rows, bd.H);
-            sw = std::max(sw, (Wd + 5) & ~1);
-            np = std::max(np, std::max(Hd, 0) * ((std::max(Wd, 0) + 1) >> 1));
-            for (int m = 0; m < n; ++m) kmax = std::max(kmax, cellv[i + m].slot_cap);
-            gmax = std::max(gmax, n);
-            i += n;
-        }
-        b.n = (int)bandv.size() - b.band0;
-        for (int q = b.band0; q < b.band0 + b.n; ++q) {
-            const int l = bandv[q].level;
-            if (band_lvln[l] == 0) band_lvl0[l] = q;
-            ++band_lvln[l];
-        }
-        b.kmax = kmax;
-        b.lay = band_lds(rows, sw, np, kmax, 72, gmax, fast_oe != 0);
-        if (b.lay.bytes > 64 * 1024) {
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_band<72, false>, hipFuncAttributeMaxDynamicSharedMemorySize, b.lay.bytes));
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_band<72, true>, hipFuncAttributeMaxDynamicSharedMemorySize, b.lay.bytes));
-        }
-    }
-    // k_fast_rows groups: runs of consecutive cells of one cell row (same level and iniY, abutting), <= 8 cells and
-    // <= 248 detection columns (lanes 1..62 of a wave; lanes 0 and 63 hold the +-3 halo)
-    rowgv.clear();
-    for (int k = 0; k < 2; ++k) {
-        RowsLaunch& rl = rows_launch[k];
-        rl.g0 = (int)rowgv.size();
-        const FastLaunch& f = fast_launch[k];
-        for (int i = f.cell0; i < f.cell0 + f.n;) {
-            const CellDev& c0 = cellv[i];
-            const int wc = c0.W - 6;
-            int n = 1;
-            while (n < 8 && i + n < f.cell0 + f.n && cellv[i + n].level == c0.level && cellv[i + n].y0 == c0.y0 &&
-                   cellv[i + n].x0 == c0.x0 + n * wc && cellv[i + n - 1].W == wc + 6 &&
-                   cellv[i + n].x0 + cellv[i + n].W - c0.x0 - 6 <= 248)
-                ++n;
-            const CellDev& cl = cellv[i + n - 1];
-            BandDev gd{c0.level, i, n, c0.x0, c0.y0, cl.x0 + cl.W - c0.x0, c0.H, std::max(wc, 1)};
-            ORBX_REQUIRE(gd.W - 6 <= 248 && gd.H <= 1024, ORBX_ERR_UNSUPPORTED, "FAST row group too large");
-            rowgv.push_back(gd);
-            i += n;
-        }
-        rl.n = (int)rowgv.size() - rl.g0;
     }
     int scap = cap;
     for (const LevelDev& L : lv) scap = std::max(scap, std::max(L.cell_end - L.cell_begin, L.nIni));
@@ -3780,10 +1945,6 @@ int Extractor::configure(int r, int c, int batch) {
     ORBX_HIP(hipMemcpy(d_levels, lv.data(), sizeof(LevelDev) * nlevels, hipMemcpyHostToDevice));
     if (!cellv.empty()) ORBX_HIP(hipMemcpy(d_cells, cellv.data(), sizeof(CellDev) * cellv.size(), hipMemcpyHostToDevice));
     ORBX_HIP(hipMemcpy(d_tiles, tilev.data(), sizeof(BlurTile) * tilev.size(), hipMemcpyHostToDevice));
-    if ((st = dev_alloc(&d_bands, bandv.size()))) return st;
-    if (!bandv.empty()) ORBX_HIP(hipMemcpy(d_bands, bandv.data(), sizeof(BandDev) * bandv.size(), hipMemcpyHostToDevice));
-    if ((st = dev_alloc(&d_rowg, rowgv.size()))) return st;
-    if (!rowgv.empty()) ORBX_HIP(hipMemcpy(d_rowg, rowgv.data(), sizeof(BandDev) * rowgv.size(), hipMemcpyHostToDevice));
 
     // ---- resize tables (pinned OpenCV 3.2 INTER_LINEAR fixed point), level l from level l-1
     rtab.assign(nlevels, ResizeTab{});
@@ -3861,27 +2022,6 @@ int Extractor::configure(int r, int c, int batch) {
         }
     }
 
-    // ---- k_resize_tail: levels tail_from .. nlevels-1 in one launch when every one has vectorised tables
-    tail_lt = nlevels;
-    if (tail_from >= 2 && tail_from < nlevels) {
-        bool ok = true;
-        for (int l = tail_from; l < nlevels; ++l) ok = ok && rvec[l].groups > 0;
-        if (ok) {
-            ResizeTail h{};
-            for (int l = tail_from; l < nlevels; ++l) {
-                h.t[l] = rvec[l];
-                h.sw[l] = lv[l - 1].w; h.sh[l] = lv[l - 1].h;
-                h.src_off[l] = lv[l - 1].pyr_off; h.dst_off[l] = lv[l].pyr_off;
-                h.dw[l] = lv[l].w; h.dh[l] = lv[l].h;
-                h.nstrips[l] = (lv[l].w + kResizeStrip - 1) / kResizeStrip;
-                h.nbands[l] = (lv[l].h + kResizeBand - 1) / kResizeBand;
-            }
-            if ((st = dev_alloc(&d_tail, 1))) return st;
-            ORBX_HIP(hipMemcpy(d_tail, &h, sizeof(h), hipMemcpyHostToDevice));
-            tail_lt = tail_from;
-        }
-    }
-
     // ---- batch buffers (HBM): pyramid + blurred pyramid + candidates + quadtree scratch
     const size_t B = (size_t)batch;
     if ((st = dev_alloc(&d_pyr_ring, (size_t)pyr_ring * B * pyr_size))) return st;
@@ -3890,8 +2030,6 @@ int Extractor::configure(int r, int c, int batch) {
     if ((st = dev_alloc(&d_blur, B * pyr_size))) return st;
     if ((st = dev_alloc(&d_cand_xy, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_cand_s, B * cand_stride))) return st;
-    if ((st = dev_alloc(&d_cand2_xy, B * cand_stride))) return st;
-    if ((st = dev_alloc(&d_cand2_s, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_cell_cnt, B * std::max<size_t>(cellv.size(), 1)))) return st;
     if ((st = dev_alloc(&d_key_xy, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_key_r, B * cand_stride))) return st;
@@ -3945,8 +2083,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     hipStream_t side = e->pipeline ? e->side : s;
     if (!e->pipeline) so = s;
     auto mark = [&](int k) {
-        const hipStream_t dq = (e->desc_side && side != s && so != s) ? side : so;
-        if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : (k == 4 || k == 5) ? dq : s);
+        if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : (k == 4 || k == 5) ? so : s);
     };
     // the previous call's describe (possibly on another stream) reads the kept keypoints and the blurred pyramid
     auto after_prev_describe = [&](hipStream_t q) -> int {
@@ -3958,63 +2095,27 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     while (t0 < (int)e->tilev.size() && e->tilev[t0].level == 0) ++t0;
     const int nt = (int)e->tilev.size();
     QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
-    auto fast = [&](hipStream_t q, const Extractor::FastLaunch& f) {
-        if (f.n <= 0) return;
-        if (e->fast_wave && !e->fast_stop_after) {
-            const Extractor::WaveLaunch& wl = e->wave_launch[&f == &e->fast_launch[0] ? 0 : 1];
-            if (wl.n <= 0) return;
-            const int wpg = e->wave_wpg, nwg = (wl.n * batch + wpg - 1) / wpg;
-            if (wl.ps == 24 && wpg == 4 && (e->wave_cells == 2 || e->wave_cells == 4)) {   // ORBX_FAST_CELLS
-                const int nwv = (wl.n * batch + e->wave_cells - 1) / e->wave_cells, nwgp = (nwv + 3) / 4;
-                auto kp = e->wave_cells == 2 ? k_fast_wave_p<4, 2> : k_fast_wave_p<4, 4>;
-                hipLaunchKernelGGL(kp, dim3(kXcds * xcd_chunk(nwgp)),
-                                   dim3(256), (size_t)4 * wl.lay.bytes, q, e->d_pyr, ps, e->d_levels, e->d_cells, wl.cell0,
-                                   wl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt,
-                                   ncells, batch, s0, wl.lay, wl.kcap, e->wave_twopass);
-                return;
-            }
-            auto kw = wl.ps == 20 ? (wpg == 4 ? k_fast_wave<20, 4> : wpg == 2 ? k_fast_wave<20, 2> : k_fast_wave<20, 1>)
-                    : wl.ps == 24 ? (wpg == 4 ? k_fast_wave<24, 4> : wpg == 2 ? k_fast_wave<24, 2> : k_fast_wave<24, 1>)
-                                  : (wpg == 4 ? k_fast_wave<40, 4> : wpg == 2 ? k_fast_wave<40, 2> : k_fast_wave<40, 1>);
-            hipLaunchKernelGGL(kw, dim3(kXcds * xcd_chunk(nwg)), dim3(64 * wpg), (size_t)wpg * wl.lay.bytes, q, e->d_pyr, ps,
-                               e->d_levels, e->d_cells, wl.cell0, wl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s,
-                               e->cand_stride, e->d_cell_cnt, ncells, batch, s0, wl.lay, wl.kcap, e->wave_twopass);
-            return;
-        }
-        if (e->fast_rows && !e->fast_stop_after) {
-            const Extractor::RowsLaunch& rl = e->rows_launch[&f == &e->fast_launch[0] ? 0 : 1];
-            if (rl.n <= 0) return;
-            hipLaunchKernelGGL(k_fast_rows<0>, dim3(kXcds * xcd_chunk((rl.n * batch + 3) / 4)), dim3(256), 0, q, e->d_pyr, ps,
-                               e->d_levels, e->d_cells, e->d_rowg, rl.g0, rl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s,
-                               e->d_cand2_xy, e->d_cand2_s, e->cand_stride, e->d_cell_cnt, ncells, batch, s0);
-            return;
-        }
-        if (e->fast_band && !e->fast_stop_after) {
-            const Extractor::BandLaunch& b = e->band_launch[&f == &e->fast_launch[0] ? 0 : 1];
-            auto kb = e->fast_oe ? k_fast_band<72, true> : k_fast_band<72, false>;
-            hipLaunchKernelGGL(kb, dim3(kXcds * xcd_chunk(b.n * batch)), dim3(256), b.lay.bytes, q, e->d_pyr, ps,
-                               e->d_levels, e->d_cells, e->d_bands, b.band0, b.n, e->iniTh, e->minTh, e->d_cand_xy,
-                               e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, batch, s0, b.lay, b.kmax);
-            return;
-        }
-        auto kern = f.ps == 24 ? k_fast_cells<24> : k_fast_cells<48>;
-        hipLaunchKernelGGL(kern, dim3(kXcds * xcd_chunk(f.n * batch)), dim3(256), f.lds, q, e->d_pyr, ps,
-                           e->d_levels, e->d_cells, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s, e->cand_stride,
-                           e->d_cell_cnt, ncells, batch, e->fast_stop_after, s0, f.R, f.C, f.cell0, f.n);
+    auto fast = [&](hipStream_t q, int k) {
+        const Extractor::WaveLaunch& wl = e->wave_launch[k];
+        if (wl.n <= 0) return;
+        constexpr int wpg = Extractor::kWaveWpg;
+        const int nwg = (wl.n * batch + wpg - 1) / wpg;
+        auto kw = wl.ps == 24 ? k_fast_wave<24, wpg> : k_fast_wave<40, wpg>;
+        hipLaunchKernelGGL(kw, dim3(kXcds * xcd_chunk(nwg)), dim3(64 * wpg), (size_t)wpg * wl.lay.bytes, q, e->d_pyr, ps,
+                           e->d_levels, e->d_cells, wl.cell0, wl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s,
+                           e->cand_stride, e->d_cell_cnt, ncells, batch, s0, wl.lay, wl.kcap, e->wave_twopass);
     };
     auto quadtree = [&](hipStream_t q, int lvl0, int n) {
         if (n <= 0) return;
-        // key capacity: the level-0 region when the launch covers level 0 (alone, or every level with qt_split 0),
-        // else the levels >= 1 region
-        const int kc = lvl0 == 0 ? e->qt_keys[0] : e->qt_keys[1];
+        const int kc = lvl0 == 0 ? e->qt_keys[0] : e->qt_keys[1];  // LDS key capacity: level 0 / levels >= 1
         hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds + 6 * (size_t)kc, q, e->d_levels, e->d_cells,
-                           e->d_cand_xy, e->d_cand_s, e->d_cand2_xy, e->d_cand2_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
+                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
                            e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err, lvl0,
                            (int)e->qt_lds, kc, seq);
     };
     auto blur = [&](hipStream_t q, int tile0, int n) {
-        if (n <= 0 || e->desc_fb) return;                           // k_describe_fb blurs per keypoint
-        hipLaunchKernelGGL(e->blur_lds ? k_blur7_lds : e->blur_dot2 ? k_blur7<true> : k_blur7<false>, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur, ps,
+        if (n <= 0) return;
+        hipLaunchKernelGGL(k_blur7, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur, ps,
                            e->d_levels, e->d_tiles, n, batch, s0, tile0);
     };
 
@@ -4023,67 +2124,35 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         ORBX_HIP(hipEventRecord(ce.fork, s));
         ORBX_HIP(hipStreamWaitEvent(side, ce.fork, 0));
     }
-    const bool split_fast = side != s && e->fast_split && e->fast_band && !e->fast_stop_after && e->fastq;
     auto resize_chain = [&]() -> int {
-      if (e->slot_call[slot] >= 0)                                  // this set's last reader
-          ORBX_HIP(hipStreamWaitEvent(s, e->cev[e->slot_call[slot]].desc, 0));
-      for (int l = 1; l < nl; ++l) {
-        if (l >= e->tail_lt) {                                      // the small levels: one launch
-            hipLaunchKernelGGL(k_resize_tail, dim3(batch), dim3(1024), 0, s, e->d_pyr, ps, e->tail_lt, nl, e->d_tail);
-            if (split_fast)
-                for (int m = l; m < nl; ++m) ORBX_HIP(hipEventRecord(e->ev_lvl[m], s));
-            break;
+        if (e->slot_call[slot] >= 0)                                // this set's last reader
+            ORBX_HIP(hipStreamWaitEvent(s, e->cev[e->slot_call[slot]].desc, 0));
+        for (int l = 1; l < nl; ++l) {
+            const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
+            const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
+            const LevelDev& L = e->lv[l];
+            if (e->rvec[l].groups > 0) {
+                const int nstrips = (L.w + kResizeStrip - 1) / kResizeStrip, nbands = (L.h + kResizeBand - 1) / kResizeBand;
+                const int nwg = (nstrips * nbands * batch + 3) / 4;
+                hipLaunchKernelGGL(k_resize4, dim3(kXcds * xcd_chunk(nwg)), dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis,
+                                   e->lv[l - 1].w, L.pyr_off, L.w, L.h, e->rvec[l], nstrips, nbands, batch);
+            } else {                                                // taps outside an 8-byte window: the scalar form
+                dim3 g((L.w + 255) / 256, L.h, batch);
+                hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis, L.pyr_off, L.w, L.h, e->rtab[l]);
+            }
         }
-        const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
-        const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
-        const LevelDev& L = e->lv[l];
-        if (e->rvec[l].groups > 0) {
-            const int nstrips = (L.w + kResizeStrip - 1) / kResizeStrip, nbands = (L.h + kResizeBand - 1) / kResizeBand;
-            const int nwg = (nstrips * nbands * batch + 3) / 4;
-            hipLaunchKernelGGL(k_resize4, dim3(kXcds * xcd_chunk(nwg)), dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis,
-                               e->lv[l - 1].w, L.pyr_off, L.w, L.h, e->rvec[l], nstrips, nbands, batch);
-        } else {
-            dim3 g((L.w + 255) / 256, L.h, batch);
-            hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, e->d_pyr, ps, src, sstep, sis, L.pyr_off, L.w, L.h, e->rtab[l]);
-        }
-        if (split_fast) ORBX_HIP(hipEventRecord(e->ev_lvl[l], s));
-      }
-      mark(1);
-      return ORBX_OK;
+        mark(1);
+        return ORBX_OK;
     };
     if (side == s) { int st = resize_chain(); if (st) return st; }  // serial: every stage contiguous on one stream
     // side stream, level 0 (reads only the caller's images)
     mark(6);
-    fast(side, e->fast_launch[0]);
+    fast(side, 0);
     mark(7);
-    const bool split = e->qt_split || side == s;
     if (int st = after_prev_describe(side)) return st;
-    if (split) quadtree(side, 0, nl > 0 ? 1 : 0);
-    else ORBX_HIP(hipEventRecord(ce.fast0, side));
+    quadtree(side, 0, nl > 0 ? 1 : 0);
     mark(8);
     blur(side, 0, t0);
-    // describe: slot table of the levels; level 0's keypoints on the side stream as soon as its quadtree and blur are
-    // done (beside the launch stream's FAST of levels 1..n-1), the rest on the launch stream after the join
-    SlotTable tab{};
-    for (int l = 0; l < nl; ++l) tab.out_off[l] = e->lv[l].out_off;
-    auto describe = [&](hipStream_t q, int slot0, int nslots, int write_count) {
-        if (nslots <= 0) return;
-        const int kpw = e->desc_fb ? 2 : e->desc_kpw;               // keypoints per wave (1, 2 or 4)
-        dim3 g(kXcds * xcd_chunk((nslots + 4 * kpw - 1) / (4 * kpw) * batch));
-        if (e->desc_fb) {
-            hipLaunchKernelGGL(k_describe_fb, g, dim3(256), 0, q, e->d_pyr, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
-                               e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, slot0, nslots, write_count,
-                               batch, s0, tab, seq, e->d_err);
-            return;
-        }
-        auto kern = kpw == 4 ? k_describe_m<4> : kpw == 2 ? k_describe_m<2> : k_describe;
-        hipLaunchKernelGGL(kern, g, dim3(256), 0, q, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy, e->d_lvl_r,
-                           e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, slot0, nslots, write_count, batch, s0,
-                           tab, seq, e->d_err);
-    };
-    const bool split_desc = side != s && split && e->desc_split && nl > 1;
-    const int d0_slots = split_desc ? e->lv[1].out_off : 0;           // level 0 = slots [0, out_off[1])
-    if (split_desc) describe(side, 0, d0_slots, 0);
     if (side != s) {
         int st = resize_chain();                                    // launch stream: levels 1..nl-1 of the pyramid
         if (st) return st;
@@ -4094,44 +2163,31 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     mark(9);
     if (side != s) ORBX_HIP(hipEventRecord(ce.join, side));
     mark(10);                                                       // launch stream: FAST, DistributeOctTree 1..nl-1
-    if (split_fast) {
-        const Extractor::BandLaunch& b = e->band_launch[1];
-        for (int l = 1; l < nl; ++l) {
-            if (e->band_lvln[l] <= 0) continue;
-            ORBX_HIP(hipStreamWaitEvent(e->fastq, e->ev_lvl[l], 0));
-            auto kb = e->fast_oe ? k_fast_band<72, true> : k_fast_band<72, false>;
-            hipLaunchKernelGGL(kb, dim3(kXcds * xcd_chunk(e->band_lvln[l] * batch)), dim3(256), b.lay.bytes, e->fastq,
-                               e->d_pyr, ps, e->d_levels, e->d_cells, e->d_bands, e->band_lvl0[l], e->band_lvln[l], e->iniTh,
-                               e->minTh, e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, ncells, batch, s0, b.lay, b.kmax);
-        }
-        ORBX_HIP(hipEventRecord(e->ev_fast1, e->fastq));
-        ORBX_HIP(hipStreamWaitEvent(s, e->ev_fast1, 0));
-    } else {
-        fast(s, e->fast_launch[1]);
-    }
+    fast(s, 1);
     mark(2);
     if (int st = after_prev_describe(s)) return st;
-    if (split) {
-        quadtree(s, 1, nl - 1);
-    } else {
-        ORBX_HIP(hipStreamWaitEvent(s, ce.fast0, 0));
-        quadtree(s, 0, nl);
-    }
+    quadtree(s, 1, nl - 1);
     mark(3);
-    // the descriptor stage: on the output stream, or (desc_side, with an output stream other than the launch stream)
-    // at the end of the side stream, so that the launch stream's next call (its resize chain) runs beside it without
-    // a further busy queue; the output stream then waits for it
-    const hipStream_t dq = (e->desc_side && side != s && so != s) ? side : so;
-    if (dq != s) {
+    // the descriptor stage on the output stream, once both streams are done; the next call's resize chain (launch
+    // stream) runs beside it
+    if (so != s) {
         ORBX_HIP(hipEventRecord(ce.front, s));
-        ORBX_HIP(hipStreamWaitEvent(dq, ce.front, 0));
+        ORBX_HIP(hipStreamWaitEvent(so, ce.front, 0));
     }
-    if (side != dq) ORBX_HIP(hipStreamWaitEvent(dq, ce.join, 0));
+    if (side != so) ORBX_HIP(hipStreamWaitEvent(so, ce.join, 0));
     mark(4);
-    describe(dq, d0_slots, e->out_stride - d0_slots, 1);
+    {
+        SlotTable tab{};
+        for (int l = 0; l < nl; ++l) tab.out_off[l] = e->lv[l].out_off;
+        const int nslots = e->out_stride;                           // every level's slots; the launch writes the counts
+        constexpr int kpw = 2;                                      // keypoints per wave
+        dim3 g(kXcds * xcd_chunk((nslots + 4 * kpw - 1) / (4 * kpw) * batch));
+        hipLaunchKernelGGL(k_describe_m<kpw>, g, dim3(256), 0, so, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy,
+                           e->d_lvl_r, e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, 0, nslots, 1, batch,
+                           s0, tab, seq, e->d_err);
+    }
     mark(5);
-    ORBX_HIP(hipEventRecord(ce.desc, dq));
-    if (dq != so) ORBX_HIP(hipStreamWaitEvent(so, ce.desc, 0));
+    ORBX_HIP(hipEventRecord(ce.desc, so));
     ce.used = true;
     e->slot_call[slot] = ci;
     e->last_call = ci;
@@ -4183,6 +2239,13 @@ int orbx_stream_create(int device, int priority, int cu_exclude, void** out) {
     return ORBX_OK;
 }
 
+int orbx_device_check(int device) {
+    ORBX_HIP(hipSetDevice(device));
+    ORBX_HIP(hipDeviceSynchronize());
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
 int orbx_stream_destroy(void* stream) {
     if (!stream) return ORBX_ERR_ARG;
     ORBX_HIP(hipStreamDestroy((hipStream_t)stream));
@@ -4214,41 +2277,15 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     const int cu_ex = std::getenv("ORBX_CU_EXCLUDE") ? std::atoi(std::getenv("ORBX_CU_EXCLUDE")) : 0;
     if (he == hipSuccess) he = create_stream_masked(&e->side, side_prio, cu_ex);
     for (auto& c : e->cev)
-        for (hipEvent_t* ev : {&c.fork, &c.pyr, &c.fast0, &c.join, &c.front, &c.desc})
+        for (hipEvent_t* ev : {&c.fork, &c.pyr, &c.join, &c.front, &c.desc})
             if (he == hipSuccess) he = hipEventCreateWithFlags(ev, hipEventDisableTiming);
-    // (every stream holds a hardware queue: streams beyond GPU_MAX_HW_QUEUES share queues and serialise, so the
-    // per-level FAST stream exists only when that schedule is on)
-    if (const char* fs = std::getenv("ORBX_FAST_SPLIT")) e->fast_split = std::atoi(fs) != 0;
-    if (he == hipSuccess && e->fast_split) he = hipStreamCreateWithFlags(&e->fastq, hipStreamNonBlocking);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fast1, hipEventDisableTiming);
-    for (int l = 0; l < kMaxLevels && he == hipSuccess; ++l) he = hipEventCreateWithFlags(&e->ev_lvl[l], hipEventDisableTiming);
     if (he != hipSuccess) {
         set_error("stream create: %s", hipGetErrorString(he));
         orbx_extractor_destroy(e);
         return ORBX_ERR_HIP;
     }
-    if (const char* ab = std::getenv("ORBX_FAST_ABLATE")) e->fast_stop_after = std::atoi(ab);
     if (const char* pl = std::getenv("ORBX_PIPELINE")) e->pipeline = std::atoi(pl) != 0;
-    if (const char* fb = std::getenv("ORBX_FAST_BAND")) e->fast_band = std::atoi(fb) != 0;
-    if (const char* fr = std::getenv("ORBX_FAST_ROWS")) e->fast_rows = std::atoi(fr) != 0;
-    if (const char* fw = std::getenv("ORBX_FAST_WAVE")) e->fast_wave = std::atoi(fw) != 0;
-    if (const char* fb = std::getenv("ORBX_DESC_FB")) e->desc_fb = std::atoi(fb) != 0;
-    if (const char* bd = std::getenv("ORBX_BLUR_DOT2")) e->blur_dot2 = std::atoi(bd) != 0;
-    if (const char* bl = std::getenv("ORBX_BLUR_LDS")) e->blur_lds = std::atoi(bl) != 0;
-    if (const char* pm = std::getenv("ORBX_FAST_PSMIN")) e->wave_psmin = std::atoi(pm);
     if (const char* tp = std::getenv("ORBX_FAST_TWOPASS")) e->wave_twopass = std::atoi(tp) != 0;
-    if (const char* fc = std::getenv("ORBX_FAST_CELLS")) e->wave_cells = std::atoi(fc);
-    if (const char* fp = std::getenv("ORBX_FAST_WPG")) e->wave_wpg = std::atoi(fp) == 1 ? 1 : std::atoi(fp) == 2 ? 2 : 4;
-    if (const char* fg = std::getenv("ORBX_FAST_G")) e->band_g = std::max(1, std::atoi(fg));
-    if (const char* fo = std::getenv("ORBX_FAST_OE")) e->fast_oe = std::atoi(fo) != 0;
-    if (const char* ds = std::getenv("ORBX_DESC_SPLIT")) e->desc_split = std::atoi(ds) != 0;
-    if (const char* dsd = std::getenv("ORBX_DESC_SIDE")) e->desc_side = std::atoi(dsd) != 0;
-    if (const char* dk = std::getenv("ORBX_DESC_KPW")) {
-        const int v = std::atoi(dk);
-        e->desc_kpw = v == 4 ? 4 : v == 1 ? 1 : 2;
-    }
-    if (const char* rt = std::getenv("ORBX_RESIZE_TAIL")) e->tail_from = std::atoi(rt);
-    if (const char* qs = std::getenv("ORBX_QT_SPLIT")) e->qt_split = std::atoi(qs) != 0;
     if (const char* sw = std::getenv("ORBX_DEBUG_SKIP_DESC_WAIT")) e->dbg_skip_desc_wait = std::atoi(sw) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
@@ -4261,22 +2298,17 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
 int orbx_extractor_destroy(orbx_extractor* e) {
     if (!e) return ORBX_OK;
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
-    if (e->side) (void)hipStreamSynchronize(e->side);
-    if (e->fastq) (void)hipStreamSynchronize(e->fastq);
-    (void)e->sync_calls();                                  // a describe on the caller's stream
+    // Every stream of the device, not only the extractor's own: callers' streams read its pyramid ring and outputs
+    // (the stereo SAD step reads orbx_extractor_pyramid_device's levels) and hipFree does not wait for them.
+    (void)hipDeviceSynchronize();
     e->free_buffers();
     for (auto& es : e->tpool)
         for (auto& ev : es.ev) (void)hipEventDestroy(ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->side) (void)hipStreamDestroy(e->side);
     for (auto& c : e->cev)
-        for (hipEvent_t ev : {c.fork, c.pyr, c.fast0, c.join, c.front, c.desc})
+        for (hipEvent_t ev : {c.fork, c.pyr, c.join, c.front, c.desc})
             if (ev) (void)hipEventDestroy(ev);
-    if (e->fastq) (void)hipStreamDestroy(e->fastq);
-    if (e->ev_fast1) (void)hipEventDestroy(e->ev_fast1);
-    for (auto& ev : e->ev_lvl)
-        if (ev) (void)hipEventDestroy(ev);
     delete e;
     return ORBX_OK;
 }
@@ -4321,10 +2353,7 @@ int orbx_extractor_set_pyramid_ring(orbx_extractor* e, int n) {
     if (n == e->pyr_ring) return ORBX_OK;
     const int r = e->rows, c = e->cols, b = e->max_batch;
     ORBX_HIP(hipSetDevice(e->device));
-    if (e->stream) ORBX_HIP(hipStreamSynchronize(e->stream));
-    if (e->side) ORBX_HIP(hipStreamSynchronize(e->side));
-    if (e->fastq) ORBX_HIP(hipStreamSynchronize(e->fastq));
-    if (int st = e->sync_calls()) return st;
+    ORBX_HIP(hipDeviceSynchronize());                       // callers' streams may still read the pyramid ring
     e->free_buffers();
     for (int& k : e->slot_call) k = -1;
     e->last_call = -1;
@@ -4446,7 +2475,6 @@ int orbx_extractor_status(orbx_extractor* e, int* flags, int reset) {
     ORBX_HIP(hipSetDevice(e->device));
     if (e->stream) ORBX_HIP(hipStreamSynchronize(e->stream));
     if (e->side) ORBX_HIP(hipStreamSynchronize(e->side));
-    if (e->fastq) ORBX_HIP(hipStreamSynchronize(e->fastq));
     if (int st = e->sync_calls()) return st;
     hipStream_t q = e->side ? e->side : e->own();
     int h = 0;
@@ -4502,7 +2530,7 @@ int orbx_extractor_level_device(orbx_extractor* e, int index, int level, const u
 
 int orbx_extractor_copy_blurred_level(orbx_extractor* e, int index, int level, uint8_t* dst, size_t dst_step) {
     ORBX_REQUIRE(e && dst, ORBX_ERR_ARG, "null argument");
-    ORBX_REQUIRE(e->d_blur && !e->desc_fb && e->last_src0.p && level >= 0 && level < e->nlevels && index >= 0 &&
+    ORBX_REQUIRE(e->d_blur && e->last_src0.p && level >= 0 && level < e->nlevels && index >= 0 &&
                      index < e->last_batch,
                  ORBX_ERR_ARG, "no blurred level for index %d level %d", index, level);
     const int w = e->lv[level].w, h = e->lv[level].h;
@@ -4549,7 +2577,6 @@ const char* orbx_extractor_stage_name(int s) { return (s >= 0 && s < ST_COUNT) ?
 int orbx_debug_qt_prof(unsigned long long* out) {   // 2 x 64 stamps (diagnostics build only)
     ORBX_HIP(hipDeviceSynchronize());
     ORBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_qtprof), sizeof(orbx::g_qtprof)));
-    ORBX_HIP(hipMemcpyFromSymbol(out + 128, HIP_SYMBOL(orbx::g_fbprof), sizeof(orbx::g_fbprof)));
     return ORBX_OK;
 }
 #endif

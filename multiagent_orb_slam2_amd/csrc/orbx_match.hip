@@ -1308,16 +1308,16 @@ struct Matcher {
     size_t scratch_bytes = 0;
     std::recursive_mutex mtx;
     hipEvent_t last_op = nullptr;
-    bool last_op_set = false;
+    bool last_op_set = false;            // last_op covers scratch work that may still be running
+    hipStream_t last_stream = nullptr;   // the stream last_op was recorded on
     int reserve(size_t bytes) { return reserve_on(bytes, own()); }
-    // order 'on' after the previous scratch user; grow the buffer (after that user has finished) if needed
+    // order 'on' after the previous scratch user (skipped on the same stream: stream order holds); grow the buffer
+    // (after every user has finished) if needed
     int reserve_on(size_t bytes, hipStream_t on) {
-        if (last_op_set) ORBX_HIP(hipStreamWaitEvent(on, last_op, 0));
+        if (last_op_set && last_stream != on) ORBX_HIP(hipStreamWaitEvent(on, last_op, 0));
         if (bytes <= scratch_bytes) return ORBX_OK;
         if (scratch) {
-            if (last_op_set) ORBX_HIP(hipEventSynchronize(last_op));
-            if (stream) (void)hipStreamSynchronize(stream);
-            (void)hipStreamSynchronize(on);
+            ORBX_HIP(hipDeviceSynchronize());   // earlier users on any stream done before the buffer goes away
             (void)hipFree(scratch);
             scratch = nullptr;
         }
@@ -1387,7 +1387,15 @@ struct orbx_matcher : public orbx::Matcher {};
 int orbx::matcher_device(const orbx_matcher* m) { return m->device; }
 void orbx::matcher_acquire(orbx_matcher* m) { m->mtx.lock(); }
 void orbx::matcher_release(orbx_matcher* m, hipStream_t s, bool used) {
-    if (used && m->last_op && hipEventRecord(m->last_op, s) == hipSuccess) m->last_op_set = true;
+    // an idle stream at the end (host-form calls synchronise) leaves nothing to wait for: no marker packet
+    if (used && m->last_op) {
+        if (hipStreamQuery(s) == hipSuccess) {
+            m->last_op_set = false;
+        } else if (hipEventRecord(m->last_op, s) == hipSuccess) {
+            m->last_op_set = true;
+            m->last_stream = s;
+        }
+    }
     m->mtx.unlock();
 }
 int orbx::matcher_scratch(orbx_matcher* m, size_t bytes, void** base, void** stream) {
@@ -1428,8 +1436,7 @@ int orbx_matcher_create(float nnratio, int checkOri, int device, orbx_matcher** 
 int orbx_matcher_destroy(orbx_matcher* m) {
     if (!m) return ORBX_OK;
     (void)hipSetDevice(m->device);
-    if (m->stream) (void)hipStreamSynchronize(m->stream);
-    if (m->last_op_set) (void)hipEventSynchronize(m->last_op);   // a device call on a caller's stream
+    (void)hipDeviceSynchronize();                                // device calls on callers' streams use the scratch
     if (m->last_op) (void)hipEventDestroy(m->last_op);
     if (m->scratch) (void)hipFree(m->scratch);
     if (m->stream) (void)hipStreamDestroy(m->stream);

@@ -415,7 +415,7 @@ int orbx_vocab_load_text(const char* path, int device, orbx_vocab** out) {
 int orbx_vocab_destroy(orbx_vocab* v) {
     if (!v) return ORBX_OK;
     (void)hipSetDevice(v->device);
-    if (v->stream) (void)hipStreamSynchronize(v->stream);
+    (void)hipDeviceSynchronize();              // device calls on callers' streams read the tree and the scratch
     if (v->mem) (void)hipFree(v->mem);
     if (v->scratch) (void)hipFree(v->scratch);
     if (v->stream) (void)hipStreamDestroy(v->stream);
@@ -469,7 +469,10 @@ int orbx_vocab_transform(orbx_vocab* v, const uint8_t* desc, int n, int levelsup
     const size_t N = (size_t)n;
     const size_t bytes = al256(32 * N) + 3 * al256(4 * N) + 2 * al256(8 * N) + 3 * al256(4 * (N + 1)) + al256(64);
     if (bytes > v->scratch_bytes) {
-        if (v->scratch) (void)hipFree(v->scratch);
+        if (v->scratch) {
+            ORBX_HIP(hipDeviceSynchronize());      // an earlier call on any stream may still read the old buffer
+            (void)hipFree(v->scratch);
+        }
         v->scratch = nullptr;
         ORBX_HIP(hipMalloc(&v->scratch, bytes));
         v->scratch_bytes = bytes;

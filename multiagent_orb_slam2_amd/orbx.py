@@ -34,21 +34,34 @@ class OrbxError(RuntimeError):
         self.code = code
 
 
-# Every live library object, in creation order.  At interpreter exit they are destroyed newest first by close_all
-# (registered with atexit after torch's own handlers, so it runs before them): each destroy waits for its own streams
-# and events and then frees its device memory while the HIP runtime is fully up, instead of in whatever order module
-# teardown and garbage collection reach them.
-_LIVE: list = []
+# Every live library object, keyed by creation number.  At interpreter exit they are destroyed newest first by
+# close_all: each destroy drains the device and then frees its memory while the HIP runtime is fully up, instead of in
+# whatever order module teardown and garbage collection reach them.  close_all is registered with atexit on the first
+# registration, after importing torch (whose own exit handlers are then registered first and run after ours: atexit
+# is last in, first out).  Dead objects drop out of the table through their weakref callback.
+_LIVE: dict = {}
+_NEXT = [0]
+_ATEXIT = [False]
 
 
 def _register(obj):
-    _LIVE.append(weakref.ref(obj))
+    if not _ATEXIT[0]:
+        try:
+            import torch  # noqa: F401  (its atexit handlers first, so close_all runs before them)
+        except ImportError:
+            pass
+        atexit.register(close_all)
+        _ATEXIT[0] = True
+    k = _NEXT[0]
+    _NEXT[0] += 1
+    _LIVE[k] = weakref.ref(obj, lambda _r, k=k: _LIVE.pop(k, None))
 
 
 def close_all():
     """Destroy every live library object (newest first).  Called at exit; callable earlier."""
-    while _LIVE:
-        o = _LIVE.pop()()
+    for k in sorted(_LIVE, reverse=True):
+        r = _LIVE.pop(k, None)
+        o = r() if r is not None else None
         if o is not None:
             try:
                 o.close()
@@ -56,7 +69,10 @@ def close_all():
                 pass
 
 
-atexit.register(close_all)
+def device_check(device: int = 0):
+    """Drain the device and raise OrbxError if it holds a pending HIP error (a kernel fault, an illegal address):
+    bench.py and smoke() call it last, so a fault during or after the timed work cannot end in exit status 0."""
+    _check(load_library().orbx_device_check(int(device)))
 
 
 class FeatVec(C.Structure):
@@ -168,6 +184,7 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_extractor_create.argtypes = [i32, f32, i32, i32, i32, i32, C.POINTER(vp)]
     lib.orbx_stream_create.argtypes = [i32, i32, i32, C.POINTER(vp)]
     lib.orbx_stream_destroy.argtypes = [vp]
+    lib.orbx_device_check.argtypes = [i32]
     lib.orbx_matcher_create.argtypes = [f32, i32, i32, C.POINTER(vp)]
     for name in ("orbx_extractor_destroy", "orbx_matcher_destroy", "orbx_extractor_get_levels"):
         getattr(lib, name).argtypes = [vp]

@@ -1,14 +1,15 @@
-# Round-3 profile of the bench's timed command: kernel trace + stats (-> kernel_share.json: the dominant kernel),
+# Profile of the bench's timed command (round 4: the bench steps only -- --alone-reps 0 and every side block off, so the
+# trace holds exactly STEPS steps and launches_per_step is exact): kernel trace + stats (-> kernel_share.json: the dominant kernel),
 # FETCH_SIZE and WRITE_SIZE passes (-> pmc_traffic.json, per-step HBM bytes per kernel family), two SQ passes
 # (-> sq_summary.json, VALU per step).  One --pmc pass per counter set, nothing else traced in a PMC pass.
-# usage: bash scripts/prof_r3.sh TAG [bench args]; outputs under gpurun_out/TAG/ (copy the summaries to profiles/).
+# usage: bash scripts/prof_r4.sh TAG [bench args]; outputs under gpurun_out/TAG/ (copy the summaries to profiles/).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${1:-prof}; shift
 ARGS=${*:-""}
 CFG=kitti; ROWS=375; COLS=1242
 case "$ARGS" in *euroc*) CFG=euroc; ROWS=480; COLS=752;; esac
-B="python3 $R/bench.py --steps 20 --warmup 5 --cpu-seconds 0 --host-api-frames 0 --no-c3 --no-cd --host-fed-steps 0 $ARGS"
+B="python3 $R/bench.py --steps 20 --warmup 5 --cpu-seconds 0 --host-api-frames 0 --no-c3 --no-cd --host-fed-steps 0 --alone-reps 0 $ARGS"
 STEPS=28   # 3 store-fill steps + 5 warmup + 20 timed, every one the same kernels
 IMG=${IMG:-512}   # images per extractor launch: 2 x bench --batch (default 256)
 O=gpurun_out/$TAG

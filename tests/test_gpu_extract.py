@@ -118,16 +118,14 @@ def test_batch_device_equals_single(gpu):
         assert np.array_equal(kb, k1) and np.array_equal(desc[i, :n], d1)
 
 
-@pytest.mark.parametrize("ring,desc_side", [(1, 0), (2, 0), (2, 1)])
-def test_split_streams_back_to_back(gpu, monkeypatch, ring, desc_side):
+@pytest.mark.parametrize("ring", [1, 2])
+def test_split_streams_back_to_back(gpu, ring):
     """orbx_extract_batch_device_split: calls issued back to back without a host sync, the descriptor stage on a
     second stream, so call k+1's front half overlaps call k's descriptor stage.  Every call must equal the
-    single-image host API (the extractor orders its own buffer reuse across calls).  desc_side: the descriptor stage
-    at the end of the extractor's side stream (ORBX_DESC_SIDE=1), the output stream waiting for it."""
+    single-image host API (the extractor orders its own buffer reuse across calls)."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
-    monkeypatch.setenv("ORBX_DESC_SIDE", str(desc_side))
     batches = [np.stack([S.kitti_like_image(300 + 7 * b + i) for i in range(3)]) for b in range(4)]
     ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
     ex.set_pyramid_ring(ring)
@@ -149,15 +147,13 @@ def test_split_streams_back_to_back(gpu, monkeypatch, ring, desc_side):
             assert np.array_equal(kb, k1) and np.array_equal(desc[i, :n], d1)
 
 
-@pytest.mark.parametrize("kpw", [1, 2, 4])
-def test_describe_keypoints_per_wave(gpu, monkeypatch, kpw):
-    """k_describe (one keypoint per wave) and k_describe_m (2 or 4 per wave, levels straddling a wave) give the same
-    bits: ORBX_DESC_KPW picks the form at extractor creation.  Batched, so waves also straddle images' slot ends."""
+def test_describe_batched_slot_ranges(gpu):
+    """k_describe_m (2 keypoints per wave, levels straddling a wave) in a batch, so waves also straddle images' slot
+    ends; then an odd feature budget and level count: level slot ranges of odd lengths."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
-    monkeypatch.setenv("ORBX_DESC_KPW", str(kpw))
     imgs = np.stack([S.kitti_like_image(400 + i) for i in range(3)])
     ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
     kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).cuda())
@@ -169,25 +165,19 @@ def test_describe_keypoints_per_wave(gpu, monkeypatch, kpw):
         kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
         assert np.array_equal(kb, ref["kps"]) and np.array_equal(desc[i, :n], ref["desc"]), _diff_report(
             kb, desc[i, :n], ref["kps"], ref["desc"])
-    # odd feature budget and level count: level slot ranges of odd lengths
     _check(S.kitti_like_image(410, rows=240, cols=333), nfeatures=777, nlevels=5, scale=1.3)
 
 
-@pytest.mark.parametrize("form", ["dot2", "row", "lds"])
-def test_blurred_pyramid_bit_exact(gpu, monkeypatch, form):
+def test_blurred_pyramid_bit_exact(gpu):
     """Every pixel of every blurred level -- not only the windows around keypoints that the descriptor tests see --
     equals the oracle's GaussianBlur(7x7, sigma 2, REFLECT_101) of the oracle's pyramid level
     (ORBextractor.cc:1085-1086): interior strips, strips at a level's left / right edge (REFLECT_101 columns by byte
-    selectors in k_blur7<true>), levels under 12 columns, bottom rows, saturation (a constant 255 image blurs to 255 with
-    taps summing to 257), batched (image index > 0).  Forms: k_blur7 in vertical row pairs (default), one row at a time,
-    and k_blur7_lds."""
+    selectors), levels under 12 columns, bottom rows, saturation (a constant 255 image blurs to 255 with taps summing to
+    257), batched (image index > 0)."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
-    monkeypatch.setenv("ORBX_BLUR_DOT2", "0" if form == "row" else "1")
-    monkeypatch.setenv("ORBX_BLUR_LDS", "1" if form == "lds" else "0")
-    monkeypatch.setenv("ORBX_DESC_FB", "0")
     for shape in ((375, 1242), (377, 1243), (480, 752), (1000, 200), (40, 40), (61, 97)):
         imgs = np.stack([S.kitti_like_image(700 + shape[1], rows=shape[0], cols=shape[1]),
                          S.uniform_noise_image(701, rows=shape[0], cols=shape[1]) if shape == (375, 1242)
@@ -207,26 +197,19 @@ def test_blurred_pyramid_bit_exact(gpu, monkeypatch, form):
                     f"shape {shape} image {i} level {l} ({lv.shape}): {len(bad)} pixels differ, first {bad[:3].tolist()}")
 
 
-@pytest.mark.parametrize("form", ["band", "band_blur1row", "rows", "wave", "wave_blurlds", "wave_1pass", "wave20", "wave2",
-                                  "wave1", "wave_cells2", "wave_cells4"])
+@pytest.mark.parametrize("form", ["twopass", "onepass", "serial"])
 def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
-    """Every FAST form -- k_fast_band (LDS band image, pre-test and survivor list), k_fast_rows (one wave per cell
-    row in registers, every pixel scored, both thresholds' lists) and k_fast_wave (one wave per cell, no barrier; 4, 2
-    or 1 waves per workgroup) -- is bit-exact against the oracle (and so is k_blur7 in both forms: vertical row pairs with
-    v_dot2 column sums, the default, one row at a time, and k_blur7_lds staged through LDS): KITTI size, odd, tall and tiny sizes, uniform noise (most
-    pixels survive the pre-test) and another parameter set, batched."""
+    """k_fast_wave (one wave per cell, no barrier) is bit-exact against the oracle in both of its pass modes -- iniTh
+    first with a minTh pass only for the cells left empty (default), and one pass at min(iniTh, minTh)
+    (ORBX_FAST_TWOPASS=0) -- and with every stage on one stream (ORBX_PIPELINE=0, the roofline_alone schedule): KITTI
+    size, odd, tall and tiny sizes, uniform noise (most pixels survive the pre-test), iniTh < minTh and another parameter
+    set (pair stride 40 on 1.3-scaled cells), batched."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
-    monkeypatch.setenv("ORBX_FAST_ROWS", "1" if form == "rows" else "0")
-    monkeypatch.setenv("ORBX_FAST_WAVE", "1" if form.startswith("wave") else "0")
-    monkeypatch.setenv("ORBX_FAST_WPG", {"wave1": "1", "wave2": "2"}.get(form, "4"))
-    monkeypatch.setenv("ORBX_FAST_PSMIN", "20" if form == "wave20" else "24")   # pair stride 20 on KITTI-size cells
-    monkeypatch.setenv("ORBX_FAST_TWOPASS", "0" if form == "wave_1pass" else "1")   # iniTh and minTh in one pass
-    monkeypatch.setenv("ORBX_BLUR_DOT2", "0" if form == "band_blur1row" else "1")   # k_blur7 one row at a time
-    monkeypatch.setenv("ORBX_BLUR_LDS", "1" if form == "wave_blurlds" else "0")     # k_blur7_lds
-    monkeypatch.setenv("ORBX_FAST_CELLS", {"wave_cells2": "2", "wave_cells4": "4"}.get(form, "1"))   # k_fast_wave_p
+    monkeypatch.setenv("ORBX_FAST_TWOPASS", "0" if form == "onepass" else "1")
+    monkeypatch.setenv("ORBX_PIPELINE", "0" if form == "serial" else "1")
     for shape, nf, kw in (((375, 1242), 2000, {}), ((377, 1243), 800, {}), ((120, 160), 300, {}),
                           ((1000, 200), 800, {}), ((40, 40), 100, {}), ((500, 500), 1000, {}),
                           ((480, 752), 1500, dict(nlevels=5, scale=1.3, ini=25, mn=10)),
@@ -246,39 +229,3 @@ def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
             kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
             assert np.array_equal(kb, ref["kps"]) and np.array_equal(desc[i, :n], ref["desc"]), _diff_report(
                 kb, desc[i, :n], ref["kps"], ref["desc"])
-
-
-@pytest.mark.parametrize("fast_wave", [0, 1])
-def test_describe_fused_blur_bit_exact(gpu, monkeypatch, fast_wave):
-    """k_describe_fb (the 7x7 GaussianBlur done per keypoint on its raw 43x48 window in LDS, no blurred pyramid) gives
-    the oracle's descriptors bit for bit: windows that cross the level border (REFLECT_101 on the raw coordinates) occur
-    on every level of these images; small and odd sizes, uniform noise, another parameter set, batched."""
-    import torch
-
-    import multiagent_orb_slam2_amd as pkg
-    from oracle import oracle as O
-    monkeypatch.setenv("ORBX_DESC_FB", "1")
-    monkeypatch.setenv("ORBX_FAST_WAVE", str(fast_wave))
-    for shape, nf, kw in (((375, 1242), 2000, {}), ((377, 1243), 800, {}), ((40, 40), 100, {}), ((120, 160), 300, {}),
-                          ((1000, 200), 800, {}), ((480, 752), 1500, dict(nlevels=5, scale=1.3, ini=25, mn=10)),
-                          ((375, 1242), 2000, dict(noise=True))):
-        if kw.get("noise"):
-            imgs = np.stack([S.uniform_noise_image(960 + i) for i in range(3)])
-        else:
-            imgs = np.stack([S.kitti_like_image(920 + i, rows=shape[0], cols=shape[1]) for i in range(3)])
-        ex = pkg.ORBextractor(nf, kw.get("scale", 1.2), kw.get("nlevels", 8), kw.get("ini", 20), kw.get("mn", 7))
-        kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).cuda())
-        torch.cuda.synchronize()
-        kps, desc, cnt = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
-        for i in range(len(imgs)):
-            ref = O.extract(imgs[i], nfeatures=nf, scale_factor=kw.get("scale", 1.2), nlevels=kw.get("nlevels", 8),
-                            ini_th=kw.get("ini", 20), min_th=kw.get("mn", 7))
-            n = int(cnt[i])
-            kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
-            assert np.array_equal(kb, ref["kps"]) and np.array_equal(desc[i, :n], ref["desc"]), _diff_report(
-                kb, desc[i, :n], ref["kps"], ref["desc"])
-        # the host API (one image per call) takes the same path
-        k1, d1 = ex(imgs[0])
-        ref = O.extract(imgs[0], nfeatures=nf, scale_factor=kw.get("scale", 1.2), nlevels=kw.get("nlevels", 8),
-                        ini_th=kw.get("ini", 20), min_th=kw.get("mn", 7))
-        assert np.array_equal(k1, ref["kps"]) and np.array_equal(d1, ref["desc"])

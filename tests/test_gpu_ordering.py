@@ -41,15 +41,14 @@ def _mismatches(outs, ref):
     return bad
 
 
-@pytest.mark.parametrize("ring,desc_side", [(1, 0), (2, 0), (2, 1)])
-def test_stalled_describe_orders_next_call(gpu, monkeypatch, ring, desc_side):
+@pytest.mark.parametrize("ring", [1, 2])
+def test_stalled_describe_orders_next_call(gpu, ring):
     """A 15 ms spin on the output stream right before each call: call k's describe starts long after call k+1's
     quadtree, blur and (ring 1) resize were enqueued.  Every result must equal the host API and the canary must stay
     clear -- i.e. every cross-call buffer reuse waits for the describe that reads it."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
-    monkeypatch.setenv("ORBX_DESC_SIDE", str(desc_side))
     batches = _batches()
     ref = _reference(batches)
     ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)

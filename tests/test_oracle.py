@@ -180,7 +180,7 @@ def test_oracle_regression_fixtures():
 
 
 def test_model_f16_score_form():
-    """k_fast_band's f16 score form (orbx_extract.hip fast_score2_f16): pixels stored as f16 1024 + value, differences,
+    """k_fast_wave's f16 score form (orbx_extract.hip fast_score_from_taps_f16): pixels stored as f16 1024 + value, differences,
     arc minima / maxima and the final max in f16, the score raised to -1 when below.  Every intermediate is an integer
     below 2048, so f16 is exact; the only change is max(s, -1), which alters no corner (s >= T >= 1) and no NMS
     outcome (a neighbour below T never blocks).  Checked against the integer score map on textured and noise images."""
