@@ -648,8 +648,9 @@ struct orbx_kfdb {
     // streams they come from (DbOp below).
     std::recursive_mutex mtx;
     hipEvent_t last_op = nullptr;        // the last enqueue on database state, on its caller's stream
-    bool last_op_set = false;            // last_op covers work that may still be running
-    hipStream_t last_stream = nullptr;   // the stream last_op was recorded on
+    bool last_op_set = false;            // last_op recorded after the previous operation (multi-stream mode)
+    bool have_last = false, multi = false;
+    hipStream_t last_stream = nullptr;   // the previous operation's stream
     void* score_stage = nullptr;   // orbx_kfdb_score's own staging (never shared with a detect in flight elsewhere)
     size_t score_stage_bytes = 0;
     std::vector<uint32_t> seq;     // host mirror of membership (add order)
@@ -666,10 +667,10 @@ struct orbx_kfdb {
 
 namespace {
 
-// One database operation: the lock for its duration; its stream (if any) ordered after the previous operation.  The
-// wait is skipped when the previous operation ran on the same stream (stream order already holds), and no event is
-// recorded when the stream is idle at the end (a host-form call that synchronised: nothing left to wait for) -- so
-// the per-call path pays neither a barrier packet nor a marker (+3 us per launch, host API 2118 -> 1309/s).
+// One database operation: the lock for its duration; its stream (if any) ordered after the previous operation.  A
+// database driven from one stream needs only stream order, so nothing is enqueued for it; the first operation from a
+// second stream drains the device once and switches to events ('multi': every operation records last_op, the next
+// one on another stream waits for it) -- the per-call path pays no barrier or marker packet.
 struct DbOp {
     orbx_kfdb* db;
     hipStream_t s;
@@ -677,16 +678,19 @@ struct DbOp {
     std::unique_lock<std::recursive_mutex> lk;
     hipError_t err = hipSuccess;
     DbOp(orbx_kfdb* d, hipStream_t st, bool uses_stream) : db(d), s(st), on_stream(uses_stream), lk(d->mtx) {
-        if (on_stream && db->last_op_set && db->last_stream != s) err = hipStreamWaitEvent(s, db->last_op, 0);
+        if (!on_stream || !db->have_last || db->last_stream == s) return;
+        if (!db->multi) {
+            err = hipDeviceSynchronize();
+            db->multi = true;
+        } else if (db->last_op_set) {
+            err = hipStreamWaitEvent(s, db->last_op, 0);
+        }
     }
     ~DbOp() {
         if (!on_stream) return;
-        if (hipStreamQuery(s) == hipSuccess) {
-            db->last_op_set = false;
-        } else if (hipEventRecord(db->last_op, s) == hipSuccess) {
-            db->last_op_set = true;
-            db->last_stream = s;
-        }
+        if (db->multi) db->last_op_set = hipEventRecord(db->last_op, s) == hipSuccess;
+        db->last_stream = s;
+        db->have_last = true;
     }
 };
 #define ORBX_DBOP(db, stream)                                                                                          \

@@ -1302,19 +1302,30 @@ struct Matcher {
     std::once_flag stream_once;
     hipStream_t own() { return lazy_stream(stream, stream_once, device); }
     // growable device scratch.  Contract: one call at a time holds the matcher ('mtx', MatcherLease), and a call's
-    // stream waits for the previous scratch user ('last_op', recorded on that call's stream) before its own kernels
-    // touch the scratch -- device calls on different streams are ordered, not racing on one buffer.
+    // stream is ordered after the previous scratch user before its own kernels touch the scratch -- device calls on
+    // different streams are ordered, not racing on one buffer.  A matcher used from one stream only (the common case:
+    // the reference builds an ORBmatcher per call site) needs nothing beyond stream order, so nothing is enqueued for
+    // it: the first call from a second stream drains the device once, and from then on ('multi') every call records
+    // 'last_op' on its stream and the next call on another stream waits for it (the per-call event wait
+    // and record cost ~3 us per launch).
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
     std::recursive_mutex mtx;
     hipEvent_t last_op = nullptr;
-    bool last_op_set = false;            // last_op covers scratch work that may still be running
-    hipStream_t last_stream = nullptr;   // the stream last_op was recorded on
+    bool last_op_set = false;            // last_op recorded after the previous call (multi-stream mode)
+    bool have_last = false, multi = false;
+    hipStream_t last_stream = nullptr;   // the previous call's stream
     int reserve(size_t bytes) { return reserve_on(bytes, own()); }
-    // order 'on' after the previous scratch user (skipped on the same stream: stream order holds); grow the buffer
-    // (after every user has finished) if needed
+    // order 'on' after the previous scratch user; grow the buffer (after every user has finished) if needed
     int reserve_on(size_t bytes, hipStream_t on) {
-        if (last_op_set && last_stream != on) ORBX_HIP(hipStreamWaitEvent(on, last_op, 0));
+        if (have_last && last_stream != on) {
+            if (!multi) {
+                ORBX_HIP(hipDeviceSynchronize());
+                multi = true;
+            } else if (last_op_set) {
+                ORBX_HIP(hipStreamWaitEvent(on, last_op, 0));
+            }
+        }
         if (bytes <= scratch_bytes) return ORBX_OK;
         if (scratch) {
             ORBX_HIP(hipDeviceSynchronize());   // earlier users on any stream done before the buffer goes away
@@ -1387,14 +1398,10 @@ struct orbx_matcher : public orbx::Matcher {};
 int orbx::matcher_device(const orbx_matcher* m) { return m->device; }
 void orbx::matcher_acquire(orbx_matcher* m) { m->mtx.lock(); }
 void orbx::matcher_release(orbx_matcher* m, hipStream_t s, bool used) {
-    // an idle stream at the end (host-form calls synchronise) leaves nothing to wait for: no marker packet
-    if (used && m->last_op) {
-        if (hipStreamQuery(s) == hipSuccess) {
-            m->last_op_set = false;
-        } else if (hipEventRecord(m->last_op, s) == hipSuccess) {
-            m->last_op_set = true;
-            m->last_stream = s;
-        }
+    if (used) {
+        if (m->multi && m->last_op) m->last_op_set = hipEventRecord(m->last_op, s) == hipSuccess;
+        m->last_stream = s;
+        m->have_last = true;
     }
     m->mtx.unlock();
 }
