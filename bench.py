@@ -213,7 +213,8 @@ class CpuAgent:
 
     def new_mappoints(self, a, kf):
         """SearchForTriangulation against the previous TRI_NEIGHBOURS keyframes with ORBmatcher(0.6, false), then the
-        distinctive descriptor of every keypoint's observation list (itself + its matches), as the GPU stage."""
+        distinctive descriptor of every new MapPoint (a keypoint with its first matching neighbour: two observations,
+        LocalMapping.cc:440-448), as the GPU stage."""
         O, n = self.O, len(a["desc"])
         d1, mp1, fv1 = kf[0], kf[2], kf[3]
         ur = np.full(n, -1, np.float32)
@@ -230,11 +231,15 @@ class CpuAgent:
                                                 False, False)
             rows.append(d2)
             m12s.append(m12)
-        hit = np.stack([np.ones(n, bool)] + [m >= 0 for m in m12s], 1)
-        parts = np.stack([d1] + [r[np.maximum(m, 0)] for r, m in zip(rows, m12s)], 1)   # (n, 1 + k, 32)
-        off = np.zeros(n + 1, np.int32)
-        off[1:] = np.cumsum(hit.sum(1))
-        O.distinctive_descriptors_flat(parts[hit], off)
+        if not m12s:
+            return
+        hit = np.stack([m >= 0 for m in m12s], 1)                              # (n, k)
+        has = hit.any(1)
+        first = np.argmax(hit, 1)
+        nb = np.stack([r[np.maximum(m, 0)] for r, m in zip(rows, m12s)], 1)      # (n, k, 32)
+        parts = np.stack([nb[np.arange(n), first], d1], 1)[has]                 # (MapPoints, 2, 32)
+        off = np.arange(0, 2 * len(parts) + 1, 2, dtype=np.int32)
+        O.distinctive_descriptors_flat(parts.reshape(-1, 32), off)
 
 
 def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds, tri=True):

@@ -305,7 +305,7 @@ int orbx_distinctive_descriptors_store_device(orbx_matcher* m, const orbx_kf_sto
  * the descriptor with the least median distance to the others (the reference's first strict minimum of
  * vDists[(size_t)(0.5*(N-1))] over rows of the all-pairs Hamming table), -1 for a MapPoint without observations
  * (the reference returns, leaving mDescriptor unchanged).  out_desc[p] (may be NULL) = that descriptor
- * (mDescriptor).  Host form and device forms; the _store_ form reads observation o as keypoint obs[2o+1] of
+ * (mDescriptor; the device forms write a zero row for a MapPoint without observations).  Host form and device forms; the _store_ form reads observation o as keypoint obs[2o+1] of
  * keyframe slot obs[2o] of a device keyframe store (e.g. MapFusion's packet ring). */
 int orbx_distinctive_descriptors(orbx_matcher* m, const uint8_t* desc, const int32_t* offsets, int n_mappoints, int32_t* best,
                                  uint8_t* out_desc);
@@ -345,11 +345,14 @@ int orbx_search_for_triangulation_pairs_device(orbx_matcher* m, const orbx_kf_st
                                                int nlevels, int only_stereo, int32_t* d_match12, int32_t* d_nmatches,
                                                void* stream);
 
-/* orbx_distinctive_descriptors for the MapPoints of new keyframes after the batched SearchForTriangulation above
- * (LocalMapping.cc:440-448 and the fused points of SearchInNeighbors, :528-533), lists read from the match table
- * itself: MapPoint j*capacity + i = keypoint i of keyframe d_new_slots[j], observed there first and then at
- * d_match12[(j*n_neighbours + k)*capacity + i] of slot d_neighbours[j*n_neighbours + k] for every k in order with a
- * neighbour (>= 0) and a match (>= 0).  n_neighbours <= 63.  d_best[mp] = list index; d_out_desc[mp] (or NULL). */
+/* ComputeDistinctiveDescriptors of the MapPoints CreateNewMapPoints makes after the batched SearchForTriangulation
+ * above (LocalMapping.cc:440-448), read from the match table itself: keypoint i of keyframe d_new_slots[j] becomes
+ * MapPoint j*capacity + i with the first neighbour k (in order, d_neighbours[j*n_neighbours + k] >= 0) whose match
+ * d_match12[(j*n_neighbours + k)*capacity + i] >= 0 -- a keypoint becomes a MapPoint at most once -- and observations
+ * [(that neighbour, its match), (the new keyframe, i)] in creation order (mObservations is keyed by KeyFrame*; pinned
+ * to creation order).  Two descriptors: both medians are 0, row 0 wins (MapPoint.cc:293-306).  d_best[mp]
+ * = 0, or -1 without a MapPoint (a zero row written then); d_out_desc[mp] (or NULL) = the chosen descriptor.
+ * n_neighbours <= 64. */
 int orbx_distinctive_descriptors_neighbours_device(orbx_matcher* m, const orbx_kf_store* store, const int32_t* d_new_slots,
                                                    const int32_t* d_neighbours, int n_new, int n_neighbours,
                                                    const int32_t* d_match12, int32_t* d_best, uint8_t* d_out_desc,
@@ -443,6 +446,63 @@ int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* param
 int orbx_proj_search(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid, const orbx_proj_query* queries,
                      const uint8_t* qdesc, int nq, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,
                      const uint8_t* blocked, int n, int32_t* q_idx, int32_t* q_dist, int32_t* owner, int* n_matches);
+
+/* The projection step in front of the search: the per-MapPoint arithmetic the reference runs before it calls
+ * GetFeaturesInArea, producing the orbx_proj_query the search consumes.
+ *   ORBX_PROJ_LASTFRAME  SearchByProjection(Frame&, const Frame&, th, bMono)   src/ORBmatcher.cc:1363-1392, :1418-1426
+ *   ORBX_PROJ_MAPPOINTS  Frame::isInFrustum (src/Frame.cc:269-325, viewingCosLimit) + the window of
+ *                        SearchByProjection(Frame&, vpMapPoints, th)           src/ORBmatcher.cc:62-71, :92-98
+ *   ORBX_PROJ_FUSE       Fuse(KeyFrame*, vpMapPoints, th)                       src/ORBmatcher.cc:854-893
+ * A point that fails a test (negative depth, outside the image, outside the scale-invariance distances, viewing angle)
+ * gets ORBX_QF_SKIP; a point whose flags already hold ORBX_QF_SKIP (NULL, bad, outlier, already matched, IsInKeyFrame)
+ * stays skipped.  Pinned arithmetic: Rcw * X + tcw as float products summed left to right, cv::norm and
+ * Mat::dot with float products accumulated in double, PredictScale (src/MapPoint.cc:389-421) with a double log. */
+typedef struct orbx_map_point {
+    float x, y, z;                /* GetWorldPos */
+    float nx, ny, nz;             /* GetNormal (MAPPOINTS, FUSE) */
+    float min_dist, max_dist;     /* mfMinDistance, mfMaxDistance (GetMin/MaxDistanceInvariance apply 0.8 / 1.2) */
+    float angle;                  /* LASTFRAME: LastFrame.mvKeysUn[i].angle (the rotation histogram) */
+    int32_t octave;               /* LASTFRAME: LastFrame.mvKeys[i].octave */
+    int32_t flags;                /* ORBX_QF_*: carried into the query (BLOCKS = Observations() > 0) */
+    int32_t pad;
+} orbx_map_point;                 /* 48 bytes */
+
+/* The view a set of MapPoints is projected into (the current Frame, or the KeyFrame of a Fuse). */
+typedef struct orbx_view {
+    float R[9], t[3], Ow[3];      /* Rcw (row-major), tcw, camera centre (GetCameraCenter / mOw) */
+    float fx, fy, cx, cy, bf;     /* intrinsics and mbf */
+    float min_x, max_x, min_y, max_y;   /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    float th;                     /* the call's th (LASTFRAME radius factor, MAPPOINTS factor if != 1, Fuse radius) */
+    float view_cos_limit;         /* MAPPOINTS: isInFrustum's viewingCosLimit (Tracking::SearchLocalPoints: 0.5) */
+    int32_t level_mode;           /* LASTFRAME: 1 bForward, -1 bBackward, 0 neither (from the two poses, :1344-1352) */
+    int32_t pad;
+} orbx_view;                      /* 112 bytes */
+
+/* n_views projections: view v projects point set s = d_view_points ? d_view_points[v] : v (points at
+ * d_points + s * capacity, d_counts[s] of them) into d_views[v]; its queries are written at d_queries + v * capacity,
+ * the rows past the set's count as ORBX_QF_SKIP (so a search may take nq = capacity).  Many views of one point set is
+ * Fuse's shape (one KeyFrame's MapPoints into each of its neighbours, LocalMapping.cc:486-496).  scale_factors:
+ * mvScaleFactors (nlevels); log_scale_factor: mfLogScaleFactor.  d_found (optional, laid out as the queries): points
+ * with d_found[v * capacity + i] >= 0 are skipped -- the MapPoints the current frame already matched
+ * (Tracking::SearchLocalPoints skips them, src/Tracking.cc:1160-1182). */
+int orbx_proj_project_device(orbx_matcher* m, int mode, const orbx_map_point* d_points, const int32_t* d_counts, int n_views,
+                             int capacity, const orbx_view* d_views, const int32_t* d_view_points, const float* scale_factors,
+                             int nlevels, float log_scale_factor, const int32_t* d_found, orbx_proj_query* d_queries,
+                             void* stream);
+
+/* MapPoints of stereo frames (Frame::UnprojectStereo src/Frame.cc:666-680 + MapPoint::MapPoint(Pos, pMap, pFrame, idxF)
+ * src/MapPoint.cc:47-68, as Tracking::StereoInitialization / CreateNewKeyFrame / UpdateLastFrame create them):
+ * for keypoint i of frame b with depth z > 0, X = Rwc * ((u - cx) z / fx, (v - cy) z / fy, z) + Ow, the normal
+ * (X - Ow) / |X - Ow|, mfMaxDistance = |X - Ow| * mvScaleFactors[octave], mfMinDistance = max / mvScaleFactors[nlevels - 1],
+ * octave and angle from the keypoint, flags = 'flags'; a keypoint without depth gets ORBX_QF_SKIP.  Keypoints at
+ * d_kps + b * capacity (d_counts[b] each), depths at d_depth + b * capacity; d_twc: per frame Rwc (9, row-major) then
+ * Ow (3) -- 12 floats; camera = {fx, fy, cx, cy}.  Output at d_points + b * capacity. */
+int orbx_stereo_mappoints_device(orbx_matcher* m, const orbx_keypoint* d_kps, const float* d_depth, const int32_t* d_counts,
+                                 int batch, int capacity, const float* d_twc, const float* camera, const float* scale_factors,
+                                 int nlevels, int flags, orbx_map_point* d_points, void* stream);
+/* Host form: one point set, one view. */
+int orbx_proj_project(orbx_matcher* m, int mode, const orbx_map_point* points, int n, const orbx_view* view,
+                      const float* scale_factors, int nlevels, float log_scale_factor, orbx_proj_query* queries);
 
 /* ------------------------------------------------------------------------------------------------
  * DBoW2 vocabulary — replaces TemplatedVocabulary<FORB>::transform (Thirdparty/DBoW2/DBoW2/

@@ -1164,7 +1164,7 @@ struct DistinctArgs {
     const int32_t* off;       // [M + 1]
     int M;
     int32_t* best;            // [M] index in the MapPoint's observation list, -1 when it has none
-    uint8_t* out;             // [M][32] the chosen descriptor (mDescriptor), or NULL
+    uint8_t* out;             // [M][32] the chosen descriptor (mDescriptor; zeros without observations), or NULL
     int nbx;
 };
 
@@ -1181,8 +1181,9 @@ __global__ __launch_bounds__(256) void k_distinctive(DistinctArgs A) {
     if (mp >= A.M) return;
     const int ln = lane_id();
     const int o0 = A.off[mp], N = A.off[mp + 1] - o0;
-    if (N <= 0) {
+    if (N <= 0) {                                          // no observation: best -1, a zero descriptor row
         if (ln == 0) A.best[mp] = -1;
+        if (A.out && ln < 8) reinterpret_cast<uint32_t*>(A.out + 32 * (size_t)mp)[ln] = 0u;
         return;
     }
     const int need = (N - 1) / 2 + 1;          // rank of vDists[(size_t)(0.5 * (N - 1))], 1-based
@@ -1223,18 +1224,24 @@ __global__ __launch_bounds__(256) void k_distinctive(DistinctArgs A) {
     }
 }
 
-// The MapPoints of new keyframes with observation lists read straight from CreateNewMapPoints' match tables
-// (no CSR built): MapPoint (j, i) = keypoint i of new keyframe j, observed there (lane 0) and at match12[j][k][i] of
-// neighbour k (lane 1 + k) when matched -- multiagent.neighbour_observations' list order.  One wave per MapPoint;
-// lane t holds observation t, list position = its rank among the observing lanes.  N <= 2: every row's median is its
-// own zero distance, so the first row wins without a distance (MapPoint.cc:296-306).
+// The MapPoints of new keyframes, read straight from CreateNewMapPoints' match tables (no CSR built).  In the reference
+// a keypoint of the new keyframe becomes a MapPoint at most once, from the first neighbour whose match triangulates
+// (LocalMapping.cc:244-448: later neighbours' searches skip keypoints that already hold a MapPoint); the new MapPoint
+// has exactly two observations, the neighbour's keypoint and the new keyframe's (:440-441), and
+// ComputeDistinctiveDescriptors over two descriptors takes row 0: both rows' medians are vDists[0] = 0
+// (MapPoint.cc:293-306), so the descriptor is that of the first observation in mObservations order -- a map keyed by
+// KeyFrame*, pinned to creation order (the neighbour, the older keyframe, first; the same pin as the quadtree's
+// heap-address tie).  Here the triangulation itself (pose checks, SVD) runs on the map side, so the first
+// neighbour with a match stands for the first that triangulates.  MapPoint (j, i): list [(neighbour k*, match),
+// (new keyframe, i)] with k* the first neighbour in order with a match; no match -> no MapPoint (best = -1, nothing
+// written).  multiagent.neighbour_observations builds the same lists as a CSR.  One wave per MapPoint.
 struct DistinctNbArgs {
     orbx_kf_store S;
     const int32_t* new_slots;   // [n]
     const int32_t* nb;          // [n][nn] neighbour slots, -1 = none
     const int32_t* m12;         // [n][nn][capacity]
     int n, nn, M;
-    int32_t* best;              // [M] list index
+    int32_t* best;              // [M] list index (0), -1 without a MapPoint
     uint8_t* out;               // [M][32] or NULL
     int nbx;
 };
@@ -1247,44 +1254,22 @@ __global__ __launch_bounds__(256) void k_distinctive_nb(DistinctNbArgs A) {
     const int ln = lane_id(), cap = A.S.capacity;
     const int j = mp / cap, i = mp - j * cap;
     int slot = -1, kp = -1;
-    if (ln == 0) { slot = A.new_slots[j]; kp = i; }
-    else if (ln <= A.nn) {
-        const int nbk = A.nb[j * A.nn + ln - 1];
+    if (ln < A.nn) {                                       // lane k: neighbour k
+        const int nbk = A.nb[j * A.nn + ln];
         if (nbk >= 0) {
-            const int m = A.m12[((size_t)j * A.nn + ln - 1) * cap + i];
+            const int m = A.m12[((size_t)j * A.nn + ln) * cap + i];
             if (m >= 0) { slot = nbk; kp = m; }
         }
     }
-    const bool has = kp >= 0;
-    const uint64_t mask = __ballot(has);
-    const int N = __builtin_popcountll(mask);
-    const int pos = __builtin_popcountll(mask & ((1ull << ln) - 1ull));
-    int win = 0;                                           // lane of the chosen observation
-    if (N > 2) {
-        uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
-        if (has) load_desc(A.S.desc + (size_t)slot * A.S.desc_stride + 32 * (size_t)kp, a0, a1);
-        const int need = (N - 1) / 2 + 1;
-        int lo = 0, hi = 256;
-#pragma unroll 1
-        for (int it = 0; it < 9; ++it) {
-            const int mid = (lo + hi) >> 1;
-            int cnt = 0;
-            for (uint64_t mq = mask; mq; mq &= mq - 1) {
-                const int t = __builtin_ctzll(mq);
-                uint4 x0, x1;
-                x0.x = __builtin_amdgcn_readlane(a0.x, t); x0.y = __builtin_amdgcn_readlane(a0.y, t);
-                x0.z = __builtin_amdgcn_readlane(a0.z, t); x0.w = __builtin_amdgcn_readlane(a0.w, t);
-                x1.x = __builtin_amdgcn_readlane(a1.x, t); x1.y = __builtin_amdgcn_readlane(a1.y, t);
-                x1.z = __builtin_amdgcn_readlane(a1.z, t); x1.w = __builtin_amdgcn_readlane(a1.w, t);
-                cnt += hamming256(a0, a1, x0, x1) <= mid;
-            }
-            if (cnt >= need) hi = mid; else lo = mid + 1;
-        }
-        const uint32_t key = has ? (((uint32_t)lo << 20) | ((uint32_t)pos << 8) | (uint32_t)ln) : 0xffffffffu;
-        win = (int)(wave_min_u32(key) & 0xff);
+    const uint64_t mask = __ballot(kp >= 0);
+    if (!mask) {                                           // no MapPoint: best -1, a zero descriptor row
+        if (ln == 0) A.best[mp] = -1;
+        if (A.out && ln < 8) reinterpret_cast<uint32_t*>(A.out + 32 * (size_t)mp)[ln] = 0u;
+        return;
     }
-    const int wslot = __builtin_amdgcn_readlane(slot, win), wkp = __builtin_amdgcn_readlane(kp, win);
-    if (ln == 0) A.best[mp] = __builtin_amdgcn_readlane(pos, win);
+    const int first = __builtin_ctzll(mask);               // the first neighbour with a match
+    const int wslot = __builtin_amdgcn_readlane(slot, first), wkp = __builtin_amdgcn_readlane(kp, first);
+    if (ln == 0) A.best[mp] = 0;                           // list row 0: the neighbour's observation
     if (A.out && ln < 8) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(A.S.desc + (size_t)wslot * A.S.desc_stride + 32 * (size_t)wkp);
         reinterpret_cast<uint32_t*>(A.out + 32 * (size_t)mp)[ln] = src[ln];
@@ -1951,7 +1936,7 @@ int orbx_distinctive_descriptors_neighbours_device(orbx_matcher* m, const orbx_k
                                                    const int32_t* d_neighbours, int n_new, int n_neighbours,
                                                    const int32_t* d_match12, int32_t* d_best, uint8_t* d_out_desc,
                                                    void* stream) {
-    ORBX_REQUIRE(m && store && n_new >= 0 && n_neighbours >= 0 && n_neighbours < kWave &&
+    ORBX_REQUIRE(m && store && n_new >= 0 && n_neighbours >= 0 && n_neighbours <= kWave &&
                      (n_new == 0 || (d_new_slots && d_best && (n_neighbours == 0 || (d_neighbours && d_match12)))),
                  ORBX_ERR_ARG, "bad argument");
     ORBX_REQUIRE(store->desc && ((uintptr_t)store->desc % 16) == 0 && store->desc_stride % 16 == 0 && store->capacity > 0,

@@ -15,6 +15,8 @@
 //                  the unique fixed point is the sequential result; real calls settle in a few rounds.
 //   k_proj_init    SearchForInitialization (src/ORBmatcher.cc:407-522), whose exclusion depends on the distance
 //                  of the current owner (stealing): one wave walks the queries in order, lanes over candidates.
+//   k_project      the per-MapPoint projection in front of the searches (LASTFRAME :1363-1392, isInFrustum
+//                  Frame.cc:269-325 + the MAPPOINTS window :62-71, Fuse :854-893): one thread per point.
 // Float arithmetic is written with explicit __f*_rn (no contraction) in the reference's operation order.
 // =====================================================================================================
 #include <hip/hip_runtime.h>
@@ -381,6 +383,144 @@ __global__ __launch_bounds__(64) void k_proj_init(orbx_proj_params P, orbx_grid 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Projection step (include/orbx.h orbx_proj_project): one thread per MapPoint, the reference's operation order for
+// each caller, pinned as the oracle (oracle/proj_oracle.cpp orc_project): Rcw * X + tcw as float products summed left
+// to right, cv::norm / Mat::dot with float products accumulated in double, PredictScale's log in double.
+// ---------------------------------------------------------------------------------------------
+struct ProjScales { float s[32]; };
+
+__device__ __forceinline__ int predict_scale(float max_dist, float dist, float log_sf, int nlevels) {   // MapPoint.cc:389-421
+    const float ratio = __fdiv_rn(max_dist, dist);
+    int n = (int)ceil(__ddiv_rn(log((double)ratio), (double)log_sf));
+    if (n < 0) n = 0;
+    else if (n >= nlevels) n = nlevels - 1;
+    return n;
+}
+
+__global__ __launch_bounds__(256) void k_project(int mode, const orbx_map_point* __restrict__ pts, const int32_t* __restrict__ counts,
+                                                 int n_fixed, int capacity, const orbx_view* __restrict__ views,
+                                                 const int32_t* __restrict__ view_points, ProjScales sc, int nlevels,
+                                                 float log_sf, const int32_t* __restrict__ found,
+                                                 orbx_proj_query* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, vi = blockIdx.y;
+    if (i >= capacity) return;
+    const int set = view_points ? view_points[vi] : vi;
+    const int n = counts ? min(counts[set], capacity) : n_fixed;
+    const orbx_view& V = views[vi];
+    orbx_proj_query q;
+    q.x = q.y = q.r = 0.0f;
+    q.min_level = -1; q.max_level = -1;
+    q.ur = 0.0f; q.ur_tol = -1.0f; q.angle = 0.0f;
+    q.level = -1;
+    q.flags = ORBX_QF_SKIP;
+    orbx_proj_query* o = out + (size_t)vi * capacity + i;
+    if (i >= n) { *o = q; return; }                                    // rows past the set's count: skipped
+    const orbx_map_point p = pts[(size_t)set * capacity + i];
+    auto dot3 = [](float a, float b, float c, float x, float y, float z, float t) {   // ((a x + b y) + c z) + t
+        return __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(a, x), __fmul_rn(b, y)), __fmul_rn(c, z)), t);
+    };
+    const float xc = dot3(V.R[0], V.R[1], V.R[2], p.x, p.y, p.z, V.t[0]);
+    const float yc = dot3(V.R[3], V.R[4], V.R[5], p.x, p.y, p.z, V.t[1]);
+    const float zc = dot3(V.R[6], V.R[7], V.R[8], p.x, p.y, p.z, V.t[2]);
+    if ((p.flags & ORBX_QF_SKIP) || (found && found[(size_t)vi * capacity + i] >= 0)) { *o = q; return; }
+    if (mode == ORBX_PROJ_LASTFRAME) {
+        const float invzc = (float)__ddiv_rn(1.0, (double)zc);                           // :1368
+        const float u = __fadd_rn(__fmul_rn(__fmul_rn(V.fx, xc), invzc), V.cx);
+        const float v = __fadd_rn(__fmul_rn(__fmul_rn(V.fy, yc), invzc), V.cy);
+        if (invzc < 0 || u < V.min_x || u > V.max_x || v < V.min_y || v > V.max_y) { *o = q; return; }
+        const int oct = p.octave;
+        const float radius = __fmul_rn(V.th, sc.s[oct]);                                   // :1384
+        q.x = u; q.y = v; q.r = radius;
+        if (V.level_mode > 0) { q.min_level = oct; q.max_level = -1; }                     // :1388-1393
+        else if (V.level_mode < 0) { q.min_level = 0; q.max_level = oct; }
+        else { q.min_level = oct - 1; q.max_level = oct + 1; }
+        q.ur = __fsub_rn(u, __fmul_rn(V.bf, invzc));                                        // :1418-1426
+        q.ur_tol = radius;
+        q.angle = p.angle;
+        q.level = oct;
+    } else {
+        float u, v, invz;
+        if (zc < 0.0f) { *o = q; return; }
+        if (mode == ORBX_PROJ_MAPPOINTS) {                                                  // Frame::isInFrustum
+            invz = __fdiv_rn(1.0f, zc);
+            u = __fadd_rn(__fmul_rn(__fmul_rn(V.fx, xc), invz), V.cx);
+            v = __fadd_rn(__fmul_rn(__fmul_rn(V.fy, yc), invz), V.cy);
+            if (u < V.min_x || u > V.max_x || v < V.min_y || v > V.max_y) { *o = q; return; }
+        } else {                                                                            // Fuse :857-871
+            invz = __fdiv_rn(1.0f, zc);
+            u = __fadd_rn(__fmul_rn(V.fx, __fmul_rn(xc, invz)), V.cx);
+            v = __fadd_rn(__fmul_rn(V.fy, __fmul_rn(yc, invz)), V.cy);
+            if (!(u >= V.min_x && u < V.max_x && v >= V.min_y && v < V.max_y)) { *o = q; return; }
+        }
+        const float maxD = __fmul_rn(1.2f, p.max_dist), minD = __fmul_rn(0.8f, p.min_dist);  // MapPoint.cc:377-387
+        const float POx = __fsub_rn(p.x, V.Ow[0]), POy = __fsub_rn(p.y, V.Ow[1]), POz = __fsub_rn(p.z, V.Ow[2]);
+        const float ss = __fadd_rn(__fadd_rn(__fmul_rn(POx, POx), __fmul_rn(POy, POy)), __fmul_rn(POz, POz));
+        const float dist = (float)__dsqrt_rn((double)ss);                                 // cv::norm
+        if (dist < minD || dist > maxD) { *o = q; return; }
+        const double dot = __dadd_rn(__dadd_rn((double)__fmul_rn(POx, p.nx), (double)__fmul_rn(POy, p.ny)),
+                                     (double)__fmul_rn(POz, p.nz));                          // PO.dot(Pn)
+        const int pred = predict_scale(p.max_dist, dist, log_sf, nlevels);
+        if (mode == ORBX_PROJ_MAPPOINTS) {
+            const float viewCos = (float)__ddiv_rn(dot, (double)dist);                       // Frame.cc:308-311
+            if (viewCos < V.view_cos_limit) { *o = q; return; }
+            float r = (double)viewCos > 0.998 ? 2.5f : 4.0f;                                 // RadiusByViewingCos
+            if (V.th != 1.0f) r = __fmul_rn(r, V.th);
+            q.x = u; q.y = v; q.r = __fmul_rn(r, sc.s[pred]);
+            q.min_level = pred - 1; q.max_level = pred;
+            q.ur = __fsub_rn(u, __fmul_rn(V.bf, invz));                                     // mTrackProjXR
+            q.ur_tol = __fmul_rn(r, sc.s[pred]);
+        } else {
+            if (dot < __dmul_rn(0.5, (double)dist)) { *o = q; return; }                    // :887-888
+            q.x = u; q.y = v; q.r = __fmul_rn(V.th, sc.s[pred]);
+            q.min_level = pred - 1; q.max_level = pred;
+            q.ur = __fsub_rn(u, __fmul_rn(V.bf, invz));
+        }
+        q.level = pred;
+    }
+    q.flags = p.flags & ~ORBX_QF_SKIP;
+    *o = q;
+}
+
+// MapPoints of stereo frames: Frame::UnprojectStereo (src/Frame.cc:666-680) and the Frame form of the MapPoint
+// constructor (src/MapPoint.cc:47-68).  One thread per keypoint.  Pinned as the projection: Rwc * x3Dc + Ow as float
+// products summed left to right; cv::norm with a float sum of squares and a double sqrt; the normal divided as
+// cv::Mat / double (the scale 1 / norm rounded to float, then a float product per component).
+__global__ __launch_bounds__(256) void k_stereo_mappoints(const orbx_keypoint* __restrict__ kps, const float* __restrict__ depth,
+                                                          const int32_t* __restrict__ counts, int capacity,
+                                                          const float* __restrict__ twc, float4 cam, ProjScales sc, int nlevels,
+                                                          int flags, orbx_map_point* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
+    const int n = min(counts[b], capacity);
+    if (i >= n) return;
+    const size_t o = (size_t)b * capacity + i;
+    const orbx_keypoint kp = kps[o];
+    const float z = depth[o];
+    orbx_map_point p{};
+    p.octave = kp.octave;
+    p.angle = kp.angle;
+    p.flags = ORBX_QF_SKIP;
+    if (z > 0) {
+        const float* T = twc + 12 * (size_t)b;
+        const float x = __fmul_rn(__fmul_rn(__fsub_rn(kp.x, cam.z), z), __fdiv_rn(1.0f, cam.x));   // (u-cx)*z*invfx
+        const float y = __fmul_rn(__fmul_rn(__fsub_rn(kp.y, cam.w), z), __fdiv_rn(1.0f, cam.y));
+        auto row = [&](int r) {
+            return __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(T[3 * r], x), __fmul_rn(T[3 * r + 1], y)), __fmul_rn(T[3 * r + 2], z)),
+                             T[9 + r]);
+        };
+        p.x = row(0); p.y = row(1); p.z = row(2);
+        const float dx = __fsub_rn(p.x, T[9]), dy = __fsub_rn(p.y, T[10]), dz = __fsub_rn(p.z, T[11]);
+        const double nrm = __dsqrt_rn((double)__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+        const float inv = (float)__ddiv_rn(1.0, nrm);
+        p.nx = __fmul_rn(dx, inv); p.ny = __fmul_rn(dy, inv); p.nz = __fmul_rn(dz, inv);
+        const float dist = (float)nrm;
+        p.max_dist = __fmul_rn(dist, sc.s[kp.octave]);
+        p.min_dist = __fdiv_rn(p.max_dist, sc.s[nlevels - 1]);
+        p.flags = flags & ~ORBX_QF_SKIP;
+    }
+    out[o] = p;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Frame::UndistortKeyPoints (src/Frame.cc:404-434) and ComputeImageBounds (:436-464): cv::undistortPoints(pts,
 // K, DistCoef, R = I, P = K), pinned to OpenCV 3.2's cvUndistortPoints (README.md:68 "Tested with ... OpenCV 3.2"):
 // double precision, normalise with 1/fx, 1/fy, five fixed iterations of
@@ -527,6 +667,80 @@ int orbx_compute_image_bounds(orbx_matcher* m, const float* K, const float* dist
     bounds[1] = std::max(u[1].x, u[3].x);
     bounds[2] = std::min(u[0].y, u[1].y);
     bounds[3] = std::max(u[2].y, u[3].y);
+    return ORBX_OK;
+}
+
+static int project_check(int mode, const float* scale_factors, int nlevels, ProjScales* sc) {
+    ORBX_REQUIRE(mode == ORBX_PROJ_LASTFRAME || mode == ORBX_PROJ_MAPPOINTS || mode == ORBX_PROJ_FUSE, ORBX_ERR_ARG,
+                 "projection mode %d (LASTFRAME, MAPPOINTS or FUSE)", mode);
+    ORBX_REQUIRE(scale_factors && nlevels >= 1 && nlevels <= 32, ORBX_ERR_ARG, "bad scale factors");
+    std::memset(sc, 0, sizeof(*sc));
+    for (int l = 0; l < nlevels; ++l) sc->s[l] = scale_factors[l];
+    return ORBX_OK;
+}
+
+int orbx_proj_project_device(orbx_matcher* m, int mode, const orbx_map_point* d_points, const int32_t* d_counts, int n_views,
+                             int capacity, const orbx_view* d_views, const int32_t* d_view_points, const float* scale_factors,
+                             int nlevels, float log_scale_factor, const int32_t* d_found, orbx_proj_query* d_queries,
+                             void* stream) {
+    ORBX_REQUIRE(m && d_points && d_counts && d_views && d_queries && n_views >= 0 && capacity > 0, ORBX_ERR_ARG,
+                 "bad argument");
+    ProjScales sc;
+    int st = project_check(mode, scale_factors, nlevels, &sc);
+    if (st) return st;
+    if (n_views == 0) return ORBX_OK;
+    ORBX_REQUIRE(n_views <= 65535, ORBX_ERR_UNSUPPORTED, "too many views");
+    ORBX_HIP(hipSetDevice(matcher_device(m)));
+    hipLaunchKernelGGL(k_project, dim3((capacity + 255) / 256, n_views), dim3(256), 0, (hipStream_t)stream, mode, d_points,
+                       d_counts, 0, capacity, d_views, d_view_points, sc, nlevels, log_scale_factor, d_found, d_queries);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_stereo_mappoints_device(orbx_matcher* m, const orbx_keypoint* d_kps, const float* d_depth, const int32_t* d_counts,
+                                 int batch, int capacity, const float* d_twc, const float* camera, const float* scale_factors,
+                                 int nlevels, int flags, orbx_map_point* d_points, void* stream) {
+    ORBX_REQUIRE(m && d_kps && d_depth && d_counts && d_twc && camera && d_points && batch >= 0 && capacity > 0, ORBX_ERR_ARG,
+                 "bad argument");
+    ProjScales sc;
+    int st = project_check(ORBX_PROJ_FUSE, scale_factors, nlevels, &sc);
+    if (st) return st;
+    ORBX_REQUIRE(camera[0] != 0.0f && camera[1] != 0.0f, ORBX_ERR_ARG, "bad camera");
+    if (batch == 0) return ORBX_OK;
+    ORBX_REQUIRE(batch <= 65535, ORBX_ERR_UNSUPPORTED, "batch too large");
+    ORBX_HIP(hipSetDevice(matcher_device(m)));
+    hipLaunchKernelGGL(k_stereo_mappoints, dim3((capacity + 255) / 256, batch), dim3(256), 0, (hipStream_t)stream, d_kps, d_depth,
+                       d_counts, capacity, d_twc, make_float4(camera[0], camera[1], camera[2], camera[3]), sc, nlevels, flags,
+                       d_points);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_proj_project(orbx_matcher* m, int mode, const orbx_map_point* points, int n, const orbx_view* view,
+                      const float* scale_factors, int nlevels, float log_scale_factor, orbx_proj_query* queries) {
+    ORBX_REQUIRE(m && view && n >= 0 && (n == 0 || (points && queries)), ORBX_ERR_ARG, "bad argument");
+    ProjScales sc;
+    int st = project_check(mode, scale_factors, nlevels, &sc);
+    if (st) return st;
+    if (n == 0) return ORBX_OK;
+    uint8_t* base = nullptr;
+    hipStream_t s = nullptr;
+    const size_t bp = a256p(sizeof(orbx_map_point) * (size_t)n), bv = a256p(sizeof(orbx_view)),
+                 bq = a256p(sizeof(orbx_proj_query) * (size_t)n);
+    MatcherLease lease_(m);
+    if ((st = matcher_scratch(m, bp + bv + bq, (void**)&base, (void**)&s))) return st;
+    lease_.on(s);
+    ORBX_HIP(hipSetDevice(matcher_device(m)));
+    orbx_map_point* dp = (orbx_map_point*)base;
+    orbx_view* dv = (orbx_view*)(base + bp);
+    orbx_proj_query* dq = (orbx_proj_query*)(base + bp + bv);
+    ORBX_HIP(hipMemcpyAsync(dp, points, sizeof(orbx_map_point) * (size_t)n, hipMemcpyHostToDevice, s));
+    ORBX_HIP(hipMemcpyAsync(dv, view, sizeof(orbx_view), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_project, dim3((n + 255) / 256, 1), dim3(256), 0, s, mode, dp, (const int32_t*)nullptr, n, n, dv,
+                       (const int32_t*)nullptr, sc, nlevels, log_scale_factor, (const int32_t*)nullptr, dq);
+    ORBX_HIP(hipGetLastError());
+    ORBX_HIP(hipMemcpyAsync(queries, dq, sizeof(orbx_proj_query) * (size_t)n, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipStreamSynchronize(s));
     return ORBX_OK;
 }
 

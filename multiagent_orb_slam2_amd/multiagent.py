@@ -504,37 +504,39 @@ def triangulation_geometry(K, Rcw, tcw, pairs):
 
 
 def neighbour_observations(new_slots, neighbours, match12):
-    """Observation lists of the MapPoints of new keyframes, built on the device without a host round trip: MapPoint
-    (j, i) = keypoint i of new keyframe j, observed there and at every neighbour keypoint it matched
-    (match12[j, k, i] >= 0, neighbours in order).  new_slots (n,), neighbours (n, nn) slots (-1 = none), match12
-    (n, nn, capacity).  Returns (obs (n*capacity*(nn+1), 2) int32 -- the first offsets[-1] rows used, offsets
-    (n*capacity + 1,) int32) for ORBmatcher.distinctive_descriptors_store_device."""
+    """Observation lists of the MapPoints CreateNewMapPoints makes, built on the device without a host round trip
+    (LocalMapping.cc:244-448): keypoint i of new keyframe j becomes a MapPoint at most once, with the first neighbour k
+    (in order) whose match match12[j, k, i] >= 0, observed [(neighbour k, its match), (new keyframe j, i)] -- creation
+    order, the pin of mObservations' KeyFrame* order; no match, no MapPoint (an empty list).  new_slots
+    (n,), neighbours (n, nn) slots (-1 = none), match12 (n, nn, capacity).  Returns (obs (n*capacity*2, 2) int32 --
+    the first offsets[-1] rows used, offsets (n*capacity + 1,) int32) for ORBmatcher.distinctive_descriptors_store_device."""
     import torch
     n, nn, cap = match12.shape
     dev = match12.device
-    hit = torch.cat([torch.ones((n, cap, 1), dtype=torch.bool, device=dev), (match12 >= 0).permute(0, 2, 1)], 2)
-    slot = torch.cat([new_slots.view(n, 1).expand(n, cap)[:, :, None].int(),
-                      neighbours.view(n, 1, nn).expand(n, cap, nn).int()], 2)
-    kp = torch.cat([torch.arange(cap, dtype=torch.int32, device=dev).view(1, cap, 1).expand(n, cap, 1),
-                    match12.permute(0, 2, 1).int()], 2)
-    cnt = hit.sum(2, dtype=torch.int32).view(-1)
+    hit = (match12 >= 0) & (neighbours.view(n, nn, 1) >= 0)                 # (n, nn, cap)
+    has = hit.any(1)                                                        # (n, cap)
+    first = torch.argmax(hit.int(), 1)                                      # first neighbour with a match
+    nb_slot = torch.gather(neighbours.int(), 1, first)                      # (n, cap)
+    nb_kp = torch.gather(match12.int(), 1, first.view(n, 1, cap)).view(n, cap)
+    cnt = has.view(-1).int() * 2
     offsets = torch.zeros((n * cap + 1,), dtype=torch.int32, device=dev)
     offsets[1:] = torch.cumsum(cnt, 0)
-    rank = torch.cumsum(hit.int(), 2) - 1                                   # position inside the MapPoint's list
-    pos = (offsets[:-1].view(n, cap, 1) + rank).long()
-    tot = n * cap * (nn + 1)
-    pos = torch.where(hit, pos, torch.full_like(pos, tot))                  # unmatched -> the spill row
-    obs = torch.zeros((tot + 1, 2), dtype=torch.int32, device=dev)
-    obs.index_copy_(0, pos.view(-1), torch.stack([slot, kp], 3).view(-1, 2))
-    return obs[:tot], offsets
+    pair = torch.stack([torch.stack([nb_slot, nb_kp], 2),
+                        torch.stack([new_slots.view(n, 1).expand(n, cap).int(),
+                                     torch.arange(cap, dtype=torch.int32, device=dev).view(1, cap).expand(n, cap)], 2)],
+                       2).view(n * cap, 2, 2)
+    obs = pair[has.view(-1)].reshape(-1, 2)
+    full = torch.zeros((n * cap * 2, 2), dtype=torch.int32, device=dev)
+    full[:obs.shape[0]] = obs
+    return full, offsets
 
 
 class NewMapPoints:
     """LocalMapping::CreateNewMapPoints' matching for a batch of new keyframes (src/LocalMapping.cc:213-274): every new
     keyframe against its best covisible neighbours with ORBmatcher(0.6, false).SearchForTriangulation, all pairs in
-    one launch, then ComputeDistinctiveDescriptors for the new keyframes' MapPoints (ProcessNewKeyFrame :150-160 and
-    the new points :440-448) over the observation lists of neighbour_observations, read from the match table in
-    place (orbx_distinctive_descriptors_neighbours_device).
+    one launch, then ComputeDistinctiveDescriptors of the MapPoints it creates (:440-448: a keypoint with its first
+    matching neighbour, two observations -- neighbour_observations' lists), read from the match table in place
+    (orbx_distinctive_descriptors_neighbours_device).
 
     The reference visits the neighbours of one keyframe in turn and a keypoint triangulated with neighbour k is
     skipped for neighbours k' > k; here every pair reads the MapPoint flags given (has_mp) and the pair results are

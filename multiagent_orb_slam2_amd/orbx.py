@@ -132,6 +132,15 @@ PROJ_MAPPOINTS, PROJ_LASTFRAME, PROJ_KEYFRAME, PROJ_SIM3, PROJ_FUSE, PROJ_BEST, 
 QF_SKIP, QF_BLOCKS = 1, 2
 
 
+# orbx_map_point (48 B) and orbx_view (112 B): the projection step's inputs (orbx_proj_project)
+MAP_POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                            ("min_dist", "<f4"), ("max_dist", "<f4"), ("angle", "<f4"), ("octave", "<i4"),
+                            ("flags", "<i4"), ("pad", "<i4")])
+VIEW_DTYPE = np.dtype([("R", "<f4", (9,)), ("t", "<f4", (3,)), ("Ow", "<f4", (3,)), ("fx", "<f4"), ("fy", "<f4"),
+                       ("cx", "<f4"), ("cy", "<f4"), ("bf", "<f4"), ("min_x", "<f4"), ("max_x", "<f4"), ("min_y", "<f4"),
+                       ("max_y", "<f4"), ("th", "<f4"), ("view_cos_limit", "<f4"), ("level_mode", "<i4"), ("pad", "<i4")])
+
+
 class ProjParams(C.Structure):
     """orbx_proj_params (include/orbx.h)."""
     _fields_ = [("mode", C.c_int32), ("accept_max", C.c_int32), ("nnratio", C.c_float), ("check_ori", C.c_int32),
@@ -185,6 +194,9 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_stream_create.argtypes = [i32, i32, i32, C.POINTER(vp)]
     lib.orbx_stream_destroy.argtypes = [vp]
     lib.orbx_device_check.argtypes = [i32]
+    lib.orbx_proj_project.argtypes = [vp, i32, vp, i32, vp, vp, i32, f32, vp]
+    lib.orbx_proj_project_device.argtypes = [vp, i32, vp, vp, i32, i32, vp, vp, vp, i32, f32, vp, vp, vp]
+    lib.orbx_stereo_mappoints_device.argtypes = [vp, vp, vp, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp]
     lib.orbx_matcher_create.argtypes = [f32, i32, i32, C.POINTER(vp)]
     for name in ("orbx_extractor_destroy", "orbx_matcher_destroy", "orbx_extractor_get_levels"):
         getattr(lib, name).argtypes = [vp]
@@ -860,6 +872,49 @@ class ORBmatcher:
         one query per F1 keypoint (window at vbPrevMatched, levels [0, 0], SKIP if its octave > 0)."""
         return self.proj_search(ProjParams.make(PROJ_INIT, self.TH_LOW, self.mfNNratio, self.mbCheckOrientation), grid,
                                 queries, qdesc, kps, desc)
+
+    def proj_project(self, mode: int, points, view, scale_factors, log_scale_factor: float):
+        """The projection step (include/orbx.h orbx_proj_project): MAP_POINT_DTYPE points, one VIEW_DTYPE view ->
+        PROJ_QUERY_DTYPE queries (ORBX_QF_SKIP for points that fail the reference's tests)."""
+        p = np.ascontiguousarray(points, MAP_POINT_DTYPE)
+        v = np.ascontiguousarray(np.asarray(view, VIEW_DTYPE).reshape(1))
+        sc = np.ascontiguousarray(scale_factors, np.float32)
+        q = np.zeros(max(len(p), 1), PROJ_QUERY_DTYPE)
+        _check(self._lib.orbx_proj_project(self._h, int(mode), _p(p), len(p), _p(v), _p(sc), len(sc),
+                                           float(log_scale_factor), _p(q)))
+        return q[:len(p)]
+
+    def proj_project_device(self, mode: int, points, counts, views, scale_factors, log_scale_factor: float, out=None,
+                            found=None, view_points=None, stream=None):
+        """Batched projection: points (S, cap, 48) uint8 device tensor of MAP_POINT_DTYPE records, counts (S,) int32,
+        views (V, 112) uint8 device tensor of VIEW_DTYPE -> (V, cap, 40) uint8 queries (PROJ_QUERY_DTYPE); view v
+        projects point set view_points[v] ((V,) int32, default v).  found: optional (V, cap) int32 -- points with
+        found >= 0 (already matched in the frame) are skipped."""
+        import torch
+        V, cap = views.shape[0], points.shape[1]
+        if out is None:
+            out = torch.empty((V, cap, 40), dtype=torch.uint8, device=points.device)
+        sc = np.ascontiguousarray(scale_factors, np.float32)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(points.device).cuda_stream)
+        _check(self._lib.orbx_proj_project_device(self._h, int(mode), _tp(points), _tp(counts), V, cap, _tp(views),
+                                                  None if view_points is None else _tp(view_points),
+                                                  _p(sc), len(sc), float(log_scale_factor),
+                                                  None if found is None else _tp(found), _tp(out), s))
+        return out
+
+    def stereo_mappoints_device(self, kps, depth, counts, twc, camera, scale_factors, flags: int, out=None, stream=None):
+        """MapPoints of stereo frames (include/orbx.h orbx_stereo_mappoints_device): kps (B, cap, 28) uint8, depth
+        (B, cap) float32, counts (B,) int32, twc (B, 12) float32 device tensors -> (B, cap, 48) uint8 MAP_POINT_DTYPE."""
+        import torch
+        B, cap = kps.shape[0], kps.shape[1]
+        if out is None:
+            out = torch.empty((B, cap, 48), dtype=torch.uint8, device=kps.device)
+        cam = np.ascontiguousarray(camera, np.float32).reshape(4)
+        sc = np.ascontiguousarray(scale_factors, np.float32)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(kps.device).cuda_stream)
+        _check(self._lib.orbx_stereo_mappoints_device(self._h, _tp(kps), _tp(depth), _tp(counts), B, cap, _tp(twc), _p(cam),
+                                                      _p(sc), len(sc), int(flags), _tp(out), s))
+        return out
 
     def grid_build_device(self, grid: Grid, kps, counts, stream=None, out=None):
         """Frame::AssignFeaturesToGrid on (B, capacity, 28) device keypoints: (cell_start, cell_idx) tensors

@@ -370,6 +370,42 @@ def proj_search(params, grid, queries, qdesc, kps, desc, uright=None, blocked=No
     return nm, qi[:nq], qdist[:nq], own[:n]
 
 
+# orbx_map_point (48 B) / orbx_view (112 B) of include/orbx.h
+MAP_POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                            ("min_dist", "<f4"), ("max_dist", "<f4"), ("angle", "<f4"), ("octave", "<i4"),
+                            ("flags", "<i4"), ("pad", "<i4")])
+VIEW_DTYPE = np.dtype([("R", "<f4", (9,)), ("t", "<f4", (3,)), ("Ow", "<f4", (3,)), ("fx", "<f4"), ("fy", "<f4"),
+                       ("cx", "<f4"), ("cy", "<f4"), ("bf", "<f4"), ("min_x", "<f4"), ("max_x", "<f4"), ("min_y", "<f4"),
+                       ("max_y", "<f4"), ("th", "<f4"), ("view_cos_limit", "<f4"), ("level_mode", "<i4"), ("pad", "<i4")])
+
+
+def project(mode, points, view, scale_factors, log_scale_factor):
+    """The projection step before the searches (oracle/proj_oracle.cpp orc_project): one query per MapPoint."""
+    p = np.ascontiguousarray(points, MAP_POINT_DTYPE)
+    v = np.ascontiguousarray(np.asarray(view, VIEW_DTYPE).reshape(1))
+    sc = np.ascontiguousarray(scale_factors, np.float32)
+    out = np.zeros(max(len(p), 1), np.dtype([("b", "V40")]))
+    L = lib()
+    L.orc_project.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_float, C.c_void_p]
+    L.orc_project(int(mode), _p(p), len(p), _p(v), _p(sc), len(sc), float(log_scale_factor), _p(out))
+    return out[:len(p)].view(np.uint8).reshape(-1, 40).copy()
+
+
+def stereo_mappoints(kps, depth, twc, camera, scale_factors, flags):
+    """MapPoints of one stereo frame (orc_stereo_mappoints): MAP_POINT_DTYPE records, SKIP where depth <= 0."""
+    k = np.ascontiguousarray(kps, KP_DTYPE)
+    d = np.ascontiguousarray(depth, np.float32)
+    T = np.ascontiguousarray(twc, np.float32).reshape(12)
+    cam = np.ascontiguousarray(camera, np.float32).reshape(4)
+    sc = np.ascontiguousarray(scale_factors, np.float32)
+    out = np.zeros(max(len(k), 1), MAP_POINT_DTYPE)
+    L = lib()
+    L.orc_stereo_mappoints.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                       C.c_void_p]
+    L.orc_stereo_mappoints(_p(k), _p(d), len(k), _p(T), _p(cam), _p(sc), len(sc), int(flags), _p(out))
+    return out[:len(k)]
+
+
 def undistort_points(xy, K, dist):
     """Frame::UndistortKeyPoints' cv::undistortPoints(K, D, R=I, P=K), OpenCV 3.2 semantics restated."""
     xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)

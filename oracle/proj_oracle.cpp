@@ -14,8 +14,10 @@
 //   ORBmatcher::Fuse(KeyFrame*, Scw, ...) — the search          src/ORBmatcher.cc:1053-1081
 //   ORBmatcher::SearchBySim3 — each direction's search          src/ORBmatcher.cc:1193-1226, 1273-1306
 //   ORBmatcher::SearchForInitialization                         src/ORBmatcher.cc:407-522
-// The projection arithmetic before each search (cv::Mat products, PredictScale) is the caller's: a query
-// carries the window the reference passes to GetFeaturesInArea and the values its inner loop tests.
+// A query carries the window the reference passes to GetFeaturesInArea and the values its inner loop tests; the
+// projection arithmetic that produces it (cv::Mat products, isInFrustum, PredictScale) is restated by orc_project,
+// and the MapPoints of a stereo frame (UnprojectStereo + the Frame form of the MapPoint constructor) by
+// orc_stereo_mappoints.
 // Struct layouts are identical to orbx_grid / orbx_proj_query / orbx_proj_params (include/orbx.h).
 // Compiled with -ffp-contract=off (oracle/Makefile): float expressions evaluate as written.
 // =====================================================================================================
@@ -86,6 +88,150 @@ struct orc_proj_params {
 enum { ORC_PROJ_MAPPOINTS = 0, ORC_PROJ_LASTFRAME, ORC_PROJ_KEYFRAME, ORC_PROJ_SIM3, ORC_PROJ_FUSE, ORC_PROJ_BEST,
        ORC_PROJ_INIT };
 enum { ORC_QF_SKIP = 1, ORC_QF_BLOCKS = 2 };
+
+// The projection step before the searches (include/orbx.h orbx_proj_project): one MapPoint -> one query, in the
+// reference's operation order for each caller.  float expressions evaluate as written (-ffp-contract=off); the
+// cv::Mat pieces are pinned as DESIGN §2 states: Rcw * X + tcw as float products summed left to right; cv::norm and
+// Mat::dot of 3-vectors as float products accumulated in double; PredictScale's log in double.
+struct orc_map_point {
+    float x, y, z, nx, ny, nz, min_dist, max_dist, angle;
+    int32_t octave, flags, pad;
+};
+struct orc_view {
+    float R[9], t[3], Ow[3];
+    float fx, fy, cx, cy, bf;
+    float min_x, max_x, min_y, max_y;
+    float th, view_cos_limit;
+    int32_t level_mode, pad;
+};
+
+static int orc_predict_scale(float max_dist, float dist, float log_sf, int nlevels) {   // MapPoint.cc:389-421
+    const float ratio = max_dist / dist;
+    int n = (int)std::ceil(std::log((double)ratio) / (double)log_sf);
+    if (n < 0) n = 0;
+    else if (n >= nlevels) n = nlevels - 1;
+    return n;
+}
+
+int orc_project(int mode, const orc_map_point* P, int n, const orc_view* V, const float* scale, int nlevels, float log_sf,
+                orc_proj_query* out) {
+    int kept = 0;
+    for (int i = 0; i < n; ++i) {
+        const orc_map_point& p = P[i];
+        orc_proj_query q{};
+        q.min_level = -1;
+        q.max_level = -1;
+        q.ur = 0.0f;
+        q.ur_tol = -1.0f;
+        q.level = -1;
+        q.flags = ORC_QF_SKIP;
+        out[i] = q;
+        if (p.flags & ORC_QF_SKIP) continue;
+        // x3Dc = Rcw * x3Dw + tcw (:1363-1364, Frame.cc:277, :855)
+        const float xc = V->R[0] * p.x + V->R[1] * p.y + V->R[2] * p.z + V->t[0];
+        const float yc = V->R[3] * p.x + V->R[4] * p.y + V->R[5] * p.z + V->t[1];
+        const float zc = V->R[6] * p.x + V->R[7] * p.y + V->R[8] * p.z + V->t[2];
+        if (mode == ORC_PROJ_LASTFRAME) {
+            const float invzc = (float)(1.0 / (double)zc);                               // :1368
+            if (invzc < 0) continue;
+            const float u = V->fx * xc * invzc + V->cx;                                  // :1373-1374
+            const float v = V->fy * yc * invzc + V->cy;
+            if (u < V->min_x || u > V->max_x) continue;
+            if (v < V->min_y || v > V->max_y) continue;
+            const int oct = p.octave;
+            const float radius = V->th * scale[oct];                                     // :1384
+            q.x = u; q.y = v; q.r = radius;
+            if (V->level_mode > 0) { q.min_level = oct; q.max_level = -1; }              // :1388-1393
+            else if (V->level_mode < 0) { q.min_level = 0; q.max_level = oct; }
+            else { q.min_level = oct - 1; q.max_level = oct + 1; }
+            q.ur = u - V->bf * invzc;                                                    // :1418-1426
+            q.ur_tol = radius;
+            q.angle = p.angle;
+            q.level = oct;
+        } else {
+            float u, v, invz;
+            if (mode == ORC_PROJ_MAPPOINTS) {                                            // Frame::isInFrustum
+                if (zc < 0.0f) continue;
+                invz = 1.0f / zc;
+                u = V->fx * xc * invz + V->cx;
+                v = V->fy * yc * invz + V->cy;
+                if (u < V->min_x || u > V->max_x) continue;
+                if (v < V->min_y || v > V->max_y) continue;
+            } else {                                                                     // Fuse :857-871
+                if (zc < 0.0f) continue;
+                invz = 1 / zc;
+                const float x = xc * invz, y = yc * invz;
+                u = V->fx * x + V->cx;
+                v = V->fy * y + V->cy;
+                if (!(u >= V->min_x && u < V->max_x && v >= V->min_y && v < V->max_y)) continue;   // KeyFrame::IsInImage
+            }
+            const float maxD = 1.2f * p.max_dist, minD = 0.8f * p.min_dist;            // MapPoint.cc:377-387
+            const float POx = p.x - V->Ow[0], POy = p.y - V->Ow[1], POz = p.z - V->Ow[2];
+            const float ss = POx * POx + POy * POy + POz * POz;
+            const float dist = (float)std::sqrt((double)ss);                             // cv::norm
+            if (dist < minD || dist > maxD) continue;
+            double dot = 0.0;                                                            // PO.dot(Pn)
+            dot += (double)(POx * p.nx);
+            dot += (double)(POy * p.ny);
+            dot += (double)(POz * p.nz);
+            const int pred = orc_predict_scale(p.max_dist, dist, log_sf, nlevels);
+            if (mode == ORC_PROJ_MAPPOINTS) {
+                const float viewCos = (float)(dot / (double)dist);                       // Frame.cc:308-311
+                if (viewCos < V->view_cos_limit) continue;
+                float r = (double)viewCos > 0.998 ? 2.5f : 4.0f;                         // RadiusByViewingCos :133-139
+                if (V->th != 1.0f) r *= V->th;                                           // :65-68
+                q.x = u; q.y = v; q.r = r * scale[pred];                                 // :70-71
+                q.min_level = pred - 1; q.max_level = pred;
+                q.ur = u - V->bf * invz;                                                 // mTrackProjXR (Frame.cc:319)
+                q.ur_tol = r * scale[pred];                                              // :92-98
+            } else {
+                if (dot < 0.5 * (double)dist) continue;                                  // :887-888
+                q.x = u; q.y = v; q.r = V->th * scale[pred];                             // :890-893
+                q.min_level = pred - 1; q.max_level = pred;                              // :915-918
+                q.ur = u - V->bf * invz;                                                 // :873
+            }
+            q.level = pred;
+        }
+        q.flags = p.flags & ~ORC_QF_SKIP;
+        out[i] = q;
+        ++kept;
+    }
+    return kept;
+}
+
+// MapPoints of one stereo frame: Frame::UnprojectStereo (src/Frame.cc:666-680) + MapPoint::MapPoint(Pos, pMap, pFrame,
+// idxF) (src/MapPoint.cc:47-68).  twc = Rwc (9, row-major) then Ow (3); camera = fx, fy, cx, cy.
+int orc_stereo_mappoints(const Kp* k, const float* depth, int n, const float* twc, const float* camera, const float* scale,
+                         int nlevels, int flags, orc_map_point* out) {
+    const float invfx = 1.0f / camera[0], invfy = 1.0f / camera[1];     // Frame.cc:94-95
+    int made = 0;
+    for (int i = 0; i < n; ++i) {
+        orc_map_point p{};
+        p.octave = k[i].octave;
+        p.angle = k[i].angle;
+        p.flags = ORC_QF_SKIP;
+        const float z = depth[i];
+        if (z > 0) {
+            const float u = k[i].x, v = k[i].y;
+            const float x = (u - camera[2]) * z * invfx;
+            const float y = (v - camera[3]) * z * invfy;
+            p.x = twc[0] * x + twc[1] * y + twc[2] * z + twc[9];               // mRwc * x3Dc + mOw
+            p.y = twc[3] * x + twc[4] * y + twc[5] * z + twc[10];
+            p.z = twc[6] * x + twc[7] * y + twc[8] * z + twc[11];
+            const float dx = p.x - twc[9], dy = p.y - twc[10], dz = p.z - twc[11];
+            const double nrm = std::sqrt((double)(dx * dx + dy * dy + dz * dz));   // cv::norm
+            const float inv = (float)(1.0 / nrm);                              // mNormalVector / cv::norm(...)
+            p.nx = dx * inv; p.ny = dy * inv; p.nz = dz * inv;
+            const float dist = (float)nrm;
+            p.max_dist = dist * scale[k[i].octave];                            // MapPoint.cc:60-64
+            p.min_dist = p.max_dist / scale[nlevels - 1];
+            p.flags = flags & ~ORC_QF_SKIP;
+            ++made;
+        }
+        out[i] = p;
+    }
+    return made;
+}
 
 // Frame::AssignFeaturesToGrid with PosInGrid: cell (ix, iy) -> CSR row ix * rows + iy; indices ascending
 // inside a cell (push_back in index order).  Returns the number of keypoints placed.

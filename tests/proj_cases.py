@@ -261,3 +261,174 @@ def py_proj_search(c):
         own = [-1] * n
     q_dist = [dd if ii >= 0 else -1 for ii, dd in zip(q_idx, q_dist)]
     return nm, np.array(q_idx, np.int32), np.array(q_dist, np.int32), np.array(own, np.int32)
+
+
+# ---- the projection step (orbx_proj_project; src/ORBmatcher.cc:1363-1392, Frame.cc:269-325, ORBmatcher.cc:854-893) ----
+def make_projection_case(seed: int, n: int = 600, W: int = 1242, H: int = 375):
+    """MapPoints around a camera with a small random pose: most project inside the image with distances inside their
+    scale-invariance range; some lie behind the camera, outside the image, outside the distance range, or are seen at
+    more than 60 degrees from their normal; a few are flagged SKIP / BLOCKS.  Returns (points, view, scale, log_sf) with
+    the dtypes of oracle.MAP_POINT_DTYPE / VIEW_DTYPE."""
+    from oracle.oracle import MAP_POINT_DTYPE, VIEW_DTYPE
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = 718.856, 718.856, 607.1928, 185.2157, 386.1448
+    yaw, pitch = rng.normal(0, 0.05), rng.normal(0, 0.02)
+    cyw, syw, cp, sp = math.cos(yaw), math.sin(yaw), math.cos(pitch), math.sin(pitch)
+    Ry = np.array([[cyw, 0, syw], [0, 1, 0], [-syw, 0, cyw]])
+    Rx = np.array([[1, 0, 0], [0, cp, -sp], [0, sp, cp]])
+    R = (Rx @ Ry).astype(np.float32)
+    Ow = rng.normal(0, 0.5, 3).astype(np.float32)
+    t = (-(R.astype(np.float64) @ Ow.astype(np.float64))).astype(np.float32)
+    # points: pixel + depth in the camera, then to the world
+    u = rng.uniform(-60, W + 60, n)
+    v = rng.uniform(-30, H + 30, n)
+    z = rng.uniform(1.5, 70.0, n)
+    z[rng.random(n) < 0.04] *= -1                                       # behind the camera
+    Xc = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1)
+    Xw = (R.astype(np.float64).T @ (Xc.T - t.astype(np.float64)[:, None])).T
+    p = np.zeros(n, MAP_POINT_DTYPE)
+    p["x"], p["y"], p["z"] = Xw[:, 0], Xw[:, 1], Xw[:, 2]
+    d = Xw - Ow.astype(np.float64)
+    dist = np.linalg.norm(d, axis=1)
+    nrm = d / dist[:, None]
+    tilt = rng.random(n) < 0.1                                          # seen from > 60 degrees
+    nrm[tilt] = np.cross(nrm[tilt], rng.normal(0, 1, (int(tilt.sum()), 3)))
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    p["nx"], p["ny"], p["nz"] = nrm[:, 0], nrm[:, 1], nrm[:, 2]
+    octave = np.minimum(rng.geometric(0.45, n) - 1, 7)
+    # mfMaxDistance = creation distance x scale^octave, mfMinDistance = max / scale^7 (MapPoint::UpdateNormalAndDepth)
+    created = dist * rng.uniform(0.7, 1.4, n)
+    created[rng.random(n) < 0.08] *= 3.0                                # now outside the invariance range
+    p["max_dist"] = (created * SCALE[octave]).astype(np.float32)
+    p["min_dist"] = (p["max_dist"] / SCALE[7]).astype(np.float32)
+    p["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+    p["octave"] = octave
+    p["flags"] = np.where(rng.random(n) < 0.05, QF_SKIP, 0) | np.where(rng.random(n) < 0.7, QF_BLOCKS, 0)
+    view = np.zeros(1, VIEW_DTYPE)[0]
+    view["R"], view["t"], view["Ow"] = R.reshape(9), t, Ow
+    view["fx"], view["fy"], view["cx"], view["cy"], view["bf"] = fx, fy, cx, cy, bf
+    view["min_x"], view["max_x"], view["min_y"], view["max_y"] = 0.0, W, 0.0, H
+    view["th"] = [7.0, 1.0, 3.0, 5.0][seed % 4]
+    view["view_cos_limit"] = 0.5
+    view["level_mode"] = [1, -1, 0][seed % 3]
+    return p, view, SCALE, np.float32(math.log(1.2))
+
+
+def project_py(mode, points, view, scale, log_sf):
+    """Pure-Python restatement of the projection step (numpy float32 scalars: IEEE single, no contraction; float64 for
+    the double parts), independent of oracle/proj_oracle.cpp.  Returns PROJ_QUERY_DTYPE queries."""
+    f = np.float32
+    out = np.zeros(len(points), PROJ_QUERY_DTYPE)
+    R, t, Ow = view["R"].astype(np.float32), view["t"].astype(np.float32), view["Ow"].astype(np.float32)
+    fx, fy, cx, cy, bf = (f(view[k]) for k in ("fx", "fy", "cx", "cy", "bf"))
+    nlev = len(scale)
+    for i, p in enumerate(points):
+        q = out[i]
+        q["min_level"] = q["max_level"] = q["level"] = -1
+        q["ur_tol"] = -1
+        q["flags"] = QF_SKIP
+        if p["flags"] & QF_SKIP:
+            continue
+        X = (f(p["x"]), f(p["y"]), f(p["z"]))
+        c = [R[3 * r] * X[0] + R[3 * r + 1] * X[1] + R[3 * r + 2] * X[2] + t[r] for r in range(3)]
+        xc, yc, zc = c
+        if mode == PROJ_LASTFRAME:
+            invz = f(1.0 / float(zc)) if zc != 0 else f(np.inf)
+            if invz < 0:
+                continue
+            u, v = fx * xc * invz + cx, fy * yc * invz + cy
+            if u < view["min_x"] or u > view["max_x"] or v < view["min_y"] or v > view["max_y"]:
+                continue
+            o = int(p["octave"])
+            rad = f(view["th"]) * scale[o]
+            q["x"], q["y"], q["r"] = u, v, rad
+            lm = int(view["level_mode"])
+            q["min_level"], q["max_level"] = (o, -1) if lm > 0 else (0, o) if lm < 0 else (o - 1, o + 1)
+            q["ur"], q["ur_tol"], q["angle"], q["level"] = u - bf * invz, rad, p["angle"], o
+        else:
+            if zc < 0:
+                continue
+            invz = f(1) / zc
+            if mode == PROJ_MAPPOINTS:
+                u, v = fx * xc * invz + cx, fy * yc * invz + cy
+                if u < view["min_x"] or u > view["max_x"] or v < view["min_y"] or v > view["max_y"]:
+                    continue
+            else:
+                u, v = fx * (xc * invz) + cx, fy * (yc * invz) + cy
+                if not (view["min_x"] <= u < view["max_x"] and view["min_y"] <= v < view["max_y"]):
+                    continue
+            maxD, minD = f(1.2) * f(p["max_dist"]), f(0.8) * f(p["min_dist"])
+            PO = [X[k] - Ow[k] for k in range(3)]
+            dist = f(math.sqrt(float(PO[0] * PO[0] + PO[1] * PO[1] + PO[2] * PO[2])))
+            if dist < minD or dist > maxD:
+                continue
+            N = (f(p["nx"]), f(p["ny"]), f(p["nz"]))
+            dot = 0.0
+            for k in range(3):
+                dot += float(PO[k] * N[k])
+            ratio = f(p["max_dist"]) / dist
+            pred = min(max(int(math.ceil(math.log(float(ratio)) / float(log_sf))), 0), nlev - 1)
+            if mode == PROJ_MAPPOINTS:
+                vc = f(dot / float(dist))
+                if vc < f(view["view_cos_limit"]):
+                    continue
+                r = f(2.5) if float(vc) > 0.998 else f(4.0)
+                if f(view["th"]) != f(1):
+                    r = r * f(view["th"])
+                q["x"], q["y"], q["r"] = u, v, r * scale[pred]
+                q["ur"], q["ur_tol"] = u - bf * invz, r * scale[pred]
+            else:
+                if dot < 0.5 * float(dist):
+                    continue
+                q["x"], q["y"], q["r"] = u, v, f(view["th"]) * scale[pred]
+                q["ur"] = u - bf * invz
+            q["min_level"], q["max_level"], q["level"] = pred - 1, pred, pred
+        q["flags"] = int(p["flags"]) & ~QF_SKIP
+    return out
+
+
+def stereo_frame_case(seed: int, n: int = 700, W: int = 1242, H: int = 375):
+    """Keypoints of a stereo frame with depths (a share without depth), its pose Twc (Rwc 9 + Ow 3) and camera."""
+    rng = np.random.default_rng(seed)
+    k = np.zeros(n, KP_DTYPE)
+    k["x"] = rng.uniform(0, W, n).astype(np.float32)
+    k["y"] = rng.uniform(0, H, n).astype(np.float32)
+    k["octave"] = np.minimum(rng.geometric(0.45, n) - 1, 7)
+    k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+    k["size"] = 31 * SCALE[k["octave"]]
+    depth = rng.uniform(1.0, 60.0, n).astype(np.float32)
+    depth[rng.random(n) < 0.3] = -1.0
+    depth[rng.random(n) < 0.02] = 0.0
+    a = rng.normal(0, 0.1)
+    Rwc = np.array([[math.cos(a), 0, math.sin(a)], [0, 1, 0], [-math.sin(a), 0, math.cos(a)]], np.float32)
+    Ow = rng.normal(0, 2.0, 3).astype(np.float32)
+    twc = np.concatenate([Rwc.reshape(9), Ow]).astype(np.float32)
+    cam = np.array([718.856, 718.856, 607.1928, 185.2157], np.float32)
+    return k, depth, twc, cam
+
+
+def stereo_mappoints_py(k, depth, twc, cam, scale, flags):
+    """numpy-float32 restatement of Frame::UnprojectStereo + MapPoint::MapPoint(Pos, pMap, pFrame, idxF)."""
+    from oracle.oracle import MAP_POINT_DTYPE
+    f = np.float32
+    out = np.zeros(len(k), MAP_POINT_DTYPE)
+    T = twc.astype(np.float32)
+    invfx, invfy = f(1) / f(cam[0]), f(1) / f(cam[1])
+    for i in range(len(k)):
+        p = out[i]
+        p["octave"], p["angle"], p["flags"] = k["octave"][i], k["angle"][i], QF_SKIP
+        z = f(depth[i])
+        if not z > 0:
+            continue
+        x = (f(k["x"][i]) - f(cam[2])) * z * invfx
+        y = (f(k["y"][i]) - f(cam[3])) * z * invfy
+        X = [T[3 * r] * x + T[3 * r + 1] * y + T[3 * r + 2] * z + T[9 + r] for r in range(3)]
+        d = [X[r] - T[9 + r] for r in range(3)]
+        nrm = math.sqrt(float(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]))
+        inv = f(1.0 / nrm)
+        p["x"], p["y"], p["z"] = X
+        p["nx"], p["ny"], p["nz"] = d[0] * inv, d[1] * inv, d[2] * inv
+        p["max_dist"] = f(nrm) * scale[int(k["octave"][i])]
+        p["min_dist"] = f(p["max_dist"]) / scale[len(scale) - 1]
+        p["flags"] = flags & ~QF_SKIP
+    return out

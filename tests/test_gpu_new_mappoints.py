@@ -94,11 +94,15 @@ def test_new_mappoints_vs_oracle(gpu, mode):
             assert (m12h[j, k, int(ch[q]):] == -1).all()
             total += rn
         for i in range(cap):
-            rows_ = [dh[q, i]] + [dh[int(nbh[j, k]), m12h[j, k, i]] for k in range(5) if m12h[j, k, i] >= 0]
-            lists.append(np.stack(rows_))
+            # LocalMapping.cc:440-448: the first neighbour with a match, two observations in creation order
+            ks = [k for k in range(5) if nbh[j, k] >= 0 and m12h[j, k, i] >= 0]
+            lists.append(np.stack([dh[int(nbh[j, ks[0]]), m12h[j, ks[0], i]], dh[q, i]]) if ks else
+                         np.zeros((0, 32), np.uint8))
     assert total >= 20, total
     ref = O.distinctive_descriptors(lists)
     assert np.array_equal(best.cpu().numpy(), ref)
+    assert (ref[[len(l) == 2 for l in lists]] == 0).all() and (ref[[len(l) == 0 for l in lists]] == -1).all()
     bd = bdesc.cpu().numpy()
     for p, l in enumerate(lists):
-        assert np.array_equal(bd[p], l[ref[p]])
+        if len(l):
+            assert np.array_equal(bd[p], l[ref[p]])

@@ -120,3 +120,88 @@ def test_grid_build_and_batched_search_device(gpu):
         nq, n = len(c["queries"]), len(c["kps"])
         got = (int(nm[i]), q_idx[i, :nq].cpu().numpy(), q_dist[i, :nq].cpu().numpy(), owner[i, :n].cpu().numpy())
         _check(c, got)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_projection_step_bit_exact(gpu, seed):
+    """orbx_proj_project (host form) and orbx_proj_project_device (a batch of views, ragged counts) give the oracle's
+    queries bit for bit for LASTFRAME, MAPPOINTS (isInFrustum) and FUSE."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from multiagent_orb_slam2_amd.orbx import MAP_POINT_DTYPE, PROJ_FUSE, PROJ_LASTFRAME, PROJ_MAPPOINTS, VIEW_DTYPE
+    from oracle import oracle as O
+    from proj_cases import make_projection_case
+    m = pkg.ORBmatcher(0.8, True)
+    cases = [make_projection_case(10 * seed + k, n=500 + 37 * k) for k in range(3)]
+    cap = max(len(c[0]) for c in cases)
+    sc, lsf = cases[0][2], cases[0][3]
+    for mode in (PROJ_LASTFRAME, PROJ_MAPPOINTS, PROJ_FUSE):
+        pts = np.zeros((len(cases), cap), MAP_POINT_DTYPE)
+        views = np.zeros(len(cases), VIEW_DTYPE)
+        for i, (p, v, _, _) in enumerate(cases):
+            pts[i, :len(p)] = p
+            views[i] = v
+        dp = torch.from_numpy(pts.view(np.uint8).reshape(len(cases), cap, 48)).cuda()
+        dv = torch.from_numpy(views.view(np.uint8).reshape(len(cases), 112)).cuda()
+        cnt = torch.tensor([len(c[0]) for c in cases], dtype=torch.int32, device="cuda")
+        out = m.proj_project_device(mode, dp, cnt, dv, sc, lsf)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for i, (p, v, _, _) in enumerate(cases):
+            ref = O.project(mode, p, v, sc, lsf)
+            assert np.array_equal(got[i, :len(p)], ref), f"mode {mode} view {i}"
+            tail = got[i, len(p):].copy().view(pkg.PROJ_QUERY_DTYPE).reshape(-1)
+            assert (tail["flags"] & 1).all(), "rows past the count must be skipped"
+            host = m.proj_project(mode, p, v, sc, lsf).view(np.uint8).reshape(-1, 40)
+            assert np.array_equal(host, ref), f"host form, mode {mode} view {i}"
+        # many views of one point set (Fuse's shape): view k projects set vp[k]
+        vp = torch.tensor([2, 0, 0, 1, 2], dtype=torch.int32, device="cuda")
+        vv = np.stack([views[j] for j in (0, 1, 2, 2, 1)])
+        dvv = torch.from_numpy(vv.view(np.uint8).reshape(5, 112)).cuda()
+        outv = m.proj_project_device(mode, dp, cnt, dvv, sc, lsf, view_points=vp).cpu().numpy()
+        for k, (s_, vix) in enumerate(zip((2, 0, 0, 1, 2), (0, 1, 2, 2, 1))):
+            p = cases[s_][0]
+            ref = O.project(mode, p, vv[k], sc, lsf)
+            assert np.array_equal(outv[k, :len(p)], ref), f"mode {mode} indirect view {k}"
+
+
+def test_stereo_mappoints_and_found_skip_bit_exact(gpu):
+    """orbx_stereo_mappoints_device over a batch of frames equals the oracle, and orbx_proj_project_device with a
+    'found' array skips exactly the points already matched (Tracking::SearchLocalPoints)."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from multiagent_orb_slam2_amd.orbx import PROJ_MAPPOINTS, QF_BLOCKS, VIEW_DTYPE
+    from oracle import oracle as O
+    from proj_cases import SCALE, make_projection_case, stereo_frame_case
+    m = pkg.ORBmatcher(0.8, True)
+    frames = [stereo_frame_case(50 + i, n=600 + 50 * i) for i in range(3)]
+    cap = max(len(f[0]) for f in frames)
+    kp = np.zeros((3, cap), pkg.KP_DTYPE)
+    dp = np.zeros((3, cap), np.float32)
+    tw = np.zeros((3, 12), np.float32)
+    for i, (k, d, t, cam) in enumerate(frames):
+        kp[i, :len(k)], dp[i, :len(k)], tw[i] = k, d, t
+    dk = torch.from_numpy(kp.view(np.uint8).reshape(3, cap, 28)).cuda()
+    dd, dt = torch.from_numpy(dp).cuda(), torch.from_numpy(tw).cuda()
+    cnt = torch.tensor([len(f[0]) for f in frames], dtype=torch.int32, device="cuda")
+    pts = m.stereo_mappoints_device(dk, dd, cnt, dt, frames[0][3], SCALE, QF_BLOCKS)
+    torch.cuda.synchronize()
+    got = pts.cpu().numpy()
+    for i, (k, d, t, cam) in enumerate(frames):
+        ref = O.stereo_mappoints(k, d, t, cam, SCALE, QF_BLOCKS)
+        assert np.array_equal(got[i, :len(k)].reshape(-1), ref.view(np.uint8).reshape(-1)), f"frame {i}"
+    # projection with 'found': the same points seen from a view close to frame 0's
+    _, view, _, lsf = make_projection_case(3)
+    views = np.zeros(3, VIEW_DTYPE)
+    for i in range(3):
+        views[i] = view
+    found = torch.full((3, cap), -1, dtype=torch.int32, device="cuda")
+    found[:, ::3] = 5
+    dv = torch.from_numpy(views.view(np.uint8).reshape(3, 112)).cuda()
+    q = m.proj_project_device(PROJ_MAPPOINTS, pts, cnt, dv, SCALE, lsf, found=found).cpu().numpy()
+    for i, (k, d, t, cam) in enumerate(frames):
+        p = O.stereo_mappoints(k, d, t, cam, SCALE, QF_BLOCKS)
+        p["flags"][::3] |= 1
+        assert np.array_equal(q[i, :len(k)], O.project(PROJ_MAPPOINTS, p, view, SCALE, lsf)), f"frame {i}"

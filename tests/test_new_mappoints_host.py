@@ -53,10 +53,11 @@ def test_neighbour_observations_match_loops():
     exp, eoff = [], [0]
     for j in range(n):
         for i in range(cap):
-            exp.append([int(new[j]), i])
+            # the first neighbour with a match makes the MapPoint: [(neighbour, match), (new keyframe, i)]
             for k in range(nn):
-                if m12[j, k, i] >= 0:
-                    exp.append([int(nb[j, k]), int(m12[j, k, i])])
+                if nb[j, k] >= 0 and m12[j, k, i] >= 0:
+                    exp += [[int(nb[j, k]), int(m12[j, k, i])], [int(new[j]), i]]
+                    break
             eoff.append(len(exp))
     assert off.tolist() == eoff
     assert obs[:eoff[-1]].tolist() == exp

@@ -56,3 +56,34 @@ def test_proj_search_exercises_conflicts():
     c = make_case(6, MODES["init"], n_target=240, n_query=200, dense=True)
     nm, qi, _, _ = O.proj_search(c["params"], c["grid"], c["queries"], c["qdesc"], c["kps"], c["desc"])
     assert nm == (qi >= 0).sum() and nm > 5
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_projection_oracle_matches_python(seed):
+    """The projection step (orc_project: LASTFRAME :1363-1392, isInFrustum + the MAPPOINTS window, Fuse :854-893)
+    equals the independent pure-Python restatement bit for bit, and every rejection branch occurs."""
+    from multiagent_orb_slam2_amd.orbx import PROJ_FUSE, PROJ_LASTFRAME, PROJ_MAPPOINTS, PROJ_QUERY_DTYPE, QF_SKIP
+    from proj_cases import make_projection_case, project_py
+    p, v, sc, lsf = make_projection_case(seed)
+    for mode in (PROJ_LASTFRAME, PROJ_MAPPOINTS, PROJ_FUSE):
+        a = O.project(mode, p, v, sc, lsf)
+        b = project_py(mode, p, v, sc, lsf).view(np.uint8).reshape(-1, 40)
+        assert np.array_equal(a, b), f"mode {mode}: {int((a != b).any(1).sum())} queries differ"
+        q = a.view(PROJ_QUERY_DTYPE).reshape(-1)
+        kept = (q["flags"] & QF_SKIP) == 0
+        assert 0.3 * len(p) < kept.sum() < 0.95 * len(p)          # both outcomes well represented
+        if mode != PROJ_LASTFRAME:
+            assert len(set(q["level"][kept].tolist())) >= 4        # PredictScale spreads the levels
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_stereo_mappoints_oracle_matches_python(seed):
+    """MapPoints of a stereo frame (UnprojectStereo + the Frame form of the MapPoint constructor): the oracle equals the
+    numpy-float32 restatement bit for bit; keypoints without depth (-1, 0) are skipped."""
+    from multiagent_orb_slam2_amd.orbx import QF_BLOCKS, QF_SKIP
+    from proj_cases import SCALE, stereo_frame_case, stereo_mappoints_py
+    k, depth, twc, cam = stereo_frame_case(seed)
+    a = O.stereo_mappoints(k, depth, twc, cam, SCALE, QF_BLOCKS)
+    b = stereo_mappoints_py(k, depth, twc, cam, SCALE, QF_BLOCKS)
+    assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+    assert np.array_equal((a["flags"] & QF_SKIP) != 0, ~(depth > 0))
