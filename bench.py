@@ -99,6 +99,10 @@ def parse():
     ap.add_argument("--no-tri", dest="tri", action="store_false",
                     help="leave CreateNewMapPoints' matching (SearchForTriangulation vs 10 neighbours + distinctive "
                          "descriptors) out of the keyframe path")
+    ap.add_argument("--no-tracking", dest="tracking", action="store_false",
+                    help="leave the tracking matches (SearchByProjection motion model + local map) out of the step")
+    ap.add_argument("--no-fuse", dest="fuse", action="store_false",
+                    help="leave SearchInNeighbors' Fuse (both ways with 10 neighbours) out of the keyframe path")
     ap.add_argument("--no-cd", dest="cd", action="store_false", help="skip the CovisibilityDiscovery-shaped block")
     ap.add_argument("--diag-skip", default="", help="diagnostics only (not the metric): comma list of stereo,keyframes "
                                                      "to leave out of the step")
@@ -118,22 +122,65 @@ def compulsory_bytes(cfg):
     return {"extraction": img + n * (28 + 32), "stereo_match": 2 * n * 32 + n * 8}
 
 
-def tri_geometry_rows(cfg):
-    """F12 and epipole rows for a keyframe and its d-th previous keyframe, d = 1..TRI_NEIGHBOURS: a synthetic
-    trajectory of 0.8 m forward and 0.01 rad of yaw per keyframe (baseline > the stereo baseline, so
-    LocalMapping.cc:252-256 keeps every neighbour).  (TRI_NEIGHBOURS, 12) float32 tensor on the CPU."""
-    import torch
-    from multiagent_orb_slam2_amd import multiagent as MA
-    n = TRI_NEIGHBOURS + 1
-    K = torch.tensor([[cfg["fx"], 0, cfg["cols"] / 2], [0, cfg["fx"], cfg["rows"] / 2], [0, 0, 1]], dtype=torch.float64)
-    yaw = 0.01 * torch.arange(n, dtype=torch.float64)
-    R = torch.zeros((n, 3, 3), dtype=torch.float64)
-    R[:, 0, 0], R[:, 0, 2], R[:, 1, 1], R[:, 2, 0], R[:, 2, 2] = yaw.cos(), -yaw.sin(), 1, yaw.sin(), yaw.cos()
-    Ow = torch.stack([0.05 * torch.sin(0.3 * torch.arange(n, dtype=torch.float64)), torch.zeros(n),
-                      0.8 * torch.arange(n, dtype=torch.float64)], 1)
-    t = -(R @ Ow[:, :, None])[:, :, 0]
-    pairs = torch.tensor([[n - 1, n - 1 - d] for d in range(1, n)])
-    return MA.triangulation_geometry(K, R, t, pairs)
+class Geometry:
+    """The synthetic camera motion the matching stages need (the reference's poses come from tracking and optimisation,
+    which are out of scope): KITTI intrinsics with the principal point at the image centre, no distortion (bounds =
+    the image); keyframes of an agent on a closed circle (multiagent.circle_trajectory: 0.8 m apart, heading along it),
+    one pose per keyframe-ring position, so the ring has no seam; for the tracking stage, frame i's last frame at the
+    origin and the current frame moved by the motion model's residual (6 cm forward, 1 cm sideways, 0.2 deg of yaw)."""
+
+    def __init__(self, cfg, ring_kf: int):
+        from multiagent_orb_slam2_amd import multiagent as MA
+        self.cfg = cfg
+        self.fx = cfg["fx"]
+        self.camera = np.array([cfg["fx"], cfg["fx"], cfg["cols"] / 2, cfg["rows"] / 2], np.float32)
+        self.bf = cfg["bf"]
+        self.bounds = (0.0, float(cfg["cols"]), 0.0, float(cfg["rows"]))
+        self.ring_kf = max(ring_kf, TRI_NEIGHBOURS + 2)
+        self.Rwc, self.Ow = MA.circle_trajectory(self.ring_kf)
+        a = 0.0035
+        self.R_cur = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+        self.O_cur = np.array([0.01, 0.0, 0.06])
+        tlc = self.O_cur                                    # the current camera centre in the last frame (:1344-1352)
+        mb = self.bf / self.fx
+        self.level_mode = 1 if tlc[2] > mb else (-1 if -tlc[2] > mb else 0)
+
+    def K(self):
+        c = self.camera
+        return np.array([[c[0], 0, c[2]], [0, c[1], c[3]], [0, 0, 1]], np.float64)
+
+    def tracking_views(self):
+        from multiagent_orb_slam2_amd import multiagent as MA
+        lf = MA.make_view(self.R_cur, self.O_cur, self.camera, self.bf, self.bounds, 7.0, level_mode=self.level_mode)
+        mp = MA.make_view(self.R_cur, self.O_cur, self.camera, self.bf, self.bounds, 1.0, view_cos_limit=0.5)
+        twc_last = np.concatenate([np.eye(3).reshape(9), np.zeros(3)]).astype(np.float32)
+        return twc_last, lf, mp
+
+    def slot_tables(self, slots: int, world: int, n_kf: int):
+        """Per keyframe-store slot: Twc (12 floats) and the Fuse view (th = 3) of the keyframe held there; slot s holds
+        keyframe c(s) of its agent (slots are rank-major per step: multiagent KeyframeFusion)."""
+        from multiagent_orb_slam2_amd import multiagent as MA
+        from multiagent_orb_slam2_amd.orbx import VIEW_DTYPE
+        per = world * n_kf
+        twc = np.zeros((slots, 12), np.float32)
+        views = np.zeros(slots, VIEW_DTYPE)
+        for s in range(slots):
+            c = ((s // per) * n_kf + (s % per) % n_kf) % self.ring_kf
+            twc[s, :9], twc[s, 9:] = self.Rwc[c].reshape(9), self.Ow[c]
+            views[s] = MA.make_view(self.Rwc[c], self.Ow[c], self.camera, self.bf, self.bounds, 3.0)
+        return twc, views
+
+    def tri_rows(self):
+        """F12 and epipole rows for a keyframe and its d-th previous keyframe on the circle, d = 1..TRI_NEIGHBOURS (the
+        same for every keyframe: the circle's relative poses repeat; every baseline (>= 0.8 m) passes
+        LocalMapping.cc:252-256).  (TRI_NEIGHBOURS, 12) float32 tensor on the CPU."""
+        import torch
+        from multiagent_orb_slam2_amd import multiagent as MA
+        n = TRI_NEIGHBOURS + 1
+        Rcw = torch.tensor(np.transpose(self.Rwc[:n], (0, 2, 1)))
+        t = -(Rcw @ torch.tensor(self.Ow[:n])[:, :, None])[:, :, 0]
+        pairs = torch.tensor([[n - 1, n - 1 - d] for d in range(1, n)])
+        return MA.triangulation_geometry(torch.tensor(self.K()), Rcw, t, pairs)
 
 
 def cpu_threads():
@@ -171,29 +218,46 @@ def cpu_model():
 
 
 class CpuAgent:
-    """The per-frame work on host cores with the oracle (oracle/orb_oracle.cpp -O3, same FP pins): extract L and R,
-    ComputeStereoMatches (band search + SAD refinement), and every KF_EVERY-th frame a keyframe: BoW transform,
-    DetectLoopCandidates over a keyframe ring of the GPU store's size, SearchByBoW against the first KF_CANDIDATES
-    candidates, then the keyframe joins the database (MapFusion's query-then-add).  One per thread, as one
-    extractor per agent (Tracking.cc:119-125)."""
+    """The per-frame work on host cores with the oracle (oracle/*.cpp -O3, same FP pins): extract L and R,
+    ComputeStereoMatches (band search + SAD refinement), the tracking matches (the last frame's stereo MapPoints
+    projected and searched, SearchByProjection(F, LastF, 7), then SearchLocalPoints: isInFrustum +
+    SearchByProjection(F, vpMapPoints, 1)), and every KF_EVERY-th frame a keyframe: BoW transform, CreateNewMapPoints'
+    SearchForTriangulation vs TRI_NEIGHBOURS neighbours + the new MapPoints' descriptors, SearchInNeighbors' Fuse both
+    ways with each neighbour, DetectLoopCandidates over a keyframe ring of the GPU store's size, SearchByBoW against the
+    first KF_CANDIDATES candidates, then the keyframe joins the database (MapFusion's query-then-add) -- the GPU step's
+    work.  One per thread, as one extractor per agent (Tracking.cc:119-125)."""
 
-    def __init__(self, O, cfg, tables, voc, n_kf_step, tri=None):
-        self.O, self.cfg, self.tables = O, cfg, tables
-        self.tri = tri                                 # (TRI_NEIGHBOURS, 12) geometry rows, None = no triangulation
+    def __init__(self, O, cfg, tables, voc, n_kf_step, geo, tri=True, track=True, fuse=True):
+        from multiagent_orb_slam2_amd.orbx import PROJ_FUSE, PROJ_LASTFRAME, PROJ_MAPPOINTS, ProjParams, frame_grid
+        self.O, self.cfg, self.tables, self.geo = O, cfg, tables, geo
+        self.tri = geo.tri_rows().numpy() if tri else None
+        self.track, self.fuse = track, fuse
         self.vocab = O.Vocabulary(voc)
         self.ring = STORE_STEPS * max(1, n_kf_step)
         self.db = O.Kfdb(int(np.sum(voc["is_leaf"])), self.ring)
         self.kfs = [None] * self.ring
         self.kps = [None] * self.ring
+        self.kfx = [None] * self.ring                  # (kps, desc, uright, MapPoints) per slot, for Fuse
         self.n_kf = 0
         self.n = 0
+        self.grid = frame_grid(0, 0, cfg["cols"], cfg["rows"])
+        self.twc_last, self.v_lf, self.v_mp = geo.tracking_views()
+        self.twc_slot, self.v_slot = geo.slot_tables(self.ring, 1, max(1, n_kf_step))
+        self.log_sf = float(np.float32(np.log(SCALE)))
+        isg = tables["inv_sigma2"]
+        self.p_lf = ProjParams.make(PROJ_LASTFRAME, 100, 0.9, True, isg)
+        self.p_mp = ProjParams.make(PROJ_MAPPOINTS, 100, 0.8, False, isg)
+        self.p_fu = ProjParams.make(PROJ_FUSE, 50, 0.6, False, isg)
+        self.modes = (PROJ_LASTFRAME, PROJ_MAPPOINTS, PROJ_FUSE)
 
     def frame(self, left, right):
         O, c = self.O, self.cfg
         a = O.extract(left, nfeatures=c["nfeatures"], want_pyramid=True)
         b = O.extract(right, nfeatures=c["nfeatures"], want_pyramid=True)
-        _, depth = O.compute_stereo_matches(a, b, self.tables["scale"], self.tables["inv_scale"], c["rows"], c["bf"],
-                                            c["bf"] / c["fx"])
+        ur, depth = O.compute_stereo_matches(a, b, self.tables["scale"], self.tables["inv_scale"], c["rows"], c["bf"],
+                                             c["bf"] / c["fx"])
+        if self.track:
+            self.tracking(a, ur, depth)
         if self.n % KF_EVERY == 0:
             bow = self.vocab.transform(a["desc"], 4)
             kf = (a["desc"], a["kps"]["angle"], (depth > 0).astype(np.uint8),
@@ -201,6 +265,8 @@ class CpuAgent:
             slot = self.n_kf % self.ring
             if self.tri is not None:
                 self.new_mappoints(a, kf)
+            if self.fuse:
+                self.local_fuse(slot, a, ur, depth)
             self.db.erase([slot])
             self.db.set_bow(slot, bow["bow_words"], bow["bow_values"])
             for cand in self.db.detect(0, slot, self.n_kf + 1, 0.0)[:KF_CANDIDATES]:
@@ -210,6 +276,35 @@ class CpuAgent:
             self.kps[slot] = a["kps"]
             self.n_kf += 1
         self.n += 1
+
+    def tracking(self, a, ur, depth):
+        """TrackWithMotionModel's search and SearchLocalPoints, as multiagent.FrameTracker."""
+        from multiagent_orb_slam2_amd.orbx import PROJ_QUERY_DTYPE, QF_BLOCKS, QF_SKIP
+        O, sc = self.O, self.tables["scale"]
+        lf, mp, _ = self.modes
+        pts = O.stereo_mappoints(a["kps"], depth, self.twc_last, self.geo.camera, sc, QF_BLOCKS)
+        q1 = O.project(lf, pts, self.v_lf, sc, self.log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
+        _, qi1, _, own1 = O.proj_search(self.p_lf, self.grid, q1, a["desc"], a["kps"], a["desc"], uright=ur)
+        pts["flags"][qi1 >= 0] |= QF_SKIP
+        q2 = O.project(mp, pts, self.v_mp, sc, self.log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
+        O.proj_search(self.p_mp, self.grid, q2, a["desc"], a["kps"], a["desc"], uright=ur,
+                      blocked=(own1 >= 0).astype(np.uint8))
+
+    def local_fuse(self, slot, a, ur, depth):
+        """SearchInNeighbors' Fuse both ways with each of the previous TRI_NEIGHBOURS keyframes, as multiagent.LocalFuse."""
+        from multiagent_orb_slam2_amd.orbx import PROJ_QUERY_DTYPE, QF_BLOCKS
+        O, sc, fu = self.O, self.tables["scale"], self.modes[2]
+        pts = O.stereo_mappoints(a["kps"], depth, self.twc_slot[slot], self.geo.camera, sc, QF_BLOCKS)
+        self.kfx[slot] = (a["kps"], a["desc"], ur, pts)
+        for d in range(1, TRI_NEIGHBOURS + 1):
+            if self.n_kf - d < 0:
+                break
+            s2 = (self.n_kf - d) % self.ring
+            k2, d2, ur2, p2 = self.kfx[s2]
+            q = O.project(fu, pts, self.v_slot[s2], sc, self.log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
+            O.proj_search(self.p_fu, self.grid, q, a["desc"], k2, d2, uright=ur2)
+            q = O.project(fu, p2, self.v_slot[slot], sc, self.log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
+            O.proj_search(self.p_fu, self.grid, q, d2, a["kps"], a["desc"], uright=ur)
 
     def new_mappoints(self, a, kf):
         """SearchForTriangulation against the previous TRI_NEIGHBOURS keyframes with ORBmatcher(0.6, false), then the
@@ -242,16 +337,16 @@ class CpuAgent:
         O.distinctive_descriptors_flat(parts.reshape(-1, 32), off)
 
 
-def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds, tri=True):
+def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds, geo, tri=True, track=True, fuse=True):
     """1-thread latency per stereo frame (median / p95) and T-thread throughput with one agent per thread on
     independent frames -- the reference drivers' timing pattern (generic_split_seq.cc:277-314, :369-379: per-frame
     steady_clock around TrackStereo, median and mean reported)."""
     from oracle import oracle as O
     tables = O.tables(cfg["nfeatures"])
     nd = len(lefts)
-    geo = tri_geometry_rows(cfg).numpy() if tri else None
+    mk = lambda: CpuAgent(O, cfg, tables, voc, n_kf_step, geo, tri=tri, track=track, fuse=fuse)  # noqa: E731
     # (i) latency, one thread
-    ag = CpuAgent(O, cfg, tables, voc, n_kf_step, geo)
+    ag = mk()
     lat = []
     t_end = time.perf_counter() + 0.4 * seconds
     while True:
@@ -263,7 +358,7 @@ def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds, tri=True):
     lat_ms = np.array(lat[1:] if len(lat) > 1 else lat) * 1e3
     # (ii) throughput, T threads (ctypes releases the GIL inside the oracle's C++)
     T = cpu_threads()
-    agents = [CpuAgent(O, cfg, tables, voc, n_kf_step, geo) for _ in range(T)]
+    agents = [mk() for _ in range(T)]
     stop = threading.Event()
 
     def run(i):
@@ -282,6 +377,10 @@ def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds, tri=True):
         t.join()
     el = time.perf_counter() - t0
     done = sum(a.n for a in agents)
+    work = "2 extractions + ComputeStereoMatches" + (" + the tracking matches (motion model + local map)" if track else "")
+    kfw = "BoW" + (f" + CreateNewMapPoints matching vs {TRI_NEIGHBOURS} neighbours" if tri else "") + \
+          (" + Fuse both ways with each neighbour" if fuse else "") + \
+          f" + DetectLoopCandidates + SearchByBoW vs the first {KF_CANDIDATES} candidates"
     return {"value": round(done / el, 3), "unit": "frames/s", "cores": T, "kind": "port",
             "cpu_model": cpu_model(), "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": cpu_quota(),
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
@@ -289,9 +388,8 @@ def cpu_baseline(lefts, rights, cfg, voc, n_kf_step, seconds, tri=True):
                                    "p95": round(float(np.percentile(lat_ms, 95)), 2), "frames": len(lat_ms)},
             "throughput_1thread_fps": round(1e3 / float(np.mean(lat_ms)), 3),
             "sample": f"{done} stereo frames on {T} threads in {el:.1f} s (+ {len(lat)} on 1 thread for latency) of the "
-                      f"same synthetic inputs and the same per-frame work (2 extractions + ComputeStereoMatches; every "
-                      f"{KF_EVERY}th frame BoW + DetectLoopCandidates + SearchByBoW vs the first {KF_CANDIDATES} "
-                      f"candidates), oracle/orb_oracle.cpp -O3 -ffp-contract=off, one agent per thread"}
+                      f"same synthetic inputs and the same per-frame work ({work}; every {KF_EVERY}th frame {kfw}), "
+                      f"oracle/*.cpp -O3 -ffp-contract=off, one agent per thread"}
 
 
 def host_api_rate(pkg, cfg, lefts, rights, n_frames, device):
@@ -729,22 +827,38 @@ def main():
     # this agent (all pairs in one launch; MapPoint flags = the store's valid field, i.e. stereo depth > 0), then
     # the distinctive descriptors of its keypoints' observation lists.  FeatureVector nodes at levelsup 4 of a k=10,
     # L=6 tree: at most 10^2 per keyframe
+    geo = Geometry(cfg, STORE_STEPS * n_kf)
     tri, tri_pat = None, {}
+
+    def tri_pattern(q):
+        """(new slots, neighbour slots) of this agent's keyframes q (a slot range) as device tensors and host arrays: the
+        d-th previous keyframe of keyframe j sits (j - d) keyframes back in this agent's ring order."""
+        if q.start not in tri_pat:
+            nq, per = len(q), world * n_kf
+            nb = [[(q.start + ((j - d) // nq) * per + (j - d) % nq) % engine.slots for d in range(1, TRI_NEIGHBOURS + 1)]
+                  for j in range(nq)]
+            tri_pat[q.start] = (torch.tensor(list(q), dtype=torch.int32, device=dev),
+                                torch.tensor(nb, dtype=torch.int32, device=dev),
+                                np.array(list(q), np.int64), np.array(nb, np.int64))
+        return tri_pat[q.start]
     if args.tri:
         tri = MA.NewMapPoints(engine.store, 100, ex.GetScaleSigmaSquares(), ex.GetScaleFactors(),
                               matcher=pkg.ORBmatcher(0.6, False, device=dev.index))
-        tri_geom = tri_geometry_rows(cfg).float().to(dev).view(1, TRI_NEIGHBOURS, 12).expand(n_kf, -1, -1).contiguous()
-
-        def tri_pattern(q):
-            """(new slots, neighbour slots) of this agent's keyframes q (a slot range): the d-th previous keyframe of
-            keyframe j sits (j - d) keyframes back in this agent's ring order."""
-            if q.start not in tri_pat:
-                nq, per = len(q), world * n_kf
-                nb = [[(q.start + ((j - d) // nq) * per + (j - d) % nq) % engine.slots for d in range(1, TRI_NEIGHBOURS + 1)]
-                      for j in range(nq)]
-                tri_pat[q.start] = (torch.tensor(list(q), dtype=torch.int32, device=dev),
-                                    torch.tensor(nb, dtype=torch.int32, device=dev))
-            return tri_pat[q.start]
+        tri_geom = geo.tri_rows().float().to(dev).view(1, TRI_NEIGHBOURS, 12).expand(n_kf, -1, -1).contiguous()
+    grid = pkg.frame_grid(0, 0, COLS, ROWS)
+    log_sf = float(np.float32(np.log(SCALE)))
+    inv_sigma2 = ex.GetInverseScaleSigmaSquares()
+    tracker = None
+    if args.tracking:
+        twc_last, v_lf, v_mp = geo.tracking_views()
+        tracker = MA.FrameTracker(pkg.ORBmatcher(0.9, True, device=dev.index), B, cap, grid, geo.camera, BF, scale, log_sf,
+                                  dev, NS, twc_last, v_lf, v_mp, inv_sigma2)
+    fuse = None
+    kf_rows_t = torch.tensor(list(range(0, KF_EVERY * n_kf, KF_EVERY)), dtype=torch.int64, device=dev)
+    if args.fuse:
+        twc_s, views_s = geo.slot_tables(engine.slots, world, n_kf)
+        fuse = MA.LocalFuse(pkg.ORBmatcher(0.6, True, device=dev.index), engine.store, engine.slots, cap, grid, geo.camera,
+                            BF, scale, log_sf, inv_sigma2, twc_s, views_s, dev)
     if world > 1:
         send = torch.empty((n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
         gathered = torch.empty((world * n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
@@ -753,8 +867,10 @@ def main():
 
     skip = set(filter(None, args.diag_skip.split(",")))
     stereo_ms = []
+    track_ms = []
     kf_ms = []
     tri_ms = []
+    fuse_ms = []
     host_split = [0.0, 0.0]                            # host enqueue seconds: front-end, keyframe path
 
     last_handoff = [None]
@@ -793,10 +909,19 @@ def main():
             bi, bd = m.stereo_match_batch_device(kps[:B], desc[:B], cnt[:B], kps[B:], desc[B:], cnt[B:], cap, scale,
                                                  ROWS, BF, BASELINE_B, stream=stereo_stream)
             ur, depth = m.stereo_refine_batch_device(kps[:B], cnt[:B], kps[B:], bi, pyr, 0, pyr, B, BF, BASELINE_B,
-                                                     stream=stereo_stream)
+                                                     stream=stereo_stream,
+                                                     out=tracker.stereo_out(buf) if tracker is not None else None)
             if time_stereo:
                 e1.record(stereo_stream)
                 stereo_ms.append((e0, e1))
+            if tracker is not None:
+                # Tracking's matches of every frame: TrackWithMotionModel's SearchByProjection(F, LastF) and
+                # SearchLocalPoints (Tracking.cc:882-904, :1160-1205) on the frame's stereo MapPoints
+                tracker.run(buf, kps[:B], desc[:B], cnt[:B], stream=stereo_stream)
+                if time_stereo:
+                    e1t = torch.cuda.Event(enable_timing=True)
+                    e1t.record(stereo_stream)
+                    track_ms.append((e1, e1t))
         handoff = torch.cuda.Event()
         handoff.record(stereo_stream)
         stereo_done[pslot] = handoff
@@ -823,15 +948,25 @@ def main():
             e3 = torch.cuda.Event(enable_timing=True)
             e3.record(kf_stream)
             kf_ms.append((e2, e3))
+        qs = engine.last_step()[1]
+        ns, nb, ns_h, nb_h = tri_pattern(qs)
+        e5 = e3 if time_stereo else None
         if tri is not None:
-            ns, nb = tri_pattern(engine.last_step()[1])
-            e4 = e3 if time_stereo else None
             with torch.cuda.stream(kf_stream):
                 tri.run(ns, nb, tri_geom)
             if time_stereo:
                 e5 = torch.cuda.Event(enable_timing=True)
                 e5.record(kf_stream)
-                tri_ms.append((e4, e5))
+                tri_ms.append((e3, e5))
+        if fuse is not None:
+            # SearchInNeighbors' Fuse (LocalMapping.cc:486-520): the new keyframes' MapPoints into each neighbour and
+            # the neighbours' MapPoints into them
+            fuse.add_keyframes(qs, kps, desc, cnt, ur, depth, kf_rows_t, stream=kf_stream)
+            fuse.run(ns_h, nb_h, stream=kf_stream)
+            if time_stereo:
+                e6 = torch.cuda.Event(enable_timing=True)
+                e6.record(kf_stream)
+                fuse_ms.append((e5, e6))
         done = torch.cuda.Event()
         done.record(kf_stream)
         kf_done[buf] = done
@@ -903,16 +1038,22 @@ def main():
         "host_wall_split_ms_per_timed_step": {"front_end": round(1000 * (split1[0] - split0[0]) / args.steps, 3),
                                               "keyframe_path": round(1000 * (split1[1] - split0[1]) / args.steps, 3)},
         "config": {"workload": f"{args.config}: stereo frame = ORBextractor x2 ({COLS}x{ROWS}, 8 levels, {NFEAT} kpts) + "
-                               "stereo L<->R 256-bit Hamming band match + SAD sub-pixel refinement; every 5th frame a "
-                               "keyframe: DBoW2 transform (k=10, L=6) + " + (f"{collective} of KF packets + " if world > 1 else "") +
+                               "stereo L<->R 256-bit Hamming band match + SAD sub-pixel refinement" +
+                               ("; tracking matches: the last frame's stereo MapPoints projected + SearchByProjection "
+                                "(motion model, th 7) + isInFrustum + SearchByProjection (local map, th 1)"
+                                if args.tracking else "") +
+                               "; every 5th frame a keyframe: DBoW2 transform (k=10, L=6) + " +
+                               (f"{collective} of KF packets + " if world > 1 else "") +
                                "KeyFrameDatabase DetectLoopCandidates (query, then add) over the KF store + "
                                f"SearchByBoW vs the first {KF_CANDIDATES} candidates" +
-                               (f"; CreateNewMapPoints matching: SearchForTriangulation vs {TRI_NEIGHBOURS} neighbour "
-                                "keyframes + distinctive descriptors of the new keyframes' observation lists"
-                                if args.tri else "") +
                                (" of other agents' maps (MapFusion.cc:136-144)" if world > 1 else
                                 " of the agent's own map with minScore 0 (LoopClosing-like: N=1 has no other map, so these "
-                                "pairs are work MapFusion itself would not do)"),
+                                "pairs are work MapFusion itself would not do)") +
+                               (f"; CreateNewMapPoints matching: SearchForTriangulation vs {TRI_NEIGHBOURS} neighbour "
+                                "keyframes + the new MapPoints' distinctive descriptors" if args.tri else "") +
+                               (f"; SearchInNeighbors' Fuse: the new keyframe's MapPoints into each of its "
+                                f"{TRI_NEIGHBOURS} neighbours and theirs into it (projection + window search, th 3)"
+                                if args.fuse else ""),
                    "settings": cfg["source"],
                    "keyframes_per_gpu_per_step": n_kf, "bow_pairs_per_gpu_per_step": n_kf * KF_CANDIDATES,
                    "global_batch": B * world, "frames_per_gpu_per_step": B, "image": [ROWS, COLS],
@@ -937,6 +1078,12 @@ def main():
         tms = [a.elapsed_time(b) for a, b in tri_ms]
         if tms:
             per_call["keyframe_new_mappoints"] = float(np.mean(tms))   # after keyframe_bow_fusion, same stream
+        fms = [a.elapsed_time(b) for a, b in fuse_ms]
+        if fms:
+            per_call["keyframe_fuse"] = float(np.mean(fms))            # after keyframe_new_mappoints, same stream
+        trk = [a.elapsed_time(b) for a, b in track_ms]
+        if trk:
+            per_call["tracking_match"] = float(np.mean(trk))           # after stereo_match, the stereo stream
         out["stage_ms_per_step"] = {k: round(v, 4) for k, v in per_call.items()}
         out["roofline"], sec = roofline_lines(per_call, cfg, 2 * B, args.config)
         if sec:
@@ -976,7 +1123,7 @@ def main():
         out["host_api"] = host_api_rate(pkg, cfg, lefts, rights, args.host_api_frames, dev.index)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(lefts[:16], rights[:16], cfg, S.synthetic_vocabulary(2024, k=10, L=6), n_kf,
-                                           args.cpu_seconds, tri=args.tri)
+                                           args.cpu_seconds, geo, tri=args.tri, track=args.tracking, fuse=args.fuse)
     if skip:
         out["diag_skip"] = sorted(skip)
     engine.check()

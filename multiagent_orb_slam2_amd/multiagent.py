@@ -567,3 +567,240 @@ class NewMapPoints:
         best, desc = self.matcher.distinctive_descriptors_neighbours_device(self.store, new_slots.int().contiguous(),
                                                                            neighbours.int().contiguous(), m12)
         return m12, nm.view(n, nn), best, desc
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# Per-frame tracking matches and LocalMapping's Fuse on the device: the reference's callers of the
+# projection matchers, batched.  The poses are the caller's (the reference's motion model and optimisation are out of
+# scope); these classes run the matching work a Tracking / LocalMapping thread issues for them.
+# ---------------------------------------------------------------------------------------------------------------------
+def problem_table(n, **cols):
+    """ProjProblem structs (include/orbx.h orbx_proj_problem, 112 B) as an (n, 14) int64 array: each keyword is a
+    field name with an int (the same for every row) or an (n,) int array; pointer fields hold addresses, nq / n their
+    counts (the little-endian low half of the 8-byte slot, the padding zero)."""
+    order = ["queries", "qdesc", "nq", "kps", "desc", "uright", "blocked", "n", "cell_start", "cell_idx", "q_idx",
+             "q_dist", "owner", "nmatches"]
+    t = np.zeros((n, 14), np.int64)
+    for k, v in cols.items():
+        t[:, order.index(k)] = v
+    return t
+
+
+class FrameTracker:
+    """Tracking's matching for a batch of stereo frames (src/Tracking.cc), each against its last frame:
+    TrackWithMotionModel (:882-904): the last frame's MapPoints (UpdateLastFrame's stereo points, :823-880 -- made here
+    by orbx_stereo_mappoints from its depths and pose) projected into the current frame (orbx_proj_project, LASTFRAME)
+    and SearchByProjection(CurrentFrame, LastFrame, th=7) with ORBmatcher(0.9, true); then TrackLocalMap's
+    SearchLocalPoints (:1160-1205): the MapPoints not matched yet through isInFrustum(0.5) and
+    SearchByProjection(F, vpLocalMapPoints, th=1) with ORBmatcher(0.8), keypoints that got a MapPoint in the first search
+    excluded (:92-93 Observations() > 0).  The current frame's grid is Frame::AssignFeaturesToGrid (orbx_grid_build).
+    One launch per stage over the whole batch; buffers per output set (n_sets), problem tables built once per set.
+    For the bench the last frame of frame i is frame i itself seen from pose 'last' (its keypoints as the MapPoints'
+    observations), and the current pose is 'last' moved by a residual motion -- the motion model's prediction error."""
+
+    def __init__(self, matcher, batch: int, capacity: int, grid, camera, bf: float, scale, log_sf: float, device,
+                 n_sets: int, twc_last, view_last_frame, view_local_map, inv_sigma2):
+        import torch
+        from .orbx import PROJ_LASTFRAME, PROJ_MAPPOINTS, ProjParams
+        self.m, self.B, self.cap, self.grid = matcher, batch, capacity, grid
+        self.camera = np.ascontiguousarray(camera, np.float32)
+        self.scale = np.ascontiguousarray(scale, np.float32)
+        self.log_sf = float(log_sf)
+        dev = torch.device("cuda", device) if isinstance(device, int) else device
+        self.dev = dev
+        B, cap = batch, capacity
+        ncell = grid.cols * grid.rows
+        self.twc = torch.from_numpy(np.tile(np.asarray(twc_last, np.float32).reshape(1, 12), (B, 1))).to(dev)
+        self.v_lf = torch.from_numpy(np.tile(view_last_frame.view(np.uint8).reshape(1, 112), (B, 1))).to(dev)
+        self.v_mp = torch.from_numpy(np.tile(view_local_map.view(np.uint8).reshape(1, 112), (B, 1))).to(dev)
+        self.p_lf = ProjParams.make(PROJ_LASTFRAME, 100, 0.9, True, inv_sigma2)          # ORBmatcher(0.9, true), TH_HIGH
+        self.p_mp = ProjParams.make(PROJ_MAPPOINTS, 100, 0.8, False, inv_sigma2)         # ORBmatcher(0.8), TH_HIGH
+        self.sets = []
+        for _ in range(n_sets):
+            z = dict(pts=torch.empty((B, cap, 48), dtype=torch.uint8, device=dev),
+                     q1=torch.empty((B, cap, 40), dtype=torch.uint8, device=dev),
+                     q2=torch.empty((B, cap, 40), dtype=torch.uint8, device=dev),
+                     cs=torch.empty((B, ncell + 1), dtype=torch.int32, device=dev),
+                     ci=torch.empty((B, cap), dtype=torch.int32, device=dev),
+                     ur=torch.empty((B, cap), dtype=torch.float32, device=dev),
+                     depth=torch.empty((B, cap), dtype=torch.float32, device=dev),
+                     blk=torch.empty((B, cap), dtype=torch.bool, device=dev))
+            for k in ("qi1", "qd1", "qi2", "qd2"):
+                z[k] = torch.empty((B, cap), dtype=torch.int32, device=dev)
+            for k in ("own1", "own2"):
+                z[k] = torch.empty((B, cap), dtype=torch.int32, device=dev)
+            for k in ("nm1", "nm2"):
+                z[k] = torch.empty((B,), dtype=torch.int32, device=dev)
+            z["probs"] = {}
+            self.sets.append(z)
+
+    def stereo_out(self, s: int):
+        """(uright, depth) buffers of set s, for ORBmatcher.stereo_refine_batch_device(out=...)."""
+        return self.sets[s]["ur"], self.sets[s]["depth"]
+
+    def _problems(self, z, kps, desc):
+        import torch
+        key = (kps.data_ptr(), desc.data_ptr())
+        if key not in z["probs"]:
+            B, cap = self.B, self.cap
+            i = np.arange(B, dtype=np.int64)
+            common = dict(nq=cap, kps=kps.data_ptr() + i * cap * 28, desc=desc.data_ptr() + i * cap * 32,
+                          qdesc=desc.data_ptr() + i * cap * 32, uright=z["ur"].data_ptr() + i * cap * 4, n=cap,
+                          cell_start=z["cs"].data_ptr() + i * z["cs"].shape[1] * 4, cell_idx=z["ci"].data_ptr() + i * cap * 4)
+            t1 = problem_table(B, queries=z["q1"].data_ptr() + i * cap * 40, q_idx=z["qi1"].data_ptr() + i * cap * 4,
+                               q_dist=z["qd1"].data_ptr() + i * cap * 4, owner=z["own1"].data_ptr() + i * cap * 4,
+                               nmatches=z["nm1"].data_ptr() + i * 4, **common)
+            t2 = problem_table(B, queries=z["q2"].data_ptr() + i * cap * 40, q_idx=z["qi2"].data_ptr() + i * cap * 4,
+                               q_dist=z["qd2"].data_ptr() + i * cap * 4, owner=z["own2"].data_ptr() + i * cap * 4,
+                               nmatches=z["nm2"].data_ptr() + i * 4, blocked=z["blk"].data_ptr() + i * cap, **common)
+            z["probs"][key] = (torch.from_numpy(t1.view(np.uint8)).to(self.dev), torch.from_numpy(t2.view(np.uint8)).to(self.dev))
+        return z["probs"][key]
+
+    def run(self, s: int, kps, desc, counts, stream=None):
+        """Frames kps / desc / counts (B, cap, 28) / (B, cap, 32) / (B,) with the stereo results already in set s's
+        (uright, depth).  Returns (q_idx motion model, nmatches, q_idx local map, nmatches) tensors of set s."""
+        import torch
+        from .orbx import PROJ_LASTFRAME, PROJ_MAPPOINTS, QF_BLOCKS
+        z, m, cap = self.sets[s], self.m, self.cap
+        p1, p2 = self._problems(z, kps, desc)
+        m.stereo_mappoints_device(kps, z["depth"], counts, self.twc, self.camera, self.scale, QF_BLOCKS, out=z["pts"],
+                                  stream=stream)
+        m.proj_project_device(PROJ_LASTFRAME, z["pts"], counts, self.v_lf, self.scale, self.log_sf, out=z["q1"],
+                              stream=stream)
+        m.grid_build_device(self.grid, kps, counts, stream=stream, out=(z["cs"], z["ci"]))
+        m.proj_search_batch_device(self.p_lf, self.grid, p1, cap, cap, stream=stream)
+        with torch.cuda.stream(stream) if stream is not None else _nullcontext():
+            torch.ge(z["own1"], 0, out=z["blk"])                    # keypoints that now hold a MapPoint
+        m.proj_project_device(PROJ_MAPPOINTS, z["pts"], counts, self.v_mp, self.scale, self.log_sf, out=z["q2"],
+                              found=z["qi1"], stream=stream)
+        m.proj_search_batch_device(self.p_mp, self.grid, p2, cap, cap, stream=stream)
+        return z["qi1"], z["nm1"], z["qi2"], z["nm2"]
+
+
+class _nullcontext:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
+def circle_trajectory(n: int, step: float = 0.8):
+    """n keyframe poses 'step' metres apart on a closed circle, heading along it (a periodic synthetic trajectory, so a
+    keyframe ring of n slots has no seam).  Returns (Rwc (n, 3, 3), Ow (n, 3)) float64."""
+    R_ = n * step / (2 * np.pi)
+    th = 2 * np.pi * np.arange(n) / n
+    c, s = np.cos(th), np.sin(th)
+    Rwc = np.zeros((n, 3, 3))
+    Rwc[:, 0, 0], Rwc[:, 0, 2], Rwc[:, 1, 1], Rwc[:, 2, 0], Rwc[:, 2, 2] = c, s, 1, -s, c
+    Ow = np.stack([R_ * (1 - c), np.zeros(n), R_ * s], 1)
+    return Rwc, Ow
+
+
+def make_view(Rwc, Ow, camera, bf, bounds, th, view_cos_limit=0.5, level_mode=0):
+    """orbx_view (VIEW_DTYPE) of a camera with pose (Rwc, Ow): Rcw = Rwc^T, tcw = -Rcw Ow."""
+    from .orbx import VIEW_DTYPE
+    v = np.zeros(1, VIEW_DTYPE)[0]
+    Rcw = np.asarray(Rwc, np.float64).T
+    v["R"] = Rcw.reshape(9)
+    v["t"] = -Rcw @ np.asarray(Ow, np.float64)
+    v["Ow"] = Ow
+    v["fx"], v["fy"], v["cx"], v["cy"] = camera
+    v["bf"] = bf
+    v["min_x"], v["max_x"], v["min_y"], v["max_y"] = bounds
+    v["th"], v["view_cos_limit"], v["level_mode"] = th, view_cos_limit, level_mode
+    return v
+
+
+class LocalFuse:
+    """LocalMapping::SearchInNeighbors' Fuse calls for a batch of new keyframes (src/LocalMapping.cc:460-520): each
+    new keyframe's MapPoints fused into each of its neighbours (Fuse(pKFi, vpMapPointMatches), :486-496) and the
+    neighbours' MapPoints fused into it (Fuse(mpCurrentKeyFrame, vpFuseCandidates), :499-520), the search part of
+    ORBmatcher::Fuse (:830-951: the projection by orbx_proj_project FUSE, th = 3, then the window search with the
+    stereo / mono reprojection tests and TH_LOW).  The replace / add-observation bookkeeping after each search is map
+    work (out of scope).  A keyframe's MapPoints come from its stereo depths (orbx_stereo_mappoints) at
+    creation and live in per-slot rings beside the keyframe store with its right coordinates and grid; the poses are
+    the caller's (here: a periodic trajectory, one pose per slot).  Fuse's candidates are deduplicated in the reference
+    (mnFuseCandidateForKF); here each neighbour's MapPoints are separate problems, as each is a separate view."""
+
+    def __init__(self, matcher, store, slots: int, capacity: int, grid, camera, bf: float, scale, log_sf: float,
+                 inv_sigma2, twc_slots, views_slots, device):
+        import torch
+        from .orbx import PROJ_FUSE, ProjParams
+        self.m, self.store, self.slots, self.cap, self.grid = matcher, store, slots, capacity, grid
+        self.camera = np.ascontiguousarray(camera, np.float32)
+        self.scale = np.ascontiguousarray(scale, np.float32)
+        self.log_sf = float(log_sf)
+        dev = torch.device("cuda", device) if isinstance(device, int) else device
+        self.dev = dev
+        ncell = grid.cols * grid.rows
+        self.pts = torch.zeros((slots, capacity, 48), dtype=torch.uint8, device=dev)
+        self.ur = torch.full((slots, capacity), -1.0, dtype=torch.float32, device=dev)
+        self.cnt = torch.zeros((slots,), dtype=torch.int32, device=dev)
+        self.cs = torch.zeros((slots, ncell + 1), dtype=torch.int32, device=dev)
+        self.ci = torch.zeros((slots, capacity), dtype=torch.int32, device=dev)
+        self.twc = torch.from_numpy(np.ascontiguousarray(twc_slots, np.float32).reshape(slots, 12)).to(dev)
+        self.views = torch.from_numpy(np.ascontiguousarray(views_slots).view(np.uint8).reshape(slots, 112)).to(dev)
+        self.params = ProjParams.make(PROJ_FUSE, 50, 0.6, False, inv_sigma2)             # TH_LOW
+        self.cache = {}
+
+    def add_keyframes(self, slots: range, kps, desc, counts, uright, depth, rows, stream=None):
+        """The new keyframes (rows of the extractor outputs) into the rings at 'slots' (a contiguous range)."""
+        import torch
+        from .orbx import QF_BLOCKS
+        a, b = slots.start, slots.stop
+        with torch.cuda.stream(stream) if stream is not None else _nullcontext():
+            torch.index_select(counts, 0, rows, out=self.cnt[a:b])
+            torch.index_select(uright, 0, rows, out=self.ur[a:b])
+            kk = torch.index_select(kps, 0, rows)
+            dk = torch.index_select(depth, 0, rows)
+        self.m.stereo_mappoints_device(kk, dk, self.cnt[a:b], self.twc[a:b], self.camera, self.scale, QF_BLOCKS,
+                                       out=self.pts[a:b], stream=stream)
+        self.m.grid_build_device(self.grid, kk, self.cnt[a:b], stream=stream, out=(self.cs[a:b], self.ci[a:b]))
+
+    def _plan(self, new_slots, neighbours):
+        """Per (new keyframe j, neighbour k): the two directions' views, point sets and problem tables (cached per
+        pattern: the ring's slot patterns repeat)."""
+        import torch
+        key = (tuple(new_slots), tuple(map(tuple, neighbours)))
+        if key in self.cache:
+            return self.cache[key]
+        n, nn = neighbours.shape
+        P, cap, st = n * nn, self.cap, self.store
+        ns = np.repeat(np.asarray(new_slots, np.int64), nn)
+        nb = np.asarray(neighbours, np.int64).reshape(-1)
+        ok = nb >= 0
+        nbc = np.where(ok, nb, 0)
+        dev = self.dev
+        out = {}
+        for d, (tgt, src) in enumerate(((nbc, ns), (ns, nbc))):   # 0: current MPs into neighbour; 1: neighbour MPs into current
+            q = torch.empty((P, cap, 40), dtype=torch.uint8, device=dev)
+            qi, qd = torch.empty((P, cap), dtype=torch.int32, device=dev), torch.empty((P, cap), dtype=torch.int32, device=dev)
+            own, nm = torch.empty((P, cap), dtype=torch.int32, device=dev), torch.empty((P,), dtype=torch.int32, device=dev)
+            i = np.arange(P, dtype=np.int64)
+            t = problem_table(P, queries=q.data_ptr() + i * cap * 40, qdesc=st.desc + src * st.desc_stride,
+                              nq=np.where(ok, cap, 0), kps=st.kps + tgt * st.kps_stride, desc=st.desc + tgt * st.desc_stride,
+                              uright=self.ur.data_ptr() + tgt * cap * 4, n=cap,
+                              cell_start=self.cs.data_ptr() + tgt * self.cs.shape[1] * 4,
+                              cell_idx=self.ci.data_ptr() + tgt * cap * 4, q_idx=qi.data_ptr() + i * cap * 4,
+                              q_dist=qd.data_ptr() + i * cap * 4, owner=own.data_ptr() + i * cap * 4,
+                              nmatches=nm.data_ptr() + i * 4)
+            views = self.views[torch.from_numpy(tgt).to(dev)].contiguous()
+            vpts = torch.from_numpy(src.astype(np.int32)).to(dev)
+            out[d] = dict(q=q, qi=qi, nm=nm, probs=torch.from_numpy(t.view(np.uint8)).to(dev), views=views, vpts=vpts)
+        self.cache[key] = out
+        return out
+
+    def run(self, new_slots, neighbours, stream=None):
+        """new_slots (n,) and neighbours (n, nn) as host int arrays (-1 = none).  Returns ((q_idx, nmatches) of the
+        current-into-neighbour searches, (q_idx, nmatches) of the neighbour-into-current ones), (n*nn, cap) / (n*nn,)."""
+        from .orbx import PROJ_FUSE
+        plan = self._plan(np.asarray(new_slots), np.asarray(neighbours))
+        res = []
+        for d in (0, 1):
+            p = plan[d]
+            self.m.proj_project_device(PROJ_FUSE, self.pts, self.cnt, p["views"], self.scale, self.log_sf, out=p["q"],
+                                       view_points=p["vpts"], stream=stream)
+            self.m.proj_search_batch_device(self.params, self.grid, p["probs"], self.cap, self.cap, stream=stream)
+            res.append((p["qi"], p["nm"]))
+        return res

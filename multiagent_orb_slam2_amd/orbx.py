@@ -620,13 +620,17 @@ class ORBmatcher:
         return ur, dp
 
     def stereo_refine_batch_device(self, kl, nl, kr, best_idx, left_pyramid, left_first, right_pyramid, right_first,
-                                   bf, b, stream=None):
+                                   bf, b, stream=None, out=None):
         """Sub-pixel half of Frame::ComputeStereoMatches (src/Frame.cc:554-639) on device batches; pyramids
-        from ORBextractor.pyramid_device().  Returns (uright, depth) (B, capacity) float32 device tensors."""
+        from ORBextractor.pyramid_device().  Returns (uright, depth) (B, capacity) float32 device tensors (written into
+        out = (uright, depth) when given)."""
         import torch
         B, cap = best_idx.shape
-        ur = torch.empty((B, cap), dtype=torch.float32, device=kl.device)
-        dp = torch.empty((B, cap), dtype=torch.float32, device=kl.device)
+        if out is None:
+            ur = torch.empty((B, cap), dtype=torch.float32, device=kl.device)
+            dp = torch.empty((B, cap), dtype=torch.float32, device=kl.device)
+        else:
+            ur, dp = out
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(kl.device).cuda_stream)
         _check(self._lib.orbx_stereo_refine_batch_device(self._h, _tp(kl), _tp(nl), _tp(kr), _tp(best_idx), B, cap,
                                                          C.byref(left_pyramid), left_first, C.byref(right_pyramid),
