@@ -574,13 +574,13 @@ class NewMapPoints:
 # projection matchers, batched.  The poses are the caller's (the reference's motion model and optimisation are out of
 # scope); these classes run the matching work a Tracking / LocalMapping thread issues for them.
 # ---------------------------------------------------------------------------------------------------------------------
-def problem_table(n, **cols):
-    """ProjProblem structs (include/orbx.h orbx_proj_problem, 112 B) as an (n, 14) int64 array: each keyword is a
-    field name with an int (the same for every row) or an (n,) int array; pointer fields hold addresses, nq / n their
+def problem_table(rows, **cols):
+    """ProjProblem structs (include/orbx.h orbx_proj_problem, 112 B) as a (rows, 14) int64 array: each keyword is a
+    field name with an int (the same for every row) or a (rows,) int array; pointer fields hold addresses, nq / n their
     counts (the little-endian low half of the 8-byte slot, the padding zero)."""
     order = ["queries", "qdesc", "nq", "kps", "desc", "uright", "blocked", "n", "cell_start", "cell_idx", "q_idx",
              "q_dist", "owner", "nmatches"]
-    t = np.zeros((n, 14), np.int64)
+    t = np.zeros((rows, 14), np.int64)
     for k, v in cols.items():
         t[:, order.index(k)] = v
     return t
@@ -611,8 +611,8 @@ class FrameTracker:
         B, cap = batch, capacity
         ncell = grid.cols * grid.rows
         self.twc = torch.from_numpy(np.tile(np.asarray(twc_last, np.float32).reshape(1, 12), (B, 1))).to(dev)
-        self.v_lf = torch.from_numpy(np.tile(view_last_frame.view(np.uint8).reshape(1, 112), (B, 1))).to(dev)
-        self.v_mp = torch.from_numpy(np.tile(view_local_map.view(np.uint8).reshape(1, 112), (B, 1))).to(dev)
+        self.v_lf = torch.from_numpy(np.tile(_view_bytes(view_last_frame), (B, 1))).to(dev)
+        self.v_mp = torch.from_numpy(np.tile(_view_bytes(view_local_map), (B, 1))).to(dev)
         self.p_lf = ProjParams.make(PROJ_LASTFRAME, 100, 0.9, True, inv_sigma2)          # ORBmatcher(0.9, true), TH_HIGH
         self.p_mp = ProjParams.make(PROJ_MAPPOINTS, 100, 0.8, False, inv_sigma2)         # ORBmatcher(0.8), TH_HIGH
         self.sets = []
@@ -675,6 +675,12 @@ class FrameTracker:
                               found=z["qi1"], stream=stream)
         m.proj_search_batch_device(self.p_mp, self.grid, p2, cap, cap, stream=stream)
         return z["qi1"], z["nm1"], z["qi2"], z["nm2"]
+
+
+def _view_bytes(v):
+    """One VIEW_DTYPE record (array element or 1-element array) as a (1, 112) uint8 array."""
+    from .orbx import VIEW_DTYPE
+    return np.frombuffer(np.asarray(v, VIEW_DTYPE).reshape(1).tobytes(), np.uint8).reshape(1, 112)
 
 
 class _nullcontext:
@@ -740,7 +746,8 @@ class LocalFuse:
         self.cs = torch.zeros((slots, ncell + 1), dtype=torch.int32, device=dev)
         self.ci = torch.zeros((slots, capacity), dtype=torch.int32, device=dev)
         self.twc = torch.from_numpy(np.ascontiguousarray(twc_slots, np.float32).reshape(slots, 12)).to(dev)
-        self.views = torch.from_numpy(np.ascontiguousarray(views_slots).view(np.uint8).reshape(slots, 112)).to(dev)
+        self.views = torch.from_numpy(np.frombuffer(np.ascontiguousarray(views_slots).tobytes(), np.uint8)
+                                      .reshape(slots, 112).copy()).to(dev)
         self.params = ProjParams.make(PROJ_FUSE, 50, 0.6, False, inv_sigma2)             # TH_LOW
         self.cache = {}
 

@@ -91,11 +91,14 @@ class KfStore(C.Structure):
 
     @classmethod
     def from_fields(cls, capacity: int, **fields):
-        """fields: name -> (device tensor whose data_ptr is slot 0 of that field, slot stride in bytes).
-        The tensors are kept alive by the returned struct."""
+        """fields: name -> (device tensor whose data_ptr is slot 0 of that field, slot stride in bytes).  A field left
+        out is NULL (for callers that read only some fields, e.g. the projection matchers: desc and kps).  The tensors
+        are kept alive by the returned struct."""
         s = cls()
         s._keep = []
         for name in cls.FIELDS:
+            if name not in fields:
+                continue
             t, stride = fields[name]
             setattr(s, name, t.data_ptr())
             setattr(s, name + "_stride", int(stride))
