@@ -283,7 +283,9 @@ class CpuAgent:
         O, sc = self.O, self.tables["scale"]
         lf, mp, _ = self.modes
         pts = O.stereo_mappoints(a["kps"], depth, self.twc_last, self.geo.camera, sc, QF_BLOCKS)
-        q1 = O.project(lf, pts, self.v_lf, sc, self.log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
+        last = pts.copy()
+        last["flags"][1::2] |= QF_SKIP                      # the last frame holds the even keypoints' MapPoints
+        q1 = O.project(lf, last, self.v_lf, sc, self.log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
         _, qi1, _, own1 = O.proj_search(self.p_lf, self.grid, q1, a["desc"], a["kps"], a["desc"], uright=ur)
         pts["flags"][qi1 >= 0] |= QF_SKIP
         q2 = O.project(mp, pts, self.v_mp, sc, self.log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)

@@ -596,7 +596,8 @@ class FrameTracker:
     excluded (:92-93 Observations() > 0).  The current frame's grid is Frame::AssignFeaturesToGrid (orbx_grid_build).
     One launch per stage over the whole batch; buffers per output set (n_sets), problem tables built once per set.
     For the bench the last frame of frame i is frame i itself seen from pose 'last' (its keypoints as the MapPoints'
-    observations), and the current pose is 'last' moved by a residual motion -- the motion model's prediction error."""
+    observations), and the current pose is 'last' moved by a residual motion -- the motion model's prediction error.
+    The last frame holds the MapPoints of the even keypoints; the local map holds all of them."""
 
     def __init__(self, matcher, batch: int, capacity: int, grid, camera, bf: float, scale, log_sf: float, device,
                  n_sets: int, twc_last, view_last_frame, view_local_map, inv_sigma2):
@@ -615,6 +616,9 @@ class FrameTracker:
         self.v_mp = torch.from_numpy(np.tile(_view_bytes(view_local_map), (B, 1))).to(dev)
         self.p_lf = ProjParams.make(PROJ_LASTFRAME, 100, 0.9, True, inv_sigma2)          # ORBmatcher(0.9, true), TH_HIGH
         self.p_mp = ProjParams.make(PROJ_MAPPOINTS, 100, 0.8, False, inv_sigma2)         # ORBmatcher(0.8), TH_HIGH
+        # the last frame holds the MapPoints of every second keypoint (its tracked points); the local map holds all of
+        # them, so SearchLocalPoints has the other half plus the motion-model misses to find (found >= 0: skipped)
+        self.lf_skip = torch.tensor([-1, 0], dtype=torch.int32).repeat(B, (cap + 1) // 2)[:, :cap].contiguous().to(dev)
         self.sets = []
         for _ in range(n_sets):
             z = dict(pts=torch.empty((B, cap, 48), dtype=torch.uint8, device=dev),
@@ -666,7 +670,7 @@ class FrameTracker:
         m.stereo_mappoints_device(kps, z["depth"], counts, self.twc, self.camera, self.scale, QF_BLOCKS, out=z["pts"],
                                   stream=stream)
         m.proj_project_device(PROJ_LASTFRAME, z["pts"], counts, self.v_lf, self.scale, self.log_sf, out=z["q1"],
-                              stream=stream)
+                              found=self.lf_skip, stream=stream)
         m.grid_build_device(self.grid, kps, counts, stream=stream, out=(z["cs"], z["ci"]))
         m.proj_search_batch_device(self.p_lf, self.grid, p1, cap, cap, stream=stream)
         with torch.cuda.stream(stream) if stream is not None else _nullcontext():
