@@ -316,19 +316,31 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
     asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return as_h2(r);
 }
+// Pair-image row r of k_fast_wave starts at dword kS * r + kC * (r / 4).  The padded form (kS = 19, kC = 4) is laid
+// out for the compass pre-test's ds_read_b32 loads: a 32-lane half reads 8 rows x 4 quads (QR = 4) at base(row) + 4u
+// + o; with kS odd, rows r .. r+3 of a group of four start in distinct residues mod 4, and rows r and r + 4 start
+// 4 kS + kC = 80 = 16 (mod 32) dwords apart, so the half's 32 dwords sit in 32 distinct banks.  (A plain stride of 24
+// put every row at a multiple of 8 dwords: 8 banks, 4-way conflicts on every pre-test load.)
+template <int kS, int kC>
+__device__ __forceinline__ int fastw_row(int r) { return kS * r + kC * (r >> 2); }
+__host__ __device__ constexpr int fastw_image_words(int rows, int s, int c) { return s * rows + c * ((rows - 1) >> 2); }
+
 // the 16 circle taps + centre of a pixel pair on the f16-biased pair image (pair words; odd offsets by v_alignbit)
-template <int kPairStride>
+template <int kS, int kC>
 __device__ __forceinline__ void fast_taps_f16(const uint32_t* __restrict__ E, int y, int j, uint32_t (&r)[17]) {
-    const uint32_t* eb = E + (y - 3) * kPairStride + j;
+    const int r0 = y - 3, m = r0 & 3;
+    const uint32_t* eb = E + fastw_row<kS, kC>(r0) + j;
+    // row r0 + d starts kS * d + kC * ((m + d) / 4) dwords after row r0
+#define ORBX_TAP_W(dy, w) eb[((dy) + 3) * kS + (kC ? kC * ((m + (dy) + 3) >> 2) : 0) + (w)]
 #define ORBX_TAP(k, dx, dy) \
-    r[k] = ((dx) & 1) ? eb[((dy) + 3) * kPairStride + (3 + (dx)) / 2] \
-                      : align16(eb[((dy) + 3) * kPairStride + 2 + (dx) / 2], eb[((dy) + 3) * kPairStride + 1 + (dx) / 2])
+    r[k] = ((dx) & 1) ? ORBX_TAP_W(dy, (3 + (dx)) / 2) : align16(ORBX_TAP_W(dy, 2 + (dx) / 2), ORBX_TAP_W(dy, 1 + (dx) / 2))
     ORBX_TAP(16, 0, 0);
     ORBX_TAP(0, 0, 3);    ORBX_TAP(1, 1, 3);    ORBX_TAP(2, 2, 2);    ORBX_TAP(3, 3, 1);
     ORBX_TAP(4, 3, 0);    ORBX_TAP(5, 3, -1);   ORBX_TAP(6, 2, -2);   ORBX_TAP(7, 1, -3);
     ORBX_TAP(8, 0, -3);   ORBX_TAP(9, -1, -3);  ORBX_TAP(10, -2, -2); ORBX_TAP(11, -3, -1);
     ORBX_TAP(12, -3, 0);  ORBX_TAP(13, -3, 1);  ORBX_TAP(14, -2, 2);  ORBX_TAP(15, -1, 3);
 #undef ORBX_TAP
+#undef ORBX_TAP_W
 }
 __device__ __forceinline__ s16x2 fast_score_from_taps_f16(const uint32_t (&r)[17]) {
     const h16x2 v = as_h2(r[16]);
@@ -394,10 +406,10 @@ __device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, 
 struct WaveLds {               // per-wave slice of k_fast_wave's dynamic LDS (byte offsets inside the slice)
     int o_sc, o_list, bytes;   // E pair image at 0 (the NMS key lists reuse it), score map, survivor list; slice size
 };
-// rows: max ROI rows; sw: max score-map row (int16); np: max pixel pairs; ps: dwords per pair-image row
-__host__ __device__ __forceinline__ WaveLds wave_lds(int rows, int sw, int np, int ps) {
+// rows: max ROI rows; sw: max score-map row (int16); np: max pixel pairs; iw: pair-image dwords (fastw_image_words)
+__host__ __device__ __forceinline__ WaveLds wave_lds(int rows, int sw, int np, int iw) {
     WaveLds b;
-    int o = rows * ps * 4;
+    int o = (iw * 4 + 15) & ~15;
     b.o_sc = o;   o += ((rows - 4) * sw * 2 + 15) & ~15;
     b.o_list = o; o += (np * 2 + 15) & ~15;
     b.bytes = o;
@@ -406,22 +418,21 @@ __host__ __device__ __forceinline__ WaveLds wave_lds(int rows, int sw, int np, i
 
 // Compass pre-test of quad (rr, u) of a cell (pairs 4u .. 4u+3 of detection row rr) at threshold t; also writes the
 // quad's score-map words (0, or -1 for the missing second pixel of an odd-width row).  A lane reads the 7 E words of
-// row y and the 5 of rows y-3 / y+3 of its 4 pixel pairs with 16 / 8-byte LDS reads (9 reads per 4 pairs, not 32).
+// row y and the 5 of rows y-3 / y+3 of its 4 pixel pairs (17 dwords, 9 ds_read2_b32 / ds_read_b32 per 4 pairs, not 32);
+// the padded row layout (fastw_row) keeps each 32-lane half of those reads on 32 distinct banks.
 struct QuadTaps { uint32_t A[7], U[6], D[6]; };   // E words of rows y (7), y-3 and y+3 (5 each) of one quad
 
-template <int kPS>
+template <int kS, int kC>
 __device__ __forceinline__ QuadTaps fastw_quad_load(const uint32_t* __restrict__ E, int rr, int u) {
-    const uint32_t* e0 = E + rr * kPS + 4 * u;                       // row y-3 (16-byte aligned)
-    const uint32_t* e1 = e0 + 3 * kPS;                               // row y
-    const uint32_t* e2 = e0 + 6 * kPS;                               // row y+3
+    const uint32_t* e0 = E + fastw_row<kS, kC>(rr) + 4 * u;          // row y-3
+    const uint32_t* e1 = E + fastw_row<kS, kC>(rr + 3) + 4 * u;      // row y
+    const uint32_t* e2 = E + fastw_row<kS, kC>(rr + 6) + 4 * u;      // row y+3
     QuadTaps q;
-    const uint4 a = *reinterpret_cast<const uint4*>(e1);
-    const uint2 b = *reinterpret_cast<const uint2*>(e1 + 4);
-    q.A[0] = a.x; q.A[1] = a.y; q.A[2] = a.z; q.A[3] = a.w; q.A[4] = b.x; q.A[5] = b.y; q.A[6] = e1[6];
-    const uint2 u23 = *reinterpret_cast<const uint2*>(e0 + 2), u45 = *reinterpret_cast<const uint2*>(e0 + 4);
-    q.U[0] = 0; q.U[1] = e0[1]; q.U[2] = u23.x; q.U[3] = u23.y; q.U[4] = u45.x; q.U[5] = u45.y;
-    const uint2 d23 = *reinterpret_cast<const uint2*>(e2 + 2), d45 = *reinterpret_cast<const uint2*>(e2 + 4);
-    q.D[0] = 0; q.D[1] = e2[1]; q.D[2] = d23.x; q.D[3] = d23.y; q.D[4] = d45.x; q.D[5] = d45.y;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) q.A[k] = e1[k];
+    q.U[0] = 0; q.D[0] = 0;
+#pragma unroll
+    for (int k = 1; k < 6; ++k) { q.U[k] = e0[k]; q.D[k] = e2[k]; }
     return q;
 }
 
@@ -468,11 +479,13 @@ __device__ __forceinline__ int rank_below(uint64_t b, int acc = 0) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, (uint32_t)acc));
 }
 
-// score-map row stride (int16) per pair stride: >= (Wd + 5) & ~1 for every cell the pair stride admits
-__host__ __device__ constexpr int fastw_sw(int ps) { return ps == 20 ? 36 : ps == 24 ? 44 : 76; }
+// score-map row stride (int16) per pair stride: >= (Wd + 5) & ~1 for every cell the pair stride admits (40 = 20 dwords
+// for the padded layout: its NMS reads model at 1.6 extra cycles per access against 1.8 for 22 dwords,
+// scripts/micro/lds_banks.py)
+__host__ __device__ constexpr int fastw_sw(int ps) { return ps == 19 ? 40 : 76; }
 
 // The part of a cell after its ROI is in LDS: pre-test, scores, NMS at both thresholds, the cell's candidate slots.
-template <int kPS>
+template <int kPS, int kPC>
 __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __restrict__ sc, uint16_t* __restrict__ list,
                                            const CellDev& cd, int img, int* __restrict__ cnt_out, int Wd, int Hd, int T1,
                                            int T2, int tp, uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
@@ -515,8 +528,8 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
             const int rb = rr, ub = u;
             step(rr, u);
             const bool va = qa < NQ4, vb = qb < NQ4;
-            const QuadTaps ta = fastw_quad_load<kPS>(E, va ? ra : 0, va ? ua : 0);
-            const QuadTaps tb = fastw_quad_load<kPS>(E, vb ? rb : 0, vb ? ub : 0);
+            const QuadTaps ta = fastw_quad_load<kPS, kPC>(E, va ? ra : 0, va ? ua : 0);
+            const QuadTaps tb = fastw_quad_load<kPS, kPC>(E, vb ? rb : 0, vb ? ub : 0);
             const uint32_t ma = va ? fastw_quad_test(ta, ua, tpre, PR, Wd) : 0u;
             const uint32_t mb = vb ? fastw_quad_test(tb, ub, tpre, PR, Wd) : 0u;
             emit(ma, ra, ua);
@@ -530,8 +543,8 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
         const uint32_t e1 = list[i], e2 = i2 < ns ? list[i2] : e1;
         const int rr1 = e1 >> 8, j1 = e1 & 0xff, rr2 = e2 >> 8, j2 = e2 & 0xff;
         uint32_t t1[17], t2[17];
-        fast_taps_f16<kPS>(E, rr1 + 3, j1, t1);
-        fast_taps_f16<kPS>(E, rr2 + 3, j2, t2);
+        fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
+        fast_taps_f16<kPS, kPC>(E, rr2 + 3, j2, t2);
         const s16x2 s1 = fast_score_from_taps_f16(t1), s2 = fast_score_from_taps_f16(t2);
         *(s16x2*)(sc + (rr1 + 1) * SW + 2 + 2 * j1) = (2 * j1 + 1 < Wd) ? s1 : (s16x2){s1.x, (short)-1};
         if (i2 < ns) *(s16x2*)(sc + (rr2 + 1) * SW + 2 + 2 * j2) = (2 * j2 + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
@@ -573,7 +586,7 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
     if (ln == 0) *cnt_out = n;
 }
 
-template <int kPS, int kWpg>
+template <int kPS, int kPC, int kWpg>
 __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restrict__ pyr, size_t pyr_stride,
                                                          const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
                                                          int cell0, int ncell, int iniTh, int minTh,
@@ -608,10 +621,10 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
         int lstride;
         const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
         const uint8_t* src0 = base + (size_t)cd.y0 * lstride + cd.x0;
-        if constexpr (kPS % 8 == 0) {
-            // 16-byte chunks (8 pair words each): a KITTI cell ROI (<= 38 x 38) is one round of <= 2 loads per lane.  The
-            // bytes past the ROI's width (< 16, inside the level row: the ROI ends >= 16 px before the level's edge) only
-            // reach pixels outside the detection window, which are masked.
+        if constexpr (kPC == 0) {
+            // 16-byte chunks (8 pair words each), rows 16-byte aligned: one round of <= 2 loads per lane for a 38 x 38
+            // ROI.  The bytes past the ROI's width (< 16, inside the level row: the ROI ends >= 16 px before the level's
+            // edge) only reach pixels outside the detection window, which are masked.
             const int cpr = (W + 15) >> 4, NQ = H * cpr;
             const int dr = kWave / cpr, dc = kWave - dr * cpr;      // item q -> q + 64 (no division per item)
             int r = ln / cpr, cc = ln - r * cpr;
@@ -638,14 +651,16 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
                                                     __builtin_amdgcn_perm(a.w, a.z, 0x0c030c02u) | 0x64006400u,
                                                     __builtin_amdgcn_perm(a.w, a.z, 0x0c050c04u) | 0x64006400u,
                                                     __builtin_amdgcn_perm(a.w, a.z, 0x0c070c06u) | 0x64006400u);
-                        uint4* dst = reinterpret_cast<uint4*>(E + rs[k] * kPS + 8 * cs[k]);
+                        uint4* dst = reinterpret_cast<uint4*>(E + fastw_row<kPS, kPC>(rs[k]) + 8 * cs[k]);
                         dst[0] = e0;
                         dst[1] = e1;
                     }
                 }
             }
         } else {
-            const int cpr = (W + 7) >> 3, NQ = H * cpr;
+            // padded rows (4-byte aligned, exactly kPS words for the widest ROI): 8-byte chunks, four ds_write_b32 per
+            // chunk, words past the ROI's (W + 1) / 2 not written (they belong to the next row)
+            const int cpr = (W + 7) >> 3, NQ = H * cpr, nw = (W + 1) >> 1;
             const int dr = kWave / cpr, dc = kWave - dr * cpr;          // item q -> q + 64 (no division per item)
             int r = ln / cpr, cc = ln - r * cpr;
             constexpr int kPf = 6;
@@ -671,11 +686,12 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
                             const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
                             lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
                         }
-                        const uint4 e = make_uint4(__builtin_amdgcn_perm(hi, lo, 0x0c010c00u) | 0x64006400u,
-                                                   __builtin_amdgcn_perm(hi, lo, 0x0c030c02u) | 0x64006400u,
-                                                   __builtin_amdgcn_perm(hi, lo, 0x0c050c04u) | 0x64006400u,
-                                                   __builtin_amdgcn_perm(hi, lo, 0x0c070c06u) | 0x64006400u);
-                        *reinterpret_cast<uint4*>(E + rs[k] * kPS + 4 * cs[k]) = e;
+                        uint32_t* dst = E + fastw_row<kPS, kPC>(rs[k]) + 4 * cs[k];
+                        const int w0 = 4 * cs[k];
+                        dst[0] = __builtin_amdgcn_perm(hi, lo, 0x0c010c00u) | 0x64006400u;
+                        if (w0 + 1 < nw) dst[1] = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u) | 0x64006400u;
+                        if (w0 + 2 < nw) dst[2] = __builtin_amdgcn_perm(hi, lo, 0x0c050c04u) | 0x64006400u;
+                        if (w0 + 3 < nw) dst[3] = __builtin_amdgcn_perm(hi, lo, 0x0c070c06u) | 0x64006400u;
                     }
                 }
         }
@@ -684,7 +700,7 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
         const int n16 = ((Hd + 2) * SW * 2 + 15) >> 4;
         for (int i = ln; i < n16; i += kWave) reinterpret_cast<uint4*>(sc)[i] = make_uint4(0, 0, 0, 0);
     }
-    fastw_body<kPS>(E, sc, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
+    fastw_body<kPS, kPC>(E, sc, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
 }
 
 // GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, integer separable path: taps {18,34,49,55,49,34,18},
@@ -1644,7 +1660,7 @@ struct Extractor {
     int node_cap = 0;
     // k_fast_wave: one wave per (cell, image), 4 waves per workgroup; launch 0 = level 0, launch 1 = levels >= 1, each
     // wave's LDS slice sized for its launch's largest cell
-    struct WaveLaunch { int cell0, n, ps, kcap; WaveLds lay; };
+    struct WaveLaunch { int cell0, n, ps, pc, kcap; WaveLds lay; };   // ps / pc: pair-image row stride / pad (fastw_row)
     WaveLaunch wave_launch[2] = {};
     static constexpr int kWaveWpg = 4;   // (1 or 2 waves per workgroup: faster alone, slower in the step)
     int wave_twopass = 1;     // iniTh first, minTh only for the cells left empty (0: one pass at min(iniTh, minTh))
@@ -1874,14 +1890,17 @@ int Extractor::configure(int r, int c, int batch) {
             for (int tx = 0; tx < (L.w + kBlurStrip - 1) / kBlurStrip; ++tx) tilev.push_back(BlurTile{l, tx, ty, 0});
     }
     ORBX_REQUIRE(cap < 32768 && cap < (1 << 20), ORBX_ERR_UNSUPPORTED, "node capacity %d too large", cap);
+    // k_quadtree's phase 1 scans (children << 16 | survivors) in one int: children <= 4 * cap must stay below 2^15
+    ORBX_REQUIRE(4 * cap < (1 << 15), ORBX_ERR_UNSUPPORTED, "node capacity %d too large for the packed split scan", cap);
     // k_fast_wave launches: level 0 (side stream) and levels 1..n-1, each wave's LDS slice sized for the launch's
-    // largest cell.  Pair stride >= 24: fewer resident FAST waves leave CUs to the overlapped stages (r3x: stride 20 is
-    // faster alone, 0.772 vs 0.825 ms serial, but 66.6k vs 67.1k frames/s in the step)
+    // largest cell.  Cells up to 38 px wide (every cell of the KITTI and EuRoC grids) use the padded 19-dword rows
+    // (fastw_row: bank-conflict-free pre-test, 20 dwords per row on average against 24 before); wider ones 40-dword
+    // rows, 16-byte aligned.
     for (int k = 0; k < 2; ++k) {
         WaveLaunch& wl = wave_launch[k];
         wl.cell0 = k == 0 ? 0 : lv[0].cell_end;
         wl.n = k == 0 ? lv[0].cell_end : (int)cellv.size() - lv[0].cell_end;
-        int rows = 8, sw = 8, np = 1, kcap = 1, psn = 24;
+        int rows = 8, sw = 8, np = 1, kcap = 1, lr = 1, psn = 1;
         for (int i = wl.cell0; i < wl.cell0 + wl.n; ++i) {
             const CellDev& cd = cellv[i];
             const int Wd = std::max(cd.W - 6, 0), Hd = std::max(cd.H - 6, 0);
@@ -1890,20 +1909,23 @@ int Extractor::configure(int r, int c, int batch) {
             sw = std::max(sw, (Wd + 5) & ~1);
             np = std::max(np, Hd * PR);
             kcap = std::max(kcap, cd.slot_cap);
-            psn = std::max({psn, 4 * ((cd.W + 7) / 8), 4 * QR + 3});   // ROI chunk words; quad reads up to 4 * QR + 2
+            lr = std::max({lr, (cd.W + 1) / 2, 4 * QR + 3});          // ROI words; quad reads up to 4 * QR + 2
+            psn = std::max({psn, 4 * ((cd.W + 7) / 8), 4 * QR + 3});   // the same with 16-byte ROI chunks
         }
         ORBX_REQUIRE(psn <= 40, ORBX_ERR_UNSUPPORTED, "cell too wide for k_fast_wave");
-        wl.ps = psn <= 24 ? 24 : 40;
+        wl.ps = lr <= 19 ? 19 : 40;
+        wl.pc = wl.ps == 19 ? 4 : 0;
         ORBX_REQUIRE(sw <= fastw_sw(wl.ps), ORBX_ERR_UNSUPPORTED, "k_fast_wave score-map row");
         sw = fastw_sw(wl.ps);
+        const int iw = fastw_image_words(rows, wl.ps, wl.pc);
         wl.kcap = kcap;                                     // two u16 key lists inside the pair image: 4 * kcap bytes
-        ORBX_REQUIRE(4 * kcap <= rows * wl.ps * 4, ORBX_ERR_UNSUPPORTED, "k_fast_wave key lists exceed the pair image");
-        wl.lay = wave_lds(rows, sw, np, wl.ps);
+        ORBX_REQUIRE(4 * kcap <= iw * 4, ORBX_ERR_UNSUPPORTED, "k_fast_wave key lists exceed the pair image");
+        wl.lay = wave_lds(rows, sw, np, iw);
         const int bytes = kWaveWpg * wl.lay.bytes;
         ORBX_REQUIRE(bytes <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "k_fast_wave LDS %d B", bytes);
         if (bytes > 64 * 1024) {
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<24, kWaveWpg>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<40, kWaveWpg>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<19, 4, kWaveWpg>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+            ORBX_HIP(hipFuncSetAttribute((const void*)k_fast_wave<40, 0, kWaveWpg>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
         }
     }
     int scap = cap;
@@ -2100,7 +2122,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         if (wl.n <= 0) return;
         constexpr int wpg = Extractor::kWaveWpg;
         const int nwg = (wl.n * batch + wpg - 1) / wpg;
-        auto kw = wl.ps == 24 ? k_fast_wave<24, wpg> : k_fast_wave<40, wpg>;
+        auto kw = wl.ps == 19 ? k_fast_wave<19, 4, wpg> : k_fast_wave<40, 0, wpg>;
         hipLaunchKernelGGL(kw, dim3(kXcds * xcd_chunk(nwg)), dim3(64 * wpg), (size_t)wpg * wl.lay.bytes, q, e->d_pyr, ps,
                            e->d_levels, e->d_cells, wl.cell0, wl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s,
                            e->cand_stride, e->d_cell_cnt, ncells, batch, s0, wl.lay, wl.kcap, e->wave_twopass);
