@@ -96,97 +96,193 @@ __device__ __forceinline__ int proj_rot_bin(float a1, float a2) {   // e.g. src/
     return bin;
 }
 
-// One query's window search in GetFeaturesInArea order.  claim[idx] < q: keypoint taken by an earlier
-// blocking query (assigning modes; nullptr otherwise).  Returns the accepted keypoint or -1.
-__device__ int proj_walk(const orbx_proj_params& P, const orbx_grid& g, const orbx_proj_problem& pb, int q,
-                         const orbx_proj_query& Q, const int* claim, int& out_dist) {
-    const int mode = P.mode;
-    const float x = Q.x, y = Q.y, r = Q.r;
-    const int nMinCellX = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, g.min_x), r), g.inv_w)));
-    if (nMinCellX >= g.cols) return -1;
-    const int nMaxCellX = min(g.cols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, g.min_x), r), g.inv_w)));
-    if (nMaxCellX < 0) return -1;
-    const int nMinCellY = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, g.min_y), r), g.inv_h)));
-    if (nMinCellY >= g.rows) return -1;
-    const int nMaxCellY = min(g.rows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, g.min_y), r), g.inv_h)));
-    if (nMaxCellY < 0) return -1;
-    const bool check = (Q.min_level > 0) || (Q.max_level >= 0);
-    const bool assigning = mode <= ORBX_PROJ_SIM3;
-    const bool stereo_tol = (mode == ORBX_PROJ_MAPPOINTS || mode == ORBX_PROJ_LASTFRAME) && pb.uright && Q.ur_tol >= 0.0f;
-    const uint4* qd = reinterpret_cast<const uint4*>(pb.qdesc + 32 * (size_t)q);
-    const uint4 a0 = qd[0], a1 = qd[1];
-    const int init = (mode == ORBX_PROJ_INIT || mode == ORBX_PROJ_BEST) ? INT_MAX : 256;
-    int bestDist = init, bestIdx = -1, bestLevel = -1, bestDist2 = init, bestLevel2 = -1;
-    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix)
-        for (int iy = nMinCellY; iy <= nMaxCellY; ++iy) {
-            const int c = ix * g.rows + iy;
-            const int j1 = pb.cell_start[c + 1];
-            for (int j = pb.cell_start[c]; j < j1; ++j) {
-                const int idx = pb.cell_idx[j];
-                const orbx_keypoint kp = pb.kps[idx];
-                if (check) {
-                    if (kp.octave < Q.min_level) continue;
-                    if (Q.max_level >= 0 && kp.octave > Q.max_level) continue;
-                }
-                if (!(fabsf(__fsub_rn(kp.x, x)) < r && fabsf(__fsub_rn(kp.y, y)) < r)) continue;
-                if (assigning) {
-                    if (pb.blocked && pb.blocked[idx]) continue;
-                    if (claim && claim[idx] < q) continue;
-                }
-                if (stereo_tol && pb.uright[idx] > 0.0f) {
-                    if (fabsf(__fsub_rn(Q.ur, pb.uright[idx])) > Q.ur_tol) continue;
-                }
-                if (mode == ORBX_PROJ_FUSE) {
-                    const float ex = __fsub_rn(Q.x, kp.x), ey = __fsub_rn(Q.y, kp.y);
-                    if (pb.uright && pb.uright[idx] >= 0.0f) {
-                        const float er = __fsub_rn(Q.ur, pb.uright[idx]);
-                        const float e2 = __fadd_rn(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), __fmul_rn(er, er));
-                        if ((double)__fmul_rn(e2, P.inv_sigma2[kp.octave]) > 7.8) continue;
-                    } else {
-                        const float e2 = __fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
-                        if ((double)__fmul_rn(e2, P.inv_sigma2[kp.octave]) > 5.99) continue;
-                    }
-                }
-                const uint4* kd = reinterpret_cast<const uint4*>(pb.desc + 32 * (size_t)idx);
-                const int dist = hamming256(a0, a1, kd[0], kd[1]);
-                if (dist < bestDist) {
-                    bestDist2 = bestDist;
-                    bestLevel2 = bestLevel;
-                    bestDist = dist;
-                    bestLevel = kp.octave;
-                    bestIdx = idx;
-                } else if (dist < bestDist2) {
-                    bestLevel2 = kp.octave;
-                    bestDist2 = dist;
-                }
-            }
-        }
-    if (bestIdx < 0 || bestDist > P.accept_max) return -1;
-    if (mode == ORBX_PROJ_MAPPOINTS && bestLevel == bestLevel2 && (float)bestDist > __fmul_rn(P.nnratio, (float)bestDist2))
-        return -1;
-    out_dist = bestDist;
-    return bestIdx;
+// ---------------------------------------------------------------------------------------------
+// k_proj_search.  A problem's target keypoints are staged into LDS once, in CSR (grid) order, as 16-byte entries
+// {x, y, uright, meta = idx | octave << 13 | blocked << 18 | has-uright << 19} next to the cell starts, so a window walk
+// costs LDS reads; only the descriptors of the candidates that pass the window's geometric tests are read from
+// memory, two at a time (independent loads in flight).  Assigning modes record each query's passing candidates
+// (keypoint, distance, octave) in walk order in an LDS list, so the fixed-point rounds re-evaluate a query from its
+// list with the current claims and touch no descriptor again; a query with more candidates than the list holds walks
+// again.  Problems whose cells and keypoints do not fit in LDS read them from memory (same walk, kLds = false).
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kMetaBlocked = 1u << 18, kMetaUr = 1u << 19;
+constexpr int kProjListMax = 16;           // candidates recorded per query (assigning modes)
+constexpr int kProjBatch = 2;              // descriptor loads in flight per query walk (2: <= 64 VGPRs, two 16-wave
+                                           // workgroups per CU)
+constexpr uint8_t kQmBlocks = 0x80, kQmSkip = 0x40, kQmCount = 0x3f;   // per-query byte: flags + list count
+constexpr uint8_t kQmOverflow = 0x3f;
+
+// The reference's running minimum and second minimum over the window in walk order (e.g. src/ORBmatcher.cc:96-110):
+// (bestDist, bestLevel, bestIdx) and (bestDist2, bestLevel2).
+struct ProjBest {
+    int d1, l1, i1, d2, l2;
+    __device__ __forceinline__ void init(int v) { d1 = d2 = v; l1 = l2 = i1 = -1; }
+    __device__ __forceinline__ void add(int dist, int lvl, int idx) {
+        if (dist < d1) { d2 = d1; l2 = l1; d1 = dist; l1 = lvl; i1 = idx; }
+        else if (dist < d2) { l2 = lvl; d2 = dist; }
+    }
+};
+__device__ __forceinline__ int proj_accept(const orbx_proj_params& P, const ProjBest& b) {
+    if (b.i1 < 0 || b.d1 > P.accept_max) return -1;
+    if (P.mode == ORBX_PROJ_MAPPOINTS && b.l1 == b.l2 && (float)b.d1 > __fmul_rn(P.nnratio, (float)b.d2)) return -1;   // :122
+    return b.i1;
 }
 
-// Modes MAPPOINTS .. BEST.  Dynamic LDS: claim[n] + own[n] (assigning modes).
-__global__ __launch_bounds__(kProjThreads) void k_proj_search(orbx_proj_params P, orbx_grid g,
-                                                              const orbx_proj_problem* __restrict__ probs) {
-    extern __shared__ int psm[];
+struct ProjWin { int x0, x1, y0, y1; };
+__device__ __forceinline__ bool proj_window(const orbx_grid& g, const orbx_proj_query& Q, ProjWin& w) {   // Frame.cc:327-345
+    const float x = Q.x, y = Q.y, r = Q.r;
+    w.x0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, g.min_x), r), g.inv_w)));
+    if (w.x0 >= g.cols) return false;
+    w.x1 = min(g.cols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, g.min_x), r), g.inv_w)));
+    if (w.x1 < 0) return false;
+    w.y0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, g.min_y), r), g.inv_h)));
+    if (w.y0 >= g.rows) return false;
+    w.y1 = min(g.rows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, g.min_y), r), g.inv_h)));
+    return w.y1 >= 0;
+}
+
+// CSR entry j of a problem: staged in LDS, or assembled from the problem's arrays
+template <bool kLds>
+__device__ __forceinline__ float4 proj_entry(const orbx_proj_problem& pb, const float4* ent, int j) {
+    if constexpr (kLds) return ent[j];
+    const int idx = pb.cell_idx[j];
+    const orbx_keypoint kp = pb.kps[idx];
+    uint32_t meta = (uint32_t)idx | ((uint32_t)kp.octave << 13);
+    if (pb.blocked && pb.blocked[idx]) meta |= kMetaBlocked;
+    float ur = 0.0f;
+    if (pb.uright) { ur = pb.uright[idx]; meta |= kMetaUr; }
+    return make_float4(kp.x, kp.y, ur, __uint_as_float(meta));
+}
+
+// The geometric / level / stereo / reprojection tests of one candidate (everything but the descriptor and the claims),
+// in the reference's order of checks (GetFeaturesInArea :352-372, then e.g. :81-94, :1406-1426, :906-941).
+template <bool kAssign>
+__device__ __forceinline__ bool proj_pass(const orbx_proj_params& P, const float* isg, const orbx_proj_query& Q, bool check,
+                                          bool stereo_tol, float4 e) {
+    const uint32_t meta = __float_as_uint(e.w);
+    const int oct = (int)((meta >> 13) & 31u);
+    if (check) {
+        if (oct < Q.min_level) return false;
+        if (Q.max_level >= 0 && oct > Q.max_level) return false;
+    }
+    if (!(fabsf(__fsub_rn(e.x, Q.x)) < Q.r && fabsf(__fsub_rn(e.y, Q.y)) < Q.r)) return false;
+    if (kAssign && (meta & kMetaBlocked)) return false;
+    if (kAssign && stereo_tol && (meta & kMetaUr) && e.z > 0.0f && fabsf(__fsub_rn(Q.ur, e.z)) > Q.ur_tol) return false;
+    if (!kAssign && P.mode == ORBX_PROJ_FUSE) {
+        const float ex = __fsub_rn(Q.x, e.x), ey = __fsub_rn(Q.y, e.y);
+        if ((meta & kMetaUr) && e.z >= 0.0f) {
+            const float er = __fsub_rn(Q.ur, e.z);
+            const float e2 = __fadd_rn(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), __fmul_rn(er, er));
+            if ((double)__fmul_rn(e2, isg[oct]) > 7.8) return false;
+        } else {
+            const float e2 = __fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
+            if ((double)__fmul_rn(e2, isg[oct]) > 5.99) return false;
+        }
+    }
+    return true;
+}
+
+// One query's window walk in GetFeaturesInArea order (cells ix-major, indices ascending inside a cell).  claim: skip
+// keypoints claimed by an earlier blocking query (nullptr: no claims).  list (stride nq, nullptr: none) receives the
+// passing candidates as idx | dist << 13 | octave << 22; returns their count, or kQmOverflow past kcap.
+template <bool kLds, bool kAssign>
+__device__ int proj_walk(const orbx_proj_params& P, const float* isg, const orbx_grid& g, const orbx_proj_problem& pb, int q,
+                         const orbx_proj_query& Q, const int* cs, const float4* ent, const int* claim, uint32_t* list,
+                         int nq, int kcap, ProjBest& best) {
+    best.init((!kAssign && P.mode == ORBX_PROJ_BEST) ? INT_MAX : 256);
+    ProjWin w;
+    if (!proj_window(g, Q, w)) return 0;
+    const bool check = (Q.min_level > 0) || (Q.max_level >= 0);
+    const bool stereo_tol = (P.mode == ORBX_PROJ_MAPPOINTS || P.mode == ORBX_PROJ_LASTFRAME) && pb.uright && Q.ur_tol >= 0.0f;
+    const uint4* qd = reinterpret_cast<const uint4*>(pb.qdesc + 32 * (size_t)q);
+    const uint4 a0 = qd[0], a1 = qd[1];
+    int nrec = 0;
+    uint32_t pm[kProjBatch];            // pending candidates: idx | octave << 22
+    int np = 0;
+    auto flush = [&]() {
+        uint4 d[kProjBatch][2];
+#pragma unroll
+        for (int k = 0; k < kProjBatch; ++k)
+            if (k < np) {
+                const uint4* kd = reinterpret_cast<const uint4*>(pb.desc + 32 * (size_t)(pm[k] & 0x1fffu));
+                d[k][0] = kd[0];
+                d[k][1] = kd[1];
+            }
+#pragma unroll
+        for (int k = 0; k < kProjBatch; ++k)
+            if (k < np) {
+                const int idx = (int)(pm[k] & 0x1fffu), oct = (int)(pm[k] >> 22);
+                const int dist = hamming256(a0, a1, d[k][0], d[k][1]);
+                best.add(dist, oct, idx);
+                if (kAssign && list) {
+                    if (nrec < kcap) list[(size_t)nrec * nq + q] = (uint32_t)idx | ((uint32_t)dist << 13) | ((uint32_t)oct << 22);
+                    ++nrec;
+                }
+            }
+        np = 0;
+    };
+    for (int ix = w.x0; ix <= w.x1; ++ix)
+        for (int iy = w.y0; iy <= w.y1; ++iy) {
+            const int c = ix * g.rows + iy;
+            const int j1 = cs[c + 1];
+            for (int j = cs[c]; j < j1; ++j) {
+                const float4 e = proj_entry<kLds>(pb, ent, j);
+                if (!proj_pass<kAssign>(P, isg, Q, check, stereo_tol, e)) continue;
+                const uint32_t meta = __float_as_uint(e.w);
+                const int idx = (int)(meta & 0x1fffu);
+                if (kAssign && claim && claim[idx] < q) continue;
+                const uint32_t v = (uint32_t)idx | (((meta >> 13) & 31u) << 22);
+                if (np == 0) pm[0] = v; else pm[kProjBatch - 1] = v;
+                if (++np == kProjBatch) flush();
+            }
+        }
+    flush();
+    return nrec > kcap ? (int)kQmOverflow : nrec;
+}
+
+// Modes MAPPOINTS .. BEST.  Dynamic LDS: [kLds: cell starts (ncell + 1), entries (16 B x n)] then, for the assigning
+// modes, claim[n], own[n], res[nq] (idx | dist << 13, or -1), qm[nq] (kQm* byte) and the lists (kcap x nq).
+template <bool kLds, bool kAssign>
+__global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(orbx_proj_params P, orbx_grid g,
+                                                              const orbx_proj_problem* __restrict__ probs, int n_cap,
+                                                              int nq_cap, int kcap) {
+    extern __shared__ __attribute__((aligned(16))) int psm[];
     __shared__ int changed, hist[32], keep[3], acc_sh, bad_sh;
+    __shared__ float isg[32];                          // mvInvLevelSigma2 (a per-lane index into the kernel arguments
+                                                       // would be a vector load from the argument buffer per candidate)
     const orbx_proj_problem pb = probs[blockIdx.x];
     const int tid = threadIdx.x, T = blockDim.x, nq = pb.nq, n = pb.n;
-    const bool assigning = P.mode <= ORBX_PROJ_SIM3;
+    if (tid < 32) isg[tid] = P.inv_sigma2[tid];
+    const int ncell = g.cols * g.rows;
+    char* lp = reinterpret_cast<char*>(psm);
+    const int* cs = pb.cell_start;
+    const float4* ent = nullptr;
+    if constexpr (kLds) {
+        int* cs_l = reinterpret_cast<int*>(lp);
+        lp += ((size_t)(ncell + 1) * 4 + 15) & ~(size_t)15;
+        float4* ent_l = reinterpret_cast<float4*>(lp);
+        lp += (size_t)16 * n_cap;
+        for (int c = tid; c <= ncell; c += T) cs_l[c] = pb.cell_start[c];
+        const int ncsr = min(pb.cell_start[ncell], n);
+        for (int j = tid; j < ncsr; j += T) ent_l[j] = proj_entry<false>(pb, nullptr, j);
+        cs = cs_l;
+        ent = ent_l;
+    }
     if (tid == 0) { acc_sh = 0; bad_sh = 0; }
     if (tid < 32) hist[tid] = 0;
     __syncthreads();
-    if (!assigning) {
+    if constexpr (!kAssign) {
         int acc = 0;
         for (int q = tid; q < nq; q += T) {
             const orbx_proj_query Q = pb.queries[q];
-            int d = -1, r = -1;
-            if (!(Q.flags & ORBX_QF_SKIP)) r = proj_walk(P, g, pb, q, Q, nullptr, d);
+            int r = -1;
+            ProjBest b;
+            if (!(Q.flags & ORBX_QF_SKIP)) {
+                proj_walk<kLds, false>(P, isg, g, pb, q, Q, cs, ent, nullptr, nullptr, nq, 0, b);
+                r = proj_accept(P, b);
+            }
             pb.q_idx[q] = r;
-            pb.q_dist[q] = r >= 0 ? d : -1;
+            pb.q_dist[q] = r >= 0 ? b.d1 : -1;
             acc += r >= 0;
         }
         acc = wave_sum(acc);
@@ -194,33 +290,63 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(orbx_proj_params P
         __syncthreads();
         if (tid == 0) *pb.nmatches = acc_sh;
         return;
+    } else {
+    int* claim = reinterpret_cast<int*>(lp);
+    int* own = claim + n_cap;
+    int* res = own + n_cap;
+    uint8_t* qm = reinterpret_cast<uint8_t*>(res + nq_cap);
+    uint32_t* list = reinterpret_cast<uint32_t*>(lp + (((size_t)8 * n_cap + 4 * (size_t)nq_cap + nq_cap + 15) & ~(size_t)15));
+    // round 0: every query's walk without claims, its candidates recorded
+    for (int q = tid; q < nq; q += T) {
+        const orbx_proj_query Q = pb.queries[q];
+        int r = -1, m = (Q.flags & ORBX_QF_BLOCKS) ? kQmBlocks : 0;
+        if (Q.flags & ORBX_QF_SKIP) {
+            m |= kQmSkip;
+        } else {
+            ProjBest b;
+            const int cnt = proj_walk<kLds, true>(P, isg, g, pb, q, Q, cs, ent, nullptr, kcap > 0 ? list : nullptr, nq, kcap, b);
+            m |= kcap > 0 ? cnt : kQmOverflow;                // no list room: every round walks again
+            r = proj_accept(P, b);
+            if (r >= 0) r |= b.d1 << 13;
+        }
+        res[q] = r;
+        qm[q] = (uint8_t)m;
     }
-    int* claim = psm;
-    int* own = psm + n;
-    for (int i = tid; i < n; i += T) claim[i] = INT_MAX;
-    __syncthreads();
-    for (int round = 0; round <= nq; ++round) {       // at most nq + 1 rounds (query q is final after q + 1)
+    // fixed-point rounds: claims from the current results, every query re-evaluated with them (from its list, or by a
+    // new walk when the list overflowed), until no result changes (at most nq rounds: query q is final after q + 1)
+    for (int round = 1; round <= nq; ++round) {
+        for (int i = tid; i < n; i += T) claim[i] = INT_MAX;
+        __syncthreads();                               // every thread has read the previous round's 'changed'
         if (tid == 0) changed = 0;
+        for (int q = tid; q < nq; q += T) {
+            const int r = res[q];
+            if (r >= 0 && (qm[q] & kQmBlocks)) atomicMin(&claim[r & 0x1fff], q);
+        }
         __syncthreads();
         int ch = 0;
         for (int q = tid; q < nq; q += T) {
-            const orbx_proj_query Q = pb.queries[q];
-            int d = -1, r = -1;
-            if (!(Q.flags & ORBX_QF_SKIP)) r = proj_walk(P, g, pb, q, Q, claim, d);
-            if (round == 0 || r != pb.q_idx[q]) ch = 1;
-            pb.q_idx[q] = r;
-            pb.q_dist[q] = r >= 0 ? d : -1;
+            const int m = qm[q];
+            if (m & kQmSkip) continue;
+            const int cnt = m & kQmCount;
+            ProjBest b;
+            if (cnt != kQmOverflow) {
+                b.init(256);
+                for (int k = 0; k < cnt; ++k) {
+                    const uint32_t v = list[(size_t)k * nq + q];
+                    const int idx = (int)(v & 0x1fffu);
+                    if (claim[idx] < q) continue;
+                    b.add((int)((v >> 13) & 0x1ffu), (int)(v >> 22), idx);
+                }
+            } else {
+                proj_walk<kLds, true>(P, isg, g, pb, q, pb.queries[q], cs, ent, claim, nullptr, nq, 0, b);
+            }
+            int r = proj_accept(P, b);
+            if (r >= 0) r |= b.d1 << 13;
+            if (r != res[q]) { ch = 1; res[q] = r; }
         }
         if (ch) changed = 1;
         __syncthreads();
         if (!changed) break;                           // workgroup-uniform
-        for (int i = tid; i < n; i += T) claim[i] = INT_MAX;
-        __syncthreads();
-        for (int q = tid; q < nq; q += T) {
-            const int r = pb.q_idx[q];
-            if (r >= 0 && (pb.queries[q].flags & ORBX_QF_BLOCKS)) atomicMin(&claim[r], q);
-        }
-        __syncthreads();
     }
     // final assignment: the last accepted query writes mvpMapPoints[idx] (src/ORBmatcher.cc:125, :1430, :1559, :398)
     for (int i = tid; i < n; i += T) own[i] = -1;
@@ -228,8 +354,11 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(orbx_proj_params P
     const bool rot = P.check_ori && (P.mode == ORBX_PROJ_LASTFRAME || P.mode == ORBX_PROJ_KEYFRAME);
     int acc = 0;
     for (int q = tid; q < nq; q += T) {
-        const int r = pb.q_idx[q];
-        if (r < 0) continue;
+        const int v = res[q];
+        pb.q_idx[q] = v >= 0 ? (v & 0x1fff) : -1;
+        pb.q_dist[q] = v >= 0 ? (v >> 13) : -1;
+        if (v < 0) continue;
+        const int r = v & 0x1fff;
         ++acc;
         atomicMax(&own[r], q);
         if (rot) atomicAdd(&hist[proj_rot_bin(pb.queries[q].angle, pb.kps[r].angle)], 1);
@@ -254,8 +383,9 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(orbx_proj_params P
         __syncthreads();
         int bad = 0;
         for (int q = tid; q < nq; q += T) {
-            const int r = pb.q_idx[q];
-            if (r < 0) continue;
+            const int v = res[q];
+            if (v < 0) continue;
+            const int r = v & 0x1fff;
             const int b = proj_rot_bin(pb.queries[q].angle, pb.kps[r].angle);
             if (b == keep[0] || b == keep[1] || b == keep[2]) continue;
             own[r] = -2;
@@ -267,6 +397,7 @@ __global__ __launch_bounds__(kProjThreads) void k_proj_search(orbx_proj_params P
     }
     for (int i = tid; i < n; i += T) pb.owner[i] = own[i];
     if (tid == 0) *pb.nmatches = acc_sh - bad_sh;
+    }
 }
 
 // SearchForInitialization: one wave per problem walks the queries in order.  Dynamic LDS: matchedDist[n],
@@ -780,11 +911,23 @@ int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* param
             ORBX_HIP(hipFuncSetAttribute((const void*)k_proj_init, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(k_proj_init, dim3(n_problems), dim3(64), lds, s, P, grid, d_problems);
     } else {
-        const size_t lds = (size_t)2 * std::max(max_n, 1) * 4;
-        ORBX_REQUIRE(lds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "too many target keypoints (%d)", max_n);
-        if (lds > 64 * 1024)
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_proj_search, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k_proj_search, dim3(n_problems), dim3(kProjThreads), lds, s, P, grid, d_problems);
+        // LDS plan (k_proj_search): staged cells + entries when they fit, then the assigning modes' claim / own / res /
+        // qm arrays and as many list slots per query (<= kProjListMax) as the rest of the 160 KiB holds
+        const size_t N = std::max(max_n, 1), NQ = std::max(max_nq, 1), ncell = (size_t)grid.cols * grid.rows;
+        const bool assigning = P.mode <= ORBX_PROJ_SIM3;
+        const size_t core = assigning ? ((8 * N + 4 * NQ + NQ + 15) & ~(size_t)15) : 0;
+        const size_t stage = ((4 * (ncell + 1) + 15) & ~(size_t)15) + 16 * N;
+        const size_t cap = 160 * 1024;
+        ORBX_REQUIRE(core <= cap, ORBX_ERR_UNSUPPORTED, "too many target keypoints (%d) / queries (%d)", max_n, max_nq);
+        const bool staged = stage + core <= cap;
+        const size_t used = core + (staged ? stage : 0);
+        int kcap = 0;
+        if (assigning) kcap = (int)std::min<size_t>(kProjListMax, (cap - used) / (4 * NQ));
+        const size_t lds = std::max<size_t>(used + (size_t)kcap * 4 * NQ, 16);
+        auto kern = assigning ? (staged ? k_proj_search<true, true> : k_proj_search<false, true>)
+                              : (staged ? k_proj_search<true, false> : k_proj_search<false, false>);
+        if (lds > 64 * 1024) ORBX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(kern, dim3(n_problems), dim3(kProjThreads), lds, s, P, grid, d_problems, (int)N, (int)NQ, kcap);
     }
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;

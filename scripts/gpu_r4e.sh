@@ -2,7 +2,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${1:-r4e}
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q -rf --timeout 120 --timeout-method thread \
     > gpurun_out/${T}_pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -8 gpurun_out/${T}_pytest_gpu.log
 [ $rc -le 1 ] || exit $rc

@@ -42,6 +42,23 @@ def test_proj_search_kitti_size(gpu, mode):
     _check(c, got)
 
 
+@pytest.mark.parametrize("mode", ["lastframe", "mappoints", "fuse", "best"])
+def test_proj_search_lds_plans(gpu, mode):
+    """The search's other LDS plans: a grid too fine to stage (320 x 240 cells: cell starts and keypoints read from
+    memory), and a query set too large for candidate lists (20000 queries: every fixed-point round walks again); the
+    dense case overflows the lists of the default plan."""
+    import multiagent_orb_slam2_amd as pkg
+    from multiagent_orb_slam2_amd.orbx import frame_grid
+    m = pkg.ORBmatcher(0.8, True)
+    c = make_case(61, MODES[mode], n_target=1500, n_query=1200, dense=True)
+    c["grid"] = frame_grid(0.0, 0.0, 640.0, 480.0, 320, 240)
+    got = m.proj_search(c["params"], c["grid"], c["queries"], c["qdesc"], c["kps"], c["desc"], c["uright"], c["blocked"])
+    assert _check(c, got)[0] > 0
+    c = make_case(62, MODES[mode], n_target=2000, n_query=20000, dense=True)
+    got = m.proj_search(c["params"], c["grid"], c["queries"], c["qdesc"], c["kps"], c["desc"], c["uright"], c["blocked"])
+    assert _check(c, got)[0] > 0
+
+
 def test_proj_search_named_wrappers(gpu):
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
