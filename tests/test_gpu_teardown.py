@@ -2,8 +2,9 @@
 
 The extractor's pyramid ring is read by the stereo SAD step on the caller's stereo stream
 (orbx_stereo_refine_batch_device over orbx_extractor_pyramid_device).  Destroying the extractor while that stream
-still has the step queued must not free the ring under it: every destroy path drains the whole device first
-(hipFree does not wait for other streams' kernels, scripts/micro/free_sync.hip).  Afterwards the device must hold no
+still has the step queued must not free the ring under it: every destroy path drains the whole device first (hipFree
+was measured to wait for other streams' kernels too, scripts/micro/free_sync.hip, but the guarantee should not rest
+on that runtime behaviour).  Afterwards the device must hold no
 pending error, and a fresh process must initialise the GPU and extract bit-exactly -- the r3w symptom was a fresh
 process failing its first HIP call after the previous process's teardown."""
 import os
