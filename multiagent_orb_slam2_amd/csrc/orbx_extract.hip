@@ -473,6 +473,18 @@ __device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, in
 }
 
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+// exclusive prefix sums of a[0, n) in place by one wave (lane ln); returns the total
+__device__ __forceinline__ int wave_excl_scan_lds(int* a, int n, int ln) {
+    int carry = 0;
+    for (int b = 0; b < n; b += kWave) {
+        const int i = b + ln;
+        const int x = i < n ? a[i] : 0;
+        const int inc = wave_incl_scan(x);
+        if (i < n) a[i] = carry + inc - x;
+        carry += __builtin_amdgcn_readlane(inc, kWave - 1);
+    }
+    return carry;
+}
 // acc + number of set bits of b below this lane: v_mbcnt_lo + v_mbcnt_hi (the compiler turns popcount(b & below) into
 // two ANDs and two v_bcnt)
 __device__ __forceinline__ int rank_below(uint64_t b, int acc = 0) {
@@ -537,17 +549,30 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
         }
     }
     wave_fence();
-    // 3. closed-form scores of the survivors, two per lane per round (both tap sets read before either is scored)
-    for (int i = ln; i < ns; i += 2 * kWave) {
-        const int i2 = i + kWave;
-        const uint32_t e1 = list[i], e2 = i2 < ns ? list[i2] : e1;
-        const int rr1 = e1 >> 8, j1 = e1 & 0xff, rr2 = e2 >> 8, j2 = e2 & 0xff;
-        uint32_t t1[17], t2[17];
-        fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
-        fast_taps_f16<kPS, kPC>(E, rr2 + 3, j2, t2);
-        const s16x2 s1 = fast_score_from_taps_f16(t1), s2 = fast_score_from_taps_f16(t2);
-        *(s16x2*)(sc + (rr1 + 1) * SW + 2 + 2 * j1) = (2 * j1 + 1 < Wd) ? s1 : (s16x2){s1.x, (short)-1};
-        if (i2 < ns) *(s16x2*)(sc + (rr2 + 1) * SW + 2 + 2 * j2) = (2 * j2 + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
+    // 3. closed-form scores of the survivors, two per lane per round (both tap sets read before either is scored); a
+    //    round with at most 64 survivors left (two cells in three at iniThFAST) scores one per lane
+    for (int i0 = 0; i0 < ns; i0 += 2 * kWave) {
+        const int i = i0 + ln;
+        if (i0 + kWave < ns) {                                        // wave-uniform
+            const int i2 = i + kWave;
+            if (i < ns) {
+                const uint32_t e1 = list[i], e2 = i2 < ns ? list[i2] : e1;
+                const int rr1 = e1 >> 8, j1 = e1 & 0xff, rr2 = e2 >> 8, j2 = e2 & 0xff;
+                uint32_t t1[17], t2[17];
+                fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
+                fast_taps_f16<kPS, kPC>(E, rr2 + 3, j2, t2);
+                const s16x2 s1 = fast_score_from_taps_f16(t1), s2 = fast_score_from_taps_f16(t2);
+                *(s16x2*)(sc + (rr1 + 1) * SW + 2 + 2 * j1) = (2 * j1 + 1 < Wd) ? s1 : (s16x2){s1.x, (short)-1};
+                if (i2 < ns) *(s16x2*)(sc + (rr2 + 1) * SW + 2 + 2 * j2) = (2 * j2 + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
+            }
+        } else if (i < ns) {
+            const uint32_t e1 = list[i];
+            const int rr1 = e1 >> 8, j1 = e1 & 0xff;
+            uint32_t t1[17];
+            fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
+            const s16x2 s1 = fast_score_from_taps_f16(t1);
+            *(s16x2*)(sc + (rr1 + 1) * SW + 2 + 2 * j1) = (2 * j1 + 1 < Wd) ? s1 : (s16x2){s1.x, (short)-1};
+        }
     }
     wave_fence();
     // 4. strict 3x3 NMS at iniTh (bits 0, 1) and minTh (bits 2, 3); kept pixels appended in list order (= row-major)
@@ -889,18 +914,9 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
 #ifndef ORBX_BLUR_WPE
 #define ORBX_BLUR_WPE 4
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_WPE))) void k_blur7(
-    const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride, const LevelDev* __restrict__ levels,
-    const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
-    // tiles [tile0, tile0 + ntiles) of every image (a level range: tiles are level-major)
-    const int nbx = (ntiles + 3) / 4;                         // 4 tiles (waves) per workgroup
-    const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
-    if (item >= nbx * batch) return;
-    const int img = item / nbx;
-    const int tl = (item - img * nbx) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (tl >= ntiles) return;
-    const int t = tile0 + tl;
-    const BlurTile bt = tiles[t];
+// one wave's blur tile (level, 256-column strip, 16-row band) of image img
+__device__ __forceinline__ void blur_tile(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride,
+                                          const LevelDev* __restrict__ levels, const BlurTile& bt, int img, const Src0& s0) {
     const LevelDev L = levels[bt.level];
     int sstride;
     const uint8_t* S = level_pixels(pyr, pyr_stride, L, bt.level, img, s0, sstride);
@@ -916,6 +932,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_W
         blur_band2<1>(S, sstride, D, L, x0, y0, y1);
     else
         blur_band2<2>(S, sstride, D, L, x0, y0, y1);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_WPE))) void k_blur7(
+    const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride, const LevelDev* __restrict__ levels,
+    const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
+    // tiles [tile0, tile0 + ntiles) of every image (a level range: tiles are level-major)
+    const int nbx = (ntiles + 3) / 4;                         // 4 tiles (waves) per workgroup
+    const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
+    if (item >= nbx * batch) return;
+    const int img = item / nbx;
+    const int tl = (item - img * nbx) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (tl >= ntiles) return;
+    blur_tile(pyr, blur, pyr_stride, levels, tiles[tile0 + tl], img, s0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1142,6 +1171,11 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
         t = A_seq; A_seq = B_seq; B_seq = t;
     };
     bool phase2 = false, finished = false, counted = false;
+    // The node-list bookkeeping of a pass (flags, prefix sums, the new list, the phase decisions) is O(nodes <= cap)
+    // and runs on wave 0 alone with wave-level scans and fences; the other waves wait at one barrier, then every thread
+    // moves the keys.  Two block barriers per pass (phase 2: plus the sort's), where block-wide scans took ~7.
+    const bool w0 = tid < kWave;
+    const int ln = tid & (kWave - 1);
     QTP(2);
     while (!finished) {
         const int prev = n;
@@ -1163,55 +1197,66 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
         QTP(20);
 
         if (!phase2) {
-            // ---------------- phase 1 pass (:606-665)
+            // ---------------- phase 1 pass (:606-665), bookkeeping on wave 0
             // per node: children (split) or 1 survivor, packed as children << 16 | survivor so that ONE scan gives both
             // prefixes (children before node i in the high half, survivors before it in the low half; totals < 2^15);
-            // base = the node's children count; nodes of >1 key to expand next (misc[0], zeroed in the last pass)
-            int nexp = 0;
-            for (int i = tid; i < n; i += T) {
-                const int* c4 = cc + 4 * i;
-                const bool split = A_cnt[i] > 1;
-                const int nch = split ? (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0) : 0;
-                sa[i] = split ? (nch << 16) : 1;
-                base[i] = nch;
-                if (split) nexp += (c4[0] > 1) + (c4[1] > 1) + (c4[2] > 1) + (c4[3] > 1);
-            }
-            nexp = wave_sum(nexp);
-            if (lane_id() == 0) atomicAdd(&misc[0], nexp);
-            __syncthreads();
-            const int CU = block_scan_array(sa, n, tmp);
-            const int C = CU >> 16, U = CU & 0xffff;
-            const int nToExpand = misc[0];
-            const int nn = C + U;
-            QTP(30);
-            if (nn > cap) { if (tid == 0) atomicOr(err, kErrQtCap); finished = true; break; }
-            for (int i = tid; i < n; i += T) {
-                const int nch = base[i];
-                if (A_cnt[i] > 1) {
-                    const int gb = C - (sa[i] >> 16) - nch;
-                    base[i] = gb;
-                    const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
+            // base = the node's children count; nodes of >1 key to expand next (nexp)
+            if (w0) {
+                int nexp = 0;
+                for (int i = ln; i < n; i += kWave) {
                     const int* c4 = cc + 4 * i;
-                    for (int q = 0; q < 4; ++q) {
-                        if (c4[q] == 0) continue;
-                        int cx0, cx1, cy0, cy1;
-                        child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
-                        const int p = gb + rank_desc(c4, q);
-                        B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
-                        B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
-                        B_cnt[p] = c4[q];
-                        B_seq[p] = (sa[i] >> 16) + rank_asc(c4, q);
-                        reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
-                    }
+                    const bool split = A_cnt[i] > 1;
+                    const int nch = split ? (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0) : 0;
+                    sa[i] = split ? (nch << 16) : 1;
+                    base[i] = nch;
+                    if (split) nexp += (c4[0] > 1) + (c4[1] > 1) + (c4[2] > 1) + (c4[3] > 1);
+                }
+                nexp = wave_sum(nexp);
+                wave_fence();
+                const int CU = wave_excl_scan_lds(sa, n, ln);
+                wave_fence();
+                const int C = CU >> 16, U = CU & 0xffff;
+                const int nn = C + U;
+                if (nn > cap) {
+                    if (ln == 0) { atomicOr(err, kErrQtCap); misc[2] = -1; }
                 } else {
-                    const int p = C + (sa[i] & 0xffff);
-                    base[i] = p;
-                    B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
-                    reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
+                    for (int i = ln; i < n; i += kWave) {
+                        const int nch = base[i];
+                        if (A_cnt[i] > 1) {
+                            const int gb = C - (sa[i] >> 16) - nch;
+                            base[i] = gb;
+                            const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
+                            const int* c4 = cc + 4 * i;
+                            for (int q = 0; q < 4; ++q) {
+                                if (c4[q] == 0) continue;
+                                int cx0, cx1, cy0, cy1;
+                                child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
+                                const int p = gb + rank_desc(c4, q);
+                                B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
+                                B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
+                                B_cnt[p] = c4[q];
+                                B_seq[p] = (sa[i] >> 16) + rank_asc(c4, q);
+                                reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
+                            }
+                        } else {
+                            const int p = C + (sa[i] & 0xffff);
+                            base[i] = p;
+                            B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
+                            reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
+                        }
+                    }
+                    if (ln == 0) {
+                        // :669-673, decided here for every thread: 1 finished, 2 on to phase 2
+                        misc[2] = (nn >= N || nn == prev) ? 1 : (nn + nexp * 3 > N) ? 2 : 0;
+                        misc[3] = nn;
+                    }
                 }
             }
             __syncthreads();
-            if (tid == 0) misc[0] = 0;                           // every thread has read nToExpand
+            QTP(30);
+            const int dec = misc[2];
+            if (dec < 0) { finished = true; break; }
+            const int nn = misc[3];
             for (int k = tid; k < K; k += T) {
                 const int i = kn[k];
                 const uint32_t xy = kxy[k];
@@ -1236,86 +1281,106 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             counted = true;
             n = nn;
             QTP(50);
-            if (n >= N || n == prev) finished = true;              // :669-672
-            else if (n + nToExpand * 3 > N) phase2 = true;         // :673
+            if (dec == 1) finished = true;
+            else if (dec == 2) phase2 = true;
         } else {
             // ---------------- phase 2 pass (:676-737)
-            // expandable nodes -> sort keys (size, creation order, node)
-            for (int i = tid; i < n; i += T) sa[i] = A_cnt[i] > 1 ? 1 : 0;
+            // expandable nodes -> sort keys (size, creation order, node), on wave 0
+            if (w0) {
+                for (int i = ln; i < n; i += kWave) sa[i] = A_cnt[i] > 1 ? 1 : 0;
+                wave_fence();
+                const int nV = wave_excl_scan_lds(sa, n, ln);
+                wave_fence();
+                int P2 = 1;
+                while (P2 < nV) P2 <<= 1;
+                for (int i = ln; i < P2; i += kWave) sk[i] = ~0ull;
+                wave_fence();
+                for (int i = ln; i < n; i += kWave)
+                    if (A_cnt[i] > 1)
+                        sk[sa[i]] = ((unsigned long long)A_cnt[i] << 40) | ((unsigned long long)A_seq[i] << 20) | (unsigned long long)i;
+                if (ln == 0) { misc[4] = nV; misc[5] = P2; }
+            }
             __syncthreads();
-            const int nV = block_scan_array(sa, n, tmp);
-            int P2 = 1;
-            while (P2 < nV) P2 <<= 1;
-            for (int i = tid; i < P2; i += T) sk[i] = ~0ull;
-            __syncthreads();
-            for (int i = tid; i < n; i += T)
-                if (A_cnt[i] > 1)
-                    sk[sa[i]] = ((unsigned long long)A_cnt[i] << 40) | ((unsigned long long)A_seq[i] << 20) | (unsigned long long)i;
-            __syncthreads();
+            const int nV = misc[4], P2 = misc[5];
             // bitonic sort ascending (keys are unique: node index in the low bits); stages inside a wave's 128 keys
             // need only a wave-level fence (block_bitonic_u64).  (Ranking each key by counting the smaller ones, no
             // dependent stages, measured slower: 9 -> 15.7 us per level-0 pass, r3am.)
             if (P2 >= 2) block_bitonic_u64(sk, P2);
             auto key_at = [&](int p) { return sk[nV - 1 - p]; };     // processing order: descending keys
-            // delta_p = children_p - 1
             QTP(31);
-            for (int p = tid; p < nV; p += T) {
-                const int i = (int)(key_at(p) & 0xfffff);
-                const int* c4 = cc + 4 * i;
-                sb[p] = (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0);
-            }
-            if (tid == 0) misc[1] = nV;          // break index (first p reaching N), nV = none
-            __syncthreads();
-            for (int p = tid; p < nV; p += T) sa[p] = sb[p] - 1;
-            __syncthreads();
-            block_scan_array(sa, nV, tmp);        // exclusive prefix of deltas
-            for (int p = tid; p < nV; p += T)
-                if (n + sa[p] + sb[p] - 1 >= N) atomicMin(&misc[1], p);
-            __syncthreads();
-            const int nproc = min(misc[1] + 1, nV);
-            // children counts prefix over processed nodes (creation order)
-            for (int p = tid; p < nV; p += T) sa[p] = (p < nproc) ? sb[p] : 0;
-            __syncthreads();
-            const int Cn = block_scan_array(sa, nV, tmp);
-            // mark processed nodes: base = group base; survivors ranked after the groups
-            for (int i = tid; i < n; i += T) base[i] = -1;
-            __syncthreads();
-            for (int p = tid; p < nproc; p += T) {
-                const int i = (int)(key_at(p) & 0xfffff);
-                base[i] = Cn - sa[p] - sb[p];
-                A_seq[i] = -1 - sa[p];           // stash creation prefix (node is erased anyway)
-            }
-            __syncthreads();
-            for (int i = tid; i < n; i += T) sb[i] = (base[i] < 0) ? 1 : 0;
-            __syncthreads();
-            const int U = block_scan_array(sb, n, tmp);
-            const int nn = Cn + U;
-            QTP(32);
-            if (nn > cap) { if (tid == 0) atomicOr(err, kErrQtCap); finished = true; break; }
-            for (int i = tid; i < n; i += T) {
-                if (base[i] >= 0) {
-                    const int gb = base[i];
-                    const int cre = -1 - A_seq[i];
-                    const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
-                    const int* c4 = cc + 4 * i;
-                    for (int q = 0; q < 4; ++q) {
-                        if (c4[q] == 0) continue;
-                        int cx0, cx1, cy0, cy1;
-                        child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
-                        const int p = gb + rank_desc(c4, q);
-                        B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
-                        B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
-                        B_cnt[p] = c4[q];
-                        B_seq[p] = cre + rank_asc(c4, q);
-                        reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
+            if (w0) {
+                // children of the p-th processed node (sb), the first p at which the list reaches N (:713-720): the
+                // list grows by children - 1 per processed node, so n + inclusive prefix of the deltas is nondecreasing
+                int brk = nV, acc = 0;
+                for (int b = 0; b < nV; b += kWave) {
+                    const int p = b + ln;
+                    int d = 0;
+                    if (p < nV) {
+                        const int i = (int)(key_at(p) & 0xfffff);
+                        const int* c4 = cc + 4 * i;
+                        const int ch = (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0);
+                        sb[p] = ch;
+                        d = ch - 1;
                     }
+                    const int inc = acc + wave_incl_scan(d);
+                    const uint64_t hit = __ballot(p < nV && n + inc >= N);
+                    if (brk == nV && hit) brk = b + (int)__builtin_ctzll(hit);
+                    acc = __builtin_amdgcn_readlane(inc, kWave - 1);
+                }
+                const int nproc = min(brk + 1, nV);
+                wave_fence();
+                // children prefix over the processed nodes (creation order of the new nodes)
+                for (int p = ln; p < nV; p += kWave) sa[p] = (p < nproc) ? sb[p] : 0;
+                wave_fence();
+                const int Cn = wave_excl_scan_lds(sa, nV, ln);
+                for (int i = ln; i < n; i += kWave) base[i] = -1;
+                wave_fence();
+                // processed nodes: base = group base; survivors ranked after the groups
+                for (int p = ln; p < nproc; p += kWave) {
+                    const int i = (int)(key_at(p) & 0xfffff);
+                    base[i] = Cn - sa[p] - sb[p];
+                    A_seq[i] = -1 - sa[p];           // stash creation prefix (node is erased anyway)
+                }
+                wave_fence();
+                for (int i = ln; i < n; i += kWave) sb[i] = (base[i] < 0) ? 1 : 0;
+                wave_fence();
+                const int U = wave_excl_scan_lds(sb, n, ln);
+                wave_fence();
+                const int nn = Cn + U;
+                if (nn > cap) {
+                    if (ln == 0) { atomicOr(err, kErrQtCap); misc[2] = -1; }
                 } else {
-                    const int p = Cn + sb[i];
-                    B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
-                    reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
+                    for (int i = ln; i < n; i += kWave) {
+                        if (base[i] >= 0) {
+                            const int gb = base[i];
+                            const int cre = -1 - A_seq[i];
+                            const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
+                            const int* c4 = cc + 4 * i;
+                            for (int q = 0; q < 4; ++q) {
+                                if (c4[q] == 0) continue;
+                                int cx0, cx1, cy0, cy1;
+                                child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
+                                const int p = gb + rank_desc(c4, q);
+                                B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
+                                B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
+                                B_cnt[p] = c4[q];
+                                B_seq[p] = cre + rank_asc(c4, q);
+                                reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
+                            }
+                        } else {
+                            const int p = Cn + sb[i];
+                            B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
+                            reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
+                        }
+                    }
+                    if (ln == 0) { misc[2] = (nn >= N || nn == prev) ? 1 : 0; misc[3] = nn; misc[6] = Cn; }   // :734-735
                 }
             }
             __syncthreads();
+            QTP(32);
+            const int dec = misc[2];
+            if (dec < 0) { finished = true; break; }
+            const int nn = misc[3], Cn = misc[6];
             for (int k = tid; k < K; k += T) {
                 const int i = kn[k];
                 const uint32_t xy = kxy[k];
@@ -1340,7 +1405,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             counted = true;
             n = nn;
             QTP(51);
-            if (n >= N || n == prev) finished = true;              // :734-735
+            if (dec == 1) finished = true;
         }
     }
 
@@ -1664,6 +1729,7 @@ struct Extractor {
     WaveLaunch wave_launch[2] = {};
     static constexpr int kWaveWpg = 4;   // (1 or 2 waves per workgroup: faster alone, slower in the step)
     int wave_twopass = 1;     // iniTh first, minTh only for the cells left empty (0: one pass at min(iniTh, minTh))
+    std::vector<int> tile_off;   // blur tiles of level l: [tile_off[l], tile_off[l + 1])
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
     size_t qt_lds = 0;        // k_quadtree dynamic LDS bytes of the node arrays (the key region follows at this offset)
     int qt_keys[2] = {0, 0};  // LDS-resident key capacity of the level-0 launch / the levels 1..n-1 launch
@@ -1698,7 +1764,8 @@ struct Extractor {
     uint8_t* h_in = nullptr;
     uint8_t* h_out = nullptr;      // pinned: count | keypoints | descriptors of one image
     size_t h_out_bytes = 0;
-    orbx_keypoint* d_kps = nullptr;
+    uint8_t* d_hblk = nullptr;      // host API outputs on the device, laid out as h_out: count, keypoints, descriptors
+    orbx_keypoint* d_kps = nullptr; // (pointers into d_hblk: one D2H copy brings all three back)
     uint8_t* d_desc = nullptr;
     int32_t* d_cnt = nullptr;
     int last_batch = 0;
@@ -1790,7 +1857,9 @@ void Extractor::free_buffers() {
     auto F = [](auto*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } };
     F(d_levels); F(d_cells); F(d_tiles); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
     F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
-    F(d_kps); F(d_desc); F(d_cnt);
+    F(d_hblk);
+    d_kps = nullptr; d_desc = nullptr; d_cnt = nullptr;
+    d_pyr = nullptr;                                       // a slot of the freed ring
     if (h_in) { (void)hipHostFree(h_in); h_in = nullptr; }
     if (h_out) { (void)hipHostFree(h_out); h_out = nullptr; }
     h_out_bytes = 0;
@@ -1827,6 +1896,7 @@ int Extractor::configure(int r, int c, int batch) {
     lv.assign(nlevels, LevelDev{});
     cellv.clear();
     tilev.clear();
+    tile_off.clear();
     size_t poff = 0;
     int cand = 0, outs = 0, cap = 4;
     for (int l = 0; l < nlevels; ++l) {
@@ -1886,9 +1956,11 @@ int Extractor::configure(int r, int c, int batch) {
         outs += L.out_cap;
         cap = std::max(cap, L.out_cap);
         // blur tiles
+        tile_off.push_back((int)tilev.size());
         for (int ty = 0; ty < (L.h + kBlurBand - 1) / kBlurBand; ++ty)
             for (int tx = 0; tx < (L.w + kBlurStrip - 1) / kBlurStrip; ++tx) tilev.push_back(BlurTile{l, tx, ty, 0});
     }
+    tile_off.push_back((int)tilev.size());
     ORBX_REQUIRE(cap < 32768 && cap < (1 << 20), ORBX_ERR_UNSUPPORTED, "node capacity %d too large", cap);
     // k_quadtree's phase 1 scans (children << 16 | survivors) in one int: children <= 4 * cap must stay below 2^15
     ORBX_REQUIRE(4 * cap < (1 << 15), ORBX_ERR_UNSUPPORTED, "node capacity %d too large for the packed split scan", cap);
@@ -2113,9 +2185,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         return ORBX_OK;
     };
     const int ncells = (int)e->cellv.size();
-    int t0 = 0;                                                     // blur tiles of level 0: [0, t0)
-    while (t0 < (int)e->tilev.size() && e->tilev[t0].level == 0) ++t0;
-    const int nt = (int)e->tilev.size();
+    const std::vector<int>& toff = e->tile_off;                     // blur tiles of level l: [toff[l], toff[l + 1])
     QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
     auto fast = [&](hipStream_t q, int k) {
         const Extractor::WaveLaunch& wl = e->wave_launch[k];
@@ -2174,14 +2244,14 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     if (int st = after_prev_describe(side)) return st;
     quadtree(side, 0, nl > 0 ? 1 : 0);
     mark(8);
-    blur(side, 0, t0);
+    blur(side, toff[0], toff[1] - toff[0]);
     if (side != s) {
         int st = resize_chain();                                    // launch stream: levels 1..nl-1 of the pyramid
         if (st) return st;
         ORBX_HIP(hipEventRecord(ce.pyr, s));
         ORBX_HIP(hipStreamWaitEvent(side, ce.pyr, 0));
     }
-    blur(side, t0, nt - t0);                                        // side: levels 1..nl-1 once the pyramid exists
+    blur(side, toff[1], toff[nl] - toff[1]);                        // side: levels 1..nl-1 once the pyramid exists
     mark(9);
     if (side != s) ORBX_HIP(hipEventRecord(ce.join, side));
     mark(10);                                                       // launch stream: FAST, DistributeOctTree 1..nl-1
@@ -2442,12 +2512,15 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
         ORBX_HIP(hipHostMalloc((void**)&e->h_in, nb, hipHostMallocDefault));
         e->in_bytes = nb;
     }
-    if (!e->d_kps) {
-        if ((st = dev_alloc(&e->d_kps, e->out_capacity))) return st;
-        if ((st = dev_alloc(&e->d_desc, (size_t)e->out_capacity * 32))) return st;
-        if ((st = dev_alloc(&e->d_cnt, 1))) return st;
+    // output block (device and pinned host alike): count at 0, keypoints at 64, descriptors 64-byte aligned after them
+    const size_t odesc = (64 + (size_t)e->out_capacity * sizeof(orbx_keypoint) + 63) & ~(size_t)63;
+    const size_t ob = odesc + (size_t)e->out_capacity * 32;
+    if (!e->d_hblk) {
+        if ((st = dev_alloc(&e->d_hblk, ob))) return st;
+        e->d_cnt = reinterpret_cast<int32_t*>(e->d_hblk);
+        e->d_kps = reinterpret_cast<orbx_keypoint*>(e->d_hblk + 64);
+        e->d_desc = e->d_hblk + odesc;
     }
-    const size_t ob = 64 + (size_t)e->out_capacity * (sizeof(orbx_keypoint) + 32);
     if (e->h_out_bytes < ob) {
         if (e->h_out) (void)hipHostFree(e->h_out);
         e->h_out = nullptr;
@@ -2466,13 +2539,11 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     if (st) return st;
     int32_t* h_cnt = (int32_t*)e->h_out;
     orbx_keypoint* h_kps = (orbx_keypoint*)(e->h_out + 64);
-    uint8_t* h_desc = e->h_out + 64 + (size_t)e->out_capacity * sizeof(orbx_keypoint);
-    ORBX_HIP(hipMemcpyAsync(h_cnt, e->d_cnt, sizeof(int), hipMemcpyDeviceToHost, e->own()));
+    uint8_t* h_desc = e->h_out + odesc;
+    // count, keypoints and descriptors of the whole capacity in one copy (a count-sized copy would need a second
+    // synchronisation; only the first n are read), the error word beside it
+    ORBX_HIP(hipMemcpyAsync(e->h_out, e->d_hblk, ob, hipMemcpyDeviceToHost, e->own()));
     ORBX_HIP(hipMemcpyAsync(h_cnt + 1, e->d_err, sizeof(int), hipMemcpyDeviceToHost, e->own()));
-    // keypoints and descriptors of the whole capacity in the same round trip (a count-sized copy would need a
-    // second synchronisation); only the first n are read
-    ORBX_HIP(hipMemcpyAsync(h_kps, e->d_kps, sizeof(orbx_keypoint) * (size_t)e->out_capacity, hipMemcpyDeviceToHost, e->own()));
-    ORBX_HIP(hipMemcpyAsync(h_desc, e->d_desc, (size_t)e->out_capacity * 32, hipMemcpyDeviceToHost, e->own()));
     ORBX_HIP(hipStreamSynchronize(e->own()));
     const int n = h_cnt[0], err = h_cnt[1];
     ORBX_REQUIRE(!(err & kErrStale), ORBX_ERR_HIP, "ordering canary: a describe read another call's keypoints (err=%d)", err);

@@ -168,16 +168,18 @@ def test_describe_batched_slot_ranges(gpu):
     _check(S.kitti_like_image(410, rows=240, cols=333), nfeatures=777, nlevels=5, scale=1.3)
 
 
-def test_blurred_pyramid_bit_exact(gpu):
+@pytest.mark.parametrize("form", ["pipelined", "serial"])
+def test_blurred_pyramid_bit_exact(gpu, monkeypatch, form):
     """Every pixel of every blurred level -- not only the windows around keypoints that the descriptor tests see --
     equals the oracle's GaussianBlur(7x7, sigma 2, REFLECT_101) of the oracle's pyramid level
     (ORBextractor.cc:1085-1086): interior strips, strips at a level's left / right edge (REFLECT_101 columns by byte
     selectors), levels under 12 columns, bottom rows, saturation (a constant 255 image blurs to 255 with taps summing to
-    257), batched (image index > 0)."""
+    257), batched (image index > 0); two streams (default) and every stage on one stream (ORBX_PIPELINE=0)."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
+    monkeypatch.setenv("ORBX_PIPELINE", "0" if form == "serial" else "1")
     for shape in ((375, 1242), (377, 1243), (480, 752), (1000, 200), (40, 40), (61, 97)):
         imgs = np.stack([S.kitti_like_image(700 + shape[1], rows=shape[0], cols=shape[1]),
                          S.uniform_noise_image(701, rows=shape[0], cols=shape[1]) if shape == (375, 1242)
