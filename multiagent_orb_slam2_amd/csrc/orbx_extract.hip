@@ -1707,6 +1707,21 @@ struct Extractor {
     int dbg_skip_desc_wait = 0;   // ORBX_DEBUG_SKIP_DESC_WAIT=1 (tests only): drop the quadtree's wait for the previous
                                   // describe, i.e. remove an ordering edge on purpose so the canary must fire
     int slot_call[8] = {-1, -1, -1, -1, -1, -1, -1, -1};   // per pyramid set: pool index of its last describe
+    // Host API (orbx_extract): the whole call -- H2D copy, run_batch's kernels on both streams, D2H copies -- is
+    // captured once per configuration as a hipGraph and replayed, one launch per call instead of ~25 stream operations.
+    // A replay is synchronised before orbx_extract returns, so it leaves no edge for later calls to wait on.
+    hipGraph_t hgraph = nullptr;
+    hipGraphExec_t hgexec = nullptr;
+    bool capturing = false;       // run_batch inside the capture: no waits on earlier calls, no host synchronisation
+    bool host_graph = true;       // ORBX_HOST_GRAPH=0: the host API issues its stream operations every call (A/B)
+    bool async_pending = false;   // a device-API call may still run: the next replay first waits for every describe
+    uint8_t* hg_pyr = nullptr;    // the pyramid set the graph's kernels write
+    void drop_graph() {
+        if (hgexec) (void)hipGraphExecDestroy(hgexec);
+        if (hgraph) (void)hipGraphDestroy(hgraph);
+        hgexec = nullptr;
+        hgraph = nullptr;
+    }
     int last_call = -1;                                    // pool index of the previous call, -1 none
     int sync_calls() {                                     // every describe issued so far is done
         for (auto& c : cev)
@@ -1854,6 +1869,7 @@ static void level_dims(const Extractor* e, int rows, int cols, int l, int* w, in
 }
 
 void Extractor::free_buffers() {
+    drop_graph();                                          // it names the buffers freed below
     auto F = [](auto*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } };
     F(d_levels); F(d_cells); F(d_tiles); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
     F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
@@ -2159,7 +2175,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     const int nl = e->nlevels;
     const size_t ps = e->pyr_size;
     Extractor::EventSet* es = nullptr;
-    if (e->timing && !e->tpool.empty()) {
+    if (e->timing && !e->tpool.empty() && !e->capturing) {
         es = &e->tpool[e->tnext++ % e->tpool.size()];
         int st = e->resolve(*es);
         if (st) return st;
@@ -2173,7 +2189,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     // this call's events: the pool entry of 32 calls ago, whose describe (and every wait on its events) is long done
     const int ci = (int)(e->cev_next++ % Extractor::kCallEv);
     Extractor::CallEvents& ce = e->cev[ci];
-    if (ce.used) ORBX_HIP(hipEventSynchronize(ce.desc));
+    if (ce.used && !e->capturing) ORBX_HIP(hipEventSynchronize(ce.desc));
     hipStream_t side = e->pipeline ? e->side : s;
     if (!e->pipeline) so = s;
     auto mark = [&](int k) {
@@ -2181,7 +2197,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     };
     // the previous call's describe (possibly on another stream) reads the kept keypoints and the blurred pyramid
     auto after_prev_describe = [&](hipStream_t q) -> int {
-        if (e->last_call >= 0 && !e->dbg_skip_desc_wait) ORBX_HIP(hipStreamWaitEvent(q, e->cev[e->last_call].desc, 0));
+        if (e->last_call >= 0 && !e->dbg_skip_desc_wait && !e->capturing)
+            ORBX_HIP(hipStreamWaitEvent(q, e->cev[e->last_call].desc, 0));
         return ORBX_OK;
     };
     const int ncells = (int)e->cellv.size();
@@ -2217,7 +2234,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         ORBX_HIP(hipStreamWaitEvent(side, ce.fork, 0));
     }
     auto resize_chain = [&]() -> int {
-        if (e->slot_call[slot] >= 0)                                // this set's last reader
+        if (e->slot_call[slot] >= 0 && !e->capturing)               // this set's last reader
             ORBX_HIP(hipStreamWaitEvent(s, e->cev[e->slot_call[slot]].desc, 0));
         for (int l = 1; l < nl; ++l) {
             const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
@@ -2280,9 +2297,16 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     }
     mark(5);
     ORBX_HIP(hipEventRecord(ce.desc, so));
-    ce.used = true;
-    e->slot_call[slot] = ci;
-    e->last_call = ci;
+    if (e->capturing) {                                             // replays are synchronous: nothing to wait on
+        ce.used = false;
+        e->slot_call[slot] = -1;
+        e->last_call = -1;
+    } else {
+        ce.used = true;
+        e->slot_call[slot] = ci;
+        e->last_call = ci;
+        e->async_pending = true;
+    }
     ORBX_HIP(hipGetLastError());
     e->last_batch = batch;
     return ORBX_OK;
@@ -2378,6 +2402,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     }
     if (const char* pl = std::getenv("ORBX_PIPELINE")) e->pipeline = std::atoi(pl) != 0;
     if (const char* tp = std::getenv("ORBX_FAST_TWOPASS")) e->wave_twopass = std::atoi(tp) != 0;
+    if (const char* hg = std::getenv("ORBX_HOST_GRAPH")) e->host_graph = std::atoi(hg) != 0;
     if (const char* sw = std::getenv("ORBX_DEBUG_SKIP_DESC_WAIT")) e->dbg_skip_desc_wait = std::atoi(sw) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
@@ -2391,9 +2416,10 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     if (!e) return ORBX_OK;
     (void)hipSetDevice(e->device);
     // Every stream of the device, not only the extractor's own: callers' streams read its pyramid ring and outputs
-    // (the stereo SAD step reads orbx_extractor_pyramid_device's levels) and hipFree does not wait for them.
+    // (the stereo SAD step reads orbx_extractor_pyramid_device's levels); hipFree was measured to wait for them too,
+    // but the guarantee should not rest on that.
     (void)hipDeviceSynchronize();
-    e->free_buffers();
+    e->free_buffers();                                      // (and the host-API graph)
     for (auto& es : e->tpool)
         for (auto& ev : es.ev) (void)hipEventDestroy(ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
@@ -2503,6 +2529,7 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     if (st) return st;
     const size_t nb = (size_t)rows * cols;
     if (e->in_bytes < nb) {
+        e->drop_graph();                                     // it names the buffers replaced here
         if (e->d_in) (void)hipFree(e->d_in);
         if (e->h_in) (void)hipHostFree(e->h_in);
         e->d_in = nullptr;
@@ -2522,6 +2549,7 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
         e->d_desc = e->d_hblk + odesc;
     }
     if (e->h_out_bytes < ob) {
+        e->drop_graph();
         if (e->h_out) (void)hipHostFree(e->h_out);
         e->h_out = nullptr;
         e->h_out_bytes = 0;
@@ -2534,17 +2562,57 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     } else {
         for (int r = 0; r < rows; ++r) std::memcpy(e->h_in + (size_t)r * cols, image + (size_t)r * step, (size_t)cols);
     }
-    ORBX_HIP(hipMemcpyAsync(e->d_in, e->h_in, nb, hipMemcpyHostToDevice, e->own()));
-    st = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, e->own(), e->own());
-    if (st) return st;
     int32_t* h_cnt = (int32_t*)e->h_out;
     orbx_keypoint* h_kps = (orbx_keypoint*)(e->h_out + 64);
     uint8_t* h_desc = e->h_out + odesc;
-    // count, keypoints and descriptors of the whole capacity in one copy (a count-sized copy would need a second
-    // synchronisation; only the first n are read), the error word beside it
-    ORBX_HIP(hipMemcpyAsync(e->h_out, e->d_hblk, ob, hipMemcpyDeviceToHost, e->own()));
-    ORBX_HIP(hipMemcpyAsync(h_cnt + 1, e->d_err, sizeof(int), hipMemcpyDeviceToHost, e->own()));
-    ORBX_HIP(hipStreamSynchronize(e->own()));
+    hipStream_t s = e->own();
+    // the call's stream operations: the image in, the extraction, count + keypoints + descriptors of the whole capacity
+    // in one copy (a count-sized copy would need a second synchronisation; only the first n are read), the error word
+    auto enqueue = [&]() -> int {
+        ORBX_HIP(hipMemcpyAsync(e->d_in, e->h_in, nb, hipMemcpyHostToDevice, s));
+        int r = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, s, s);
+        if (r) return r;
+        ORBX_HIP(hipMemcpyAsync(e->h_out, e->d_hblk, ob, hipMemcpyDeviceToHost, s));
+        ORBX_HIP(hipMemcpyAsync(h_cnt + 1, e->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+        return ORBX_OK;
+    };
+    if (e->host_graph && !e->hgexec) {
+        // first call of this configuration: finish every earlier call, then capture this one's operations
+        if (int r = e->sync_calls()) return r;
+        if (e->side) ORBX_HIP(hipStreamSynchronize(e->side));
+        ORBX_HIP(hipStreamSynchronize(s));
+        e->async_pending = false;
+        ORBX_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+        e->capturing = true;
+        const int r = enqueue();
+        e->capturing = false;
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(s, &g);
+        hipGraphExec_t x = nullptr;
+        const hipError_t ei = (r == ORBX_OK && ec == hipSuccess) ? hipGraphInstantiate(&x, g, nullptr, nullptr, 0) : ec;
+        if (r != ORBX_OK || ei != hipSuccess) {              // no graph for this extractor: per-call stream operations
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();
+            e->host_graph = false;
+        } else {
+            e->hgraph = g;
+            e->hgexec = x;
+            e->hg_pyr = e->d_pyr;                            // the pyramid set the graph writes
+        }
+    }
+    if (e->host_graph && e->hgexec) {
+        if (e->async_pending) {                              // a device-API call may still use the buffers
+            if (int r = e->sync_calls()) return r;
+            e->async_pending = false;
+        }
+        ORBX_HIP(hipGraphLaunch(e->hgexec, s));
+        e->d_pyr = e->hg_pyr;                                // what orbx_extractor_pyramid_device now names
+        e->last_src0 = Src0{e->d_in, (size_t)cols, nb};
+        e->last_batch = 1;
+    } else {
+        if ((st = enqueue())) return st;
+    }
+    ORBX_HIP(hipStreamSynchronize(s));
     const int n = h_cnt[0], err = h_cnt[1];
     ORBX_REQUIRE(!(err & kErrStale), ORBX_ERR_HIP, "ordering canary: a describe read another call's keypoints (err=%d)", err);
     ORBX_REQUIRE(err == 0, ORBX_ERR_UNSUPPORTED, "quadtree node capacity exceeded (err=%d)", err);

@@ -1300,6 +1300,20 @@ struct Matcher {
     bool last_op_set = false;            // last_op recorded after the previous call (multi-stream mode)
     bool have_last = false, multi = false;
     hipStream_t last_stream = nullptr;   // the previous call's stream
+    // pinned host staging of the host API (one H2D and one D2H copy per call instead of one pageable copy per array;
+    // host calls end synchronised, so the next call may reuse it)
+    uint8_t* h_stage = nullptr;
+    size_t h_stage_bytes = 0;
+    int stage_host(size_t bytes) {
+        if (bytes <= h_stage_bytes) return ORBX_OK;
+        if (h_stage) (void)hipHostFree(h_stage);
+        h_stage = nullptr;
+        h_stage_bytes = 0;
+        const size_t nb = std::max(bytes, h_stage_bytes * 2);
+        ORBX_HIP(hipHostMalloc((void**)&h_stage, nb, hipHostMallocDefault));
+        h_stage_bytes = nb;
+        return ORBX_OK;
+    }
     int reserve(size_t bytes) { return reserve_on(bytes, own()); }
     // order 'on' after the previous scratch user; grow the buffer (after every user has finished) if needed
     int reserve_on(size_t bytes, hipStream_t on) {
@@ -1431,6 +1445,7 @@ int orbx_matcher_destroy(orbx_matcher* m) {
     (void)hipDeviceSynchronize();                                // device calls on callers' streams use the scratch
     if (m->last_op) (void)hipEventDestroy(m->last_op);
     if (m->scratch) (void)hipFree(m->scratch);
+    if (m->h_stage) (void)hipHostFree(m->h_stage);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
     return ORBX_OK;
@@ -1594,19 +1609,27 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
         A.lrow_idx = bp.take<int32_t>(cap);
     }
     hipStream_t s = m->own();
-    ORBX_HIP(hipMemcpyAsync(dkl, kpl, 28 * (size_t)nl, hipMemcpyHostToDevice, s));
-    ORBX_HIP(hipMemcpyAsync(ddl, desc_l, 32 * (size_t)nl, hipMemcpyHostToDevice, s));
+    // the four inputs into pinned staging laid out as the scratch (keypoints / descriptors of both sides are
+    // contiguous there), one H2D copy; the two outputs come back the same way
+    const size_t in_bytes = (size_t)((uint8_t*)dbi - (uint8_t*)dkl), out_off = in_bytes;
+    const size_t out_bytes = (size_t)((uint8_t*)dbd - (uint8_t*)dbi) + 4 * (size_t)nl;
+    if ((st = m->stage_host(std::max(in_bytes, out_off + out_bytes)))) return st;
+    uint8_t* hs = m->h_stage;
+    std::memcpy(hs, kpl, 28 * (size_t)nl);
+    std::memcpy(hs + ((uint8_t*)ddl - (uint8_t*)dkl), desc_l, 32 * (size_t)nl);
     if (nr > 0) {
-        ORBX_HIP(hipMemcpyAsync(dkr, kpr, 28 * (size_t)nr, hipMemcpyHostToDevice, s));
-        ORBX_HIP(hipMemcpyAsync(ddr, desc_r, 32 * (size_t)nr, hipMemcpyHostToDevice, s));
+        std::memcpy(hs + ((uint8_t*)dkr - (uint8_t*)dkl), kpr, 28 * (size_t)nr);
+        std::memcpy(hs + ((uint8_t*)ddr - (uint8_t*)dkl), desc_r, 32 * (size_t)nr);
     }
+    ORBX_HIP(hipMemcpyAsync(dkl, hs, in_bytes, hipMemcpyHostToDevice, s));
     A.kl = dkl; A.dl = ddl; A.kr = dkr; A.dr = ddr; A.nl = nullptr; A.nr = nullptr;
     A.nl_fixed = nl; A.nr_fixed = nr; A.capacity = cap;
     A.best_idx = dbi; A.best_dist = dbd;
     if ((st = stereo_launch(A, 1, nl, s))) return st;
-    ORBX_HIP(hipMemcpyAsync(best_idx, dbi, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
-    ORBX_HIP(hipMemcpyAsync(best_dist, dbd, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(hs + out_off, dbi, out_bytes, hipMemcpyDeviceToHost, s));
     ORBX_HIP(hipStreamSynchronize(s));
+    std::memcpy(best_idx, hs + out_off, 4 * (size_t)nl);
+    std::memcpy(best_dist, hs + out_off + ((uint8_t*)dbd - (uint8_t*)dbi), 4 * (size_t)nl);
     int n = 0;
     for (int i = 0; i < nl; ++i) n += best_idx[i] >= 0;
     *n_matched = n;
@@ -1693,12 +1716,19 @@ int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, con
     float* ddp = bp.take<float>(cap);
     int32_t* dsad = bp.take<int32_t>(cap);
     hipStream_t s = m->own();
-    ORBX_HIP(hipMemcpyAsync(dkl, kpl, 28 * (size_t)nl, hipMemcpyHostToDevice, s));
-    ORBX_HIP(hipMemcpyAsync(ddl, desc_l, 32 * (size_t)nl, hipMemcpyHostToDevice, s));
+    // the four inputs into pinned staging laid out as the scratch (keypoints / descriptors of both sides are
+    // contiguous there), one H2D copy; the two outputs come back the same way
+    const size_t in_bytes = (size_t)((uint8_t*)dbi - (uint8_t*)dkl), out_off = (size_t)((uint8_t*)dur - (uint8_t*)dkl);
+    const size_t out_bytes = (size_t)((uint8_t*)ddp - (uint8_t*)dur) + 4 * (size_t)nl;
+    if ((st = m->stage_host(std::max(in_bytes, out_off + out_bytes)))) return st;
+    uint8_t* hs = m->h_stage;
+    std::memcpy(hs, kpl, 28 * (size_t)nl);
+    std::memcpy(hs + ((uint8_t*)ddl - (uint8_t*)dkl), desc_l, 32 * (size_t)nl);
     if (nr > 0) {
-        ORBX_HIP(hipMemcpyAsync(dkr, kpr, 28 * (size_t)nr, hipMemcpyHostToDevice, s));
-        ORBX_HIP(hipMemcpyAsync(ddr, desc_r, 32 * (size_t)nr, hipMemcpyHostToDevice, s));
+        std::memcpy(hs + ((uint8_t*)dkr - (uint8_t*)dkl), kpr, 28 * (size_t)nr);
+        std::memcpy(hs + ((uint8_t*)ddr - (uint8_t*)dkl), desc_r, 32 * (size_t)nr);
     }
+    ORBX_HIP(hipMemcpyAsync(dkl, hs, in_bytes, hipMemcpyHostToDevice, s));
     A.kl = dkl; A.dl = ddl; A.kr = dkr; A.dr = ddr; A.nl = nullptr; A.nr = nullptr;
     A.nl_fixed = nl; A.nr_fixed = nr; A.capacity = cap;
     A.best_idx = dbi; A.best_dist = dbd;
@@ -1709,9 +1739,10 @@ int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, con
     R.bf = bf; R.maxD = bf / b;
     R.uright = dur; R.depth = ddp; R.sad = dsad;
     if ((st = refine_launch(R, 1, s))) return st;
-    ORBX_HIP(hipMemcpyAsync(uright, dur, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
-    ORBX_HIP(hipMemcpyAsync(depth, ddp, 4 * (size_t)nl, hipMemcpyDeviceToHost, s));
+    ORBX_HIP(hipMemcpyAsync(hs + out_off, dur, out_bytes, hipMemcpyDeviceToHost, s));
     ORBX_HIP(hipStreamSynchronize(s));
+    std::memcpy(uright, hs + out_off, 4 * (size_t)nl);
+    std::memcpy(depth, hs + out_off + ((uint8_t*)ddp - (uint8_t*)dur), 4 * (size_t)nl);
     int n = 0;
     for (int i = 0; i < nl; ++i) n += depth[i] > 0;
     *n_stereo = n;
