@@ -2556,20 +2556,34 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
         ORBX_HIP(hipHostMalloc((void**)&e->h_out, ob, hipHostMallocDefault));
         e->h_out_bytes = ob;
     }
-    // the previous call's transfers out of h_in / h_out completed before it returned (stream synchronised)
-    if (step == (size_t)cols) {
-        std::memcpy(e->h_in, image, nb);
-    } else {
-        for (int r = 0; r < rows; ++r) std::memcpy(e->h_in + (size_t)r * cols, image + (size_t)r * step, (size_t)cols);
-    }
     int32_t* h_cnt = (int32_t*)e->h_out;
     orbx_keypoint* h_kps = (orbx_keypoint*)(e->h_out + 64);
     uint8_t* h_desc = e->h_out + odesc;
     hipStream_t s = e->own();
-    // the call's stream operations: the image in, the extraction, count + keypoints + descriptors of the whole capacity
-    // in one copy (a count-sized copy would need a second synchronisation; only the first n are read), the error word
+    // The image in (outside the graph: its source changes every call).  The previous call's transfers out of h_in
+    // completed before it returned (stream synchronised).  Mode 0: packed into pinned staging in row bands, each band's
+    // H2D copy issued as soon as it is packed, so the DMA of one band overlaps the packing of the next; mode 1: one
+    // pageable copy from the caller's image (the runtime stages it; dense rows only); ORBX_HOST_H2D (A/B).
+    static const int h2d_mode = std::getenv("ORBX_HOST_H2D") ? std::atoi(std::getenv("ORBX_HOST_H2D")) : 0;
+    if (h2d_mode == 1 && step == (size_t)cols) {
+        ORBX_HIP(hipMemcpyAsync(e->d_in, image, nb, hipMemcpyHostToDevice, s));
+    } else {
+        const int bands = h2d_mode == 2 ? 1 : 4;
+        const int rb = (rows + bands - 1) / bands;
+        for (int r0 = 0; r0 < rows; r0 += rb) {
+            const int r1 = std::min(rows, r0 + rb);
+            if (step == (size_t)cols) {
+                std::memcpy(e->h_in + (size_t)r0 * cols, image + (size_t)r0 * cols, (size_t)(r1 - r0) * cols);
+            } else {
+                for (int r = r0; r < r1; ++r) std::memcpy(e->h_in + (size_t)r * cols, image + (size_t)r * step, (size_t)cols);
+            }
+            ORBX_HIP(hipMemcpyAsync(e->d_in + (size_t)r0 * cols, e->h_in + (size_t)r0 * cols, (size_t)(r1 - r0) * cols,
+                                    hipMemcpyHostToDevice, s));
+        }
+    }
+    // the call's other stream operations: the extraction, count + keypoints + descriptors of the whole capacity in one
+    // copy (a count-sized copy would need a second synchronisation; only the first n are read), the error word
     auto enqueue = [&]() -> int {
-        ORBX_HIP(hipMemcpyAsync(e->d_in, e->h_in, nb, hipMemcpyHostToDevice, s));
         int r = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, s, s);
         if (r) return r;
         ORBX_HIP(hipMemcpyAsync(e->h_out, e->d_hblk, ob, hipMemcpyDeviceToHost, s));
