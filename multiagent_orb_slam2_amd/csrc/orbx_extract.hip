@@ -1017,64 +1017,60 @@ __device__ unsigned long long g_qtprof[2][64];
 #define QTP(tag) do {} while (0)
 #endif
 
-__global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
-                                                         const uint32_t* __restrict__ cand_xy, const uint8_t* __restrict__ cand_s,
-                                                         int cand_stride, const int* __restrict__ cell_cnt, int ncells,
-                                                         QtScratch qs, uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r,
-                                                         int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
-                                                         int scan_cap, int* __restrict__ err, int lvl0, int key_lds_off,
-                                                         int key_lds_cap, unsigned seq) {
-    extern __shared__ __attribute__((aligned(16))) int smem[];
-    const int lvl = lvl0 + (int)blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
-#ifdef ORBX_QT_PROF
-    int qtp_n = 0;
-#endif
-    QTP(0);
-    const LevelDev L = levels[lvl];
-    // LDS layout
-    int* A_xr = smem;              // x0 | x1 << 16
-    int* A_yr = A_xr + cap;        // y0 | y1 << 16
-    int* A_cnt = A_yr + cap;
-    int* A_seq = A_cnt + cap;
-    int* B_xr = A_seq + cap;
-    int* B_yr = B_xr + cap;
-    int* B_cnt = B_yr + cap;
-    int* B_seq = B_cnt + cap;
-    int* cc = B_seq + cap;         // [cap][4] child counts of the current list
-    int* cc2 = cc + 4 * cap;       // [cap][4] child counts of the list being built (counted while keys move)
-    int* base = cc2 + 4 * cap;     // new list position (unsplit) / group base (split)
-    int* sa = base + cap;          // scan array [scan_cap]
-    int* sb = sa + scan_cap;       // scan array [scan_cap]
-    int* tmp = sb + scan_cap;      // 32 ints
-    int* misc = tmp + 32;          // 16 ints
-    unsigned long long* sk = (unsigned long long*)(misc + 16 + ((misc + 16 - smem) & 1));  // [pow2 >= cap]
-    const int ncl = L.cell_end - L.cell_begin;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) int16_t lds_i16;
 
-    // ---- 1. compact the level's cell candidates into reference order (cell row-major, then FAST order)
-    // (per cell: count -> sa, slot offset -> sb; all loads independent)
-    for (int i = tid; i < ncl; i += T) {
-        const int cw = cell_cnt[(size_t)img * ncells + L.cell_begin + i];
-        sa[i] = cw;
-        sb[i] = cells[L.cell_begin + i].slot_off;
-    }
-    __syncthreads();
-    const int K = block_scan_array(sa, ncl, tmp);
-    // Every pass walks all K keys two or three times: they live in LDS when the level's keys fit the launch's key
-    // region (the common case: ~2-4k keys at level 0 of a KITTI frame), in the HBM scratch otherwise.  The pointers
-    // are generic, so one code path serves both (flat loads resolve to LDS or global at run time).
-    uint32_t* kxy;
-    int16_t* kn;
-    if (K <= key_lds_cap) {
-        kxy = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(smem) + key_lds_off);
-        kn = reinterpret_cast<int16_t*>(kxy + key_lds_cap);
-    } else {
-        kxy = qs.key_xy + (size_t)img * cand_stride + L.cand_off;
-        kn = qs.key_node + (size_t)img * cand_stride + L.cand_off;
-    }
-    uint8_t* kr = qs.key_r + (size_t)img * cand_stride + L.cand_off;
+// split point of a node, packed (x0 + ceil((x1-x0)/2)) | (y0 + ceil((y1-y0)/2)) << 16 (DivideNode :483-509; the float
+// halving of an integer width is exact, so its ceiling is (w + 1) >> 1); a key's quadrant is (x >= mx) + 2 (y >= my)
+__device__ __forceinline__ int node_mid(int x0, int x1, int y0, int y1) {
+    return (x0 + ((x1 - x0 + 1) >> 1)) | ((y0 + ((y1 - y0 + 1) >> 1)) << 16);
+}
+__device__ __forceinline__ int mid_quadrant(uint32_t xy, int mid) {
+    return ((int)(xy & 0xffff) >= (mid & 0xffff) ? 1 : 0) + ((int)(xy >> 16) >= (mid >> 16) ? 2 : 0);
+}
+
+struct QtState {         // one workgroup's LDS arrays (k_quadtree)
+    int *A_xr, *A_yr, *A_cnt, *A_seq, *A_mid, *B_xr, *B_yr, *B_cnt, *B_seq, *B_mid;
+    int *cc, *cc2, *base, *sa, *sb, *tmp, *misc;
+    unsigned long long* sk;
+};
+
+// Everything after the level's key count is known, for keys in LDS (PXY / PN address-space-3 pointers: ds_ loads) or
+// in the HBM scratch (plain pointers).
+template <typename PXY, typename PN>
+__device__ __forceinline__ void qt_level(QtState S, const LevelDev& L, int lvl, int img, int K, int ncl, PXY kxy, PN kn,
+                                         uint8_t* __restrict__ kr, const uint32_t* __restrict__ cand_xy,
+                                         const uint8_t* __restrict__ cand_s, int cand_stride,
+                                         uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r, int out_stride,
+                                         int* __restrict__ level_cnt, int nlevels, int cap, int* __restrict__ err,
+                                         unsigned seq) {
+    const int tid = threadIdx.x, T = blockDim.x;
+#ifdef ORBX_QT_PROF
+    int qtp_n = 1;
+    const int lvl0 = lvl;      // QTP stamps the blockIdx.x == 0 workgroup, whose level is the launch's first
+#endif
+    int *A_xr = S.A_xr, *A_yr = S.A_yr, *A_cnt = S.A_cnt, *A_seq = S.A_seq, *A_mid = S.A_mid;
+    int *B_xr = S.B_xr, *B_yr = S.B_yr, *B_cnt = S.B_cnt, *B_seq = S.B_seq, *B_mid = S.B_mid;
+    int *cc = S.cc, *cc2 = S.cc2, *base = S.base, *sa = S.sa, *sb = S.sb, *misc = S.misc;
+    unsigned long long* sk = S.sk;
     const int minB = kEdge - 3;
+    // ---- 2. root nodes (:543-585), laid out before the gather so that the gather also assigns every key to its root
+    //    and counts the root's quadrants (the first pass's child counts)
+    const int nIni = L.nIni;
+    const float hX = L.hX;
+    for (int i = tid; i < nIni; i += T) {
+        const int x0 = (int)__fmul_rn(hX, (float)i), x1 = (int)__fmul_rn(hX, (float)(i + 1));
+        A_xr[i] = (x0 & 0xffff) | (x1 << 16);
+        A_yr[i] = 0 | (L.win_h << 16);
+        A_mid[i] = node_mid(x0, x1, 0, L.win_h);
+        A_cnt[i] = 0;
+        A_seq[i] = i;
+    }
+    for (int i = tid; i < 4 * nIni; i += T) cc2[i] = 0;
     // owner cell of every key (LDS / scratch writes only), then one flat gather over the keys with every load
-    // independent: a walk cell by cell chains three dependent HBM loads per cell (~150 us at level 0)
+    // independent, each key assigned to its root and counted in the root's quadrant on the way (a walk cell by cell
+    // chains three dependent HBM loads per cell: ~150 us at level 0; G threads per cell walking its slots: 19.4 against
+    // 15.3 us to here, r4q)
     for (int c = tid; c < ncl; c += T) {
         const int b = sa[c], e = (c + 1 < ncl) ? sa[c + 1] : K;
         for (int k = b; k < e; ++k) kn[k] = (int16_t)c;
@@ -1101,14 +1097,19 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             for (int u = 0; u < U; ++u) {
                 const int k = k0 + u * T;
                 if (k < K) {
-                    kxy[k] = ((xy[u] & 0xffff) - minB) | (((xy[u] >> 16) - minB) << 16);
+                    const uint32_t w = ((xy[u] & 0xffff) - minB) | (((xy[u] >> 16) - minB) << 16);
+                    kxy[k] = w;
                     kr[k] = r[u];
+                    const int x = (int)(w & 0xffff);
+                    const int rt = min((int)__fdiv_rn((float)x, hX), nIni - 1);
+                    kn[k] = (int16_t)rt;
+                    atomicAdd(&A_cnt[rt], 1);
+                    atomicAdd(&cc2[4 * rt + mid_quadrant(w, A_mid[rt])], 1);
                 }
             }
         }
     }
     __syncthreads();
-
     QTP(1);
 #ifdef ORBX_QT_TRIVIAL
     {   // diagnostics build only (upper bound of a faster DistributeOctTree): the level's first N keys, no quadtree --
@@ -1125,40 +1126,37 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
         return;
     }
 #endif
-    // ---- 2. root nodes (:543-585)
-    const int nIni = L.nIni;
-    const float hX = L.hX;
-    for (int i = tid; i < nIni; i += T) {
-        const int x0 = (int)__fmul_rn(hX, (float)i), x1 = (int)__fmul_rn(hX, (float)(i + 1));
-        A_xr[i] = (x0 & 0xffff) | (x1 << 16);
-        A_yr[i] = 0 | (L.win_h << 16);
-        A_cnt[i] = 0;
-        A_seq[i] = i;
-    }
-    __syncthreads();
-    for (int k = tid; k < K; k += T) {
-        const int x = (int)(kxy[k] & 0xffff);
-        int r = (int)__fdiv_rn((float)x, hX);
-        r = min(r, nIni - 1);
-        kn[k] = (int16_t)r;
-        atomicAdd(&A_cnt[r], 1);
-    }
-    __syncthreads();
-    // drop empty roots (order preserved)
-    for (int i = tid; i < nIni; i += T) sa[i] = A_cnt[i] > 0 ? 1 : 0;
-    __syncthreads();
-    int n = block_scan_array(sa, nIni, tmp);
-    for (int i = tid; i < nIni; i += T) {
-        if (A_cnt[i] > 0) {
-            const int p = sa[i];
-            B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
+    // drop empty roots (order preserved), on wave 0: the list, its child counts, and the root -> position map in sb
+    // that the first key move reads
+    const bool w0 = tid < kWave;
+    const int ln = tid & (kWave - 1);
+    if (w0) {
+        int carry = 0;
+        for (int b0 = 0; b0 < nIni; b0 += kWave) {
+            const int i = b0 + ln;
+            const bool keep = i < nIni && A_cnt[i] > 0;
+            const uint64_t m = __ballot(keep);
+            const int p = carry + lanes_below(m);
+            if (keep) {
+                B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i]; B_mid[p] = A_mid[i];
+                reinterpret_cast<int4*>(cc)[p] = reinterpret_cast<const int4*>(cc2)[i];
+            }
+            if (i < nIni) sb[i] = keep ? p : -1;
+            carry += __popcll(m);
         }
+        if (ln == 0) misc[7] = carry;
     }
     __syncthreads();
-    for (int k = tid; k < K; k += T) kn[k] = (int16_t)sa[kn[k]];
-    for (int i = tid; i < n; i += T) { A_xr[i] = B_xr[i]; A_yr[i] = B_yr[i]; A_cnt[i] = B_cnt[i]; A_seq[i] = B_seq[i]; }
-    if (tid == 0) misc[0] = 0;                               // phase 1's count of nodes to expand
-    __syncthreads();
+    int n = misc[7];
+    {
+        int* t;
+        t = A_xr; A_xr = B_xr; B_xr = t;
+        t = A_yr; A_yr = B_yr; B_yr = t;
+        t = A_cnt; A_cnt = B_cnt; B_cnt = t;
+        t = A_seq; A_seq = B_seq; B_seq = t;
+        t = A_mid; A_mid = B_mid; B_mid = t;
+    }
+    bool remap = true;                                     // kn holds root indices until the first key move
 
     const int N = L.N;
     // A = the node list of the current pass, B = the list it builds; after a pass the two swap roles
@@ -1169,33 +1167,58 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
         t = A_yr; A_yr = B_yr; B_yr = t;
         t = A_cnt; A_cnt = B_cnt; B_cnt = t;
         t = A_seq; A_seq = B_seq; B_seq = t;
+        t = A_mid; A_mid = B_mid; B_mid = t;
     };
-    bool phase2 = false, finished = false, counted = false;
+    // A split node's children (quadrant q) go to the new list from group base gb on, in the reference's order (n4 .. n1,
+    // empty children dropped: gb + rank_desc), with their rectangle, count, creation order and split point;
+    // base[i] = the new position of a node that stays, or -2 - gb for a split node.
+    auto write_children = [&](int i, int gb, int cre) {
+        const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
+        const int mid = A_mid[i], mx = mid & 0xffff, my = mid >> 16;
+        const int* c4 = cc + 4 * i;
+        for (int q = 0; q < 4; ++q) {
+            if (c4[q] == 0) continue;
+            const int cx0 = (q & 1) ? mx : x0, cx1 = (q & 1) ? x1 : mx, cy0 = (q & 2) ? my : y0, cy1 = (q & 2) ? y1 : my;
+            const int p = gb + rank_desc(c4, q);
+            B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
+            B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
+            B_cnt[p] = c4[q];
+            B_seq[p] = cre + rank_asc(c4, q);
+            B_mid[p] = node_mid(cx0, cx1, cy0, cy1);
+            reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
+        }
+        base[i] = -2 - gb;
+    };
+    auto keep_node = [&](int i, int p) {
+        base[i] = p;
+        B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i]; B_mid[p] = A_mid[i];
+        reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
+    };
+    // every key to its node of the new list; the new list's child counts taken on the way (the next pass's cc)
+    auto move_keys = [&]() {
+        for (int k = tid; k < K; k += T) {
+            const int i = remap ? sb[kn[k]] : kn[k];
+            const uint32_t xy = kxy[k];
+            const int b = base[i];
+            int p = b;
+            if (b < 0) {                                     // split: one 16-byte read of the node's child counts
+                const int4 c = reinterpret_cast<const int4*>(cc)[i];
+                const int c4[4] = {c.x, c.y, c.z, c.w};
+                p = -2 - b + rank_desc(c4, mid_quadrant(xy, A_mid[i]));
+            }
+            kn[k] = (int16_t)p;
+            if (B_cnt[p] > 1) atomicAdd(&cc2[4 * p + mid_quadrant(xy, B_mid[p])], 1);
+        }
+    };
+    bool phase2 = false, finished = false;
     // The node-list bookkeeping of a pass (flags, prefix sums, the new list, the phase decisions) is O(nodes <= cap)
     // and runs on wave 0 alone with wave-level scans and fences; the other waves wait at one barrier, then every thread
     // moves the keys.  Two block barriers per pass (phase 2: plus the sort's), where block-wide scans took ~7.
-    const bool w0 = tid < kWave;
-    const int ln = tid & (kWave - 1);
     QTP(2);
     while (!finished) {
         const int prev = n;
         QTP(10 + phase2);
-        // -- child counts of every expandable node (phase 1 splits all of them, phase 2 needs their sizes); after the
-        //    first pass they were counted while the previous pass moved the keys (cc2, now cc)
-        if (!counted) {
-        for (int i = tid; i < 4 * n; i += T) cc[i] = 0;
-        __syncthreads();
-        for (int k = tid; k < K; k += T) {
-            const int i = kn[k];
-            if (A_cnt[i] > 1) {
-                const int q = quadrant(kxy[k], A_xr[i] & 0xffff, A_xr[i] >> 16, A_yr[i] & 0xffff, A_yr[i] >> 16);
-                atomicAdd(&cc[4 * i + q], 1);
-            }
-        }
-        __syncthreads();
-        }
         QTP(20);
-
         if (!phase2) {
             // ---------------- phase 1 pass (:606-665), bookkeeping on wave 0
             // per node: children (split) or 1 survivor, packed as children << 16 | survivor so that ONE scan gives both
@@ -1221,29 +1244,8 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                     if (ln == 0) { atomicOr(err, kErrQtCap); misc[2] = -1; }
                 } else {
                     for (int i = ln; i < n; i += kWave) {
-                        const int nch = base[i];
-                        if (A_cnt[i] > 1) {
-                            const int gb = C - (sa[i] >> 16) - nch;
-                            base[i] = gb;
-                            const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
-                            const int* c4 = cc + 4 * i;
-                            for (int q = 0; q < 4; ++q) {
-                                if (c4[q] == 0) continue;
-                                int cx0, cx1, cy0, cy1;
-                                child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
-                                const int p = gb + rank_desc(c4, q);
-                                B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
-                                B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
-                                B_cnt[p] = c4[q];
-                                B_seq[p] = (sa[i] >> 16) + rank_asc(c4, q);
-                                reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
-                            }
-                        } else {
-                            const int p = C + (sa[i] & 0xffff);
-                            base[i] = p;
-                            B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
-                            reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
-                        }
+                        if (A_cnt[i] > 1) write_children(i, C - (sa[i] >> 16) - base[i], sa[i] >> 16);
+                        else keep_node(i, C + (sa[i] & 0xffff));
                     }
                     if (ln == 0) {
                         // :669-673, decided here for every thread: 1 finished, 2 on to phase 2
@@ -1257,28 +1259,10 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
             const int dec = misc[2];
             if (dec < 0) { finished = true; break; }
             const int nn = misc[3];
-            for (int k = tid; k < K; k += T) {
-                const int i = kn[k];
-                const uint32_t xy = kxy[k];
-                int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
-                int p, c;                                        // new list position, its key count
-                if (A_cnt[i] > 1) {
-                    const int q = quadrant(xy, x0, x1, y0, y1);
-                    p = base[i] + rank_desc(cc + 4 * i, q);
-                    c = cc[4 * i + q];
-                    int cx0, cx1, cy0, cy1;
-                    child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
-                    x0 = cx0; x1 = cx1; y0 = cy0; y1 = cy1;
-                } else {
-                    p = base[i];
-                    c = A_cnt[i];
-                }
-                kn[k] = (int16_t)p;
-                if (c > 1) atomicAdd(&cc2[4 * p + quadrant(xy, x0, x1, y0, y1)], 1);   // the next pass's counts
-            }
+            move_keys();
             __syncthreads();
+            remap = false;
             swap_nodes();                                        // the new list becomes A (no copy, no barrier)
-            counted = true;
             n = nn;
             QTP(50);
             if (dec == 1) finished = true;
@@ -1312,8 +1296,8 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                 // children of the p-th processed node (sb), the first p at which the list reaches N (:713-720): the
                 // list grows by children - 1 per processed node, so n + inclusive prefix of the deltas is nondecreasing
                 int brk = nV, acc = 0;
-                for (int b = 0; b < nV; b += kWave) {
-                    const int p = b + ln;
+                for (int b0 = 0; b0 < nV; b0 += kWave) {
+                    const int p = b0 + ln;
                     int d = 0;
                     if (p < nV) {
                         const int i = (int)(key_at(p) & 0xfffff);
@@ -1324,7 +1308,7 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                     }
                     const int inc = acc + wave_incl_scan(d);
                     const uint64_t hit = __ballot(p < nV && n + inc >= N);
-                    if (brk == nV && hit) brk = b + (int)__builtin_ctzll(hit);
+                    if (brk == nV && hit) brk = b0 + (int)__builtin_ctzll(hit);
                     acc = __builtin_amdgcn_readlane(inc, kWave - 1);
                 }
                 const int nproc = min(brk + 1, nV);
@@ -1333,16 +1317,17 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                 for (int p = ln; p < nV; p += kWave) sa[p] = (p < nproc) ? sb[p] : 0;
                 wave_fence();
                 const int Cn = wave_excl_scan_lds(sa, nV, ln);
-                for (int i = ln; i < n; i += kWave) base[i] = -1;
+                for (int i = ln; i < n; i += kWave) base[i] = 0;
                 wave_fence();
-                // processed nodes: base = group base; survivors ranked after the groups
+                // processed nodes: their group base (kept in base as -2 - gb) and creation prefix (in A_seq: the node is
+                // erased anyway); the survivors are ranked after the groups
                 for (int p = ln; p < nproc; p += kWave) {
                     const int i = (int)(key_at(p) & 0xfffff);
-                    base[i] = Cn - sa[p] - sb[p];
-                    A_seq[i] = -1 - sa[p];           // stash creation prefix (node is erased anyway)
+                    base[i] = -2 - (Cn - sa[p] - sb[p]);
+                    A_seq[i] = -1 - sa[p];
                 }
                 wave_fence();
-                for (int i = ln; i < n; i += kWave) sb[i] = (base[i] < 0) ? 1 : 0;
+                for (int i = ln; i < n; i += kWave) sb[i] = (base[i] >= 0) ? 1 : 0;
                 wave_fence();
                 const int U = wave_excl_scan_lds(sb, n, ln);
                 wave_fence();
@@ -1351,62 +1336,30 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                     if (ln == 0) { atomicOr(err, kErrQtCap); misc[2] = -1; }
                 } else {
                     for (int i = ln; i < n; i += kWave) {
-                        if (base[i] >= 0) {
-                            const int gb = base[i];
-                            const int cre = -1 - A_seq[i];
-                            const int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
-                            const int* c4 = cc + 4 * i;
-                            for (int q = 0; q < 4; ++q) {
-                                if (c4[q] == 0) continue;
-                                int cx0, cx1, cy0, cy1;
-                                child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
-                                const int p = gb + rank_desc(c4, q);
-                                B_xr[p] = (cx0 & 0xffff) | (cx1 << 16);
-                                B_yr[p] = (cy0 & 0xffff) | (cy1 << 16);
-                                B_cnt[p] = c4[q];
-                                B_seq[p] = cre + rank_asc(c4, q);
-                                reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
-                            }
-                        } else {
-                            const int p = Cn + sb[i];
-                            B_xr[p] = A_xr[i]; B_yr[p] = A_yr[i]; B_cnt[p] = A_cnt[i]; B_seq[p] = A_seq[i];
-                            reinterpret_cast<int4*>(cc2)[p] = make_int4(0, 0, 0, 0);
-                        }
+                        const int b = base[i];
+                        if (b < 0) write_children(i, -2 - b, -1 - A_seq[i]);
+                        else keep_node(i, Cn + sb[i]);
                     }
-                    if (ln == 0) { misc[2] = (nn >= N || nn == prev) ? 1 : 0; misc[3] = nn; misc[6] = Cn; }   // :734-735
+                    if (ln == 0) { misc[2] = (nn >= N || nn == prev) ? 1 : 0; misc[3] = nn; }   // :734-735
                 }
             }
             __syncthreads();
             QTP(32);
             const int dec = misc[2];
             if (dec < 0) { finished = true; break; }
-            const int nn = misc[3], Cn = misc[6];
-            for (int k = tid; k < K; k += T) {
-                const int i = kn[k];
-                const uint32_t xy = kxy[k];
-                int x0 = A_xr[i] & 0xffff, x1 = A_xr[i] >> 16, y0 = A_yr[i] & 0xffff, y1 = A_yr[i] >> 16;
-                int p, c;
-                if (base[i] >= 0) {
-                    const int q = quadrant(xy, x0, x1, y0, y1);
-                    p = base[i] + rank_desc(cc + 4 * i, q);
-                    c = cc[4 * i + q];
-                    int cx0, cx1, cy0, cy1;
-                    child_rect(x0, x1, y0, y1, q, cx0, cx1, cy0, cy1);
-                    x0 = cx0; x1 = cx1; y0 = cy0; y1 = cy1;
-                } else {
-                    p = Cn + sb[i];
-                    c = A_cnt[i];
-                }
-                kn[k] = (int16_t)p;
-                if (c > 1) atomicAdd(&cc2[4 * p + quadrant(xy, x0, x1, y0, y1)], 1);   // the next pass's counts
-            }
+            const int nn = misc[3];
+            move_keys();
             __syncthreads();
+            remap = false;
             swap_nodes();
-            counted = true;
             n = nn;
             QTP(51);
             if (dec == 1) finished = true;
         }
+    }
+    if (remap) {                                             // no pass ran: the keys still name their roots
+        for (int k = tid; k < K; k += T) kn[k] = (int16_t)sb[kn[k]];
+        __syncthreads();
     }
 
     QTP(80);
@@ -1430,6 +1383,71 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
     // count | call sequence number << 16: the describe that reads this level checks the stamp (ordering canary)
     if (tid == 0) level_cnt[img * nlevels + lvl] = nout | (int)((seq & 0x7fffu) << 16);
     QTP(90);
+}
+
+__global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restrict__ levels, const CellDev* __restrict__ cells,
+                                                         const uint32_t* __restrict__ cand_xy, const uint8_t* __restrict__ cand_s,
+                                                         int cand_stride, const int* __restrict__ cell_cnt, int ncells,
+                                                         QtScratch qs, uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r,
+                                                         int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
+                                                         int scan_cap, int* __restrict__ err, int lvl0, int key_lds_off,
+                                                         int key_lds_cap, unsigned seq) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    const int lvl = lvl0 + (int)blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
+#ifdef ORBX_QT_PROF
+    int qtp_n = 0;
+#endif
+    QTP(0);
+    const LevelDev L = levels[lvl];
+    // LDS layout
+    QtState S;
+    const int cs = (cap + 3) & ~3;     // array stride (16-byte aligned int4 rows below)
+    S.A_xr = smem;               // x0 | x1 << 16
+    S.A_yr = S.A_xr + cs;       // y0 | y1 << 16
+    S.A_cnt = S.A_yr + cs;
+    S.A_seq = S.A_cnt + cs;
+    S.A_mid = S.A_seq + cs;     // split point (node_mid)
+    S.B_xr = S.A_mid + cs;
+    S.B_yr = S.B_xr + cs;
+    S.B_cnt = S.B_yr + cs;
+    S.B_seq = S.B_cnt + cs;
+    S.B_mid = S.B_seq + cs;
+    S.cc = S.B_mid + cs;        // [cap][4] child counts of the current list 
+    S.cc2 = S.cc + 4 * cs;      // [cap][4] child counts of the list being built (counted while keys move)
+    S.base = S.cc2 + 4 * cs;    // new list position of a node that stays, -2 - group base: split
+    S.sa = S.base + cs;         // scan array [scan_cap]
+    S.sb = S.sa + scan_cap;      // scan array [scan_cap]
+    S.tmp = S.sb + scan_cap;     // 32 ints
+    S.misc = S.tmp + 32;         // 16 ints
+    S.sk = (unsigned long long*)(S.misc + 16 + ((S.misc + 16 - smem) & 1));  // [pow2 >= cap]
+    const int ncl = L.cell_end - L.cell_begin;
+    int* sa = S.sa;
+    int* sb = S.sb;
+
+    // ---- 1. compact the level's cell candidates into reference order (cell row-major, then FAST order)
+    // (per cell: count -> sa, slot offset -> sb; all loads independent)
+    for (int i = tid; i < ncl; i += T) {
+        const int cw = cell_cnt[(size_t)img * ncells + L.cell_begin + i];
+        sa[i] = cw;
+        sb[i] = cells[L.cell_begin + i].slot_off;
+    }
+    __syncthreads();
+    const int K = block_scan_array(sa, ncl, S.tmp);
+    // Every pass walks all K keys: they live in LDS when the level's keys fit the launch's key region (the common case:
+    // ~2-4k keys at level 0 of a KITTI frame) -- then every key access is an LDS instruction -- and in the HBM scratch
+    // otherwise.
+    uint8_t* kr = qs.key_r + (size_t)img * cand_stride + L.cand_off;
+    if (K <= key_lds_cap) {
+        lds_u32* kxy = (lds_u32*)(reinterpret_cast<char*>(smem) + key_lds_off);
+        lds_i16* kn = (lds_i16*)(kxy + key_lds_cap);
+        qt_level(S, L, lvl, img, K, ncl, kxy, kn, kr, cand_xy, cand_s, cand_stride, out_xy, out_r, out_stride, level_cnt,
+                 nlevels, cap, err, seq);
+    } else {
+        uint32_t* kxy = qs.key_xy + (size_t)img * cand_stride + L.cand_off;
+        int16_t* kn = qs.key_node + (size_t)img * cand_stride + L.cand_off;
+        qt_level(S, L, lvl, img, K, ncl, kxy, kn, kr, cand_xy, cand_s, cand_stride, out_xy, out_r, out_stride, level_cnt,
+                 nlevels, cap, err, seq);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2161,10 +2179,11 @@ int Extractor::configure(int r, int c, int batch) {
     return ORBX_OK;
 }
 
-static size_t qt_lds_bytes(int cap, int scan_cap) {
+static size_t qt_lds_bytes(int cap, int scan_cap) {   // k_quadtree's layout (QtState)
     int p2 = 1;
     while (p2 < cap) p2 <<= 1;
-    const size_t ints = 8 * (size_t)cap + 8 * (size_t)cap + (size_t)cap + 2 * (size_t)scan_cap + 32 + 16 + 2;
+    const size_t cs = ((size_t)cap + 3) & ~(size_t)3;
+    const size_t ints = 10 * cs + 8 * cs + cs + 2 * (size_t)scan_cap + 32 + 16 + 2;
     return ints * 4 + (size_t)p2 * 8;
 }
 
@@ -2560,27 +2579,16 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     orbx_keypoint* h_kps = (orbx_keypoint*)(e->h_out + 64);
     uint8_t* h_desc = e->h_out + odesc;
     hipStream_t s = e->own();
-    // The image in (outside the graph: its source changes every call).  The previous call's transfers out of h_in
-    // completed before it returned (stream synchronised).  Mode 0: packed into pinned staging in row bands, each band's
-    // H2D copy issued as soon as it is packed, so the DMA of one band overlaps the packing of the next; mode 1: one
-    // pageable copy from the caller's image (the runtime stages it; dense rows only); ORBX_HOST_H2D (A/B).
-    static const int h2d_mode = std::getenv("ORBX_HOST_H2D") ? std::atoi(std::getenv("ORBX_HOST_H2D")) : 0;
-    if (h2d_mode == 1 && step == (size_t)cols) {
-        ORBX_HIP(hipMemcpyAsync(e->d_in, image, nb, hipMemcpyHostToDevice, s));
+    // The image in, outside the graph (its source changes every call): packed into pinned staging, one H2D copy.  (r4n,
+    // native per-call path: one staged copy 0.397 / 0.396 ms per frame, a pageable copy 0.398 / 0.393, four row bands
+    // each copied as soon as packed 0.427 / 0.424.)  The previous call's transfers out of h_in completed before it
+    // returned (stream synchronised).
+    if (step == (size_t)cols) {
+        std::memcpy(e->h_in, image, nb);
     } else {
-        const int bands = h2d_mode == 2 ? 1 : 4;
-        const int rb = (rows + bands - 1) / bands;
-        for (int r0 = 0; r0 < rows; r0 += rb) {
-            const int r1 = std::min(rows, r0 + rb);
-            if (step == (size_t)cols) {
-                std::memcpy(e->h_in + (size_t)r0 * cols, image + (size_t)r0 * cols, (size_t)(r1 - r0) * cols);
-            } else {
-                for (int r = r0; r < r1; ++r) std::memcpy(e->h_in + (size_t)r * cols, image + (size_t)r * step, (size_t)cols);
-            }
-            ORBX_HIP(hipMemcpyAsync(e->d_in + (size_t)r0 * cols, e->h_in + (size_t)r0 * cols, (size_t)(r1 - r0) * cols,
-                                    hipMemcpyHostToDevice, s));
-        }
+        for (int r = 0; r < rows; ++r) std::memcpy(e->h_in + (size_t)r * cols, image + (size_t)r * step, (size_t)cols);
     }
+    ORBX_HIP(hipMemcpyAsync(e->d_in, e->h_in, nb, hipMemcpyHostToDevice, s));
     // the call's other stream operations: the extraction, count + keypoints + descriptors of the whole capacity in one
     // copy (a count-sized copy would need a second synchronisation; only the first n are read), the error word
     auto enqueue = [&]() -> int {
