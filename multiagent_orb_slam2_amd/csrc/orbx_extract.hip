@@ -473,6 +473,41 @@ __device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, in
 }
 
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+// Bitonic sort (ascending) of 64 * R 64-bit keys in LDS by ONE wave, in registers: element e = lane * R + r, stages
+// with j < R swap registers of a lane, the others exchange with lane ^ (j / R) by a cross-lane shuffle -- no LDS traffic
+// or fence inside the network, no block barrier.
+template <int R>
+__device__ __forceinline__ void wave_bitonic_u64(unsigned long long* a, int ln) {
+    unsigned long long v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = a[ln * R + r];
+#pragma unroll
+    for (int k = 2; k <= 64 * R; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= R) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int e = ln * R + r;
+                    const unsigned long long o = __shfl_xor(v[r], j / R, kWave);
+                    const bool keep_min = ((e & k) == 0) == ((e & j) == 0);
+                    v[r] = keep_min ? (v[r] < o ? v[r] : o) : (v[r] < o ? o : v[r]);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (r & j) continue;
+                    const int e = ln * R + r;
+                    const unsigned long long x = v[r], y = v[r | j];
+                    if ((x > y) == ((e & k) == 0)) { v[r] = y; v[r | j] = x; }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) a[ln * R + r] = v[r];
+}
+
 // exclusive prefix sums of a[0, n) in place by one wave (lane ln); returns the total
 __device__ __forceinline__ int wave_excl_scan_lds(int* a, int n, int ln) {
     int carry = 0;
@@ -1019,6 +1054,7 @@ __device__ unsigned long long g_qtprof[2][64];
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) int16_t lds_i16;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 // split point of a node, packed (x0 + ceil((x1-x0)/2)) | (y0 + ceil((y1-y0)/2)) << 16 (DivideNode :483-509; the float
 // halving of an integer width is exact, so its ceiling is (w + 1) >> 1); a key's quadrant is (x >= mx) + 2 (y >= my)
@@ -1037,9 +1073,9 @@ struct QtState {         // one workgroup's LDS arrays (k_quadtree)
 
 // Everything after the level's key count is known, for keys in LDS (PXY / PN address-space-3 pointers: ds_ loads) or
 // in the HBM scratch (plain pointers).
-template <typename PXY, typename PN>
+template <typename PXY, typename PN, typename PR>
 __device__ __forceinline__ void qt_level(QtState S, const LevelDev& L, int lvl, int img, int K, int ncl, PXY kxy, PN kn,
-                                         uint8_t* __restrict__ kr, const uint32_t* __restrict__ cand_xy,
+                                         PR kr, const uint32_t* __restrict__ cand_xy,
                                          const uint8_t* __restrict__ cand_s, int cand_stride,
                                          uint32_t* __restrict__ out_xy, uint8_t* __restrict__ out_r, int out_stride,
                                          int* __restrict__ level_cnt, int nlevels, int cap, int* __restrict__ err,
@@ -1269,54 +1305,68 @@ __device__ __forceinline__ void qt_level(QtState S, const LevelDev& L, int lvl, 
             else if (dec == 2) phase2 = true;
         } else {
             // ---------------- phase 2 pass (:676-737)
-            // expandable nodes -> sort keys (size, creation order, node), on wave 0
+            // expandable nodes -> sort keys (size, creation order, node), on wave 0; up to 512 of them wave 0 sorts in
+            // registers too and goes straight on to the bookkeeping (one block barrier for the pass's list work)
+            int nV = 0, P2 = 1;
+            const bool wsort = n <= 512;                       // workgroup-uniform: nV <= n
             if (w0) {
                 for (int i = ln; i < n; i += kWave) sa[i] = A_cnt[i] > 1 ? 1 : 0;
                 wave_fence();
-                const int nV = wave_excl_scan_lds(sa, n, ln);
+                nV = wave_excl_scan_lds(sa, n, ln);
                 wave_fence();
-                int P2 = 1;
                 while (P2 < nV) P2 <<= 1;
-                for (int i = ln; i < P2; i += kWave) sk[i] = ~0ull;
+                const int PW = wsort ? max(P2, kWave) : P2;      // the wave sort pads to at least 64 keys
+                for (int i = ln; i < PW; i += kWave) sk[i] = ~0ull;
                 wave_fence();
                 for (int i = ln; i < n; i += kWave)
                     if (A_cnt[i] > 1)
                         sk[sa[i]] = ((unsigned long long)A_cnt[i] << 40) | ((unsigned long long)A_seq[i] << 20) | (unsigned long long)i;
+                wave_fence();
+                if (wsort) {
+                    if (PW <= kWave) wave_bitonic_u64<1>(sk, ln);
+                    else if (PW <= 2 * kWave) wave_bitonic_u64<2>(sk, ln);
+                    else if (PW <= 4 * kWave) wave_bitonic_u64<4>(sk, ln);
+                    else wave_bitonic_u64<8>(sk, ln);
+                    wave_fence();
+                }
                 if (ln == 0) { misc[4] = nV; misc[5] = P2; }
             }
-            __syncthreads();
-            const int nV = misc[4], P2 = misc[5];
-            // bitonic sort ascending (keys are unique: node index in the low bits); stages inside a wave's 128 keys
-            // need only a wave-level fence (block_bitonic_u64).  (Ranking each key by counting the smaller ones, no
-            // dependent stages, measured slower: 9 -> 15.7 us per level-0 pass, r3am.)
-            if (P2 >= 2) block_bitonic_u64(sk, P2);
+            if (!wsort) {
+                // larger lists: every wave sorts (stages inside a wave's 128 keys need only a wave-level fence,
+                // block_bitonic_u64).  (Ranking each key by counting the smaller ones measured slower, r3am.)
+                __syncthreads();
+                nV = misc[4];
+                P2 = misc[5];
+                if (P2 >= 2) block_bitonic_u64(sk, P2);
+            }
             auto key_at = [&](int p) { return sk[nV - 1 - p]; };     // processing order: descending keys
             QTP(31);
             if (w0) {
                 // children of the p-th processed node (sb), the first p at which the list reaches N (:713-720): the
-                // list grows by children - 1 per processed node, so n + inclusive prefix of the deltas is nondecreasing
-                int brk = nV, acc = 0;
+                // list grows by children - 1 per processed node, so n + inclusive prefix of the deltas is nondecreasing;
+                // the children before p (the new nodes' creation prefix, sa) = the deltas' exclusive prefix + p
+                int brk = nV, acc = 0, inc_brk = 0;
                 for (int b0 = 0; b0 < nV; b0 += kWave) {
                     const int p = b0 + ln;
                     int d = 0;
                     if (p < nV) {
                         const int i = (int)(key_at(p) & 0xfffff);
-                        const int* c4 = cc + 4 * i;
-                        const int ch = (c4[0] > 0) + (c4[1] > 0) + (c4[2] > 0) + (c4[3] > 0);
+                        const int4 c = reinterpret_cast<const int4*>(cc)[i];
+                        const int ch = (c.x > 0) + (c.y > 0) + (c.z > 0) + (c.w > 0);
                         sb[p] = ch;
                         d = ch - 1;
                     }
                     const int inc = acc + wave_incl_scan(d);
+                    if (p < nV) sa[p] = inc - d + p;
                     const uint64_t hit = __ballot(p < nV && n + inc >= N);
-                    if (brk == nV && hit) brk = b0 + (int)__builtin_ctzll(hit);
+                    if (brk == nV && hit) {
+                        brk = b0 + (int)__builtin_ctzll(hit);
+                        inc_brk = __builtin_amdgcn_readlane(inc, brk - b0);
+                    }
                     acc = __builtin_amdgcn_readlane(inc, kWave - 1);
                 }
                 const int nproc = min(brk + 1, nV);
-                wave_fence();
-                // children prefix over the processed nodes (creation order of the new nodes)
-                for (int p = ln; p < nV; p += kWave) sa[p] = (p < nproc) ? sb[p] : 0;
-                wave_fence();
-                const int Cn = wave_excl_scan_lds(sa, nV, ln);
+                const int Cn = (brk < nV ? inc_brk : acc) + nproc;   // children of the processed nodes
                 for (int i = ln; i < n; i += kWave) base[i] = 0;
                 wave_fence();
                 // processed nodes: their group base (kept in base as -2 - gb) and creation prefix (in A_seq: the node is
@@ -1327,9 +1377,15 @@ __device__ __forceinline__ void qt_level(QtState S, const LevelDev& L, int lvl, 
                     A_seq[i] = -1 - sa[p];
                 }
                 wave_fence();
-                for (int i = ln; i < n; i += kWave) sb[i] = (base[i] >= 0) ? 1 : 0;
-                wave_fence();
-                const int U = wave_excl_scan_lds(sb, n, ln);
+                // survivors' ranks (base >= 0) into sb
+                int U = 0;
+                for (int b0 = 0; b0 < n; b0 += kWave) {
+                    const int i = b0 + ln;
+                    const bool sv = i < n && base[i] >= 0;
+                    const uint64_t m = __ballot(sv);
+                    if (i < n) sb[i] = U + lanes_below(m);
+                    U += __popcll(m);
+                }
                 wave_fence();
                 const int nn = Cn + U;
                 if (nn > cap) {
@@ -1436,15 +1492,16 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
     // Every pass walks all K keys: they live in LDS when the level's keys fit the launch's key region (the common case:
     // ~2-4k keys at level 0 of a KITTI frame) -- then every key access is an LDS instruction -- and in the HBM scratch
     // otherwise.
-    uint8_t* kr = qs.key_r + (size_t)img * cand_stride + L.cand_off;
     if (K <= key_lds_cap) {
         lds_u32* kxy = (lds_u32*)(reinterpret_cast<char*>(smem) + key_lds_off);
         lds_i16* kn = (lds_i16*)(kxy + key_lds_cap);
+        lds_u8* kr = (lds_u8*)(kn + key_lds_cap);
         qt_level(S, L, lvl, img, K, ncl, kxy, kn, kr, cand_xy, cand_s, cand_stride, out_xy, out_r, out_stride, level_cnt,
                  nlevels, cap, err, seq);
     } else {
         uint32_t* kxy = qs.key_xy + (size_t)img * cand_stride + L.cand_off;
         int16_t* kn = qs.key_node + (size_t)img * cand_stride + L.cand_off;
+        uint8_t* kr = qs.key_r + (size_t)img * cand_stride + L.cand_off;
         qt_level(S, L, lvl, img, K, ncl, kxy, kn, kr, cand_xy, cand_s, cand_stride, out_xy, out_r, out_stride, level_cnt,
                  nlevels, cap, err, seq);
     }
@@ -2041,21 +2098,33 @@ int Extractor::configure(int r, int c, int batch) {
         const size_t lds = (qt_lds_bytes(cap, scan_cap) + 15) & ~(size_t)15;
         ORBX_REQUIRE(lds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "quadtree LDS %zu B exceeds 160 KiB", lds);
         qt_lds = lds;
-        // LDS key region (6 B per key: xy + node) per launch: level 0 (one workgroup per image, ~2-4k keys on a
+        // LDS key region (7 B per key: xy, node, response) per launch: level 0 (one workgroup per image, ~2-4k keys on a
         // KITTI frame) and levels >= 1 (seven workgroups per image, ~1-1.5k keys at level 1), each bounded by the
         // largest candidate count its levels can produce; levels whose keys overflow it use the HBM scratch
         int lcap[2] = {0, 0};
         for (int l = 0; l < nlevels; ++l) lcap[l ? 1 : 0] = std::max(lcap[l ? 1 : 0], lv[l].cand_cap);
-        int want[2] = {6144, 2048};
+        // sized so that two level-0 workgroups (256 threads) and three of levels >= 1 share a CU's 160 KiB. The budget is
+        // rounded down to 1,280 B, the allocation granule that fits the measured packing: levels >= 1 with 53,344 B per
+        // workgroup run three per CU, with 53,792 B two (0.156 -> 0.212 ms alone, r4y), level 0 with 81,904 B two (r4x;
+        // a 512 B granule would give three at 53,792 B, a 2 KiB one two at 53,344 B). No LDS keys at levels >= 1: 0.186 ms.
+        const int per_cu[2] = {2, 3};
+        int want[2];
+        for (int k = 0; k < 2; ++k) {
+            const size_t budget = (size_t)160 * 1024 / per_cu[k] / 1280 * 1280;
+            want[k] = budget > lds ? (int)((budget - lds) / 7) : 0;
+        }
         if (const char* v = std::getenv("ORBX_QT_KEYS0")) want[0] = std::atoi(v);   // diagnostics
         if (const char* v = std::getenv("ORBX_QT_KEYS1")) want[1] = std::atoi(v);
         size_t maxl = lds;
         for (int k = 0; k < 2; ++k) {
             int kc = std::min(want[k], lcap[k]);
-            kc = (int)std::min<size_t>((size_t)kc, (160 * 1024 - lds) / 6) & ~7;
+            kc = (int)std::min<size_t>((size_t)kc, (160 * 1024 - lds) / 7) & ~7;
             qt_keys[k] = std::max(kc, 0);
-            maxl = std::max(maxl, lds + 6 * (size_t)qt_keys[k]);
+            maxl = std::max(maxl, lds + 7 * (size_t)qt_keys[k]);
         }
+        if (std::getenv("ORBX_QT_VERBOSE"))                                          // diagnostics
+            std::fprintf(stderr, "orbx: k_quadtree LDS %zu B + 7 B x keys %d (level 0) / %d (levels >= 1)\n", lds,
+                         qt_keys[0], qt_keys[1]);
         if (maxl > 64 * 1024)
             ORBX_HIP(hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxl));
     }
@@ -2180,7 +2249,7 @@ int Extractor::configure(int r, int c, int batch) {
 }
 
 static size_t qt_lds_bytes(int cap, int scan_cap) {   // k_quadtree's layout (QtState)
-    int p2 = 1;
+    int p2 = 64;                                            // the sort keys: >= 64 for the one-wave sort's padding
     while (p2 < cap) p2 <<= 1;
     const size_t cs = ((size_t)cap + 3) & ~(size_t)3;
     const size_t ints = 10 * cs + 8 * cs + cs + 2 * (size_t)scan_cap + 32 + 16 + 2;
@@ -2236,7 +2305,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     auto quadtree = [&](hipStream_t q, int lvl0, int n) {
         if (n <= 0) return;
         const int kc = lvl0 == 0 ? e->qt_keys[0] : e->qt_keys[1];  // LDS key capacity: level 0 / levels >= 1
-        hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds + 6 * (size_t)kc, q, e->d_levels, e->d_cells,
+        hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds + 7 * (size_t)kc, q, e->d_levels, e->d_cells,
                            e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
                            e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err, lvl0,
                            (int)e->qt_lds, kc, seq);
