@@ -404,20 +404,22 @@ def host_api_rate(pkg, cfg, lefts, rights, n_frames, device):
     b = cfg["bf"] / cfg["fx"]
     from concurrent.futures import ThreadPoolExecutor
     pool = ThreadPoolExecutor(1)                     # the right extraction on its own thread, as Frame.cc:78-81
-    lat = []
-    for i in range(n_frames + 3):
+    lat, warm = [], []
+    # 10 untimed frames: among the first ~10 calls one takes 7-20 ms (one-time runtime set-up on the extractor's
+    # thread, r4hac); their maximum is reported as warmup_ms_max
+    n_warm = 10
+    for i in range(n_frames + n_warm):
         t0 = time.perf_counter()
         fr = pool.submit(ex_r, rights[i % len(rights)])
         kl, dl = ex_l(lefts[i % len(lefts)])       # ctypes releases the GIL: both extractions run natively at once
         kr, dr = fr.result()
         m.ComputeStereoMatches(ex_l, ex_r, kl, dl, kr, dr, cfg["bf"], b)
-        if i >= 3:
-            lat.append(time.perf_counter() - t0)
+        (lat if i >= n_warm else warm).append(time.perf_counter() - t0)
     pool.shutdown()
     lat_ms = np.array(lat) * 1e3
     out = {"frames_per_s": round(1e3 / float(np.mean(lat_ms)), 1), "latency_ms_median": round(float(np.median(lat_ms)), 3),
            "latency_ms_p95": round(float(np.percentile(lat_ms, 95)), 3), "latency_ms_max": round(float(np.max(lat_ms)), 3),
-           "frames": len(lat),
+           "frames": len(lat), "warmup_frames": n_warm, "warmup_ms_max": round(1e3 * max(warm), 3),
            "path": "Python ctypes: orbx_extract(L) and orbx_extract(R) on two threads (Frame.cc:78-81) + "
                    "orbx_compute_stereo_matches, host buffers, one frame per call"}
     # the same per-call path from a C++ caller (the reference's own language): scripts/micro/host_api_bench.cpp, built

@@ -1789,6 +1789,10 @@ struct Extractor {
     hipGraphExec_t hgexec = nullptr;
     bool capturing = false;       // run_batch inside the capture: no waits on earlier calls, no host synchronisation
     bool host_graph = true;       // ORBX_HOST_GRAPH=0: the host API issues its stream operations every call (A/B)
+    // ORBX_HOST_SERIAL=0: the host API's one-image calls fork the level-0 branch onto the side stream like the batches.
+    // Serial by default: two extractors called from two threads (Frame.cc:78-81) then use one hardware queue each
+    // instead of sharing the process's 4 among four streams (r4haf: 0.370 -> 0.297 ms per stereo frame, median)
+    bool host_serial = true;
     bool async_pending = false;   // a device-API call may still run: the next replay first waits for every describe
     uint8_t* hg_pyr = nullptr;    // the pyramid set the graph's kernels write
     void drop_graph() {
@@ -2259,7 +2263,7 @@ static size_t qt_lds_bytes(int cap, int scan_cap) {   // k_quadtree's layout (Qt
 
 static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t step, size_t istride,
                      orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int capacity, hipStream_t s,
-                     hipStream_t so) {
+                     hipStream_t so, bool pipelined) {
     const int nl = e->nlevels;
     const size_t ps = e->pyr_size;
     Extractor::EventSet* es = nullptr;
@@ -2278,8 +2282,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     const int ci = (int)(e->cev_next++ % Extractor::kCallEv);
     Extractor::CallEvents& ce = e->cev[ci];
     if (ce.used && !e->capturing) ORBX_HIP(hipEventSynchronize(ce.desc));
-    hipStream_t side = e->pipeline ? e->side : s;
-    if (!e->pipeline) so = s;
+    hipStream_t side = pipelined ? e->side : s;
+    if (!pipelined) so = s;
     auto mark = [&](int k) {
         if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : (k == 4 || k == 5) ? so : s);
     };
@@ -2491,6 +2495,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* pl = std::getenv("ORBX_PIPELINE")) e->pipeline = std::atoi(pl) != 0;
     if (const char* tp = std::getenv("ORBX_FAST_TWOPASS")) e->wave_twopass = std::atoi(tp) != 0;
     if (const char* hg = std::getenv("ORBX_HOST_GRAPH")) e->host_graph = std::atoi(hg) != 0;
+    if (const char* hs = std::getenv("ORBX_HOST_SERIAL")) e->host_serial = std::atoi(hs) != 0;
     if (const char* sw = std::getenv("ORBX_DEBUG_SKIP_DESC_WAIT")) e->dbg_skip_desc_wait = std::atoi(sw) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
@@ -2590,7 +2595,8 @@ int orbx_extract_batch_device(orbx_extractor* e, const uint8_t* d_images, int ba
     if (st) return st;
     ORBX_REQUIRE(capacity >= e->out_capacity, ORBX_ERR_CAPACITY, "capacity %d < required %d", capacity, e->out_capacity);
     hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream
-    return run_batch(e, d_images, batch, step, image_stride, d_keypoints, d_descriptors, d_counts, capacity, s, s);
+    return run_batch(e, d_images, batch, step, image_stride, d_keypoints, d_descriptors, d_counts, capacity, s, s,
+                     e->pipeline);
 }
 
 int orbx_extract_batch_device_split(orbx_extractor* e, const uint8_t* d_images, int batch, int rows, int cols, size_t step,
@@ -2603,7 +2609,7 @@ int orbx_extract_batch_device_split(orbx_extractor* e, const uint8_t* d_images, 
     if (st) return st;
     ORBX_REQUIRE(capacity >= e->out_capacity, ORBX_ERR_CAPACITY, "capacity %d < required %d", capacity, e->out_capacity);
     return run_batch(e, d_images, batch, step, image_stride, d_keypoints, d_descriptors, d_counts, capacity,
-                     (hipStream_t)in_stream, (hipStream_t)out_stream);
+                     (hipStream_t)in_stream, (hipStream_t)out_stream, e->pipeline);
 }
 
 int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, size_t step, orbx_keypoint* kps,
@@ -2661,7 +2667,8 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     // the call's other stream operations: the extraction, count + keypoints + descriptors of the whole capacity in one
     // copy (a count-sized copy would need a second synchronisation; only the first n are read), the error word
     auto enqueue = [&]() -> int {
-        int r = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, s, s);
+        int r = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, s, s,
+                          e->pipeline && !e->host_serial);
         if (r) return r;
         ORBX_HIP(hipMemcpyAsync(e->h_out, e->d_hblk, ob, hipMemcpyDeviceToHost, s));
         ORBX_HIP(hipMemcpyAsync(h_cnt + 1, e->d_err, sizeof(int), hipMemcpyDeviceToHost, s));

@@ -362,6 +362,7 @@ class ORBextractor:
         self.nfeatures, self.nlevels, self.device = nfeatures, nlevels, device
         _register(self)
         self._last_shape = None
+        self._out = None          # host output staging of __call__
 
     def close(self):
         if getattr(self, "_h", None):
@@ -430,8 +431,11 @@ class ORBextractor:
         assert img.ndim == 2, "8UC1 image expected"
         rows, cols = img.shape
         cap = self.max_keypoints(rows, cols)
-        kps = np.zeros(cap, KP_DTYPE)
-        desc = np.zeros((cap, 32), np.uint8)
+        # output staging reused across calls (only the first n entries are written and copied out): fresh zeroed
+        # arrays of the full capacity (480 KB at KITTI) cost page faults and a memset per call
+        if self._out is None or len(self._out[0]) < cap:
+            self._out = (np.empty(cap, KP_DTYPE), np.empty((cap, 32), np.uint8))
+        kps, desc = self._out
         n = C.c_int()
         _check(self._lib.orbx_extract(self._h, _p(img), rows, cols, img.strides[0], _p(kps), _p(desc), cap,
                                       C.byref(n)))

@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -89,7 +90,8 @@ int main(int argc, char** argv) {
     const float fx = 718.856f, bf = 386.1448f;
     std::vector<double> t_frame, t_left, t_right, t_stereo;
     int bad = 0;
-    for (int f = -5; f < frames; ++f) {
+    double warm_max = 0;                                          // 10 untimed frames (one-time runtime set-up)
+    for (int f = -10; f < frames; ++f) {
         const int k = (f + kDistinct * 4) % kDistinct;
         int nl = 0, nr = 0, ns = 0, str = 0;
         double tr = 0;
@@ -107,15 +109,22 @@ int main(int argc, char** argv) {
                                                     bf / fx, ur.data(), depth.data(), &ns);
         const double tsm = ms_since(t1), tf = ms_since(t0);
         if (stl || str || sts) { ++bad; std::fprintf(stderr, "frame %d: %s\n", f, orbx_last_error()); }
-        if (f < 0) continue;
+        if (f < 0) { warm_max = std::max(warm_max, tf); continue; }
         t_frame.push_back(tf); t_left.push_back(tl); t_right.push_back(tr); t_stereo.push_back(tsm);
     }
     const Stats F = stats(t_frame), A = stats(t_left), B = stats(t_right), S = stats(t_stereo);
+    std::vector<int> order(t_frame.size());                      // the slowest frames, for outlier attribution
+    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return t_frame[a] > t_frame[b]; });
+    std::string slow;
+    for (size_t i = 0; i < std::min<size_t>(3, order.size()); ++i)
+        slow += (i ? ", " : "") + std::string("[") + std::to_string(order[i]) + ", " + std::to_string(t_frame[order[i]]) + ", " +
+                std::to_string(t_left[order[i]]) + ", " + std::to_string(t_right[order[i]]) + ", " + std::to_string(t_stereo[order[i]]) + "]";
     std::printf("{\"lib\": \"%s\", \"frames\": %d, \"frames_per_s\": %.1f, \"frame_ms\": {\"median\": %.4f, \"p95\": %.4f, "
                 "\"max\": %.4f, \"mean\": %.4f}, \"extract_left_ms\": {\"median\": %.4f, \"p95\": %.4f}, "
                 "\"extract_right_ms\": {\"median\": %.4f, \"p95\": %.4f}, \"stereo_ms\": {\"median\": %.4f, \"p95\": %.4f}, "
-                "\"errors\": %d}\n",
-                argv[1], frames, 1e3 / F.mean, F.med, F.p95, F.max, F.mean, A.med, A.p95, B.med, B.p95, S.med, S.p95, bad);
+                "\"errors\": %d, \"slowest\": [%s], \"warmup_frames\": 10, \"warmup_ms_max\": %.4f}\n",
+                argv[1], frames, 1e3 / F.mean, F.med, F.p95, F.max, F.mean, A.med, A.p95, B.med, B.p95, S.med, S.p95, bad, slow.c_str(), warm_max);
     orbx_matcher_destroy(m);
     orbx_extractor_destroy(exl);
     orbx_extractor_destroy(exr);
