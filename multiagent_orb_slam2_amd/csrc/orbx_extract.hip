@@ -977,7 +977,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_W
     const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
     if (item >= nbx * batch) return;
     const int img = item / nbx;
-    const int tl = (item - img * nbx) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // the tile index is wave-uniform: as an SGPR the tile and its level load by scalar loads and every row address
+    // and reflection is scalar work
+    const int tl = __builtin_amdgcn_readfirstlane((item - img * nbx) * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (tl >= ntiles) return;
     blur_tile(pyr, blur, pyr_stride, levels, tiles[tile0 + tl], img, s0);
 }
