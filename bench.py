@@ -645,8 +645,9 @@ def source_sha16():
 
 def active_kernel_names():
     """Names (as rocprofv3 prints them) of the extractor kernels this process runs (csrc/orbx_extract.hip run_batch):
-    k_fast_wave's pair stride is 24 for every cell of the KITTI / EuRoC configs (40 only for cells wider than 46)."""
-    return {"fast": "k_fast_wave<24, 4>", "describe": "k_describe_m<2>", "blur": "k_blur7",
+    k_fast_wave's padded pair rows are 19 dwords for every cell of the KITTI / EuRoC configs (cells up to 38 columns;
+    the 40-dword form only for wider ones), 4 waves per workgroup."""
+    return {"fast": "k_fast_wave<19, 4, 4>", "describe": "k_describe_m<2>", "blur": "k_blur7",
             "families": {"k_fast_wave", "k_describe_m", "k_quadtree", "k_blur7", "k_resize4"}}
 
 
