@@ -101,6 +101,9 @@ def parse():
                          "descriptors) out of the keyframe path")
     ap.add_argument("--no-tracking", dest="tracking", action="store_false",
                     help="leave the tracking matches (SearchByProjection motion model + local map) out of the step")
+    ap.add_argument("--track-stream", choices=["stereo", "kf"], default="stereo",
+                    help="queue of the tracking matches: after the stereo step on the stereo queue, or at the head of "
+                         "the keyframe queue")
     ap.add_argument("--no-fuse", dest="fuse", action="store_false",
                     help="leave SearchInNeighbors' Fuse (both ways with 10 neighbours) out of the keyframe path")
     ap.add_argument("--no-cd", dest="cd", action="store_false", help="skip the CovisibilityDiscovery-shaped block")
@@ -919,7 +922,7 @@ def main():
             if time_stereo:
                 e1.record(stereo_stream)
                 stereo_ms.append((e0, e1))
-            if tracker is not None:
+            if tracker is not None and args.track_stream == "stereo":
                 # Tracking's matches of every frame: TrackWithMotionModel's SearchByProjection(F, LastF) and
                 # SearchLocalPoints (Tracking.cc:882-904, :1160-1205) on the frame's stereo MapPoints
                 tracker.run(buf, kps[:B], desc[:B], cnt[:B], stream=stereo_stream)
@@ -931,6 +934,19 @@ def main():
         handoff.record(stereo_stream)
         stereo_done[pslot] = handoff
         last_handoff[0] = handoff
+        if tracker is not None and args.track_stream == "kf":
+            # the tracking matches on the keyframe queue, after the stereo step that gives their MapPoints (depth),
+            # so that the stereo queue (describe, stereo) is free for the next step
+            kf_stream.wait_event(handoff)
+            with torch.cuda.stream(kf_stream):
+                if time_stereo:
+                    e0t = torch.cuda.Event(enable_timing=True)
+                    e0t.record(kf_stream)
+                tracker.run(buf, kps[:B], desc[:B], cnt[:B], stream=kf_stream)
+                if time_stereo:
+                    e1t = torch.cuda.Event(enable_timing=True)
+                    e1t.record(kf_stream)
+                    track_ms.append((e0t, e1t))
         h1 = time.perf_counter()
         if "keyframes" in skip:
             n_step[0] += 1

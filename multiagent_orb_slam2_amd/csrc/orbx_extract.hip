@@ -947,7 +947,7 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
 }
 
 #ifndef ORBX_BLUR_WPE
-#define ORBX_BLUR_WPE 4
+#define ORBX_BLUR_WPE 6     // 80 VGPRs: 6 waves per SIMD (r4ak: serial blur 0.588 -> 0.571 ms; 8 spills 25 VGPRs)
 #endif
 // one wave's blur tile (level, 256-column strip, 16-row band) of image img
 __device__ __forceinline__ void blur_tile(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride,
@@ -1544,6 +1544,10 @@ __device__ __forceinline__ bool lvl_stale(int packed, unsigned seq) {
 constexpr int kBriefR = 18;                      // max |rotated pattern offset|: round(hypot(-13, -13)) = 18
 constexpr int kBriefRow = 40;                    // LDS bytes per window row (5 x 8-byte chunks)
 constexpr int kBriefWin = (2 * kBriefR + 1) * kBriefRow;
+#ifndef ORBX_BRIEF_BATCH
+#define ORBX_BRIEF_BATCH 4
+#endif
+constexpr int kBriefBatch = ORBX_BRIEF_BATCH;                 // BRIEF test groups whose LDS reads are issued together
 
 // Sum of v over the kLp-lane group of each lane (groups of 16, 32 or 64 lanes), in every lane of the group.
 template <int kLp>
@@ -1682,21 +1686,34 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
     float a, b;
     orbx_sincos_brief(ang, &a, &b);
     const uint8_t* center = win + kBriefR * kBriefRow + kBriefR;
+    // kBriefBatch groups of tests at a time: their LDS offsets, then their reads back to back, then the comparisons
+    // (no branch: a rotated offset is within kBriefR of the centre, inside the slice, for invalid lanes too, whose
+    // moments are 0 and angle 0)
     uint32_t words[kNT];                                          // this lane's keypoint: tests g*kLp .. g*kLp+kLp-1
 #pragma unroll
-    for (int g = 0; g < kNT; ++g) {
-        const int t = g * kLp + lk;
-        const uint32_t pw = reinterpret_cast<const uint32_t*>(c_pattern)[t];
-        int vals[2] = {0, 0};
+    for (int g0 = 0; g0 < kNT; g0 += kBriefBatch) {
+        int toff[kBriefBatch][2], vals[kBriefBatch][2];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float fx = (float)(int)(signed char)(pw >> (16 * e)), fy = (float)(int)(signed char)(pw >> (16 * e + 8));
-            const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
-            const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
-            if (valid) vals[e] = center[__mul24(__float2int_rn(ry), kBriefRow) + __float2int_rn(rx)];
+        for (int h = 0; h < kBriefBatch; ++h) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const uint32_t w = reinterpret_cast<const uint32_t*>(c_pattern)[(g0 + h) * kLp + lk];
+                const float fx = (float)(int)(signed char)(w >> (16 * e)), fy = (float)(int)(signed char)(w >> (16 * e + 8));
+                const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
+                const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
+                toff[h][e] = __mul24(__float2int_rn(ry), kBriefRow) + __float2int_rn(rx);
+            }
         }
-        const uint64_t bm = __ballot(vals[0] < vals[1]);
-        words[g] = (uint32_t)(bm >> (sub * kLp)) & (uint32_t)((1ull << kLp) - 1ull);
+#pragma unroll
+        for (int h = 0; h < kBriefBatch; ++h) {
+            vals[h][0] = center[toff[h][0]];
+            vals[h][1] = center[toff[h][1]];
+        }
+#pragma unroll
+        for (int h = 0; h < kBriefBatch; ++h) {
+            const uint64_t bm = __ballot(vals[h][0] < vals[h][1]);
+            words[g0 + h] = (uint32_t)(bm >> (sub * kLp)) & (uint32_t)((1ull << kLp) - 1ull);
+        }
     }
     if (!valid) return;
     // descriptor dword j (j < 8) of this lane's keypoint, written by lane lk = j
