@@ -928,8 +928,17 @@ int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* param
         auto kern = assigning ? (staged ? k_proj_search<true, true> : k_proj_search<false, true>)
                               : (staged ? k_proj_search<true, false> : k_proj_search<false, false>);
         if (lds > 64 * 1024) ORBX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        // 1024-thread workgroups for every mode (r4m: Fuse with 256 threads, 61.8k vs 68.1k frames/s)
-        hipLaunchKernelGGL(kern, dim3(n_problems), dim3(kProjThreads), lds, s, P, grid, d_problems, (int)N, (int)NQ, kcap);
+        // 1024-thread workgroups for the assigning modes (their fixed-point rounds are workgroup-wide), 512 for the
+        // non-assigning ones (Fuse: a workgroup waits for a CU with as many free wave slots beside the front end;
+        // r4ao/r4ap, step 3.66-3.69 ms at 1024, 3.59-3.63 at 512, 3.62-3.64 at 384 / 768, 256 unstable 3.62-3.87).
+        // ORBX_PROJ_NA_THREADS (diagnostics) overrides the latter.
+        static const int na_threads = [] {
+            const char* v = std::getenv("ORBX_PROJ_NA_THREADS");
+            const int t = v ? std::atoi(v) : 512;
+            return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
+        }();
+        const int threads = assigning ? kProjThreads : na_threads;
+        hipLaunchKernelGGL(kern, dim3(n_problems), dim3(threads), lds, s, P, grid, d_problems, (int)N, (int)NQ, kcap);
     }
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
