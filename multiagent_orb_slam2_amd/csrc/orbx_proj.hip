@@ -937,7 +937,12 @@ int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* param
             const int t = v ? std::atoi(v) : 512;
             return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
         }();
-        const int threads = assigning ? kProjThreads : na_threads;
+        static const int a_threads = [] {                       // ORBX_PROJ_A_THREADS (diagnostics): assigning modes
+            const char* v = std::getenv("ORBX_PROJ_A_THREADS");
+            const int t = v ? std::atoi(v) : kProjThreads;
+            return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
+        }();
+        const int threads = assigning ? a_threads : na_threads;
         hipLaunchKernelGGL(kern, dim3(n_problems), dim3(threads), lds, s, P, grid, d_problems, (int)N, (int)NQ, kcap);
     }
     ORBX_HIP(hipGetLastError());
