@@ -89,6 +89,56 @@ __global__ __launch_bounds__(kProjThreads) void k_grid_build(const orbx_keypoint
         if (gkey[i] != 0xffffffffu) ci[i] = (int32_t)(gkey[i] & 0x1fffu);
 }
 
+// Counting form of the same grid (grids of < 32767 cells, the reference's 64 x 48 among them): cell counts by LDS
+// atomics, an exclusive scan gives the cell starts, the keypoints are scattered into their cells by atomic cursors
+// (after the scatter the cursor of cell c is the start of cell c + 1), and each cell's few indices are put back in
+// ascending order by one thread -- the CSR arrays of k_grid_build (cells ascending, indices ascending inside a cell)
+// from O(n) work and 4 barriers instead of the 66 stages of a 2048-key bitonic sort.
+// LDS: cnt[ncell + 1] ints, then cell[cap] and idx[cap] as u16.
+__global__ __launch_bounds__(kProjThreads) void k_grid_count(const orbx_keypoint* __restrict__ kps, const int32_t* __restrict__ counts,
+                                                             int n_fixed, int capacity, orbx_grid g,
+                                                             int32_t* __restrict__ cell_start, int32_t* __restrict__ cell_idx) {
+    extern __shared__ int gcs[];
+    __shared__ int tmp[kProjThreads / 64 + 1];
+    const int set = blockIdx.x, tid = threadIdx.x, T = blockDim.x;
+    const int n = min(counts ? counts[set] : n_fixed, capacity);
+    const int ncell = g.cols * g.rows;
+    const orbx_keypoint* K = kps + (size_t)set * capacity;
+    int32_t* cs = cell_start + (size_t)set * (ncell + 1);
+    int32_t* ci = cell_idx + (size_t)set * capacity;
+    int* cnt = gcs;
+    uint16_t* cof = reinterpret_cast<uint16_t*>(cnt + ncell + 1);
+    uint16_t* idx = cof + capacity;
+    for (int c = tid; c <= ncell; c += T) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += T) {
+        const int c = grid_cell(g, K[i].x, K[i].y);
+        cof[i] = (uint16_t)(c < 0 ? 0xffff : c);
+        if (c >= 0) atomicAdd(&cnt[c], 1);
+    }
+    __syncthreads();
+    block_scan_array(cnt, ncell + 1, tmp);               // cnt[c] = start of cell c; cnt[ncell] = valid keypoints
+    for (int c = tid; c <= ncell; c += T) cs[c] = cnt[c];
+    __syncthreads();
+    for (int i = tid; i < n; i += T) {
+        const int c = cof[i];
+        if (c != 0xffff) idx[atomicAdd(&cnt[c], 1)] = (uint16_t)i;
+    }
+    __syncthreads();
+    for (int c = tid; c < ncell; c += T) {               // cell c: [end of cell c - 1, cnt[c])
+        const int b = c ? cnt[c - 1] : 0, e = cnt[c];
+        for (int j = b + 1; j < e; ++j) {
+            const uint16_t v = idx[j];
+            int k = j - 1;
+            while (k >= b && idx[k] > v) { idx[k + 1] = idx[k]; --k; }
+            idx[k + 1] = v;
+        }
+    }
+    __syncthreads();
+    const int total = ncell ? cnt[ncell - 1] : 0;
+    for (int j = tid; j < total; j += T) ci[j] = idx[j];
+}
+
 __device__ __forceinline__ int proj_rot_bin(float a1, float a2) {   // e.g. src/ORBmatcher.cc:1435-1440
     float rot = __fsub_rn(a1, a2);
     if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
@@ -876,6 +926,34 @@ int orbx_proj_project(orbx_matcher* m, int mode, const orbx_map_point* points, i
     return ORBX_OK;
 }
 
+}  // extern "C"
+
+// k_grid_count when its LDS (cell counts + two u16 arrays) fits and cells and indices fit in u16, else k_grid_build
+static void launch_grid_build(const orbx_grid& grid, const orbx_keypoint* d_kps, const int32_t* d_counts, int n_fixed,
+                              int capacity, int batch, int32_t* d_cs, int32_t* d_ci, hipStream_t s) {
+    const size_t ncell = (size_t)grid.cols * grid.rows;
+    const size_t lds_c = ((ncell + 1) * 4 + 4 * (size_t)capacity + 15) & ~(size_t)15;
+    static const bool counting = !std::getenv("ORBX_GRID_BITONIC");          // diagnostics: the bitonic form
+    if (counting && ncell < 0xffff && capacity < 0xffff && lds_c <= 64 * 1024) {
+        static const int threads = [] {                                       // ORBX_GRID_THREADS (diagnostics)
+            const char* v = std::getenv("ORBX_GRID_THREADS");
+            const int t = v ? std::atoi(v) : kProjThreads;
+            return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
+        }();
+        // r4at/r4au: 11 us against the bitonic form's 29 us per launch at least (the tracking frames' grids, 256 sets);
+        // in the step the two are even (3.59-3.64 ms), 256 threads slower (3.66)
+        hipLaunchKernelGGL(k_grid_count, dim3(batch), dim3(threads), lds_c, s, d_kps, d_counts, n_fixed, capacity, grid,
+                           d_cs, d_ci);
+        return;
+    }
+    int p2 = 1;
+    while (p2 < capacity) p2 <<= 1;
+    hipLaunchKernelGGL(k_grid_build, dim3(batch), dim3(kProjThreads), (size_t)p2 * 4, s, d_kps, d_counts, n_fixed, capacity,
+                       grid, d_cs, d_ci);
+}
+
+extern "C" {
+
 int orbx_grid_build_device(orbx_matcher* m, orbx_grid grid, const orbx_keypoint* d_kps, const int32_t* d_counts, int batch,
                            int capacity, int32_t* d_cell_start, int32_t* d_cell_idx, void* stream) {
     ORBX_REQUIRE(m && d_kps && d_counts && d_cell_start && d_cell_idx && batch >= 0 && capacity > 0, ORBX_ERR_ARG,
@@ -885,10 +963,7 @@ int orbx_grid_build_device(orbx_matcher* m, orbx_grid grid, const orbx_keypoint*
     ORBX_REQUIRE(capacity <= kGridMaxKps, ORBX_ERR_UNSUPPORTED, "capacity %d > %d", capacity, kGridMaxKps);
     if (batch == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(matcher_device(m)));
-    int p2 = 1;
-    while (p2 < capacity) p2 <<= 1;
-    hipLaunchKernelGGL(k_grid_build, dim3(batch), dim3(kProjThreads), (size_t)p2 * 4, (hipStream_t)stream, d_kps, d_counts, 0,
-                       capacity, grid, d_cell_start, d_cell_idx);
+    launch_grid_build(grid, d_kps, d_counts, 0, capacity, batch, d_cell_start, d_cell_idx, (hipStream_t)stream);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }
@@ -1001,10 +1076,7 @@ int orbx_proj_search(orbx_matcher* m, const orbx_proj_params* params, orbx_grid 
     pb.cell_start = dcs; pb.cell_idx = dci;
     pb.q_idx = dqi; pb.q_dist = dqdist; pb.owner = down; pb.nmatches = dnm;
     ORBX_HIP(hipMemcpyAsync(dpb, &pb, sizeof(pb), hipMemcpyHostToDevice, s));
-    int p2 = 1;
-    while (p2 < n) p2 <<= 1;
-    hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(kProjThreads), (size_t)p2 * 4, s, dk, (const int32_t*)nullptr, n,
-                       std::max(n, 1), grid, dcs, dci);
+    launch_grid_build(grid, dk, nullptr, n, std::max(n, 1), 1, dcs, dci, s);
     ORBX_HIP(hipGetLastError());
     if ((st = orbx_proj_search_batch_device(m, params, grid, dpb, 1, n, nq, s))) return st;
     int nm = 0;

@@ -82,6 +82,37 @@ def test_proj_search_empty(gpu):
     assert got[0] == 0 and (got[1] == -1).all()
 
 
+def test_grid_build_clustered_and_empty(gpu):
+    """The grid's CSR arrays (cell starts, indices ascending inside a cell) when keypoints pile into a few cells (the
+    counting kernel's per-cell ordering at its longest), when some fall outside the grid, and for an empty set."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    m = pkg.ORBmatcher(0.8, True)
+    grid = make_case(7, MODES["mappoints"])["grid"]
+    rng = np.random.default_rng(11)
+    cap = 2100
+    sets = []
+    k = np.zeros(cap, pkg.KP_DTYPE)                      # 2100 keypoints in 3 cells
+    k["x"] = rng.choice([100.5, 101.0, 300.25], cap).astype(np.float32)
+    k["y"] = rng.choice([50.0, 50.5, 200.75], cap).astype(np.float32)
+    sets.append(k)
+    k = np.zeros(cap, pkg.KP_DTYPE)                      # uniform, a tenth outside the image bounds
+    k["x"] = rng.uniform(-60, 700, cap).astype(np.float32)
+    k["y"] = rng.uniform(-40, 520, cap).astype(np.float32)
+    sets.append(k)
+    sets.append(np.zeros(cap, pkg.KP_DTYPE))            # counted as 0
+    kps = torch.from_numpy(np.stack([s_.view(np.uint8).reshape(cap, 28) for s_ in sets])).cuda()
+    counts = torch.tensor([cap, cap - 37, 0], dtype=torch.int32, device="cuda")
+    cs, ci = m.grid_build_device(grid, kps, counts)
+    torch.cuda.synchronize()
+    for i, (s_, n) in enumerate(zip(sets, [cap, cap - 37, 0])):
+        rcs, rci = O.grid_assign(s_[:n], grid)
+        assert np.array_equal(cs[i].cpu().numpy(), rcs)
+        assert np.array_equal(ci[i, :rcs[-1]].cpu().numpy(), rci)
+
+
 def test_grid_build_and_batched_search_device(gpu):
     """orbx_grid_build_device + orbx_proj_search_batch_device over several (query set, view) problems."""
     import torch
