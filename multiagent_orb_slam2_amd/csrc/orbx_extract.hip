@@ -1563,6 +1563,31 @@ __device__ __forceinline__ int group_sum(int v, int sub) {
     return r0 + r1 + r2 + r3;
 }
 
+// Disc masks of the IC box chunks for 32 lanes per keypoint (the shipped kKpw = 2): chunk q = lane + 32 k covers row
+// q / 4 - kHalfPatch, columns 8 (q % 4) - kHalfPatch .. +7; byte b is inside the disc iff |u| <= umax[|v|]
+// (ORBextractor.cc:84-99).  Built at compile time from kUmax: the per-lane bounds, shifts and 64-bit masks are then one
+// constant load per chunk instead of ~20 VALU.
+struct IcMaskTab { unsigned long long m[4][32]; };
+constexpr IcMaskTab make_ic_masks() {
+    IcMaskTab t{};
+    for (int k = 0; k < 4; ++k)
+        for (int lk = 0; lk < 32; ++lk) {
+            const int q = lk + 32 * k;
+            unsigned long long m = 0;
+            if (q < 4 * (2 * kHalfPatch + 1)) {
+                const int v = (q >> 2) - kHalfPatch, av = v < 0 ? -v : v;
+                const int um = kUmax[av > 15 ? 15 : av], u0 = 8 * (q & 3) - kHalfPatch;
+                for (int b = 0; b < 8; ++b) {
+                    const int u = u0 + b;
+                    if (u >= -um && u <= um) m |= 0xffull << (8 * b);
+                }
+            }
+            t.m[k][lk] = m;
+        }
+    return t;
+}
+__constant__ IcMaskTab c_ic_mask = make_ic_masks();
+
 // IC angle + steered BRIEF + output assembly, kKpw keypoints per wave (kLp = 64 / kKpw lanes each; the shipped form is
 // 2 -- one keypoint per wave measured 449 vs 444 us serial, 4 no faster): the wave-uniform part of a keypoint (level
 // lookup, moment reductions, fastAtan2, the double sin/cos, the keypoint record) is paid once per kKpw keypoints,
@@ -1657,11 +1682,15 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
         for (int k = 0; k < kNI; ++k) {
             const int q = lk + kLp * k;
             const int v = (q >> 2) - kHalfPatch, av = v < 0 ? -v : v;
-            const int um = kUmax[av > 15 ? 15 : av];
             const int u0 = 8 * (q & 3) - kHalfPatch;
-            const int lo = max(0, -um - u0), hi = min(7, um - u0);
             uint64_t m = 0;
-            if (valid && q < kIcItems && lo <= hi) m = (hi >= 7 ? ~0ull : ((1ull << (8 * hi + 8)) - 1ull)) & (~0ull << (8 * lo));
+            if constexpr (kLp == 32) {
+                m = valid ? c_ic_mask.m[k][lk] : 0ull;
+            } else {
+                const int um = kUmax[av > 15 ? 15 : av];
+                const int lo = max(0, -um - u0), hi = min(7, um - u0);
+                if (valid && q < kIcItems && lo <= hi) m = (hi >= 7 ? ~0ull : ((1ull << (8 * hi + 8)) - 1ull)) & (~0ull << (8 * lo));
+            }
             const uint64_t px = ic[k] & m;
             const uint32_t a = (uint32_t)px, b = (uint32_t)(px >> 32);
             const uint32_t wa = (uint32_t)(u0 + 16) * 0x01010101u + 0x03020100u, wb = wa + 0x04040404u;
