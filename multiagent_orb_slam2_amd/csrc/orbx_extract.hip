@@ -1627,9 +1627,8 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
     const int sub = ln / kLp, lk = ln - sub * kLp;
     const int rel = wrel * kKpw + sub;
     const int slot = slot0 + rel;
-    int lvl = 0;
-#pragma unroll
-    for (int l = 1; l < kMaxLevels; ++l) lvl += (l < nlevels && slot >= tab.out_off[l]) ? 1 : 0;
+    int lvl = 0;                                                 // a uniform loop over the levels in use (the unrolled
+    for (int l = 1; l < nlevels; ++l) lvl += slot >= tab.out_off[l] ? 1 : 0;   // kMaxLevels form was 62 VALU)
     const int* lcs = level_cnt + img * nlevels;
     int off = 0, total = 0;
     for (int l = 0; l < nlevels; ++l) {
