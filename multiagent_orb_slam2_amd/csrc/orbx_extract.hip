@@ -780,7 +780,7 @@ __device__ __forceinline__ int refl101(int i, int n) {
 // Per input row a lane issues one 12-byte load (x0-4 .. x0+7; global loads need no alignment on gfx950);
 // a horizontal row sum is at most 255 * 257 = 65535, exact in u16.  The 4 output bytes leave as one dword store.
 #ifndef ORBX_BLUR_BAND
-#define ORBX_BLUR_BAND 16     // rows per wave (r2y A/B: 16 ≈ +0.6 % over 32; 8 and 64 slower)
+#define ORBX_BLUR_BAND 32     // rows per wave (r4ax/r4ay with scalar tiles at 6 waves per SIMD: step 3.53-3.56 ms at 16, 3.49-3.50 at 24, 3.48 at 32, 3.49 at 48)
 #endif
 constexpr int kBlurBand = ORBX_BLUR_BAND, kBlurStrip = 256;
 
