@@ -1840,6 +1840,7 @@ struct Extractor {
     // Serial by default: two extractors called from two threads (Frame.cc:78-81) then use one hardware queue each
     // instead of sharing the process's 4 among four streams (r4haf: 0.370 -> 0.297 ms per stereo frame, median)
     bool host_serial = true;
+    bool host_merged = true;      // ORBX_HOST_MERGED=0: serial host calls keep the level-0 / levels >= 1 launch split
     bool async_pending = false;   // a device-API call may still run: the next replay first waits for every describe
     uint8_t* hg_pyr = nullptr;    // the pyramid set the graph's kernels write
     void drop_graph() {
@@ -1867,8 +1868,11 @@ struct Extractor {
     // k_fast_wave: one wave per (cell, image), 4 waves per workgroup; launch 0 = level 0, launch 1 = levels >= 1, each
     // wave's LDS slice sized for its launch's largest cell
     struct WaveLaunch { int cell0, n, ps, pc, kcap; WaveLds lay; };   // ps / pc: pair-image row stride / pad (fastw_row)
-    WaveLaunch wave_launch[2] = {};
-    static constexpr int kWaveWpg = 4;   // (1 or 2 waves per workgroup: faster alone, slower in the step)
+    WaveLaunch wave_launch[3] = {};   // level 0, levels 1..n-1, all levels (the host API's one-launch-per-stage form)
+#ifndef ORBX_FAST_WPG
+#define ORBX_FAST_WPG 4
+#endif
+    static constexpr int kWaveWpg = ORBX_FAST_WPG;   // (1 or 2 waves per workgroup: faster alone, slower in the step)
     int wave_twopass = 1;     // iniTh first, minTh only for the cells left empty (0: one pass at min(iniTh, minTh))
     std::vector<int> tile_off;   // blur tiles of level l: [tile_off[l], tile_off[l + 1])
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
@@ -2110,10 +2114,10 @@ int Extractor::configure(int r, int c, int batch) {
     // largest cell.  Cells up to 38 px wide (every cell of the KITTI and EuRoC grids) use the padded 19-dword rows
     // (fastw_row: bank-conflict-free pre-test, 20 dwords per row on average against 24 before); wider ones 40-dword
     // rows, 16-byte aligned.
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 3; ++k) {
         WaveLaunch& wl = wave_launch[k];
-        wl.cell0 = k == 0 ? 0 : lv[0].cell_end;
-        wl.n = k == 0 ? lv[0].cell_end : (int)cellv.size() - lv[0].cell_end;
+        wl.cell0 = k == 1 ? lv[0].cell_end : 0;
+        wl.n = k == 0 ? lv[0].cell_end : k == 1 ? (int)cellv.size() - lv[0].cell_end : (int)cellv.size();
         int rows = 8, sw = 8, np = 1, kcap = 1, lr = 1, psn = 1;
         for (int i = wl.cell0; i < wl.cell0 + wl.n; ++i) {
             const CellDev& cd = cellv[i];
@@ -2310,7 +2314,7 @@ static size_t qt_lds_bytes(int cap, int scan_cap) {   // k_quadtree's layout (Qt
 
 static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t step, size_t istride,
                      orbx_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int capacity, hipStream_t s,
-                     hipStream_t so, bool pipelined) {
+                     hipStream_t so, bool pipelined, bool merged = false) {
     const int nl = e->nlevels;
     const size_t ps = e->pyr_size;
     Extractor::EventSet* es = nullptr;
@@ -2393,6 +2397,21 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         return ORBX_OK;
     };
     if (side == s) { int st = resize_chain(); if (st) return st; }  // serial: every stage contiguous on one stream
+    if (merged && side == s) {
+        // one launch per stage over every level (the host API's one-image calls, where the chain of dependent launches
+        // is the latency): FAST, DistributeOctTree, blur
+        mark(6);
+        fast(s, 2);
+        mark(7);
+        if (int st = after_prev_describe(s)) return st;
+        quadtree(s, 0, nl);
+        mark(8);
+        blur(s, toff[0], toff[nl] - toff[0]);
+        mark(9);
+        mark(10);
+        mark(2);
+        mark(3);
+    } else {
     // side stream, level 0 (reads only the caller's images)
     mark(6);
     fast(side, 0);
@@ -2416,6 +2435,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     if (int st = after_prev_describe(s)) return st;
     quadtree(s, 1, nl - 1);
     mark(3);
+    }
     // the descriptor stage on the output stream, once both streams are done; the next call's resize chain (launch
     // stream) runs beside it
     if (so != s) {
@@ -2543,6 +2563,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* tp = std::getenv("ORBX_FAST_TWOPASS")) e->wave_twopass = std::atoi(tp) != 0;
     if (const char* hg = std::getenv("ORBX_HOST_GRAPH")) e->host_graph = std::atoi(hg) != 0;
     if (const char* hs = std::getenv("ORBX_HOST_SERIAL")) e->host_serial = std::atoi(hs) != 0;
+    if (const char* hm = std::getenv("ORBX_HOST_MERGED")) e->host_merged = std::atoi(hm) != 0;
     if (const char* sw = std::getenv("ORBX_DEBUG_SKIP_DESC_WAIT")) e->dbg_skip_desc_wait = std::atoi(sw) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
@@ -2715,7 +2736,7 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     // copy (a count-sized copy would need a second synchronisation; only the first n are read), the error word
     auto enqueue = [&]() -> int {
         int r = run_batch(e, e->d_in, 1, cols, nb, e->d_kps, e->d_desc, e->d_cnt, e->out_capacity, s, s,
-                          e->pipeline && !e->host_serial);
+                          e->pipeline && !e->host_serial, e->host_serial && e->host_merged);
         if (r) return r;
         ORBX_HIP(hipMemcpyAsync(e->h_out, e->d_hblk, ob, hipMemcpyDeviceToHost, s));
         ORBX_HIP(hipMemcpyAsync(h_cnt + 1, e->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
