@@ -718,12 +718,16 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
                 }
             }
         } else {
-            // padded rows (4-byte aligned, exactly kPS words for the widest ROI): 8-byte chunks, four ds_write_b32 per
-            // chunk, words past the ROI's (W + 1) / 2 not written (they belong to the next row)
-            const int cpr = (W + 7) >> 3, NQ = H * cpr, nw = (W + 1) >> 1;
+            // padded rows (4-byte aligned, exactly kPS = 19 words for the widest ROI, 38 columns): 8-byte chunks, four
+            // ds_write_b32 per chunk without a per-word test.  Only word 3 of a row's last chunk can fall past the row:
+            // on the next row's word 0 (or the pad after every fourth row, or after the last row on the score map, which
+            // is cleared after the staging).  It is stored first, behind a compiler barrier, so that the next row's own
+            // word 0 -- item q + 1, in the same round or a later one, never an earlier -- is written after it (one
+            // wave's LDS stores complete in issue order).
+            const int cpr = (W + 7) >> 3, NQ = H * cpr;
             const int dr = kWave / cpr, dc = kWave - dr * cpr;          // item q -> q + 64 (no division per item)
             int r = ln / cpr, cc = ln - r * cpr;
-            constexpr int kPf = 6;
+            constexpr int kPf = 4;                                      // 256 items: a 40 x 48 ROI in one round
             for (int q0 = 0; q0 < NQ; q0 += kPf * kWave) {
                 uint32_t pf[2 * kPf];
                 int rs[kPf], cs[kPf];
@@ -747,11 +751,12 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
                             lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
                         }
                         uint32_t* dst = E + fastw_row<kPS, kPC>(rs[k]) + 4 * cs[k];
-                        const int w0 = 4 * cs[k];
+                        dst[3] = __builtin_amdgcn_perm(hi, lo, 0x0c070c06u) | 0x64006400u;
+                        asm volatile("" ::: "memory");
+                        dst[2] = __builtin_amdgcn_perm(hi, lo, 0x0c050c04u) | 0x64006400u;
+                        dst[1] = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u) | 0x64006400u;
                         dst[0] = __builtin_amdgcn_perm(hi, lo, 0x0c010c00u) | 0x64006400u;
-                        if (w0 + 1 < nw) dst[1] = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u) | 0x64006400u;
-                        if (w0 + 2 < nw) dst[2] = __builtin_amdgcn_perm(hi, lo, 0x0c050c04u) | 0x64006400u;
-                        if (w0 + 3 < nw) dst[3] = __builtin_amdgcn_perm(hi, lo, 0x0c070c06u) | 0x64006400u;
+                        asm volatile("" ::: "memory");
                     }
                 }
         }
