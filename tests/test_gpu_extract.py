@@ -231,3 +231,25 @@ def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
             kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
             assert np.array_equal(kb, ref["kps"]) and np.array_equal(desc[i, :n], ref["desc"]), _diff_report(
                 kb, desc[i, :n], ref["kps"], ref["desc"])
+
+
+@pytest.mark.parametrize("form", ["default", "unmerged", "forked", "no_graph"])
+def test_host_api_schedules(gpu, monkeypatch, form):
+    """orbx_extract (host image in, host keypoints out) on each of its schedules: the default (a hipGraph replay, every
+    stage on the extractor's stream, FAST / quadtree / blur one launch over all levels), the per-level launch split
+    (ORBX_HOST_MERGED=0), the level-0 branch forked onto the side stream (ORBX_HOST_SERIAL=0) and plain stream
+    operations every call (ORBX_HOST_GRAPH=0): bit-exact against the oracle over repeated calls of two sizes, including
+    a capture per size and replays."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    env = {"unmerged": ("ORBX_HOST_MERGED", "0"), "forked": ("ORBX_HOST_SERIAL", "0"),
+           "no_graph": ("ORBX_HOST_GRAPH", "0")}.get(form)
+    if env:
+        monkeypatch.setenv(*env)
+    ex = pkg.ORBextractor(1500, 1.2, 8, 20, 7, device=0)
+    for i, (rows, cols) in enumerate([(375, 1242), (375, 1242), (240, 320), (375, 1242), (240, 320)]):
+        img = S.kitti_like_image(700 + i, rows=rows, cols=cols)
+        k, d = ex(img)
+        ref = O.extract(img, nfeatures=1500)
+        assert np.array_equal(k, ref["kps"]) and np.array_equal(d, ref["desc"]), _diff_report(k, d, ref["kps"], ref["desc"])
+    ex.close()
