@@ -112,9 +112,92 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group: nccl (RCCL over xGMI, the measured path) or gloo (rehearsal: several ranks "
                          "sharing one GPU, packets staged through host memory)")
+    ap.add_argument("--exchange", default="torch", choices=["torch", "native"],
+                    help="N>1 keyframe all-gather in the step: torch (torch.distributed all_gather_into_tensor; RCCL under "
+                         "the nccl backend) or native (liborbx's orbx_exchange: its own RCCL communicator, the path a C++ "
+                         "MultiAgentServer without torch takes; nccl backend only)")
+    ap.add_argument("--xgmi-mb", default="0.17,2,16,64",
+                    help="N>1: per-rank payloads (MB) of the all-gather bandwidth sweep after the timed steps (empty = skip)")
     ap.add_argument("--sync-each", action="store_true",
                     help="diagnostics: synchronise after every timed step (host_enqueue_* = pure host cost, no back-pressure)")
     return ap.parse_args()
+
+
+def rank_env(base: dict, rank: int, world: int, port: int) -> dict:
+    """The environment torch.distributed.run gives rank `rank` of a one-node job of `world` ranks (one per GPU,
+    LOCAL_RANK = RANK), rendezvous on 127.0.0.1 (the container hostname may not resolve)."""
+    env = dict(base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", ROLE_RANK=str(rank), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               ORBX_LAUNCHER="bench.py --gpus")
+    return env
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(world: int, cmd: list, poll_s: float = 0.2, grace_s: float = 20.0) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh child processes (rank r on GPU r) before this process
+    makes any GPU call, rank 0's stdout passed through (its one JSON line), the other ranks' stdout sent to stderr so
+    that stdout holds that line only.  When a rank fails, the others are stopped (SIGTERM, then SIGKILL after
+    grace_s: a rank blocked in a collective whose peer died never returns).  Returns the first non-zero exit status
+    (or 0).  The children are started as subprocesses, never exec'd into this process."""
+    import signal
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(world):
+        procs.append(subprocess.Popen(cmd, env=rank_env(os.environ, r, world, port),
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+
+    def forward(pipe):
+        # rank 0's JSON line to stdout; anything else it prints there (gloo's "[Gloo] Rank 0 is connected ..." banner,
+        # library chatter) to stderr
+        for raw in iter(pipe.readline, b""):
+            line = raw.decode(errors="replace")
+            dst = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+            dst.write(line)
+            dst.flush()
+    fwd = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+    fwd.start()
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except OSError:
+                    pass
+
+    prev = {s: signal.getsignal(s) for s in (signal.SIGTERM, signal.SIGINT)}
+
+    def on_signal(signum, _frame):
+        stop_all(signal.SIGTERM)
+        raise SystemExit(128 + signum)
+    for s in prev:
+        signal.signal(s, on_signal)
+    rc, failed_at = 0, None
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad and rc == 0:
+                rc, failed_at = bad[0], time.monotonic()
+                stop_all(signal.SIGTERM)
+            if all(c is not None for c in codes):
+                break
+            if failed_at is not None and time.monotonic() - failed_at > grace_s:
+                stop_all(signal.SIGKILL)
+            time.sleep(poll_s)
+    finally:
+        for s, h in prev.items():
+            signal.signal(s, h)
+    fwd.join(timeout=10.0)
+    return rc
 
 
 def compulsory_bytes(cfg):
@@ -282,6 +365,7 @@ class CpuAgent:
 
     def tracking(self, a, ur, depth):
         """TrackWithMotionModel's search and SearchLocalPoints, as multiagent.FrameTracker."""
+        from multiagent_orb_slam2_amd import multiagent as MA
         from multiagent_orb_slam2_amd.orbx import PROJ_QUERY_DTYPE, QF_BLOCKS, QF_SKIP
         O, sc = self.O, self.tables["scale"]
         lf, mp, _ = self.modes
@@ -290,7 +374,7 @@ class CpuAgent:
         last["flags"][1::2] |= QF_SKIP                      # the last frame holds the even keypoints' MapPoints
         q1 = O.project(lf, last, self.v_lf, sc, self.log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
         _, qi1, _, own1 = O.proj_search(self.p_lf, self.grid, q1, a["desc"], a["kps"], a["desc"], uright=ur)
-        pts["flags"][qi1 >= 0] |= QF_SKIP
+        pts["flags"][MA.found_in_frame(qi1, own1)] |= QF_SKIP      # in mCurrentFrame.mvpMapPoints (Tracking.cc:1158-1174)
         q2 = O.project(mp, pts, self.v_mp, sc, self.log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
         O.proj_search(self.p_mp, self.grid, q2, a["desc"], a["kps"], a["desc"], uright=ur,
                       blocked=(own1 >= 0).astype(np.uint8))
@@ -706,23 +790,43 @@ def roofline_lines(per_call, cfg, units, config):
     if main_line is not None:
         main_line["selected_by"] = (f"largest share of GPU time in profiles/kernel_share.json ({tag})" if tag else
                                     "default (no kernel_share.json for this config)")
+        # the live figure: the union of the launches' HIP-event spans in the overlapped step, which includes each
+        # launch's wait for CU slots behind the other queues
+        main_line["achieved_live"] = main_line["achieved"]
+        main_line["frac_live"] = main_line["frac"]
+        main_line["frac_source"] = "live"
         if prof:
             k0 = prof[0]
+            grids = k0.get("grids", [])
             main_line["rocprof_busy_ms_per_step"] = k0.get("busy_ms_per_step")
             main_line["rocprof_launches_per_step"] = k0.get("launches_per_step")
-            main_line["rocprof_launch_avg_us"] = [g["avg_us"] for g in k0.get("grids", [])]
+            main_line["rocprof_launch_avg_us"] = [g["avg_us"] for g in grids]
+            # headline: the kernel's own duration = the profiled average duration of each of its launches per step
+            # (one launch per grid per step), summed; bytes per step / that time
+            dur_ms = sum(g["avg_us"] for g in grids) * 1e-3 if grids else k0.get("busy_ms_per_step")
+            if dur_ms and not stale:
+                ach = main_line["algorithmic_bytes_per_step"] / (dur_ms * 1e-3) / 1e9
+                main_line.update(achieved=round(ach, 3), frac=round(ach / HBM_PEAK_GBS, 6),
+                                 kernel_ms_per_step=round(dur_ms, 4), frac_source="rocprof launch durations")
             if k0.get("busy_ms_per_step"):
                 main_line["frac_rocprof"] = round(main_line["algorithmic_bytes_per_step"] /
                                                   (k0["busy_ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
             main_line["profile"] = f"profiles/kernel_share.json ({tag})"
             main_line["profile_stale"] = stale
+        pmc = load_profile("pmc_traffic.json")
+        if pmc and pmc.get("step_hbm_bytes") and pmc.get("batch_images") == units and pmc.get("config", "kitti") == config:
+            # every kernel of the step, not the dominant one only: what the whole step moves through HBM
+            main_line["traffic_step"] = pmc["step_hbm_bytes"]
+            main_line["traffic_step_kernels_ms"] = pmc.get("step_kernel_ms")
+            main_line["traffic_step_source"] = pmc.get("source")
     sec = line(kernel_family(desc_name), desc_name) if kernel_family(desc_name) != dom else None
     return main_line, sec
 
 
 def valu_line(roof, config, units):
     """VALU roofline of the same kernel: SQ_INSTS_VALU x 64 lane-ops per step from the committed SQ pass
-    (profiles/sq_summary.json), over the live time; dropped when the SQ profile was taken on other sources."""
+    (profiles/sq_summary.json), over the same kernel time as the HBM line (profiled launch durations when the profile
+    matches the sources, else the live spans); dropped when the SQ profile was taken on other sources."""
     sq = load_profile("sq_summary.json")
     if not (roof and sq and sq.get("config", "kitti") == config and sq.get("batch_images") == units):
         return None
@@ -739,11 +843,29 @@ def valu_line(roof, config, units):
             "frac": round(tops / VALU_PEAK_TOPS, 4), "kernel": roof["kernel"], "valu_lane_ops_per_step": ops,
             "profiled_valu_frac": {k: v.get("valu_frac") for k, v in ks},
             "source": f"SQ_INSTS_VALU x 64 per launch from profiles/sq_summary.json ({sq.get('tag')}, sources "
-                      f"{sq.get('source_sha16')}), time measured live"}
+                      f"{sq.get('source_sha16')}), over the roofline's kernel_ms_per_step ({roof.get('frac_source', 'live')})"}
+
+
+def world_from_env(gpus: int):
+    """(launch here?, world size) from --gpus and a launcher's WORLD_SIZE: without WORLD_SIZE, --gpus N > 1 means this
+    process starts the N ranks itself; with it, the two must agree (a torchrun of N ranks asked for M GPUs is an error,
+    not a silent 1-rank line)."""
+    env = os.environ.get("WORLD_SIZE")
+    if env is None:
+        return gpus > 1, 1
+    if int(env) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={env} from the launcher but --gpus {gpus}")
+    return False, int(env)
 
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    spawn, world = world_from_env(args.gpus)
+    if spawn:
+        # before anything touches the GPU: the children initialise it, one device each
+        sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     cfg = dict(CONFIGS[args.config])
     os.environ["ORBX_CU_EXCLUDE"] = str(max(args.cu_exclude, 0))   # the extractors' side streams (read at creation)
     ROWS, COLS, NFEAT, BF = cfg["rows"], cfg["cols"], cfg["nfeatures"], cfg["bf"]
@@ -755,19 +877,28 @@ def main():
     from multiagent_orb_slam2_amd import multiagent as MA
     from multiagent_orb_slam2_amd import synthetic as S
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_dev = torch.cuda.device_count()
     if world > 1:
-        local = local % max(1, torch.cuda.device_count())   # (rehearsal: more ranks than GPUs share them)
+        if n_dev < world and args.dist_backend == "nccl":
+            raise SystemExit(f"bench.py: {world} ranks over RCCL need {world} GPUs, {n_dev} visible "
+                             "(--dist-backend gloo rehearses the N>1 step with ranks sharing a GPU)")
+        if args.exchange == "native" and args.dist_backend != "nccl":
+            raise SystemExit("bench.py: --exchange native needs --dist-backend nccl (one GPU per rank)")
+        local = local % max(1, n_dev)                        # (gloo rehearsal: more ranks than GPUs share them)
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, expected {world}")
+        world = dist.get_world_size()
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    devices_used = min(world, max(1, n_dev))
 
     B = args.batch
     nd = max(1, min(args.distinct, B)) if args.distinct > 0 else B
@@ -826,7 +957,10 @@ def main():
     n_kf = max(1, B // KF_EVERY)
     voc = S.synthetic_vocabulary(2024, k=10, L=6)      # ORBvoc.txt's shape ("10 6 0 0"); the file is absent
     vocab = pkg.ORBVocabulary.from_arrays(voc, device=dev.index)
-    exchange = MA.KeyframeExchange(timed=not args.no_timing) if world > 1 else None
+    exchange = None
+    if world > 1:
+        exchange = (MA.NativeKeyframeExchange(timed=not args.no_timing, device=dev.index) if args.exchange == "native"
+                    else MA.KeyframeExchange(timed=not args.no_timing))
     engine = pkg.KeyframeFusionEngine(vocab, pkg.ORBmatcher(0.75, True, device=dev.index), cap,
                                       slots=STORE_STEPS * world * n_kf, max_keyframes=n_kf, candidates=KF_CANDIDATES,
                                       agent=rank, world=world, device=dev.index)
@@ -1044,8 +1178,9 @@ def main():
 
     frames = B * args.steps * world
     value = frames / el
-    collective = ("RCCL all-gather (torch.distributed nccl, xGMI)" if args.dist_backend == "nccl" else
-                  "gloo all-gather staged through host memory (rehearsal, not xGMI)")
+    collective = ("gloo all-gather staged through host memory (rehearsal, not xGMI)" if args.dist_backend == "gloo" else
+                  "RCCL all-gather (liborbx orbx_exchange: native communicator, xGMI)" if args.exchange == "native" else
+                  "RCCL all-gather (torch.distributed nccl, xGMI)")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True,
@@ -1082,7 +1217,12 @@ def main():
                    "input_sets": len(img_sets), "input_bytes_resident": int(sum(t.numel() for t in img_sets)),
                    "sequence_chunk": [chunk.start, chunk.stop],
                    "parallelism": f"agent-per-gpu x{world}"},
+        "ranks": {"world_size": world, "devices_used": devices_used, "backend": args.dist_backend if world > 1 else None,
+                  "launched_by": os.environ.get("ORBX_LAUNCHER", "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                                else "bench.py" if world > 1 else "single process")},
     }
+    if world > devices_used:
+        out["rehearsal"] = f"{world} ranks sharing {devices_used} GPU(s): not a scaling measurement"
 
     if not args.no_timing:
         st, calls = {}, 0
@@ -1117,6 +1257,16 @@ def main():
         if xs:
             out["exchange"] = dict(xs, collective=collective,
                                    packet_bytes=engine.packet_bytes, keyframes_per_rank=n_kf)
+        sizes = [float(s) for s in args.xgmi_mb.split(",") if s.strip()]
+        if sizes:
+            # after the timed region: the same collective alone, at the step's packet payload and larger ones
+            torch.cuda.synchronize()
+            with torch.cuda.stream(kf_stream):
+                sweep = MA.allgather_sweep(exchange, dev, sizes)
+            out["xgmi_allgather"] = {"collective": collective, "world_size": world, "sweep": sweep,
+                                     "link_peak_GBps_per_direction": 153.6 if args.dist_backend == "nccl" else None,
+                                     "note": "busbw = bytes each rank receives / time; xGMI is point-to-point (7 links "
+                                             "per MI355X), so a ring all-gather's busbw is bounded by one link"}
 
     if rank == 0 and world == 1 and args.c3:
         out["c3_bruteforce"] = c3_bench(pkg, dev)

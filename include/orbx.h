@@ -438,7 +438,8 @@ int orbx_compute_image_bounds(orbx_matcher* m, const float* K, const float* dist
 int orbx_grid_build_device(orbx_matcher* m, orbx_grid grid, const orbx_keypoint* d_kps, const int32_t* d_counts,
                            int batch, int capacity, int32_t* d_cell_start, int32_t* d_cell_idx, void* stream);
 /* The searches of n_problems problems (device array) in one launch; max_n / max_nq bound the target
- * keypoints / queries of any problem. */
+ * keypoints / queries of any problem (they size the launch's LDS plan).  A problem above either bound is not
+ * searched: its q_idx / q_dist are -1 and its *nmatches is -1. */
 int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
                                   const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq,
                                   void* stream);

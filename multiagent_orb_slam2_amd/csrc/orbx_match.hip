@@ -1306,10 +1306,10 @@ struct Matcher {
     size_t h_stage_bytes = 0;
     int stage_host(size_t bytes) {
         if (bytes <= h_stage_bytes) return ORBX_OK;
+        const size_t nb = std::max(bytes, h_stage_bytes * 2);     // geometric growth over the old size
         if (h_stage) (void)hipHostFree(h_stage);
         h_stage = nullptr;
         h_stage_bytes = 0;
-        const size_t nb = std::max(bytes, h_stage_bytes * 2);
         ORBX_HIP(hipHostMalloc((void**)&h_stage, nb, hipHostMallocDefault));
         h_stage_bytes = nb;
         return ORBX_OK;

@@ -291,6 +291,15 @@ __device__ int proj_walk(const orbx_proj_params& P, const float* isg, const orbx
     return nrec > kcap ? (int)kQmOverflow : nrec;
 }
 
+// A problem larger than the launch's LDS plan (max_n / max_nq of orbx_proj_search_batch_device) is not searched:
+// its q_idx / q_dist are -1 and *nmatches = -1, never an LDS overrun.  Workgroup-uniform (one problem per workgroup).
+__device__ __forceinline__ bool proj_over_cap(const orbx_proj_problem& pb, int n_cap, int nq_cap, int tid, int T) {
+    if (pb.n <= n_cap && pb.nq <= nq_cap) return false;
+    for (int q = tid; q < pb.nq; q += T) { pb.q_idx[q] = -1; pb.q_dist[q] = -1; }
+    if (tid == 0 && pb.nmatches) *pb.nmatches = -1;
+    return true;
+}
+
 // Modes MAPPOINTS .. BEST.  Dynamic LDS: [kLds: cell starts (ncell + 1), entries (16 B x n)] then, for the assigning
 // modes, claim[n], own[n], res[nq] (idx | dist << 13, or -1), qm[nq] (kQm* byte) and the lists (kcap x nq).
 template <bool kLds, bool kAssign>
@@ -303,6 +312,7 @@ __global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(o
                                                        // would be a vector load from the argument buffer per candidate)
     const orbx_proj_problem pb = probs[blockIdx.x];
     const int tid = threadIdx.x, T = blockDim.x, nq = pb.nq, n = pb.n;
+    if (proj_over_cap(pb, n_cap, nq_cap, tid, T)) return;
     if (tid < 32) isg[tid] = P.inv_sigma2[tid];
     const int ncell = g.cols * g.rows;
     char* lp = reinterpret_cast<char*>(psm);
@@ -455,11 +465,13 @@ __global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(o
 // m21[n] (vMatchedDistance / vnMatches21 of :417-418) and res[nq] (vnMatches12).
 constexpr int kInitNone = 1023;   // "INT_MAX" distance inside the packed (distance << 20 | position) key
 
-__global__ __launch_bounds__(64) void k_proj_init(orbx_proj_params P, orbx_grid g, const orbx_proj_problem* __restrict__ probs) {
+__global__ __launch_bounds__(64) void k_proj_init(orbx_proj_params P, orbx_grid g, const orbx_proj_problem* __restrict__ probs,
+                                                  int n_cap, int nq_cap) {
     extern __shared__ int ism[];
     __shared__ int hist[32];
     const orbx_proj_problem pb = probs[blockIdx.x];
     const int ln = lane_id(), nq = pb.nq, n = pb.n;
+    if (proj_over_cap(pb, n_cap, nq_cap, ln, kWave)) return;
     int* mdist = ism;
     int* m21 = ism + n;
     int* res = ism + 2 * n;
@@ -567,9 +579,19 @@ __global__ __launch_bounds__(64) void k_proj_init(orbx_proj_params P, orbx_grid 
 // ---------------------------------------------------------------------------------------------
 // Projection step (include/orbx.h orbx_proj_project): one thread per MapPoint, the reference's operation order for
 // each caller, pinned as the oracle (oracle/proj_oracle.cpp orc_project): Rcw * X + tcw as float products summed left
-// to right, cv::norm / Mat::dot with float products accumulated in double, PredictScale's log in double.
+// to right (OpenCV's 3x3 gemm fast path), cv::norm / Mat::dot of a 3-vector with double products accumulated left to
+// right in double (OpenCV 3.2 normL2Sqr<float, double> / dotProd_), PredictScale's log in double.
 // ---------------------------------------------------------------------------------------------
 struct ProjScales { float s[32]; };
+
+__device__ __forceinline__ double norm2_d(float x, float y, float z) {          // ((0 + x*x) + y*y) + z*z in double
+    const double a = x, b = y, c = z;
+    return __dadd_rn(__dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b)), __dmul_rn(c, c));
+}
+__device__ __forceinline__ double dot3_d(float x, float y, float z, float u, float v, float w) {
+    return __dadd_rn(__dadd_rn(__dmul_rn((double)x, (double)u), __dmul_rn((double)y, (double)v)),
+                     __dmul_rn((double)z, (double)w));
+}
 
 __device__ __forceinline__ int predict_scale(float max_dist, float dist, float log_sf, int nlevels) {   // MapPoint.cc:389-421
     const float ratio = __fdiv_rn(max_dist, dist);
@@ -636,11 +658,9 @@ __global__ __launch_bounds__(256) void k_project(int mode, const orbx_map_point*
         }
         const float maxD = __fmul_rn(1.2f, p.max_dist), minD = __fmul_rn(0.8f, p.min_dist);  // MapPoint.cc:377-387
         const float POx = __fsub_rn(p.x, V.Ow[0]), POy = __fsub_rn(p.y, V.Ow[1]), POz = __fsub_rn(p.z, V.Ow[2]);
-        const float ss = __fadd_rn(__fadd_rn(__fmul_rn(POx, POx), __fmul_rn(POy, POy)), __fmul_rn(POz, POz));
-        const float dist = (float)__dsqrt_rn((double)ss);                                 // cv::norm
+        const float dist = (float)__dsqrt_rn(norm2_d(POx, POy, POz));                   // cv::norm
         if (dist < minD || dist > maxD) { *o = q; return; }
-        const double dot = __dadd_rn(__dadd_rn((double)__fmul_rn(POx, p.nx), (double)__fmul_rn(POy, p.ny)),
-                                     (double)__fmul_rn(POz, p.nz));                          // PO.dot(Pn)
+        const double dot = dot3_d(POx, POy, POz, p.nx, p.ny, p.nz);                         // PO.dot(Pn)
         const int pred = predict_scale(p.max_dist, dist, log_sf, nlevels);
         if (mode == ORBX_PROJ_MAPPOINTS) {
             const float viewCos = (float)__ddiv_rn(dot, (double)dist);                       // Frame.cc:308-311
@@ -665,7 +685,7 @@ __global__ __launch_bounds__(256) void k_project(int mode, const orbx_map_point*
 
 // MapPoints of stereo frames: Frame::UnprojectStereo (src/Frame.cc:666-680) and the Frame form of the MapPoint
 // constructor (src/MapPoint.cc:47-68).  One thread per keypoint.  Pinned as the projection: Rwc * x3Dc + Ow as float
-// products summed left to right; cv::norm with a float sum of squares and a double sqrt; the normal divided as
+// products summed left to right; cv::norm with double squares summed in double and a double sqrt; the normal divided as
 // cv::Mat / double (the scale 1 / norm rounded to float, then a float product per component).
 __global__ __launch_bounds__(256) void k_stereo_mappoints(const orbx_keypoint* __restrict__ kps, const float* __restrict__ depth,
                                                           const int32_t* __restrict__ counts, int capacity,
@@ -691,7 +711,7 @@ __global__ __launch_bounds__(256) void k_stereo_mappoints(const orbx_keypoint* _
         };
         p.x = row(0); p.y = row(1); p.z = row(2);
         const float dx = __fsub_rn(p.x, T[9]), dy = __fsub_rn(p.y, T[10]), dz = __fsub_rn(p.z, T[11]);
-        const double nrm = __dsqrt_rn((double)__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+        const double nrm = __dsqrt_rn(norm2_d(dx, dy, dz));                                   // cv::norm
         const float inv = (float)__ddiv_rn(1.0, nrm);
         p.nx = __fmul_rn(dx, inv); p.ny = __fmul_rn(dy, inv); p.nz = __fmul_rn(dz, inv);
         const float dist = (float)nrm;
@@ -985,7 +1005,8 @@ int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* param
                      max_nq);
         if (lds > 64 * 1024)
             ORBX_HIP(hipFuncSetAttribute((const void*)k_proj_init, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k_proj_init, dim3(n_problems), dim3(64), lds, s, P, grid, d_problems);
+        hipLaunchKernelGGL(k_proj_init, dim3(n_problems), dim3(64), lds, s, P, grid, d_problems, std::max(max_n, 1),
+                           std::max(max_nq, 1));
     } else {
         // LDS plan (k_proj_search): staged cells + entries when they fit, then the assigning modes' claim / own / res /
         // qm arrays and as many list slots per query (<= kProjListMax) as the rest of the 160 KiB holds

@@ -16,6 +16,7 @@ agents.
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from dataclasses import dataclass
 
 import numpy as np
@@ -208,6 +209,73 @@ class KeyframeExchange:
         return {"calls": len(us), "us_per_allgather": round(mean_us, 2), "us_min": round(float(np.min(us)), 2),
                 "bytes_per_allgather": int(nbytes), "bytes_received_per_rank": int(recv),
                 "recv_GBps": round(recv / (mean_us * 1e-6) / 1e9, 3) if mean_us > 0 else None}
+
+
+class NativeKeyframeExchange(KeyframeExchange):
+    """The same all-gather through liborbx's own RCCL communicator (orbx_exchange, KeyframeExchangeRCCL): what a C++
+    MultiAgentServer without torch would call.  The communicator's unique id is made on rank 0 and handed to the others
+    over the torch process group (broadcast_object_list), then every call is stream-ordered on the current stream."""
+
+    def __init__(self, group=None, timed: bool = False, device: int = 0):
+        super().__init__(group, timed)
+        from .orbx import KeyframeExchangeRCCL
+        uid = [KeyframeExchangeRCCL.unique_id() if self.rank == 0 else None]
+        self.dist.broadcast_object_list(uid, src=0, group=group)
+        self.x = KeyframeExchangeRCCL(uid[0], self.world, self.rank, device)
+
+    def exchange(self, packets, out=None):
+        import torch
+        n, P = packets.shape
+        if out is None:
+            out = torch.empty((self.world * n, P), dtype=torch.uint8, device=packets.device)
+        stream = torch.cuda.current_stream(packets.device)
+        ev = None
+        if self.timed:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(stream)
+        self.x.allgather(packets.contiguous(), out, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+            self._events.append((ev, out.numel()))
+        self.bytes_moved += out.numel()
+        self.calls += 1
+        return out
+
+    def close(self):
+        self.x.close()
+
+
+def allgather_sweep(exchange: KeyframeExchange, device, sizes_mb, reps: int = 10, warmup: int = 3):
+    """All-gather bandwidth over the exchange's collective at several per-rank payloads: mean microseconds per call
+    (HIP events on the current stream), the bytes each rank receives ((world-1) x payload) per second, and the
+    ring-algorithm bus bandwidth (payload x (world-1) / time = the bytes each rank receives per second), the algorithm
+    bandwidth (world x payload / time) beside it; data_ok checks every rank's block arrived."""
+    import torch
+    out = []
+    w = exchange.world
+    for mb in sizes_mb:
+        nbytes = max(16, int(mb * 1e6) // 16 * 16)
+        send = torch.full((1, nbytes), exchange.rank & 0xFF, dtype=torch.uint8, device=device)
+        recv = torch.empty((w, nbytes), dtype=torch.uint8, device=device)
+        for _ in range(warmup):
+            exchange.exchange(send, out=recv)
+        s = torch.cuda.current_stream(device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        saved = exchange.timed
+        exchange.timed = False
+        e0.record(s)
+        for _ in range(reps):
+            exchange.exchange(send, out=recv)
+        e1.record(s)
+        e1.synchronize()
+        exchange.timed = saved
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        ok = bool(all(int(recv[r, 0].item()) == (r & 0xFF) and int(recv[r, -1].item()) == (r & 0xFF) for r in range(w)))
+        recv_b = nbytes * (w - 1)
+        out.append({"bytes_per_rank": nbytes, "us_per_allgather": round(us, 2),
+                    "algbw_GBps": round(w * nbytes / (us * 1e-6) / 1e9, 2),
+                    "busbw_GBps": round(recv_b / (us * 1e-6) / 1e9, 2), "data_ok": ok})
+    return out
 
 
 class MapFusionStore:
@@ -619,6 +687,7 @@ class FrameTracker:
         # the last frame holds the MapPoints of every second keypoint (its tracked points); the local map holds all of
         # them, so SearchLocalPoints has the other half plus the motion-model misses to find (found >= 0: skipped)
         self.lf_skip = torch.tensor([-1, 0], dtype=torch.int32).repeat(B, (cap + 1) // 2)[:, :cap].contiguous().to(dev)
+        self.q_ar = torch.arange(cap, dtype=torch.int32, device=dev).view(1, cap).expand(B, cap)
         self.sets = []
         for _ in range(n_sets):
             z = dict(pts=torch.empty((B, cap, 48), dtype=torch.uint8, device=dev),
@@ -631,7 +700,7 @@ class FrameTracker:
                      blk=torch.empty((B, cap), dtype=torch.bool, device=dev))
             for k in ("qi1", "qd1", "qi2", "qd2"):
                 z[k] = torch.empty((B, cap), dtype=torch.int32, device=dev)
-            for k in ("own1", "own2"):
+            for k in ("own1", "own2", "fnd"):
                 z[k] = torch.empty((B, cap), dtype=torch.int32, device=dev)
             for k in ("nm1", "nm2"):
                 z[k] = torch.empty((B,), dtype=torch.int32, device=dev)
@@ -675,10 +744,26 @@ class FrameTracker:
         m.proj_search_batch_device(self.p_lf, self.grid, p1, cap, cap, stream=stream)
         with torch.cuda.stream(stream) if stream is not None else _nullcontext():
             torch.ge(z["own1"], 0, out=z["blk"])                    # keypoints that now hold a MapPoint
+            # SearchLocalPoints skips the MapPoints that are in mCurrentFrame.mvpMapPoints (Tracking.cc:1163-1177):
+            # query q's match stands only if the keypoint's owner is still q -- the rotation filter sets the entries
+            # it drops back to NULL (ORBmatcher.cc:1456-1466; owner -2), and those MapPoints are searched again
+            own_at = torch.gather(z["own1"], 1, z["qi1"].clamp(min=0).long())
+            z["fnd"].fill_(-1)
+            z["fnd"].masked_fill_((z["qi1"] >= 0) & (own_at == self.q_ar), 0)
         m.proj_project_device(PROJ_MAPPOINTS, z["pts"], counts, self.v_mp, self.scale, self.log_sf, out=z["q2"],
-                              found=z["qi1"], stream=stream)
+                              found=z["fnd"], stream=stream)
         m.proj_search_batch_device(self.p_mp, self.grid, p2, cap, cap, stream=stream)
         return z["qi1"], z["nm1"], z["qi2"], z["nm2"]
+
+
+def found_in_frame(q_idx, owner):
+    """Host form of FrameTracker's rule: MapPoint q is in the current frame after SearchByProjection(F, LastF) iff it
+    was assigned a keypoint (q_idx[q] >= 0) and that keypoint still holds it (owner[q_idx[q]] == q; the rotation
+    filter resets dropped entries, owner -2).  Returns the boolean mask over queries."""
+    q_idx = np.asarray(q_idx)
+    owner = np.asarray(owner)
+    at = owner[np.maximum(q_idx, 0)] if len(owner) else np.full(q_idx.shape, -1)
+    return (q_idx >= 0) & (at == np.arange(len(q_idx)))
 
 
 def _view_bytes(v):
@@ -753,7 +838,10 @@ class LocalFuse:
         self.views = torch.from_numpy(np.frombuffer(np.ascontiguousarray(views_slots).tobytes(), np.uint8)
                                       .reshape(slots, 112).copy()).to(dev)
         self.params = ProjParams.make(PROJ_FUSE, 50, 0.6, False, inv_sigma2)             # TH_LOW
-        self.cache = {}
+        # plans per (new slots, neighbours) pattern, least recently used evicted: the bench's ring repeats a few
+        # patterns, real covisibility would not (2 directions x P x cap x ~56 B of device buffers per plan)
+        self.cache = OrderedDict()
+        self.cache_max = 8
 
     def add_keyframes(self, slots: range, kps, desc, counts, uright, depth, rows, stream=None):
         """The new keyframes (rows of the extractor outputs) into the rings at 'slots' (a contiguous range)."""
@@ -775,7 +863,10 @@ class LocalFuse:
         import torch
         key = (tuple(new_slots), tuple(map(tuple, neighbours)))
         if key in self.cache:
+            self.cache.move_to_end(key)
             return self.cache[key]
+        while len(self.cache) >= self.cache_max:
+            self.cache.popitem(last=False)     # its tensors were record_stream'ed on the streams that used them
         n, nn = neighbours.shape
         P, cap, st = n * nn, self.cap, self.store
         ns = np.repeat(np.asarray(new_slots, np.int64), nn)
@@ -798,7 +889,10 @@ class LocalFuse:
                               nmatches=nm.data_ptr() + i * 4)
             views = self.views[torch.from_numpy(tgt).to(dev)].contiguous()
             vpts = torch.from_numpy(src.astype(np.int32)).to(dev)
-            out[d] = dict(q=q, qi=qi, nm=nm, probs=torch.from_numpy(t.view(np.uint8)).to(dev), views=views, vpts=vpts)
+            # every buffer the problem table points at stays referenced here (q_dist and owner too: a freed block would
+            # be handed to another tensor while the searches still write it)
+            out[d] = dict(q=q, qi=qi, qd=qd, own=own, nm=nm, probs=torch.from_numpy(t.view(np.uint8)).to(dev), views=views,
+                          vpts=vpts)
         self.cache[key] = out
         return out
 
@@ -813,5 +907,10 @@ class LocalFuse:
             self.m.proj_project_device(PROJ_FUSE, self.pts, self.cnt, p["views"], self.scale, self.log_sf, out=p["q"],
                                        view_points=p["vpts"], stream=stream)
             self.m.proj_search_batch_device(self.params, self.grid, p["probs"], self.cap, self.cap, stream=stream)
+            if stream is not None:
+                # the kernels read / write these through raw pointers on 'stream': an evicted plan's memory must not be
+                # handed out again before that stream's work is done
+                for t in p.values():
+                    t.record_stream(stream)
             res.append((p["qi"], p["nm"]))
         return res

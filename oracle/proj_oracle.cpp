@@ -92,7 +92,7 @@ enum { ORC_QF_SKIP = 1, ORC_QF_BLOCKS = 2 };
 // The projection step before the searches (include/orbx.h orbx_proj_project): one MapPoint -> one query, in the
 // reference's operation order for each caller.  float expressions evaluate as written (-ffp-contract=off); the
 // cv::Mat pieces are pinned as DESIGN §2 states: Rcw * X + tcw as float products summed left to right; cv::norm and
-// Mat::dot of 3-vectors as float products accumulated in double; PredictScale's log in double.
+// Mat::dot of 3-vectors as double products accumulated in double (orc_norm2); PredictScale's log in double.
 struct orc_map_point {
     float x, y, z, nx, ny, nz, min_dist, max_dist, angle;
     int32_t octave, flags, pad;
@@ -104,6 +104,17 @@ struct orc_view {
     float th, view_cos_limit;
     int32_t level_mode, pad;
 };
+
+// cv::norm(3x1 CV_32F) in OpenCV 3.2's generic path: normL2_32f -> normL2Sqr<float, double>: each element widened to
+// double, squared and summed left to right in double, then std::sqrt (stat.cpp).  Mat::dot likewise (dotProd_32f ->
+// dotProd_<float>: (double)a[i] * b[i] summed in double; the SSE block loop does not run for 3 elements).
+static double orc_norm2(float x, float y, float z) {
+    double s = 0.0;
+    s += (double)x * x;
+    s += (double)y * y;
+    s += (double)z * z;
+    return s;
+}
 
 static int orc_predict_scale(float max_dist, float dist, float log_sf, int nlevels) {   // MapPoint.cc:389-421
     const float ratio = max_dist / dist;
@@ -167,13 +178,12 @@ int orc_project(int mode, const orc_map_point* P, int n, const orc_view* V, cons
             }
             const float maxD = 1.2f * p.max_dist, minD = 0.8f * p.min_dist;            // MapPoint.cc:377-387
             const float POx = p.x - V->Ow[0], POy = p.y - V->Ow[1], POz = p.z - V->Ow[2];
-            const float ss = POx * POx + POy * POy + POz * POz;
-            const float dist = (float)std::sqrt((double)ss);                             // cv::norm
+            const float dist = (float)std::sqrt(orc_norm2(POx, POy, POz));              // cv::norm
             if (dist < minD || dist > maxD) continue;
-            double dot = 0.0;                                                            // PO.dot(Pn)
-            dot += (double)(POx * p.nx);
-            dot += (double)(POy * p.ny);
-            dot += (double)(POz * p.nz);
+            double dot = 0.0;                                                            // PO.dot(Pn): dotProd_
+            dot += (double)POx * p.nx;
+            dot += (double)POy * p.ny;
+            dot += (double)POz * p.nz;
             const int pred = orc_predict_scale(p.max_dist, dist, log_sf, nlevels);
             if (mode == ORC_PROJ_MAPPOINTS) {
                 const float viewCos = (float)(dot / (double)dist);                       // Frame.cc:308-311
@@ -219,7 +229,7 @@ int orc_stereo_mappoints(const Kp* k, const float* depth, int n, const float* tw
             p.y = twc[3] * x + twc[4] * y + twc[5] * z + twc[10];
             p.z = twc[6] * x + twc[7] * y + twc[8] * z + twc[11];
             const float dx = p.x - twc[9], dy = p.y - twc[10], dz = p.z - twc[11];
-            const double nrm = std::sqrt((double)(dx * dx + dy * dy + dz * dz));   // cv::norm
+            const double nrm = std::sqrt(orc_norm2(dx, dy, dz));                 // cv::norm
             const float inv = (float)(1.0 / nrm);                              // mNormalVector / cv::norm(...)
             p.nx = dx * inv; p.ny = dy * inv; p.nz = dz * inv;
             const float dist = (float)nrm;

@@ -88,6 +88,9 @@ def main():
     json.dump({"tag": tag, "kernel": dom, "batch_images": batch, "config": "kitti" if cols == 1242 else "euroc",
                "hbm_bytes_per_launch": d["hbm_bytes"], "avg_ns": d["avg_ns"],
                "hbm_bytes_per_step": d.get("hbm_bytes_per_step"), "ms_per_step": d.get("ms_per_step"),
+               # the whole step: every kernel family's HBM bytes per step (FETCH calibrated + WRITE), summed
+               "step_hbm_bytes": sum(v.get("hbm_bytes_per_step") or 0.0 for v in summary["kernels"].values()) or None,
+               "step_kernel_ms": sum(v.get("ms_per_step") or 0.0 for v in summary["kernels"].values()) or None,
                "source": f"profiles/{tag}_pmc_summary.json"},
               open(os.path.join(out, "pmc_traffic.json"), "w"), indent=1)
     for k, v in sorted(summary["kernels"].items(), key=lambda kv: -(kv[1]["avg_ns"] or 0))[:14]:

@@ -359,13 +359,13 @@ def project_py(mode, points, view, scale, log_sf):
                     continue
             maxD, minD = f(1.2) * f(p["max_dist"]), f(0.8) * f(p["min_dist"])
             PO = [X[k] - Ow[k] for k in range(3)]
-            dist = f(math.sqrt(float(PO[0] * PO[0] + PO[1] * PO[1] + PO[2] * PO[2])))
+            dist = f(math.sqrt(norm2_d(PO)))                       # cv::norm: double squares summed in double
             if dist < minD or dist > maxD:
                 continue
             N = (f(p["nx"]), f(p["ny"]), f(p["nz"]))
             dot = 0.0
             for k in range(3):
-                dot += float(PO[k] * N[k])
+                dot += float(PO[k]) * float(N[k])                     # Mat::dot: double products
             ratio = f(p["max_dist"]) / dist
             pred = min(max(int(math.ceil(math.log(float(ratio)) / float(log_sf))), 0), nlev - 1)
             if mode == PROJ_MAPPOINTS:
@@ -385,6 +385,15 @@ def project_py(mode, points, view, scale, log_sf):
             q["min_level"], q["max_level"], q["level"] = pred - 1, pred, pred
         q["flags"] = int(p["flags"]) & ~QF_SKIP
     return out
+
+
+def norm2_d(v):
+    """cv::norm's sum of squares for a 3x1 CV_32F Mat (OpenCV 3.2 normL2Sqr<float, double>): elements widened to double,
+    squared and summed left to right in double."""
+    s = 0.0
+    for x in v:
+        s += float(x) * float(x)
+    return s
 
 
 def stereo_frame_case(seed: int, n: int = 700, W: int = 1242, H: int = 375):
@@ -424,7 +433,7 @@ def stereo_mappoints_py(k, depth, twc, cam, scale, flags):
         y = (f(k["y"][i]) - f(cam[3])) * z * invfy
         X = [T[3 * r] * x + T[3 * r + 1] * y + T[3 * r + 2] * z + T[9 + r] for r in range(3)]
         d = [X[r] - T[9 + r] for r in range(3)]
-        nrm = math.sqrt(float(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]))
+        nrm = math.sqrt(norm2_d(d))
         inv = f(1.0 / nrm)
         p["x"], p["y"], p["z"] = X
         p["nx"], p["ny"], p["nz"] = d[0] * inv, d[1] * inv, d[2] * inv

@@ -168,6 +168,18 @@ def test_grid_build_and_batched_search_device(gpu):
         nq, n = len(c["queries"]), len(c["kps"])
         got = (int(nm[i]), q_idx[i, :nq].cpu().numpy(), q_dist[i, :nq].cpu().numpy(), owner[i, :n].cpu().numpy())
         _check(c, got)
+    # a caller that understates max_nq / max_n (the LDS plan's bounds): the problems above them are not searched
+    # (q_idx -1, nmatches -1) and the others are unaffected -- never an LDS overrun
+    for max_n, max_nq in ((cap, 560), (800, nqmax)):
+        m.proj_search_batch_device(cases[0]["params"], grid, dprobs, max_n, max_nq)
+        torch.cuda.synchronize()
+        for i, c in enumerate(cases):
+            nq, n = len(c["queries"]), len(c["kps"])
+            if nq > max_nq or n > max_n:
+                assert int(nm[i]) == -1 and bool((q_idx[i, :nq] == -1).all()), (i, max_n, max_nq)
+            else:
+                got = (int(nm[i]), q_idx[i, :nq].cpu().numpy(), q_dist[i, :nq].cpu().numpy(), owner[i, :n].cpu().numpy())
+                _check(c, got)
 
 
 @pytest.mark.parametrize("seed", range(4))

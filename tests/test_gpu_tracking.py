@@ -64,7 +64,7 @@ def test_frame_tracker_vs_oracle(gpu):
     kh, dh, ch = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
     p_lf = ProjParams.make(PROJ_LASTFRAME, 100, 0.9, True, isg)
     p_mp = ProjParams.make(PROJ_MAPPOINTS, 100, 0.8, False, isg)
-    tot1 = tot2 = 0
+    tot1 = tot2 = dropped = 0
     for i in range(B):
         n = int(ch[i])
         k = kh[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
@@ -75,12 +75,18 @@ def test_frame_tracker_vs_oracle(gpu):
         q1 = O.project(PROJ_LASTFRAME, last, v_lf, scale, log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
         r1, ri1, _, own1 = O.proj_search(p_lf, grid, q1, d, k, d, uright=ur[i, :n])
         assert nm1[i] == r1 and np.array_equal(qi1[i, :n], ri1), f"motion-model search, frame {i}"
-        pts["flags"][ri1 >= 0] |= QF_SKIP
+        # SearchLocalPoints skips the MapPoints in mCurrentFrame.mvpMapPoints (Tracking.cc:1158-1174): assigned AND
+        # kept by the rotation filter (ORBmatcher.cc:1456-1466 resets the ones it drops, owner -2)
+        fnd = MA.found_in_frame(ri1, own1)
+        dropped += int(((ri1 >= 0) & ~fnd).sum())
+        pts["flags"][fnd] |= QF_SKIP
         q2 = O.project(PROJ_MAPPOINTS, pts, v_mp, scale, log_sf).view(PROJ_QUERY_DTYPE).reshape(-1)
         r2, ri2, _, _ = O.proj_search(p_mp, grid, q2, d, k, d, uright=ur[i, :n], blocked=(own1 >= 0).astype(np.uint8))
         assert nm2[i] == r2 and np.array_equal(qi2[i, :n], ri2), f"local-map search, frame {i}"
         tot1, tot2 = tot1 + r1, tot2 + r2
     assert tot1 > 100 * B and tot2 > 100 * B, (tot1, tot2)
+    # the case the owner rule exists for: motion-model matches the rotation filter dropped are searched again
+    assert dropped > 0, "no rotation-filter drops in these frames: the local-map skip rule is not exercised"
 
 
 def test_local_fuse_vs_oracle(gpu):
