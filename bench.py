@@ -34,10 +34,11 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# Hardware queues per process (HIP's default is 4).  The bench drives 8 streams (front-end, keyframe path,
-# the extractor's blur side stream, and the library objects' own queues); with 4 queues, round-robin puts
-# the front-end and keyframe streams on one queue and serialises them.  Read by the HIP runtime at init.
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("ORBX_HW_QUEUES", "8")
+# Hardware queues per process: HIP's default (4 on the box).  r5a: 4 and 8 queues measured equal (73,954 / 74,196
+# stereo frames/s in one call, profiles/r5a_hwq*.log); ORBX_HW_QUEUES overrides (read by the HIP runtime
+# at init, before any GPU call).
+if os.environ.get("ORBX_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["ORBX_HW_QUEUES"]
 
 METRIC = "frames/sec ORB extract+match, KITTI 1242×375 @2000 kpts, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0                         # MI355X HBM3E peak (MI355X_MICROARCH.md)
@@ -81,8 +82,8 @@ def parse():
                     help="front-end and stereo streams leave this many CUs out of their CU mask (the keyframe stream keeps "
                          "every CU), so the keyframe path's small kernels are not starved; 0 = plain streams")
     ap.add_argument("--distinct", type=int, default=0,
-                    help="distinct synthetic stereo pairs per rank, tiled to the batch (0: as many as the batch, so no image "
-                         "of a step repeats)")
+                    help="distinct synthetic stereo pairs per rank, tiled to the batch (0: the largest multiple of 5 <= the "
+                         "batch -- 255 at 256 -- so every agent's keyframes show the same scenes, see main())")
     ap.add_argument("--input-sets", type=int, default=3,
                     help="resident input batches read in turn (set k = the batch rolled by 3k rows / 11k columns): 3 x 119 MB "
                          "exceeds the 256 MB Infinity Cache, so every step's level-0 reads come from HBM (1 = one batch "
@@ -901,7 +902,10 @@ def main():
     devices_used = min(world, max(1, n_dev))
 
     B = args.batch
-    nd = max(1, min(args.distinct, B)) if args.distinct > 0 else B
+    # distinct scenes: a multiple of KF_EVERY by default (255 at B = 256: one scene shown twice in a step), so that every
+    # agent's keyframes -- the frames f = 0 mod KF_EVERY of its chunk -- show the same nd / KF_EVERY scenes whatever its
+    # chunk offset, as agents mapping one area revisit what the others saw, and MapFusion finds cross-agent candidates
+    nd = max(1, min(args.distinct, B)) if args.distinct > 0 else (B - B % KF_EVERY if B >= KF_EVERY else B)
     # this agent's contiguous chunk of one synthetic sequence (generic_split_seq.cc:543-589); frame f of the
     # sequence is the synthetic stereo pair of seed f
     chunk = MA.split_sequence(cfg["seq_frames"], world)[rank]
@@ -964,7 +968,12 @@ def main():
     engine = pkg.KeyframeFusionEngine(vocab, pkg.ORBmatcher(0.75, True, device=dev.index), cap,
                                       slots=STORE_STEPS * world * n_kf, max_keyframes=n_kf, candidates=KF_CANDIDATES,
                                       agent=rank, world=world, device=dev.index)
-    kf_rows = range(0, KF_EVERY * n_kf, KF_EVERY)      # every 5th left frame of the batch becomes a keyframe
+    # every 5th frame of the sequence becomes a keyframe: batch rows kf_off + 5j, the frames of the chunk = 0 mod 5
+    # (kf_off <= 4, so the 51 rows of a 256-frame batch end at row <= 254)
+    kf_off = (-chunk.start) % KF_EVERY
+    if kf_off + KF_EVERY * (n_kf - 1) >= B:
+        kf_off = 0
+    kf_rows = range(kf_off, kf_off + KF_EVERY * n_kf, KF_EVERY)
     # CreateNewMapPoints' matching per new keyframe: SearchForTriangulation vs its TRI_NEIGHBOURS previous keyframes of
     # this agent (all pairs in one launch; MapPoint flags = the store's valid field, i.e. stereo depth > 0), then
     # the distinctive descriptors of its keypoints' observation lists.  FeatureVector nodes at levelsup 4 of a k=10,
@@ -996,7 +1005,7 @@ def main():
         tracker = MA.FrameTracker(pkg.ORBmatcher(0.9, True, device=dev.index), B, cap, grid, geo.camera, BF, scale, log_sf,
                                   dev, NS, twc_last, v_lf, v_mp, inv_sigma2)
     fuse = None
-    kf_rows_t = torch.tensor(list(range(0, KF_EVERY * n_kf, KF_EVERY)), dtype=torch.int64, device=dev)
+    kf_rows_t = torch.tensor(list(kf_rows), dtype=torch.int64, device=dev)
     if args.fuse:
         twc_s, views_s = geo.slot_tables(engine.slots, world, n_kf)
         fuse = MA.LocalFuse(pkg.ORBmatcher(0.6, True, device=dev.index), engine.store, engine.slots, cap, grid, geo.camera,
@@ -1093,9 +1102,9 @@ def main():
             e2 = torch.cuda.Event(enable_timing=True)
             e2.record(kf_stream)
         if world == 1:
-            engine.step(kps, desc, cnt, kf_rows, frame_no[0], KF_EVERY, depth=depth, stream=kf_stream)
+            engine.step(kps, desc, cnt, kf_rows, frame_no[0] + kf_off, KF_EVERY, depth=depth, stream=kf_stream)
         else:
-            engine.pack(kps, desc, cnt, kf_rows, frame_no[0], KF_EVERY, depth=depth, send=send, stream=kf_stream)
+            engine.pack(kps, desc, cnt, kf_rows, frame_no[0] + kf_off, KF_EVERY, depth=depth, send=send, stream=kf_stream)
             with torch.cuda.stream(kf_stream):
                 exchange.exchange(send, out=gathered)
             engine.commit(gathered, stream=kf_stream)
@@ -1214,6 +1223,7 @@ def main():
                    "keyframes_per_gpu_per_step": n_kf, "bow_pairs_per_gpu_per_step": n_kf * KF_CANDIDATES,
                    "global_batch": B * world, "frames_per_gpu_per_step": B, "image": [ROWS, COLS],
                    "nfeatures": NFEAT, "nlevels": NLEV, "distinct_stereo_pairs_per_gpu": nd,
+                   "keyframe_rows": [kf_rows.start, kf_rows.stop, kf_rows.step],
                    "input_sets": len(img_sets), "input_bytes_resident": int(sum(t.numel() for t in img_sets)),
                    "sequence_chunk": [chunk.start, chunk.stop],
                    "parallelism": f"agent-per-gpu x{world}"},

@@ -286,6 +286,113 @@ __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size
     resize4_item(pyr, pyr_stride, src, src_step, src_istride, sw, dst_off, dw, dh, t, strip, band, img);
 }
 
+// Two pyramid levels per launch (lb = la + 1 and lc = la + 2, ComputePyramid :1120 chained twice): one 256-thread
+// workgroup per (image, band of kResizeBand lc rows).  Phase 1 computes the lb rows the band's lc rows read, [c0, c1),
+// from level la in HBM into LDS and writes the lb rows the band owns, [own0, own1) (the bands partition lb's rows, so
+// every lb row is written once; a row two bands read is computed by both); phase 2 computes the band's lc rows from
+// LDS.  Same arithmetic, tables and rounding as k_resize4: bit-identical levels, half the dependent launches, and lb
+// is never read back from HBM.
+struct ResizePair {
+    ResizeVec tb, tc;        // tables of lb (from la) and lc (from lb)
+    const int4* band;        // per lc band: c0, c1, own0, own1 (lb rows)
+    int nbands, stride;      // lc bands; LDS bytes per lb row (>= wb + 8, a multiple of 4)
+    int wa, wb, hb, wc, hc;  // source width, lb and lc sizes
+    int off_b, off_c;        // lb / lc offsets inside one image's pyramid
+};
+
+__device__ __forceinline__ void resize_lds_window(const uint8_t* __restrict__ row, int xb, uint32_t& lo, uint32_t& hi) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(row) + (xb >> 2);
+    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
+    lo = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)(xb & 3));
+    hi = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)(xb & 3));
+}
+
+__device__ __forceinline__ uint32_t resize_group(uint32_t lo0, uint32_t hi0, uint32_t lo1, uint32_t hi1, const uint4& sel,
+                                                 const uint4& coef, int b0, int b1) {
+    const uint32_t sl[4] = {sel.x, sel.y, sel.z, sel.w}, cf[4] = {coef.x, coef.y, coef.z, coef.w};
+    uint32_t acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const u16x2 c = __builtin_bit_cast(u16x2, cf[k]);
+        const uint32_t hv0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi0, lo0, sl[k])), c, 0u, false);
+        const uint32_t hv1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi1, lo1, sl[k])), c, 0u, false);
+        acc[k] = resize_acc(hv0, hv1, b0, b1);
+    }
+    return resize_pack(acc);
+}
+
+__device__ __forceinline__ void resize_store4(uint8_t* __restrict__ o, uint32_t packed, int x, int w) {
+    if (x + 4 <= w) {
+        __builtin_memcpy(o, &packed, 4);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (x + k < w) o[k] = (uint8_t)(packed >> (8 * k));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_resize_pair(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
+                                                     size_t src_step, size_t src_istride, ResizePair P, int batch) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
+    const int nwg = P.nbands * batch;
+    const int wg = xcd_item(xcd_chunk(nwg));
+    if (wg >= nwg) return;                                           // workgroup-uniform
+    const int img = wg / P.nbands, band = wg - img * P.nbands;
+    const int4 bd = P.band[band];
+    const int tid = threadIdx.x;
+    const uint8_t* S = src + img * src_istride;
+    uint8_t* Db = pyr + img * pyr_stride + P.off_b;
+    uint8_t* Dc = pyr + img * pyr_stride + P.off_c;
+    uint8_t* L = reinterpret_cast<uint8_t*>(rsm);
+    // phase 1: items (lb row r, group g), r in [c0, c1), walked incrementally (item q -> q + 256); two per round, both
+    // windows loaded before either is computed
+    {
+        const int Gb = P.tb.groups, items = (bd.y - bd.x) * Gb;
+        const int dr = 256 / Gb, dg = 256 - dr * Gb;                 // Gb > 64 (lb >= 257 columns: host-checked)
+        int r = tid / Gb, g = tid - r * Gb;
+        for (int i0 = 0; i0 < items; i0 += 512) {
+            int rr[2], gg[2];
+            uint32_t lo[4], hi[4];
+            int4 yr[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                rr[k] = r; gg[k] = g;
+                r += dr; g += dg;
+                if (g >= Gb) { g -= Gb; ++r; }
+                const bool v = i0 + tid + 256 * k < items;
+                yr[k] = P.tb.yrow[v ? bd.x + rr[k] : 0];
+                const int xb = P.tb.xb[v ? gg[k] : 0];
+                resize_window8(S + (size_t)yr[k].x * src_step, xb, P.wa, lo[2 * k], hi[2 * k]);
+                resize_window8(S + (size_t)yr[k].y * src_step, xb, P.wa, lo[2 * k + 1], hi[2 * k + 1]);
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (i0 + tid + 256 * k >= items) continue;
+                const uint32_t packed = resize_group(lo[2 * k], hi[2 * k], lo[2 * k + 1], hi[2 * k + 1], P.tb.sel[gg[k]],
+                                                     P.tb.coef[gg[k]], yr[k].z, yr[k].w);
+                const int row = bd.x + rr[k], x = 4 * gg[k];
+                *reinterpret_cast<uint32_t*>(L + (size_t)rr[k] * P.stride + x) = packed;   // row slack >= 8 bytes
+                if (row >= bd.z && row < bd.w) resize_store4(Db + (size_t)row * P.wb + x, packed, x, P.wb);
+            }
+        }
+    }
+    __syncthreads();
+    // phase 2: the band's lc rows from the lb rows in LDS
+    {
+        const int Gc = P.tc.groups, y0 = band * kResizeBand, ny = min(kResizeBand, P.hc - y0), items = ny * Gc;
+        for (int q = tid; q < items; q += 256) {
+            const int r = q / Gc, g = q - r * Gc, y = y0 + r;
+            const int4 yr = P.tc.yrow[y];
+            const int xb = P.tc.xb[g];
+            uint32_t lo0, hi0, lo1, hi1;
+            resize_lds_window(L + (size_t)(yr.x - bd.x) * P.stride, xb, lo0, hi0);
+            resize_lds_window(L + (size_t)(yr.y - bd.x) * P.stride, xb, lo1, hi1);
+            const uint32_t packed = resize_group(lo0, hi0, lo1, hi1, P.tc.sel[g], P.tc.coef[g], yr.z, yr.w);
+            resize_store4(Dc + (size_t)y * P.wc + 4 * g, packed, 4 * g, P.wc);
+        }
+    }
+}
+
 // FAST-9/16 corner score in closed form.  For pixel value v and circle values p_k (Bresenham r=3,
 // OpenCV order), with d_k = v - p_k:  m_dark = max over the 16 arcs of 9 of min d, m_bright = max
 // over arcs of min(-d).  OpenCV's cornerScore<16> returns max(t, m_dark, m_bright) - 1 and the pixel
@@ -529,7 +636,10 @@ __device__ __forceinline__ int rank_below(uint64_t b, int acc = 0) {
 // score-map row stride (int16) per pair stride: >= (Wd + 5) & ~1 for every cell the pair stride admits (40 = 20 dwords
 // for the padded layout: its NMS reads model at 1.6 extra cycles per access against 1.8 for 22 dwords,
 // scripts/micro/lds_banks.py)
-__host__ __device__ constexpr int fastw_sw(int ps) { return ps == 19 ? 40 : 76; }
+#ifndef ORBX_FAST_SW19
+#define ORBX_FAST_SW19 40
+#endif
+__host__ __device__ constexpr int fastw_sw(int ps) { return ps == 19 ? ORBX_FAST_SW19 : 76; }
 
 // The part of a cell after its ROI is in LDS: pre-test, scores, NMS at both thresholds, the cell's candidate slots.
 template <int kPS, int kPC>
@@ -769,7 +879,7 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
 }
 
 // GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, integer separable path: taps {18,34,49,55,49,34,18},
-// column pass (acc + 2^15) >> 16 saturated.  Tile 64 x 16 per workgroup; tiles of all levels in one grid.
+// column pass (acc + 2^15) >> 16 saturated.  Tiles (level, strip, band) of all levels in one grid.
 struct BlurTile { int level, tx, ty, pad; };
 
 __device__ __forceinline__ int refl101(int i, int n) {
@@ -778,8 +888,8 @@ __device__ __forceinline__ int refl101(int i, int n) {
     return i;
 }
 
-// Register-streaming form: one wave per (level, 256-column strip, 16-row band).  Lane l owns the 4
-// output columns x0 = strip*256 + 4l .. x0+3, walks down the band's 22 input rows once, and keeps the
+// Register-streaming form: one wave per (level, 256-column strip, ORBX_BLUR_BAND-row band, 32 rows).  Lane l owns
+// the 4 output columns x0 = strip*256 + 4l .. x0+3, walks down the band's 38 input rows once, and keeps the
 // last 4 row pairs of horizontal sums in registers (a ring unrolled by 4, so no moves); no LDS, no
 // divisions.  Reflection only at the level borders (scalar for rows, byte selectors for edge lanes).
 // Per input row a lane issues one 12-byte load (x0-4 .. x0+7; global loads need no alignment on gfx950);
@@ -954,7 +1064,7 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
 #ifndef ORBX_BLUR_WPE
 #define ORBX_BLUR_WPE 6     // 80 VGPRs: 6 waves per SIMD (r4ak: serial blur 0.588 -> 0.571 ms; 8 spills 25 VGPRs)
 #endif
-// one wave's blur tile (level, 256-column strip, 16-row band) of image img
+// one wave's blur tile (level, 256-column strip, ORBX_BLUR_BAND-row band) of image img
 __device__ __forceinline__ void blur_tile(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride,
                                           const LevelDev* __restrict__ levels, const BlurTile& bt, int img, const Src0& s0) {
     const LevelDev L = levels[bt.level];
@@ -1891,6 +2001,9 @@ struct Extractor {
     BlurTile* d_tiles = nullptr;
     std::vector<ResizeTab> rtab;
     std::vector<ResizeVec> rvec;      // per level: vectorised tables (groups == 0 -> use rtab)
+    std::vector<ResizePair> rpair;    // per level la: the pair launch la -> la + 1, la + 2 (nbands == 0: none)
+    std::vector<int> rpair_lds;       // its dynamic LDS bytes
+    bool resize_pair = false;         // ORBX_RESIZE_PAIR=1: two levels per launch (read at configure)
     std::vector<void*> rtab_mem;
     uint8_t* d_pyr = nullptr;         // pyramid set of the current / last call (a slot of d_pyr_ring)
     uint8_t* d_pyr_ring = nullptr;    // pyr_ring sets of max_batch pyramids: a caller that reads the pyramid of call
@@ -2206,6 +2319,7 @@ int Extractor::configure(int r, int c, int batch) {
     // ---- resize tables (pinned OpenCV 3.2 INTER_LINEAR fixed point), level l from level l-1
     rtab.assign(nlevels, ResizeTab{});
     rvec.assign(nlevels, ResizeVec{});
+    std::vector<std::vector<int>> ry0(nlevels), ry1(nlevels);        // source rows of every level's rows (pair bands)
     for (int l = 1; l < nlevels; ++l) {
         const int sw = lv[l - 1].w, sh = lv[l - 1].h, dw = lv[l].w, dh = lv[l].h;
         const double sxs = 1.0 / ((double)dw / sw), sys = 1.0 / ((double)dh / sh);
@@ -2235,6 +2349,8 @@ int Extractor::configure(int r, int c, int batch) {
             hy0[y] = std::min(std::max(iy, 0), sh - 1);
             hy1[y] = std::min(std::max(iy + 1, 0), sh - 1);
         }
+        ry0[l] = hy0;
+        ry1[l] = hy1;
         int* mem;
         if ((st = dev_alloc(&mem, 4 * (size_t)dw + 4 * (size_t)dh))) return st;
         rtab_mem.push_back(mem);
@@ -2277,6 +2393,48 @@ int Extractor::configure(int r, int c, int batch) {
             rv.yrow = (const int4*)(vm + bx + 2 * bs); rv.groups = G;
             rvec[l] = rv;
         }
+    }
+    // pair launches la -> lb = la + 1, lc = la + 2 for la = 0, 2, 4, ...: lc's bands of kResizeBand rows, the lb rows
+    // each reads ([c0, c1)) and the lb rows each writes (a partition of lb's rows: band k owns [c0_k, c0_{k+1}), the
+    // first from row 0, the last to the end)
+    rpair.assign(nlevels, ResizePair{});
+    rpair_lds.assign(nlevels, 0);
+    {
+        const char* v = std::getenv("ORBX_RESIZE_PAIR");
+        resize_pair = v && std::atoi(v) == 1;
+    }
+    for (int la = 0; la + 2 < nlevels; la += 2) {
+        const int lb = la + 1, lc = la + 2;
+        if (!rvec[lb].groups || !rvec[lc].groups || lv[la].w < 8 || lv[lb].w < 257) continue;
+        const int hb = lv[lb].h, hc = lv[lc].h, nb = (hc + kResizeBand - 1) / kResizeBand;
+        std::vector<int4> bands(nb);
+        int maxrows = 0;
+        for (int k = 0; k < nb; ++k) {
+            const int ya = k * kResizeBand, yz = std::min(ya + kResizeBand, hc) - 1;
+            bands[k].x = std::min(ry0[lc][ya], ry1[lc][ya]);
+            bands[k].y = std::max(ry0[lc][yz], ry1[lc][yz]) + 1;
+        }
+        for (int k = 0; k < nb; ++k) {
+            bands[k].z = k == 0 ? 0 : bands[k].x;
+            bands[k].w = k + 1 < nb ? bands[k + 1].x : hb;
+            bands[k].x = std::min(bands[k].x, bands[k].z);              // compute every owned row too
+            bands[k].y = std::max(bands[k].y, bands[k].w);
+            maxrows = std::max(maxrows, bands[k].y - bands[k].x);
+        }
+        bool ok = true;
+        for (int k = 0; k < nb; ++k) ok = ok && bands[k].x >= 0 && bands[k].y <= hb && bands[k].z <= bands[k].w;
+        const int stride = ((lv[lb].w + 3) & ~3) + 8;
+        const int lds = maxrows * stride + 16;
+        if (!ok || lds > 64 * 1024) continue;
+        int4* dband;
+        if ((st = dev_alloc(&dband, nb))) return st;
+        rtab_mem.push_back(dband);
+        ORBX_HIP(hipMemcpy(dband, bands.data(), sizeof(int4) * nb, hipMemcpyHostToDevice));
+        ResizePair& P = rpair[la];
+        P.tb = rvec[lb]; P.tc = rvec[lc]; P.band = dband; P.nbands = nb; P.stride = stride;
+        P.wa = lv[la].w; P.wb = lv[lb].w; P.hb = hb; P.wc = lv[lc].w; P.hc = hc;
+        P.off_b = lv[lb].pyr_off; P.off_c = lv[lc].pyr_off;
+        rpair_lds[la] = lds;
     }
 
     // ---- batch buffers (HBM): pyramid + blurred pyramid + candidates + quadtree scratch
@@ -2388,6 +2546,13 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
             const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
             const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
             const LevelDev& L = e->lv[l];
+            if (e->resize_pair && l + 1 < nl && e->rpair[l - 1].nbands > 0) {   // levels l and l + 1 in one launch
+                const ResizePair& P = e->rpair[l - 1];
+                hipLaunchKernelGGL(k_resize_pair, dim3(kXcds * xcd_chunk(P.nbands * batch)), dim3(256),
+                                   (size_t)e->rpair_lds[l - 1], s, e->d_pyr, ps, src, sstep, sis, P, batch);
+                ++l;
+                continue;
+            }
             if (e->rvec[l].groups > 0) {
                 const int nstrips = (L.w + kResizeStrip - 1) / kResizeStrip, nbands = (L.h + kResizeBand - 1) / kResizeBand;
                 const int nwg = (nstrips * nbands * batch + 3) / 4;

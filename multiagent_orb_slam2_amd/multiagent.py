@@ -16,6 +16,7 @@ agents.
 """
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 
@@ -807,6 +808,9 @@ def make_view(Rwc, Ow, camera, bf, bounds, th, view_cos_limit=0.5, level_mode=0)
     return v
 
 
+_FUSE_SPLIT = os.environ.get("ORBX_FUSE_SPLIT", "0") == "1"
+
+
 class LocalFuse:
     """LocalMapping::SearchInNeighbors' Fuse calls for a batch of new keyframes (src/LocalMapping.cc:460-520): each
     new keyframe's MapPoints fused into each of its neighbours (Fuse(pKFi, vpMapPointMatches), :486-496) and the
@@ -859,7 +863,8 @@ class LocalFuse:
 
     def _plan(self, new_slots, neighbours):
         """Per (new keyframe j, neighbour k): the two directions' views, point sets and problem tables (cached per
-        pattern: the ring's slot patterns repeat)."""
+        pattern: the ring's slot patterns repeat).  Both directions are one problem array of 2P problems (direction 0
+        first), searched by one projection launch and one search launch."""
         import torch
         key = (tuple(new_slots), tuple(map(tuple, neighbours)))
         if key in self.cache:
@@ -871,28 +876,27 @@ class LocalFuse:
         P, cap, st = n * nn, self.cap, self.store
         ns = np.repeat(np.asarray(new_slots, np.int64), nn)
         nb = np.asarray(neighbours, np.int64).reshape(-1)
-        ok = nb >= 0
-        nbc = np.where(ok, nb, 0)
+        ok = np.concatenate([nb >= 0, nb >= 0])
+        nbc = np.where(nb >= 0, nb, 0)
+        tgt, src = np.concatenate([nbc, ns]), np.concatenate([ns, nbc])   # 0: current MPs into neighbour; 1: the reverse
         dev = self.dev
-        out = {}
-        for d, (tgt, src) in enumerate(((nbc, ns), (ns, nbc))):   # 0: current MPs into neighbour; 1: neighbour MPs into current
-            q = torch.empty((P, cap, 40), dtype=torch.uint8, device=dev)
-            qi, qd = torch.empty((P, cap), dtype=torch.int32, device=dev), torch.empty((P, cap), dtype=torch.int32, device=dev)
-            own, nm = torch.empty((P, cap), dtype=torch.int32, device=dev), torch.empty((P,), dtype=torch.int32, device=dev)
-            i = np.arange(P, dtype=np.int64)
-            t = problem_table(P, queries=q.data_ptr() + i * cap * 40, qdesc=st.desc + src * st.desc_stride,
-                              nq=np.where(ok, cap, 0), kps=st.kps + tgt * st.kps_stride, desc=st.desc + tgt * st.desc_stride,
-                              uright=self.ur.data_ptr() + tgt * cap * 4, n=cap,
-                              cell_start=self.cs.data_ptr() + tgt * self.cs.shape[1] * 4,
-                              cell_idx=self.ci.data_ptr() + tgt * cap * 4, q_idx=qi.data_ptr() + i * cap * 4,
-                              q_dist=qd.data_ptr() + i * cap * 4, owner=own.data_ptr() + i * cap * 4,
-                              nmatches=nm.data_ptr() + i * 4)
-            views = self.views[torch.from_numpy(tgt).to(dev)].contiguous()
-            vpts = torch.from_numpy(src.astype(np.int32)).to(dev)
-            # every buffer the problem table points at stays referenced here (q_dist and owner too: a freed block would
-            # be handed to another tensor while the searches still write it)
-            out[d] = dict(q=q, qi=qi, qd=qd, own=own, nm=nm, probs=torch.from_numpy(t.view(np.uint8)).to(dev), views=views,
-                          vpts=vpts)
+        q = torch.empty((2 * P, cap, 40), dtype=torch.uint8, device=dev)
+        qi, qd = torch.empty((2 * P, cap), dtype=torch.int32, device=dev), torch.empty((2 * P, cap), dtype=torch.int32, device=dev)
+        own, nm = torch.empty((2 * P, cap), dtype=torch.int32, device=dev), torch.empty((2 * P,), dtype=torch.int32, device=dev)
+        i = np.arange(2 * P, dtype=np.int64)
+        t = problem_table(2 * P, queries=q.data_ptr() + i * cap * 40, qdesc=st.desc + src * st.desc_stride,
+                          nq=np.where(ok, cap, 0), kps=st.kps + tgt * st.kps_stride, desc=st.desc + tgt * st.desc_stride,
+                          uright=self.ur.data_ptr() + tgt * cap * 4, n=cap,
+                          cell_start=self.cs.data_ptr() + tgt * self.cs.shape[1] * 4,
+                          cell_idx=self.ci.data_ptr() + tgt * cap * 4, q_idx=qi.data_ptr() + i * cap * 4,
+                          q_dist=qd.data_ptr() + i * cap * 4, owner=own.data_ptr() + i * cap * 4,
+                          nmatches=nm.data_ptr() + i * 4)
+        views = self.views[torch.from_numpy(tgt).to(dev)].contiguous()
+        vpts = torch.from_numpy(src.astype(np.int32)).to(dev)
+        # every buffer the problem table points at stays referenced here (q_dist and owner too: a freed block would be
+        # handed to another tensor while the searches still write it)
+        out = dict(q=q, qi=qi, qd=qd, own=own, nm=nm, probs=torch.from_numpy(t.view(np.uint8)).to(dev), views=views,
+                   vpts=vpts)
         self.cache[key] = out
         return out
 
@@ -900,17 +904,20 @@ class LocalFuse:
         """new_slots (n,) and neighbours (n, nn) as host int arrays (-1 = none).  Returns ((q_idx, nmatches) of the
         current-into-neighbour searches, (q_idx, nmatches) of the neighbour-into-current ones), (n*nn, cap) / (n*nn,)."""
         from .orbx import PROJ_FUSE
-        plan = self._plan(np.asarray(new_slots), np.asarray(neighbours))
-        res = []
-        for d in (0, 1):
-            p = plan[d]
-            self.m.proj_project_device(PROJ_FUSE, self.pts, self.cnt, p["views"], self.scale, self.log_sf, out=p["q"],
-                                       view_points=p["vpts"], stream=stream)
-            self.m.proj_search_batch_device(self.params, self.grid, p["probs"], self.cap, self.cap, stream=stream)
-            if stream is not None:
-                # the kernels read / write these through raw pointers on 'stream': an evicted plan's memory must not be
-                # handed out again before that stream's work is done
-                for t in p.values():
-                    t.record_stream(stream)
-            res.append((p["qi"], p["nm"]))
-        return res
+        nb = np.asarray(neighbours)
+        p = self._plan(np.asarray(new_slots), nb)
+        P = nb.shape[0] * nb.shape[1]
+        # one projection + one search launch over both directions (ORBX_FUSE_SPLIT=1, diagnostics: one pair per direction)
+        parts = ((0, 2 * P),) if not _FUSE_SPLIT else ((0, P), (P, 2 * P))
+        pb = p["probs"].numel() // (2 * P)
+        for a, b in parts:
+            self.m.proj_project_device(PROJ_FUSE, self.pts, self.cnt, p["views"][a:b], self.scale, self.log_sf,
+                                       out=p["q"][a:b], view_points=p["vpts"][a:b], stream=stream)
+            self.m.proj_search_batch_device(self.params, self.grid, p["probs"][a * pb:b * pb], self.cap, self.cap,
+                                            stream=stream)
+        if stream is not None:
+            # the kernels read / write these through raw pointers on 'stream': an evicted plan's memory must not be
+            # handed out again before that stream's work is done
+            for t in p.values():
+                t.record_stream(stream)
+        return [(p["qi"][:P], p["nm"][:P]), (p["qi"][P:], p["nm"][P:])]

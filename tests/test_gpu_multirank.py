@@ -15,7 +15,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SMALL = ["--steps", "2", "--warmup", "2", "--batch", "16", "--distinct", "2", "--cpu-seconds", "0", "--host-api-frames", "0", "--no-c3",
+SMALL = ["--steps", "2", "--warmup", "2", "--batch", "16", "--cpu-seconds", "0", "--host-api-frames", "0", "--no-c3",
          "--no-cd", "--host-fed-steps", "0", "--alone-reps", "0"]
 
 
@@ -43,6 +43,8 @@ def _check_world2(d, backend):
     assert d["config"]["global_batch"] == 32 and d["config"]["parallelism"] == "agent-per-gpu x2"
     # rank r's frames are its chunk of the sequence (generic_split_seq.cc:543-589): rank 0 holds the first half
     assert d["config"]["sequence_chunk"] == [0, 2271]
+    # default scenes: 15 distinct (a multiple of 5), keyframes at the sequence's frames = 0 mod 5 (rows 0, 5, 10 on rank 0)
+    assert d["config"]["distinct_stereo_pairs_per_gpu"] == 15 and d["config"]["keyframe_rows"] == [0, 15, 5]
     x = d["exchange"]
     assert x["calls"] == 2 and x["bytes_per_allgather"] == 2 * 3 * x["packet_bytes"]
     assert all(s["data_ok"] for s in d["xgmi_allgather"]["sweep"])
