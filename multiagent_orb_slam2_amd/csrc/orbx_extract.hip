@@ -300,6 +300,11 @@ struct ResizePair {
     int off_b, off_c;        // lb / lc offsets inside one image's pyramid
 };
 
+#ifndef ORBX_PAIR_K
+#define ORBX_PAIR_K 6       // phase-1 items per thread and round (all their loads in flight together)
+#endif
+constexpr int kPairK = ORBX_PAIR_K;
+
 __device__ __forceinline__ void resize_lds_window(const uint8_t* __restrict__ row, int xb, uint32_t& lo, uint32_t& hi) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(row) + (xb >> 2);
     const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
@@ -344,18 +349,19 @@ __global__ __launch_bounds__(256) void k_resize_pair(uint8_t* __restrict__ pyr, 
     uint8_t* Db = pyr + img * pyr_stride + P.off_b;
     uint8_t* Dc = pyr + img * pyr_stride + P.off_c;
     uint8_t* L = reinterpret_cast<uint8_t*>(rsm);
-    // phase 1: items (lb row r, group g), r in [c0, c1), walked incrementally (item q -> q + 256); two per round, both
-    // windows loaded before either is computed
+    // phase 1: items (lb row r, group g), r in [c0, c1), walked incrementally (item q -> q + 256); kPairK per round,
+    // every window of the round loaded before the first is computed
     {
+        constexpr int K = kPairK;
         const int Gb = P.tb.groups, items = (bd.y - bd.x) * Gb;
         const int dr = 256 / Gb, dg = 256 - dr * Gb;                 // Gb > 64 (lb >= 257 columns: host-checked)
         int r = tid / Gb, g = tid - r * Gb;
-        for (int i0 = 0; i0 < items; i0 += 512) {
-            int rr[2], gg[2];
-            uint32_t lo[4], hi[4];
-            int4 yr[2];
+        for (int i0 = 0; i0 < items; i0 += 256 * K) {
+            int rr[K], gg[K];
+            uint32_t lo[2 * K], hi[2 * K];
+            int4 yr[K];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < K; ++k) {
                 rr[k] = r; gg[k] = g;
                 r += dr; g += dg;
                 if (g >= Gb) { g -= Gb; ++r; }
@@ -366,7 +372,7 @@ __global__ __launch_bounds__(256) void k_resize_pair(uint8_t* __restrict__ pyr, 
                 resize_window8(S + (size_t)yr[k].y * src_step, xb, P.wa, lo[2 * k + 1], hi[2 * k + 1]);
             }
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < K; ++k) {
                 if (i0 + tid + 256 * k >= items) continue;
                 const uint32_t packed = resize_group(lo[2 * k], hi[2 * k], lo[2 * k + 1], hi[2 * k + 1], P.tb.sel[gg[k]],
                                                      P.tb.coef[gg[k]], yr[k].z, yr[k].w);
@@ -633,11 +639,12 @@ __device__ __forceinline__ int rank_below(uint64_t b, int acc = 0) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, (uint32_t)acc));
 }
 
-// score-map row stride (int16) per pair stride: >= (Wd + 5) & ~1 for every cell the pair stride admits (40 = 20 dwords
-// for the padded layout: its NMS reads model at 1.6 extra cycles per access against 1.8 for 22 dwords,
-// scripts/micro/lds_banks.py)
+// score-map row stride (int16) per pair stride: >= (Wd + 5) & ~1 for every cell the pair stride admits.  The padded
+// layout's 36 (18 dwords) is that minimum for its 38-column ROIs; the bank model put 20 dwords at 1.6 extra cycles per
+// NMS access against 1.8 for 22 (scripts/micro/lds_banks.py), but the smaller map is what lets more waves in.
 #ifndef ORBX_FAST_SW19
-#define ORBX_FAST_SW19 40
+#define ORBX_FAST_SW19 36   // r5b: 36 (18 dwords, the minimum for 32-column detection windows) -> 5 / 6 FAST workgroups per
+                            // CU at levels >= 1 / level 0 instead of 4 / 5: serial FAST 1.153 -> 1.060 ms, step +0.9 %
 #endif
 __host__ __device__ constexpr int fastw_sw(int ps) { return ps == 19 ? ORBX_FAST_SW19 : 76; }
 
