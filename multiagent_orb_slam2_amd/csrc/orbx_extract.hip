@@ -286,8 +286,8 @@ __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size
     resize4_item(pyr, pyr_stride, src, src_step, src_istride, sw, dst_off, dw, dh, t, strip, band, img);
 }
 
-// Two pyramid levels per launch (lb = la + 1 and lc = la + 2, ComputePyramid :1120 chained twice): one 256-thread
-// workgroup per (image, band of kResizeBand lc rows).  Phase 1 computes the lb rows the band's lc rows read, [c0, c1),
+// Two pyramid levels per launch (lb = la + 1 and lc = la + 2, ComputePyramid :1120 chained twice): one workgroup per
+// (image, band of kResizeBand lc rows), one thread per 4-column group of lb (blockDim = groups rounded to 64).  Phase 1 computes the lb rows the band's lc rows read, [c0, c1),
 // from level la in HBM into LDS and writes the lb rows the band owns, [own0, own1) (the bands partition lb's rows, so
 // every lb row is written once; a row two bands read is computed by both); phase 2 computes the band's lc rows from
 // LDS.  Same arithmetic, tables and rounding as k_resize4: bit-identical levels, half the dependent launches, and lb
@@ -301,7 +301,7 @@ struct ResizePair {
 };
 
 #ifndef ORBX_PAIR_K
-#define ORBX_PAIR_K 6       // phase-1 items per thread and round (all their loads in flight together)
+#define ORBX_PAIR_K 6       // phase-1 lb rows per round (all their source windows in flight together)
 #endif
 constexpr int kPairK = ORBX_PAIR_K;
 
@@ -336,65 +336,58 @@ __device__ __forceinline__ void resize_store4(uint8_t* __restrict__ o, uint32_t 
     }
 }
 
-__global__ __launch_bounds__(256) void k_resize_pair(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
+__global__ __launch_bounds__(512) void k_resize_pair(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
                                                      size_t src_step, size_t src_istride, ResizePair P, int batch) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
     const int nwg = P.nbands * batch;
     const int wg = xcd_item(xcd_chunk(nwg));
     if (wg >= nwg) return;                                           // workgroup-uniform
-    const int img = wg / P.nbands, band = wg - img * P.nbands;
+    const int img = __builtin_amdgcn_readfirstlane(wg / P.nbands), band = __builtin_amdgcn_readfirstlane(wg - img * P.nbands);
     const int4 bd = P.band[band];
-    const int tid = threadIdx.x;
+    const int g = threadIdx.x;                                       // one 4-column group per thread, as k_resize4's lanes
     const uint8_t* S = src + img * src_istride;
     uint8_t* Db = pyr + img * pyr_stride + P.off_b;
     uint8_t* Dc = pyr + img * pyr_stride + P.off_c;
     uint8_t* L = reinterpret_cast<uint8_t*>(rsm);
-    // phase 1: items (lb row r, group g), r in [c0, c1), walked incrementally (item q -> q + 256); kPairK per round,
-    // every window of the round loaded before the first is computed
-    {
+    // phase 1: lb rows [c0, c1) of group g, kPairK rows per round with all their source windows loaded first; the row
+    // tables are workgroup-uniform (scalar loads)
+    if (g < P.tb.groups) {
         constexpr int K = kPairK;
-        const int Gb = P.tb.groups, items = (bd.y - bd.x) * Gb;
-        const int dr = 256 / Gb, dg = 256 - dr * Gb;                 // Gb > 64 (lb >= 257 columns: host-checked)
-        int r = tid / Gb, g = tid - r * Gb;
-        for (int i0 = 0; i0 < items; i0 += 256 * K) {
-            int rr[K], gg[K];
-            uint32_t lo[2 * K], hi[2 * K];
+        const int xb = P.tb.xb[g];
+        const uint4 sel = P.tb.sel[g], coef = P.tb.coef[g];
+        const int x = 4 * g;
+        for (int r0 = bd.x; r0 < bd.y; r0 += K) {
             int4 yr[K];
+            uint32_t lo[2 * K], hi[2 * K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                rr[k] = r; gg[k] = g;
-                r += dr; g += dg;
-                if (g >= Gb) { g -= Gb; ++r; }
-                const bool v = i0 + tid + 256 * k < items;
-                yr[k] = P.tb.yrow[v ? bd.x + rr[k] : 0];
-                const int xb = P.tb.xb[v ? gg[k] : 0];
+                yr[k] = P.tb.yrow[min(r0 + k, bd.y - 1)];
                 resize_window8(S + (size_t)yr[k].x * src_step, xb, P.wa, lo[2 * k], hi[2 * k]);
                 resize_window8(S + (size_t)yr[k].y * src_step, xb, P.wa, lo[2 * k + 1], hi[2 * k + 1]);
             }
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                if (i0 + tid + 256 * k >= items) continue;
-                const uint32_t packed = resize_group(lo[2 * k], hi[2 * k], lo[2 * k + 1], hi[2 * k + 1], P.tb.sel[gg[k]],
-                                                     P.tb.coef[gg[k]], yr[k].z, yr[k].w);
-                const int row = bd.x + rr[k], x = 4 * gg[k];
-                *reinterpret_cast<uint32_t*>(L + (size_t)rr[k] * P.stride + x) = packed;   // row slack >= 8 bytes
+                const int row = r0 + k;
+                if (row >= bd.y) break;                              // uniform
+                const uint32_t packed = resize_group(lo[2 * k], hi[2 * k], lo[2 * k + 1], hi[2 * k + 1], sel, coef, yr[k].z,
+                                                     yr[k].w);
+                *reinterpret_cast<uint32_t*>(L + (size_t)(row - bd.x) * P.stride + x) = packed;   // row slack >= 8 bytes
                 if (row >= bd.z && row < bd.w) resize_store4(Db + (size_t)row * P.wb + x, packed, x, P.wb);
             }
         }
     }
     __syncthreads();
-    // phase 2: the band's lc rows from the lb rows in LDS
-    {
-        const int Gc = P.tc.groups, y0 = band * kResizeBand, ny = min(kResizeBand, P.hc - y0), items = ny * Gc;
-        for (int q = tid; q < items; q += 256) {
-            const int r = q / Gc, g = q - r * Gc, y = y0 + r;
+    // phase 2: the band's lc rows of group g from the lb rows in LDS
+    if (g < P.tc.groups) {
+        const int xb = P.tc.xb[g];
+        const uint4 sel = P.tc.sel[g], coef = P.tc.coef[g];
+        const int x = 4 * g, y0 = band * kResizeBand, y1 = min(y0 + kResizeBand, P.hc);
+        for (int y = y0; y < y1; ++y) {
             const int4 yr = P.tc.yrow[y];
-            const int xb = P.tc.xb[g];
             uint32_t lo0, hi0, lo1, hi1;
             resize_lds_window(L + (size_t)(yr.x - bd.x) * P.stride, xb, lo0, hi0);
             resize_lds_window(L + (size_t)(yr.y - bd.x) * P.stride, xb, lo1, hi1);
-            const uint32_t packed = resize_group(lo0, hi0, lo1, hi1, P.tc.sel[g], P.tc.coef[g], yr.z, yr.w);
-            resize_store4(Dc + (size_t)y * P.wc + 4 * g, packed, 4 * g, P.wc);
+            resize_store4(Dc + (size_t)y * P.wc + x, resize_group(lo0, hi0, lo1, hi1, sel, coef, yr.z, yr.w), x, P.wc);
         }
     }
 }
@@ -2412,7 +2405,7 @@ int Extractor::configure(int r, int c, int batch) {
     }
     for (int la = 0; la + 2 < nlevels; la += 2) {
         const int lb = la + 1, lc = la + 2;
-        if (!rvec[lb].groups || !rvec[lc].groups || lv[la].w < 8 || lv[lb].w < 257) continue;
+        if (!rvec[lb].groups || !rvec[lc].groups || lv[la].w < 8 || rvec[lb].groups > 512) continue;
         const int hb = lv[lb].h, hc = lv[lc].h, nb = (hc + kResizeBand - 1) / kResizeBand;
         std::vector<int4> bands(nb);
         int maxrows = 0;
@@ -2555,7 +2548,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
             const LevelDev& L = e->lv[l];
             if (e->resize_pair && l + 1 < nl && e->rpair[l - 1].nbands > 0) {   // levels l and l + 1 in one launch
                 const ResizePair& P = e->rpair[l - 1];
-                hipLaunchKernelGGL(k_resize_pair, dim3(kXcds * xcd_chunk(P.nbands * batch)), dim3(256),
+                hipLaunchKernelGGL(k_resize_pair, dim3(kXcds * xcd_chunk(P.nbands * batch)), dim3((P.tb.groups + 63) & ~63),
                                    (size_t)e->rpair_lds[l - 1], s, e->d_pyr, ps, src, sstep, sis, P, batch);
                 ++l;
                 continue;
