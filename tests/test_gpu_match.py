@@ -20,6 +20,19 @@ def stereo_pair():
     return dict(kl=kl, dl=dl, kr=kr, dr=dr, scale=ex.GetScaleFactors(), rows=left.shape[0])
 
 
+@pytest.fixture(params=["two_launches", "fused"])
+def bf_mode(request, monkeypatch):
+    """C3 both ways: tile + merge launches, and one launch whose last-arriving chunk workgroup folds the partials
+    (ORBX_BF_FUSED=1, read per call).  The fused form's arrival counters are zeroed at allocation and reset by each
+    last arriver; the r4bo variant lacked the zeroing: a fresh matcher's first launch saw a non-zero counter, no
+    workgroup took the last ticket and the outputs were never written."""
+    if request.param == "fused":
+        monkeypatch.setenv("ORBX_BF_FUSED", "1")
+    else:
+        monkeypatch.delenv("ORBX_BF_FUSED", raising=False)
+    return request.param
+
+
 def test_descriptor_distance(gpu):
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
@@ -33,7 +46,7 @@ def test_descriptor_distance(gpu):
 
 
 @pytest.mark.parametrize("nq,nt", [(2000, 2000), (1, 1), (37, 5000), (3000, 700), (64, 0)])
-def test_bf_match_c3(gpu, nq, nt):
+def test_bf_match_c3(gpu, bf_mode, nq, nt):
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
     q, t = S.planted_pairs(7, nq, max(nt, 1))
@@ -46,7 +59,7 @@ def test_bf_match_c3(gpu, nq, nt):
 
 
 @pytest.mark.parametrize("P,nq,nt", [(1, 2000, 2000), (16, 2000, 2000), (5, 300, 17), (3, 64, 0), (70, 33, 1200)])
-def test_bf_match_batch_device(gpu, P, nq, nt):
+def test_bf_match_batch_device(gpu, bf_mode, P, nq, nt):
     """orbx_bf_match_batch_device: P independent all-pairs problems in one launch, each equal to the oracle's."""
     import torch
     import multiagent_orb_slam2_amd as pkg
@@ -67,7 +80,7 @@ def test_bf_match_batch_device(gpu, P, nq, nt):
             assert np.array_equal(g, r), (z, name)
 
 
-def test_bf_match_ties_and_full_distance(gpu):
+def test_bf_match_ties_and_full_distance(gpu, bf_mode):
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
     q = np.zeros((3, 32), np.uint8)
@@ -230,7 +243,7 @@ def test_search_for_triangulation(gpu, only_stereo):
     assert n == rn and np.array_equal(m12, rm)
 
 
-def test_bf_match_ties_across_chunks(gpu):
+def test_bf_match_ties_across_chunks(gpu, bf_mode):
     """Long train sets split into many chunks (the grouped merge): equal distances in different chunks keep the first
     train index, and the second distance counts the tie (strict '<' of ORBmatcher.cc:568-598)."""
     import multiagent_orb_slam2_amd as pkg
