@@ -88,10 +88,10 @@ __device__ __forceinline__ void bf_fold_write(const uint32_t* __restrict__ pb, c
 // partial record: best (dist << 20 | train idx), second dist.  blockIdx.z = problem: query set z at q + z*q_stride,
 // train set z at t + z*t_stride (bytes), partials at z * nchunks * nq.
 // kFused: the chunk workgroup of a (problem, query block) that arrives last folds the block's partials itself (no
-// k_bf_merge launch).  Hand-off (MI355X: per-XCD L2s are not coherent): partials by plain stores, every wave drains
-// them (vmcnt 0), barrier, lane 0 releases at agent scope and takes a ticket (relaxed agent fetch_add on the block's
-// counter); the ticket nchunks - 1 resets the counter, acquires at agent scope, and after a barrier every wave reads
-// the partials with plain loads.  The counters are zeroed when they are allocated and by each last arriver.
+// k_bf_merge launch).  Hand-off (MI355X: per-XCD L2s are not coherent): partials by write-through (sc1) stores, so no
+// release fence; every wave drains them (vmcnt 0), barrier, lane 0 takes a ticket (relaxed agent fetch_add on the
+// block's counter); the ticket nchunks - 1 resets the counter, acquires at agent scope, and after a barrier every wave
+// reads the partials with plain loads.  The counters are zeroed when they are allocated and by each last arriver.
 template <bool kFused>
 __global__ __launch_bounds__(256) void k_bf_tile(const uint8_t* __restrict__ q, int nq, size_t q_stride, const uint8_t* __restrict__ t,
                                                  int nt, size_t t_stride, int chunk, uint32_t* __restrict__ pbest,
@@ -130,16 +130,19 @@ __global__ __launch_bounds__(256) void k_bf_tile(const uint8_t* __restrict__ q, 
     }
     if (qi < nq) {
         const size_t o = ((size_t)z * nch + c) * nq + qi;
-        pbest[o] = best;
-        psecond[o] = second;
+        if constexpr (kFused) {                 // write-through (sc1) stores: visible device-wide once drained
+            __hip_atomic_store(pbest + o, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(psecond + o, second, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            pbest[o] = best;
+            psecond[o] = second;
+        }
     }
     if constexpr (kFused) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // every wave: its partial stores done
         __syncthreads();
         int* flag = reinterpret_cast<int*>(tile);                        // the kernel's one LDS array (free now)
         if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");            // this XCD's dirty L2 lines written back
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             int* cnt = arrive + (size_t)z * gridDim.x + blockIdx.x;
             const int last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
             if (last) {
