@@ -117,6 +117,10 @@ def parse():
                     help="N>1 keyframe all-gather in the step: torch (torch.distributed all_gather_into_tensor; RCCL under "
                          "the nccl backend) or native (liborbx's orbx_exchange: its own RCCL communicator, the path a C++ "
                          "MultiAgentServer without torch takes; nccl backend only)")
+    ap.add_argument("--emulate-agents", type=int, default=0,
+                    help="diagnostics, N=1 only: the keyframe path as rank 0 of this many agents -- this rank's packets stand "
+                         "in for every agent's (copied rank-major into the ring as if all-gathered), so the KeyFrameDatabase "
+                         "and ring carry an N-agent load on one GPU (not a scaling figure: no collective, one front end)")
     ap.add_argument("--xgmi-mb", default="0.17,2,16,64",
                     help="N>1: per-rank payloads (MB) of the all-gather bandwidth sweep after the timed steps (empty = skip)")
     ap.add_argument("--sync-each", action="store_true",
@@ -908,6 +912,8 @@ def main():
     nd = max(1, min(args.distinct, B)) if args.distinct > 0 else (B - B % KF_EVERY if B >= KF_EVERY else B)
     # this agent's contiguous chunk of one synthetic sequence (generic_split_seq.cc:543-589); frame f of the
     # sequence is the synthetic stereo pair of seed f
+    emu = max(args.emulate_agents, 1) if world == 1 else 1
+    kfw = world if world > 1 else emu                 # agents whose keyframes fill the ring (emulated at N = 1)
     chunk = MA.split_sequence(cfg["seq_frames"], world)[rank]
     # frame f of the sequence shows synthetic scene f mod nd: every agent's chunk revisits the same nd scenes (in its
     # own order), as agents exploring one area do -- MapFusion's cross-agent candidates exist at every N, so the
@@ -966,8 +972,8 @@ def main():
         exchange = (MA.NativeKeyframeExchange(timed=not args.no_timing, device=dev.index) if args.exchange == "native"
                     else MA.KeyframeExchange(timed=not args.no_timing))
     engine = pkg.KeyframeFusionEngine(vocab, pkg.ORBmatcher(0.75, True, device=dev.index), cap,
-                                      slots=STORE_STEPS * world * n_kf, max_keyframes=n_kf, candidates=KF_CANDIDATES,
-                                      agent=rank, world=world, device=dev.index)
+                                      slots=STORE_STEPS * kfw * n_kf, max_keyframes=n_kf, candidates=KF_CANDIDATES,
+                                      agent=rank, world=kfw, device=dev.index)
     # every 5th frame of the sequence becomes a keyframe: batch rows kf_off + 5j, the frames of the chunk = 0 mod 5
     # (kf_off <= 4, so the 51 rows of a 256-frame batch end at row <= 254)
     kf_off = (-chunk.start) % KF_EVERY
@@ -985,7 +991,7 @@ def main():
         """(new slots, neighbour slots) of this agent's keyframes q (a slot range) as device tensors and host arrays: the
         d-th previous keyframe of keyframe j sits (j - d) keyframes back in this agent's ring order."""
         if q.start not in tri_pat:
-            nq, per = len(q), world * n_kf
+            nq, per = len(q), kfw * n_kf
             nb = [[(q.start + ((j - d) // nq) * per + (j - d) % nq) % engine.slots for d in range(1, TRI_NEIGHBOURS + 1)]
                   for j in range(nq)]
             tri_pat[q.start] = (torch.tensor(list(q), dtype=torch.int32, device=dev),
@@ -1007,12 +1013,12 @@ def main():
     fuse = None
     kf_rows_t = torch.tensor(list(kf_rows), dtype=torch.int64, device=dev)
     if args.fuse:
-        twc_s, views_s = geo.slot_tables(engine.slots, world, n_kf)
+        twc_s, views_s = geo.slot_tables(engine.slots, kfw, n_kf)
         fuse = MA.LocalFuse(pkg.ORBmatcher(0.6, True, device=dev.index), engine.store, engine.slots, cap, grid, geo.camera,
                             BF, scale, log_sf, inv_sigma2, twc_s, views_s, dev)
-    if world > 1:
+    if kfw > 1:
         send = torch.empty((n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
-        gathered = torch.empty((world * n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
+        gathered = torch.empty((kfw * n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
     frame_no = [chunk.start]
     n_step = [0]
 
@@ -1101,12 +1107,15 @@ def main():
         if time_stereo:
             e2 = torch.cuda.Event(enable_timing=True)
             e2.record(kf_stream)
-        if world == 1:
+        if kfw == 1:
             engine.step(kps, desc, cnt, kf_rows, frame_no[0] + kf_off, KF_EVERY, depth=depth, stream=kf_stream)
         else:
             engine.pack(kps, desc, cnt, kf_rows, frame_no[0] + kf_off, KF_EVERY, depth=depth, send=send, stream=kf_stream)
             with torch.cuda.stream(kf_stream):
-                exchange.exchange(send, out=gathered)
+                if world > 1:
+                    exchange.exchange(send, out=gathered)
+                else:                                  # --emulate-agents: every agent's block is this rank's packets
+                    gathered.view(kfw, n_kf, -1).copy_(send.unsqueeze(0).expand(kfw, -1, -1))
             engine.commit(gathered, stream=kf_stream)
         if time_stereo:
             e3 = torch.cuda.Event(enable_timing=True)
@@ -1233,6 +1242,10 @@ def main():
     }
     if world > devices_used:
         out["rehearsal"] = f"{world} ranks sharing {devices_used} GPU(s): not a scaling measurement"
+    if emu > 1:
+        out["emulated_agents"] = {"agents": emu, "ring_slots": engine.slots,
+                                  "note": "diagnostics: rank 0's keyframe path under an N-agent ring load on one GPU; the "
+                                          "packets are this rank's own copied N times, no collective"}
 
     if not args.no_timing:
         st, calls = {}, 0
