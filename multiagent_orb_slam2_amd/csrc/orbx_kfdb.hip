@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -782,13 +783,18 @@ int rebuild_inverted_file(orbx_kfdb* db, hipStream_t s) {
     return ORBX_OK;
 }
 
-constexpr int kPairwiseMaxMembers = 2048;   // auto strategy: below this, intersect pairwise (no inverted file)
+// auto strategy: up to this many members, intersect pairwise (no inverted file); ORBX_KFDB_PAIRWISE_MAX overrides
+// (diagnostics: A/B of the two strategies at a given ring size)
+static int pairwise_max_members() {
+    static const int v = [] { const char* e = std::getenv("ORBX_KFDB_PAIRWISE_MAX"); return e ? std::atoi(e) : 2048; }();
+    return v;
+}
 
 // The query batch on stream s; d_* are device pointers.  Scratch rows at 'base' (nq x S).
 int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned char* base, int32_t* d_out, int out_stride,
                  int32_t* d_out_n, int32_t* d_status, hipStream_t s) {
     const bool pairwise = db->strategy == ORBX_KFDB_PAIRWISE ||
-                          (db->strategy == ORBX_KFDB_AUTO && (int)db->members.size() <= kPairwiseMaxMembers);
+                          (db->strategy == ORBX_KFDB_AUTO && (int)db->members.size() <= pairwise_max_members());
     int st = pairwise ? upload_membership(db, s) : rebuild_inverted_file(db, s);
     if (st) return st;
     QScratch X;
