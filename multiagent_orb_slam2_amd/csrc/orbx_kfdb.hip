@@ -285,19 +285,18 @@ __global__ __launch_bounds__(256) void k_kfdb_share(DbDev D, QueryIn Q, QScratch
 }
 
 // Small databases: no inverted file.  One wave per (query, slot) intersects the slot's BowVector with the
-// query's and produces the same word count and first shared query word as k_kfdb_share -- plus the L1 score, summed in
-// ascending word order as k_kfdb_score does.  The query's words sit in an LDS hash table (open addressing, load <= 1/2,
-// word -> its index in the query's ascending list): one or two probes per slot word instead of a binary search's
-// ~log2(n) dependent LDS reads (r5: the kernel grows with the ring -- 3 steps x agents x 51 slots -- 0.07 ms per step
-// at one agent, 0.38 at eight before the table).
+// query's and produces the same word count and first shared query word as k_kfdb_share.  The query's words sit in an
+// LDS hash table (open addressing, load <= 1/2, word -> its index in the query's ascending list).  The L1 scores are
+// left to k_kfdb_score, for the keyframes that pass minCommonWords only (:113-126), as on the inverted-file path: the
+// score is a sequential double sum in word order, one lane at a time, and summing it for every (query, slot) pair was
+// most of this kernel's time (r5: 0.07 ms per step at one agent, 0.36 at eight, where the ring holds 1,224 slots).
 constexpr uint32_t kHashEmpty = 0xffffffffu;
 __device__ __forceinline__ uint32_t kfdb_hash(uint32_t w, int log_t) { return (w * 0x9e3779b1u) >> (32 - log_t); }
 
 __global__ __launch_bounds__(512) void k_kfdb_pairwise(DbDev D, QueryIn Q, QScratch X, int kind, int log_t) {
     extern __shared__ unsigned char smem[];
     const int T = 1 << log_t, mask = T - 1;
-    double* qv = reinterpret_cast<double*>(smem);                  // [maxw] query values by list index
-    uint32_t* hk = reinterpret_cast<uint32_t*>(qv + D.maxw);       // [T] word keys (kHashEmpty = free)
+    uint32_t* hk = reinterpret_cast<uint32_t*>(smem);               // [T] word keys (kHashEmpty = free)
     uint16_t* hi = reinterpret_cast<uint16_t*>(hk + T);            // [T] list index of the key
     const int q = blockIdx.y;
     const int qs = Q.slot[q];
@@ -306,7 +305,6 @@ __global__ __launch_bounds__(512) void k_kfdb_pairwise(DbDev D, QueryIn Q, QScra
     __syncthreads();
     for (int i = threadIdx.x; i < nq; i += blockDim.x) {              // BowVector words are distinct: no duplicate keys
         const uint32_t w = D.bw[(size_t)qs * D.maxw + i];
-        qv[i] = D.bv[(size_t)qs * D.maxw + i];
         for (uint32_t h = kfdb_hash(w, log_t);; h = (h + 1) & mask) {
             if (atomicCAS(&hk[h], kHashEmpty, w) == kHashEmpty) { hi[h] = (uint16_t)i; break; }
         }
@@ -315,43 +313,26 @@ __global__ __launch_bounds__(512) void k_kfdb_pairwise(DbDev D, QueryIn Q, QScra
     const int waves = blockDim.x / kWave;
     const size_t row = (size_t)q * D.S;
     for (int k = blockIdx.x * waves + (int)(threadIdx.x / kWave); k < D.S; k += gridDim.x * waves) {
-        int c = 0, first = 0x7f7f7f7f;
-        double score = 0.0;
-        if (kf_visible(D, Q, q, k) && !(kind == KIND_COVIS && excl_at(X, row + k))) {
+        int c = 0;
+        uint32_t first = 0x7f7f7f7fu;
+        if (kf_visible(D, Q, q, k) && !(kind == KIND_COVIS && excl_at(X, row + k)) && nq > 0) {
             const uint32_t* cw = D.bw + (size_t)k * D.maxw;
-            const double* cv = D.bv + (size_t)k * D.maxw;
             const int nc = D.bn[k];
-            for (int base = 0; base < nc; base += kWave) {
-                const int i = base + lane_id();
-                double term = 0.0;
-                int pos = 0x7f7f7f7f;
-                bool found = false;
-                if (i < nc && nq > 0) {
-                    const uint32_t w = cw[i];
-                    uint32_t h = kfdb_hash(w, log_t), key;
-                    while ((key = hk[h]) != kHashEmpty && key != w) h = (h + 1) & mask;
-                    if (key == w) {
-                        const int lo = hi[h];
-                        const double vi = qv[lo], wi = cv[i];
-                        term = __dsub_rn(__dsub_rn(fabs(__dsub_rn(vi, wi)), fabs(vi)), fabs(wi));
-                        pos = lo;
-                        found = true;
-                    }
-                }
-                uint64_t m = __ballot(found);
-                c += __popcll(m);
-                first = min(first, (int)wave_min_u32((uint32_t)pos));
-                while (m) {
-                    const int l = __builtin_ctzll(m);
-                    score = __dadd_rn(score, readlane_f64(term, l));
-                    m &= m - 1;
+            for (int i = lane_id(); i < nc; i += kWave) {
+                const uint32_t w = cw[i];
+                uint32_t h = kfdb_hash(w, log_t), key;
+                while ((key = hk[h]) != kHashEmpty && key != w) h = (h + 1) & mask;
+                if (key == w) {
+                    ++c;
+                    first = min(first, (uint32_t)hi[h]);
                 }
             }
+            c = wave_sum(c);
+            first = wave_min_u32(first);
         }
         if (lane_id() == 0) {
             X.cnt[row + k] = c;
-            X.first[row + k] = first;
-            X.si[row + k] = (float)(-score / 2.0);
+            X.first[row + k] = (int)first;
         }
     }
 }
@@ -812,7 +793,7 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
         const int gx = std::min((db->S + 7) / 8, 64);
         int log_t = 1;
         while ((1 << log_t) < 2 * db->maxw) ++log_t;                // load factor <= 1/2
-        const size_t plds = (size_t)db->maxw * sizeof(double) + ((size_t)6 << log_t);
+        const size_t plds = (size_t)6 << log_t;
         ORBX_REQUIRE(plds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "pairwise LDS %zu B", plds);
         if (plds > 64 * 1024)
             ORBX_HIP(hipFuncSetAttribute((const void*)k_kfdb_pairwise, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));
@@ -823,7 +804,7 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
         hipLaunchKernelGGL(k_kfdb_share, dim3((db->maxw + 255) / 256, nq), dim3(256), 0, s, D, Q, X, kind);
     }
     hipLaunchKernelGGL(k_kfdb_select, dim3(nq), dim3(1024), 0, s, D, Q, X, St, kind);
-    if (!pairwise) hipLaunchKernelGGL(k_kfdb_score, dim3(32, nq), dim3(256), lds, s, D, Q, X);
+    hipLaunchKernelGGL(k_kfdb_score, dim3(32, nq), dim3(256), lds, s, D, Q, X);   // the minCommonWords candidates
     hipLaunchKernelGGL(k_kfdb_accum, dim3(nq), dim3(256), 0, s, D, Q, X, St, kind, d_out, out_stride, d_out_n, d_status);
     hipLaunchKernelGGL(k_kfdb_state, dim3((db->S + 255) / 256), dim3(256), 0, s, D, Q, X, St, kind, nq, d_status);
     ORBX_HIP(hipGetLastError());
