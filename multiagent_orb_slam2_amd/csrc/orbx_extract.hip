@@ -2009,7 +2009,11 @@ struct Extractor {
     uint8_t* d_pyr_ring = nullptr;    // pyr_ring sets of max_batch pyramids: a caller that reads the pyramid of call
     int pyr_ring = 1;                 // k (Frame::ComputeStereoMatches' SAD step) on another stream can overlap call
     unsigned long long ncalls = 0;    // k+1, which writes the next set
-    uint8_t* d_blur = nullptr;
+    uint8_t* d_blur = nullptr;        // desc_sets sets of the blurred pyramid / kept keypoints (d_*_c: the current call's)
+    uint8_t* d_blur_c = nullptr;
+    int desc_sets = 1;                // ORBX_DESC_SETS=2: call k + 1's blur and DistributeOctTree write the other set
+    unsigned long long dcalls = 0;    // while call k's describe reads its own (no wait on that describe)
+    int dset_call[2] = {-1, -1};      // event-pool index of the last call that used each set
     uint32_t* d_cand_xy = nullptr;
     uint8_t* d_cand_s = nullptr;
     int* d_cell_cnt = nullptr;
@@ -2019,6 +2023,9 @@ struct Extractor {
     uint32_t* d_lvl_xy = nullptr;
     uint8_t* d_lvl_r = nullptr;
     int* d_lvl_cnt = nullptr;
+    uint32_t* d_lvl_xy_c = nullptr;
+    uint8_t* d_lvl_r_c = nullptr;
+    int* d_lvl_cnt_c = nullptr;
     int* d_err = nullptr;
     // host-API staging: the image is packed into pinned host memory and goes over PCIe as one DMA (a pageable
     // 2-D copy of an odd-width image falls back to per-row transfers); results come back through pinned memory
@@ -2442,16 +2449,24 @@ int Extractor::configure(int r, int c, int batch) {
     if ((st = dev_alloc(&d_pyr_ring, (size_t)pyr_ring * B * pyr_size))) return st;
     d_pyr = d_pyr_ring;
     ncalls = 0;
-    if ((st = dev_alloc(&d_blur, B * pyr_size))) return st;
+    {
+        const char* v = std::getenv("ORBX_DESC_SETS");
+        desc_sets = (v && std::atoi(v) == 2) ? 2 : 1;
+    }
+    dcalls = 0;
+    dset_call[0] = dset_call[1] = -1;
+    if ((st = dev_alloc(&d_blur, (size_t)desc_sets * B * pyr_size))) return st;
+    d_blur_c = d_blur;
     if ((st = dev_alloc(&d_cand_xy, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_cand_s, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_cell_cnt, B * std::max<size_t>(cellv.size(), 1)))) return st;
     if ((st = dev_alloc(&d_key_xy, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_key_r, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_key_node, B * cand_stride))) return st;
-    if ((st = dev_alloc(&d_lvl_xy, B * out_stride))) return st;
-    if ((st = dev_alloc(&d_lvl_r, B * out_stride))) return st;
-    if ((st = dev_alloc(&d_lvl_cnt, B * nlevels))) return st;
+    if ((st = dev_alloc(&d_lvl_xy, (size_t)desc_sets * B * out_stride))) return st;
+    if ((st = dev_alloc(&d_lvl_r, (size_t)desc_sets * B * out_stride))) return st;
+    if ((st = dev_alloc(&d_lvl_cnt, (size_t)desc_sets * B * nlevels))) return st;
+    d_lvl_xy_c = d_lvl_xy; d_lvl_r_c = d_lvl_r; d_lvl_cnt_c = d_lvl_cnt;
     if ((st = dev_alloc(&d_err, 1))) return st;
     // diagnostics: delay the null stream right before the counter initialisation (tests/test_gpu_ordering.py)
     if (const char* dl = std::getenv("ORBX_DEBUG_UPLOAD_DELAY_MS")) ORBX_HIP(debug_spin(nullptr, std::atof(dl)));
@@ -2492,6 +2507,14 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     const unsigned seq = ++e->call_seq;                             // ordering canary stamp (k_quadtree -> describe)
     const int slot = (int)(e->ncalls++ % (unsigned long long)e->pyr_ring);
     e->d_pyr = e->d_pyr_ring + (size_t)slot * e->max_batch * ps;
+    const int dset = (int)(e->dcalls++ % (unsigned long long)e->desc_sets);
+    {
+        const size_t B = (size_t)e->max_batch;
+        e->d_blur_c = e->d_blur + (size_t)dset * B * ps;
+        e->d_lvl_xy_c = e->d_lvl_xy + (size_t)dset * B * e->out_stride;
+        e->d_lvl_r_c = e->d_lvl_r + (size_t)dset * B * e->out_stride;
+        e->d_lvl_cnt_c = e->d_lvl_cnt + (size_t)dset * B * nl;
+    }
     // this call's events: the pool entry of 32 calls ago, whose describe (and every wait on its events) is long done
     const int ci = (int)(e->cev_next++ % Extractor::kCallEv);
     Extractor::CallEvents& ce = e->cev[ci];
@@ -2502,9 +2525,10 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : (k == 4 || k == 5) ? so : s);
     };
     // the previous call's describe (possibly on another stream) reads the kept keypoints and the blurred pyramid
+    // the last describe that read this call's set of kept keypoints / blurred pyramid (the previous call's with one set)
     auto after_prev_describe = [&](hipStream_t q) -> int {
-        if (e->last_call >= 0 && !e->dbg_skip_desc_wait && !e->capturing)
-            ORBX_HIP(hipStreamWaitEvent(q, e->cev[e->last_call].desc, 0));
+        const int prev = e->dset_call[dset];
+        if (prev >= 0 && !e->dbg_skip_desc_wait && !e->capturing) ORBX_HIP(hipStreamWaitEvent(q, e->cev[prev].desc, 0));
         return ORBX_OK;
     };
     const int ncells = (int)e->cellv.size();
@@ -2524,13 +2548,13 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         if (n <= 0) return;
         const int kc = lvl0 == 0 ? e->qt_keys[0] : e->qt_keys[1];  // LDS key capacity: level 0 / levels >= 1
         hipLaunchKernelGGL(k_quadtree, dim3(n, batch), dim3(kQtThreads), e->qt_lds + 7 * (size_t)kc, q, e->d_levels, e->d_cells,
-                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy,
-                           e->d_lvl_r, e->out_stride, e->d_lvl_cnt, nl, e->node_cap, e->scan_cap, e->d_err, lvl0,
+                           e->d_cand_xy, e->d_cand_s, e->cand_stride, e->d_cell_cnt, std::max(ncells, 1), qs, e->d_lvl_xy_c,
+                           e->d_lvl_r_c, e->out_stride, e->d_lvl_cnt_c, nl, e->node_cap, e->scan_cap, e->d_err, lvl0,
                            (int)e->qt_lds, kc, seq);
     };
     auto blur = [&](hipStream_t q, int tile0, int n) {
         if (n <= 0) return;
-        hipLaunchKernelGGL(k_blur7, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur, ps,
+        hipLaunchKernelGGL(k_blur7, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur_c, ps,
                            e->d_levels, e->d_tiles, n, batch, s0, tile0);
     };
 
@@ -2620,8 +2644,8 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         const int nslots = e->out_stride;                           // every level's slots; the launch writes the counts
         constexpr int kpw = 2;                                      // keypoints per wave
         dim3 g(kXcds * xcd_chunk((nslots + 4 * kpw - 1) / (4 * kpw) * batch));
-        hipLaunchKernelGGL(k_describe_m<kpw>, g, dim3(256), 0, so, e->d_pyr, e->d_blur, ps, e->d_levels, nl, e->d_lvl_xy,
-                           e->d_lvl_r, e->out_stride, e->d_lvl_cnt, d_kps, d_desc, d_counts, capacity, 0, nslots, 1, batch,
+        hipLaunchKernelGGL(k_describe_m<kpw>, g, dim3(256), 0, so, e->d_pyr, e->d_blur_c, ps, e->d_levels, nl, e->d_lvl_xy_c,
+                           e->d_lvl_r_c, e->out_stride, e->d_lvl_cnt_c, d_kps, d_desc, d_counts, capacity, 0, nslots, 1, batch,
                            s0, tab, seq, e->d_err);
     }
     mark(5);
@@ -2630,10 +2654,12 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         ce.used = false;
         e->slot_call[slot] = -1;
         e->last_call = -1;
+        e->dset_call[dset] = -1;
     } else {
         ce.used = true;
         e->slot_call[slot] = ci;
         e->last_call = ci;
+        e->dset_call[dset] = ci;
         e->async_pending = true;
     }
     ORBX_HIP(hipGetLastError());
@@ -3034,7 +3060,7 @@ int orbx_extractor_copy_blurred_level(orbx_extractor* e, int index, int level, u
     ORBX_REQUIRE(dst_step >= (size_t)w, ORBX_ERR_ARG, "bad destination");
     ORBX_HIP(hipSetDevice(e->device));
     ORBX_HIP(hipDeviceSynchronize());                                  // the last call's blur may run on any of its streams
-    const uint8_t* p = e->d_blur + (size_t)index * e->pyr_size + e->lv[level].pyr_off;   // as k_blur7 writes it
+    const uint8_t* p = e->d_blur_c + (size_t)index * e->pyr_size + e->lv[level].pyr_off;   // as k_blur7 writes it
     ORBX_HIP(hipMemcpy2D(dst, dst_step, p, (size_t)w, (size_t)w, (size_t)h, hipMemcpyDeviceToHost));
     return ORBX_OK;
 }
