@@ -1031,6 +1031,7 @@ def main():
     host_split = [0.0, 0.0]                            # host enqueue seconds: front-end, keyframe path
 
     last_handoff = [None]
+    timeline = []                                      # per timed step: {point: event}, read after the timed region
 
     def step(time_stereo=False, src=None):
         h0 = time.perf_counter()
@@ -1051,9 +1052,16 @@ def main():
             stream.wait_event(stereo_done[pslot])     # the resize chain overwrites the set that stereo step read
         if src is None:
             src = img_sets[n_step[0] % len(img_sets)]
+        tl = {}                                        # timeline events of this step (timed steps only)
+        if time_stereo:
+            tl["front_end_start"] = torch.cuda.Event(enable_timing=True)
+            tl["front_end_start"].record(stream)
         ex.extract_batch_device(src, kps, desc, cnt, stream=stream, out_stream=dstream)
-        extracted = torch.cuda.Event()
+        extracted = torch.cuda.Event(enable_timing=time_stereo)
         extracted.record(ostream)
+        if time_stereo:
+            tl["describe_end"] = extracted
+            timeline.append(tl)
         pyr = ex.pyramid_device()                      # this call's pyramid set (a slot of the ring of 2)
         if "stereo" in skip:
             n_step[0] += 1
@@ -1071,6 +1079,7 @@ def main():
             if time_stereo:
                 e1.record(stereo_stream)
                 stereo_ms.append((e0, e1))
+                tl["stereo_start"], tl["stereo_end"] = e0, e1
             if tracker is not None and args.track_stream == "stereo":
                 # Tracking's matches of every frame: TrackWithMotionModel's SearchByProjection(F, LastF) and
                 # SearchLocalPoints (Tracking.cc:882-904, :1160-1205) on the frame's stereo MapPoints
@@ -1079,6 +1088,7 @@ def main():
                     e1t = torch.cuda.Event(enable_timing=True)
                     e1t.record(stereo_stream)
                     track_ms.append((e1, e1t))
+                    tl["tracking_end"] = e1t
         handoff = torch.cuda.Event()
         handoff.record(stereo_stream)
         stereo_done[pslot] = handoff
@@ -1121,6 +1131,7 @@ def main():
             e3 = torch.cuda.Event(enable_timing=True)
             e3.record(kf_stream)
             kf_ms.append((e2, e3))
+            tl["keyframe_start"], tl["keyframe_bow_fusion_end"] = e2, e3
         qs = engine.last_step()[1]
         ns, nb, ns_h, nb_h = tri_pattern(qs)
         e5 = e3 if time_stereo else None
@@ -1140,6 +1151,7 @@ def main():
                 e6 = torch.cuda.Event(enable_timing=True)
                 e6.record(kf_stream)
                 fuse_ms.append((e5, e6))
+                tl["keyframe_end"] = e6
         done = torch.cuda.Event()
         done.record(kf_stream)
         kf_done[buf] = done
@@ -1175,6 +1187,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    tl_base = torch.cuda.Event(enable_timing=True)
+    tl_base.record(streams[0])
     t0 = time.perf_counter()
     host_s = 0.0
     split0 = list(host_split)
@@ -1269,6 +1283,15 @@ def main():
         if trk:
             per_call["tracking_match"] = float(np.mean(trk))           # after stereo_match, the stereo stream
         out["stage_ms_per_step"] = {k: round(v, 4) for k, v in per_call.items()}
+        if len(timeline) >= 4:
+            # when each stage of step i happens, relative to step i's front-end start (the launch stream reaching the
+            # extraction, after its waits); medians over the timed steps from the 2nd on.  Read with the period
+            # (median front-end start to the next step's) to see how consecutive steps overlap.
+            offs = [{k: tl_base.elapsed_time(e) for k, e in t.items()} for t in timeline]
+            period = [offs[i + 1]["front_end_start"] - offs[i]["front_end_start"] for i in range(1, len(offs) - 1)]
+            rel = {k: round(float(np.median([o[k] - o["front_end_start"] for o in offs[1:] if k in o])), 3)
+                   for k in offs[1]}
+            out["timeline_ms"] = dict(rel, step_period=round(float(np.median(period)), 3))
         out["roofline"], sec = roofline_lines(per_call, cfg, 2 * B, args.config)
         if sec:
             out["roofline_secondary"] = sec
