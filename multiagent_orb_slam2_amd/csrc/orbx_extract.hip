@@ -512,11 +512,36 @@ __device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, 
 struct WaveLds {               // per-wave slice of k_fast_wave's dynamic LDS (byte offsets inside the slice)
     int o_sc, o_list, bytes;   // E pair image at 0 (the NMS key lists reuse it), score map, survivor list; slice size
 };
-// rows: max ROI rows; sw: max score-map row (int16); np: max pixel pairs; iw: pair-image dwords (fastw_image_words)
-__host__ __device__ __forceinline__ WaveLds wave_lds(int rows, int sw, int np, int iw) {
+// The same rule on a u8 score map holding s + 1 (0 = no score / -1, never a corner and never blocking): per row the 4
+// bytes of columns 2j+1 .. 2j+4 (two aligned dwords and one v_alignbyte), spread into u16 pairs by v_perm and maxed
+// with v_pk_max_u16; the map is half the LDS of the i16 form.
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2v as_u2(uint32_t v) { return __builtin_bit_cast(u16x2v, v); }
+__device__ __forceinline__ uint32_t sc_row4(const uint8_t* __restrict__ scb, int b) {    // bytes b .. b+3
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(scb + (b & ~3));
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(b & 3));
+}
+__device__ __forceinline__ int nms_pair_u8(const uint8_t* __restrict__ scb, int SWB, int rr, int j, int T1, int T2,
+                                           bool second) {
+    const int b = rr * SWB + 2 * j + 1;
+    const uint32_t x0 = sc_row4(scb, b), x1 = sc_row4(scb, b + SWB), x2 = sc_row4(scb, b + 2 * SWB);
+    auto p01 = [](uint32_t x) { return as_u2(__builtin_amdgcn_perm(x, x, 0x0c010c00u)); };
+    auto p12 = [](uint32_t x) { return as_u2(__builtin_amdgcn_perm(x, x, 0x0c020c01u)); };
+    auto p23 = [](uint32_t x) { return as_u2(__builtin_amdgcn_perm(x, x, 0x0c030c02u)); };
+    u16x2v m = __builtin_elementwise_max(__builtin_elementwise_max(p01(x0), p12(x0)), p23(x0));
+    m = __builtin_elementwise_max(m, __builtin_elementwise_max(__builtin_elementwise_max(p01(x2), p12(x2)), p23(x2)));
+    m = __builtin_elementwise_max(m, __builtin_elementwise_max(p01(x1), p23(x1)));    // the middle row without the pair
+    const u16x2v sv = p12(x1);
+    const int g0 = sv.x > m.x, g1 = second && (sv.y > m.y);
+    const int t1 = T1 + 1, t2 = T2 + 1;
+    return (g0 & (sv.x >= t1)) | ((g1 & (sv.y >= t1)) << 1) | ((g0 & (sv.x >= t2)) << 2) | ((g1 & (sv.y >= t2)) << 3);
+}
+
+// rows: max ROI rows; scrow: score-map row bytes; np: max pixel pairs; iw: pair-image dwords (fastw_image_words)
+__host__ __device__ __forceinline__ WaveLds wave_lds(int rows, int scrow, int np, int iw) {
     WaveLds b;
     int o = (iw * 4 + 15) & ~15;
-    b.o_sc = o;   o += ((rows - 4) * sw * 2 + 15) & ~15;
+    b.o_sc = o;   o += ((rows - 4) * scrow + 15) & ~15;
     b.o_list = o; o += (np * 2 + 15) & ~15;
     b.bytes = o;
     return b;
@@ -640,14 +665,29 @@ __device__ __forceinline__ int rank_below(uint64_t b, int acc = 0) {
                             // CU at levels >= 1 / level 0 instead of 4 / 5: serial FAST 1.153 -> 1.060 ms, step +0.9 %
 #endif
 __host__ __device__ constexpr int fastw_sw(int ps) { return ps == 19 ? ORBX_FAST_SW19 : 76; }
+// score map as u8 (s + 1) instead of i16: ORBX_FAST_U8SC=1 (the NMS reads bytes 2j+1 .. 2j+8 of a row: row >= Wd + 8)
+#ifndef ORBX_FAST_U8SC
+#define ORBX_FAST_U8SC 0
+#endif
+constexpr bool kScU8 = ORBX_FAST_U8SC != 0;
+__host__ __device__ constexpr int fastw_scrow(int ps) { return kScU8 ? (ps == 19 ? 40 : 80) : 2 * fastw_sw(ps); }
+
+__device__ __forceinline__ void sc_store(uint8_t* __restrict__ scb, int SWB, int rr, int j, s16x2 v, bool second) {
+    if constexpr (kScU8) {
+        const uint32_t u = ((uint32_t)(v.x + 1) & 0xffu) | (second ? (((uint32_t)(v.y + 1) & 0xffu) << 8) : 0u);
+        *reinterpret_cast<uint16_t*>(scb + (rr + 1) * SWB + 2 + 2 * j) = (uint16_t)u;
+    } else {
+        *reinterpret_cast<s16x2*>(scb + (rr + 1) * SWB + 4 + 4 * j) = second ? v : (s16x2){v.x, (short)-1};
+    }
+}
 
 // The part of a cell after its ROI is in LDS: pre-test, scores, NMS at both thresholds, the cell's candidate slots.
 template <int kPS, int kPC>
-__device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __restrict__ sc, uint16_t* __restrict__ list,
+__device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __restrict__ scb, uint16_t* __restrict__ list,
                                            const CellDev& cd, int img, int* __restrict__ cnt_out, int Wd, int Hd, int T1,
                                            int T2, int tp, uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
                                            int cand_stride, int kcap, int two_pass, int ln) {
-    constexpr int SW = fastw_sw(kPS);
+    constexpr int SWB = fastw_scrow(kPS);                             // score-map row bytes
     wave_fence();
     // 2. compass pre-test at min(iniTh, minTh) in quads; survivors compacted in row-major order
     const int PR = (Wd + 1) >> 1, QR = (PR + 3) >> 2, NQ4 = Hd * QR;
@@ -707,8 +747,8 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
                 fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
                 fast_taps_f16<kPS, kPC>(E, rr2 + 3, j2, t2);
                 const s16x2 s1 = fast_score_from_taps_f16(t1), s2 = fast_score_from_taps_f16(t2);
-                *(s16x2*)(sc + (rr1 + 1) * SW + 2 + 2 * j1) = (2 * j1 + 1 < Wd) ? s1 : (s16x2){s1.x, (short)-1};
-                if (i2 < ns) *(s16x2*)(sc + (rr2 + 1) * SW + 2 + 2 * j2) = (2 * j2 + 1 < Wd) ? s2 : (s16x2){s2.x, (short)-1};
+                sc_store(scb, SWB, rr1, j1, s1, 2 * j1 + 1 < Wd);
+                if (i2 < ns) sc_store(scb, SWB, rr2, j2, s2, 2 * j2 + 1 < Wd);
             }
         } else if (i < ns) {
             const uint32_t e1 = list[i];
@@ -716,7 +756,7 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
             uint32_t t1[17];
             fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
             const s16x2 s1 = fast_score_from_taps_f16(t1);
-            *(s16x2*)(sc + (rr1 + 1) * SW + 2 + 2 * j1) = (2 * j1 + 1 < Wd) ? s1 : (s16x2){s1.x, (short)-1};
+            sc_store(scb, SWB, rr1, j1, s1, 2 * j1 + 1 < Wd);
         }
     }
     wave_fence();
@@ -727,7 +767,8 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
         int f = 0, key = 0;
         if (i < ns) {
             const int rr = list[i] >> 8, j = list[i] & 0xff;
-            f = nms_pair(sc, SW, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
+            if constexpr (kScU8) f = nms_pair_u8(scb, SWB, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
+            else f = nms_pair(reinterpret_cast<const int16_t*>(scb), SWB / 2, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
             key = rr * 128 + 2 * j;
         }
         const uint64_t a0 = __ballot(f & 1), a1 = __ballot(f & 2), c0 = __ballot(f & 4), c1 = __ballot(f & 8);
@@ -751,7 +792,8 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, int16_t* __
     for (int i = ln; i < n; i += kWave) {
         const int k = ks[i], rr = k >> 7, x = k & 127;
         oxy[i] = (uint32_t)(cd.x0 + 3 + x) | ((uint32_t)(cd.y0 + rr + 3) << 16);
-        os[i] = (uint8_t)sc[(rr + 1) * SW + 2 + x];
+        if constexpr (kScU8) os[i] = (uint8_t)(scb[(rr + 1) * SWB + 2 + x] - 1);
+        else os[i] = (uint8_t)reinterpret_cast<const int16_t*>(scb)[(rr + 1) * (SWB / 2) + 2 + x];
     }
     if (ln == 0) *cnt_out = n;
 }
@@ -772,7 +814,7 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
     const int img = item / ncell, c = cell0 + (item - img * ncell);
     char* lds = reinterpret_cast<char*>(fsm) + w * lay.bytes;
     uint32_t* E = reinterpret_cast<uint32_t*>(lds);
-    int16_t* sc = reinterpret_cast<int16_t*>(lds + lay.o_sc);
+    uint8_t* scb = reinterpret_cast<uint8_t*>(lds + lay.o_sc);
     uint16_t* list = reinterpret_cast<uint16_t*>(lds + lay.o_list);
     const CellDev cd = cells[c];
     const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
@@ -783,7 +825,7 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
     }
     const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
     const int tp = min(T1, T2);
-    constexpr int SW = fastw_sw(kPS);
+    constexpr int SWB = fastw_scrow(kPS);
     {
         // 1. cell ROI -> f16-biased pair image: lane items (row, 8-column chunk), one 8-byte load each, all of a round
         //    issued before the first use; bytes past the ROI's width read as 0
@@ -872,10 +914,10 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
         }
         }
         // score map cleared to 0: pixels that fail the pre-test and the pad ring (a 0 never blocks a kept score >= 1)
-        const int n16 = ((Hd + 2) * SW * 2 + 15) >> 4;
-        for (int i = ln; i < n16; i += kWave) reinterpret_cast<uint4*>(sc)[i] = make_uint4(0, 0, 0, 0);
+        const int n16 = ((Hd + 2) * SWB + 15) >> 4;
+        for (int i = ln; i < n16; i += kWave) reinterpret_cast<uint4*>(scb)[i] = make_uint4(0, 0, 0, 0);
     }
-    fastw_body<kPS, kPC>(E, sc, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
+    fastw_body<kPS, kPC>(E, scb, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
 }
 
 // GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, integer separable path: taps {18,34,49,55,49,34,18},
@@ -2263,7 +2305,7 @@ int Extractor::configure(int r, int c, int batch) {
         const int iw = fastw_image_words(rows, wl.ps, wl.pc);
         wl.kcap = kcap;                                     // two u16 key lists inside the pair image: 4 * kcap bytes
         ORBX_REQUIRE(4 * kcap <= iw * 4, ORBX_ERR_UNSUPPORTED, "k_fast_wave key lists exceed the pair image");
-        wl.lay = wave_lds(rows, sw, np, iw);
+        wl.lay = wave_lds(rows, fastw_scrow(wl.ps), np, iw);
         const int bytes = kWaveWpg * wl.lay.bytes;
         ORBX_REQUIRE(bytes <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "k_fast_wave LDS %d B", bytes);
         if (bytes > 64 * 1024) {
