@@ -669,6 +669,9 @@ __host__ __device__ constexpr int fastw_sw(int ps) { return ps == 19 ? ORBX_FAST
 #ifndef ORBX_FAST_U8SC
 #define ORBX_FAST_U8SC 0
 #endif
+#ifndef ORBX_FAST_STOP
+#define ORBX_FAST_STOP 0   // diagnostics (wrong keypoints): 1 = ROI staging only, 2 = + pre-test, 3 = + scores
+#endif
 constexpr bool kScU8 = ORBX_FAST_U8SC != 0;
 __host__ __device__ constexpr int fastw_scrow(int ps) { return kScU8 ? (ps == 19 ? 40 : 80) : 2 * fastw_sw(ps); }
 
@@ -734,6 +737,11 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __
         }
     }
     wave_fence();
+#if ORBX_FAST_STOP == 2
+    if (ns < 0) list[0] = 0;                                          // (keeps the pre-test live)
+    if (ln == 0) *cnt_out = 0;                                        // diagnostics: staging + pre-test
+    return;
+#endif
     // 3. closed-form scores of the survivors, two per lane per round (both tap sets read before either is scored); a
     //    round with at most 64 survivors left (two cells in three at iniThFAST) scores one per lane
     for (int i0 = 0; i0 < ns; i0 += 2 * kWave) {
@@ -760,6 +768,10 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __
         }
     }
     wave_fence();
+#if ORBX_FAST_STOP == 3
+    if (ln == 0) *cnt_out = 0;                                        // diagnostics: staging + pre-test + scores
+    return;
+#endif
     // 4. strict 3x3 NMS at iniTh (bits 0, 1) and minTh (bits 2, 3); kept pixels appended in list order (= row-major)
     //    to the two key lists, which take over the pair image's LDS (key = row * 128 + column in the detection window)
     for (int i0 = 0; i0 < ns; i0 += kWave) {
@@ -917,6 +929,10 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
         const int n16 = ((Hd + 2) * SWB + 15) >> 4;
         for (int i = ln; i < n16; i += kWave) reinterpret_cast<uint4*>(scb)[i] = make_uint4(0, 0, 0, 0);
     }
+#if ORBX_FAST_STOP == 1
+    if (ln == 0) *cnt_out = 0;                                        // diagnostics: the ROI staging only
+    return;
+#endif
     fastw_body<kPS, kPC>(E, scb, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
 }
 
