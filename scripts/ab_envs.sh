@@ -16,6 +16,6 @@ for r in $(seq 1 $ROUNDS); do
     python3 -c "
 import json; d=json.loads(open('$log').read().strip().splitlines()[-1])
 a=d.get('roofline_alone',{}).get('stage_ms_alone',{}); s=d.get('stage_ms_per_step',{})
-print('r$r %-8s' % '$name', d['value'], d['ms_per_step'], 'alone', {k: round(v, 3) for k, v in a.items()}, 'fuse', s.get('keyframe_fuse'), 'trk', s.get('tracking_match'))"
+print('r$r %-8s' % '$name', d['value'], d['ms_per_step'], 'fast_busy_live', s.get('fast_busy'), 'blur_live', s.get('blur7'), 'alone', {k: round(v, 3) for k, v in a.items() if k in ('fast_busy', 'blur7', 'describe', 'resize')}, 'fuse', s.get('keyframe_fuse'), 'trk', s.get('tracking_match'))"
   done
 done
