@@ -334,12 +334,8 @@ __global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(o
     __syncthreads();
     if constexpr (!kAssign) {
         int acc = 0;
-        // the next query's record is loaded while this one walks (its load is the head of every walk's dependency chain)
-        orbx_proj_query Qn;
-        if (tid < nq) Qn = pb.queries[tid];
         for (int q = tid; q < nq; q += T) {
-            const orbx_proj_query Q = Qn;
-            if (q + T < nq) Qn = pb.queries[q + T];
+            const orbx_proj_query Q = pb.queries[q];
             int r = -1;
             ProjBest b;
             if (!(Q.flags & ORBX_QF_SKIP)) {
@@ -361,12 +357,9 @@ __global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(o
     int* res = own + n_cap;
     uint8_t* qm = reinterpret_cast<uint8_t*>(res + nq_cap);
     uint32_t* list = reinterpret_cast<uint32_t*>(lp + (((size_t)8 * n_cap + 4 * (size_t)nq_cap + nq_cap + 15) & ~(size_t)15));
-    // round 0: every query's walk without claims, its candidates recorded (the next query's record prefetched)
-    orbx_proj_query Qn;
-    if (tid < nq) Qn = pb.queries[tid];
+    // round 0: every query's walk without claims, its candidates recorded
     for (int q = tid; q < nq; q += T) {
-        const orbx_proj_query Q = Qn;
-        if (q + T < nq) Qn = pb.queries[q + T];
+        const orbx_proj_query Q = pb.queries[q];
         int r = -1, m = (Q.flags & ORBX_QF_BLOCKS) ? kQmBlocks : 0;
         if (Q.flags & ORBX_QF_SKIP) {
             m |= kQmSkip;
