@@ -496,24 +496,38 @@ def host_api_rate(pkg, cfg, lefts, rights, n_frames, device):
     b = cfg["bf"] / cfg["fx"]
     from concurrent.futures import ThreadPoolExecutor
     pool = ThreadPoolExecutor(1)                     # the right extraction on its own thread, as Frame.cc:78-81
-    lat, warm = [], []
     # 10 untimed frames: among the first ~10 calls one takes 7-20 ms (one-time runtime set-up on the extractor's
     # thread, r4hac); their maximum is reported as warmup_ms_max
     n_warm = 10
-    for i in range(n_frames + n_warm):
-        t0 = time.perf_counter()
+
+    def two_threads(i):
         fr = pool.submit(ex_r, rights[i % len(rights)])
         kl, dl = ex_l(lefts[i % len(lefts)])       # ctypes releases the GIL: both extractions run natively at once
         kr, dr = fr.result()
         m.ComputeStereoMatches(ex_l, ex_r, kl, dl, kr, dr, cfg["bf"], b)
-        (lat if i >= n_warm else warm).append(time.perf_counter() - t0)
+
+    def pair(i):
+        (kl, dl), (kr, dr) = pkg.extract_pair(ex_l, ex_r, lefts[i % len(lefts)], rights[i % len(rights)])
+        m.ComputeStereoMatches(ex_l, ex_r, kl, dl, kr, dr, cfg["bf"], b)
+
+    def run(fn):
+        lat, warm = [], []
+        for i in range(n_frames + n_warm):
+            t0 = time.perf_counter()
+            fn(i)
+            (lat if i >= n_warm else warm).append(time.perf_counter() - t0)
+        lat_ms = np.array(lat) * 1e3
+        return {"frames_per_s": round(1e3 / float(np.mean(lat_ms)), 1),
+                "latency_ms_median": round(float(np.median(lat_ms)), 3),
+                "latency_ms_p95": round(float(np.percentile(lat_ms, 95)), 3),
+                "latency_ms_max": round(float(np.max(lat_ms)), 3), "frames": len(lat), "warmup_frames": n_warm,
+                "warmup_ms_max": round(1e3 * max(warm), 3)}
+    out = run(pair)
+    out["path"] = ("Python ctypes: orbx_extract_pair (the left and right extractions of a stereo Frame, Frame.cc:78-81, "
+                   "enqueued together from one thread) + orbx_compute_stereo_matches, host buffers, one frame per call")
+    out["two_threads"] = dict(run(two_threads), path="Python ctypes: orbx_extract(L) and orbx_extract(R) on two threads "
+                                                     "(as Frame.cc:78-81) + orbx_compute_stereo_matches")
     pool.shutdown()
-    lat_ms = np.array(lat) * 1e3
-    out = {"frames_per_s": round(1e3 / float(np.mean(lat_ms)), 1), "latency_ms_median": round(float(np.median(lat_ms)), 3),
-           "latency_ms_p95": round(float(np.percentile(lat_ms, 95)), 3), "latency_ms_max": round(float(np.max(lat_ms)), 3),
-           "frames": len(lat), "warmup_frames": n_warm, "warmup_ms_max": round(1e3 * max(warm), 3),
-           "path": "Python ctypes: orbx_extract(L) and orbx_extract(R) on two threads (Frame.cc:78-81) + "
-                   "orbx_compute_stereo_matches, host buffers, one frame per call"}
     # the same per-call path from a C++ caller (the reference's own language): scripts/micro/host_api_bench.cpp, built
     # by build() into build/host_api_bench, run as a child process on the same GPU
     exe = os.path.join(ROOT, "build", "host_api_bench")

@@ -100,6 +100,14 @@ int orbx_extractor_level_sizes(orbx_extractor* ex, int rows, int cols, int* leve
  * If capacity < needed, returns ORBX_ERR_CAPACITY with *n_out = needed and writes nothing. */
 int orbx_extract(orbx_extractor* ex, const uint8_t* image, int rows, int cols, size_t step,
                  orbx_keypoint* keypoints, uint8_t* descriptors, int capacity, int* n_out);
+/* The stereo Frame constructor's two extractions (src/Frame.cc:78-81: mpORBextractorLeft on the left image and
+ * mpORBextractorRight on the right one, in two threads) from ONE host thread: both are enqueued before either is
+ * waited for, so they run together on the two extractors' streams.  Same outputs and error behaviour as two
+ * orbx_extract calls (an empty image gives 0 keypoints for its side); left and right must be distinct extractors. */
+int orbx_extract_pair(orbx_extractor* left, orbx_extractor* right, const uint8_t* image_left, size_t step_left,
+                      const uint8_t* image_right, size_t step_right, int rows, int cols, orbx_keypoint* keypoints_left,
+                      uint8_t* descriptors_left, int capacity_left, int* n_left, orbx_keypoint* keypoints_right,
+                      uint8_t* descriptors_right, int capacity_right, int* n_right);
 
 /* mvImagePyramid (include/ORBextractor.h:85): copy level 'level' of image 'index' of the last call
  * into a host buffer with row stride dst_step (unpadded level view, as Frame::ComputeStereoMatches

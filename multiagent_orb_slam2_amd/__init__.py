@@ -6,9 +6,10 @@ the host-side mirror of the reference's ORBextractor / ORBmatcher interface plus
 """
 from .orbx import (KFDB_COVIS, KFDB_LOOP, KFDB_RELOC, KP_DTYPE, PROJ_QUERY_DTYPE, Grid, KeyFrameDatabase,  # noqa: F401
                    KeyframeExchangeRCCL, KeyframeFusionEngine, KfStore, ORBextractor, ORBmatcher, ORBVocabulary,
-                   OrbxError, ProjParams, ProjProblem, declared_symbols, device_count, frame_grid, load_library,
-                   packet_layout)
+                   OrbxError, ProjParams, ProjProblem, declared_symbols, device_count, extract_pair, frame_grid,
+                   load_library, packet_layout)
 
 __all__ = ["KFDB_COVIS", "KFDB_LOOP", "KFDB_RELOC", "KeyFrameDatabase", "KeyframeExchangeRCCL", "KeyframeFusionEngine",
            "KP_DTYPE", "PROJ_QUERY_DTYPE", "Grid", "ProjParams", "ProjProblem", "frame_grid", "KfStore", "ORBextractor",
-           "ORBmatcher", "ORBVocabulary", "OrbxError", "declared_symbols", "device_count", "load_library", "packet_layout"]
+           "ORBmatcher", "ORBVocabulary", "OrbxError", "declared_symbols", "device_count", "extract_pair", "load_library",
+           "packet_layout"]

@@ -2934,11 +2934,11 @@ int orbx_extract_batch_device_split(orbx_extractor* e, const uint8_t* d_images, 
                      (hipStream_t)in_stream, (hipStream_t)out_stream, e->pipeline);
 }
 
-int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, size_t step, orbx_keypoint* kps,
-                 uint8_t* desc, int capacity, int* n_out) {
-    ORBX_REQUIRE(e && n_out, ORBX_ERR_ARG, "null argument");
-    *n_out = 0;
-    if (!image || rows <= 0 || cols <= 0) return ORBX_OK;   // _image.empty() -> return (:1046-1047)
+// The host call in two halves: extract_begin stages the image and enqueues the extraction and the result copy on the
+// extractor's stream (no synchronisation); extract_end waits for that stream and hands the results out.  orbx_extract
+// is begin + end; orbx_extract_pair begins both extractors before ending either, so one host thread keeps the left and
+// right extractions in flight together (what Frame.cc:78-81 gets from two threads).
+static int extract_begin(orbx_extractor* e, const uint8_t* image, int rows, int cols, size_t step) {
     ORBX_REQUIRE(step >= (size_t)cols, ORBX_ERR_ARG, "step < cols");
     ORBX_HIP(hipSetDevice(e->device));
     int st = e->configure(rows, cols, std::max(e->max_batch, 1));
@@ -2972,9 +2972,7 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
         ORBX_HIP(hipHostMalloc((void**)&e->h_out, ob, hipHostMallocDefault));
         e->h_out_bytes = ob;
     }
-    int32_t* h_cnt = (int32_t*)e->h_out;
-    orbx_keypoint* h_kps = (orbx_keypoint*)(e->h_out + 64);
-    uint8_t* h_desc = e->h_out + odesc;
+    int32_t* h_cnt = (int32_t*)e->h_out;                    // count, then the error word (extract_end reads both)
     hipStream_t s = e->own();
     // The image in, outside the graph (its source changes every call): packed into pinned staging, one H2D copy.  (r4n,
     // native per-call path: one staged copy 0.397 / 0.396 ms per frame, a pageable copy 0.398 / 0.393, four row bands
@@ -3032,7 +3030,16 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
     } else {
         if ((st = enqueue())) return st;
     }
-    ORBX_HIP(hipStreamSynchronize(s));
+    return ORBX_OK;
+}
+
+static int extract_end(orbx_extractor* e, orbx_keypoint* kps, uint8_t* desc, int capacity, int* n_out) {
+    ORBX_HIP(hipSetDevice(e->device));
+    const size_t odesc = (64 + (size_t)e->out_capacity * sizeof(orbx_keypoint) + 63) & ~(size_t)63;
+    const int32_t* h_cnt = (const int32_t*)e->h_out;
+    const orbx_keypoint* h_kps = (const orbx_keypoint*)(e->h_out + 64);
+    const uint8_t* h_desc = e->h_out + odesc;
+    ORBX_HIP(hipStreamSynchronize(e->own()));
     const int n = h_cnt[0], err = h_cnt[1];
     ORBX_REQUIRE(!(err & kErrStale), ORBX_ERR_HIP, "ordering canary: a describe read another call's keypoints (err=%d)", err);
     ORBX_REQUIRE(err == 0, ORBX_ERR_UNSUPPORTED, "quadtree node capacity exceeded (err=%d)", err);
@@ -3047,6 +3054,35 @@ int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, si
         std::memcpy(desc, h_desc, (size_t)n * 32);
     }
     return ORBX_OK;
+}
+
+int orbx_extract(orbx_extractor* e, const uint8_t* image, int rows, int cols, size_t step, orbx_keypoint* kps,
+                 uint8_t* desc, int capacity, int* n_out) {
+    ORBX_REQUIRE(e && n_out, ORBX_ERR_ARG, "null argument");
+    *n_out = 0;
+    if (!image || rows <= 0 || cols <= 0) return ORBX_OK;   // _image.empty() -> return (:1046-1047)
+    if (int st = extract_begin(e, image, rows, cols, step)) return st;
+    return extract_end(e, kps, desc, capacity, n_out);
+}
+
+int orbx_extract_pair(orbx_extractor* left, orbx_extractor* right, const uint8_t* image_left, size_t step_left,
+                      const uint8_t* image_right, size_t step_right, int rows, int cols, orbx_keypoint* kps_left,
+                      uint8_t* desc_left, int capacity_left, int* n_left, orbx_keypoint* kps_right, uint8_t* desc_right,
+                      int capacity_right, int* n_right) {
+    ORBX_REQUIRE(left && right && left != right && n_left && n_right, ORBX_ERR_ARG,
+                 "two distinct extractors and both counts are required");
+    *n_left = *n_right = 0;
+    const bool l_ok = image_left && rows > 0 && cols > 0, r_ok = image_right && rows > 0 && cols > 0;
+    if (l_ok) if (int st = extract_begin(left, image_left, rows, cols, step_left)) return st;
+    if (r_ok) {
+        if (int st = extract_begin(right, image_right, rows, cols, step_right)) {
+            if (l_ok) (void)hipStreamSynchronize(left->own());   // leave the left call finished, not half-done
+            return st;
+        }
+    }
+    int st = l_ok ? extract_end(left, kps_left, desc_left, capacity_left, n_left) : ORBX_OK;
+    const int sr = r_ok ? extract_end(right, kps_right, desc_right, capacity_right, n_right) : ORBX_OK;
+    return st ? st : sr;
 }
 
 int orbx_extractor_status(orbx_extractor* e, int* flags, int reset) {

@@ -204,6 +204,8 @@ def load_library(path: str = LIB_PATH):
     for name in ("orbx_extractor_destroy", "orbx_matcher_destroy", "orbx_extractor_get_levels"):
         getattr(lib, name).argtypes = [vp]
     lib.orbx_extract.argtypes = [vp, vp, i32, i32, C.c_size_t, vp, vp, i32, C.POINTER(i32)]
+    lib.orbx_extract_pair.argtypes = [vp, vp, vp, C.c_size_t, vp, C.c_size_t, i32, i32, vp, vp, i32, C.POINTER(i32), vp, vp,
+                                      i32, C.POINTER(i32)]
     lib.orbx_extract_batch_device.argtypes = [vp, vp, i32, i32, i32, C.c_size_t, C.c_size_t, vp, vp, vp, i32, vp]
     lib.orbx_extract_batch_device_split.argtypes = [vp, vp, i32, i32, i32, C.c_size_t, C.c_size_t, vp, vp, vp, i32, vp, vp]
     lib.orbx_extractor_reserve.argtypes = [vp, i32, i32, i32]
@@ -363,6 +365,7 @@ class ORBextractor:
         _register(self)
         self._last_shape = None
         self._out = None          # host output staging of __call__
+        self._cap, self._cap_for = 0, None
 
     def close(self):
         if getattr(self, "_h", None):
@@ -430,17 +433,23 @@ class ORBextractor:
             return np.zeros(0, KP_DTYPE), np.zeros((0, 32), np.uint8)
         assert img.ndim == 2, "8UC1 image expected"
         rows, cols = img.shape
-        cap = self.max_keypoints(rows, cols)
-        # output staging reused across calls (only the first n entries are written and copied out): fresh zeroed
-        # arrays of the full capacity (480 KB at KITTI) cost page faults and a memset per call
-        if self._out is None or len(self._out[0]) < cap:
-            self._out = (np.empty(cap, KP_DTYPE), np.empty((cap, 32), np.uint8))
-        kps, desc = self._out
+        kps, desc = self._staging(rows, cols)
         n = C.c_int()
-        _check(self._lib.orbx_extract(self._h, _p(img), rows, cols, img.strides[0], _p(kps), _p(desc), cap,
+        _check(self._lib.orbx_extract(self._h, _p(img), rows, cols, img.strides[0], _p(kps), _p(desc), len(kps),
                                       C.byref(n)))
         self._last_shape = (rows, cols)
         return kps[: n.value].copy(), desc[: n.value].copy()
+
+    def _staging(self, rows: int, cols: int):
+        """Output staging reused across calls (only the first n entries are written and copied out; fresh zeroed arrays
+        of the full capacity, 480 KB at KITTI, cost page faults and a memset per call); the capacity is asked once per
+        image size."""
+        if self._cap_for != (rows, cols):
+            self._cap = self.max_keypoints(rows, cols)
+            self._cap_for = (rows, cols)
+        if self._out is None or len(self._out[0]) < self._cap:
+            self._out = (np.empty(self._cap, KP_DTYPE), np.empty((self._cap, 32), np.uint8))
+        return self._out[0][: self._cap], self._out[1][: self._cap]
 
     def pyramid_device(self) -> "Pyramid":
         """orbx_pyramid of the last call (device pointers; valid until the next call on this extractor)."""
@@ -524,6 +533,26 @@ class StereoResult:
     best_idx: np.ndarray   # right index or -1 (accepted if best_dist < 75)
     best_dist: np.ndarray
     n_matched: int
+
+
+def extract_pair(left: "ORBextractor", right: "ORBextractor", image_left: np.ndarray, image_right: np.ndarray):
+    """The stereo Frame constructor's two extractions (src/Frame.cc:78-81) from one thread (orbx_extract_pair: both
+    enqueued before either is waited for).  Returns ((keypoints, descriptors) left, (keypoints, descriptors) right), as
+    two ORBextractor calls would."""
+    il = np.ascontiguousarray(image_left, np.uint8)
+    ir = np.ascontiguousarray(image_right, np.uint8)
+    assert il.ndim == 2 and il.shape == ir.shape, "two 8UC1 images of one size expected"
+    rows, cols = il.shape
+    if il.size == 0:
+        e = (np.zeros(0, KP_DTYPE), np.zeros((0, 32), np.uint8))
+        return e, e
+    kl, dl = left._staging(rows, cols)
+    kr, dr = right._staging(rows, cols)
+    nl, nr = C.c_int(), C.c_int()
+    _check(left._lib.orbx_extract_pair(left._h, right._h, _p(il), il.strides[0], _p(ir), ir.strides[0], rows, cols, _p(kl),
+                                       _p(dl), len(kl), C.byref(nl), _p(kr), _p(dr), len(kr), C.byref(nr)))
+    left._last_shape = right._last_shape = (rows, cols)
+    return (kl[: nl.value].copy(), dl[: nl.value].copy()), (kr[: nr.value].copy(), dr[: nr.value].copy())
 
 
 class ORBmatcher:

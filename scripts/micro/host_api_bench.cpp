@@ -6,7 +6,7 @@
 //   host_api_bench <liborbx.so> [frames=300] [rows=375] [cols=1242] [nfeatures=2000]
 //
 // Prints one JSON line: frames/s from the mean, and median / p95 / max of the frame, left-extract, right-extract
-// and stereo phases (ms).
+// and stereo phases (ms); "pair": the same frames through orbx_extract_pair from one thread.
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -112,6 +112,28 @@ int main(int argc, char** argv) {
         if (f < 0) { warm_max = std::max(warm_max, tf); continue; }
         t_frame.push_back(tf); t_left.push_back(tl); t_right.push_back(tr); t_stereo.push_back(tsm);
     }
+    // the same frames through orbx_extract_pair from this one thread (both extractions enqueued before either is waited
+    // for), when the library has it
+    std::string pair = "null";
+    if (auto ep = (decltype(&::orbx_extract_pair))dlsym(h, "orbx_extract_pair")) {
+        std::vector<double> t_pair;
+        for (int f = -10; f < frames; ++f) {
+            const int k = (f + kDistinct * 4) % kDistinct;
+            int nl = 0, nr = 0, ns = 0;
+            const auto t0 = clk::now();
+            const int st = ep(exl, exr, L[k].data(), (size_t)cols, R[k].data(), (size_t)cols, rows, cols, kl.data(), dl.data(), cap,
+                              &nl, kr.data(), dr.data(), cap, &nr);
+            const int sts = orbx_compute_stereo_matches(m, exl, exr, kl.data(), dl.data(), nl, kr.data(), dr.data(), nr, bf,
+                                                        bf / fx, ur.data(), depth.data(), &ns);
+            if (st || sts) { ++bad; std::fprintf(stderr, "pair frame %d: %s\n", f, orbx_last_error()); }
+            if (f >= 0) t_pair.push_back(ms_since(t0));
+        }
+        const Stats P = stats(t_pair);
+        char buf[256];
+        std::snprintf(buf, sizeof buf, "{\"frames_per_s\": %.1f, \"frame_ms\": {\"median\": %.4f, \"p95\": %.4f, \"max\": %.4f, "
+                      "\"mean\": %.4f}}", 1e3 / P.mean, P.med, P.p95, P.max, P.mean);
+        pair = buf;
+    }
     const Stats F = stats(t_frame), A = stats(t_left), B = stats(t_right), S = stats(t_stereo);
     std::vector<int> order(t_frame.size());                      // the slowest frames, for outlier attribution
     for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
@@ -123,8 +145,9 @@ int main(int argc, char** argv) {
     std::printf("{\"lib\": \"%s\", \"frames\": %d, \"frames_per_s\": %.1f, \"frame_ms\": {\"median\": %.4f, \"p95\": %.4f, "
                 "\"max\": %.4f, \"mean\": %.4f}, \"extract_left_ms\": {\"median\": %.4f, \"p95\": %.4f}, "
                 "\"extract_right_ms\": {\"median\": %.4f, \"p95\": %.4f}, \"stereo_ms\": {\"median\": %.4f, \"p95\": %.4f}, "
-                "\"errors\": %d, \"slowest\": [%s], \"warmup_frames\": 10, \"warmup_ms_max\": %.4f}\n",
-                argv[1], frames, 1e3 / F.mean, F.med, F.p95, F.max, F.mean, A.med, A.p95, B.med, B.p95, S.med, S.p95, bad, slow.c_str(), warm_max);
+                "\"errors\": %d, \"slowest\": [%s], \"warmup_frames\": 10, \"warmup_ms_max\": %.4f, \"pair\": %s}\n",
+                argv[1], frames, 1e3 / F.mean, F.med, F.p95, F.max, F.mean, A.med, A.p95, B.med, B.p95, S.med, S.p95, bad, slow.c_str(), warm_max,
+                pair.c_str());
     orbx_matcher_destroy(m);
     orbx_extractor_destroy(exl);
     orbx_extractor_destroy(exr);

@@ -286,3 +286,37 @@ def test_resize_pair_bit_exact(gpu, monkeypatch, rows, cols, nf):
     ref = O.extract(imgs[0], nfeatures=nf, want_pyramid=True)
     assert np.array_equal(k1, ref["kps"]) and np.array_equal(d1, ref["desc"])
     assert all(np.array_equal(a, b) for a, b in zip(ex1.mvImagePyramid, ref["pyramid"]))
+
+
+def test_extract_pair_equals_two_calls(gpu):
+    """orbx_extract_pair (the stereo Frame's two extractions from one thread, Frame.cc:78-81) returns what two
+    orbx_extract calls return -- and the oracle -- on repeated frames of two sizes; an empty pair gives nothing, one
+    extractor for both sides is refused, a short capacity is reported as for orbx_extract."""
+    import ctypes as C
+
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    exl, exr = pkg.ORBextractor(2000, 1.2, 8, 20, 7), pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    ex1 = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    for k, (rows, cols) in enumerate([(375, 1242), (375, 1242), (240, 320), (375, 1242)]):
+        left = S.kitti_like_image(500 + k, rows=rows, cols=cols)
+        right = S.shifted_right_view(left, 500 + k)
+        (kl, dl), (kr, dr) = pkg.extract_pair(exl, exr, left, right)
+        for img, kk, dd in ((left, kl, dl), (right, kr, dr)):
+            k1, d1 = ex1(img)
+            assert np.array_equal(kk, k1) and np.array_equal(dd, d1)
+            ref = O.extract(img, nfeatures=2000)
+            assert np.array_equal(kk, ref["kps"]) and np.array_equal(dd, ref["desc"])
+        # the pyramids the stereo step reads are the pair call's
+        assert np.array_equal(exr.mvImagePyramid[0], right)
+    (a, b), (c, d) = pkg.extract_pair(exl, exr, np.zeros((0, 0), np.uint8), np.zeros((0, 0), np.uint8))
+    assert len(a) == len(c) == 0
+    with pytest.raises(pkg.OrbxError):
+        pkg.extract_pair(exl, exl, left, right)
+    kp = np.empty(10, pkg.KP_DTYPE)
+    ds = np.empty((10, 32), np.uint8)
+    nl, nr = C.c_int(), C.c_int()
+    st = exl._lib.orbx_extract_pair(exl._h, exr._h, left.ctypes.data, left.strides[0], right.ctypes.data, right.strides[0],
+                                    left.shape[0], left.shape[1], kp.ctypes.data, ds.ctypes.data, 10, C.byref(nl),
+                                    kp.ctypes.data, ds.ctypes.data, 10, C.byref(nr))
+    assert st == pkg.orbx.ORBX_ERR_CAPACITY and nl.value > 10
