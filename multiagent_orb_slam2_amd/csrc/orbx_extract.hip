@@ -108,9 +108,28 @@ struct ResizeTab {       // per level >= 1, device arrays
     int* y0; int* y1; int* b0; int* b1;   // [h]
 };
 
-// Initialised in its declaration: the table is part of the code object, so every device the module is loaded on
-// holds it (an uninitialised __constant__ filled by hipMemcpyToSymbol is written on the current device only).
-__constant__ __attribute__((aligned(16))) signed char c_pattern[ORBX_PATTERN_TESTS * 4] = ORBX_PATTERN_INIT;
+// The rBRIEF tests laid out per describe lane: with kLp lanes per keypoint, lane lk runs tests g * kLp + lk (g < 256 /
+// kLp), and its words sit contiguously at [lk * (256 / kLp) + g], so a lane fetches them with 16-byte loads from one
+// base address instead of one dword load and one 64-bit address per test.
+constexpr signed char kPatternInit[ORBX_PATTERN_TESTS * 4] = ORBX_PATTERN_INIT;
+template <int kLp>
+struct PatternByLane { uint32_t w[ORBX_PATTERN_TESTS]; };
+template <int kLp>
+constexpr PatternByLane<kLp> make_pattern_by_lane() {
+    PatternByLane<kLp> t{};
+    constexpr int nt = ORBX_PATTERN_TESTS / kLp;
+    for (int lk = 0; lk < kLp; ++lk)
+        for (int g = 0; g < nt; ++g) {
+            const int s = 4 * (g * kLp + lk);
+            t.w[lk * nt + g] = (uint32_t)(uint8_t)kPatternInit[s] | ((uint32_t)(uint8_t)kPatternInit[s + 1] << 8) |
+                               ((uint32_t)(uint8_t)kPatternInit[s + 2] << 16) | ((uint32_t)(uint8_t)kPatternInit[s + 3] << 24);
+        }
+    return t;
+}
+// Initialised in their declarations: the tables are part of the code object, so every device the module is loaded on
+// holds them (an uninitialised __constant__ filled by hipMemcpyToSymbol is written on the current device only).
+__constant__ __attribute__((aligned(16))) PatternByLane<32> c_pattern_l32 = make_pattern_by_lane<32>();
+__constant__ __attribute__((aligned(16))) PatternByLane<16> c_pattern_l16 = make_pattern_by_lane<16>();
 // umax for HALF_PATCH_SIZE = 15 (ORBextractor ctor :454-469); the host recomputes it and checks equality
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
@@ -1725,10 +1744,12 @@ constexpr int kBriefBatch = ORBX_BRIEF_BATCH;                 // BRIEF test grou
 // Sum of v over the kLp-lane group of each lane (groups of 16, 32 or 64 lanes), in every lane of the group.
 template <int kLp>
 __device__ __forceinline__ int group_sum(int v, int sub) {
-    v += __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);    // quad_perm 1,0,3,2
-    v += __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);    // quad_perm 2,3,0,1
-    v += __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);   // row_half_mirror
-    v += __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false);   // row_mirror: row sum in every lane of the row
+    // old = 0, the sum's identity: the compiler folds each move into its add as a DPP operand (one v_add_u32_dpp
+    // instead of a copy, a v_mov_b32_dpp and an add); same rule in orbx_common.h's reductions
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);     // quad_perm 1,0,3,2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);     // quad_perm 2,3,0,1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);    // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);    // row_mirror: row sum in every lane of the row
     if (kLp == 16) return v;
     const int r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
     const int r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
@@ -1887,6 +1908,24 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
     float a, b;
     orbx_sincos_brief(ang, &a, &b);
     const uint8_t* center = win + kBriefR * kBriefRow + kBriefR;
+    // this lane's pattern words (tests g * kLp + lk), contiguous in the per-lane table
+    uint32_t pat[kNT];
+    {
+        const uint32_t* pw = (kLp == 32 ? c_pattern_l32.w : c_pattern_l16.w) + lk * kNT;
+#pragma unroll
+        for (int g = 0; g < kNT; g += 4) __builtin_memcpy(&pat[g], pw + g, 16);
+    }
+    // The rotated offsets (computeOrbDescriptor :120-124): ry = fx b + fy a, rx = fx a - fy b, each product and sum
+    // rounded separately (no fusion): two v_pk_mul_f32 ({b, a} and {a, -b}; the negated product is exact) and a
+    // v_pk_add_f32.  cvRound (ties to even) by the magic constant M = 1.5 * 2^23: for |v| < 2^22 the float sum v + M is
+    // an integer and its bits are 0x4B400000 + rint(v), so bits(ry + M) [low 24 bits, v_mad_i32_i24] * kBriefRow +
+    // bits(rx + M) - kMagicOff is the window offset -- one packed add per point instead of two v_rndne_f32 and two
+    // v_cvt_i32_f32.  Written as asm: the compiler's own pairing of the scalar form costs ~40 register moves per lane.
+    // (The elements are copied to floats before their bits are taken: this compiler turns __builtin_bit_cast of an
+    // ext_vector element .y into element .x.)
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 ab1 = {b, a}, ab2 = {a, -b}, magic = {12582912.0f, 12582912.0f};
+    constexpr int kMagicOff = (int)(0x400000u * (unsigned)kBriefRow + 0x4B400000u);
     // kBriefBatch groups of tests at a time: their LDS offsets, then their reads back to back, then the comparisons
     // (no branch: a rotated offset is within kBriefR of the centre, inside the slice, for invalid lanes too, whose
     // moments are 0 and angle 0)
@@ -1898,11 +1937,18 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
         for (int h = 0; h < kBriefBatch; ++h) {
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const uint32_t w = reinterpret_cast<const uint32_t*>(c_pattern)[(g0 + h) * kLp + lk];
+                const uint32_t w = pat[g0 + h];
                 const float fx = (float)(int)(signed char)(w >> (16 * e)), fy = (float)(int)(signed char)(w >> (16 * e + 8));
-                const float ry = __fadd_rn(__fmul_rn(fx, b), __fmul_rn(fy, a));
-                const float rx = __fsub_rn(__fmul_rn(fx, a), __fmul_rn(fy, b));
-                toff[h][e] = __mul24(__float2int_rn(ry), kBriefRow) + __float2int_rn(rx);
+                const f32x2 fxy = {fx, fy};
+                f32x2 p, q, r;
+                asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(p) : "v"(fxy), "v"(ab1));             // {fx b, fx a}
+                asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(q) : "v"(fxy), "v"(ab2)); // {fy a, -fy b}
+                asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(p), "v"(q));                                 // {ry, rx}
+                asm("v_pk_add_f32 %0, %1, %2" : "=v"(p) : "v"(r), "v"(magic));                             // + M
+                const float ryM = p.x, rxM = p.y;
+                int t;
+                asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(t) : "v"(__float_as_int(ryM)), "n"(kBriefRow), "v"(__float_as_int(rxM)));
+                toff[h][e] = t - kMagicOff;
             }
         }
 #pragma unroll
