@@ -586,15 +586,18 @@ __device__ __forceinline__ QuadTaps fastw_quad_load(const uint32_t* __restrict__
     return q;
 }
 
-// Test of a loaded quad at threshold t: bit k = pair 4u+k has a pixel inside the detection window (column < Wd) whose
-// compass value exceeds t.  f16 form of the compass test (the pair image is f16-biased: differences are exact): per
-// pair 4 packed differences, dk / br by 3-input packed min / max, m = max(dk, -br); z = m - (t + 1) has its sign bit
-// set iff m <= t, and the 8 sign bits of the quad (2 per pair) are gathered by two v_perm into one byte each.
-__device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, int t, int PR, int Wd) {
-    (void)PR;
+// Test of a loaded quad at threshold t: bit 8k + 7 is set iff pair 4u+k lies in the detection window's pairs (4u + k <
+// PR) and one of its pixels has a compass value above t.  f16 form of the compass test (the pair image is f16-biased:
+// differences are exact): per pair 4 packed differences, dk / br by packed min / max, m = max(dk, -br); the two pixels
+// of a pair are merged by one packed max over two pairs' re-paired halves (v_perm), and z = max - (t + 1) has its sign
+// bit set iff both pixels have m <= t; one more v_perm gathers the four sign bytes.  The second pixel of an odd-width
+// row's last pair (column Wd) is not masked: it can only add that pair to the survivor list, where the score store and
+// the NMS take the pair's second pixel only when 2j + 1 < Wd, and a pixel that failed the pre-test scores <= t, below
+// every threshold it is kept at, and never blocks a kept neighbour.
+__device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, int t, int PR) {
     const uint32_t *A = q.A, *U = q.U, *D = q.D;
     const h16x2 tq = {(_Float16)(t + 1), (_Float16)(t + 1)};
-    uint32_t z[4];
+    uint32_t mk[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const h16x2 v = as_h2(align16(A[k + 2], A[k + 1]));             // pixels of pair 4u+k
@@ -608,18 +611,15 @@ __device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, in
         // the same values as the 6-op forms in 3 ops each
         const h16x2 dk = hmin(hmax(d0, d8), hmax(d4, d12));
         const h16x2 br = hmax(hmin(d0, d8), hmin(d4, d12));
-        const h16x2 m = hmax(dk, -br);
-        z[k] = __builtin_bit_cast(uint32_t, m - tq);
+        mk[k] = __builtin_bit_cast(uint32_t, hmax(dk, -br));
     }
-    // sign bytes: pixel 2k at byte 2k, pixel 2k+1 at byte 2k+1 of the 8-byte (lo | hi << 32) pack
-    const uint32_t lo = __builtin_amdgcn_perm(z[1], z[0], 0x07050301u), hi = __builtin_amdgcn_perm(z[3], z[2], 0x07050301u);
-    const int nv = min(max(Wd - 8 * u, 0), 8);                         // pixels of the quad inside the window
-    const uint64_t inv = nv >= 8 ? 0ull : (0x8080808080808080ull << (8 * nv));
-    const uint64_t f = ((((uint64_t)hi << 32) | lo) | inv) & 0x8080808080808080ull;   // 0x80: pixel fails
-    const uint64_t g = f & (f >> 8) & 0x0080008000800080ull;          // bit 7 of byte 2k: both pixels of pair k fail
-    const uint32_t gl = (uint32_t)g, gh = (uint32_t)(g >> 32);
-    const uint32_t failq = ((gl >> 7) & 1u) | ((gl >> 22) & 2u) | ((gh >> 5) & 4u) | ((gh >> 20) & 8u);
-    return ~failq & 15u;
+    // {max over pair 2i, max over pair 2i+1}: the low halves of two pairs against their high halves
+    const h16x2 p01 = hmax(as_h2(__builtin_amdgcn_perm(mk[1], mk[0], 0x05040100u)), as_h2(__builtin_amdgcn_perm(mk[1], mk[0], 0x07060302u)));
+    const h16x2 p23 = hmax(as_h2(__builtin_amdgcn_perm(mk[3], mk[2], 0x05040100u)), as_h2(__builtin_amdgcn_perm(mk[3], mk[2], 0x07060302u)));
+    const uint32_t z01 = __builtin_bit_cast(uint32_t, p01 - tq), z23 = __builtin_bit_cast(uint32_t, p23 - tq);
+    const uint32_t fail = __builtin_amdgcn_perm(z23, z01, 0x07050301u);   // sign byte of pair k at byte k
+    const int sh = min(max(32 * u + 32 - 8 * PR, 0), 24);               // 8 x (4 - pairs of the quad in the window)
+    return ~fail & (0x80808080u >> sh);
 }
 
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
@@ -731,13 +731,13 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __
         const int dr = kWave / QR, du = kWave - dr * QR;
         int rr = ln / QR, u = ln - rr * QR;
         auto step = [&](int& r0, int& u0) { r0 += dr; u0 += du; if (u0 >= QR) { u0 -= QR; ++r0; } };
-        auto emit = [&](uint32_t mq, int r0, int u0) {
+        auto emit = [&](uint32_t mq, int r0, int u0) {                 // mq: bit 8k + 7 = pair 4 u0 + k survives
             const int cq = __builtin_popcount(mq);
             const uint64_t b0 = __ballot(cq & 1), b1 = __ballot(cq & 2), b2 = __ballot(cq & 4);
             int pos = rank_below(b0, ns) + 2 * rank_below(b1) + 4 * rank_below(b2);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if ((mq >> k) & 1u) list[pos++] = (uint16_t)((r0 << 8) | (4 * u0 + k));
+                if ((mq >> (8 * k + 7)) & 1u) list[pos++] = (uint16_t)((r0 << 8) | (4 * u0 + k));
             ns += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
         };
         for (int q0 = 0; q0 < NQ4; q0 += 2 * kWave) {
@@ -749,8 +749,8 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __
             const bool va = qa < NQ4, vb = qb < NQ4;
             const QuadTaps ta = fastw_quad_load<kPS, kPC>(E, va ? ra : 0, va ? ua : 0);
             const QuadTaps tb = fastw_quad_load<kPS, kPC>(E, vb ? rb : 0, vb ? ub : 0);
-            const uint32_t ma = va ? fastw_quad_test(ta, ua, tpre, PR, Wd) : 0u;
-            const uint32_t mb = vb ? fastw_quad_test(tb, ub, tpre, PR, Wd) : 0u;
+            const uint32_t ma = va ? fastw_quad_test(ta, ua, tpre, PR) : 0u;
+            const uint32_t mb = vb ? fastw_quad_test(tb, ub, tpre, PR) : 0u;
             emit(ma, ra, ua);
             emit(mb, rb, ub);
         }
@@ -857,6 +857,9 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
     const int T1 = max(min(max(iniTh, 0), 255), 1), T2 = max(min(max(minTh, 0), 255), 1);
     const int tp = min(T1, T2);
     constexpr int SWB = fastw_scrow(kPS);
+    // a pair word is (1024 + p1, 1024 + p0) as f16: bytes (p0, 0x64, p1, 0x64), one v_perm_b32 from a source dword and
+    // this constant (selectors 4-7 pick its bytes) instead of a perm and an OR
+    constexpr uint32_t kBias8 = 0x64646464u;
     {
         // 1. cell ROI -> f16-biased pair image: lane items (row, 8-column chunk), one 8-byte load each, all of a round
         //    issued before the first use; bytes past the ROI's width read as 0
@@ -886,14 +889,14 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
                 for (int k = 0; k < kPf; ++k) {
                     if (q0 + ln + k * kWave < NQ) {
                         const uint4 a = pf[k];
-                        const uint4 e0 = make_uint4(__builtin_amdgcn_perm(a.y, a.x, 0x0c010c00u) | 0x64006400u,
-                                                    __builtin_amdgcn_perm(a.y, a.x, 0x0c030c02u) | 0x64006400u,
-                                                    __builtin_amdgcn_perm(a.y, a.x, 0x0c050c04u) | 0x64006400u,
-                                                    __builtin_amdgcn_perm(a.y, a.x, 0x0c070c06u) | 0x64006400u);
-                        const uint4 e1 = make_uint4(__builtin_amdgcn_perm(a.w, a.z, 0x0c010c00u) | 0x64006400u,
-                                                    __builtin_amdgcn_perm(a.w, a.z, 0x0c030c02u) | 0x64006400u,
-                                                    __builtin_amdgcn_perm(a.w, a.z, 0x0c050c04u) | 0x64006400u,
-                                                    __builtin_amdgcn_perm(a.w, a.z, 0x0c070c06u) | 0x64006400u);
+                        const uint4 e0 = make_uint4(__builtin_amdgcn_perm(kBias8, a.x, 0x04010400u),
+                                                    __builtin_amdgcn_perm(kBias8, a.x, 0x04030402u),
+                                                    __builtin_amdgcn_perm(kBias8, a.y, 0x04010400u),
+                                                    __builtin_amdgcn_perm(kBias8, a.y, 0x04030402u));
+                        const uint4 e1 = make_uint4(__builtin_amdgcn_perm(kBias8, a.z, 0x04010400u),
+                                                    __builtin_amdgcn_perm(kBias8, a.z, 0x04030402u),
+                                                    __builtin_amdgcn_perm(kBias8, a.w, 0x04010400u),
+                                                    __builtin_amdgcn_perm(kBias8, a.w, 0x04030402u));
                         uint4* dst = reinterpret_cast<uint4*>(E + fastw_row<kPS, kPC>(rs[k]) + 8 * cs[k]);
                         dst[0] = e0;
                         dst[1] = e1;
@@ -934,11 +937,11 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
                             lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
                         }
                         uint32_t* dst = E + fastw_row<kPS, kPC>(rs[k]) + 4 * cs[k];
-                        dst[3] = __builtin_amdgcn_perm(hi, lo, 0x0c070c06u) | 0x64006400u;
+                        dst[3] = __builtin_amdgcn_perm(kBias8, hi, 0x04030402u);
                         asm volatile("" ::: "memory");
-                        dst[2] = __builtin_amdgcn_perm(hi, lo, 0x0c050c04u) | 0x64006400u;
-                        dst[1] = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u) | 0x64006400u;
-                        dst[0] = __builtin_amdgcn_perm(hi, lo, 0x0c010c00u) | 0x64006400u;
+                        dst[2] = __builtin_amdgcn_perm(kBias8, hi, 0x04010400u);
+                        dst[1] = __builtin_amdgcn_perm(kBias8, lo, 0x04030402u);
+                        dst[0] = __builtin_amdgcn_perm(kBias8, lo, 0x04010400u);
                         asm volatile("" ::: "memory");
                     }
                 }
