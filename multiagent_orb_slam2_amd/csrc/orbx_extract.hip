@@ -484,8 +484,9 @@ __device__ __forceinline__ s16x2 fast_score_from_taps_f16(const uint32_t (&r)[17
         dk[m] = hmin3(a4[m], a4[(m + 2) & 7], hmax(e0, e9));
         br[m] = hmax3(b4[m], b4[(m + 2) & 7], hmin(e0, e9));
     }
-    const h16x2 dmax = hmax3(hmax3(dk[0], dk[1], dk[2]), hmax3(dk[3], dk[4], dk[5]), hmax(dk[6], dk[7]));
-    const h16x2 bmin = hmin3(hmin3(br[0], br[1], br[2]), hmin3(br[3], br[4], br[5]), hmin(br[6], br[7]));
+    // (the 2-input steps as 3-input asm too: a builtin max of asm results canonicalises its inputs first)
+    const h16x2 dmax = hmax3(hmax3(dk[0], dk[1], dk[2]), hmax3(dk[3], dk[4], dk[5]), hmax3(dk[6], dk[7], dk[7]));
+    const h16x2 bmin = hmin3(hmin3(br[0], br[1], br[2]), hmin3(br[3], br[4], br[5]), hmin3(br[6], br[7], br[7]));
     const h16x2 zero = {(_Float16)0, (_Float16)0}, bias = {(_Float16)1024, (_Float16)1024};
     const h16x2 m = hmax3(dmax, -bmin, zero) + bias;                // 1024 + max(m, 0): bits 0x6400 + value
     return as_s2(__builtin_bit_cast(uint32_t, m)) - (s16x2){0x6401, 0x6401};
@@ -613,10 +614,15 @@ __device__ __forceinline__ uint32_t fastw_quad_test(const QuadTaps& q, int u, in
         const h16x2 br = hmax(hmin(d0, d8), hmin(d4, d12));
         mk[k] = __builtin_bit_cast(uint32_t, hmax(dk, -br));
     }
-    // {max over pair 2i, max over pair 2i+1}: the low halves of two pairs against their high halves
-    const h16x2 p01 = hmax(as_h2(__builtin_amdgcn_perm(mk[1], mk[0], 0x05040100u)), as_h2(__builtin_amdgcn_perm(mk[1], mk[0], 0x07060302u)));
-    const h16x2 p23 = hmax(as_h2(__builtin_amdgcn_perm(mk[3], mk[2], 0x05040100u)), as_h2(__builtin_amdgcn_perm(mk[3], mk[2], 0x07060302u)));
-    const uint32_t z01 = __builtin_bit_cast(uint32_t, p01 - tq), z23 = __builtin_bit_cast(uint32_t, p23 - tq);
+    // {max over pair 2i, max over pair 2i+1}: the low halves of two pairs against their high halves (asm: as a builtin
+    // the compiler canonicalises both v_perm results first, two more packed maxes per call)
+    auto pairmax = [](uint32_t a, uint32_t b) {
+        uint32_t r;
+        asm("v_pk_max_f16 %0, %1, %2" : "=v"(r) : "v"(__builtin_amdgcn_perm(b, a, 0x05040100u)), "v"(__builtin_amdgcn_perm(b, a, 0x07060302u)));
+        return as_h2(r);
+    };
+    const uint32_t z01 = __builtin_bit_cast(uint32_t, pairmax(mk[0], mk[1]) - tq);
+    const uint32_t z23 = __builtin_bit_cast(uint32_t, pairmax(mk[2], mk[3]) - tq);
     const uint32_t fail = __builtin_amdgcn_perm(z23, z01, 0x07050301u);   // sign byte of pair k at byte k
     const int sh = min(max(32 * u + 32 - 8 * PR, 0), 24);               // 8 x (4 - pairs of the quad in the window)
     return ~fail & (0x80808080u >> sh);
