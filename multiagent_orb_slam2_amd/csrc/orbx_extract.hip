@@ -441,20 +441,28 @@ __device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) {
     asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return as_h2(r);
 }
+// LDS-typed element types (address space 3): indexing through them is 32-bit address arithmetic
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) int16_t lds_i16;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+typedef __attribute__((address_space(3))) s16x2 lds_s16x2;
 // Pair-image row r of k_fast_wave starts at dword kS * r + kC * (r / 4).  The padded form (kS = 19, kC = 4) is laid
 // out for the compass pre-test's ds_read_b32 loads: a 32-lane half reads 8 rows x 4 quads (QR = 4) at base(row) + 4u
 // + o; with kS odd, rows r .. r+3 of a group of four start in distinct residues mod 4, and rows r and r + 4 start
 // 4 kS + kC = 80 = 16 (mod 32) dwords apart, so the half's 32 dwords sit in 32 distinct banks.  (A plain stride of 24
 // put every row at a multiple of 8 dwords: 8 banks, 4-way conflicts on every pre-test load.)
 template <int kS, int kC>
-__device__ __forceinline__ int fastw_row(int r) { return kS * r + kC * (r >> 2); }
+__device__ __forceinline__ int fastw_row(int r) { return __mul24(r, kS) + kC * (r >> 2); }   // v_mad_u32_u24, not a 64-bit mad
 __host__ __device__ constexpr int fastw_image_words(int rows, int s, int c) { return s * rows + c * ((rows - 1) >> 2); }
 
 // the 16 circle taps + centre of a pixel pair on the f16-biased pair image (pair words; odd offsets by v_alignbit)
 template <int kS, int kC>
-__device__ __forceinline__ void fast_taps_f16(const uint32_t* __restrict__ E, int y, int j, uint32_t (&r)[17]) {
+__device__ __forceinline__ void fast_taps_f16(const lds_u32* __restrict__ E, int y, int j, uint32_t (&r)[17]) {
     const int r0 = y - 3, m = r0 & 3;
-    const uint32_t* eb = E + fastw_row<kS, kC>(r0) + j;
+    const lds_u32* eb = E + fastw_row<kS, kC>(r0) + j;
     // row r0 + d starts kS * d + kC * ((m + d) / 4) dwords after row r0
 #define ORBX_TAP_W(dy, w) eb[((dy) + 3) * kS + (kC ? kC * ((m + (dy) + 3) >> 2) : 0) + (w)]
 #define ORBX_TAP(k, dx, dy) \
@@ -498,11 +506,11 @@ __device__ __forceinline__ s16x2 fast_score_from_taps_f16(const uint32_t (&r)[17
 // For a pixel pair the 8 neighbour pairs come from 3 aligned dwords per row (v_alignbit for the odd
 // shifts) and 7 v_pk_max_i16.
 
-__device__ __forceinline__ int nms_pair(const int16_t* __restrict__ sc, int SW, int rr, int j, int T1, int T2,
+__device__ __forceinline__ int nms_pair(const lds_i16* __restrict__ sc, int SW, int rr, int j, int T1, int T2,
                                         bool second) {
-    const uint32_t* r0 = (const uint32_t*)(sc + rr * SW + 2 * j);
-    const uint32_t* r1 = r0 + (SW >> 1);
-    const uint32_t* r2 = r1 + (SW >> 1);
+    const lds_u32* r0 = (const lds_u32*)(sc + rr * SW + 2 * j);
+    const lds_u32* r1 = r0 + (SW >> 1);
+    const lds_u32* r2 = r1 + (SW >> 1);
     const uint32_t a0 = r0[0], a1 = r0[1], a2 = r0[2];
     const uint32_t b0 = r1[0], b1 = r1[1], b2 = r1[2];
     const uint32_t c0 = r2[0], c1 = r2[1], c2 = r2[2];
@@ -537,11 +545,11 @@ struct WaveLds {               // per-wave slice of k_fast_wave's dynamic LDS (b
 // with v_pk_max_u16; the map is half the LDS of the i16 form.
 typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2v as_u2(uint32_t v) { return __builtin_bit_cast(u16x2v, v); }
-__device__ __forceinline__ uint32_t sc_row4(const uint8_t* __restrict__ scb, int b) {    // bytes b .. b+3
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(scb + (b & ~3));
+__device__ __forceinline__ uint32_t sc_row4(const lds_u8* __restrict__ scb, int b) {    // bytes b .. b+3
+    const lds_u32* w = (const lds_u32*)(scb + (b & ~3));
     return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(b & 3));
 }
-__device__ __forceinline__ int nms_pair_u8(const uint8_t* __restrict__ scb, int SWB, int rr, int j, int T1, int T2,
+__device__ __forceinline__ int nms_pair_u8(const lds_u8* __restrict__ scb, int SWB, int rr, int j, int T1, int T2,
                                            bool second) {
     const int b = rr * SWB + 2 * j + 1;
     const uint32_t x0 = sc_row4(scb, b), x1 = sc_row4(scb, b + SWB), x2 = sc_row4(scb, b + 2 * SWB);
@@ -574,10 +582,10 @@ __host__ __device__ __forceinline__ WaveLds wave_lds(int rows, int scrow, int np
 struct QuadTaps { uint32_t A[7], U[6], D[6]; };   // E words of rows y (7), y-3 and y+3 (5 each) of one quad
 
 template <int kS, int kC>
-__device__ __forceinline__ QuadTaps fastw_quad_load(const uint32_t* __restrict__ E, int rr, int u) {
-    const uint32_t* e0 = E + fastw_row<kS, kC>(rr) + 4 * u;          // row y-3
-    const uint32_t* e1 = E + fastw_row<kS, kC>(rr + 3) + 4 * u;      // row y
-    const uint32_t* e2 = E + fastw_row<kS, kC>(rr + 6) + 4 * u;      // row y+3
+__device__ __forceinline__ QuadTaps fastw_quad_load(const lds_u32* __restrict__ E, int rr, int u) {
+    const lds_u32* e0 = E + fastw_row<kS, kC>(rr) + 4 * u;          // row y-3
+    const lds_u32* e1 = E + fastw_row<kS, kC>(rr + 3) + 4 * u;      // row y
+    const lds_u32* e2 = E + fastw_row<kS, kC>(rr + 6) + 4 * u;      // row y+3
     QuadTaps q;
 #pragma unroll
     for (int k = 0; k < 7; ++k) q.A[k] = e1[k];
@@ -700,18 +708,18 @@ __host__ __device__ constexpr int fastw_sw(int ps) { return ps == 19 ? ORBX_FAST
 constexpr bool kScU8 = ORBX_FAST_U8SC != 0;
 __host__ __device__ constexpr int fastw_scrow(int ps) { return kScU8 ? (ps == 19 ? 40 : 80) : 2 * fastw_sw(ps); }
 
-__device__ __forceinline__ void sc_store(uint8_t* __restrict__ scb, int SWB, int rr, int j, s16x2 v, bool second) {
+__device__ __forceinline__ void sc_store(lds_u8* __restrict__ scb, int SWB, int rr, int j, s16x2 v, bool second) {
     if constexpr (kScU8) {
         const uint32_t u = ((uint32_t)(v.x + 1) & 0xffu) | (second ? (((uint32_t)(v.y + 1) & 0xffu) << 8) : 0u);
-        *reinterpret_cast<uint16_t*>(scb + (rr + 1) * SWB + 2 + 2 * j) = (uint16_t)u;
+        *(lds_u16*)(scb + (rr + 1) * SWB + 2 + 2 * j) = (uint16_t)u;
     } else {
-        *reinterpret_cast<s16x2*>(scb + (rr + 1) * SWB + 4 + 4 * j) = second ? v : (s16x2){v.x, (short)-1};
+        *(lds_s16x2*)(scb + (rr + 1) * SWB + 4 + 4 * j) = second ? v : (s16x2){v.x, (short)-1};
     }
 }
 
 // The part of a cell after its ROI is in LDS: pre-test, scores, NMS at both thresholds, the cell's candidate slots.
 template <int kPS, int kPC>
-__device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __restrict__ scb, uint16_t* __restrict__ list,
+__device__ __forceinline__ void fastw_body(lds_u32* __restrict__ E, lds_u8* __restrict__ scb, lds_u16* __restrict__ list,
                                            const CellDev& cd, int img, int* __restrict__ cnt_out, int Wd, int Hd, int T1,
                                            int T2, int tp, uint32_t* __restrict__ cand_xy, uint8_t* __restrict__ cand_s,
                                            int cand_stride, int kcap, int two_pass, int ln) {
@@ -724,8 +732,8 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __
     // second pass finds every minTh survivor (a superset of the first pass's, whose scores it rewrites with the same
     // values) and starts its list afresh.  Otherwise one pass at min(iniTh, minTh) keeps both thresholds' pixels.
     const bool two = two_pass && T2 < T1;
-    uint16_t* k1 = reinterpret_cast<uint16_t*>(E);                  // key lists over the pair image (dead after scoring)
-    uint16_t* k2 = k1 + kcap;
+    lds_u16* k1 = (lds_u16*)E;                  // key lists over the pair image (dead after scoring)
+    lds_u16* k2 = k1 + kcap;
     int n1 = 0, n2 = 0;                                               // wave-uniform
     for (int pass = 0; pass < 2; ++pass) {
     const int tpre = two ? (pass == 0 ? T1 : T2) : tp;
@@ -805,7 +813,7 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __
         if (i < ns) {
             const int rr = list[i] >> 8, j = list[i] & 0xff;
             if constexpr (kScU8) f = nms_pair_u8(scb, SWB, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
-            else f = nms_pair(reinterpret_cast<const int16_t*>(scb), SWB / 2, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
+            else f = nms_pair((const lds_i16*)scb, SWB / 2, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
             key = rr * 128 + 2 * j;
         }
         const uint64_t a0 = __ballot(f & 1), a1 = __ballot(f & 2), c0 = __ballot(f & 4), c1 = __ballot(f & 8);
@@ -822,7 +830,7 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __
     if (!two || n1 > 0) break;                                        // wave-uniform
     }
     // 5. the cell's list (iniTh, or minTh when iniTh kept nothing: :812-816) -> its candidate slots, coalesced
-    const uint16_t* ks = n1 > 0 ? k1 : k2;
+    const lds_u16* ks = n1 > 0 ? k1 : k2;
     const int n = min(n1 > 0 ? n1 : n2, min(kcap, cd.slot_cap));
     uint32_t* oxy = cand_xy + (size_t)img * cand_stride + cd.slot_off;
     uint8_t* os = cand_s + (size_t)img * cand_stride + cd.slot_off;
@@ -830,7 +838,7 @@ __device__ __forceinline__ void fastw_body(uint32_t* __restrict__ E, uint8_t* __
         const int k = ks[i], rr = k >> 7, x = k & 127;
         oxy[i] = (uint32_t)(cd.x0 + 3 + x) | ((uint32_t)(cd.y0 + rr + 3) << 16);
         if constexpr (kScU8) os[i] = (uint8_t)(scb[(rr + 1) * SWB + 2 + x] - 1);
-        else os[i] = (uint8_t)reinterpret_cast<const int16_t*>(scb)[(rr + 1) * (SWB / 2) + 2 + x];
+        else os[i] = (uint8_t)((const lds_i16*)scb)[(rr + 1) * (SWB / 2) + 2 + x];
     }
     if (ln == 0) *cnt_out = n;
 }
@@ -849,10 +857,12 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
     const int item = __builtin_amdgcn_readfirstlane(wg * kWpg + w);
     if (wg >= nwg || item >= total) return;                         // whole wave (no barrier in this kernel)
     const int img = item / ncell, c = cell0 + (item - img * ncell);
-    char* lds = reinterpret_cast<char*>(fsm) + w * lay.bytes;
-    uint32_t* E = reinterpret_cast<uint32_t*>(lds);
-    uint8_t* scb = reinterpret_cast<uint8_t*>(lds + lay.o_sc);
-    uint16_t* list = reinterpret_cast<uint16_t*>(lds + lay.o_list);
+    // typed LDS pointers: every address below is 32-bit arithmetic (through generic pointers the compiler formed them
+    // with 64-bit multiply-adds)
+    lds_u8* lds = (lds_u8*)fsm + w * lay.bytes;
+    lds_u32* E = (lds_u32*)lds;
+    lds_u8* scb = lds + lay.o_sc;
+    lds_u16* list = (lds_u16*)(lds + lay.o_list);
     const CellDev cd = cells[c];
     const int W = cd.W, H = cd.H, Wd = W - 6, Hd = H - 6;
     int* cnt_out = cell_cnt + (size_t)img * ncells + c;
@@ -868,7 +878,10 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
     constexpr uint32_t kBias8 = 0x64646464u;
     {
         // 1. cell ROI -> f16-biased pair image: lane items (row, 8-column chunk), one 8-byte load each, all of a round
-        //    issued before the first use; bytes past the ROI's width read as 0
+        //    issued before the first use.  Columns past the ROI's width (the last chunk's tail, real level pixels) are
+        //    staged as they are: no pre-test, score or NMS of a detection-window pixel reads past column W - 1 (its taps
+        //    reach 3 + 3 columns right of the window's last column Wd - 1 + 3); only the outside second pixel of an
+        //    odd-width row's last pair reads column W, and its result is never kept (fastw_quad_test).
         const LevelDev& L = levels[cd.level];
         int lstride;
         const uint8_t* base = level_pixels(pyr, pyr_stride, L, cd.level, img, s0, lstride);
@@ -889,21 +902,20 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
                     rs[k] = r; cs[k] = cc;
                     r += dr; cc += dc;
                     if (cc >= cpr) { cc -= cpr; ++r; }
-                    if (q0 + ln + k * kWave < NQ) __builtin_memcpy(&pf[k], src0 + (size_t)rs[k] * lstride + 16 * cs[k], 16);
+                    // every lane loads (an item past the ROI re-reads its last row and stores nothing), so a round's loads
+                    // issue back to back from the wave-uniform ROI base plus a 32-bit offset
+                    __builtin_memcpy(&pf[k], src0 + (uint32_t)(__mul24(min(rs[k], H - 1), lstride) + 16 * cs[k]), 16);
                 }
+                asm volatile("" : "+v"(pf[0].x), "+v"(pf[0].y), "+v"(pf[0].z), "+v"(pf[0].w));   // (as in the padded form)
 #pragma unroll
                 for (int k = 0; k < kPf; ++k) {
                     if (q0 + ln + k * kWave < NQ) {
                         const uint4 a = pf[k];
-                        const uint4 e0 = make_uint4(__builtin_amdgcn_perm(kBias8, a.x, 0x04010400u),
-                                                    __builtin_amdgcn_perm(kBias8, a.x, 0x04030402u),
-                                                    __builtin_amdgcn_perm(kBias8, a.y, 0x04010400u),
-                                                    __builtin_amdgcn_perm(kBias8, a.y, 0x04030402u));
-                        const uint4 e1 = make_uint4(__builtin_amdgcn_perm(kBias8, a.z, 0x04010400u),
-                                                    __builtin_amdgcn_perm(kBias8, a.z, 0x04030402u),
-                                                    __builtin_amdgcn_perm(kBias8, a.w, 0x04010400u),
-                                                    __builtin_amdgcn_perm(kBias8, a.w, 0x04030402u));
-                        uint4* dst = reinterpret_cast<uint4*>(E + fastw_row<kPS, kPC>(rs[k]) + 8 * cs[k]);
+                        const u32x4 e0 = {__builtin_amdgcn_perm(kBias8, a.x, 0x04010400u), __builtin_amdgcn_perm(kBias8, a.x, 0x04030402u),
+                                          __builtin_amdgcn_perm(kBias8, a.y, 0x04010400u), __builtin_amdgcn_perm(kBias8, a.y, 0x04030402u)};
+                        const u32x4 e1 = {__builtin_amdgcn_perm(kBias8, a.z, 0x04010400u), __builtin_amdgcn_perm(kBias8, a.z, 0x04030402u),
+                                          __builtin_amdgcn_perm(kBias8, a.w, 0x04010400u), __builtin_amdgcn_perm(kBias8, a.w, 0x04030402u)};
+                        lds_u32x4* dst = (lds_u32x4*)(E + fastw_row<kPS, kPC>(rs[k]) + 8 * cs[k]);
                         dst[0] = e0;
                         dst[1] = e1;
                     }
@@ -925,24 +937,21 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
                 int rs[kPf], cs[kPf];
 #pragma unroll
                 for (int k = 0; k < kPf; ++k) {
-                    const int q = q0 + ln + k * kWave;
                     rs[k] = r; cs[k] = cc;
                     r += dr; cc += dc;
                     if (cc >= cpr) { cc -= cpr; ++r; }
-                    pf[2 * k] = pf[2 * k + 1] = 0;
-                    if (q < NQ) __builtin_memcpy(&pf[2 * k], src0 + (size_t)rs[k] * lstride + 8 * cs[k], 8);
+                    // every lane loads (an item past the ROI re-reads its last row and stores nothing), so a round's loads
+                    // issue back to back from the wave-uniform ROI base plus a 32-bit offset
+                    __builtin_memcpy(&pf[2 * k], src0 + (uint32_t)(__mul24(min(rs[k], H - 1), lstride) + 8 * cs[k]), 8);
                 }
+                // the first item's bytes pass through an empty asm on every path: otherwise the compiler sinks its load
+                // into its store branch, issued after the others, and the first store waits for all four
+                asm volatile("" : "+v"(pf[0]), "+v"(pf[1]));
 #pragma unroll
                 for (int k = 0; k < kPf; ++k) {
                     if (q0 + ln + k * kWave < NQ) {
-                        uint32_t lo = pf[2 * k], hi = pf[2 * k + 1];
-                        const int keep = W - 8 * cs[k];
-                        if (keep < 8) {
-                            const uint64_t m = (1ull << (8 * keep)) - 1ull;        // keep >= 1
-                            const uint64_t v = (((uint64_t)hi << 32) | lo) & m;
-                            lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
-                        }
-                        uint32_t* dst = E + fastw_row<kPS, kPC>(rs[k]) + 4 * cs[k];
+                        const uint32_t lo = pf[2 * k], hi = pf[2 * k + 1];
+                        lds_u32* dst = E + fastw_row<kPS, kPC>(rs[k]) + 4 * cs[k];
                         dst[3] = __builtin_amdgcn_perm(kBias8, hi, 0x04030402u);
                         asm volatile("" ::: "memory");
                         dst[2] = __builtin_amdgcn_perm(kBias8, hi, 0x04010400u);
@@ -955,7 +964,7 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
         }
         // score map cleared to 0: pixels that fail the pre-test and the pad ring (a 0 never blocks a kept score >= 1)
         const int n16 = ((Hd + 2) * SWB + 15) >> 4;
-        for (int i = ln; i < n16; i += kWave) reinterpret_cast<uint4*>(scb)[i] = make_uint4(0, 0, 0, 0);
+        for (int i = ln; i < n16; i += kWave) ((lds_u32x4*)scb)[i] = (u32x4){0u, 0u, 0u, 0u};
     }
 #if ORBX_FAST_STOP == 1
     if (ln == 0) *cnt_out = 0;                                        // diagnostics: the ROI staging only
@@ -1255,9 +1264,6 @@ __device__ unsigned long long g_qtprof[2][64];
 #define QTP(tag) do {} while (0)
 #endif
 
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef __attribute__((address_space(3))) int16_t lds_i16;
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 // split point of a node, packed (x0 + ceil((x1-x0)/2)) | (y0 + ceil((y1-y0)/2)) << 16 (DivideNode :483-509; the float
 // halving of an integer width is exact, so its ceiling is (w + 1) >> 1); a key's quadrant is (x >= mx) + 2 (y >= my)
