@@ -1157,7 +1157,9 @@ __device__ __forceinline__ void blur_band2(const uint8_t* __restrict__ S, int ss
 }
 
 #ifndef ORBX_BLUR_WPE
-#define ORBX_BLUR_WPE 6     // 80 VGPRs: 6 waves per SIMD (r4ak: serial blur 0.588 -> 0.571 ms; 8 spills 25 VGPRs)
+#define ORBX_BLUR_WPE 5     // 82 VGPRs, no spills: 5 waves per SIMD.  r5ae: serial blur 0.550 -> 0.561 ms, but the step
+                            // +1.6 % (72.6k -> 73.8k frames/s, 4 ties 5, two rounds): fewer blur waves beside FAST and the
+                            // describe.  (6 per SIMD at 80 VGPRs was r4ak's choice by the serial time: 0.588 -> 0.571 ms.)
 #endif
 // one wave's blur tile (level, 256-column strip, ORBX_BLUR_BAND-row band) of image img
 __device__ __forceinline__ void blur_tile(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride,
