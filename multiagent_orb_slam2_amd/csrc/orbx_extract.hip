@@ -133,6 +133,12 @@ __constant__ __attribute__((aligned(16))) PatternByLane<16> c_pattern_l16 = make
 // umax for HALF_PATCH_SIZE = 15 (ORBextractor ctor :454-469); the host recomputes it and checks equality
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
+// Diagnostics builds only: ORBX_VCLOB_<KERNEL>=r makes that kernel allocate r + 1 VGPRs (an empty asm clobbering v<r>),
+// capping its waves per SIMD at 512 / (r + 1), to measure how its occupancy trades against the kernels beside it.
+#define ORBX_VSTR2(x) #x
+#define ORBX_VSTR(x) ORBX_VSTR2(x)
+#define ORBX_VCLOB_AT(n) asm volatile("" ::: "v" ORBX_VSTR(n))
+
 // =============================================================================================
 // kernels
 // =============================================================================================
@@ -294,6 +300,9 @@ __device__ __forceinline__ void resize4_item(uint8_t* __restrict__ pyr, size_t p
 __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
                                                  size_t src_step, size_t src_istride, int sw, int dst_off, int dw, int dh,
                                                  ResizeVec t, int nstrips, int nbands, int batch) {
+#ifdef ORBX_VCLOB_RESIZE
+    ORBX_VCLOB_AT(ORBX_VCLOB_RESIZE);
+#endif
     const int nwaves = nstrips * nbands * batch;
     const int nwg = (nwaves + 3) / 4;
     const int wg = xcd_item(xcd_chunk(nwg));
@@ -1184,6 +1193,9 @@ __device__ __forceinline__ void blur_tile(const uint8_t* __restrict__ pyr, uint8
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_WPE))) void k_blur7(
     const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride, const LevelDev* __restrict__ levels,
     const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
+#ifdef ORBX_VCLOB_BLUR
+    ORBX_VCLOB_AT(ORBX_VCLOB_BLUR);
+#endif
     // tiles [tile0, tile0 + ntiles) of every image (a level range: tiles are level-major)
     const int nbx = (ntiles + 3) / 4;                         // 4 tiles (waves) per workgroup
     const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
@@ -1659,6 +1671,9 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                                                          int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
                                                          int scan_cap, int* __restrict__ err, int lvl0, int key_lds_off,
                                                          int key_lds_cap, unsigned seq) {
+#ifdef ORBX_VCLOB_QT
+    ORBX_VCLOB_AT(ORBX_VCLOB_QT);
+#endif
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int lvl = lvl0 + (int)blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
 #ifdef ORBX_QT_PROF
@@ -1819,6 +1834,9 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
                                                     int32_t* __restrict__ counts, int capacity, int slot0, int nslots,
                                                     int write_count, int batch, Src0 s0, SlotTable tab, unsigned seq,
                                                     int* __restrict__ err) {
+#ifdef ORBX_VCLOB_DESC
+    ORBX_VCLOB_AT(ORBX_VCLOB_DESC);
+#endif
     constexpr int kLp = kWave / kKpw;
     constexpr int kWinItems = 5 * (2 * kBriefR + 1);             // 37 rows x 5 chunks of 8 bytes
     constexpr int kNW = (kWinItems + kLp - 1) / kLp;             // window chunks per lane
