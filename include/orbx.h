@@ -499,6 +499,16 @@ int orbx_proj_project_device(orbx_matcher* m, int mode, const orbx_map_point* d_
                              int nlevels, float log_scale_factor, const int32_t* d_found, orbx_proj_query* d_queries,
                              void* stream);
 
+/* What SearchLocalPoints skips after SearchByProjection(CurrentFrame, LastFrame) (src/Tracking.cc:1160-1182), for
+ * n_sets (query set, frame) pairs in one launch: d_found[s * n_queries + q] = 0 when MapPoint q is in the frame --
+ * it was assigned a keypoint (k = d_q_idx[s * n_queries + q] >= 0) and that keypoint still holds it
+ * (d_owner[s * n_keypoints + k] == q; the rotation filter resets the entries it drops, ORBmatcher.cc:1456-1466) --
+ * else -1 (the d_found layout of orbx_proj_project_device); d_blocked[s * n_keypoints + i] (optional) = 1 when keypoint
+ * i holds a MapPoint (owner >= 0), else 0 (a problem's `blocked` bytes).  Replaces the host loop over
+ * mCurrentFrame.mvpMapPoints that sets mbTrackInView = false. */
+int orbx_proj_found_device(orbx_matcher* m, const int32_t* d_q_idx, const int32_t* d_owner, int n_sets, int n_queries,
+                           int n_keypoints, int32_t* d_found, uint8_t* d_blocked, void* stream);
+
 /* MapPoints of stereo frames (Frame::UnprojectStereo src/Frame.cc:666-680 + MapPoint::MapPoint(Pos, pMap, pFrame, idxF)
  * src/MapPoint.cc:47-68, as Tracking::StereoInitialization / CreateNewKeyFrame / UpdateLastFrame create them):
  * for keypoint i of frame b with depth z > 0, X = Rwc * ((u - cx) z / fx, (v - cy) z / fy, z) + Ow, the normal

@@ -779,6 +779,19 @@ __global__ __launch_bounds__(256) void k_undistort(Undist U, int copy_only, cons
     out[(size_t)b * capacity + i] = kp;
 }
 
+// SearchLocalPoints' skip rule after the motion-model search (src/Tracking.cc:1160-1182): one thread per (set, query) and
+// per (set, keypoint); the grid's x covers max(n_queries, n_keypoints).
+__global__ __launch_bounds__(256) void k_proj_found(const int32_t* __restrict__ q_idx, const int32_t* __restrict__ owner,
+                                                    int nq, int nk, int32_t* __restrict__ found, uint8_t* __restrict__ blocked) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
+    const int32_t* ow = owner + (size_t)s * nk;
+    if (i < nq) {
+        const int k = q_idx[(size_t)s * nq + i];
+        found[(size_t)s * nq + i] = (k >= 0 && k < nk && ow[k] == i) ? 0 : -1;
+    }
+    if (blocked && i < nk) blocked[(size_t)s * nk + i] = ow[i] >= 0 ? 1 : 0;
+}
+
 }  // namespace orbx
 
 using namespace orbx;
@@ -895,6 +908,20 @@ int orbx_proj_project_device(orbx_matcher* m, int mode, const orbx_map_point* d_
     ORBX_HIP(hipSetDevice(matcher_device(m)));
     hipLaunchKernelGGL(k_project, dim3((capacity + 255) / 256, n_views), dim3(256), 0, (hipStream_t)stream, mode, d_points,
                        d_counts, 0, capacity, d_views, d_view_points, sc, nlevels, log_scale_factor, d_found, d_queries);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_proj_found_device(orbx_matcher* m, const int32_t* d_q_idx, const int32_t* d_owner, int n_sets, int n_queries,
+                           int n_keypoints, int32_t* d_found, uint8_t* d_blocked, void* stream) {
+    ORBX_REQUIRE(m && d_q_idx && d_owner && d_found && n_sets >= 0 && n_queries >= 0 && n_keypoints >= 0, ORBX_ERR_ARG,
+                 "bad argument");
+    const int n = std::max(n_queries, n_keypoints);
+    if (n_sets == 0 || n == 0) return ORBX_OK;
+    ORBX_REQUIRE(n_sets <= 65535, ORBX_ERR_UNSUPPORTED, "too many sets");
+    ORBX_HIP(hipSetDevice(matcher_device(m)));
+    hipLaunchKernelGGL(k_proj_found, dim3((n + 255) / 256, n_sets), dim3(256), 0, (hipStream_t)stream, d_q_idx, d_owner,
+                       n_queries, n_keypoints, d_found, d_blocked);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }

@@ -19,6 +19,8 @@ from __future__ import annotations
 from collections import OrderedDict
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 
 HEADER = 32        # int32 count, agent, frame, n_fv (FeatureVector nodes), n_words (BowVector entries), 3 x pad
@@ -687,7 +689,6 @@ class FrameTracker:
         # the last frame holds the MapPoints of every second keypoint (its tracked points); the local map holds all of
         # them, so SearchLocalPoints has the other half plus the motion-model misses to find (found >= 0: skipped)
         self.lf_skip = torch.tensor([-1, 0], dtype=torch.int32).repeat(B, (cap + 1) // 2)[:, :cap].contiguous().to(dev)
-        self.q_ar = torch.arange(cap, dtype=torch.int32, device=dev).view(1, cap).expand(B, cap)
         self.sets = []
         for _ in range(n_sets):
             z = dict(pts=torch.empty((B, cap, 48), dtype=torch.uint8, device=dev),
@@ -732,7 +733,6 @@ class FrameTracker:
     def run(self, s: int, kps, desc, counts, stream=None):
         """Frames kps / desc / counts (B, cap, 28) / (B, cap, 32) / (B,) with the stereo results already in set s's
         (uright, depth).  Returns (q_idx motion model, nmatches, q_idx local map, nmatches) tensors of set s."""
-        import torch
         from .orbx import PROJ_LASTFRAME, PROJ_MAPPOINTS, QF_BLOCKS
         z, m, cap = self.sets[s], self.m, self.cap
         p1, p2 = self._problems(z, kps, desc)
@@ -740,16 +740,25 @@ class FrameTracker:
                                   stream=stream)
         m.proj_project_device(PROJ_LASTFRAME, z["pts"], counts, self.v_lf, self.scale, self.log_sf, out=z["q1"],
                               found=self.lf_skip, stream=stream)
-        m.grid_build_device(self.grid, kps, counts, stream=stream, out=(z["cs"], z["ci"]))
+        if not (os.environ.get("ORBX_TRACK_SKIP_GRID") and z.get("grid_done")):   # timing probe only (stale grid)
+            m.grid_build_device(self.grid, kps, counts, stream=stream, out=(z["cs"], z["ci"]))
+            z["grid_done"] = True
         m.proj_search_batch_device(self.p_lf, self.grid, p1, cap, cap, stream=stream)
-        with torch.cuda.stream(stream) if stream is not None else _nullcontext():
-            torch.ge(z["own1"], 0, out=z["blk"])                    # keypoints that now hold a MapPoint
-            # SearchLocalPoints skips the MapPoints that are in mCurrentFrame.mvpMapPoints (Tracking.cc:1163-1177):
-            # query q's match stands only if the keypoint's owner is still q -- the rotation filter sets the entries
-            # it drops back to NULL (ORBmatcher.cc:1456-1466; owner -2), and those MapPoints are searched again
-            own_at = torch.gather(z["own1"], 1, z["qi1"].clamp(min=0).long())
-            z["fnd"].fill_(-1)
-            z["fnd"].masked_fill_((z["qi1"] >= 0) & (own_at == self.q_ar), 0)
+        # SearchLocalPoints skips the MapPoints that are in mCurrentFrame.mvpMapPoints (Tracking.cc:1163-1177): query
+        # q's match stands only if the keypoint's owner is still q -- the rotation filter sets the entries it drops back
+        # to NULL (ORBmatcher.cc:1456-1466; owner -2), and those MapPoints are searched again; the keypoints that now
+        # hold a MapPoint are blocked for the second search.  One launch (orbx_proj_found_device) instead of eight
+        # elementwise torch kernels on the stereo queue.
+        if os.environ.get("ORBX_TRACK_TORCH_FOUND"):              # A/B only: the elementwise torch form
+            import torch
+            with torch.cuda.stream(stream) if stream is not None else _nullcontext():
+                torch.ge(z["own1"], 0, out=z["blk"])
+                q_ar = torch.arange(cap, dtype=torch.int32, device=self.dev).view(1, cap)
+                own_at = torch.gather(z["own1"], 1, z["qi1"].clamp(min=0).long())
+                z["fnd"].fill_(-1)
+                z["fnd"].masked_fill_((z["qi1"] >= 0) & (own_at == q_ar), 0)
+        else:
+            m.proj_found_device(z["qi1"], z["own1"], z["fnd"], blocked=z["blk"], stream=stream)
         m.proj_project_device(PROJ_MAPPOINTS, z["pts"], counts, self.v_mp, self.scale, self.log_sf, out=z["q2"],
                               found=z["fnd"], stream=stream)
         m.proj_search_batch_device(self.p_mp, self.grid, p2, cap, cap, stream=stream)

@@ -200,6 +200,7 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_proj_project.argtypes = [vp, i32, vp, i32, vp, vp, i32, f32, vp]
     lib.orbx_proj_project_device.argtypes = [vp, i32, vp, vp, i32, i32, vp, vp, vp, i32, f32, vp, vp, vp]
     lib.orbx_stereo_mappoints_device.argtypes = [vp, vp, vp, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp]
+    lib.orbx_proj_found_device.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp]
     lib.orbx_matcher_create.argtypes = [f32, i32, i32, C.POINTER(vp)]
     for name in ("orbx_extractor_destroy", "orbx_matcher_destroy", "orbx_extractor_get_levels"):
         getattr(lib, name).argtypes = [vp]
@@ -941,6 +942,18 @@ class ORBmatcher:
                                                   _p(sc), len(sc), float(log_scale_factor),
                                                   None if found is None else _tp(found), _tp(out), s))
         return out
+
+    def proj_found_device(self, q_idx, owner, found, blocked=None, stream=None):
+        """SearchLocalPoints' skip rule after the motion-model search (include/orbx.h orbx_proj_found_device): q_idx
+        (S, nq) and owner (S, n) int32 device tensors -> found (S, nq) int32 (0: MapPoint q is in the frame, else -1)
+        and, when given, blocked (S, n) bool/uint8 (the keypoint holds a MapPoint), in one launch."""
+        import torch
+        S, nq = q_idx.shape
+        n = owner.shape[1]
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(q_idx.device).cuda_stream)
+        _check(self._lib.orbx_proj_found_device(self._h, _tp(q_idx), _tp(owner), S, nq, n, _tp(found),
+                                                None if blocked is None else _tp(blocked), s))
+        return found
 
     def stereo_mappoints_device(self, kps, depth, counts, twc, camera, scale_factors, flags: int, out=None, stream=None):
         """MapPoints of stereo frames (include/orbx.h orbx_stereo_mappoints_device): kps (B, cap, 28) uint8, depth

@@ -148,3 +148,36 @@ def test_local_fuse_vs_oracle(gpu):
             assert nb_[p] == r2 and np.array_equal(qb[p, :len(p2)], ri2), (s, t, "neighbour into current")
             found += r + r2
     assert na[3] > 500 and nb_[3] > 500, (na, nb_)          # slot 5 <-> slot 4: the same scene from the same pose
+
+
+def test_proj_found_device_rule(gpu):
+    """orbx_proj_found_device against the host rule (multiagent.found_in_frame) on random assignments: unmatched
+    queries (-1), queries whose keypoint the rotation filter released (owner -2) or re-assigned to another query, and
+    the blocked bytes (owner >= 0); nq != n and one empty set."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from multiagent_orb_slam2_amd.multiagent import found_in_frame
+    rng = np.random.default_rng(7)
+    S_, nq, n = 5, 700, 450
+    q_idx = np.full((S_, nq), -1, np.int32)
+    owner = np.full((S_, n), -1, np.int32)
+    for s in range(1, S_):                       # set 0: nothing matched
+        qs = rng.choice(nq, size=300, replace=False)
+        ks = rng.choice(n, size=300, replace=False)
+        q_idx[s, qs] = ks
+        owner[s, ks] = qs
+        drop = rng.choice(300, size=40, replace=False)
+        owner[s, ks[drop[:20]]] = -2             # released by the rotation filter
+        owner[s, ks[drop[20:]]] = qs[(drop[20:] + 1) % 300]   # held by another query
+    m = pkg.ORBmatcher(0.9, True)
+    dq, do = torch.from_numpy(q_idx).cuda(), torch.from_numpy(owner).cuda()
+    found = torch.empty((S_, nq), dtype=torch.int32, device="cuda")
+    blocked = torch.empty((S_, n), dtype=torch.bool, device="cuda")
+    m.proj_found_device(dq, do, found, blocked=blocked)
+    torch.cuda.synchronize()
+    for s in range(S_):
+        want = np.where(found_in_frame(q_idx[s], owner[s]), 0, -1)
+        assert np.array_equal(found[s].cpu().numpy(), want), s
+        assert np.array_equal(blocked[s].cpu().numpy(), owner[s] >= 0), s
+    assert (found[1:] == 0).sum().item() == 4 * 260
