@@ -451,6 +451,14 @@ int orbx_grid_build_device(orbx_matcher* m, orbx_grid grid, const orbx_keypoint*
 int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
                                   const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq,
                                   void* stream);
+/* As orbx_proj_search_batch_device, with each problem's grid built inside its search: problem p's cell_start /
+ * cell_idx are OUTPUTS, Frame::AssignFeaturesToGrid (src/Frame.cc:230-245) of its first d_grid_counts[p] (<= n) target
+ * keypoints -- the same CSR arrays as orbx_grid_build_device, for later searches of the frame -- so a frame's first
+ * search (Tracking::TrackWithMotionModel's, on a fresh Frame) needs no separate grid launch.  Not for
+ * ORBX_PROJ_INIT; ORBX_ERR_UNSUPPORTED when the grid and the keypoints do not fit the launch's LDS plan. */
+int orbx_proj_search_grid_batch_device(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
+                                       const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq,
+                                       const int32_t* d_grid_counts, void* stream);
 /* Host form: one query set against one view (host buffers; uright / blocked / owner may be NULL). */
 int orbx_proj_search(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid, const orbx_proj_query* queries,
                      const uint8_t* qdesc, int nq, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,

@@ -193,10 +193,14 @@ __device__ __forceinline__ bool proj_window(const orbx_grid& g, const orbx_proj_
 }
 
 // CSR entry j of a problem: staged in LDS, or assembled from the problem's arrays
+__device__ __forceinline__ float4 proj_entry_of(const orbx_proj_problem& pb, int idx);
 template <bool kLds>
 __device__ __forceinline__ float4 proj_entry(const orbx_proj_problem& pb, const float4* ent, int j) {
     if constexpr (kLds) return ent[j];
-    const int idx = pb.cell_idx[j];
+    return proj_entry_of(pb, pb.cell_idx[j]);
+}
+// the 16-byte staged entry of target keypoint idx: {x, y, uright, idx | octave << 13 | blocked | has-uright}
+__device__ __forceinline__ float4 proj_entry_of(const orbx_proj_problem& pb, int idx) {
     const orbx_keypoint kp = pb.kps[idx];
     uint32_t meta = (uint32_t)idx | ((uint32_t)kp.octave << 13);
     if (pb.blocked && pb.blocked[idx]) meta |= kMetaBlocked;
@@ -300,12 +304,74 @@ __device__ __forceinline__ bool proj_over_cap(const orbx_proj_problem& pb, int n
     return true;
 }
 
+// Frame::AssignFeaturesToGrid (src/Frame.cc:230-245) of a problem's first ng target keypoints inside its search
+// workgroup -- the counting form of k_grid_count (cell counts by LDS atomics, exclusive scan, scatter by atomic cursors,
+// each cell's indices put back in ascending order by one thread), so the CSR arrays are the same -- leaving the cell
+// starts in cs_l[0 .. ncell] and the entries in CSR order in ent_l, and writing both arrays to the problem's cell_start /
+// cell_idx for later searches of the same frame.  cof / idx: 2 x ng u16 of scratch LDS; tmp: nwaves + 1 ints.
+__device__ void proj_grid_stage(const orbx_proj_problem& pb, const orbx_grid& g, int ng, int ncell, int* cs_l, float4* ent_l,
+                                uint16_t* cof, uint16_t* idx, int* tmp) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    for (int c = tid; c <= ncell; c += T) cs_l[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < ng; i += T) {
+        const int c = grid_cell(g, pb.kps[i].x, pb.kps[i].y);
+        cof[i] = (uint16_t)(c < 0 ? 0xffff : c);
+        if (c >= 0) atomicAdd(&cs_l[c], 1);
+    }
+    __syncthreads();
+    block_scan_array(cs_l, ncell + 1, tmp);              // cs_l[c] = start of cell c; cs_l[ncell] = keypoints in cells
+    int32_t* gcs = const_cast<int32_t*>(pb.cell_start);
+    for (int c = tid; c <= ncell; c += T) gcs[c] = cs_l[c];
+    __syncthreads();
+    for (int i = tid; i < ng; i += T) {
+        const int c = cof[i];
+        if (c != 0xffff) idx[atomicAdd(&cs_l[c], 1)] = (uint16_t)i;
+    }
+    __syncthreads();                                     // cs_l[c] = end of cell c
+    for (int c = tid; c < ncell; c += T) {
+        const int b = c ? cs_l[c - 1] : 0, e = cs_l[c];
+        for (int j = b + 1; j < e; ++j) {
+            const uint16_t v = idx[j];
+            int k = j - 1;
+            while (k >= b && idx[k] > v) { idx[k + 1] = idx[k]; --k; }
+            idx[k + 1] = v;
+        }
+    }
+    __syncthreads();
+    const int total = ncell ? cs_l[ncell - 1] : 0;
+    int32_t* gci = const_cast<int32_t*>(pb.cell_idx);
+    for (int j = tid; j < total; j += T) {
+        const int k = idx[j];
+        gci[j] = k;
+        ent_l[j] = proj_entry_of(pb, k);
+    }
+    // starts back in place (start[c] = end[c - 1], start[ncell] = total): chunks of 4 T cells from the top down, so a
+    // chunk reads its lower neighbour before that neighbour is rewritten
+    const int nch = (ncell + 1 + 4 * T - 1) / (4 * T);
+    for (int ch = nch - 1; ch >= 0; --ch) {
+        int v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int c = ch * 4 * T + r * T + tid;
+            v[r] = (c <= ncell && c > 0) ? cs_l[c - 1] : 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int c = ch * 4 * T + r * T + tid;
+            if (c <= ncell) cs_l[c] = v[r];
+        }
+        __syncthreads();
+    }
+}
+
 // Modes MAPPOINTS .. BEST.  Dynamic LDS: [kLds: cell starts (ncell + 1), entries (16 B x n)] then, for the assigning
 // modes, claim[n], own[n], res[nq] (idx | dist << 13, or -1), qm[nq] (kQm* byte) and the lists (kcap x nq).
 template <bool kLds, bool kAssign>
 __global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(orbx_proj_params P, orbx_grid g,
                                                               const orbx_proj_problem* __restrict__ probs, int n_cap,
-                                                              int nq_cap, int kcap) {
+                                                              int nq_cap, int kcap, const int32_t* __restrict__ grid_counts) {
     extern __shared__ __attribute__((aligned(16))) int psm[];
     __shared__ int changed, hist[32], keep[3], acc_sh, bad_sh;
     __shared__ float isg[32];                          // mvInvLevelSigma2 (a per-lane index into the kernel arguments
@@ -323,9 +389,16 @@ __global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(o
         lp += ((size_t)(ncell + 1) * 4 + 15) & ~(size_t)15;
         float4* ent_l = reinterpret_cast<float4*>(lp);
         lp += (size_t)16 * n_cap;
-        for (int c = tid; c <= ncell; c += T) cs_l[c] = pb.cell_start[c];
-        const int ncsr = min(pb.cell_start[ncell], n);
-        for (int j = tid; j < ncsr; j += T) ent_l[j] = proj_entry<false>(pb, nullptr, j);
+        if (grid_counts) {
+            // the grid built here (orbx_proj_search_grid_batch_device); scratch: the LDS after the entries, free until the
+            // assigning modes' arrays are initialised below (the launch reserves it for the non-assigning ones)
+            uint16_t* cof = reinterpret_cast<uint16_t*>(lp);
+            proj_grid_stage(pb, g, min(grid_counts[blockIdx.x], n), ncell, cs_l, ent_l, cof, cof + n_cap, hist);
+        } else {
+            for (int c = tid; c <= ncell; c += T) cs_l[c] = pb.cell_start[c];
+            const int ncsr = min(pb.cell_start[ncell], n);
+            for (int j = tid; j < ncsr; j += T) ent_l[j] = proj_entry<false>(pb, nullptr, j);
+        }
         cs = cs_l;
         ent = ent_l;
     }
@@ -1015,8 +1088,9 @@ int orbx_grid_build_device(orbx_matcher* m, orbx_grid grid, const orbx_keypoint*
     return ORBX_OK;
 }
 
-int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
-                                  const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq, void* stream) {
+static int proj_search_batch(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
+                             const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq,
+                             const int32_t* d_grid_counts, void* stream) {
     ORBX_REQUIRE(m && params && d_problems && n_problems >= 0 && max_n >= 0 && max_nq >= 0, ORBX_ERR_ARG, "bad argument");
     int st = grid_check(grid);
     if (st) return st;
@@ -1026,6 +1100,7 @@ int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* param
     if (n_problems == 0) return ORBX_OK;
     ORBX_HIP(hipSetDevice(matcher_device(m)));
     hipStream_t s = (hipStream_t)stream;
+    ORBX_REQUIRE(!d_grid_counts || P.mode != ORBX_PROJ_INIT, ORBX_ERR_UNSUPPORTED, "grid built in the search: not for INIT");
     if (P.mode == ORBX_PROJ_INIT) {
         const size_t lds = (size_t)(2 * std::max(max_n, 1) + std::max(max_nq, 1)) * 4;
         ORBX_REQUIRE(lds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "too many keypoints for SearchForInitialization (%d, %d)", max_n,
@@ -1043,8 +1118,13 @@ int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* param
         const size_t stage = ((4 * (ncell + 1) + 15) & ~(size_t)15) + 16 * N;
         const size_t cap = 160 * 1024;
         ORBX_REQUIRE(core <= cap, ORBX_ERR_UNSUPPORTED, "too many target keypoints (%d) / queries (%d)", max_n, max_nq);
-        const bool staged = stage + core <= cap;
-        const size_t used = core + (staged ? stage : 0);
+        // a grid built in the search needs 4 B per target keypoint of scratch after the entries (the assigning modes'
+        // claim / own arrays serve) and the staged form, u16 cells and indices
+        const size_t gscr = (d_grid_counts && !assigning) ? ((4 * N + 15) & ~(size_t)15) : 0;
+        const bool staged = stage + core + gscr <= cap;
+        ORBX_REQUIRE(!d_grid_counts || (staged && ncell < 0xffff && N < 0xffff), ORBX_ERR_UNSUPPORTED,
+                     "grid built in the search: %d keypoints, %d cells do not fit the staged plan", max_n, (int)ncell);
+        const size_t used = core + (staged ? stage + gscr : 0);
         int kcap = 0;
         if (assigning) kcap = (int)std::min<size_t>(kProjListMax, (cap - used) / (4 * NQ));
         const size_t lds = std::max<size_t>(used + (size_t)kcap * 4 * NQ, 16);
@@ -1066,10 +1146,23 @@ int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* param
             return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
         }();
         const int threads = assigning ? a_threads : na_threads;
-        hipLaunchKernelGGL(kern, dim3(n_problems), dim3(threads), lds, s, P, grid, d_problems, (int)N, (int)NQ, kcap);
+        hipLaunchKernelGGL(kern, dim3(n_problems), dim3(threads), lds, s, P, grid, d_problems, (int)N, (int)NQ, kcap,
+                           d_grid_counts);
     }
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
+}
+
+int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
+                                  const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq, void* stream) {
+    return proj_search_batch(m, params, grid, d_problems, n_problems, max_n, max_nq, nullptr, stream);
+}
+
+int orbx_proj_search_grid_batch_device(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
+                                       const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq,
+                                       const int32_t* d_grid_counts, void* stream) {
+    ORBX_REQUIRE(d_grid_counts, ORBX_ERR_ARG, "bad argument");
+    return proj_search_batch(m, params, grid, d_problems, n_problems, max_n, max_nq, d_grid_counts, stream);
 }
 
 // Host form: one query set against one view; builds the view's grid, runs the search, copies results back.

@@ -740,25 +740,19 @@ class FrameTracker:
                                   stream=stream)
         m.proj_project_device(PROJ_LASTFRAME, z["pts"], counts, self.v_lf, self.scale, self.log_sf, out=z["q1"],
                               found=self.lf_skip, stream=stream)
-        if not (os.environ.get("ORBX_TRACK_SKIP_GRID") and z.get("grid_done")):   # timing probe only (stale grid)
+        if os.environ.get("ORBX_TRACK_GRID_LAUNCH"):               # A/B only: Frame::AssignFeaturesToGrid as its own launch
             m.grid_build_device(self.grid, kps, counts, stream=stream, out=(z["cs"], z["ci"]))
-            z["grid_done"] = True
-        m.proj_search_batch_device(self.p_lf, self.grid, p1, cap, cap, stream=stream)
+            m.proj_search_batch_device(self.p_lf, self.grid, p1, cap, cap, stream=stream)
+        else:
+            # the frame's grid (Frame::AssignFeaturesToGrid) built inside the motion-model search, which writes it out
+            # for the local-map search: one 1024-thread workgroup per frame to place beside the front end instead of two
+            m.proj_search_batch_device(self.p_lf, self.grid, p1, cap, cap, stream=stream, grid_counts=counts)
         # SearchLocalPoints skips the MapPoints that are in mCurrentFrame.mvpMapPoints (Tracking.cc:1163-1177): query
         # q's match stands only if the keypoint's owner is still q -- the rotation filter sets the entries it drops back
         # to NULL (ORBmatcher.cc:1456-1466; owner -2), and those MapPoints are searched again; the keypoints that now
         # hold a MapPoint are blocked for the second search.  One launch (orbx_proj_found_device) instead of eight
         # elementwise torch kernels on the stereo queue.
-        if os.environ.get("ORBX_TRACK_TORCH_FOUND"):              # A/B only: the elementwise torch form
-            import torch
-            with torch.cuda.stream(stream) if stream is not None else _nullcontext():
-                torch.ge(z["own1"], 0, out=z["blk"])
-                q_ar = torch.arange(cap, dtype=torch.int32, device=self.dev).view(1, cap)
-                own_at = torch.gather(z["own1"], 1, z["qi1"].clamp(min=0).long())
-                z["fnd"].fill_(-1)
-                z["fnd"].masked_fill_((z["qi1"] >= 0) & (own_at == q_ar), 0)
-        else:
-            m.proj_found_device(z["qi1"], z["own1"], z["fnd"], blocked=z["blk"], stream=stream)
+        m.proj_found_device(z["qi1"], z["own1"], z["fnd"], blocked=z["blk"], stream=stream)
         m.proj_project_device(PROJ_MAPPOINTS, z["pts"], counts, self.v_mp, self.scale, self.log_sf, out=z["q2"],
                               found=z["fnd"], stream=stream)
         m.proj_search_batch_device(self.p_mp, self.grid, p2, cap, cap, stream=stream)

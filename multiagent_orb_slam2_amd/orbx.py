@@ -254,6 +254,7 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_undistort_keypoints_device.argtypes = [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]
     lib.orbx_compute_image_bounds.argtypes = [vp, vp, vp, i32, i32, i32, vp]
     lib.orbx_proj_search_batch_device.argtypes = [vp, C.POINTER(ProjParams), Grid, vp, i32, i32, i32, vp]
+    lib.orbx_proj_search_grid_batch_device.argtypes = [vp, C.POINTER(ProjParams), Grid, vp, i32, i32, i32, vp, vp]
     lib.orbx_proj_search.argtypes = [vp, C.POINTER(ProjParams), Grid, vp, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp,
                                      C.POINTER(i32)]
     lib.orbx_vocab_load_text.argtypes = [C.c_char_p, i32, C.POINTER(vp)]
@@ -987,12 +988,19 @@ class ORBmatcher:
         _check(self._lib.orbx_grid_build_device(self._h, grid, _tp(kps), _tp(counts), B, cap, _tp(cs), _tp(ci), s))
         return cs, ci
 
-    def proj_search_batch_device(self, params: ProjParams, grid: Grid, problems, max_n: int, max_nq: int, stream=None):
-        """problems: uint8 device tensor holding n ProjProblem structs (see ProjProblem)."""
+    def proj_search_batch_device(self, params: ProjParams, grid: Grid, problems, max_n: int, max_nq: int, stream=None,
+                                 grid_counts=None):
+        """problems: uint8 device tensor holding n ProjProblem structs (see ProjProblem).  grid_counts: optional (n,)
+        int32 device tensor -- each problem's grid is built inside its search from its first grid_counts[p] target
+        keypoints and written to its cell_start / cell_idx (orbx_proj_search_grid_batch_device)."""
         import torch
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(problems.device).cuda_stream)
         n = problems.numel() // C.sizeof(ProjProblem)
-        _check(self._lib.orbx_proj_search_batch_device(self._h, C.byref(params), grid, _tp(problems), n, max_n, max_nq, s))
+        if grid_counts is None:
+            _check(self._lib.orbx_proj_search_batch_device(self._h, C.byref(params), grid, _tp(problems), n, max_n, max_nq, s))
+        else:
+            _check(self._lib.orbx_proj_search_grid_batch_device(self._h, C.byref(params), grid, _tp(problems), n, max_n,
+                                                                max_nq, _tp(grid_counts), s))
 
 
 @dataclass

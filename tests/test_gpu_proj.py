@@ -265,3 +265,79 @@ def test_stereo_mappoints_and_found_skip_bit_exact(gpu):
         p = O.stereo_mappoints(k, d, t, cam, SCALE, QF_BLOCKS)
         p["flags"][::3] |= 1
         assert np.array_equal(q[i, :len(k)], O.project(PROJ_MAPPOINTS, p, view, SCALE, lsf)), f"frame {i}"
+
+
+@pytest.mark.parametrize("mode", ["lastframe", "mappoints", "fuse", "best"])
+def test_search_with_grid_built_inside(gpu, mode):
+    """orbx_proj_search_grid_batch_device: each problem's grid built inside its search from the first grid_counts[p]
+    keypoints -- the written cell_start / cell_idx equal the oracle's AssignFeaturesToGrid and the search results equal
+    the oracle's, for problems whose target arrays hold more rows than are counted (rows past the count carry keypoints
+    that must not enter the grid) and for an empty problem."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    m = pkg.ORBmatcher(0.8, True)
+    cases = [make_case(80 + i, MODES[mode], n_target=600 + 90 * i, n_query=400 + 30 * i) for i in range(3)]
+    cases.append(make_case(90, MODES[mode], n_target=8, n_query=50))
+    B = len(cases)
+    cap = max(len(c["kps"]) for c in cases) + 64
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    junk = np.zeros(cap, pkg.KP_DTYPE)                  # rows past every count: keypoints inside the image
+    junk["x"] = rng.uniform(20, 600, cap).astype(np.float32)
+    junk["y"] = rng.uniform(20, 460, cap).astype(np.float32)
+    kps = torch.from_numpy(np.tile(junk.view(np.uint8).reshape(1, cap, 28), (B, 1, 1)))
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8)
+    ur = torch.full((B, cap), -1.0)
+    bl = torch.zeros((B, cap), dtype=torch.uint8)
+    ncount = []
+    for i, c in enumerate(cases):
+        n = len(c["kps"]) if i < 3 else 0               # the last problem counts none of its keypoints
+        ncount.append(n)
+        kps[i, :len(c["kps"])] = torch.from_numpy(c["kps"].view(np.uint8).reshape(len(c["kps"]), 28))
+        desc[i, :len(c["kps"])] = torch.from_numpy(c["desc"])
+        if c["uright"] is not None:
+            ur[i, :len(c["kps"])] = torch.from_numpy(c["uright"])
+        if c["blocked"] is not None:
+            bl[i, :len(c["kps"])] = torch.from_numpy(c["blocked"])
+    kps, desc, ur, bl = kps.to(dev), desc.to(dev), ur.to(dev), bl.to(dev)
+    has_ur, has_bl = cases[0]["uright"] is not None, cases[0]["blocked"] is not None
+    grid = cases[0]["grid"]
+    ncell = grid.cols * grid.rows
+    cs = torch.full((B, ncell + 1), -7, dtype=torch.int32, device=dev)
+    ci = torch.full((B, cap), -7, dtype=torch.int32, device=dev)
+    nqmax = max(len(c["queries"]) for c in cases)
+    qs = torch.zeros((B, nqmax, 40), dtype=torch.uint8)
+    qd = torch.zeros((B, nqmax, 32), dtype=torch.uint8)
+    for i, c in enumerate(cases):
+        nq = len(c["queries"])
+        qs[i, :nq] = torch.from_numpy(c["queries"].view(np.uint8).reshape(nq, 40))
+        qd[i, :nq] = torch.from_numpy(c["qdesc"])
+    qs, qd = qs.to(dev), qd.to(dev)
+    q_idx = torch.empty((B, nqmax), dtype=torch.int32, device=dev)
+    q_dist = torch.empty((B, nqmax), dtype=torch.int32, device=dev)
+    owner = torch.full((B, cap), -1, dtype=torch.int32, device=dev)     # the non-assigning modes leave it untouched
+    nm = torch.empty((B,), dtype=torch.int32, device=dev)
+    probs = (pkg.ProjProblem * B)()
+    for i, c in enumerate(cases):
+        probs[i] = pkg.ProjProblem(qs[i].data_ptr(), qd[i].data_ptr(), len(c["queries"]), kps[i].data_ptr(),
+                                   desc[i].data_ptr(), ur[i].data_ptr() if has_ur else None,
+                                   bl[i].data_ptr() if has_bl else None, cap,
+                                   cs[i].data_ptr(), ci[i].data_ptr(), q_idx[i].data_ptr(), q_dist[i].data_ptr(),
+                                   owner[i].data_ptr(), nm[i:i + 1].data_ptr())
+    dprobs = torch.frombuffer(bytearray(bytes(probs)), dtype=torch.uint8).to(dev)
+    counts = torch.tensor(ncount, dtype=torch.int32, device=dev)
+    m.proj_search_batch_device(cases[0]["params"], grid, dprobs, cap, nqmax, grid_counts=counts)
+    torch.cuda.synchronize()
+    for i, c in enumerate(cases):
+        n = ncount[i]
+        rcs, rci = O.grid_assign(c["kps"][:n], grid)
+        assert np.array_equal(cs[i].cpu().numpy(), rcs), i
+        assert np.array_equal(ci[i, :rcs[-1]].cpu().numpy(), rci), i
+        if i < 3:
+            nq = len(c["queries"])
+            got = (int(nm[i]), q_idx[i, :nq].cpu().numpy(), q_dist[i, :nq].cpu().numpy(), owner[i, :n].cpu().numpy())
+            _check(c, got)
+        else:                                            # no keypoint in the grid: nothing accepted
+            assert int(nm[i]) == 0 and bool((q_idx[i, :len(c["queries"])] == -1).all())
