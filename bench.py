@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--batch", type=int, default=256, help="stereo frames per GPU per step (512 images per extractor launch; "
                                                           "r3ag: 128 / 192 / 256 frames -> 65.7k / 66.4k / 66.9k frames/s)")
-    ap.add_argument("--desc-stream", type=int, default=1,
+    ap.add_argument("--desc-stream", type=int, default=int(os.environ.get("ORBX_BENCH_DESC_STREAM", "1")),
                     help="1: the extractor's descriptor stage on the stereo stream (orbx_extract_batch_device_split), "
                          "so step k+1's front end overlaps step k's descriptor stage; 2: on a stream of its own; 0: on "
                          "the launch stream")
@@ -102,9 +102,11 @@ def parse():
                          "descriptors) out of the keyframe path")
     ap.add_argument("--no-tracking", dest="tracking", action="store_false",
                     help="leave the tracking matches (SearchByProjection motion model + local map) out of the step")
-    ap.add_argument("--track-stream", choices=["stereo", "kf"], default="stereo",
-                    help="queue of the tracking matches: after the stereo step on the stereo queue, or at the head of "
-                         "the keyframe queue")
+    ap.add_argument("--track-stream", choices=["stereo", "kf", "own"],
+                    default=os.environ.get("ORBX_BENCH_TRACK_STREAM", "stereo"),
+                    help="queue of the tracking matches: after the stereo step on the stereo queue, at the head of "
+                         "the keyframe queue, or on a queue of its own after the stereo step (diagnostics; with "
+                         "ORBX_HW_QUEUES > 4 so it gets a hardware queue)")
     ap.add_argument("--no-fuse", dest="fuse", action="store_false",
                     help="leave SearchInNeighbors' Fuse (both ways with 10 neighbours) out of the keyframe path")
     ap.add_argument("--no-cd", dest="cd", action="store_false", help="skip the CovisibilityDiscovery-shaped block")
@@ -979,6 +981,7 @@ def main():
     # A stream of another priority gets a hardware queue of its own: two same-priority streams can land on one HW
     # queue (observed in a kernel trace: front-end and keyframe kernels then serialise, +0.5 ms per step).
     kf_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("ORBX_KF_PRIORITY", "-1")))
+    track_stream = mk() if args.track_stream == "own" else None
     kf_done = [None] * NS
     n_kf = max(1, B // KF_EVERY)
     voc = S.synthetic_vocabulary(2024, k=10, L=6)      # ORBvoc.txt's shape ("10 6 0 0"); the file is absent
@@ -1109,19 +1112,25 @@ def main():
         handoff.record(stereo_stream)
         stereo_done[pslot] = handoff
         last_handoff[0] = handoff
-        if tracker is not None and args.track_stream == "kf":
-            # the tracking matches on the keyframe queue, after the stereo step that gives their MapPoints (depth),
-            # so that the stereo queue (describe, stereo) is free for the next step
-            kf_stream.wait_event(handoff)
-            with torch.cuda.stream(kf_stream):
+        if tracker is not None and args.track_stream in ("kf", "own"):
+            # the tracking matches on the keyframe queue (or a queue of their own), after the stereo step that gives
+            # their MapPoints (depth), so that the stereo queue (describe, stereo) is free for the next step
+            tq = kf_stream if args.track_stream == "kf" else track_stream
+            tq.wait_event(handoff)
+            with torch.cuda.stream(tq):
                 if time_stereo:
                     e0t = torch.cuda.Event(enable_timing=True)
-                    e0t.record(kf_stream)
-                tracker.run(buf, kps[:B], desc[:B], cnt[:B], stream=kf_stream)
+                    e0t.record(tq)
+                tracker.run(buf, kps[:B], desc[:B], cnt[:B], stream=tq)
                 if time_stereo:
                     e1t = torch.cuda.Event(enable_timing=True)
-                    e1t.record(kf_stream)
+                    e1t.record(tq)
                     track_ms.append((e0t, e1t))
+                    tl["tracking_end"] = e1t
+            if args.track_stream == "own":
+                tdone = torch.cuda.Event()
+                tdone.record(track_stream)
+                kf_stream.wait_event(tdone)            # kf_done[buf] then also covers the tracking's reads of set buf
         h1 = time.perf_counter()
         if "keyframes" in skip:
             n_step[0] += 1
