@@ -23,6 +23,8 @@
 // covisibility accumulation) or order-free reductions (max).  Kernels per query batch:
 //   k_kfdb_share    one thread per (query word): walk the word's inverted list, atomic word count and
 //                   atomic-min first position per keyframe slot
+//   (small databases: k_kfdb_bits + k_kfdb_pairwise_gb intersect every (query, slot) pair against a bitmap of the
+//                   query's words instead of walking an inverted file; same word count and first position)
 //   k_kfdb_select   one workgroup per query: list membership from the scratch fields, max common words,
 //                   compaction of the keyframes to score
 //   k_kfdb_score    query BowVector staged in LDS; one wave per scored keyframe walks its words, finds
@@ -337,15 +339,97 @@ __global__ __launch_bounds__(512) void k_kfdb_pairwise(DbDev D, QueryIn Q, QScra
     }
 }
 
+// The same intersection against a bitmap of the query's words over the vocabulary, in memory (nbw words per query;
+// DBoW2's k = 10, L = 6 tree has 10^6 leaves, 122 KB per query, L2-resident: the workgroups of one query are dealt to
+// one XCD) -- no LDS, so it never holds a CU's LDS that FAST beside it could use.  Per slot wave: four slot words per
+// lane in flight, then their four bitmap words; the hit count is the ballots' popcounts.  The words are ascending in
+// both lists, so the first shared query word is the slot's first hit (the lowest lane of the first ballot that has
+// one), and its position in the query's list is its rank there, found with two ballots over the list.  Words outside
+// the vocabulary never match (as in k_kfdb_share's inverted file).  k_kfdb_bits sets the bits; k_kfdb_select clears
+// the words it set once the counts are read.
+__global__ __launch_bounds__(256) void k_kfdb_bits(DbDev D, QueryIn Q, uint32_t* __restrict__ qbits, int nbw) {
+    const int q = blockIdx.x, qs = Q.slot[q], nq = D.bn[qs];
+    uint32_t* bm = qbits + (size_t)q * nbw;
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+        const uint32_t w = D.bw[(size_t)qs * D.maxw + i];
+        if (w < (uint32_t)D.n_vocab) atomicOr(&bm[w >> 5], 1u << (w & 31));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_kfdb_pairwise_gb(DbDev D, QueryIn Q, QScratch X, int kind,
+                                                          const uint32_t* __restrict__ qbits, int nbw, int nqry, int gx) {
+    const int item = xcd_item(xcd_chunk(gx * nqry));
+    if (item >= gx * nqry) return;
+    const int q = item / gx, bx = item - q * gx;
+    const int qs = Q.slot[q];
+    const int nq = D.bn[qs];
+    const uint32_t nv = (uint32_t)D.n_vocab;
+    const uint32_t* bm = qbits + (size_t)q * nbw;
+    const uint32_t* ql = D.bw + (size_t)qs * D.maxw;
+    const int waves = blockDim.x / kWave, ln = lane_id();
+    const size_t row = (size_t)q * D.S;
+    for (int k = bx * waves + (int)(threadIdx.x / kWave); k < D.S; k += gx * waves) {
+        int c = 0;                                                    // wave-uniform
+        uint32_t first = 0x7f7f7f7fu;
+        if (kf_visible(D, Q, q, k) && !(kind == KIND_COVIS && excl_at(X, row + k)) && nq > 0) {
+            const uint32_t* cw = D.bw + (size_t)k * D.maxw;
+            const int nc = D.bn[k];
+            bool found = false;
+            uint32_t m = 0;                                           // the first (lowest) shared word
+            for (int i0 = 0; i0 < nc; i0 += 4 * kWave) {
+                uint32_t w[4], b[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int i = i0 + j * kWave + ln;
+                    w[j] = i < nc ? cw[i] : 0xffffffffu;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) b[j] = w[j] < nv ? bm[w[j] >> 5] : 0u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint64_t hb = __ballot((b[j] >> (w[j] & 31)) & 1u);
+                    c += __popcll(hb);
+                    if (!found && hb) {
+                        found = true;
+                        m = __builtin_amdgcn_readlane(w[j], __builtin_ctzll(hb));
+                    }
+                }
+            }
+            if (found) {
+                // rank of m in the query's list (nq <= 4096 = 64 segments of <= 64): its segment, then within it
+                const int step = (nq + kWave - 1) / kWave;
+                const int p0 = ln * step;
+                const uint64_t sb = __ballot(p0 < nq && ql[min(p0, nq - 1)] <= m);
+                const int base = (__popcll(sb) - 1) * step;
+                const int p1 = base + ln;
+                const uint64_t rb = __ballot(ln < step && p1 < nq && ql[min(p1, nq - 1)] < m);
+                first = (uint32_t)(base + __popcll(rb));
+            }
+        }
+        if (ln == 0) {
+            X.cnt[row + k] = c;
+            X.first[row + k] = (int)first;
+        }
+    }
+}
+
 // A keyframe enters lKFsSharingWords when it shares a word, its query field is not already this id
 // (:93 / :221 / :325) and, for loop queries, it is not connected to the query (:96).
 __device__ __forceinline__ bool kf_pushed(int kind, int c, bool stale, bool ex) {
     return c > 0 && !stale && !(kind == KIND_LOOP && ex);
 }
 
-__global__ __launch_bounds__(1024) void k_kfdb_select(DbDev D, QueryIn Q, QScratch X, StateDev St, int kind) {
+__global__ __launch_bounds__(1024) void k_kfdb_select(DbDev D, QueryIn Q, QScratch X, StateDev St, int kind,
+                                                      uint32_t* __restrict__ qbits, int nbw) {
     __shared__ int s_max, s_np, s_nc;
     const int q = blockIdx.x;
+    if (qbits) {                                                      // k_kfdb_pairwise_gb is done with this query's bits
+        const int qs = Q.slot[q], nq = D.bn[qs];
+        for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+            const uint32_t w = D.bw[(size_t)qs * D.maxw + i];
+            if (w < (uint32_t)D.n_vocab) qbits[(size_t)q * nbw + (w >> 5)] = 0u;
+        }
+    }
     const unsigned long long id = Q.id[q];
     const size_t row = (size_t)q * D.S;
     if (threadIdx.x == 0) { s_max = 0; s_np = 0; s_nc = 0; }
@@ -634,6 +718,8 @@ struct orbx_kfdb {
     float* d_s[3] = {nullptr, nullptr, nullptr};
     void* scratch = nullptr;       // per-query rows + host-form staging
     size_t scratch_bytes = 0;
+    uint32_t* d_qbits = nullptr;   // per-query vocabulary bitmaps of the pairwise intersection: all zero between
+    size_t qbits_bytes = 0;        // operations (each batch clears the words it set, k_kfdb_select)
     // Thread and stream contract (KeyFrameDatabase.cc:42,50,84,210,316 lock mMutex in add / erase / every Detect*):
     // every entry point holds 'mtx' while it runs, and every one that enqueues device work on the database's state
     // (BowVectors, membership, inverted file, scratch fields, 'scratch') first makes its stream wait for 'last_op' and
@@ -771,6 +857,12 @@ static int pairwise_max_members() {
     return v;
 }
 
+// the pairwise intersection over per-query vocabulary bitmaps in memory (ORBX_KFDB_BITMAP=0: the LDS hash table)
+static bool pairwise_bitmap() {
+    static const bool v = [] { const char* e = std::getenv("ORBX_KFDB_BITMAP"); return !e || std::atoi(e) != 0; }();
+    return v;
+}
+
 // The query batch on stream s; d_* are device pointers.  Scratch rows at 'base' (nq x S).
 int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned char* base, int32_t* d_out, int out_stride,
                  int32_t* d_out_n, int32_t* d_status, hipStream_t s) {
@@ -789,7 +881,27 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
         hipLaunchKernelGGL(k_kfdb_mark_excl, dim3(nq), dim3(256), 0, s, Q, X, db->S);
     }
     const size_t lds = (size_t)db->maxw * (sizeof(double) + sizeof(uint32_t));
-    if (pairwise) {
+    const int nbw = (db->n_vocab + 31) / 32;
+    uint32_t* qbits = nullptr;
+    if (pairwise && pairwise_bitmap()) {
+        const size_t need = (size_t)4 * nbw * nq;
+        if (need > db->qbits_bytes) {
+            if (db->d_qbits) {
+                ORBX_HIP(hipDeviceSynchronize());
+                ORBX_HIP(hipFree(db->d_qbits));
+                db->d_qbits = nullptr;
+                db->qbits_bytes = 0;
+            }
+            ORBX_HIP(hipMalloc((void**)&db->d_qbits, need));
+            ORBX_HIP(hipMemsetAsync(db->d_qbits, 0, need, s));
+            db->qbits_bytes = need;
+        }
+        qbits = db->d_qbits;
+        hipLaunchKernelGGL(k_kfdb_bits, dim3(nq), dim3(256), 0, s, D, Q, qbits, nbw);
+        const int gx = std::max(1, std::min((db->S + 15) / 16, 128));   // ~4 slots per wave
+        hipLaunchKernelGGL(k_kfdb_pairwise_gb, dim3(kXcds * xcd_chunk(gx * nq)), dim3(256), 0, s, D, Q, X, kind, qbits,
+                           nbw, nq, gx);
+    } else if (pairwise) {
         const int gx = std::min((db->S + 7) / 8, 64);
         int log_t = 1;
         while ((1 << log_t) < 2 * db->maxw) ++log_t;                // load factor <= 1/2
@@ -803,7 +915,7 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
         ORBX_HIP(hipMemsetAsync(X.first, 0x7f, 4 * r, s));
         hipLaunchKernelGGL(k_kfdb_share, dim3((db->maxw + 255) / 256, nq), dim3(256), 0, s, D, Q, X, kind);
     }
-    hipLaunchKernelGGL(k_kfdb_select, dim3(nq), dim3(1024), 0, s, D, Q, X, St, kind);
+    hipLaunchKernelGGL(k_kfdb_select, dim3(nq), dim3(1024), 0, s, D, Q, X, St, kind, qbits, nbw);
     hipLaunchKernelGGL(k_kfdb_score, dim3(32, nq), dim3(256), lds, s, D, Q, X);   // the minCommonWords candidates
     hipLaunchKernelGGL(k_kfdb_accum, dim3(nq), dim3(256), 0, s, D, Q, X, St, kind, d_out, out_stride, d_out_n, d_status);
     hipLaunchKernelGGL(k_kfdb_state, dim3((db->S + 255) / 256), dim3(256), 0, s, D, Q, X, St, kind, nq, d_status);
@@ -873,7 +985,7 @@ int orbx_kfdb_destroy(orbx_kfdb* db) {
     (void)hipSetDevice(db->device);
     (void)hipDeviceSynchronize();              // operations on callers' streams read the database's buffers
     void* bufs[] = {db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_cur, db->d_if_slot,
-                    db->d_scan, db->d_members, db->scratch, db->score_stage};
+                    db->d_scan, db->d_members, db->scratch, db->score_stage, db->d_qbits};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (int k = 0; k < 3; ++k) {
