@@ -467,7 +467,9 @@ __global__ __launch_bounds__(256) void k_kfdb_score(DbDev D, QueryIn Q, QScratch
     uint32_t* qw = reinterpret_cast<uint32_t*>(qv + D.maxw);
     const int q = blockIdx.y;
     const int nc = X.meta[q * 4 + 2];
-    if (nc == 0) return;
+    const int waves = blockDim.x / kWave;
+    // a few candidates per query pass minCommonWords: the workgroups past them leave before staging the query
+    if ((int)blockIdx.x * waves >= nc) return;
     const int qs = Q.slot[q];
     const int nq = D.bn[qs];
     for (int i = threadIdx.x; i < nq; i += blockDim.x) {
@@ -475,7 +477,6 @@ __global__ __launch_bounds__(256) void k_kfdb_score(DbDev D, QueryIn Q, QScratch
         qv[i] = D.bv[(size_t)qs * D.maxw + i];
     }
     __syncthreads();
-    const int waves = blockDim.x / kWave;
     const size_t row = (size_t)q * D.S;
     for (int c = blockIdx.x * waves + (int)(threadIdx.x / kWave); c < nc; c += gridDim.x * waves) {
         const int k = X.cand[row + c];
