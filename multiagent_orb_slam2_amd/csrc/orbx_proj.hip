@@ -1125,8 +1125,13 @@ static int proj_search_batch(orbx_matcher* m, const orbx_proj_params* params, or
         ORBX_REQUIRE(!d_grid_counts || (staged && ncell < 0xffff && N < 0xffff), ORBX_ERR_UNSUPPORTED,
                      "grid built in the search: %d keypoints, %d cells do not fit the staged plan", max_n, (int)ncell);
         const size_t used = core + (staged ? stage + gscr : 0);
+        static const int list_max = [] {                        // ORBX_PROJ_LIST_MAX (diagnostics): list slots per query
+            const char* v = std::getenv("ORBX_PROJ_LIST_MAX");
+            const int t = v ? std::atoi(v) : kProjListMax;
+            return (t >= 0 && t <= kProjListMax) ? t : kProjListMax;
+        }();
         int kcap = 0;
-        if (assigning) kcap = (int)std::min<size_t>(kProjListMax, (cap - used) / (4 * NQ));
+        if (assigning) kcap = (int)std::min<size_t>(list_max, (cap - used) / (4 * NQ));
         const size_t lds = std::max<size_t>(used + (size_t)kcap * 4 * NQ, 16);
         auto kern = assigning ? (staged ? k_proj_search<true, true> : k_proj_search<false, true>)
                               : (staged ? k_proj_search<true, false> : k_proj_search<false, false>);
