@@ -2426,12 +2426,17 @@ int Extractor::configure(int r, int c, int batch) {
         // rounded down to 1,280 B, the allocation granule that fits the measured packing: levels >= 1 with 53,344 B per
         // workgroup run three per CU, with 53,792 B two (0.156 -> 0.212 ms alone, r4y), level 0 with 81,904 B two (r4x;
         // a 512 B granule would give three at 53,792 B, a 2 KiB one two at 53,344 B). No LDS keys at levels >= 1: 0.186 ms.
+        // r5bg: level 0 at 3,072 LDS keys (62.7 KB per workgroup) instead of the two-per-CU budget's 5,808 (81.9 KB):
+        // the rest in the HBM scratch, and the LDS the two workgroups leave on their CU goes to FAST beside them --
+        // step +0.8 % (75.2k -> 75.8k frames/s; 0 / 1k / 2k / 4k keys 75.7k / 75.8k / 75.4k / 75.8k, two rounds each)
         const int per_cu[2] = {2, 3};
+        constexpr int kQtKeys0Max = 3072;
         int want[2];
         for (int k = 0; k < 2; ++k) {
             const size_t budget = (size_t)160 * 1024 / per_cu[k] / 1280 * 1280;
             want[k] = budget > lds ? (int)((budget - lds) / 7) : 0;
         }
+        want[0] = std::min(want[0], kQtKeys0Max);
         if (const char* v = std::getenv("ORBX_QT_KEYS0")) want[0] = std::atoi(v);   // diagnostics
         if (const char* v = std::getenv("ORBX_QT_KEYS1")) want[1] = std::atoi(v);
         size_t maxl = lds;
