@@ -1121,7 +1121,9 @@ static int proj_search_batch(orbx_matcher* m, const orbx_proj_params* params, or
         // a grid built in the search needs 4 B per target keypoint of scratch after the entries (the assigning modes'
         // claim / own arrays serve) and the staged form, u16 cells and indices
         const size_t gscr = (d_grid_counts && !assigning) ? ((4 * N + 15) & ~(size_t)15) : 0;
-        const bool staged = stage + core + gscr <= cap;
+        // ORBX_PROJ_NA_STAGE=0 (diagnostics): the non-assigning modes walk cells and entries in memory, no staged LDS
+        static const bool na_stage = [] { const char* v = std::getenv("ORBX_PROJ_NA_STAGE"); return !v || std::atoi(v) != 0; }();
+        const bool staged = stage + core + gscr <= cap && (assigning || d_grid_counts || na_stage);
         ORBX_REQUIRE(!d_grid_counts || (staged && ncell < 0xffff && N < 0xffff), ORBX_ERR_UNSUPPORTED,
                      "grid built in the search: %d keypoints, %d cells do not fit the staged plan", max_n, (int)ncell);
         const size_t used = core + (staged ? stage + gscr : 0);
