@@ -2074,8 +2074,9 @@ struct Extractor {
     // describe).
     static constexpr int kCallEv = 32;
     struct CallEvents {
-        hipEvent_t fork, pyr, join, front, desc;          // fork from the caller, pyramid built, side join,
-        bool used;                                         // launch-stream quadtree, describe done
+        hipEvent_t fork, pyr, join, front, desc, qt;      // fork from the caller, pyramid built, side join,
+        bool used;                                         // launch-stream FAST / quadtree, describe done, levels
+                                                           // 1..n-1 quadtree on the output stream (qt_out)
     };
     CallEvents cev[kCallEv] = {};
     unsigned long long cev_next = 0;
@@ -2132,6 +2133,9 @@ struct Extractor {
     int scan_cap = 0;         // scan arrays: >= nodes, cells of a level, roots
     size_t qt_lds = 0;        // k_quadtree dynamic LDS bytes of the node arrays (the key region follows at this offset)
     int qt_keys[2] = {0, 0};  // LDS-resident key capacity of the level-0 launch / the levels 1..n-1 launch
+    int qt_prev = -1;         // call event set whose ce.qt the next FAST of levels >= 1 waits for (qt_out)
+    int qt_out = 1;           // levels 1..n-1 quadtree on the output stream when it differs (ORBX_QT_OUT=0: the launch
+                              // stream, the round-4 schedule)
     int out_capacity = 0;     // max keypoints per image
 
     // device buffers
@@ -2665,8 +2669,13 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     if (ce.used && !e->capturing) ORBX_HIP(hipEventSynchronize(ce.desc));
     hipStream_t side = pipelined ? e->side : s;
     if (!pipelined) so = s;
+    // DistributeOctTree of levels 1..n-1 on the output stream ahead of the describe (qt_out), so that the launch stream
+    // goes on to the next call's resize chain right after FAST; the next call's FAST of levels >= 1 then waits for it
+    // (it overwrites the candidates this quadtree reads).  Step +1.0 % (r5bj: 75.7k -> 76.4k) / +0.4 % (r5bk: 75.7k -> 76.1k
+    // against both other schedules), EuRoC +0.6 %.
+    const bool qto = e->qt_out && pipelined && so != s && !e->capturing;
     auto mark = [&](int k) {
-        if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : (k == 4 || k == 5) ? so : s);
+        if (es) (void)hipEventRecord(es->ev[k], (k >= 6 && k <= 9) ? side : (k == 4 || k == 5 || (qto && k == 3)) ? so : s);
     };
     // the previous call's describe (possibly on another stream) reads the kept keypoints and the blurred pyramid
     // the last describe that read this call's set of kept keypoints / blurred pyramid (the previous call's with one set)
@@ -2681,6 +2690,10 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     auto fast = [&](hipStream_t q, int k) {
         const Extractor::WaveLaunch& wl = e->wave_launch[k];
         if (wl.n <= 0) return;
+        if (k != 0 && e->qt_prev >= 0) {                            // the previous call's quadtree on its output stream
+            (void)hipStreamWaitEvent(q, e->cev[e->qt_prev].qt, 0);
+            if (!qto) e->qt_prev = -1;
+        }
         constexpr int wpg = Extractor::kWaveWpg;
         const int nwg = (wl.n * batch + wpg - 1) / wpg;
         auto kw = wl.ps == 19 ? k_fast_wave<19, 4, wpg> : k_fast_wave<40, 0, wpg>;
@@ -2770,9 +2783,11 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     mark(10);                                                       // launch stream: FAST, DistributeOctTree 1..nl-1
     fast(s, 1);
     mark(2);
-    if (int st = after_prev_describe(s)) return st;
-    quadtree(s, 1, nl - 1);
-    mark(3);
+    if (!qto) {
+        if (int st = after_prev_describe(s)) return st;
+        quadtree(s, 1, nl - 1);
+        mark(3);
+    }
     }
     // the descriptor stage on the output stream, once both streams are done; the next call's resize chain (launch
     // stream) runs beside it
@@ -2781,6 +2796,13 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         ORBX_HIP(hipStreamWaitEvent(so, ce.front, 0));
     }
     if (side != so) ORBX_HIP(hipStreamWaitEvent(so, ce.join, 0));
+    if (qto) {
+        if (int st = after_prev_describe(so)) return st;
+        quadtree(so, 1, nl - 1);
+        mark(3);
+        ORBX_HIP(hipEventRecord(ce.qt, so));
+        e->qt_prev = ci;
+    }
     mark(4);
     {
         SlotTable tab{};
@@ -2892,7 +2914,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     const int cu_ex = std::getenv("ORBX_CU_EXCLUDE") ? std::atoi(std::getenv("ORBX_CU_EXCLUDE")) : 0;
     if (he == hipSuccess) he = create_stream_masked(&e->side, side_prio, cu_ex);
     for (auto& c : e->cev)
-        for (hipEvent_t* ev : {&c.fork, &c.pyr, &c.join, &c.front, &c.desc})
+        for (hipEvent_t* ev : {&c.fork, &c.pyr, &c.join, &c.front, &c.desc, &c.qt})
             if (he == hipSuccess) he = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (he != hipSuccess) {
         set_error("stream create: %s", hipGetErrorString(he));
@@ -2905,6 +2927,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* hs = std::getenv("ORBX_HOST_SERIAL")) e->host_serial = std::atoi(hs) != 0;
     if (const char* hm = std::getenv("ORBX_HOST_MERGED")) e->host_merged = std::atoi(hm) != 0;
     if (const char* sw = std::getenv("ORBX_DEBUG_SKIP_DESC_WAIT")) e->dbg_skip_desc_wait = std::atoi(sw) != 0;
+    if (const char* qo = std::getenv("ORBX_QT_OUT")) e->qt_out = std::atoi(qo) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
         return st;
@@ -2926,7 +2949,7 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->side) (void)hipStreamDestroy(e->side);
     for (auto& c : e->cev)
-        for (hipEvent_t ev : {c.fork, c.pyr, c.join, c.front, c.desc})
+        for (hipEvent_t ev : {c.fork, c.pyr, c.join, c.front, c.desc, c.qt})
             if (ev) (void)hipEventDestroy(ev);
     delete e;
     return ORBX_OK;

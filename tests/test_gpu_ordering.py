@@ -41,14 +41,17 @@ def _mismatches(outs, ref):
     return bad
 
 
+@pytest.mark.parametrize("qt_out", ["1", "0"])
 @pytest.mark.parametrize("ring", [1, 2])
-def test_stalled_describe_orders_next_call(gpu, ring):
+def test_stalled_describe_orders_next_call(gpu, ring, qt_out, monkeypatch):
     """A 15 ms spin on the output stream right before each call: call k's describe starts long after call k+1's
     quadtree, blur and (ring 1) resize were enqueued.  Every result must equal the host API and the canary must stay
-    clear -- i.e. every cross-call buffer reuse waits for the describe that reads it."""
+    clear -- i.e. every cross-call buffer reuse waits for the describe that reads it.  qt_out "1" (the default): the
+    quadtree of levels >= 1 on the output stream, and call k+1's FAST waits for call k's; "0": on the launch stream."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
+    monkeypatch.setenv("ORBX_QT_OUT", qt_out)
     batches = _batches()
     ref = _reference(batches)
     ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
@@ -75,6 +78,10 @@ def test_canary_fires_when_an_edge_is_missing(gpu, monkeypatch):
 
     import multiagent_orb_slam2_amd as pkg
     monkeypatch.setenv("ORBX_DEBUG_SKIP_DESC_WAIT", "1")
+    # the schedule with the quadtree of levels >= 1 on the launch stream, where the missing edge races (with it on the
+    # output stream, the default, that quadtree is stream-ordered after the previous describe and the next call's FAST
+    # waits for it, so the stall delays the launch stream too and the race does not arise)
+    monkeypatch.setenv("ORBX_QT_OUT", "0")
     batches = _batches(n=3)
     ref = _reference(batches)
     ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
