@@ -978,9 +978,11 @@ def main():
     # keyframe queue: BoW, packets, exchange, KeyFrameDatabase, SearchByBoW -- the native orbx_fusion object.  As in
     # the reference, where LoopClosing and MapFusion run in their own threads beside Tracking, step k's keyframe work
     # overlaps step k+1's extraction.
-    # A stream of another priority gets a hardware queue of its own: two same-priority streams can land on one HW
-    # queue (observed in a kernel trace: front-end and keyframe kernels then serialise, +0.5 ms per step).
-    kf_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("ORBX_KF_PRIORITY", "-1")))
+    # Priority: -1 (high) until r5bt, where with the DistributeOctTree of levels >= 1 on the stereo queue (r5bk) the
+    # keyframe stream at normal priority measured +0.8 % (76.5k -> 77.1k frames/s, three rounds; +0.9 % at 8 emulated
+    # agents).  (A stream of another priority gets a hardware queue of its own; two same-priority streams can share one,
+    # which in round 3 serialised front-end and keyframe kernels, +0.5 ms per step.)  ORBX_KF_PRIORITY overrides.
+    kf_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("ORBX_KF_PRIORITY", "0")))
     track_stream = mk() if args.track_stream == "own" else None
     kf_done = [None] * NS
     n_kf = max(1, B // KF_EVERY)
