@@ -329,7 +329,7 @@ __global__ __launch_bounds__(kStereoRowsThreads) void k_stereo_rows(StereoArgs A
 // candidate set and the (distance, index) minimum are exactly k_stereo's; a candidate outside a left keypoint's own
 // bucket window never passes its row test.  Replaces ~8 dependent HBM round trips per left keypoint by one staged
 // load per block.
-constexpr int kStereoRows = 8, kStereoRC = 512, kStereoLC = 128;
+constexpr int kStereoRows = 8, kStereoRC = 256, kStereoLC = 64;
 __global__ __launch_bounds__(256) void k_stereo_blk(StereoArgs A, int nblk) {
     __shared__ uint4 rd[2 * kStereoRC];
     __shared__ float rx[kStereoRC];
