@@ -3,7 +3,8 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 PKG := multiagent_orb_slam2_amd
 SRC := $(PKG)/csrc
-HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result
+HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result \
+            -mllvm -amdgpu-mfma-vgpr-form
 HDRS := include/orbx.h $(SRC)/orbx_common.h $(SRC)/orbx_pattern.h $(SRC)/orbx_sincos.h
 OBJS := $(SRC)/orbx_extract.o $(SRC)/orbx_match.o $(SRC)/orbx_vocab.o $(SRC)/orbx_proj.o $(SRC)/orbx_kfdb.o $(SRC)/orbx_fusion.o
 

@@ -133,11 +133,6 @@ __constant__ __attribute__((aligned(16))) PatternByLane<16> c_pattern_l16 = make
 // umax for HALF_PATCH_SIZE = 15 (ORBextractor ctor :454-469); the host recomputes it and checks equality
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
-// Diagnostics builds only: ORBX_VCLOB_<KERNEL>=r makes that kernel allocate r + 1 VGPRs (an empty asm clobbering v<r>),
-// capping its waves per SIMD at 512 / (r + 1), to measure how its occupancy trades against the kernels beside it.
-#define ORBX_VSTR2(x) #x
-#define ORBX_VSTR(x) ORBX_VSTR2(x)
-#define ORBX_VCLOB_AT(n) asm volatile("" ::: "v" ORBX_VSTR(n))
 
 // =============================================================================================
 // kernels
@@ -300,9 +295,6 @@ __device__ __forceinline__ void resize4_item(uint8_t* __restrict__ pyr, size_t p
 __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
                                                  size_t src_step, size_t src_istride, int sw, int dst_off, int dw, int dh,
                                                  ResizeVec t, int nstrips, int nbands, int batch) {
-#ifdef ORBX_VCLOB_RESIZE
-    ORBX_VCLOB_AT(ORBX_VCLOB_RESIZE);
-#endif
     const int nwaves = nstrips * nbands * batch;
     const int nwg = (nwaves + 3) / 4;
     const int wg = xcd_item(xcd_chunk(nwg));
@@ -312,112 +304,6 @@ __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size
     const int rem = wv - img * nstrips * nbands;
     const int band = rem / nstrips, strip = rem - band * nstrips;
     resize4_item(pyr, pyr_stride, src, src_step, src_istride, sw, dst_off, dw, dh, t, strip, band, img);
-}
-
-// Two pyramid levels per launch (lb = la + 1 and lc = la + 2, ComputePyramid :1120 chained twice): one workgroup per
-// (image, band of kResizeBand lc rows), one thread per 4-column group of lb (blockDim = groups rounded to 64).  Phase 1 computes the lb rows the band's lc rows read, [c0, c1),
-// from level la in HBM into LDS and writes the lb rows the band owns, [own0, own1) (the bands partition lb's rows, so
-// every lb row is written once; a row two bands read is computed by both); phase 2 computes the band's lc rows from
-// LDS.  Same arithmetic, tables and rounding as k_resize4: bit-identical levels, half the dependent launches, and lb
-// is never read back from HBM.
-struct ResizePair {
-    ResizeVec tb, tc;        // tables of lb (from la) and lc (from lb)
-    const int4* band;        // per lc band: c0, c1, own0, own1 (lb rows)
-    int nbands, stride;      // lc bands; LDS bytes per lb row (>= wb + 8, a multiple of 4)
-    int wa, wb, hb, wc, hc;  // source width, lb and lc sizes
-    int off_b, off_c;        // lb / lc offsets inside one image's pyramid
-};
-
-#ifndef ORBX_PAIR_K
-#define ORBX_PAIR_K 6       // phase-1 lb rows per round (all their source windows in flight together)
-#endif
-constexpr int kPairK = ORBX_PAIR_K;
-
-__device__ __forceinline__ void resize_lds_window(const uint8_t* __restrict__ row, int xb, uint32_t& lo, uint32_t& hi) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(row) + (xb >> 2);
-    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
-    lo = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)(xb & 3));
-    hi = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)(xb & 3));
-}
-
-__device__ __forceinline__ uint32_t resize_group(uint32_t lo0, uint32_t hi0, uint32_t lo1, uint32_t hi1, const uint4& sel,
-                                                 const uint4& coef, int b0, int b1) {
-    const uint32_t sl[4] = {sel.x, sel.y, sel.z, sel.w}, cf[4] = {coef.x, coef.y, coef.z, coef.w};
-    uint32_t acc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const u16x2 c = __builtin_bit_cast(u16x2, cf[k]);
-        const uint32_t hv0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi0, lo0, sl[k])), c, 0u, false);
-        const uint32_t hv1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi1, lo1, sl[k])), c, 0u, false);
-        acc[k] = resize_acc(hv0, hv1, b0, b1);
-    }
-    return resize_pack(acc);
-}
-
-__device__ __forceinline__ void resize_store4(uint8_t* __restrict__ o, uint32_t packed, int x, int w) {
-    if (x + 4 <= w) {
-        __builtin_memcpy(o, &packed, 4);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (x + k < w) o[k] = (uint8_t)(packed >> (8 * k));
-    }
-}
-
-__global__ __launch_bounds__(512) void k_resize_pair(uint8_t* __restrict__ pyr, size_t pyr_stride, const uint8_t* __restrict__ src,
-                                                     size_t src_step, size_t src_istride, ResizePair P, int batch) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
-    const int nwg = P.nbands * batch;
-    const int wg = xcd_item(xcd_chunk(nwg));
-    if (wg >= nwg) return;                                           // workgroup-uniform
-    const int img = __builtin_amdgcn_readfirstlane(wg / P.nbands), band = __builtin_amdgcn_readfirstlane(wg - img * P.nbands);
-    const int4 bd = P.band[band];
-    const int g = threadIdx.x;                                       // one 4-column group per thread, as k_resize4's lanes
-    const uint8_t* S = src + img * src_istride;
-    uint8_t* Db = pyr + img * pyr_stride + P.off_b;
-    uint8_t* Dc = pyr + img * pyr_stride + P.off_c;
-    uint8_t* L = reinterpret_cast<uint8_t*>(rsm);
-    // phase 1: lb rows [c0, c1) of group g, kPairK rows per round with all their source windows loaded first; the row
-    // tables are workgroup-uniform (scalar loads)
-    if (g < P.tb.groups) {
-        constexpr int K = kPairK;
-        const int xb = P.tb.xb[g];
-        const uint4 sel = P.tb.sel[g], coef = P.tb.coef[g];
-        const int x = 4 * g;
-        for (int r0 = bd.x; r0 < bd.y; r0 += K) {
-            int4 yr[K];
-            uint32_t lo[2 * K], hi[2 * K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                yr[k] = P.tb.yrow[min(r0 + k, bd.y - 1)];
-                resize_window8(S + (size_t)yr[k].x * src_step, xb, P.wa, lo[2 * k], hi[2 * k]);
-                resize_window8(S + (size_t)yr[k].y * src_step, xb, P.wa, lo[2 * k + 1], hi[2 * k + 1]);
-            }
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int row = r0 + k;
-                if (row >= bd.y) break;                              // uniform
-                const uint32_t packed = resize_group(lo[2 * k], hi[2 * k], lo[2 * k + 1], hi[2 * k + 1], sel, coef, yr[k].z,
-                                                     yr[k].w);
-                *reinterpret_cast<uint32_t*>(L + (size_t)(row - bd.x) * P.stride + x) = packed;   // row slack >= 8 bytes
-                if (row >= bd.z && row < bd.w) resize_store4(Db + (size_t)row * P.wb + x, packed, x, P.wb);
-            }
-        }
-    }
-    __syncthreads();
-    // phase 2: the band's lc rows of group g from the lb rows in LDS
-    if (g < P.tc.groups) {
-        const int xb = P.tc.xb[g];
-        const uint4 sel = P.tc.sel[g], coef = P.tc.coef[g];
-        const int x = 4 * g, y0 = band * kResizeBand, y1 = min(y0 + kResizeBand, P.hc);
-        for (int y = y0; y < y1; ++y) {
-            const int4 yr = P.tc.yrow[y];
-            uint32_t lo0, hi0, lo1, hi1;
-            resize_lds_window(L + (size_t)(yr.x - bd.x) * P.stride, xb, lo0, hi0);
-            resize_lds_window(L + (size_t)(yr.y - bd.x) * P.stride, xb, lo1, hi1);
-            resize_store4(Dc + (size_t)y * P.wc + x, resize_group(lo0, hi0, lo1, hi1, sel, coef, yr.z, yr.w), x, P.wc);
-        }
-    }
 }
 
 // FAST-9/16 corner score in closed form.  For pixel value v and circle values p_k (Bresenham r=3,
@@ -549,30 +435,6 @@ __device__ __forceinline__ int nms_pair(const lds_i16* __restrict__ sc, int SW, 
 struct WaveLds {               // per-wave slice of k_fast_wave's dynamic LDS (byte offsets inside the slice)
     int o_sc, o_list, bytes;   // E pair image at 0 (the NMS key lists reuse it), score map, survivor list; slice size
 };
-// The same rule on a u8 score map holding s + 1 (0 = no score / -1, never a corner and never blocking): per row the 4
-// bytes of columns 2j+1 .. 2j+4 (two aligned dwords and one v_alignbyte), spread into u16 pairs by v_perm and maxed
-// with v_pk_max_u16; the map is half the LDS of the i16 form.
-typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ u16x2v as_u2(uint32_t v) { return __builtin_bit_cast(u16x2v, v); }
-__device__ __forceinline__ uint32_t sc_row4(const lds_u8* __restrict__ scb, int b) {    // bytes b .. b+3
-    const lds_u32* w = (const lds_u32*)(scb + (b & ~3));
-    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(b & 3));
-}
-__device__ __forceinline__ int nms_pair_u8(const lds_u8* __restrict__ scb, int SWB, int rr, int j, int T1, int T2,
-                                           bool second) {
-    const int b = rr * SWB + 2 * j + 1;
-    const uint32_t x0 = sc_row4(scb, b), x1 = sc_row4(scb, b + SWB), x2 = sc_row4(scb, b + 2 * SWB);
-    auto p01 = [](uint32_t x) { return as_u2(__builtin_amdgcn_perm(x, x, 0x0c010c00u)); };
-    auto p12 = [](uint32_t x) { return as_u2(__builtin_amdgcn_perm(x, x, 0x0c020c01u)); };
-    auto p23 = [](uint32_t x) { return as_u2(__builtin_amdgcn_perm(x, x, 0x0c030c02u)); };
-    u16x2v m = __builtin_elementwise_max(__builtin_elementwise_max(p01(x0), p12(x0)), p23(x0));
-    m = __builtin_elementwise_max(m, __builtin_elementwise_max(__builtin_elementwise_max(p01(x2), p12(x2)), p23(x2)));
-    m = __builtin_elementwise_max(m, __builtin_elementwise_max(p01(x1), p23(x1)));    // the middle row without the pair
-    const u16x2v sv = p12(x1);
-    const int g0 = sv.x > m.x, g1 = second && (sv.y > m.y);
-    const int t1 = T1 + 1, t2 = T2 + 1;
-    return (g0 & (sv.x >= t1)) | ((g1 & (sv.y >= t1)) << 1) | ((g0 & (sv.x >= t2)) << 2) | ((g1 & (sv.y >= t2)) << 3);
-}
 
 // rows: max ROI rows; scrow: score-map row bytes; np: max pixel pairs; iw: pair-image dwords (fastw_image_words)
 __host__ __device__ __forceinline__ WaveLds wave_lds(int rows, int scrow, int np, int iw) {
@@ -707,23 +569,10 @@ __device__ __forceinline__ int rank_below(uint64_t b, int acc = 0) {
                             // CU at levels >= 1 / level 0 instead of 4 / 5: serial FAST 1.153 -> 1.060 ms, step +0.9 %
 #endif
 __host__ __device__ constexpr int fastw_sw(int ps) { return ps == 19 ? ORBX_FAST_SW19 : 76; }
-// score map as u8 (s + 1) instead of i16: ORBX_FAST_U8SC=1 (the NMS reads bytes 2j+1 .. 2j+8 of a row: row >= Wd + 8)
-#ifndef ORBX_FAST_U8SC
-#define ORBX_FAST_U8SC 0
-#endif
-#ifndef ORBX_FAST_STOP
-#define ORBX_FAST_STOP 0   // diagnostics (wrong keypoints): 1 = ROI staging only, 2 = + pre-test, 3 = + scores
-#endif
-constexpr bool kScU8 = ORBX_FAST_U8SC != 0;
-__host__ __device__ constexpr int fastw_scrow(int ps) { return kScU8 ? (ps == 19 ? 40 : 80) : 2 * fastw_sw(ps); }
+__host__ __device__ constexpr int fastw_scrow(int ps) { return 2 * fastw_sw(ps); }
 
 __device__ __forceinline__ void sc_store(lds_u8* __restrict__ scb, int SWB, int rr, int j, s16x2 v, bool second) {
-    if constexpr (kScU8) {
-        const uint32_t u = ((uint32_t)(v.x + 1) & 0xffu) | (second ? (((uint32_t)(v.y + 1) & 0xffu) << 8) : 0u);
-        *(lds_u16*)(scb + (rr + 1) * SWB + 2 + 2 * j) = (uint16_t)u;
-    } else {
-        *(lds_s16x2*)(scb + (rr + 1) * SWB + 4 + 4 * j) = second ? v : (s16x2){v.x, (short)-1};
-    }
+    *(lds_s16x2*)(scb + (rr + 1) * SWB + 4 + 4 * j) = second ? v : (s16x2){v.x, (short)-1};
 }
 
 // The part of a cell after its ROI is in LDS: pre-test, scores, NMS at both thresholds, the cell's candidate slots.
@@ -779,11 +628,6 @@ __device__ __forceinline__ void fastw_body(lds_u32* __restrict__ E, lds_u8* __re
         }
     }
     wave_fence();
-#if ORBX_FAST_STOP == 2
-    if (ns < 0) list[0] = 0;                                          // (keeps the pre-test live)
-    if (ln == 0) *cnt_out = 0;                                        // diagnostics: staging + pre-test
-    return;
-#endif
     // 3. closed-form scores of the survivors, two per lane per round (both tap sets read before either is scored); a
     //    round with at most 64 survivors left (two cells in three at iniThFAST) scores one per lane
     for (int i0 = 0; i0 < ns; i0 += 2 * kWave) {
@@ -810,10 +654,6 @@ __device__ __forceinline__ void fastw_body(lds_u32* __restrict__ E, lds_u8* __re
         }
     }
     wave_fence();
-#if ORBX_FAST_STOP == 3
-    if (ln == 0) *cnt_out = 0;                                        // diagnostics: staging + pre-test + scores
-    return;
-#endif
     // 4. strict 3x3 NMS at iniTh (bits 0, 1) and minTh (bits 2, 3); kept pixels appended in list order (= row-major)
     //    to the two key lists, which take over the pair image's LDS (key = row * 128 + column in the detection window)
     for (int i0 = 0; i0 < ns; i0 += kWave) {
@@ -821,8 +661,7 @@ __device__ __forceinline__ void fastw_body(lds_u32* __restrict__ E, lds_u8* __re
         int f = 0, key = 0;
         if (i < ns) {
             const int rr = list[i] >> 8, j = list[i] & 0xff;
-            if constexpr (kScU8) f = nms_pair_u8(scb, SWB, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
-            else f = nms_pair((const lds_i16*)scb, SWB / 2, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
+            f = nms_pair((const lds_i16*)scb, SWB / 2, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
             key = rr * 128 + 2 * j;
         }
         const uint64_t a0 = __ballot(f & 1), a1 = __ballot(f & 2), c0 = __ballot(f & 4), c1 = __ballot(f & 8);
@@ -846,8 +685,7 @@ __device__ __forceinline__ void fastw_body(lds_u32* __restrict__ E, lds_u8* __re
     for (int i = ln; i < n; i += kWave) {
         const int k = ks[i], rr = k >> 7, x = k & 127;
         oxy[i] = (uint32_t)(cd.x0 + 3 + x) | ((uint32_t)(cd.y0 + rr + 3) << 16);
-        if constexpr (kScU8) os[i] = (uint8_t)(scb[(rr + 1) * SWB + 2 + x] - 1);
-        else os[i] = (uint8_t)((const lds_i16*)scb)[(rr + 1) * (SWB / 2) + 2 + x];
+        os[i] = (uint8_t)((const lds_i16*)scb)[(rr + 1) * (SWB / 2) + 2 + x];
     }
     if (ln == 0) *cnt_out = n;
 }
@@ -975,10 +813,6 @@ __global__ __launch_bounds__(64 * kWpg) void k_fast_wave(const uint8_t* __restri
         const int n16 = ((Hd + 2) * SWB + 15) >> 4;
         for (int i = ln; i < n16; i += kWave) ((lds_u32x4*)scb)[i] = (u32x4){0u, 0u, 0u, 0u};
     }
-#if ORBX_FAST_STOP == 1
-    if (ln == 0) *cnt_out = 0;                                        // diagnostics: the ROI staging only
-    return;
-#endif
     fastw_body<kPS, kPC>(E, scb, list, cd, img, cnt_out, Wd, Hd, T1, T2, tp, cand_xy, cand_s, cand_stride, kcap, two_pass, ln);
 }
 
@@ -1193,9 +1027,6 @@ __device__ __forceinline__ void blur_tile(const uint8_t* __restrict__ pyr, uint8
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORBX_BLUR_WPE))) void k_blur7(
     const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, size_t pyr_stride, const LevelDev* __restrict__ levels,
     const BlurTile* __restrict__ tiles, int ntiles, int batch, Src0 s0, int tile0) {
-#ifdef ORBX_VCLOB_BLUR
-    ORBX_VCLOB_AT(ORBX_VCLOB_BLUR);
-#endif
     // tiles [tile0, tile0 + ntiles) of every image (a level range: tiles are level-major)
     const int nbx = (ntiles + 3) / 4;                         // 4 tiles (waves) per workgroup
     const int item = xcd_item(xcd_chunk(nbx * batch));       // bands of one image on one XCD
@@ -1370,21 +1201,6 @@ __device__ __forceinline__ void qt_level(QtState S, const LevelDev& L, int lvl, 
     }
     __syncthreads();
     QTP(1);
-#ifdef ORBX_QT_TRIVIAL
-    {   // diagnostics build only (upper bound of a faster DistributeOctTree): the level's first N keys, no quadtree --
-        // wrong keypoints, the same amount of work downstream
-        uint32_t* oxy = out_xy + (size_t)img * out_stride + L.out_off;
-        uint8_t* orr = out_r + (size_t)img * out_stride + L.out_off;
-        const int nout = min(min(K, L.N), L.out_cap);
-        for (int i = tid; i < nout; i += T) {
-            const uint32_t xy = kxy[i];
-            oxy[i] = ((xy & 0xffff) + minB) | (((xy >> 16) + minB) << 16);
-            orr[i] = kr[i];
-        }
-        if (tid == 0) level_cnt[img * nlevels + lvl] = nout | (int)((seq & 0x7fffu) << 16);
-        return;
-    }
-#endif
     // drop empty roots (order preserved), on wave 0: the list, its child counts, and the root -> position map in sb
     // that the first key move reads
     const bool w0 = tid < kWave;
@@ -1671,9 +1487,6 @@ __global__ __launch_bounds__(kQtThreads) void k_quadtree(const LevelDev* __restr
                                                          int out_stride, int* __restrict__ level_cnt, int nlevels, int cap,
                                                          int scan_cap, int* __restrict__ err, int lvl0, int key_lds_off,
                                                          int key_lds_cap, unsigned seq) {
-#ifdef ORBX_VCLOB_QT
-    ORBX_VCLOB_AT(ORBX_VCLOB_QT);
-#endif
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int lvl = lvl0 + (int)blockIdx.x, img = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
 #ifdef ORBX_QT_PROF
@@ -1834,9 +1647,6 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
                                                     int32_t* __restrict__ counts, int capacity, int slot0, int nslots,
                                                     int write_count, int batch, Src0 s0, SlotTable tab, unsigned seq,
                                                     int* __restrict__ err) {
-#ifdef ORBX_VCLOB_DESC
-    ORBX_VCLOB_AT(ORBX_VCLOB_DESC);
-#endif
     constexpr int kLp = kWave / kKpw;
     constexpr int kWinItems = 5 * (2 * kBriefR + 1);             // 37 rows x 5 chunks of 8 bytes
     constexpr int kNW = (kWinItems + kLp - 1) / kLp;             // window chunks per lane
@@ -2020,6 +1830,276 @@ __global__ __launch_bounds__(256) void k_describe_m(const uint8_t* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_describe_sb: IC angle + steered BRIEF with the Gaussian blur taken at the BRIEF sample points (no blurred pyramid)
+// ---------------------------------------------------------------------------------------------
+// The pinned GaussianBlur (7 x 7, sigma 2, taps {18,34,49,55,49,34,18}, REFLECT_101; ORBextractor.cc:1085-1086,
+// DESIGN §2) is exact integer arithmetic rounded once: out = (sum_ij k_i k_j p + 2^15) >> 16, so its two passes can run
+// in either order and the second one only where computeOrbDescriptor reads (:108-147, the 512 rotated sample points,
+// |offset| <= kBriefR).  Per keypoint, the whole wave:
+//   pass 1, matrix cores: H = R K over the raw 43 x 43 window (rows cy-21..cy+21, columns cx-21..cx+21; keypoints lie
+//     >= 19 px inside the level, so the REFLECT_101 rows and columns are at most 2 px outside it).  H column c (0..36,
+//     raw column cx-18+c) is the horizontal 7-tap sum over raw window columns c..c+6, H row h the raw row cy-21+h.  As
+//     3 x 3 tiles of v_mfma_i32_16x16x64_i8: A = the raw bytes - 128 (the i8 range; lane groups 2 s, 2 s + 1 hold
+//     keypoint s's raw columns 16 (nt + g % 2) .. +15 of tile column nt, zeros past the window's third chunk), B = the
+//     tap band of keypoint s (constant; element e of group 2 s + h is tap 16 h + e - n, the other groups zero), C = 0;
+//     adding 128 * 257 to each packed u16 half gives the exact horizontal sum (<= 255 * 257).  A and B share the k labelling and the C map is col = lane & 15, row = 4 (lane >> 4) + reg
+//     (scripts/micro/mx_probe.hip).  H is stored column-major in the wave's LDS slice: kSbRows u16 per column.
+//   pass 2, vector ALU: the blurred pixel at (ry, rx) is (sum_j k_j H[rx + 18][ry + 18 + j] + 2^15) >> 16 -- 7
+//     consecutive u16 of one column: two ds_read2_b32 from the even row at or above, the u16 pairs realigned by
+//     v_alignbit when the first row is odd, and four v_dot2_u32_u16 against the tap pairs, accumulated from 2^15.  The blurred value saturates at 255 (taps summing to 257: (S >> 16) reaches 257), so a test (a < b on the
+//     rounded, saturated values) is S_a < min(S_b & ~0xffff, 255 << 16): an S_a of 256 << 16 or more fails it as its
+//     saturated 255 must.
+// The IC moments and the BRIEF tests run as in k_describe_m<2> (32 lanes per keypoint); the raw window loads of both
+// keypoints share one A operand (lanes 32 s .. 32 s + 31 hold keypoint s's rows), and each keypoint has its own H slice.
+constexpr int kSbRows = 44;                       // u16 rows per H column: rows 0..43 (a sample reads r0 .. r0 + 7)
+constexpr int kSbCols = 2 * kBriefR + 1;          // 37 H columns
+constexpr int kSbSlice = kSbCols * kSbRows * 2;   // 3,256 B of LDS per keypoint, two per wave
+constexpr int kSbC0 = 128 * 257;                  // 128 * (sum of the taps): undoes the -128 of the i8 operand
+#ifndef ORBX_SB_BATCH
+#define ORBX_SB_BATCH 4
+#endif
+constexpr int kSbBatch = ORBX_SB_BATCH;           // BRIEF tests per lane whose sample reads are issued together (1, 2, 4)
+struct BlurBandTab { uint32_t w[2 * 64 * 4]; };   // per keypoint s of a wave and lane: the 16 B operand of its tap band
+constexpr BlurBandTab make_blur_band() {
+    BlurBandTab t{};
+    constexpr int taps[7] = {18, 34, 49, 55, 49, 34, 18};
+    for (int s = 0; s < 2; ++s)
+        for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < 16; ++e) {
+                const int g = l >> 4, n = l & 15, i = 16 * (g & 1) + e - n;
+                const uint32_t v = ((g >> 1) == s && i >= 0 && i < 7) ? (uint32_t)taps[i] : 0u;
+                t.w[(s * 64 + l) * 4 + e / 4] |= v << (8 * (e & 3));
+            }
+    return t;
+}
+__constant__ __attribute__((aligned(16))) BlurBandTab c_blur_band = make_blur_band();
+
+__global__ __launch_bounds__(256) void k_describe_sb(const uint8_t* __restrict__ pyr, size_t pyr_stride,
+                                                     const LevelDev* __restrict__ levels, int nlevels,
+                                                     const uint32_t* __restrict__ lvl_xy, const uint8_t* __restrict__ lvl_r,
+                                                     int out_stride, const int* __restrict__ level_cnt,
+                                                     orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                     int32_t* __restrict__ counts, int capacity, int slot0, int nslots,
+                                                     int write_count, int batch, Src0 s0, SlotTable tab, unsigned seq,
+                                                     int* __restrict__ err) {
+    constexpr int kKpw = 2, kLp = 32;
+    constexpr int kIcItems = 4 * (2 * kHalfPatch + 1);           // 31 rows x 4 chunks (124)
+    constexpr int kNI = (kIcItems + kLp - 1) / kLp;              // IC chunks per lane
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    __shared__ __attribute__((aligned(16))) uint8_t hbuf[4 * kKpw * kSbSlice];
+    const int per_wg = 4 * kKpw;
+    const int nbx = (nslots + per_wg - 1) / per_wg;
+    const int item = xcd_item(xcd_chunk(nbx * batch));
+    if (item >= nbx * batch) return;
+    const int img = item / nbx;
+    const int wrel = __builtin_amdgcn_readfirstlane(((item - img * nbx) * blockDim.x + threadIdx.x) >> 6);
+    if (wrel * kKpw >= nslots) return;                           // whole wave
+    const int ln = lane_id();
+    const int sub = ln / kLp, lk = ln - sub * kLp;
+    const int rel = wrel * kKpw + sub;
+    const int slot = slot0 + rel;
+    int lvl = 0;
+    for (int l = 1; l < nlevels; ++l) lvl += slot >= tab.out_off[l] ? 1 : 0;
+    const int* lcs = level_cnt + img * nlevels;
+    int off = 0, total = 0;
+    for (int l = 0; l < nlevels; ++l) {
+        const int c = lcs[l] & 0xffff;
+        off += l < lvl ? c : 0;
+        total += c;
+    }
+    const int craw = lcs[lvl], ci = craw & 0xffff;
+    if (__ballot(rel < nslots && lvl_stale(craw, seq)) && ln == 0) atomicOr(err, kErrStale);
+    if (write_count && wrel == 0 && ln == 0) counts[img] = min(total, capacity);
+    const LevelDev& L = levels[lvl];
+    const int lpo = L.pyr_off, loo = L.out_off;
+    const int i = slot - loo;
+    const int o = off + i;
+    const bool valid = rel < nslots && i < ci && o < capacity;
+    const uint64_t vmask = __ballot(valid);
+    if (vmask == 0) return;                                      // whole wave
+
+    const uint32_t xy = valid ? lvl_xy[(size_t)img * out_stride + loo + i] : 0u;
+    const int cx = (int)(xy & 0xffff), cy = (int)(xy >> 16);
+    const uint8_t* P = lvl == 0 ? s0.p + img * s0.istride : pyr + img * pyr_stride + lpo;
+    const int pstride = lvl == 0 ? (int)s0.step : L.w;
+    // IC_Angle (:77-104), as k_describe_m<2>
+    int m10 = 0, m01 = 0;
+    {
+        uint64_t ic[kNI];
+        const uint8_t* p0 = P + (size_t)(cy - kHalfPatch) * pstride + (cx - kHalfPatch);
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < kNI; ++k) {
+                const int q = lk + kLp * k, r = min(q >> 2, 2 * kHalfPatch);
+                __builtin_memcpy(&ic[k], p0 + (size_t)r * pstride + 8 * (q & 3), 8);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kNI; ++k) {
+            const int q = lk + kLp * k;
+            const int v = (q >> 2) - kHalfPatch;
+            const int u0 = 8 * (q & 3) - kHalfPatch;
+            const uint64_t m = valid ? c_ic_mask.m[k][lk] : 0ull;
+            const uint64_t px = ic[k] & m;
+            const uint32_t a = (uint32_t)px, b = (uint32_t)(px >> 32);
+            const uint32_t wa = (uint32_t)(u0 + 16) * 0x01010101u + 0x03020100u, wb = wa + 0x04040404u;
+            const int dot = (int)__builtin_amdgcn_udot4(b, wb, __builtin_amdgcn_udot4(a, wa, 0u, false), false);
+            const int sum = (int)__builtin_amdgcn_udot4(b, 0x01010101u, __builtin_amdgcn_udot4(a, 0x01010101u, 0u, false), false);
+            m10 += dot - 16 * sum;
+            m01 += v * sum;
+        }
+    }
+    m10 = group_sum<kLp>(m10, sub);
+    m01 = group_sum<kLp>(m01, sub);
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    const float ang = __fmul_rn(angle, (float)(M_PI / 180.f));
+    float sa, sb;
+    orbx_sincos_brief(ang, &sa, &sb);
+
+    uint8_t* hb = hbuf + (threadIdx.x >> 6) * kKpw * kSbSlice;
+    const int g = ln >> 4, n16 = ln & 15;
+    // ---- pass 1 operands of BOTH keypoints, loaded once: lanes 32 sub + 16 gh + n (gh = g & 1) hold raw window row
+    // 16 mt + n of keypoint sub, columns 16 (nt + gh) .. +15.  Keypoint s's product takes band s, whose taps sit in
+    // lane groups 2 s, 2 s + 1 (the other keypoint's bytes meet zeros), so one A operand serves both.
+    v4i a[3][3];
+    {
+        const int gh = g & 1;
+        const int ws = L.w, hs = L.h;
+        // chunks reach raw columns cx-21 .. cx+26; closer to a level edge every byte is placed by REFLECT_101
+        const bool edge = cx < kBriefR + 3 || cx + 26 > ws - 1;
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt) {
+            int y = cy - (kBriefR + 3) + min(16 * mt + n16, 2 * kBriefR + 6);
+            y = y < 0 ? -y : (y > hs - 1 ? 2 * (hs - 1) - y : y);
+            const uint8_t* rowp = P + (size_t)y * pstride;
+#pragma unroll
+            for (int nt = 0; nt < 3; ++nt) {
+                const int cc = nt + gh;                           // 16-column chunk of the window
+                a[mt][nt] = v4i{0, 0, 0, 0};
+                if (valid && cc < 3) {
+                    const int x0 = cx - (kBriefR + 3) + 16 * cc;
+                    if (!edge) {
+                        __builtin_memcpy(&a[mt][nt], rowp + x0, 16);
+                    } else {
+                        int wv[4];
+#pragma unroll 1
+                        for (int d = 0; d < 4; ++d) {
+                            uint32_t v = 0;
+                            for (int e = 0; e < 4; ++e) {
+                                int x = x0 + 4 * d + e;
+                                x = x < 0 ? -x : (x > ws - 1 ? 2 * (ws - 1) - x : x);
+                                x = min(max(x, 0), ws - 1);           // columns past cx+21 have zero taps
+                                v |= (uint32_t)rowp[x] << (8 * e);
+                            }
+                            wv[d] = (int)v;
+                        }
+                        a[mt][nt] = v4i{wv[0], wv[1], wv[2], wv[3]};
+                    }
+                    a[mt][nt] ^= (int)0x80808080;
+                }
+            }
+        }
+    }
+    // ---- pass 1: H = R K on the matrix cores for both keypoints, each into its own LDS slice, column-major
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt) {
+        const int r0 = 16 * mt + 4 * g;
+#pragma unroll
+        for (int nt = 0; nt < 3; ++nt) {
+            const int c = 16 * nt + n16;
+#pragma unroll
+            for (int s = 0; s < kKpw; ++s) {
+                const v4i band = *reinterpret_cast<const v4i*>(&c_blur_band.w[(s * 64 + ln) * 4]);
+                // C = 0 (an inline operand): the tile is H - 128 * 257; the u16 halves get 128 * 257 back after packing
+                const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[mt][nt], band, v4i{0, 0, 0, 0}, 0, 0, 0);
+                if (c < kSbCols && r0 < kSbRows) {
+                    const u16x2 off = {kSbC0, kSbC0};
+                    const u16x2 lo = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm((uint32_t)acc.y, (uint32_t)acc.x, 0x05040100u)) + off;
+                    const u16x2 hi = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm((uint32_t)acc.w, (uint32_t)acc.z, 0x05040100u)) + off;
+                    *reinterpret_cast<uint2*>(hb + s * kSbSlice + c * (2 * kSbRows) + 2 * r0) =
+                        make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // ---- pass 2 + BRIEF, 32 lanes per keypoint (tests g * 32 + lk, as k_describe_m<2>): the vertical taps at the two
+    // sample points of each test, read from the lane's keypoint's slice
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 ab1 = {sb, sa}, ab2 = {sa, -sb}, magic = {12582912.0f, 12582912.0f};
+    // u16 H[rx + 18][ry + 18] from the magic-constant bits (see k_describe_m): the i24 product t is
+    // (0x400000 + rx) * kSbRows + 0x4B400000 + ry, so t - kSbMagic is the element index; kSbMagic is even, so t's parity
+    // is the row's, and the dword at or above it is at byte 2 (t & ~1) - 2 kSbMagic
+    constexpr uint32_t kSbMagic = 0x400000u * (uint32_t)kSbRows + 0x4B400000u - (uint32_t)(kBriefR * kSbRows + kBriefR);
+    static_assert((kSbMagic & 1u) == 0u, "row parity from t");
+    const uint32_t hb_base = (uint32_t)(uintptr_t)(hb + sub * kSbSlice) - 2u * kSbMagic;
+    const u16x2 t01 = {18, 34}, t23 = {49, 55}, t45 = {49, 34}, t6 = {18, 0};
+    constexpr int kNT = 256 / kLp;
+    uint32_t pat[kNT];
+    {
+        const uint32_t* pw = c_pattern_l32.w + lk * kNT;
+#pragma unroll
+        for (int q = 0; q < kNT; q += 4) __builtin_memcpy(&pat[q], pw + q, 16);
+    }
+    uint32_t words[kNT];
+#pragma unroll
+    for (int q0 = 0; q0 < kNT; q0 += kSbBatch) {
+        uint32_t S[kSbBatch][2];
+#pragma unroll
+        for (int qb = 0; qb < kSbBatch; ++qb) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const uint32_t w = pat[q0 + qb];
+                const float fx = (float)(int)(signed char)(w >> (16 * e)), fy = (float)(int)(signed char)(w >> (16 * e + 8));
+                const f32x2 fxy = {fx, fy};
+                f32x2 p, qq, r;
+                asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(p) : "v"(fxy), "v"(ab1));              // {fx b, fx a}
+                asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(qq) : "v"(fxy), "v"(ab2)); // {fy a, -fy b}
+                asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(p), "v"(qq));                                 // {ry, rx}
+                asm("v_pk_add_f32 %0, %1, %2" : "=v"(p) : "v"(r), "v"(magic));                              // + M
+                const float ryM = p.x, rxM = p.y;
+                int t;
+                asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(t) : "v"(__float_as_int(rxM)), "n"(kSbRows), "v"(__float_as_int(ryM)));
+                // 4-byte-aligned reads from the even row at or above r0 (a 32-bit LDS read off its 4-byte alignment returns
+                // the right bytes but is replayed: r6b, 3.5 ms against 0.67), then the u16 pairs realigned by 16 bits
+                // when r0 is odd (v_alignbit reads the low 5 bits of the shift: t << 4 is 16 or 0)
+                const uint32_t* hp = reinterpret_cast<const uint32_t*>((uintptr_t)(hb_base + 2u * ((uint32_t)t & ~1u)));
+                const uint32_t d0 = hp[0], d1 = hp[1], d2 = hp[2], d3 = hp[3], sh = (uint32_t)t << 4;
+                uint32_t acc = 0x8000u;
+                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_alignbit(d1, d0, sh)), t01, acc, false);
+                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_alignbit(d2, d1, sh)), t23, acc, false);
+                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_alignbit(d3, d2, sh)), t45, acc, false);
+                acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_alignbit(d3, d3, sh)), t6, acc, false);
+                S[qb][e] = acc;
+            }
+        }
+#pragma unroll
+        for (int qb = 0; qb < kSbBatch; ++qb) {
+            const uint64_t bm = __ballot(S[qb][0] < min(S[qb][1] & 0xffff0000u, 0x00ff0000u));
+            words[q0 + qb] = (uint32_t)(bm >> (sub * kLp));
+        }
+    }
+    if (!valid) return;
+    uint32_t dw = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dw = lk == j ? words[j] : dw;
+    if (lk < 8) reinterpret_cast<uint32_t*>(desc + ((size_t)img * capacity + o) * 32)[lk] = dw;
+    if (lk == 0) {
+        orbx_keypoint k;
+        float x = (float)cx, y = (float)cy;
+        if (lvl != 0) { x = __fmul_rn(x, L.scale); y = __fmul_rn(y, L.scale); }
+        k.x = x; k.y = y;
+        k.size = (float)L.patch;
+        k.angle = angle;
+        k.response = (float)lvl_r[(size_t)img * out_stride + loo + i];
+        k.octave = lvl;
+        k.class_id = -1;
+        kps[(size_t)img * capacity + o] = k;
+    }
+}
+
 // =============================================================================================
 // host side
 // =============================================================================================
@@ -2144,9 +2224,6 @@ struct Extractor {
     BlurTile* d_tiles = nullptr;
     std::vector<ResizeTab> rtab;
     std::vector<ResizeVec> rvec;      // per level: vectorised tables (groups == 0 -> use rtab)
-    std::vector<ResizePair> rpair;    // per level la: the pair launch la -> la + 1, la + 2 (nbands == 0: none)
-    std::vector<int> rpair_lds;       // its dynamic LDS bytes
-    bool resize_pair = false;         // ORBX_RESIZE_PAIR=1: two levels per launch (read at configure)
     std::vector<void*> rtab_mem;
     uint8_t* d_pyr = nullptr;         // pyramid set of the current / last call (a slot of d_pyr_ring)
     uint8_t* d_pyr_ring = nullptr;    // pyr_ring sets of max_batch pyramids: a caller that reads the pyramid of call
@@ -2154,6 +2231,10 @@ struct Extractor {
     unsigned long long ncalls = 0;    // k+1, which writes the next set
     uint8_t* d_blur = nullptr;        // desc_sets sets of the blurred pyramid / kept keypoints (d_*_c: the current call's)
     uint8_t* d_blur_c = nullptr;
+    // k_describe_sb (blur at the BRIEF sample points) instead of k_blur7 + k_describe_m: no blurred pyramid is kept
+    // (ORBX_DESC_SB, read at create)
+    bool desc_sb = false;
+    uint8_t* d_blur_diag = nullptr;   // one image's blurred pyramid, made on demand by orbx_extractor_copy_blurred_level
     int desc_sets = 2;                // call k + 1's blur and DistributeOctTree write the other set (ORBX_DESC_SETS=1: one)
     unsigned long long dcalls = 0;    // while call k's describe reads its own (no wait on that describe)
     int dset_call[2] = {-1, -1};      // event-pool index of the last call that used each set
@@ -2269,7 +2350,7 @@ static void level_dims(const Extractor* e, int rows, int cols, int l, int* w, in
 void Extractor::free_buffers() {
     drop_graph();                                          // it names the buffers freed below
     auto F = [](auto*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } };
-    F(d_levels); F(d_cells); F(d_tiles); F(d_pyr_ring); F(d_blur); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
+    F(d_levels); F(d_cells); F(d_tiles); F(d_pyr_ring); F(d_blur); F(d_blur_diag); F(d_cand_xy); F(d_cand_s); F(d_cell_cnt);
     F(d_key_xy); F(d_key_r); F(d_key_node); F(d_lvl_xy); F(d_lvl_r); F(d_lvl_cnt); F(d_err); F(d_in);
     F(d_hblk);
     d_kps = nullptr; d_desc = nullptr; d_cnt = nullptr;
@@ -2474,7 +2555,6 @@ int Extractor::configure(int r, int c, int batch) {
     // ---- resize tables (pinned OpenCV 3.2 INTER_LINEAR fixed point), level l from level l-1
     rtab.assign(nlevels, ResizeTab{});
     rvec.assign(nlevels, ResizeVec{});
-    std::vector<std::vector<int>> ry0(nlevels), ry1(nlevels);        // source rows of every level's rows (pair bands)
     for (int l = 1; l < nlevels; ++l) {
         const int sw = lv[l - 1].w, sh = lv[l - 1].h, dw = lv[l].w, dh = lv[l].h;
         const double sxs = 1.0 / ((double)dw / sw), sys = 1.0 / ((double)dh / sh);
@@ -2504,8 +2584,6 @@ int Extractor::configure(int r, int c, int batch) {
             hy0[y] = std::min(std::max(iy, 0), sh - 1);
             hy1[y] = std::min(std::max(iy + 1, 0), sh - 1);
         }
-        ry0[l] = hy0;
-        ry1[l] = hy1;
         int* mem;
         if ((st = dev_alloc(&mem, 4 * (size_t)dw + 4 * (size_t)dh))) return st;
         rtab_mem.push_back(mem);
@@ -2549,48 +2627,6 @@ int Extractor::configure(int r, int c, int batch) {
             rvec[l] = rv;
         }
     }
-    // pair launches la -> lb = la + 1, lc = la + 2 for la = 0, 2, 4, ...: lc's bands of kResizeBand rows, the lb rows
-    // each reads ([c0, c1)) and the lb rows each writes (a partition of lb's rows: band k owns [c0_k, c0_{k+1}), the
-    // first from row 0, the last to the end)
-    rpair.assign(nlevels, ResizePair{});
-    rpair_lds.assign(nlevels, 0);
-    {
-        const char* v = std::getenv("ORBX_RESIZE_PAIR");
-        resize_pair = v && std::atoi(v) == 1;
-    }
-    for (int la = 0; la + 2 < nlevels; la += 2) {
-        const int lb = la + 1, lc = la + 2;
-        if (!rvec[lb].groups || !rvec[lc].groups || lv[la].w < 8 || rvec[lb].groups > 512) continue;
-        const int hb = lv[lb].h, hc = lv[lc].h, nb = (hc + kResizeBand - 1) / kResizeBand;
-        std::vector<int4> bands(nb);
-        int maxrows = 0;
-        for (int k = 0; k < nb; ++k) {
-            const int ya = k * kResizeBand, yz = std::min(ya + kResizeBand, hc) - 1;
-            bands[k].x = std::min(ry0[lc][ya], ry1[lc][ya]);
-            bands[k].y = std::max(ry0[lc][yz], ry1[lc][yz]) + 1;
-        }
-        for (int k = 0; k < nb; ++k) {
-            bands[k].z = k == 0 ? 0 : bands[k].x;
-            bands[k].w = k + 1 < nb ? bands[k + 1].x : hb;
-            bands[k].x = std::min(bands[k].x, bands[k].z);              // compute every owned row too
-            bands[k].y = std::max(bands[k].y, bands[k].w);
-            maxrows = std::max(maxrows, bands[k].y - bands[k].x);
-        }
-        bool ok = true;
-        for (int k = 0; k < nb; ++k) ok = ok && bands[k].x >= 0 && bands[k].y <= hb && bands[k].z <= bands[k].w;
-        const int stride = ((lv[lb].w + 3) & ~3) + 8;
-        const int lds = maxrows * stride + 16;
-        if (!ok || lds > 64 * 1024) continue;
-        int4* dband;
-        if ((st = dev_alloc(&dband, nb))) return st;
-        rtab_mem.push_back(dband);
-        ORBX_HIP(hipMemcpy(dband, bands.data(), sizeof(int4) * nb, hipMemcpyHostToDevice));
-        ResizePair& P = rpair[la];
-        P.tb = rvec[lb]; P.tc = rvec[lc]; P.band = dband; P.nbands = nb; P.stride = stride;
-        P.wa = lv[la].w; P.wb = lv[lb].w; P.hb = hb; P.wc = lv[lc].w; P.hc = hc;
-        P.off_b = lv[lb].pyr_off; P.off_c = lv[lc].pyr_off;
-        rpair_lds[la] = lds;
-    }
 
     // ---- batch buffers (HBM): pyramid + blurred pyramid + candidates + quadtree scratch
     const size_t B = (size_t)batch;
@@ -2603,7 +2639,7 @@ int Extractor::configure(int r, int c, int batch) {
     }
     dcalls = 0;
     dset_call[0] = dset_call[1] = -1;
-    if ((st = dev_alloc(&d_blur, (size_t)desc_sets * B * pyr_size))) return st;
+    if (!desc_sb && (st = dev_alloc(&d_blur, (size_t)desc_sets * B * pyr_size))) return st;
     d_blur_c = d_blur;
     if ((st = dev_alloc(&d_cand_xy, B * cand_stride))) return st;
     if ((st = dev_alloc(&d_cand_s, B * cand_stride))) return st;
@@ -2658,7 +2694,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     const int dset = (int)(e->dcalls++ % (unsigned long long)e->desc_sets);
     {
         const size_t B = (size_t)e->max_batch;
-        e->d_blur_c = e->d_blur + (size_t)dset * B * ps;
+        e->d_blur_c = e->d_blur ? e->d_blur + (size_t)dset * B * ps : nullptr;
         e->d_lvl_xy_c = e->d_lvl_xy + (size_t)dset * B * e->out_stride;
         e->d_lvl_r_c = e->d_lvl_r + (size_t)dset * B * e->out_stride;
         e->d_lvl_cnt_c = e->d_lvl_cnt + (size_t)dset * B * nl;
@@ -2687,11 +2723,12 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     const int ncells = (int)e->cellv.size();
     const std::vector<int>& toff = e->tile_off;                     // blur tiles of level l: [toff[l], toff[l + 1])
     QtScratch qs{e->d_key_xy, e->d_key_r, e->d_key_node};
-    auto fast = [&](hipStream_t q, int k) {
+    auto fast = [&](hipStream_t q, int k) -> int {
         const Extractor::WaveLaunch& wl = e->wave_launch[k];
-        if (wl.n <= 0) return;
+        if (wl.n <= 0) return ORBX_OK;
         if (k != 0 && e->qt_prev >= 0) {                            // the previous call's quadtree on its output stream
-            (void)hipStreamWaitEvent(q, e->cev[e->qt_prev].qt, 0);
+            // (a capture follows sync_calls and stream synchronisations, so that quadtree is done: no edge into it)
+            if (!e->capturing) ORBX_HIP(hipStreamWaitEvent(q, e->cev[e->qt_prev].qt, 0));
             if (!qto) e->qt_prev = -1;
         }
         constexpr int wpg = Extractor::kWaveWpg;
@@ -2700,6 +2737,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         hipLaunchKernelGGL(kw, dim3(kXcds * xcd_chunk(nwg)), dim3(64 * wpg), (size_t)wpg * wl.lay.bytes, q, e->d_pyr, ps,
                            e->d_levels, e->d_cells, wl.cell0, wl.n, e->iniTh, e->minTh, e->d_cand_xy, e->d_cand_s,
                            e->cand_stride, e->d_cell_cnt, ncells, batch, s0, wl.lay, wl.kcap, e->wave_twopass);
+        return ORBX_OK;
     };
     auto quadtree = [&](hipStream_t q, int lvl0, int n) {
         if (n <= 0) return;
@@ -2710,7 +2748,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
                            (int)e->qt_lds, kc, seq);
     };
     auto blur = [&](hipStream_t q, int tile0, int n) {
-        if (n <= 0) return;
+        if (n <= 0 || e->desc_sb) return;                           // k_describe_sb blurs at the sample points
         hipLaunchKernelGGL(k_blur7, dim3(kXcds * xcd_chunk((n + 3) / 4 * batch)), dim3(256), 0, q, e->d_pyr, e->d_blur_c, ps,
                            e->d_levels, e->d_tiles, n, batch, s0, tile0);
     };
@@ -2727,13 +2765,6 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
             const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
             const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
             const LevelDev& L = e->lv[l];
-            if (e->resize_pair && l + 1 < nl && e->rpair[l - 1].nbands > 0) {   // levels l and l + 1 in one launch
-                const ResizePair& P = e->rpair[l - 1];
-                hipLaunchKernelGGL(k_resize_pair, dim3(kXcds * xcd_chunk(P.nbands * batch)), dim3((P.tb.groups + 63) & ~63),
-                                   (size_t)e->rpair_lds[l - 1], s, e->d_pyr, ps, src, sstep, sis, P, batch);
-                ++l;
-                continue;
-            }
             if (e->rvec[l].groups > 0) {
                 const int nstrips = (L.w + kResizeStrip - 1) / kResizeStrip, nbands = (L.h + kResizeBand - 1) / kResizeBand;
                 const int nwg = (nstrips * nbands * batch + 3) / 4;
@@ -2752,7 +2783,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         // one launch per stage over every level (the host API's one-image calls, where the chain of dependent launches
         // is the latency): FAST, DistributeOctTree, blur
         mark(6);
-        fast(s, 2);
+        if (int st = fast(s, 2)) return st;
         mark(7);
         if (int st = after_prev_describe(s)) return st;
         quadtree(s, 0, nl);
@@ -2765,7 +2796,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     } else {
     // side stream, level 0 (reads only the caller's images)
     mark(6);
-    fast(side, 0);
+    if (int st = fast(side, 0)) return st;
     mark(7);
     if (int st = after_prev_describe(side)) return st;
     quadtree(side, 0, nl > 0 ? 1 : 0);
@@ -2781,7 +2812,7 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
     mark(9);
     if (side != s) ORBX_HIP(hipEventRecord(ce.join, side));
     mark(10);                                                       // launch stream: FAST, DistributeOctTree 1..nl-1
-    fast(s, 1);
+    if (int st = fast(s, 1)) return st;
     mark(2);
     if (!qto) {
         if (int st = after_prev_describe(s)) return st;
@@ -2810,9 +2841,14 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
         const int nslots = e->out_stride;                           // every level's slots; the launch writes the counts
         constexpr int kpw = 2;                                      // keypoints per wave
         dim3 g(kXcds * xcd_chunk((nslots + 4 * kpw - 1) / (4 * kpw) * batch));
-        hipLaunchKernelGGL(k_describe_m<kpw>, g, dim3(256), 0, so, e->d_pyr, e->d_blur_c, ps, e->d_levels, nl, e->d_lvl_xy_c,
-                           e->d_lvl_r_c, e->out_stride, e->d_lvl_cnt_c, d_kps, d_desc, d_counts, capacity, 0, nslots, 1, batch,
-                           s0, tab, seq, e->d_err);
+        if (e->desc_sb)
+            hipLaunchKernelGGL(k_describe_sb, g, dim3(256), 0, so, e->d_pyr, ps, e->d_levels, nl, e->d_lvl_xy_c, e->d_lvl_r_c,
+                               e->out_stride, e->d_lvl_cnt_c, d_kps, d_desc, d_counts, capacity, 0, nslots, 1, batch, s0, tab,
+                               seq, e->d_err);
+        else
+            hipLaunchKernelGGL(k_describe_m<kpw>, g, dim3(256), 0, so, e->d_pyr, e->d_blur_c, ps, e->d_levels, nl,
+                               e->d_lvl_xy_c, e->d_lvl_r_c, e->out_stride, e->d_lvl_cnt_c, d_kps, d_desc, d_counts, capacity, 0,
+                               nslots, 1, batch, s0, tab, seq, e->d_err);
     }
     mark(5);
     ORBX_HIP(hipEventRecord(ce.desc, so));
@@ -2928,6 +2964,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* hm = std::getenv("ORBX_HOST_MERGED")) e->host_merged = std::atoi(hm) != 0;
     if (const char* sw = std::getenv("ORBX_DEBUG_SKIP_DESC_WAIT")) e->dbg_skip_desc_wait = std::atoi(sw) != 0;
     if (const char* qo = std::getenv("ORBX_QT_OUT")) e->qt_out = std::atoi(qo) != 0;
+    if (const char* sb = std::getenv("ORBX_DESC_SB")) e->desc_sb = std::atoi(sb) != 0;
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
         return st;
@@ -3256,14 +3293,24 @@ int orbx_extractor_level_device(orbx_extractor* e, int index, int level, const u
 
 int orbx_extractor_copy_blurred_level(orbx_extractor* e, int index, int level, uint8_t* dst, size_t dst_step) {
     ORBX_REQUIRE(e && dst, ORBX_ERR_ARG, "null argument");
-    ORBX_REQUIRE(e->d_blur && e->last_src0.p && level >= 0 && level < e->nlevels && index >= 0 &&
+    ORBX_REQUIRE(e->d_pyr && e->last_src0.p && level >= 0 && level < e->nlevels && index >= 0 &&
                      index < e->last_batch,
                  ORBX_ERR_ARG, "no blurred level for index %d level %d", index, level);
     const int w = e->lv[level].w, h = e->lv[level].h;
     ORBX_REQUIRE(dst_step >= (size_t)w, ORBX_ERR_ARG, "bad destination");
     ORBX_HIP(hipSetDevice(e->device));
-    ORBX_HIP(hipDeviceSynchronize());                                  // the last call's blur may run on any of its streams
-    const uint8_t* p = e->d_blur_c + (size_t)index * e->pyr_size + e->lv[level].pyr_off;   // as k_blur7 writes it
+    ORBX_HIP(hipDeviceSynchronize());                                  // the last call's kernels may run on any stream
+    // k_blur7 over every tile of image `index` of the last call's pyramid (d_pyr, and level 0 = the caller's image),
+    // into a one-image buffer: whatever the describe form, and whichever describe-input set the last call used
+    if (!e->d_blur_diag) ORBX_HIP(hipMalloc((void**)&e->d_blur_diag, e->pyr_size));
+    const int ntiles = e->tile_off[e->nlevels] - e->tile_off[0];
+    const Src0 s0{e->last_src0.p + (size_t)index * e->last_src0.istride, e->last_src0.step, e->last_src0.istride};
+    hipLaunchKernelGGL(k_blur7, dim3(kXcds * xcd_chunk((ntiles + 3) / 4)), dim3(256), 0, e->own(),
+                       e->d_pyr + (size_t)index * e->pyr_size, e->d_blur_diag, e->pyr_size, e->d_levels, e->d_tiles, ntiles, 1,
+                       s0, e->tile_off[0]);
+    ORBX_HIP(hipGetLastError());
+    ORBX_HIP(hipStreamSynchronize(e->own()));
+    const uint8_t* p = e->d_blur_diag + e->lv[level].pyr_off;          // as k_blur7 writes it
     ORBX_HIP(hipMemcpy2D(dst, dst_step, p, (size_t)w, (size_t)w, (size_t)h, hipMemcpyDeviceToHost));
     return ORBX_OK;
 }

@@ -286,60 +286,11 @@ __global__ __launch_bounds__(256) void k_kfdb_share(DbDev D, QueryIn Q, QScratch
     }
 }
 
-// Small databases: no inverted file.  One wave per (query, slot) intersects the slot's BowVector with the
-// query's and produces the same word count and first shared query word as k_kfdb_share.  The query's words sit in an
-// LDS hash table (open addressing, load <= 1/2, word -> its index in the query's ascending list).  The L1 scores are
-// left to k_kfdb_score, for the keyframes that pass minCommonWords only (:113-126), as on the inverted-file path: the
-// score is a sequential double sum in word order, one lane at a time, and summing it for every (query, slot) pair was
-// most of this kernel's time (r5: 0.07 ms per step at one agent, 0.36 at eight, where the ring holds 1,224 slots).
-constexpr uint32_t kHashEmpty = 0xffffffffu;
-__device__ __forceinline__ uint32_t kfdb_hash(uint32_t w, int log_t) { return (w * 0x9e3779b1u) >> (32 - log_t); }
-
-__global__ __launch_bounds__(512) void k_kfdb_pairwise(DbDev D, QueryIn Q, QScratch X, int kind, int log_t) {
-    extern __shared__ unsigned char smem[];
-    const int T = 1 << log_t, mask = T - 1;
-    uint32_t* hk = reinterpret_cast<uint32_t*>(smem);               // [T] word keys (kHashEmpty = free)
-    uint16_t* hi = reinterpret_cast<uint16_t*>(hk + T);            // [T] list index of the key
-    const int q = blockIdx.y;
-    const int qs = Q.slot[q];
-    const int nq = D.bn[qs];
-    for (int i = threadIdx.x; i < T; i += blockDim.x) hk[i] = kHashEmpty;
-    __syncthreads();
-    for (int i = threadIdx.x; i < nq; i += blockDim.x) {              // BowVector words are distinct: no duplicate keys
-        const uint32_t w = D.bw[(size_t)qs * D.maxw + i];
-        for (uint32_t h = kfdb_hash(w, log_t);; h = (h + 1) & mask) {
-            if (atomicCAS(&hk[h], kHashEmpty, w) == kHashEmpty) { hi[h] = (uint16_t)i; break; }
-        }
-    }
-    __syncthreads();
-    const int waves = blockDim.x / kWave;
-    const size_t row = (size_t)q * D.S;
-    for (int k = blockIdx.x * waves + (int)(threadIdx.x / kWave); k < D.S; k += gridDim.x * waves) {
-        int c = 0;
-        uint32_t first = 0x7f7f7f7fu;
-        if (kf_visible(D, Q, q, k) && !(kind == KIND_COVIS && excl_at(X, row + k)) && nq > 0) {
-            const uint32_t* cw = D.bw + (size_t)k * D.maxw;
-            const int nc = D.bn[k];
-            for (int i = lane_id(); i < nc; i += kWave) {
-                const uint32_t w = cw[i];
-                uint32_t h = kfdb_hash(w, log_t), key;
-                while ((key = hk[h]) != kHashEmpty && key != w) h = (h + 1) & mask;
-                if (key == w) {
-                    ++c;
-                    first = min(first, (uint32_t)hi[h]);
-                }
-            }
-            c = wave_sum(c);
-            first = wave_min_u32(first);
-        }
-        if (lane_id() == 0) {
-            X.cnt[row + k] = c;
-            X.first[row + k] = (int)first;
-        }
-    }
-}
-
-// The same intersection against a bitmap of the query's words over the vocabulary, in memory (nbw words per query;
+// Small databases: no inverted file.  One wave per (query, slot) intersects the slot's BowVector with the query's and
+// produces the same word count and first shared query word as k_kfdb_share; the L1 scores are left to k_kfdb_score,
+// for the keyframes that pass minCommonWords only (:113-126), as on the inverted-file path (summing the score for every
+// (query, slot) pair was most of the pairwise time: r5, 0.07 ms per step at one agent, 0.36 at eight).  The query's
+// words are a bitmap over the vocabulary, in memory (nbw words per query;
 // DBoW2's k = 10, L = 6 tree has 10^6 leaves, 122 KB per query, L2-resident: the workgroups of one query are dealt to
 // one XCD) -- no LDS, so it never holds a CU's LDS that FAST beside it could use.  Per slot wave: four slot words per
 // lane in flight, then their four bitmap words; the hit count is the ballots' popcounts.  The words are ascending in
@@ -858,11 +809,6 @@ static int pairwise_max_members() {
     return v;
 }
 
-// the pairwise intersection over per-query vocabulary bitmaps in memory (ORBX_KFDB_BITMAP=0: the LDS hash table)
-static bool pairwise_bitmap() {
-    static const bool v = [] { const char* e = std::getenv("ORBX_KFDB_BITMAP"); return !e || std::atoi(e) != 0; }();
-    return v;
-}
 
 // The query batch on stream s; d_* are device pointers.  Scratch rows at 'base' (nq x S).
 int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned char* base, int32_t* d_out, int out_stride,
@@ -884,7 +830,7 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
     const size_t lds = (size_t)db->maxw * (sizeof(double) + sizeof(uint32_t));
     const int nbw = (db->n_vocab + 31) / 32;
     uint32_t* qbits = nullptr;
-    if (pairwise && pairwise_bitmap()) {
+    if (pairwise) {
         const size_t need = (size_t)4 * nbw * nq;
         if (need > db->qbits_bytes) {
             if (db->d_qbits) {
@@ -902,15 +848,6 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
         const int gx = std::max(1, std::min((db->S + 15) / 16, 128));   // ~4 slots per wave
         hipLaunchKernelGGL(k_kfdb_pairwise_gb, dim3(kXcds * xcd_chunk(gx * nq)), dim3(256), 0, s, D, Q, X, kind, qbits,
                            nbw, nq, gx);
-    } else if (pairwise) {
-        const int gx = std::min((db->S + 7) / 8, 64);
-        int log_t = 1;
-        while ((1 << log_t) < 2 * db->maxw) ++log_t;                // load factor <= 1/2
-        const size_t plds = (size_t)6 << log_t;
-        ORBX_REQUIRE(plds <= 160 * 1024, ORBX_ERR_UNSUPPORTED, "pairwise LDS %zu B", plds);
-        if (plds > 64 * 1024)
-            ORBX_HIP(hipFuncSetAttribute((const void*)k_kfdb_pairwise, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));
-        hipLaunchKernelGGL(k_kfdb_pairwise, dim3(gx, nq), dim3(512), plds, s, D, Q, X, kind, log_t);
     } else {
         ORBX_HIP(hipMemsetAsync(X.cnt, 0, 4 * r, s));
         ORBX_HIP(hipMemsetAsync(X.first, 0x7f, 4 * r, s));
@@ -920,7 +857,13 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
     hipLaunchKernelGGL(k_kfdb_score, dim3(32, nq), dim3(256), lds, s, D, Q, X);   // the minCommonWords candidates
     hipLaunchKernelGGL(k_kfdb_accum, dim3(nq), dim3(256), 0, s, D, Q, X, St, kind, d_out, out_stride, d_out_n, d_status);
     hipLaunchKernelGGL(k_kfdb_state, dim3((db->S + 255) / 256), dim3(256), 0, s, D, Q, X, St, kind, nq, d_status);
-    ORBX_HIP(hipGetLastError());
+    const hipError_t le = hipGetLastError();
+    if (le != hipSuccess && qbits) {
+        // the bitmaps must be all zero between batches (k_kfdb_select clears what k_kfdb_bits set): if a launch of this
+        // batch failed, clear them all so the next batch does not count words it does not share
+        (void)hipMemsetAsync(qbits, 0, db->qbits_bytes, s);
+    }
+    ORBX_HIP(le);
     return ORBX_OK;
 }
 

@@ -50,54 +50,13 @@ __global__ __launch_bounds__(256) void k_hamming_pairs(const uint8_t* __restrict
 constexpr int kBfQ = 256;      // queries per workgroup (4 waves, one query per lane)
 constexpr int kBfStage = 256;  // train rows staged in LDS per step (8 KB)
 
-// The chunk partials of one query, in ascending chunk order, folded into (best key, second distance) and written out
-// (ORBmatcher's best / second rule over the whole train set; see k_bf_merge_g for why the fold is order-free).
-__device__ __forceinline__ void bf_fold_write(const uint32_t* __restrict__ pb, const int32_t* __restrict__ ps, int nq, int nchunks,
-                                              size_t o, int32_t* __restrict__ best_idx, int32_t* __restrict__ best_dist,
-                                              int32_t* __restrict__ second_dist) {
-    uint32_t best = 256u << 20;
-    int second = 256;
-    auto fold = [&](uint32_t b, int sc) {
-        if (b < best) {
-            second = min(sc, (int)(best >> 20));
-            best = b;
-        } else {
-            second = min(second, (int)(b >> 20));
-        }
-    };
-    constexpr int U = 8;                                   // independent loads in flight: full groups load unconditionally
-    int c0 = 0;
-    for (; c0 + U <= nchunks; c0 += U) {
-        uint32_t b[U];
-        int32_t sc[U];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            b[k] = __builtin_nontemporal_load(pb + (size_t)(c0 + k) * nq);
-            sc[k] = __builtin_nontemporal_load(ps + (size_t)(c0 + k) * nq);
-        }
-#pragma unroll
-        for (int k = 0; k < U; ++k) fold(b[k], sc[k]);
-    }
-    for (; c0 < nchunks; ++c0) fold(pb[(size_t)c0 * nq], ps[(size_t)c0 * nq]);
-    const int bd = (int)(best >> 20);
-    best_dist[o] = bd;
-    best_idx[o] = bd < 256 ? (int)(best & 0xfffff) : -1;
-    second_dist[o] = second;
-}
-
 // partial record: best (dist << 20 | train idx), second dist.  blockIdx.z = problem: query set z at q + z*q_stride,
 // train set z at t + z*t_stride (bytes), partials at z * nchunks * nq.
-// kFused: the chunk workgroup of a (problem, query block) that arrives last folds the block's partials itself (no
-// k_bf_merge launch).  Hand-off (MI355X: per-XCD L2s are not coherent): partials by write-through (sc1) stores, so no
-// release fence; every wave drains them (vmcnt 0), barrier, lane 0 takes a ticket (relaxed agent fetch_add on the
-// block's counter); the ticket nchunks - 1 resets the counter, acquires at agent scope, and after a barrier every wave
-// reads the partials with plain loads.  The counters are zeroed when they are allocated and by each last arriver.
-template <bool kFused>
+// (A one-launch form whose last-arriving chunk workgroup folded the partials measured 17.6 us against 11.65 for tile +
+// merge; removed in round 6.)
 __global__ __launch_bounds__(256) void k_bf_tile(const uint8_t* __restrict__ q, int nq, size_t q_stride, const uint8_t* __restrict__ t,
                                                  int nt, size_t t_stride, int chunk, uint32_t* __restrict__ pbest,
-                                                 int32_t* __restrict__ psecond, int* __restrict__ arrive,
-                                                 int32_t* __restrict__ best_idx, int32_t* __restrict__ best_dist,
-                                                 int32_t* __restrict__ second_dist) {
+                                                 int32_t* __restrict__ psecond) {
     __shared__ uint4 tile[kBfStage * 2];
     const int qi = blockIdx.x * kBfQ + threadIdx.x;
     const int c = blockIdx.y, z = blockIdx.z, nch = gridDim.y;
@@ -130,32 +89,8 @@ __global__ __launch_bounds__(256) void k_bf_tile(const uint8_t* __restrict__ q, 
     }
     if (qi < nq) {
         const size_t o = ((size_t)z * nch + c) * nq + qi;
-        if constexpr (kFused) {                 // write-through (sc1) stores: visible device-wide once drained
-            __hip_atomic_store(pbest + o, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(psecond + o, second, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            pbest[o] = best;
-            psecond[o] = second;
-        }
-    }
-    if constexpr (kFused) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // every wave: its partial stores done
-        __syncthreads();
-        int* flag = reinterpret_cast<int*>(tile);                        // the kernel's one LDS array (free now)
-        if (threadIdx.x == 0) {
-            int* cnt = arrive + (size_t)z * gridDim.x + blockIdx.x;
-            const int last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nch - 1;
-            if (last) {
-                __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");        // drop stale lines of the others' partials
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            flag[0] = last;
-        }
-        __syncthreads();
-        if (!flag[0] || qi >= nq) return;                                 // workgroup-uniform, then per query
-        bf_fold_write(pbest + (size_t)z * nch * nq + qi, psecond + (size_t)z * nch * nq + qi, nq, nch, (size_t)z * nq + qi,
-                      best_idx, best_dist, second_dist);
+        pbest[o] = best;
+        psecond[o] = second;
     }
 }
 
@@ -1371,23 +1306,6 @@ struct Matcher {
     // host calls end synchronised, so the next call may reuse it)
     uint8_t* h_stage = nullptr;
     size_t h_stage_bytes = 0;
-    // arrival counters of the fused all-pairs launch (k_bf_tile<true>): zero at allocation, reset by each last arriver;
-    // grown (device drained first) when a launch needs more (problem, query block) pairs
-    int* d_bf_arrive = nullptr;
-    size_t bf_arrive_n = 0;
-    int bf_counters(size_t n) {
-        if (n <= bf_arrive_n) return ORBX_OK;
-        ORBX_HIP(hipDeviceSynchronize());
-        if (d_bf_arrive) (void)hipFree(d_bf_arrive);
-        d_bf_arrive = nullptr;
-        bf_arrive_n = 0;
-        const size_t nb = std::max<size_t>(n, 256);
-        ORBX_HIP(hipMalloc((void**)&d_bf_arrive, nb * sizeof(int)));
-        ORBX_HIP(hipMemset(d_bf_arrive, 0, nb * sizeof(int)));
-        ORBX_HIP(hipDeviceSynchronize());
-        bf_arrive_n = nb;
-        return ORBX_OK;
-    }
     int stage_host(size_t bytes) {
         if (bytes <= h_stage_bytes) return ORBX_OK;
         const size_t nb = std::max(bytes, h_stage_bytes * 2);     // geometric growth over the old size
@@ -1449,10 +1367,6 @@ static size_t bf_scratch(int nq, int nt, int nprob) {
     const int nch = bf_chunks(nq, nt, nprob);
     return 2 * a256((size_t)nch * nq * nprob * 4) + 256;
 }
-static bool bf_fused() {   // ORBX_BF_FUSED=1: tile + last-arriver fold in one launch (read per call: tests switch it)
-    const char* e = std::getenv("ORBX_BF_FUSED");
-    return e && std::atoi(e) == 1;
-}
 static int bf_launch(Matcher* m, const uint8_t* dq, int nq, size_t qs, const uint8_t* dt, int nt, size_t ts, int nprob, int32_t* bi,
                      int32_t* bd, int32_t* sd, hipStream_t s, void* scratch) {
     if (nt == 0) {
@@ -1466,15 +1380,7 @@ static int bf_launch(Matcher* m, const uint8_t* dq, int nq, size_t qs, const uin
     nch = (nt + chunk - 1) / chunk;
     uint32_t* pb = (uint32_t*)scratch;
     int32_t* ps = (int32_t*)((uint8_t*)scratch + a256((size_t)nch * nq * nprob * 4));
-    if (bf_fused()) {
-        if (int st = m->bf_counters((size_t)qb * nprob)) return st;
-        hipLaunchKernelGGL(k_bf_tile<true>, dim3(qb, nch, nprob), dim3(256), 0, s, dq, nq, qs, dt, nt, ts, chunk, pb, ps,
-                           m->d_bf_arrive, bi, bd, sd);
-        ORBX_HIP(hipGetLastError());
-        return ORBX_OK;
-    }
-    hipLaunchKernelGGL(k_bf_tile<false>, dim3(qb, nch, nprob), dim3(256), 0, s, dq, nq, qs, dt, nt, ts, chunk, pb, ps, nullptr,
-                       nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL(k_bf_tile, dim3(qb, nch, nprob), dim3(256), 0, s, dq, nq, qs, dt, nt, ts, chunk, pb, ps);
     if (nch >= 2 * kBfMergeG)   // a long chunk walk: split it over 8 lanes per query
         hipLaunchKernelGGL(k_bf_merge_g, dim3((nq + 256 / kBfMergeG - 1) / (256 / kBfMergeG), nprob), dim3(256), 0, s, pb, ps,
                            nq, nch, bi, bd, sd);
@@ -1541,7 +1447,6 @@ int orbx_matcher_destroy(orbx_matcher* m) {
     if (m->last_op) (void)hipEventDestroy(m->last_op);
     if (m->scratch) (void)hipFree(m->scratch);
     if (m->h_stage) (void)hipHostFree(m->h_stage);
-    if (m->d_bf_arrive) (void)hipFree(m->d_bf_arrive);
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
     return ORBX_OK;

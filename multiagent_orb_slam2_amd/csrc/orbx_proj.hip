@@ -297,10 +297,15 @@ __device__ int proj_walk(const orbx_proj_params& P, const float* isg, const orbx
 
 // A problem larger than the launch's LDS plan (max_n / max_nq of orbx_proj_search_batch_device) is not searched:
 // its q_idx / q_dist are -1 and *nmatches = -1, never an LDS overrun.  Workgroup-uniform (one problem per workgroup).
-__device__ __forceinline__ bool proj_over_cap(const orbx_proj_problem& pb, int n_cap, int nq_cap, int tid, int T) {
+// When the launch builds the grid (ncell >= 0: orbx_proj_search_grid_batch_device) the problem's grid is written empty
+// (every cell_start 0), so a later search of the same frame walks no stale CSR entries.
+__device__ __forceinline__ bool proj_over_cap(const orbx_proj_problem& pb, int n_cap, int nq_cap, int tid, int T,
+                                              int ncell = -1) {
     if (pb.n <= n_cap && pb.nq <= nq_cap) return false;
     for (int q = tid; q < pb.nq; q += T) { pb.q_idx[q] = -1; pb.q_dist[q] = -1; }
     if (tid == 0 && pb.nmatches) *pb.nmatches = -1;
+    if (ncell >= 0)
+        for (int c = tid; c <= ncell; c += T) const_cast<int32_t*>(pb.cell_start)[c] = 0;
     return true;
 }
 
@@ -378,9 +383,9 @@ __global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(o
                                                        // would be a vector load from the argument buffer per candidate)
     const orbx_proj_problem pb = probs[blockIdx.x];
     const int tid = threadIdx.x, T = blockDim.x, nq = pb.nq, n = pb.n;
-    if (proj_over_cap(pb, n_cap, nq_cap, tid, T)) return;
-    if (tid < 32) isg[tid] = P.inv_sigma2[tid];
     const int ncell = g.cols * g.rows;
+    if (proj_over_cap(pb, n_cap, nq_cap, tid, T, (kLds && grid_counts) ? ncell : -1)) return;
+    if (tid < 32) isg[tid] = P.inv_sigma2[tid];
     char* lp = reinterpret_cast<char*>(psm);
     const int* cs = pb.cell_start;
     const float4* ent = nullptr;

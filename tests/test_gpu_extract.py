@@ -255,39 +255,6 @@ def test_host_api_schedules(gpu, monkeypatch, form):
     ex.close()
 
 
-@pytest.mark.parametrize("rows,cols,nf", [(375, 1242, 2000), (480, 752, 1200), (200, 1000, 1000), (480, 640, 1000)])
-def test_resize_pair_bit_exact(gpu, monkeypatch, rows, cols, nf):
-    """Two pyramid levels per launch (k_resize_pair, ORBX_RESIZE_PAIR=1): every level of every image of a batch, and the
-    keypoints / descriptors, equal the oracle's chained INTER_LINEAR (ORBextractor.cc:1107-1132); the one-image host
-    call too."""
-    import ctypes as C
-
-    import torch
-
-    import multiagent_orb_slam2_amd as pkg
-    from oracle import oracle as O
-    monkeypatch.setenv("ORBX_RESIZE_PAIR", "1")                 # read when the extractor is configured
-    imgs = [S.kitti_like_image(300 + i, rows=rows, cols=cols) for i in range(3)]
-    ex = pkg.ORBextractor(nf, 1.2, 8, 20, 7)
-    kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(np.stack(imgs)).cuda())
-    torch.cuda.synchronize()
-    sizes = ex.level_sizes(rows, cols)
-    for i, img in enumerate(imgs):
-        ref = O.extract(img, nfeatures=nf, want_pyramid=True)
-        for l, (h, w) in enumerate(sizes):
-            a = np.zeros((h, w), np.uint8)
-            assert ex._lib.orbx_extractor_copy_level(ex._h, i, l, a.ctypes.data_as(C.c_void_p), w) == 0
-            assert np.array_equal(a, ref["pyramid"][l]), (i, l)
-        n = int(cnt[i])
-        k = kps[i, :n].cpu().numpy().copy().view(pkg.KP_DTYPE).reshape(-1)
-        assert np.array_equal(k, ref["kps"]) and np.array_equal(desc[i, :n].cpu().numpy(), ref["desc"]), i
-    ex1 = pkg.ORBextractor(nf, 1.2, 8, 20, 7)
-    k1, d1 = ex1(imgs[0])
-    ref = O.extract(imgs[0], nfeatures=nf, want_pyramid=True)
-    assert np.array_equal(k1, ref["kps"]) and np.array_equal(d1, ref["desc"])
-    assert all(np.array_equal(a, b) for a, b in zip(ex1.mvImagePyramid, ref["pyramid"]))
-
-
 def test_extract_pair_equals_two_calls(gpu):
     """orbx_extract_pair (the stereo Frame's two extractions from one thread, Frame.cc:78-81) returns what two
     orbx_extract calls return -- and the oracle -- on repeated frames of two sizes; an empty pair gives nothing, one

@@ -20,16 +20,10 @@ def stereo_pair():
     return dict(kl=kl, dl=dl, kr=kr, dr=dr, scale=ex.GetScaleFactors(), rows=left.shape[0])
 
 
-@pytest.fixture(params=["two_launches", "fused"])
+@pytest.fixture(params=["tile"])
 def bf_mode(request, monkeypatch):
-    """C3 both ways: tile + merge launches, and one launch whose last-arriving chunk workgroup folds the partials
-    (ORBX_BF_FUSED=1, read per call).  The fused form's arrival counters are zeroed at allocation and reset by each
-    last arriver; the r4bo variant lacked the zeroing: a fresh matcher's first launch saw a non-zero counter, no
-    workgroup took the last ticket and the outputs were never written."""
-    if request.param == "fused":
-        monkeypatch.setenv("ORBX_BF_FUSED", "1")
-    else:
-        monkeypatch.delenv("ORBX_BF_FUSED", raising=False)
+    """The C3 all-pairs forms (k_bf_tile + k_bf_merge).  (Round 5's one-launch form with a last-arriver fold was slower
+    and is gone)"""
     return request.param
 
 

@@ -341,3 +341,10 @@ def test_search_with_grid_built_inside(gpu, mode):
             _check(c, got)
         else:                                            # no keypoint in the grid: nothing accepted
             assert int(nm[i]) == 0 and bool((q_idx[i, :len(c["queries"])] == -1).all())
+    # every problem above the launch's bound (max_n < n): not searched, and its grid is written empty
+    cs.fill_(-7)
+    m.proj_search_batch_device(cases[0]["params"], grid, dprobs, cap - 1, nqmax, grid_counts=counts)
+    torch.cuda.synchronize()
+    assert bool((cs == 0).all()) and bool((nm == -1).all())
+    for i, c in enumerate(cases):
+        assert bool((q_idx[i, :len(c["queries"])] == -1).all()), i
