@@ -2034,7 +2034,9 @@ __global__ __launch_bounds__(256) void k_describe_sb(const uint8_t* __restrict__
     // is the row's, and the dword at or above it is at byte 2 (t & ~1) - 2 kSbMagic
     constexpr uint32_t kSbMagic = 0x400000u * (uint32_t)kSbRows + 0x4B400000u - (uint32_t)(kBriefR * kSbRows + kBriefR);
     static_assert((kSbMagic & 1u) == 0u, "row parity from t");
-    const uint32_t hb_base = (uint32_t)(uintptr_t)(hb + sub * kSbSlice) - 2u * kSbMagic;
+    // (an LDS-typed pointer: 32-bit offsets on the LDS address itself; a generic pointer cast to an integer would be
+    // the flat address, whose aperture bits a 32-bit truncation loses)
+    const lds_u8* hsl = (const lds_u8*)(hb + sub * kSbSlice);
     const u16x2 t01 = {18, 34}, t23 = {49, 55}, t45 = {49, 34}, t6 = {18, 0};
     constexpr int kNT = 256 / kLp;
     uint32_t pat[kNT];
@@ -2065,7 +2067,7 @@ __global__ __launch_bounds__(256) void k_describe_sb(const uint8_t* __restrict__
                 // 4-byte-aligned reads from the even row at or above r0 (a 32-bit LDS read off its 4-byte alignment returns
                 // the right bytes but is replayed: r6b, 3.5 ms against 0.67), then the u16 pairs realigned by 16 bits
                 // when r0 is odd (v_alignbit reads the low 5 bits of the shift: t << 4 is 16 or 0)
-                const uint32_t* hp = reinterpret_cast<const uint32_t*>((uintptr_t)(hb_base + 2u * ((uint32_t)t & ~1u)));
+                const lds_u32* hp = (const lds_u32*)(hsl + (2u * ((uint32_t)t & ~1u) - 2u * kSbMagic));
                 const uint32_t d0 = hp[0], d1 = hp[1], d2 = hp[2], d3 = hp[3], sh = (uint32_t)t << 4;
                 uint32_t acc = 0x8000u;
                 acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_alignbit(d1, d0, sh)), t01, acc, false);
