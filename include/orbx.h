@@ -454,7 +454,9 @@ int orbx_proj_search_batch_device(orbx_matcher* m, const orbx_proj_params* param
 /* As orbx_proj_search_batch_device, with each problem's grid built inside its search: problem p's cell_start /
  * cell_idx are OUTPUTS, Frame::AssignFeaturesToGrid (src/Frame.cc:230-245) of its first d_grid_counts[p] (<= n) target
  * keypoints -- the same CSR arrays as orbx_grid_build_device, for later searches of the frame -- so a frame's first
- * search (Tracking::TrackWithMotionModel's, on a fresh Frame) needs no separate grid launch.  Not for
+ * search (Tracking::TrackWithMotionModel's, on a fresh Frame) needs no separate grid launch.  A problem with
+ * d_grid_counts[p] < 0 reads its grid (inputs, as orbx_proj_search_batch_device); problems of one launch that build the
+ * grid of the same keypoint set write identical arrays.  Not for
  * ORBX_PROJ_INIT; ORBX_ERR_UNSUPPORTED when the grid and the keypoints do not fit the launch's LDS plan.  A problem
  * above max_n / max_nq is not searched (as above) and its grid is written empty: every cell_start entry 0. */
 int orbx_proj_search_grid_batch_device(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,

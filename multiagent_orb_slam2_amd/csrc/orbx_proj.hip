@@ -384,7 +384,10 @@ __global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(o
     const orbx_proj_problem pb = probs[blockIdx.x];
     const int tid = threadIdx.x, T = blockDim.x, nq = pb.nq, n = pb.n;
     const int ncell = g.cols * g.rows;
-    if (proj_over_cap(pb, n_cap, nq_cap, tid, T, (kLds && grid_counts) ? ncell : -1)) return;
+    // grid_counts[p] >= 0: this problem's grid is built here from its first grid_counts[p] keypoints and written out;
+    // < 0: it is read (staged) from cell_start / cell_idx as without grid_counts
+    const int gcount = grid_counts ? grid_counts[blockIdx.x] : -1;
+    if (proj_over_cap(pb, n_cap, nq_cap, tid, T, (kLds && gcount >= 0) ? ncell : -1)) return;
     if (tid < 32) isg[tid] = P.inv_sigma2[tid];
     char* lp = reinterpret_cast<char*>(psm);
     const int* cs = pb.cell_start;
@@ -394,11 +397,11 @@ __global__ __launch_bounds__(kProjThreads, kAssign ? 4 : 8) void k_proj_search(o
         lp += ((size_t)(ncell + 1) * 4 + 15) & ~(size_t)15;
         float4* ent_l = reinterpret_cast<float4*>(lp);
         lp += (size_t)16 * n_cap;
-        if (grid_counts) {
+        if (gcount >= 0) {
             // the grid built here (orbx_proj_search_grid_batch_device); scratch: the LDS after the entries, free until the
             // assigning modes' arrays are initialised below (the launch reserves it for the non-assigning ones)
             uint16_t* cof = reinterpret_cast<uint16_t*>(lp);
-            proj_grid_stage(pb, g, min(grid_counts[blockIdx.x], n), ncell, cs_l, ent_l, cof, cof + n_cap, hist);
+            proj_grid_stage(pb, g, min(gcount, n), ncell, cs_l, ent_l, cof, cof + n_cap, hist);
         } else {
             for (int c = tid; c <= ncell; c += T) cs_l[c] = pb.cell_start[c];
             const int ncsr = min(pb.cell_start[ncell], n);

@@ -991,8 +991,9 @@ class ORBmatcher:
     def proj_search_batch_device(self, params: ProjParams, grid: Grid, problems, max_n: int, max_nq: int, stream=None,
                                  grid_counts=None):
         """problems: uint8 device tensor holding n ProjProblem structs (see ProjProblem).  grid_counts: optional (n,)
-        int32 device tensor -- each problem's grid is built inside its search from its first grid_counts[p] target
-        keypoints and written to its cell_start / cell_idx (orbx_proj_search_grid_batch_device)."""
+        int32 device tensor -- problem p's grid is built inside its search from its first grid_counts[p] target
+        keypoints and written to its cell_start / cell_idx (orbx_proj_search_grid_batch_device); a problem with
+        grid_counts[p] < 0 reads its grid from them."""
         import torch
         s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(problems.device).cuda_stream)
         n = problems.numel() // C.sizeof(ProjProblem)

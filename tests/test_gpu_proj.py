@@ -341,6 +341,18 @@ def test_search_with_grid_built_inside(gpu, mode):
             _check(c, got)
         else:                                            # no keypoint in the grid: nothing accepted
             assert int(nm[i]) == 0 and bool((q_idx[i, :len(c["queries"])] == -1).all())
+    # a problem with grid count -1 reads the grid the launch above wrote; the others build theirs again (same arrays)
+    counts_mixed = counts.clone()
+    counts_mixed[0] = -1
+    nm.fill_(-9)
+    owner.fill_(-1)
+    m.proj_search_batch_device(cases[0]["params"], grid, dprobs, cap, nqmax, grid_counts=counts_mixed)
+    torch.cuda.synchronize()
+    for i, c in enumerate(cases[:3]):
+        rcs, rci = O.grid_assign(c["kps"][:ncount[i]], grid)
+        assert np.array_equal(cs[i].cpu().numpy(), rcs), i
+        nq = len(c["queries"])
+        _check(c, (int(nm[i]), q_idx[i, :nq].cpu().numpy(), q_dist[i, :nq].cpu().numpy(), owner[i, :ncount[i]].cpu().numpy()))
     # every problem above the launch's bound (max_n < n): not searched, and its grid is written empty
     cs.fill_(-7)
     m.proj_search_batch_device(cases[0]["params"], grid, dprobs, cap - 1, nqmax, grid_counts=counts)
