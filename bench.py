@@ -119,6 +119,9 @@ def parse():
                     help="N>1 keyframe all-gather in the step: torch (torch.distributed all_gather_into_tensor; RCCL under "
                          "the nccl backend) or native (liborbx's orbx_exchange: its own RCCL communicator, the path a C++ "
                          "MultiAgentServer without torch takes; nccl backend only)")
+    ap.add_argument("--exchange-copy", action="store_true",
+                    help="A/B only: all-gather into a separate buffer that the MapFusion commit copies into the ring "
+                         "(round 5's form) instead of straight into the ring slots")
     ap.add_argument("--emulate-agents", type=int, default=0,
                     help="diagnostics, N=1 only: the keyframe path as rank 0 of this many agents -- this rank's packets stand "
                          "in for every agent's (copied rank-major into the ring as if all-gathered), so the KeyFrameDatabase "
@@ -694,8 +697,15 @@ def c3_bench(pkg, dev, n_problems=64, reps=30):
     tb = torch.from_numpy(np.stack([ts[z % 8] for z in range(n_problems)])).to(dev)
     s = torch.cuda.current_stream(dev)
     out = {}
+    # both forms, the env switch read per call: the matrix-core form (k_bf_mfma, the default) and the VALU tile kernel
+    # (ORBX_BF_MFMA=0, "tile_*"), each checked against the other on the batched outputs
+    prev = os.environ.pop("ORBX_BF_MFMA", None)
     for name, fn, nprob in (("single", lambda: m.bf_match_device(q1, t1, stream=s), 1),
-                            ("batched", lambda: m.bf_match_batch_device(qb, tb, stream=s), n_problems)):
+                            ("batched", lambda: m.bf_match_batch_device(qb, tb, stream=s), n_problems),
+                            ("tile_single", lambda: m.bf_match_device(q1, t1, stream=s), 1),
+                            ("tile_batched", lambda: m.bf_match_batch_device(qb, tb, stream=s), n_problems)):
+        if name.startswith("tile"):
+            os.environ["ORBX_BF_MFMA"] = "0"
         for _ in range(3):
             fn()
         rounds = []                                # median of 5 windows of `reps` launches (one window once read
@@ -713,11 +723,20 @@ def c3_bench(pkg, dev, n_problems=64, reps=30):
         out[name] = {"problems": nprob, "us_per_launch": round(us, 2), "us_per_launch_windows": [round(r, 2) for r in rounds], "matches_per_s": round(nprob / (us * 1e-6), 1),
                      "pair_distances_per_s": round(pairs / (us * 1e-6), 1),
                      "algorithmic_GBps": round(alg / (us * 1e-6) / 1e9, 2)}
-    out["kernels"] = ("k_bf_tile (256 queries per workgroup, one per lane, train rows staged in LDS) + k_bf_merge_g "
-                      "(chunk walk split over 16 lanes per query; k_bf_merge for short walks)")
+    os.environ["ORBX_BF_MFMA"] = "0"
+    ref = [x.cpu() for x in m.bf_match_batch_device(qb, tb, stream=s)]
+    os.environ.pop("ORBX_BF_MFMA", None)
+    got = [x.cpu() for x in m.bf_match_batch_device(qb, tb, stream=s)]
+    if prev is not None:
+        os.environ["ORBX_BF_MFMA"] = prev
+    out["mfma_equals_tile"] = all(bool(torch.equal(a, b)) for a, b in zip(ref, got))
+    out["kernels"] = ("k_bf_mfma (popcount(q & t) by v_mfma_i32_16x16x64_i8 on bits unpacked to 0/1 bytes, 64 queries "
+                      "per workgroup, train rows unpacked into LDS; one chunk per problem writes the outputs directly, "
+                      "else k_bf_merge(_g)); tile_*: k_bf_tile (256 queries per workgroup, one per lane, v_bcnt) + "
+                      "k_bf_merge_g")
     c3p = load_profile("r2w_c3_summary.json")
     if c3p:   # VALU fraction of the tile kernel per launch shape (SQ_INSTS_VALU x 64 / profiled duration / peak)
-        out["valu_frac_profiled"] = {("batched" if e["grid"] >= 524288 else "single"): e["valu_frac"]
+        out["tile_valu_frac_profiled"] = {("batched" if e["grid"] >= 524288 else "single"): e["valu_frac"]
                                      for e in c3p["launches"].values() if e["kernel"] == "k_bf_tile"}
         out["profile"] = "profiles/r2w_c3_summary.json"
     return out
@@ -1039,7 +1058,8 @@ def main():
                             BF, scale, log_sf, inv_sigma2, twc_s, views_s, dev)
     if kfw > 1:
         send = torch.empty((n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
-        gathered = torch.empty((kfw * n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev)
+        # --exchange-copy (A/B only): gather into a separate buffer and let commit copy it into the ring (round 5)
+        gathered = torch.empty((kfw * n_kf, engine.packet_bytes), dtype=torch.uint8, device=dev) if args.exchange_copy else None
     frame_no = [chunk.start]
     n_step = [0]
 
@@ -1148,11 +1168,14 @@ def main():
             engine.step(kps, desc, cnt, kf_rows, frame_no[0] + kf_off, KF_EVERY, depth=depth, stream=kf_stream)
         else:
             engine.pack(kps, desc, cnt, kf_rows, frame_no[0] + kf_off, KF_EVERY, depth=depth, send=send, stream=kf_stream)
+            # the all-gather lands in the ring slots pack() reserved (engine.exchange_view()), and commit takes them in
+            # place; with --exchange-copy through a separate buffer that commit copies into the ring
+            dst = gathered if gathered is not None else engine.exchange_view()
             with torch.cuda.stream(kf_stream):
                 if world > 1:
-                    exchange.exchange(send, out=gathered)
+                    exchange.exchange(send, out=dst)
                 else:                                  # --emulate-agents: every agent's block is this rank's packets
-                    gathered.view(kfw, n_kf, -1).copy_(send.unsqueeze(0).expand(kfw, -1, -1))
+                    dst.view(kfw, n_kf, -1).copy_(send.unsqueeze(0).expand(kfw, -1, -1))
             engine.commit(gathered, stream=kf_stream)
         if time_stereo:
             e3 = torch.cuda.Event(enable_timing=True)

@@ -306,6 +306,29 @@ __global__ __launch_bounds__(256) void k_resize4(uint8_t* __restrict__ pyr, size
     resize4_item(pyr, pyr_stride, src, src_step, src_istride, sw, dst_off, dw, dh, t, strip, band, img);
 }
 
+// The small levels of the chain in one launch: one 256-thread workgroup per image, no LDS, computes
+// levels l0 .. n-1 in order from the pyramid in memory -- its 4 waves walk level l's (strip, band) items as k_resize4's
+// waves do, then a workgroup barrier (the level's rows, written through to L2 by this CU, are read by the next level's
+// waves of the same workgroup) -- so the chain's upper levels are one launch instead of n - l0 dependent ones.
+struct TailLevel { ResizeVec t; int sw, src_off, dst_off, dw, dh, nstrips, nbands; };
+constexpr int kTailMax = 6;
+struct TailArgs { TailLevel lv[kTailMax]; int n; };
+__global__ __launch_bounds__(256) void k_resize_tail(uint8_t* __restrict__ pyr, size_t pyr_stride, TailArgs A, int batch) {
+    const int img = blockIdx.x;
+    if (img >= batch) return;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (int k = 0; k < A.n; ++k) {
+        const TailLevel& L = A.lv[k];
+        const int items = L.nstrips * L.nbands;
+        for (int it = w; it < items; it += 4) {
+            const int band = it / L.nstrips, strip = it - band * L.nstrips;
+            resize4_item(pyr, pyr_stride, pyr + L.src_off, (size_t)L.sw, pyr_stride, L.sw, L.dst_off, L.dw, L.dh, L.t, strip,
+                         band, img);
+        }
+        __syncthreads();
+    }
+}
+
 // FAST-9/16 corner score in closed form.  For pixel value v and circle values p_k (Bresenham r=3,
 // OpenCV order), with d_k = v - p_k:  m_dark = max over the 16 arcs of 9 of min d, m_bright = max
 // over arcs of min(-d).  OpenCV's cornerScore<16> returns max(t, m_dark, m_bright) - 1 and the pixel
@@ -2236,6 +2259,7 @@ struct Extractor {
     // k_describe_sb (blur at the BRIEF sample points) instead of k_blur7 + k_describe_m: no blurred pyramid is kept
     // (ORBX_DESC_SB, read at create)
     bool desc_sb = false;
+    int resize_tail = 0;              // ORBX_RESIZE_TAIL=l (>= 2): levels l .. n-1 in one k_resize_tail launch
     uint8_t* d_blur_diag = nullptr;   // one image's blurred pyramid, made on demand by orbx_extractor_copy_blurred_level
     int desc_sets = 2;                // call k + 1's blur and DistributeOctTree write the other set (ORBX_DESC_SETS=1: one)
     unsigned long long dcalls = 0;    // while call k's describe reads its own (no wait on that describe)
@@ -2767,6 +2791,22 @@ static int run_batch(Extractor* e, const uint8_t* d_images, int batch, size_t st
             const uint8_t* src = (l == 1) ? d_images : e->d_pyr + e->lv[l - 1].pyr_off;
             const size_t sstep = (l == 1) ? step : (size_t)e->lv[l - 1].w, sis = (l == 1) ? istride : ps;
             const LevelDev& L = e->lv[l];
+            if (e->resize_tail > 1 && l == e->resize_tail && nl - l <= kTailMax) {
+                bool ok = true;
+                for (int k = l; k < nl; ++k) ok = ok && e->rvec[k].groups > 0 && e->lv[k - 1].w >= 8;
+                if (ok) {                                           // levels l .. nl-1 in one launch
+                    TailArgs A{};
+                    A.n = nl - l;
+                    for (int k = l; k < nl; ++k) {
+                        TailLevel& T = A.lv[k - l];
+                        T.t = e->rvec[k]; T.sw = e->lv[k - 1].w; T.src_off = e->lv[k - 1].pyr_off; T.dst_off = e->lv[k].pyr_off;
+                        T.dw = e->lv[k].w; T.dh = e->lv[k].h;
+                        T.nstrips = (T.dw + kResizeStrip - 1) / kResizeStrip; T.nbands = (T.dh + kResizeBand - 1) / kResizeBand;
+                    }
+                    hipLaunchKernelGGL(k_resize_tail, dim3(batch), dim3(256), 0, s, e->d_pyr, ps, A, batch);
+                    break;
+                }
+            }
             if (e->rvec[l].groups > 0) {
                 const int nstrips = (L.w + kResizeStrip - 1) / kResizeStrip, nbands = (L.h + kResizeBand - 1) / kResizeBand;
                 const int nwg = (nstrips * nbands * batch + 3) / 4;
@@ -2967,6 +3007,7 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     if (const char* sw = std::getenv("ORBX_DEBUG_SKIP_DESC_WAIT")) e->dbg_skip_desc_wait = std::atoi(sw) != 0;
     if (const char* qo = std::getenv("ORBX_QT_OUT")) e->qt_out = std::atoi(qo) != 0;
     if (const char* sb = std::getenv("ORBX_DESC_SB")) e->desc_sb = std::atoi(sb) != 0;
+    if (const char* rt = std::getenv("ORBX_RESIZE_TAIL")) e->resize_tail = std::atoi(rt);
     if (int st = check_constants(e)) {
         orbx_extractor_destroy(e);
         return st;

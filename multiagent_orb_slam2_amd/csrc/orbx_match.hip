@@ -189,6 +189,131 @@ __global__ __launch_bounds__(256) void k_bf_empty(int n, int32_t* __restrict__ b
 }
 
 // ---------------------------------------------------------------------------------------------
+// all-pairs brute force on the matrix cores (the default; ORBX_BF_MFMA=0: k_bf_tile)
+// ---------------------------------------------------------------------------------------------
+// popcount(q ^ t) = |q| + |t| - 2 popcount(q & t), and popcount(q & t) is the dot product of the two descriptors' bits
+// unpacked to 0 / 1 bytes: a 16 x 16 tile of (query, train) pairs is 4 v_mfma_i32_16x16x64_i8 over K = 256 bits.  A
+// workgroup takes 64 queries (16 per wave, unpacked once into the A operands) against a chunk of the train set, staged
+// 64 rows at a time: the 256 threads unpack the rows' bits into LDS (256 B per row, padded to kMxStride so the 16
+// lanes of a B read sit on distinct banks) with |t| + 256 beside them.  Lane (g, n) of a tile holds train row n and
+// query rows 4 g .. 4 g + 3 (the C map); per pair e = |t| + 256 - 2 acc = d - |q| + 256 (|q| is constant per query,
+// so e orders the pairs of a query as d does) and the key (e << 20 | train index) runs through the best / second rule
+// as k_bf_tile's (best = min key; second = min over the keys that are not the best, as keys: its distance is the
+// second order statistic).  At the end the 16 lanes of a row group merge their pairs by shuffles, and the keys go back
+// to distances with |q|: the chunk partials of k_bf_merge, or the outputs directly when the train set is one chunk.
+// Bits are labelled alike on both operands: element e of lane group g of K-step s is bit 64 s + 16 g + e.
+constexpr int kMxQ = 64, kMxRows = 64, kMxStride = 272;
+typedef int mx_v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t mx_nibble(uint32_t v, int j) {   // bits 4 j .. 4 j + 3 of v as four 0 / 1 bytes
+    return (((v >> (4 * j)) & 15u) * 0x00204081u) & 0x01010101u;
+}
+__global__ __launch_bounds__(256) void k_bf_mfma(const uint8_t* __restrict__ q, int nq, size_t q_stride,
+                                                 const uint8_t* __restrict__ t, int nt, size_t t_stride, int chunk,
+                                                 uint32_t* __restrict__ pbest, int32_t* __restrict__ psecond,
+                                                 int32_t* __restrict__ best_idx, int32_t* __restrict__ best_dist,
+                                                 int32_t* __restrict__ second_dist) {
+    __shared__ __attribute__((aligned(16))) uint8_t tb[kMxRows * kMxStride];
+    __shared__ int tsum[kMxRows];
+    const int w = threadIdx.x >> 6, l = lane_id(), g = l >> 4, n = l & 15;
+    const int c = blockIdx.y, z = blockIdx.z, nch = gridDim.y;
+    q += (size_t)z * q_stride;
+    t += (size_t)z * t_stride;
+    const int qb = blockIdx.x * kMxQ + 16 * w;                   // the wave's 16 queries
+    const int t0 = c * chunk, t1 = min(nt, t0 + chunk);
+    mx_v4i a[4];
+    {
+        uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
+        if (qb + n < nq) load_desc(q + 32 * (size_t)(qb + n), d0, d1);
+        const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {                           // bits 64 s + 16 g .. + 15: half g & 1 of dword 2 s + g / 2
+            const uint32_t word = (g >> 1) ? dw[2 * s + 1] : dw[2 * s];
+            const uint32_t h = (g & 1) ? word >> 16 : word & 0xffffu;
+            a[s] = mx_v4i{(int)mx_nibble(h, 0), (int)mx_nibble(h, 1), (int)mx_nibble(h, 2), (int)mx_nibble(h, 3)};
+        }
+    }
+    uint32_t best[4], second[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) best[j] = second[j] = 0xffffffffu;
+    for (int s0 = t0; s0 < t1; s0 += kMxRows) {
+        const int cnt = min(kMxRows, t1 - s0);
+        __syncthreads();
+        {   // thread -> (row r, quarter qq): descriptor bytes 8 qq .. 8 qq + 7 -> unpacked bytes 64 qq .. 64 qq + 63
+            const int r = threadIdx.x >> 2, qq = threadIdx.x & 3;
+            uint32_t v0 = 0, v1 = 0;
+            if (r < cnt) {
+                const uint2 v = *reinterpret_cast<const uint2*>(t + 32 * (size_t)(s0 + r) + 8 * qq);
+                v0 = v.x; v1 = v.y;
+            }
+            int pc = popc32(v0) + popc32(v1);
+            pc += __builtin_amdgcn_update_dpp(0, pc, 0xB1, 0xF, 0xF, false);    // quad_perm 1,0,3,2
+            pc += __builtin_amdgcn_update_dpp(0, pc, 0x4E, 0xF, 0xF, false);    // quad_perm 2,3,0,1
+            uint4* dst = reinterpret_cast<uint4*>(tb + r * kMxStride + 64 * qq);
+            dst[0] = make_uint4(mx_nibble(v0, 0), mx_nibble(v0, 1), mx_nibble(v0, 2), mx_nibble(v0, 3));
+            dst[1] = make_uint4(mx_nibble(v0, 4), mx_nibble(v0, 5), mx_nibble(v0, 6), mx_nibble(v0, 7));
+            dst[2] = make_uint4(mx_nibble(v1, 0), mx_nibble(v1, 1), mx_nibble(v1, 2), mx_nibble(v1, 3));
+            dst[3] = make_uint4(mx_nibble(v1, 4), mx_nibble(v1, 5), mx_nibble(v1, 6), mx_nibble(v1, 7));
+            // rows past the chunk: e = 1023 > any real e (<= 512), never a best; as a second it clamps to 256 below
+            if (qq == 0) tsum[r] = r < cnt ? pc + 256 : 1023;
+        }
+        __syncthreads();
+        for (int tt = 0; tt < kMxRows / 16; ++tt) {
+            if (16 * tt >= cnt) break;                           // workgroup-uniform
+            const int row = 16 * tt + n;
+            mx_v4i acc = {0, 0, 0, 0};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const mx_v4i b = *reinterpret_cast<const mx_v4i*>(tb + row * kMxStride + 64 * s + 16 * g);
+                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], b, acc, 0, 0, 0);
+            }
+            const int ts = tsum[row];
+            const uint32_t tidx = (uint32_t)(s0 + row);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t key = ((uint32_t)(ts - 2 * acc[j]) << 20) | tidx;
+                const uint32_t hi = max(best[j], key);
+                best[j] = min(best[j], key);
+                second[j] = min(second[j], hi);
+            }
+        }
+    }
+    // the 16 lanes of a row group (one train column each) merge: (b1, s1) + (b2, s2) = (min b, min(s1, s2, max b))
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t ob = (uint32_t)__shfl_xor((int)best[j], o, 16), os = (uint32_t)__shfl_xor((int)second[j], o, 16);
+            second[j] = min(min(second[j], os), max(best[j], ob));
+            best[j] = min(best[j], ob);
+        }
+    }
+    if (n >= 4) return;
+    const int j = n, qi = qb + 4 * g + j;                        // lane n < 4 of row group g writes row 4 g + n
+    if (qi >= nq) return;
+    uint32_t bk = best[0], sk = second[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) { bk = j == k ? best[k] : bk; sk = j == k ? second[k] : sk; }
+    uint4 d0, d1;
+    load_desc(q + 32 * (size_t)qi, d0, d1);
+    const int nq1 = popc32(d0.x) + popc32(d0.y) + popc32(d0.z) + popc32(d0.w) + popc32(d1.x) + popc32(d1.y) +
+                    popc32(d1.z) + popc32(d1.w);
+    // back to distances; the reference's initial (256, 256) with strict < : a best needs d < 256, distances clamp at 256
+    const int db = bk == 0xffffffffu ? 256 : (int)(bk >> 20) - 256 + nq1;
+    const int ds = sk == 0xffffffffu ? 256 : min(256, (int)(sk >> 20) - 256 + nq1);
+    const bool found = db < 256;
+    if (pbest) {
+        const size_t o = ((size_t)z * nch + c) * nq + qi;
+        pbest[o] = found ? ((uint32_t)db << 20) | (bk & 0xfffffu) : (256u << 20);
+        psecond[o] = found ? ds : 256;
+    } else {
+        const size_t o = (size_t)z * nq + qi;
+        best_dist[o] = found ? db : 256;
+        best_idx[o] = found ? (int)(bk & 0xfffffu) : -1;
+        second_dist[o] = found ? ds : 256;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // stereo band match
 // ---------------------------------------------------------------------------------------------
 struct StereoArgs {
@@ -1363,14 +1488,49 @@ static int bf_chunks(int nq, int nt, int nprob) {
     const int want = (bf_target_wgs() + qb * nprob - 1) / (qb * nprob);
     return std::max(1, std::min(want, (nt + 31) / 32));
 }
+// k_bf_mfma: 64 queries per workgroup, chunks of >= 64 train rows (one LDS stage)
+static int bf_chunks_mx(int nq, int nt, int nprob) {
+    const int qb = (nq + kMxQ - 1) / kMxQ;
+    const int want = (bf_target_wgs() + qb * nprob - 1) / (qb * nprob);
+    return std::max(1, std::min(want, (nt + kMxRows - 1) / kMxRows));
+}
 static size_t bf_scratch(int nq, int nt, int nprob) {
-    const int nch = bf_chunks(nq, nt, nprob);
+    const int nch = std::max(bf_chunks(nq, nt, nprob), bf_chunks_mx(nq, nt, nprob));
     return 2 * a256((size_t)nch * nq * nprob * 4) + 256;
+}
+// The matrix-core form is the default (r6h, 64 problems of 2000 x 2000 per launch: 108.5 us against 171.0 for k_bf_tile
+// + merge; one problem: 11.4-12.0 against 11.8-11.9, launch-bound); ORBX_BF_MFMA=0 selects the tile form (read per call:
+// the tests run both).
+static bool bf_mfma() {
+    const char* e = std::getenv("ORBX_BF_MFMA");
+    return !e || std::atoi(e) != 0;
 }
 static int bf_launch(Matcher* m, const uint8_t* dq, int nq, size_t qs, const uint8_t* dt, int nt, size_t ts, int nprob, int32_t* bi,
                      int32_t* bd, int32_t* sd, hipStream_t s, void* scratch) {
     if (nt == 0) {
         hipLaunchKernelGGL(k_bf_empty, dim3(((size_t)nq * nprob + 255) / 256), dim3(256), 0, s, nq * nprob, bi, bd, sd);
+        ORBX_HIP(hipGetLastError());
+        return ORBX_OK;
+    }
+    if (bf_mfma()) {
+        const int qb = (nq + kMxQ - 1) / kMxQ;
+        int nch = bf_chunks_mx(nq, nt, nprob);
+        const int chunk = (nt + nch - 1) / nch;
+        nch = (nt + chunk - 1) / chunk;
+        uint32_t* pb = (uint32_t*)scratch;
+        int32_t* ps = (int32_t*)((uint8_t*)scratch + a256((size_t)nch * nq * nprob * 4));
+        if (nch == 1) {                                            // one chunk: the outputs directly, no merge launch
+            hipLaunchKernelGGL(k_bf_mfma, dim3(qb, 1, nprob), dim3(256), 0, s, dq, nq, qs, dt, nt, ts, chunk, nullptr, nullptr,
+                               bi, bd, sd);
+        } else {
+            hipLaunchKernelGGL(k_bf_mfma, dim3(qb, nch, nprob), dim3(256), 0, s, dq, nq, qs, dt, nt, ts, chunk, pb, ps,
+                               nullptr, nullptr, nullptr);
+            if (nch >= 2 * kBfMergeG)
+                hipLaunchKernelGGL(k_bf_merge_g, dim3((nq + 256 / kBfMergeG - 1) / (256 / kBfMergeG), nprob), dim3(256), 0, s,
+                                   pb, ps, nq, nch, bi, bd, sd);
+            else
+                hipLaunchKernelGGL(k_bf_merge, dim3((nq + 255) / 256, nprob), dim3(256), 0, s, pb, ps, nq, nch, bi, bd, sd);
+        }
         ORBX_HIP(hipGetLastError());
         return ORBX_OK;
     }

@@ -1283,6 +1283,21 @@ def packet_layout(capacity: int):
     return dict(zip(PACKET_FIELDS, list(off))), nb.value
 
 
+class _DeviceRegion:
+    """Device memory owned by liborbx, exposed to torch without a copy (__cuda_array_interface__, which torch's ROCm
+    build reads for HIP device pointers); 'owner' stays referenced as long as the tensor's storage is alive."""
+
+    def __init__(self, ptr: int, shape, owner):
+        self.owner = owner
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": "|u1", "data": (int(ptr), False),
+                                         "version": 2, "strides": None}
+
+
+def _device_view(ptr: int, shape, device: int, owner):
+    import torch
+    return torch.as_tensor(_DeviceRegion(ptr, shape, owner), device=torch.device("cuda", device))
+
+
 def _stream_ptr(stream, device):
     import torch
     return C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(device).cuda_stream)
@@ -1371,11 +1386,19 @@ class KeyframeFusionEngine:
                                                  None if send is None else _tp(send), C.byref(dst), C.byref(snd),
                                                  _stream_ptr(stream, kps.device)))
         self._pending = n
+        self._dst = dst.value
         return n
 
+    def exchange_view(self):
+        """The ring slots the last pack() reserved for this step's world * n packets (rank-major), as a (world*n, P)
+        uint8 device tensor aliasing them (orbx_fusion_pack_device's d_exchange_dst): all-gather into it, then
+        commit(None) -- no gathered buffer and no copy into the ring (70 MB per step at 8 agents)."""
+        return _device_view(self._dst, (self.world * self._pending, self.packet_bytes), self.device, self)
+
     def commit(self, exchanged=None, outputs=None, stream=None):
-        """Phase 2.  exchanged: (world*n, P) uint8 tensor of the gathered packets (world > 1).  outputs: optional
-        (pairs (n*k, 2), match12 (n*k, cap), nmatches (n*k,)) int32 tensors to fill."""
+        """Phase 2.  exchanged: (world*n, P) uint8 tensor of the gathered packets when they were gathered elsewhere
+        (world > 1), None when they are already in the ring (exchange_view).  outputs: optional (pairs (n*k, 2),
+        match12 (n*k, cap), nmatches (n*k,)) int32 tensors to fill."""
         o = outputs or (None, None, None)
         dev = exchanged.device if exchanged is not None else (o[0].device if o[0] is not None else None)
         _check(self._lib.orbx_fusion_commit_device(self._h, None if exchanged is None else _tp(exchanged),

@@ -84,7 +84,9 @@ def test_native_fusion_single_agent_vs_oracle(gpu):
 
 def test_native_fusion_two_agents_one_gpu(gpu):
     """Two engines (agents 0 and 1, world 2) on one GPU; the test all-gathers their packets (rank-major) and hands
-    them to phase 2, as the bench does with torch.distributed at N > 1."""
+    them to phase 2, as the bench does with torch.distributed at N > 1: engine 0 takes them from a separate buffer
+    (commit copies them into its ring), engine 1 has them written straight into the ring slots its pack reserved
+    (exchange_view, a zero-copy view) and commits in place -- the two rings must agree."""
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O
     kps, desc, cnt, depth, cap = _inputs(91, 16)
@@ -106,7 +108,13 @@ def test_native_fusion_two_agents_one_gpu(gpu):
         outs = []
         for r in range(W):
             o = eng[r].new_outputs(n)
-            eng[r].commit(gathered, o)
+            if r == 0:
+                eng[r].commit(gathered, o)
+            else:
+                view = eng[r].exchange_view()
+                assert view.shape == gathered.shape and view.data_ptr() != gathered.data_ptr()
+                view.copy_(gathered)
+                eng[r].commit(None, o)
             outs.append(o)
         torch.cuda.synchronize()
         rings = [e.read_ring() for e in eng]

@@ -20,10 +20,12 @@ def stereo_pair():
     return dict(kl=kl, dl=dl, kr=kr, dr=dr, scale=ex.GetScaleFactors(), rows=left.shape[0])
 
 
-@pytest.fixture(params=["tile"])
+@pytest.fixture(params=["tile", "mfma"])
 def bf_mode(request, monkeypatch):
-    """The C3 all-pairs forms (k_bf_tile + k_bf_merge).  (Round 5's one-launch form with a last-arriver fold was slower
-    and is gone)"""
+    """C3 both ways: the VALU tile kernel (k_bf_tile + k_bf_merge, ORBX_BF_MFMA=0) and the matrix-core form (k_bf_mfma,
+    the default: bits unpacked to 0 / 1 bytes, popcount(q & t) by v_mfma_i32_16x16x64_i8; read per call).  (Round 5's one-launch form
+    with a last-arriver fold was slower and is gone)"""
+    monkeypatch.setenv("ORBX_BF_MFMA", "1" if request.param == "mfma" else "0")
     return request.param
 
 
