@@ -1099,7 +1099,9 @@ int orbx_grid_build_device(orbx_matcher* m, orbx_grid grid, const orbx_keypoint*
 static int proj_search_batch(orbx_matcher* m, const orbx_proj_params* params, orbx_grid grid,
                              const orbx_proj_problem* d_problems, int n_problems, int max_n, int max_nq,
                              const int32_t* d_grid_counts, void* stream) {
-    ORBX_REQUIRE(m && params && d_problems && n_problems >= 0 && max_n >= 0 && max_nq >= 0, ORBX_ERR_ARG, "bad argument");
+    // (an empty batch may pass a NULL problem array -- an empty torch slice's data pointer: r5bab failed on exactly that)
+    ORBX_REQUIRE(m && params && (d_problems || n_problems == 0) && n_problems >= 0 && max_n >= 0 && max_nq >= 0, ORBX_ERR_ARG,
+                 "bad argument");
     int st = grid_check(grid);
     if (st) return st;
     const orbx_proj_params& P = *params;

@@ -80,6 +80,11 @@ def test_proj_search_empty(gpu):
     assert got[0] == 0 and len(got[1]) == 0 and (got[3] == -1).all()
     got = m.proj_search(c["params"], c["grid"], c["queries"], c["qdesc"], c["kps"][:0], c["desc"][:0])
     assert got[0] == 0 and (got[1] == -1).all()
+    # an empty problem batch (an empty slice's data pointer may be NULL: r5bab) is a no-op, not a bad argument
+    import torch
+    m.proj_search_batch_device(c["params"], c["grid"], torch.empty((0,), dtype=torch.uint8, device="cuda"), 64, 64)
+    assert pkg.orbx.load_library().orbx_proj_search_batch_device(m._h, C.byref(c["params"]), c["grid"], None, 0, 64, 64,
+                                                                  None) == 0
 
 
 def test_grid_build_clustered_and_empty(gpu):
