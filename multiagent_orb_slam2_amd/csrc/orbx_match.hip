@@ -193,16 +193,22 @@ __global__ __launch_bounds__(256) void k_bf_empty(int n, int32_t* __restrict__ b
 // ---------------------------------------------------------------------------------------------
 // popcount(q ^ t) = |q| + |t| - 2 popcount(q & t), and popcount(q & t) is the dot product of the two descriptors' bits
 // unpacked to 0 / 1 bytes: a 16 x 16 tile of (query, train) pairs is 4 v_mfma_i32_16x16x64_i8 over K = 256 bits.  A
-// workgroup takes 64 queries (16 per wave, unpacked once into the A operands) against a chunk of the train set, staged
+// workgroup takes 64 kMxQt queries (16 kMxQt per wave, unpacked once into the A operands) against a chunk of the train set, staged
 // 64 rows at a time: the 256 threads unpack the rows' bits into LDS (256 B per row, padded to kMxStride so the 16
 // lanes of a B read sit on distinct banks) with |t| + 256 beside them.  Lane (g, n) of a tile holds train row n and
 // query rows 4 g .. 4 g + 3 (the C map); per pair e = |t| + 256 - 2 acc = d - |q| + 256 (|q| is constant per query,
-// so e orders the pairs of a query as d does) and the key (e << 20 | train index) runs through the best / second rule
-// as k_bf_tile's (best = min key; second = min over the keys that are not the best, as keys: its distance is the
-// second order statistic).  At the end the 16 lanes of a row group merge their pairs by shuffles, and the keys go back
+// so e orders the pairs of a query as d does) and the key ((1024 - e) << 20 | 0xfffff - train index) runs through the
+// best / second rule as k_bf_tile's, as maxima (best = max key; second = max over the keys that are not the best: its
+// distance is the second order statistic).  At the end the 16 lanes of a row group merge their pairs by shuffles, and the keys go back
 // to distances with |q|: the chunk partials of k_bf_merge, or the outputs directly when the train set is one chunk.
+// A wave holds kMxQt query tiles, so each B fragment it reads from LDS feeds kMxQt MFMAs (the LDS reads and the
+// unpack stores per pair were the limit at one tile per wave: 64 queries per workgroup, 112 us for 64 problems).
 // Bits are labelled alike on both operands: element e of lane group g of K-step s is bit 64 s + 16 g + e.
-constexpr int kMxQ = 64, kMxRows = 64, kMxStride = 272;
+#ifndef ORBX_MX_QT
+#define ORBX_MX_QT 2
+#endif
+constexpr int kMxQt = ORBX_MX_QT;                 // 16-query tiles per wave: each B fragment read feeds kMxQt MFMAs
+constexpr int kMxQ = 64 * kMxQt, kMxRows = 64, kMxStride = 272;
 typedef int mx_v4i __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t mx_nibble(uint32_t v, int j) {   // bits 4 j .. 4 j + 3 of v as four 0 / 1 bytes
     return (((v >> (4 * j)) & 15u) * 0x00204081u) & 0x01010101u;
@@ -218,33 +224,41 @@ __global__ __launch_bounds__(256) void k_bf_mfma(const uint8_t* __restrict__ q, 
     const int c = blockIdx.y, z = blockIdx.z, nch = gridDim.y;
     q += (size_t)z * q_stride;
     t += (size_t)z * t_stride;
-    const int qb = blockIdx.x * kMxQ + 16 * w;                   // the wave's 16 queries
+    const int qb = blockIdx.x * kMxQ + 16 * kMxQt * w;          // the wave's kMxQt x 16 queries
     const int t0 = c * chunk, t1 = min(nt, t0 + chunk);
-    mx_v4i a[4];
-    {
+    mx_v4i a[kMxQt][4];
+#pragma unroll
+    for (int u = 0; u < kMxQt; ++u) {
         uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
-        if (qb + n < nq) load_desc(q + 32 * (size_t)(qb + n), d0, d1);
+        const int qi = qb + 16 * u + n;
+        if (qi < nq) load_desc(q + 32 * (size_t)qi, d0, d1);
         const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {                           // bits 64 s + 16 g .. + 15: half g & 1 of dword 2 s + g / 2
             const uint32_t word = (g >> 1) ? dw[2 * s + 1] : dw[2 * s];
             const uint32_t h = (g & 1) ? word >> 16 : word & 0xffffu;
-            a[s] = mx_v4i{(int)mx_nibble(h, 0), (int)mx_nibble(h, 1), (int)mx_nibble(h, 2), (int)mx_nibble(h, 3)};
+            a[u][s] = mx_v4i{(int)mx_nibble(h, 0), (int)mx_nibble(h, 1), (int)mx_nibble(h, 2), (int)mx_nibble(h, 3)};
         }
     }
-    uint32_t best[4], second[4];
+    // keys run as maxima: key = ((1024 - e) << 20) | (0xfffff - index), e = |t| + 256 - 2 acc, so the largest key is the
+    // smallest distance with the lowest index; 0 = none (a real key is >= 1 << 20)
+    uint32_t best[kMxQt][4], second[kMxQt][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) best[j] = second[j] = 0xffffffffu;
+    for (int u = 0; u < kMxQt; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) best[u][j] = second[u][j] = 0u;
+    // thread -> (row r, quarter qq) of a stage: descriptor bytes 8 qq .. 8 qq + 7 -> unpacked bytes 64 qq .. 64 qq + 63.
+    // The next stage's bytes are loaded while this stage's tiles run.
+    const int r = threadIdx.x >> 2, qq = threadIdx.x & 3;
+    uint2 nx = make_uint2(0, 0);
+    if (t0 + r < t1) nx = *reinterpret_cast<const uint2*>(t + 32 * (size_t)(t0 + r) + 8 * qq);
     for (int s0 = t0; s0 < t1; s0 += kMxRows) {
         const int cnt = min(kMxRows, t1 - s0);
+        const uint32_t v0 = nx.x, v1 = nx.y;
+        nx = make_uint2(0, 0);                                   // rows past the chunk unpack to zeros
+        if (s0 + kMxRows + r < t1) nx = *reinterpret_cast<const uint2*>(t + 32 * (size_t)(s0 + kMxRows + r) + 8 * qq);
         __syncthreads();
-        {   // thread -> (row r, quarter qq): descriptor bytes 8 qq .. 8 qq + 7 -> unpacked bytes 64 qq .. 64 qq + 63
-            const int r = threadIdx.x >> 2, qq = threadIdx.x & 3;
-            uint32_t v0 = 0, v1 = 0;
-            if (r < cnt) {
-                const uint2 v = *reinterpret_cast<const uint2*>(t + 32 * (size_t)(s0 + r) + 8 * qq);
-                v0 = v.x; v1 = v.y;
-            }
+        {
             int pc = popc32(v0) + popc32(v1);
             pc += __builtin_amdgcn_update_dpp(0, pc, 0xB1, 0xF, 0xF, false);    // quad_perm 1,0,3,2
             pc += __builtin_amdgcn_update_dpp(0, pc, 0x4E, 0xF, 0xF, false);    // quad_perm 2,3,0,1
@@ -260,55 +274,73 @@ __global__ __launch_bounds__(256) void k_bf_mfma(const uint8_t* __restrict__ q, 
         for (int tt = 0; tt < kMxRows / 16; ++tt) {
             if (16 * tt >= cnt) break;                           // workgroup-uniform
             const int row = 16 * tt + n;
-            mx_v4i acc = {0, 0, 0, 0};
+            mx_v4i b[4];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const mx_v4i b = *reinterpret_cast<const mx_v4i*>(tb + row * kMxStride + 64 * s + 16 * g);
-                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], b, acc, 0, 0, 0);
-            }
-            const int ts = tsum[row];
-            const uint32_t tidx = (uint32_t)(s0 + row);
+            for (int s = 0; s < 4; ++s) b[s] = *reinterpret_cast<const mx_v4i*>(tb + row * kMxStride + 64 * s + 16 * g);
+            // key = acc * 2^21 + k0 with k0 = ((1024 - |t| - 256) << 20) | (0xfffff - index): one v_mad_u32_u24 per pair
+            // (acc <= 256; emitted by the compiler, which also pads the MFMA -> VALU read of acc)
+            const uint32_t k0 = ((uint32_t)(1024 - tsum[row]) << 20) | (uint32_t)(0xfffff - (s0 + row));
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t key = ((uint32_t)(ts - 2 * acc[j]) << 20) | tidx;
-                const uint32_t hi = max(best[j], key);
-                best[j] = min(best[j], key);
-                second[j] = min(second[j], hi);
+            for (int u = 0; u < kMxQt; ++u) {
+                mx_v4i acc = {0, 0, 0, 0};
+#pragma unroll
+                for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[u][s], b[s], acc, 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t key = __umul24((uint32_t)acc[j], 1u << 21) + k0;
+                    // best >= second always, so max(second, min(best, key)) is the median of the three (asm: the
+                    // compiler does not form v_med3_u32 from variables; its operands are VALU results, no MFMA hazard)
+                    uint32_t m3;
+                    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m3) : "v"(best[u][j]), "v"(key), "v"(second[u][j]));
+                    second[u][j] = m3;
+                    best[u][j] = max(best[u][j], key);
+                }
             }
         }
     }
-    // the 16 lanes of a row group (one train column each) merge: (b1, s1) + (b2, s2) = (min b, min(s1, s2, max b))
+    // the 16 lanes of a row group (one train column each) merge: (b1, s1) + (b2, s2) = (max b, max(s1, s2, min b))
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t ob = (uint32_t)__shfl_xor((int)best[j], o, 16), os = (uint32_t)__shfl_xor((int)second[j], o, 16);
-            second[j] = min(min(second[j], os), max(best[j], ob));
-            best[j] = min(best[j], ob);
-        }
-    }
-    if (n >= 4) return;
-    const int j = n, qi = qb + 4 * g + j;                        // lane n < 4 of row group g writes row 4 g + n
-    if (qi >= nq) return;
-    uint32_t bk = best[0], sk = second[0];
+        for (int u = 0; u < kMxQt; ++u)
 #pragma unroll
-    for (int k = 1; k < 4; ++k) { bk = j == k ? best[k] : bk; sk = j == k ? second[k] : sk; }
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t ob = (uint32_t)__shfl_xor((int)best[u][j], o, 16);
+                const uint32_t os = (uint32_t)__shfl_xor((int)second[u][j], o, 16);
+                second[u][j] = max(max(second[u][j], os), min(best[u][j], ob));
+                best[u][j] = max(best[u][j], ob);
+            }
+    }
+    if (n >= 4 * kMxQt) return;
+    const int u = n >> 2, j = n & 3, qi = qb + 16 * u + 4 * g + j;   // lane n < 4 kMxQt of row group g: tile u, row 4 g + j
+    if (qi >= nq) return;
+    uint32_t bk = best[0][0], sk = second[0][0];
+#pragma unroll
+    for (int uu = 0; uu < kMxQt; ++uu)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool me = u == uu && j == k;
+            bk = me ? best[uu][k] : bk;
+            sk = me ? second[uu][k] : sk;
+        }
     uint4 d0, d1;
     load_desc(q + 32 * (size_t)qi, d0, d1);
     const int nq1 = popc32(d0.x) + popc32(d0.y) + popc32(d0.z) + popc32(d0.w) + popc32(d1.x) + popc32(d1.y) +
                     popc32(d1.z) + popc32(d1.w);
-    // back to distances; the reference's initial (256, 256) with strict < : a best needs d < 256, distances clamp at 256
-    const int db = bk == 0xffffffffu ? 256 : (int)(bk >> 20) - 256 + nq1;
-    const int ds = sk == 0xffffffffu ? 256 : min(256, (int)(sk >> 20) - 256 + nq1);
+    // back to distances (d = e - 256 + |q| = 768 - (key >> 20) + |q|, index = 0xfffff - low bits); the reference's
+    // initial (256, 256) with strict < : a best needs d < 256, distances clamp at 256
+    const int db = bk == 0u ? 256 : 768 - (int)(bk >> 20) + nq1;
+    const int ds = sk == 0u ? 256 : min(256, 768 - (int)(sk >> 20) + nq1);
     const bool found = db < 256;
+    const uint32_t bidx = 0xfffffu - (bk & 0xfffffu);
     if (pbest) {
         const size_t o = ((size_t)z * nch + c) * nq + qi;
-        pbest[o] = found ? ((uint32_t)db << 20) | (bk & 0xfffffu) : (256u << 20);
+        pbest[o] = found ? ((uint32_t)db << 20) | bidx : (256u << 20);
         psecond[o] = found ? ds : 256;
     } else {
         const size_t o = (size_t)z * nq + qi;
         best_dist[o] = found ? db : 256;
-        best_idx[o] = found ? (int)(bk & 0xfffffu) : -1;
+        best_idx[o] = found ? (int)bidx : -1;
         second_dist[o] = found ? ds : 256;
     }
 }
