@@ -530,6 +530,14 @@ int orbx_proj_found_device(orbx_matcher* m, const int32_t* d_q_idx, const int32_
 int orbx_stereo_mappoints_device(orbx_matcher* m, const orbx_keypoint* d_kps, const float* d_depth, const int32_t* d_counts,
                                  int batch, int capacity, const float* d_twc, const float* camera, const float* scale_factors,
                                  int nlevels, int flags, orbx_map_point* d_points, void* stream);
+/* A batch of new keyframes' orbx_stereo_mappoints_device and orbx_grid_build_device (same outputs) in one launch of
+ * one workgroup per keyframe -- LocalMapping's keyframe insertion (src/LocalMapping.cc:157-200 with the KeyFrame's grid
+ * of src/KeyFrame.cc:44-49) before SearchInNeighbors' Fuse reads both.  Grid outputs at d_cell_start + b *
+ * (cols * rows + 1) and d_cell_idx + b * capacity. */
+int orbx_keyframe_prep_device(orbx_matcher* m, const orbx_keypoint* d_kps, const float* d_depth, const int32_t* d_counts,
+                              int batch, int capacity, const float* d_twc, const float* camera, const float* scale_factors,
+                              int nlevels, int flags, orbx_map_point* d_points, orbx_grid grid, int32_t* d_cell_start,
+                              int32_t* d_cell_idx, void* stream);
 /* Host form: one point set, one view. */
 int orbx_proj_project(orbx_matcher* m, int mode, const orbx_map_point* points, int n, const orbx_view* view,
                       const float* scale_factors, int nlevels, float log_scale_factor, orbx_proj_query* queries);

@@ -95,13 +95,13 @@ __global__ __launch_bounds__(kProjThreads) void k_grid_build(const orbx_keypoint
 // ascending order by one thread -- the CSR arrays of k_grid_build (cells ascending, indices ascending inside a cell)
 // from O(n) work and 4 barriers instead of the 66 stages of a 2048-key bitonic sort.
 // LDS: cnt[ncell + 1] ints, then cell[cap] and idx[cap] as u16.
-__global__ __launch_bounds__(kProjThreads) void k_grid_count(const orbx_keypoint* __restrict__ kps, const int32_t* __restrict__ counts,
-                                                             int n_fixed, int capacity, orbx_grid g,
-                                                             int32_t* __restrict__ cell_start, int32_t* __restrict__ cell_idx) {
+// The counting grid of keypoint set 'set' (its first n keypoints) by the whole workgroup; dynamic LDS gcs: (ncell + 1)
+// ints + 2 x capacity u16.
+__device__ __forceinline__ void grid_count_set(const orbx_keypoint* __restrict__ kps, int n, int capacity, const orbx_grid& g,
+                                               int32_t* __restrict__ cell_start, int32_t* __restrict__ cell_idx, int set) {
     extern __shared__ int gcs[];
     __shared__ int tmp[kProjThreads / 64 + 1];
-    const int set = blockIdx.x, tid = threadIdx.x, T = blockDim.x;
-    const int n = min(counts ? counts[set] : n_fixed, capacity);
+    const int tid = threadIdx.x, T = blockDim.x;
     const int ncell = g.cols * g.rows;
     const orbx_keypoint* K = kps + (size_t)set * capacity;
     int32_t* cs = cell_start + (size_t)set * (ncell + 1);
@@ -137,6 +137,13 @@ __global__ __launch_bounds__(kProjThreads) void k_grid_count(const orbx_keypoint
     __syncthreads();
     const int total = ncell ? cnt[ncell - 1] : 0;
     for (int j = tid; j < total; j += T) ci[j] = idx[j];
+}
+
+__global__ __launch_bounds__(kProjThreads) void k_grid_count(const orbx_keypoint* __restrict__ kps, const int32_t* __restrict__ counts,
+                                                             int n_fixed, int capacity, orbx_grid g,
+                                                             int32_t* __restrict__ cell_start, int32_t* __restrict__ cell_idx) {
+    const int set = blockIdx.x;
+    grid_count_set(kps, min(counts ? counts[set] : n_fixed, capacity), capacity, g, cell_start, cell_idx, set);
 }
 
 __device__ __forceinline__ int proj_rot_bin(float a1, float a2) {   // e.g. src/ORBmatcher.cc:1435-1440
@@ -768,13 +775,10 @@ __global__ __launch_bounds__(256) void k_project(int mode, const orbx_map_point*
 // constructor (src/MapPoint.cc:47-68).  One thread per keypoint.  Pinned as the projection: Rwc * x3Dc + Ow as float
 // products summed left to right; cv::norm with double squares summed in double and a double sqrt; the normal divided as
 // cv::Mat / double (the scale 1 / norm rounded to float, then a float product per component).
-__global__ __launch_bounds__(256) void k_stereo_mappoints(const orbx_keypoint* __restrict__ kps, const float* __restrict__ depth,
-                                                          const int32_t* __restrict__ counts, int capacity,
-                                                          const float* __restrict__ twc, float4 cam, ProjScales sc, int nlevels,
-                                                          int flags, orbx_map_point* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
-    const int n = min(counts[b], capacity);
-    if (i >= n) return;
+__device__ __forceinline__ void stereo_mappoint(const orbx_keypoint* __restrict__ kps, const float* __restrict__ depth,
+                                                int capacity, const float* __restrict__ twc, const float4& cam,
+                                                const ProjScales& sc, int nlevels, int flags, orbx_map_point* __restrict__ out,
+                                                int b, int i) {
     const size_t o = (size_t)b * capacity + i;
     const orbx_keypoint kp = kps[o];
     const float z = depth[o];
@@ -801,6 +805,31 @@ __global__ __launch_bounds__(256) void k_stereo_mappoints(const orbx_keypoint* _
         p.flags = flags & ~ORBX_QF_SKIP;
     }
     out[o] = p;
+}
+
+__global__ __launch_bounds__(256) void k_stereo_mappoints(const orbx_keypoint* __restrict__ kps, const float* __restrict__ depth,
+                                                          const int32_t* __restrict__ counts, int capacity,
+                                                          const float* __restrict__ twc, float4 cam, ProjScales sc, int nlevels,
+                                                          int flags, orbx_map_point* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, b = blockIdx.y;
+    const int n = min(counts[b], capacity);
+    if (i >= n) return;
+    stereo_mappoint(kps, depth, capacity, twc, cam, sc, nlevels, flags, out, b, i);
+}
+
+// A new keyframe's stereo MapPoints and its grid (Frame::AssignFeaturesToGrid, src/Frame.cc:230-245) in one
+// workgroup: the MapPoints as k_stereo_mappoints, then the counting grid of k_grid_count (the same CSR arrays) -- one
+// launch of one 256-thread workgroup per keyframe instead of a MapPoint launch and a 1,024-thread grid launch
+// (LocalMapping's new keyframes).  Dynamic LDS: k_grid_count's.
+__global__ __launch_bounds__(kProjThreads) void k_kf_prep(const orbx_keypoint* __restrict__ kps, const float* __restrict__ depth,
+                                                 const int32_t* __restrict__ counts, int capacity, const float* __restrict__ twc,
+                                                 float4 cam, ProjScales sc, int nlevels, int flags,
+                                                 orbx_map_point* __restrict__ out, orbx_grid g, int32_t* __restrict__ cell_start,
+                                                 int32_t* __restrict__ cell_idx) {
+    const int b = blockIdx.x;
+    const int n = min(counts[b], capacity);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) stereo_mappoint(kps, depth, capacity, twc, cam, sc, nlevels, flags, out, b, i);
+    grid_count_set(kps, n, capacity, g, cell_start, cell_idx, b);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1022,6 +1051,36 @@ int orbx_stereo_mappoints_device(orbx_matcher* m, const orbx_keypoint* d_kps, co
     hipLaunchKernelGGL(k_stereo_mappoints, dim3((capacity + 255) / 256, batch), dim3(256), 0, (hipStream_t)stream, d_kps, d_depth,
                        d_counts, capacity, d_twc, make_float4(camera[0], camera[1], camera[2], camera[3]), sc, nlevels, flags,
                        d_points);
+    ORBX_HIP(hipGetLastError());
+    return ORBX_OK;
+}
+
+int orbx_keyframe_prep_device(orbx_matcher* m, const orbx_keypoint* d_kps, const float* d_depth, const int32_t* d_counts,
+                              int batch, int capacity, const float* d_twc, const float* camera, const float* scale_factors,
+                              int nlevels, int flags, orbx_map_point* d_points, orbx_grid grid, int32_t* d_cell_start,
+                              int32_t* d_cell_idx, void* stream) {
+    ORBX_REQUIRE(m && d_kps && d_depth && d_counts && d_twc && camera && d_points && d_cell_start && d_cell_idx && batch >= 0 &&
+                     capacity > 0, ORBX_ERR_ARG, "bad argument");
+    ProjScales sc;
+    int st = project_check(ORBX_PROJ_FUSE, scale_factors, nlevels, &sc);
+    if (st) return st;
+    if ((st = grid_check(grid))) return st;
+    ORBX_REQUIRE(camera[0] != 0.0f && camera[1] != 0.0f, ORBX_ERR_ARG, "bad camera");
+    if (batch == 0) return ORBX_OK;
+    const size_t ncell = (size_t)grid.cols * grid.rows;
+    const size_t lds = ((ncell + 1) * 4 + 4 * (size_t)capacity + 15) & ~(size_t)15;
+    ORBX_REQUIRE(ncell < 0xffff && capacity < 0xffff && lds <= 64 * 1024, ORBX_ERR_UNSUPPORTED,
+                 "keyframe grid of %d cells x %d keypoints does not fit the one-workgroup form", (int)ncell, capacity);
+    ORBX_REQUIRE(batch <= 65535, ORBX_ERR_UNSUPPORTED, "batch too large");
+    ORBX_HIP(hipSetDevice(matcher_device(m)));
+    static const int threads = [] {                                           // ORBX_KF_PREP_THREADS (diagnostics)
+        const char* v = std::getenv("ORBX_KF_PREP_THREADS");
+        const int t = v ? std::atoi(v) : kProjThreads;
+        return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
+    }();
+    hipLaunchKernelGGL(k_kf_prep, dim3(batch), dim3(threads), lds, (hipStream_t)stream, d_kps, d_depth, d_counts, capacity, d_twc,
+                       make_float4(camera[0], camera[1], camera[2], camera[3]), sc, nlevels, flags, d_points, grid, d_cell_start,
+                       d_cell_idx);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }

@@ -856,9 +856,14 @@ class LocalFuse:
             torch.index_select(uright, 0, rows, out=self.ur[a:b])
             kk = torch.index_select(kps, 0, rows)
             dk = torch.index_select(depth, 0, rows)
-        self.m.stereo_mappoints_device(kk, dk, self.cnt[a:b], self.twc[a:b], self.camera, self.scale, QF_BLOCKS,
-                                       out=self.pts[a:b], stream=stream)
-        self.m.grid_build_device(self.grid, kk, self.cnt[a:b], stream=stream, out=(self.cs[a:b], self.ci[a:b]))
+        if os.environ.get("ORBX_KF_PREP_SPLIT"):                  # A/B only: the MapPoints and the grid as two launches
+            self.m.stereo_mappoints_device(kk, dk, self.cnt[a:b], self.twc[a:b], self.camera, self.scale, QF_BLOCKS,
+                                           out=self.pts[a:b], stream=stream)
+            self.m.grid_build_device(self.grid, kk, self.cnt[a:b], stream=stream, out=(self.cs[a:b], self.ci[a:b]))
+        else:
+            # the keyframes' MapPoints and grids in one launch of one workgroup per keyframe
+            self.m.keyframe_prep_device(self.grid, kk, dk, self.cnt[a:b], self.twc[a:b], self.camera, self.scale, QF_BLOCKS,
+                                        self.pts[a:b], self.cs[a:b], self.ci[a:b], stream=stream)
 
     def _plan(self, new_slots, neighbours):
         """Per (new keyframe j, neighbour k): the two directions' views, point sets and problem tables (cached per

@@ -200,6 +200,7 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_proj_project.argtypes = [vp, i32, vp, i32, vp, vp, i32, f32, vp]
     lib.orbx_proj_project_device.argtypes = [vp, i32, vp, vp, i32, i32, vp, vp, vp, i32, f32, vp, vp, vp]
     lib.orbx_stereo_mappoints_device.argtypes = [vp, vp, vp, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp]
+    lib.orbx_keyframe_prep_device.argtypes = [vp, vp, vp, vp, i32, i32, vp, vp, vp, i32, i32, vp, Grid, vp, vp, vp]
     lib.orbx_proj_found_device.argtypes = [vp, vp, vp, i32, i32, i32, vp, vp, vp]
     lib.orbx_matcher_create.argtypes = [f32, i32, i32, C.POINTER(vp)]
     for name in ("orbx_extractor_destroy", "orbx_matcher_destroy", "orbx_extractor_get_levels"):
@@ -969,6 +970,25 @@ class ORBmatcher:
         _check(self._lib.orbx_stereo_mappoints_device(self._h, _tp(kps), _tp(depth), _tp(counts), B, cap, _tp(twc), _p(cam),
                                                       _p(sc), len(sc), int(flags), _tp(out), s))
         return out
+
+    def keyframe_prep_device(self, grid: Grid, kps, depth, counts, twc, camera, scale_factors, flags: int, points, cell_start,
+                             cell_idx, stream=None):
+        """stereo_mappoints_device and grid_build_device of a batch of new keyframes in one launch (include/orbx.h
+        orbx_keyframe_prep_device), written into points (B, cap, 48) uint8 and cell_start / cell_idx int32 (B, cells + 1)
+        / (B, cap)."""
+        import torch
+        B, cap = kps.shape[0], kps.shape[1]
+        ncell = grid.cols * grid.rows
+        if tuple(cell_start.shape) != (B, ncell + 1) or tuple(cell_idx.shape) != (B, cap) or \
+                cell_start.dtype != torch.int32 or cell_idx.dtype != torch.int32 or tuple(points.shape) != (B, cap, 48):
+            raise ValueError("keyframe_prep_device: points (B, capacity, 48) uint8, grid int32 (B, cells+1), (B, capacity)")
+        cam = np.ascontiguousarray(camera, np.float32).reshape(4)
+        sc = np.ascontiguousarray(scale_factors, np.float32)
+        s = C.c_void_p(stream.cuda_stream if stream is not None else torch.cuda.current_stream(kps.device).cuda_stream)
+        _check(self._lib.orbx_keyframe_prep_device(self._h, _tp(kps), _tp(depth), _tp(counts), B, cap, _tp(twc), _p(cam),
+                                                   _p(sc), len(sc), int(flags), _tp(points), grid, _tp(cell_start),
+                                                   _tp(cell_idx), s))
+        return points, cell_start, cell_idx
 
     def grid_build_device(self, grid: Grid, kps, counts, stream=None, out=None):
         """Frame::AssignFeaturesToGrid on (B, capacity, 28) device keypoints: (cell_start, cell_idx) tensors

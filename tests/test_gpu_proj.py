@@ -272,6 +272,52 @@ def test_stereo_mappoints_and_found_skip_bit_exact(gpu):
         assert np.array_equal(q[i, :len(k)], O.project(PROJ_MAPPOINTS, p, view, SCALE, lsf)), f"frame {i}"
 
 
+def test_keyframe_prep_equals_oracle(gpu):
+    """orbx_keyframe_prep_device (a keyframe's MapPoints and grid in one workgroup) equals the oracle's stereo MapPoints
+    and Frame::AssignFeaturesToGrid, bit for bit, including an empty keyframe."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from multiagent_orb_slam2_amd.orbx import QF_BLOCKS
+    from oracle import oracle as O
+    from proj_cases import SCALE, stereo_frame_case
+    m = pkg.ORBmatcher(0.8, True)
+    grid = make_case(7, MODES["mappoints"])["grid"]
+    frames = [stereo_frame_case(70 + i, n=900 + 300 * i) for i in range(3)]
+    cap = max(len(f[0]) for f in frames)
+    B = 4
+    kp = np.zeros((B, cap), pkg.KP_DTYPE)
+    dp = np.zeros((B, cap), np.float32)
+    tw = np.zeros((B, 12), np.float32)
+    for i, (k, d, t, cam) in enumerate(frames):
+        kp[i, :len(k)], dp[i, :len(k)], tw[i] = k, d, t
+    ns = [len(f[0]) for f in frames] + [0]
+    dk = torch.from_numpy(kp.view(np.uint8).reshape(B, cap, 28)).cuda()
+    dd, dt = torch.from_numpy(dp).cuda(), torch.from_numpy(tw).cuda()
+    cnt = torch.tensor(ns, dtype=torch.int32, device="cuda")
+    pts = torch.zeros((B, cap, 48), dtype=torch.uint8, device="cuda")
+    cs = torch.full((B, grid.cols * grid.rows + 1), -7, dtype=torch.int32, device="cuda")
+    ci = torch.full((B, cap), -7, dtype=torch.int32, device="cuda")
+    m.keyframe_prep_device(grid, dk, dd, cnt, dt, frames[0][3], SCALE, QF_BLOCKS, pts, cs, ci)
+    torch.cuda.synchronize()
+    got, gcs, gci = pts.cpu().numpy(), cs.cpu().numpy(), ci.cpu().numpy()
+    for i, n in enumerate(ns):
+        k = kp[i, :n]
+        if n:
+            ref = O.stereo_mappoints(k, dp[i, :n], tw[i], frames[0][3], SCALE, QF_BLOCKS)
+            assert np.array_equal(got[i, :n].reshape(-1), ref.view(np.uint8).reshape(-1)), f"keyframe {i}"
+        rcs, rci = O.grid_assign(k, grid)
+        assert np.array_equal(gcs[i], rcs), f"keyframe {i} grid"
+        assert np.array_equal(gci[i, :rcs[-1]], rci), f"keyframe {i} grid"
+    # the same through the two-launch form
+    pts2 = m.stereo_mappoints_device(dk, dd, cnt, dt, frames[0][3], SCALE, QF_BLOCKS)
+    cs2, ci2 = m.grid_build_device(grid, dk, cnt)
+    torch.cuda.synchronize()
+    for i, n in enumerate(ns):
+        assert torch.equal(pts2[i, :n], pts[i, :n]) and torch.equal(cs2[i], cs[i])
+        assert torch.equal(ci2[i, :int(cs[i, -1])], ci[i, :int(cs[i, -1])])
+
+
 @pytest.mark.parametrize("mode", ["lastframe", "mappoints", "fuse", "best"])
 def test_search_with_grid_built_inside(gpu, mode):
     """orbx_proj_search_grid_batch_device: each problem's grid built inside its search from the first grid_counts[p]
