@@ -605,8 +605,11 @@ int orbx_kfdb_info(const orbx_kfdb* db, int* n_vocab_words, int* max_slots, int*
 /* How a query finds the keyframes sharing its words (results are identical):
  * ORBX_KFDB_INVERTED walks the inverted file (rebuilt on the device after membership changes), as the
  * reference does; ORBX_KFDB_PAIRWISE intersects the query with every member's BowVector (no rebuild, cheaper
- * for small databases); ORBX_KFDB_AUTO (default) picks pairwise up to 2048 members. */
-enum { ORBX_KFDB_AUTO = 0, ORBX_KFDB_INVERTED = 1, ORBX_KFDB_PAIRWISE = 2 };
+ * for small databases); ORBX_KFDB_WORDMAP reads, per query word, that word's row of a word x slot bit matrix
+ * the database keeps beside the BowVectors (databases of <= 2048 slots whose matrix is <= 1 GB, e.g. 156 MB for
+ * 1,224 slots over a 10^6-word vocabulary; ORBX_ERR_UNSUPPORTED otherwise); ORBX_KFDB_AUTO (default) picks the
+ * word map when the database has one, else pairwise up to 2048 members, else the inverted file. */
+enum { ORBX_KFDB_AUTO = 0, ORBX_KFDB_INVERTED = 1, ORBX_KFDB_PAIRWISE = 2, ORBX_KFDB_WORDMAP = 3 };
 int orbx_kfdb_set_strategy(orbx_kfdb* db, int strategy);
 /* Store a slot's BowVector (KeyFrame::mBowVec); word ids strictly ascending and < n_vocab_words. */
 int orbx_kfdb_set_bow(orbx_kfdb* db, int slot, const uint32_t* words, const double* values, int n);

@@ -598,6 +598,12 @@ __device__ __forceinline__ void sc_store(lds_u8* __restrict__ scb, int SWB, int 
     *(lds_s16x2*)(scb + (rr + 1) * SWB + 4 + 4 * j) = second ? v : (s16x2){v.x, (short)-1};
 }
 
+// ORBX_FAST_ATTR (diagnostics builds only, `make variant`; wrong keypoints): bit 0 reads the score taps, bit 1 the NMS
+// neighbourhoods at one row and columns ln & 15 of the cell instead of the survivor's -- the same LDS instructions on
+// addresses a 32-lane half reads without bank conflicts -- so a PMC pass attributes SQ_LDS_BANK_CONFLICT to them.
+#ifndef ORBX_FAST_ATTR
+#define ORBX_FAST_ATTR 0
+#endif
 // The part of a cell after its ROI is in LDS: pre-test, scores, NMS at both thresholds, the cell's candidate slots.
 template <int kPS, int kPC>
 __device__ __forceinline__ void fastw_body(lds_u32* __restrict__ E, lds_u8* __restrict__ scb, lds_u16* __restrict__ list,
@@ -661,8 +667,13 @@ __device__ __forceinline__ void fastw_body(lds_u32* __restrict__ E, lds_u8* __re
                 const uint32_t e1 = list[i], e2 = i2 < ns ? list[i2] : e1;
                 const int rr1 = e1 >> 8, j1 = e1 & 0xff, rr2 = e2 >> 8, j2 = e2 & 0xff;
                 uint32_t t1[17], t2[17];
-                fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
-                fast_taps_f16<kPS, kPC>(E, rr2 + 3, j2, t2);
+                if constexpr (ORBX_FAST_ATTR & 1) {
+                    fast_taps_f16<kPS, kPC>(E, 3, ln & 15, t1);
+                    fast_taps_f16<kPS, kPC>(E, 3, (ln & 15) ^ 1, t2);
+                } else {
+                    fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
+                    fast_taps_f16<kPS, kPC>(E, rr2 + 3, j2, t2);
+                }
                 const s16x2 s1 = fast_score_from_taps_f16(t1), s2 = fast_score_from_taps_f16(t2);
                 sc_store(scb, SWB, rr1, j1, s1, 2 * j1 + 1 < Wd);
                 if (i2 < ns) sc_store(scb, SWB, rr2, j2, s2, 2 * j2 + 1 < Wd);
@@ -671,7 +682,8 @@ __device__ __forceinline__ void fastw_body(lds_u32* __restrict__ E, lds_u8* __re
             const uint32_t e1 = list[i];
             const int rr1 = e1 >> 8, j1 = e1 & 0xff;
             uint32_t t1[17];
-            fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
+            if constexpr (ORBX_FAST_ATTR & 1) fast_taps_f16<kPS, kPC>(E, 3, ln & 15, t1);
+            else fast_taps_f16<kPS, kPC>(E, rr1 + 3, j1, t1);
             const s16x2 s1 = fast_score_from_taps_f16(t1);
             sc_store(scb, SWB, rr1, j1, s1, 2 * j1 + 1 < Wd);
         }
@@ -684,7 +696,8 @@ __device__ __forceinline__ void fastw_body(lds_u32* __restrict__ E, lds_u8* __re
         int f = 0, key = 0;
         if (i < ns) {
             const int rr = list[i] >> 8, j = list[i] & 0xff;
-            f = nms_pair((const lds_i16*)scb, SWB / 2, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
+            if constexpr (ORBX_FAST_ATTR & 2) f = nms_pair((const lds_i16*)scb, SWB / 2, 0, ln & 15, T1, T2, 2 * j + 1 < Wd) & fmask;
+            else f = nms_pair((const lds_i16*)scb, SWB / 2, rr, j, T1, T2, 2 * j + 1 < Wd) & fmask;
             key = rr * 128 + 2 * j;
         }
         const uint64_t a0 = __ballot(f & 1), a1 = __ballot(f & 2), c0 = __ballot(f & 4), c1 = __ballot(f & 8);

@@ -25,6 +25,8 @@
 //                   atomic-min first position per keyframe slot
 //   (small databases: k_kfdb_bits + k_kfdb_pairwise_gb intersect every (query, slot) pair against a bitmap of the
 //                   query's words instead of walking an inverted file; same word count and first position)
+//   (<= 2048 slots: k_kfdb_wmap_count reads, per query word, the word's row of a word x slot bit matrix kept
+//                   beside the BowVectors; same word count and first position from 1/32 of a word per slot)
 //   k_kfdb_select   one workgroup per query: list membership from the scratch fields, max common words,
 //                   compaction of the keyframes to score
 //   k_kfdb_score    query BowVector staged in LDS; one wave per scored keyframe walks its words, finds
@@ -80,6 +82,8 @@ struct DbDev {
     const int32_t* if_off;   // [n_vocab + 1]
     const int32_t* if_slot;  // inverted file entries
     int S, maxw, n_vocab;
+    uint32_t* wmap;          // [n_vocab][wdw] bit k % 32 of word dw k / 32: slot k's BowVector holds the word; or NULL
+    int wdw;                 // dwords per word row: ceil(S / 32)
 };
 
 struct StateDev {
@@ -159,6 +163,19 @@ __global__ __launch_bounds__(256) void k_if_scatter(DbDev D, const int32_t* __re
     }
 }
 
+// slot k's first n words into (set) or out of the word map, by the workgroup (each slot owns its bit: atomics only
+// against other slots' bits in the same dword)
+__device__ __forceinline__ void wmap_slot(const DbDev& D, int k, int n, bool set) {
+    const uint32_t bit = 1u << (k & 31);
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        const uint32_t w = D.bw[(size_t)k * D.maxw + j];
+        if (w >= (uint32_t)D.n_vocab) continue;
+        uint32_t* a = &D.wmap[(size_t)w * D.wdw + (k >> 5)];
+        if (set) atomicOr(a, bit);
+        else atomicAnd(a, ~bit);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_set_bow(DbDev D, uint32_t* __restrict__ bw, double* __restrict__ bv, int32_t* __restrict__ bn,
                                                  const int32_t* __restrict__ slots, const uint32_t* __restrict__ words, long long word_stride,
                                                  const double* __restrict__ values, long long value_stride,
@@ -167,12 +184,21 @@ __global__ __launch_bounds__(256) void k_set_bow(DbDev D, uint32_t* __restrict__
     const int k = slots[i];
     if (k < 0 || k >= D.S) return;
     const int n = max(0, min(n_words[(size_t)i * n_stride], D.maxw));
+    if (D.wmap) {                                     // the old BowVector's bits out of the word map first
+        wmap_slot(D, k, bn[k], false);
+        __syncthreads();
+    }
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        bw[(size_t)k * D.maxw + j] = words[(size_t)i * word_stride + j];
+        const uint32_t w = words[(size_t)i * word_stride + j];
+        bw[(size_t)k * D.maxw + j] = w;
         bv[(size_t)k * D.maxw + j] = values[(size_t)i * value_stride + j];
+        if (D.wmap && w < (uint32_t)D.n_vocab) atomicOr(&D.wmap[(size_t)w * D.wdw + (k >> 5)], 1u << (k & 31));
     }
     if (threadIdx.x == 0) bn[k] = n;
 }
+
+// the host form of set_bow: slot k's current words out of (set false) or into (set true) the word map
+__global__ __launch_bounds__(256) void k_wmap_slot(DbDev D, int k, bool set) { wmap_slot(D, k, D.bn[k], set); }
 
 // MapFusion keeps the first k candidates of another map (src/MapFusion.cc:136-144 drops same-map
 // candidates) and matches the query against each (:275).  One thread per query; pairs (query, cand) or
@@ -361,6 +387,90 @@ __global__ __launch_bounds__(256) void k_kfdb_pairwise_gb(DbDev D, QueryIn Q, QS
             X.cnt[row + k] = c;
             X.first[row + k] = (int)first;
         }
+    }
+}
+
+// Word-map form of the same counts.  One workgroup per query: thread t owns slot dword d = t % wdw (32 slots) for the
+// query words p = g, g + G, ... (g = t / wdw, G = 256 / wdw groups; wdw <= 64), reads word p's dword d, and counts
+// its 32 slots' hits with a Harley-Seal carry-save tree (16 words per flush: ones / twos / fours / eights registers,
+// the sixteens rippled into 9 bit planes) -- ~7 bit operations per word for 32 slots, instead of a wave per (query,
+// slot) walking the slot's words.  Words are walked in ascending position, so a slot's first hit in a thread is that
+// thread's smallest position; the groups' firsts and counts merge by LDS atomics (once per slot and group).
+constexpr int kWmapMaxSlots = 2048;
+__device__ __forceinline__ void csa(uint32_t& h, uint32_t& l, uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t u = a ^ b;
+    h = (a & b) | (u & c);
+    l = u ^ c;
+}
+
+__global__ __launch_bounds__(256) void k_kfdb_wmap_count(DbDev D, QueryIn Q, QScratch X, int kind) {
+    extern __shared__ int wsm[];
+    int* s_cnt = wsm;                       // [S]
+    int* s_first = wsm + D.S;               // [S]
+    uint32_t* s_qw = (uint32_t*)(wsm + 2 * D.S);   // [maxw]
+    const int q = blockIdx.x, tid = threadIdx.x;
+    const int qs = Q.slot[q], nq = D.bn[qs];
+    const uint32_t nv = (uint32_t)D.n_vocab;
+    for (int k = tid; k < D.S; k += blockDim.x) { s_cnt[k] = 0; s_first[k] = 0x7f7f7f7f; }
+    for (int i = tid; i < nq; i += blockDim.x) s_qw[i] = D.bw[(size_t)qs * D.maxw + i];
+    __syncthreads();
+    const int dw = D.wdw, G = blockDim.x / dw, g = tid / dw, d = tid - g * dw;
+    if (g < G) {
+        uint32_t ones = 0, twos = 0, fours = 0, eights = 0, seen = 0;
+        uint32_t pl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // sixteens, bit planes
+        for (int p0 = g; p0 < nq; p0 += 16 * G) {
+            uint32_t x[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int p = p0 + r * G;
+                const uint32_t w = p < nq ? s_qw[p] : 0xffffffffu;
+                x[r] = w < nv ? D.wmap[(size_t)w * dw + d] : 0u;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t nw = x[r] & ~seen;
+                if (nw) {                                      // this thread's first hit of these slots: position p
+                    seen |= nw;
+                    uint32_t m = nw;
+                    while (m) {
+                        const int b = __builtin_ctz(m);
+                        atomicMin(&s_first[d * 32 + b], p0 + r * G);
+                        m &= m - 1;
+                    }
+                }
+            }
+            uint32_t ta, tb, fa, fb, ea, eb, six;
+            csa(ta, ones, ones, x[0], x[1]);   csa(tb, ones, ones, x[2], x[3]);   csa(fa, twos, twos, ta, tb);
+            csa(ta, ones, ones, x[4], x[5]);   csa(tb, ones, ones, x[6], x[7]);   csa(fb, twos, twos, ta, tb);
+            csa(ea, fours, fours, fa, fb);
+            csa(ta, ones, ones, x[8], x[9]);   csa(tb, ones, ones, x[10], x[11]); csa(fa, twos, twos, ta, tb);
+            csa(ta, ones, ones, x[12], x[13]); csa(tb, ones, ones, x[14], x[15]); csa(fb, twos, twos, ta, tb);
+            csa(eb, fours, fours, fa, fb);
+            csa(six, eights, eights, ea, eb);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) { const uint32_t t = pl[j] & six; pl[j] ^= six; six = t; }
+        }
+        if (seen) {
+            for (int b = 0; b < 32; ++b) {
+                if (!((seen >> b) & 1u)) continue;
+                int c = (int)((ones >> b) & 1u) + 2 * (int)((twos >> b) & 1u) + 4 * (int)((fours >> b) & 1u) +
+                        8 * (int)((eights >> b) & 1u);
+#pragma unroll
+                for (int j = 0; j < 9; ++j) c += (int)((pl[j] >> b) & 1u) << (4 + j);
+                atomicAdd(&s_cnt[d * 32 + b], c);
+            }
+        }
+    }
+    __syncthreads();
+    const size_t row = (size_t)q * D.S;
+    for (int k = tid; k < D.S; k += blockDim.x) {
+        int c = 0, first = 0x7f7f7f7f;
+        if (kf_visible(D, Q, q, k) && !(kind == KIND_COVIS && excl_at(X, row + k)) && nq > 0 && s_cnt[k] > 0) {
+            c = s_cnt[k];
+            first = s_first[k];
+        }
+        X.cnt[row + k] = c;
+        X.first[row + k] = first;
     }
 }
 
@@ -670,6 +780,8 @@ struct orbx_kfdb {
     float* d_s[3] = {nullptr, nullptr, nullptr};
     void* scratch = nullptr;       // per-query rows + host-form staging
     size_t scratch_bytes = 0;
+    uint32_t* d_wmap = nullptr;    // word x slot bit matrix (k_kfdb_wmap_count), kept by every set_bow; NULL above
+    int wmap_dw = 0;               // kWmapMaxSlots slots or a 1 GB matrix
     uint32_t* d_qbits = nullptr;   // per-query vocabulary bitmaps of the pairwise intersection: all zero between
     size_t qbits_bytes = 0;        // operations (each batch clears the words it set, k_kfdb_select)
     // Thread and stream contract (KeyFrameDatabase.cc:42,50,84,210,316 lock mMutex in add / erase / every Detect*):
@@ -730,7 +842,8 @@ struct DbOp {
 #define ORBX_DBLOCK(db) std::lock_guard<std::recursive_mutex> lock_((db)->mtx)
 
 DbDev dev_view(const orbx_kfdb* db) {
-    return DbDev{db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_slot, db->S, db->maxw, db->n_vocab};
+    return DbDev{db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_slot, db->S, db->maxw, db->n_vocab,
+                 db->d_wmap, db->wmap_dw};
 }
 
 int grow_scratch(orbx_kfdb* db, size_t bytes) {
@@ -804,6 +917,12 @@ int rebuild_inverted_file(orbx_kfdb* db, hipStream_t s) {
 
 // auto strategy: up to this many members, intersect pairwise (no inverted file); ORBX_KFDB_PAIRWISE_MAX overrides
 // (diagnostics: A/B of the two strategies at a given ring size)
+// ORBX_KFDB_WORDMAP=0 (diagnostics): no word map, AUTO falls back to the pairwise / inverted-file rule
+static bool wmap_enabled() {
+    static const bool v = [] { const char* e = std::getenv("ORBX_KFDB_WORDMAP"); return !e || std::atoi(e) != 0; }();
+    return v;
+}
+
 static int pairwise_max_members() {
     static const int v = [] { const char* e = std::getenv("ORBX_KFDB_PAIRWISE_MAX"); return e ? std::atoi(e) : 2048; }();
     return v;
@@ -813,9 +932,10 @@ static int pairwise_max_members() {
 // The query batch on stream s; d_* are device pointers.  Scratch rows at 'base' (nq x S).
 int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned char* base, int32_t* d_out, int out_stride,
                  int32_t* d_out_n, int32_t* d_status, hipStream_t s) {
-    const bool pairwise = db->strategy == ORBX_KFDB_PAIRWISE ||
-                          (db->strategy == ORBX_KFDB_AUTO && (int)db->members.size() <= pairwise_max_members());
-    int st = pairwise ? upload_membership(db, s) : rebuild_inverted_file(db, s);
+    const bool wordmap = db->d_wmap && (db->strategy == ORBX_KFDB_WORDMAP || db->strategy == ORBX_KFDB_AUTO);
+    const bool pairwise = !wordmap && (db->strategy == ORBX_KFDB_PAIRWISE ||
+                                       (db->strategy == ORBX_KFDB_AUTO && (int)db->members.size() <= pairwise_max_members()));
+    int st = (pairwise || wordmap) ? upload_membership(db, s) : rebuild_inverted_file(db, s);
     if (st) return st;
     QScratch X;
     qscratch_layout(nq, db->S, base, &X);
@@ -830,7 +950,10 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
     const size_t lds = (size_t)db->maxw * (sizeof(double) + sizeof(uint32_t));
     const int nbw = (db->n_vocab + 31) / 32;
     uint32_t* qbits = nullptr;
-    if (pairwise) {
+    if (wordmap) {
+        const size_t wl = (size_t)db->S * 8 + (size_t)db->maxw * 4;
+        hipLaunchKernelGGL(k_kfdb_wmap_count, dim3(nq), dim3(256), wl, s, D, Q, X, kind);
+    } else if (pairwise) {
         const size_t need = (size_t)4 * nbw * nq;
         if (need > db->qbits_bytes) {
             if (db->d_qbits) {
@@ -904,6 +1027,13 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
     alloc((void**)&db->d_if_slot, 4 * S * W);
     alloc((void**)&db->d_scan, 4 * ((size_t)(n_vocab_words + 1 + kScanChunk - 1) / kScanChunk + 1));
     alloc((void**)&db->d_members, 4 * S);
+    if (wmap_enabled() && max_slots <= kWmapMaxSlots) {
+        const size_t dw = ((size_t)max_slots + 31) / 32;
+        if ((size_t)n_vocab_words * dw * 4 <= ((size_t)1 << 30)) {
+            db->wmap_dw = (int)dw;
+            alloc((void**)&db->d_wmap, (size_t)n_vocab_words * dw * 4);
+        }
+    }
     for (int k = 0; k < 3; ++k) {
         alloc((void**)&db->d_q[k], 8 * S);
         alloc((void**)&db->d_w[k], 4 * S);
@@ -929,7 +1059,7 @@ int orbx_kfdb_destroy(orbx_kfdb* db) {
     (void)hipSetDevice(db->device);
     (void)hipDeviceSynchronize();              // operations on callers' streams read the database's buffers
     void* bufs[] = {db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_cur, db->d_if_slot,
-                    db->d_scan, db->d_members, db->scratch, db->score_stage, db->d_qbits};
+                    db->d_scan, db->d_members, db->scratch, db->score_stage, db->d_qbits, db->d_wmap};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (int k = 0; k < 3; ++k) {
@@ -960,8 +1090,10 @@ int orbx_kfdb_info(const orbx_kfdb* db, int* n_vocab_words, int* max_slots, int*
 }
 
 int orbx_kfdb_set_strategy(orbx_kfdb* db, int strategy) {
-    ORBX_REQUIRE(db && strategy >= ORBX_KFDB_AUTO && strategy <= ORBX_KFDB_PAIRWISE, ORBX_ERR_ARG, "bad strategy");
+    ORBX_REQUIRE(db && strategy >= ORBX_KFDB_AUTO && strategy <= ORBX_KFDB_WORDMAP, ORBX_ERR_ARG, "bad strategy");
     ORBX_DBLOCK(db);
+    ORBX_REQUIRE(strategy != ORBX_KFDB_WORDMAP || db->d_wmap, ORBX_ERR_UNSUPPORTED,
+                 "no word map for this database (%d slots, %d words)", db->S, db->n_vocab);
     db->strategy = strategy;
     return ORBX_OK;
 }
@@ -976,11 +1108,15 @@ int orbx_kfdb_set_bow(orbx_kfdb* db, int slot, const uint32_t* words, const doub
     ORBX_HIP(hipSetDevice(db->device));
     ORBX_DBOP(db, db->own());
     const size_t o = (size_t)slot * db->maxw;
+    DbDev D = dev_view(db);
+    if (db->d_wmap) hipLaunchKernelGGL(k_wmap_slot, dim3(1), dim3(256), 0, db->own(), D, slot, false);
     if (n) {
         ORBX_HIP(hipMemcpyAsync(db->d_bw + o, words, 4 * (size_t)n, hipMemcpyHostToDevice, db->own()));
         ORBX_HIP(hipMemcpyAsync(db->d_bv + o, values, 8 * (size_t)n, hipMemcpyHostToDevice, db->own()));
     }
     ORBX_HIP(hipMemcpyAsync(db->d_bn + slot, &n, 4, hipMemcpyHostToDevice, db->own()));
+    if (db->d_wmap) hipLaunchKernelGGL(k_wmap_slot, dim3(1), dim3(256), 0, db->own(), D, slot, true);
+    ORBX_HIP(hipGetLastError());
     ORBX_HIP(hipStreamSynchronize(db->own()));
     if (db->seq[slot] != kNoSeq) db->dirty = true;
     return ORBX_OK;

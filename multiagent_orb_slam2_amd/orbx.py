@@ -1108,7 +1108,7 @@ class ORBVocabulary:
 
 
 KFDB_LOOP, KFDB_COVIS, KFDB_RELOC = 0, 1, 2
-KFDB_AUTO, KFDB_INVERTED, KFDB_PAIRWISE = 0, 1, 2   # how a query finds the keyframes sharing its words
+KFDB_AUTO, KFDB_INVERTED, KFDB_PAIRWISE, KFDB_WORDMAP = 0, 1, 2, 3   # how a query finds the keyframes sharing its words
 KFDB_COVIS_WIDTH = 10   # GetBestCovisibilityKeyFrames(10)
 
 
@@ -1139,8 +1139,9 @@ class KeyFrameDatabase:
             pass
 
     def set_strategy(self, strategy: int):
-        """KFDB_INVERTED (inverted file, as the reference), KFDB_PAIRWISE (intersect with every member) or
-        KFDB_AUTO; results are identical."""
+        """KFDB_INVERTED (inverted file, as the reference), KFDB_PAIRWISE (intersect with every member),
+        KFDB_WORDMAP (rows of the database's word x slot bit matrix; <= 2048 slots) or KFDB_AUTO; results are
+        identical."""
         _check(self._lib.orbx_kfdb_set_strategy(self._h, strategy))
 
     def n_members(self) -> int:

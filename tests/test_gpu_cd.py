@@ -21,7 +21,7 @@ def _maps(n, seed, nfeat=1000, rows=240, cols=480):
     return ex.extract_batch_device(torch.from_numpy(np.stack(left + right)).cuda())
 
 
-@pytest.mark.parametrize("strategy", [1, 2])
+@pytest.mark.parametrize("strategy", [1, 2, 3])
 def test_covisibility_discovery_vs_oracle(gpu, strategy):
     import multiagent_orb_slam2_amd as pkg
     from oracle import oracle as O

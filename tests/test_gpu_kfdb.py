@@ -47,23 +47,23 @@ def _run_both(case, batched=True, strategy=0):
     return n_results
 
 
-INVERTED, PAIRWISE = 1, 2
+INVERTED, PAIRWISE, WORDMAP = 1, 2, 3
 
 
-@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE, WORDMAP])
 @pytest.mark.parametrize("seed", range(8))
 def test_detect_sequences(gpu, seed, strategy):
     case = make_kfdb_case(100 + seed, n_slots=150, n_queries=48, words_hi=400)
     assert _run_both(case, strategy=strategy) > 0
 
 
-@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE, WORDMAP])
 def test_detect_one_by_one(gpu, strategy):
     case = make_kfdb_case(200, n_slots=100, n_queries=30)
     assert _run_both(case, batched=False, strategy=strategy) > 0
 
 
-@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE, WORDMAP])
 def test_detect_fresh_ids_large(gpu, strategy):
     """KITTI-like keyframes (1000-1500 words of a 1M-word vocabulary), 600 slots, fresh query ids only."""
     case = make_kfdb_case(300, n_slots=600, n_vocab=1_000_000, n_places=30, words_lo=900, words_hi=1500,
@@ -86,7 +86,7 @@ def test_scores_bit_exact(gpu):
     assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
 
 
-@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE, WORDMAP])
 def test_edge_cases(gpu, strategy):
     import multiagent_orb_slam2_amd as pkg
     g = pkg.KeyFrameDatabase(16, 4, max_words=8)
@@ -116,7 +116,7 @@ def test_edge_cases(gpu, strategy):
 
 
 @pytest.mark.parametrize("kind", [LOOP, COVIS, RELOC])
-@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE])
+@pytest.mark.parametrize("strategy", [INVERTED, PAIRWISE, WORDMAP])
 def test_detect_sequential_batch(gpu, kind, strategy):
     """orbx_kfdb_detect_sequential: a batch of new keyframes added in order and queried in one call equals
     MapFusion's loop detect(k0); add(k0); detect(k1); add(k1); ... (src/MapFusion.cc:133, :149 / :222) --
@@ -152,3 +152,67 @@ def test_detect_sequential_batch(gpu, kind, strategy):
     assert np.array_equal(gs.view(np.uint32), os_.view(np.uint32))
     # the query slots are members afterwards, in the same order as the oracle's
     assert g.n_members() == len(old) + len(new)
+
+
+def test_wordmap_follows_set_bow(gpu):
+    """The word map (ORBX_KFDB_WORDMAP) follows BowVectors re-set by the host and the device form: after slots are
+    overwritten (other slots' words, an empty vector), detections equal the oracle's and the pairwise form's."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    case = make_kfdb_case(600, n_slots=200, n_queries=8, words_hi=500)
+    dbs = {}
+    for st in (PAIRWISE, WORDMAP):
+        dbs[st] = pkg.KeyFrameDatabase(case["n_vocab"], case["n_slots"], max_words=2048)
+        dbs[st].set_strategy(st)
+        setup_db(case, dbs[st])
+    o = O.Kfdb(case["n_vocab"], case["n_slots"])
+    setup_db(case, o)
+    members = [k for k in range(100) if k != 7]        # BowVectors are re-set only outside the database, as
+                                                       # KeyFrame::ComputeBoW runs before KeyFrameDatabase::add
+    for db in (*dbs.values(), o):
+        db.add(members)
+    rng = np.random.default_rng(6)
+    queries = rng.choice(200, 8, replace=False).tolist()
+
+    def check(qid0):
+        for kind in (LOOP, COVIS, RELOC):
+            ids = list(range(qid0, qid0 + len(queries)))
+            ms = [0.0] * len(queries)
+            ex = [[] for _ in queries]
+            ref = [list(o.detect(kind, q, i, m_, e)) for q, i, m_, e in zip(queries, ids, ms, ex)]
+            for st, db in dbs.items():
+                got = [list(r) for r in db.detect(kind, queries, ids, ms, ex)]
+                assert got == ref, (st, kind)
+            qid0 += 100
+
+    check(5000)
+    # host form: 20 slots take other slots' BowVectors, one becomes empty
+    src = rng.integers(0, 200, 20)
+    for k, s_ in zip(range(100, 120), src):
+        w, v = case["bows"][int(s_)]
+        for db in (*dbs.values(), o):
+            db.set_bow(k, w, v)
+    for db in (*dbs.values(), o):
+        db.set_bow(7, [], [])
+        db.add(list(range(100, 120)) + [7])
+    check(6000)
+    # device form: 20 more slots (a (B, cap) batch, rows padded)
+    cap = 2048
+    dst = list(range(120, 140))
+    src = rng.integers(0, 200, 20)
+    W = np.zeros((20, cap), np.uint32)
+    V = np.zeros((20, cap), np.float64)
+    N = np.zeros(20, np.int32)
+    for i, s_ in enumerate(src):
+        w, v = case["bows"][int(s_)]
+        W[i, :len(w)], V[i, :len(w)], N[i] = w, v, len(w)
+        o.set_bow(dst[i], w, v)
+    for db in dbs.values():
+        db.set_bow_device(torch.tensor(dst, dtype=torch.int32, device="cuda"), torch.from_numpy(W.view(np.int32)).cuda(),
+                          torch.from_numpy(V).cuda(), torch.from_numpy(N).cuda())
+    torch.cuda.synchronize()
+    for db in (*dbs.values(), o):
+        db.add(dst)
+    check(7000)

@@ -17,7 +17,7 @@ from kfdb_cases import LOOP, RELOC, make_kfdb_case, setup_db
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("strategy", [1, 2])
+@pytest.mark.parametrize("strategy", [1, 2, 3])
 def test_three_threads_one_database(gpu, strategy):
     import torch
 
