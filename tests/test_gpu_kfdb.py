@@ -216,3 +216,17 @@ def test_wordmap_follows_set_bow(gpu):
     for db in (*dbs.values(), o):
         db.add(dst)
     check(7000)
+
+
+def test_wordmap_unsupported_above_2048_slots(gpu):
+    """A database of more than 2,048 slots keeps no word map: asking for it is ORBX_ERR_UNSUPPORTED, and AUTO still
+    answers (pairwise / inverted file)."""
+    import multiagent_orb_slam2_amd as pkg
+    g = pkg.KeyFrameDatabase(64, 3000, max_words=8)
+    with pytest.raises(pkg.OrbxError):
+        g.set_strategy(WORDMAP)
+    g.set_strategy(0)
+    g.set_bow(0, [1, 5], [0.5, 0.5])
+    g.set_bow(1, [1, 6], [0.5, 0.5])
+    g.add([1])
+    assert g.DetectRelocalizationCandidates(0, 1).tolist() == [1]
