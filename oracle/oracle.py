@@ -391,6 +391,21 @@ def project(mode, points, view, scale_factors, log_scale_factor):
     return out[:len(p)].view(np.uint8).reshape(-1, 40).copy()
 
 
+def found_in_frame(q_idx, owner):
+    """Tracking::SearchLocalPoints' skip set (src/Tracking.cc:1158-1183: the MapPoints in mCurrentFrame.mvpMapPoints
+    get mnLastFrameSeen = this frame and are skipped): after SearchByProjection(F, LastF) (src/ORBmatcher.cc:1330-1470)
+    MapPoint q is there iff it took keypoint q_idx[q] >= 0 and that keypoint's slot still holds it (the rotation
+    filter, :1448-1468, resets the slots it drops to NULL -- owner -2 here; a later query may hold the slot).
+    Sequential restatement, one query at a time.  Returns a bool array over q."""
+    q_idx = np.asarray(q_idx)
+    owner = np.asarray(owner)
+    out = np.zeros(len(q_idx), bool)
+    for q in range(len(q_idx)):
+        k = int(q_idx[q])
+        out[q] = k >= 0 and k < len(owner) and int(owner[k]) == q
+    return out
+
+
 def stereo_mappoints(kps, depth, twc, camera, scale_factors, flags):
     """MapPoints of one stereo frame (orc_stereo_mappoints): MAP_POINT_DTYPE records, SKIP where depth <= 0."""
     k = np.ascontiguousarray(kps, KP_DTYPE)

@@ -151,13 +151,13 @@ def test_local_fuse_vs_oracle(gpu):
 
 
 def test_proj_found_device_rule(gpu):
-    """orbx_proj_found_device against the host rule (multiagent.found_in_frame) on random assignments: unmatched
+    """orbx_proj_found_device against the oracle's rule (oracle.found_in_frame) on random assignments: unmatched
     queries (-1), queries whose keypoint the rotation filter released (owner -2) or re-assigned to another query, and
     the blocked bytes (owner >= 0); nq != n and one empty set."""
     import torch
 
     import multiagent_orb_slam2_amd as pkg
-    from multiagent_orb_slam2_amd.multiagent import found_in_frame
+    from oracle.oracle import found_in_frame
     rng = np.random.default_rng(7)
     S_, nq, n = 5, 700, 450
     q_idx = np.full((S_, nq), -1, np.int32)
