@@ -2274,7 +2274,7 @@ struct Extractor {
     bool desc_sb = false;
     int resize_tail = 0;              // ORBX_RESIZE_TAIL=l (>= 2): levels l .. n-1 in one k_resize_tail launch
     uint8_t* d_blur_diag = nullptr;   // one image's blurred pyramid, made on demand by orbx_extractor_copy_blurred_level
-    int desc_sets = 2;                // call k + 1's blur and DistributeOctTree write the other set (ORBX_DESC_SETS=1: one)
+    int desc_sets = 2;                // call k + 1's blur and DistributeOctTree write the other set
     unsigned long long dcalls = 0;    // while call k's describe reads its own (no wait on that describe)
     int dset_call[2] = {-1, -1};      // event-pool index of the last call that used each set
     uint32_t* d_cand_xy = nullptr;
@@ -2561,8 +2561,6 @@ int Extractor::configure(int r, int c, int batch) {
             want[k] = budget > lds ? (int)((budget - lds) / 7) : 0;
         }
         want[0] = std::min(want[0], kQtKeys0Max);
-        if (const char* v = std::getenv("ORBX_QT_KEYS0")) want[0] = std::atoi(v);   // diagnostics
-        if (const char* v = std::getenv("ORBX_QT_KEYS1")) want[1] = std::atoi(v);
         size_t maxl = lds;
         for (int k = 0; k < 2; ++k) {
             int kc = std::min(want[k], lcap[k]);
@@ -2570,9 +2568,6 @@ int Extractor::configure(int r, int c, int batch) {
             qt_keys[k] = std::max(kc, 0);
             maxl = std::max(maxl, lds + 7 * (size_t)qt_keys[k]);
         }
-        if (std::getenv("ORBX_QT_VERBOSE"))                                          // diagnostics
-            std::fprintf(stderr, "orbx: k_quadtree LDS %zu B + 7 B x keys %d (level 0) / %d (levels >= 1)\n", lds,
-                         qt_keys[0], qt_keys[1]);
         if (maxl > 64 * 1024)
             ORBX_HIP(hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)maxl));
     }
@@ -2672,10 +2667,7 @@ int Extractor::configure(int r, int c, int batch) {
     if ((st = dev_alloc(&d_pyr_ring, (size_t)pyr_ring * B * pyr_size))) return st;
     d_pyr = d_pyr_ring;
     ncalls = 0;
-    {
-        const char* v = std::getenv("ORBX_DESC_SETS");            // r5n: 2 sets +0.8 % in the step (two rounds)
-        desc_sets = (v && std::atoi(v) == 1) ? 1 : 2;
-    }
+    desc_sets = 2;                                                // r5n: 2 sets +0.8 % in the step against 1
     dcalls = 0;
     dset_call[0] = dset_call[1] = -1;
     if (!desc_sb && (st = dev_alloc(&d_blur, (size_t)desc_sets * B * pyr_size))) return st;
@@ -3000,8 +2992,8 @@ int orbx_extractor_create(int nfeatures, float scaleFactor, int nlevels, int ini
     hipError_t he = hipSetDevice(device);
     e->own_stream = true;
     // High priority for the side stream: its level-0 quadtree (128 long-lived workgroups) must not queue behind the
-    // launch stream's FAST grid (measured: 35.1k -> 37.6k frames/s).  ORBX_SIDE_PRIORITY overrides (A/B).
-    const int side_prio = std::getenv("ORBX_SIDE_PRIORITY") ? std::atoi(std::getenv("ORBX_SIDE_PRIORITY")) : -1;
+    // launch stream's FAST grid (measured: 35.1k -> 37.6k frames/s; at normal priority -1 %, r5bu).
+    const int side_prio = -1;
     const int cu_ex = std::getenv("ORBX_CU_EXCLUDE") ? std::atoi(std::getenv("ORBX_CU_EXCLUDE")) : 0;
     if (he == hipSuccess) he = create_stream_masked(&e->side, side_prio, cu_ex);
     for (auto& c : e->cev)

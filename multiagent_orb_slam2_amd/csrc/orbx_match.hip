@@ -2,13 +2,15 @@
 // orbx_match.hip — MI355X (gfx950) 256-bit Hamming matchers behind include/orbx.h.
 //
 //   k_hamming_pairs     ORBmatcher::DescriptorDistance over n row pairs        (src/ORBmatcher.cc:1649-1665)
-//   k_bf_tile/k_bf_merge tiled all-pairs match: 64 queries per workgroup (one per lane, descriptor in
+//   k_bf_mfma           all-pairs match on the matrix cores (default): popcount(q & t) as an i8 dot product of
+//                        the unpacked bits, v_mfma_i32_16x16x64_i8, best / second as keys.
+//   k_bf_tile/k_bf_merge the VALU form (ORBX_BF_MFMA=0): 64 queries per workgroup (one per lane, descriptor in
 //                        8 VGPRs), train descriptors staged through LDS in 256-row blocks and read as
 //                        wave-uniform broadcasts; v_xor + v_bcnt_u32_b32; per-(query, train-chunk)
-//                        partial best/second merged by a second launch.  No MFMA: popcount-bound.
-//   k_stereo_rows/k_stereo  Frame::ComputeStereoMatches descriptor search (src/Frame.cc:466-552): right
-//                        keypoints bucketed by row, then one wave per left keypoint over the rows its
-//                        band can reach, band/octave/disparity mask, packed (dist, index) wave min.
+//                        partial best/second merged by a second launch.
+//   k_stereo_rows/k_stereo_blk  Frame::ComputeStereoMatches descriptor search (src/Frame.cc:466-552): both
+//                        images' keypoints bucketed by row, then one workgroup per (pair, 8 left rows) with the
+//                        reachable right buckets staged in LDS, band/octave/disparity mask, packed (dist, index) min.
 //   k_bow_kfkf / k_bow_kff / k_triangulate   BoW-bucketed matchers (src/ORBmatcher.cc:161-290, 524-657,
 //                        659-825): one wave per FeatureVector node of the first view; the greedy
 //                        "already matched" state is node-local (a feature belongs to one node), so the
@@ -362,7 +364,7 @@ struct StereoArgs {
     int32_t* lrow_start;    // [batch][rows + 1]  left keypoints bucketed by vRowIndices row (int)y (k_stereo_blk)
     int32_t* lrow_idx;      // [batch][capacity]
     int32_t* best_idx; int32_t* best_dist;
-    int batch, nbx;         // k_stereo: images, workgroups per image (XCD-aware 1-D grid)
+    int batch, nbx;         // images; (unused by the row-block search)
 };
 
 // Counting sort of one image pair's right keypoints by row (the row table of Frame.cc:476-493, kept as
@@ -418,8 +420,8 @@ __global__ __launch_bounds__(kStereoRowsThreads) void k_stereo_rows(StereoArgs A
 // keypoint's own [vrow - band, vrow + band]) are staged in LDS once -- descriptor, x, the octave and the row band
 // [floor(y - 2s), ceil(y + 2s)] of :487-492 -- and each wave takes left keypoints of the block with lanes over the
 // staged candidates.  The per-candidate tests are the reference's (row band, octave +-1, disparity window), so the
-// candidate set and the (distance, index) minimum are exactly k_stereo's; a candidate outside a left keypoint's own
-// bucket window never passes its row test.  Replaces ~8 dependent HBM round trips per left keypoint by one staged
+// candidate set and the (distance, index) minimum are exactly the per-keypoint search's; a candidate outside a left
+// keypoint's own bucket window never passes its row test.  Replaces ~8 dependent HBM round trips per left keypoint by one staged
 // load per block.
 constexpr int kStereoRows = 8, kStereoRC = 256, kStereoLC = 64;
 __global__ __launch_bounds__(256) void k_stereo_blk(StereoArgs A, int nblk) {
@@ -502,49 +504,6 @@ __global__ __launch_bounds__(256) void k_stereo_blk(StereoArgs A, int nblk) {
             A.best_dist[ob + lidx[t]] = d;
             A.best_idx[ob + lidx[t]] = (d < thOrb) ? (int)(best & 0xfffff) : -1;        // :552
         }
-    }
-}
-
-__global__ __launch_bounds__(256) void k_stereo(StereoArgs A) {
-    const int item = xcd_item(xcd_chunk(A.nbx * A.batch));   // left keypoints of one pair on one XCD
-    if (item >= A.nbx * A.batch) return;
-    const int img = item / A.nbx;
-    const int iL = ((item - img * A.nbx) * blockDim.x + threadIdx.x) >> 6;
-    const int ln = lane_id();
-    const int nl = A.nl ? A.nl[img] : A.nl_fixed;
-    if (iL >= nl) return;
-    const size_t ob = (size_t)img * A.capacity;
-    const orbx_keypoint kL = A.kl[ob + iL];
-    const int vrow = (int)kL.y;                      // vRowIndices[vL] (:511)
-    const float uL = kL.x;
-    const float minU = uL - A.maxD, maxU = uL - 0.0f;
-    uint32_t best = 0xffffffffu;
-    if (vrow >= 0 && vrow < A.rows && !(maxU < 0)) {
-        uint4 a0, a1;
-        load_desc(A.dl + 32 * (ob + iL), a0, a1);
-        const int32_t* rs = A.row_start + (size_t)img * (A.rows + 1);
-        const int c0 = rs[max(vrow - A.band, 0)], c1 = rs[min(vrow + A.band, A.rows - 1) + 1];
-        for (int c = c0 + ln; c < c1; c += kWave) {
-            const int iR = A.row_idx[ob + c];
-            const orbx_keypoint kR = A.kr[ob + iR];
-            const float r = 2.0f * A.scale[kR.octave];                       // :487
-            const int maxr = (int)ceilf(kR.y + r), minr = (int)floorf(kR.y - r);
-            if (vrow < minr || vrow > maxr) continue;                        // row band (:491-492)
-            if (kR.octave < kL.octave - 1 || kR.octave > kL.octave + 1) continue;   // :533
-            if (!(kR.x >= minU && kR.x <= maxU)) continue;                   // :538
-            uint4 b0, b1;
-            load_desc(A.dr + 32 * (ob + iR), b0, b1);
-            const uint32_t key = ((uint32_t)hamming256(a0, a1, b0, b1) << 20) | (uint32_t)iR;
-            best = min(best, key);
-        }
-    }
-    best = wave_min_u32(best);
-    if (ln == 0) {
-        int d = (best == 0xffffffffu) ? kThHigh : (int)(best >> 20);
-        d = min(d, kThHigh);                                                // init TH_HIGH, strict < (:522-547)
-        const int thOrb = (kThHigh + kThLow) / 2;                           // :471
-        A.best_dist[ob + iL] = d;
-        A.best_idx[ob + iL] = (d < thOrb) ? (int)(best & 0xfffff) : -1;    // :552
     }
 }
 
@@ -1015,10 +974,8 @@ struct RefineArgs {
     int left_first, right_first;
     float bf, maxD;
     float* uright; float* depth; int32_t* sad;
-    int batch, nbx;         // k_stereo_sad: pairs, workgroups per pair (XCD-aware 1-D grid)
+    int batch, nbx;         // k_stereo_sad_rows: pairs, workgroups per pair (XCD-aware 1-D grid)
 };
-
-constexpr int kRefKp = 23;   // keypoints per 256-thread workgroup: 23 x 11 window shifts = 253 lanes
 
 __device__ __forceinline__ const uint8_t* pyr_level(const orbx_pyramid& P, int img, int l, int& step) {
     if (l == 0) {
@@ -1029,91 +986,14 @@ __device__ __forceinline__ const uint8_t* pyr_level(const orbx_pyramid& P, int i
     return P.levels + (size_t)img * P.image_stride + P.offset[l];
 }
 
-// Lane (keypoint q, shift inc) computes one 11x11 SAD of the centre-subtracted windows: every value is a
-// small integer, so the reference's float Mats and cv::norm(NORM_L1) give exactly this integer.  The
-// shift-(-5) lane of each keypoint then runs the reference's sequential tail (first minimum, parabola,
-// disparity test) in float with the same operation order.
-__global__ __launch_bounds__(256) void k_stereo_sad(RefineArgs A) {
-    __shared__ int dist[kRefKp][11];
-    const int item = xcd_item(xcd_chunk(A.nbx * A.batch));   // keypoints of one pair on one XCD
-    if (item >= A.nbx * A.batch) return;
-    const int img = item / A.nbx, t = threadIdx.x;
-    const int q = t / 11, inc = t % 11 - 5;
-    const int l = (item - img * A.nbx) * kRefKp + q;
-    if (q >= kRefKp || l >= A.capacity) return;          // whole keypoints only: no barrier below is split
-    const int nl = A.nl ? A.nl[img] : A.nl_fixed;
-    const size_t o = (size_t)img * A.capacity + l;
-    const int bi = l < nl ? A.best_idx[o] : -1;
-    constexpr int w = 5, W = 2 * w + 1, Ls = 5;
-    int oct = 0, ivL = 0, iuL = 0, iuR0 = 0;
-    float suR0 = 0.f, uL = 0.f;
-    bool ok = bi >= 0;
-    if (ok) {
-        const orbx_keypoint kp = A.kl[o];
-        oct = kp.octave;
-        uL = kp.x;
-        const float sf = A.L.inv_scale[oct];
-        const float uR0 = A.kr[(size_t)img * A.capacity + bi].x;
-        const float suL = __builtin_roundf(__fmul_rn(kp.x, sf)), svL = __builtin_roundf(__fmul_rn(kp.y, sf));
-        suR0 = __builtin_roundf(__fmul_rn(uR0, sf));
-        iuL = (int)suL; ivL = (int)svL; iuR0 = (int)suR0;
-        ok = !(ivL - w < 0 || ivL + w >= A.L.rows[oct] || iuL - w < 0 || iuL + w >= A.L.cols[oct] ||
-               ivL + w >= A.R.rows[oct] || iuR0 - Ls - w < 0);
-        const float endu = suR0 + (float)(Ls + w + 1);
-        ok = ok && !(suR0 < 0.f || endu >= (float)A.R.cols[oct]);   // iniu = scaleduR0 + L - w
-    }
-    if (ok) {
-        int sl, sr;
-        const uint8_t* IL = pyr_level(A.L, A.left_first + img, oct, sl) + (size_t)(ivL - w) * sl + (iuL - w);
-        const uint8_t* IR = pyr_level(A.R, A.right_first + img, oct, sr) + (size_t)(ivL - w) * sr + (iuR0 + inc - w);
-        const int cL = IL[(size_t)w * sl + w], cR = IR[(size_t)w * sr + w];
-        int d = 0;
-#pragma unroll
-        for (int y = 0; y < W; ++y) {
-#pragma unroll
-            for (int x = 0; x < W; ++x) d += abs((IL[(size_t)y * sl + x] - cL) - (IR[(size_t)y * sr + x] - cR));
-        }
-        dist[q][inc + Ls] = d;
-    }
-    __syncthreads();
-    if (inc != -Ls) return;
-    float ur = -1.0f, dp = -1.0f;
-    int sd = -1;
-    if (ok) {
-        int best = 0x7fffffff, binc = 0;
-        for (int k = -Ls; k <= Ls; ++k) {
-            const int d = dist[q][k + Ls];
-            if ((float)d < (float)best) { best = d; binc = k; }
-        }
-        if (binc != -Ls && binc != Ls) {
-            const float d1 = (float)dist[q][Ls + binc - 1], d2 = (float)dist[q][Ls + binc], d3 = (float)dist[q][Ls + binc + 1];
-            const float den = __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2)));
-            const float deltaR = __fdiv_rn(__fsub_rn(d1, d3), den);
-            if (!(deltaR < -1.f || deltaR > 1.f)) {
-                float bestuR = __fmul_rn(A.L.scale[oct], __fadd_rn(__fadd_rn(suR0, (float)binc), deltaR));
-                float disparity = __fsub_rn(uL, bestuR);
-                if (disparity >= 0.f && disparity < A.maxD) {
-                    if (disparity <= 0.f) {
-                        disparity = 0.01f;
-                        bestuR = (float)((double)uL - 0.01);
-                    }
-                    dp = __fdiv_rn(A.bf, disparity);
-                    ur = bestuR;
-                    sd = best;
-                }
-            }
-        }
-    }
-    A.uright[o] = ur;
-    A.depth[o] = dp;
-    A.sad[o] = sd;
-}
-
 // Row-parallel form: lane (keypoint k of 5 per wave, window row y of 11) loads its row of the left 11 x 11 window
 // (11 bytes) and of the right strip that every shift touches (21 bytes: columns iuR0 - 10 .. iuR0 + 10), once, and
 // computes its row's share of all 11 SADs -- |(L - cL) - (R - cR(inc))| = |(L + 512 - d) - (R + 512)| with
 // d = cL - cR(inc), two pixels per v_sad_u16 -- instead of one lane per (keypoint, shift) re-reading 242 single
-// bytes.  Row shares are summed through LDS; the tail (first minimum, parabola, disparity test) is k_stereo_sad's.
+// bytes (the first form, one lane per (keypoint, shift); removed in round 6).  Row shares are summed through LDS; each
+// keypoint's shift-(-5) lane then runs the reference's sequential tail (first minimum, parabola, disparity test) in
+// float with the same operation order.  Every value is a small integer, so the reference's float Mats and
+// cv::norm(NORM_L1) give exactly these integer SADs.
 constexpr int kSadKpWave = 5;
 __device__ __forceinline__ uint32_t pair16(uint32_t lo4, uint32_t hi4, int b) {   // bytes b, b+1 of (hi4:lo4) as u16x2
     return __builtin_amdgcn_perm(hi4, lo4, 0x0c000c00u | (uint32_t)b | ((uint32_t)(b + 1) << 16));
@@ -1511,10 +1391,7 @@ static size_t a256(size_t b) { return (b + 255) & ~(size_t)255; }
 // Grid: 256 queries per workgroup x train chunks x problems.  The train set of a problem is split into chunks so that
 // the whole launch has >= ~2048 workgroups when the problems are few (a single 2000 x 2000 match is 8 query blocks:
 // 64 chunks of 32 rows fill the chip; at many problems one chunk per problem suffices).
-static int bf_target_wgs() {   // workgroups the train chunking aims for (ORBX_BF_WGS, diagnostics)
-    static const int v = [] { const char* e = std::getenv("ORBX_BF_WGS"); return e ? std::max(1, std::atoi(e)) : 2048; }();
-    return v;
-}
+static int bf_target_wgs() { return 2048; }   // workgroups the train chunking aims for
 static int bf_chunks(int nq, int nt, int nprob) {
     const int qb = (nq + kBfQ - 1) / kBfQ;
     const int want = (bf_target_wgs() + qb * nprob - 1) / (qb * nprob);
@@ -1726,20 +1603,12 @@ static int stereo_launch(StereoArgs& A, int batch, int nl_max, hipStream_t s) {
     hipLaunchKernelGGL(k_stereo_rows, dim3(batch, A.lrow_start ? 2 : 1), dim3(kStereoRowsThreads),
                        (size_t)(A.rows + 1) * sizeof(int), s, A);
     A.batch = batch;
-    if (A.lrow_start) {                                   // row-block search (default)
-        const int nblk = (A.rows + kStereoRows - 1) / kStereoRows;
-        hipLaunchKernelGGL(k_stereo_blk, dim3(kXcds * xcd_chunk(nblk * batch)), dim3(256), 0, s, A, nblk);
-    } else {
-        A.nbx = (nl_max * 64 + 255) / 256;
-        hipLaunchKernelGGL(k_stereo, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
-    }
+    (void)nl_max;
+    // row-block search (the wave-per-keypoint form it replaced walked ~8 dependent HBM round trips per keypoint)
+    const int nblk = (A.rows + kStereoRows - 1) / kStereoRows;
+    hipLaunchKernelGGL(k_stereo_blk, dim3(kXcds * xcd_chunk(nblk * batch)), dim3(256), 0, s, A, nblk);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
-}
-
-static bool stereo_blocks() {   // ORBX_STEREO_BLK=0 selects the wave-per-keypoint k_stereo (A/B)
-    static const bool on = !(std::getenv("ORBX_STEREO_BLK") && std::atoi(std::getenv("ORBX_STEREO_BLK")) == 0);
-    return on;
 }
 
 static size_t stereo_scratch(int batch, int rows, int capacity) {
@@ -1762,10 +1631,8 @@ int orbx_stereo_match_batch_device(orbx_matcher* m, const orbx_keypoint* kl, con
     Bump bp{(uint8_t*)m->scratch};
     A.row_start = bp.take<int32_t>((size_t)batch * (rows + 1));
     A.row_idx = bp.take<int32_t>((size_t)batch * capacity);
-    if (stereo_blocks()) {
-        A.lrow_start = bp.take<int32_t>((size_t)batch * (rows + 1));
-        A.lrow_idx = bp.take<int32_t>((size_t)batch * capacity);
-    }
+    A.lrow_start = bp.take<int32_t>((size_t)batch * (rows + 1));
+    A.lrow_idx = bp.take<int32_t>((size_t)batch * capacity);
     A.kl = kl; A.dl = dl; A.nl = nl; A.kr = kr; A.dr = dr; A.nr = nr; A.capacity = capacity;
     A.best_idx = bi; A.best_dist = bd;
     return stereo_launch(A, batch, capacity, s);
@@ -1797,10 +1664,8 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
     int32_t* dbd = bp.take<int32_t>(cap);
     A.row_start = bp.take<int32_t>((size_t)rows + 1);
     A.row_idx = bp.take<int32_t>(cap);
-    if (stereo_blocks()) {
-        A.lrow_start = bp.take<int32_t>((size_t)rows + 1);
-        A.lrow_idx = bp.take<int32_t>(cap);
-    }
+    A.lrow_start = bp.take<int32_t>((size_t)rows + 1);
+    A.lrow_idx = bp.take<int32_t>(cap);
     hipStream_t s = m->own();
     // the four inputs into pinned staging laid out as the scratch (keypoints / descriptors of both sides are
     // contiguous there), one H2D copy; the two outputs come back the same way
@@ -1831,14 +1696,8 @@ int orbx_stereo_match(orbx_matcher* m, const orbx_keypoint* kpl, const uint8_t* 
 
 static int refine_launch(RefineArgs& A, int batch, hipStream_t s) {
     A.batch = batch;
-    static const bool rows = !(std::getenv("ORBX_SAD_ROWS") && std::atoi(std::getenv("ORBX_SAD_ROWS")) == 0);
-    if (rows) {
-        A.nbx = (A.capacity + 4 * kSadKpWave - 1) / (4 * kSadKpWave);
-        hipLaunchKernelGGL(k_stereo_sad_rows, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
-    } else {
-        A.nbx = (A.capacity + kRefKp - 1) / kRefKp;
-        hipLaunchKernelGGL(k_stereo_sad, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
-    }
+    A.nbx = (A.capacity + 4 * kSadKpWave - 1) / (4 * kSadKpWave);
+    hipLaunchKernelGGL(k_stereo_sad_rows, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
     hipLaunchKernelGGL(k_stereo_median, dim3(batch), dim3(1024), 0, s, A);
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;

@@ -1073,12 +1073,8 @@ int orbx_keyframe_prep_device(orbx_matcher* m, const orbx_keypoint* d_kps, const
                  "keyframe grid of %d cells x %d keypoints does not fit the one-workgroup form", (int)ncell, capacity);
     ORBX_REQUIRE(batch <= 65535, ORBX_ERR_UNSUPPORTED, "batch too large");
     ORBX_HIP(hipSetDevice(matcher_device(m)));
-    static const int threads = [] {                                           // ORBX_KF_PREP_THREADS (diagnostics)
-        const char* v = std::getenv("ORBX_KF_PREP_THREADS");
-        const int t = v ? std::atoi(v) : kProjThreads;
-        return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
-    }();
-    hipLaunchKernelGGL(k_kf_prep, dim3(batch), dim3(threads), lds, (hipStream_t)stream, d_kps, d_depth, d_counts, capacity, d_twc,
+    // 1,024 threads: r6q +0.4 % against the two launches; 256 threads -1.5 % (r6p: the workgroups run ~4x longer)
+    hipLaunchKernelGGL(k_kf_prep, dim3(batch), dim3(kProjThreads), lds, (hipStream_t)stream, d_kps, d_depth, d_counts, capacity, d_twc,
                        make_float4(camera[0], camera[1], camera[2], camera[3]), sc, nlevels, flags, d_points, grid, d_cell_start,
                        d_cell_idx);
     ORBX_HIP(hipGetLastError());
@@ -1120,16 +1116,10 @@ static void launch_grid_build(const orbx_grid& grid, const orbx_keypoint* d_kps,
                               int capacity, int batch, int32_t* d_cs, int32_t* d_ci, hipStream_t s) {
     const size_t ncell = (size_t)grid.cols * grid.rows;
     const size_t lds_c = ((ncell + 1) * 4 + 4 * (size_t)capacity + 15) & ~(size_t)15;
-    static const bool counting = !std::getenv("ORBX_GRID_BITONIC");          // diagnostics: the bitonic form
-    if (counting && ncell < 0xffff && capacity < 0xffff && lds_c <= 64 * 1024) {
-        static const int threads = [] {                                       // ORBX_GRID_THREADS (diagnostics)
-            const char* v = std::getenv("ORBX_GRID_THREADS");
-            const int t = v ? std::atoi(v) : kProjThreads;
-            return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
-        }();
+    if (ncell < 0xffff && capacity < 0xffff && lds_c <= 64 * 1024) {
         // r4at/r4au: 11 us against the bitonic form's 29 us per launch at least (the tracking frames' grids, 256 sets);
         // in the step the two are even (3.59-3.64 ms), 256 threads slower (3.66)
-        hipLaunchKernelGGL(k_grid_count, dim3(batch), dim3(threads), lds_c, s, d_kps, d_counts, n_fixed, capacity, grid,
+        hipLaunchKernelGGL(k_grid_count, dim3(batch), dim3(kProjThreads), lds_c, s, d_kps, d_counts, n_fixed, capacity, grid,
                            d_cs, d_ci);
         return;
     }
@@ -1190,19 +1180,14 @@ static int proj_search_batch(orbx_matcher* m, const orbx_proj_params* params, or
         // a grid built in the search needs 4 B per target keypoint of scratch after the entries (the assigning modes'
         // claim / own arrays serve) and the staged form, u16 cells and indices
         const size_t gscr = (d_grid_counts && !assigning) ? ((4 * N + 15) & ~(size_t)15) : 0;
-        // ORBX_PROJ_NA_STAGE=0 (diagnostics): the non-assigning modes walk cells and entries in memory, no staged LDS
-        static const bool na_stage = [] { const char* v = std::getenv("ORBX_PROJ_NA_STAGE"); return !v || std::atoi(v) != 0; }();
-        const bool staged = stage + core + gscr <= cap && (assigning || d_grid_counts || na_stage);
+        // (the non-assigning modes walking cells and entries in memory instead: 70.9k against 75.4k frames/s, r5bi)
+        const bool staged = stage + core + gscr <= cap;
         ORBX_REQUIRE(!d_grid_counts || (staged && ncell < 0xffff && N < 0xffff), ORBX_ERR_UNSUPPORTED,
                      "grid built in the search: %d keypoints, %d cells do not fit the staged plan", max_n, (int)ncell);
         const size_t used = core + (staged ? stage + gscr : 0);
-        static const int list_max = [] {                        // ORBX_PROJ_LIST_MAX (diagnostics): list slots per query
-            const char* v = std::getenv("ORBX_PROJ_LIST_MAX");
-            const int t = v ? std::atoi(v) : kProjListMax;
-            return (t >= 0 && t <= kProjListMax) ? t : kProjListMax;
-        }();
+        // list slots per query: as many as fit up to kProjListMax (0 / 2 / 4 / 8 slots: -7 % .. -0.1 %, r5bb)
         int kcap = 0;
-        if (assigning) kcap = (int)std::min<size_t>(list_max, (cap - used) / (4 * NQ));
+        if (assigning) kcap = (int)std::min<size_t>(kProjListMax, (cap - used) / (4 * NQ));
         const size_t lds = std::max<size_t>(used + (size_t)kcap * 4 * NQ, 16);
         auto kern = assigning ? (staged ? k_proj_search<true, true> : k_proj_search<false, true>)
                               : (staged ? k_proj_search<true, false> : k_proj_search<false, false>);
@@ -1210,18 +1195,8 @@ static int proj_search_batch(orbx_matcher* m, const orbx_proj_params* params, or
         // 1024-thread workgroups for the assigning modes (their fixed-point rounds are workgroup-wide), 512 for the
         // non-assigning ones (Fuse: a workgroup waits for a CU with as many free wave slots beside the front end;
         // r4ao/r4ap, step 3.66-3.69 ms at 1024, 3.59-3.63 at 512, 3.62-3.64 at 384 / 768, 256 unstable 3.62-3.87).
-        // ORBX_PROJ_NA_THREADS (diagnostics) overrides the latter.
-        static const int na_threads = [] {
-            const char* v = std::getenv("ORBX_PROJ_NA_THREADS");
-            const int t = v ? std::atoi(v) : 512;
-            return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
-        }();
-        static const int a_threads = [] {                       // ORBX_PROJ_A_THREADS (diagnostics): assigning modes
-            const char* v = std::getenv("ORBX_PROJ_A_THREADS");
-            const int t = v ? std::atoi(v) : kProjThreads;
-            return (t >= 64 && t <= kProjThreads && t % 64 == 0) ? t : kProjThreads;
-        }();
-        const int threads = assigning ? a_threads : na_threads;
+        // (assigning modes at 512 / 768 threads: -2 % / -0.4 %, r5al)
+        const int threads = assigning ? kProjThreads : 512;
         hipLaunchKernelGGL(kern, dim3(n_problems), dim3(threads), lds, s, P, grid, d_problems, (int)N, (int)NQ, kcap,
                            d_grid_counts);
     }

@@ -251,9 +251,7 @@ __global__ __launch_bounds__(kT) void k_vocab_aggregate(const int32_t* __restric
 struct Vocab {
     int k = 0, L = 0, scoring = 0, weighting = 0, device = 0;
     int n_nodes = 0, n_words = 0;
-    bool agg_wide = std::getenv("ORBX_VOCAB_AGG_WIDE") != nullptr;   // diagnostics: 1024-thread aggregation always
     int max_children = 0;              // the descent uses 16-lane groups when every node has <= 16 children
-    bool words_scalar = std::getenv("ORBX_VOCAB_SCALAR") != nullptr;   // diagnostics: one thread per descriptor
     hipStream_t stream = nullptr;      // lazy: own() on first host-API use
     std::once_flag stream_once;
     hipStream_t own() { return lazy_stream(stream, stream_once, device); }
@@ -341,7 +339,7 @@ static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 static int vocab_launch(orbx_vocab* v, const uint8_t* d_desc, const int32_t* d_counts, int n_fixed, int batch, int stride,
                         int levelsup, int32_t* d_word, double* d_wgt, int32_t* d_node, BowOut out, hipStream_t s, bool aggregate) {
     const int nid_level = v->L - levelsup;   // nid_level <= 0 -> root (node 0), as :1226
-    if (v->max_children <= 16 && !v->words_scalar)
+    if (v->max_children <= 16)
         hipLaunchKernelGGL(k_vocab_words16, dim3((stride + 15) / 16, batch), dim3(256), 0, s, v->dev, d_desc, d_counts, n_fixed,
                            stride, nid_level > 0 ? nid_level : -1, d_word, d_wgt, d_node);
     else
@@ -349,7 +347,7 @@ static int vocab_launch(orbx_vocab* v, const uint8_t* d_desc, const int32_t* d_c
                            stride, nid_level > 0 ? nid_level : -1, d_word, d_wgt, d_node);
     if (aggregate)
     {
-        const bool small = stride <= 2048 && !v->agg_wide;
+        const bool small = stride <= 2048;
         auto kagg = small ? k_vocab_aggregate<256, 2048> : k_vocab_aggregate<kVocabAggThreads, kVocabMaxSet>;
         hipLaunchKernelGGL(kagg, dim3(batch, 2), dim3(small ? 256 : kVocabAggThreads), 0, s, d_counts, n_fixed, stride, d_word,
                            d_wgt, d_node, v->weighting, v->scoring, out);

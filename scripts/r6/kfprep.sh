@@ -1,3 +1,4 @@
+# (ORBX_KF_PREP_THREADS, used by r6q below, was removed after the measurement: 1,024 threads fixed)
 # r6p: k_kf_prep (a new keyframe's MapPoints + grid in one workgroup) -- its tests, then A/B against the two-launch form
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp

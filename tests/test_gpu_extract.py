@@ -233,6 +233,45 @@ def test_fast_kernels_bit_exact(gpu, monkeypatch, form):
                 kb, desc[i, :n], ref["kps"], ref["desc"])
 
 
+@pytest.mark.parametrize("form", ["desc_sb", "resize_tail4", "resize_tail3"])
+def test_opt_in_forms_bit_exact(gpu, monkeypatch, form):
+    """The measured-and-opt-in forms stay bit-exact against the oracle: k_describe_sb (ORBX_DESC_SB=1: the Gaussian blur
+    taken at the BRIEF sample points on the matrix cores, no blurred pyramid; ORBextractor.cc:108-147, 1085-1086) and
+    k_resize_tail (ORBX_RESIZE_TAIL=l: levels l..7 of ComputePyramid, :1107-1132, in one launch of one workgroup per
+    image) -- KITTI size batched, odd and tiny sizes, uniform noise, a 5-level 1.3-scale pyramid, and the host API."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    env = {"desc_sb": ("ORBX_DESC_SB", "1"), "resize_tail4": ("ORBX_RESIZE_TAIL", "4"),
+           "resize_tail3": ("ORBX_RESIZE_TAIL", "3")}[form]
+    monkeypatch.setenv(*env)
+    for shape, nf, kw in (((375, 1242), 2000, {}), ((377, 1243), 800, {}), ((40, 40), 100, {}),
+                          ((480, 752), 1500, dict(nlevels=5, scale=1.3, ini=25, mn=10)),
+                          ((375, 1242), 2000, dict(noise=True))):
+        if kw.get("noise"):
+            imgs = np.stack([S.uniform_noise_image(960 + i) for i in range(2)])
+        else:
+            imgs = np.stack([S.kitti_like_image(920 + i, rows=shape[0], cols=shape[1]) for i in range(2)])
+        ex = pkg.ORBextractor(nf, kw.get("scale", 1.2), kw.get("nlevels", 8), kw.get("ini", 20), kw.get("mn", 7))
+        kps, desc, cnt = ex.extract_batch_device(torch.from_numpy(imgs).cuda())
+        torch.cuda.synchronize()
+        kps, desc, cnt = kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy()
+        for i in range(len(imgs)):
+            ref = O.extract(imgs[i], nfeatures=nf, scale_factor=kw.get("scale", 1.2), nlevels=kw.get("nlevels", 8),
+                            ini_th=kw.get("ini", 20), min_th=kw.get("mn", 7))
+            n = int(cnt[i])
+            kb = kps[i, :n].copy().view(pkg.KP_DTYPE).reshape(-1)
+            assert np.array_equal(kb, ref["kps"]) and np.array_equal(desc[i, :n], ref["desc"]), _diff_report(
+                kb, desc[i, :n], ref["kps"], ref["desc"])
+    ex = pkg.ORBextractor(1500, 1.2, 8, 20, 7, device=0)
+    img = S.kitti_like_image(990)
+    k, d = ex(img)
+    ref = O.extract(img, nfeatures=1500)
+    assert np.array_equal(k, ref["kps"]) and np.array_equal(d, ref["desc"]), _diff_report(k, d, ref["kps"], ref["desc"])
+    ex.close()
+
+
 @pytest.mark.parametrize("form", ["default", "unmerged", "forked", "no_graph"])
 def test_host_api_schedules(gpu, monkeypatch, form):
     """orbx_extract (host image in, host keypoints out) on each of its schedules: the default (a hipGraph replay, every
