@@ -1600,6 +1600,8 @@ static int stereo_common(orbx_matcher* m, StereoArgs& A, const float* scale, int
 }
 
 static int stereo_launch(StereoArgs& A, int batch, int nl_max, hipStream_t s) {
+    // the row-block search reads both images' row buckets: every caller carves lrow_* from its scratch
+    ORBX_REQUIRE(A.row_start && A.row_idx && A.lrow_start && A.lrow_idx, ORBX_ERR_ARG, "stereo search without row buckets");
     hipLaunchKernelGGL(k_stereo_rows, dim3(batch, A.lrow_start ? 2 : 1), dim3(kStereoRowsThreads),
                        (size_t)(A.rows + 1) * sizeof(int), s, A);
     A.batch = batch;
@@ -1764,6 +1766,8 @@ int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, con
     int32_t* dbd = bp.take<int32_t>(cap);
     A.row_start = bp.take<int32_t>((size_t)PL.rows[0] + 1);
     A.row_idx = bp.take<int32_t>(cap);
+    A.lrow_start = bp.take<int32_t>((size_t)PL.rows[0] + 1);
+    A.lrow_idx = bp.take<int32_t>(cap);
     float* dur = bp.take<float>(cap);
     float* ddp = bp.take<float>(cap);
     int32_t* dsad = bp.take<int32_t>(cap);
