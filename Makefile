@@ -37,11 +37,13 @@ qtprof: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/qtprof/liborbx.so build/qtprof/orbx_extract.o $(filter-out $(SRC)/orbx_extract.o,$(OBJS)) -ldl
 .PHONY: qtprof
 
-# A/B builds of compile-time variants: make variant V=name D="-DORBX_X=1" -> build/<name>/liborbx.so (ORBX_LIB=...)
+# A/B builds of compile-time variants: make variant V=name D="-DORBX_X=1" [VF=orbx_proj] -> build/<name>/liborbx.so
+# (ORBX_LIB=...); VF is the source file the defines apply to (default orbx_extract)
+VF ?= orbx_extract
 variant: $(OBJS)
 	mkdir -p build/$(V)
-	$(HIPCC) $(HIPFLAGS) $(D) -c $(SRC)/orbx_extract.hip -o build/$(V)/orbx_extract.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/$(V)/liborbx.so build/$(V)/orbx_extract.o $(filter-out $(SRC)/orbx_extract.o,$(OBJS)) -ldl
+	$(HIPCC) $(HIPFLAGS) $(D) -c $(SRC)/$(VF).hip -o build/$(V)/$(VF).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/$(V)/liborbx.so build/$(V)/$(VF).o $(filter-out $(SRC)/$(VF).o,$(OBJS)) -ldl
 .PHONY: variant
 
 # ThreadSanitizer on the host code of liborbx and the native concurrency driver (tests/native/concurrency.cpp):

@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--cu-exclude", type=int, default=int(os.environ.get("ORBX_CU_EXCLUDE", "0")),
                     help="front-end and stereo streams leave this many CUs out of their CU mask (the keyframe stream keeps "
                          "every CU), so the keyframe path's small kernels are not starved; 0 = plain streams")
+    ap.add_argument("--kf-cus", type=int, default=0,
+                    help="diagnostics: the keyframe stream keeps only this many CUs in its CU mask (0 = every CU)")
     ap.add_argument("--distinct", type=int, default=0,
                     help="distinct synthetic stereo pairs per rank, tiled to the batch (0: the largest multiple of 5 <= the "
                          "batch -- 255 at 256 -- so every agent's keyframes show the same scenes, see main())")
@@ -1001,7 +1003,9 @@ def main():
     # keyframe stream at normal priority measured +0.8 % (76.5k -> 77.1k frames/s, three rounds; +0.9 % at 8 emulated
     # agents).  (A stream of another priority gets a hardware queue of its own; two same-priority streams can share one,
     # which in round 3 serialised front-end and keyframe kernels, +0.5 ms per step.)  ORBX_KF_PRIORITY overrides.
-    kf_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("ORBX_KF_PRIORITY", "0")))
+    kf_prio = int(os.environ.get("ORBX_KF_PRIORITY", "0"))
+    kf_stream = (pkg.orbx.create_stream(dev.index, kf_prio, -args.kf_cus) if args.kf_cus > 0 else
+                 torch.cuda.Stream(dev, priority=kf_prio))
     track_stream = mk() if args.track_stream == "own" else None
     kf_done = [None] * NS
     n_kf = max(1, B // KF_EVERY)

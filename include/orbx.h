@@ -58,7 +58,8 @@ int orbx_device_check(int device);
 
 /* A non-blocking stream on `device` (no reference counterpart: scheduling plumbing for device-API callers).
  * cu_exclude > 0 leaves that many compute units out of the stream's CU mask (spread over the device), so that
- * streams without a mask keep free CUs for latency-bound work; cu_exclude <= 0: a plain stream of `priority`.
+ * streams without a mask keep free CUs for latency-bound work; cu_exclude = -k keeps only k CUs (every (CUs / k)-th);
+ * cu_exclude = 0: a plain stream of `priority`.
  * *out receives the hipStream_t. */
 int orbx_stream_create(int device, int priority, int cu_exclude, void** out);
 int orbx_stream_destroy(void* stream);

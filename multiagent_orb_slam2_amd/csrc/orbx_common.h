@@ -20,16 +20,26 @@ namespace orbx {
 // streams without the mask (the keyframe path's chain of small kernels) finds free CUs while the front end fills the
 // rest.  CU masks carry no priority; cu_exclude <= 0 gives a plain stream of the given priority.
 inline hipError_t create_stream_masked(hipStream_t* s, int priority, int cu_exclude) {
-    if (cu_exclude <= 0) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, priority);
+    if (cu_exclude == 0 || cu_exclude < -4096) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, priority);
     int dev = 0, n = 0;
     hipError_t he = hipGetDevice(&dev);
     if (he == hipSuccess) he = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     if (he != hipSuccess) return he;
+    uint32_t mask[32] = {};
+    const int words = (n + 31) / 32;
+    if (words > 32) return hipErrorInvalidValue;
+    if (cu_exclude < 0) {                              // keep -cu_exclude CUs, every (n / keep)-th one
+        const int keep = -cu_exclude;
+        if (keep >= n) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, priority);
+        const int k = n / keep;
+        int kept = 0;
+        for (int i = 0; i < n && kept < keep; ++i)
+            if (i % k == 0) { mask[i >> 5] |= 1u << (i & 31); ++kept; }
+        return hipExtStreamCreateWithCUMask(s, (uint32_t)words, mask);
+    }
     if (cu_exclude >= n) return hipErrorInvalidValue;
     const int k = n / cu_exclude;
-    uint32_t mask[32] = {};
-    int words = (n + 31) / 32, dropped = 0;
-    if (words > 32) return hipErrorInvalidValue;
+    int dropped = 0;
     for (int i = 0; i < n; ++i) {
         const bool drop = dropped < cu_exclude && (i % k) == k - 1;
         dropped += drop ? 1 : 0;

@@ -821,6 +821,9 @@ __global__ __launch_bounds__(256) void k_stereo_mappoints(const orbx_keypoint* _
 // workgroup: the MapPoints as k_stereo_mappoints, then the counting grid of k_grid_count (the same CSR arrays) -- one
 // launch of one 256-thread workgroup per keyframe instead of a MapPoint launch and a 1,024-thread grid launch
 // (LocalMapping's new keyframes).  Dynamic LDS: k_grid_count's.
+#ifndef ORBX_KF_PREP_WG
+#define ORBX_KF_PREP_WG 1024   // threads per keyframe workgroup (compile-time; A/B builds: make variant)
+#endif
 __global__ __launch_bounds__(kProjThreads) void k_kf_prep(const orbx_keypoint* __restrict__ kps, const float* __restrict__ depth,
                                                  const int32_t* __restrict__ counts, int capacity, const float* __restrict__ twc,
                                                  float4 cam, ProjScales sc, int nlevels, int flags,
@@ -1074,7 +1077,7 @@ int orbx_keyframe_prep_device(orbx_matcher* m, const orbx_keypoint* d_kps, const
     ORBX_REQUIRE(batch <= 65535, ORBX_ERR_UNSUPPORTED, "batch too large");
     ORBX_HIP(hipSetDevice(matcher_device(m)));
     // 1,024 threads: r6q +0.4 % against the two launches; 256 threads -1.5 % (r6p: the workgroups run ~4x longer)
-    hipLaunchKernelGGL(k_kf_prep, dim3(batch), dim3(kProjThreads), lds, (hipStream_t)stream, d_kps, d_depth, d_counts, capacity, d_twc,
+    hipLaunchKernelGGL(k_kf_prep, dim3(batch), dim3(ORBX_KF_PREP_WG), lds, (hipStream_t)stream, d_kps, d_depth, d_counts, capacity, d_twc,
                        make_float4(camera[0], camera[1], camera[2], camera[3]), sc, nlevels, flags, d_points, grid, d_cell_start,
                        d_cell_idx);
     ORBX_HIP(hipGetLastError());
