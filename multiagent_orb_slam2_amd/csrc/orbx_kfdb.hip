@@ -1027,12 +1027,18 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
     alloc((void**)&db->d_if_slot, 4 * S * W);
     alloc((void**)&db->d_scan, 4 * ((size_t)(n_vocab_words + 1 + kScanChunk - 1) / kScanChunk + 1));
     alloc((void**)&db->d_members, 4 * S);
-    if (wmap_enabled() && max_slots <= kWmapMaxSlots) {
-        const size_t dw = ((size_t)max_slots + 31) / 32;
-        if ((size_t)n_vocab_words * dw * 4 <= ((size_t)1 << 30)) {
-            db->wmap_dw = (int)dw;
-            alloc((void**)&db->d_wmap, (size_t)n_vocab_words * dw * 4);
+    if (e == hipSuccess && wmap_enabled() && max_slots <= kWmapMaxSlots) {
+        // optional: a database whose word map does not fit in device memory works without it (pairwise / inverted file)
+        const size_t dw = ((size_t)max_slots + 31) / 32, bytes = (size_t)n_vocab_words * dw * 4;
+        if (bytes <= ((size_t)1 << 30) && hipMalloc((void**)&db->d_wmap, bytes) == hipSuccess) {
+            if (hipMemset(db->d_wmap, 0, bytes) == hipSuccess) {
+                db->wmap_dw = (int)dw;
+            } else {
+                (void)hipFree(db->d_wmap);
+                db->d_wmap = nullptr;
+            }
         }
+        (void)hipGetLastError();                     // a refused allocation leaves no sticky error behind
     }
     for (int k = 0; k < 3; ++k) {
         alloc((void**)&db->d_q[k], 8 * S);

@@ -1414,6 +1414,8 @@ class KeyframeFusionEngine:
         """The ring slots the last pack() reserved for this step's world * n packets (rank-major), as a (world*n, P)
         uint8 device tensor aliasing them (orbx_fusion_pack_device's d_exchange_dst): all-gather into it, then
         commit(None) -- no gathered buffer and no copy into the ring (70 MB per step at 8 agents)."""
+        if not getattr(self, "_dst", None):
+            raise OrbxError(ORBX_ERR_ARG, "exchange_view() before pack(): no ring slots are reserved")
         return _device_view(self._dst, (self.world * self._pending, self.packet_bytes), self.device, self)
 
     def commit(self, exchanged=None, outputs=None, stream=None):

@@ -97,6 +97,8 @@ def test_native_fusion_two_agents_one_gpu(gpu):
                                     agent=r, world=W) for r in range(W)]
     odb = O.Kfdb(v.info()["n_words"], SLOTS)
     kf_id, total_real, cross = 1, 0, 0
+    with pytest.raises(pkg.OrbxError):
+        eng[1].exchange_view()                   # nothing reserved before the first pack()
     for step in range(3):
         sends = []
         for r in range(W):
