@@ -167,12 +167,21 @@ __global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, size_
 #endif
 constexpr int kResizeBand = ORBX_RESIZE_BAND, kResizeStrip = 256;
 struct ResizeVec {       // per level >= 1 with every group's span <= 8 bytes
-    const int* xb;       // [groups]
+    const int* xb;       // [groups] (host copy; the kernel recomputes it from sxs, resize_xb)
     const uint4* sel;    // [groups] perm selectors of the 4 columns
     const uint4* coef;   // [groups] a0 | a1 << 16 of the 4 columns
     const int4* yrow;    // [h] y0, y1, b0, b1
     int groups;
+    double sxs;          // source / destination width, as the host tables use it
 };
+
+// A group's window column, hx0[4 g] of the host tables (the OpenCV 3.2 fixed-point INTER_LINEAR x map: fx = (float)((x +
+// 0.5) * sxs - 0.5), floor, clamped to [0, sw - 1]) recomputed in the lane with the same IEEE operations: the window
+// loads then need no table load in front of them (one dependent memory round trip less per wave).
+__device__ __forceinline__ int resize_xb(int g, double sxs, int sw) {
+    const float fx = __double2float_rn(__dsub_rn(__dmul_rn(__dadd_rn((double)(4 * g), 0.5), sxs), 0.5));
+    return min(max((int)floorf(fx), 0), sw - 1);
+}
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void resize_window(const uint8_t* __restrict__ row, int xb, int sw, bool fast, uint32_t& lo,
@@ -220,7 +229,7 @@ __device__ __forceinline__ void resize4_item(uint8_t* __restrict__ pyr, size_t p
                                              const ResizeVec& t, int strip, int band, int img) {
     const int g = strip * (kResizeStrip / 4) + lane_id();
     if (g >= t.groups) return;
-    const int xb = t.xb[g];
+    const int xb = resize_xb(g, t.sxs, sw);
     const uint4 sel = t.sel[g], coef = t.coef[g];
     const bool fast = xb + 8 <= sw;
     const int x = 4 * g;
@@ -2657,7 +2666,7 @@ int Extractor::configure(int r, int c, int batch) {
             ORBX_HIP(hipMemcpy(vm + bx + 2 * bs, yr.data(), by, hipMemcpyHostToDevice));
             ResizeVec rv;
             rv.xb = (const int*)vm; rv.sel = (const uint4*)(vm + bx); rv.coef = (const uint4*)(vm + bx + bs);
-            rv.yrow = (const int4*)(vm + bx + 2 * bs); rv.groups = G;
+            rv.yrow = (const int4*)(vm + bx + 2 * bs); rv.groups = G; rv.sxs = sxs;
             rvec[l] = rv;
         }
     }
