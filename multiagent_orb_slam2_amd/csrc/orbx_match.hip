@@ -10,7 +10,8 @@
 //                        partial best/second merged by a second launch.
 //   k_stereo_rows/k_stereo_blk  Frame::ComputeStereoMatches descriptor search (src/Frame.cc:466-552): both
 //                        images' keypoints bucketed by row, then one workgroup per (pair, 8 left rows) with the
-//                        reachable right buckets staged in LDS, band/octave/disparity mask, packed (dist, index) min.
+//                        reachable right buckets staged in LDS, band/octave/disparity mask, packed (dist, index) min;
+//                        k_stereo (one wave per left keypoint) for the host API's single frame.
 //   k_bow_kfkf / k_bow_kff / k_triangulate   BoW-bucketed matchers (src/ORBmatcher.cc:161-290, 524-657,
 //                        659-825): one wave per FeatureVector node of the first view; the greedy
 //                        "already matched" state is node-local (a feature belongs to one node), so the
@@ -364,7 +365,7 @@ struct StereoArgs {
     int32_t* lrow_start;    // [batch][rows + 1]  left keypoints bucketed by vRowIndices row (int)y (k_stereo_blk)
     int32_t* lrow_idx;      // [batch][capacity]
     int32_t* best_idx; int32_t* best_dist;
-    int batch, nbx;         // images; (unused by the row-block search)
+    int batch, nbx;         // images; k_stereo: workgroups per image (XCD-aware 1-D grid)
 };
 
 // Counting sort of one image pair's right keypoints by row (the row table of Frame.cc:476-493, kept as
@@ -504,6 +505,53 @@ __global__ __launch_bounds__(256) void k_stereo_blk(StereoArgs A, int nblk) {
             A.best_dist[ob + lidx[t]] = d;
             A.best_idx[ob + lidx[t]] = (d < thOrb) ? (int)(best & 0xfffff) : -1;        // :552
         }
+    }
+}
+
+// Per-keypoint form of the same search (one wave per left keypoint, lanes over the right buckets its band reaches, the
+// same tests and (distance, index) minimum): the host API's single stereo frame (orbx_compute_stereo_matches), where
+// the row-block form's 47 staged workgroups per frame cost more latency than ~2,000 independent waves (r6zn: the host
+// call's stereo 0.060 -> 0.077 ms with the row-block form).
+__global__ __launch_bounds__(256) void k_stereo(StereoArgs A) {
+    const int item = xcd_item(xcd_chunk(A.nbx * A.batch));   // left keypoints of one pair on one XCD
+    if (item >= A.nbx * A.batch) return;
+    const int img = item / A.nbx;
+    const int iL = ((item - img * A.nbx) * blockDim.x + threadIdx.x) >> 6;
+    const int ln = lane_id();
+    const int nl = A.nl ? A.nl[img] : A.nl_fixed;
+    if (iL >= nl) return;
+    const size_t ob = (size_t)img * A.capacity;
+    const orbx_keypoint kL = A.kl[ob + iL];
+    const int vrow = (int)kL.y;                      // vRowIndices[vL] (:511)
+    const float uL = kL.x;
+    const float minU = uL - A.maxD, maxU = uL - 0.0f;
+    uint32_t best = 0xffffffffu;
+    if (vrow >= 0 && vrow < A.rows && !(maxU < 0)) {
+        uint4 a0, a1;
+        load_desc(A.dl + 32 * (ob + iL), a0, a1);
+        const int32_t* rs = A.row_start + (size_t)img * (A.rows + 1);
+        const int c0 = rs[max(vrow - A.band, 0)], c1 = rs[min(vrow + A.band, A.rows - 1) + 1];
+        for (int c = c0 + ln; c < c1; c += kWave) {
+            const int iR = A.row_idx[ob + c];
+            const orbx_keypoint kR = A.kr[ob + iR];
+            const float r = 2.0f * A.scale[kR.octave];                       // :487
+            const int maxr = (int)ceilf(kR.y + r), minr = (int)floorf(kR.y - r);
+            if (vrow < minr || vrow > maxr) continue;                        // row band (:491-492)
+            if (kR.octave < kL.octave - 1 || kR.octave > kL.octave + 1) continue;   // :533
+            if (!(kR.x >= minU && kR.x <= maxU)) continue;                   // :538
+            uint4 b0, b1;
+            load_desc(A.dr + 32 * (ob + iR), b0, b1);
+            const uint32_t key = ((uint32_t)hamming256(a0, a1, b0, b1) << 20) | (uint32_t)iR;
+            best = min(best, key);
+        }
+    }
+    best = wave_min_u32(best);
+    if (ln == 0) {
+        int d = (best == 0xffffffffu) ? kThHigh : (int)(best >> 20);
+        d = min(d, kThHigh);                                                // init TH_HIGH, strict < (:522-547)
+        const int thOrb = (kThHigh + kThLow) / 2;                           // :471
+        A.best_dist[ob + iL] = d;
+        A.best_idx[ob + iL] = (d < thOrb) ? (int)(best & 0xfffff) : -1;    // :552
     }
 }
 
@@ -1600,15 +1648,19 @@ static int stereo_common(orbx_matcher* m, StereoArgs& A, const float* scale, int
 }
 
 static int stereo_launch(StereoArgs& A, int batch, int nl_max, hipStream_t s) {
-    // the row-block search reads both images' row buckets: every caller carves lrow_* from its scratch
-    ORBX_REQUIRE(A.row_start && A.row_idx && A.lrow_start && A.lrow_idx, ORBX_ERR_ARG, "stereo search without row buckets");
+    // with left-row buckets (lrow_*): the row-block search (batches: ~8 dependent HBM round trips per keypoint fewer);
+    // without: one wave per left keypoint (the host API's single frame, where latency rules)
+    ORBX_REQUIRE(A.row_start && A.row_idx && (!A.lrow_start) == (!A.lrow_idx), ORBX_ERR_ARG, "stereo search without row buckets");
     hipLaunchKernelGGL(k_stereo_rows, dim3(batch, A.lrow_start ? 2 : 1), dim3(kStereoRowsThreads),
                        (size_t)(A.rows + 1) * sizeof(int), s, A);
     A.batch = batch;
-    (void)nl_max;
-    // row-block search (the wave-per-keypoint form it replaced walked ~8 dependent HBM round trips per keypoint)
-    const int nblk = (A.rows + kStereoRows - 1) / kStereoRows;
-    hipLaunchKernelGGL(k_stereo_blk, dim3(kXcds * xcd_chunk(nblk * batch)), dim3(256), 0, s, A, nblk);
+    if (A.lrow_start) {
+        const int nblk = (A.rows + kStereoRows - 1) / kStereoRows;
+        hipLaunchKernelGGL(k_stereo_blk, dim3(kXcds * xcd_chunk(nblk * batch)), dim3(256), 0, s, A, nblk);
+    } else {
+        A.nbx = (nl_max * 64 + 255) / 256;
+        hipLaunchKernelGGL(k_stereo, dim3(kXcds * xcd_chunk(A.nbx * batch)), dim3(256), 0, s, A);
+    }
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }
@@ -1766,8 +1818,8 @@ int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, con
     int32_t* dbd = bp.take<int32_t>(cap);
     A.row_start = bp.take<int32_t>((size_t)PL.rows[0] + 1);
     A.row_idx = bp.take<int32_t>(cap);
-    A.lrow_start = bp.take<int32_t>((size_t)PL.rows[0] + 1);
-    A.lrow_idx = bp.take<int32_t>(cap);
+    (void)bp.take<int32_t>((size_t)PL.rows[0] + 1);      // (the scratch layout keeps the batch form's left-row buckets;
+    (void)bp.take<int32_t>(cap);                          // this single-frame path searches per keypoint: none needed)
     float* dur = bp.take<float>(cap);
     float* ddp = bp.take<float>(cap);
     int32_t* dsad = bp.take<int32_t>(cap);
