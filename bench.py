@@ -536,6 +536,11 @@ def host_api_rate(pkg, cfg, lefts, rights, n_frames, device):
                    "enqueued together from one thread) + orbx_compute_stereo_matches, host buffers, one frame per call")
     out["two_threads"] = dict(run(two_threads), path="Python ctypes: orbx_extract(L) and orbx_extract(R) on two threads "
                                                      "(as Frame.cc:78-81) + orbx_compute_stereo_matches")
+
+    def frame(i):
+        m.StereoFrame(ex_l, ex_r, lefts[i % len(lefts)], rights[i % len(rights)], cfg["bf"], b)
+    out["stereo_frame"] = dict(run(frame), path="Python ctypes: orbx_stereo_frame (both extractions + ComputeStereoMatches "
+                                                "in one call, the stereo search on the extractions' device outputs)")
     pool.shutdown()
     # the same per-call path from a C++ caller (the reference's own language): scripts/micro/host_api_bench.cpp, built
     # by build() into build/host_api_bench, run as a child process on the same GPU

@@ -82,6 +82,15 @@ int matcher_scratch(orbx_matcher* m, size_t bytes, void** base, void** stream);
 // the call's stream recorded as the last scratch user, which the next call's stream waits for (Matcher::reserve_on).
 void matcher_acquire(orbx_matcher* m);
 void matcher_release(orbx_matcher* m, hipStream_t s, bool used);
+// Internal entry points across the library's files (not in include/orbx.h): the halves of an extractor's host call and
+// where its device outputs are (orbx_extract.hip), for orbx_stereo_frame (orbx_match.hip).
+extern "C" {
+int orbx_internal_extract_begin(orbx_extractor* e, const uint8_t* image, int rows, int cols, size_t step);
+int orbx_internal_extract_end(orbx_extractor* e, orbx_keypoint* kps, uint8_t* desc, int capacity, int* n_out);
+int orbx_internal_host_outputs(orbx_extractor* e, const orbx_keypoint** kps, const uint8_t** desc, const int32_t** count,
+                               int* capacity, void** stream);
+}
+
 struct MatcherLease {
     orbx_matcher* m;
     hipStream_t s = nullptr;

@@ -3288,6 +3288,26 @@ int orbx_extract_pair(orbx_extractor* left, orbx_extractor* right, const uint8_t
     return st ? st : sr;
 }
 
+// The host call's halves and its device outputs, for orbx_stereo_frame (orbx_match.hip; declared in orbx_common.h, not a
+// public entry point): the stereo search of a Frame reads the extractions' device outputs where extract_begin leaves
+// them (count, keypoints, descriptors of the whole capacity), on the extractor's own stream.
+int orbx_internal_extract_begin(orbx_extractor* e, const uint8_t* image, int rows, int cols, size_t step) {
+    return extract_begin(e, image, rows, cols, step);
+}
+int orbx_internal_extract_end(orbx_extractor* e, orbx_keypoint* kps, uint8_t* desc, int capacity, int* n_out) {
+    return extract_end(e, kps, desc, capacity, n_out);
+}
+int orbx_internal_host_outputs(orbx_extractor* e, const orbx_keypoint** kps, const uint8_t** desc, const int32_t** count,
+                               int* capacity, void** stream) {
+    ORBX_REQUIRE(e && e->d_hblk, ORBX_ERR_ARG, "no host call in flight on this extractor");
+    *kps = e->d_kps;
+    *desc = e->d_desc;
+    *count = e->d_cnt;
+    *capacity = e->out_capacity;
+    *stream = (void*)e->own();
+    return ORBX_OK;
+}
+
 int orbx_extractor_status(orbx_extractor* e, int* flags, int reset) {
     ORBX_REQUIRE(e && flags, ORBX_ERR_ARG, "null argument");
     *flags = 0;

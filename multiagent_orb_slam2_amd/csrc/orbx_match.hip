@@ -1384,6 +1384,7 @@ struct Matcher {
     size_t scratch_bytes = 0;
     std::recursive_mutex mtx;
     hipEvent_t last_op = nullptr;
+    hipEvent_t frame_ev[2] = {nullptr, nullptr};   // orbx_stereo_frame: the two extractions' ends (lazy)
     bool last_op_set = false;            // last_op recorded after the previous call (multi-stream mode)
     bool have_last = false, multi = false;
     hipStream_t last_stream = nullptr;   // the previous call's stream
@@ -1562,6 +1563,8 @@ int orbx_matcher_destroy(orbx_matcher* m) {
     (void)hipSetDevice(m->device);
     (void)hipDeviceSynchronize();                                // device calls on callers' streams use the scratch
     if (m->last_op) (void)hipEventDestroy(m->last_op);
+    for (hipEvent_t ev : m->frame_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (m->scratch) (void)hipFree(m->scratch);
     if (m->h_stage) (void)hipHostFree(m->h_stage);
     if (m->stream) (void)hipStreamDestroy(m->stream);
@@ -1786,6 +1789,100 @@ int orbx_stereo_refine_batch_device(orbx_matcher* m, const orbx_keypoint* kl, co
     A.bf = bf; A.maxD = bf / b;
     A.uright = uright; A.depth = depth; A.sad = (int32_t*)m->scratch;
     return refine_launch(A, batch, s);
+}
+
+int orbx_stereo_frame(orbx_matcher* m, orbx_extractor* left, orbx_extractor* right, const uint8_t* image_left,
+                      size_t step_left, const uint8_t* image_right, size_t step_right, int rows, int cols,
+                      orbx_keypoint* kps_left, uint8_t* desc_left, int capacity_left, int* n_left, orbx_keypoint* kps_right,
+                      uint8_t* desc_right, int capacity_right, int* n_right, float bf, float b, float* uright, float* depth,
+                      int* n_stereo) {
+    ORBX_REQUIRE(m && left && right && left != right && n_left && n_right && n_stereo, ORBX_ERR_ARG,
+                 "a matcher, two distinct extractors and the three counts are required");
+    *n_left = *n_right = *n_stereo = 0;
+    if (!image_left || !image_right || rows <= 0 || cols <= 0) {
+        // an empty side: the extractions as orbx_extract_pair gives them, no stereo (ComputeStereoMatches finds nothing)
+        return orbx_extract_pair(left, right, image_left, step_left, image_right, step_right, rows, cols, kps_left, desc_left,
+                                 capacity_left, n_left, kps_right, desc_right, capacity_right, n_right);
+    }
+    int st;
+    if ((st = orbx_internal_extract_begin(left, image_left, rows, cols, step_left))) return st;
+    auto finish_left = [&]() { int n = 0; (void)orbx_internal_extract_end(left, nullptr, nullptr, 1 << 30, &n); };
+    if ((st = orbx_internal_extract_begin(right, image_right, rows, cols, step_right))) { finish_left(); return st; }
+    const orbx_keypoint *dkl = nullptr, *dkr = nullptr;
+    const uint8_t *ddl = nullptr, *ddr = nullptr;
+    const int32_t *dcl = nullptr, *dcr = nullptr;
+    int capl = 0, capr = 0;
+    void *sl = nullptr, *sr = nullptr;
+    orbx_pyramid PL, PR;
+    StereoArgs A{};
+    st = orbx_internal_host_outputs(left, &dkl, &ddl, &dcl, &capl, &sl);
+    if (!st) st = orbx_internal_host_outputs(right, &dkr, &ddr, &dcr, &capr, &sr);
+    if (!st) st = orbx_extractor_pyramid_device(left, &PL);
+    if (!st) st = orbx_extractor_pyramid_device(right, &PR);
+    if (!st && (PL.nlevels != PR.nlevels || capl != capr || capl > 4096)) {
+        set_error("left/right extractors differ (levels %d / %d, capacity %d / %d) or capacity > 4096", PL.nlevels, PR.nlevels,
+                  capl, capr);
+        st = ORBX_ERR_ARG;
+    }
+    if (!st) st = stereo_common(m, A, PL.scale, PL.nlevels, PL.rows[0], bf, b);
+    if (st) {
+        finish_left();
+        int n = 0;
+        (void)orbx_internal_extract_end(right, nullptr, nullptr, 1 << 30, &n);
+        return st;
+    }
+    // the stereo search on the matcher's stream once both extractions are done, straight on their device outputs (the
+    // two-call form copies them to the host and back): one wait per side, one result copy, one synchronisation
+    ORBX_HIP(hipSetDevice(m->device));
+    hipStream_t s = m->own();
+    for (hipEvent_t& ev : m->frame_ev)
+        if (!ev) ORBX_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    ORBX_HIP(hipEventRecord(m->frame_ev[0], (hipStream_t)sl));
+    ORBX_HIP(hipEventRecord(m->frame_ev[1], (hipStream_t)sr));
+    ORBX_HIP(hipStreamWaitEvent(s, m->frame_ev[0], 0));
+    ORBX_HIP(hipStreamWaitEvent(s, m->frame_ev[1], 0));
+    const int cap = capl;
+    const size_t bytes = 2 * a256(4 * (size_t)cap) + stereo_scratch(1, PL.rows[0], cap) + 3 * a256(4 * (size_t)cap);
+    {
+        MatcherLease lease_(m, s);
+        if ((st = m->reserve(bytes))) return st;
+        Bump bp{(uint8_t*)m->scratch};
+        int32_t* dbi = bp.take<int32_t>(cap);
+        int32_t* dbd = bp.take<int32_t>(cap);
+        A.row_start = bp.take<int32_t>((size_t)PL.rows[0] + 1);
+        A.row_idx = bp.take<int32_t>(cap);
+        (void)bp.take<int32_t>((size_t)PL.rows[0] + 1);      // the batch form's left-row buckets: unused (per-keypoint search)
+        (void)bp.take<int32_t>(cap);
+        float* dur = bp.take<float>(cap);
+        float* ddp = bp.take<float>(cap);
+        int32_t* dsad = bp.take<int32_t>(cap);
+        A.kl = dkl; A.dl = ddl; A.kr = dkr; A.dr = ddr; A.nl = dcl; A.nr = dcr; A.capacity = cap;
+        A.best_idx = dbi; A.best_dist = dbd;
+        if ((st = stereo_launch(A, 1, cap, s))) return st;
+        RefineArgs R{};
+        R.kl = dkl; R.nl = dcl; R.kr = dkr; R.best_idx = dbi; R.capacity = cap;
+        R.L = PL; R.R = PR; R.left_first = 0; R.right_first = 0;
+        R.bf = bf; R.maxD = bf / b;
+        R.uright = dur; R.depth = ddp; R.sad = dsad;
+        if ((st = refine_launch(R, 1, s))) return st;
+        const size_t out_bytes = (size_t)((uint8_t*)ddp - (uint8_t*)dur) + 4 * (size_t)cap;
+        if ((st = m->stage_host(out_bytes))) return st;
+        ORBX_HIP(hipMemcpyAsync(m->h_stage, dur, out_bytes, hipMemcpyDeviceToHost, s));
+        // the extractions' results (their streams were synchronised by extract_end); the stereo copy runs meanwhile
+        const int stl = orbx_internal_extract_end(left, kps_left, desc_left, capacity_left, n_left);
+        const int str = orbx_internal_extract_end(right, kps_right, desc_right, capacity_right, n_right);
+        ORBX_HIP(hipStreamSynchronize(s));
+        if (stl) return stl;
+        if (str) return str;
+        ORBX_REQUIRE((uright && depth) || *n_left == 0, ORBX_ERR_ARG, "null uright / depth");
+        const int nl = *n_left;
+        std::memcpy(uright, m->h_stage, 4 * (size_t)nl);
+        std::memcpy(depth, m->h_stage + ((uint8_t*)ddp - (uint8_t*)dur), 4 * (size_t)nl);
+        int n = 0;
+        for (int i = 0; i < nl; ++i) n += depth[i] > 0;
+        *n_stereo = n;
+    }
+    return ORBX_OK;
 }
 
 int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, const orbx_extractor* right, const orbx_keypoint* kpl,

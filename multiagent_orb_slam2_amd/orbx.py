@@ -237,6 +237,8 @@ def load_library(path: str = LIB_PATH):
     lib.orbx_stereo_refine_batch_device.argtypes = [vp, vp, vp, vp, vp, i32, i32, C.POINTER(Pyramid), i32,
                                                     C.POINTER(Pyramid), i32, f32, f32, vp, vp, vp]
     lib.orbx_compute_stereo_matches.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, i32, f32, f32, vp, vp, C.POINTER(i32)]
+    lib.orbx_stereo_frame.argtypes = [vp, vp, vp, vp, C.c_size_t, vp, C.c_size_t, i32, i32, vp, vp, i32, C.POINTER(i32), vp, vp,
+                                      i32, C.POINTER(i32), f32, f32, vp, vp, C.POINTER(i32)]
     lib.orbx_search_by_bow_kfkf.argtypes = [vp, vp, vp, vp, i32, FeatVec, vp, vp, vp, i32, FeatVec, vp,
                                             C.POINTER(i32)]
     lib.orbx_search_by_bow_kff.argtypes = [vp, vp, vp, vp, i32, FeatVec, vp, vp, i32, FeatVec, vp, C.POINTER(i32)]
@@ -657,6 +659,30 @@ class ORBmatcher:
         _check(self._lib.orbx_compute_stereo_matches(self._h, left._h, right._h, _p(kl), _p(dl), len(kl), _p(kr), _p(dr),
                                                      len(kr), bf, b, _p(ur), _p(dp), C.byref(n)))
         return ur, dp
+
+    def StereoFrame(self, left, right, image_left, image_right, bf, b):
+        """The stereo Frame constructor's ORB work in one call (orbx_stereo_frame: src/Frame.cc:78-81 ExtractORB x2,
+        :101 ComputeStereoMatches): ((keypoints, descriptors) left, (keypoints, descriptors) right, mvuRight, mvDepth),
+        the values of extract_pair + ComputeStereoMatches without the keypoints' host round trip between them."""
+        il = np.ascontiguousarray(image_left, np.uint8)
+        ir = np.ascontiguousarray(image_right, np.uint8)
+        assert il.ndim == 2 and il.shape == ir.shape, "two 8UC1 images of one size expected"
+        rows, cols = il.shape
+        if il.size == 0:
+            e = (np.zeros(0, KP_DTYPE), np.zeros((0, 32), np.uint8))
+            return e, e, np.zeros(0, np.float32), np.zeros(0, np.float32)
+        kl, dl = left._staging(rows, cols)
+        kr, dr = right._staging(rows, cols)
+        ur = np.empty(len(kl), np.float32)
+        dp = np.empty(len(kl), np.float32)
+        nl, nr, ns = C.c_int(), C.c_int(), C.c_int()
+        _check(self._lib.orbx_stereo_frame(self._h, left._h, right._h, _p(il), il.strides[0], _p(ir), ir.strides[0], rows,
+                                           cols, _p(kl), _p(dl), len(kl), C.byref(nl), _p(kr), _p(dr), len(kr), C.byref(nr),
+                                           bf, b, _p(ur), _p(dp), C.byref(ns)))
+        left._last_shape = right._last_shape = (rows, cols)
+        n = nl.value
+        return ((kl[:n].copy(), dl[:n].copy()), (kr[: nr.value].copy(), dr[: nr.value].copy()), ur[:n].copy(),
+                dp[:n].copy())
 
     def stereo_refine_batch_device(self, kl, nl, kr, best_idx, left_pyramid, left_first, right_pyramid, right_first,
                                    bf, b, stream=None, out=None):

@@ -6,7 +6,8 @@
 //   host_api_bench <liborbx.so> [frames=300] [rows=375] [cols=1242] [nfeatures=2000]
 //
 // Prints one JSON line: frames/s from the mean, and median / p95 / max of the frame, left-extract, right-extract
-// and stereo phases (ms); "pair": the same frames through orbx_extract_pair from one thread.
+// and stereo phases (ms); "pair": the same frames through orbx_extract_pair from one thread; "stereo_frame": through
+// orbx_stereo_frame (extractions + stereo search in one call).
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -134,6 +135,25 @@ int main(int argc, char** argv) {
                       "\"mean\": %.4f}}", 1e3 / P.mean, P.med, P.p95, P.max, P.mean);
         pair = buf;
     }
+    // ... and through orbx_stereo_frame (both extractions and the stereo search in one call), when the library has it
+    std::string sframe = "null";
+    if (auto sf = (decltype(&::orbx_stereo_frame))dlsym(h, "orbx_stereo_frame")) {
+        std::vector<double> t_sf;
+        for (int f = -10; f < frames; ++f) {
+            const int k = (f + kDistinct * 4) % kDistinct;
+            int nl = 0, nr = 0, ns = 0;
+            const auto t0 = clk::now();
+            const int st = sf(m, exl, exr, L[k].data(), (size_t)cols, R[k].data(), (size_t)cols, rows, cols, kl.data(), dl.data(),
+                              cap, &nl, kr.data(), dr.data(), cap, &nr, bf, bf / fx, ur.data(), depth.data(), &ns);
+            if (st) { ++bad; std::fprintf(stderr, "stereo_frame %d: %s\n", f, orbx_last_error()); }
+            if (f >= 0) t_sf.push_back(ms_since(t0));
+        }
+        const Stats P = stats(t_sf);
+        char buf[256];
+        std::snprintf(buf, sizeof buf, "{\"frames_per_s\": %.1f, \"frame_ms\": {\"median\": %.4f, \"p95\": %.4f, \"max\": %.4f, "
+                      "\"mean\": %.4f}}", 1e3 / P.mean, P.med, P.p95, P.max, P.mean);
+        sframe = buf;
+    }
     const Stats F = stats(t_frame), A = stats(t_left), B = stats(t_right), S = stats(t_stereo);
     std::vector<int> order(t_frame.size());                      // the slowest frames, for outlier attribution
     for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
@@ -145,9 +165,10 @@ int main(int argc, char** argv) {
     std::printf("{\"lib\": \"%s\", \"frames\": %d, \"frames_per_s\": %.1f, \"frame_ms\": {\"median\": %.4f, \"p95\": %.4f, "
                 "\"max\": %.4f, \"mean\": %.4f}, \"extract_left_ms\": {\"median\": %.4f, \"p95\": %.4f}, "
                 "\"extract_right_ms\": {\"median\": %.4f, \"p95\": %.4f}, \"stereo_ms\": {\"median\": %.4f, \"p95\": %.4f}, "
-                "\"errors\": %d, \"slowest\": [%s], \"warmup_frames\": 10, \"warmup_ms_max\": %.4f, \"pair\": %s}\n",
+                "\"errors\": %d, \"slowest\": [%s], \"warmup_frames\": 10, \"warmup_ms_max\": %.4f, \"pair\": %s, "
+                "\"stereo_frame\": %s}\n",
                 argv[1], frames, 1e3 / F.mean, F.med, F.p95, F.max, F.mean, A.med, A.p95, B.med, B.p95, S.med, S.p95, bad, slow.c_str(), warm_max,
-                pair.c_str());
+                pair.c_str(), sframe.c_str());
     orbx_matcher_destroy(m);
     orbx_extractor_destroy(exl);
     orbx_extractor_destroy(exr);

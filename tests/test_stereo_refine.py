@@ -105,6 +105,33 @@ def test_gpu_compute_stereo_matches_host(gpu, seed, shape, nf):
 
 
 @pytest.mark.gpu
+def test_gpu_stereo_frame_one_call(gpu):
+    """orbx_stereo_frame (the stereo Frame constructor's extractions + ComputeStereoMatches in one call, the search on the
+    extractions' device outputs) equals the oracle and the two-call form, frame after frame on the same objects, over
+    two image sizes (a reconfiguration between them) and an empty pair."""
+    import multiagent_orb_slam2_amd as pkg
+    exl, exr = pkg.ORBextractor(2000, 1.2, 8, 20, 7), pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    m = pkg.ORBmatcher()
+    t = O.tables(2000)
+    for i, shape in enumerate([(375, 1242), (375, 1242), (240, 420), (375, 1242)]):
+        l = S.kitti_like_image(40 + i, rows=shape[0], cols=shape[1])
+        r = S.shifted_right_view(l, 40 + i)
+        (kl, dl), (kr, dr), ur, dp = m.StereoFrame(exl, exr, l, r, BF, B)
+        a, b = O.extract(l, nfeatures=2000, want_pyramid=True), O.extract(r, nfeatures=2000, want_pyramid=True)
+        assert np.array_equal(kl, a["kps"]) and np.array_equal(dl, a["desc"]), i
+        assert np.array_equal(kr, b["kps"]) and np.array_equal(dr, b["desc"]), i
+        rur, rdp = O.compute_stereo_matches(a, b, t["scale"], t["inv_scale"], shape[0], BF, B)
+        assert ur.tobytes() == rur.tobytes() and dp.tobytes() == rdp.tobytes(), i
+        assert (dp > 0).sum() > 0.2 * len(kl)
+        (kl2, dl2), (kr2, dr2) = pkg.extract_pair(exl, exr, l, r)
+        ur2, dp2 = m.ComputeStereoMatches(exl, exr, kl2, dl2, kr2, dr2, BF, B)
+        assert ur.tobytes() == ur2.tobytes() and dp.tobytes() == dp2.tobytes(), i
+    e = np.zeros((0, 0), np.uint8)
+    (kl, _), (kr, _), ur, dp = m.StereoFrame(exl, exr, e, e, BF, B)
+    assert len(kl) == len(kr) == len(ur) == len(dp) == 0
+
+
+@pytest.mark.gpu
 def test_gpu_stereo_refine_batch_device(gpu):
     import torch
 
