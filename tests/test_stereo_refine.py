@@ -129,6 +129,12 @@ def test_gpu_stereo_frame_one_call(gpu):
     e = np.zeros((0, 0), np.uint8)
     (kl, _), (kr, _), ur, dp = m.StereoFrame(exl, exr, e, e, BF, B)
     assert len(kl) == len(kr) == len(ur) == len(dp) == 0
+    with pytest.raises(pkg.OrbxError):                  # one extractor for both sides is refused, as orbx_extract_pair
+        m.StereoFrame(exl, exl, l, r, BF, B)
+    # the objects stay usable after a refused call
+    (kl, dl), (kr, dr), ur, dp = m.StereoFrame(exl, exr, l, r, BF, B)
+    (kl2, dl2), (kr2, dr2) = pkg.extract_pair(exl, exr, l, r)
+    assert np.array_equal(kl, kl2) and np.array_equal(dr, dr2)
 
 
 @pytest.mark.gpu
