@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--batch", type=int, default=256, help="stereo frames per GPU per step (512 images per extractor launch; "
-                                                          "r3ag: 128 / 192 / 256 frames -> 65.7k / 66.4k / 66.9k frames/s)")
+                                                          "r6zv/r6zw: 128 / 192 / 256 / 384 / 512 frames -> 75.4k / 78.0k / 78.6k / 76.8k / 76.6k frames/s)")
     ap.add_argument("--desc-stream", type=int, default=int(os.environ.get("ORBX_BENCH_DESC_STREAM", "1")),
                     help="1: the extractor's descriptor stage on the stereo stream (orbx_extract_batch_device_split), "
                          "so step k+1's front end overlaps step k's descriptor stage; 2: on a stream of its own; 0: on "
