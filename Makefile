@@ -8,7 +8,12 @@ HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -fno-f
 HDRS := include/orbx.h $(SRC)/orbx_common.h $(SRC)/orbx_pattern.h $(SRC)/orbx_sincos.h
 OBJS := $(SRC)/orbx_extract.o $(SRC)/orbx_match.o $(SRC)/orbx_vocab.o $(SRC)/orbx_proj.o $(SRC)/orbx_kfdb.o $(SRC)/orbx_fusion.o
 
-all: $(PKG)/liborbx.so oracle build/host_api_bench
+all: $(PKG)/liborbx.so oracle build/host_api_bench build/concurrency
+
+# native multi-thread check of the C-ABI (tests/test_gpu_native_concurrency.py runs it; make tsan = the TSan form)
+build/concurrency: tests/native/concurrency.cpp include/orbx.h $(PKG)/liborbx.so
+	mkdir -p build
+	g++ -O2 -std=c++17 -pthread $< -L$(PKG) -lorbx -Wl,-rpath,'$$ORIGIN/../$(PKG)' -o $@
 
 # native per-call latency driver (bench.py host_api.native; dlopens a liborbx.so by path)
 build/host_api_bench: scripts/micro/host_api_bench.cpp include/orbx.h

@@ -252,10 +252,6 @@ int orbx_stereo_refine_batch_device(orbx_matcher* m, const orbx_keypoint* d_kpl,
                                     int right_first, float bf, float b, float* d_uright, float* d_depth,
                                     void* stream);
 
-/* Frame::ComputeStereoMatches (src/Frame.cc:466-639) as one host call: the keypoints/descriptors the two
- * extractors returned from their last host orbx_extract, whose pyramids (image 0) it reads, like the
- * reference reads mpORBextractorLeft/Right->mvImagePyramid.  uright/depth: nl floats (-1 = none);
- * *n_stereo = keypoints with depth. */
 /* The stereo Frame constructor's ORB work in one call (src/Frame.cc:61-117: ExtractORB(0) / ExtractORB(1) on two
  * threads, :78-81, then ComputeStereoMatches, :101): the two extractions of orbx_extract_pair, then the stereo search
  * and SAD refinement on their device outputs (no host round trip of the keypoints between them), host keypoints /
@@ -266,6 +262,10 @@ int orbx_stereo_frame(orbx_matcher* m, orbx_extractor* left, orbx_extractor* rig
                       orbx_keypoint* kps_left, uint8_t* desc_left, int capacity_left, int* n_left, orbx_keypoint* kps_right,
                       uint8_t* desc_right, int capacity_right, int* n_right, float bf, float b, float* uright, float* depth,
                       int* n_stereo);
+/* Frame::ComputeStereoMatches (src/Frame.cc:466-639) as one host call: the keypoints/descriptors the two
+ * extractors returned from their last host orbx_extract, whose pyramids (image 0) it reads, like the
+ * reference reads mpORBextractorLeft/Right->mvImagePyramid.  uright/depth: nl floats (-1 = none);
+ * *n_stereo = keypoints with depth. */
 int orbx_compute_stereo_matches(orbx_matcher* m, const orbx_extractor* left, const orbx_extractor* right,
                                 const orbx_keypoint* kpl, const uint8_t* desc_l, int nl, const orbx_keypoint* kpr,
                                 const uint8_t* desc_r, int nr, float bf, float b, float* uright, float* depth,

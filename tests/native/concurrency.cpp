@@ -1,8 +1,9 @@
 // Native concurrency check of the C-ABI (the reference's threading: Frame.cc:78-81 runs the left and right
 // ORBextractor::operator() on two std::threads; Tracking, LocalMapping, LoopClosing and MapFusion call ORBmatcher from
-// their own threads).  Two extractors on two threads and four matchers on four threads, each repeating its call and
-// comparing every result with its single-threaded first result (bit-exact).  Built with ThreadSanitizer on the host
-// code (make tsan; scripts/tsan_gpu.sh runs it on the GPU box); exit status = number of mismatches.
+// their own threads).  Two extractors on two threads and four matchers on four threads, three agents' stereo Frames on
+// three threads, and the KeyFrameDatabase's threads, each repeating its call and comparing every result with its
+// single-threaded first result (bit-exact).  Plain build: build/concurrency (make; tests/test_gpu_native_concurrency.py);
+// with ThreadSanitizer on the host code: make tsan, scripts/tsan_gpu.sh.  Exit status = number of mismatches.
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -171,6 +172,85 @@ int kfdb_concurrency(int reps) {
     return mismatch + errors + reader_bad;
 }
 
+// ---- Stereo frames of several agents at once: each agent's Tracking thread builds its stereo Frames (Frame.cc:61-117,
+// the two extractions of :78-81 and ComputeStereoMatches :101) with its own left / right extractors and matcher, the
+// multi-agent system running one Tracking per agent in one process.  Agent a alternates orbx_stereo_frame with
+// orbx_extract_pair + orbx_compute_stereo_matches on its own images; every result must equal its first one.
+struct StereoOut {
+    Extraction l, r;
+    std::vector<float> ur, dp;
+    int ns = 0;
+};
+
+int stereo_frame_concurrency(int reps, int rows, int cols) {
+    constexpr int kAgents = 3;
+    orbx_extractor* ex[kAgents][2] = {};
+    orbx_matcher* mt[kAgents] = {};
+    std::vector<uint8_t> im[kAgents][2];
+    const float bf = 386.1448f, b = 0.537166f;   // KITTI 00-02 stereo baseline x fx, baseline (m)
+    int st = 0;
+    for (int a = 0; a < kAgents && !st; ++a) {
+        for (int s = 0; s < 2 && !st; ++s) {
+            st = orbx_extractor_create(2000, 1.2f, 8, 20, 7, 0, &ex[a][s]);
+        }
+        // the right view: the left one shifted by a disparity of 6 + 3a px (right x = left x - d)
+        im[a][0] = make_image(rows, cols, 10 + a);
+        im[a][1] = im[a][0];
+        const int d = 6 + 3 * a;
+        for (int y = 0; y < rows; ++y)
+            for (int x = 0; x < cols; ++x) im[a][1][(size_t)y * cols + x] = im[a][0][(size_t)y * cols + std::min(x + d, cols - 1)];
+        if (!st) st = orbx_matcher_create(0.6f, 1, 0, &mt[a]);
+    }
+    auto run = [&](int a, bool one_call, StereoOut& o) {
+        const int cap = orbx_extractor_max_keypoints(ex[a][0], rows, cols);
+        if (cap < 0) return cap;
+        o.l.kps.assign(cap, orbx_keypoint{}); o.l.desc.assign((size_t)cap * 32, 0);
+        o.r.kps.assign(cap, orbx_keypoint{}); o.r.desc.assign((size_t)cap * 32, 0);
+        o.ur.assign(cap, 0.f); o.dp.assign(cap, 0.f);
+        if (one_call)
+            return orbx_stereo_frame(mt[a], ex[a][0], ex[a][1], im[a][0].data(), (size_t)cols, im[a][1].data(), (size_t)cols,
+                                     rows, cols, o.l.kps.data(), o.l.desc.data(), cap, &o.l.n, o.r.kps.data(),
+                                     o.r.desc.data(), cap, &o.r.n, bf, b, o.ur.data(), o.dp.data(), &o.ns);
+        int e = orbx_extract_pair(ex[a][0], ex[a][1], im[a][0].data(), (size_t)cols, im[a][1].data(), (size_t)cols, rows,
+                                  cols, o.l.kps.data(), o.l.desc.data(), cap, &o.l.n, o.r.kps.data(), o.r.desc.data(), cap,
+                                  &o.r.n);
+        if (!e)
+            e = orbx_compute_stereo_matches(mt[a], ex[a][0], ex[a][1], o.l.kps.data(), o.l.desc.data(), o.l.n,
+                                            o.r.kps.data(), o.r.desc.data(), o.r.n, bf, b, o.ur.data(), o.dp.data(), &o.ns);
+        return e;
+    };
+    auto equal = [](const StereoOut& x, const StereoOut& y) {
+        return same(x.l, y.l) && same(x.r, y.r) && x.ns == y.ns &&
+               std::memcmp(x.ur.data(), y.ur.data(), sizeof(float) * x.l.n) == 0 &&
+               std::memcmp(x.dp.data(), y.dp.data(), sizeof(float) * x.l.n) == 0;
+    };
+    StereoOut ref[kAgents];
+    for (int a = 0; a < kAgents && !st; ++a) st = run(a, true, ref[a]);
+    int bad[kAgents] = {}, errors = 0;
+    if (st) {
+        std::fprintf(stderr, "stereo frame setup: %s\n", orbx_last_error());
+        errors = 1;
+    } else {
+        std::vector<std::thread> th;
+        for (int a = 0; a < kAgents; ++a)
+            th.emplace_back([&, a] {
+                for (int r = 0; r < reps; ++r) {
+                    StereoOut o;
+                    if (run(a, r & 1, o) || !equal(o, ref[a])) ++bad[a];
+                }
+            });
+        for (auto& t : th) t.join();
+    }
+    int total = errors;
+    for (int a = 0; a < kAgents; ++a) total += bad[a];
+    std::printf("stereo frames: %d agents x %d frames on %d threads (%d / %d / %d stereo matches), %d mismatches\n", kAgents,
+                reps, kAgents, ref[0].ns, ref[1].ns, ref[2].ns, total);
+    for (auto& m : mt) orbx_matcher_destroy(m);
+    for (auto& p : ex)
+        for (auto& e : p) orbx_extractor_destroy(e);
+    return total;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -226,5 +306,5 @@ int main(int argc, char** argv) {
                 2 * reps, ref[0].n, ref[1].n, 4 * reps, total);
     for (auto& m : mt) orbx_matcher_destroy(m);
     for (auto& e : ex) orbx_extractor_destroy(e);
-    return total + kfdb_concurrency(reps);
+    return total + stereo_frame_concurrency(reps, rows, cols) + kfdb_concurrency(reps);
 }
