@@ -1806,8 +1806,21 @@ int orbx_stereo_frame(orbx_matcher* m, orbx_extractor* left, orbx_extractor* rig
     }
     int st;
     if ((st = orbx_internal_extract_begin(left, image_left, rows, cols, step_left))) return st;
-    auto finish_left = [&]() { int n = 0; (void)orbx_internal_extract_end(left, nullptr, nullptr, 1 << 30, &n); };
-    if ((st = orbx_internal_extract_begin(right, image_right, rows, cols, step_right))) { finish_left(); return st; }
+    // Until both extract_end calls below have run, an early return still finishes the extractions in flight (their
+    // streams synchronised, results dropped): the next call on an extractor packs its image into the pinned staging
+    // this call's upload may still be reading.
+    struct Finish {
+        orbx_extractor* e[2];
+        ~Finish() {
+            if (!e[0] && !e[1]) return;
+            const std::string why = orbx_last_error();                // the error being returned, not the drop's
+            for (orbx_extractor* x : e)
+                if (x) { int n = 0; (void)orbx_internal_extract_end(x, nullptr, nullptr, 1 << 30, &n); }
+            set_error("%s", why.c_str());
+        }
+    } pending{{left, nullptr}};
+    if ((st = orbx_internal_extract_begin(right, image_right, rows, cols, step_right))) return st;
+    pending.e[1] = right;
     const orbx_keypoint *dkl = nullptr, *dkr = nullptr;
     const uint8_t *ddl = nullptr, *ddr = nullptr;
     const int32_t *dcl = nullptr, *dcr = nullptr;
@@ -1825,12 +1838,7 @@ int orbx_stereo_frame(orbx_matcher* m, orbx_extractor* left, orbx_extractor* rig
         st = ORBX_ERR_ARG;
     }
     if (!st) st = stereo_common(m, A, PL.scale, PL.nlevels, PL.rows[0], bf, b);
-    if (st) {
-        finish_left();
-        int n = 0;
-        (void)orbx_internal_extract_end(right, nullptr, nullptr, 1 << 30, &n);
-        return st;
-    }
+    if (st) return st;
     // the stereo search on the matcher's stream once both extractions are done, straight on their device outputs (the
     // two-call form copies them to the host and back): one wait per side, one result copy, one synchronisation
     ORBX_HIP(hipSetDevice(m->device));
@@ -1869,6 +1877,7 @@ int orbx_stereo_frame(orbx_matcher* m, orbx_extractor* left, orbx_extractor* rig
         if ((st = m->stage_host(out_bytes))) return st;
         ORBX_HIP(hipMemcpyAsync(m->h_stage, dur, out_bytes, hipMemcpyDeviceToHost, s));
         // the extractions' results (their streams were synchronised by extract_end); the stereo copy runs meanwhile
+        pending.e[0] = pending.e[1] = nullptr;
         const int stl = orbx_internal_extract_end(left, kps_left, desc_left, capacity_left, n_left);
         const int str = orbx_internal_extract_end(right, kps_right, desc_right, capacity_right, n_right);
         ORBX_HIP(hipStreamSynchronize(s));

@@ -135,6 +135,16 @@ def test_gpu_stereo_frame_one_call(gpu):
     (kl, dl), (kr, dr), ur, dp = m.StereoFrame(exl, exr, l, r, BF, B)
     (kl2, dl2), (kr2, dr2) = pkg.extract_pair(exl, exr, l, r)
     assert np.array_equal(kl, kl2) and np.array_equal(dr, dr2)
+    # refused after both extractions were enqueued (the sides' pyramids differ): the call reports that reason, and the
+    # extractions it dropped leave both objects usable
+    ex4 = pkg.ORBextractor(2000, 1.2, 4, 20, 7)
+    with pytest.raises(pkg.OrbxError, match="differ"):
+        m.StereoFrame(exl, ex4, l, r, BF, B)
+    k4, d4 = ex4(r)
+    k4f, d4f = pkg.ORBextractor(2000, 1.2, 4, 20, 7)(r)
+    assert np.array_equal(k4, k4f) and np.array_equal(d4, d4f)
+    (kl3, dl3), _, ur3, dp3 = m.StereoFrame(exl, exr, l, r, BF, B)
+    assert np.array_equal(kl3, kl) and ur3.tobytes() == ur.tobytes() and dp3.tobytes() == dp.tobytes()
 
 
 @pytest.mark.gpu
