@@ -2486,7 +2486,11 @@ int Extractor::configure(int r, int c, int batch) {
         }
         L.cell_end = (int)cellv.size();
         L.cand_cap = cand - L.cand_off;
-        ORBX_REQUIRE(L.cand_cap < (1 << 20), ORBX_ERR_UNSUPPORTED, "too many FAST candidates per level");
+        // k_quadtree's phase-2 sort keys hold a node's key count in bits 40..63 (< 2^24 keys per level) and the key
+        // gather stores a key's cell as int16 (< 2^15 cells per level); a 4K frame's level 0 has ~2.3M candidate slots
+        // in ~8.8k cells
+        ORBX_REQUIRE(L.cand_cap < (1 << 24), ORBX_ERR_UNSUPPORTED, "too many FAST candidates per level");
+        ORBX_REQUIRE(L.cell_end - L.cell_begin < 32768, ORBX_ERR_UNSUPPORTED, "too many FAST cells per level");
         if (L.win_w > 0 && L.win_h > 0) {
             // nIni = 0 (window more than twice as tall as wide) is undefined in the reference; pinned to 1
             L.nIni = std::max(1, (int)std::round((float)(maxBX - minB) / (maxBY - minB)));

@@ -88,6 +88,22 @@ def test_other_params(gpu):
     _check(S.kitti_like_image(8), nfeatures=1500, nlevels=5, scale=1.3, ini=25, mn=10)
 
 
+@pytest.mark.parametrize("shape,nf", [((1080, 1920), 2000), ((1536, 2048), 4000), ((2160, 3840), 3000)])
+def test_large_frames(gpu, shape, nf):
+    """HD to 4K camera frames (the reference extracts any image size, ORBextractor.cc:1043-1105)."""
+    _, k, _ = _check(S.kitti_like_image(12, rows=shape[0], cols=shape[1]), nfeatures=nf)
+    assert len(k) >= 0.9 * nf
+
+
+@pytest.mark.parametrize("kw", [dict(nlevels=1), dict(nlevels=12, scale=1.1), dict(nlevels=4, scale=2.0),
+                                dict(ini=20, mn=20), dict(ini=12, mn=30), dict(ini=0, mn=0), dict(ini=255, mn=60)],
+                         ids=["one_level", "12_levels", "scale2", "min_eq_ini", "min_above_ini", "zero_th", "high_th"])
+def test_extreme_settings(gpu, kw):
+    """Settings a YAML can hold (ORBextractor ctor :410-470, the iniTh -> minTh fallback :812-816): one level, many
+    levels, a coarse scale, minThFAST equal to or above iniThFAST, thresholds at 0 and at the u8 top."""
+    _check(S.kitti_like_image(13), nfeatures=kw.pop("nf", 1200), **kw)
+
+
 def test_pyramid_matches_oracle(gpu):
     from oracle import oracle as O
     img = S.kitti_like_image(9)
