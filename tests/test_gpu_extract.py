@@ -115,11 +115,12 @@ def test_pyramid_matches_oracle(gpu):
         assert a.shape == b.shape and np.array_equal(a, b), f"level {l}"
 
 
-def test_batch_device_equals_single(gpu):
+@pytest.mark.parametrize("shape", [(375, 1242), (2160, 3840)])
+def test_batch_device_equals_single(gpu, shape):
     import torch
 
     import multiagent_orb_slam2_amd as pkg
-    imgs = np.stack([S.kitti_like_image(100 + i) for i in range(5)])
+    imgs = np.stack([S.kitti_like_image(100 + i, rows=shape[0], cols=shape[1]) for i in range(5 if shape[0] < 1000 else 3)])
     ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
     t = torch.from_numpy(imgs).cuda()
     kps, desc, cnt = ex.extract_batch_device(t)

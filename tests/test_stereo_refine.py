@@ -87,7 +87,7 @@ def test_oracle_refine_empty_and_no_matches():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,shape,nf", [(11, (375, 1242), 2000), (12, (375, 1242), 2000), (13, (480, 752), 1200),
-                                           (14, (200, 420), 500)])
+                                           (14, (200, 420), 500), (15, (1080, 1920), 3000)])
 def test_gpu_compute_stereo_matches_host(gpu, seed, shape, nf):
     import multiagent_orb_slam2_amd as pkg
     l = S.kitti_like_image(seed, rows=shape[0], cols=shape[1])
@@ -108,12 +108,12 @@ def test_gpu_compute_stereo_matches_host(gpu, seed, shape, nf):
 def test_gpu_stereo_frame_one_call(gpu):
     """orbx_stereo_frame (the stereo Frame constructor's extractions + ComputeStereoMatches in one call, the search on the
     extractions' device outputs) equals the oracle and the two-call form, frame after frame on the same objects, over
-    two image sizes (a reconfiguration between them) and an empty pair."""
+    three image sizes up to 1920 x 1080 (reconfigurations between them) and an empty pair."""
     import multiagent_orb_slam2_amd as pkg
     exl, exr = pkg.ORBextractor(2000, 1.2, 8, 20, 7), pkg.ORBextractor(2000, 1.2, 8, 20, 7)
     m = pkg.ORBmatcher()
     t = O.tables(2000)
-    for i, shape in enumerate([(375, 1242), (375, 1242), (240, 420), (375, 1242)]):
+    for i, shape in enumerate([(375, 1242), (375, 1242), (240, 420), (1080, 1920), (375, 1242)]):
         l = S.kitti_like_image(40 + i, rows=shape[0], cols=shape[1])
         r = S.shifted_right_view(l, 40 + i)
         (kl, dl), (kr, dr), ur, dp = m.StereoFrame(exl, exr, l, r, BF, B)
