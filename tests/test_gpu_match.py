@@ -255,3 +255,34 @@ def test_bf_match_ties_across_chunks(gpu, bf_mode):
     for g, r, name in zip(got, ref, ("best_idx", "best_dist", "second_dist")):
         assert np.array_equal(g, r), name
     assert got[0][0] == 4000 and got[1][0] == 0 and got[2][0] == 0
+
+
+def test_matchers_empty_and_degenerate_inputs(gpu, bf_mode):
+    """What the reference's loops do with nothing to loop over (ORBmatcher.cc:161-290, :524-657; Frame.cc:466-549):
+    no queries, no train rows, a keyframe without FeatureVector nodes, no MapPoints (every vpMapPoints entry NULL),
+    an empty right image -- no matches and no error, as the oracle."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    m = pkg.ORBmatcher(0.75, True)
+    q, t = S.planted_pairs(3, 50, 80)
+    for qq, tt in ((q[:0], t), (q, t[:0]), (q[:0], t[:0]), (q[:1], t[:1])):
+        got, ref = m.bf_match(qq, tt), O.bf_match(qq, tt)
+        for g, r in zip(got, ref):
+            assert np.array_equal(g, r), (len(qq), len(tt))
+    k1, d1, fv1, v1 = _kf(330, n_nodes=30)
+    no_nodes = (np.zeros(0, np.uint32), np.zeros(1, np.int32), np.zeros(0, np.int32))
+    cases = [(fv1, v1, no_nodes, v1), (no_nodes, v1, fv1, v1), (fv1, np.zeros_like(v1), fv1, v1),
+             (fv1, v1, fv1, np.zeros_like(v1))]
+    for i, (fa, va, fb, vb) in enumerate(cases):
+        n, m12 = m.SearchByBoW_KF_KF(d1, k1["angle"], va, fa, d1, k1["angle"], vb, fb)
+        rn, rm = O.search_by_bow_kfkf(d1, k1["angle"], va, fa, d1, k1["angle"], vb, fb, 0.75, True)
+        assert n == rn == 0 and np.array_equal(m12, rm), i
+    n, mf = m.SearchByBoW_KF_F(d1, k1["angle"], np.zeros_like(v1), fv1, d1, k1["angle"], fv1)
+    rn, rm = O.search_by_bow_kff(d1, k1["angle"], np.zeros_like(v1), fv1, d1, k1["angle"], fv1, 0.75, True)
+    assert n == rn == 0 and np.array_equal(mf, rm)
+    scale = pkg.ORBextractor(2000, 1.2, 8, 20, 7).GetScaleFactors()
+    kl = _dense_rows_kps(4, 300, 20.0, 350.0)
+    for nl, nr in ((300, 0), (0, 300)):
+        res = m.stereo_descriptor_search(kl[:nl], np.resize(q, (nl, 32)), kl[:nr], np.resize(t, (nr, 32)), scale, 375, BF, B)
+        rn, idx, dist = O.stereo_match(kl[:nl], np.resize(q, (nl, 32)), kl[:nr], np.resize(t, (nr, 32)), scale, 375, BF, B)
+        assert res.n_matched == rn == 0 and np.array_equal(res.best_idx, idx) and np.array_equal(res.best_dist, dist)
