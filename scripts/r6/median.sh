@@ -1,3 +1,4 @@
+# (Record: the fused form was reverted after r7k; this script ran against that tree.)
 # Stereo median rejection fused into k_stereo_sad_rows (last workgroup per pair) vs its own launch (ORBX_MEDIAN_SPLIT
 # build): the stereo / tracking / smoke parity tests on the product library, then the A/B.  usage: bash scripts/r6/median.sh TAG
 set -o pipefail
