@@ -87,7 +87,10 @@ int orbx_extractor_get_inverse_scale_sigma_squares(const orbx_extractor* ex, flo
 int orbx_extractor_get_features_per_level(const orbx_extractor* ex, int* out);
 
 /* Configure the context for images of rows x cols, up to max_batch images per device call
- * (allocates HBM once).  Called implicitly by orbx_extract with max_batch 1. */
+ * (allocates HBM once).  Called implicitly by orbx_extract with max_batch 1.  Limits (ORBX_ERR_UNSUPPORTED past
+ * them): < 2^15 FAST cells and < 2^24 candidate slots per level (3840 x 2160 is tested), < 8,192 DistributeOctTree
+ * nodes per level (about nfeatures 37,000 at scaleFactor 1.2 / 8 levels); the stereo calls take <= 4,096 keypoints
+ * per image. */
 int orbx_extractor_reserve(orbx_extractor* ex, int rows, int cols, int max_batch);
 /* Maximum keypoints one image can yield for rows x cols (output capacity to allocate). */
 int orbx_extractor_max_keypoints(orbx_extractor* ex, int rows, int cols);
