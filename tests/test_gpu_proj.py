@@ -42,6 +42,19 @@ def test_proj_search_kitti_size(gpu, mode):
     _check(c, got)
 
 
+@pytest.mark.parametrize("mode", ["mappoints", "lastframe", "fuse"])
+@pytest.mark.parametrize("size", [(1920, 1080, 3000, 5000), (3840, 2160, 4000, 8000)], ids=["1080p", "4k"])
+def test_proj_search_large_frames(gpu, mode, size):
+    """Camera frames of 1920 x 1080 and 3840 x 2160 with their 64 x 48 grid (Frame.cc:230-245: cells of 30-80 px) and
+    a local map of 5000-8000 projected points: whichever LDS plan the launch picks, the oracle's assignment."""
+    import multiagent_orb_slam2_amd as pkg
+    W, H, nt, nq = size
+    m = pkg.ORBmatcher(0.8, True)
+    c = make_case(71, MODES[mode], n_target=nt, n_query=nq, W=W, H=H)
+    got = m.proj_search(c["params"], c["grid"], c["queries"], c["qdesc"], c["kps"], c["desc"], c["uright"], c["blocked"])
+    assert _check(c, got)[0] > 0
+
+
 @pytest.mark.parametrize("mode", ["lastframe", "mappoints", "fuse", "best"])
 def test_proj_search_lds_plans(gpu, mode):
     """The search's other LDS plans: a grid too fine to stage (320 x 240 cells: cell starts and keypoints read from
