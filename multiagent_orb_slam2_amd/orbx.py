@@ -322,6 +322,16 @@ def _p(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
+def _as_8uc1(image) -> np.ndarray:
+    """An 8UC1 image as the C-ABI takes it: rows of contiguous bytes at a row step (a cv::Mat ROI's layout).  A
+    uint8 view whose pixels are contiguous within a row (a crop of a larger frame) is passed as it is, with its step;
+    anything else is copied."""
+    a = np.asarray(image)
+    if a.dtype == np.uint8 and a.ndim == 2 and a.strides[1] == 1 and a.strides[0] >= a.shape[1]:
+        return a
+    return np.ascontiguousarray(a, np.uint8)
+
+
 def _tp(t):
     """device pointer of a torch tensor"""
     return C.c_void_p(t.data_ptr())
@@ -433,7 +443,7 @@ class ORBextractor:
     def __call__(self, image: np.ndarray, mask=None):
         """Returns (keypoints: structured array KP_DTYPE, descriptors: (n, 32) uint8).  Mask is ignored, as in
         the reference (include/ORBextractor.h:58)."""
-        img = np.ascontiguousarray(image, np.uint8)
+        img = _as_8uc1(image)
         if img.size == 0:
             return np.zeros(0, KP_DTYPE), np.zeros((0, 32), np.uint8)
         assert img.ndim == 2, "8UC1 image expected"
@@ -544,8 +554,8 @@ def extract_pair(left: "ORBextractor", right: "ORBextractor", image_left: np.nda
     """The stereo Frame constructor's two extractions (src/Frame.cc:78-81) from one thread (orbx_extract_pair: both
     enqueued before either is waited for).  Returns ((keypoints, descriptors) left, (keypoints, descriptors) right), as
     two ORBextractor calls would."""
-    il = np.ascontiguousarray(image_left, np.uint8)
-    ir = np.ascontiguousarray(image_right, np.uint8)
+    il = _as_8uc1(image_left)
+    ir = _as_8uc1(image_right)
     assert il.ndim == 2 and il.shape == ir.shape, "two 8UC1 images of one size expected"
     rows, cols = il.shape
     if il.size == 0:
@@ -664,8 +674,8 @@ class ORBmatcher:
         """The stereo Frame constructor's ORB work in one call (orbx_stereo_frame: src/Frame.cc:78-81 ExtractORB x2,
         :101 ComputeStereoMatches): ((keypoints, descriptors) left, (keypoints, descriptors) right, mvuRight, mvDepth),
         the values of extract_pair + ComputeStereoMatches without the keypoints' host round trip between them."""
-        il = np.ascontiguousarray(image_left, np.uint8)
-        ir = np.ascontiguousarray(image_right, np.uint8)
+        il = _as_8uc1(image_left)
+        ir = _as_8uc1(image_right)
         assert il.ndim == 2 and il.shape == ir.shape, "two 8UC1 images of one size expected"
         rows, cols = il.shape
         if il.size == 0:

@@ -343,3 +343,26 @@ def test_extract_pair_equals_two_calls(gpu):
                                     left.shape[0], left.shape[1], kp.ctypes.data, ds.ctypes.data, 10, C.byref(nl),
                                     kp.ctypes.data, ds.ctypes.data, 10, C.byref(nr))
     assert st == pkg.orbx.ORBX_ERR_CAPACITY and nl.value > 10
+
+
+def test_roi_views_with_a_row_step(gpu):
+    """A crop of a larger frame (a cv::Mat ROI: contiguous rows at the parent's step) goes in as it is, with its step,
+    through ORBextractor, orbx_extract_pair and orbx_stereo_frame: the same results as a contiguous copy and the oracle."""
+    import multiagent_orb_slam2_amd as pkg
+    from oracle import oracle as O
+    big = S.kitti_like_image(14, rows=420, cols=1300)
+    bigr = S.shifted_right_view(big, 14)
+    roi, roir = big[17:392, 29:1271], bigr[17:392, 29:1271]
+    assert roi.shape == (375, 1242) and not roi.flags.c_contiguous and roi.strides == (1300, 1)
+    ex, k, d = _check(roi)
+    exr = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+    (kl, dl), (kr, dr) = pkg.extract_pair(ex, exr, roi, roir)
+    (kl2, dl2), (kr2, dr2) = pkg.extract_pair(ex, exr, roi.copy(), roir.copy())
+    assert np.array_equal(kl, k) and np.array_equal(dl, d)
+    assert np.array_equal(kl, kl2) and np.array_equal(kr, kr2) and np.array_equal(dr, dr2)
+    m = pkg.ORBmatcher()
+    _, _, ur, dp = m.StereoFrame(ex, exr, roi, roir, 386.1448, 0.537165)
+    _, _, ur2, dp2 = m.StereoFrame(ex, exr, roi.copy(), roir.copy(), 386.1448, 0.537165)
+    assert ur.tobytes() == ur2.tobytes() and dp.tobytes() == dp2.tobytes() and (dp > 0).sum() > 0.2 * len(k)
+    ref = O.extract(roir, nfeatures=2000)
+    assert np.array_equal(kr, ref["kps"]) and np.array_equal(dr, ref["desc"])
