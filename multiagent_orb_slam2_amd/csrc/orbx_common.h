@@ -58,6 +58,23 @@ inline hipError_t init_done() { return hipStreamSynchronize(nullptr); }
 // clock), used by tests to delay one stream and expose a missing ordering edge deterministically.
 hipError_t debug_spin(hipStream_t stream, double ms);
 
+// Host-graph captures and the library's device-wide / legacy-stream operations, process-wide.  An extractor captures
+// its host call on its first call per configuration (orbx_extract); a hipDeviceSynchronize, a hipFree or a
+// synchronous hipMemset / hipMemcpy from another thread meanwhile (a second extractor configuring itself on the
+// first frame, Frame.cc:78-81) fails with "operation would make the legacy stream depend on a capturing blocking
+// stream" and invalidates the capture.  Both hold this lock, innermost: no other lock is taken while it is held.
+inline std::recursive_mutex& legacy_mutex() {
+    static std::recursive_mutex m;
+    return m;
+}
+struct LegacyLock {
+    std::lock_guard<std::recursive_mutex> g{legacy_mutex()};
+};
+inline hipError_t device_sync() {
+    LegacyLock l;
+    return hipDeviceSynchronize();
+}
+
 inline hipStream_t lazy_stream(hipStream_t& s, std::once_flag& once, int device) {
     std::call_once(once, [&] {
         int cur = 0;

@@ -2426,7 +2426,8 @@ static int dev_alloc(T** p, size_t count) {
 int Extractor::configure(int r, int c, int batch) {
     if (r == rows && c == cols && batch <= max_batch) return ORBX_OK;
     ORBX_HIP(hipSetDevice(device));
-    ORBX_HIP(hipDeviceSynchronize());                       // callers' streams may still read the buffers freed below
+    ::orbx::LegacyLock legacy_;                              // frees, synchronous uploads and memsets below
+    ORBX_HIP(::orbx::device_sync());                       // callers' streams may still read the buffers freed below
     for (int& k : slot_call) k = -1;
     last_call = -1;
     const int keep_batch = std::max(batch, (r == rows && c == cols) ? max_batch : 0);
@@ -2974,7 +2975,7 @@ int orbx_stream_create(int device, int priority, int cu_exclude, void** out) {
 
 int orbx_device_check(int device) {
     ORBX_HIP(hipSetDevice(device));
-    ORBX_HIP(hipDeviceSynchronize());
+    ORBX_HIP(::orbx::device_sync());
     ORBX_HIP(hipGetLastError());
     return ORBX_OK;
 }
@@ -3040,7 +3041,8 @@ int orbx_extractor_destroy(orbx_extractor* e) {
     // Every stream of the device, not only the extractor's own: callers' streams read its pyramid ring and outputs
     // (the stereo SAD step reads orbx_extractor_pyramid_device's levels); hipFree was measured to wait for them too,
     // but the guarantee should not rest on that.
-    (void)hipDeviceSynchronize();
+    ::orbx::LegacyLock legacy_;
+    (void)::orbx::device_sync();
     e->free_buffers();                                      // (and the host-API graph)
     for (auto& es : e->tpool)
         for (auto& ev : es.ev) (void)hipEventDestroy(ev);
@@ -3093,7 +3095,8 @@ int orbx_extractor_set_pyramid_ring(orbx_extractor* e, int n) {
     if (n == e->pyr_ring) return ORBX_OK;
     const int r = e->rows, c = e->cols, b = e->max_batch;
     ORBX_HIP(hipSetDevice(e->device));
-    ORBX_HIP(hipDeviceSynchronize());                       // callers' streams may still read the pyramid ring
+    ::orbx::LegacyLock legacy_;
+    ORBX_HIP(::orbx::device_sync());                       // callers' streams may still read the pyramid ring
     e->free_buffers();
     for (int& k : e->slot_call) k = -1;
     e->last_call = -1;
@@ -3151,6 +3154,10 @@ static int extract_begin(orbx_extractor* e, const uint8_t* image, int rows, int 
     int st = e->configure(rows, cols, std::max(e->max_batch, 1));
     if (st) return st;
     const size_t nb = (size_t)rows * cols;
+    // buffer (re)allocation and the capture of this configuration's graph hold the process-wide legacy lock: another
+    // thread's device synchronisation or synchronous upload during the capture would invalidate it (orbx_common.h)
+    std::unique_lock<std::recursive_mutex> legacy_(::orbx::legacy_mutex(), std::defer_lock);
+    if (!(e->host_graph && e->hgexec) || e->in_bytes < nb || !e->d_hblk) legacy_.lock();
     if (e->in_bytes < nb) {
         e->drop_graph();                                     // it names the buffers replaced here
         if (e->d_in) (void)hipFree(e->d_in);
@@ -3217,6 +3224,15 @@ static int extract_begin(orbx_extractor* e, const uint8_t* image, int rows, int 
         const hipError_t ei = (r == ORBX_OK && ec == hipSuccess) ? hipGraphInstantiate(&x, g, nullptr, nullptr, 0) : ec;
         if (r != ORBX_OK || ei != hipSuccess) {              // no graph for this extractor: per-call stream operations
             if (g) (void)hipGraphDestroy(g);
+            // a capture that failed part-way can leave the side stream (forked into it) capturing: end whatever is
+            // still capturing, so that the per-call path below and later calls find usable streams
+            for (hipStream_t q : {s, e->side}) {
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                if (q && hipStreamIsCapturing(q, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+                    hipGraph_t gq = nullptr;
+                    if (hipStreamEndCapture(q, &gq) == hipSuccess && gq) (void)hipGraphDestroy(gq);
+                }
+            }
             (void)hipGetLastError();
             e->host_graph = false;
         } else {
@@ -3380,7 +3396,8 @@ int orbx_extractor_copy_blurred_level(orbx_extractor* e, int index, int level, u
     const int w = e->lv[level].w, h = e->lv[level].h;
     ORBX_REQUIRE(dst_step >= (size_t)w, ORBX_ERR_ARG, "bad destination");
     ORBX_HIP(hipSetDevice(e->device));
-    ORBX_HIP(hipDeviceSynchronize());                                  // the last call's kernels may run on any stream
+    ::orbx::LegacyLock legacy_;
+    ORBX_HIP(::orbx::device_sync());                                  // the last call's kernels may run on any stream
     // k_blur7 over every tile of image `index` of the last call's pyramid (d_pyr, and level 0 = the caller's image),
     // into a one-image buffer: whatever the describe form, and whichever describe-input set the last call used
     if (!e->d_blur_diag) ORBX_HIP(hipMalloc((void**)&e->d_blur_diag, e->pyr_size));
@@ -3429,7 +3446,7 @@ int orbx_extractor_stage_count(void) { return ST_COUNT; }
 const char* orbx_extractor_stage_name(int s) { return (s >= 0 && s < ST_COUNT) ? kStageNames[s] : ""; }
 #ifdef ORBX_QT_PROF
 int orbx_debug_qt_prof(unsigned long long* out) {   // 2 x 64 stamps (diagnostics build only)
-    ORBX_HIP(hipDeviceSynchronize());
+    ORBX_HIP(::orbx::device_sync());
     ORBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_qtprof), sizeof(orbx::g_qtprof)));
     return ORBX_OK;
 }

@@ -261,6 +261,7 @@ int orbx_fusion_create(orbx_vocab* vocab, orbx_matcher* matcher, int capacity, i
         (st = falloc(&f->pairs, 2 * N * std::max(candidates, 1))) || (st = falloc(&f->m12, N * std::max(candidates, 1) * C)) ||
         (st = falloc(&f->nm, N * std::max(candidates, 1))) || (st = falloc(&f->gate, 1)))
         return fail(st);
+    ::orbx::LegacyLock legacy_;
     if (hipMemset(f->ring, 0, S * f->lay.bytes) != hipSuccess || hipMemset(f->slot_group, 0xff, 4 * S) != hipSuccess ||
         hipMemset(f->status, 0, 4) != hipSuccess || hipMemset(f->gate, 0, 8) != hipSuccess ||
         init_done() != hipSuccess) {   // complete before the first kernel on a caller's (non-blocking) stream
@@ -274,11 +275,12 @@ int orbx_fusion_create(orbx_vocab* vocab, orbx_matcher* matcher, int capacity, i
 int orbx_fusion_destroy(orbx_fusion* f) {
     if (!f) return ORBX_OK;
     (void)hipSetDevice(f->device);
-    (void)hipDeviceSynchronize();
+    (void)::orbx::device_sync();
     if (f->db) orbx_kfdb_destroy(f->db);
     void* bufs[] = {f->ring, f->send, f->g_desc, f->g_counts, f->v_word, f->v_weight, f->v_node, f->v_bw, f->v_bv, f->v_nw,
                     f->v_fvn, f->v_fvo, f->v_fvi, f->v_nfv, f->new_slots, f->qslots, f->ids, f->zeros, f->slot_group,
                     f->qgroup, f->cand, f->ncand, f->status, f->pairs, f->m12, f->nm, f->gate};
+    ::orbx::LegacyLock legacy_;
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     delete f;
@@ -393,7 +395,8 @@ int orbx_fusion_commit_device(orbx_fusion* f, const void* d_exchanged, int32_t* 
 int orbx_fusion_read_ring(orbx_fusion* f, uint8_t* host_dst) {
     ORBX_REQUIRE(f && host_dst, ORBX_ERR_ARG, "bad argument");
     ORBX_HIP(hipSetDevice(f->device));
-    ORBX_HIP(hipDeviceSynchronize());
+    ::orbx::LegacyLock legacy_;
+    ORBX_HIP(::orbx::device_sync());
     ORBX_HIP(hipMemcpy(host_dst, f->ring, (size_t)f->slots * f->lay.bytes, hipMemcpyDeviceToHost));
     return ORBX_OK;
 }
@@ -410,7 +413,8 @@ int orbx_fusion_last_step(const orbx_fusion* f, int* first_slot, int* n_new, int
 int orbx_fusion_stats(orbx_fusion* f, long long* gate_passed, int* status) {
     ORBX_REQUIRE(f, ORBX_ERR_ARG, "null fusion");
     ORBX_HIP(hipSetDevice(f->device));
-    ORBX_HIP(hipDeviceSynchronize());
+    ::orbx::LegacyLock legacy_;
+    ORBX_HIP(::orbx::device_sync());
     unsigned long long g = 0;
     int s = 0;
     ORBX_HIP(hipMemcpy(&g, f->gate, 8, hipMemcpyDeviceToHost));

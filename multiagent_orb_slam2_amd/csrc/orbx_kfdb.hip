@@ -823,7 +823,7 @@ struct DbOp {
     DbOp(orbx_kfdb* d, hipStream_t st, bool uses_stream) : db(d), s(st), on_stream(uses_stream), lk(d->mtx) {
         if (!on_stream || !db->have_last || db->last_stream == s) return;
         if (!db->multi) {
-            err = hipDeviceSynchronize();
+            err = ::orbx::device_sync();
             db->multi = true;
         } else if (db->last_op_set) {
             err = hipStreamWaitEvent(s, db->last_op, 0);
@@ -850,7 +850,8 @@ int grow_scratch(orbx_kfdb* db, size_t bytes) {
     if (bytes <= db->scratch_bytes) return ORBX_OK;
     if (db->scratch) {
         // earlier operations may have run on callers' streams: every stream drained before the buffer goes away
-        ORBX_HIP(hipDeviceSynchronize());
+        ::orbx::LegacyLock legacy_;
+        ORBX_HIP(::orbx::device_sync());
         ORBX_HIP(hipFree(db->scratch));
         db->scratch = nullptr;
         db->scratch_bytes = 0;
@@ -957,7 +958,8 @@ int detect_batch(orbx_kfdb* db, int kind, const QueryIn& Q, int nq, unsigned cha
         const size_t need = (size_t)4 * nbw * nq;
         if (need > db->qbits_bytes) {
             if (db->d_qbits) {
-                ORBX_HIP(hipDeviceSynchronize());
+                ::orbx::LegacyLock legacy_;
+                ORBX_HIP(::orbx::device_sync());
                 ORBX_HIP(hipFree(db->d_qbits));
                 db->d_qbits = nullptr;
                 db->qbits_bytes = 0;
@@ -1012,6 +1014,7 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
     db->seq.assign(max_slots, kNoSeq);
     const size_t S = max_slots, W = max_words;
     hipError_t e = hipSetDevice(device);
+    ::orbx::LegacyLock legacy_;
     auto alloc = [&](void** p, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc(p, bytes);
         if (e == hipSuccess) e = hipMemset(*p, 0, bytes);
@@ -1063,9 +1066,10 @@ int orbx_kfdb_create(int n_vocab_words, int max_slots, int max_words, int device
 int orbx_kfdb_destroy(orbx_kfdb* db) {
     if (!db) return ORBX_OK;
     (void)hipSetDevice(db->device);
-    (void)hipDeviceSynchronize();              // operations on callers' streams read the database's buffers
+    (void)::orbx::device_sync();              // operations on callers' streams read the database's buffers
     void* bufs[] = {db->d_bw, db->d_bv, db->d_bn, db->d_covis, db->d_seq, db->d_if_off, db->d_if_cur, db->d_if_slot,
                     db->d_scan, db->d_members, db->scratch, db->score_stage, db->d_qbits, db->d_wmap};
+    ::orbx::LegacyLock legacy_;
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (int k = 0; k < 3; ++k) {
@@ -1252,7 +1256,8 @@ int orbx_kfdb_score(orbx_kfdb* db, const int32_t* pairs, int n, double* scores) 
     ORBX_DBOP(db, db->own());
     const size_t need = align_up(8 * (size_t)n) + align_up(8 * (size_t)n);
     if (need > db->score_stage_bytes) {          // the db's own stream is the only user of this buffer
-        ORBX_HIP(hipDeviceSynchronize());
+        ::orbx::LegacyLock legacy_;
+        ORBX_HIP(::orbx::device_sync());
         if (db->score_stage) ORBX_HIP(hipFree(db->score_stage));
         db->score_stage = nullptr;
         db->score_stage_bytes = 0;

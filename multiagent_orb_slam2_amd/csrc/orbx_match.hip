@@ -1395,6 +1395,7 @@ struct Matcher {
     int stage_host(size_t bytes) {
         if (bytes <= h_stage_bytes) return ORBX_OK;
         const size_t nb = std::max(bytes, h_stage_bytes * 2);     // geometric growth over the old size
+        ::orbx::LegacyLock legacy_;
         if (h_stage) (void)hipHostFree(h_stage);
         h_stage = nullptr;
         h_stage_bytes = 0;
@@ -1407,15 +1408,16 @@ struct Matcher {
     int reserve_on(size_t bytes, hipStream_t on) {
         if (have_last && last_stream != on) {
             if (!multi) {
-                ORBX_HIP(hipDeviceSynchronize());
+                ORBX_HIP(::orbx::device_sync());
                 multi = true;
             } else if (last_op_set) {
                 ORBX_HIP(hipStreamWaitEvent(on, last_op, 0));
             }
         }
         if (bytes <= scratch_bytes) return ORBX_OK;
+        ::orbx::LegacyLock legacy_;
         if (scratch) {
-            ORBX_HIP(hipDeviceSynchronize());   // earlier users on any stream done before the buffer goes away
+            ORBX_HIP(::orbx::device_sync());   // earlier users on any stream done before the buffer goes away
             (void)hipFree(scratch);
             scratch = nullptr;
         }
@@ -1561,10 +1563,11 @@ int orbx_matcher_create(float nnratio, int checkOri, int device, orbx_matcher** 
 int orbx_matcher_destroy(orbx_matcher* m) {
     if (!m) return ORBX_OK;
     (void)hipSetDevice(m->device);
-    (void)hipDeviceSynchronize();                                // device calls on callers' streams use the scratch
+    (void)::orbx::device_sync();                                // device calls on callers' streams use the scratch
     if (m->last_op) (void)hipEventDestroy(m->last_op);
     for (hipEvent_t ev : m->frame_ev)
         if (ev) (void)hipEventDestroy(ev);
+    ::orbx::LegacyLock legacy_;
     if (m->scratch) (void)hipFree(m->scratch);
     if (m->h_stage) (void)hipHostFree(m->h_stage);
     if (m->stream) (void)hipStreamDestroy(m->stream);

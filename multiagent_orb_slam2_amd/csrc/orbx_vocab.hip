@@ -295,6 +295,7 @@ static int vocab_build(Vocab* v, int n_lines, const int32_t* parent, const uint8
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t total = al(bd) + al(bo) + al(bc) + al(bw) + al(bwi);
     ORBX_HIP(hipSetDevice(v->device));
+    ::orbx::LegacyLock legacy_;
     ORBX_HIP(hipMalloc(&v->mem, total));
     uint8_t* p = (uint8_t*)v->mem;
     v->dev.desc = (const uint4*)p;             ORBX_HIP(hipMemcpy(p, d.data(), bd, hipMemcpyHostToDevice)); p += al(bd);
@@ -413,7 +414,8 @@ int orbx_vocab_load_text(const char* path, int device, orbx_vocab** out) {
 int orbx_vocab_destroy(orbx_vocab* v) {
     if (!v) return ORBX_OK;
     (void)hipSetDevice(v->device);
-    (void)hipDeviceSynchronize();              // device calls on callers' streams read the tree and the scratch
+    ::orbx::LegacyLock legacy_;
+    (void)::orbx::device_sync();              // device calls on callers' streams read the tree and the scratch
     if (v->mem) (void)hipFree(v->mem);
     if (v->scratch) (void)hipFree(v->scratch);
     if (v->stream) (void)hipStreamDestroy(v->stream);
@@ -468,7 +470,8 @@ int orbx_vocab_transform(orbx_vocab* v, const uint8_t* desc, int n, int levelsup
     const size_t bytes = al256(32 * N) + 3 * al256(4 * N) + 2 * al256(8 * N) + 3 * al256(4 * (N + 1)) + al256(64);
     if (bytes > v->scratch_bytes) {
         if (v->scratch) {
-            ORBX_HIP(hipDeviceSynchronize());      // an earlier call on any stream may still read the old buffer
+            ::orbx::LegacyLock legacy_;
+            ORBX_HIP(::orbx::device_sync());      // an earlier call on any stream may still read the old buffer
             (void)hipFree(v->scratch);
         }
         v->scratch = nullptr;
