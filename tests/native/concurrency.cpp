@@ -1,7 +1,7 @@
 // Native concurrency check of the C-ABI (the reference's threading: Frame.cc:78-81 runs the left and right
 // ORBextractor::operator() on two std::threads; Tracking, LocalMapping, LoopClosing and MapFusion call ORBmatcher from
 // their own threads).  Two extractors on two threads and four matchers on four threads, three agents' stereo Frames on
-// three threads, and the KeyFrameDatabase's threads, each repeating its call and comparing every result with its
+// three threads, fresh extractors' first calls racing, and the KeyFrameDatabase's threads, each repeating its call and comparing every result with its
 // single-threaded first result (bit-exact).  Plain build: build/concurrency (make; tests/test_gpu_native_concurrency.py);
 // with ThreadSanitizer on the host code: make tsan, scripts/tsan_gpu.sh.  Exit status = number of mismatches.
 #include <algorithm>
@@ -172,6 +172,47 @@ int kfdb_concurrency(int reps) {
     return mismatch + errors + reader_bad;
 }
 
+// ---- First calls racing: fresh extractors used for the first time by several threads at once (the first stereo frame,
+// Frame.cc:78-81, and agents starting together): one thread's configuration must not break another's host-graph
+// capture.  Every first and second result must equal a warm extractor's.
+int first_calls_concurrency(int trials, int rows, int cols) {
+    constexpr int kThreads = 6;
+    std::vector<uint8_t> im[2] = {make_image(rows, cols, 31), make_image(rows, cols, 32)};
+    Extraction warm[2];
+    {
+        orbx_extractor* w = nullptr;
+        if (orbx_extractor_create(2000, 1.2f, 8, 20, 7, 0, &w) || extract(w, im[0], rows, cols, warm[0]) ||
+            extract(w, im[1], rows, cols, warm[1])) {
+            std::fprintf(stderr, "first calls setup: %s\n", orbx_last_error());
+            return 1;
+        }
+        orbx_extractor_destroy(w);
+    }
+    int bad = 0;
+    for (int t = 0; t < trials; ++t) {
+        orbx_extractor* ex[kThreads] = {};
+        for (auto& e : ex)
+            if (orbx_extractor_create(2000, 1.2f, 8, 20, 7, 0, &e)) return 1;
+        std::atomic<int> ready{0};
+        int fails[kThreads] = {};
+        std::vector<std::thread> th;
+        for (int k = 0; k < kThreads; ++k)
+            th.emplace_back([&, k] {
+                ready.fetch_add(1);
+                while (ready.load() < kThreads) std::this_thread::yield();   // all first calls at once
+                for (int r = 0; r < 2; ++r) {
+                    Extraction e;
+                    if (extract(ex[k], im[k & 1], rows, cols, e) || !same(e, warm[k & 1])) ++fails[k];
+                }
+            });
+        for (auto& x : th) x.join();
+        for (int k = 0; k < kThreads; ++k) bad += fails[k];
+        for (auto& e : ex) orbx_extractor_destroy(e);
+    }
+    std::printf("first calls: %d trials x %d fresh extractors on %d threads, %d mismatches\n", trials, kThreads, kThreads, bad);
+    return bad;
+}
+
 // ---- Stereo frames of several agents at once: each agent's Tracking thread builds its stereo Frames (Frame.cc:61-117,
 // the two extractions of :78-81 and ComputeStereoMatches :101) with its own left / right extractors and matcher, the
 // multi-agent system running one Tracking per agent in one process.  Agent a alternates orbx_stereo_frame with
@@ -306,5 +347,6 @@ int main(int argc, char** argv) {
                 2 * reps, ref[0].n, ref[1].n, 4 * reps, total);
     for (auto& m : mt) orbx_matcher_destroy(m);
     for (auto& e : ex) orbx_extractor_destroy(e);
-    return total + stereo_frame_concurrency(reps, rows, cols) + kfdb_concurrency(reps);
+    return total + stereo_frame_concurrency(reps, rows, cols) + first_calls_concurrency(std::max(2, reps / 2), rows, cols) +
+           kfdb_concurrency(reps);
 }
