@@ -3224,17 +3224,27 @@ static int extract_begin(orbx_extractor* e, const uint8_t* image, int rows, int 
         const hipError_t ei = (r == ORBX_OK && ec == hipSuccess) ? hipGraphInstantiate(&x, g, nullptr, nullptr, 0) : ec;
         if (r != ORBX_OK || ei != hipSuccess) {              // no graph for this extractor: per-call stream operations
             if (g) (void)hipGraphDestroy(g);
-            // a capture that failed part-way can leave the side stream (forked into it) capturing: end whatever is
-            // still capturing, so that the per-call path below and later calls find usable streams
-            for (hipStream_t q : {s, e->side}) {
-                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-                if (q && hipStreamIsCapturing(q, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
-                    hipGraph_t gq = nullptr;
-                    if (hipStreamEndCapture(q, &gq) == hipSuccess && gq) (void)hipGraphDestroy(gq);
-                }
-            }
             (void)hipGetLastError();
             e->host_graph = false;
+            // A capture invalidated part-way (another thread synchronised the device: liborbx's own such operations
+            // wait for the legacy lock, a caller's cannot) can leave the extractor's streams in the capture sequence and
+            // its call events recorded inside it.  The extractor continues on fresh streams and events; the old ones
+            // are left alone (neither ended nor destroyed: both crash or fail on a stream still in the sequence, r7z).
+            hipStream_t ns = nullptr, nside = nullptr;
+            ORBX_HIP(hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
+            ORBX_HIP(create_stream_masked(&nside, -1, std::getenv("ORBX_CU_EXCLUDE") ? std::atoi(std::getenv("ORBX_CU_EXCLUDE")) : 0));
+            e->stream = ns;
+            e->side = nside;
+            s = ns;
+            for (auto& c : e->cev) {
+                for (hipEvent_t* ev : {&c.fork, &c.pyr, &c.join, &c.front, &c.desc, &c.qt})
+                    ORBX_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+                c.used = false;
+            }
+            for (int& k : e->slot_call) k = -1;
+            e->dset_call[0] = e->dset_call[1] = -1;
+            e->last_call = -1;
+            e->qt_prev = -1;
         } else {
             e->hgraph = g;
             e->hgexec = x;

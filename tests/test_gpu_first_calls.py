@@ -44,3 +44,35 @@ def test_fresh_extractors_first_calls_concurrent(gpu):
             wk, wd = warm[t % 3]
             assert np.array_equal(k1, wk) and np.array_equal(d1, wd), (trial, t, "first call")
             assert np.array_equal(k2, wk) and np.array_equal(d2, wd), (trial, t, "second call")
+
+
+def test_first_call_beside_foreign_device_syncs(gpu):
+    """A caller's own code synchronising the device (torch.cuda.synchronize on another thread, which liborbx's lock
+    cannot order) while an extractor captures its first call: the capture may be invalidated, and then the call falls
+    back to per-call stream operations -- its results, and every later call's, still equal a warm extractor's."""
+    import torch
+
+    import multiagent_orb_slam2_amd as pkg
+    img = S.kitti_like_image(90)
+    wk, wd = pkg.ORBextractor(2000, 1.2, 8, 20, 7)(img)
+    for trial in range(6):
+        ex = pkg.ORBextractor(2000, 1.2, 8, 20, 7)
+        stop = threading.Event()
+        errs = []
+
+        def spin():
+            try:
+                while not stop.is_set():
+                    torch.cuda.synchronize()
+            except Exception as e:                      # noqa: BLE001 -- a foreign sync refused during a capture
+                errs.append(str(e))
+        t = threading.Thread(target=spin)
+        t.start()
+        try:
+            res = [ex(img) for _ in range(3)]
+        finally:
+            stop.set()
+            t.join()
+        for i, (k, d) in enumerate(res):
+            assert np.array_equal(k, wk) and np.array_equal(d, wd), (trial, i)
+    torch.cuda.synchronize()
